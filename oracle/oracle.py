@@ -1,0 +1,163 @@
+"""ctypes wrapper around the C oracle (oracle/sbeacon_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py — never by the product package.
+
+``OracleVcf(path).perform_query(payload_dict)`` returns the dict the reference
+``PerformQueryResponse.dump()`` would return
+(``shared_resources/payloads/lambda_responses.py:14-23``) or raises the Python
+exception class the reference raises on the same input.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, 'liboracle.so')
+
+GRAN = {'boolean': 0, 'count': 1, 'aggregated': 2, 'record': 3}
+ERRORS = {1: UnboundLocalError, 2: IndexError, 3: ValueError, 4: AttributeError,
+          9: NotImplementedError}
+
+
+class OrcQuery(C.Structure):
+    _fields_ = [('region', C.c_char_p), ('end_min', C.c_int64), ('end_max', C.c_int64),
+                ('reference_bases', C.c_char_p), ('alternate_bases', C.c_char_p),
+                ('variant_type', C.c_char_p), ('include_details', C.c_int32),
+                ('granularity', C.c_int32), ('variant_min_length', C.c_int64),
+                ('variant_max_length', C.c_int64), ('include_samples', C.c_int32),
+                ('selected_samples_only', C.c_int32), ('sample_names', C.c_char_p),
+                ('patched', C.c_int32)]
+
+
+class OrcResult(C.Structure):
+    _fields_ = [('error', C.c_int32), ('exists', C.c_int32), ('call_count', C.c_int64),
+                ('all_alleles_count', C.c_int64), ('variants', C.c_void_p),
+                ('n_variants', C.c_int64), ('sample_indices', C.POINTER(C.c_int32)),
+                ('n_sample_indices', C.c_int64), ('sample_names', C.c_void_p),
+                ('n_sample_names', C.c_int64)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.orc_load_vcf.restype = C.c_void_p
+        L.orc_load_vcf.argtypes = [C.c_char_p, C.c_int]
+        L.orc_free.argtypes = [C.c_void_p]
+        L.orc_n_records.restype = C.c_int64
+        L.orc_n_records.argtypes = [C.c_void_p]
+        L.orc_n_samples.restype = C.c_int32
+        L.orc_n_samples.argtypes = [C.c_void_p]
+        L.orc_query_one.argtypes = [C.c_void_p, C.POINTER(OrcQuery), C.POINTER(OrcResult)]
+        L.orc_query_batch.argtypes = [C.c_void_p, C.POINTER(OrcQuery), C.c_int64,
+                                      C.POINTER(OrcResult), C.c_int]
+        L.orc_result_free.argtypes = [C.POINTER(OrcResult)]
+        L.orc_records_in_region.restype = C.c_int64
+        L.orc_records_in_region.argtypes = [C.c_void_p, C.c_char_p]
+        _lib = L
+    return _lib
+
+
+def build():
+    import subprocess
+    subprocess.check_call(['make', '-s', '-C', HERE])
+
+
+def _b(s):
+    return None if s is None else str(s).encode()
+
+
+def make_query(p: dict, patched: bool = False):
+    """PerformQueryPayload dict -> OrcQuery (keeps the encoded strings alive)."""
+    pt = p.get('passthrough') or {}
+    names = pt.get('sampleNames', None)
+    keep = [_b(p['region']), _b(p.get('reference_bases')), _b(p.get('alternate_bases')),
+            _b(p.get('variant_type')), _b(','.join(names)) if names is not None else None]
+    q = OrcQuery(keep[0], int(p['end_min']), int(p['end_max']), keep[1], keep[2], keep[3],
+                 1 if p.get('include_details') else 0, GRAN.get(p.get('requested_granularity'), -1),
+                 int(p['variant_min_length']), int(p['variant_max_length']),
+                 1 if pt.get('includeSamples', False) else 0,
+                 1 if pt.get('selectedSamplesOnly', False) else 0, keep[4], 1 if patched else 0)
+    return q, keep
+
+
+def _result_dict(r: OrcResult, p: dict):
+    pt = p.get('passthrough') or {}
+    samples_variant = bool(pt.get('selectedSamplesOnly', False))
+    variants = C.string_at(r.variants).decode() if r.variants else ''
+    names = C.string_at(r.sample_names).decode() if r.sample_names else ''
+    return {
+        'exists': bool(r.exists),
+        'vcf_location': p.get('vcf_location'),
+        'dataset_id': p.get('dataset_id'),
+        'all_alleles_count': int(r.all_alleles_count),
+        'variants': variants.split('\n') if r.n_variants else [],
+        'call_count': int(r.call_count),
+        'sample_indices': [r.sample_indices[i] for i in range(r.n_sample_indices)] if samples_variant else [],
+        'sample_names': names.split(',') if r.n_sample_names else [],
+    }
+
+
+class OracleVcf:
+    def __init__(self, path: str, load_gt: bool = True):
+        self.path = path
+        self.h = lib().orc_load_vcf(path.encode(), 1 if load_gt else 0)
+        if not self.h:
+            raise FileNotFoundError(path)
+
+    def close(self):
+        if self.h:
+            lib().orc_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def n_records(self):
+        return lib().orc_n_records(self.h)
+
+    def perform_query(self, payload: dict, patched: bool = False) -> dict:
+        q, _keep = make_query(payload, patched)
+        r = OrcResult()
+        lib().orc_query_one(self.h, C.byref(q), C.byref(r))
+        try:
+            if r.error:
+                raise ERRORS.get(r.error, RuntimeError)(f'oracle error {r.error}')
+            return _result_dict(r, payload)
+        finally:
+            lib().orc_result_free(C.byref(r))
+
+    def perform_query_batch(self, payloads, patched=False, threads=0, want_results=True):
+        """Run many queries (OpenMP); returns list of dict | Exception class."""
+        n = len(payloads)
+        arr = (OrcQuery * n)()
+        keep = []
+        for i, p in enumerate(payloads):
+            q, k = make_query(p, patched)
+            arr[i] = q
+            keep.append(k)
+        res = (OrcResult * n)()
+        lib().orc_query_batch(self.h, arr, n, res, int(threads))
+        out = []
+        for i in range(n):
+            if want_results:
+                if res[i].error:
+                    out.append(ERRORS.get(res[i].error, RuntimeError))
+                else:
+                    out.append(_result_dict(res[i], payloads[i]))
+            lib().orc_result_free(C.byref(res[i]))
+        return out
+
+    def records_in_region(self, region: str) -> int:
+        return lib().orc_records_in_region(self.h, region.encode())
