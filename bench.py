@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""Benchmark: batched Beacon g_variants slice queries on an HBM-resident store.
+
+Workload (BASELINE.json configs[1]): a 1000G chr22-
+shape store — 1,103,547 records x 2,504 samples, seed 22 — and 10,000 Beacon
+requests (5,000 range + 5,000 point ref/alt, seed 1022 + rank), sliced into
+PerformQueryPayloads exactly as splitQuery does.  One step = one device pass
+of the whole batch (bounds -> capacity scan -> range scan -> hit compaction)
+with the queries already resident in HBM.
+
+Multi-GPU (`torch.distributed.run`, one rank per GPU): every rank holds its
+own store replica and answers its own 10k requests — the slices are
+independent (the reference fans them out as separate Lambdas), so there is
+no data-path collective; `value` = all ranks' requests / max-over-ranks time
+(weak scaling).  The barrier and the timing reduction use torch.distributed.
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, 'terraform-aws-serverless-beacon_amd')
+sys.path.insert(0, PKG)
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=3)
+    ap.add_argument('--records', type=int, default=1103547)
+    ap.add_argument('--samples', type=int, default=2504)
+    ap.add_argument('--range-requests', type=int, default=5000)
+    ap.add_argument('--point-requests', type=int, default=5000)
+    ap.add_argument('--threads', type=int, default=16, help='host ingest / CPU-baseline threads')
+    ap.add_argument('--cpu-seconds', type=float, default=15.0, help='target CPU-baseline sample duration')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--parity-requests', type=int, default=300,
+                    help='requests re-checked against the C oracle after timing (rank 0)')
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(local)
+
+    from sbeacon.workload import SyntheticVcf, config2_requests, requests_to_payloads
+
+    t0 = time.perf_counter()
+    gen = SyntheticVcf(seed=22, n_records=args.records, n_samples=args.samples)
+    loc = 'synthetic/chr22-1000g-shape.vcf.gz'
+    store = gen.build_store(loc, device=local, keep_genotypes=True, threads=args.threads)
+    info = store.info()
+    t_ingest = time.perf_counter() - t0
+    log(f'[rank {rank}] store: {info["n_records"]} records, {info["n_alt_rows"]} alt rows, '
+        f'{info["device_bytes"] / 2**20:.0f} MiB HBM, ingest {t_ingest:.1f} s')
+    reqs = config2_requests(gen, n_range=args.range_requests, n_point=args.point_requests, seed=1022 + rank)
+    payloads, owner = requests_to_payloads(reqs, vcf_location=loc, chrom='22')
+    batch = store.prepare(payloads)
+    log(f'[rank {rank}] {len(reqs)} requests -> {len(payloads)} slice queries')
+
+    for _ in range(args.warmup):
+        batch.run()
+    batch.sync()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        batch.run()
+    batch.sync()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t1
+    if dist:
+        dist.barrier()
+    timing = batch.timing()  # per-launch averages over the timed steps (HIP events)
+    rs = batch.fetch()
+    st = rs.stats()
+    n_req, n_slice = len(reqs), len(payloads)
+    scanned, hits = st['records_scanned'], st['hits']
+    if dist:
+        t = torch.tensor([elapsed, timing['scan_ms'], timing['total_ms']], dtype=torch.float64, device='cuda')
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, scan_ms_max, total_ms_max = t.tolist()
+        tot = torch.tensor([n_req, n_slice, scanned, hits], dtype=torch.float64, device='cuda')
+        dist.all_reduce(tot)
+        tot_req, tot_slice, tot_scanned, tot_hits = tot.tolist()
+    else:
+        tot_req, tot_slice, tot_scanned, tot_hits = n_req, n_slice, scanned, hits
+
+    ms_per_step = elapsed / args.steps * 1e3
+    value = tot_req * args.steps / elapsed
+    # roofline of the dominant kernel (the range scan), algorithmic bytes per
+    # launch: 32 B per scanned record + 8 B per emitted hit
+    scan_bytes = 32.0 * scanned + 8.0 * hits
+    achieved = scan_bytes / (timing['scan_ms'] * 1e-3) / 1e9 if timing['scan_ms'] > 0 else 0.0
+    traffic = None
+    tf = os.path.join(REPO, 'profiles', 'traffic.json')
+    if os.path.exists(tf):
+        try:
+            tj = json.load(open(tf))
+            if tj.get('records') == args.records and tj.get('requests') == n_req:
+                traffic = tj.get('scan_kernel_hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+
+    cpu = None
+    parity = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu, parity = cpu_baseline_and_parity(args, gen, reqs, payloads, owner, rs)
+
+    out = {
+        'metric': 'region queries/sec (Beacon g_variants requests, 10 kb-sliced performQuery payloads)',
+        'value': round(value, 1),
+        'unit': 'requests/s',
+        'n_gpus': world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(ms_per_step, 4),
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'int64',
+        'data': 'synthetic (seeded 1000G chr22-shape VCF, generated + ingested in-process)',
+        'config': {'workload': 'config2-chr22-shape', 'records': args.records, 'samples': args.samples,
+                   'requests_per_gpu': n_req, 'slice_queries_per_gpu': n_slice,
+                   'parallelism': f'replicas x{world} (independent slices, no data-path collective)'},
+        'slice_queries_per_s': round(tot_slice * args.steps / elapsed, 1),
+        'records_scanned_per_s': round(tot_scanned * args.steps / elapsed, 1),
+        'hits_per_step': int(tot_hits),
+        'device_ms_per_step': {'total': round(timing['total_ms'], 4), 'scan_kernel': round(timing['scan_ms'], 4),
+                               'bounds_and_caps': round(timing['bounds_ms'], 4)},
+        'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                     'kernel': 'scan_kernel', 'algorithmic_bytes_per_launch': scan_bytes},
+        'cpu_baseline': cpu,
+        'parity_sample': parity,
+        'ingest_s': round(t_ingest, 2),
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+def cpu_baseline_and_parity(args, gen, reqs, payloads, owner, rs):
+    """C oracle (the CPU restatement of the reference loop, OpenMP over the
+    host cores) on a bounded sample of the same requests; also re-checks the
+    device answers for a sample of requests against it."""
+    from oracle.oracle import OracleVcf
+    tmp = tempfile.mkdtemp(prefix='sbeacon-bench-')
+    path = os.path.join(tmp, 'sites.vcf')
+    gen.write(path, sites_only=True, threads=args.threads)  # config 2 queries read no GT
+    orc = OracleVcf(path, load_gt=False)
+    threads = args.threads
+    by_req = {}
+    for j, r in enumerate(owner):
+        by_req.setdefault(r, []).append(j)
+    # interleave request kinds so the sample is representative of the mix
+    order = []
+    nr = args.range_requests
+    for k in range(max(nr, len(reqs) - nr)):
+        if k < nr:
+            order.append(k)
+        if nr + k < len(reqs):
+            order.append(nr + k)
+    # calibrate on a small prefix, then size the sample to ~cpu_seconds
+    def run(req_ids):
+        pl = [payloads[j] for r in req_ids for j in by_req[r]]
+        t = time.perf_counter()
+        res = orc.perform_query_batch(pl, patched=True, threads=threads, want_results=False)
+        return time.perf_counter() - t, len(pl), res
+    dt, _, _ = run(order[:100])
+    if dt * len(order) / 100 > args.cpu_seconds:  # bigger than the budget: a prefix sample
+        m = int(min(len(order), max(100, 100 * args.cpu_seconds / max(dt, 1e-6))))
+        dt, npl, _ = run(order[:m])
+        passes, done = 1, m
+        sample = f'first {m} of {len(reqs)} requests (interleaved range/point; {npl} slice payloads)'
+    else:  # the whole workload is cheaper than the budget: repeat full passes
+        total, passes, npl = 0.0, 0, 0
+        while total < args.cpu_seconds and passes < 10000:
+            d, npl, _ = run(order)
+            total += d
+            passes += 1
+        dt, done = total, passes * len(order)
+        sample = f'all {len(reqs)} requests ({npl} slice payloads) x {passes} passes'
+    cpu = {'value': round(done / dt, 1), 'unit': 'requests/s', 'cores': threads, 'kind': 'port',
+           'sample': sample + f' through oracle/sbeacon_oracle.c (CPU restatement of search_variants.py), '
+                              f'OpenMP x{threads}, sites-only VCF text (config-2 queries read no GT)',
+           'seconds': round(dt, 2), 'host_cpus': os.cpu_count()}
+    # parity: device answers vs oracle for a sample of requests
+    chk = order[:args.parity_requests]
+    idx = [j for r in chk for j in by_req[r]]
+    exp = orc.perform_query_batch([payloads[j] for j in idx], patched=True, threads=threads)
+    bad = 0
+    for j, e in zip(idx, exp):
+        try:
+            g = rs.response(j).dump()
+        except Exception as ex:  # noqa: BLE001
+            g = type(ex)
+        if isinstance(e, type) or isinstance(g, type):
+            bad += int(e is not g)
+        else:
+            g['sample_indices'] = sorted(g['sample_indices'])
+            e['sample_indices'] = sorted(e['sample_indices'])
+            bad += int(g != e)
+    parity = {'requests': len(chk), 'slice_queries': len(idx), 'mismatches': bad,
+              'variants_checked': int(sum(len(e['variants']) for e in exp if isinstance(e, dict)))}
+    orc.close()
+    try:
+        os.remove(path)
+        os.rmdir(tmp)
+    except OSError:
+        pass
+    return cpu, parity
+
+
+if __name__ == '__main__':
+    main()

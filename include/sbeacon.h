@@ -1,0 +1,173 @@
+/*
+ * sbeacon.h — C ABI of the MI355X-native sBeacon variant-query engine
+ * (libsbeacon_hip.so).
+ *
+ * Drop-in boundary for the reference's genomic-variant query path
+ * (SURVEY.md §8b).  In the reference, each performQuery Lambda shells out to
+ * `bcftools query --regions chrom:a-b ...` and filters the text in a Python
+ * loop (lambda/performQuery/search_variants.py:33-271,
+ * search_variants_in_samples.py:31-259).  Here the VCFs are ingested once into
+ * a position-sorted columnar store resident in HBM and every slice query of a
+ * request is answered by one batched HIP launch sequence.
+ *
+ * Conventions: every function returns 0 on success or a negative SB_E* code;
+ * sb_last_error() then holds a thread-local message.  Strings are
+ * (pointer, length) pairs — no NUL requirement.  The library owns everything
+ * it returns until the matching *_free call.  Inputs are borrowed for the
+ * duration of the call.  All entry points are re-entrant; concurrent queries
+ * on one store are serialised per device internally.
+ */
+#ifndef SBEACON_H
+#define SBEACON_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SB_ABI_VERSION 1
+
+/* ---- error codes ------------------------------------------------------- */
+enum {
+    SB_OK = 0,
+    SB_EINVAL = -1,     /* malformed argument / payload */
+    SB_ENOSTORE = -2,   /* unknown vcf id / store not built */
+    SB_EHIP = -3,       /* HIP runtime failure */
+    SB_EIO = -4,        /* file / decompression failure */
+    SB_EPARSE = -5,     /* VCF text the store cannot represent exactly */
+    SB_ENOMEM = -6,
+};
+
+/* per-query error: the Python exception the reference raises on this input
+ * (sb_result_view.error); the query's other fields are then undefined */
+enum {
+    SB_QERR_NONE = 0,
+    SB_QERR_UNBOUND_LOCAL = 1, /* search_variants.py:101 (variantType, strict mode) */
+    SB_QERR_INDEX = 2,         /* search_variants.py:207 / :223 */
+    SB_QERR_VALUE = 3,         /* search_variants.py:199 int(AN) / :206 int(AC) */
+    SB_QERR_ATTRIBUTE = 4,     /* search_variants_in_samples.py:89 None.replace */
+    SB_QERR_UNSUPPORTED = 9,   /* regex metacharacters in referenceBases */
+};
+
+enum { SB_GRAN_BOOLEAN = 0, SB_GRAN_COUNT = 1, SB_GRAN_AGGREGATED = 2, SB_GRAN_RECORD = 3 };
+
+const char *sb_last_error(void);
+int sb_abi_version(void);
+
+/* ---- store build (ingest) ---------------------------------------------- */
+/* Replaces: the VCF-on-S3 + CSI/TBI + bcftools region retrieval the reference
+ * performs per slice (search_variants.py:42-50; init.sh:73-91 builds htslib). */
+typedef struct sb_builder sb_builder;
+typedef struct sb_store sb_store;
+
+typedef struct {
+    int32_t keep_genotypes; /* build per-alt carrier bitplanes (sample path) */
+    int32_t n_threads;      /* host parse threads (0 = all) */
+} sb_build_opts;
+
+int sb_builder_new(const sb_build_opts *opts, sb_builder **out);
+/* register one VCF; `location` is the string payloads carry as vcf_location */
+int sb_builder_begin_vcf(sb_builder *b, const char *location, size_t location_len, uint32_t *vcf_id);
+/* feed VCF text (header and/or whole records; chunks must end on '\n') */
+int sb_builder_add_text(sb_builder *b, uint32_t vcf_id, const char *text, size_t len);
+/* convenience: plain or gzip/BGZF file from disk (zlib) */
+int sb_builder_add_file(sb_builder *b, uint32_t vcf_id, const char *path);
+/* upload to device `device` (HIP ordinal) and return an immutable store */
+int sb_builder_finish(sb_builder *b, int device, sb_store **out);
+void sb_builder_free(sb_builder *b);
+void sb_store_close(sb_store *s);
+
+typedef struct {
+    uint64_t n_records;
+    uint64_t n_alt_rows;
+    uint32_t n_vcfs;
+    uint32_t n_segments; /* (vcf, contig) position-sorted segments */
+    uint64_t device_bytes;
+    uint32_t max_samples;
+    int32_t device;
+} sb_store_info;
+int sb_store_get_info(const sb_store *s, sb_store_info *out);
+/* vcf id for a vcf_location string, or SB_ENOSTORE */
+int sb_store_find_vcf(const sb_store *s, const char *location, size_t len, uint32_t *vcf_id);
+int sb_store_n_samples(const sb_store *s, uint32_t vcf_id, uint32_t *n);
+/* header-order sample name i of a VCF */
+int sb_store_sample_name(const sb_store *s, uint32_t vcf_id, uint32_t i, const char **p, size_t *len);
+
+/* ---- query batch --------------------------------------------------------
+ * One sb_query = one PerformQueryPayload
+ * (shared_resources/payloads/lambda_payloads.py:46-77) after splitQuery has
+ * cut the request into 10 kb slices (lambda/splitQuery/lambda_function.py:74-110).
+ * Strings: ptr == NULL means Python None. */
+typedef struct {
+    uint32_t vcf_id;
+    uint32_t _pad0;
+    const char *region; size_t region_len; /* "chrom:a-b" exactly as in the payload */
+    int64_t end_min, end_max;
+    const char *reference_bases; size_t reference_len;
+    const char *alternate_bases; size_t alternate_len;
+    const char *variant_type; size_t variant_type_len;
+    int64_t variant_min_length, variant_max_length; /* max < 0 = infinity */
+    uint8_t granularity;           /* SB_GRAN_* */
+    uint8_t include_details;       /* splitQuery: includeResultsetResponses in {HIT, ALL} */
+    uint8_t include_samples;       /* passthrough.includeSamples */
+    uint8_t selected_samples_only; /* passthrough.selectedSamplesOnly -> samples variant */
+    uint8_t strict_variant_type;   /* 1 = reproduce the reference's UnboundLocalError */
+    uint8_t _pad1[3];
+    const char *sample_names; size_t sample_names_len; /* ','-joined passthrough.sampleNames, NULL = ['_'] */
+} sb_query;
+
+typedef struct sb_result_set sb_result_set;
+
+/* Runs the whole batch on the store's device.  Results stay valid until
+ * sb_result_free. */
+int sb_query_batch(sb_store *s, const sb_query *q, size_t nq, uint32_t flags, sb_result_set **out);
+
+typedef struct {
+    int32_t error;      /* SB_QERR_* */
+    int32_t exists;
+    int64_t call_count;
+    int64_t all_alleles_count;
+    uint64_t n_variants;      /* hits = (record, alt) pairs, reference order */
+    const uint32_t *hit_record; /* global record ids */
+    const uint32_t *hit_alt;    /* alt index used for the label (0-based) */
+    uint64_t n_sample_indices;  /* indices into the emitted sample list */
+    const uint32_t *sample_indices;
+} sb_result_view;
+
+int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out);
+/* Reference-format strings for query i: variants '\n'-joined
+ * (f'{chrom}\t{POS}\t{REF}\t{ALT}\t{VT}', search_variants.py:210) and
+ * sample names ','-joined.  Pointers valid until sb_result_free. */
+int sb_result_variants_text(sb_result_set *r, size_t i, const char **p, size_t *len);
+int sb_result_sample_names_text(sb_result_set *r, size_t i, const char **p, size_t *len);
+
+typedef struct {
+    uint64_t n_queries;
+    uint64_t records_scanned; /* records with POS inside each slice, summed */
+    uint64_t hits;
+    double device_ms;         /* HIP-event time of the kernel sequence */
+} sb_batch_stats;
+int sb_result_stats(const sb_result_set *r, sb_batch_stats *out);
+void sb_result_free(sb_result_set *r);
+
+/* ---- device-resident batch (benchmarks / fused pipelines) ----------------
+ * Upload a batch once, then launch the query kernels repeatedly on the
+ * store's stream with inputs already resident in HBM. */
+typedef struct sb_batch sb_batch;
+int sb_batch_prepare(sb_store *s, const sb_query *q, size_t nq, sb_batch **out);
+int sb_batch_run(sb_batch *b);               /* enqueue only (async) */
+int sb_batch_sync(sb_batch *b);              /* wait for the store stream */
+/* average per-launch device times (ms) over every sb_batch_run since the
+ * previous sync, measured with hipEvents on the launch stream: whole
+ * sequence, bounds + capacity prefix sum, range-scan kernel */
+int sb_batch_last_timing(const sb_batch *b, double *total_ms, double *scan_ms, double *bounds_ms);
+int sb_batch_get_stats(const sb_batch *b, sb_batch_stats *out);
+int sb_batch_fetch(sb_batch *b, sb_result_set **out); /* D2H + host views */
+void sb_batch_free(sb_batch *b);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SBEACON_H */

@@ -1,0 +1,826 @@
+// api.cpp — the C ABI (include/sbeacon.h): builder, HBM store, query batches.
+//
+// The query path mirrors one splitQuery fan-out (lambda/splitQuery/
+// lambda_function.py:74-110) handed to the device as ONE batch: every
+// PerformQueryPayload becomes a QDev, and the kernel sequence
+//   bounds (64-ary lower_bound) -> caps prefix sum -> range scan -> hit
+//   prefix sum -> dense compaction
+// runs on the store's HIP stream.  Result strings are formatted on the host
+// from the store's allele blob in the reference's exact format.
+#include <algorithm>
+#include <array>
+#include <cstdio>
+#include <memory>
+#include <thread>
+
+#include "kernels.hpp"
+#include "store.hpp"
+
+namespace sb {
+void builder_add_text(sb_builder &b, uint32_t vcf_id, const char *text, size_t len);
+void builder_add_file(sb_builder &b, uint32_t vcf_id, const char *path);
+void builder_flush(sb_builder &b, uint32_t vcf_id);
+
+namespace {
+thread_local std::string g_last_error;
+
+#define HIP_OK(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            throw ::sb::Error(SB_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));            \
+    } while (0)
+
+template <class F>
+int guard(F &&f) {
+    try {
+        f();
+        return SB_OK;
+    } catch (const Error &e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        set_last_error("out of host memory");
+        return SB_ENOMEM;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return SB_EINVAL;
+    }
+}
+
+template <class T>
+T *dev_upload(sb_store &s, const std::vector<T> &v) {
+    DeviceBuffer b;
+    b.bytes = std::max<size_t>(v.size() * sizeof(T), 16);
+    HIP_OK(hipMalloc(&b.p, b.bytes));
+    if (!v.empty()) HIP_OK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s.stream));
+    s.bufs.push_back(b);
+    s.device_bytes += b.bytes;
+    return static_cast<T *>(b.p);
+}
+
+struct DevMem {  // RAII device allocation for batches
+    void *p = nullptr;
+    size_t bytes = 0;
+    void alloc(size_t n) {
+        release();
+        bytes = std::max<size_t>(n, 16);
+        HIP_OK(hipMalloc(&p, bytes));
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T>
+    T *as() const { return static_cast<T *>(p); }
+    ~DevMem() { release(); }
+};
+
+
+struct ParsedRegion {
+    std::string chrom;
+    int64_t first = 0, last = 0;
+    bool ok = false;
+};
+
+// search_variants.py:56-58 — chrom up to the first ':', first_bp up to the
+// first '-', last_bp after it (Python int()).
+ParsedRegion parse_region(const char *p, size_t n) {
+    ParsedRegion r;
+    const std::string s(p, n);
+    const size_t c = s.find(':'), d = s.find('-');
+    if (c == std::string::npos || d == std::string::npos || d < c) return r;
+    r.chrom = s.substr(0, c);
+    if (!py_int(s.data() + c + 1, d - c - 1, &r.first)) return r;
+    if (!py_int(s.data() + d + 1, s.size() - d - 1, &r.last)) return r;
+    r.ok = true;
+    return r;
+}
+
+bool starts(const std::string &s, const char *pre) { return s.compare(0, strlen(pre), pre) == 0; }
+
+// Host-side evaluation of the symbolic-ALT predicates of :101-166 for one
+// variantType string over the store's symbolic dictionary.
+std::vector<uint32_t> sym_lut(const sb_store &s, uint32_t kind, const std::string &vprefix) {
+    std::vector<uint32_t> lut((s.sym.items.size() + 31) / 32 + 1, 0u);
+    for (size_t i = 0; i < s.sym.items.size(); ++i) {
+        const std::string &a = s.sym.items[i];
+        bool ok = starts(a, vprefix.c_str());
+        switch (kind) {
+            case VT_DEL: ok = ok || a == "<CN0>"; break;
+            case VT_DUP: ok = ok || (starts(a, "<CN") && a != "<CN0>" && a != "<CN1>"); break;
+            case VT_DUPT: ok = ok || a == "<CN2>"; break;
+            case VT_CNV: ok = ok || starts(a, "<CN") || starts(a, "<DEL") || starts(a, "<DUP"); break;
+            default: break;
+        }
+        if (ok) lut[i / 32] |= 1u << (i % 32);
+    }
+    return lut;
+}
+
+}  // namespace
+
+void set_last_error(const std::string &msg) { g_last_error = msg; }
+const char *last_error_cstr() { return g_last_error.c_str(); }
+
+}  // namespace sb
+
+using namespace sb;
+
+sb_store::~sb_store() {
+    if (device >= 0) (void)hipSetDevice(device);
+    for (auto &b : bufs) (void)hipFree(b.p);
+    if (stream) (void)hipStreamDestroy(stream);
+}
+
+// ------------------------------------------------------------------ batch
+struct sb_batch {
+    sb_store *s = nullptr;
+    uint32_t nq = 0;
+    std::vector<QDev> hq;
+    std::vector<int32_t> host_err;         // errors raised before any record is read
+    std::vector<std::string> chrom;        // region chrom per query (variant strings)
+    std::vector<std::vector<uint32_t>> emitted;  // header indices of the emitted samples
+    std::vector<uint8_t> samples_variant;
+    std::vector<uint32_t> vcf;
+    uint64_t cap_total = 0, samples_words = 0;
+    DevMem q, qbytes, subsets, lut, lohi, caps, hit_off, scan_tmp, hit_rec, hit_alt, res, nhits, dense_off,
+        dense_rec, dense_alt, samples_out;
+    // one event quad per run since the last sync: start, after bounds+caps
+    // scan, after the range scan, end.  sync() averages them.
+    std::vector<std::array<hipEvent_t, 4>> ev;
+    size_t runs_pending = 0;
+    float last_total_ms = 0, last_scan_ms = 0, last_bounds_ms = 0;
+    uint64_t runs_timed = 0;
+    bool ran = false;
+    ~sb_batch() {
+        for (auto &q : ev)
+            for (auto &e : q)
+                if (e) (void)hipEventDestroy(e);
+    }
+};
+
+struct sb_result_set {
+    sb_store *s = nullptr;
+    std::vector<QRes> res;
+    std::vector<uint64_t> dense_off;
+    std::vector<uint32_t> rec, alt;
+    std::vector<std::vector<uint32_t>> sidx;   // emitted-list positions
+    std::vector<std::vector<uint32_t>> emitted;
+    std::vector<uint32_t> vcf_of;
+    std::vector<uint8_t> samples_variant;
+    std::vector<std::string> chrom;
+    std::vector<std::string> vtext, ntext;
+    std::vector<uint8_t> vbuilt, nbuilt;
+    sb_batch_stats stats{};
+};
+
+
+namespace {
+
+void upload_store(sb_builder &b, sb_store &s) {
+    std::vector<uint32_t> pos, end, meta, alt_lo, alt_len, alt_cls, fb;
+    std::vector<int32_t> an, ac;
+    std::vector<uint64_t> ref_key, ref_off, alt_key, alt_off, planes;
+    std::vector<int64_t> fb_off;
+    std::vector<uint8_t> blob;
+    uint64_t nr = 0, na = 0;
+    for (auto &v : b.vcfs) {
+        nr += v.c.pos.size();
+        na += v.c.alt_key.size();
+    }
+    if (nr >= 0xffffffffull || na >= 0xffffffffull) throw Error(SB_EINVAL, "store exceeds 2^32 records/alt rows per device; shard it");
+    pos.reserve(nr);
+    end.reserve(nr);
+    meta.reserve(nr);
+    an.reserve(nr);
+    ref_key.reserve(nr);
+    ref_off.reserve(nr);
+    fb_off.reserve(nr);
+    alt_lo.reserve(nr + 1);
+    alt_key.reserve(na);
+    alt_len.reserve(na);
+    alt_cls.reserve(na);
+    ac.reserve(na);
+    alt_off.reserve(na);
+    for (auto &v : b.vcfs) {
+        VcfCols &c = v.c;
+        const uint32_t rec_base = static_cast<uint32_t>(pos.size());
+        const uint32_t alt_base = static_cast<uint32_t>(alt_key.size());
+        const uint64_t blob_base = blob.size();
+        const int64_t fb_base = static_cast<int64_t>(fb.size());
+        v.rec_base = rec_base;
+        v.alt_base = alt_base;
+        v.plane_base = planes.size();
+        const size_t n = c.pos.size();
+        pos.insert(pos.end(), c.pos.begin(), c.pos.end());
+        end.insert(end.end(), c.end.begin(), c.end.end());
+        meta.insert(meta.end(), c.meta.begin(), c.meta.end());
+        an.insert(an.end(), c.an.begin(), c.an.end());
+        ref_key.insert(ref_key.end(), c.ref_key.begin(), c.ref_key.end());
+        for (size_t i = 0; i < n; ++i) ref_off.push_back(c.ref_off[i] + blob_base);
+        for (size_t i = 0; i < n; ++i) fb_off.push_back(c.fb_off[i] < 0 ? -1 : c.fb_off[i] + fb_base);
+        for (size_t i = 0; i < n; ++i) alt_lo.push_back(c.alt_lo[i] + alt_base);
+        alt_key.insert(alt_key.end(), c.alt_key.begin(), c.alt_key.end());
+        alt_len.insert(alt_len.end(), c.alt_len.begin(), c.alt_len.end());
+        alt_cls.insert(alt_cls.end(), c.alt_cls.begin(), c.alt_cls.end());
+        ac.insert(ac.end(), c.ac.begin(), c.ac.end());
+        for (size_t i = 0; i < c.alt_off.size(); ++i) alt_off.push_back(c.alt_off[i] + blob_base);
+        blob.insert(blob.end(), c.blob.begin(), c.blob.end());
+        planes.insert(planes.end(), c.planes.begin(), c.planes.end());
+        fb.insert(fb.end(), c.fb.begin(), c.fb.end());
+        for (auto &sg : v.segments) {
+            sg.lo += rec_base;
+            sg.hi += rec_base;
+        }
+        s.max_words = std::max(s.max_words, c.planes.empty() ? 0u : v.words);
+        c = VcfCols();  // release the per-vcf copy
+    }
+    alt_lo.push_back(static_cast<uint32_t>(alt_key.size()));
+    s.n_records = pos.size();
+    s.n_alt = alt_key.size();
+
+    s.d.pos = dev_upload(s, pos);
+    s.d.end = dev_upload(s, end);
+    s.d.ref_key = dev_upload(s, ref_key);
+    s.d.meta = dev_upload(s, meta);
+    s.d.an = dev_upload(s, an);
+    s.d.alt_lo = dev_upload(s, alt_lo);
+    s.d.ref_off = dev_upload(s, ref_off);
+    s.d.fb_off = dev_upload(s, fb_off);
+    s.d.alt_key = dev_upload(s, alt_key);
+    s.d.alt_len = dev_upload(s, alt_len);
+    s.d.alt_cls = dev_upload(s, alt_cls);
+    s.d.ac = dev_upload(s, ac);
+    s.d.alt_off = dev_upload(s, alt_off);
+    s.d.blob = dev_upload(s, blob);
+    s.d.planes = dev_upload(s, planes);
+    s.d.fb = dev_upload(s, fb);
+    HIP_OK(hipStreamSynchronize(s.stream));
+    // host copies for result formatting
+    s.h_pos = std::move(pos);
+    s.h_end = std::move(end);
+    s.h_meta = std::move(meta);
+    s.h_ref_off = std::move(ref_off);
+    s.h_alt_off = std::move(alt_off);
+    s.h_alt_len = std::move(alt_len);
+    s.h_alt_lo = std::move(alt_lo);
+    s.h_blob = std::move(blob);
+}
+
+const char *kRegexMeta = "^$*+?{}[]\\|()";
+
+void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
+    sb_store &s = *B.s;
+    if (nq >= (1u << 31)) throw Error(SB_EINVAL, "batch too large");
+    B.nq = static_cast<uint32_t>(nq);
+    B.hq.assign(nq, QDev{});
+    B.host_err.assign(nq, 0);
+    B.chrom.assign(nq, std::string());
+    B.emitted.assign(nq, std::vector<uint32_t>());
+    B.samples_variant.assign(nq, 0);
+    B.vcf.assign(nq, 0);
+    std::vector<uint8_t> qbytes;
+    std::vector<uint64_t> subsets;
+    std::vector<uint32_t> lut_all;
+    std::unordered_map<std::string, uint32_t> lut_cache;
+    uint64_t samples_words = 0;
+    for (size_t i = 0; i < nq; ++i) {
+        const sb_query &x = qs[i];
+        QDev &d = B.hq[i];
+        d.subset_off = ~0ull;
+        d.samples_out_off = ~0ull;
+        if (x.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "query " + std::to_string(i) + ": unknown vcf id");
+        const VcfData &v = s.vcfs[x.vcf_id];
+        B.vcf[i] = x.vcf_id;
+        if (!x.region) throw Error(SB_EINVAL, "query " + std::to_string(i) + ": region is NULL");
+        const ParsedRegion rg = parse_region(x.region, x.region_len);
+        B.chrom[i] = rg.chrom;
+        if (!rg.ok) {
+            B.host_err[i] = SB_QERR_VALUE;  // int() of the region bounds (:56-57)
+            d.flags |= F_EMPTY;
+        }
+        d.first_bp = rg.first;
+        d.last_bp = rg.last;
+        auto it = v.seg_index.find(rg.chrom);
+        if (it == v.seg_index.end()) {
+            d.flags |= F_EMPTY;
+            d.seg_lo = d.seg_hi = 0;
+        } else {
+            d.seg_lo = v.segments[it->second].lo;
+            d.seg_hi = v.segments[it->second].hi;
+        }
+        d.end_min = x.end_min;
+        d.end_max = x.end_max;
+        const bool samples_variant = x.selected_samples_only != 0;
+        B.samples_variant[i] = samples_variant;
+        const uint32_t n_samples = static_cast<uint32_t>(v.samples.size());
+        d.words = v.words;
+        d.n_samples = n_samples;
+        d.alt_base = v.alt_base;
+        d.plane_base = v.plane_base;
+        if (samples_variant) {  // bcftools --samples (svs:36-42), header order
+            const std::string names = x.sample_names ? std::string(x.sample_names, x.sample_names_len) : std::string("_");
+            std::vector<uint8_t> sel(n_samples, 0);
+            size_t p = 0;
+            for (;;) {
+                const size_t c = names.find(',', p);
+                const std::string nm = names.substr(p, c == std::string::npos ? std::string::npos : c - p);
+                bool found = false;
+                for (uint32_t k = 0; k < n_samples; ++k)
+                    if (v.samples[k] == nm) {
+                        sel[k] = 1;
+                        found = true;
+                    }
+                if (!found) d.flags |= F_EMPTY;  // unknown sample: bcftools exits, no output
+                if (c == std::string::npos) break;
+                p = c + 1;
+            }
+            d.subset_off = subsets.size();
+            subsets.resize(subsets.size() + std::max(1u, v.words), 0ull);
+            for (uint32_t k = 0; k < n_samples; ++k)
+                if (sel[k]) {
+                    B.emitted[i].push_back(k);
+                    subsets[d.subset_off + (k >> 6)] |= 1ull << (k & 63);
+                }
+        }
+        // REF predicate (:59, :94 / svs:87-91)
+        d.qbytes_off = static_cast<uint32_t>(qbytes.size());
+        if (!x.reference_bases) {
+            if (samples_variant) {
+                d.ref_mode = REF_ERROR;
+                d.ref_err = SB_QERR_ATTRIBUTE;
+            } else {
+                d.ref_mode = REF_NEVER;
+            }
+        } else {
+            const std::string rb(x.reference_bases, x.reference_len);
+            d.ref_len = static_cast<uint32_t>(rb.size());
+            qbytes.insert(qbytes.end(), rb.begin(), rb.end());
+            if (rb == "N") {
+                d.ref_mode = REF_ANY;
+            } else if (samples_variant && rb.find_first_of(kRegexMeta) != std::string::npos) {
+                d.ref_mode = REF_ERROR;
+                d.ref_err = SB_QERR_UNSUPPORTED;
+            } else if (samples_variant && rb.find_first_of("N.") != std::string::npos) {
+                d.ref_mode = REF_WILD;
+            } else {
+                d.ref_mode = REF_EXACT;
+                bool h;
+                d.ref_key = allele_key(reinterpret_cast<const uint8_t *>(rb.data()), rb.size(), false, &h);
+            }
+        }
+        // ALT predicate (:100-183)
+        if (!x.alternate_bases) {
+            d.alt_mode = ALT_VTYPE;
+            if (x.strict_variant_type) d.flags |= F_STRICT_UNBOUND;
+            const std::string vt = x.variant_type ? std::string(x.variant_type, x.variant_type_len) : std::string("None");
+            const bool has = x.variant_type != nullptr;
+            d.vt_kind = !has ? VT_OTHER
+                        : vt == "DEL" ? VT_DEL
+                        : vt == "INS" ? VT_INS
+                        : vt == "DUP" ? VT_DUP
+                        : vt == "DUP:TANDEM" ? VT_DUPT
+                        : vt == "CNV" ? VT_CNV
+                                      : VT_OTHER;
+            const std::string key = std::to_string(d.vt_kind) + "|" + vt;
+            auto lt = lut_cache.find(key);
+            if (lt == lut_cache.end()) {
+                const auto lut = sym_lut(s, d.vt_kind, "<" + vt);
+                const uint32_t off = static_cast<uint32_t>(lut_all.size());
+                lut_all.insert(lut_all.end(), lut.begin(), lut.end());
+                lt = lut_cache.emplace(key, off).first;
+            }
+            d.lut_off = lt->second;
+        } else {
+            const std::string ab(x.alternate_bases, x.alternate_len);
+            d.alt_len = static_cast<uint32_t>(ab.size());
+            qbytes.insert(qbytes.end(), ab.begin(), ab.end());
+            if (ab == "N") {
+                d.alt_mode = ALT_N;
+            } else {
+                d.alt_mode = ALT_EXACT;
+                bool h;
+                d.alt_key = allele_key(reinterpret_cast<const uint8_t *>(ab.data()), ab.size(), false, &h);
+            }
+        }
+        d.vmin = x.variant_min_length;
+        d.vmax = x.variant_max_length < 0 ? INT64_MAX : x.variant_max_length;
+        if (x.include_details) d.flags |= F_DETAILS;
+        if (samples_variant) d.flags |= F_SAMPLES_VARIANT;
+        if (x.granularity == SB_GRAN_BOOLEAN && !samples_variant) d.flags |= F_BOOL_BREAK;
+        const bool collect = (x.granularity == SB_GRAN_RECORD || x.granularity == SB_GRAN_AGGREGATED) &&
+                             (samples_variant || x.include_samples);
+        if (collect) {
+            d.flags |= F_COLLECT;
+            if (x.include_details && v.words) {
+                if (s.max_words == 0) throw Error(SB_EINVAL, "sample path requested but the store was built without genotypes");
+                d.samples_out_off = samples_words;
+                samples_words += v.words;
+            }
+        }
+    }
+    B.samples_words = samples_words;
+    if (lut_all.empty()) lut_all.push_back(0);
+    // ---- device buffers
+    HIP_OK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    B.q.alloc(nq * sizeof(QDev));
+    B.qbytes.alloc(qbytes.size());
+    B.subsets.alloc(subsets.size() * 8);
+    B.lut.alloc(lut_all.size() * 4);
+    if (nq) HIP_OK(hipMemcpyAsync(B.q.p, B.hq.data(), nq * sizeof(QDev), hipMemcpyHostToDevice, st));
+    if (!qbytes.empty()) HIP_OK(hipMemcpyAsync(B.qbytes.p, qbytes.data(), qbytes.size(), hipMemcpyHostToDevice, st));
+    if (!subsets.empty()) HIP_OK(hipMemcpyAsync(B.subsets.p, subsets.data(), subsets.size() * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(B.lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
+    B.lohi.alloc(size_t(nq) * 8);
+    B.caps.alloc(size_t(nq) * 4);
+    B.hit_off.alloc((size_t(nq) + 1) * 8);
+    B.dense_off.alloc((size_t(nq) + 1) * 8);
+    B.scan_tmp.alloc(scan_tmp_words(static_cast<uint32_t>(nq)) * 8 + 64);
+    B.res.alloc(size_t(nq) * sizeof(QRes));
+    B.nhits.alloc(size_t(nq) * 4);
+    B.samples_out.alloc(samples_words * 8);
+    // size the hit buffers: bounds + capacity prefix sum, then one 8-byte readback
+    DStore d = s.d;
+    d.sym_lut = B.lut.as<uint32_t>();
+    launch_bounds(d, B.q.as<QDev>(), B.nq, B.lohi.as<uint32_t>(), B.caps.as<uint32_t>(), st);
+    launch_exclusive_scan(B.caps.as<uint32_t>(), B.nq, B.hit_off.as<uint64_t>(), B.scan_tmp.as<uint64_t>(), st);
+    HIP_OK(hipGetLastError());
+    uint64_t total = 0;
+    HIP_OK(hipMemcpyAsync(&total, B.hit_off.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    B.cap_total = total;
+    B.hit_rec.alloc(total * 4);
+    B.hit_alt.alloc(total * 4);
+    B.dense_rec.alloc(total * 4);
+    B.dense_alt.alloc(total * 4);
+}
+
+void run(sb_batch &B) {
+    sb_store &s = *B.s;
+    HIP_OK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    DStore d = s.d;
+    d.sym_lut = B.lut.as<uint32_t>();
+    const uint32_t nq = B.nq;
+    if (B.runs_pending == B.ev.size()) {
+        std::array<hipEvent_t, 4> q{};
+        for (auto &e : q) HIP_OK(hipEventCreate(&e));
+        B.ev.push_back(q);
+    }
+    const auto &E = B.ev[B.runs_pending++];
+    HIP_OK(hipEventRecord(E[0], st));
+    launch_bounds(d, B.q.as<QDev>(), nq, B.lohi.as<uint32_t>(), B.caps.as<uint32_t>(), st);
+    launch_exclusive_scan(B.caps.as<uint32_t>(), nq, B.hit_off.as<uint64_t>(), B.scan_tmp.as<uint64_t>(), st);
+    HIP_OK(hipEventRecord(E[1], st));
+    launch_scan(d, B.q.as<QDev>(), nq, B.lohi.as<uint32_t>(), B.hit_off.as<uint64_t>(), B.qbytes.as<uint8_t>(),
+                B.subsets.as<uint64_t>(), s.max_words, B.res.as<QRes>(), B.nhits.as<uint32_t>(),
+                B.hit_rec.as<uint32_t>(), B.hit_alt.as<uint32_t>(), B.samples_out.as<uint64_t>(), st);
+    HIP_OK(hipEventRecord(E[2], st));
+    launch_exclusive_scan(B.nhits.as<uint32_t>(), nq, B.dense_off.as<uint64_t>(), B.scan_tmp.as<uint64_t>(), st);
+    launch_compact(B.hit_off.as<uint64_t>(), B.dense_off.as<uint64_t>(), B.nhits.as<uint32_t>(), nq,
+                   B.hit_rec.as<uint32_t>(), B.hit_alt.as<uint32_t>(), B.dense_rec.as<uint32_t>(),
+                   B.dense_alt.as<uint32_t>(), st);
+    HIP_OK(hipEventRecord(E[3], st));
+    HIP_OK(hipGetLastError());
+    B.ran = true;
+}
+
+void sync(sb_batch &B) {
+    HIP_OK(hipSetDevice(B.s->device));
+    HIP_OK(hipStreamSynchronize(B.s->stream));
+    if (B.runs_pending) {
+        double t = 0, b = 0, sc = 0;
+        for (size_t i = 0; i < B.runs_pending; ++i) {
+            float x;
+            HIP_OK(hipEventElapsedTime(&x, B.ev[i][0], B.ev[i][3]));
+            t += x;
+            HIP_OK(hipEventElapsedTime(&x, B.ev[i][0], B.ev[i][1]));
+            b += x;
+            HIP_OK(hipEventElapsedTime(&x, B.ev[i][1], B.ev[i][2]));
+            sc += x;
+        }
+        const double n = static_cast<double>(B.runs_pending);
+        B.last_total_ms = static_cast<float>(t / n);
+        B.last_bounds_ms = static_cast<float>(b / n);
+        B.last_scan_ms = static_cast<float>(sc / n);
+        B.runs_timed = B.runs_pending;
+        B.runs_pending = 0;
+    }
+}
+
+sb_result_set *fetch(sb_batch &B) {
+    sync(B);
+    sb_store &s = *B.s;
+    hipStream_t st = s.stream;
+    auto R = std::make_unique<sb_result_set>();
+    R->s = &s;
+    const uint32_t nq = B.nq;
+    R->res.resize(nq);
+    R->dense_off.resize(size_t(nq) + 1);
+    if (nq) HIP_OK(hipMemcpyAsync(R->res.data(), B.res.p, nq * sizeof(QRes), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(R->dense_off.data(), B.dense_off.p, (size_t(nq) + 1) * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    const uint64_t total = R->dense_off[nq];
+    R->rec.resize(total);
+    R->alt.resize(total);
+    std::vector<uint64_t> sout(B.samples_words);
+    if (total) {
+        HIP_OK(hipMemcpyAsync(R->rec.data(), B.dense_rec.p, total * 4, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipMemcpyAsync(R->alt.data(), B.dense_alt.p, total * 4, hipMemcpyDeviceToHost, st));
+    }
+    if (!sout.empty()) HIP_OK(hipMemcpyAsync(sout.data(), B.samples_out.p, sout.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    R->sidx.assign(nq, std::vector<uint32_t>());
+    R->emitted = B.emitted;
+    R->chrom = B.chrom;
+    R->vcf_of.resize(nq);
+    uint64_t scanned = 0;
+    for (uint32_t i = 0; i < nq; ++i) {
+        const QDev &d = B.hq[i];
+        if (B.host_err[i]) R->res[i].error = B.host_err[i];
+        scanned += R->res[i].n_scanned;
+        if (d.samples_out_off != ~0ull && !R->res[i].error) {
+            const uint64_t *w = sout.data() + d.samples_out_off;
+            if (B.samples_variant[i]) {
+                const auto &em = B.emitted[i];
+                for (uint32_t j = 0; j < em.size(); ++j)
+                    if ((w[em[j] >> 6] >> (em[j] & 63)) & 1) R->sidx[i].push_back(j);
+            } else {
+                for (uint32_t h = 0; h < d.n_samples; ++h)
+                    if ((w[h >> 6] >> (h & 63)) & 1) R->sidx[i].push_back(h);
+            }
+        }
+    }
+    R->vcf_of = B.vcf;
+    R->samples_variant = B.samples_variant;
+    R->vtext.assign(nq, std::string());
+    R->ntext.assign(nq, std::string());
+    R->vbuilt.assign(nq, 0);
+    R->nbuilt.assign(nq, 0);
+    R->stats.n_queries = nq;
+    R->stats.records_scanned = scanned;
+    R->stats.hits = total;
+    R->stats.device_ms = B.last_total_ms;
+    return R.release();
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *sb_last_error(void) { return sb::last_error_cstr(); }
+int sb_abi_version(void) { return SB_ABI_VERSION; }
+
+int sb_builder_new(const sb_build_opts *opts, sb_builder **out) {
+    return guard([&] {
+        if (!out) throw Error(SB_EINVAL, "out is NULL");
+        auto b = std::make_unique<sb_builder>();
+        if (opts) {
+            b->opts = *opts;
+        } else {
+            b->opts.keep_genotypes = 1;
+            b->opts.n_threads = 0;
+        }
+        b->vt.get("N/A");
+        *out = b.release();
+    });
+}
+
+int sb_builder_begin_vcf(sb_builder *b, const char *location, size_t len, uint32_t *vcf_id) {
+    return guard([&] {
+        if (!b || !location || !vcf_id) throw Error(SB_EINVAL, "NULL argument");
+        const std::string loc(location, len);
+        for (const auto &v : b->vcfs)
+            if (v.location == loc) throw Error(SB_EINVAL, "duplicate vcf location " + loc);
+        b->vcfs.emplace_back();
+        b->vcfs.back().location = loc;
+        *vcf_id = static_cast<uint32_t>(b->vcfs.size() - 1);
+    });
+}
+
+int sb_builder_add_text(sb_builder *b, uint32_t vcf_id, const char *text, size_t len) {
+    return guard([&] {
+        if (!b || (!text && len)) throw Error(SB_EINVAL, "NULL argument");
+        builder_add_text(*b, vcf_id, text, len);
+    });
+}
+
+int sb_builder_add_file(sb_builder *b, uint32_t vcf_id, const char *path) {
+    return guard([&] {
+        if (!b || !path) throw Error(SB_EINVAL, "NULL argument");
+        builder_add_file(*b, vcf_id, path);
+    });
+}
+
+int sb_builder_finish(sb_builder *b, int device, sb_store **out) {
+    return guard([&] {
+        if (!b || !out) throw Error(SB_EINVAL, "NULL argument");
+        for (uint32_t i = 0; i < b->vcfs.size(); ++i) builder_flush(*b, i);
+        int n_dev = 0;
+        HIP_OK(hipGetDeviceCount(&n_dev));
+        if (device < 0 || device >= n_dev) throw Error(SB_EHIP, "device ordinal out of range");
+        auto s = std::make_unique<sb_store>();
+        s->device = device;
+        HIP_OK(hipSetDevice(device));
+        HIP_OK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        upload_store(*b, *s);
+        s->vcfs = std::move(b->vcfs);
+        s->vt = std::move(b->vt);
+        s->sym = std::move(b->sym);
+        for (uint32_t i = 0; i < s->vcfs.size(); ++i) s->vcf_by_location.emplace(s->vcfs[i].location, i);
+        b->vcfs.clear();
+        b->vt = Dict();
+        b->vt.get("N/A");
+        b->sym = Dict();
+        *out = s.release();
+    });
+}
+
+void sb_builder_free(sb_builder *b) { delete b; }
+void sb_store_close(sb_store *s) { delete s; }
+
+int sb_store_get_info(const sb_store *s, sb_store_info *out) {
+    return guard([&] {
+        if (!s || !out) throw Error(SB_EINVAL, "NULL argument");
+        out->n_records = s->n_records;
+        out->n_alt_rows = s->n_alt;
+        out->n_vcfs = static_cast<uint32_t>(s->vcfs.size());
+        uint32_t nseg = 0, ms = 0;
+        for (const auto &v : s->vcfs) {
+            nseg += static_cast<uint32_t>(v.segments.size());
+            ms = std::max(ms, static_cast<uint32_t>(v.samples.size()));
+        }
+        out->n_segments = nseg;
+        out->device_bytes = s->device_bytes;
+        out->max_samples = ms;
+        out->device = s->device;
+    });
+}
+
+int sb_store_find_vcf(const sb_store *s, const char *location, size_t len, uint32_t *vcf_id) {
+    if (!s || !location || !vcf_id) return SB_EINVAL;
+    auto it = s->vcf_by_location.find(std::string(location, len));
+    if (it == s->vcf_by_location.end()) return SB_ENOSTORE;
+    *vcf_id = it->second;
+    return SB_OK;
+}
+
+int sb_store_n_samples(const sb_store *s, uint32_t vcf_id, uint32_t *n) {
+    if (!s || !n || vcf_id >= s->vcfs.size()) return SB_EINVAL;
+    *n = static_cast<uint32_t>(s->vcfs[vcf_id].samples.size());
+    return SB_OK;
+}
+
+int sb_store_sample_name(const sb_store *s, uint32_t vcf_id, uint32_t i, const char **p, size_t *len) {
+    if (!s || !p || !len || vcf_id >= s->vcfs.size() || i >= s->vcfs[vcf_id].samples.size()) return SB_EINVAL;
+    *p = s->vcfs[vcf_id].samples[i].data();
+    *len = s->vcfs[vcf_id].samples[i].size();
+    return SB_OK;
+}
+
+int sb_batch_prepare(sb_store *s, const sb_query *q, size_t nq, sb_batch **out) {
+    return guard([&] {
+        if (!s || (!q && nq) || !out) throw Error(SB_EINVAL, "NULL argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        auto B = std::make_unique<sb_batch>();
+        B->s = s;
+        prepare(*B, q, nq);
+        *out = B.release();
+    });
+}
+
+int sb_batch_run(sb_batch *b) {
+    return guard([&] {
+        if (!b) throw Error(SB_EINVAL, "NULL batch");
+        std::lock_guard<std::mutex> lk(b->s->mu);
+        run(*b);
+    });
+}
+
+int sb_batch_sync(sb_batch *b) {
+    return guard([&] {
+        if (!b) throw Error(SB_EINVAL, "NULL batch");
+        sync(*b);
+    });
+}
+
+int sb_batch_last_timing(const sb_batch *b, double *total_ms, double *scan_ms, double *bounds_ms) {
+    if (!b) return SB_EINVAL;
+    if (total_ms) *total_ms = b->last_total_ms;
+    if (scan_ms) *scan_ms = b->last_scan_ms;
+    if (bounds_ms) *bounds_ms = b->last_bounds_ms;
+    return SB_OK;
+}
+
+int sb_batch_get_stats(const sb_batch *b, sb_batch_stats *out) {
+    if (!b || !out) return SB_EINVAL;
+    out->n_queries = b->nq;
+    out->records_scanned = 0;
+    out->hits = b->cap_total;
+    out->device_ms = b->last_total_ms;
+    return SB_OK;
+}
+
+int sb_batch_fetch(sb_batch *b, sb_result_set **out) {
+    return guard([&] {
+        if (!b || !out) throw Error(SB_EINVAL, "NULL argument");
+        std::lock_guard<std::mutex> lk(b->s->mu);
+        *out = fetch(*b);
+    });
+}
+
+void sb_batch_free(sb_batch *b) {
+    if (!b) return;
+    (void)hipSetDevice(b->s->device);
+    delete b;
+}
+
+int sb_query_batch(sb_store *s, const sb_query *q, size_t nq, uint32_t flags, sb_result_set **out) {
+    (void)flags;
+    return guard([&] {
+        if (!s || (!q && nq) || !out) throw Error(SB_EINVAL, "NULL argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        sb_batch B;
+        B.s = s;
+        prepare(B, q, nq);
+        run(B);
+        *out = fetch(B);
+        (void)hipSetDevice(s->device);
+    });
+}
+
+int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out) {
+    if (!r || !out || i >= r->res.size()) return SB_EINVAL;
+    const QRes &q = r->res[i];
+    out->error = q.error;
+    out->exists = q.exists;
+    out->call_count = q.call_count;
+    out->all_alleles_count = q.all_alleles_count;
+    const uint64_t a = r->dense_off[i], b = r->dense_off[i + 1];
+    out->n_variants = q.error ? 0 : b - a;
+    out->hit_record = r->rec.data() + a;
+    out->hit_alt = r->alt.data() + a;
+    out->n_sample_indices = r->sidx[i].size();
+    out->sample_indices = r->sidx[i].data();
+    return SB_OK;
+}
+
+int sb_result_variants_text(sb_result_set *r, size_t i, const char **p, size_t *len) {
+    if (!r || !p || !len || i >= r->res.size()) return SB_EINVAL;
+    if (!r->vbuilt[i]) {
+        const sb_store &s = *r->s;
+        std::string &o = r->vtext[i];
+        const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
+        char num[16];
+        for (uint64_t h = a; h < b; ++h) {
+            const uint32_t rec = r->rec[h];
+            const uint32_t alt_row = s.h_alt_lo[rec] + r->alt[h];
+            if (h > a) o.push_back('\n');
+            o += r->chrom[i];
+            o.push_back('\t');
+            const int nn = snprintf(num, sizeof num, "%u", s.h_pos[rec]);
+            o.append(num, static_cast<size_t>(nn));
+            o.push_back('\t');
+            o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_ref_off[rec]), s.h_end[rec] - s.h_pos[rec] + 1);
+            o.push_back('\t');
+            o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_alt_off[alt_row]), s.h_alt_len[alt_row]);
+            o.push_back('\t');
+            o += s.vt.items[s.h_meta[rec] >> M_VT_SHIFT];
+        }
+        r->vbuilt[i] = 1;
+    }
+    *p = r->vtext[i].data();
+    *len = r->vtext[i].size();
+    return SB_OK;
+}
+
+int sb_result_sample_names_text(sb_result_set *r, size_t i, const char **p, size_t *len) {
+    if (!r || !p || !len || i >= r->res.size()) return SB_EINVAL;
+    if (!r->nbuilt[i]) {
+        std::string &o = r->ntext[i];
+        const VcfData &v = r->s->vcfs[r->vcf_of[i]];
+        const auto &ix = r->sidx[i];
+        for (size_t j = 0; j < ix.size(); ++j) {
+            const uint32_t h = r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j];
+            if (j) o.push_back(',');
+            o += v.samples[h];
+        }
+        r->nbuilt[i] = 1;
+    }
+    *p = r->ntext[i].data();
+    *len = r->ntext[i].size();
+    return SB_OK;
+}
+
+int sb_result_stats(const sb_result_set *r, sb_batch_stats *out) {
+    if (!r || !out) return SB_EINVAL;
+    *out = r->stats;
+    return SB_OK;
+}
+
+void sb_result_free(sb_result_set *r) { delete r; }
+
+}  // extern "C"

@@ -1,0 +1,519 @@
+// ingest.cpp — VCF text -> columnar store (host, multi-threaded).
+//
+// This replaces what the reference gets from htslib/bcftools per query
+// (lambda/performQuery/search_variants.py:42-50): it decodes each record
+// ONCE and precomputes, per record and per ALT, every quantity the query
+// loop at :84-250 derives from the record text, so the device scan never
+// parses text:
+//   * end = POS + len(REF) - 1                        (:87-91)
+//   * key(REF.upper()), key(ALT.upper())              (:94, :173, :180)
+//   * ALT classes: single base, symbolic, '.', REF-repeat count (:101-166)
+//   * last AC= / AN= / VT= of INFO with the int() failure modes (:195-206)
+//   * genotype fallbacks: count of each allele number and of all calls in
+//     the GT text (re '[0-9]+', :28, :219, :249) for records without AC/AN
+//   * per-ALT carrier bitplanes: sample whose GT has a token equal to the
+//     1-based allele number (the regex at :233-236)
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <zlib.h>
+
+#include "store.hpp"
+
+namespace sb {
+namespace {
+
+struct Local {  // one thread's parse of a run of lines
+    VcfCols c;
+    std::vector<uint32_t> contig_of;  // per record: index into contigs
+    std::vector<std::string> contigs;
+    std::string vtbuf;
+    std::vector<int64_t> vt_off;  // -1 = no VT tag
+    std::vector<uint32_t> vt_len;
+    int err = 0;
+    std::string msg;
+    size_t err_line = 0;
+};
+
+inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
+
+struct Parser {
+    uint32_t n_samples;
+    uint32_t words;
+    bool keep_gt;
+
+    // Returns false and sets L.err on failure.
+    bool line(const char *p, const char *e, Local &L) {
+        // ---- fixed columns
+        const char *f[9];
+        size_t n[9];
+        const char *q = p;
+        int col = 0;
+        while (col < 9 && q <= e) {
+            const char *t = static_cast<const char *>(memchr(q, '\t', static_cast<size_t>(e - q)));
+            if (!t) t = e;
+            f[col] = q;
+            n[col] = static_cast<size_t>(t - q);
+            ++col;
+            q = t + 1;
+        }
+        if (col < 8) return fail(L, "record with fewer than 8 columns");
+        // CHROM
+        const std::string chrom(f[0], n[0]);
+        if (L.contigs.empty() || L.contigs.back() != chrom) L.contigs.push_back(chrom);
+        L.contig_of.push_back(static_cast<uint32_t>(L.contigs.size() - 1));
+        // POS: canonical decimal (bcftools prints it back canonically)
+        if (n[1] == 0 || n[1] > 10 || (n[1] > 1 && f[1][0] == '0')) return fail(L, "non-canonical POS");
+        uint64_t pos = 0;
+        for (size_t i = 0; i < n[1]; ++i) {
+            if (!is_digit(f[1][i])) return fail(L, "non-numeric POS");
+            pos = pos * 10 + static_cast<uint64_t>(f[1][i] - '0');
+        }
+        if (pos > 0xffffffffull) return fail(L, "POS beyond 32 bits");
+        // REF
+        const uint8_t *ref = reinterpret_cast<const uint8_t *>(f[3]);
+        const size_t ref_len = n[3];
+        if (ref_len == 0) return fail(L, "empty REF");
+        const uint64_t end = pos + ref_len - 1;
+        if (end > 0xffffffffull) return fail(L, "POS+len(REF) beyond 32 bits");
+        bool ref_hashed;
+        const uint64_t ref_key = allele_key(ref, ref_len, true, &ref_hashed);
+        VcfCols &c = L.c;
+        c.pos.push_back(static_cast<uint32_t>(pos));
+        c.end.push_back(static_cast<uint32_t>(end));
+        c.ref_key.push_back(ref_key);
+        c.ref_off.push_back(c.blob.size());
+        c.blob.insert(c.blob.end(), ref, ref + ref_len);
+        // ALT split on ',' (:97)
+        const char *alts[64];
+        size_t alens[64];
+        uint32_t na = 0;
+        {
+            const char *a = f[4], *ae = f[4] + n[4];
+            for (;;) {
+                const char *cm = static_cast<const char *>(memchr(a, ',', static_cast<size_t>(ae - a)));
+                if (!cm) cm = ae;
+                if (na == 64) return fail(L, "more than 64 ALT alleles");
+                alts[na] = a;
+                alens[na] = static_cast<size_t>(cm - a);
+                ++na;
+                if (cm == ae) break;
+                a = cm + 1;
+            }
+        }
+        // ---- INFO (:195-201): last AC= string, every AN= parsed, last VT=
+        const char *ac_p = nullptr;
+        size_t ac_n = 0;
+        bool has_ac = false, has_an = false, an_bad = false;
+        int64_t an_val = 0;
+        int64_t vt_off = -1;
+        uint32_t vt_len = 0;
+        {
+            const char *a = f[7], *ae = f[7] + n[7];
+            for (;;) {
+                const char *sc = static_cast<const char *>(memchr(a, ';', static_cast<size_t>(ae - a)));
+                if (!sc) sc = ae;
+                const size_t fl = static_cast<size_t>(sc - a);
+                if (fl >= 3 && a[2] == '=') {
+                    if (a[0] == 'A' && a[1] == 'C') {
+                        has_ac = true;
+                        ac_p = a + 3;
+                        ac_n = fl - 3;
+                    } else if (a[0] == 'A' && a[1] == 'N') {
+                        int64_t v;
+                        if (!an_bad) {
+                            if (py_int(a + 3, fl - 3, &v)) {
+                                an_val = v;
+                                has_an = true;
+                            } else {
+                                an_bad = true;
+                            }
+                        }
+                    } else if (a[0] == 'V' && a[1] == 'T') {
+                        vt_off = static_cast<int64_t>(L.vtbuf.size());
+                        vt_len = static_cast<uint32_t>(fl - 3);
+                        L.vtbuf.append(a + 3, fl - 3);
+                    }
+                }
+                if (sc == ae) break;
+                a = sc + 1;
+            }
+        }
+        L.vt_off.push_back(vt_off);
+        L.vt_len.push_back(vt_len);
+        if (has_an && (an_val > INT32_MAX || an_val < INT32_MIN)) return fail(L, "AN beyond int32");
+        // AC values (:206)
+        int64_t acv[64];
+        uint32_t n_ac = 0;
+        bool ac_bad = false;
+        if (has_ac) {
+            const char *a = ac_p, *ae = ac_p + ac_n;
+            for (;;) {
+                const char *cm = static_cast<const char *>(memchr(a, ',', static_cast<size_t>(ae - a)));
+                if (!cm) cm = ae;
+                int64_t v;
+                if (!py_int(a, static_cast<size_t>(cm - a), &v)) {
+                    ac_bad = true;
+                } else {
+                    if (v > INT32_MAX || v < INT32_MIN) return fail(L, "AC beyond int32");
+                    if (n_ac < 64) acv[n_ac] = v;
+                    ++n_ac;
+                }
+                if (cm == ae) break;
+                a = cm + 1;
+            }
+        }
+        // ---- genotypes
+        int64_t gtcount[64];
+        for (uint32_t i = 0; i < na; ++i) gtcount[i] = 0;
+        int64_t gt_an = 0;
+        const bool need_fb = (!has_ac || !has_an || an_bad) && n_samples > 0;
+        const size_t plane0 = c.planes.size();
+        if (keep_gt && n_samples) c.planes.resize(plane0 + static_cast<size_t>(na) * words, 0ull);
+        int64_t fb_row = -1;
+        if (need_fb) {
+            fb_row = static_cast<int64_t>(c.fb.size());
+            c.fb.resize(c.fb.size() + n_samples, 0u);
+        }
+        if (n_samples) {
+            if (col < 9) return fail(L, "missing FORMAT/sample columns");
+            // FORMAT: index of GT
+            int gt_idx = -1;
+            {
+                int k = 0;
+                const char *a = f[8], *ae = f[8] + n[8];
+                for (;;) {
+                    const char *cl = static_cast<const char *>(memchr(a, ':', static_cast<size_t>(ae - a)));
+                    if (!cl) cl = ae;
+                    if (cl - a == 2 && a[0] == 'G' && a[1] == 'T') gt_idx = k;
+                    ++k;
+                    if (cl == ae) break;
+                    a = cl + 1;
+                }
+            }
+            uint32_t s = 0;
+            const char *a = q;
+            while (s < n_samples) {
+                if (a > e) return fail(L, "fewer sample columns than header samples");
+                const char *t = static_cast<const char *>(memchr(a, '\t', static_cast<size_t>(e - a)));
+                if (!t) t = e;
+                // GT subfield
+                const char *g = a, *ge = t;
+                if (gt_idx < 0) {
+                    g = ".";
+                    ge = g + 1;  // no GT key: bcftools prints '.'  (unpinned)
+                } else {
+                    for (int k = 0; k < gt_idx && g < ge; ++k) {
+                        const char *cl = static_cast<const char *>(memchr(g, ':', static_cast<size_t>(ge - g)));
+                        g = cl ? cl + 1 : ge;
+                    }
+                    const char *cl = static_cast<const char *>(memchr(g, ':', static_cast<size_t>(ge - g)));
+                    if (cl) ge = cl;
+                }
+                const size_t gl = static_cast<size_t>(ge - g);
+                if (gl == 3 && g[0] == '0' && g[2] == '0' && (g[1] == '|' || g[1] == '/')) {
+                    gt_an += 2;  // hot path: homozygous REF
+                    if (need_fb) c.fb[static_cast<size_t>(fb_row) + s] = 2u;
+                } else {
+                    // digit runs (re '[0-9]+'): calls for counts / AN fallback
+                    uint32_t nrun = 0, vals[3] = {0, 0, 0};
+                    for (size_t i = 0; i < gl;) {
+                        if (is_digit(g[i])) {
+                            uint64_t v = 0;
+                            size_t j = i;
+                            while (j < gl && is_digit(g[j])) {
+                                if (v < (1ull << 40)) v = v * 10 + static_cast<uint64_t>(g[j] - '0');
+                                ++j;
+                            }
+                            ++gt_an;
+                            if (v >= 1 && v <= na) gtcount[v - 1]++;
+                            if (need_fb) {
+                                if (nrun >= 3 || v > 254) return fail(L, "genotype fallback row needs ploidy <= 3 and allele < 255");
+                                vals[nrun] = static_cast<uint32_t>(v);
+                            }
+                            ++nrun;
+                            i = j;
+                        } else {
+                            ++i;
+                        }
+                    }
+                    if (need_fb) c.fb[static_cast<size_t>(fb_row) + s] = nrun | (vals[0] << 8) | (vals[1] << 16) | (vals[2] << 24);
+                    // carrier: a token (split on | and /) equal to str(allele number)
+                    if (keep_gt) {
+                        size_t i = 0;
+                        while (i <= gl) {
+                            size_t j = i;
+                            while (j < gl && g[j] != '|' && g[j] != '/') ++j;
+                            const size_t tl = j - i;
+                            if (tl >= 1 && tl <= 2 && is_digit(g[i]) && (tl == 1 || (g[i] != '0' && is_digit(g[i + 1])))) {
+                                const uint32_t v = tl == 1 ? static_cast<uint32_t>(g[i] - '0')
+                                                           : static_cast<uint32_t>((g[i] - '0') * 10 + (g[i + 1] - '0'));
+                                if (v >= 1 && v <= na)
+                                    c.planes[plane0 + static_cast<size_t>(v - 1) * words + (s >> 6)] |= 1ull << (s & 63);
+                            }
+                            i = j + 1;
+                        }
+                    }
+                }
+                ++s;
+                a = t + 1;
+            }
+        }
+        // ---- record columns
+        uint32_t meta = 0;
+        if (has_ac) meta |= M_HAS_AC;
+        if (has_an) meta |= M_HAS_AN;
+        if (ac_bad) meta |= M_AC_BAD;
+        if (an_bad) meta |= M_AN_BAD;
+        if (need_fb) meta |= M_HAS_FB;
+        if (ref_hashed) meta |= M_REF_HASHED;
+        c.meta.push_back(meta);
+        const int64_t anv = has_an ? an_val : gt_an;
+        if (anv > INT32_MAX) return fail(L, "called-allele count beyond int32");
+        c.an.push_back(static_cast<int32_t>(anv));
+        c.fb_off.push_back(fb_row);
+        // ---- alt rows
+        for (uint32_t i = 0; i < na; ++i) {
+            const uint8_t *ap = reinterpret_cast<const uint8_t *>(alts[i]);
+            const size_t al = alens[i];
+            bool hashed;
+            c.alt_key.push_back(allele_key(ap, al, true, &hashed));
+            c.alt_len.push_back(static_cast<uint32_t>(al));
+            uint32_t cls = 0;
+            if (al == 1) {
+                const uint8_t u = upc(ap[0]);
+                if (u == 'A' || u == 'C' || u == 'G' || u == 'T' || u == 'N') cls |= A_SINGLE_BASE;
+            }
+            if (al >= 1 && ap[0] == '<') cls |= A_SYMBOLIC;
+            if (al == 1 && ap[0] == '.') cls |= A_DOT;
+            if (hashed) cls |= A_HASHED;
+            // alt == REF * k (raw bytes): fullmatch of '(REF){2,}' / '(REF)*' (:124,:146)
+            uint32_t rep = A_REP_NONE;
+            if (al % ref_len == 0) {
+                const size_t k = al / ref_len;
+                bool ok = true;
+                for (size_t j = 0; j < k && ok; ++j) ok = memcmp(ap + j * ref_len, ref, ref_len) == 0;
+                if (ok) rep = k >= 62 ? 62u : static_cast<uint32_t>(k);
+            }
+            cls |= rep << A_REP_SHIFT;
+            int64_t acval;
+            if (has_ac) {
+                if (i >= n_ac) cls |= A_AC_MISSING;
+                acval = (!ac_bad && i < n_ac && i < 64) ? acv[i] : 0;
+            } else {
+                acval = gtcount[i];
+            }
+            c.alt_cls.push_back(cls);
+            c.ac.push_back(static_cast<int32_t>(acval));
+            c.alt_off.push_back(c.blob.size());
+            c.blob.insert(c.blob.end(), ap, ap + al);
+        }
+        c.alt_lo.push_back(static_cast<uint32_t>(c.alt_key.size()));
+        return true;
+    }
+
+    static bool fail(Local &L, const char *m) {
+        L.err = SB_EPARSE;
+        L.msg = m;
+        return false;
+    }
+};
+
+void parse_header_line(VcfData &v, const char *p, const char *e) {
+    if (e - p >= 2 && p[1] == '#') return;
+    // #CHROM POS ID REF ALT QUAL FILTER INFO [FORMAT samples...]
+    std::vector<std::string> cols;
+    const char *q = p;
+    for (;;) {
+        const char *t = static_cast<const char *>(memchr(q, '\t', static_cast<size_t>(e - q)));
+        if (!t) t = e;
+        cols.emplace_back(q, static_cast<size_t>(t - q));
+        if (t == e) break;
+        q = t + 1;
+    }
+    v.samples.clear();
+    for (size_t i = 9; i < cols.size(); ++i) v.samples.push_back(cols[i]);
+    v.words = static_cast<uint32_t>((v.samples.size() + 63) / 64);
+    v.header_seen = true;
+}
+
+void merge(sb_builder &b, VcfData &v, Local &L) {
+    VcfCols &d = v.c;
+    const VcfCols &s = L.c;
+    const uint32_t rec0 = static_cast<uint32_t>(d.pos.size());
+    const uint32_t alt0 = static_cast<uint32_t>(d.alt_key.size());
+    const uint64_t blob0 = d.blob.size();
+    const int64_t fb0 = static_cast<int64_t>(d.fb.size());
+    const size_t nr = s.pos.size();
+    // segments + sortedness (bcftools needs a sorted, indexed VCF)
+    for (size_t i = 0; i < nr; ++i) {
+        const std::string &ctg = L.contigs[L.contig_of[i]];
+        const uint32_t r = rec0 + static_cast<uint32_t>(i);
+        if (v.segments.empty() || v.segments.back().contig != ctg) {
+            if (v.seg_index.count(ctg)) throw Error(SB_EPARSE, "contig " + ctg + " is not contiguous (unsorted VCF)");
+            v.seg_index.emplace(ctg, static_cast<uint32_t>(v.segments.size()));
+            v.segments.push_back(Segment{ctg, r, r + 1});
+        } else {
+            if (s.pos[i] < (r > 0 ? (i > 0 ? s.pos[i - 1] : d.pos.back()) : 0u))
+                throw Error(SB_EPARSE, "unsorted file: POS decreases on contig " + ctg);
+            v.segments.back().hi = r + 1;
+        }
+    }
+    auto app = [](auto &dst, const auto &src) { dst.insert(dst.end(), src.begin(), src.end()); };
+    app(d.pos, s.pos);
+    app(d.end, s.end);
+    app(d.an, s.an);
+    app(d.ref_key, s.ref_key);
+    d.meta.reserve(d.meta.size() + nr);
+    std::string last_vt;
+    uint32_t last_id = 0;
+    bool have_last = false;
+    for (size_t i = 0; i < nr; ++i) {
+        uint32_t id = 0;
+        if (L.vt_off[i] >= 0) {
+            if (have_last && last_vt.size() == L.vt_len[i] &&
+                !memcmp(last_vt.data(), L.vtbuf.data() + L.vt_off[i], L.vt_len[i])) {
+                id = last_id;
+            } else {
+                last_vt.assign(L.vtbuf.data() + L.vt_off[i], L.vt_len[i]);
+                id = b.vt.get(last_vt);
+                last_id = id;
+                have_last = true;
+            }
+            if (id > 0xffff) throw Error(SB_EPARSE, "more than 65535 distinct VT values");
+        }
+        d.meta.push_back(s.meta[i] | (id << M_VT_SHIFT));
+    }
+    for (size_t i = 0; i < nr; ++i) d.ref_off.push_back(s.ref_off[i] + blob0);
+    for (size_t i = 0; i < nr; ++i) d.fb_off.push_back(s.fb_off[i] < 0 ? -1 : s.fb_off[i] + fb0);
+    for (size_t i = 1; i < s.alt_lo.size(); ++i) d.alt_lo.push_back(s.alt_lo[i] + alt0);
+    app(d.alt_key, s.alt_key);
+    app(d.alt_len, s.alt_len);
+    app(d.ac, s.ac);
+    for (size_t i = 0; i < s.alt_off.size(); ++i) d.alt_off.push_back(s.alt_off[i] + blob0);
+    d.alt_cls.reserve(d.alt_cls.size() + s.alt_cls.size());
+    for (size_t i = 0; i < s.alt_cls.size(); ++i) {
+        uint32_t cls = s.alt_cls[i];
+        if (cls & A_SYMBOLIC) {
+            const std::string str(reinterpret_cast<const char *>(s.blob.data() + s.alt_off[i]), s.alt_len[i]);
+            const uint32_t id = b.sym.get(str);
+            if (id > 0xffff) throw Error(SB_EPARSE, "more than 65535 distinct symbolic ALT strings");
+            cls |= id << A_SYM_SHIFT;
+        }
+        d.alt_cls.push_back(cls);
+    }
+    app(d.blob, s.blob);
+    app(d.planes, s.planes);
+    app(d.fb, s.fb);
+}
+
+void parse_records(sb_builder &b, VcfData &v, const char *p, size_t len) {
+    // line starts
+    std::vector<const char *> starts;
+    const char *e = p + len;
+    for (const char *q = p; q < e;) {
+        const char *nl = static_cast<const char *>(memchr(q, '\n', static_cast<size_t>(e - q)));
+        if (!nl) nl = e;
+        if (nl > q && !(nl - q == 1 && *q == '\r')) starts.push_back(q);
+        q = nl + 1;
+    }
+    if (starts.empty()) return;
+    for (const char *s : starts)
+        if (*s == '#') throw Error(SB_EPARSE, "header line after records");
+    if (!v.header_seen) throw Error(SB_EPARSE, "records before the #CHROM header line");
+    const size_t nl = starts.size();
+    unsigned nt = b.opts.n_threads > 0 ? static_cast<unsigned>(b.opts.n_threads) : std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min<unsigned>(nt, static_cast<unsigned>((nl + 4095) / 4096)));
+    nt = std::min(nt, 64u);
+    std::vector<Local> locals(nt);
+    Parser proto{static_cast<uint32_t>(v.samples.size()), v.words, b.opts.keep_genotypes != 0};
+    auto work = [&](unsigned t) {
+        const size_t lo = nl * t / nt, hi = nl * (t + 1) / nt;
+        Parser P = proto;
+        Local &L = locals[t];
+        for (size_t i = lo; i < hi; ++i) {
+            const char *s = starts[i];
+            const char *le = static_cast<const char *>(memchr(s, '\n', static_cast<size_t>(e - s)));
+            if (!le) le = e;
+            if (le > s && le[-1] == '\r') --le;
+            if (!P.line(s, le, L)) {
+                L.err_line = i;
+                return;
+            }
+        }
+    };
+    if (nt == 1) {
+        work(0);
+    } else {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t) th.emplace_back(work, t);
+        for (auto &t : th) t.join();
+    }
+    for (auto &L : locals)
+        if (L.err) throw Error(L.err, L.msg);
+    for (auto &L : locals) merge(b, v, L);
+}
+
+void add_text(sb_builder &b, VcfData &v, const char *text, size_t len) {
+    std::string joined;
+    if (!v.carry.empty()) {
+        joined = v.carry;
+        joined.append(text, len);
+        v.carry.clear();
+        text = joined.data();
+        len = joined.size();
+    }
+    // keep an unterminated tail for the next call
+    size_t upto = len;
+    while (upto > 0 && text[upto - 1] != '\n') --upto;
+    if (upto < len) v.carry.assign(text + upto, len - upto);
+    const char *p = text, *e = text + upto;
+    // header lines first (sequential)
+    while (p < e && *p == '#') {
+        const char *nl = static_cast<const char *>(memchr(p, '\n', static_cast<size_t>(e - p)));
+        if (!nl) nl = e;
+        const char *le = nl;
+        if (le > p && le[-1] == '\r') --le;
+        parse_header_line(v, p, le);
+        p = nl + 1;
+    }
+    if (p < e) parse_records(b, v, p, static_cast<size_t>(e - p));
+}
+
+}  // namespace
+
+void builder_add_text(sb_builder &b, uint32_t vcf_id, const char *text, size_t len) {
+    if (vcf_id >= b.vcfs.size()) throw Error(SB_ENOSTORE, "unknown vcf id");
+    add_text(b, b.vcfs[vcf_id], text, len);
+}
+
+void builder_flush(sb_builder &b, uint32_t vcf_id) {
+    VcfData &v = b.vcfs[vcf_id];
+    if (!v.carry.empty()) {
+        std::string tail = v.carry + "\n";
+        v.carry.clear();
+        add_text(b, v, tail.data(), tail.size());
+    }
+}
+
+void builder_add_file(sb_builder &b, uint32_t vcf_id, const char *path) {
+    if (vcf_id >= b.vcfs.size()) throw Error(SB_ENOSTORE, "unknown vcf id");
+    gzFile f = gzopen(path, "rb");
+    if (!f) throw Error(SB_EIO, std::string("cannot open ") + path);
+    gzbuffer(f, 1 << 20);
+    const size_t chunk = size_t(64) << 20;
+    std::vector<char> buf(chunk);
+    for (;;) {
+        const int r = gzread(f, buf.data(), static_cast<unsigned>(chunk));
+        if (r < 0) {
+            gzclose(f);
+            throw Error(SB_EIO, std::string("decompression failed: ") + path);
+        }
+        if (r == 0) break;
+        add_text(b, b.vcfs[vcf_id], buf.data(), static_cast<size_t>(r));
+    }
+    gzclose(f);
+    builder_flush(b, vcf_id);
+}
+
+}  // namespace sb

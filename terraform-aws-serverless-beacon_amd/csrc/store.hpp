@@ -1,0 +1,100 @@
+// store.hpp — host-side columnar variant store and its HBM image.
+//
+// Built once at ingest from VCF text (what bcftools would have decoded per
+// slice, lambda/performQuery/search_variants.py:42-50), then uploaded to one
+// device and queried by query_kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.hpp"
+#include "devtypes.hpp"
+
+namespace sb {
+
+struct Segment {  // one (vcf, contig), position-sorted, contiguous records
+    std::string contig;
+    uint32_t lo = 0, hi = 0;  // record range (vcf-local while building, global in a store)
+};
+
+// Columns of one VCF (vcf-local indices while building).
+struct VcfCols {
+    std::vector<uint32_t> pos, end, meta;
+    std::vector<int32_t> an;
+    std::vector<uint64_t> ref_key, ref_off;
+    std::vector<int64_t> fb_off;
+    std::vector<uint32_t> alt_lo{0};
+    std::vector<uint64_t> alt_key, alt_off;
+    std::vector<uint32_t> alt_len, alt_cls;
+    std::vector<int32_t> ac;
+    std::vector<uint8_t> blob;
+    std::vector<uint64_t> planes;  // [alt row][words]
+    std::vector<uint32_t> fb;      // [fallback row][n_samples]
+};
+
+struct VcfData {
+    std::string location;
+    std::vector<std::string> samples;
+    uint32_t words = 0;  // ceil(n_samples / 64)
+    bool header_seen = false;
+    std::vector<Segment> segments;
+    std::unordered_map<std::string, uint32_t> seg_index;
+    VcfCols c;
+    std::string carry;  // partial line kept between add_text calls
+    // global placement (set by finish)
+    uint32_t rec_base = 0, alt_base = 0;
+    uint64_t plane_base = 0;
+};
+
+struct Dict {
+    std::vector<std::string> items;
+    std::unordered_map<std::string, uint32_t> index;
+    uint32_t get(const std::string &s) {
+        auto it = index.find(s);
+        if (it != index.end()) return it->second;
+        const uint32_t id = static_cast<uint32_t>(items.size());
+        items.push_back(s);
+        index.emplace(s, id);
+        return id;
+    }
+};
+
+struct DeviceBuffer {
+    void *p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace sb
+
+struct sb_builder {
+    sb_build_opts opts{};
+    std::vector<sb::VcfData> vcfs;
+    sb::Dict vt;   // id 0 = "N/A" (no VT= tag, search_variants.py:193)
+    sb::Dict sym;  // symbolic ALT strings
+};
+
+struct sb_store {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;  // serialises batches on this device
+    std::vector<sb::VcfData> vcfs;  // host columns kept for result formatting
+    std::unordered_map<std::string, uint32_t> vcf_by_location;
+    sb::Dict vt, sym;
+    uint64_t n_records = 0, n_alt = 0;
+    uint32_t max_words = 0;
+    // host copies needed to format results (global indexing)
+    std::vector<uint32_t> h_pos, h_meta, h_end;
+    std::vector<uint64_t> h_ref_off, h_alt_off;
+    std::vector<uint32_t> h_alt_len, h_alt_lo;
+    std::vector<uint8_t> h_blob;
+    // device image
+    sb::DStore d{};
+    std::vector<sb::DeviceBuffer> bufs;
+    uint64_t device_bytes = 0;
+    ~sb_store();
+};

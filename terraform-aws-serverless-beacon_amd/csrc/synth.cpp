@@ -1,0 +1,331 @@
+// synth.cpp — seeded 1000 Genomes-shape VCF text generator (libsbeacon_synth.so).
+//
+// Synthetic-data source for the BASELINE.json configs; the
+// reference ships no VCF.  Shape of config 2 (chr22): geometric POS gaps,
+// 96.8 % SNV / 3.0 % indel (len 1-50) / 0.2 % symbolic, 1.5 % multiallelic,
+// P(AC = k) ~ 1/k, AN = 2 x samples, INFO
+// AC;AF;AN;NS;DP;EAS_AF;AMR_AF;AFR_AF;EUR_AF;SAS_AF;AA=.|||;VT, phased GTs
+// consistent with AC.  Every record is a pure function of (seed, index), so
+// chunks are generated in parallel and any record range is reproducible
+// (also "sites-only": the same records without FORMAT/sample columns, for
+// the CPU oracle).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace {
+
+inline uint64_t splitmix(uint64_t &x) {
+    uint64_t z = (x += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+struct Rng {
+    uint64_t s;
+    Rng(uint64_t seed, uint64_t idx, uint64_t stream) : s(seed * 0x9E3779B97F4A7C15ull ^ (idx + 1) * 0xD1B54A32D192ED03ull ^ stream) {
+        splitmix(s);
+    }
+    uint64_t next() { return splitmix(s); }
+    double uni() { return static_cast<double>(next() >> 11) * (1.0 / 9007199254740992.0); }
+    uint32_t below(uint32_t n) { return static_cast<uint32_t>((next() >> 32) * n >> 32); }
+};
+
+const char *kBase = "ACGT";
+const char *kSym[] = {"<DEL>", "<DUP>", "<CN0>", "<INS>", "<INV>", "<CN2>", "<DUP:TANDEM>", "<DEL:ME:ALU>"};
+
+struct Gen {
+    uint64_t seed;
+    uint64_t n;
+    uint32_t n_samples;
+    uint32_t start;
+    double mean_gap;
+    std::string contig;
+    std::vector<uint32_t> pos;
+};
+
+struct Rec {
+    std::string ref;
+    std::vector<std::string> alts;
+    std::vector<uint32_t> ac;
+    const char *vt;
+    bool sym;
+};
+
+void make_record(const Gen &g, uint64_t i, Rec &r) {
+    Rng rng(g.seed, i, 1);
+    const double u = rng.uni();
+    r.alts.clear();
+    r.ac.clear();
+    r.sym = false;
+    const uint32_t hap = 2 * g.n_samples;
+    const uint32_t N = hap ? hap : 5008;
+    auto draw_ac = [&](uint32_t cap) {
+        // P(k) ~ 1/k on [1, cap]: k = floor((cap+1)^u)
+        const double x = std::pow(static_cast<double>(cap) + 1.0, rng.uni());
+        uint32_t k = static_cast<uint32_t>(x);
+        return std::max(1u, std::min(k, cap));
+    };
+    if (u < 0.002) {  // symbolic SV
+        r.ref.assign(1, kBase[rng.below(4)]);
+        r.alts.push_back(kSym[rng.below(8)]);
+        r.vt = "SV";
+        r.sym = true;
+    } else if (u < 0.032) {  // indel, len 1..50
+        const uint32_t len = 1 + rng.below(50);
+        std::string s(len + 1, 'A');
+        for (auto &c : s) c = kBase[rng.below(4)];
+        if (rng.uni() < 0.5) {
+            r.ref = s;
+            r.alts.push_back(s.substr(0, 1));
+        } else {
+            r.ref = s.substr(0, 1);
+            r.alts.push_back(s);
+        }
+        r.vt = "INDEL";
+    } else {  // SNV (1.5 % of all records multiallelic)
+        const uint32_t b = rng.below(4);
+        r.ref.assign(1, kBase[b]);
+        uint32_t na = 1;
+        if (rng.uni() < 0.015 / 0.968) na = 2 + rng.below(2);
+        uint32_t used = 1u << b;
+        for (uint32_t k = 0; k < na; ++k) {
+            uint32_t a;
+            do a = rng.below(4);
+            while (used & (1u << a));
+            used |= 1u << a;
+            r.alts.emplace_back(1, kBase[a]);
+        }
+        r.vt = "SNP";
+    }
+    uint32_t left = N;
+    for (size_t k = 0; k < r.alts.size(); ++k) {
+        const uint32_t cap = std::max(1u, left / static_cast<uint32_t>(r.alts.size() - k + 1));
+        const uint32_t c = std::min(draw_ac(cap), left);
+        r.ac.push_back(c);
+        left -= c;
+    }
+}
+
+size_t write_u(char *p, uint64_t v) {
+    char t[24];
+    int n = 0;
+    do {
+        t[n++] = static_cast<char>('0' + v % 10);
+        v /= 10;
+    } while (v);
+    for (int i = 0; i < n; ++i) p[i] = t[n - 1 - i];
+    return static_cast<size_t>(n);
+}
+
+// Render records [lo, hi) into out (appends).
+void render(const Gen &g, uint64_t lo, uint64_t hi, bool sites_only, std::string &out) {
+    Rec r;
+    const uint32_t ns = sites_only ? 0 : g.n_samples;
+    const uint32_t hap = 2 * g.n_samples;
+    std::string gt;
+    if (ns) {
+        gt.resize(static_cast<size_t>(ns) * 4);
+        for (uint32_t s = 0; s < ns; ++s) memcpy(&gt[4 * s], "0|0\t", 4);
+        gt[4 * ns - 1] = '\n';
+    }
+    std::vector<uint8_t> taken(hap ? hap : 1);
+    char buf[4096];
+    for (uint64_t i = lo; i < hi; ++i) {
+        make_record(g, i, r);
+        Rng rng(g.seed, i, 2);
+        size_t n = 0;
+        auto put = [&](const char *s, size_t l) {
+            if (n + l > sizeof buf) {
+                out.append(buf, n);
+                n = 0;
+            }
+            memcpy(buf + n, s, l);
+            n += l;
+        };
+        auto puts_ = [&](const std::string &s) { put(s.data(), s.size()); };
+        auto putc_ = [&](char c) { put(&c, 1); };
+        auto putu = [&](uint64_t v) {
+            char t[24];
+            put(t, write_u(t, v));
+        };
+        puts_(g.contig);
+        putc_('\t');
+        putu(g.pos[i]);
+        put("\t.\t", 3);
+        puts_(r.ref);
+        putc_('\t');
+        for (size_t k = 0; k < r.alts.size(); ++k) {
+            if (k) putc_(',');
+            puts_(r.alts[k]);
+        }
+        put("\t100\tPASS\tAC=", 13);
+        for (size_t k = 0; k < r.ac.size(); ++k) {
+            if (k) putc_(',');
+            putu(r.ac[k]);
+        }
+        const uint32_t an = hap ? hap : 5008;
+        put(";AF=", 4);
+        for (size_t k = 0; k < r.ac.size(); ++k) {
+            if (k) putc_(',');
+            char t[32];
+            const int l = snprintf(t, sizeof t, "%.4g", static_cast<double>(r.ac[k]) / an);
+            put(t, static_cast<size_t>(l));
+        }
+        put(";AN=", 4);
+        putu(an);
+        put(";NS=", 4);
+        putu(g.n_samples ? g.n_samples : 2504);
+        put(";DP=", 4);
+        putu(5000 + rng.below(30000));
+        static const char *pops[] = {";EAS_AF=", ";AMR_AF=", ";AFR_AF=", ";EUR_AF=", ";SAS_AF="};
+        for (const char *pp : pops) {
+            put(pp, 8);
+            for (size_t k = 0; k < r.ac.size(); ++k) {
+                if (k) putc_(',');
+                char t[16];
+                const int l = snprintf(t, sizeof t, "%.2f", rng.uni() * 0.1);
+                put(t, static_cast<size_t>(l));
+            }
+        }
+        if (r.sym) {
+            put(";END=", 5);
+            putu(g.pos[i] + 50 + rng.below(5000));
+        }
+        put(";AA=.|||;VT=", 12);
+        put(r.vt, strlen(r.vt));
+        if (!ns) {
+            putc_('\n');
+            out.append(buf, n);
+            continue;
+        }
+        put("\tGT\t", 4);
+        out.append(buf, n);
+        // genotypes consistent with AC: distinct carrier haplotypes per allele
+        const size_t g0 = out.size();
+        out.append(gt);
+        std::fill(taken.begin(), taken.end(), 0);
+        for (size_t k = 0; k < r.ac.size(); ++k) {
+            const char digit = static_cast<char>('1' + k);
+            for (uint32_t c = 0; c < r.ac[k]; ++c) {
+                uint32_t h;
+                do h = rng.below(hap);
+                while (taken[h]);
+                taken[h] = 1;
+                out[g0 + 4 * (h >> 1) + 2 * (h & 1)] = digit;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+// contig: NUL-terminated; mean_gap: geometric mean gap between POS values.
+void *sbs_new(uint64_t seed, uint64_t n_records, uint32_t n_samples, uint32_t start_pos, double mean_gap,
+              const char *contig) {
+    auto *g = new Gen;
+    g->seed = seed;
+    g->n = n_records;
+    g->n_samples = n_samples;
+    g->start = start_pos;
+    g->mean_gap = mean_gap;
+    g->contig = contig;
+    g->pos.resize(n_records);
+    uint64_t p = start_pos;
+    const double lq = std::log(1.0 - 1.0 / mean_gap);
+    for (uint64_t i = 0; i < n_records; ++i) {
+        if (i) {
+            Rng rng(seed, i, 0);
+            // geometric on {0,1,...} with mean ~ mean_gap - 1, plus 1 (same-POS records stay rare)
+            const double x = std::floor(std::log(1.0 - rng.uni()) / lq);
+            p += 1 + static_cast<uint64_t>(x);
+        }
+        g->pos[i] = static_cast<uint32_t>(std::min<uint64_t>(p, 0xfffffff0ull));
+    }
+    return g;
+}
+
+void sbs_free(void *h) { delete static_cast<Gen *>(h); }
+
+uint32_t sbs_pos(void *h, uint64_t i) { return static_cast<Gen *>(h)->pos[i]; }
+
+// copy POS array (n_records u32)
+void sbs_positions(void *h, uint32_t *out) {
+    auto *g = static_cast<Gen *>(h);
+    memcpy(out, g->pos.data(), g->pos.size() * 4);
+}
+
+// REF / first ALT of record i into caller buffers (for point-query generation)
+int sbs_alleles(void *h, uint64_t i, char *ref, size_t ref_cap, char *alt, size_t alt_cap) {
+    auto *g = static_cast<Gen *>(h);
+    Rec r;
+    make_record(*g, i, r);
+    if (r.ref.size() + 1 > ref_cap || r.alts[0].size() + 1 > alt_cap) return -1;
+    memcpy(ref, r.ref.c_str(), r.ref.size() + 1);
+    memcpy(alt, r.alts[0].c_str(), r.alts[0].size() + 1);
+    return static_cast<int>(r.alts.size());
+}
+
+// Header text (caller frees with sbs_free_text).
+char *sbs_header(void *h, int sites_only, size_t *len) {
+    auto *g = static_cast<Gen *>(h);
+    std::string s = "##fileformat=VCFv4.2\n##contig=<ID=" + g->contig + ">\n";
+    s += "##INFO=<ID=AC,Number=A,Type=Integer,Description=\"Allele count\">\n";
+    s += "##INFO=<ID=AN,Number=1,Type=Integer,Description=\"Total alleles\">\n";
+    s += "#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO";
+    if (!sites_only && g->n_samples) {
+        s += "\tFORMAT";
+        char t[32];
+        for (uint32_t i = 0; i < g->n_samples; ++i) {
+            snprintf(t, sizeof t, "\tHG%05u", i + 96);
+            s += t;
+        }
+    }
+    s += "\n";
+    char *o = static_cast<char *>(malloc(s.size()));
+    memcpy(o, s.data(), s.size());
+    *len = s.size();
+    return o;
+}
+
+// Records [lo, hi) as VCF text, rendered by n_threads threads.
+char *sbs_records(void *h, uint64_t lo, uint64_t hi, int sites_only, int n_threads, size_t *len) {
+    auto *g = static_cast<Gen *>(h);
+    hi = std::min<uint64_t>(hi, g->n);
+    if (lo >= hi) {
+        *len = 0;
+        return static_cast<char *>(malloc(1));
+    }
+    unsigned nt = n_threads > 0 ? static_cast<unsigned>(n_threads) : std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min<unsigned>(nt, static_cast<unsigned>((hi - lo + 1023) / 1024)));
+    std::vector<std::string> parts(nt);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            const uint64_t a = lo + (hi - lo) * t / nt, b = lo + (hi - lo) * (t + 1) / nt;
+            render(*g, a, b, sites_only != 0, parts[t]);
+        });
+    for (auto &x : th) x.join();
+    size_t total = 0;
+    for (auto &p : parts) total += p.size();
+    char *o = static_cast<char *>(malloc(total ? total : 1));
+    size_t off = 0;
+    for (auto &p : parts) {
+        memcpy(o + off, p.data(), p.size());
+        off += p.size();
+    }
+    *len = total;
+    return o;
+}
+
+void sbs_free_text(char *p) { free(p); }
+
+}  // extern "C"

@@ -1,0 +1,115 @@
+"""ctypes binding of libsbeacon_hip.so (declared in include/sbeacon.h).
+
+The product path has no CPU fallback: if the HIP library is missing or cannot
+be loaded, importing the engine raises immediately.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_NAME = 'libsbeacon_hip.so'
+LIB_PATH = os.environ.get('SBEACON_LIB', os.path.join(PKG_ROOT, LIB_NAME))
+
+SB_OK = 0
+SB_GRAN = {'boolean': 0, 'count': 1, 'aggregated': 2, 'record': 3}
+
+
+class SbError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f'sbeacon error {code}: {msg}')
+        self.code = code
+
+
+class BuildOpts(C.Structure):
+    _fields_ = [('keep_genotypes', C.c_int32), ('n_threads', C.c_int32)]
+
+
+class StoreInfo(C.Structure):
+    _fields_ = [('n_records', C.c_uint64), ('n_alt_rows', C.c_uint64), ('n_vcfs', C.c_uint32),
+                ('n_segments', C.c_uint32), ('device_bytes', C.c_uint64), ('max_samples', C.c_uint32),
+                ('device', C.c_int32)]
+
+
+class Query(C.Structure):
+    _fields_ = [('vcf_id', C.c_uint32), ('_pad0', C.c_uint32),
+                ('region', C.c_char_p), ('region_len', C.c_size_t),
+                ('end_min', C.c_int64), ('end_max', C.c_int64),
+                ('reference_bases', C.c_char_p), ('reference_len', C.c_size_t),
+                ('alternate_bases', C.c_char_p), ('alternate_len', C.c_size_t),
+                ('variant_type', C.c_char_p), ('variant_type_len', C.c_size_t),
+                ('variant_min_length', C.c_int64), ('variant_max_length', C.c_int64),
+                ('granularity', C.c_uint8), ('include_details', C.c_uint8),
+                ('include_samples', C.c_uint8), ('selected_samples_only', C.c_uint8),
+                ('strict_variant_type', C.c_uint8), ('_pad1', C.c_uint8 * 3),
+                ('sample_names', C.c_char_p), ('sample_names_len', C.c_size_t)]
+
+
+class ResultView(C.Structure):
+    _fields_ = [('error', C.c_int32), ('exists', C.c_int32), ('call_count', C.c_int64),
+                ('all_alleles_count', C.c_int64), ('n_variants', C.c_uint64),
+                ('hit_record', C.POINTER(C.c_uint32)), ('hit_alt', C.POINTER(C.c_uint32)),
+                ('n_sample_indices', C.c_uint64), ('sample_indices', C.POINTER(C.c_uint32))]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [('n_queries', C.c_uint64), ('records_scanned', C.c_uint64), ('hits', C.c_uint64),
+                ('device_ms', C.c_double)]
+
+
+# every exported symbol of include/sbeacon.h: name -> (restype, argtypes)
+P = C.c_void_p
+SIGNATURES = {
+    'sb_last_error': (C.c_char_p, []),
+    'sb_abi_version': (C.c_int, []),
+    'sb_builder_new': (C.c_int, [C.POINTER(BuildOpts), C.POINTER(P)]),
+    'sb_builder_begin_vcf': (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(C.c_uint32)]),
+    'sb_builder_add_text': (C.c_int, [P, C.c_uint32, C.c_char_p, C.c_size_t]),
+    'sb_builder_add_file': (C.c_int, [P, C.c_uint32, C.c_char_p]),
+    'sb_builder_finish': (C.c_int, [P, C.c_int, C.POINTER(P)]),
+    'sb_builder_free': (None, [P]),
+    'sb_store_close': (None, [P]),
+    'sb_store_get_info': (C.c_int, [P, C.POINTER(StoreInfo)]),
+    'sb_store_find_vcf': (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(C.c_uint32)]),
+    'sb_store_n_samples': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    'sb_store_sample_name': (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_char_p),
+                                       C.POINTER(C.c_size_t)]),
+    'sb_query_batch': (C.c_int, [P, C.POINTER(Query), C.c_size_t, C.c_uint32, C.POINTER(P)]),
+    'sb_result_get': (C.c_int, [P, C.c_size_t, C.POINTER(ResultView)]),
+    'sb_result_variants_text': (C.c_int, [P, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    'sb_result_sample_names_text': (C.c_int, [P, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    'sb_result_stats': (C.c_int, [P, C.POINTER(BatchStats)]),
+    'sb_result_free': (None, [P]),
+    'sb_batch_prepare': (C.c_int, [P, C.POINTER(Query), C.c_size_t, C.POINTER(P)]),
+    'sb_batch_run': (C.c_int, [P]),
+    'sb_batch_sync': (C.c_int, [P]),
+    'sb_batch_last_timing': (C.c_int, [P, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    'sb_batch_get_stats': (C.c_int, [P, C.POINTER(BatchStats)]),
+    'sb_batch_fetch': (C.c_int, [P, C.POINTER(P)]),
+    'sb_batch_free': (None, [P]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libsbeacon_hip.so (raises OSError if it is missing: no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise OSError(f'{LIB_PATH} not found: build it with `python -c "import __graft_entry__ as g; g.build()"`')
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != SB_OK:
+        msg = lib().sb_last_error()
+        raise SbError(rc, msg.decode() if msg else '')
+    return rc

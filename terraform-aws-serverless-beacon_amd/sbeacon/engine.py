@@ -1,0 +1,322 @@
+"""Host-side engine: HBM variant stores and batched slice queries.
+
+A :class:`Store` is the HBM-resident columnar image of one or more VCFs
+(ingested once, replacing the per-slice ``bcftools query`` subprocess of
+``lambda/performQuery/search_variants.py:42-50``).  :meth:`Store.query` takes
+a list of ``PerformQueryPayload``-shaped dicts — what splitQuery would have
+sent to N performQuery Lambdas — and answers all of them in one call into
+``libsbeacon_hip.so``.
+
+``registry`` maps ``vcf_location`` strings to stores so that the
+reference-shaped handlers (``perform_query.py``, ``split_query.py``) can
+resolve a payload's ``vcf_location`` exactly like the reference resolves it
+to an S3 object.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Iterable
+
+from . import _lib
+from ._lib import BatchStats, BuildOpts, Query, ResultView, StoreInfo, check, lib
+from .payloads import PerformQueryResponse
+
+QERR = {1: UnboundLocalError, 2: IndexError, 3: ValueError, 4: AttributeError, 9: NotImplementedError}
+QERR_MSG = {
+    1: "local variable 'variant_type' referenced before assignment",
+    2: 'list index out of range',
+    3: 'invalid literal for int() with base 10',
+    4: "'NoneType' object has no attribute 'replace'",
+    9: 'referenceBases contains regex metacharacters (outside the restated contract)',
+}
+
+
+def _b(s):
+    return None if s is None else (s if isinstance(s, bytes) else str(s).encode())
+
+
+class Store:
+    """An immutable HBM store built from VCF files or text."""
+
+    def __init__(self, handle, locations):
+        self._h = handle
+        self.locations = list(locations)
+
+    # ---------------------------------------------------------------- build
+    @classmethod
+    def build(cls, sources, *, device: int = 0, keep_genotypes: bool = True, n_threads: int = 0):
+        """``sources``: iterable of ``(vcf_location, path_or_text)``; a value
+        that is an existing path is read (plain or gzip), otherwise it is
+        VCF text (``str``/``bytes``) or an iterable of text chunks."""
+        L = lib()
+        b = C.c_void_p()
+        opts = BuildOpts(1 if keep_genotypes else 0, int(n_threads))
+        check(L.sb_builder_new(C.byref(opts), C.byref(b)))
+        locs = []
+        try:
+            for loc, src in sources:
+                vid = C.c_uint32()
+                lb = _b(loc)
+                check(L.sb_builder_begin_vcf(b, lb, len(lb), C.byref(vid)))
+                locs.append(loc)
+                if isinstance(src, (str, os.PathLike)) and os.path.exists(src):
+                    check(L.sb_builder_add_file(b, vid.value, os.fsencode(src)))
+                elif isinstance(src, (str, bytes)):
+                    t = _b(src)
+                    check(L.sb_builder_add_text(b, vid.value, t, len(t)))
+                else:
+                    for chunk in src:
+                        t = _b(chunk)
+                        check(L.sb_builder_add_text(b, vid.value, t, len(t)))
+            s = C.c_void_p()
+            check(L.sb_builder_finish(b, int(device), C.byref(s)))
+        finally:
+            L.sb_builder_free(b)
+        return cls(s, locs)
+
+    def close(self):
+        if self._h:
+            lib().sb_store_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def info(self) -> dict:
+        i = StoreInfo()
+        check(lib().sb_store_get_info(self._h, C.byref(i)))
+        return {f: getattr(i, f) for f, _ in StoreInfo._fields_}
+
+    def vcf_id(self, location: str) -> int:
+        v = C.c_uint32()
+        lb = _b(location)
+        check(lib().sb_store_find_vcf(self._h, lb, len(lb), C.byref(v)))
+        return v.value
+
+    def sample_names(self, location: str) -> list[str]:
+        vid = self.vcf_id(location)
+        n = C.c_uint32()
+        check(lib().sb_store_n_samples(self._h, vid, C.byref(n)))
+        out = []
+        p = C.c_char_p()
+        ln = C.c_size_t()
+        for i in range(n.value):
+            check(lib().sb_store_sample_name(self._h, vid, i, C.byref(p), C.byref(ln)))
+            out.append(C.string_at(p, ln.value).decode())
+        return out
+
+    # ---------------------------------------------------------------- query
+    def make_queries(self, payloads: list[dict], *, strict_variant_type: bool = False):
+        """PerformQueryPayload dicts -> (ctypes Query array, keep-alive list)."""
+        n = len(payloads)
+        arr = (Query * n)()
+        keep = []
+        vid_cache = {}
+        for i, p in enumerate(payloads):
+            loc = p['vcf_location']
+            vid = vid_cache.get(loc)
+            if vid is None:
+                vid = vid_cache[loc] = self.vcf_id(loc)
+            pt = p.get('passthrough') or {}
+            region = _b(p['region'])
+            ref = _b(p.get('reference_bases'))
+            alt = _b(p.get('alternate_bases'))
+            vt = _b(p.get('variant_type'))
+            names = pt.get('sampleNames', None)
+            sn = _b(','.join(names)) if names is not None else None
+            keep.append((region, ref, alt, vt, sn))
+            if p.get('end_min') is None or p.get('end_max') is None:
+                raise TypeError("'<=' not supported between instances of 'NoneType' and 'int'")
+            q = arr[i]
+            q.vcf_id = vid
+            q.region, q.region_len = region, len(region)
+            q.end_min, q.end_max = int(p['end_min']), int(p['end_max'])
+            q.reference_bases, q.reference_len = ref, len(ref) if ref is not None else 0
+            q.alternate_bases, q.alternate_len = alt, len(alt) if alt is not None else 0
+            q.variant_type, q.variant_type_len = vt, len(vt) if vt is not None else 0
+            q.variant_min_length = int(p['variant_min_length'])
+            q.variant_max_length = int(p['variant_max_length'])
+            q.granularity = _lib.SB_GRAN.get(p.get('requested_granularity'), 255)
+            q.include_details = 1 if p.get('include_details') else 0
+            q.include_samples = 1 if pt.get('includeSamples', False) else 0
+            q.selected_samples_only = 1 if pt.get('selectedSamplesOnly', False) else 0
+            q.strict_variant_type = 1 if strict_variant_type else 0
+            q.sample_names, q.sample_names_len = sn, len(sn) if sn is not None else 0
+        return arr, keep
+
+    def query(self, payloads: list[dict], *, strict_variant_type: bool = False) -> 'ResultSet':
+        arr, keep = self.make_queries(payloads, strict_variant_type=strict_variant_type)
+        r = C.c_void_p()
+        check(lib().sb_query_batch(self._h, arr, len(payloads), 0, C.byref(r)))
+        del keep
+        return ResultSet(r, payloads, self)
+
+    def prepare(self, payloads: list[dict], *, strict_variant_type: bool = False) -> 'Batch':
+        arr, keep = self.make_queries(payloads, strict_variant_type=strict_variant_type)
+        b = C.c_void_p()
+        check(lib().sb_batch_prepare(self._h, arr, len(payloads), C.byref(b)))
+        del keep
+        return Batch(b, payloads, self)
+
+
+class Batch:
+    """A device-resident query batch (inputs stay in HBM across runs)."""
+
+    def __init__(self, handle, payloads, store):
+        self._h = handle
+        self.payloads = payloads
+        self.store = store
+
+    def run(self):
+        check(lib().sb_batch_run(self._h))
+
+    def sync(self):
+        check(lib().sb_batch_sync(self._h))
+
+    def timing(self):
+        t, s, b = C.c_double(), C.c_double(), C.c_double()
+        check(lib().sb_batch_last_timing(self._h, C.byref(t), C.byref(s), C.byref(b)))
+        return {'total_ms': t.value, 'scan_ms': s.value, 'bounds_ms': b.value}
+
+    def fetch(self) -> 'ResultSet':
+        r = C.c_void_p()
+        check(lib().sb_batch_fetch(self._h, C.byref(r)))
+        return ResultSet(r, self.payloads, self.store)
+
+    def free(self):
+        if self._h:
+            lib().sb_batch_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class ResultSet:
+    def __init__(self, handle, payloads, store):
+        self._h = handle
+        self.payloads = payloads
+        self.store = store
+
+    def __len__(self):
+        return len(self.payloads)
+
+    def __del__(self):
+        try:
+            if self._h:
+                lib().sb_result_free(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+    def stats(self) -> dict:
+        s = BatchStats()
+        check(lib().sb_result_stats(self._h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in BatchStats._fields_}
+
+    def view(self, i: int) -> ResultView:
+        v = ResultView()
+        check(lib().sb_result_get(self._h, i, C.byref(v)))
+        return v
+
+    def hits(self, i: int):
+        v = self.view(i)
+        return [(v.hit_record[k], v.hit_alt[k]) for k in range(v.n_variants)]
+
+    def _text(self, fn, i):
+        p = C.c_void_p()
+        n = C.c_size_t()
+        check(fn(self._h, i, C.byref(p), C.byref(n)))
+        return C.string_at(p, n.value).decode() if n.value else ''
+
+    def response(self, i: int) -> PerformQueryResponse:
+        """The reference PerformQueryResponse for query i, or raise the
+        exception the reference would raise (search_variants.py:262-271)."""
+        p = self.payloads[i]
+        v = self.view(i)
+        if v.error:
+            raise QERR.get(v.error, RuntimeError)(QERR_MSG.get(v.error, 'error'))
+        pt = p.get('passthrough') or {}
+        samples_variant = bool(pt.get('selectedSamplesOnly', False))
+        include_samples = bool(pt.get('includeSamples', False))
+        vt = self._text(lib().sb_result_variants_text, i)
+        variants = vt.split('\n') if v.n_variants else []
+        names_t = self._text(lib().sb_result_sample_names_text, i)
+        names = names_t.split(',') if v.n_sample_indices else []
+        if samples_variant:
+            sample_indices = [v.sample_indices[k] for k in range(v.n_sample_indices)]
+            sample_names = names
+        else:
+            sample_indices = []
+            sample_names = names if include_samples else []
+        return PerformQueryResponse(
+            exists=bool(v.exists), dataset_id=p.get('dataset_id'), vcf_location=p.get('vcf_location'),
+            all_alleles_count=int(v.all_alleles_count), variants=variants, call_count=int(v.call_count),
+            sample_indices=sample_indices, sample_names=sample_names)
+
+    def responses(self) -> list:
+        """All responses; an entry is the exception instance where the
+        reference would have raised."""
+        out = []
+        for i in range(len(self.payloads)):
+            try:
+                out.append(self.response(i))
+            except (UnboundLocalError, IndexError, ValueError, AttributeError, NotImplementedError) as e:
+                out.append(e)
+        return out
+
+
+# ------------------------------------------------------------------ registry
+class Registry:
+    """vcf_location -> Store (the analogue of the S3 objects the reference reads)."""
+
+    def __init__(self):
+        self._by_loc: dict[str, Store] = {}
+
+    def register(self, store: Store):
+        for loc in store.locations:
+            self._by_loc[loc] = store
+
+    def store_for(self, location: str) -> Store:
+        try:
+            return self._by_loc[location]
+        except KeyError:
+            raise KeyError(f'no HBM store holds vcf_location {location!r}') from None
+
+    def clear(self):
+        self._by_loc.clear()
+
+    def group(self, payloads: Iterable[dict]):
+        """Split payloads by store, preserving order inside each group."""
+        groups: dict[int, tuple[Store, list[int]]] = {}
+        for i, p in enumerate(payloads):
+            s = self.store_for(p['vcf_location'])
+            groups.setdefault(id(s), (s, []))[1].append(i)
+        return list(groups.values())
+
+
+registry = Registry()
+
+
+def query_payloads(payloads: list[dict], *, strict_variant_type: bool = False) -> list:
+    """Answer PerformQueryPayload dicts through the registry in as few
+    device batches as there are stores.  Returns responses/exceptions in
+    payload order."""
+    out = [None] * len(payloads)
+    for store, idx in registry.group(payloads):
+        sub = [payloads[i] for i in idx]
+        rs = store.query(sub, strict_variant_type=strict_variant_type)
+        for j, r in zip(idx, rs.responses()):
+            out[j] = r
+    return out

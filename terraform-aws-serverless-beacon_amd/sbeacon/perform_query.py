@@ -1,0 +1,56 @@
+"""performQuery handler, backed by the HBM store instead of bcftools.
+
+Mirrors ``lambda/performQuery/lambda_function.py:23-49`` (event handling and
+the ``selectedSamplesOnly`` dispatch) and the two query modules
+``search_variants.perform_query`` (``search_variants.py:33-271``) and
+``search_variants_in_samples.perform_query`` (``search_variants_in_samples.py:31-259``):
+same payload, same ``PerformQueryResponse``, same exception class where the
+reference raises.  The dispatch on ``passthrough.selectedSamplesOnly`` happens
+inside the engine (one flag per query), so a batch may mix both variants.
+
+``STRICT_VARIANT_TYPE``: the reference raises ``UnboundLocalError`` for every
+``alternate_bases=None`` (variantType) query that reaches a record
+(``search_variants.py:101``).  By default the engine answers such queries
+with the evident intent (branch on ``payload.variant_type``; SURVEY.md
+§8a.1-4); set ``SBEACON_STRICT_VARIANT_TYPE=1`` to reproduce the crash.
+
+The async path (``is_async``: DynamoDB/S3 result hand-off, ``:273-317``) is
+out of scope: results are always returned synchronously.
+"""
+from __future__ import annotations
+
+import json
+import os
+
+from .engine import query_payloads
+from .payloads import PerformQueryPayload, PerformQueryResponse
+
+STRICT_VARIANT_TYPE = os.environ.get('SBEACON_STRICT_VARIANT_TYPE', '0') == '1'
+
+
+def _as_dict(payload) -> dict:
+    return payload.dump() if hasattr(payload, 'dump') else dict(payload)
+
+
+def perform_query(payload, is_async=False) -> PerformQueryResponse:
+    res = query_payloads([_as_dict(payload)], strict_variant_type=STRICT_VARIANT_TYPE)[0]
+    if isinstance(res, Exception):
+        raise res
+    return res
+
+
+def perform_query_batch(payloads) -> list:
+    """Batched entry: one device pass for many PerformQueryPayloads.
+    Entries are responses or the exception the reference would raise."""
+    return query_payloads([_as_dict(p) for p in payloads], strict_variant_type=STRICT_VARIANT_TYPE)
+
+
+def lambda_handler(event, context):
+    is_async = False
+    try:  # lambda_function.py:33-39 SNS unwrap
+        event = json.loads(event['Records'][0]['Sns']['Message'])
+        is_async = True
+    except Exception:
+        is_async = False
+    payload = PerformQueryPayload.load(event)
+    return perform_query(payload, is_async).dump()

@@ -1,0 +1,165 @@
+"""BASELINE.json workloads: 1000G-shape synthetic stores and their query mixes.
+
+Config 2: chr22-shape store, 1,103,547 records x 2,504
+samples (seed 22); 10,000 Beacon requests (seed 1022): 5,000 range requests
+(start uniform over the span, width uniform 1-100,000 bp, ref = alt = 'N',
+granularity record, includeResultsetResponses HIT) and 5,000 point ref/alt
+requests (70 % drawn from existing rows, 30 % random SNVs; start=[POS-1],
+end=[POS-1+len(alt)] as route_g_variants_id.py builds them).  Each request is
+converted exactly as shared_resources/variantutils/search_variants.py:179-199
+and sliced as lambda/splitQuery/lambda_function.py:82-106, so the unit the
+device answers is the reference's PerformQueryPayload.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+from ._lib import PKG_ROOT
+from .payloads import SplitQueryPayload
+from .split_query import split_payloads
+
+SYNTH_PATH = os.path.join(PKG_ROOT, 'libsbeacon_synth.so')
+_syn = None
+
+
+def synth_lib():
+    global _syn
+    if _syn is None:
+        L = C.CDLL(SYNTH_PATH)
+        L.sbs_new.restype = C.c_void_p
+        L.sbs_new.argtypes = [C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_double, C.c_char_p]
+        L.sbs_free.argtypes = [C.c_void_p]
+        L.sbs_positions.argtypes = [C.c_void_p, C.c_void_p]
+        L.sbs_alleles.restype = C.c_int
+        L.sbs_alleles.argtypes = [C.c_void_p, C.c_uint64, C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t]
+        L.sbs_header.restype = C.c_void_p
+        L.sbs_header.argtypes = [C.c_void_p, C.c_int, C.POINTER(C.c_size_t)]
+        L.sbs_records.restype = C.c_void_p
+        L.sbs_records.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_size_t)]
+        L.sbs_free_text.argtypes = [C.c_void_p]
+        _syn = L
+    return _syn
+
+
+CHR22_SPAN = (16050075, 51244237)
+
+
+class SyntheticVcf:
+    """Seeded 1000G-shape VCF (records are pure functions of seed + index)."""
+
+    def __init__(self, *, seed=22, n_records=1103547, n_samples=2504, start=CHR22_SPAN[0],
+                 mean_gap=(CHR22_SPAN[1] - CHR22_SPAN[0]) / (1103547 - 1), contig='22'):
+        self.seed, self.n_records, self.n_samples, self.contig = seed, n_records, n_samples, contig
+        self._h = synth_lib().sbs_new(seed, n_records, n_samples, start, float(mean_gap), contig.encode())
+        self._pos = None
+
+    def __del__(self):
+        try:
+            synth_lib().sbs_free(self._h)
+        except Exception:
+            pass
+
+    def _take(self, p, n):
+        b = C.string_at(p, n.value)
+        synth_lib().sbs_free_text(p)
+        return b
+
+    def header(self, sites_only=False) -> bytes:
+        n = C.c_size_t()
+        return self._take(synth_lib().sbs_header(self._h, 1 if sites_only else 0, C.byref(n)), n)
+
+    def records(self, lo, hi, sites_only=False, threads=0) -> bytes:
+        n = C.c_size_t()
+        return self._take(synth_lib().sbs_records(self._h, lo, hi, 1 if sites_only else 0, threads, C.byref(n)), n)
+
+    def chunks(self, sites_only=False, chunk=1 << 16, threads=0):
+        yield self.header(sites_only)
+        for lo in range(0, self.n_records, chunk):
+            yield self.records(lo, min(lo + chunk, self.n_records), sites_only, threads)
+
+    def write(self, path, sites_only=True, threads=0):
+        with open(path, 'wb') as f:
+            for c in self.chunks(sites_only, threads=threads):
+                f.write(c)
+        return path
+
+    def positions(self) -> np.ndarray:
+        if self._pos is None:
+            a = np.empty(self.n_records, dtype=np.uint32)
+            synth_lib().sbs_positions(self._h, a.ctypes.data)
+            self._pos = a
+        return self._pos
+
+    def alleles(self, i):
+        ref = C.create_string_buffer(256)
+        alt = C.create_string_buffer(256)
+        n = synth_lib().sbs_alleles(self._h, i, ref, 256, alt, 256)
+        return ref.value.decode(), alt.value.decode(), n
+
+    def build_store(self, location, *, device=0, keep_genotypes=True, threads=0, sites_only=False):
+        from .engine import Store
+        return Store.build([(location, self.chunks(sites_only=sites_only, threads=threads))], device=device,
+                           keep_genotypes=keep_genotypes, n_threads=threads)
+
+
+def beacon_request_payloads(*, vcf_location, chrom, start, end, reference_bases, alternate_bases,
+                            granularity='record', include='HIT', variant_type=None, vmin=0, vmax=-1,
+                            passthrough=None, dataset_id='synthetic', query_id='bench'):
+    """One Beacon request -> its PerformQueryPayloads (search_variants.py:179-238
+    + splitQuery)."""
+    if len(start) == 2:
+        start_min, start_max = start
+    else:
+        start_min = start[0]
+    if len(end) == 2:
+        end_min, end_max = end
+    else:
+        end_min, end_max = start_min, end[0]
+    if len(start) != 2:
+        start_max = end_max
+    sp = SplitQueryPayload(passthrough=passthrough or {}, dataset_id=dataset_id, query_id=query_id,
+                           reference_bases=reference_bases, start_min=start_min + 1, start_max=start_max + 1,
+                           end_min=end_min + 1, end_max=end_max + 1, alternate_bases=alternate_bases,
+                           variant_type=variant_type, include_datasets=include, vcf_locations={vcf_location: chrom},
+                           vcf_groups=[], requested_granularity=granularity, variant_min_length=vmin,
+                           variant_max_length=vmax)
+    return split_payloads(sp)
+
+
+def config2_requests(gen: SyntheticVcf, *, n_range=5000, n_point=5000, seed=1022):
+    """The 10k-request mix of config 2 as (kind, request-kwargs) tuples."""
+    rng = np.random.default_rng(seed)
+    pos = gen.positions()
+    lo, hi = int(pos[0]), int(pos[-1])
+    reqs = []
+    starts = rng.integers(lo, hi, n_range)
+    widths = rng.integers(1, 100001, n_range)
+    for s, w in zip(starts, widths):
+        reqs.append(dict(start=[int(s) - 1], end=[int(s) - 1 + int(w)], reference_bases='N',
+                         alternate_bases='N'))
+    for k in range(n_point):
+        if rng.random() < 0.7:
+            i = int(rng.integers(0, gen.n_records))
+            p = int(pos[i])
+            ref, alt, _ = gen.alleles(i)
+            ref, alt = ref.upper(), alt.upper()
+        else:
+            p = int(rng.integers(lo, hi))
+            b = rng.choice(list('ACGT'), 2, replace=False)
+            ref, alt = str(b[0]), str(b[1])
+        reqs.append(dict(start=[p - 1], end=[p - 1 + len(alt)], reference_bases=ref, alternate_bases=alt))
+    return reqs
+
+
+def requests_to_payloads(reqs, *, vcf_location, chrom):
+    """Flatten requests into slice payloads; returns (payloads, owner) where
+    owner[j] = request index of payload j."""
+    payloads, owner = [], []
+    for ri, r in enumerate(reqs):
+        ps = beacon_request_payloads(vcf_location=vcf_location, chrom=chrom, **r)
+        payloads.extend(ps)
+        owner.extend([ri] * len(ps))
+    return payloads, owner

@@ -1,0 +1,137 @@
+"""Device parity: libsbeacon_hip.so (HIP kernels on an MI355X) against the
+reference goldens and the C oracle.  Bit-exact: integer and string work."""
+import os
+import random
+
+import pytest
+
+from conftest import FIXTURES, normalise
+from payload_gen import random_payload, read_records
+
+pytestmark = pytest.mark.gpu
+
+
+def _cmp(got, c):
+    """got: response object or exception; c: golden case."""
+    if c['error']:
+        assert isinstance(got, Exception) and type(got).__name__ == c['error'], (c['payload'], got)
+    else:
+        assert not isinstance(got, Exception), (c['payload'], got)
+        assert normalise(got.dump()) == normalise(c['response']), c['payload']
+
+
+@pytest.fixture(scope='module')
+def fixture_stores():
+    from sbeacon.engine import Store
+    return {n: Store.build([(n + '.vcf', os.path.join(FIXTURES, n + '.vcf'))], device=0)
+            for n in ('tiny22', 'quirk22')}
+
+
+@pytest.mark.parametrize('fixture', ['tiny22', 'quirk22'])
+def test_reference_goldens(goldens, fixture_stores, fixture):
+    cases = [c for c in goldens if c['fixture'] == fixture and c['oracle'] == 'reference']
+    rs = fixture_stores[fixture].query([c['payload'] for c in cases], strict_variant_type=True)
+    got = rs.responses()
+    for g, c in zip(got, cases):
+        _cmp(g, c)
+
+
+@pytest.mark.parametrize('fixture', ['tiny22', 'quirk22'])
+def test_patched_variant_type_goldens(goldens, fixture_stores, fixture):
+    cases = [c for c in goldens if c['fixture'] == fixture and c['oracle'] == 'patched-oracle']
+    assert cases
+    got = fixture_stores[fixture].query([c['payload'] for c in cases]).responses()
+    for g, c in zip(got, cases):
+        _cmp(g, c)
+
+
+def _vs_oracle(store, orc, payloads):
+    got = store.query(payloads).responses()
+    exp = orc.perform_query_batch(payloads, patched=True)
+    for p, g, e in zip(payloads, got, exp):
+        if isinstance(e, type):
+            assert isinstance(g, e), (p, g)
+        else:
+            assert not isinstance(g, Exception), (p, g)
+            assert normalise(g.dump()) == normalise(e), p
+
+
+@pytest.mark.parametrize('seed,quirks,n_rec,n_samp', [(11, False, 20000, 40), (12, True, 6000, 70),
+                                                        (13, False, 3000, 130)])
+def test_random_vs_oracle(tmp_path, seed, quirks, n_rec, n_samp):
+    from oracle.oracle import OracleVcf
+    from sbeacon import synth
+    from sbeacon.engine import Store
+    path = str(tmp_path / f'r{seed}.vcf')
+    synth.make_fixture(path, n_records=n_rec, n_samples=n_samp, seed=seed, quirks=quirks)
+    store = Store.build([('r.vcf', path)], device=0)
+    orc = OracleVcf(path)
+    recs, names = read_records(path)
+    rng = random.Random(seed)
+    payloads = [random_payload(rng, recs, names, 'r.vcf') for _ in range(3000)]
+    _vs_oracle(store, orc, payloads)
+
+
+def test_multi_vcf_store_and_unknown_contig():
+    from oracle.oracle import OracleVcf
+    from sbeacon.engine import Store
+    locs = {n: os.path.join(FIXTURES, n + '.vcf') for n in ('tiny22', 'quirk22')}
+    store = Store.build(list(locs.items()), device=0)
+    rng = random.Random(3)
+    payloads = []
+    for n, path in locs.items():
+        recs, names = read_records(path)
+        payloads += [random_payload(rng, recs, names, n) for _ in range(400)]
+    rng.shuffle(payloads)
+    payloads[0] = dict(payloads[0], region='7:1-100000000')  # contig absent -> empty slice
+    got = store.query(payloads).responses()
+    orcs = {n: OracleVcf(p) for n, p in locs.items()}
+    for p, g in zip(payloads, got):
+        try:
+            e = orcs[p['vcf_location']].perform_query(p, patched=True)
+        except Exception as ex:  # noqa: BLE001
+            assert type(g) is type(ex), p
+            continue
+        assert normalise(g.dump()) == normalise(e), p
+
+
+def test_prepared_batch_is_repeatable():
+    from sbeacon.engine import Store
+    path = os.path.join(FIXTURES, 'tiny22.vcf')
+    store = Store.build([('t.vcf', path)], device=0)
+    recs, names = read_records(path)
+    rng = random.Random(9)
+    payloads = [random_payload(rng, recs, names, 't.vcf', alt_none_p=0.0) for _ in range(500)]
+    b = store.prepare(payloads)
+    outs = []
+    for _ in range(3):
+        b.run()
+        b.sync()
+        t = b.timing()
+        assert t['total_ms'] > 0 and t['scan_ms'] > 0
+        outs.append([r.dump() if not isinstance(r, Exception) else type(r) for r in b.fetch().responses()])
+    assert outs[0] == outs[1] == outs[2]
+    one = [r.dump() if not isinstance(r, Exception) else type(r) for r in store.query(payloads).responses()]
+    assert one == outs[0]
+
+
+def test_handlers_through_registry():
+    from sbeacon import engine, perform_query, split_query
+    from sbeacon.engine import Store
+    path = os.path.join(FIXTURES, 'tiny22.vcf')
+    store = Store.build([('s3://bucket/tiny22.vcf.gz', path)], device=0)
+    engine.registry.register(store)
+    out = split_query.lambda_handler(dict(passthrough={}, dataset_id='d', query_id='q', reference_bases='N',
+                                          start_min=16050000, start_max=16080000, end_min=16050000,
+                                          end_max=16080000, alternate_bases='N', variant_type=None,
+                                          include_datasets='HIT', vcf_locations={'s3://bucket/tiny22.vcf.gz': '22'},
+                                          vcf_groups=[], requested_granularity='record', variant_min_length=0,
+                                          variant_max_length=-1), None)
+    assert len(out) == 4 and all(o['exists'] for o in out[:3])
+    ev = {'Records': [{'Sns': {'Message': __import__('json').dumps(dict(
+        region='22:16050000-16059999', reference_bases='N', end_min=0, end_max=10**9, alternate_bases='N',
+        include_details=True, requested_granularity='count', variant_min_length=0, variant_max_length=-1,
+        vcf_location='s3://bucket/tiny22.vcf.gz', dataset_id='d'))}}]}
+    r = perform_query.lambda_handler(ev, None)
+    assert r['exists'] and r['call_count'] > 0 and r['variants']
+    engine.registry.clear()
