@@ -2,11 +2,11 @@
 //
 // The query path mirrors one splitQuery fan-out (lambda/splitQuery/
 // lambda_function.py:74-110) handed to the device as ONE batch: every
-// PerformQueryPayload becomes a QDev, and the kernel sequence
-//   bounds (64-ary lower_bound) -> caps prefix sum -> range scan -> hit
-//   prefix sum -> dense compaction
-// runs on the store's HIP stream.  Result strings are formatted on the host
-// from the store's allele blob in the reference's exact format.
+// PerformQueryPayload becomes a QDev; the host plans each query's output
+// region from the store's coarse POS index (an upper bound on its hits), so
+// a query step is a single kernel launch (query_kernels.hip).  Result strings
+// are formatted on the host from the store's allele blob in the reference's
+// exact format.
 #include <algorithm>
 #include <array>
 #include <cstdio>
@@ -77,7 +77,6 @@ struct DevMem {  // RAII device allocation for batches
     ~DevMem() { release(); }
 };
 
-
 struct ParsedRegion {
     std::string chrom;
     int64_t first = 0, last = 0;
@@ -139,24 +138,20 @@ struct sb_batch {
     sb_store *s = nullptr;
     uint32_t nq = 0;
     std::vector<QDev> hq;
-    std::vector<int32_t> host_err;         // errors raised before any record is read
-    std::vector<std::string> chrom;        // region chrom per query (variant strings)
+    std::vector<int32_t> host_err;               // errors raised before any record is read
+    std::vector<std::string> chrom;              // region chrom per query (variant strings)
     std::vector<std::vector<uint32_t>> emitted;  // header indices of the emitted samples
     std::vector<uint8_t> samples_variant;
     std::vector<uint32_t> vcf;
     uint64_t cap_total = 0, samples_words = 0;
-    DevMem q, qbytes, subsets, lut, lohi, caps, hit_off, scan_tmp, hit_rec, hit_alt, res, nhits, dense_off,
-        dense_rec, dense_alt, samples_out;
-    // one event quad per run since the last sync: start, after bounds+caps
-    // scan, after the range scan, end.  sync() averages them.
-    std::vector<std::array<hipEvent_t, 4>> ev;
+    DevMem q, qbytes, subsets, lut, res, hits, samples_out;
+    // one event pair per run since the last sync; sync() averages them
+    std::vector<std::array<hipEvent_t, 2>> ev;
     size_t runs_pending = 0;
-    float last_total_ms = 0, last_scan_ms = 0, last_bounds_ms = 0;
-    uint64_t runs_timed = 0;
-    bool ran = false;
+    float last_total_ms = 0;
     ~sb_batch() {
-        for (auto &q : ev)
-            for (auto &e : q)
+        for (auto &q2 : ev)
+            for (auto &e : q2)
                 if (e) (void)hipEventDestroy(e);
     }
 };
@@ -165,111 +160,171 @@ struct sb_result_set {
     sb_store *s = nullptr;
     std::vector<QRes> res;
     std::vector<uint64_t> dense_off;
-    std::vector<uint32_t> rec, alt;
-    std::vector<std::vector<uint32_t>> sidx;   // emitted-list positions
+    std::vector<uint64_t> hit;                  // rec | alt << 32
+    std::vector<std::vector<uint32_t>> sidx;    // emitted-list positions
     std::vector<std::vector<uint32_t>> emitted;
     std::vector<uint32_t> vcf_of;
     std::vector<uint8_t> samples_variant;
     std::vector<std::string> chrom;
     std::vector<std::string> vtext, ntext;
     std::vector<uint8_t> vbuilt, nbuilt;
+    std::vector<uint32_t> tmp_rec, tmp_alt;     // views for sb_result_get
     sb_batch_stats stats{};
 };
 
-
 namespace {
 
+// coarse POS index of one segment: bucket[b] = first record with
+// POS >= base + (b << shift), for b in [0, n]; bucket[n] = segment end
+void build_buckets(const std::vector<uint32_t> &pos, const Segment &sg, BucketIndex &bi,
+                   std::vector<uint32_t> &bucket) {
+    bi.off = bucket.size();
+    if (sg.hi <= sg.lo) {
+        bi.base = 0;
+        bi.shift = 31;
+        bi.n = 1;
+        bucket.push_back(sg.lo);
+        bucket.push_back(sg.hi);
+        return;
+    }
+    const uint32_t base = pos[sg.lo];
+    const uint64_t span = static_cast<uint64_t>(pos[sg.hi - 1]) - base;
+    const uint64_t n = sg.hi - sg.lo;
+    // aim for ~32 records per bucket on average
+    const double gap = n > 1 ? static_cast<double>(span) / static_cast<double>(n - 1) : 1.0;
+    uint32_t shift = 0;
+    while (shift < 31 && static_cast<double>(1ull << (shift + 1)) <= gap * 32.0) ++shift;
+    const uint64_t nb = (span >> shift) + 1;
+    bi.base = base;
+    bi.shift = shift;
+    bi.n = static_cast<uint32_t>(nb);
+    uint32_t r = sg.lo;
+    for (uint64_t b = 0; b <= nb; ++b) {
+        const uint64_t x = static_cast<uint64_t>(base) + (b << shift);
+        while (r < sg.hi && pos[r] < x) ++r;
+        bucket.push_back(r);
+    }
+    bucket.back() = sg.hi;
+}
+
 void upload_store(sb_builder &b, sb_store &s) {
-    std::vector<uint32_t> pos, end, meta, alt_lo, alt_len, alt_cls, fb;
-    std::vector<int32_t> an, ac;
-    std::vector<uint64_t> ref_key, ref_off, alt_key, alt_off, planes;
+    std::vector<RecHot> rec;
+    std::vector<uint32_t> pos, a0_len, x_lo, x_cls, x_len, fb, bucket;
+    std::vector<int32_t> x_ac;
+    std::vector<uint64_t> ref_key, a0_key, ref_off, a0_off, x_key, x_off, planes;
     std::vector<int64_t> fb_off;
+    std::vector<uint16_t> vt;
     std::vector<uint8_t> blob;
-    uint64_t nr = 0, na = 0;
+    uint64_t nr = 0, nx = 0, np = 0;
     for (auto &v : b.vcfs) {
         nr += v.c.pos.size();
-        na += v.c.alt_key.size();
+        nx += v.c.x_key.size();
+        np += v.c.planes0.size() + v.c.planesx.size();
     }
-    if (nr >= 0xffffffffull || na >= 0xffffffffull) throw Error(SB_EINVAL, "store exceeds 2^32 records/alt rows per device; shard it");
+    if (nr >= 0xfffffff0ull || nx >= 0xfffffff0ull)
+        throw Error(SB_EINVAL, "store exceeds 2^32 records per device; shard it across devices");
+    rec.reserve(nr);
     pos.reserve(nr);
-    end.reserve(nr);
-    meta.reserve(nr);
-    an.reserve(nr);
-    ref_key.reserve(nr);
-    ref_off.reserve(nr);
-    fb_off.reserve(nr);
-    alt_lo.reserve(nr + 1);
-    alt_key.reserve(na);
-    alt_len.reserve(na);
-    alt_cls.reserve(na);
-    ac.reserve(na);
-    alt_off.reserve(na);
+    planes.reserve(np);
     for (auto &v : b.vcfs) {
         VcfCols &c = v.c;
         const uint32_t rec_base = static_cast<uint32_t>(pos.size());
-        const uint32_t alt_base = static_cast<uint32_t>(alt_key.size());
+        const uint32_t x_base = static_cast<uint32_t>(x_key.size());
         const uint64_t blob_base = blob.size();
         const int64_t fb_base = static_cast<int64_t>(fb.size());
-        v.rec_base = rec_base;
-        v.alt_base = alt_base;
-        v.plane_base = planes.size();
         const size_t n = c.pos.size();
+        v.rec_base = rec_base;
+        v.x_base = x_base;
+        v.nonneg = !c.any_negative;
+        v.has_planes = !c.planes0.empty();
+        v.plane0_base = planes.size();
+        planes.insert(planes.end(), c.planes0.begin(), c.planes0.end());
+        v.planex_base = planes.size();
+        planes.insert(planes.end(), c.planesx.begin(), c.planesx.end());
+        rec.insert(rec.end(), c.rec.begin(), c.rec.end());
         pos.insert(pos.end(), c.pos.begin(), c.pos.end());
-        end.insert(end.end(), c.end.begin(), c.end.end());
-        meta.insert(meta.end(), c.meta.begin(), c.meta.end());
-        an.insert(an.end(), c.an.begin(), c.an.end());
+        a0_len.insert(a0_len.end(), c.a0_len.begin(), c.a0_len.end());
         ref_key.insert(ref_key.end(), c.ref_key.begin(), c.ref_key.end());
-        for (size_t i = 0; i < n; ++i) ref_off.push_back(c.ref_off[i] + blob_base);
-        for (size_t i = 0; i < n; ++i) fb_off.push_back(c.fb_off[i] < 0 ? -1 : c.fb_off[i] + fb_base);
-        for (size_t i = 0; i < n; ++i) alt_lo.push_back(c.alt_lo[i] + alt_base);
-        alt_key.insert(alt_key.end(), c.alt_key.begin(), c.alt_key.end());
-        alt_len.insert(alt_len.end(), c.alt_len.begin(), c.alt_len.end());
-        alt_cls.insert(alt_cls.end(), c.alt_cls.begin(), c.alt_cls.end());
-        ac.insert(ac.end(), c.ac.begin(), c.ac.end());
-        for (size_t i = 0; i < c.alt_off.size(); ++i) alt_off.push_back(c.alt_off[i] + blob_base);
+        a0_key.insert(a0_key.end(), c.a0_key.begin(), c.a0_key.end());
+        vt.insert(vt.end(), c.vt.begin(), c.vt.end());
+        for (size_t i = 0; i < n; ++i) {
+            ref_off.push_back(c.ref_off[i] + blob_base);
+            a0_off.push_back(c.a0_off[i] + blob_base);
+            fb_off.push_back(c.fb_off[i] < 0 ? -1 : c.fb_off[i] + fb_base);
+            x_lo.push_back(c.x_lo[i] + x_base);
+        }
+        x_cls.insert(x_cls.end(), c.x_cls.begin(), c.x_cls.end());
+        x_len.insert(x_len.end(), c.x_len.begin(), c.x_len.end());
+        x_ac.insert(x_ac.end(), c.x_ac.begin(), c.x_ac.end());
+        x_key.insert(x_key.end(), c.x_key.begin(), c.x_key.end());
+        for (size_t i = 0; i < c.x_off.size(); ++i) x_off.push_back(c.x_off[i] + blob_base);
         blob.insert(blob.end(), c.blob.begin(), c.blob.end());
-        planes.insert(planes.end(), c.planes.begin(), c.planes.end());
         fb.insert(fb.end(), c.fb.begin(), c.fb.end());
         for (auto &sg : v.segments) {
             sg.lo += rec_base;
             sg.hi += rec_base;
         }
-        s.max_words = std::max(s.max_words, c.planes.empty() ? 0u : v.words);
+        s.max_words = std::max(s.max_words, v.has_planes ? v.words : 0u);
         c = VcfCols();  // release the per-vcf copy
     }
-    alt_lo.push_back(static_cast<uint32_t>(alt_key.size()));
+    x_lo.push_back(static_cast<uint32_t>(x_key.size()));
+    for (auto &v : b.vcfs) {
+        v.buckets.resize(v.segments.size());
+        for (size_t i = 0; i < v.segments.size(); ++i) build_buckets(pos, v.segments[i], v.buckets[i], bucket);
+    }
     s.n_records = pos.size();
-    s.n_alt = alt_key.size();
+    s.n_extra = x_key.size();
 
+    s.d.rec = dev_upload(s, rec);
     s.d.pos = dev_upload(s, pos);
-    s.d.end = dev_upload(s, end);
     s.d.ref_key = dev_upload(s, ref_key);
-    s.d.meta = dev_upload(s, meta);
-    s.d.an = dev_upload(s, an);
-    s.d.alt_lo = dev_upload(s, alt_lo);
+    s.d.a0_key = dev_upload(s, a0_key);
+    s.d.a0_len = dev_upload(s, a0_len);
+    s.d.x_lo = dev_upload(s, x_lo);
     s.d.ref_off = dev_upload(s, ref_off);
+    s.d.a0_off = dev_upload(s, a0_off);
     s.d.fb_off = dev_upload(s, fb_off);
-    s.d.alt_key = dev_upload(s, alt_key);
-    s.d.alt_len = dev_upload(s, alt_len);
-    s.d.alt_cls = dev_upload(s, alt_cls);
-    s.d.ac = dev_upload(s, ac);
-    s.d.alt_off = dev_upload(s, alt_off);
+    s.d.x_cls = dev_upload(s, x_cls);
+    s.d.x_ac = dev_upload(s, x_ac);
+    s.d.x_key = dev_upload(s, x_key);
+    s.d.x_len = dev_upload(s, x_len);
+    s.d.x_off = dev_upload(s, x_off);
     s.d.blob = dev_upload(s, blob);
     s.d.planes = dev_upload(s, planes);
     s.d.fb = dev_upload(s, fb);
+    s.d.bucket = dev_upload(s, bucket);
     HIP_OK(hipStreamSynchronize(s.stream));
-    // host copies for result formatting
+    // host copies for output planning and result formatting
     s.h_pos = std::move(pos);
-    s.h_end = std::move(end);
-    s.h_meta = std::move(meta);
+    s.h_end.resize(rec.size());
+    for (size_t i = 0; i < rec.size(); ++i) s.h_end[i] = rec[i].end;
+    s.h_a0_len = std::move(a0_len);
+    s.h_x_lo = std::move(x_lo);
+    s.h_x_len = std::move(x_len);
+    s.h_bucket = std::move(bucket);
+    s.h_vt = std::move(vt);
     s.h_ref_off = std::move(ref_off);
-    s.h_alt_off = std::move(alt_off);
-    s.h_alt_len = std::move(alt_len);
-    s.h_alt_lo = std::move(alt_lo);
+    s.h_a0_off = std::move(a0_off);
+    s.h_x_off = std::move(x_off);
     s.h_blob = std::move(blob);
 }
 
 const char *kRegexMeta = "^$*+?{}[]\\|()";
+
+// coarse bracket used to plan the output region: first record of the bucket
+// holding x (<= the exact lower bound) / end of that bucket (>= it)
+uint32_t bucket_floor(const sb_store &s, const QDev &d, int64_t x) {
+    if (x <= static_cast<int64_t>(d.bucket_base)) return d.seg_lo;
+    const uint64_t b = static_cast<uint64_t>(x - d.bucket_base) >> d.bucket_shift;
+    if (b >= d.n_buckets) return d.seg_hi;
+    return s.h_bucket[d.bucket_off + b];
+}
+uint32_t bucket_ceil(const sb_store &s, const QDev &d, int64_t x) {
+    if (x <= static_cast<int64_t>(d.bucket_base)) return d.seg_lo;
+    const uint64_t b = static_cast<uint64_t>(x - d.bucket_base) >> d.bucket_shift;
+    if (b >= d.n_buckets) return d.seg_hi;
+    return s.h_bucket[d.bucket_off + b + 1];
+}
 
 void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     sb_store &s = *B.s;
@@ -285,7 +340,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     std::vector<uint64_t> subsets;
     std::vector<uint32_t> lut_all;
     std::unordered_map<std::string, uint32_t> lut_cache;
-    uint64_t samples_words = 0;
+    uint64_t samples_words = 0, cap_total = 0;
     for (size_t i = 0; i < nq; ++i) {
         const sb_query &x = qs[i];
         QDev &d = B.hq[i];
@@ -306,10 +361,15 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         auto it = v.seg_index.find(rg.chrom);
         if (it == v.seg_index.end()) {
             d.flags |= F_EMPTY;
-            d.seg_lo = d.seg_hi = 0;
         } else {
-            d.seg_lo = v.segments[it->second].lo;
-            d.seg_hi = v.segments[it->second].hi;
+            const Segment &sg = v.segments[it->second];
+            const BucketIndex &bi = v.buckets[it->second];
+            d.seg_lo = sg.lo;
+            d.seg_hi = sg.hi;
+            d.bucket_off = bi.off;
+            d.bucket_base = bi.base;
+            d.bucket_shift = bi.shift;
+            d.n_buckets = bi.n;
         }
         d.end_min = x.end_min;
         d.end_max = x.end_max;
@@ -318,8 +378,11 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         const uint32_t n_samples = static_cast<uint32_t>(v.samples.size());
         d.words = v.words;
         d.n_samples = n_samples;
-        d.alt_base = v.alt_base;
-        d.plane_base = v.plane_base;
+        d.rec_base = v.rec_base;
+        d.x_base = v.x_base;
+        d.plane0_base = v.plane0_base;
+        d.planex_base = v.planex_base;
+        if (v.nonneg) d.flags |= F_NONNEG;
         if (samples_variant) {  // bcftools --samples (svs:36-42), header order
             const std::string names = x.sample_names ? std::string(x.sample_names, x.sample_names_len) : std::string("_");
             std::vector<uint8_t> sel(n_samples, 0);
@@ -377,13 +440,13 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
             if (x.strict_variant_type) d.flags |= F_STRICT_UNBOUND;
             const std::string vt = x.variant_type ? std::string(x.variant_type, x.variant_type_len) : std::string("None");
             const bool has = x.variant_type != nullptr;
-            d.vt_kind = !has ? VT_OTHER
-                        : vt == "DEL" ? VT_DEL
-                        : vt == "INS" ? VT_INS
-                        : vt == "DUP" ? VT_DUP
+            d.vt_kind = !has                 ? VT_OTHER
+                        : vt == "DEL"        ? VT_DEL
+                        : vt == "INS"        ? VT_INS
+                        : vt == "DUP"        ? VT_DUP
                         : vt == "DUP:TANDEM" ? VT_DUPT
-                        : vt == "CNV" ? VT_CNV
-                                      : VT_OTHER;
+                        : vt == "CNV"        ? VT_CNV
+                                             : VT_OTHER;
             const std::string key = std::to_string(d.vt_kind) + "|" + vt;
             auto lt = lut_cache.find(key);
             if (lt == lut_cache.end()) {
@@ -415,13 +478,21 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         if (collect) {
             d.flags |= F_COLLECT;
             if (x.include_details && v.words) {
-                if (s.max_words == 0) throw Error(SB_EINVAL, "sample path requested but the store was built without genotypes");
+                if (!v.has_planes) throw Error(SB_EINVAL, "sample path requested but the store was built without genotypes");
                 d.samples_out_off = samples_words;
                 samples_words += v.words;
             }
         }
+        // output region: every ALT row of the records in the coarse bracket
+        d.hit_off = cap_total;
+        if (!(d.flags & F_EMPTY) && d.first_bp <= d.last_bp) {
+            const uint32_t lo = bucket_floor(s, d, d.first_bp);
+            const uint32_t hi = std::max(lo, bucket_ceil(s, d, d.last_bp + 1));
+            cap_total += static_cast<uint64_t>(hi - lo) + (s.h_x_lo[hi] - s.h_x_lo[lo]);
+        }
     }
     B.samples_words = samples_words;
+    B.cap_total = cap_total;
     if (lut_all.empty()) lut_all.push_back(0);
     // ---- device buffers
     HIP_OK(hipSetDevice(s.device));
@@ -434,28 +505,10 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     if (!qbytes.empty()) HIP_OK(hipMemcpyAsync(B.qbytes.p, qbytes.data(), qbytes.size(), hipMemcpyHostToDevice, st));
     if (!subsets.empty()) HIP_OK(hipMemcpyAsync(B.subsets.p, subsets.data(), subsets.size() * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(B.lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
-    B.lohi.alloc(size_t(nq) * 8);
-    B.caps.alloc(size_t(nq) * 4);
-    B.hit_off.alloc((size_t(nq) + 1) * 8);
-    B.dense_off.alloc((size_t(nq) + 1) * 8);
-    B.scan_tmp.alloc(scan_tmp_words(static_cast<uint32_t>(nq)) * 8 + 64);
     B.res.alloc(size_t(nq) * sizeof(QRes));
-    B.nhits.alloc(size_t(nq) * 4);
+    B.hits.alloc(cap_total * 8);
     B.samples_out.alloc(samples_words * 8);
-    // size the hit buffers: bounds + capacity prefix sum, then one 8-byte readback
-    DStore d = s.d;
-    d.sym_lut = B.lut.as<uint32_t>();
-    launch_bounds(d, B.q.as<QDev>(), B.nq, B.lohi.as<uint32_t>(), B.caps.as<uint32_t>(), st);
-    launch_exclusive_scan(B.caps.as<uint32_t>(), B.nq, B.hit_off.as<uint64_t>(), B.scan_tmp.as<uint64_t>(), st);
-    HIP_OK(hipGetLastError());
-    uint64_t total = 0;
-    HIP_OK(hipMemcpyAsync(&total, B.hit_off.as<uint64_t>() + nq, 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    B.cap_total = total;
-    B.hit_rec.alloc(total * 4);
-    B.hit_alt.alloc(total * 4);
-    B.dense_rec.alloc(total * 4);
-    B.dense_alt.alloc(total * 4);
 }
 
 void run(sb_batch &B) {
@@ -464,49 +517,30 @@ void run(sb_batch &B) {
     hipStream_t st = s.stream;
     DStore d = s.d;
     d.sym_lut = B.lut.as<uint32_t>();
-    const uint32_t nq = B.nq;
     if (B.runs_pending == B.ev.size()) {
-        std::array<hipEvent_t, 4> q{};
+        std::array<hipEvent_t, 2> q{};
         for (auto &e : q) HIP_OK(hipEventCreate(&e));
         B.ev.push_back(q);
     }
     const auto &E = B.ev[B.runs_pending++];
     HIP_OK(hipEventRecord(E[0], st));
-    launch_bounds(d, B.q.as<QDev>(), nq, B.lohi.as<uint32_t>(), B.caps.as<uint32_t>(), st);
-    launch_exclusive_scan(B.caps.as<uint32_t>(), nq, B.hit_off.as<uint64_t>(), B.scan_tmp.as<uint64_t>(), st);
+    launch_scan(d, B.q.as<QDev>(), B.nq, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(), s.max_words,
+                B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), st);
     HIP_OK(hipEventRecord(E[1], st));
-    launch_scan(d, B.q.as<QDev>(), nq, B.lohi.as<uint32_t>(), B.hit_off.as<uint64_t>(), B.qbytes.as<uint8_t>(),
-                B.subsets.as<uint64_t>(), s.max_words, B.res.as<QRes>(), B.nhits.as<uint32_t>(),
-                B.hit_rec.as<uint32_t>(), B.hit_alt.as<uint32_t>(), B.samples_out.as<uint64_t>(), st);
-    HIP_OK(hipEventRecord(E[2], st));
-    launch_exclusive_scan(B.nhits.as<uint32_t>(), nq, B.dense_off.as<uint64_t>(), B.scan_tmp.as<uint64_t>(), st);
-    launch_compact(B.hit_off.as<uint64_t>(), B.dense_off.as<uint64_t>(), B.nhits.as<uint32_t>(), nq,
-                   B.hit_rec.as<uint32_t>(), B.hit_alt.as<uint32_t>(), B.dense_rec.as<uint32_t>(),
-                   B.dense_alt.as<uint32_t>(), st);
-    HIP_OK(hipEventRecord(E[3], st));
     HIP_OK(hipGetLastError());
-    B.ran = true;
 }
 
 void sync(sb_batch &B) {
     HIP_OK(hipSetDevice(B.s->device));
     HIP_OK(hipStreamSynchronize(B.s->stream));
     if (B.runs_pending) {
-        double t = 0, b = 0, sc = 0;
+        double t = 0;
         for (size_t i = 0; i < B.runs_pending; ++i) {
             float x;
-            HIP_OK(hipEventElapsedTime(&x, B.ev[i][0], B.ev[i][3]));
-            t += x;
             HIP_OK(hipEventElapsedTime(&x, B.ev[i][0], B.ev[i][1]));
-            b += x;
-            HIP_OK(hipEventElapsedTime(&x, B.ev[i][1], B.ev[i][2]));
-            sc += x;
+            t += x;
         }
-        const double n = static_cast<double>(B.runs_pending);
-        B.last_total_ms = static_cast<float>(t / n);
-        B.last_bounds_ms = static_cast<float>(b / n);
-        B.last_scan_ms = static_cast<float>(sc / n);
-        B.runs_timed = B.runs_pending;
+        B.last_total_ms = static_cast<float>(t / static_cast<double>(B.runs_pending));
         B.runs_pending = 0;
     }
 }
@@ -519,28 +553,37 @@ sb_result_set *fetch(sb_batch &B) {
     R->s = &s;
     const uint32_t nq = B.nq;
     R->res.resize(nq);
-    R->dense_off.resize(size_t(nq) + 1);
     if (nq) HIP_OK(hipMemcpyAsync(R->res.data(), B.res.p, nq * sizeof(QRes), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(R->dense_off.data(), B.dense_off.p, (size_t(nq) + 1) * 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    const uint64_t total = R->dense_off[nq];
-    R->rec.resize(total);
-    R->alt.resize(total);
     std::vector<uint64_t> sout(B.samples_words);
-    if (total) {
-        HIP_OK(hipMemcpyAsync(R->rec.data(), B.dense_rec.p, total * 4, hipMemcpyDeviceToHost, st));
-        HIP_OK(hipMemcpyAsync(R->alt.data(), B.dense_alt.p, total * 4, hipMemcpyDeviceToHost, st));
-    }
     if (!sout.empty()) HIP_OK(hipMemcpyAsync(sout.data(), B.samples_out.p, sout.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    for (uint32_t i = 0; i < nq; ++i)
+        if (B.host_err[i]) R->res[i].error = B.host_err[i];
+    // dense offsets on the host, gather on the device, one D2H
+    R->dense_off.assign(size_t(nq) + 1, 0);
+    for (uint32_t i = 0; i < nq; ++i) R->dense_off[i + 1] = R->dense_off[i] + (R->res[i].error ? 0 : R->res[i].n_hits);
+    const uint64_t total = R->dense_off[nq];
+    R->hit.resize(total);
+    if (total) {
+        DevMem doff, dense;
+        doff.alloc((size_t(nq) + 1) * 8);
+        dense.alloc(total * 8);
+        HIP_OK(hipMemcpyAsync(doff.p, R->dense_off.data(), (size_t(nq) + 1) * 8, hipMemcpyHostToDevice, st));
+        // queries with an error report n_hits = 0 on the device (host errors are F_EMPTY)
+        launch_compact(B.q.as<QDev>(), doff.as<uint64_t>(), B.res.as<QRes>(), nq, B.hits.as<uint64_t>(),
+                       dense.as<uint64_t>(), st);
+        HIP_OK(hipGetLastError());
+        HIP_OK(hipMemcpyAsync(R->hit.data(), dense.p, total * 8, hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+    }
     R->sidx.assign(nq, std::vector<uint32_t>());
     R->emitted = B.emitted;
     R->chrom = B.chrom;
-    R->vcf_of.resize(nq);
+    R->vcf_of = B.vcf;
+    R->samples_variant = B.samples_variant;
     uint64_t scanned = 0;
     for (uint32_t i = 0; i < nq; ++i) {
         const QDev &d = B.hq[i];
-        if (B.host_err[i]) R->res[i].error = B.host_err[i];
         scanned += R->res[i].n_scanned;
         if (d.samples_out_off != ~0ull && !R->res[i].error) {
             const uint64_t *w = sout.data() + d.samples_out_off;
@@ -554,12 +597,16 @@ sb_result_set *fetch(sb_batch &B) {
             }
         }
     }
-    R->vcf_of = B.vcf;
-    R->samples_variant = B.samples_variant;
     R->vtext.assign(nq, std::string());
     R->ntext.assign(nq, std::string());
     R->vbuilt.assign(nq, 0);
     R->nbuilt.assign(nq, 0);
+    R->tmp_rec.resize(total);
+    R->tmp_alt.resize(total);
+    for (uint64_t h = 0; h < total; ++h) {
+        R->tmp_rec[h] = static_cast<uint32_t>(R->hit[h]);
+        R->tmp_alt[h] = static_cast<uint32_t>(R->hit[h] >> kHitAltShift);
+    }
     R->stats.n_queries = nq;
     R->stats.records_scanned = scanned;
     R->stats.hits = total;
@@ -646,7 +693,7 @@ int sb_store_get_info(const sb_store *s, sb_store_info *out) {
     return guard([&] {
         if (!s || !out) throw Error(SB_EINVAL, "NULL argument");
         out->n_records = s->n_records;
-        out->n_alt_rows = s->n_alt;
+        out->n_alt_rows = s->n_records + s->n_extra;
         out->n_vcfs = static_cast<uint32_t>(s->vcfs.size());
         uint32_t nseg = 0, ms = 0;
         for (const auto &v : s->vcfs) {
@@ -709,9 +756,10 @@ int sb_batch_sync(sb_batch *b) {
 
 int sb_batch_last_timing(const sb_batch *b, double *total_ms, double *scan_ms, double *bounds_ms) {
     if (!b) return SB_EINVAL;
+    // the query step is one launch: bounds are found inside the scan kernel
     if (total_ms) *total_ms = b->last_total_ms;
-    if (scan_ms) *scan_ms = b->last_scan_ms;
-    if (bounds_ms) *bounds_ms = b->last_bounds_ms;
+    if (scan_ms) *scan_ms = b->last_total_ms;
+    if (bounds_ms) *bounds_ms = 0.0;
     return SB_OK;
 }
 
@@ -748,7 +796,6 @@ int sb_query_batch(sb_store *s, const sb_query *q, size_t nq, uint32_t flags, sb
         prepare(B, q, nq);
         run(B);
         *out = fetch(B);
-        (void)hipSetDevice(s->device);
     });
 }
 
@@ -761,8 +808,8 @@ int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out) {
     out->all_alleles_count = q.all_alleles_count;
     const uint64_t a = r->dense_off[i], b = r->dense_off[i + 1];
     out->n_variants = q.error ? 0 : b - a;
-    out->hit_record = r->rec.data() + a;
-    out->hit_alt = r->alt.data() + a;
+    out->hit_record = r->tmp_rec.data() + a;
+    out->hit_alt = r->tmp_alt.data() + a;
     out->n_sample_indices = r->sidx[i].size();
     out->sample_indices = r->sidx[i].data();
     return SB_OK;
@@ -776,19 +823,24 @@ int sb_result_variants_text(sb_result_set *r, size_t i, const char **p, size_t *
         const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
         char num[16];
         for (uint64_t h = a; h < b; ++h) {
-            const uint32_t rec = r->rec[h];
-            const uint32_t alt_row = s.h_alt_lo[rec] + r->alt[h];
+            const uint32_t rec = static_cast<uint32_t>(r->hit[h]);
+            const uint32_t k = static_cast<uint32_t>(r->hit[h] >> kHitAltShift);
             if (h > a) o.push_back('\n');
-            o += r->chrom[i];
+            o += r->chrom[i];  // f'{chrom}\t{position}\t{reference}\t{alts[i]}\t{variant_type}' (:210)
             o.push_back('\t');
             const int nn = snprintf(num, sizeof num, "%u", s.h_pos[rec]);
             o.append(num, static_cast<size_t>(nn));
             o.push_back('\t');
             o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_ref_off[rec]), s.h_end[rec] - s.h_pos[rec] + 1);
             o.push_back('\t');
-            o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_alt_off[alt_row]), s.h_alt_len[alt_row]);
+            if (k == 0) {
+                o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_a0_off[rec]), s.h_a0_len[rec]);
+            } else {
+                const uint32_t x = s.h_x_lo[rec] + k - 1;
+                o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_x_off[x]), s.h_x_len[x]);
+            }
             o.push_back('\t');
-            o += s.vt.items[s.h_meta[rec] >> M_VT_SHIFT];
+            o += s.vt.items[s.h_vt[rec]];
         }
         r->vbuilt[i] = 1;
     }

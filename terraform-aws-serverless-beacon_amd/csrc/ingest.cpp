@@ -80,7 +80,6 @@ struct Parser {
         const uint64_t ref_key = allele_key(ref, ref_len, true, &ref_hashed);
         VcfCols &c = L.c;
         c.pos.push_back(static_cast<uint32_t>(pos));
-        c.end.push_back(static_cast<uint32_t>(end));
         c.ref_key.push_back(ref_key);
         c.ref_off.push_back(c.blob.size());
         c.blob.insert(c.blob.end(), ref, ref + ref_len);
@@ -168,8 +167,11 @@ struct Parser {
         for (uint32_t i = 0; i < na; ++i) gtcount[i] = 0;
         int64_t gt_an = 0;
         const bool need_fb = (!has_ac || !has_an || an_bad) && n_samples > 0;
-        const size_t plane0 = c.planes.size();
-        if (keep_gt && n_samples) c.planes.resize(plane0 + static_cast<size_t>(na) * words, 0ull);
+        const size_t plane0 = c.planes0.size(), planex = c.planesx.size();
+        if (keep_gt && n_samples) {
+            c.planes0.resize(plane0 + words, 0ull);
+            c.planesx.resize(planex + static_cast<size_t>(na - 1) * words, 0ull);
+        }
         int64_t fb_row = -1;
         if (need_fb) {
             fb_row = static_cast<int64_t>(c.fb.size());
@@ -248,8 +250,10 @@ struct Parser {
                             if (tl >= 1 && tl <= 2 && is_digit(g[i]) && (tl == 1 || (g[i] != '0' && is_digit(g[i + 1])))) {
                                 const uint32_t v = tl == 1 ? static_cast<uint32_t>(g[i] - '0')
                                                            : static_cast<uint32_t>((g[i] - '0') * 10 + (g[i + 1] - '0'));
-                                if (v >= 1 && v <= na)
-                                    c.planes[plane0 + static_cast<size_t>(v - 1) * words + (s >> 6)] |= 1ull << (s & 63);
+                                if (v == 1)
+                                    c.planes0[plane0 + (s >> 6)] |= 1ull << (s & 63);
+                                else if (v >= 2 && v <= na)
+                                    c.planesx[planex + static_cast<size_t>(v - 2) * words + (s >> 6)] |= 1ull << (s & 63);
                             }
                             i = j + 1;
                         }
@@ -259,56 +263,64 @@ struct Parser {
                 a = t + 1;
             }
         }
-        // ---- record columns
-        uint32_t meta = 0;
-        if (has_ac) meta |= M_HAS_AC;
-        if (has_an) meta |= M_HAS_AN;
-        if (ac_bad) meta |= M_AC_BAD;
-        if (an_bad) meta |= M_AN_BAD;
-        if (need_fb) meta |= M_HAS_FB;
-        if (ref_hashed) meta |= M_REF_HASHED;
-        c.meta.push_back(meta);
+        // ---- per-ALT class words (symbolic ids are resolved at merge)
+        uint32_t hot = 0;
+        if (has_ac) hot |= H_HAS_AC;
+        if (has_an) hot |= H_HAS_AN;
+        if (ac_bad) hot |= H_AC_BAD;
+        if (an_bad) hot |= H_AN_BAD;
+        if (need_fb) hot |= H_HAS_FB;
+        if (na > 1) hot |= H_MULTI;
         const int64_t anv = has_an ? an_val : gt_an;
         if (anv > INT32_MAX) return fail(L, "called-allele count beyond int32");
-        c.an.push_back(static_cast<int32_t>(anv));
-        c.fb_off.push_back(fb_row);
-        // ---- alt rows
+        int32_t ac0 = 0;
         for (uint32_t i = 0; i < na; ++i) {
             const uint8_t *ap = reinterpret_cast<const uint8_t *>(alts[i]);
             const size_t al = alens[i];
             bool hashed;
-            c.alt_key.push_back(allele_key(ap, al, true, &hashed));
-            c.alt_len.push_back(static_cast<uint32_t>(al));
+            const uint64_t key = allele_key(ap, al, true, &hashed);
             uint32_t cls = 0;
             if (al == 1) {
                 const uint8_t u = upc(ap[0]);
-                if (u == 'A' || u == 'C' || u == 'G' || u == 'T' || u == 'N') cls |= A_SINGLE_BASE;
+                if (u == 'A' || u == 'C' || u == 'G' || u == 'T' || u == 'N') cls |= C_SINGLE_BASE;
             }
-            if (al >= 1 && ap[0] == '<') cls |= A_SYMBOLIC;
-            if (al == 1 && ap[0] == '.') cls |= A_DOT;
-            if (hashed) cls |= A_HASHED;
+            if (al >= 1 && ap[0] == '<') cls |= C_SYMBOLIC;
+            if (al == 1 && ap[0] == '.') cls |= C_DOT;
             // alt == REF * k (raw bytes): fullmatch of '(REF){2,}' / '(REF)*' (:124,:146)
-            uint32_t rep = A_REP_NONE;
+            uint32_t rep = C_REP_NONE;
             if (al % ref_len == 0) {
                 const size_t k = al / ref_len;
                 bool ok = true;
                 for (size_t j = 0; j < k && ok; ++j) ok = memcmp(ap + j * ref_len, ref, ref_len) == 0;
                 if (ok) rep = k >= 62 ? 62u : static_cast<uint32_t>(k);
             }
-            cls |= rep << A_REP_SHIFT;
+            cls |= rep << C_REP_SHIFT;
             int64_t acval;
             if (has_ac) {
-                if (i >= n_ac) cls |= A_AC_MISSING;
+                if (i >= n_ac) cls |= C_AC_MISSING;
                 acval = (!ac_bad && i < n_ac && i < 64) ? acv[i] : 0;
+                if (acval < 0) c.any_negative = true;
             } else {
                 acval = gtcount[i];
             }
-            c.alt_cls.push_back(cls);
-            c.ac.push_back(static_cast<int32_t>(acval));
-            c.alt_off.push_back(c.blob.size());
+            if (i == 0) {
+                hot |= cls;
+                ac0 = static_cast<int32_t>(acval);
+                c.a0_key.push_back(key);
+                c.a0_len.push_back(static_cast<uint32_t>(al));
+                c.a0_off.push_back(c.blob.size());
+            } else {
+                c.x_key.push_back(key);
+                c.x_len.push_back(static_cast<uint32_t>(al));
+                c.x_cls.push_back(cls);
+                c.x_ac.push_back(static_cast<int32_t>(acval));
+                c.x_off.push_back(c.blob.size());
+            }
             c.blob.insert(c.blob.end(), ap, ap + al);
         }
-        c.alt_lo.push_back(static_cast<uint32_t>(c.alt_key.size()));
+        c.rec.push_back(RecHot{static_cast<uint32_t>(end), hot, static_cast<int32_t>(anv), ac0});
+        c.fb_off.push_back(fb_row);
+        c.x_lo.push_back(static_cast<uint32_t>(c.x_key.size()));
         return true;
     }
 
@@ -337,11 +349,17 @@ void parse_header_line(VcfData &v, const char *p, const char *e) {
     v.header_seen = true;
 }
 
+uint32_t sym_id(sb_builder &b, const uint8_t *p, uint32_t n) {
+    const uint32_t id = b.sym.get(std::string(reinterpret_cast<const char *>(p), n));
+    if (id > 0xffff) throw Error(SB_EPARSE, "more than 65535 distinct symbolic ALT strings");
+    return id;
+}
+
 void merge(sb_builder &b, VcfData &v, Local &L) {
     VcfCols &d = v.c;
     const VcfCols &s = L.c;
     const uint32_t rec0 = static_cast<uint32_t>(d.pos.size());
-    const uint32_t alt0 = static_cast<uint32_t>(d.alt_key.size());
+    const uint32_t x0 = static_cast<uint32_t>(d.x_key.size());
     const uint64_t blob0 = d.blob.size();
     const int64_t fb0 = static_cast<int64_t>(d.fb.size());
     const size_t nr = s.pos.size();
@@ -354,17 +372,18 @@ void merge(sb_builder &b, VcfData &v, Local &L) {
             v.seg_index.emplace(ctg, static_cast<uint32_t>(v.segments.size()));
             v.segments.push_back(Segment{ctg, r, r + 1});
         } else {
-            if (s.pos[i] < (r > 0 ? (i > 0 ? s.pos[i - 1] : d.pos.back()) : 0u))
-                throw Error(SB_EPARSE, "unsorted file: POS decreases on contig " + ctg);
+            const uint32_t prev = i > 0 ? s.pos[i - 1] : d.pos.back();
+            if (s.pos[i] < prev) throw Error(SB_EPARSE, "unsorted file: POS decreases on contig " + ctg);
             v.segments.back().hi = r + 1;
         }
     }
     auto app = [](auto &dst, const auto &src) { dst.insert(dst.end(), src.begin(), src.end()); };
     app(d.pos, s.pos);
-    app(d.end, s.end);
-    app(d.an, s.an);
     app(d.ref_key, s.ref_key);
-    d.meta.reserve(d.meta.size() + nr);
+    app(d.a0_key, s.a0_key);
+    app(d.a0_len, s.a0_len);
+    d.rec.reserve(d.rec.size() + nr);
+    d.vt.reserve(d.vt.size() + nr);
     std::string last_vt;
     uint32_t last_id = 0;
     bool have_last = false;
@@ -382,29 +401,30 @@ void merge(sb_builder &b, VcfData &v, Local &L) {
             }
             if (id > 0xffff) throw Error(SB_EPARSE, "more than 65535 distinct VT values");
         }
-        d.meta.push_back(s.meta[i] | (id << M_VT_SHIFT));
+        d.vt.push_back(static_cast<uint16_t>(id));
+        RecHot h = s.rec[i];
+        if (h.hot & C_SYMBOLIC) h.hot |= sym_id(b, s.blob.data() + s.a0_off[i], s.a0_len[i]) << C_SYM_SHIFT;
+        d.rec.push_back(h);
     }
     for (size_t i = 0; i < nr; ++i) d.ref_off.push_back(s.ref_off[i] + blob0);
+    for (size_t i = 0; i < nr; ++i) d.a0_off.push_back(s.a0_off[i] + blob0);
     for (size_t i = 0; i < nr; ++i) d.fb_off.push_back(s.fb_off[i] < 0 ? -1 : s.fb_off[i] + fb0);
-    for (size_t i = 1; i < s.alt_lo.size(); ++i) d.alt_lo.push_back(s.alt_lo[i] + alt0);
-    app(d.alt_key, s.alt_key);
-    app(d.alt_len, s.alt_len);
-    app(d.ac, s.ac);
-    for (size_t i = 0; i < s.alt_off.size(); ++i) d.alt_off.push_back(s.alt_off[i] + blob0);
-    d.alt_cls.reserve(d.alt_cls.size() + s.alt_cls.size());
-    for (size_t i = 0; i < s.alt_cls.size(); ++i) {
-        uint32_t cls = s.alt_cls[i];
-        if (cls & A_SYMBOLIC) {
-            const std::string str(reinterpret_cast<const char *>(s.blob.data() + s.alt_off[i]), s.alt_len[i]);
-            const uint32_t id = b.sym.get(str);
-            if (id > 0xffff) throw Error(SB_EPARSE, "more than 65535 distinct symbolic ALT strings");
-            cls |= id << A_SYM_SHIFT;
-        }
-        d.alt_cls.push_back(cls);
+    for (size_t i = 1; i < s.x_lo.size(); ++i) d.x_lo.push_back(s.x_lo[i] + x0);
+    app(d.x_key, s.x_key);
+    app(d.x_len, s.x_len);
+    app(d.x_ac, s.x_ac);
+    for (size_t i = 0; i < s.x_off.size(); ++i) d.x_off.push_back(s.x_off[i] + blob0);
+    d.x_cls.reserve(d.x_cls.size() + s.x_cls.size());
+    for (size_t i = 0; i < s.x_cls.size(); ++i) {
+        uint32_t cls = s.x_cls[i];
+        if (cls & C_SYMBOLIC) cls |= sym_id(b, s.blob.data() + s.x_off[i], s.x_len[i]) << C_SYM_SHIFT;
+        d.x_cls.push_back(cls);
     }
     app(d.blob, s.blob);
-    app(d.planes, s.planes);
+    app(d.planes0, s.planes0);
+    app(d.planesx, s.planesx);
     app(d.fb, s.fb);
+    d.any_negative = d.any_negative || s.any_negative;
 }
 
 void parse_records(sb_builder &b, VcfData &v, const char *p, size_t len) {

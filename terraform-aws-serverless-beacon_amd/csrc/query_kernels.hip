@@ -1,15 +1,22 @@
-// query_kernels.hip — CDNA4 (gfx950) kernels of the slice-query hot path.
+// query_kernels.hip — CDNA4 (gfx950) kernel of the slice-query hot path.
 //
 // Reference semantics: lambda/performQuery/search_variants.py:33-271 and
 // search_variants_in_samples.py:31-259 (restated in SURVEY.md §8a.1).  The
 // reference walks `bcftools query` output record by record in a Python loop;
-// here one 64-lane wavefront owns one slice query and walks its records 64 at
-// a time with coalesced SoA loads, turning the loop's order-dependent state
-// (cumulative call_count, include_details/boolean early exits, first error)
-// into ballots and wave prefix sums.
-//
-// All arithmetic is integer; nothing here is a dense contraction, so no MFMA.
-// The bound is HBM/Infinity-Cache bandwidth on the record columns.
+// here one 64-lane wavefront owns one slice query:
+//   1. exact [lo, hi) bounds of the slice from the segment's coarse POS index
+//      (two dependent rounds: scalar bucket loads, then 64-wide POS reads);
+//   2. a walk over the records 64 at a time, one 16-byte RecHot word per lane
+//      (global_load_dwordx4), the next chunk prefetched while this one is
+//      evaluated;
+//   3. the loop's order-dependent state — running call_count, `if
+//      call_count:`, include_details / boolean early exits, the first
+//      exception — as ballots, find-first-set and prefix sums;
+//   4. hits written as packed u64 into the query's host-planned region,
+//      positions from mbcnt (or a wave prefix sum for multi-hit lanes).
+// One launch answers a whole splitQuery fan-out.  All arithmetic is integer;
+// nothing here is a dense contraction, so no MFMA: the bound is memory
+// bandwidth on the RecHot stream.
 #include <hip/hip_runtime.h>
 
 #include "../../include/sbeacon.h"
@@ -27,6 +34,8 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+__device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll(static_cast<unsigned long long>(m)) - 1; }
 
 __device__ __forceinline__ int64_t shfl_i64(int64_t v, int src) {
     const int lo = __shfl(static_cast<int>(static_cast<uint64_t>(v) & 0xffffffffu), src, kWave);
@@ -68,133 +77,38 @@ __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
     return v;
 }
 
+// number of lanes strictly below this one whose bit is set in m
+__device__ __forceinline__ uint32_t popc_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(m >> 32),
+                                     __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(m), 0u));
+}
+
 __device__ __forceinline__ uint8_t up(uint8_t c) { return (c >= 'a' && c <= 'z') ? c - 32 : c; }
 
-// 64-ary search: first idx in [L, H) with pos[idx] >= x, H if none.  Each
-// step is one dependent round of 64 independent loads (the
-// lower_bound term 4 B x ceil(log2 N) per query).
-__device__ uint32_t wave_lower_bound(const uint32_t *__restrict__ pos, uint32_t L, uint32_t H, int64_t x) {
+// ---------------------------------------------------------------- bounds
+// First record of the segment with POS >= x.  The bucket b holding x brackets
+// the answer in [bucket[b], bucket[b+1]]; one 64-wide read (rarely more)
+// finds it.
+__device__ uint32_t lower_bound_bucketed(const DStore &st, const QDev &Q, int64_t x) {
+    if (x <= static_cast<int64_t>(Q.bucket_base)) return Q.seg_lo;
+    const uint64_t b = static_cast<uint64_t>(x - Q.bucket_base) >> Q.bucket_shift;
+    if (b >= Q.n_buckets) return Q.seg_hi;
+    uint32_t L = st.bucket[Q.bucket_off + b];
+    const uint32_t H = st.bucket[Q.bucket_off + b + 1];
     const int lane = lane_id();
-    while (H - L > kWave) {
-        const uint32_t step = (H - L + kWave - 1) / kWave;
-        const uint32_t s = L + static_cast<uint32_t>(lane) * step;
-        const bool ge = (s < H) ? (static_cast<int64_t>(pos[s]) >= x) : true;
+    for (;;) {
+        const uint32_t i = L + static_cast<uint32_t>(lane);
+        const bool ge = (i < H) ? (static_cast<int64_t>(st.pos[i]) >= x) : true;
         const uint64_t m = __ballot(ge);
-        const int f = m ? __ffsll(static_cast<unsigned long long>(m)) - 1 : kWave;
-        if (f == 0) return L;
-        const uint32_t prev = L + static_cast<uint32_t>(f - 1) * step;
-        uint32_t nh = H;
-        if (f < kWave) {
-            const uint32_t sf = L + static_cast<uint32_t>(f) * step;
-            nh = sf < H ? sf : H;
+        if (m) {
+            const uint32_t r = L + static_cast<uint32_t>(ffs64(m));
+            return r < H ? r : H;
         }
-        L = prev + 1;
-        H = nh;
-    }
-    const uint32_t i = L + static_cast<uint32_t>(lane);
-    const bool ge = (i < H) ? (static_cast<int64_t>(pos[i]) >= x) : true;
-    const uint64_t m = __ballot(ge);
-    if (!m) return H;
-    const uint32_t r = L + static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(m)) - 1);
-    return r < H ? r : H;
-}
-
-__global__ __launch_bounds__(kBlock) void bounds_kernel(DStore st, const QDev *__restrict__ qs, uint32_t nq,
-                                                        uint32_t *__restrict__ lohi, uint32_t *__restrict__ caps) {
-    const uint32_t q = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    if (q >= nq) return;
-    const QDev &Q = qs[q];
-    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
-    if (!(Q.flags & F_EMPTY) && Q.first_bp <= Q.last_bp) {
-        lo = wave_lower_bound(st.pos, Q.seg_lo, Q.seg_hi, Q.first_bp);
-        hi = wave_lower_bound(st.pos, lo, Q.seg_hi, Q.last_bp + 1);
-    }
-    if (lane_id() == 0) {
-        lohi[2 * q] = lo;
-        lohi[2 * q + 1] = hi;
-        caps[q] = st.alt_lo[hi] - st.alt_lo[lo];
+        L += kWave;  // every POS in this window < x (bucket longer than 64)
     }
 }
 
-// ---------------------------------------------------------------- prefix sum
-constexpr uint32_t kScanItems = 8;
-constexpr uint32_t kScanTile = kBlock * kScanItems;
-
-__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t *lds, uint64_t *total) {
-    // wave scan then scan of wave totals
-    const int lane = lane_id();
-    const int wave = threadIdx.x >> 6;
-    uint64_t x = v;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint64_t t = static_cast<uint64_t>(shfl_up_i64(static_cast<int64_t>(x), d));
-        if (lane >= d) x += t;
-    }
-    if (lane == kWave - 1) lds[wave] = x;
-    __syncthreads();
-    uint64_t off = 0, tot = 0;
-    for (int w = 0; w < kWavesPerBlock; ++w) {
-        if (w < wave) off += lds[w];
-        tot += lds[w];
-    }
-    __syncthreads();
-    *total = tot;
-    return off + x - v;
-}
-
-__global__ __launch_bounds__(kBlock) void scan_reduce_kernel(const uint32_t *__restrict__ in, uint32_t n,
-                                                             uint64_t *__restrict__ block_sums) {
-    __shared__ uint64_t lds[kWavesPerBlock];
-    const uint32_t base = blockIdx.x * kScanTile;
-    uint64_t s = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kScanItems; ++k) {
-        const uint32_t i = base + k * kBlock + threadIdx.x;
-        if (i < n) s += in[i];
-    }
-    uint64_t tot;
-    block_excl_scan_u64(s, lds, &tot);
-    if (threadIdx.x == 0) block_sums[blockIdx.x] = tot;
-}
-
-__global__ __launch_bounds__(kBlock) void scan_blocks_kernel(uint64_t *__restrict__ block_sums, uint32_t nb) {
-    __shared__ uint64_t lds[kWavesPerBlock];
-    uint64_t carry = 0;
-    for (uint32_t base = 0; base < nb; base += kBlock) {
-        const uint32_t i = base + threadIdx.x;
-        const uint64_t v = i < nb ? block_sums[i] : 0;
-        uint64_t tot;
-        const uint64_t ex = block_excl_scan_u64(v, lds, &tot);
-        if (i < nb) block_sums[i] = carry + ex;
-        carry += tot;
-    }
-    if (threadIdx.x == 0) block_sums[nb] = carry;
-}
-
-__global__ __launch_bounds__(kBlock) void scan_apply_kernel(const uint32_t *__restrict__ in, uint32_t n,
-                                                            const uint64_t *__restrict__ block_off,
-                                                            uint32_t nb, uint64_t *__restrict__ out) {
-    __shared__ uint64_t lds[kWavesPerBlock];
-    // each thread owns kScanItems consecutive elements of the tile
-    const uint32_t base = blockIdx.x * kScanTile + threadIdx.x * kScanItems;
-    uint32_t v[kScanItems];
-    uint64_t s = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kScanItems; ++k) {
-        v[k] = (base + k < n) ? in[base + k] : 0u;
-        s += v[k];
-    }
-    uint64_t tot;
-    uint64_t run = block_off[blockIdx.x] + block_excl_scan_u64(s, lds, &tot);
-#pragma unroll
-    for (uint32_t k = 0; k < kScanItems; ++k) {
-        if (base + k < n) out[base + k] = run;
-        run += v[k];
-    }
-    if (blockIdx.x == nb - 1 && threadIdx.x == 0) out[n] = block_off[nb];
-}
-
-// ---------------------------------------------------------------- scan kernel
+// ---------------------------------------------------------------- predicates
 __device__ __forceinline__ bool blob_eq_upper(const uint8_t *__restrict__ blob, uint64_t off, uint32_t len,
                                               const uint8_t *__restrict__ q, uint32_t qlen) {
     if (len != qlen) return false;
@@ -214,7 +128,7 @@ __device__ bool ref_wild_match(const DStore &st, uint32_t r, uint32_t ref_len, c
                                uint32_t plen) {
     if (ref_len != plen) return false;
     const uint64_t key = st.ref_key[r];
-    if (!(st.meta[r] & M_REF_HASHED)) {
+    if (!(key >> 63)) {
         for (uint32_t i = 0; i < plen; ++i)
             if (!wild_char(static_cast<uint8_t>(key >> (8 * i)), pat[i])) return false;
         return true;
@@ -225,10 +139,27 @@ __device__ bool ref_wild_match(const DStore &st, uint32_t r, uint32_t ref_len, c
     return true;
 }
 
-// genotype fallback over the selected samples (samples variant, record
-// without AC / AN): search_variants_in_samples.py:211-222 and :239-245 with
-// bcftools --samples restricting the GT text.  `value` = allele number to
-// count (0 = count every call).  Rare path: one lane walks the subset.
+// :100-166 variantType predicate of one non-None-alt-less query
+__device__ __forceinline__ bool vtype_hit(const QDev &Q, const DStore &st, uint32_t cls, int64_t len,
+                                          int64_t ref_len) {
+    if (cls & C_SYMBOLIC) {
+        const uint32_t sym = cls >> C_SYM_SHIFT;
+        return (st.sym_lut[Q.lut_off + (sym >> 5)] >> (sym & 31)) & 1u;
+    }
+    const uint32_t rep = (cls >> C_REP_SHIFT) & 63u;
+    switch (Q.vt_kind) {
+        case VT_DEL: return len < ref_len;
+        case VT_INS: return len > ref_len;
+        case VT_DUP: return rep != C_REP_NONE && rep >= 2;
+        case VT_DUPT: return rep == 2;
+        case VT_CNV: return (cls & C_DOT) || rep != C_REP_NONE;
+        default: return false;
+    }
+}
+
+// genotype fallback over the selected samples (samples variant, record without
+// AC / AN): search_variants_in_samples.py:211-222 / :239-245 with bcftools
+// --samples restricting the GT text.  value = allele number (0 = every call).
 __device__ int64_t fallback_count(const DStore &st, uint32_t r, const uint64_t *__restrict__ subset,
                                   uint32_t n_samples, uint32_t value) {
     const int64_t base = st.fb_off[r];
@@ -249,46 +180,56 @@ __device__ int64_t fallback_count(const DStore &st, uint32_t r, const uint64_t *
 
 template <int NACC>
 __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__restrict__ qs, uint32_t nq,
-                                                      const uint32_t *__restrict__ lohi,
-                                                      const uint64_t *__restrict__ hit_off,
                                                       const uint8_t *__restrict__ qbytes,
                                                       const uint64_t *__restrict__ subsets,
-                                                      QRes *__restrict__ res, uint32_t *__restrict__ nhits,
-                                                      uint32_t *__restrict__ hit_rec,
-                                                      uint32_t *__restrict__ hit_alt,
+                                                      QRes *__restrict__ res, uint64_t *__restrict__ hits,
                                                       uint64_t *__restrict__ samples_out) {
     const uint32_t q = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     if (q >= nq) return;
     const int lane = lane_id();
     const QDev &Q = qs[q];
-    const uint32_t lo = lohi[2 * q], hi = lohi[2 * q + 1];
-    const uint64_t out = hit_off[q];
     const uint32_t flags = Q.flags;
     const bool details = flags & F_DETAILS;
     const bool samples_variant = flags & F_SAMPLES_VARIANT;
     const bool collect = (flags & F_COLLECT) && details;
     const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
+    const bool nonneg = flags & F_NONNEG;
     const uint8_t *qref = qbytes + Q.qbytes_off;
     const uint8_t *qalt = qref + Q.ref_len;
     const uint64_t *subset = (Q.subset_off != ~0ull) ? subsets + Q.subset_off : nullptr;
 
-    int64_t carry = 0, an_sum = 0;
+    // ---- 1. bounds of the slice: a <= POS <= b (:84-85)
+    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
+    if (!(flags & F_EMPTY) && Q.first_bp <= Q.last_bp) {
+        lo = lower_bound_bucketed(st, Q, Q.first_bp);
+        hi = lower_bound_bucketed(st, Q, Q.last_bp + 1);
+        if (hi < lo) hi = lo;
+    }
+
+    int64_t carry = 0;      // running call_count (general path)
+    bool carry_nz = false;  // running call_count != 0 (non-negative path)
+    int64_t cc_acc = 0, an_acc = 0;  // per-lane partial sums, reduced once at the end
     uint32_t n_out = 0;
     bool exists = false;
     int err_out = 0;
     uint64_t acc[NACC];
 #pragma unroll
     for (int j = 0; j < NACC; ++j) acc[j] = 0;
+    uint64_t *out = hits + Q.hit_off;
 
+    RecHot cur = {0, 0, 0, 0};
+    if (lo + static_cast<uint32_t>(lane) < hi) cur = st.rec[lo + lane];
     for (uint32_t base = lo; base < hi; base += kWave) {
         const uint32_t r = base + static_cast<uint32_t>(lane);
+        RecHot nxt = {0, 0, 0, 0};
+        if (r + kWave < hi) nxt = st.rec[r + kWave];  // prefetch the next chunk
         int err = 0;
         uint64_t hm = 0, em = 0;
         int64_t c = 0, anv = 0;
-        uint32_t a0 = 0;
         if (r < hi) {
-            const uint32_t e = st.end[r];
-            bool pass = static_cast<int64_t>(e) >= Q.end_min && static_cast<int64_t>(e) <= Q.end_max; // :90
+            const uint32_t e = cur.end;
+            const uint32_t h = cur.hot;
+            bool pass = static_cast<int64_t>(e) >= Q.end_min && static_cast<int64_t>(e) <= Q.end_max;  // :90
             if (pass) {
                 switch (Q.ref_mode) {  // :94 / svs:88-91
                     case REF_ANY:
@@ -296,10 +237,8 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
                     case REF_EXACT: {
                         const uint64_t k = st.ref_key[r];
                         pass = k == Q.ref_key;
-                        if (pass && (k >> 63)) {
-                            const uint32_t rl = e - st.pos[r] + 1;
-                            pass = blob_eq_upper(st.blob, st.ref_off[r], rl, qref, Q.ref_len);
-                        }
+                        if (pass && (k >> 63))
+                            pass = blob_eq_upper(st.blob, st.ref_off[r], e - st.pos[r] + 1, qref, Q.ref_len);
                         break;
                     }
                     case REF_WILD:
@@ -318,122 +257,148 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
                 err = SB_QERR_UNBOUND_LOCAL;
                 pass = false;
             }
+            uint32_t x0 = 0, nx = 0;
             if (pass) {
-                a0 = st.alt_lo[r];
-                const uint32_t na = st.alt_lo[r + 1] - a0;
                 const int64_t ref_len = (Q.alt_mode == ALT_VTYPE) ? static_cast<int64_t>(e) - st.pos[r] + 1 : 0;
-                for (uint32_t k = 0; k < na && k < 64; ++k) {  // :100-183 hit_indexes
-                    const uint32_t a = a0 + k;
-                    const uint32_t cls = st.alt_cls[a];
+                {  // ALT 0: class bits live in RecHot::hot
                     bool ok;
                     int64_t len = 1;
                     if (Q.alt_mode == ALT_N) {
-                        ok = cls & A_SINGLE_BASE;
+                        ok = h & C_SINGLE_BASE;
                     } else if (Q.alt_mode == ALT_EXACT) {
-                        ok = st.alt_key[a] == Q.alt_key;
-                        len = st.alt_len[a];
-                        if (ok && (cls & A_HASHED))
-                            ok = blob_eq_upper(st.blob, st.alt_off[a], static_cast<uint32_t>(len), qalt, Q.alt_len);
+                        const uint64_t k = st.a0_key[r];
+                        ok = k == Q.alt_key;
+                        len = Q.alt_len;
+                        if (ok && (k >> 63)) ok = blob_eq_upper(st.blob, st.a0_off[r], st.a0_len[r], qalt, Q.alt_len);
                     } else {
-                        len = st.alt_len[a];
-                        if (cls & A_SYMBOLIC) {
-                            const uint32_t sym = cls >> A_SYM_SHIFT;
-                            ok = (st.sym_lut[Q.lut_off + (sym >> 5)] >> (sym & 31)) & 1u;
-                        } else {
-                            const uint32_t rep = (cls >> A_REP_SHIFT) & 63u;
-                            switch (Q.vt_kind) {
-                                case VT_DEL: ok = len < ref_len; break;
-                                case VT_INS: ok = len > ref_len; break;
-                                case VT_DUP: ok = rep != A_REP_NONE && rep >= 2; break;
-                                case VT_DUPT: ok = rep == 2; break;
-                                case VT_CNV: ok = (cls & A_DOT) || rep != A_REP_NONE; break;
-                                default: ok = false; break;
-                            }
-                        }
+                        len = st.a0_len[r];
+                        ok = vtype_hit(Q, st, h, len, ref_len);
                     }
-                    if (ok && len >= Q.vmin && len <= Q.vmax) hm |= 1ull << k;
+                    if (ok && len >= Q.vmin && len <= Q.vmax) hm = 1;
                 }
-                if (hm) {
-                    const uint32_t m = st.meta[r];
-                    const bool sub = samples_variant && (m & M_HAS_FB);
-                    if (m & M_AN_BAD) {
-                        err = SB_QERR_VALUE;  // :199
-                    } else if (m & M_HAS_AC) {  // :205-214
-                        if (m & M_AC_BAD) {
-                            err = SB_QERR_VALUE;  // :206
+                if (h & H_MULTI) {  // ALTs 1..n-1 of multiallelic records
+                    x0 = st.x_lo[r];
+                    nx = st.x_lo[r + 1] - x0;
+                    for (uint32_t k = 0; k < nx && k < 63; ++k) {
+                        const uint32_t x = x0 + k;
+                        const uint32_t cls = st.x_cls[x];
+                        bool ok;
+                        int64_t len = 1;
+                        if (Q.alt_mode == ALT_N) {
+                            ok = cls & C_SINGLE_BASE;
+                        } else if (Q.alt_mode == ALT_EXACT) {
+                            const uint64_t key = st.x_key[x];
+                            ok = key == Q.alt_key;
+                            len = Q.alt_len;
+                            if (ok && (key >> 63)) ok = blob_eq_upper(st.blob, st.x_off[x], st.x_len[x], qalt, Q.alt_len);
                         } else {
-                            for (uint64_t b = hm; b; b &= b - 1) {
-                                const int k = __ffsll(static_cast<unsigned long long>(b)) - 1;
-                                if (st.alt_cls[a0 + k] & A_AC_MISSING) err = SB_QERR_INDEX;  // :207
-                                const int64_t v = st.ac[a0 + k];
-                                c += v;
-                                if (v != 0) em |= 1ull << k;
-                            }
+                            len = st.x_len[x];
+                            ok = vtype_hit(Q, st, cls, len, ref_len);
                         }
-                    } else {  // :215-226 genotype fallback (1-based alts[] label)
-                        for (uint64_t b = hm; b; b &= b - 1) {
-                            const int k = __ffsll(static_cast<unsigned long long>(b)) - 1;
-                            const int64_t v = sub ? fallback_count(st, r, subset, Q.n_samples, k + 1) : st.ac[a0 + k];
-                            c += v;
-                            if (v > 0) {
-                                if (static_cast<uint32_t>(k + 1) >= na) err = SB_QERR_INDEX;  // :223
-                                else em |= 1ull << (k + 1);
-                            }
-                        }
-                    }
-                    // :244-250
-                    anv = (m & M_HAS_AN) ? st.an[r] : (sub ? fallback_count(st, r, subset, Q.n_samples, 0) : st.an[r]);
-                    if (err) {
-                        hm = 0;
-                        em = 0;
-                        c = 0;
+                        if (ok && len >= Q.vmin && len <= Q.vmax) hm |= 2ull << k;
                     }
                 }
             }
+            if (hm) {
+                const uint32_t na = 1 + nx;
+                const bool sub = samples_variant && (h & H_HAS_FB);
+                if (h & H_AN_BAD) {
+                    err = SB_QERR_VALUE;  // :199
+                } else if (h & H_HAS_AC) {  // :205-214
+                    if (h & H_AC_BAD) {
+                        err = SB_QERR_VALUE;  // :206
+                    } else {
+                        for (uint64_t b = hm; b; b &= b - 1) {
+                            const int k = ffs64(b);
+                            const uint32_t cls = k ? st.x_cls[x0 + k - 1] : h;
+                            if (cls & C_AC_MISSING) err = SB_QERR_INDEX;  // :207
+                            const int64_t v = k ? st.x_ac[x0 + k - 1] : cur.ac0;
+                            c += v;
+                            if (v != 0) em |= 1ull << k;
+                        }
+                    }
+                } else {  // :215-226 genotype fallback, labelled alts[i] with 1-based i
+                    for (uint64_t b = hm; b; b &= b - 1) {
+                        const int k = ffs64(b);
+                        const int64_t v = sub ? fallback_count(st, r, subset, Q.n_samples, k + 1)
+                                              : (k ? st.x_ac[x0 + k - 1] : cur.ac0);
+                        c += v;
+                        if (v > 0) {
+                            if (static_cast<uint32_t>(k + 1) >= na) err = SB_QERR_INDEX;  // :223
+                            else em |= 1ull << (k + 1);
+                        }
+                    }
+                }
+                anv = (h & H_HAS_AN) ? cur.an : (sub ? fallback_count(st, r, subset, Q.n_samples, 0) : cur.an);
+                if (err) {
+                    hm = 0;
+                    em = 0;
+                    c = 0;
+                }
+            }
         }
-        // ---- order-dependent loop state (:229-254) as wave operations
+        // ---- 3. order-dependent loop state (:229-254)
         const bool hit = hm != 0;
         const uint64_t errm = __ballot(err != 0);
-        const int64_t cum = carry + wave_incl_scan_i64(hit ? c : 0);
-        const bool trig = hit && cum != 0;  // `if call_count:` on the running total
-        const uint64_t trigm = __ballot(trig);
+        const uint64_t hitm = __ballot(hit);
+        int64_t cum = 0;
+        uint64_t trigm;  // hit lanes where the running call_count is non-zero
+        if (nonneg) {
+            const uint64_t pm = __ballot(hit && c > 0);
+            trigm = carry_nz ? hitm : (pm ? (hitm & ~((1ull << ffs64(pm)) - 1ull)) : 0ull);
+        } else {
+            cum = carry + wave_incl_scan_i64(hit ? c : 0);
+            trigm = __ballot(hit && cum != 0);
+        }
         const uint64_t stopm = errm | (stop_on_exists ? trigm : 0ull);
-        const int s = stopm ? __ffsll(static_cast<unsigned long long>(stopm)) - 1 : kWave;
+        const int s = stopm ? ffs64(stopm) : kWave;
         if (s < kWave && ((errm >> s) & 1ull)) {
             err_out = __shfl(err, s, kWave);
             break;
         }
         const uint64_t upto = (s >= kWave - 1) ? ~0ull : ((2ull << s) - 1ull);
         const bool in = (upto >> lane) & 1ull;
-        // compacted emission of variant strings (:209-213 / :222-225)
+        // ---- 4. compacted emission of variant strings (:209-213 / :222-225)
         const uint32_t cnt = (hit && in) ? static_cast<uint32_t>(__popcll(em)) : 0u;
-        const uint32_t incl = wave_incl_scan_u32(cnt);
-        if (cnt) {
-            uint64_t dst = out + n_out + (incl - cnt);
-            for (uint64_t b = em; b; b &= b - 1) {
-                hit_rec[dst] = r;
-                hit_alt[dst] = static_cast<uint32_t>(__ffsll(static_cast<unsigned long long>(b)) - 1);
-                ++dst;
-            }
+        const uint64_t multi = __ballot(cnt > 1);
+        uint32_t pos0, total;
+        if (!multi) {
+            const uint64_t one = __ballot(cnt == 1);
+            pos0 = popc_below(one);
+            total = static_cast<uint32_t>(__popcll(one));
+        } else {
+            const uint32_t incl = wave_incl_scan_u32(cnt);
+            pos0 = incl - cnt;
+            total = __shfl(incl, kWave - 1, kWave);
         }
-        n_out += __shfl(incl, kWave - 1, kWave);
-        // all_alleles_count: lanes before the stop, plus the stop lane when the
-        // stop is the boolean break (AN added before :253) rather than :231
-        const bool an_in = hit && (lane < s || (lane == s && details));
-        an_sum += wave_sum_i64(an_in ? anv : 0);
+        if (cnt) {
+            uint64_t *dst = out + n_out + pos0;
+            for (uint64_t b = em; b; b &= b - 1)
+                *dst++ = static_cast<uint64_t>(r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
+        }
+        n_out += total;
+        // call_count and all_alleles_count: lanes up to the stop; the stop lane's
+        // AN only for the boolean break (after :244), not for :231
+        if (hit && in) cc_acc += c;
+        if (hit && (lane < s || (lane == s && details))) an_acc += anv;
         exists = exists || ((trigm & upto) != 0ull);
-        carry = shfl_i64(cum, s < kWave ? s : kWave - 1);
+        if (nonneg)
+            carry_nz = exists;
+        else
+            carry = shfl_i64(cum, s < kWave ? s : kWave - 1);
         // sample path (:233-236): OR the carrier planes of every hit allele
         if (collect) {
             uint64_t cm = trigm & upto;
             while (cm) {
-                const int L = __ffsll(static_cast<unsigned long long>(cm)) - 1;
+                const int L = ffs64(cm);
                 cm &= cm - 1;
                 const uint64_t hml = static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(hm), L));
-                const uint32_t a0l = static_cast<uint32_t>(__shfl(static_cast<int>(a0), L, kWave));
+                const uint32_t rl = static_cast<uint32_t>(__shfl(static_cast<int>(r), L, kWave));
+                const uint32_t xl = (hml >> 1) ? st.x_lo[rl] : 0u;
                 for (uint64_t b = hml; b; b &= b - 1) {
-                    const int k = __ffsll(static_cast<unsigned long long>(b)) - 1;
-                    const uint64_t row = Q.plane_base + static_cast<uint64_t>(a0l + k - Q.alt_base) * Q.words;
+                    const int k = ffs64(b);
+                    const uint64_t row = k ? Q.planex_base + static_cast<uint64_t>(xl + k - 1 - Q.x_base) * Q.words
+                                           : Q.plane0_base + static_cast<uint64_t>(rl - Q.rec_base) * Q.words;
 #pragma unroll
                     for (int j = 0; j < NACC; ++j) {
                         const uint32_t w = static_cast<uint32_t>(lane) + 64u * j;
@@ -442,19 +407,21 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
                 }
             }
         }
+        cur = nxt;
         if (s < kWave) break;
     }
 
+    const int64_t call_count = nonneg ? wave_sum_i64(cc_acc) : carry;
+    const int64_t an_sum = wave_sum_i64(an_acc);
     if (lane == 0) {
         QRes o;
         o.error = err_out;
         o.exists = exists ? 1 : 0;
-        o.call_count = carry;
+        o.call_count = call_count;
         o.all_alleles_count = an_sum;
         o.n_hits = err_out ? 0u : n_out;
         o.n_scanned = hi - lo;
         res[q] = o;
-        nhits[q] = o.n_hits;
     }
     if (collect && Q.samples_out_off != ~0ull) {
 #pragma unroll
@@ -469,67 +436,40 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
     }
 }
 
-__global__ __launch_bounds__(kBlock) void compact_kernel(const uint64_t *__restrict__ hit_off,
+// Gather each query's hits from its planned region into a dense array
+// (result shipping at fetch time; not part of the timed query step).
+__global__ __launch_bounds__(kBlock) void compact_kernel(const QDev *__restrict__ qs,
                                                          const uint64_t *__restrict__ dense_off,
-                                                         const uint32_t *__restrict__ nhits, uint32_t nq,
-                                                         const uint32_t *__restrict__ hit_rec,
-                                                         const uint32_t *__restrict__ hit_alt,
-                                                         uint32_t *__restrict__ out_rec,
-                                                         uint32_t *__restrict__ out_alt) {
+                                                         const QRes *__restrict__ res, uint32_t nq,
+                                                         const uint64_t *__restrict__ hits,
+                                                         uint64_t *__restrict__ out) {
     const uint32_t q = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     if (q >= nq) return;
-    const uint64_t src = hit_off[q], dst = dense_off[q];
-    const uint32_t n = nhits[q];
-    for (uint32_t i = static_cast<uint32_t>(lane_id()); i < n; i += kWave) {
-        out_rec[dst + i] = hit_rec[src + i];
-        out_alt[dst + i] = hit_alt[src + i];
-    }
+    const uint64_t src = qs[q].hit_off, dst = dense_off[q];
+    const uint32_t n = res[q].n_hits;
+    for (uint32_t i = static_cast<uint32_t>(lane_id()); i < n; i += kWave) out[dst + i] = hits[src + i];
 }
 
 inline uint32_t blocks_for(uint32_t nq) { return (nq + kWavesPerBlock - 1) / kWavesPerBlock; }
 
 }  // namespace
 
-void launch_bounds(const DStore &st, const QDev *q, uint32_t nq, uint32_t *lohi, uint32_t *caps, hipStream_t s) {
+void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,
+                    uint64_t *out, hipStream_t s) {
     if (!nq) return;
-    hipLaunchKernelGGL(bounds_kernel, dim3(blocks_for(nq)), dim3(kBlock), 0, s, st, q, nq, lohi, caps);
+    hipLaunchKernelGGL(compact_kernel, dim3(blocks_for(nq)), dim3(kBlock), 0, s, q, dense_off, res, nq, hits, out);
 }
 
-size_t scan_tmp_words(uint32_t n) { return (n + kScanTile - 1) / kScanTile + 1; }
-
-void launch_exclusive_scan(const uint32_t *in, uint32_t n, uint64_t *out, uint64_t *tmp, hipStream_t s) {
-    const uint32_t nb = n ? (n + kScanTile - 1) / kScanTile : 1;
-    if (!n) {
-        (void)hipMemsetAsync(out, 0, sizeof(uint64_t), s);
-        return;
-    }
-    hipLaunchKernelGGL(scan_reduce_kernel, dim3(nb), dim3(kBlock), 0, s, in, n, tmp);
-    hipLaunchKernelGGL(scan_blocks_kernel, dim3(1), dim3(kBlock), 0, s, tmp, nb);
-    hipLaunchKernelGGL(scan_apply_kernel, dim3(nb), dim3(kBlock), 0, s, in, n, tmp, nb, out);
-}
-
-void launch_scan(const DStore &st, const QDev *q, uint32_t nq, const uint32_t *lohi, const uint64_t *hit_off,
-                 const uint8_t *qbytes, const uint64_t *subsets, uint32_t max_words, QRes *res, uint32_t *nhits,
-                 uint32_t *hit_rec, uint32_t *hit_alt, uint64_t *samples_out, hipStream_t s) {
+void launch_scan(const DStore &st, const QDev *q, uint32_t nq, const uint8_t *qbytes, const uint64_t *subsets,
+                 uint32_t max_words, QRes *res, uint64_t *hits, uint64_t *samples_out, hipStream_t s) {
     if (!nq) return;
     const dim3 g(blocks_for(nq)), b(kBlock);
     if (max_words <= 64)
-        hipLaunchKernelGGL(scan_kernel<1>, g, b, 0, s, st, q, nq, lohi, hit_off, qbytes, subsets, res, nhits, hit_rec,
-                           hit_alt, samples_out);
+        hipLaunchKernelGGL(scan_kernel<1>, g, b, 0, s, st, q, nq, qbytes, subsets, res, hits, samples_out);
     else if (max_words <= 256)
-        hipLaunchKernelGGL(scan_kernel<4>, g, b, 0, s, st, q, nq, lohi, hit_off, qbytes, subsets, res, nhits, hit_rec,
-                           hit_alt, samples_out);
+        hipLaunchKernelGGL(scan_kernel<4>, g, b, 0, s, st, q, nq, qbytes, subsets, res, hits, samples_out);
     else
-        hipLaunchKernelGGL(scan_kernel<16>, g, b, 0, s, st, q, nq, lohi, hit_off, qbytes, subsets, res, nhits,
-                           hit_rec, hit_alt, samples_out);
-}
-
-void launch_compact(const uint64_t *hit_off, const uint64_t *dense_off, const uint32_t *nhits, uint32_t nq,
-                    const uint32_t *hit_rec, const uint32_t *hit_alt, uint32_t *out_rec, uint32_t *out_alt,
-                    hipStream_t s) {
-    if (!nq) return;
-    hipLaunchKernelGGL(compact_kernel, dim3(blocks_for(nq)), dim3(kBlock), 0, s, hit_off, dense_off, nhits, nq,
-                       hit_rec, hit_alt, out_rec, out_alt);
+        hipLaunchKernelGGL(scan_kernel<16>, g, b, 0, s, st, q, nq, qbytes, subsets, res, hits, samples_out);
 }
 
 }  // namespace sb

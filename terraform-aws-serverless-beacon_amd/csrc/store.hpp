@@ -24,17 +24,29 @@ struct Segment {  // one (vcf, contig), position-sorted, contiguous records
 
 // Columns of one VCF (vcf-local indices while building).
 struct VcfCols {
-    std::vector<uint32_t> pos, end, meta;
-    std::vector<int32_t> an;
-    std::vector<uint64_t> ref_key, ref_off;
+    // record-indexed
+    std::vector<RecHot> rec;
+    std::vector<uint32_t> pos, a0_len, x_lo{0};
+    std::vector<uint64_t> ref_key, a0_key, ref_off, a0_off;
     std::vector<int64_t> fb_off;
-    std::vector<uint32_t> alt_lo{0};
-    std::vector<uint64_t> alt_key, alt_off;
-    std::vector<uint32_t> alt_len, alt_cls;
-    std::vector<int32_t> ac;
+    std::vector<uint16_t> vt;  // VT dictionary id (host-side formatting only)
+    // extra-ALT rows (ALT index >= 1)
+    std::vector<uint32_t> x_cls, x_len;
+    std::vector<int32_t> x_ac;
+    std::vector<uint64_t> x_key, x_off;
+    // bulk
     std::vector<uint8_t> blob;
-    std::vector<uint64_t> planes;  // [alt row][words]
-    std::vector<uint32_t> fb;      // [fallback row][n_samples]
+    std::vector<uint64_t> planes0;  // [record][words]
+    std::vector<uint64_t> planesx;  // [extra row][words]
+    std::vector<uint32_t> fb;       // [fallback row][n_samples]
+    bool any_negative = false;      // some INFO AC entry < 0
+};
+
+struct BucketIndex {  // coarse POS index of one segment
+    uint64_t off = 0;    // into the store's bucket array
+    uint32_t base = 0;   // POS of the segment's first record
+    uint32_t shift = 0;  // bucket width = 1 << shift bp
+    uint32_t n = 0;      // buckets; bucket[off + n] = segment end
 };
 
 struct VcfData {
@@ -44,11 +56,14 @@ struct VcfData {
     bool header_seen = false;
     std::vector<Segment> segments;
     std::unordered_map<std::string, uint32_t> seg_index;
+    std::vector<BucketIndex> buckets;  // parallel to segments (set by finish)
     VcfCols c;
     std::string carry;  // partial line kept between add_text calls
     // global placement (set by finish)
-    uint32_t rec_base = 0, alt_base = 0;
-    uint64_t plane_base = 0;
+    uint32_t rec_base = 0, x_base = 0;
+    uint64_t plane0_base = 0, planex_base = 0;
+    bool nonneg = true;
+    bool has_planes = false;
 };
 
 struct Dict {
@@ -82,15 +97,15 @@ struct sb_store {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;  // serialises batches on this device
-    std::vector<sb::VcfData> vcfs;  // host columns kept for result formatting
+    std::vector<sb::VcfData> vcfs;  // metadata (columns are moved to the globals below)
     std::unordered_map<std::string, uint32_t> vcf_by_location;
     sb::Dict vt, sym;
-    uint64_t n_records = 0, n_alt = 0;
+    uint64_t n_records = 0, n_extra = 0;
     uint32_t max_words = 0;
-    // host copies needed to format results (global indexing)
-    std::vector<uint32_t> h_pos, h_meta, h_end;
-    std::vector<uint64_t> h_ref_off, h_alt_off;
-    std::vector<uint32_t> h_alt_len, h_alt_lo;
+    // host copies needed to plan outputs and format results (global indexing)
+    std::vector<uint32_t> h_pos, h_end, h_a0_len, h_x_lo, h_x_len, h_bucket;
+    std::vector<uint16_t> h_vt;
+    std::vector<uint64_t> h_ref_off, h_a0_off, h_x_off;
     std::vector<uint8_t> h_blob;
     // device image
     sb::DStore d{};
