@@ -14,8 +14,11 @@ namespace sb {
 // early exits and writes packed hits into its host-planned region at
 // q.hit_off, per-query totals into res and, for the sample path, a carrier
 // bitset per query into samples_out.
-void launch_scan(const DStore &st, const QDev *q, uint32_t nq, const uint8_t *qbytes, const uint64_t *subsets,
-                 uint32_t max_words, QRes *res, uint64_t *hits, uint64_t *samples_out, hipStream_t s);
+// qidx (optional) lists the queries this launch covers (n of them); max_words
+// = 0 compiles out the sample path; nonneg selects the monotone call_count path.
+void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t n, bool nonneg, uint32_t max_words,
+                 const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out,
+                 hipStream_t s);
 
 // Fetch-time gather of every query's hits into one dense array.
 void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,

@@ -86,26 +86,47 @@ __device__ __forceinline__ uint32_t popc_below(uint64_t m) {
 __device__ __forceinline__ uint8_t up(uint8_t c) { return (c >= 'a' && c <= 'z') ? c - 32 : c; }
 
 // ---------------------------------------------------------------- bounds
-// First record of the segment with POS >= x.  The bucket b holding x brackets
-// the answer in [bucket[b], bucket[b+1]]; one 64-wide read (rarely more)
-// finds it.
-__device__ uint32_t lower_bound_bucketed(const DStore &st, const QDev &Q, int64_t x) {
-    if (x <= static_cast<int64_t>(Q.bucket_base)) return Q.seg_lo;
+// [lo, hi) = records of the segment with x1 <= POS < x2.  The bucket holding
+// x brackets lower_bound(x) in [bucket[b], bucket[b+1]]; both searches issue
+// their bucket loads and their 64-wide POS reads together, so the bounds cost
+// two dependent memory rounds (a bucket longer than 64 records loops).
+struct Bracket {
+    uint32_t L, H;
+    bool done;  // answer already known (= L)
+};
+
+__device__ __forceinline__ Bracket bracket(const DStore &st, const QDev &Q, int64_t x) {
+    if (x <= static_cast<int64_t>(Q.bucket_base)) return {Q.seg_lo, Q.seg_lo, true};
     const uint64_t b = static_cast<uint64_t>(x - Q.bucket_base) >> Q.bucket_shift;
-    if (b >= Q.n_buckets) return Q.seg_hi;
-    uint32_t L = st.bucket[Q.bucket_off + b];
-    const uint32_t H = st.bucket[Q.bucket_off + b + 1];
+    if (b >= Q.n_buckets) return {Q.seg_hi, Q.seg_hi, true};
+    return {st.bucket[Q.bucket_off + b], st.bucket[Q.bucket_off + b + 1], false};
+}
+
+__device__ __forceinline__ uint32_t finish_bound(const DStore &st, Bracket k, int64_t x, uint32_t v_first) {
+    // v_first: this lane's POS at k.L + lane (already loaded), UINT32_MAX past H
     const int lane = lane_id();
+    uint32_t L = k.L;
+    uint32_t v = v_first;
     for (;;) {
-        const uint32_t i = L + static_cast<uint32_t>(lane);
-        const bool ge = (i < H) ? (static_cast<int64_t>(st.pos[i]) >= x) : true;
-        const uint64_t m = __ballot(ge);
+        const uint64_t m = __ballot(static_cast<int64_t>(v) >= x || L + static_cast<uint32_t>(lane) >= k.H);
         if (m) {
             const uint32_t r = L + static_cast<uint32_t>(ffs64(m));
-            return r < H ? r : H;
+            return r < k.H ? r : k.H;
         }
-        L += kWave;  // every POS in this window < x (bucket longer than 64)
+        L += kWave;  // all 64 POS < x: the bucket is longer than one wave
+        const uint32_t i = L + static_cast<uint32_t>(lane);
+        v = i < k.H ? st.pos[i] : 0xffffffffu;
     }
+}
+
+__device__ __forceinline__ void slice_bounds(const DStore &st, const QDev &Q, uint32_t *lo, uint32_t *hi) {
+    const Bracket a = bracket(st, Q, Q.first_bp), b = bracket(st, Q, Q.last_bp + 1);
+    const uint32_t ia = a.L + static_cast<uint32_t>(lane_id()), ib = b.L + static_cast<uint32_t>(lane_id());
+    const uint32_t va = (!a.done && ia < a.H) ? st.pos[ia] : 0xffffffffu;
+    const uint32_t vb = (!b.done && ib < b.H) ? st.pos[ib] : 0xffffffffu;
+    *lo = a.done ? a.L : finish_bound(st, a, Q.first_bp, va);
+    *hi = b.done ? b.L : finish_bound(st, b, Q.last_bp + 1, vb);
+    if (*hi < *lo) *hi = *lo;
 }
 
 // ---------------------------------------------------------------- predicates
@@ -178,33 +199,34 @@ __device__ int64_t fallback_count(const DStore &st, uint32_t r, const uint64_t *
     return n_match;
 }
 
-template <int NACC>
-__global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__restrict__ qs, uint32_t nq,
-                                                      const uint8_t *__restrict__ qbytes,
-                                                      const uint64_t *__restrict__ subsets,
-                                                      QRes *__restrict__ res, uint64_t *__restrict__ hits,
-                                                      uint64_t *__restrict__ samples_out) {
-    const uint32_t q = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    if (q >= nq) return;
+// NACC: 64-bit sample-bitset words per lane (0 = no query in this launch
+// collects samples); NONNEG: every AC in the store is >= 0, so the running
+// call_count is monotone and `if call_count:` reduces to ballots.
+// <= 80 SGPRs keeps 8 workgroups per CU resident (MI355X_MICROARCH.md,
+// Residency: 800 / (sgpr + 16)); the surplus spills to VGPR lanes, not scratch.
+template <int NACC, bool NONNEG>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void scan_kernel(
+    DStore st, const QDev *__restrict__ qs, const uint32_t *__restrict__ qidx, uint32_t nq,
+    const uint8_t *__restrict__ qbytes, const uint64_t *__restrict__ subsets, QRes *__restrict__ res,
+    uint64_t *__restrict__ hits, uint64_t *__restrict__ samples_out) {
+    const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    if (w >= nq) return;
+    const uint32_t q = qidx ? uniform(qidx[w]) : w;
     const int lane = lane_id();
     const QDev &Q = qs[q];
     const uint32_t flags = Q.flags;
     const bool details = flags & F_DETAILS;
     const bool samples_variant = flags & F_SAMPLES_VARIANT;
-    const bool collect = (flags & F_COLLECT) && details;
+    const bool collect = NACC > 0 && (flags & F_COLLECT) && details;
     const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
-    const bool nonneg = flags & F_NONNEG;
+    constexpr bool nonneg = NONNEG;
     const uint8_t *qref = qbytes + Q.qbytes_off;
     const uint8_t *qalt = qref + Q.ref_len;
     const uint64_t *subset = (Q.subset_off != ~0ull) ? subsets + Q.subset_off : nullptr;
 
     // ---- 1. bounds of the slice: a <= POS <= b (:84-85)
     uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
-    if (!(flags & F_EMPTY) && Q.first_bp <= Q.last_bp) {
-        lo = lower_bound_bucketed(st, Q, Q.first_bp);
-        hi = lower_bound_bucketed(st, Q, Q.last_bp + 1);
-        if (hi < lo) hi = lo;
-    }
+    if (!(flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
 
     int64_t carry = 0;      // running call_count (general path)
     bool carry_nz = false;  // running call_count != 0 (non-negative path)
@@ -212,17 +234,18 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
     uint32_t n_out = 0;
     bool exists = false;
     int err_out = 0;
-    uint64_t acc[NACC];
+    uint64_t acc[NACC > 0 ? NACC : 1];
 #pragma unroll
-    for (int j = 0; j < NACC; ++j) acc[j] = 0;
+    for (int j = 0; j < (NACC > 0 ? NACC : 1); ++j) acc[j] = 0;
     uint64_t *out = hits + Q.hit_off;
 
-    RecHot cur = {0, 0, 0, 0};
+    RecHot cur = {0, 0, 0, 0}, nxt = {0, 0, 0, 0};
     if (lo + static_cast<uint32_t>(lane) < hi) cur = st.rec[lo + lane];
+    if (lo + kWave + static_cast<uint32_t>(lane) < hi) nxt = st.rec[lo + kWave + lane];
     for (uint32_t base = lo; base < hi; base += kWave) {
         const uint32_t r = base + static_cast<uint32_t>(lane);
-        RecHot nxt = {0, 0, 0, 0};
-        if (r + kWave < hi) nxt = st.rec[r + kWave];  // prefetch the next chunk
+        RecHot nxt2 = {0, 0, 0, 0};
+        if (r + 2 * kWave < hi) nxt2 = st.rec[r + 2 * kWave];  // two chunks in flight
         int err = 0;
         uint64_t hm = 0, em = 0;
         int64_t c = 0, anv = 0;
@@ -343,7 +366,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
         const uint64_t hitm = __ballot(hit);
         int64_t cum = 0;
         uint64_t trigm;  // hit lanes where the running call_count is non-zero
-        if (nonneg) {
+        if constexpr (NONNEG) {
             const uint64_t pm = __ballot(hit && c > 0);
             trigm = carry_nz ? hitm : (pm ? (hitm & ~((1ull << ffs64(pm)) - 1ull)) : 0ull);
         } else {
@@ -382,12 +405,12 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
         if (hit && in) cc_acc += c;
         if (hit && (lane < s || (lane == s && details))) an_acc += anv;
         exists = exists || ((trigm & upto) != 0ull);
-        if (nonneg)
+        if constexpr (NONNEG)
             carry_nz = exists;
         else
             carry = shfl_i64(cum, s < kWave ? s : kWave - 1);
         // sample path (:233-236): OR the carrier planes of every hit allele
-        if (collect) {
+        if constexpr (NACC > 0) if (collect) {
             uint64_t cm = trigm & upto;
             while (cm) {
                 const int L = ffs64(cm);
@@ -408,6 +431,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
             }
         }
         cur = nxt;
+        nxt = nxt2;
         if (s < kWave) break;
     }
 
@@ -423,7 +447,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
         o.n_scanned = hi - lo;
         res[q] = o;
     }
-    if (collect && Q.samples_out_off != ~0ull) {
+    if constexpr (NACC > 0) if (collect && Q.samples_out_off != ~0ull) {
 #pragma unroll
         for (int j = 0; j < NACC; ++j) {
             const uint32_t w = static_cast<uint32_t>(lane) + 64u * j;
@@ -460,16 +484,30 @@ void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, u
     hipLaunchKernelGGL(compact_kernel, dim3(blocks_for(nq)), dim3(kBlock), 0, s, q, dense_off, res, nq, hits, out);
 }
 
-void launch_scan(const DStore &st, const QDev *q, uint32_t nq, const uint8_t *qbytes, const uint64_t *subsets,
-                 uint32_t max_words, QRes *res, uint64_t *hits, uint64_t *samples_out, hipStream_t s) {
-    if (!nq) return;
-    const dim3 g(blocks_for(nq)), b(kBlock);
-    if (max_words <= 64)
-        hipLaunchKernelGGL(scan_kernel<1>, g, b, 0, s, st, q, nq, qbytes, subsets, res, hits, samples_out);
-    else if (max_words <= 256)
-        hipLaunchKernelGGL(scan_kernel<4>, g, b, 0, s, st, q, nq, qbytes, subsets, res, hits, samples_out);
-    else
-        hipLaunchKernelGGL(scan_kernel<16>, g, b, 0, s, st, q, nq, qbytes, subsets, res, hits, samples_out);
+template <bool NONNEG>
+void launch_variant(int nacc, dim3 g, const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t n,
+                    const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out,
+                    hipStream_t s) {
+    const dim3 b(kBlock);
+    switch (nacc) {
+        case 0: hipLaunchKernelGGL((scan_kernel<0, NONNEG>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out); break;
+        case 1: hipLaunchKernelGGL((scan_kernel<1, NONNEG>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out); break;
+        case 4: hipLaunchKernelGGL((scan_kernel<4, NONNEG>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out); break;
+        default: hipLaunchKernelGGL((scan_kernel<16, NONNEG>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out); break;
+    }
 }
+
+void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t n, bool nonneg, uint32_t max_words,
+                 const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out,
+                 hipStream_t s) {
+    if (!n) return;
+    const int nacc = max_words == 0 ? 0 : max_words <= 64 ? 1 : max_words <= 256 ? 4 : 16;
+    const dim3 g(blocks_for(n));
+    if (nonneg)
+        launch_variant<true>(nacc, g, st, q, qidx, n, qbytes, subsets, res, hits, samples_out, s);
+    else
+        launch_variant<false>(nacc, g, st, q, qidx, n, qbytes, subsets, res, hits, samples_out, s);
+}
+
 
 }  // namespace sb
