@@ -145,6 +145,10 @@ struct sb_batch {
     std::vector<uint32_t> vcf;
     uint64_t cap_total = 0, samples_words = 0;
     DevMem q, qbytes, subsets, lut, res, hits, samples_out;
+    // queries split by kernel variant: the sample path compiled in or out
+    DevMem idx_plain, idx_collect;
+    uint32_t n_plain = 0, n_collect = 0;
+    bool all_plain = true, nonneg = true;
     // one event pair per run since the last sync; sync() averages them
     std::vector<std::array<hipEvent_t, 2>> ev;
     size_t runs_pending = 0;
@@ -493,6 +497,14 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     }
     B.samples_words = samples_words;
     B.cap_total = cap_total;
+    std::vector<uint32_t> plain, coll;
+    for (uint32_t i = 0; i < B.nq; ++i) {
+        (B.hq[i].samples_out_off != ~0ull ? coll : plain).push_back(i);
+        if (!(B.hq[i].flags & F_NONNEG)) B.nonneg = false;
+    }
+    B.n_plain = static_cast<uint32_t>(plain.size());
+    B.n_collect = static_cast<uint32_t>(coll.size());
+    B.all_plain = coll.empty();
     if (lut_all.empty()) lut_all.push_back(0);
     // ---- device buffers
     HIP_OK(hipSetDevice(s.device));
@@ -505,6 +517,12 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     if (!qbytes.empty()) HIP_OK(hipMemcpyAsync(B.qbytes.p, qbytes.data(), qbytes.size(), hipMemcpyHostToDevice, st));
     if (!subsets.empty()) HIP_OK(hipMemcpyAsync(B.subsets.p, subsets.data(), subsets.size() * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(B.lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
+    if (!B.all_plain) {
+        B.idx_plain.alloc(plain.size() * 4);
+        B.idx_collect.alloc(coll.size() * 4);
+        if (!plain.empty()) HIP_OK(hipMemcpyAsync(B.idx_plain.p, plain.data(), plain.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(B.idx_collect.p, coll.data(), coll.size() * 4, hipMemcpyHostToDevice, st));
+    }
     B.res.alloc(size_t(nq) * sizeof(QRes));
     B.hits.alloc(cap_total * 8);
     B.samples_out.alloc(samples_words * 8);
@@ -524,8 +542,17 @@ void run(sb_batch &B) {
     }
     const auto &E = B.ev[B.runs_pending++];
     HIP_OK(hipEventRecord(E[0], st));
-    launch_scan(d, B.q.as<QDev>(), B.nq, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(), s.max_words,
-                B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), st);
+    if (B.all_plain) {
+        launch_scan(d, B.q.as<QDev>(), nullptr, B.nq, B.nonneg, 0, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(),
+                    B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), st);
+    } else {
+        launch_scan(d, B.q.as<QDev>(), B.idx_collect.as<uint32_t>(), B.n_collect, B.nonneg, s.max_words,
+                    B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(), B.res.as<QRes>(), B.hits.as<uint64_t>(),
+                    B.samples_out.as<uint64_t>(), st);
+        launch_scan(d, B.q.as<QDev>(), B.idx_plain.as<uint32_t>(), B.n_plain, B.nonneg, 0, B.qbytes.as<uint8_t>(),
+                    B.subsets.as<uint64_t>(), B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(),
+                    st);
+    }
     HIP_OK(hipEventRecord(E[1], st));
     HIP_OK(hipGetLastError());
 }
