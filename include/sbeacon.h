@@ -152,6 +152,34 @@ typedef struct {
 int sb_result_stats(const sb_result_set *r, sb_batch_stats *out);
 void sb_result_free(sb_result_set *r);
 
+/* ---- summariseSlice --------------------------------------------------------
+ * One sb_slice = one summariseSlice SNS message {"location", "virtual_start",
+ * "virtual_end"} (lambda/summariseSlice/source/main.cpp:446-453); the result
+ * is its RegionStats {numVariants, numCalls} (main.cpp:43-49, 195-245),
+ * including the reference's record-skip heuristic (main.cpp:226,234-235).
+ * The VCF must have been ingested from its BGZF file (sb_builder_add_file)
+ * so virtual offsets resolve.  Slices must start on a record and must not cut
+ * one (CSI/TBI chunk boundaries do neither); otherwise error =
+ * SB_QERR_UNSUPPORTED. */
+typedef struct {
+    uint32_t vcf_id;
+    uint32_t _pad;
+    uint64_t virtual_start, virtual_end; /* BGZF virtual offsets (coffset << 16 | uoffset) */
+} sb_slice;
+
+typedef struct {
+    int32_t error;
+    int32_t _pad;
+    uint64_t num_variants;
+    uint64_t num_calls;
+    uint64_t records; /* records the reference reader visits */
+} sb_slice_stats;
+
+/* device_ms (optional): HIP-event time of the summarise kernel */
+int sb_summarise_slices(sb_store *s, const sb_slice *slices, size_t n, sb_slice_stats *out, double *device_ms);
+/* BGZF block count and text-stream length of an ingested VCF */
+int sb_store_vcf_stream(const sb_store *s, uint32_t vcf_id, uint64_t *n_blocks, uint64_t *stream_len);
+
 /* ---- device-resident batch (benchmarks / fused pipelines) ----------------
  * Upload a batch once, then launch the query kernels repeatedly on the
  * store's stream with inputs already resident in HBM. */

@@ -161,3 +161,71 @@ class OracleVcf:
 
     def records_in_region(self, region: str) -> int:
         return lib().orc_records_in_region(self.h, region.encode())
+
+
+# ------------------------------------------------------------ summariseSlice
+def _summ_lib():
+    L = lib()
+    if not hasattr(L, '_summ_ready'):
+        L.orc_bgzf_open.restype = C.c_void_p
+        L.orc_bgzf_open.argtypes = [C.c_char_p]
+        L.orc_bgzf_close.argtypes = [C.c_void_p]
+        L.orc_bgzf_ulen.restype = C.c_int64
+        L.orc_bgzf_ulen.argtypes = [C.c_void_p]
+        L.orc_bgzf_nblocks.restype = C.c_int64
+        L.orc_bgzf_nblocks.argtypes = [C.c_void_p]
+        L.orc_bgzf_voff_to_u.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
+        L.orc_summarise_slice.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64),
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.orc_region_stats.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_uint64)]
+        L._summ_ready = True
+    return L
+
+
+def region_stats(text: bytes):
+    """getRegionStats (summariseSlice/source/main.cpp:195-245) over raw text."""
+    L = _summ_lib()
+    nv, nc, rec = C.c_uint64(), C.c_uint64(), C.c_uint64()
+    rc = L.orc_region_stats(text, len(text), C.byref(nv), C.byref(nc), C.byref(rec))
+    if rc:
+        raise ValueError(f'unsupported record (oracle rc={rc})')
+    return {'numVariants': nv.value, 'numCalls': nc.value, 'records': rec.value}
+
+
+class OracleBgzf:
+    """A BGZF file decompressed in memory; summarise_slice restates one
+    summariseSlice invocation {location, virtual_start, virtual_end}."""
+
+    def __init__(self, path):
+        self.h = _summ_lib().orc_bgzf_open(os.fsencode(path))
+        if not self.h:
+            raise ValueError(f'not a BGZF file: {path}')
+
+    def close(self):
+        if self.h:
+            _summ_lib().orc_bgzf_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def ulen(self):
+        return _summ_lib().orc_bgzf_ulen(self.h)
+
+    def voff_to_u(self, voff):
+        u = C.c_uint64()
+        if _summ_lib().orc_bgzf_voff_to_u(self.h, voff, C.byref(u)):
+            raise ValueError(voff)
+        return u.value
+
+    def summarise_slice(self, vstart, vend):
+        nv, nc, rec = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        rc = _summ_lib().orc_summarise_slice(self.h, vstart, vend, C.byref(nv), C.byref(nc), C.byref(rec))
+        if rc:
+            raise ValueError(f'unsupported slice (oracle rc={rc})')
+        return {'numVariants': nv.value, 'numCalls': nc.value, 'records': rec.value}

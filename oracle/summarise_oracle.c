@@ -1,0 +1,302 @@
+/*
+ * summarise_oracle.c — CPU restatement of the reference summariseSlice counter.
+ *
+ * TEST INFRASTRUCTURE ONLY (checker for the device summarise path).
+ *
+ * Restates lambda/summariseSlice/source/main.cpp:195-245 (getRegionStats),
+ * :52-109 (addCounts), write_data_to_s3.h:150-228 (recordHeader's reader
+ * movement) and vcf_chunk_reader.h:24-373 (VcfChunkReader) over a BGZF file
+ * held in memory.  The reader's block walk is equivalent to a character
+ * stream S = uncompressed[U(vstart), U(vend)): every read stops where the
+ * final block's blockChars = endUncompressed cuts it (vcf_chunk_reader.h:172,
+ * :223-231), keepReading() is "cursor < |S|", and seek() may overshoot.
+ *
+ * The reference C++ cannot be compiled here (AWS SDK C++ and
+ * aws-lambda-runtime are absent), so this restatement is
+ * "parity unpinned": it is checked against hand-derived cases in
+ * tests/test_summarise_oracle.py, not against reference output.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <zlib.h>
+
+typedef struct {
+    uint8_t *u;       /* whole uncompressed stream */
+    int64_t ulen;
+    int64_t nblk;
+    uint64_t *coff;   /* compressed offset of block i */
+    uint64_t *ustart; /* uncompressed offset of block i */
+    uint32_t *isize;
+} bgzf_t;
+
+void orc_bgzf_close(void *h) {
+    bgzf_t *b = (bgzf_t *)h;
+    if (!b) return;
+    free(b->u);
+    free(b->coff);
+    free(b->ustart);
+    free(b->isize);
+    free(b);
+}
+
+/* parse + inflate every BGZF block (gzip header with the BC extra subfield) */
+void *orc_bgzf_open(const char *path) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return NULL;
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    uint8_t *c = (uint8_t *)malloc((size_t)n + 1);
+    if (fread(c, 1, (size_t)n, f) != (size_t)n) {
+        fclose(f);
+        free(c);
+        return NULL;
+    }
+    fclose(f);
+    bgzf_t *b = (bgzf_t *)calloc(1, sizeof(bgzf_t));
+    int64_t cap = 1024;
+    b->coff = (uint64_t *)malloc(8 * (size_t)cap);
+    b->ustart = (uint64_t *)malloc(8 * (size_t)cap);
+    b->isize = (uint32_t *)malloc(4 * (size_t)cap);
+    int64_t p = 0, u = 0;
+    while (p + 18 <= n) {
+        if (c[p] != 0x1f || c[p + 1] != 0x8b || c[p + 2] != 8 || !(c[p + 3] & 4)) goto bad;
+        const uint32_t xlen = c[p + 10] | (c[p + 11] << 8);
+        int64_t bsize = -1;
+        for (int64_t x = p + 12; x + 4 <= p + 12 + xlen;) {
+            const uint32_t slen = c[x + 2] | (c[x + 3] << 8);
+            if (c[x] == 'B' && c[x + 1] == 'C' && slen == 2) bsize = (c[x + 4] | (c[x + 5] << 8)) + 1;
+            x += 4 + slen;
+        }
+        if (bsize < 0 || p + bsize > n) goto bad;
+        if (b->nblk == cap) {
+            cap *= 2;
+            b->coff = (uint64_t *)realloc(b->coff, 8 * (size_t)cap);
+            b->ustart = (uint64_t *)realloc(b->ustart, 8 * (size_t)cap);
+            b->isize = (uint32_t *)realloc(b->isize, 4 * (size_t)cap);
+        }
+        const uint32_t is = c[p + bsize - 4] | (c[p + bsize - 3] << 8) | (c[p + bsize - 2] << 16) |
+                            ((uint32_t)c[p + bsize - 1] << 24);
+        b->coff[b->nblk] = (uint64_t)p;
+        b->ustart[b->nblk] = (uint64_t)u;
+        b->isize[b->nblk] = is;
+        b->nblk++;
+        u += is;
+        p += bsize;
+    }
+    b->ulen = u;
+    b->u = (uint8_t *)malloc((size_t)u + 1);
+    for (int64_t i = 0; i < b->nblk; ++i) {
+        const int64_t s = (int64_t)b->coff[i];
+        const uint32_t xlen = c[s + 10] | (c[s + 11] << 8);
+        const int64_t bsize = (i + 1 < b->nblk ? (int64_t)b->coff[i + 1] : n) - s;
+        z_stream z;
+        memset(&z, 0, sizeof z);
+        inflateInit2(&z, -15);
+        z.next_in = c + s + 12 + xlen;
+        z.avail_in = (uInt)(bsize - 12 - xlen - 8);
+        z.next_out = b->u + b->ustart[i];
+        z.avail_out = b->isize[i];
+        inflate(&z, Z_FINISH);
+        inflateEnd(&z);
+    }
+    free(c);
+    return b;
+bad:
+    free(c);
+    orc_bgzf_close(b);
+    return NULL;
+}
+
+int64_t orc_bgzf_ulen(void *h) { return ((bgzf_t *)h)->ulen; }
+int64_t orc_bgzf_nblocks(void *h) { return ((bgzf_t *)h)->nblk; }
+
+/* virtual offset (coffset << 16 | uoffset) -> absolute uncompressed offset */
+int orc_bgzf_voff_to_u(void *h, uint64_t voff, uint64_t *out) {
+    bgzf_t *b = (bgzf_t *)h;
+    const uint64_t co = voff >> 16, uo = voff & 0xffff;
+    int64_t lo = 0, hi = b->nblk;
+    while (lo < hi) {
+        int64_t m = (lo + hi) / 2;
+        if (b->coff[m] < co)
+            lo = m + 1;
+        else
+            hi = m;
+    }
+    if (lo == b->nblk || b->coff[lo] != co) {
+        if (co >= (b->nblk ? b->coff[b->nblk - 1] + 1 : 0)) { /* at / past the end */
+            *out = (uint64_t)b->ulen;
+            return 0;
+        }
+        return -1;
+    }
+    *out = b->ustart[lo] + uo;
+    return 0;
+}
+
+/* ------------------------------------------------------------ reader on S */
+typedef struct {
+    const char *s;
+    int64_t n, pos;
+} rd_t;
+
+/* readPastChars<A, B> (vcf_chunk_reader.h:262-301): '\0' at the cut */
+static char read_past(rd_t *r, char a, char b, const char **f, int64_t *fl) {
+    const int64_t st = r->pos;
+    while (r->pos < r->n) {
+        const char c = r->s[r->pos];
+        if (c == a || c == b) {
+            *f = r->s + st;
+            *fl = r->pos - st;
+            r->pos++;
+            return c;
+        }
+        r->pos++;
+    }
+    *f = r->s + st;
+    *fl = r->pos - st;
+    return '\0';
+}
+
+/* skipPast<N, delim> (:308-328) */
+static int skip_past(rd_t *r, char d, int N) {
+    int num = N;
+    while (r->pos < r->n)
+        if (r->s[r->pos++] == d && (N == 1 || --num == 0)) return 1;
+    return 0;
+}
+
+/* skipPastAndCountChars (:330-350) */
+static uint64_t skip_count(rd_t *r, char d) {
+    uint64_t k = 0;
+    while (r->pos < r->n) {
+        const char c = r->s[r->pos];
+        k += (c == '\t') || (c == '/') || (c == '|') || (c == ';') || (c == ':');
+        r->pos++;
+        if (c == d) return k;
+    }
+    return k;
+}
+
+/* fast_atoi.h:73-99 atoui64(str, len) for len <= 20 (UB beyond) */
+static int atoui64_len(const char *str, uint8_t len, uint64_t *out) {
+    static const uint64_t off[21] = {0,
+                                     (uint64_t)'0',
+                                     (uint64_t)'0' * 11ull,
+                                     (uint64_t)'0' * 111ull,
+                                     (uint64_t)'0' * 1111ull,
+                                     (uint64_t)'0' * 11111ull,
+                                     (uint64_t)'0' * 111111ull,
+                                     (uint64_t)'0' * 1111111ull,
+                                     (uint64_t)'0' * 11111111ull,
+                                     (uint64_t)'0' * 111111111ull,
+                                     (uint64_t)'0' * 1111111111ull,
+                                     (uint64_t)'0' * 11111111111ull,
+                                     (uint64_t)'0' * 111111111111ull,
+                                     (uint64_t)'0' * 1111111111111ull,
+                                     (uint64_t)'0' * 11111111111111ull,
+                                     (uint64_t)'0' * 111111111111111ull,
+                                     (uint64_t)'0' * 1111111111111111ull,
+                                     (uint64_t)'0' * 11111111111111111ull,
+                                     (uint64_t)'0' * 111111111111111111ull,
+                                     (uint64_t)'0' * 1111111111111111111ull,
+                                     (uint64_t)'0' * 11111111111111111111ull};
+    if (len > 20) return -1;
+    uint64_t v = 0, p10 = 1;
+    for (int k = 1; k <= len; ++k) {
+        v += (uint64_t)(int64_t)(signed char)str[len - k] * p10;
+        p10 *= 10ull;
+    }
+    *out = v - off[len];
+    return 0;
+}
+
+/* write_data_to_s3.h:150-228 recordHeader: reader movement only */
+static void record_header(rd_t *r, int *contig_set) {
+    int loop_pos = 0;
+    if (*contig_set) {
+        skip_past(r, '\t', 1);
+        loop_pos = 1;
+    }
+    do {
+        const char *f;
+        int64_t fl;
+        const char last = read_past(r, '\t', ',', &f, &fl);
+        if (last == '\0') break;
+        if (fl >= 1) {
+            switch (++loop_pos) {
+                case 1:
+                    *contig_set = 1;
+                    break;
+                case 2:
+                    skip_past(r, '\t', 1);
+                    loop_pos++;
+                    break;
+                case 5:
+                    if (last == ',') loop_pos--;
+                    break;
+                default:
+                    break;
+            }
+        }
+    } while (loop_pos <= 4);
+    skip_past(r, '\t', 2);
+}
+
+/* main.cpp:52-109 addCounts */
+static int add_counts(rd_t *r, uint64_t *nv, uint64_t *nc) {
+    int found_ac = 0, found_an = 0;
+    do {
+        const char *f;
+        int64_t fl;
+        const char last = read_past(r, ';', '\t', &f, &fl);
+        if (last == '\0') break;
+        if (fl >= 4) {
+            if (!memcmp(f, "AC=", 3)) {
+                found_ac = 1;
+                *nv += 1;
+                for (int64_t j = 3; j < fl; ++j)
+                    if (f[j] == ',') *nv += 1;
+            } else if (!memcmp(f, "AN=", 3)) {
+                uint64_t v;
+                found_an = 1;
+                if (atoui64_len(f + 3, (uint8_t)((uint8_t)fl - 3), &v)) return -1;
+                *nc += v;
+            }
+        }
+        if (last == '\t' && !(found_ac && found_an)) break;
+    } while (!(found_ac && found_an));
+    return 0;
+}
+
+/* main.cpp:195-245 getRegionStats over S = U[u_start, u_end) */
+int orc_region_stats(const char *s, int64_t n, uint64_t *num_variants, uint64_t *num_calls, uint64_t *records) {
+    rd_t r = {s, n, 0};
+    uint64_t nv = 0, nc = 0, recs = n > 0; /* `records` is diagnostic only (main.cpp:230) */
+    int contig_set = 0;
+    record_header(&r, &contig_set);
+    if (add_counts(&r, &nv, &nc)) return -1;
+    const uint64_t skip = 2 * skip_count(&r, '\n');
+    while (r.pos < r.n) { /* keepReading() */
+        record_header(&r, &contig_set);
+        if (add_counts(&r, &nv, &nc)) return -1;
+        r.pos += (int64_t)skip; /* seek(skipSize) */
+        skip_past(&r, '\n', 1);
+        recs++;
+    }
+    *num_variants = nv;
+    *num_calls = nc;
+    *records = recs;
+    return 0;
+}
+
+int orc_summarise_slice(void *h, uint64_t vstart, uint64_t vend, uint64_t *num_variants, uint64_t *num_calls,
+                        uint64_t *records) {
+    bgzf_t *b = (bgzf_t *)h;
+    uint64_t u0, u1;
+    if (orc_bgzf_voff_to_u(b, vstart, &u0) || orc_bgzf_voff_to_u(b, vend, &u1)) return -2;
+    if (u1 < u0) u1 = u0;
+    return orc_region_stats((const char *)b->u + u0, (int64_t)(u1 - u0), num_variants, num_calls, records);
+}

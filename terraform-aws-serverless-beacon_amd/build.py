@@ -68,7 +68,7 @@ def build(verbose: bool = False) -> str:
     # synthetic-data generator (bench / tests input only; host C++)
     syn = os.path.join(CSRC, 'synth.cpp')
     if _stale(SYNTH_LIB, [syn]):
-        run(['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-pthread', '-Wall', '-o', SYNTH_LIB, syn])
+        run(['g++', '-O2', '-std=c++17', '-fPIC', '-shared', '-pthread', '-Wall', '-o', SYNTH_LIB, syn, '-lz'])
     return LIB
 
 

@@ -178,6 +178,8 @@ struct sb_result_set {
 
 namespace {
 
+constexpr uint32_t kBlockRecs = 256;  // summarise_kernel workgroup size
+
 // coarse POS index of one segment: bucket[b] = first record with
 // POS >= base + (b << shift), for b in [0, n]; bucket[n] = segment end
 void build_buckets(const std::vector<uint32_t> &pos, const Segment &sg, BucketIndex &bi,
@@ -219,6 +221,9 @@ void upload_store(sb_builder &b, sb_store &s) {
     std::vector<int64_t> fb_off;
     std::vector<uint16_t> vt;
     std::vector<uint8_t> blob;
+    std::vector<uint64_t> start;
+    std::vector<SumHot> sum;
+    std::vector<uint32_t> cur, dcount;
     uint64_t nr = 0, nx = 0, np = 0;
     for (auto &v : b.vcfs) {
         nr += v.c.pos.size();
@@ -251,6 +256,10 @@ void upload_store(sb_builder &b, sb_store &s) {
         ref_key.insert(ref_key.end(), c.ref_key.begin(), c.ref_key.end());
         a0_key.insert(a0_key.end(), c.a0_key.begin(), c.a0_key.end());
         vt.insert(vt.end(), c.vt.begin(), c.vt.end());
+        start.insert(start.end(), c.start.begin(), c.start.end());
+        sum.insert(sum.end(), c.sum.begin(), c.sum.end());
+        cur.insert(cur.end(), c.cur.begin(), c.cur.end());
+        dcount.insert(dcount.end(), c.dcount.begin(), c.dcount.end());
         for (size_t i = 0; i < n; ++i) {
             ref_off.push_back(c.ref_off[i] + blob_base);
             a0_off.push_back(c.a0_off[i] + blob_base);
@@ -297,7 +306,12 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.d.planes = dev_upload(s, planes);
     s.d.fb = dev_upload(s, fb);
     s.d.bucket = dev_upload(s, bucket);
+    s.ds.sum = dev_upload(s, sum);
+    s.ds.start = dev_upload(s, start);
+    s.ds.cur = dev_upload(s, cur);
+    s.ds.dcount = dev_upload(s, dcount);
     HIP_OK(hipStreamSynchronize(s.stream));
+    s.h_start = std::move(start);
     // host copies for output planning and result formatting
     s.h_pos = std::move(pos);
     s.h_end.resize(rec.size());
@@ -641,9 +655,105 @@ sb_result_set *fetch(sb_batch &B) {
     return R.release();
 }
 
+// virtual offset -> offset in the VCF text stream (block table of the BGZF file)
+bool voff_to_stream(const VcfData &v, uint64_t voff, uint64_t *u) {
+    const uint64_t co = voff >> 16, uo = voff & 0xffffu;
+    auto it = std::lower_bound(v.blk_coff.begin(), v.blk_coff.end(), co);
+    if (it == v.blk_coff.end()) {
+        if (uo) return false;
+        *u = v.stream_len;  // one past the last block
+        return true;
+    }
+    if (*it != co) return false;
+    *u = v.blk_ustart[static_cast<size_t>(it - v.blk_coff.begin())] + uo;
+    return *u <= v.stream_len;
+}
+
+void summarise(sb_store &s, const sb_slice *sl, size_t n, sb_slice_stats *out, double *device_ms) {
+    std::vector<SDev> hs(n);
+    std::vector<int32_t> herr(n, 0);
+    uint64_t words = 0;
+    for (size_t i = 0; i < n; ++i) {
+        SDev &d = hs[i];
+        d.lo = d.hi = 0;
+        d.bitmap_off = words;
+        if (sl[i].vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "slice " + std::to_string(i) + ": unknown vcf id");
+        const VcfData &v = s.vcfs[sl[i].vcf_id];
+        if (v.blk_coff.empty()) throw Error(SB_EINVAL, "summarise needs a VCF ingested from a BGZF file (virtual offsets)");
+        uint64_t u0, u1;
+        if (!voff_to_stream(v, sl[i].virtual_start, &u0) || !voff_to_stream(v, sl[i].virtual_end, &u1)) {
+            herr[i] = SB_QERR_UNSUPPORTED;  // offset not on a block of this file
+            continue;
+        }
+        if (u1 < u0) u1 = u0;
+        const uint32_t rb = v.rec_base;
+        uint32_t re = rb;
+        for (const auto &sg : v.segments) re = std::max(re, sg.hi);
+        auto first = s.h_start.begin() + rb, last = s.h_start.begin() + re;
+        const uint32_t lo = rb + static_cast<uint32_t>(std::lower_bound(first, last, u0) - first);
+        const uint32_t hi = rb + static_cast<uint32_t>(std::lower_bound(first, last, u1) - first);
+        if (hi > lo) {
+            // the slice must start on a record and must not cut one (index
+            // chunk boundaries are record boundaries); header bytes likewise
+            const uint64_t end_last = hi < re ? s.h_start[hi] : v.stream_len;
+            if (s.h_start[lo] != u0 || end_last > u1) herr[i] = SB_QERR_UNSUPPORTED;
+        } else if (u1 > u0) {
+            herr[i] = SB_QERR_UNSUPPORTED;  // a non-empty stretch with no record start
+        }
+        if (herr[i]) continue;
+        d.lo = lo;
+        d.hi = hi;
+        words += static_cast<uint64_t>((hi - lo + kBlockRecs - 1) / kBlockRecs) * 4;
+    }
+    HIP_OK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    DevMem dsl, dbm, dres;
+    dsl.alloc(n * sizeof(SDev));
+    dbm.alloc(words * 8);
+    dres.alloc(n * sizeof(SRes));
+    if (n) HIP_OK(hipMemcpyAsync(dsl.p, hs.data(), n * sizeof(SDev), hipMemcpyHostToDevice, st));
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, st));
+    launch_summarise(s.ds, dsl.as<SDev>(), static_cast<uint32_t>(n), dbm.as<uint64_t>(), dres.as<SRes>(), st);
+    HIP_OK(hipEventRecord(e1, st));
+    HIP_OK(hipGetLastError());
+    std::vector<SRes> r(n);
+    if (n) HIP_OK(hipMemcpyAsync(r.data(), dres.p, n * sizeof(SRes), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (device_ms) *device_ms = ms;
+    for (size_t i = 0; i < n; ++i) {
+        out[i].error = herr[i] ? herr[i] : r[i].error;
+        out[i]._pad = 0;
+        out[i].num_variants = out[i].error ? 0 : r[i].num_variants;
+        out[i].num_calls = out[i].error ? 0 : r[i].num_calls;
+        out[i].records = out[i].error ? 0 : r[i].records;
+    }
+}
+
 }  // namespace
 
 extern "C" {
+
+int sb_summarise_slices(sb_store *s, const sb_slice *slices, size_t n, sb_slice_stats *out, double *device_ms) {
+    return guard([&] {
+        if (!s || (!slices && n) || (!out && n)) throw Error(SB_EINVAL, "NULL argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        summarise(*s, slices, n, out, device_ms);
+    });
+}
+
+int sb_store_vcf_stream(const sb_store *s, uint32_t vcf_id, uint64_t *n_blocks, uint64_t *stream_len) {
+    if (!s || vcf_id >= s->vcfs.size()) return SB_EINVAL;
+    if (n_blocks) *n_blocks = s->vcfs[vcf_id].blk_coff.size();
+    if (stream_len) *stream_len = s->vcfs[vcf_id].stream_len;
+    return SB_OK;
+}
 
 const char *sb_last_error(void) { return sb::last_error_cstr(); }
 int sb_abi_version(void) { return SB_ABI_VERSION; }

@@ -125,4 +125,43 @@ struct QRes {
 // fallback labels with alts[i] for a 1-based i, search_variants.py:223)
 inline constexpr uint64_t kHitAltShift = 32;
 
+// ---- summariseSlice (lambda/summariseSlice/source/main.cpp:52-109,195-245)
+// What one record contributes when the reference's VcfChunkReader visits it,
+// precomputed at ingest from the record's own line:
+//   rem = bytes from the cursor addCounts leaves (after the delimiter that
+//         ended the AC/AN scan) to the end of the line incl. '\n'; the skip
+//         heuristic (seek(skipSize) + skipPast('\n'), main.cpp:234-235) swallows
+//         the next record iff skipSize >= rem;
+//   nvf = numVariants contribution (1 + commas per AC= field seen) | bit 31 =
+//         record the restatement cannot represent (its reads would leave the
+//         line: INFO ending in '\n' before AC and AN were both seen, empty
+//         CHROM/REF/ALT fields, AN= values longer than atoui64 handles);
+//   nc  = numCalls contribution (atoui64 of each AN= field seen).
+struct alignas(16) SumHot {
+    uint32_t rem;
+    uint32_t nvf;
+    uint64_t nc;
+};
+inline constexpr uint32_t kSumUnsupported = 1u << 31;
+
+struct SDev {  // one summariseSlice invocation after host planning
+    uint32_t lo, hi;        // records whose line starts in [U(vstart), U(vend))
+    uint64_t bitmap_off;    // u64-word offset of this slice's overshoot bitmap
+};
+
+struct SRes {
+    int32_t error;
+    int32_t pad;
+    uint64_t num_variants;
+    uint64_t num_calls;
+    uint64_t records;  // records visited (the reference's `records` log count)
+};
+
+struct SStore {  // summary columns
+    const SumHot *sum;
+    const uint64_t *start;  // line start, absolute offset in the VCF text stream
+    const uint32_t *cur;    // cursor offset after addCounts, relative to start
+    const uint32_t *dcount; // delimiters {\t / | ; :} from the cursor to '\n'
+};
+
 }  // namespace sb

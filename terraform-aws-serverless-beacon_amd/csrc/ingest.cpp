@@ -37,13 +37,149 @@ struct Local {  // one thread's parse of a run of lines
 
 inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
 
+// ---- summariseSlice per-record restatement --------------------------------
+// The reference reader walks one record as recordHeader (write_data_to_s3.h:
+// 150-228) then addCounts (main.cpp:52-109).  Both are simulated here on the
+// record's own line; a read that would run off the line (into the next
+// record) marks the record unsupported.
+struct LineRd {
+    const char *s;
+    size_t n, pos;
+    bool off_end;
+};
+
+char lr_read_past(LineRd &r, char a, char b, size_t *fs, size_t *fl) {  // readPastChars<a, b>
+    const size_t st = r.pos;
+    while (r.pos < r.n) {
+        const char c = r.s[r.pos];
+        if (c == a || c == b) {
+            *fs = st;
+            *fl = r.pos - st;
+            ++r.pos;
+            return c;
+        }
+        ++r.pos;
+    }
+    r.off_end = true;
+    return '\0';
+}
+
+bool lr_skip_past(LineRd &r, char d, int N) {  // skipPast<N, d>
+    int num = N;
+    while (r.pos < r.n)
+        if (r.s[r.pos++] == d && (N == 1 || --num == 0)) return true;
+    r.off_end = true;
+    return false;
+}
+
+// fast_atoi.h:73-99 atoui64(str, len); false where the reference is UB (len > 20)
+bool atoui64_len(const char *str, uint8_t len, uint64_t *out) {
+    if (len > 20) return false;
+    static const uint64_t ones[21] = {0, 1ull, 11ull, 111ull, 1111ull, 11111ull, 111111ull, 1111111ull, 11111111ull,
+                                      111111111ull, 1111111111ull, 11111111111ull, 111111111111ull,
+                                      1111111111111ull, 11111111111111ull, 111111111111111ull,
+                                      1111111111111111ull, 11111111111111111ull, 111111111111111111ull,
+                                      1111111111111111111ull, 11111111111111111111ull};
+    uint64_t v = 0, p10 = 1;
+    for (int k = 1; k <= len; ++k) {
+        v += static_cast<uint64_t>(static_cast<int64_t>(static_cast<signed char>(str[len - k]))) * p10;
+        p10 *= 10ull;
+    }
+    *out = v - static_cast<uint64_t>('0') * ones[len];
+    return true;
+}
+
+// line = record bytes incl. its '\n' (if any); fills the summary columns
+void summarise_line(const char *line, size_t len, SumHot *sum, uint32_t *cur, uint32_t *dcount) {
+    LineRd r{line, len, 0, false};
+    bool bad = false;
+    // recordHeader with the contig already known: skip CHROM, POS field,
+    // skip ID, REF, ALT (',' continues ALT), then skip QUAL and FILTER.
+    // A first record reads CHROM as a field instead: identical unless CHROM
+    // is empty or holds ',' (flagged).
+    {
+        size_t fs, fl;
+        const char c0 = lr_read_past(r, '\t', ',', &fs, &fl);
+        if (c0 != '\t' || fl == 0) bad = true;
+    }
+    int loop_pos = 1;
+    do {
+        size_t fs, fl;
+        const char last = lr_read_past(r, '\t', ',', &fs, &fl);
+        if (last == '\0') break;
+        if (fl >= 1) {
+            switch (++loop_pos) {
+                case 2:
+                    lr_skip_past(r, '\t', 1);
+                    ++loop_pos;
+                    break;
+                case 5:
+                    if (last == ',') --loop_pos;
+                    break;
+                default:
+                    break;
+            }
+        } else {
+            bad = true;  // empty REF/ALT part: the reference re-reads the next field
+        }
+    } while (loop_pos <= 4);
+    lr_skip_past(r, '\t', 2);
+    // addCounts
+    uint64_t nv = 0, nc = 0;
+    bool found_ac = false, found_an = false;
+    do {
+        size_t fs, fl;
+        const char last = lr_read_past(r, ';', '\t', &fs, &fl);
+        if (last == '\0') break;
+        if (fl >= 4) {
+            const char *f = line + fs;
+            if (!memcmp(f, "AC=", 3)) {
+                found_ac = true;
+                nv += 1;
+                for (size_t j = 3; j < fl; ++j) nv += f[j] == ',';
+            } else if (!memcmp(f, "AN=", 3)) {
+                found_an = true;
+                uint64_t v;
+                if (!atoui64_len(f + 3, static_cast<uint8_t>(static_cast<uint8_t>(fl) - 3), &v)) bad = true;
+                else nc += v;
+            }
+        }
+        if (last == '\t' && !(found_ac && found_an)) break;
+    } while (!(found_ac && found_an));
+    if (r.off_end) bad = true;  // the reference would continue into the next line
+    const size_t c = r.pos;
+    uint32_t d = 0;
+    for (size_t i = c; i < len && line[i] != '\n'; ++i) {
+        const char ch = line[i];
+        d += (ch == '\t') | (ch == '/') | (ch == '|') | (ch == ';') | (ch == ':');
+    }
+    if (nv >= kSumUnsupported || len > 0xffffffffull) bad = true;
+    sum->rem = static_cast<uint32_t>(len - c);
+    sum->nvf = static_cast<uint32_t>(nv & 0x7fffffffu) | (bad ? kSumUnsupported : 0u);
+    sum->nc = nc;
+    *cur = static_cast<uint32_t>(c);
+    *dcount = d;
+}
+
 struct Parser {
     uint32_t n_samples;
     uint32_t words;
     bool keep_gt;
 
-    // Returns false and sets L.err on failure.
-    bool line(const char *p, const char *e, Local &L) {
+    // [p, e) = the record without its line terminator; [p, full_end) with it;
+    // abs = offset of p in the VCF text stream.  Returns false and sets L.err
+    // on failure.
+    bool line(const char *p, const char *e, const char *full_end, uint64_t abs, Local &L) {
+        {
+            VcfCols &c = L.c;
+            SumHot sh;
+            uint32_t cu, dc;
+            summarise_line(p, static_cast<size_t>(full_end - p), &sh, &cu, &dc);
+            c.start.push_back(abs);
+            c.sum.push_back(sh);
+            c.cur.push_back(cu);
+            c.dcount.push_back(dc);
+        }
         // ---- fixed columns
         const char *f[9];
         size_t n[9];
@@ -424,10 +560,15 @@ void merge(sb_builder &b, VcfData &v, Local &L) {
     app(d.planes0, s.planes0);
     app(d.planesx, s.planesx);
     app(d.fb, s.fb);
+    app(d.start, s.start);
+    app(d.sum, s.sum);
+    app(d.cur, s.cur);
+    app(d.dcount, s.dcount);
     d.any_negative = d.any_negative || s.any_negative;
 }
 
-void parse_records(sb_builder &b, VcfData &v, const char *p, size_t len) {
+// [p, p + len): whole lines; base = offset of p in the VCF text stream
+void parse_records(sb_builder &b, VcfData &v, const char *p, size_t len, uint64_t base) {
     // line starts
     std::vector<const char *> starts;
     const char *e = p + len;
@@ -454,9 +595,10 @@ void parse_records(sb_builder &b, VcfData &v, const char *p, size_t len) {
         for (size_t i = lo; i < hi; ++i) {
             const char *s = starts[i];
             const char *le = static_cast<const char *>(memchr(s, '\n', static_cast<size_t>(e - s)));
+            const char *full = le ? le + 1 : e;
             if (!le) le = e;
             if (le > s && le[-1] == '\r') --le;
-            if (!P.line(s, le, L)) {
+            if (!P.line(s, le, full, base + static_cast<uint64_t>(s - p), L)) {
                 L.err_line = i;
                 return;
             }
@@ -483,10 +625,12 @@ void add_text(sb_builder &b, VcfData &v, const char *text, size_t len) {
         text = joined.data();
         len = joined.size();
     }
+    const uint64_t base = v.stream_off;  // stream offset of text[0]
     // keep an unterminated tail for the next call
     size_t upto = len;
     while (upto > 0 && text[upto - 1] != '\n') --upto;
     if (upto < len) v.carry.assign(text + upto, len - upto);
+    v.stream_off = base + upto;
     const char *p = text, *e = text + upto;
     // header lines first (sequential)
     while (p < e && *p == '#') {
@@ -497,7 +641,22 @@ void add_text(sb_builder &b, VcfData &v, const char *text, size_t len) {
         parse_header_line(v, p, le);
         p = nl + 1;
     }
-    if (p < e) parse_records(b, v, p, static_cast<size_t>(e - p));
+    if (p < e) parse_records(b, v, p, static_cast<size_t>(e - p), base + static_cast<uint64_t>(p - text));
+}
+
+// BGZF (SAMv1 §4.1): gzip members with a 'BC' extra subfield holding BSIZE-1
+bool bgzf_block_size(const uint8_t *c, size_t avail, size_t *bsize) {
+    if (avail < 18 || c[0] != 0x1f || c[1] != 0x8b || c[2] != 8 || !(c[3] & 4)) return false;
+    const size_t xlen = c[10] | (c[11] << 8);
+    for (size_t x = 12; x + 4 <= 12 + xlen && x + 4 <= avail;) {
+        const size_t slen = c[x + 2] | (c[x + 3] << 8);
+        if (c[x] == 'B' && c[x + 1] == 'C' && slen == 2 && x + 6 <= avail) {
+            *bsize = (c[x + 4] | (c[x + 5] << 8)) + 1u;
+            return *bsize >= 26;
+        }
+        x += 4 + slen;
+    }
+    return false;
 }
 
 }  // namespace
@@ -516,8 +675,90 @@ void builder_flush(sb_builder &b, uint32_t vcf_id) {
     }
 }
 
+// BGZF ingest: block table for virtual offsets, blocks inflated in parallel
+// in ~64 MiB batches that are fed to the text parser in order.
+void add_bgzf(sb_builder &b, VcfData &v, const std::vector<uint8_t> &c, const char *path) {
+    if (v.stream_off != 0 || !v.carry.empty()) throw Error(SB_EINVAL, "a BGZF file must be the only text source of its VCF");
+    struct Blk {
+        size_t coff, bsize;
+        uint32_t isize;
+        uint64_t ustart;
+    };
+    std::vector<Blk> blks;
+    uint64_t u = 0;
+    for (size_t p = 0; p < c.size();) {
+        size_t bs;
+        if (!bgzf_block_size(c.data() + p, c.size() - p, &bs) || p + bs > c.size())
+            throw Error(SB_EIO, std::string("corrupt BGZF block in ") + path);
+        const uint8_t *t = c.data() + p + bs - 4;
+        const uint32_t is = t[0] | (t[1] << 8) | (t[2] << 16) | (static_cast<uint32_t>(t[3]) << 24);
+        blks.push_back(Blk{p, bs, is, u});
+        v.blk_coff.push_back(p);
+        v.blk_ustart.push_back(u);
+        u += is;
+        p += bs;
+    }
+    v.stream_len = u;
+    const unsigned nt = std::max(1u, std::min(16u, b.opts.n_threads > 0 ? static_cast<unsigned>(b.opts.n_threads)
+                                                                          : std::thread::hardware_concurrency()));
+    std::vector<char> buf;
+    for (size_t i = 0; i < blks.size();) {
+        size_t j = i;
+        uint64_t bu = 0;
+        while (j < blks.size() && (bu < (uint64_t(64) << 20) || j == i)) bu += blks[j++].isize;
+        buf.resize(bu);
+        std::atomic<size_t> next{i};
+        std::atomic<int> bad{0};
+        auto work = [&] {
+            for (size_t k; (k = next.fetch_add(1)) < j;) {
+                const Blk &bk = blks[k];
+                const size_t xlen = c[bk.coff + 10] | (c[bk.coff + 11] << 8);
+                z_stream z;
+                memset(&z, 0, sizeof z);
+                if (inflateInit2(&z, -15) != Z_OK) {
+                    bad = 1;
+                    continue;
+                }
+                z.next_in = const_cast<uint8_t *>(c.data() + bk.coff + 12 + xlen);
+                z.avail_in = static_cast<uInt>(bk.bsize - 12 - xlen - 8);
+                z.next_out = reinterpret_cast<Bytef *>(buf.data() + (bk.ustart - blks[i].ustart));
+                z.avail_out = bk.isize;
+                const int rc = inflate(&z, Z_FINISH);
+                if (bk.isize && rc != Z_STREAM_END) bad = 1;
+                inflateEnd(&z);
+            }
+        };
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t) th.emplace_back(work);
+        for (auto &t : th) t.join();
+        if (bad) throw Error(SB_EIO, std::string("BGZF inflate failed in ") + path);
+        add_text(b, v, buf.data(), buf.size());
+        i = j;
+    }
+}
+
 void builder_add_file(sb_builder &b, uint32_t vcf_id, const char *path) {
     if (vcf_id >= b.vcfs.size()) throw Error(SB_ENOSTORE, "unknown vcf id");
+    {
+        FILE *fp = fopen(path, "rb");
+        if (!fp) throw Error(SB_EIO, std::string("cannot open ") + path);
+        uint8_t hdr[18];
+        const size_t got = fread(hdr, 1, sizeof hdr, fp);
+        size_t bs;
+        if (got == sizeof hdr && bgzf_block_size(hdr, got, &bs)) {
+            fseek(fp, 0, SEEK_END);
+            const long n = ftell(fp);
+            fseek(fp, 0, SEEK_SET);
+            std::vector<uint8_t> c(static_cast<size_t>(n));
+            const size_t rd = fread(c.data(), 1, c.size(), fp);
+            fclose(fp);
+            if (rd != c.size()) throw Error(SB_EIO, std::string("short read: ") + path);
+            add_bgzf(b, b.vcfs[vcf_id], c, path);
+            builder_flush(b, vcf_id);
+            return;
+        }
+        fclose(fp);
+    }
     gzFile f = gzopen(path, "rb");
     if (!f) throw Error(SB_EIO, std::string("cannot open ") + path);
     gzbuffer(f, 1 << 20);

@@ -476,7 +476,125 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(const QDev *__restrict_
 
 inline uint32_t blocks_for(uint32_t nq) { return (nq + kWavesPerBlock - 1) / kWavesPerBlock; }
 
+// ------------------------------------------------------------ summariseSlice
+// lambda/summariseSlice/source/main.cpp:195-245.  The reader visits the first
+// record, then for every later record r: recordHeader + addCounts, seek
+// (skipSize = 2 x delimiters after the first record's AC/AN cursor) and
+// skipPast('\n').  That skips record r+1.. whenever skipSize >= rem_r (the
+// bytes left on r's line).  Phase A sums every record of the slice and marks
+// those overshoots; phase B (wave 0) walks the marks in order, keeps only the
+// overshoots of visited records and subtracts the records their jumps skip.
+__global__ __launch_bounds__(kBlock) void summarise_kernel(SStore ss, const SDev *__restrict__ slices, uint32_t ns,
+                                                           uint64_t *__restrict__ bitmap, SRes *__restrict__ out) {
+    __shared__ uint64_t red_nv[kWavesPerBlock], red_nc[kWavesPerBlock];
+    __shared__ uint32_t red_bad[kWavesPerBlock];
+    const uint32_t sid = blockIdx.x;
+    if (sid >= ns) return;
+    const SDev S = slices[sid];
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    const uint32_t lo = S.lo, hi = S.hi;
+    if (lo >= hi) {
+        if (threadIdx.x == 0) out[sid] = SRes{0, 0, 0, 0, 0};
+        return;
+    }
+    const uint64_t skip = 2ull * ss.dcount[lo];
+    uint64_t nv = 0, nc = 0;
+    uint32_t bad = 0;
+    uint64_t *bm = bitmap + S.bitmap_off;
+    for (uint32_t base = lo; base < hi; base += kBlock) {
+        const uint32_t r = base + threadIdx.x;
+        bool o = false;
+        if (r < hi) {
+            const SumHot h = ss.sum[r];
+            nv += h.nvf & ~kSumUnsupported;
+            nc += h.nc;
+            bad += h.nvf >> 31;
+            o = r > lo && skip >= h.rem;
+        }
+        const uint64_t m = __ballot(o);
+        if (lane == 0) bm[(base - lo) / kWave + wave] = m;
+    }
+    nv = static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(nv)));
+    nc = static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(nc)));
+    bad = static_cast<uint32_t>(wave_sum_i64(bad));
+    if (lane == 0) {
+        red_nv[wave] = nv;
+        red_nc[wave] = nc;
+        red_bad[wave] = bad;
+    }
+    __syncthreads();  // bitmap words of every wave are visible to wave 0 (same CU)
+    if (wave != 0) return;
+    uint64_t tnv = 0, tnc = 0, tbad = 0;
+    for (int w = 0; w < kWavesPerBlock; ++w) {
+        tnv += red_nv[w];
+        tnc += red_nc[w];
+        tbad += red_bad[w];
+    }
+    uint64_t sub_nv = 0, sub_nc = 0, sub_bad = 0, skipped = 0;
+    uint32_t resume = lo;  // records >= resume are visited until the next jump
+    const uint32_t nwords = (hi - lo + kWave - 1) / kWave;
+    for (uint32_t w0 = 0; w0 < nwords; w0 += kWave) {
+        const uint64_t word = (w0 + lane < nwords) ? bm[w0 + lane] : 0ull;
+        uint64_t nz = __ballot(word != 0ull);
+        while (nz) {
+            const int L = ffs64(nz);
+            nz &= nz - 1;
+            uint64_t bits = static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(word), L));
+            while (bits) {
+                const int b = ffs64(bits);
+                bits &= bits - 1;
+                const uint32_t r = lo + (w0 + static_cast<uint32_t>(L)) * kWave + static_cast<uint32_t>(b);
+                if (r < resume) continue;  // r itself was skipped: it never seeks
+                // visited overshoot: the seek lands at P, skipPast('\n') resumes
+                // at the first record starting after P
+                const uint64_t P = ss.start[r] + ss.cur[r] + skip;
+                uint32_t t = hi;
+                for (uint32_t c0 = r + 1; c0 < hi; c0 += kWave) {
+                    const uint32_t i = c0 + static_cast<uint32_t>(lane);
+                    const uint64_t m = __ballot(i < hi && ss.start[i] > P);
+                    if (m) {
+                        t = c0 + static_cast<uint32_t>(ffs64(m));
+                        break;
+                    }
+                }
+                // subtract the skipped records (r, t)
+                for (uint32_t c0 = r + 1; c0 < t; c0 += kWave) {
+                    const uint32_t i = c0 + static_cast<uint32_t>(lane);
+                    uint64_t a = 0, c = 0, d = 0;
+                    if (i < t) {
+                        const SumHot h = ss.sum[i];
+                        a = h.nvf & ~kSumUnsupported;
+                        c = h.nc;
+                        d = h.nvf >> 31;
+                    }
+                    sub_nv += static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(a)));
+                    sub_nc += static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(c)));
+                    sub_bad += static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(d)));
+                }
+                skipped += t - (r + 1);
+                resume = t;
+            }
+        }
+    }
+    if (lane == 0) {
+        SRes o;
+        o.error = (tbad - sub_bad) ? SB_QERR_UNSUPPORTED : 0;
+        o.pad = 0;
+        o.num_variants = tnv - sub_nv;
+        o.num_calls = tnc - sub_nc;
+        o.records = (hi - lo) - skipped;
+        out[sid] = o;
+    }
+}
+
 }  // namespace
+
+void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, uint64_t *bitmap, SRes *out,
+                      hipStream_t s) {
+    if (!ns) return;
+    hipLaunchKernelGGL(summarise_kernel, dim3(ns), dim3(kBlock), 0, s, ss, slices, ns, bitmap, out);
+}
 
 void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,
                     uint64_t *out, hipStream_t s) {

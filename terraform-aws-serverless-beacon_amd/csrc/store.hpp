@@ -40,6 +40,10 @@ struct VcfCols {
     std::vector<uint64_t> planesx;  // [extra row][words]
     std::vector<uint32_t> fb;       // [fallback row][n_samples]
     bool any_negative = false;      // some INFO AC entry < 0
+    // summariseSlice columns (record-indexed)
+    std::vector<uint64_t> start;    // absolute line start in the VCF text stream
+    std::vector<SumHot> sum;
+    std::vector<uint32_t> cur, dcount;
 };
 
 struct BucketIndex {  // coarse POS index of one segment
@@ -59,6 +63,11 @@ struct VcfData {
     std::vector<BucketIndex> buckets;  // parallel to segments (set by finish)
     VcfCols c;
     std::string carry;  // partial line kept between add_text calls
+    uint64_t stream_off = 0;  // text bytes consumed so far (incl. carry)
+    // BGZF block table (compressed offset, uncompressed start) incl. the EOF
+    // block, for virtual-offset -> stream-offset conversion; empty for text
+    std::vector<uint64_t> blk_coff, blk_ustart;
+    uint64_t stream_len = 0;
     // global placement (set by finish)
     uint32_t rec_base = 0, x_base = 0;
     uint64_t plane0_base = 0, planex_base = 0;
@@ -107,8 +116,10 @@ struct sb_store {
     std::vector<uint16_t> h_vt;
     std::vector<uint64_t> h_ref_off, h_a0_off, h_x_off;
     std::vector<uint8_t> h_blob;
+    std::vector<uint64_t> h_start;  // line start in the VCF text stream (summariseSlice planning)
     // device image
     sb::DStore d{};
+    sb::SStore ds{};
     std::vector<sb::DeviceBuffer> bufs;
     uint64_t device_bytes = 0;
     ~sb_store();

@@ -329,3 +329,84 @@ char *sbs_records(void *h, uint64_t lo, uint64_t hi, int sites_only, int n_threa
 void sbs_free_text(char *p) { free(p); }
 
 }  // extern "C"
+
+// ---------------------------------------------------------------- BGZF writer
+// bgzip-compatible output: blocks of <= 0xff00 input bytes, each a gzip
+// member with the BC extra subfield (SAMv1 §4.1), then the 28-byte EOF block.
+#include <zlib.h>
+
+namespace {
+size_t bgzf_block(const uint8_t *in, size_t n, int level, uint8_t *out) {
+    z_stream z;
+    memset(&z, 0, sizeof z);
+    deflateInit2(&z, level, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+    z.next_in = const_cast<uint8_t *>(in);
+    z.avail_in = static_cast<uInt>(n);
+    z.next_out = out + 18;
+    z.avail_out = 65536 - 18 - 8;
+    int rc = deflate(&z, Z_FINISH);
+    size_t clen = z.total_out;
+    deflateEnd(&z);
+    if (rc != Z_STREAM_END) {  // incompressible: stored block
+        memset(&z, 0, sizeof z);
+        deflateInit2(&z, 0, Z_DEFLATED, -15, 8, Z_DEFAULT_STRATEGY);
+        z.next_in = const_cast<uint8_t *>(in);
+        z.avail_in = static_cast<uInt>(n);
+        z.next_out = out + 18;
+        z.avail_out = 65536 - 18 - 8;
+        deflate(&z, Z_FINISH);
+        clen = z.total_out;
+        deflateEnd(&z);
+    }
+    const size_t bsize = 18 + clen + 8;
+    static const uint8_t hdr[12] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0};
+    memcpy(out, hdr, 12);
+    out[12] = 'B';
+    out[13] = 'C';
+    out[14] = 2;
+    out[15] = 0;
+    out[16] = static_cast<uint8_t>((bsize - 1) & 0xff);
+    out[17] = static_cast<uint8_t>((bsize - 1) >> 8);
+    const uint32_t crc = static_cast<uint32_t>(crc32(crc32(0L, Z_NULL, 0), in, static_cast<uInt>(n)));
+    uint8_t *t = out + 18 + clen;
+    for (int i = 0; i < 4; ++i) t[i] = static_cast<uint8_t>(crc >> (8 * i));
+    for (int i = 0; i < 4; ++i) t[4 + i] = static_cast<uint8_t>(static_cast<uint32_t>(n) >> (8 * i));
+    return bsize;
+}
+}  // namespace
+
+extern "C" {
+
+// Compress `n` bytes into BGZF (appending the EOF block when eof != 0).
+char *sbs_bgzf_compress(const char *in, size_t n, int level, int eof, int n_threads, size_t *out_len) {
+    const size_t B = 0xff00;
+    const size_t nb = (n + B - 1) / B;
+    std::vector<std::vector<uint8_t>> blocks(nb);
+    unsigned nt = n_threads > 0 ? static_cast<unsigned>(n_threads) : std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min<unsigned>(nt, static_cast<unsigned>(nb ? nb : 1)));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            for (size_t i = t; i < nb; i += nt) {
+                blocks[i].resize(65536);
+                const size_t off = i * B, len = std::min(B, n - off);
+                blocks[i].resize(bgzf_block(reinterpret_cast<const uint8_t *>(in) + off, len, level, blocks[i].data()));
+            }
+        });
+    for (auto &x : th) x.join();
+    static const uint8_t kEof[28] = {0x1f, 0x8b, 8, 4, 0, 0, 0, 0, 0, 0xff, 6, 0, 0x42, 0x43,
+                                     2, 0, 0x1b, 0, 3, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    size_t total = eof ? 28 : 0;
+    for (auto &b : blocks) total += b.size();
+    char *o = static_cast<char *>(malloc(total ? total : 1));
+    size_t off = 0;
+    for (auto &b : blocks) {
+        memcpy(o + off, b.data(), b.size());
+        off += b.size();
+    }
+    if (eof) memcpy(o + off, kEof, 28);
+    *out_len = total;
+    return o;
+}
+
+}  // extern "C"

@@ -58,6 +58,16 @@ class BatchStats(C.Structure):
                 ('device_ms', C.c_double)]
 
 
+class Slice(C.Structure):
+    _fields_ = [('vcf_id', C.c_uint32), ('_pad', C.c_uint32), ('virtual_start', C.c_uint64),
+                ('virtual_end', C.c_uint64)]
+
+
+class SliceStats(C.Structure):
+    _fields_ = [('error', C.c_int32), ('_pad', C.c_int32), ('num_variants', C.c_uint64),
+                ('num_calls', C.c_uint64), ('records', C.c_uint64)]
+
+
 # every exported symbol of include/sbeacon.h: name -> (restype, argtypes)
 P = C.c_void_p
 SIGNATURES = {
@@ -88,6 +98,9 @@ SIGNATURES = {
     'sb_batch_get_stats': (C.c_int, [P, C.POINTER(BatchStats)]),
     'sb_batch_fetch': (C.c_int, [P, C.POINTER(P)]),
     'sb_batch_free': (None, [P]),
+    'sb_summarise_slices': (C.c_int, [P, C.POINTER(Slice), C.c_size_t, C.POINTER(SliceStats),
+                                      C.POINTER(C.c_double)]),
+    'sb_store_vcf_stream': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

@@ -19,7 +19,7 @@ import os
 from typing import Iterable
 
 from . import _lib
-from ._lib import BatchStats, BuildOpts, Query, ResultView, StoreInfo, check, lib
+from ._lib import BatchStats, BuildOpts, Query, ResultView, Slice, SliceStats, StoreInfo, check, lib
 from .payloads import PerformQueryResponse
 
 QERR = {1: UnboundLocalError, 2: IndexError, 3: ValueError, 4: AttributeError, 9: NotImplementedError}
@@ -112,6 +112,35 @@ class Store:
             check(lib().sb_store_sample_name(self._h, vid, i, C.byref(p), C.byref(ln)))
             out.append(C.string_at(p, ln.value).decode())
         return out
+
+    # ---------------------------------------------------------------- summarise
+    def summarise_slices(self, slices, *, with_timing=False):
+        """slices: iterable of (vcf_location, virtual_start, virtual_end).
+        Returns one RegionStats dict {numVariants, numCalls, records} per
+        slice (or the exception for a slice the engine cannot represent)."""
+        slices = list(slices)
+        n = len(slices)
+        arr = (Slice * max(n, 1))()
+        for i, (loc, vs, ve) in enumerate(slices):
+            arr[i].vcf_id = self.vcf_id(loc)
+            arr[i].virtual_start = int(vs)
+            arr[i].virtual_end = int(ve)
+        out = (SliceStats * max(n, 1))()
+        ms = C.c_double()
+        check(lib().sb_summarise_slices(self._h, arr, n, out, C.byref(ms)))
+        res = []
+        for i in range(n):
+            if out[i].error:
+                res.append(NotImplementedError(f'slice {slices[i]} is not record-aligned / not representable'))
+            else:
+                res.append({'numVariants': out[i].num_variants, 'numCalls': out[i].num_calls,
+                             'records': out[i].records})
+        return (res, ms.value) if with_timing else res
+
+    def vcf_stream(self, location):
+        nb, ln = C.c_uint64(), C.c_uint64()
+        check(lib().sb_store_vcf_stream(self._h, self.vcf_id(location), C.byref(nb), C.byref(ln)))
+        return {'blocks': nb.value, 'stream_len': ln.value}
 
     # ---------------------------------------------------------------- query
     def make_queries(self, payloads: list[dict], *, strict_variant_type: bool = False):

@@ -40,8 +40,34 @@ def synth_lib():
         L.sbs_records.restype = C.c_void_p
         L.sbs_records.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_size_t)]
         L.sbs_free_text.argtypes = [C.c_void_p]
+        L.sbs_bgzf_compress.restype = C.c_void_p
+        L.sbs_bgzf_compress.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t)]
         _syn = L
     return _syn
+
+
+def bgzf_compress(data: bytes, *, level=6, eof=True, threads=0) -> bytes:
+    """bgzip-compatible BGZF (0xff00-byte blocks + EOF block)."""
+    n = C.c_size_t()
+    p = synth_lib().sbs_bgzf_compress(data, len(data), level, 1 if eof else 0, threads, C.byref(n))
+    out = C.string_at(p, n.value)
+    synth_lib().sbs_free_text(p)
+    return out
+
+
+def write_bgzf(path, chunks, *, level=6, threads=0):
+    """Stream text chunks into one BGZF file (block boundaries fall every
+    0xff00 bytes of the concatenated text, as bgzip places them)."""
+    pending = b''
+    with open(path, 'wb') as f:
+        for c in chunks:
+            pending += c
+            cut = len(pending) - len(pending) % 0xff00
+            if cut:
+                f.write(bgzf_compress(pending[:cut], level=level, eof=False, threads=threads))
+                pending = pending[cut:]
+        f.write(bgzf_compress(pending, level=level, eof=True, threads=threads))
+    return path
 
 
 CHR22_SPAN = (16050075, 51244237)

@@ -1,0 +1,119 @@
+"""Device summariseSlice vs the C restatement (oracle/summarise_oracle.c) on
+BGZF files: random record-aligned slices (both spellings of a block-boundary
+virtual offset), including a fixture built so the reference's skip heuristic
+swallows records."""
+import os
+import random
+
+import pytest
+
+from bgzf_util import blocks, random_slices, record_starts, text
+from conftest import FIXTURES
+from payload_gen import random_payload, read_records
+
+pytestmark = pytest.mark.gpu
+
+
+def skip_quirk_vcf(n=3000, seed=5):
+    """Records whose INFO tails vary a lot: a slice that starts on a long-tail
+    record gets a large skipSize and swallows the records after short ones."""
+    rng = random.Random(seed)
+    out = [b'##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tA\tB\tC\n']
+    pos = 1000
+    for i in range(n):
+        pos += rng.randrange(0, 40)
+        k = rng.choice([0, 0, 0, 1, 2, 40])
+        tail = ''.join(f';T{j}={rng.randrange(100)}' for j in range(k))
+        info = f'AC={rng.randrange(0, 9)};AN={rng.randrange(6, 7)}{tail}'
+        if rng.random() < 0.1:
+            info = f'AN={rng.randrange(10)};AC=1,{rng.randrange(3)}'
+        alt = 'G' if rng.random() < 0.9 else 'G,T'
+        gts = '\t'.join(rng.choice(['0|0', '0|1', '1|1', '0/1']) for _ in range(3))
+        out.append(f'7\t{pos}\t.\tA\t{alt}\t.\tPASS\t{info}\tGT\t{gts}\n'.encode())
+    return b''.join(out)
+
+
+@pytest.fixture(scope='module')
+def bgzf_files(tmp_path_factory):
+    from sbeacon.workload import SyntheticVcf, write_bgzf
+    d = tmp_path_factory.mktemp('bgzf')
+    files = {}
+    for name in ('tiny22', 'quirk22'):
+        files[name] = write_bgzf(str(d / f'{name}.vcf.gz'), [open(os.path.join(FIXTURES, name + '.vcf'), 'rb').read()])
+    files['skip7'] = write_bgzf(str(d / 'skip7.vcf.gz'), [skip_quirk_vcf()])
+    g = SyntheticVcf(n_records=30000, n_samples=24, seed=99)
+    files['synth'] = write_bgzf(str(d / 'synth.vcf.gz'), g.chunks(threads=4), threads=4)
+    return files
+
+
+@pytest.fixture(scope='module')
+def bgzf_store(bgzf_files):
+    from sbeacon.engine import Store
+    return Store.build([(n + '.vcf.gz', p) for n, p in bgzf_files.items()], device=0)
+
+
+@pytest.mark.parametrize('name', ['tiny22', 'quirk22', 'skip7', 'synth'])
+def test_summarise_slices_vs_oracle(bgzf_files, bgzf_store, name):
+    from oracle.oracle import OracleBgzf
+    path = bgzf_files[name]
+    o = OracleBgzf(path)
+    blk, txt = blocks(path), text(path)
+    rng = random.Random(len(name))
+    slices = random_slices(txt, blk, rng, 300, max_records=2000)
+    starts = record_starts(txt)
+    slices.append(((blk[0][0] << 16) | starts[0], blk[-1][0] << 16))  # whole file
+    got = bgzf_store.summarise_slices([(name + '.vcf.gz', vs, ve) for vs, ve in slices])
+    n_skipped = 0
+    for (vs, ve), g in zip(slices, got):
+        e = o.summarise_slice(vs, ve)
+        assert g == e, (name, vs, ve, g, e)
+        u0, u1 = o.voff_to_u(vs), o.voff_to_u(ve)
+        n_recs = sum(1 for s in starts if u0 <= s < u1)
+        n_skipped += n_recs - e['records'] if n_recs else 0
+    if name == 'skip7':
+        assert n_skipped > 0  # the fixture really exercises the skip heuristic
+
+
+def test_summarise_rejects_unaligned_slices(bgzf_files, bgzf_store):
+    path = bgzf_files['tiny22']
+    blk, txt = blocks(path), text(path)
+    starts = record_starts(txt)
+    from bgzf_util import voff
+    mid = voff(blk, starts[10] + 3)
+    got = bgzf_store.summarise_slices([('tiny22.vcf.gz', mid, voff(blk, starts[20]))])
+    assert isinstance(got[0], NotImplementedError)
+
+
+def test_bgzf_ingest_matches_text_ingest_for_queries(bgzf_files, bgzf_store):
+    """The same VCF ingested from BGZF answers performQuery identically."""
+    from oracle.oracle import OracleVcf
+    plain = os.path.join(FIXTURES, 'tiny22.vcf')
+    orc = OracleVcf(plain)
+    recs, names = read_records(plain)
+    rng = random.Random(77)
+    payloads = [random_payload(rng, recs, names, 'tiny22.vcf.gz') for _ in range(800)]
+    got = bgzf_store.query(payloads).responses()
+    exp = orc.perform_query_batch(payloads, patched=True)
+    for p, g, e in zip(payloads, got, exp):
+        if isinstance(e, type):
+            assert isinstance(g, e), p
+        else:
+            d = g.dump()
+            d['sample_indices'] = sorted(d['sample_indices'])
+            e['sample_indices'] = sorted(e['sample_indices'])
+            assert d == e, p
+
+
+def test_summarise_handler(bgzf_files, bgzf_store):
+    import json
+
+    from sbeacon import engine, summarise
+    engine.registry.register(bgzf_store)
+    path = bgzf_files['synth']
+    blk, txt = blocks(path), text(path)
+    starts = record_starts(txt)
+    msg = {'location': 'synth.vcf.gz', 'virtual_start': (blk[0][0] << 16) | starts[0],
+           'virtual_end': blk[-1][0] << 16}
+    r = summarise.lambda_handler({'Records': [{'Sns': {'Message': json.dumps(msg)}}]})
+    assert r['numVariants'] >= 30000 and r['numCalls'] == 48 * 30000
+    engine.registry.clear()
