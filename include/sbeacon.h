@@ -180,6 +180,37 @@ int sb_summarise_slices(sb_store *s, const sb_slice *slices, size_t n, sb_slice_
 /* BGZF block count and text-stream length of an ingested VCF */
 int sb_store_vcf_stream(const sb_store *s, uint32_t vcf_id, uint64_t *n_blocks, uint64_t *stream_len);
 
+/* ---- duplicateVariantSearch -------------------------------------------------
+ * One sb_dedup_job = one duplicateVariantSearch SNS message {"rangeStart",
+ * "rangeEnd", "contig", "targetFilepaths", "dataset"} (lambda/
+ * duplicateVariantSearch/source/main.cpp:31-43) with its region files named
+ * by the VCFs they summarise.  unique = |{ to_string(pos) + ref'_alt' }| over
+ * every region-file entry (record x ALT, write_data_to_s3.h:150-228) of those
+ * VCFs on `contig` with range_start <= pos <= range_end
+ * (duplicateVariantSearch.cpp:31-84, readVcfData.cpp:3-38; see DESIGN.md for
+ * the reference's end-of-file range quirk this does not reproduce).  A job
+ * over VCFs of several datasets is a cross-dataset union count.  Jobs whose
+ * range holds a record the reference's summariseSlice would throw on
+ * (compressSeq of an IUPAC code, write_data_to_s3.h:103-134) get
+ * status SB_QERR_UNSUPPORTED. */
+typedef struct {
+    const uint32_t *vcf_ids;
+    uint32_t n_vcf;
+    uint32_t contig_len;
+    const char *contig; /* CHROM text, length-delimited */
+    uint64_t range_start, range_end; /* inclusive */
+} sb_dedup_job;
+
+typedef struct {
+    uint64_t keys;        /* keys gathered and sorted (all jobs) */
+    uint64_t collisions;  /* equal 64-bit words holding different strings (recounted on the host) */
+    double device_ms;     /* HIP-event time: gather + radix sort + unique */
+} sb_dedup_stats;
+
+/* unique[i] / status[i] per job; stats optional */
+int sb_dedup_count(sb_store *s, const sb_dedup_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,
+                   sb_dedup_stats *stats);
+
 /* ---- device-resident batch (benchmarks / fused pipelines) ----------------
  * Upload a batch once, then launch the query kernels repeatedly on the
  * store's stream with inputs already resident in HBM. */

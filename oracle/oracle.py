@@ -229,3 +229,24 @@ class OracleBgzf:
         if rc:
             raise ValueError(f'unsupported slice (oracle rc={rc})')
         return {'numVariants': nv.value, 'numCalls': nc.value, 'records': rec.value}
+
+
+# ---------------------------------------------------- duplicateVariantSearch
+def dedup_count(texts, contig: str, range_start: int, range_end: int):
+    """|{to_string(pos) + ref'_alt'}| over the region entries of `contig` in
+    the VCF texts with range_start <= pos <= range_end
+    (duplicateVariantSearch.cpp:31-84; intended range semantics).
+    Raises ValueError where the reference's summariseSlice throws."""
+    L = lib()
+    if not hasattr(L, '_dedup_ready'):
+        L.orc_dedup_count.argtypes = [C.POINTER(C.c_char_p), C.POINTER(C.c_int64), C.c_int, C.c_char_p, C.c_int64,
+                                      C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64)]
+        L._dedup_ready = True
+    texts = [t if isinstance(t, bytes) else t.encode() for t in texts]
+    arr = (C.c_char_p * max(len(texts), 1))(*texts)
+    lens = (C.c_int64 * max(len(texts), 1))(*[len(t) for t in texts])
+    cb = contig.encode()
+    u = C.c_uint64()
+    if L.orc_dedup_count(arr, lens, len(texts), cb, len(cb), range_start, range_end, C.byref(u)):
+        raise ValueError('a record in range makes summariseSlice throw (compressSeq)')
+    return u.value

@@ -1,7 +1,9 @@
 /*
- * summarise_oracle.c — CPU restatement of the reference summariseSlice counter.
+ * summarise_oracle.c — CPU restatement of the reference summariseSlice counter
+ * and of duplicateVariantSearch's unique count over the region entries
+ * summariseSlice writes.
  *
- * TEST INFRASTRUCTURE ONLY (checker for the device summarise path).
+ * TEST INFRASTRUCTURE ONLY (checker for the device summarise / dedup paths).
  *
  * Restates lambda/summariseSlice/source/main.cpp:195-245 (getRegionStats),
  * :52-109 (addCounts), write_data_to_s3.h:150-228 (recordHeader's reader
@@ -213,9 +215,110 @@ static int atoui64_len(const char *str, uint8_t len, uint64_t *out) {
     return 0;
 }
 
-/* write_data_to_s3.h:150-228 recordHeader: reader movement only */
-static void record_header(rd_t *r, int *contig_set) {
-    int loop_pos = 0;
+/* generalutils.hpp:19-36 sequenceToBinary (-1: std::map::at throws) */
+static int seq_code(char c) {
+    switch (c) {
+        case 'A': case 'a': return 1;
+        case 'C': case 'c': return 2;
+        case 'G': case 'g': return 3;
+        case 'T': case 't': return 4;
+        case 'N': case 'n': return 5;
+        case '*': return 6;
+        case '.': return 7;
+        default: return -1;
+    }
+}
+
+/* write_data_to_s3.h:103-134 compressSeq into out (returns length, -1 where
+ * the reference throws).  Each packed byte is appended once (the reference's
+ * append((char *)&contigBin) reads a C string past the byte: UB) */
+static int64_t compress_seq(const char *s, int64_t n, char *out) {
+    if (n == 1) {
+        const int v = seq_code(s[0]);
+        if (v < 0) return -1;
+        out[0] = (char)v;
+        return 1;
+    }
+    if (s[0] == '<' && s[n - 1] == '>') {
+        memcpy(out, s + 1, (size_t)(n - 2));
+        return n - 2;
+    }
+    int64_t k = 0;
+    for (int64_t i = 0; i < n; i += 2) {
+        int v = seq_code(s[i]);
+        if (v < 0) return -1;
+        if (i + 1 < n) {
+            const int w = seq_code(s[i + 1]);
+            if (w < 0) return -1;
+            v = (v << 4) | w;
+        }
+        out[k++] = (char)v;
+    }
+    return k;
+}
+
+/* region-file entries {pos, ref', alt'} as key strings to_string(pos) +
+ * ref' + '_' + alt' (readVcfData.cpp:23) */
+typedef struct {
+    char **s;
+    int64_t *len;
+    uint64_t *pos;
+    int64_t n, cap;
+} keys_t;
+
+static void keys_push(keys_t *k, uint64_t pos, const char *ref, int64_t rl, const char *alt, int64_t al) {
+    if (k->n == k->cap) {
+        k->cap = k->cap ? 2 * k->cap : 1024;
+        k->s = (char **)realloc(k->s, sizeof(char *) * (size_t)k->cap);
+        k->len = (int64_t *)realloc(k->len, sizeof(int64_t) * (size_t)k->cap);
+        k->pos = (uint64_t *)realloc(k->pos, sizeof(uint64_t) * (size_t)k->cap);
+    }
+    char d[24];
+    const int nd = snprintf(d, sizeof d, "%llu", (unsigned long long)pos);
+    const int64_t L = nd + rl + 1 + al;
+    char *p = (char *)malloc((size_t)L);
+    memcpy(p, d, (size_t)nd);
+    memcpy(p + nd, ref, (size_t)rl);
+    p[nd + rl] = '_';
+    memcpy(p + nd + rl + 1, alt, (size_t)al);
+    k->s[k->n] = p;
+    k->len[k->n] = L;
+    k->pos[k->n] = pos;
+    k->n++;
+}
+
+/* move entry i of src to the end of dst */
+static void keys_move(keys_t *dst, keys_t *src, int64_t i) {
+    if (dst->n == dst->cap) {
+        dst->cap = dst->cap ? 2 * dst->cap : 1024;
+        dst->s = (char **)realloc(dst->s, sizeof(char *) * (size_t)dst->cap);
+        dst->len = (int64_t *)realloc(dst->len, sizeof(int64_t) * (size_t)dst->cap);
+        dst->pos = (uint64_t *)realloc(dst->pos, sizeof(uint64_t) * (size_t)dst->cap);
+    }
+    dst->s[dst->n] = src->s[i];
+    dst->len[dst->n] = src->len[i];
+    dst->pos[dst->n] = src->pos[i];
+    dst->n++;
+    src->s[i] = NULL;
+}
+
+static void keys_free(keys_t *k) {
+    for (int64_t i = 0; i < k->n; ++i) free(k->s[i]);
+    free(k->s);
+    free(k->len);
+    free(k->pos);
+}
+
+/* write_data_to_s3.h:150-228 recordHeader: reader movement, the POS parse
+ * (fast_atoi, generalutils.hpp:38-45), compressSeq of REF and each ALT part
+ * and the region entries pushed (into keys when non-NULL).  Returns -1 where
+ * the reference throws (compressSeq on a character outside the table).  *pos
+ * receives the record's POS. */
+static int record_header(rd_t *r, int *contig_set, keys_t *keys, uint64_t *pos_out) {
+    int loop_pos = 0, bad = 0;
+    uint64_t pos = 0;
+    char ref[65536], alt[65536];
+    int64_t rl = 0;
     if (*contig_set) {
         skip_past(r, '\t', 1);
         loop_pos = 1;
@@ -231,18 +334,30 @@ static void record_header(rd_t *r, int *contig_set) {
                     *contig_set = 1;
                     break;
                 case 2:
+                    pos = 0;
+                    for (int64_t i = 0; i < fl; ++i) pos = pos * 10 + (uint64_t)(int64_t)(f[i] - '0');
                     skip_past(r, '\t', 1);
                     loop_pos++;
                     break;
-                case 5:
+                case 4:
+                    rl = fl <= 65535 ? compress_seq(f, fl, ref) : -1;
+                    if (rl < 0) bad = 1;
+                    break;
+                case 5: {
+                    const int64_t al = fl <= 65535 ? compress_seq(f, fl, alt) : -1;
+                    if (al < 0) bad = 1;
+                    if (!bad && keys) keys_push(keys, pos, ref, rl, alt, al);
                     if (last == ',') loop_pos--;
                     break;
+                }
                 default:
                     break;
             }
         }
     } while (loop_pos <= 4);
     skip_past(r, '\t', 2);
+    if (pos_out) *pos_out = pos;
+    return bad ? -1 : 0;
 }
 
 /* main.cpp:52-109 addCounts */
@@ -276,11 +391,11 @@ int orc_region_stats(const char *s, int64_t n, uint64_t *num_variants, uint64_t 
     rd_t r = {s, n, 0};
     uint64_t nv = 0, nc = 0, recs = n > 0; /* `records` is diagnostic only (main.cpp:230) */
     int contig_set = 0;
-    record_header(&r, &contig_set);
+    if (record_header(&r, &contig_set, NULL, NULL)) return -1;
     if (add_counts(&r, &nv, &nc)) return -1;
     const uint64_t skip = 2 * skip_count(&r, '\n');
     while (r.pos < r.n) { /* keepReading() */
-        record_header(&r, &contig_set);
+        if (record_header(&r, &contig_set, NULL, NULL)) return -1;
         if (add_counts(&r, &nv, &nc)) return -1;
         r.pos += (int64_t)skip; /* seek(skipSize) */
         skip_past(&r, '\n', 1);
@@ -299,4 +414,66 @@ int orc_summarise_slice(void *h, uint64_t vstart, uint64_t vend, uint64_t *num_v
     if (orc_bgzf_voff_to_u(b, vstart, &u0) || orc_bgzf_voff_to_u(b, vend, &u1)) return -2;
     if (u1 < u0) u1 = u0;
     return orc_region_stats((const char *)b->u + u0, (int64_t)(u1 - u0), num_variants, num_calls, records);
+}
+
+/* ------------------------------------------------ duplicateVariantSearch */
+static int cmp_key(const void *a, const void *b) {
+    const char *const *x = (const char *const *)a, *const *y = (const char *const *)b;
+    const int64_t lx = *(const int64_t *)(*x - 8), ly = *(const int64_t *)(*y - 8);
+    const int64_t m = lx < ly ? lx : ly;
+    const int c = memcmp(*x, *y, (size_t)m);
+    if (c) return c;
+    return lx < ly ? -1 : lx > ly;
+}
+
+/* duplicateVariantSearch.cpp:31-84 + readVcfData.cpp:3-38 (intended range
+ * semantics: every entry with range_start <= pos <= range_end) over the
+ * region entries summariseSlice would write for the records of `contig` in
+ * each VCF text (write_data_to_s3.h:150-228).  Returns -1 when a record in
+ * the range makes the reference's summariseSlice throw. */
+int orc_dedup_count(const char *const *texts, const int64_t *lens, int nvcf, const char *contig, int64_t clen,
+                    uint64_t rs, uint64_t re, uint64_t *unique) {
+    keys_t k = {0};
+    int rc = 0;
+    for (int v = 0; v < nvcf && !rc; ++v) {
+        const char *t = texts[v];
+        const int64_t n = lens[v];
+        int64_t p = 0;
+        while (p < n) {
+            const char *nl = (const char *)memchr(t + p, '\n', (size_t)(n - p));
+            const int64_t e = nl ? (int64_t)(nl - t) + 1 : n;
+            if (t[p] != '#' && e - p > clen && !memcmp(t + p, contig, (size_t)clen) && t[p + clen] == '\t') {
+                rd_t r = {t + p, e - p, 0};
+                int contig_set = 1;
+                keys_t one = {0};
+                uint64_t pos = 0;
+                const int bad = record_header(&r, &contig_set, &one, &pos);
+                if (pos >= rs && pos <= re) {
+                    if (bad) rc = -1;
+                    for (int64_t i = 0; i < one.n && !bad; ++i) keys_move(&k, &one, i);
+                }
+                keys_free(&one);
+            }
+            p = e;
+        }
+    }
+    if (!rc) {
+        /* sort (length-prefixed copies) and count distinct */
+        char **arr = (char **)malloc(sizeof(char *) * (size_t)(k.n ? k.n : 1));
+        for (int64_t i = 0; i < k.n; ++i) {
+            char *c = (char *)malloc((size_t)k.len[i] + 8);
+            memcpy(c, &k.len[i], 8);
+            memcpy(c + 8, k.s[i], (size_t)k.len[i]);
+            arr[i] = c + 8;
+        }
+        qsort(arr, (size_t)k.n, sizeof(char *), cmp_key);
+        uint64_t u = 0;
+        for (int64_t i = 0; i < k.n; ++i)
+            if (i == 0 || cmp_key(&arr[i - 1], &arr[i])) u++;
+        for (int64_t i = 0; i < k.n; ++i) free(arr[i] - 8);
+        free(arr);
+        *unique = u;
+    }
+    keys_free(&k);
+    return rc;
 }

@@ -224,13 +224,17 @@ void upload_store(sb_builder &b, sb_store &s) {
     std::vector<uint64_t> start;
     std::vector<SumHot> sum;
     std::vector<uint32_t> cur, dcount;
-    uint64_t nr = 0, nx = 0, np = 0;
+    std::vector<uint32_t> dk_pos, dk_lo, dk_bad;
+    std::vector<uint64_t> dk_hash, dk_tail;
+    std::vector<uint8_t> dk_blob;
+    uint64_t nr = 0, nx = 0, np = 0, nk = 0;
     for (auto &v : b.vcfs) {
         nr += v.c.pos.size();
         nx += v.c.x_key.size();
+        nk += v.c.dk_hash.size();
         np += v.c.planes0.size() + v.c.planesx.size();
     }
-    if (nr >= 0xfffffff0ull || nx >= 0xfffffff0ull)
+    if (nr >= 0xfffffff0ull || nx >= 0xfffffff0ull || nk >= 0xfffffff0ull)
         throw Error(SB_EINVAL, "store exceeds 2^32 records per device; shard it across devices");
     rec.reserve(nr);
     pos.reserve(nr);
@@ -273,6 +277,16 @@ void upload_store(sb_builder &b, sb_store &s) {
         for (size_t i = 0; i < c.x_off.size(); ++i) x_off.push_back(c.x_off[i] + blob_base);
         blob.insert(blob.end(), c.blob.begin(), c.blob.end());
         fb.insert(fb.end(), c.fb.begin(), c.fb.end());
+        {
+            const uint32_t kbase = static_cast<uint32_t>(dk_hash.size());
+            const uint64_t kblob = dk_blob.size();
+            for (size_t i = 0; i < n; ++i) dk_lo.push_back(c.dk_lo[i] + kbase);
+            dk_pos.insert(dk_pos.end(), c.dk_pos.begin(), c.dk_pos.end());
+            dk_hash.insert(dk_hash.end(), c.dk_hash.begin(), c.dk_hash.end());
+            for (uint64_t t : c.dk_tail) dk_tail.push_back((t & kTailBlob) ? t + kblob : t);
+            dk_blob.insert(dk_blob.end(), c.dk_blob.begin(), c.dk_blob.end());
+            for (uint32_t r : c.dk_bad) dk_bad.push_back(r + rec_base);
+        }
         for (auto &sg : v.segments) {
             sg.lo += rec_base;
             sg.hi += rec_base;
@@ -281,6 +295,7 @@ void upload_store(sb_builder &b, sb_store &s) {
         c = VcfCols();  // release the per-vcf copy
     }
     x_lo.push_back(static_cast<uint32_t>(x_key.size()));
+    dk_lo.push_back(static_cast<uint32_t>(dk_hash.size()));
     for (auto &v : b.vcfs) {
         v.buckets.resize(v.segments.size());
         for (size_t i = 0; i < v.segments.size(); ++i) build_buckets(pos, v.segments[i], v.buckets[i], bucket);
@@ -310,7 +325,17 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.ds.start = dev_upload(s, start);
     s.ds.cur = dev_upload(s, cur);
     s.ds.dcount = dev_upload(s, dcount);
+    s.dk.hash = dev_upload(s, dk_hash);
+    s.dk.tail = dev_upload(s, dk_tail);
+    s.dk.pos = dev_upload(s, dk_pos);
+    s.dk.blob = dev_upload(s, dk_blob);
+    s.n_keys = dk_hash.size();
     HIP_OK(hipStreamSynchronize(s.stream));
+    s.h_dk_pos = std::move(dk_pos);
+    s.h_dk_lo = std::move(dk_lo);
+    s.h_dk_bad = std::move(dk_bad);
+    s.h_dk_tail = std::move(dk_tail);
+    s.h_dk_blob = std::move(dk_blob);
     s.h_start = std::move(start);
     // host copies for output planning and result formatting
     s.h_pos = std::move(pos);
@@ -736,6 +761,140 @@ void summarise(sb_store &s, const sb_slice *sl, size_t n, sb_slice_stats *out, d
     }
 }
 
+// the key string of store key k: decimal(pos) ++ ref'_alt'
+std::string key_string(const sb_store &s, uint32_t k) {
+    std::string out = std::to_string(s.h_dk_pos[k]);
+    const uint64_t t = s.h_dk_tail[k];
+    if (t & kTailBlob) {
+        const uint64_t off = t & ((1ull << 40) - 1), len = (t >> 40) & 0xffff;
+        out.append(reinterpret_cast<const char *>(s.h_dk_blob.data() + off), len);
+    } else {
+        for (uint64_t j = 0, len = t >> 56; j < len; ++j) out.push_back(static_cast<char>((t >> (8 * j)) & 0xff));
+    }
+    return out;
+}
+
+void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, int32_t *status,
+           sb_dedup_stats *stats) {
+    if (nj > (1u << 20)) throw Error(SB_EINVAL, "more than 2^20 dedup jobs in one call");
+    std::vector<KSeg> segs;
+    uint64_t n = 0;
+    for (size_t j = 0; j < nj; ++j) {
+        const sb_dedup_job &J = jobs[j];
+        status[j] = 0;
+        unique[j] = 0;
+        if ((!J.vcf_ids && J.n_vcf) || (!J.contig && J.contig_len)) throw Error(SB_EINVAL, "dedup job: NULL array");
+        const std::string contig(J.contig ? J.contig : "", J.contig_len);
+        std::vector<uint32_t> seen;
+        const size_t seg0 = segs.size();
+        for (uint32_t t = 0; t < J.n_vcf; ++t) {
+            const uint32_t id = J.vcf_ids[t];
+            if (id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "dedup job " + std::to_string(j) + ": unknown vcf id");
+            if (std::find(seen.begin(), seen.end(), id) != seen.end()) continue;  // a file listed twice adds nothing
+            seen.push_back(id);
+            const VcfData &v = s.vcfs[id];
+            auto it = v.seg_index.find(contig);
+            if (it == v.seg_index.end() || J.range_start > J.range_end || J.range_start > 0xffffffffull) continue;
+            const Segment &sg = v.segments[it->second];
+            const uint32_t rs = static_cast<uint32_t>(J.range_start);
+            const uint32_t re = static_cast<uint32_t>(std::min<uint64_t>(J.range_end, 0xffffffffull));
+            // records the reference's summariseSlice throws on, inside the range
+            auto b0 = std::lower_bound(s.h_dk_bad.begin(), s.h_dk_bad.end(), sg.lo);
+            for (auto b = b0; b != s.h_dk_bad.end() && *b < sg.hi; ++b)
+                if (s.h_pos[*b] >= rs && s.h_pos[*b] <= re) status[j] = SB_QERR_UNSUPPORTED;
+            const auto kb = s.h_dk_pos.begin();
+            const uint32_t klo = s.h_dk_lo[sg.lo], khi = s.h_dk_lo[sg.hi];
+            const uint32_t a = static_cast<uint32_t>(std::lower_bound(kb + klo, kb + khi, rs) - kb);
+            const uint32_t e = static_cast<uint32_t>(std::upper_bound(kb + klo, kb + khi, re) - kb);
+            if (e > a) {
+                segs.push_back(KSeg{a, n, e - a, static_cast<uint32_t>(j)});
+                n += e - a;
+            }
+        }
+        if (status[j]) {  // drop the job's keys
+            for (size_t g = seg0; g < segs.size(); ++g) n -= segs[g].n;
+            segs.resize(seg0);
+        }
+    }
+    if (n >= 0xffffffffull) throw Error(SB_EINVAL, "dedup batch exceeds 2^32 keys; split it");
+    uint32_t job_bits = 0;
+    while ((1ull << job_bits) < nj) ++job_bits;
+    uint64_t mask = ~0ull;
+    if (const char *e = getenv("SBEACON_DEDUP_HASH_BITS")) {  // test hook: force collisions
+        const int b = atoi(e);
+        if (b > 0 && b < 64) mask = (1ull << b) - 1;
+    }
+    HIP_OK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    DevMem dseg, k0, v0, k1, v1, hist, bsum, counts, coll, ncoll;
+    dseg.alloc(segs.size() * sizeof(KSeg));
+    k0.alloc(n * 8);
+    v0.alloc(n * 4);
+    k1.alloc(n * 8);
+    v1.alloc(n * 4);
+    hist.alloc(radix_hist_words(n) * 4);
+    bsum.alloc(radix_bsum_words(n) * 4);
+    counts.alloc(std::max<size_t>(nj, 1) * 8);
+    coll.alloc(n * 4);
+    ncoll.alloc(4);
+    if (!segs.empty()) HIP_OK(hipMemcpyAsync(dseg.p, segs.data(), segs.size() * sizeof(KSeg), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(counts.p, 0, counts.bytes, st));
+    HIP_OK(hipMemsetAsync(ncoll.p, 0, 4, st));
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, st));
+    launch_dedup_gather(s.dk, dseg.as<KSeg>(), static_cast<uint32_t>(segs.size()), n, job_bits, mask,
+                        k0.as<uint64_t>(), v0.as<uint32_t>(), st);
+    launch_radix_sort(k0.as<uint64_t>(), v0.as<uint32_t>(), k1.as<uint64_t>(), v1.as<uint32_t>(), n,
+                      hist.as<uint32_t>(), bsum.as<uint32_t>(), st);
+    launch_dedup_unique(k0.as<uint64_t>(), v0.as<uint32_t>(), n, s.dk, job_bits, counts.as<unsigned long long>(),
+                        coll.as<uint32_t>(), ncoll.as<uint32_t>(), st);
+    HIP_OK(hipEventRecord(e1, st));
+    HIP_OK(hipGetLastError());
+    std::vector<uint64_t> cnt(std::max<size_t>(nj, 1));
+    uint32_t nc = 0;
+    HIP_OK(hipMemcpyAsync(cnt.data(), counts.p, cnt.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(&nc, ncoll.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (nc) {
+        // exact recount of every group holding a collision: the device counted
+        // 1 + (adjacent string changes) for it; replace that by |distinct|
+        std::vector<uint64_t> hk(n);
+        std::vector<uint32_t> hv(n), ci(nc);
+        HIP_OK(hipMemcpy(hk.data(), k0.p, n * 8, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(hv.data(), v0.p, n * 4, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(ci.data(), coll.p, nc * 4, hipMemcpyDeviceToHost));
+        std::sort(ci.begin(), ci.end());
+        uint64_t done_to = 0;  // groups end before this index
+        for (uint32_t i : ci) {
+            if (i < done_to) continue;
+            uint64_t g0 = i, g1 = i + 1;
+            while (g0 > 0 && hk[g0 - 1] == hk[i]) --g0;
+            while (g1 < n && hk[g1] == hk[i]) ++g1;
+            std::vector<std::string> strs;
+            for (uint64_t x = g0; x < g1; ++x) strs.push_back(key_string(s, hv[x]));
+            uint64_t adjacent = 1;
+            for (size_t x = 1; x < strs.size(); ++x) adjacent += strs[x] != strs[x - 1];
+            std::sort(strs.begin(), strs.end());
+            const uint64_t exact = static_cast<uint64_t>(std::unique(strs.begin(), strs.end()) - strs.begin());
+            const uint32_t job = job_bits ? static_cast<uint32_t>(hk[i] >> (64 - job_bits)) : 0u;
+            cnt[job] = cnt[job] - adjacent + exact;
+            done_to = g1;
+        }
+    }
+    for (size_t j = 0; j < nj; ++j) unique[j] = status[j] ? 0 : cnt[j];
+    if (stats) {
+        stats->keys = n;
+        stats->collisions = nc;
+        stats->device_ms = ms;
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -745,6 +904,15 @@ int sb_summarise_slices(sb_store *s, const sb_slice *slices, size_t n, sb_slice_
         if (!s || (!slices && n) || (!out && n)) throw Error(SB_EINVAL, "NULL argument");
         std::lock_guard<std::mutex> lk(s->mu);
         summarise(*s, slices, n, out, device_ms);
+    });
+}
+
+int sb_dedup_count(sb_store *s, const sb_dedup_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,
+                   sb_dedup_stats *stats) {
+    return guard([&] {
+        if (!s || (n_jobs && (!jobs || !unique || !status))) throw Error(SB_EINVAL, "NULL argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        dedup(*s, jobs, n_jobs, unique, status, stats);
     });
 }
 

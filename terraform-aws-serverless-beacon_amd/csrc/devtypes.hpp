@@ -164,4 +164,29 @@ struct SStore {  // summary columns
     const uint32_t *dcount; // delimiters {\t / | ; :} from the cursor to '\n'
 };
 
+// ---- duplicateVariantSearch (lambda/duplicateVariantSearch/source/
+// duplicateVariantSearch.cpp:31-84, readVcfData.cpp:3-38)
+// A key is the string to_string(pos) + ref' + '_' + alt' (readVcfData.cpp:23,
+// write_data_to_s3.h:30-37) where x' = compressSeq(x).  The store keeps, per
+// key: pos, a 64-bit hash of the whole string and the tail ref'_alt' as one
+// word: bit 63 clear = inline (bytes in bits 0..55, length in bits 56..62,
+// length <= 7); bit 63 set = bytes in the key blob (offset bits 0..39,
+// length bits 40..55).
+inline constexpr uint64_t kTailBlob = 1ull << 63;
+inline constexpr int kTailInlineMax = 7;
+
+struct KStore {
+    const uint64_t *hash;
+    const uint64_t *tail;
+    const uint32_t *pos;
+    const uint8_t *blob;
+};
+
+struct KSeg {  // one run of store keys gathered for a job
+    uint64_t key_lo;   // first store key
+    uint64_t out_lo;   // first output slot
+    uint32_t n;
+    uint32_t job;
+};
+
 }  // namespace sb

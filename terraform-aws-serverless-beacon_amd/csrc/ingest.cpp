@@ -89,10 +89,100 @@ bool atoui64_len(const char *str, uint8_t len, uint64_t *out) {
     return true;
 }
 
-// line = record bytes incl. its '\n' (if any); fills the summary columns
-void summarise_line(const char *line, size_t len, SumHot *sum, uint32_t *cur, uint32_t *dcount) {
+// generalutils.hpp:19-36 sequenceToBinary; -1 where std::map::at throws
+inline int seq_code(char c) {
+    switch (c) {
+        case 'A': case 'a': return 1;
+        case 'C': case 'c': return 2;
+        case 'G': case 'g': return 3;
+        case 'T': case 't': return 4;
+        case 'N': case 'n': return 5;
+        case '*': return 6;
+        case '.': return 7;
+        default: return -1;
+    }
+}
+
+// write_data_to_s3.h:103-134 compressSeq; false where the reference throws.
+// The reference appends each packed byte with append((char *)&contigBin),
+// i.e. as a C string running past the byte (UB); the intended single byte is
+// appended here.
+bool compress_seq(const char *s, size_t n, std::string &out) {
+    if (n == 1) {
+        const int v = seq_code(s[0]);
+        if (v < 0) return false;
+        out.push_back(static_cast<char>(v));
+        return true;
+    }
+    if (s[0] == '<' && s[n - 1] == '>') {
+        out.append(s + 1, n - 2);
+        return true;
+    }
+    for (size_t i = 0; i < n; i += 2) {
+        int v = seq_code(s[i]);
+        if (v < 0) return false;
+        if (i + 1 < n) {
+            const int w = seq_code(s[i + 1]);
+            if (w < 0) return false;
+            v = (v << 4) | w;
+        }
+        out.push_back(static_cast<char>(v));
+    }
+    return true;
+}
+
+// hash of a duplicateVariantSearch key string (FNV-1a + splitmix finaliser)
+uint64_t key_hash(const char *p, size_t n, uint64_t h = 0xcbf29ce484222325ull) {
+    for (size_t i = 0; i < n; ++i) {
+        h ^= static_cast<uint8_t>(p[i]);
+        h *= 0x100000001b3ull;
+    }
+    return h;
+}
+uint64_t key_finish(uint64_t h) {
+    h ^= h >> 30;
+    h *= 0xbf58476d1ce4e5b9ull;
+    h ^= h >> 27;
+    h *= 0x94d049bb133111ebull;
+    return h ^ (h >> 31);
+}
+
+// one region-file entry {pos, ref', alt'} -> key columns
+void push_key(VcfCols &c, uint64_t pos, const std::string &ref, const std::string &alt) {
+    char digits[24];
+    const int nd = snprintf(digits, sizeof digits, "%llu", static_cast<unsigned long long>(pos));
+    uint64_t h = key_hash(digits, static_cast<size_t>(nd));
+    h = key_hash(ref.data(), ref.size(), h);
+    h = key_hash("_", 1, h);
+    h = key_hash(alt.data(), alt.size(), h);
+    const size_t tl = ref.size() + 1 + alt.size();
+    uint64_t tail;
+    if (tl <= static_cast<size_t>(kTailInlineMax)) {
+        tail = static_cast<uint64_t>(tl) << 56;
+        size_t k = 0;
+        for (char ch : ref) tail |= static_cast<uint64_t>(static_cast<uint8_t>(ch)) << (8 * k++);
+        tail |= static_cast<uint64_t>('_') << (8 * k++);
+        for (char ch : alt) tail |= static_cast<uint64_t>(static_cast<uint8_t>(ch)) << (8 * k++);
+    } else {
+        tail = kTailBlob | (static_cast<uint64_t>(tl) << 40) | c.dk_blob.size();
+        c.dk_blob.insert(c.dk_blob.end(), ref.begin(), ref.end());
+        c.dk_blob.push_back('_');
+        c.dk_blob.insert(c.dk_blob.end(), alt.begin(), alt.end());
+    }
+    c.dk_pos.push_back(static_cast<uint32_t>(pos));
+    c.dk_hash.push_back(key_finish(h));
+    c.dk_tail.push_back(tail);
+}
+
+// line = record bytes incl. its '\n' (if any); fills the summary columns and
+// the record's region-file keys (c.dk_*)
+void summarise_line(const char *line, size_t len, uint32_t rec, VcfCols &cols, SumHot *sum, uint32_t *cur,
+                    uint32_t *dcount) {
     LineRd r{line, len, 0, false};
-    bool bad = false;
+    bool bad = false, key_bad = false;
+    uint64_t kpos = 0;
+    std::string ref, alt;
+    std::vector<std::string> alts;
     // recordHeader with the contig already known: skip CHROM, POS field,
     // skip ID, REF, ALT (',' continues ALT), then skip QUAL and FILTER.
     // A first record reads CHROM as a field instead: identical unless CHROM
@@ -107,22 +197,40 @@ void summarise_line(const char *line, size_t len, SumHot *sum, uint32_t *cur, ui
         size_t fs, fl;
         const char last = lr_read_past(r, '\t', ',', &fs, &fl);
         if (last == '\0') break;
-        if (fl >= 1) {
+        if (fl >= 1) {  // empty parts are skipped, as the reference does
             switch (++loop_pos) {
-                case 2:
+                case 2:  // fast_atoi<uint64_t> (generalutils.hpp:38-45)
+                    kpos = 0;
+                    for (size_t i = 0; i < fl; ++i)
+                        kpos = kpos * 10 + static_cast<uint64_t>(static_cast<int64_t>(line[fs + i] - '0'));
                     lr_skip_past(r, '\t', 1);
                     ++loop_pos;
                     break;
+                case 4:
+                    ref.clear();
+                    if (!compress_seq(line + fs, fl, ref)) key_bad = true;
+                    break;
                 case 5:
+                    alt.clear();
+                    if (!compress_seq(line + fs, fl, alt)) key_bad = true;
+                    alts.push_back(alt);
                     if (last == ',') --loop_pos;
                     break;
                 default:
                     break;
             }
-        } else {
-            bad = true;  // empty REF/ALT part: the reference re-reads the next field
         }
     } while (loop_pos <= 4);
+    if (r.off_end || kpos > 0xffffffffull) key_bad = true;
+    for (const auto &a : alts)
+        if (ref.size() + 1 + a.size() > 0xffff) key_bad = true;  // beyond the region file's u16 length
+    if (key_bad) {
+        cols.dk_bad.push_back(rec);  // the reference's summariseSlice throws here
+        bad = true;
+    } else {
+        for (const auto &a : alts) push_key(cols, kpos, ref, a);
+    }
+    cols.dk_lo.push_back(static_cast<uint32_t>(cols.dk_hash.size()));
     lr_skip_past(r, '\t', 2);
     // addCounts
     uint64_t nv = 0, nc = 0;
@@ -174,7 +282,8 @@ struct Parser {
             VcfCols &c = L.c;
             SumHot sh;
             uint32_t cu, dc;
-            summarise_line(p, static_cast<size_t>(full_end - p), &sh, &cu, &dc);
+            summarise_line(p, static_cast<size_t>(full_end - p), static_cast<uint32_t>(c.start.size()), c, &sh, &cu,
+                           &dc);
             c.start.push_back(abs);
             c.sum.push_back(sh);
             c.cur.push_back(cu);
@@ -564,6 +673,17 @@ void merge(sb_builder &b, VcfData &v, Local &L) {
     app(d.sum, s.sum);
     app(d.cur, s.cur);
     app(d.dcount, s.dcount);
+    {
+        const uint32_t k0 = static_cast<uint32_t>(d.dk_hash.size());
+        const uint64_t kb0 = d.dk_blob.size();
+        for (size_t i = 1; i < s.dk_lo.size(); ++i) d.dk_lo.push_back(s.dk_lo[i] + k0);
+        app(d.dk_pos, s.dk_pos);
+        app(d.dk_hash, s.dk_hash);
+        d.dk_tail.reserve(d.dk_tail.size() + s.dk_tail.size());
+        for (uint64_t t : s.dk_tail) d.dk_tail.push_back((t & kTailBlob) ? t + kb0 : t);
+        app(d.dk_blob, s.dk_blob);
+        for (uint32_t r : s.dk_bad) d.dk_bad.push_back(r + rec0);
+    }
     d.any_negative = d.any_negative || s.any_negative;
 }
 

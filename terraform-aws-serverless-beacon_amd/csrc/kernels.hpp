@@ -31,4 +31,20 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, uint64_
 void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,
                     uint64_t *out, hipStream_t s);
 
+// duplicateVariantSearch (dedup_kernels.hip).  gather writes (job | hash,
+// key id) for every key of every segment; mask trims the hash (tests force
+// collisions with it).  The radix sort ping-pongs (k0, v0) <-> (k1, v1) over
+// 8 passes, so the sorted result is back in (k0, v0); hist needs
+// radix_hist_words(n) and bsum radix_bsum_words(n) u32.  unique adds each
+// job's distinct count into counts[job] and lists (into coll, capacity n)
+// every sorted position whose string differs from its equal-word neighbour.
+size_t radix_hist_words(uint64_t n);
+size_t radix_bsum_words(uint64_t n);
+void launch_dedup_gather(const KStore &ks, const KSeg *segs, uint32_t nseg, uint64_t n, uint32_t job_bits,
+                         uint64_t mask, uint64_t *keys, uint32_t *vals, hipStream_t s);
+int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t *hist,
+                      uint32_t *bsum, hipStream_t s);
+void launch_dedup_unique(const uint64_t *keys, const uint32_t *vals, uint64_t n, const KStore &ks, uint32_t job_bits,
+                         unsigned long long *counts, uint32_t *coll, uint32_t *ncoll, hipStream_t s);
+
 }  // namespace sb

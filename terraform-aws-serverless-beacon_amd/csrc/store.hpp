@@ -44,6 +44,12 @@ struct VcfCols {
     std::vector<uint64_t> start;    // absolute line start in the VCF text stream
     std::vector<SumHot> sum;
     std::vector<uint32_t> cur, dcount;
+    // duplicateVariantSearch keys: one per region-file entry (record x ALT,
+    // write_data_to_s3.h:150-228), in record order
+    std::vector<uint32_t> dk_pos, dk_lo{0};  // dk_lo: first key of each record (+ end)
+    std::vector<uint64_t> dk_hash, dk_tail;   // hash of the key string; tail word (devtypes.hpp)
+    std::vector<uint8_t> dk_blob;             // tails longer than 7 bytes
+    std::vector<uint32_t> dk_bad;             // records where compressSeq would throw
 };
 
 struct BucketIndex {  // coarse POS index of one segment
@@ -117,9 +123,15 @@ struct sb_store {
     std::vector<uint64_t> h_ref_off, h_a0_off, h_x_off;
     std::vector<uint8_t> h_blob;
     std::vector<uint64_t> h_start;  // line start in the VCF text stream (summariseSlice planning)
+    // duplicateVariantSearch keys (global indexing): planning + collision fixup
+    uint64_t n_keys = 0;
+    std::vector<uint32_t> h_dk_pos, h_dk_lo, h_dk_bad;
+    std::vector<uint64_t> h_dk_tail;
+    std::vector<uint8_t> h_dk_blob;
     // device image
     sb::DStore d{};
     sb::SStore ds{};
+    sb::KStore dk{};
     std::vector<sb::DeviceBuffer> bufs;
     uint64_t device_bytes = 0;
     ~sb_store();

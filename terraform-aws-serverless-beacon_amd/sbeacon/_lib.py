@@ -68,6 +68,15 @@ class SliceStats(C.Structure):
                 ('num_calls', C.c_uint64), ('records', C.c_uint64)]
 
 
+class DedupJob(C.Structure):
+    _fields_ = [('vcf_ids', C.POINTER(C.c_uint32)), ('n_vcf', C.c_uint32), ('contig_len', C.c_uint32),
+                ('contig', C.c_char_p), ('range_start', C.c_uint64), ('range_end', C.c_uint64)]
+
+
+class DedupStats(C.Structure):
+    _fields_ = [('keys', C.c_uint64), ('collisions', C.c_uint64), ('device_ms', C.c_double)]
+
+
 # every exported symbol of include/sbeacon.h: name -> (restype, argtypes)
 P = C.c_void_p
 SIGNATURES = {
@@ -100,6 +109,8 @@ SIGNATURES = {
     'sb_batch_free': (None, [P]),
     'sb_summarise_slices': (C.c_int, [P, C.POINTER(Slice), C.c_size_t, C.POINTER(SliceStats),
                                       C.POINTER(C.c_double)]),
+    'sb_dedup_count': (C.c_int, [P, C.POINTER(DedupJob), C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_int32),
+                                 C.POINTER(DedupStats)]),
     'sb_store_vcf_stream': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 }
 

@@ -19,7 +19,8 @@ import os
 from typing import Iterable
 
 from . import _lib
-from ._lib import BatchStats, BuildOpts, Query, ResultView, Slice, SliceStats, StoreInfo, check, lib
+from ._lib import (BatchStats, BuildOpts, DedupJob, DedupStats, Query, ResultView, Slice, SliceStats, StoreInfo,
+                   check, lib)
 from .payloads import PerformQueryResponse
 
 QERR = {1: UnboundLocalError, 2: IndexError, 3: ValueError, 4: AttributeError, 9: NotImplementedError}
@@ -136,6 +137,36 @@ class Store:
                 res.append({'numVariants': out[i].num_variants, 'numCalls': out[i].num_calls,
                              'records': out[i].records})
         return (res, ms.value) if with_timing else res
+
+    def dedup_counts(self, jobs, *, with_stats=False):
+        """jobs: iterable of (vcf_locations, contig, range_start, range_end).
+        Returns the unique region-key count per job (duplicateVariantSearch's
+        |uniqueVariants|), or a NotImplementedError for a job whose range
+        holds a record the reference's summariseSlice throws on."""
+        jobs = list(jobs)
+        n = len(jobs)
+        arr = (DedupJob * max(n, 1))()
+        keep = []
+        for i, (locs, contig, rs, re_) in enumerate(jobs):
+            ids = (C.c_uint32 * max(len(locs), 1))(*[self.vcf_id(l) for l in locs])
+            cb = _b(contig)
+            keep.append((ids, cb))
+            arr[i].vcf_ids = ids
+            arr[i].n_vcf = len(locs)
+            arr[i].contig = cb
+            arr[i].contig_len = len(cb)
+            arr[i].range_start = int(rs)
+            arr[i].range_end = int(re_)
+        uniq = (C.c_uint64 * max(n, 1))()
+        status = (C.c_int32 * max(n, 1))()
+        st = DedupStats()
+        check(lib().sb_dedup_count(self._h, arr, n, uniq, status, C.byref(st)))
+        res = [NotImplementedError(f'dedup job {jobs[i][1:]}: a record in range has an allele compressSeq '
+                                   'rejects (the reference summariseSlice throws)') if status[i] else uniq[i]
+               for i in range(n)]
+        if with_stats:
+            return res, {'keys': st.keys, 'collisions': st.collisions, 'device_ms': st.device_ms}
+        return res
 
     def vcf_stream(self, location):
         nb, ln = C.c_uint64(), C.c_uint64()
@@ -325,6 +356,9 @@ class Registry:
 
     def clear(self):
         self._by_loc.clear()
+
+    def locations(self) -> list[str]:
+        return list(self._by_loc)
 
     def group(self, payloads: Iterable[dict]):
         """Split payloads by store, preserving order inside each group."""
