@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Benchmark of the ingest-side hot paths on config 4:
+summariseSlice over index-style slices, then per-dataset
+duplicateVariantSearch, plus the cross-dataset union count (extension).
+
+Workload: D datasets (default 10; config 4 names 50) over one chr22-shape
+site pool (1,103,547 records, seed 4); each dataset = two VCFs with the same
+sites (a vcfGroup split by samples), 70 % of records shared with the pool.
+The VCFs are written as BGZF (sites-only text to bound generation time —
+neither path reads genotypes except through summariseSlice's skip-heuristic
+delimiter count, which the sites-only records still exercise) and ingested
+from the files, so virtual offsets are real.
+
+Prints one JSON line per workload (rank 0, one GPU):
+  summarise: every slice of every VCF (summariseVcf's partition) in one
+             sb_summarise_slices call; unit records/s.
+  dedup:     one sb_dedup_count call holding the D per-dataset jobs (whole
+             contig each); unit region keys/s.  The union job is reported in
+             the same line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import shutil
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, 'terraform-aws-serverless-beacon_amd'))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--datasets', type=int, default=10)
+    ap.add_argument('--records', type=int, default=1103547)
+    ap.add_argument('--steps', type=int, default=10)
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--threads', type=int, default=16)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    from sbeacon.engine import Store
+    from sbeacon.summarise_vcf import plan_slices
+    from sbeacon.workload import config4_cohort, write_bgzf
+
+    tmp = tempfile.mkdtemp(prefix='sbeacon-paths-')
+    try:
+        t0 = time.perf_counter()
+        pool, datasets = config4_cohort(n_datasets=args.datasets, n_records=args.records)
+        files = []
+        for ds, parts in datasets:
+            for loc, gen in parts:
+                p = os.path.join(tmp, loc.replace('/', '_').replace(':', ''))
+                if parts.index((loc, gen)) == 0:
+                    write_bgzf(p, gen.chunks(sites_only=True, threads=args.threads), level=1, threads=args.threads)
+                    first = p
+                else:
+                    shutil.copyfile(first, p)  # same sites: the vcfGroup's other sample half
+                files.append((loc, p))
+        t_gen = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        store = Store.build(files, device=0, keep_genotypes=False, n_threads=args.threads)
+        t_ingest = time.perf_counter() - t0
+        info = store.info()
+        log(f'{len(files)} VCFs, {info["n_records"]} records, {info["device_bytes"] / 2**20:.0f} MiB HBM; '
+            f'generate {t_gen:.1f} s, ingest {t_ingest:.1f} s')
+        summarise_line(args, store, files, plan_slices)
+        dedup_line(args, store, datasets, files)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def summarise_line(args, store, files, plan_slices):
+    slices = []
+    for loc, _ in files:
+        slices += [(loc, a, b) for a, b in plan_slices(store, loc)]
+    for _ in range(args.warmup):
+        store.summarise_slices(slices)
+    dev = []
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        res, ms = store.summarise_slices(slices, with_timing=True)
+        dev.append(ms)
+    wall = (time.perf_counter() - t) / args.steps
+    recs = sum(r['records'] for r in res if isinstance(r, dict))
+    n_records = store.info()['n_records']
+    dev_ms = sum(dev) / len(dev)
+    # algorithmic bytes: 8 B per record; the kernel reads the
+    # 16-byte SumHot per record (+ 4 B cursor / delimiter count on overshoots)
+    alg = 8.0 * n_records
+    achieved = alg / (dev_ms * 1e-3) / 1e9
+    cpu = parity = None
+    if not args.no_cpu_baseline:
+        cpu, parity = summarise_cpu(files[0], [s for s in slices if s[0] == files[0][0]],
+                                    [r for s, r in zip(slices, res) if s[0] == files[0][0]])
+    print(json.dumps({
+        'metric': 'summariseSlice records/s (all slices of every VCF in one call)',
+        'value': round(n_records / (wall * 1e-0), 1) if wall > 0 else None,
+        'unit': 'records/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(wall * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'uint64', 'data': 'synthetic config-4 cohort, sites-only BGZF',
+        'config': {'workload': f'config4-summarise-{args.datasets}ds', 'vcfs': len(files), 'records': n_records,
+                   'slices': len(slices), 'records_visited': recs},
+        'device_ms_per_step': round(dev_ms, 4),
+        'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None, 'kernel': 'summarise_kernel',
+                     'algorithmic_bytes_per_launch': alg},
+        'cpu_baseline': cpu, 'parity_sample': parity}), flush=True)
+
+
+def summarise_cpu(file, slices, got):
+    from oracle.oracle import OracleBgzf
+    o = OracleBgzf(file[1])
+    t = time.perf_counter()
+    exp = [o.summarise_slice(a, b) for _, a, b in slices]
+    dt = time.perf_counter() - t
+    recs = sum(e['records'] for e in exp)
+    bad = sum(int(g != e) for g, e in zip(got, exp))
+    o.close()
+    cpu = {'value': round(recs / dt, 1), 'unit': 'records/s', 'cores': 1, 'kind': 'port',
+           'sample': f'every slice of one VCF ({len(slices)} slices, {recs} records) through '
+                     'oracle/summarise_oracle.c (inflated stream in memory; inflate time excluded)',
+           'seconds': round(dt, 3)}
+    return cpu, {'slices': len(slices), 'mismatches': bad}
+
+
+def dedup_line(args, store, datasets, files):
+    jobs = [([loc for loc, _ in parts], '22', 0, 2**32 - 1) for _, parts in datasets]
+    union = [([loc for loc, _ in files], '22', 0, 2**32 - 1)]
+    for _ in range(args.warmup):
+        store.dedup_counts(jobs)
+    dev, keys = [], 0
+    t = time.perf_counter()
+    for _ in range(args.steps):
+        res, st = store.dedup_counts(jobs, with_stats=True)
+        dev.append(st['device_ms'])
+        keys = st['keys']
+    wall = (time.perf_counter() - t) / args.steps
+    dev_ms = sum(dev) / len(dev)
+    ures, ust = store.dedup_counts(union, with_stats=True)
+    ures, ust = store.dedup_counts(union, with_stats=True)
+    alg = 8.0 * keys  # compulsory: one read of the 64-bit key stream
+    impl = 20.0 * keys + 8 * 32.0 * keys + 16.0 * keys  # gather + 8 radix passes + unique (implementation bytes)
+    achieved = alg / (dev_ms * 1e-3) / 1e9
+    cpu = parity = None
+    if not args.no_cpu_baseline:
+        from oracle.oracle import dedup_count
+        ds, parts = datasets[0]
+        text = b''.join(parts[0][1].chunks(sites_only=True))
+        t = time.perf_counter()
+        e = dedup_count([text, text], '22', 0, 2**32 - 1)
+        dt = time.perf_counter() - t
+        cpu = {'value': round(2 * args.records / dt, 1), 'unit': 'keys/s', 'cores': 1, 'kind': 'port',
+               'sample': f'dataset {ds}: its 2 VCFs ({2 * args.records} records) through orc_dedup_count '
+                         '(string keys, qsort + unique; text parse included)', 'seconds': round(dt, 3)}
+        parity = {'jobs': 1, 'mismatches': int(res[0] != e), 'unique': e}
+    print(json.dumps({
+        'metric': 'duplicateVariantSearch region keys/s (per-dataset unique counts, one batched call)',
+        'value': round(keys / wall, 1) if wall > 0 else None,
+        'unit': 'keys/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
+        'ms_per_step': round(wall * 1e3, 3), 'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'uint64', 'data': 'synthetic config-4 cohort, sites-only BGZF',
+        'config': {'workload': f'config4-dedup-{args.datasets}ds', 'jobs': len(jobs), 'keys': keys,
+                   'unique_per_dataset_mean': sum(r for r in res if isinstance(r, int)) / max(len(res), 1)},
+        'device_ms_per_step': round(dev_ms, 4),
+        'union': {'vcfs': len(files), 'keys': ust['keys'], 'unique': ures[0], 'device_ms': round(ust['device_ms'], 4)},
+        'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                     'kernel': 'gather + radix sort + unique', 'algorithmic_bytes_per_launch': alg,
+                     'implementation_bytes_per_launch': impl,
+                     'implementation_GBs': round(impl / (dev_ms * 1e-3) / 1e9, 1)},
+        'cpu_baseline': cpu, 'parity_sample': parity}), flush=True)
+
+
+if __name__ == '__main__':
+    main()

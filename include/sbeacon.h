@@ -179,6 +179,17 @@ typedef struct {
 int sb_summarise_slices(sb_store *s, const sb_slice *slices, size_t n, sb_slice_stats *out, double *device_ms);
 /* BGZF block count and text-stream length of an ingested VCF */
 int sb_store_vcf_stream(const sb_store *s, uint32_t vcf_id, uint64_t *n_blocks, uint64_t *stream_len);
+/* contigs (CHROM values) of an ingested VCF, in file order */
+int sb_store_n_contigs(const sb_store *s, uint32_t vcf_id, uint32_t *n);
+int sb_store_contig_name(const sb_store *s, uint32_t vcf_id, uint32_t i, const char **p, size_t *len);
+/* Chunk boundaries of one contig for summariseVcf's partition_chunks
+ * (lambda/summariseVcf/lambda_function.py:90-104,197-214): the virtual
+ * offsets of every stride-th record start of the contig, then the offset just
+ * past its last record.  The reference takes them from the CSI/TBI index
+ * (chunk_beg/chunk_end of non-pseudo bins), which are record starts too; the
+ * store knows every record start.  *n = count (voffs gets min(count, cap)). */
+int sb_store_chunk_boundaries(const sb_store *s, uint32_t vcf_id, const char *contig, size_t contig_len,
+                              uint32_t stride, uint64_t *voffs, size_t cap, size_t *n);
 
 /* ---- duplicateVariantSearch -------------------------------------------------
  * One sb_dedup_job = one duplicateVariantSearch SNS message {"rangeStart",

@@ -916,6 +916,53 @@ int sb_dedup_count(sb_store *s, const sb_dedup_job *jobs, size_t n_jobs, uint64_
     });
 }
 
+int sb_store_n_contigs(const sb_store *s, uint32_t vcf_id, uint32_t *n) {
+    if (!s || !n) return SB_EINVAL;
+    if (vcf_id >= s->vcfs.size()) return SB_ENOSTORE;
+    *n = static_cast<uint32_t>(s->vcfs[vcf_id].segments.size());
+    return SB_OK;
+}
+
+int sb_store_contig_name(const sb_store *s, uint32_t vcf_id, uint32_t i, const char **p, size_t *len) {
+    if (!s || !p || !len) return SB_EINVAL;
+    if (vcf_id >= s->vcfs.size() || i >= s->vcfs[vcf_id].segments.size()) return SB_ENOSTORE;
+    const std::string &c = s->vcfs[vcf_id].segments[i].contig;
+    *p = c.data();
+    *len = c.size();
+    return SB_OK;
+}
+
+int sb_store_chunk_boundaries(const sb_store *s, uint32_t vcf_id, const char *contig, size_t contig_len,
+                              uint32_t stride, uint64_t *voffs, size_t cap, size_t *n) {
+    return guard([&] {
+        if (!s || !n || (!contig && contig_len) || (!voffs && cap)) throw Error(SB_EINVAL, "NULL argument");
+        if (vcf_id >= s->vcfs.size()) throw Error(SB_ENOSTORE, "unknown vcf id");
+        const VcfData &v = s->vcfs[vcf_id];
+        if (v.blk_coff.empty()) throw Error(SB_EINVAL, "chunk boundaries need a VCF ingested from a BGZF file");
+        auto it = v.seg_index.find(std::string(contig ? contig : "", contig_len));
+        *n = 0;
+        if (it == v.seg_index.end()) return;
+        const Segment &sg = v.segments[it->second];
+        uint32_t re = v.rec_base;  // end of this vcf's records
+        for (const auto &g : v.segments) re = std::max(re, g.hi);
+        const uint32_t st = std::max(1u, stride);
+        auto voff = [&](uint64_t u) {  // stream offset -> (block coffset << 16 | in-block offset)
+            auto b = std::upper_bound(v.blk_ustart.begin(), v.blk_ustart.end(), u);
+            size_t i = static_cast<size_t>(b - v.blk_ustart.begin()) - 1;
+            while (i + 1 < v.blk_ustart.size() && v.blk_ustart[i + 1] == v.blk_ustart[i]) ++i;  // skip empty blocks
+            return (v.blk_coff[i] << 16) | (u - v.blk_ustart[i]);
+        };
+        size_t k = 0;
+        auto put = [&](uint64_t x) {
+            if (k < cap) voffs[k] = x;
+            ++k;
+        };
+        for (uint32_t r = sg.lo; r < sg.hi; r += st) put(voff(s->h_start[r]));
+        put(voff(sg.hi < re ? s->h_start[sg.hi] : v.stream_len));
+        *n = k;
+    });
+}
+
 int sb_store_vcf_stream(const sb_store *s, uint32_t vcf_id, uint64_t *n_blocks, uint64_t *stream_len) {
     if (!s || vcf_id >= s->vcfs.size()) return SB_EINVAL;
     if (n_blocks) *n_blocks = s->vcfs[vcf_id].blk_coff.size();

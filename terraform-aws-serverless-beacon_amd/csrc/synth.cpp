@@ -48,6 +48,15 @@ struct Gen {
     double mean_gap;
     std::string contig;
     std::vector<uint32_t> pos;
+    // cohort member (config 4): record i comes from the pool's seed with
+    // probability `share`, otherwise from this member's own seed
+    uint64_t own_seed = 0;
+    double share = 1.0;
+    uint64_t rec_seed(uint64_t i) const {
+        if (share >= 1.0) return seed;
+        Rng r(own_seed, i, 7);
+        return r.uni() < share ? seed : own_seed;
+    }
 };
 
 struct Rec {
@@ -59,7 +68,7 @@ struct Rec {
 };
 
 void make_record(const Gen &g, uint64_t i, Rec &r) {
-    Rng rng(g.seed, i, 1);
+    Rng rng(g.rec_seed(i), i, 1);
     const double u = rng.uni();
     r.alts.clear();
     r.ac.clear();
@@ -139,7 +148,7 @@ void render(const Gen &g, uint64_t lo, uint64_t hi, bool sites_only, std::string
     char buf[4096];
     for (uint64_t i = lo; i < hi; ++i) {
         make_record(g, i, r);
-        Rng rng(g.seed, i, 2);
+        Rng rng(g.rec_seed(i), i, 2);
         size_t n = 0;
         auto put = [&](const char *s, size_t l) {
             if (n + l > sizeof buf) {
@@ -250,6 +259,16 @@ void *sbs_new(uint64_t seed, uint64_t n_records, uint32_t n_samples, uint32_t st
         }
         g->pos[i] = static_cast<uint32_t>(std::min<uint64_t>(p, 0xfffffff0ull));
     }
+    return g;
+}
+
+// A cohort member of `pool`: same positions, record i shared with the pool
+// with probability share (else drawn from own_seed), n_samples of its own.
+void *sbs_new_member(void *pool, uint64_t own_seed, double share, uint32_t n_samples) {
+    auto *g = new Gen(*static_cast<Gen *>(pool));
+    g->own_seed = own_seed;
+    g->share = share;
+    g->n_samples = n_samples;
     return g;
 }
 

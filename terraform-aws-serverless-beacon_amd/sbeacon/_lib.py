@@ -111,6 +111,10 @@ SIGNATURES = {
                                       C.POINTER(C.c_double)]),
     'sb_dedup_count': (C.c_int, [P, C.POINTER(DedupJob), C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_int32),
                                  C.POINTER(DedupStats)]),
+    'sb_store_n_contigs': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),
+    'sb_store_contig_name': (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t)]),
+    'sb_store_chunk_boundaries': (C.c_int, [P, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint32,
+                                            C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_size_t)]),
     'sb_store_vcf_stream': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
 }
 

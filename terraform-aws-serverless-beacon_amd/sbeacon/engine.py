@@ -168,6 +168,29 @@ class Store:
             return res, {'keys': st.keys, 'collisions': st.collisions, 'device_ms': st.device_ms}
         return res
 
+    def contigs(self, location) -> list[str]:
+        vid = self.vcf_id(location)
+        n = C.c_uint32()
+        check(lib().sb_store_n_contigs(self._h, vid, C.byref(n)))
+        out = []
+        p = C.c_char_p()
+        ln = C.c_size_t()
+        for i in range(n.value):
+            check(lib().sb_store_contig_name(self._h, vid, i, C.byref(p), C.byref(ln)))
+            out.append(C.string_at(p, ln.value).decode())
+        return out
+
+    def chunk_boundaries(self, location, contig, stride=1):
+        """Record-start virtual offsets of one contig (+ its end), the
+        stand-in for a CSI/TBI index's chunk boundaries."""
+        vid = self.vcf_id(location)
+        cb = _b(contig)
+        n = C.c_size_t()
+        check(lib().sb_store_chunk_boundaries(self._h, vid, cb, len(cb), stride, None, 0, C.byref(n)))
+        arr = (C.c_uint64 * max(n.value, 1))()
+        check(lib().sb_store_chunk_boundaries(self._h, vid, cb, len(cb), stride, arr, n.value, C.byref(n)))
+        return list(arr[:n.value])
+
     def vcf_stream(self, location):
         nb, ln = C.c_uint64(), C.c_uint64()
         check(lib().sb_store_vcf_stream(self._h, self.vcf_id(location), C.byref(nb), C.byref(ln)))

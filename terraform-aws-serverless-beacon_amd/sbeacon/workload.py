@@ -40,6 +40,8 @@ def synth_lib():
         L.sbs_records.restype = C.c_void_p
         L.sbs_records.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_size_t)]
         L.sbs_free_text.argtypes = [C.c_void_p]
+        L.sbs_new_member.restype = C.c_void_p
+        L.sbs_new_member.argtypes = [C.c_void_p, C.c_uint64, C.c_double, C.c_uint32]
         L.sbs_bgzf_compress.restype = C.c_void_p
         L.sbs_bgzf_compress.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t)]
         _syn = L
@@ -119,6 +121,16 @@ class SyntheticVcf:
             self._pos = a
         return self._pos
 
+    def member(self, own_seed, *, share=0.7, n_samples=None):
+        """A cohort member (config 4): the same positions, record i taken
+        from this generator with probability `share`, else from own_seed."""
+        m = SyntheticVcf.__new__(SyntheticVcf)
+        m.seed, m.n_records, m.contig = own_seed, self.n_records, self.contig
+        m.n_samples = self.n_samples if n_samples is None else n_samples
+        m._h = synth_lib().sbs_new_member(self._h, own_seed, float(share), m.n_samples)
+        m._pos = self._pos
+        return m
+
     def alleles(self, i):
         ref = C.create_string_buffer(256)
         alt = C.create_string_buffer(256)
@@ -189,3 +201,17 @@ def requests_to_payloads(reqs, *, vcf_location, chrom):
         payloads.extend(ps)
         owner.extend([ri] * len(ps))
     return payloads, owner
+
+
+def config4_cohort(*, n_datasets=50, n_records=1103547, seed=4, share=0.7, n_samples=250):
+    """Config 4: datasets over one shared chr22-shape site
+    pool.  Dataset d holds two VCFs (a vcfGroup split by samples, 250 + 250)
+    with the same sites: each record is the pool's with probability `share`,
+    else a private one at the same position.  Returns
+    (pool, [(dataset_id, [(vcf_location, SyntheticVcf), ...]), ...])."""
+    pool = SyntheticVcf(seed=seed, n_records=n_records, n_samples=n_samples)
+    out = []
+    for d in range(n_datasets):
+        m = pool.member(seed * 1000 + d + 1, share=share, n_samples=n_samples)
+        out.append((f'ds{d:02d}', [(f's3://cohort/ds{d:02d}/part{k}.vcf.gz', m) for k in (0, 1)]))
+    return pool, out

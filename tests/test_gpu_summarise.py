@@ -117,3 +117,24 @@ def test_summarise_handler(bgzf_files, bgzf_store):
     r = summarise.lambda_handler({'Records': [{'Sns': {'Message': json.dumps(msg)}}]})
     assert r['numVariants'] >= 30000 and r['numCalls'] == 48 * 30000
     engine.registry.clear()
+
+
+def test_summarise_vcf_partition(bgzf_files, bgzf_store):
+    """summariseVcf's partition over store chunk boundaries: slices tile each
+    contig, and every slice agrees with the oracle."""
+    from oracle.oracle import OracleBgzf
+    from sbeacon.summarise_vcf import chunk_boundaries, plan_slices, summarise_vcf
+    for name in ('synth', 'tiny22'):
+        loc = name + '.vcf.gz'
+        cb = chunk_boundaries(bgzf_store, loc)
+        slices = plan_slices(bgzf_store, loc)
+        assert slices and slices[0][0] == next(iter(cb.values()))[0]
+        for (a, b), (c, d) in zip(slices, slices[1:]):
+            assert b == c or any(b == v[-1] and c == w[0] for v, w in zip(cb.values(), list(cb.values())[1:]))
+        o = OracleBgzf(bgzf_files[name])
+        _, stats, tot = summarise_vcf(bgzf_store, loc)
+        exp = [o.summarise_slice(a, b) for a, b in slices]
+        assert stats == exp
+        assert tot['variantCount'] == sum(e['numVariants'] for e in exp)
+    # a small stride still covers every record
+    assert plan_slices(bgzf_store, 'synth.vcf.gz', stride=7)

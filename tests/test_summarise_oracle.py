@@ -89,3 +89,14 @@ def test_bgzf_slices_agree_with_stream_restatement(tiny_bgzf):
     starts = record_starts(txt)
     whole = o.summarise_slice((blk[0][0] << 16) | starts[0], (blk[-1][0] << 16))
     assert whole['records'] == len(starts)
+
+
+def test_partition_chunks_and_split_model():
+    from sbeacon.summarise_vcf import find_best_split, partition_chunks
+    b = {'1': [0, 5 << 16, (9 << 16) | 7, 20 << 16, 21 << 16], '2': [30 << 16, 31 << 16]}
+    # a slice closes at the first boundary >= 8 blocks-bytes past its start block
+    assert partition_chunks(b, 8) == [(0, (9 << 16) | 7), ((9 << 16) | 7, 20 << 16), (20 << 16, 21 << 16),
+                                      (30 << 16, 31 << 16)]
+    # the Newton model converges to a positive size that grows with the file
+    s1, s2 = find_best_split(1e7, 1000), find_best_split(5e9, 1000)
+    assert 0 < s1 < s2
