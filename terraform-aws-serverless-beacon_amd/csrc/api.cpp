@@ -178,7 +178,6 @@ struct sb_result_set {
 
 namespace {
 
-constexpr uint32_t kBlockRecs = 256;  // summarise_kernel workgroup size
 
 // coarse POS index of one segment: bucket[b] = first record with
 // POS >= base + (b << shift), for b in [0, n]; bucket[n] = segment end
@@ -326,8 +325,11 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.ds.cur = dev_upload(s, cur);
     s.ds.dcount = dev_upload(s, dcount);
     s.dk.hash = dev_upload(s, dk_hash);
-    s.dk.tail = dev_upload(s, dk_tail);
-    s.dk.pos = dev_upload(s, dk_pos);
+    {
+        std::vector<KBody> body(dk_hash.size());
+        for (size_t k = 0; k < body.size(); ++k) body[k] = KBody{dk_tail[k], dk_pos[k], 0};
+        s.dk.body = dev_upload(s, body);
+    }
     s.dk.blob = dev_upload(s, dk_blob);
     s.n_keys = dk_hash.size();
     HIP_OK(hipStreamSynchronize(s.stream));
@@ -696,11 +698,14 @@ bool voff_to_stream(const VcfData &v, uint64_t voff, uint64_t *u) {
 
 void summarise(sb_store &s, const sb_slice *sl, size_t n, sb_slice_stats *out, double *device_ms) {
     std::vector<SDev> hs(n);
+    std::vector<uint32_t> chunk_slice;  // phase-A chunk -> slice
     std::vector<int32_t> herr(n, 0);
     uint64_t words = 0;
     for (size_t i = 0; i < n; ++i) {
         SDev &d = hs[i];
         d.lo = d.hi = 0;
+        d.chunk_lo = static_cast<uint32_t>(chunk_slice.size());
+        d.n_chunks = 0;
         d.bitmap_off = words;
         if (sl[i].vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "slice " + std::to_string(i) + ": unknown vcf id");
         const VcfData &v = s.vcfs[sl[i].vcf_id];
@@ -728,20 +733,29 @@ void summarise(sb_store &s, const sb_slice *sl, size_t n, sb_slice_stats *out, d
         if (herr[i]) continue;
         d.lo = lo;
         d.hi = hi;
-        words += static_cast<uint64_t>((hi - lo + kBlockRecs - 1) / kBlockRecs) * 4;
+        d.chunk_lo = static_cast<uint32_t>(chunk_slice.size());
+        d.n_chunks = (hi - lo + kSumChunk - 1) / kSumChunk;
+        chunk_slice.insert(chunk_slice.end(), d.n_chunks, static_cast<uint32_t>(i));
+        words += (hi - lo + 63) / 64;
     }
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
-    DevMem dsl, dbm, dres;
+    DevMem dsl, dbm, dres, dcs, dpart;
     dsl.alloc(n * sizeof(SDev));
     dbm.alloc(words * 8);
     dres.alloc(n * sizeof(SRes));
+    dcs.alloc(chunk_slice.size() * 4);
+    dpart.alloc(chunk_slice.size() * sizeof(SPart));
     if (n) HIP_OK(hipMemcpyAsync(dsl.p, hs.data(), n * sizeof(SDev), hipMemcpyHostToDevice, st));
+    if (!chunk_slice.empty())
+        HIP_OK(hipMemcpyAsync(dcs.p, chunk_slice.data(), chunk_slice.size() * 4, hipMemcpyHostToDevice, st));
     hipEvent_t e0, e1;
     HIP_OK(hipEventCreate(&e0));
     HIP_OK(hipEventCreate(&e1));
     HIP_OK(hipEventRecord(e0, st));
-    launch_summarise(s.ds, dsl.as<SDev>(), static_cast<uint32_t>(n), dbm.as<uint64_t>(), dres.as<SRes>(), st);
+    launch_summarise(s.ds, dsl.as<SDev>(), static_cast<uint32_t>(n), dcs.as<uint32_t>(),
+                     static_cast<uint32_t>(chunk_slice.size()), dbm.as<uint64_t>(), dpart.as<SPart>(), dres.as<SRes>(),
+                     st);
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipGetLastError());
     std::vector<SRes> r(n);

@@ -61,71 +61,18 @@ __global__ __launch_bounds__(kThreads) void upsweep_kernel(const uint64_t *keys,
     for (int i = threadIdx.x; i < kWaves * 256; i += kThreads) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kTile;
-#pragma unroll 4
+    uint32_t dg[kItems];
+#pragma unroll
     for (int r = 0; r < kItems; ++r) {
         const uint64_t i = base + static_cast<uint64_t>(r) * kThreads + threadIdx.x;
-        if (i < n) atomicAdd(&h[w][(keys[i] >> shift) & 255u], 1u);
+        dg[r] = i < n ? static_cast<uint32_t>(keys[i] >> shift) & 255u : 256u;
     }
+#pragma unroll
+    for (int r = 0; r < kItems; ++r)
+        if (dg[r] < 256u) atomicAdd(&h[w][dg[r]], 1u);
     __syncthreads();
     const int d = threadIdx.x;
     hist[static_cast<uint64_t>(d) * ntiles + blockIdx.x] = h[0][d] + h[1][d] + h[2][d] + h[3][d];
-}
-
-__global__ __launch_bounds__(kThreads) void downsweep_kernel(const uint64_t *kin, const uint32_t *vin,
-                                                             uint64_t *kout, uint32_t *vout, uint64_t n,
-                                                             uint32_t shift, const uint32_t *off, uint32_t ntiles) {
-    __shared__ uint32_t cnt[kWaves][256];
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (int i = threadIdx.x; i < kWaves * 256; i += kThreads) (&cnt[0][0])[i] = 0;
-    __syncthreads();
-    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kTile + static_cast<uint64_t>(w) * kWaveKeys;
-    uint64_t k[kItems];
-    uint32_t v[kItems], rank[kItems];
-    // rank keys in index order: wave w owns a contiguous quarter of the tile
-#pragma unroll
-    for (int r = 0; r < kItems; ++r) {
-        const uint64_t i = base + static_cast<uint64_t>(r) * 64 + lane;
-        const bool ok = i < n;
-        k[r] = ok ? kin[i] : 0;
-        v[r] = ok ? vin[i] : 0;
-        const uint32_t d = static_cast<uint32_t>(k[r] >> shift) & 255u;
-        uint64_t peers = __ballot(ok);
-#pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            const bool bit = (d >> b) & 1u;
-            const uint64_t m = __ballot(bit);
-            peers &= bit ? m : ~m;
-        }
-        const uint32_t before = popc_below(peers);
-        uint32_t c = 0;
-        if (ok) c = cnt[w][d];
-        rank[r] = c + before;
-        __builtin_amdgcn_wave_barrier();
-        if (ok && before == 0) cnt[w][d] = c + static_cast<uint32_t>(__popcll(peers));
-        __builtin_amdgcn_wave_barrier();
-    }
-    __syncthreads();
-    {  // per digit: global tile offset + exclusive over waves
-        const int d = threadIdx.x;
-        uint32_t run = off[static_cast<uint64_t>(d) * ntiles + blockIdx.x];
-#pragma unroll
-        for (int ww = 0; ww < kWaves; ++ww) {
-            const uint32_t t = cnt[ww][d];
-            cnt[ww][d] = run;
-            run += t;
-        }
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < kItems; ++r) {
-        const uint64_t i = base + static_cast<uint64_t>(r) * 64 + lane;
-        if (i < n) {
-            const uint32_t d = static_cast<uint32_t>(k[r] >> shift) & 255u;
-            const uint32_t dst = cnt[w][d] + rank[r];
-            kout[dst] = k[r];
-            vout[dst] = v[r];
-        }
-    }
 }
 
 // exclusive scan of m u32 (block sums, top scan, down-sweep); kTile per block
@@ -149,6 +96,90 @@ __device__ __forceinline__ uint32_t block_exclusive(uint32_t x, uint32_t *lds, u
     __syncthreads();
     *total = tot;
     return wofs + inc - x;
+}
+
+__global__ __launch_bounds__(kThreads) void downsweep_kernel(const uint64_t *kin, const uint32_t *vin,
+                                                             uint64_t *kout, uint32_t *vout, uint64_t n,
+                                                             uint32_t shift, const uint32_t *off, uint32_t ntiles) {
+    __shared__ uint32_t cnt[kWaves][256];
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (int i = threadIdx.x; i < kWaves * 256; i += kThreads) (&cnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kTile + static_cast<uint64_t>(w) * kWaveKeys;
+    uint64_t k[kItems];
+    uint32_t v[kItems], rank[kItems];
+    // all of the wave's loads in flight first, then rank in index order
+    // (wave w owns a contiguous quarter of the tile)
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const uint64_t i = base + static_cast<uint64_t>(r) * 64 + lane;
+        k[r] = i < n ? kin[i] : 0;
+        v[r] = i < n ? vin[i] : 0;
+    }
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const bool ok = base + static_cast<uint64_t>(r) * 64 + lane < n;
+        const uint32_t d = static_cast<uint32_t>(k[r] >> shift) & 255u;
+        uint64_t peers = __ballot(ok);
+#pragma unroll
+        for (int b = 0; b < 8; ++b) {
+            const bool bit = (d >> b) & 1u;
+            const uint64_t m = __ballot(bit);
+            peers &= bit ? m : ~m;
+        }
+        const uint32_t before = popc_below(peers);
+        uint32_t c = 0;
+        if (ok) c = cnt[w][d];
+        rank[r] = c + before;
+        __builtin_amdgcn_wave_barrier();
+        if (ok && before == 0) cnt[w][d] = c + static_cast<uint32_t>(__popcll(peers));
+        __builtin_amdgcn_wave_barrier();
+    }
+    __syncthreads();
+    __shared__ uint32_t gbase[256], lds_scan[kWaves];
+    {  // per digit: exclusive over waves, tile-local start, global start
+        const int d = threadIdx.x;
+        uint32_t run = 0;
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ++ww) {
+            const uint32_t t = cnt[ww][d];
+            cnt[ww][d] = run;
+            run += t;
+        }
+        uint32_t tot;
+        const uint32_t local0 = block_exclusive(run, lds_scan, &tot);  // keys of smaller digits in this tile
+#pragma unroll
+        for (int ww = 0; ww < kWaves; ++ww) cnt[ww][d] += local0;
+        gbase[d] = off[static_cast<uint64_t>(d) * ntiles + blockIdx.x] - local0;
+    }
+    __syncthreads();
+    // stage the tile in digit order, then write runs of equal digits
+    // contiguously (avg. 16 keys = 128 B per digit run)
+    __shared__ uint64_t sk[kTile];
+    __shared__ uint32_t sv[kTile];
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const uint64_t i = base + static_cast<uint64_t>(r) * 64 + lane;
+        if (i < n) {
+            const uint32_t d = static_cast<uint32_t>(k[r] >> shift) & 255u;
+            const uint32_t loc = cnt[w][d] + rank[r];
+            sk[loc] = k[r];
+            sv[loc] = v[r];
+        }
+    }
+    __syncthreads();
+    const uint64_t tile0 = static_cast<uint64_t>(blockIdx.x) * kTile;
+    const uint32_t tn = static_cast<uint32_t>(min(static_cast<uint64_t>(kTile), n - tile0));
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const uint32_t loc = static_cast<uint32_t>(r) * kThreads + threadIdx.x;
+        if (loc < tn) {
+            const uint64_t key = sk[loc];
+            const uint32_t dst = gbase[static_cast<uint32_t>(key >> shift) & 255u] + loc;
+            kout[dst] = key;
+            vout[dst] = sv[loc];
+        }
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void scan_reduce_kernel(const uint32_t *a, uint64_t m, uint32_t *bsum) {
@@ -211,9 +242,9 @@ struct KeyStr {
     }
 };
 
-__device__ KeyStr key_str(const KStore &ks, uint32_t k) {
+__device__ KeyStr key_str(const KStore &ks, const KBody &k) {
     KeyStr s;
-    uint32_t p = ks.pos[k];
+    uint32_t p = k.pos;
     char tmp[10];
     uint32_t nd = 0;
     do {
@@ -222,7 +253,7 @@ __device__ KeyStr key_str(const KStore &ks, uint32_t k) {
     } while (p);
     for (uint32_t j = 0; j < nd; ++j) s.dig[j] = tmp[nd - 1 - j];
     s.nd = nd;
-    s.tail = ks.tail[k];
+    s.tail = k.tail;
     s.tl = (s.tail & kTailBlob) ? static_cast<uint32_t>((s.tail >> 40) & 0xffff) : static_cast<uint32_t>(s.tail >> 56);
     s.blob = ks.blob;
     return s;
@@ -230,43 +261,58 @@ __device__ KeyStr key_str(const KStore &ks, uint32_t k) {
 
 __device__ bool key_equal(const KStore &ks, uint32_t a, uint32_t b) {
     if (a == b) return true;
-    const uint32_t pa = ks.pos[a], pb = ks.pos[b];
-    const uint64_t ta = ks.tail[a], tb = ks.tail[b];
-    if (pa == pb && ta == tb) return true;  // same pos and same inline bytes / same blob bytes
-    const KeyStr x = key_str(ks, a), y = key_str(ks, b);
-    if (x.nd + x.tl != y.nd + y.tl) return false;
-    for (uint32_t j = 0; j < x.nd + x.tl; ++j)
-        if (x.at(j) != y.at(j)) return false;
+    const KBody x = ks.body[a], y = ks.body[b];
+    if (x.pos == y.pos && x.tail == y.tail) return true;  // same pos and same inline bytes / same blob bytes
+    const KeyStr u = key_str(ks, x), v = key_str(ks, y);
+    if (u.nd + u.tl != v.nd + v.tl) return false;
+    for (uint32_t j = 0; j < u.nd + u.tl; ++j)
+        if (u.at(j) != v.at(j)) return false;
     return true;
 }
 
+// kItems sorted positions per thread (coalesced: item r of the block is
+// r * kThreads + threadIdx.x); the block's distinct count goes out with one
+// atomic per job it touches (one in the common single-job block)
 __global__ __launch_bounds__(kThreads) void unique_kernel(const uint64_t *keys, const uint32_t *vals, uint64_t n,
                                                           KStore ks, uint32_t job_bits, unsigned long long *counts,
                                                           uint32_t *coll, uint32_t *ncoll) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-    const bool ok = i < n;
-    bool fresh = false;
-    uint32_t job = 0;
-    if (ok) {
+    __shared__ uint32_t s_job[2];
+    __shared__ unsigned int s_cnt;
+    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kTile;
+    if (threadIdx.x == 0) {
+        s_cnt = 0;
+        const uint64_t last = min(n, base + kTile) - 1;
+        s_job[0] = job_bits ? static_cast<uint32_t>(keys[base] >> (64 - job_bits)) : 0u;
+        s_job[1] = job_bits ? static_cast<uint32_t>(keys[last] >> (64 - job_bits)) : 0u;
+    }
+    __syncthreads();
+    const bool one_job = s_job[0] == s_job[1];
+    uint32_t mine = 0;
+#pragma unroll 4
+    for (int r = 0; r < kItems; ++r) {
+        const uint64_t i = base + static_cast<uint64_t>(r) * kThreads + threadIdx.x;
+        if (i >= n) break;
         const uint64_t k = keys[i];
-        job = job_bits ? static_cast<uint32_t>(k >> (64 - job_bits)) : 0u;
+        bool fresh = false;
         if (i == 0 || keys[i - 1] != k) {
             fresh = true;
         } else if (!key_equal(ks, vals[i - 1], vals[i])) {
             fresh = true;  // a different string under the same word: the host recounts its group
             coll[atomicAdd(ncoll, 1u)] = static_cast<uint32_t>(i);
         }
+        if (!fresh) continue;
+        if (one_job) {
+            ++mine;
+        } else {
+            atomicAdd(&counts[job_bits ? static_cast<uint32_t>(k >> (64 - job_bits)) : 0u], 1ull);
+        }
     }
-    // one atomic per wave when the wave's keys belong to one job
-    const uint64_t act = __ballot(ok);
-    const uint64_t fm = __ballot(fresh);
-    const int first = __ffsll(static_cast<long long>(act)) - 1;
-    const uint32_t j0 = __shfl(job, first < 0 ? 0 : first, 64);
-    const bool same = __ballot(ok && job != j0) == 0;
-    if (same) {
-        if ((threadIdx.x & 63) == first && fm) atomicAdd(&counts[j0], static_cast<unsigned long long>(__popcll(fm)));
-    } else if (fresh) {
-        atomicAdd(&counts[job], 1ull);
+    if (one_job) {
+        // wave sum, then one LDS add per wave and one global atomic per block
+        for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
+        if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&s_cnt, mine);
+        __syncthreads();
+        if (threadIdx.x == 0 && s_cnt) atomicAdd(&counts[s_job[0]], static_cast<unsigned long long>(s_cnt));
     }
 }
 
@@ -310,7 +356,7 @@ int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, ui
 void launch_dedup_unique(const uint64_t *keys, const uint32_t *vals, uint64_t n, const KStore &ks, uint32_t job_bits,
                          unsigned long long *counts, uint32_t *coll, uint32_t *ncoll, hipStream_t s) {
     if (!n) return;
-    unique_kernel<<<static_cast<uint32_t>((n + kThreads - 1) / kThreads), kThreads, 0, s>>>(keys, vals, n, ks,
+    unique_kernel<<<tiles_of(n), kThreads, 0, s>>>(keys, vals, n, ks,
                                                                                            job_bits, counts, coll,
                                                                                            ncoll);
 }

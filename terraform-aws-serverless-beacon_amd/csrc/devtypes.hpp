@@ -144,9 +144,18 @@ struct alignas(16) SumHot {
 };
 inline constexpr uint32_t kSumUnsupported = 1u << 31;
 
+inline constexpr uint32_t kSumChunk = 4096;  // records per phase-A workgroup
+
 struct SDev {  // one summariseSlice invocation after host planning
     uint32_t lo, hi;        // records whose line starts in [U(vstart), U(vend))
     uint64_t bitmap_off;    // u64-word offset of this slice's overshoot bitmap
+    uint32_t chunk_lo;      // first phase-A chunk of this slice
+    uint32_t n_chunks;      // ceil((hi - lo) / kSumChunk)
+};
+
+struct SPart {  // phase-A partial of one chunk
+    uint64_t nv, nc;
+    uint32_t bad, overshoot_words;
 };
 
 struct SRes {
@@ -175,10 +184,15 @@ struct SStore {  // summary columns
 inline constexpr uint64_t kTailBlob = 1ull << 63;
 inline constexpr int kTailInlineMax = 7;
 
+struct alignas(16) KBody {  // what the equality check reads: one 16-byte load
+    uint64_t tail;
+    uint32_t pos;
+    uint32_t pad;
+};
+
 struct KStore {
     const uint64_t *hash;
-    const uint64_t *tail;
-    const uint32_t *pos;
+    const KBody *body;
     const uint8_t *blob;
 };
 

@@ -20,12 +20,13 @@ void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t
                  const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out,
                  hipStream_t s);
 
-// summariseSlice: one workgroup per slice — a reduction of the records'
-// (numVariants, numCalls) contributions plus an overshoot bitmap, then one
-// wave replays the skip heuristic over the (rare) overshooting records.
-// bitmap needs sum over slices of ceil((hi - lo) / 256) * 4 words.
-void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, uint64_t *bitmap, SRes *out,
-                      hipStream_t s);
+// summariseSlice: phase A = one workgroup per chunk of kSumChunk records
+// (chunk_slice[c] = its slice), reducing the records' (numVariants, numCalls)
+// contributions into part[c] and writing the overshoot bitmap; phase B = one
+// wave per slice replaying the skip heuristic over the (rare) overshooting
+// records.  bitmap needs ceil((hi - lo) / 64) words per slice.
+void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const uint32_t *chunk_slice, uint32_t nchunks,
+                      uint64_t *bitmap, SPart *part, SRes *out, hipStream_t s);
 
 // Fetch-time gather of every query's hits into one dense array.
 void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,

@@ -484,36 +484,43 @@ inline uint32_t blocks_for(uint32_t nq) { return (nq + kWavesPerBlock - 1) / kWa
 // bytes left on r's line).  Phase A sums every record of the slice and marks
 // those overshoots; phase B (wave 0) walks the marks in order, keeps only the
 // overshoots of visited records and subtracts the records their jumps skip.
-__global__ __launch_bounds__(kBlock) void summarise_kernel(SStore ss, const SDev *__restrict__ slices, uint32_t ns,
-                                                           uint64_t *__restrict__ bitmap, SRes *__restrict__ out) {
+// Phase A: one workgroup per chunk of kSumChunk records of one slice (chunks
+// never straddle slices) — sums the chunk's contributions and writes its
+// overshoot bitmap words.
+__global__ __launch_bounds__(kBlock) void summarise_chunk_kernel(SStore ss, const SDev *__restrict__ slices,
+                                                                 const uint32_t *__restrict__ chunk_slice,
+                                                                 uint32_t nchunks, uint64_t *__restrict__ bitmap,
+                                                                 SPart *__restrict__ part) {
     __shared__ uint64_t red_nv[kWavesPerBlock], red_nc[kWavesPerBlock];
-    __shared__ uint32_t red_bad[kWavesPerBlock];
-    const uint32_t sid = blockIdx.x;
-    if (sid >= ns) return;
-    const SDev S = slices[sid];
+    __shared__ uint32_t red_bad[kWavesPerBlock], red_ov[kWavesPerBlock];
+    const uint32_t c = blockIdx.x;
+    if (c >= nchunks) return;
+    const SDev S = slices[chunk_slice[c]];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-    const uint32_t lo = S.lo, hi = S.hi;
-    if (lo >= hi) {
-        if (threadIdx.x == 0) out[sid] = SRes{0, 0, 0, 0, 0};
-        return;
-    }
-    const uint64_t skip = 2ull * ss.dcount[lo];
+    const uint32_t c0 = S.lo + (c - S.chunk_lo) * kSumChunk;
+    const uint32_t c1 = min(S.hi, c0 + kSumChunk);
+    const uint64_t skip = 2ull * ss.dcount[S.lo];
     uint64_t nv = 0, nc = 0;
-    uint32_t bad = 0;
+    uint32_t bad = 0, ov = 0;
     uint64_t *bm = bitmap + S.bitmap_off;
-    for (uint32_t base = lo; base < hi; base += kBlock) {
+    constexpr int kPer = kSumChunk / kBlock;
+    SumHot h[kPer];  // all loads in flight before any use
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t r = c0 + k * kBlock + threadIdx.x;
+        h[k] = r < c1 ? ss.sum[r] : SumHot{0xffffffffu, 0, 0};
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t base = c0 + k * kBlock;
         const uint32_t r = base + threadIdx.x;
-        bool o = false;
-        if (r < hi) {
-            const SumHot h = ss.sum[r];
-            nv += h.nvf & ~kSumUnsupported;
-            nc += h.nc;
-            bad += h.nvf >> 31;
-            o = r > lo && skip >= h.rem;
-        }
-        const uint64_t m = __ballot(o);
-        if (lane == 0) bm[(base - lo) / kWave + wave] = m;
+        nv += h[k].nvf & ~kSumUnsupported;
+        nc += h[k].nc;
+        bad += h[k].nvf >> 31;
+        const uint64_t m = __ballot(r < c1 && r > S.lo && skip >= h[k].rem);
+        ov += m != 0;
+        if (lane == 0 && base + wave * kWave < c1) bm[(base - S.lo) / kWave + wave] = m;
     }
     nv = static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(nv)));
     nc = static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(nc)));
@@ -522,58 +529,95 @@ __global__ __launch_bounds__(kBlock) void summarise_kernel(SStore ss, const SDev
         red_nv[wave] = nv;
         red_nc[wave] = nc;
         red_bad[wave] = bad;
+        red_ov[wave] = ov;
     }
-    __syncthreads();  // bitmap words of every wave are visible to wave 0 (same CU)
-    if (wave != 0) return;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        SPart P{0, 0, 0, 0};
+        for (int w = 0; w < kWavesPerBlock; ++w) {
+            P.nv += red_nv[w];
+            P.nc += red_nc[w];
+            P.bad += red_bad[w];
+            P.overshoot_words += red_ov[w];
+        }
+        part[c] = P;
+    }
+}
+
+// Phase B: one wave per slice — totals of its chunks, then the in-order walk
+// of the overshoot marks (only chunks that have any): a visited overshoot
+// seeks to P = start + cursor + skipSize and skipPast('\n') resumes at the
+// first record starting after P; the records in between are subtracted.
+__global__ __launch_bounds__(kBlock) void summarise_finish_kernel(SStore ss, const SDev *__restrict__ slices,
+                                                                  uint32_t ns, const uint64_t *__restrict__ bitmap,
+                                                                  const SPart *__restrict__ part,
+                                                                  SRes *__restrict__ out) {
+    const uint32_t sid = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6);
+    if (sid >= ns) return;
+    const SDev S = slices[sid];
+    const int lane = lane_id();
+    const uint32_t lo = S.lo, hi = S.hi;
+    if (lo >= hi) {
+        if (lane == 0) out[sid] = SRes{0, 0, 0, 0, 0};
+        return;
+    }
+    const uint64_t skip = 2ull * ss.dcount[lo];
     uint64_t tnv = 0, tnc = 0, tbad = 0;
-    for (int w = 0; w < kWavesPerBlock; ++w) {
-        tnv += red_nv[w];
-        tnc += red_nc[w];
-        tbad += red_bad[w];
+    for (uint32_t k = lane; k < S.n_chunks; k += kWave) {
+        const SPart P = part[S.chunk_lo + k];
+        tnv += P.nv;
+        tnc += P.nc;
+        tbad += P.bad;
     }
+    tnv = static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(tnv)));
+    tnc = static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(tnc)));
+    tbad = static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(tbad)));
+    const uint64_t *bm = bitmap + S.bitmap_off;
     uint64_t sub_nv = 0, sub_nc = 0, sub_bad = 0, skipped = 0;
     uint32_t resume = lo;  // records >= resume are visited until the next jump
-    const uint32_t nwords = (hi - lo + kWave - 1) / kWave;
-    for (uint32_t w0 = 0; w0 < nwords; w0 += kWave) {
-        const uint64_t word = (w0 + lane < nwords) ? bm[w0 + lane] : 0ull;
-        uint64_t nz = __ballot(word != 0ull);
-        while (nz) {
-            const int L = ffs64(nz);
-            nz &= nz - 1;
-            uint64_t bits = static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(word), L));
-            while (bits) {
-                const int b = ffs64(bits);
-                bits &= bits - 1;
-                const uint32_t r = lo + (w0 + static_cast<uint32_t>(L)) * kWave + static_cast<uint32_t>(b);
-                if (r < resume) continue;  // r itself was skipped: it never seeks
-                // visited overshoot: the seek lands at P, skipPast('\n') resumes
-                // at the first record starting after P
-                const uint64_t P = ss.start[r] + ss.cur[r] + skip;
-                uint32_t t = hi;
-                for (uint32_t c0 = r + 1; c0 < hi; c0 += kWave) {
-                    const uint32_t i = c0 + static_cast<uint32_t>(lane);
-                    const uint64_t m = __ballot(i < hi && ss.start[i] > P);
-                    if (m) {
-                        t = c0 + static_cast<uint32_t>(ffs64(m));
-                        break;
+    constexpr uint32_t kWordsPerChunk = kSumChunk / kWave;
+    for (uint32_t k = 0; k < S.n_chunks; ++k) {
+        if (part[S.chunk_lo + k].overshoot_words == 0) continue;
+        const uint32_t wbeg = k * kWordsPerChunk;
+        const uint32_t wend = min((hi - lo + kWave - 1) / kWave, wbeg + kWordsPerChunk);
+        for (uint32_t w0 = wbeg; w0 < wend; w0 += kWave) {
+            const uint64_t word = (w0 + lane < wend) ? bm[w0 + lane] : 0ull;
+            uint64_t nz = __ballot(word != 0ull);
+            while (nz) {
+                const int L = ffs64(nz);
+                nz &= nz - 1;
+                uint64_t bits = static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(word), L));
+                while (bits) {
+                    const int b = ffs64(bits);
+                    bits &= bits - 1;
+                    const uint32_t r = lo + (w0 + static_cast<uint32_t>(L)) * kWave + static_cast<uint32_t>(b);
+                    if (r < resume) continue;  // r itself was skipped: it never seeks
+                    const uint64_t P = ss.start[r] + ss.cur[r] + skip;
+                    uint32_t t = hi;
+                    for (uint32_t q0 = r + 1; q0 < hi; q0 += kWave) {
+                        const uint32_t i = q0 + static_cast<uint32_t>(lane);
+                        const uint64_t m = __ballot(i < hi && ss.start[i] > P);
+                        if (m) {
+                            t = q0 + static_cast<uint32_t>(ffs64(m));
+                            break;
+                        }
                     }
-                }
-                // subtract the skipped records (r, t)
-                for (uint32_t c0 = r + 1; c0 < t; c0 += kWave) {
-                    const uint32_t i = c0 + static_cast<uint32_t>(lane);
-                    uint64_t a = 0, c = 0, d = 0;
-                    if (i < t) {
-                        const SumHot h = ss.sum[i];
-                        a = h.nvf & ~kSumUnsupported;
-                        c = h.nc;
-                        d = h.nvf >> 31;
+                    for (uint32_t q0 = r + 1; q0 < t; q0 += kWave) {
+                        const uint32_t i = q0 + static_cast<uint32_t>(lane);
+                        uint64_t a = 0, c = 0, d = 0;
+                        if (i < t) {
+                            const SumHot h = ss.sum[i];
+                            a = h.nvf & ~kSumUnsupported;
+                            c = h.nc;
+                            d = h.nvf >> 31;
+                        }
+                        sub_nv += static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(a)));
+                        sub_nc += static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(c)));
+                        sub_bad += static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(d)));
                     }
-                    sub_nv += static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(a)));
-                    sub_nc += static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(c)));
-                    sub_bad += static_cast<uint64_t>(wave_sum_i64(static_cast<int64_t>(d)));
+                    skipped += t - (r + 1);
+                    resume = t;
                 }
-                skipped += t - (r + 1);
-                resume = t;
             }
         }
     }
@@ -590,10 +634,14 @@ __global__ __launch_bounds__(kBlock) void summarise_kernel(SStore ss, const SDev
 
 }  // namespace
 
-void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, uint64_t *bitmap, SRes *out,
-                      hipStream_t s) {
+void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const uint32_t *chunk_slice, uint32_t nchunks,
+                      uint64_t *bitmap, SPart *part, SRes *out, hipStream_t s) {
     if (!ns) return;
-    hipLaunchKernelGGL(summarise_kernel, dim3(ns), dim3(kBlock), 0, s, ss, slices, ns, bitmap, out);
+    if (nchunks)
+        hipLaunchKernelGGL(summarise_chunk_kernel, dim3(nchunks), dim3(kBlock), 0, s, ss, slices, chunk_slice, nchunks,
+                           bitmap, part);
+    hipLaunchKernelGGL(summarise_finish_kernel, dim3((ns + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, s,
+                       ss, slices, ns, bitmap, part, out);
 }
 
 void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,
