@@ -59,9 +59,26 @@ T *dev_upload(sb_store &s, const std::vector<T> &v) {
     return static_cast<T *>(b.p);
 }
 
-struct DevMem {  // RAII device allocation for batches
+struct DevMem {  // RAII device allocation for batches (move-only)
     void *p = nullptr;
     size_t bytes = 0;
+    DevMem() = default;
+    DevMem(const DevMem &) = delete;
+    DevMem &operator=(const DevMem &) = delete;
+    DevMem(DevMem &&o) noexcept : p(o.p), bytes(o.bytes) {
+        o.p = nullptr;
+        o.bytes = 0;
+    }
+    DevMem &operator=(DevMem &&o) noexcept {
+        if (this != &o) {
+            release();
+            p = o.p;
+            bytes = o.bytes;
+            o.p = nullptr;
+            o.bytes = 0;
+        }
+        return *this;
+    }
     void alloc(size_t n) {
         release();
         bytes = std::max<size_t>(n, 16);
@@ -146,9 +163,15 @@ struct sb_batch {
     uint64_t cap_total = 0, samples_words = 0;
     DevMem q, qbytes, subsets, lut, res, hits, samples_out;
     // queries split by kernel variant: the sample path compiled in or out
-    DevMem idx_plain, idx_collect;
-    uint32_t n_plain = 0, n_collect = 0;
-    bool all_plain = true, nonneg = true;
+    // queries grouped by kernel specialisation: one launch per non-empty group
+    struct Group {
+        int mode;
+        uint32_t max_words;  // 0 = sample path compiled out
+        std::vector<uint32_t> idx;
+        DevMem d_idx;
+    };
+    std::vector<Group> groups;
+    bool nonneg = true;
     // one event pair per run since the last sync; sync() averages them
     std::vector<std::array<hipEvent_t, 2>> ev;
     size_t runs_pending = 0;
@@ -214,6 +237,7 @@ void build_buckets(const std::vector<uint32_t> &pos, const Segment &sg, BucketIn
 
 void upload_store(sb_builder &b, sb_store &s) {
     std::vector<RecHot> rec;
+    std::vector<RangeHot> rng;
     std::vector<uint32_t> pos, a0_len, x_lo, x_cls, x_len, fb, bucket;
     std::vector<int32_t> x_ac;
     std::vector<uint64_t> ref_key, a0_key, ref_off, a0_off, x_key, x_off, planes;
@@ -254,6 +278,7 @@ void upload_store(sb_builder &b, sb_store &s) {
         v.planex_base = planes.size();
         planes.insert(planes.end(), c.planesx.begin(), c.planesx.end());
         rec.insert(rec.end(), c.rec.begin(), c.rec.end());
+        rng.insert(rng.end(), c.rng.begin(), c.rng.end());
         pos.insert(pos.end(), c.pos.begin(), c.pos.end());
         a0_len.insert(a0_len.end(), c.a0_len.begin(), c.a0_len.end());
         ref_key.insert(ref_key.end(), c.ref_key.begin(), c.ref_key.end());
@@ -303,6 +328,8 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.n_extra = x_key.size();
 
     s.d.rec = dev_upload(s, rec);
+    s.d.rng = dev_upload(s, rng);
+    std::vector<RangeHot>().swap(rng);
     s.d.pos = dev_upload(s, pos);
     s.d.ref_key = dev_upload(s, ref_key);
     s.d.a0_key = dev_upload(s, a0_key);
@@ -311,8 +338,11 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.d.ref_off = dev_upload(s, ref_off);
     s.d.a0_off = dev_upload(s, a0_off);
     s.d.fb_off = dev_upload(s, fb_off);
-    s.d.x_cls = dev_upload(s, x_cls);
-    s.d.x_ac = dev_upload(s, x_ac);
+    {
+        std::vector<XRow> xrow(x_cls.size());
+        for (size_t i = 0; i < xrow.size(); ++i) xrow[i] = XRow{x_cls[i], x_ac[i]};
+        s.d.xrow = dev_upload(s, xrow);
+    }
     s.d.x_key = dev_upload(s, x_key);
     s.d.x_len = dev_upload(s, x_len);
     s.d.x_off = dev_upload(s, x_off);
@@ -538,14 +568,33 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     }
     B.samples_words = samples_words;
     B.cap_total = cap_total;
-    std::vector<uint32_t> plain, coll;
-    for (uint32_t i = 0; i < B.nq; ++i) {
-        (B.hq[i].samples_out_off != ~0ull ? coll : plain).push_back(i);
-        if (!(B.hq[i].flags & F_NONNEG)) B.nonneg = false;
+    {
+        // collect -> general kernel with the sample path; otherwise the
+        // narrowest specialisation whose predicates cover the query
+        B.groups.clear();
+        for (int g = 0; g < 4; ++g) B.groups.push_back(sb_batch::Group{g == 3 ? MODE_GENERAL : g, g == 3 ? s.max_words : 0u, {}, {}});
+        for (uint32_t i = 0; i < B.nq; ++i) {
+            const QDev &d = B.hq[i];
+            if (!(d.flags & F_NONNEG)) B.nonneg = false;
+            int g;
+            if (d.samples_out_off != ~0ull) {
+                g = 3;
+            } else if (d.flags & (F_STRICT_UNBOUND | F_SAMPLES_VARIANT)) {
+                g = MODE_GENERAL;
+            } else if (d.ref_mode == REF_ANY && d.alt_mode == ALT_N) {
+                g = MODE_RANGE_N;
+            } else if (d.ref_mode == REF_EXACT && d.alt_mode == ALT_EXACT) {
+                g = MODE_EXACT;
+            } else {
+                g = MODE_GENERAL;
+            }
+            B.groups[static_cast<size_t>(g)].idx.push_back(i);
+        }
+        std::vector<sb_batch::Group> keep;
+        for (auto &g : B.groups)
+            if (!g.idx.empty()) keep.push_back(std::move(g));
+        B.groups = std::move(keep);
     }
-    B.n_plain = static_cast<uint32_t>(plain.size());
-    B.n_collect = static_cast<uint32_t>(coll.size());
-    B.all_plain = coll.empty();
     if (lut_all.empty()) lut_all.push_back(0);
     // ---- device buffers
     HIP_OK(hipSetDevice(s.device));
@@ -558,11 +607,10 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     if (!qbytes.empty()) HIP_OK(hipMemcpyAsync(B.qbytes.p, qbytes.data(), qbytes.size(), hipMemcpyHostToDevice, st));
     if (!subsets.empty()) HIP_OK(hipMemcpyAsync(B.subsets.p, subsets.data(), subsets.size() * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(B.lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
-    if (!B.all_plain) {
-        B.idx_plain.alloc(plain.size() * 4);
-        B.idx_collect.alloc(coll.size() * 4);
-        if (!plain.empty()) HIP_OK(hipMemcpyAsync(B.idx_plain.p, plain.data(), plain.size() * 4, hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemcpyAsync(B.idx_collect.p, coll.data(), coll.size() * 4, hipMemcpyHostToDevice, st));
+    for (auto &g : B.groups) {
+        if (B.groups.size() == 1) break;  // one group covers every query in order: no index list
+        g.d_idx.alloc(g.idx.size() * 4);
+        HIP_OK(hipMemcpyAsync(g.d_idx.p, g.idx.data(), g.idx.size() * 4, hipMemcpyHostToDevice, st));
     }
     B.res.alloc(size_t(nq) * sizeof(QRes));
     B.hits.alloc(cap_total * 8);
@@ -583,17 +631,11 @@ void run(sb_batch &B) {
     }
     const auto &E = B.ev[B.runs_pending++];
     HIP_OK(hipEventRecord(E[0], st));
-    if (B.all_plain) {
-        launch_scan(d, B.q.as<QDev>(), nullptr, B.nq, B.nonneg, 0, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(),
-                    B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), st);
-    } else {
-        launch_scan(d, B.q.as<QDev>(), B.idx_collect.as<uint32_t>(), B.n_collect, B.nonneg, s.max_words,
-                    B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(), B.res.as<QRes>(), B.hits.as<uint64_t>(),
-                    B.samples_out.as<uint64_t>(), st);
-        launch_scan(d, B.q.as<QDev>(), B.idx_plain.as<uint32_t>(), B.n_plain, B.nonneg, 0, B.qbytes.as<uint8_t>(),
+    for (const auto &g : B.groups)
+        launch_scan(d, B.q.as<QDev>(), B.groups.size() == 1 ? nullptr : g.d_idx.as<uint32_t>(),
+                    static_cast<uint32_t>(g.idx.size()), B.nonneg, g.max_words, g.mode, B.qbytes.as<uint8_t>(),
                     B.subsets.as<uint64_t>(), B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(),
                     st);
-    }
     HIP_OK(hipEventRecord(E[1], st));
     HIP_OK(hipGetLastError());
 }

@@ -39,6 +39,21 @@ struct alignas(16) RecHot {
     int32_t ac0;   // INFO AC entry of ALT 0, or its GT count when AC is absent
 };
 
+// What a referenceBases='N' / alternateBases='N' query (MODE_RANGE_N) needs of
+// a record, precomputed at ingest because none of it depends on the query
+// (search_variants.py:170-176 with len(alt) = 1 for a single base, :205-214):
+//   info bits 0..7 = ALTs emitted as variants (single base and AC != 0),
+//   RH_HIT = some ALT is a single base, RH_SLOW = the record needs the general
+//   evaluation (no AC tag, int() failures, AC entries missing, > 8 ALTs,
+//   |sum| beyond int32);  c = sum of AC over the single-base ALTs.
+struct alignas(16) RangeHot {
+    uint32_t end;
+    uint32_t info;
+    int32_t an;
+    int32_t c;
+};
+enum : uint32_t { RH_EMIT_MASK = 0xffu, RH_HIT = 1u << 8, RH_SLOW = 1u << 9 };
+
 // ---- query modes -----------------------------------------------------------
 enum : uint32_t {
     REF_ANY = 0,    // reference_bases == 'N' (:59)
@@ -48,6 +63,8 @@ enum : uint32_t {
     REF_ERROR = 4,  // raise ref_err at the first record passing the end filter
 };
 enum : uint32_t { ALT_N = 0, ALT_EXACT = 1, ALT_VTYPE = 2 };
+// scan-kernel specialisations (query classes launched separately)
+enum : int { MODE_GENERAL = 0, MODE_RANGE_N = 1, MODE_EXACT = 2 };
 enum : uint32_t { VT_DEL = 0, VT_INS = 1, VT_DUP = 2, VT_DUPT = 3, VT_CNV = 4, VT_OTHER = 5 };
 enum : uint32_t {
     F_DETAILS = 1u << 0,         // include_details
@@ -59,9 +76,15 @@ enum : uint32_t {
     F_NONNEG = 1u << 6,          // every AC/GT count in the store is >= 0
 };
 
+struct alignas(8) XRow {
+    uint32_t cls;  // C_* class bits + symbolic id (layout of RecHot::hot bits 6..31)
+    int32_t ac;    // INFO AC entry, or its GT count when AC is absent
+};
+
 struct DStore {
     // record-indexed
     const RecHot *rec;
+    const RangeHot *rng;      // MODE_RANGE_N view of the same records
     const uint32_t *pos;
     const uint64_t *ref_key;  // key(REF.upper())
     const uint64_t *a0_key;   // key(ALT0.upper())
@@ -71,8 +94,7 @@ struct DStore {
     const uint64_t *a0_off;
     const int64_t *fb_off;    // genotype fallback row (u32 words) or -1
     // extra-ALT rows (ALT index >= 1)
-    const uint32_t *x_cls;
-    const int32_t *x_ac;
+    const XRow *xrow;  // (class, AC) of each extra row: one 8-byte load
     const uint64_t *x_key;
     const uint32_t *x_len;
     const uint64_t *x_off;

@@ -519,6 +519,8 @@ struct Parser {
         const int64_t anv = has_an ? an_val : gt_an;
         if (anv > INT32_MAX) return fail(L, "called-allele count beyond int32");
         int32_t ac0 = 0;
+        uint32_t rh_info = 0;  // RangeHot (MODE_RANGE_N) view
+        int64_t rh_c = 0;
         for (uint32_t i = 0; i < na; ++i) {
             const uint8_t *ap = reinterpret_cast<const uint8_t *>(alts[i]);
             const size_t al = alens[i];
@@ -548,6 +550,12 @@ struct Parser {
             } else {
                 acval = gtcount[i];
             }
+            if (cls & C_SINGLE_BASE) {
+                rh_info |= RH_HIT;
+                if (!has_ac || (cls & C_AC_MISSING)) rh_info |= RH_SLOW;
+                rh_c += acval;
+                if (acval != 0) rh_info |= i < 8 ? (1u << i) : RH_SLOW;
+            }
             if (i == 0) {
                 hot |= cls;
                 ac0 = static_cast<int32_t>(acval);
@@ -564,6 +572,9 @@ struct Parser {
             c.blob.insert(c.blob.end(), ap, ap + al);
         }
         c.rec.push_back(RecHot{static_cast<uint32_t>(end), hot, static_cast<int32_t>(anv), ac0});
+        if (an_bad || ac_bad || rh_c > INT32_MAX || rh_c < INT32_MIN) rh_info |= RH_SLOW;
+        c.rng.push_back(RangeHot{static_cast<uint32_t>(end), rh_info, static_cast<int32_t>(anv),
+                                 static_cast<int32_t>((rh_info & RH_SLOW) ? 0 : rh_c)});
         c.fb_off.push_back(fb_row);
         c.x_lo.push_back(static_cast<uint32_t>(c.x_key.size()));
         return true;
@@ -628,6 +639,7 @@ void merge(sb_builder &b, VcfData &v, Local &L) {
     app(d.a0_key, s.a0_key);
     app(d.a0_len, s.a0_len);
     d.rec.reserve(d.rec.size() + nr);
+    app(d.rng, s.rng);
     d.vt.reserve(d.vt.size() + nr);
     std::string last_vt;
     uint32_t last_id = 0;

@@ -15,10 +15,11 @@ namespace sb {
 // q.hit_off, per-query totals into res and, for the sample path, a carrier
 // bitset per query into samples_out.
 // qidx (optional) lists the queries this launch covers (n of them); max_words
-// = 0 compiles out the sample path; nonneg selects the monotone call_count path.
+// = 0 compiles out the sample path; nonneg selects the monotone call_count path;
+// mode (MODE_*) picks the predicate specialisation every listed query fits.
 void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t n, bool nonneg, uint32_t max_words,
-                 const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out,
-                 hipStream_t s);
+                 int mode, const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits,
+                 uint64_t *samples_out, hipStream_t s);
 
 // summariseSlice: phase A = one workgroup per chunk of kSumChunk records
 // (chunk_slice[c] = its slice), reducing the records' (numVariants, numCalls)

@@ -199,13 +199,232 @@ __device__ int64_t fallback_count(const DStore &st, uint32_t r, const uint64_t *
     return n_match;
 }
 
+// ---------------------------------------------------------------- scan
+// What one record contributes to its slice query (search_variants.py:84-226):
+// hm = hit ALTs (bit k = ALT k), em = ALTs emitted as variant strings (bit =
+// label index; the GT fallback labels with alts[k+1], :223), c = its call
+// count contribution, anv = its all_alleles_count contribution, err = the
+// exception the reference raises at this record (SB_QERR_*).
+struct LaneOut {
+    int err;
+    uint64_t hm, em;
+    int64_t c, anv;
+};
+
+struct QView {  // per-wave query constants, specialised by MODE
+    uint32_t flags, ref_mode, alt_mode;
+    bool samples_variant, strict_unbound;
+    const uint8_t *qref, *qalt;
+    const uint64_t *subset;
+};
+
+// General evaluation of record r (RecHot h already loaded); extra ALTs and
+// hashed-key confirmations are loaded on demand.
+__device__ __forceinline__ LaneOut eval_record(const DStore &st, const QDev &Q, const QView &V, uint32_t r,
+                                            const RecHot h0) {
+    LaneOut o{0, 0, 0, 0, 0};
+    const uint32_t e = h0.end;
+    const uint32_t h = h0.hot;
+    bool pass = static_cast<int64_t>(e) >= Q.end_min && static_cast<int64_t>(e) <= Q.end_max;  // :90
+    if (pass) {
+        switch (V.ref_mode) {  // :94 / svs:88-91
+            case REF_ANY:
+                break;
+            case REF_EXACT: {
+                const uint64_t k = st.ref_key[r];
+                pass = k == Q.ref_key;
+                if (pass && (k >> 63)) pass = blob_eq_upper(st.blob, st.ref_off[r], e - st.pos[r] + 1, V.qref, Q.ref_len);
+                break;
+            }
+            case REF_WILD:
+                pass = ref_wild_match(st, r, e - st.pos[r] + 1, V.qref, Q.ref_len);
+                break;
+            case REF_NEVER:
+                pass = false;
+                break;
+            default:
+                o.err = static_cast<int>(Q.ref_err);
+                pass = false;
+                break;
+        }
+    }
+    if (pass && V.strict_unbound) {  // :101 in the unpatched reference
+        o.err = SB_QERR_UNBOUND_LOCAL;
+        pass = false;
+    }
+    if (!pass) return o;
+    uint32_t x0 = 0, nx = 0;
+    const int64_t ref_len = (V.alt_mode == ALT_VTYPE) ? static_cast<int64_t>(e) - st.pos[r] + 1 : 0;
+    {  // ALT 0: class bits live in RecHot::hot
+        bool ok;
+        int64_t len = 1;
+        if (V.alt_mode == ALT_N) {
+            ok = h & C_SINGLE_BASE;
+        } else if (V.alt_mode == ALT_EXACT) {
+            const uint64_t k = st.a0_key[r];
+            ok = k == Q.alt_key;
+            len = Q.alt_len;
+            if (ok && (k >> 63)) ok = blob_eq_upper(st.blob, st.a0_off[r], st.a0_len[r], V.qalt, Q.alt_len);
+        } else {
+            len = st.a0_len[r];
+            ok = vtype_hit(Q, st, h, len, ref_len);
+        }
+        if (ok && len >= Q.vmin && len <= Q.vmax) o.hm = 1;
+    }
+    if (h & H_MULTI) {  // ALTs 1..n-1 of multiallelic records
+        x0 = st.x_lo[r];
+        nx = st.x_lo[r + 1] - x0;
+        for (uint32_t k = 0; k < nx && k < 63; ++k) {
+            const uint32_t x = x0 + k;
+            const uint32_t cls = st.xrow[x].cls;
+            bool ok;
+            int64_t len = 1;
+            if (V.alt_mode == ALT_N) {
+                ok = cls & C_SINGLE_BASE;
+            } else if (V.alt_mode == ALT_EXACT) {
+                const uint64_t key = st.x_key[x];
+                ok = key == Q.alt_key;
+                len = Q.alt_len;
+                if (ok && (key >> 63)) ok = blob_eq_upper(st.blob, st.x_off[x], st.x_len[x], V.qalt, Q.alt_len);
+            } else {
+                len = st.x_len[x];
+                ok = vtype_hit(Q, st, cls, len, ref_len);
+            }
+            if (ok && len >= Q.vmin && len <= Q.vmax) o.hm |= 2ull << k;
+        }
+    }
+    if (!o.hm) return o;
+    const uint32_t na = 1 + nx;
+    const bool sub = V.samples_variant && (h & H_HAS_FB);
+    if (h & H_AN_BAD) {
+        o.err = SB_QERR_VALUE;  // :199
+    } else if (h & H_HAS_AC) {  // :205-214
+        if (h & H_AC_BAD) {
+            o.err = SB_QERR_VALUE;  // :206
+        } else {
+            for (uint64_t b = o.hm; b; b &= b - 1) {
+                const int k = ffs64(b);
+                const XRow xk = k ? st.xrow[x0 + k - 1] : XRow{h, h0.ac0};
+                if (xk.cls & C_AC_MISSING) o.err = SB_QERR_INDEX;  // :207
+                const int64_t v = xk.ac;
+                o.c += v;
+                if (v != 0) o.em |= 1ull << k;
+            }
+        }
+    } else {  // :215-226 genotype fallback, labelled alts[i] with 1-based i
+        for (uint64_t b = o.hm; b; b &= b - 1) {
+            const int k = ffs64(b);
+            const int64_t v = sub ? fallback_count(st, r, V.subset, Q.n_samples, k + 1)
+                                  : (k ? st.xrow[x0 + k - 1].ac : h0.ac0);
+            o.c += v;
+            if (v > 0) {
+                if (static_cast<uint32_t>(k + 1) >= na) o.err = SB_QERR_INDEX;  // :223
+                else o.em |= 1ull << (k + 1);
+            }
+        }
+    }
+    o.anv = (h & H_HAS_AN) ? h0.an : (sub ? fallback_count(st, r, V.subset, Q.n_samples, 0) : h0.an);
+    if (o.err) {
+        o.hm = 0;
+        o.em = 0;
+        o.c = 0;
+    }
+    return o;
+}
+
+struct ScanState {
+    int64_t carry = 0;      // running call_count (general path)
+    bool carry_nz = false;  // running call_count != 0 (non-negative path)
+    int64_t cc_acc = 0, an_acc = 0;  // per-lane partial sums, reduced once at the end
+    uint32_t n_out = 0;
+    bool exists = false;
+    int err_out = 0;
+};
+
+// The reference loop's order-dependent state over one 64-record chunk
+// (:229-254): running call_count, `if call_count:`, the include_details /
+// boolean early exits and the first exception, then the compacted emission
+// of variant strings (:209-213 / :222-225).  Returns the stop lane (kWave =
+// none); *collectm = hit lanes whose samples are collected (:233-236).
+template <bool NONNEG>
+__device__ __forceinline__ int chunk_tail(ScanState &S, const LaneOut &o, uint32_t r, bool stop_on_exists,
+                                          bool details, uint64_t *__restrict__ out, uint64_t *collectm) {
+    const int lane = lane_id();
+    const bool hit = o.hm != 0;
+    const uint64_t errm = __ballot(o.err != 0);
+    const uint64_t hitm = __ballot(hit);
+    int64_t cum = 0;
+    uint64_t trigm;  // hit lanes where the running call_count is non-zero
+    if constexpr (NONNEG) {
+        const uint64_t pm = __ballot(hit && o.c > 0);
+        trigm = S.carry_nz ? hitm : (pm ? (hitm & ~((1ull << ffs64(pm)) - 1ull)) : 0ull);
+    } else {
+        cum = S.carry + wave_incl_scan_i64(hit ? o.c : 0);
+        trigm = __ballot(hit && cum != 0);
+    }
+    const uint64_t stopm = errm | (stop_on_exists ? trigm : 0ull);
+    const int s = stopm ? ffs64(stopm) : kWave;
+    if (s < kWave && ((errm >> s) & 1ull)) {
+        S.err_out = __shfl(o.err, s, kWave);
+        *collectm = 0;
+        return s;
+    }
+    const uint64_t upto = (s >= kWave - 1) ? ~0ull : ((2ull << s) - 1ull);
+    const bool in = (upto >> lane) & 1ull;
+    const uint32_t cnt = (hit && in) ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
+    const uint64_t multi = __ballot(cnt > 1);
+    uint32_t pos0, total;
+    if (!multi) {
+        const uint64_t one = __ballot(cnt == 1);
+        pos0 = popc_below(one);
+        total = static_cast<uint32_t>(__popcll(one));
+    } else {
+        const uint32_t incl = wave_incl_scan_u32(cnt);
+        pos0 = incl - cnt;
+        total = __shfl(incl, kWave - 1, kWave);
+    }
+    if (cnt) {
+        uint64_t *dst = out + S.n_out + pos0;
+        for (uint64_t b = o.em; b; b &= b - 1)
+            *dst++ = static_cast<uint64_t>(r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
+    }
+    S.n_out += total;
+    // call_count and all_alleles_count: lanes up to the stop; the stop lane's
+    // AN only for the boolean break (after :244), not for :231
+    if (hit && in) S.cc_acc += o.c;
+    if (hit && (lane < s || (lane == s && details))) S.an_acc += o.anv;
+    S.exists = S.exists || ((trigm & upto) != 0ull);
+    if constexpr (NONNEG)
+        S.carry_nz = S.exists;
+    else
+        S.carry = shfl_i64(cum, s < kWave ? s : kWave - 1);
+    *collectm = trigm & upto;
+    return s;
+}
+
+template <bool NONNEG>
+__device__ __forceinline__ void finish_query(const ScanState &S, uint32_t q, uint32_t n_scanned, QRes *res) {
+    const int64_t call_count = NONNEG ? wave_sum_i64(S.cc_acc) : S.carry;
+    const int64_t an_sum = wave_sum_i64(S.an_acc);
+    if (lane_id() == 0) {
+        QRes o;
+        o.error = S.err_out;
+        o.exists = S.exists ? 1 : 0;
+        o.call_count = call_count;
+        o.all_alleles_count = an_sum;
+        o.n_hits = S.err_out ? 0u : S.n_out;
+        o.n_scanned = n_scanned;
+        res[q] = o;
+    }
+}
+
 // NACC: 64-bit sample-bitset words per lane (0 = no query in this launch
 // collects samples); NONNEG: every AC in the store is >= 0, so the running
-// call_count is monotone and `if call_count:` reduces to ballots.
-// <= 80 SGPRs keeps 8 workgroups per CU resident (MI355X_MICROARCH.md,
-// Residency: 800 / (sgpr + 16)); the surplus spills to VGPR lanes, not scratch.
-template <int NACC, bool NONNEG>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void scan_kernel(
+// call_count is monotone and `if call_count:` reduces to ballots.  MODE_EXACT
+// specialises the predicates for REF/ALT point queries; MODE_GENERAL handles
+// every payload (variantType, samples variant, strict mode, wildcards).
+template <int NACC, bool NONNEG, int MODE>
+__global__ __launch_bounds__(kBlock) void scan_kernel(
     DStore st, const QDev *__restrict__ qs, const uint32_t *__restrict__ qidx, uint32_t nq,
     const uint8_t *__restrict__ qbytes, const uint64_t *__restrict__ subsets, QRes *__restrict__ res,
     uint64_t *__restrict__ hits, uint64_t *__restrict__ samples_out) {
@@ -214,26 +433,24 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void s
     const uint32_t q = qidx ? uniform(qidx[w]) : w;
     const int lane = lane_id();
     const QDev &Q = qs[q];
-    const uint32_t flags = Q.flags;
-    const bool details = flags & F_DETAILS;
-    const bool samples_variant = flags & F_SAMPLES_VARIANT;
-    const bool collect = NACC > 0 && (flags & F_COLLECT) && details;
-    const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
-    constexpr bool nonneg = NONNEG;
-    const uint8_t *qref = qbytes + Q.qbytes_off;
-    const uint8_t *qalt = qref + Q.ref_len;
-    const uint64_t *subset = (Q.subset_off != ~0ull) ? subsets + Q.subset_off : nullptr;
+    constexpr bool kGeneral = MODE == MODE_GENERAL;
+    QView V;
+    V.flags = Q.flags;
+    V.ref_mode = MODE == MODE_EXACT ? REF_EXACT : Q.ref_mode;
+    V.alt_mode = MODE == MODE_EXACT ? ALT_EXACT : Q.alt_mode;
+    V.samples_variant = kGeneral && (V.flags & F_SAMPLES_VARIANT);
+    V.strict_unbound = kGeneral && (V.flags & F_STRICT_UNBOUND);
+    V.qref = qbytes + Q.qbytes_off;
+    V.qalt = V.qref + Q.ref_len;
+    V.subset = (Q.subset_off != ~0ull) ? subsets + Q.subset_off : nullptr;
+    const bool details = V.flags & F_DETAILS;
+    const bool collect = NACC > 0 && (V.flags & F_COLLECT) && details;
+    const bool stop_on_exists = !details || (V.flags & F_BOOL_BREAK);
 
-    // ---- 1. bounds of the slice: a <= POS <= b (:84-85)
-    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
-    if (!(flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
+    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;  // a <= POS <= b (:84-85)
+    if (!(V.flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
 
-    int64_t carry = 0;      // running call_count (general path)
-    bool carry_nz = false;  // running call_count != 0 (non-negative path)
-    int64_t cc_acc = 0, an_acc = 0;  // per-lane partial sums, reduced once at the end
-    uint32_t n_out = 0;
-    bool exists = false;
-    int err_out = 0;
+    ScanState S;
     uint64_t acc[NACC > 0 ? NACC : 1];
 #pragma unroll
     for (int j = 0; j < (NACC > 0 ? NACC : 1); ++j) acc[j] = 0;
@@ -241,181 +458,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void s
 
     RecHot cur = {0, 0, 0, 0}, nxt = {0, 0, 0, 0};
     if (lo + static_cast<uint32_t>(lane) < hi) cur = st.rec[lo + lane];
-    if (lo + kWave + static_cast<uint32_t>(lane) < hi) nxt = st.rec[lo + kWave + lane];
     for (uint32_t base = lo; base < hi; base += kWave) {
         const uint32_t r = base + static_cast<uint32_t>(lane);
-        RecHot nxt2 = {0, 0, 0, 0};
-        if (r + 2 * kWave < hi) nxt2 = st.rec[r + 2 * kWave];  // two chunks in flight
-        int err = 0;
-        uint64_t hm = 0, em = 0;
-        int64_t c = 0, anv = 0;
-        if (r < hi) {
-            const uint32_t e = cur.end;
-            const uint32_t h = cur.hot;
-            bool pass = static_cast<int64_t>(e) >= Q.end_min && static_cast<int64_t>(e) <= Q.end_max;  // :90
-            if (pass) {
-                switch (Q.ref_mode) {  // :94 / svs:88-91
-                    case REF_ANY:
-                        break;
-                    case REF_EXACT: {
-                        const uint64_t k = st.ref_key[r];
-                        pass = k == Q.ref_key;
-                        if (pass && (k >> 63))
-                            pass = blob_eq_upper(st.blob, st.ref_off[r], e - st.pos[r] + 1, qref, Q.ref_len);
-                        break;
-                    }
-                    case REF_WILD:
-                        pass = ref_wild_match(st, r, e - st.pos[r] + 1, qref, Q.ref_len);
-                        break;
-                    case REF_NEVER:
-                        pass = false;
-                        break;
-                    default:
-                        err = static_cast<int>(Q.ref_err);
-                        pass = false;
-                        break;
-                }
-            }
-            if (pass && (flags & F_STRICT_UNBOUND)) {  // :101 in the unpatched reference
-                err = SB_QERR_UNBOUND_LOCAL;
-                pass = false;
-            }
-            uint32_t x0 = 0, nx = 0;
-            if (pass) {
-                const int64_t ref_len = (Q.alt_mode == ALT_VTYPE) ? static_cast<int64_t>(e) - st.pos[r] + 1 : 0;
-                {  // ALT 0: class bits live in RecHot::hot
-                    bool ok;
-                    int64_t len = 1;
-                    if (Q.alt_mode == ALT_N) {
-                        ok = h & C_SINGLE_BASE;
-                    } else if (Q.alt_mode == ALT_EXACT) {
-                        const uint64_t k = st.a0_key[r];
-                        ok = k == Q.alt_key;
-                        len = Q.alt_len;
-                        if (ok && (k >> 63)) ok = blob_eq_upper(st.blob, st.a0_off[r], st.a0_len[r], qalt, Q.alt_len);
-                    } else {
-                        len = st.a0_len[r];
-                        ok = vtype_hit(Q, st, h, len, ref_len);
-                    }
-                    if (ok && len >= Q.vmin && len <= Q.vmax) hm = 1;
-                }
-                if (h & H_MULTI) {  // ALTs 1..n-1 of multiallelic records
-                    x0 = st.x_lo[r];
-                    nx = st.x_lo[r + 1] - x0;
-                    for (uint32_t k = 0; k < nx && k < 63; ++k) {
-                        const uint32_t x = x0 + k;
-                        const uint32_t cls = st.x_cls[x];
-                        bool ok;
-                        int64_t len = 1;
-                        if (Q.alt_mode == ALT_N) {
-                            ok = cls & C_SINGLE_BASE;
-                        } else if (Q.alt_mode == ALT_EXACT) {
-                            const uint64_t key = st.x_key[x];
-                            ok = key == Q.alt_key;
-                            len = Q.alt_len;
-                            if (ok && (key >> 63)) ok = blob_eq_upper(st.blob, st.x_off[x], st.x_len[x], qalt, Q.alt_len);
-                        } else {
-                            len = st.x_len[x];
-                            ok = vtype_hit(Q, st, cls, len, ref_len);
-                        }
-                        if (ok && len >= Q.vmin && len <= Q.vmax) hm |= 2ull << k;
-                    }
-                }
-            }
-            if (hm) {
-                const uint32_t na = 1 + nx;
-                const bool sub = samples_variant && (h & H_HAS_FB);
-                if (h & H_AN_BAD) {
-                    err = SB_QERR_VALUE;  // :199
-                } else if (h & H_HAS_AC) {  // :205-214
-                    if (h & H_AC_BAD) {
-                        err = SB_QERR_VALUE;  // :206
-                    } else {
-                        for (uint64_t b = hm; b; b &= b - 1) {
-                            const int k = ffs64(b);
-                            const uint32_t cls = k ? st.x_cls[x0 + k - 1] : h;
-                            if (cls & C_AC_MISSING) err = SB_QERR_INDEX;  // :207
-                            const int64_t v = k ? st.x_ac[x0 + k - 1] : cur.ac0;
-                            c += v;
-                            if (v != 0) em |= 1ull << k;
-                        }
-                    }
-                } else {  // :215-226 genotype fallback, labelled alts[i] with 1-based i
-                    for (uint64_t b = hm; b; b &= b - 1) {
-                        const int k = ffs64(b);
-                        const int64_t v = sub ? fallback_count(st, r, subset, Q.n_samples, k + 1)
-                                              : (k ? st.x_ac[x0 + k - 1] : cur.ac0);
-                        c += v;
-                        if (v > 0) {
-                            if (static_cast<uint32_t>(k + 1) >= na) err = SB_QERR_INDEX;  // :223
-                            else em |= 1ull << (k + 1);
-                        }
-                    }
-                }
-                anv = (h & H_HAS_AN) ? cur.an : (sub ? fallback_count(st, r, subset, Q.n_samples, 0) : cur.an);
-                if (err) {
-                    hm = 0;
-                    em = 0;
-                    c = 0;
-                }
-            }
-        }
-        // ---- 3. order-dependent loop state (:229-254)
-        const bool hit = hm != 0;
-        const uint64_t errm = __ballot(err != 0);
-        const uint64_t hitm = __ballot(hit);
-        int64_t cum = 0;
-        uint64_t trigm;  // hit lanes where the running call_count is non-zero
-        if constexpr (NONNEG) {
-            const uint64_t pm = __ballot(hit && c > 0);
-            trigm = carry_nz ? hitm : (pm ? (hitm & ~((1ull << ffs64(pm)) - 1ull)) : 0ull);
-        } else {
-            cum = carry + wave_incl_scan_i64(hit ? c : 0);
-            trigm = __ballot(hit && cum != 0);
-        }
-        const uint64_t stopm = errm | (stop_on_exists ? trigm : 0ull);
-        const int s = stopm ? ffs64(stopm) : kWave;
-        if (s < kWave && ((errm >> s) & 1ull)) {
-            err_out = __shfl(err, s, kWave);
-            break;
-        }
-        const uint64_t upto = (s >= kWave - 1) ? ~0ull : ((2ull << s) - 1ull);
-        const bool in = (upto >> lane) & 1ull;
-        // ---- 4. compacted emission of variant strings (:209-213 / :222-225)
-        const uint32_t cnt = (hit && in) ? static_cast<uint32_t>(__popcll(em)) : 0u;
-        const uint64_t multi = __ballot(cnt > 1);
-        uint32_t pos0, total;
-        if (!multi) {
-            const uint64_t one = __ballot(cnt == 1);
-            pos0 = popc_below(one);
-            total = static_cast<uint32_t>(__popcll(one));
-        } else {
-            const uint32_t incl = wave_incl_scan_u32(cnt);
-            pos0 = incl - cnt;
-            total = __shfl(incl, kWave - 1, kWave);
-        }
-        if (cnt) {
-            uint64_t *dst = out + n_out + pos0;
-            for (uint64_t b = em; b; b &= b - 1)
-                *dst++ = static_cast<uint64_t>(r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
-        }
-        n_out += total;
-        // call_count and all_alleles_count: lanes up to the stop; the stop lane's
-        // AN only for the boolean break (after :244), not for :231
-        if (hit && in) cc_acc += c;
-        if (hit && (lane < s || (lane == s && details))) an_acc += anv;
-        exists = exists || ((trigm & upto) != 0ull);
-        if constexpr (NONNEG)
-            carry_nz = exists;
-        else
-            carry = shfl_i64(cum, s < kWave ? s : kWave - 1);
+        if (r + kWave < hi) nxt = st.rec[r + kWave];
+        LaneOut o{0, 0, 0, 0, 0};
+        if (r < hi) o = eval_record(st, Q, V, r, cur);
+        uint64_t cm;
+        const int s = chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm);
+        if (s < kWave && S.err_out) break;
         // sample path (:233-236): OR the carrier planes of every hit allele
         if constexpr (NACC > 0) if (collect) {
-            uint64_t cm = trigm & upto;
             while (cm) {
                 const int L = ffs64(cm);
                 cm &= cm - 1;
-                const uint64_t hml = static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(hm), L));
+                const uint64_t hml = static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(o.hm), L));
                 const uint32_t rl = static_cast<uint32_t>(__shfl(static_cast<int>(r), L, kWave));
                 const uint32_t xl = (hml >> 1) ? st.x_lo[rl] : 0u;
                 for (uint64_t b = hml; b; b &= b - 1) {
@@ -424,40 +480,93 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_num_sgpr(80))) void s
                                            : Q.plane0_base + static_cast<uint64_t>(rl - Q.rec_base) * Q.words;
 #pragma unroll
                     for (int j = 0; j < NACC; ++j) {
-                        const uint32_t w = static_cast<uint32_t>(lane) + 64u * j;
-                        if (w < Q.words) acc[j] |= st.planes[row + w];
+                        const uint32_t wd = static_cast<uint32_t>(lane) + 64u * j;
+                        if (wd < Q.words) acc[j] |= st.planes[row + wd];
                     }
                 }
             }
         }
         cur = nxt;
-        nxt = nxt2;
         if (s < kWave) break;
     }
-
-    const int64_t call_count = nonneg ? wave_sum_i64(cc_acc) : carry;
-    const int64_t an_sum = wave_sum_i64(an_acc);
-    if (lane == 0) {
-        QRes o;
-        o.error = err_out;
-        o.exists = exists ? 1 : 0;
-        o.call_count = call_count;
-        o.all_alleles_count = an_sum;
-        o.n_hits = err_out ? 0u : n_out;
-        o.n_scanned = hi - lo;
-        res[q] = o;
-    }
+    finish_query<NONNEG>(S, q, hi - lo, res);
     if constexpr (NACC > 0) if (collect && Q.samples_out_off != ~0ull) {
 #pragma unroll
         for (int j = 0; j < NACC; ++j) {
-            const uint32_t w = static_cast<uint32_t>(lane) + 64u * j;
-            if (w < Q.words) {
-                uint64_t v = err_out ? 0ull : acc[j];
-                if (subset) v &= subset[w];
-                samples_out[Q.samples_out_off + w] = v;
+            const uint32_t wd = static_cast<uint32_t>(lane) + 64u * j;
+            if (wd < Q.words) {
+                uint64_t v = S.err_out ? 0ull : acc[j];
+                if (V.subset) v &= V.subset[wd];
+                samples_out[Q.samples_out_off + wd] = v;
             }
         }
     }
+}
+
+// MODE_RANGE_N: referenceBases 'N' + alternateBases 'N' range queries (the
+// bulk of Beacon traffic).  Every per-record quantity such a query needs is
+// query-independent and sits in one 16-byte RangeHot word (devtypes.hpp), so
+// a record costs one coalesced dwordx4 load and a handful of VALU ops; records
+// flagged RH_SLOW (no AC, int() failures, > 8 ALTs ...) take eval_record.
+// The stream is unrolled two chunks per trip so the prefetched words rotate
+// by register name, never by copy (a copy of an in-flight load would wait).
+template <bool NONNEG>
+__global__ __launch_bounds__(kBlock) void range_n_kernel(DStore st, const QDev *__restrict__ qs,
+                                                         const uint32_t *__restrict__ qidx, uint32_t nq,
+                                                         QRes *__restrict__ res, uint64_t *__restrict__ hits) {
+    const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    if (w >= nq) return;
+    const uint32_t q = qidx ? uniform(qidx[w]) : w;
+    const int lane = lane_id();
+    const QDev &Q = qs[q];
+    const uint32_t flags = Q.flags;
+    const bool details = flags & F_DETAILS;
+    const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
+    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
+    if (!(flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
+    ScanState S;
+    // len(alt) = 1 for every ALT an 'N' query can hit (:174)
+    const bool len_ok = Q.vmin <= 1 && Q.vmax >= 1;
+    const uint32_t emin = Q.end_min < 0 ? 0u : Q.end_min > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_min);
+    const uint32_t emax = Q.end_max < 0 ? 0u : Q.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_max);
+    const bool end_void = Q.end_max < 0 || Q.end_min > 0xffffffffll || Q.end_min > Q.end_max;
+    const uint32_t hit_bits = (len_ok && !end_void) ? RH_HIT : 0u;
+    uint64_t *out = hits + Q.hit_off;
+    QView V{flags, REF_ANY, ALT_N, false, false, nullptr, nullptr, nullptr};
+
+    auto chunk = [&](uint32_t base, const RangeHot h) -> bool {  // true = keep going
+        const uint32_t r = base + static_cast<uint32_t>(lane);
+        const bool cand = r < hi && (h.info & hit_bits) && h.end >= emin && h.end <= emax;
+        LaneOut o{0, 0, 0, 0, 0};
+        if (cand) {
+            o.hm = 1;
+            o.em = h.info & RH_EMIT_MASK;
+            o.c = h.c;
+            o.anv = h.an;
+        }
+        if (__ballot(cand && (h.info & RH_SLOW))) {
+            if (cand && (h.info & RH_SLOW)) o = eval_record(st, Q, V, r, st.rec[r]);
+        }
+        uint64_t cm;
+        return chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) >= kWave;
+    };
+    const uint32_t l0 = lo + static_cast<uint32_t>(lane);
+    RangeHot a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+    if (l0 < hi) a = st.rng[l0];
+    if (l0 + kWave < hi) b = st.rng[l0 + kWave];
+    for (uint32_t base = lo; base < hi; base += 2 * kWave) {
+        const uint32_t r = base + static_cast<uint32_t>(lane);
+        RangeHot c2 = {0, 0, 0, 0};
+        if (r + 2 * kWave < hi) c2 = st.rng[r + 2 * kWave];
+        if (!chunk(base, a)) break;
+        if (base + kWave >= hi) break;
+        RangeHot d2 = {0, 0, 0, 0};
+        if (r + 3 * kWave < hi) d2 = st.rng[r + 3 * kWave];
+        if (!chunk(base + kWave, b)) break;
+        a = c2;
+        b = d2;
+    }
+    finish_query<NONNEG>(S, q, hi - lo, res);
 }
 
 // Gather each query's hits from its planned region into a dense array
@@ -651,29 +760,35 @@ void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, u
 }
 
 template <bool NONNEG>
-void launch_variant(int nacc, dim3 g, const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t n,
+void launch_variant(int nacc, int mode, dim3 g, const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t n,
                     const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out,
                     hipStream_t s) {
     const dim3 b(kBlock);
-    switch (nacc) {
-        case 0: hipLaunchKernelGGL((scan_kernel<0, NONNEG>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out); break;
-        case 1: hipLaunchKernelGGL((scan_kernel<1, NONNEG>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out); break;
-        case 4: hipLaunchKernelGGL((scan_kernel<4, NONNEG>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out); break;
-        default: hipLaunchKernelGGL((scan_kernel<16, NONNEG>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out); break;
+    if (nacc == 0 && mode == MODE_RANGE_N) {
+        hipLaunchKernelGGL((range_n_kernel<NONNEG>), g, b, 0, s, st, q, qidx, n, res, hits);
+        return;
     }
+#define SB_SCAN(NA, MO) hipLaunchKernelGGL((scan_kernel<NA, NONNEG, MO>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out)
+    if (nacc == 0 && mode == MODE_EXACT) { SB_SCAN(0, MODE_EXACT); return; }
+    switch (nacc) {
+        case 0: SB_SCAN(0, MODE_GENERAL); break;
+        case 1: SB_SCAN(1, MODE_GENERAL); break;
+        case 4: SB_SCAN(4, MODE_GENERAL); break;
+        default: SB_SCAN(16, MODE_GENERAL); break;
+    }
+#undef SB_SCAN
 }
 
 void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t n, bool nonneg, uint32_t max_words,
-                 const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out,
-                 hipStream_t s) {
+                 int mode, const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits,
+                 uint64_t *samples_out, hipStream_t s) {
     if (!n) return;
     const int nacc = max_words == 0 ? 0 : max_words <= 64 ? 1 : max_words <= 256 ? 4 : 16;
     const dim3 g(blocks_for(n));
     if (nonneg)
-        launch_variant<true>(nacc, g, st, q, qidx, n, qbytes, subsets, res, hits, samples_out, s);
+        launch_variant<true>(nacc, mode, g, st, q, qidx, n, qbytes, subsets, res, hits, samples_out, s);
     else
-        launch_variant<false>(nacc, g, st, q, qidx, n, qbytes, subsets, res, hits, samples_out, s);
+        launch_variant<false>(nacc, mode, g, st, q, qidx, n, qbytes, subsets, res, hits, samples_out, s);
 }
-
 
 }  // namespace sb

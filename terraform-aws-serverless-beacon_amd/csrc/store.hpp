@@ -26,6 +26,7 @@ struct Segment {  // one (vcf, contig), position-sorted, contiguous records
 struct VcfCols {
     // record-indexed
     std::vector<RecHot> rec;
+    std::vector<RangeHot> rng;
     std::vector<uint32_t> pos, a0_len, x_lo{0};
     std::vector<uint64_t> ref_key, a0_key, ref_off, a0_off;
     std::vector<int64_t> fb_off;

@@ -13,6 +13,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -52,6 +53,7 @@ struct Gen {
     // probability `share`, otherwise from this member's own seed
     uint64_t own_seed = 0;
     double share = 1.0;
+    double multi_frac = 0.015;  // multiallelic share of all records (SBS_MULTI_FRAC overrides; experiments)
     uint64_t rec_seed(uint64_t i) const {
         if (share >= 1.0) return seed;
         Rng r(own_seed, i, 7);
@@ -102,7 +104,7 @@ void make_record(const Gen &g, uint64_t i, Rec &r) {
         const uint32_t b = rng.below(4);
         r.ref.assign(1, kBase[b]);
         uint32_t na = 1;
-        if (rng.uni() < 0.015 / 0.968) na = 2 + rng.below(2);
+        if (rng.uni() < g.multi_frac / 0.968) na = 2 + rng.below(2);
         uint32_t used = 1u << b;
         for (uint32_t k = 0; k < na; ++k) {
             uint32_t a;
@@ -247,6 +249,7 @@ void *sbs_new(uint64_t seed, uint64_t n_records, uint32_t n_samples, uint32_t st
     g->start = start_pos;
     g->mean_gap = mean_gap;
     g->contig = contig;
+    if (const char *e = getenv("SBS_MULTI_FRAC")) g->multi_frac = atof(e);
     g->pos.resize(n_records);
     uint64_t p = start_pos;
     const double lq = std::log(1.0 - 1.0 / mean_gap);
