@@ -5,8 +5,12 @@ Workload (BASELINE.json configs[1]): a 1000G chr22-
 shape store — 1,103,547 records x 2,504 samples, seed 22 — and 10,000 Beacon
 requests (5,000 range + 5,000 point ref/alt, seed 1022 + rank), sliced into
 PerformQueryPayloads exactly as splitQuery does.  One step = one device pass
-of the whole batch (bounds -> capacity scan -> range scan -> hit compaction)
-with the queries already resident in HBM.
+of the whole batch with the queries already resident in HBM: the host plans
+each slice query's private output region once (sb_batch_prepare), and a step
+launches one range-scan kernel per query class (range_n_kernel for ref=alt='N'
+range requests, scan_kernel<EXACT> for point ref/alt requests), each doing the
+coarse-index lower_bound, interval/ref/alt filters, wave-prefix-sum call
+counts and ballot compaction of hits in a single pass.
 
 Multi-GPU (`torch.distributed.run`, one rank per GPU): every rank holds its
 own store replica and answers its own 10k requests — the slices are
@@ -156,7 +160,8 @@ def main():
         'device_ms_per_step': {'scan_kernel': round(timing['scan_ms'], 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                     'kernel': 'scan_kernel', 'algorithmic_bytes_per_launch': scan_bytes},
+                     'kernel': 'query step: range_n_kernel + scan_kernel<EXACT> (HIP events around both launches)',
+                     'algorithmic_bytes_per_launch': scan_bytes},
         'cpu_baseline': cpu,
         'parity_sample': parity,
         'ingest_s': round(t_ingest, 2),

@@ -13,5 +13,5 @@ step() {  # name, limit, command...
 cd /tmp
 step pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_fetch -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline
 step pmc_write 900 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_write -o run -- python3 $R/bench.py --steps 5 --warmup 1 --no-cpu-baseline
-cd $R && python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write
+cd $R && python3 tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write --out gpurun_out/traffic.json
 exit 0

@@ -1,50 +1,83 @@
-"""Fold rocprofv3 FETCH_SIZE / WRITE_SIZE passes of bench.py into
-profiles/traffic.json: average memory-side bytes per scan_kernel dispatch.
+#!/usr/bin/env python3
+"""Fold two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) of a short
+bench.py run into profiles/traffic.json: HBM-side bytes per step of the
+timed query phase (range_n_kernel + scan_kernel launches).
 
-MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts 64 B per L2 memory-side
-read request, i.e. exactly half the bytes of a 16-B/lane streaming read —
-doubled here; WRITE_SIZE is exact for 16-B/lane streaming stores.  Both
-count Infinity-Cache hits (the config-2 scan columns fit in the 256 MB
-L3), so this is L2->fabric traffic, an upper bound on HBM bytes.  Units: the
-counters report KB (1024 B)."""
+Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE/WRITE_SIZE are
+reported in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
+coalesced streaming read, so it is doubled.  Both counters include
+Infinity-Cache hits (they are L2 memory-side request counters).
+
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR [--out profiles/traffic.json]
+"""
+from __future__ import annotations
+
+import argparse
 import csv
 import glob
 import json
 import os
+import re
 import sys
 
+PHASE = re.compile(r'(range_n_kernel|scan_kernel)')
 
-def per_dispatch(d, counter, kernel='scan_kernel'):
+
+def load(d, counter):
     files = glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True)
-    vals = {}
+    if not files:
+        sys.exit(f'no counter_collection.csv under {d}')
+    per = {}  # kernel name -> list of values in dispatch order
     for f in files:
-        for r in csv.DictReader(open(f)):
-            if kernel in r.get('Kernel_Name', '') and r.get('Counter_Name') == counter:
-                key = r.get('Dispatch_Id') or r.get('Correlation_Id')
-                vals[key] = vals.get(key, 0.0) + float(r['Counter_Value'])
-    return list(vals.values())
+        with open(f) as fh:
+            for row in csv.DictReader(fh):
+                if row['Counter_Name'] != counter:
+                    continue
+                name = row['Kernel_Name']
+                if not PHASE.search(name):
+                    continue
+                per.setdefault(name, []).append((int(row['Dispatch_Id']), float(row['Counter_Value'])))
+    return {k: [v for _, v in sorted(x)] for k, x in per.items()}
 
 
-def main(fetch_dir, write_dir):
-    f = per_dispatch(fetch_dir, 'FETCH_SIZE')
-    w = per_dispatch(write_dir, 'WRITE_SIZE')
-    if not f or not w:
-        print('no scan_kernel dispatches found', file=sys.stderr)
-        return 1
-    fb = 2 * 1024 * sum(f) / len(f)
-    wb = 1024 * sum(w) / len(w)
-    bench = json.load(open(os.path.join(os.path.dirname(fetch_dir), 'bench.json'))) if os.path.exists(
-        os.path.join(os.path.dirname(fetch_dir), 'bench.json')) else {}
-    out = {'records': 1103547, 'requests': 10000, 'kernel': 'scan_kernel', 'dispatches': [len(f), len(w)],
-           'fetch_bytes_per_launch': fb, 'write_bytes_per_launch': wb,
-           'scan_kernel_hbm_bytes_per_launch': fb + wb,
-           'method': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), FETCH_SIZE x2 (gfx950 '
-                     '16B/lane streaming correction), KB->B; includes Infinity-Cache hits'}
-    os.makedirs('profiles', exist_ok=True)
-    json.dump(out, open('profiles/traffic.json', 'w'), indent=1)
-    print(json.dumps(out))
-    return 0
+def short(name):
+    m = re.search(r'(\w+_kernel<[^>]*>|\w+_kernel)', name)
+    return m.group(1) if m else name
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('fetch_dir')
+    ap.add_argument('write_dir')
+    ap.add_argument('--out', default='profiles/traffic.json')
+    ap.add_argument('--records', type=int, default=1103547)
+    ap.add_argument('--requests', type=int, default=10000)
+    a = ap.parse_args()
+    fetch = load(a.fetch_dir, 'FETCH_SIZE')
+    write = load(a.write_dir, 'WRITE_SIZE')
+    kernels = {}
+    step_bytes = 0.0
+    for name in sorted(set(fetch) | set(write)):
+        f = fetch.get(name, [])
+        w = write.get(name, [])
+        fb = 2.0 * 1024.0 * sum(f) / max(1, len(f))   # gfx950 streaming-read correction, KiB -> B
+        wb = 1024.0 * sum(w) / max(1, len(w))
+        kernels[short(name)] = {'dispatches': [len(f), len(w)], 'fetch_bytes_per_launch': fb,
+                                'write_bytes_per_launch': wb, 'hbm_bytes_per_launch': fb + wb}
+        step_bytes += fb + wb
+    out = {
+        'records': a.records,
+        'requests': a.requests,
+        'phase': 'query step = one launch of each kernel below (range_n_kernel + scan_kernel<EXACT>)',
+        'kernels': kernels,
+        'scan_kernel_hbm_bytes_per_launch': step_bytes,
+        'method': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, kernel trace only), '
+                  'FETCH_SIZE x2 (gfx950 16B/lane streaming correction), KiB->B; includes Infinity-Cache hits',
+    }
+    with open(a.out, 'w') as fh:
+        json.dump(out, fh, indent=1)
+    print(json.dumps(out, indent=1))
 
 
 if __name__ == '__main__':
-    sys.exit(main(*sys.argv[1:3]))
+    main()
