@@ -56,11 +56,19 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--parity-requests', type=int, default=300,
                     help='requests re-checked against the C oracle after timing (rank 0)')
+    ap.add_argument('--workload', choices=['chr22', 'genome'], default='chr22',
+                    help='chr22: config 2 (default; replicas across GPUs). genome: config 3 (whole-genome store '
+                         'sharded by contig across the GPUs, request rows gathered to rank 0 over RCCL)')
+    ap.add_argument('--genome-records', type=int, default=85_000_000)
+    ap.add_argument('--genome-requests', type=int, default=1_000_000)
     return ap.parse_args()
 
 
 def main():
     args = parse()
+    if args.workload == 'genome':
+        from bench_genome import main_genome
+        return main_genome(args)
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
@@ -193,26 +201,12 @@ def cpu_baseline_and_parity(args, gen, reqs, payloads, owner, rs):
             order.append(k)
         if nr + k < len(reqs):
             order.append(nr + k)
-    # calibrate on a small prefix, then size the sample to ~cpu_seconds
-    def run(req_ids):
-        pl = [payloads[j] for r in req_ids for j in by_req[r]]
-        t = time.perf_counter()
-        res = orc.perform_query_batch(pl, patched=True, threads=threads, want_results=False)
-        return time.perf_counter() - t, len(pl), res
-    dt, _, _ = run(order[:100])
-    if dt * len(order) / 100 > args.cpu_seconds:  # bigger than the budget: a prefix sample
-        m = int(min(len(order), max(100, 100 * args.cpu_seconds / max(dt, 1e-6))))
-        dt, npl, _ = run(order[:m])
-        passes, done = 1, m
-        sample = f'first {m} of {len(reqs)} requests (interleaved range/point; {npl} slice payloads)'
-    else:  # the whole workload is cheaper than the budget: repeat full passes
-        total, passes, npl = 0.0, 0, 0
-        while total < args.cpu_seconds and passes < 10000:
-            d, npl, _ = run(order)
-            total += d
-            passes += 1
-        dt, done = total, passes * len(order)
-        sample = f'all {len(reqs)} requests ({npl} slice payloads) x {passes} passes'
+    # the whole request set, payloads converted once; C time only, repeated
+    # passes until ~cpu_seconds (the oracle takes no Python per query)
+    pl = [payloads[j] for r in order for j in by_req[r]]
+    dt, passes = orc.time_batch(pl, patched=True, threads=threads, min_seconds=args.cpu_seconds)
+    done = passes * len(order)
+    sample = f'all {len(reqs)} requests ({len(pl)} slice payloads) x {passes} passes'
     cpu = {'value': round(done / dt, 1), 'unit': 'requests/s', 'cores': threads, 'kind': 'port',
            'sample': sample + f' through oracle/sbeacon_oracle.c (CPU restatement of search_variants.py), '
                               f'OpenMP x{threads}, sites-only VCF text (config-2 queries read no GT)',

@@ -235,6 +235,27 @@ int sb_batch_sync(sb_batch *b);              /* wait for the store stream */
 int sb_batch_last_timing(const sb_batch *b, double *total_ms, double *scan_ms, double *bounds_ms);
 int sb_batch_get_stats(const sb_batch *b, sb_batch_stats *out);
 int sb_batch_fetch(sb_batch *b, sb_result_set **out); /* D2H + host views */
+
+/* ---- per-request reduction (sharded fan-out) -------------------------------
+ * The route-level aggregation of lambda/getGenomicVariants/route_g_variants.py
+ * :144-171 (exists = OR over the request's performQuery responses; the
+ * counts summed) for the slice queries one store (shard) holds, so that a
+ * request whose slices live on several GPUs is answered by summing the
+ * shards' rows (an RCCL reduce / gather).  owner[i] = row of query i (rows are
+ * the caller's requests, 0 <= owner < n_rows, non-decreasing in query order).
+ * sb_batch_reduce_requests enqueues, on the store's stream after the
+ * preceding sb_batch_run, n_rows sb_request_partial rows into dev_out — a
+ * device pointer on the store's device (e.g. a torch tensor's data_ptr);
+ * sb_batch_sync waits for it.  Rows without a query are zero. */
+typedef struct {
+    int64_t exists;            /* slices whose response has exists = True */
+    int64_t n_variants;        /* variant strings emitted (hits) */
+    int64_t call_count;
+    int64_t all_alleles_count;
+    int64_t errors;            /* slices whose performQuery raised */
+} sb_request_partial;
+int sb_batch_set_owners(sb_batch *b, const uint32_t *owner, size_t nq, uint32_t n_rows);
+int sb_batch_reduce_requests(sb_batch *b, void *dev_out);
 void sb_batch_free(sb_batch *b);
 
 #ifdef __cplusplus

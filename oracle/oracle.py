@@ -159,6 +159,30 @@ class OracleVcf:
             lib().orc_result_free(C.byref(res[i]))
         return out
 
+    def time_batch(self, payloads, patched=False, threads=0, min_seconds=0.0, max_passes=10000):
+        """CPU-baseline timing: the payloads are converted once, then the C
+        restatement runs over the whole batch (OpenMP x threads) pass after
+        pass until min_seconds of C time have accumulated.  Returns
+        (seconds inside the C calls, passes)."""
+        import time
+        n = len(payloads)
+        arr = (OrcQuery * n)()
+        keep = []
+        for i, p in enumerate(payloads):
+            q, k = make_query(p, patched)
+            arr[i] = q
+            keep.append(k)
+        res = (OrcResult * n)()
+        total, passes = 0.0, 0
+        while passes < max_passes and (passes == 0 or total < min_seconds):
+            t = time.perf_counter()
+            lib().orc_query_batch(self.h, arr, n, res, int(threads))
+            total += time.perf_counter() - t
+            passes += 1
+            for i in range(n):
+                lib().orc_result_free(C.byref(res[i]))
+        return total, passes
+
     def records_in_region(self, region: str) -> int:
         return lib().orc_records_in_region(self.h, region.encode())
 

@@ -172,6 +172,9 @@ struct sb_batch {
     };
     std::vector<Group> groups;
     bool nonneg = true;
+    // per-request rows (sb_batch_set_owners): seg = n_rows + 1 query offsets
+    uint32_t n_rows = 0;
+    DevMem seg, herr;
     // one event pair per run since the last sync; sync() averages them
     std::vector<std::array<hipEvent_t, 2>> ev;
     size_t runs_pending = 0;
@@ -1178,6 +1181,45 @@ int sb_batch_get_stats(const sb_batch *b, sb_batch_stats *out) {
     out->hits = b->cap_total;
     out->device_ms = b->last_total_ms;
     return SB_OK;
+}
+
+static_assert(sizeof(ReqPartial) == sizeof(sb_request_partial), "sb_request_partial layout");
+
+int sb_batch_set_owners(sb_batch *b, const uint32_t *owner, size_t nq, uint32_t n_rows) {
+    return guard([&] {
+        if (!b || (!owner && nq)) throw Error(SB_EINVAL, "NULL argument");
+        if (nq != b->nq) throw Error(SB_EINVAL, "owner array length differs from the batch's query count");
+        std::vector<uint32_t> seg(size_t(n_rows) + 1, 0);
+        for (size_t i = 0; i < nq; ++i) {
+            if (owner[i] >= n_rows) throw Error(SB_EINVAL, "owner " + std::to_string(owner[i]) + " >= n_rows");
+            if (i && owner[i] < owner[i - 1]) throw Error(SB_EINVAL, "owners must be non-decreasing in query order");
+            ++seg[owner[i] + 1];
+        }
+        for (uint32_t w = 0; w < n_rows; ++w) seg[w + 1] += seg[w];
+        std::vector<uint8_t> he(std::max<size_t>(nq, 1), 0);
+        for (size_t i = 0; i < nq; ++i) he[i] = b->host_err[i] ? 1 : 0;
+        std::lock_guard<std::mutex> lk(b->s->mu);
+        HIP_OK(hipSetDevice(b->s->device));
+        hipStream_t st = b->s->stream;
+        b->seg.alloc(seg.size() * 4);
+        b->herr.alloc(he.size());
+        HIP_OK(hipMemcpyAsync(b->seg.p, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(b->herr.p, he.data(), he.size(), hipMemcpyHostToDevice, st));
+        HIP_OK(hipStreamSynchronize(st));
+        b->n_rows = n_rows;
+    });
+}
+
+int sb_batch_reduce_requests(sb_batch *b, void *dev_out) {
+    return guard([&] {
+        if (!b || (!dev_out && b->n_rows)) throw Error(SB_EINVAL, "NULL argument");
+        if (!b->seg.p && b->n_rows) throw Error(SB_EINVAL, "sb_batch_set_owners was not called");
+        std::lock_guard<std::mutex> lk(b->s->mu);
+        HIP_OK(hipSetDevice(b->s->device));
+        launch_request_reduce(b->res.as<QRes>(), b->seg.as<uint32_t>(), b->herr.as<uint8_t>(), b->n_rows,
+                              static_cast<ReqPartial *>(dev_out), b->s->stream);
+        HIP_OK(hipGetLastError());
+    });
 }
 
 int sb_batch_fetch(sb_batch *b, sb_result_set **out) {

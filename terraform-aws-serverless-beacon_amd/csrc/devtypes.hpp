@@ -143,6 +143,16 @@ struct QRes {
     uint32_t n_scanned;
 };
 
+// one request row of sb_batch_reduce_requests (include/sbeacon.h
+// sb_request_partial, same layout)
+struct ReqPartial {
+    int64_t exists;  // slices with exists = True
+    int64_t n_variants;
+    int64_t call_count;
+    int64_t all_alleles_count;
+    int64_t errors;  // slices whose performQuery raised
+};
+
 // hit = record | (alt index << 32); alt index is the label index (the GT
 // fallback labels with alts[i] for a 1-based i, search_variants.py:223)
 inline constexpr uint64_t kHitAltShift = 32;

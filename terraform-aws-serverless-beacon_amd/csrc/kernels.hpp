@@ -29,6 +29,11 @@ void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t
 void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const uint32_t *chunk_slice, uint32_t nchunks,
                       uint64_t *bitmap, SPart *part, SRes *out, hipStream_t s);
 
+// Per-request partials of one shard (sb_batch_reduce_requests): row w sums
+// the answers of queries [seg[w], seg[w+1]).
+void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, uint32_t n_rows,
+                           ReqPartial *out, hipStream_t s);
+
 // Fetch-time gather of every query's hits into one dense array.
 void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,
                     uint64_t *out, hipStream_t s);

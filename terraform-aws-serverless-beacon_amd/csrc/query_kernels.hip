@@ -583,6 +583,35 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(const QDev *__restrict_
     for (uint32_t i = static_cast<uint32_t>(lane_id()); i < n; i += kWave) out[dst + i] = hits[src + i];
 }
 
+// Route-level reduction of one shard's slice answers
+// (lambda/getGenomicVariants/route_g_variants.py:144-171): request row w owns
+// the contiguous queries [seg[w], seg[w+1]).  exists is OR-ed (kept as the
+// number of slices that exist, so shard partials combine by sum), n_variants,
+// call_count and all_alleles_count are summed; a slice that raised (device
+// error or host-detected error flag) counts in `errors` and contributes
+// nothing else.  One thread per row; rows of a shard are few (10^5-10^6) and
+// each reads ~5 QRes, so this is a small streaming pass.
+__global__ __launch_bounds__(kBlock) void request_reduce_kernel(const QRes *__restrict__ res,
+                                                                const uint32_t *__restrict__ seg,
+                                                                const uint8_t *__restrict__ host_err,
+                                                                uint32_t n_rows, ReqPartial *__restrict__ out) {
+    const uint32_t w = blockIdx.x * kBlock + threadIdx.x;
+    if (w >= n_rows) return;
+    ReqPartial P{0, 0, 0, 0, 0};
+    for (uint32_t q = seg[w], e = seg[w + 1]; q < e; ++q) {
+        const QRes r = res[q];
+        if (r.error || host_err[q]) {
+            ++P.errors;
+            continue;
+        }
+        P.exists += r.exists != 0;
+        P.n_variants += r.n_hits;
+        P.call_count += r.call_count;
+        P.all_alleles_count += r.all_alleles_count;
+    }
+    out[w] = P;
+}
+
 inline uint32_t blocks_for(uint32_t nq) { return (nq + kWavesPerBlock - 1) / kWavesPerBlock; }
 
 // ------------------------------------------------------------ summariseSlice
@@ -751,6 +780,13 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const u
                            bitmap, part);
     hipLaunchKernelGGL(summarise_finish_kernel, dim3((ns + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, s,
                        ss, slices, ns, bitmap, part, out);
+}
+
+void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, uint32_t n_rows,
+                           ReqPartial *out, hipStream_t s) {
+    if (!n_rows) return;
+    hipLaunchKernelGGL(request_reduce_kernel, dim3((n_rows + kBlock - 1) / kBlock), dim3(kBlock), 0, s, res, seg,
+                       host_err, n_rows, out);
 }
 
 void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,

@@ -107,6 +107,8 @@ SIGNATURES = {
     'sb_batch_get_stats': (C.c_int, [P, C.POINTER(BatchStats)]),
     'sb_batch_fetch': (C.c_int, [P, C.POINTER(P)]),
     'sb_batch_free': (None, [P]),
+    'sb_batch_set_owners': (C.c_int, [P, C.POINTER(C.c_uint32), C.c_size_t, C.c_uint32]),
+    'sb_batch_reduce_requests': (C.c_int, [P, C.c_void_p]),
     'sb_summarise_slices': (C.c_int, [P, C.POINTER(Slice), C.c_size_t, C.POINTER(SliceStats),
                                       C.POINTER(C.c_double)]),
     'sb_dedup_count': (C.c_int, [P, C.POINTER(DedupJob), C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_int32),

@@ -37,6 +37,46 @@ def _b(s):
     return None if s is None else (s if isinstance(s, bytes) else str(s).encode())
 
 
+def queries_from_payloads(payloads: list[dict], vcf_id, *, strict_variant_type: bool = False):
+    """PerformQueryPayload dicts -> (ctypes Query array, keep-alive list);
+    vcf_id(location) -> the store's vcf id."""
+    n = len(payloads)
+    arr = (Query * n)()
+    keep = []
+    vid_cache = {}
+    for i, p in enumerate(payloads):
+        loc = p['vcf_location']
+        vid = vid_cache.get(loc)
+        if vid is None:
+            vid = vid_cache[loc] = vcf_id(loc)
+        pt = p.get('passthrough') or {}
+        region = _b(p['region'])
+        ref = _b(p.get('reference_bases'))
+        alt = _b(p.get('alternate_bases'))
+        vt = _b(p.get('variant_type'))
+        names = pt.get('sampleNames', None)
+        sn = _b(','.join(names)) if names is not None else None
+        keep.append((region, ref, alt, vt, sn))
+        if p.get('end_min') is None or p.get('end_max') is None:
+            raise TypeError("'<=' not supported between instances of 'NoneType' and 'int'")
+        q = arr[i]
+        q.vcf_id = vid
+        q.region, q.region_len = region, len(region)
+        q.end_min, q.end_max = int(p['end_min']), int(p['end_max'])
+        q.reference_bases, q.reference_len = ref, len(ref) if ref is not None else 0
+        q.alternate_bases, q.alternate_len = alt, len(alt) if alt is not None else 0
+        q.variant_type, q.variant_type_len = vt, len(vt) if vt is not None else 0
+        q.variant_min_length = int(p['variant_min_length'])
+        q.variant_max_length = int(p['variant_max_length'])
+        q.granularity = _lib.SB_GRAN.get(p.get('requested_granularity'), 255)
+        q.include_details = 1 if p.get('include_details') else 0
+        q.include_samples = 1 if pt.get('includeSamples', False) else 0
+        q.selected_samples_only = 1 if pt.get('selectedSamplesOnly', False) else 0
+        q.strict_variant_type = 1 if strict_variant_type else 0
+        q.sample_names, q.sample_names_len = sn, len(sn) if sn is not None else 0
+    return arr, keep
+
+
 class Store:
     """An immutable HBM store built from VCF files or text."""
 
@@ -199,41 +239,7 @@ class Store:
     # ---------------------------------------------------------------- query
     def make_queries(self, payloads: list[dict], *, strict_variant_type: bool = False):
         """PerformQueryPayload dicts -> (ctypes Query array, keep-alive list)."""
-        n = len(payloads)
-        arr = (Query * n)()
-        keep = []
-        vid_cache = {}
-        for i, p in enumerate(payloads):
-            loc = p['vcf_location']
-            vid = vid_cache.get(loc)
-            if vid is None:
-                vid = vid_cache[loc] = self.vcf_id(loc)
-            pt = p.get('passthrough') or {}
-            region = _b(p['region'])
-            ref = _b(p.get('reference_bases'))
-            alt = _b(p.get('alternate_bases'))
-            vt = _b(p.get('variant_type'))
-            names = pt.get('sampleNames', None)
-            sn = _b(','.join(names)) if names is not None else None
-            keep.append((region, ref, alt, vt, sn))
-            if p.get('end_min') is None or p.get('end_max') is None:
-                raise TypeError("'<=' not supported between instances of 'NoneType' and 'int'")
-            q = arr[i]
-            q.vcf_id = vid
-            q.region, q.region_len = region, len(region)
-            q.end_min, q.end_max = int(p['end_min']), int(p['end_max'])
-            q.reference_bases, q.reference_len = ref, len(ref) if ref is not None else 0
-            q.alternate_bases, q.alternate_len = alt, len(alt) if alt is not None else 0
-            q.variant_type, q.variant_type_len = vt, len(vt) if vt is not None else 0
-            q.variant_min_length = int(p['variant_min_length'])
-            q.variant_max_length = int(p['variant_max_length'])
-            q.granularity = _lib.SB_GRAN.get(p.get('requested_granularity'), 255)
-            q.include_details = 1 if p.get('include_details') else 0
-            q.include_samples = 1 if pt.get('includeSamples', False) else 0
-            q.selected_samples_only = 1 if pt.get('selectedSamplesOnly', False) else 0
-            q.strict_variant_type = 1 if strict_variant_type else 0
-            q.sample_names, q.sample_names_len = sn, len(sn) if sn is not None else 0
-        return arr, keep
+        return queries_from_payloads(payloads, self.vcf_id, strict_variant_type=strict_variant_type)
 
     def query(self, payloads: list[dict], *, strict_variant_type: bool = False) -> 'ResultSet':
         arr, keep = self.make_queries(payloads, strict_variant_type=strict_variant_type)
@@ -268,6 +274,18 @@ class Batch:
         t, s, b = C.c_double(), C.c_double(), C.c_double()
         check(lib().sb_batch_last_timing(self._h, C.byref(t), C.byref(s), C.byref(b)))
         return {'total_ms': t.value, 'scan_ms': s.value, 'bounds_ms': b.value}
+
+    def set_owners(self, owner, n_rows: int):
+        """Query i belongs to request row owner[i] (non-decreasing)."""
+        import numpy as np
+        o = np.ascontiguousarray(owner, dtype=np.uint32)
+        check(lib().sb_batch_set_owners(self._h, o.ctypes.data_as(C.POINTER(C.c_uint32)), len(o), int(n_rows)))
+
+    def reduce_requests(self, dev_ptr: int):
+        """Enqueue the per-request reduction into dev_ptr (n_rows x 5 int64
+        on the store's device: exists, n_variants, call_count,
+        all_alleles_count, errors)."""
+        check(lib().sb_batch_reduce_requests(self._h, C.c_void_p(dev_ptr)))
 
     def fetch(self) -> 'ResultSet':
         r = C.c_void_p()

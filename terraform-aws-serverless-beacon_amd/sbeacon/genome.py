@@ -1,0 +1,295 @@
+"""Whole-genome workload and contig sharding (BASELINE.json configs[2];
+SURVEY.md §8d config 3, §8e).
+
+Store: a 1000 Genomes-shape whole genome — ~85 M records over contigs 1-22,
+X, Y, counts proportional to contig length (``chrom_matching.py:12-38``),
+one synthetic generator per contig (seed ``1000 * seed + contig index``),
+sites-only (the config-3 queries never read genotypes).
+
+Sharding (one rank per GPU).  The genome's records, in (contig, POS) order,
+are cut into ``world`` ranges of equal record count; rank r's *core* is
+``[cut_r, cut_{r+1})`` in (contig index, POS) order.  A performQuery slice
+(``splitQuery``: ``[a, min(a + 9999, start_max)]``, one contig) is answered
+by the rank whose core holds ``(contig, a)``.  Its records lie in
+``[a, a + 9999]``, so every rank also holds a right *halo* of 10,000 bp past
+its core: each slice is answered whole by one GPU and the reference's
+order-dependent per-slice semantics (cumulative call_count, early exits)
+need no cross-GPU exchange.  A request whose slices fall on several ranks
+is combined at the route level (exists OR, counts summed —
+``route_g_variants.py:144-171``), which is what the RCCL step carries.
+
+Requests (config 3): ``n`` Beacon requests, seed 1003 + 0: contig drawn
+proportional to length, start uniform over the contig's populated span,
+width uniform 1-100,000 bp, ``referenceBases='N'``, ``alternateBases=None``,
+``variantType`` in {DEL, INS, DUP, DUP:TANDEM, CNV} with length bounds,
+granularity ``record``, ``includeResultsetResponses='HIT'``.  They are
+ordered by (contig, start) so every rank's requests form one contiguous
+window of request rows (the router keeps the permutation to the arrival
+order).
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from .chrom_matching import CHROMOSOME_LENGTHS
+from .workload import SyntheticVcf
+
+CONTIGS = [c for c in CHROMOSOME_LENGTHS if c != 'MT']
+SPLIT_SIZE = 10000  # lambda/splitQuery/lambda_function.py:12
+HALO = SPLIT_SIZE
+EDGE = 10000  # records start EDGE bp into each contig and stop EDGE bp before its end
+LOCATION = 'synthetic/wgs-1000g-shape.vcf.gz'
+VARIANT_TYPES = ['DEL', 'INS', 'DUP', 'DUP:TANDEM', 'CNV']
+VMIN = [0, 0, 1, 5]
+VMAX = [-1, -1, 10, 50, 1000]
+
+
+class GenomeShape:
+    def __init__(self, *, n_total: int = 85_000_000, seed: int = 3, n_samples: int = 2504):
+        self.seed, self.n_total, self.n_samples = seed, n_total, n_samples
+        lens = np.array([CHROMOSOME_LENGTHS[c] for c in CONTIGS], dtype=np.float64)
+        counts = np.floor(n_total * lens / lens.sum()).astype(np.int64)
+        counts[0] += n_total - counts.sum()
+        self.counts = counts
+        self.offsets = np.concatenate([[0], np.cumsum(counts)])  # global record index of each contig's first
+        self._gens: dict[int, SyntheticVcf] = {}
+
+    def gen(self, ci: int) -> SyntheticVcf:
+        g = self._gens.get(ci)
+        if g is None:
+            c = CONTIGS[ci]
+            n = int(self.counts[ci])
+            span = CHROMOSOME_LENGTHS[c] - 2 * EDGE
+            g = SyntheticVcf(seed=1000 * self.seed + ci, n_records=n, n_samples=self.n_samples, start=EDGE,
+                             mean_gap=span / max(n - 1, 1), contig=c)
+            self._gens[ci] = g
+        return g
+
+    def span(self, ci: int):
+        p = self.gen(ci).positions()
+        return int(p[0]), int(p[-1])
+
+    # ------------------------------------------------------------- sharding
+    def cuts(self, world: int):
+        """world + 1 cut points (contig index, POS); rank r's core is
+        [cuts[r], cuts[r + 1]) in lexicographic order."""
+        out = [(0, 0)]
+        for r in range(1, world):
+            g = r * self.n_total // world
+            ci = int(np.searchsorted(self.offsets, g, side='right') - 1)
+            i = g - int(self.offsets[ci])
+            out.append((ci, int(self.gen(ci).positions()[i])))
+        out.append((len(CONTIGS), 0))
+        return out
+
+    def shard_pieces(self, world: int, rank: int):
+        """[(contig index, record lo, record hi)] of rank's store: its core
+        plus the right halo (records of the cut contig with POS < P + HALO)."""
+        cuts = self.cuts(world)
+        (c0, p0), (c1, p1) = cuts[rank], cuts[rank + 1]
+        pieces = []
+        for ci in range(c0, min(c1, len(CONTIGS) - 1) + 1):
+            pos = self.gen(ci).positions()
+            lo = int(np.searchsorted(pos, p0, side='left')) if ci == c0 else 0
+            if ci == c1:
+                hi = int(np.searchsorted(pos, p1 + HALO, side='left'))  # halo into the next rank's core
+            else:
+                hi = len(pos)
+            if hi > lo:
+                pieces.append((ci, lo, hi))
+        return pieces
+
+    def shard_chunks(self, world: int, rank: int, chunk=1 << 16, threads=0):
+        """VCF text of rank's shard (one VCF, contigs in order, sites only)."""
+        pieces = self.shard_pieces(world, rank)
+        first = True
+        for ci, lo, hi in pieces:
+            g = self.gen(ci)
+            if first:
+                yield g.header(sites_only=True)
+                first = False
+            for a in range(lo, hi, chunk):
+                yield g.records(a, min(a + chunk, hi), sites_only=True, threads=threads)
+
+    def build_shard_store(self, world: int, rank: int, *, device=0, threads=0):
+        from .engine import Store
+        return Store.build([(LOCATION, self.shard_chunks(world, rank, threads=threads))], device=device,
+                           keep_genotypes=False, n_threads=threads)
+
+    def shard_records(self, world: int, rank: int) -> int:
+        return sum(hi - lo for _, lo, hi in self.shard_pieces(world, rank))
+
+
+@dataclass
+class Requests:
+    """Config-3 requests, ordered by (contig, start); Beacon 0-based start."""
+    ci: np.ndarray     # contig index
+    start: np.ndarray  # requestParameters.start[0] (0-based)
+    width: np.ndarray  # end[0] - start[0]
+    vt: np.ndarray     # index into VARIANT_TYPES
+    vmin: np.ndarray
+    vmax: np.ndarray
+
+    def __len__(self):
+        return len(self.ci)
+
+
+def config3_requests(shape: GenomeShape, n: int = 1_000_000, seed: int = 1003) -> Requests:
+    rng = np.random.default_rng(seed)
+    lens = np.array([CHROMOSOME_LENGTHS[c] for c in CONTIGS], dtype=np.float64)
+    ci = rng.choice(len(CONTIGS), size=n, p=lens / lens.sum())
+    width = rng.integers(1, 100001, n)
+    lo = np.array([shape.span(c)[0] for c in range(len(CONTIGS))])
+    hi = np.array([shape.span(c)[1] for c in range(len(CONTIGS))])
+    u = rng.random(n)
+    start = (lo[ci] - 1 + u * (hi[ci] - lo[ci])).astype(np.int64)
+    vt = rng.integers(0, len(VARIANT_TYPES), n)
+    vmin = np.array(VMIN)[rng.integers(0, len(VMIN), n)]
+    vmax = np.array(VMAX)[rng.integers(0, len(VMAX), n)]
+    order = np.lexsort((start, ci))
+    return Requests(ci[order], start[order], width[order], vt[order], vmin[order], vmax[order])
+
+
+@dataclass
+class ShardSlices:
+    """The performQuery slices one rank answers: request row (relative to
+    row_lo), contig, [a, b], the request's end bracket and filters."""
+    row_lo: int
+    n_rows: int
+    req: np.ndarray
+    ci: np.ndarray
+    a: np.ndarray
+    b: np.ndarray
+    end_min: np.ndarray
+    end_max: np.ndarray
+    vt: np.ndarray
+    vmin: np.ndarray
+    vmax: np.ndarray
+
+    def __len__(self):
+        return len(self.a)
+
+
+def request_slices(reqs: Requests):
+    """Every slice of every request, as perform_variant_search_sync +
+    split_query build them (search_variants.py:179-199: start=[s], end=[e]
+    -> start_min = s+1, start_max = end_max = e+1, end_min = s+1;
+    splitQuery: a = start_min + 10000 k, b = min(a + 9999, start_max))."""
+    smin = reqs.start + 1
+    smax = reqs.start + reqs.width + 1
+    nsl = (smax - smin) // SPLIT_SIZE + 1
+    req = np.repeat(np.arange(len(reqs), dtype=np.int64), nsl)
+    first = np.repeat(np.cumsum(nsl) - nsl, nsl)
+    k = np.arange(len(req), dtype=np.int64) - first
+    a = smin[req] + SPLIT_SIZE * k
+    b = np.minimum(a + SPLIT_SIZE - 1, smax[req])
+    return req, a, b, smin[req], smax[req]
+
+
+def rank_of_slices(shape: GenomeShape, world: int, ci: np.ndarray, a: np.ndarray) -> np.ndarray:
+    cuts = shape.cuts(world)
+    key = ci.astype(np.int64) * (1 << 32) + a
+    ck = np.array([c * (1 << 32) + p for c, p in cuts], dtype=np.int64)
+    return np.searchsorted(ck, key, side='right') - 1
+
+
+def shard_slices(shape: GenomeShape, reqs: Requests, world: int, rank: int) -> ShardSlices:
+    req, a, b, emin, emax = request_slices(reqs)
+    ci = reqs.ci[req]
+    mine = rank_of_slices(shape, world, ci, a) == rank
+    req, a, b, emin, emax, ci = req[mine], a[mine], b[mine], emin[mine], emax[mine], ci[mine]
+    if len(req):
+        row_lo, n_rows = int(req[0]), int(req[-1]) - int(req[0]) + 1
+    else:
+        row_lo, n_rows = 0, 0
+    return ShardSlices(row_lo, n_rows, (req - row_lo).astype(np.uint32), ci, a, b, emin, emax,
+                       reqs.vt[req], reqs.vmin[req], reqs.vmax[req])
+
+
+def slice_payloads(sl: ShardSlices, lo=0, hi=None):
+    """PerformQueryPayload dicts of slices [lo, hi) (tests / small batches)."""
+    hi = len(sl) if hi is None else hi
+    out = []
+    for j in range(lo, hi):
+        out.append(dict(passthrough={}, dataset_id='wgs', query_id='genome', region=f'{CONTIGS[sl.ci[j]]}:'
+                        f'{sl.a[j]}-{sl.b[j]}', reference_bases='N', end_min=int(sl.end_min[j]),
+                        end_max=int(sl.end_max[j]), alternate_bases=None, variant_type=VARIANT_TYPES[sl.vt[j]],
+                        include_details=True, requested_granularity='record',
+                        variant_min_length=int(sl.vmin[j]), variant_max_length=int(sl.vmax[j]),
+                        vcf_location=LOCATION))
+    return out
+
+
+def shard_query_array(sl: ShardSlices, vid: int):
+    """Vectorised sb_query array for a rank's slices: the same field values
+    slice_payloads + engine.queries_from_payloads produce, without
+    per-query Python objects.  Returns (array, keep-alive buffers)."""
+    from . import _lib
+    from ._lib import Query
+    n = len(sl)
+    arr = (Query * max(n, 1))()
+    keep = []
+    if n:
+        regions = '\n'.join(f'{CONTIGS[c]}:{a}-{b}' for c, a, b in zip(sl.ci.tolist(), sl.a.tolist(),
+                                                                        sl.b.tolist())).encode() + b'\n'
+        rbuf = C.create_string_buffer(regions, len(regions))
+        nl = np.flatnonzero(np.frombuffer(regions, dtype=np.uint8) == 10)
+        starts = np.concatenate([[0], nl[:-1] + 1])
+        lens = nl - starts
+        consts = {k: C.create_string_buffer(k.encode(), len(k)) for k in ['N'] + VARIANT_TYPES}
+        caddr = {k: C.addressof(v) for k, v in consts.items()}
+        keep += [rbuf, consts]
+        dt = np.dtype({'names': ['vcf_id', 'region', 'region_len', 'end_min', 'end_max', 'reference_bases',
+                                 'reference_len', 'alternate_bases', 'alternate_len', 'variant_type',
+                                 'variant_type_len', 'variant_min_length', 'variant_max_length', 'granularity',
+                                 'include_details', 'include_samples', 'selected_samples_only',
+                                 'strict_variant_type', 'sample_names', 'sample_names_len'],
+                       'formats': ['u4', 'u8', 'u8', 'i8', 'i8', 'u8', 'u8', 'u8', 'u8', 'u8', 'u8', 'i8', 'i8',
+                                   'u1', 'u1', 'u1', 'u1', 'u1', 'u8', 'u8'],
+                       'offsets': [getattr(Query, f).offset for f in
+                                   ['vcf_id', 'region', 'region_len', 'end_min', 'end_max', 'reference_bases',
+                                    'reference_len', 'alternate_bases', 'alternate_len', 'variant_type',
+                                    'variant_type_len', 'variant_min_length', 'variant_max_length', 'granularity',
+                                    'include_details', 'include_samples', 'selected_samples_only',
+                                    'strict_variant_type', 'sample_names', 'sample_names_len']],
+                       'itemsize': C.sizeof(Query)})
+        v = np.frombuffer((C.c_char * (C.sizeof(Query) * n)).from_address(C.addressof(arr)), dtype=dt)
+        v['vcf_id'] = vid
+        v['region'] = C.addressof(rbuf) + starts
+        v['region_len'] = lens
+        v['end_min'] = sl.end_min
+        v['end_max'] = sl.end_max
+        v['reference_bases'] = caddr['N']
+        v['reference_len'] = 1
+        v['alternate_bases'] = 0
+        v['alternate_len'] = 0
+        vt_addr = np.array([caddr[k] for k in VARIANT_TYPES], dtype=np.uint64)
+        vt_len = np.array([len(k) for k in VARIANT_TYPES], dtype=np.uint64)
+        v['variant_type'] = vt_addr[sl.vt]
+        v['variant_type_len'] = vt_len[sl.vt]
+        v['variant_min_length'] = sl.vmin
+        v['variant_max_length'] = sl.vmax
+        v['granularity'] = _lib.SB_GRAN['record']
+        v['include_details'] = 1
+        v['include_samples'] = 0
+        v['selected_samples_only'] = 0
+        v['strict_variant_type'] = 0
+        v['sample_names'] = 0
+        v['sample_names_len'] = 0
+    return arr, keep
+
+
+def prepare_shard_batch(store, sl: ShardSlices):
+    """The rank's slices prepared on its device, request rows attached."""
+    from ._lib import check, lib
+    from .engine import Batch
+    arr, keep = shard_query_array(sl, store.vcf_id(LOCATION))
+    h = C.c_void_p()
+    check(lib().sb_batch_prepare(store.handle, arr, len(sl), C.byref(h)))
+    del keep
+    batch = Batch(h, None, store)
+    batch.set_owners(sl.req, sl.n_rows)
+    return batch
