@@ -46,7 +46,15 @@ def main_genome(args):
 
     t0 = time.perf_counter()
     shape = GenomeShape(n_total=args.genome_records, seed=3)
-    store = shape.build_shard_store(world, rank, device=local, threads=args.threads)
+    n_shard = shape.shard_records(world, rank)
+    last = [0.0]
+
+    def progress(contig, done):
+        if time.perf_counter() - last[0] > 20:
+            last[0] = time.perf_counter()
+            log(f'[rank {rank}] ingest: {done}/{n_shard} records (contig {contig}), {last[0] - t0:.0f} s')
+
+    store = shape.build_shard_store(world, rank, device=local, threads=args.threads, progress=progress)
     info = store.info()
     t_ingest = time.perf_counter() - t0
     log(f'[rank {rank}] shard: {info["n_records"]} records, {info["device_bytes"] / 2**20:.0f} MiB HBM, '

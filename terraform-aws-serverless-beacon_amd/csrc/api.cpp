@@ -333,6 +333,16 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.d.rec = dev_upload(s, rec);
     s.d.rng = dev_upload(s, rng);
     std::vector<RangeHot>().swap(rng);
+    {
+        std::vector<VtHot> vth(rec.size());
+        for (size_t i = 0; i < rec.size(); ++i) {
+            const uint64_t rl = static_cast<uint64_t>(rec[i].end) - pos[i] + 1, al = a0_len[i];
+            vth[i] = VtHot{rec[i].end, rec[i].hot,
+                           static_cast<uint32_t>(std::min<uint64_t>(rl, 0xffff) | (std::min<uint64_t>(al, 0xffff) << 16)),
+                           rec[i].ac0};
+        }
+        s.d.vth = dev_upload(s, vth);
+    }
     s.d.pos = dev_upload(s, pos);
     s.d.ref_key = dev_upload(s, ref_key);
     s.d.a0_key = dev_upload(s, a0_key);
@@ -575,19 +585,25 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         // collect -> general kernel with the sample path; otherwise the
         // narrowest specialisation whose predicates cover the query
         B.groups.clear();
-        for (int g = 0; g < 4; ++g) B.groups.push_back(sb_batch::Group{g == 3 ? MODE_GENERAL : g, g == 3 ? s.max_words : 0u, {}, {}});
+        // groups 0..3 = MODE_GENERAL/RANGE_N/EXACT/VTYPE without the sample
+        // path; group 4 = MODE_GENERAL with the sample planes compiled in
+        constexpr int kCollect = 4;
+        for (int g = 0; g <= kCollect; ++g)
+            B.groups.push_back(sb_batch::Group{g == kCollect ? MODE_GENERAL : g, g == kCollect ? s.max_words : 0u, {}, {}});
         for (uint32_t i = 0; i < B.nq; ++i) {
             const QDev &d = B.hq[i];
             if (!(d.flags & F_NONNEG)) B.nonneg = false;
             int g;
             if (d.samples_out_off != ~0ull) {
-                g = 3;
+                g = kCollect;
             } else if (d.flags & (F_STRICT_UNBOUND | F_SAMPLES_VARIANT)) {
                 g = MODE_GENERAL;
             } else if (d.ref_mode == REF_ANY && d.alt_mode == ALT_N) {
                 g = MODE_RANGE_N;
             } else if (d.ref_mode == REF_EXACT && d.alt_mode == ALT_EXACT) {
                 g = MODE_EXACT;
+            } else if (d.ref_mode == REF_ANY && d.alt_mode == ALT_VTYPE) {
+                g = MODE_VTYPE;
             } else {
                 g = MODE_GENERAL;
             }

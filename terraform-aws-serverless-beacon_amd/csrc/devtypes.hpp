@@ -54,6 +54,19 @@ struct alignas(16) RangeHot {
 };
 enum : uint32_t { RH_EMIT_MASK = 0xffu, RH_HIT = 1u << 8, RH_SLOW = 1u << 9 };
 
+// What a referenceBases='N' / alternateBases=None variantType query
+// (MODE_VTYPE) reads of a record: the first ALT's class and lengths sit next
+// to END, so the predicate of search_variants.py:100-183 needs one 16-byte
+// load; AN is fetched for hit lanes only.  Built at upload from RecHot, POS
+// and len(ALT0); lens saturate at 0xffff (those records take eval_record, as
+// do multiallelic / AC-less / int()-failing ones).
+struct alignas(16) VtHot {
+    uint32_t end;
+    uint32_t hot;   // RecHot::hot
+    uint32_t lens;  // len(REF) | len(ALT0) << 16
+    int32_t ac0;
+};
+
 // ---- query modes -----------------------------------------------------------
 enum : uint32_t {
     REF_ANY = 0,    // reference_bases == 'N' (:59)
@@ -64,7 +77,7 @@ enum : uint32_t {
 };
 enum : uint32_t { ALT_N = 0, ALT_EXACT = 1, ALT_VTYPE = 2 };
 // scan-kernel specialisations (query classes launched separately)
-enum : int { MODE_GENERAL = 0, MODE_RANGE_N = 1, MODE_EXACT = 2 };
+enum : int { MODE_GENERAL = 0, MODE_RANGE_N = 1, MODE_EXACT = 2, MODE_VTYPE = 3 };
 enum : uint32_t { VT_DEL = 0, VT_INS = 1, VT_DUP = 2, VT_DUPT = 3, VT_CNV = 4, VT_OTHER = 5 };
 enum : uint32_t {
     F_DETAILS = 1u << 0,         // include_details
@@ -85,6 +98,7 @@ struct DStore {
     // record-indexed
     const RecHot *rec;
     const RangeHot *rng;      // MODE_RANGE_N view of the same records
+    const VtHot *vth;         // MODE_VTYPE view of the same records
     const uint32_t *pos;
     const uint64_t *ref_key;  // key(REF.upper())
     const uint64_t *a0_key;   // key(ALT0.upper())

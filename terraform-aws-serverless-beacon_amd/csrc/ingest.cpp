@@ -611,6 +611,14 @@ uint32_t sym_id(sb_builder &b, const uint8_t *p, uint32_t n) {
     return id;
 }
 
+// reserve room for `extra` more elements with geometric growth (an exact
+// reserve per merged chunk would copy the whole column every chunk)
+template <class V>
+void grow(V &v, size_t extra) {
+    const size_t need = v.size() + extra;
+    if (need > v.capacity()) v.reserve(std::max(need, 2 * v.capacity()));
+}
+
 void merge(sb_builder &b, VcfData &v, Local &L) {
     VcfCols &d = v.c;
     const VcfCols &s = L.c;
@@ -638,9 +646,9 @@ void merge(sb_builder &b, VcfData &v, Local &L) {
     app(d.ref_key, s.ref_key);
     app(d.a0_key, s.a0_key);
     app(d.a0_len, s.a0_len);
-    d.rec.reserve(d.rec.size() + nr);
+    grow(d.rec, nr);
     app(d.rng, s.rng);
-    d.vt.reserve(d.vt.size() + nr);
+    grow(d.vt, nr);
     std::string last_vt;
     uint32_t last_id = 0;
     bool have_last = false;
@@ -671,7 +679,7 @@ void merge(sb_builder &b, VcfData &v, Local &L) {
     app(d.x_len, s.x_len);
     app(d.x_ac, s.x_ac);
     for (size_t i = 0; i < s.x_off.size(); ++i) d.x_off.push_back(s.x_off[i] + blob0);
-    d.x_cls.reserve(d.x_cls.size() + s.x_cls.size());
+    grow(d.x_cls, s.x_cls.size());
     for (size_t i = 0; i < s.x_cls.size(); ++i) {
         uint32_t cls = s.x_cls[i];
         if (cls & C_SYMBOLIC) cls |= sym_id(b, s.blob.data() + s.x_off[i], s.x_len[i]) << C_SYM_SHIFT;
@@ -691,7 +699,7 @@ void merge(sb_builder &b, VcfData &v, Local &L) {
         for (size_t i = 1; i < s.dk_lo.size(); ++i) d.dk_lo.push_back(s.dk_lo[i] + k0);
         app(d.dk_pos, s.dk_pos);
         app(d.dk_hash, s.dk_hash);
-        d.dk_tail.reserve(d.dk_tail.size() + s.dk_tail.size());
+        grow(d.dk_tail, s.dk_tail.size());
         for (uint64_t t : s.dk_tail) d.dk_tail.push_back((t & kTailBlob) ? t + kb0 : t);
         app(d.dk_blob, s.dk_blob);
         for (uint32_t r : s.dk_bad) d.dk_bad.push_back(r + rec0);

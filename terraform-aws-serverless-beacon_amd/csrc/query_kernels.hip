@@ -569,6 +569,77 @@ __global__ __launch_bounds__(kBlock) void range_n_kernel(DStore st, const QDev *
     finish_query<NONNEG>(S, q, hi - lo, res);
 }
 
+// MODE_VTYPE: referenceBases 'N' + alternateBases None + variantType queries
+// (search_variants.py:100-166, the patched-oracle branch selector; strict
+// mode goes to MODE_GENERAL).  One 16-byte VtHot word per record carries END,
+// the first ALT's class bits and len(REF) | len(ALT0); the predicate, the
+// length bounds (:177-183) and the AC contribution (:205-214) of a clean
+// biallelic record need no other load, and AN is gathered for hit lanes only
+// (hits are rare: most records are SNVs no variantType matches).  Records
+// that are multiallelic, lack AC, carry int() failures or missing AC entries,
+// or have lengths >= 0xffff take eval_record.
+template <bool NONNEG>
+__global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__restrict__ qs,
+                                                    const uint32_t *__restrict__ qidx, uint32_t nq,
+                                                    QRes *__restrict__ res, uint64_t *__restrict__ hits) {
+    const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    if (w >= nq) return;
+    const uint32_t q = qidx ? uniform(qidx[w]) : w;
+    const int lane = lane_id();
+    const QDev &Q = qs[q];
+    const uint32_t flags = Q.flags;
+    const bool details = flags & F_DETAILS;
+    const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
+    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
+    if (!(flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
+    ScanState S;
+    const uint32_t emin = Q.end_min < 0 ? 0u : Q.end_min > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_min);
+    const uint32_t emax = Q.end_max < 0 ? 0u : Q.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_max);
+    const bool end_void = Q.end_max < 0 || Q.end_min > 0xffffffffll || Q.end_min > Q.end_max;
+    constexpr uint32_t kSlowBits = H_MULTI | H_AC_BAD | H_AN_BAD | C_AC_MISSING;
+    uint64_t *out = hits + Q.hit_off;
+    QView V{flags, REF_ANY, ALT_VTYPE, false, false, nullptr, nullptr, nullptr};
+
+    auto chunk = [&](uint32_t base, const VtHot h) -> bool {  // true = keep going
+        const uint32_t r = base + static_cast<uint32_t>(lane);
+        const bool cand = !end_void && r < hi && h.end >= emin && h.end <= emax;
+        const uint32_t rl = h.lens & 0xffffu, al = h.lens >> 16;
+        const bool slow = (h.hot & kSlowBits) || !(h.hot & H_HAS_AC) || rl == 0xffffu || al == 0xffffu;
+        LaneOut o{0, 0, 0, 0, 0};
+        if (cand && !slow) {
+            const int64_t len = al;
+            if (vtype_hit(Q, st, h.hot, len, rl) && len >= Q.vmin && len <= Q.vmax) {
+                o.hm = 1;
+                o.c = h.ac0;
+                o.em = h.ac0 != 0 ? 1ull : 0ull;
+                o.anv = st.rec[r].an;
+            }
+        }
+        if (__ballot(cand && slow)) {
+            if (cand && slow) o = eval_record(st, Q, V, r, st.rec[r]);
+        }
+        uint64_t cm;
+        return chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) >= kWave;
+    };
+    const uint32_t l0 = lo + static_cast<uint32_t>(lane);
+    VtHot a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
+    if (l0 < hi) a = st.vth[l0];
+    if (l0 + kWave < hi) b = st.vth[l0 + kWave];
+    for (uint32_t base = lo; base < hi; base += 2 * kWave) {
+        const uint32_t r = base + static_cast<uint32_t>(lane);
+        VtHot c2 = {0, 0, 0, 0};
+        if (r + 2 * kWave < hi) c2 = st.vth[r + 2 * kWave];
+        if (!chunk(base, a)) break;
+        if (base + kWave >= hi) break;
+        VtHot d2 = {0, 0, 0, 0};
+        if (r + 3 * kWave < hi) d2 = st.vth[r + 3 * kWave];
+        if (!chunk(base + kWave, b)) break;
+        a = c2;
+        b = d2;
+    }
+    finish_query<NONNEG>(S, q, hi - lo, res);
+}
+
 // Gather each query's hits from its planned region into a dense array
 // (result shipping at fetch time; not part of the timed query step).
 __global__ __launch_bounds__(kBlock) void compact_kernel(const QDev *__restrict__ qs,
@@ -802,6 +873,10 @@ void launch_variant(int nacc, int mode, dim3 g, const DStore &st, const QDev *q,
     const dim3 b(kBlock);
     if (nacc == 0 && mode == MODE_RANGE_N) {
         hipLaunchKernelGGL((range_n_kernel<NONNEG>), g, b, 0, s, st, q, qidx, n, res, hits);
+        return;
+    }
+    if (nacc == 0 && mode == MODE_VTYPE) {
+        hipLaunchKernelGGL((vt_kernel<NONNEG>), g, b, 0, s, st, q, qidx, n, res, hits);
         return;
     }
 #define SB_SCAN(NA, MO) hipLaunchKernelGGL((scan_kernel<NA, NONNEG, MO>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out)

@@ -127,6 +127,13 @@ def lib():
     """Load libsbeacon_hip.so (raises OSError if it is missing: no fallback)."""
     global _lib
     if _lib is None:
+        try:
+            # torch bundles its own libamdhip64.so.7 (same soname as ROCm's):
+            # load it first so the process has ONE HIP runtime whichever of
+            # torch / this library the caller touches first
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         if not os.path.exists(LIB_PATH):
             raise OSError(f'{LIB_PATH} not found: build it with `python -c "import __graft_entry__ as g; g.build()"`')
         L = C.CDLL(LIB_PATH)

@@ -102,22 +102,28 @@ class GenomeShape:
                 pieces.append((ci, lo, hi))
         return pieces
 
-    def shard_chunks(self, world: int, rank: int, chunk=1 << 16, threads=0):
-        """VCF text of rank's shard (one VCF, contigs in order, sites only)."""
+    def shard_chunks(self, world: int, rank: int, chunk=1 << 20, threads=0, progress=None):
+        """VCF text of rank's shard (one VCF, contigs in order, sites only).
+        Large chunks: the builder parses each chunk with all its threads."""
         pieces = self.shard_pieces(world, rank)
         first = True
+        done = 0
         for ci, lo, hi in pieces:
             g = self.gen(ci)
             if first:
                 yield g.header(sites_only=True)
                 first = False
             for a in range(lo, hi, chunk):
-                yield g.records(a, min(a + chunk, hi), sites_only=True, threads=threads)
+                b = min(a + chunk, hi)
+                yield g.records(a, b, sites_only=True, threads=threads)
+                done += b - a
+                if progress:
+                    progress(CONTIGS[ci], done)
 
-    def build_shard_store(self, world: int, rank: int, *, device=0, threads=0):
+    def build_shard_store(self, world: int, rank: int, *, device=0, threads=0, progress=None):
         from .engine import Store
-        return Store.build([(LOCATION, self.shard_chunks(world, rank, threads=threads))], device=device,
-                           keep_genotypes=False, n_threads=threads)
+        return Store.build([(LOCATION, self.shard_chunks(world, rank, threads=threads, progress=progress))],
+                           device=device, keep_genotypes=False, n_threads=threads)
 
     def shard_records(self, world: int, rank: int) -> int:
         return sum(hi - lo for _, lo, hi in self.shard_pieces(world, rank))

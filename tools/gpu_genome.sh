@@ -1,5 +1,5 @@
-# GPU tests, then the config-3 (whole-genome, contig-sharded) bench at N=1:
-# a reduced size first, then the full 85 M records / 1 M requests.
+# GPU parity tests for the query kernels, then the config-3 (whole-genome,
+# contig-sharded) bench at N=1, full size
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -9,7 +9,6 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; tail -4 $R/gpurun_out/$name.log
   case $rc in 0) return 0;; *) exit $rc;; esac
 }
-step gpu_tests 600 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
-step genome_small 600 python3 -u $R/bench.py --workload genome --genome-records 10000000 --genome-requests 100000 --steps 5 --warmup 1 --cpu-seconds 5
-step genome_full 900 python3 -u $R/bench.py --workload genome --steps 5 --warmup 1
+step gpu_tests_q 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_genome.py tests/test_route_golden.py -m gpu -x -v --timeout 300 --timeout-method thread
+step genome_full 900 python3 -u $R/bench.py --workload genome --steps ${STEPS:-5} --warmup 1 ${EXTRA:-}
 exit 0
