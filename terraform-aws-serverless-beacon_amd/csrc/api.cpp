@@ -363,6 +363,11 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.d.planes = dev_upload(s, planes);
     s.d.fb = dev_upload(s, fb);
     s.d.bucket = dev_upload(s, bucket);
+    {
+        std::vector<uint64_t> sum8(sum.size());
+        for (size_t i = 0; i < sum.size(); ++i) sum8[i] = pack_sum(sum[i]);
+        s.ds.sum8 = dev_upload(s, sum8);
+    }
     s.ds.sum = dev_upload(s, sum);
     s.ds.start = dev_upload(s, start);
     s.ds.cur = dev_upload(s, cur);
@@ -613,6 +618,14 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         for (auto &g : B.groups)
             if (!g.idx.empty()) keep.push_back(std::move(g));
         B.groups = std::move(keep);
+        // launch order = (segment, first base): neighbouring waves scan
+        // neighbouring records (with the kernels' XCD-aware block order,
+        // one XCD's L2 serves a contiguous stretch of the store)
+        for (auto &g : B.groups)
+            std::stable_sort(g.idx.begin(), g.idx.end(), [&](uint32_t a, uint32_t b) {
+                const QDev &x = B.hq[a], &y = B.hq[b];
+                return x.seg_lo != y.seg_lo ? x.seg_lo < y.seg_lo : x.first_bp < y.first_bp;
+            });
     }
     if (lut_all.empty()) lut_all.push_back(0);
     // ---- device buffers
@@ -627,7 +640,6 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     if (!subsets.empty()) HIP_OK(hipMemcpyAsync(B.subsets.p, subsets.data(), subsets.size() * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(B.lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
     for (auto &g : B.groups) {
-        if (B.groups.size() == 1) break;  // one group covers every query in order: no index list
         g.d_idx.alloc(g.idx.size() * 4);
         HIP_OK(hipMemcpyAsync(g.d_idx.p, g.idx.data(), g.idx.size() * 4, hipMemcpyHostToDevice, st));
     }
@@ -651,7 +663,7 @@ void run(sb_batch &B) {
     const auto &E = B.ev[B.runs_pending++];
     HIP_OK(hipEventRecord(E[0], st));
     for (const auto &g : B.groups)
-        launch_scan(d, B.q.as<QDev>(), B.groups.size() == 1 ? nullptr : g.d_idx.as<uint32_t>(),
+        launch_scan(d, B.q.as<QDev>(), g.d_idx.as<uint32_t>(),
                     static_cast<uint32_t>(g.idx.size()), B.nonneg, g.max_words, g.mode, B.qbytes.as<uint8_t>(),
                     B.subsets.as<uint64_t>(), B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(),
                     st);
@@ -882,7 +894,7 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
             const uint32_t a = static_cast<uint32_t>(std::lower_bound(kb + klo, kb + khi, rs) - kb);
             const uint32_t e = static_cast<uint32_t>(std::upper_bound(kb + klo, kb + khi, re) - kb);
             if (e > a) {
-                segs.push_back(KSeg{a, n, e - a, static_cast<uint32_t>(j)});
+                segs.push_back(KSeg{a, n, e - a, static_cast<uint32_t>(j), rs, 0});
                 n += e - a;
             }
         }
@@ -899,39 +911,90 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
         const int b = atoi(e);
         if (b > 0 && b < 64) mask = (1ull << b) - 1;
     }
+    // exact-word window: POS - rangeStart of every gathered key fits pos_bits
+    uint64_t max_rel = 0;
+    for (const KSeg &g : segs) max_rel = std::max<uint64_t>(max_rel, s.h_dk_pos[g.key_lo + g.n - 1] - g.range_start);
+    uint32_t pos_bits = 1;
+    while (pos_bits < 40 && (max_rel >> pos_bits)) ++pos_bits;
+    if (job_bits + pos_bits + 6 > 64 || mask != ~0ull) pos_bits = 0;  // exact stream off (all keys hashed)
+    const uint32_t exact_job_shift = pos_bits + 6;
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
-    DevMem dseg, k0, v0, k1, v1, hist, bsum, counts, coll, ncoll;
+    std::vector<uint2> tiles;  // gather tiles: (segment, first key offset)
+    const uint32_t gt = dedup_gather_tile();
+    for (uint32_t g = 0; g < segs.size(); ++g)
+        for (uint32_t o = 0; o < segs[g].n; o += gt) tiles.push_back(uint2{g, o});
+    const uint32_t ntiles = static_cast<uint32_t>(tiles.size());
+    const uint64_t slots = static_cast<uint64_t>(ntiles) * gt;  // sparse gather layout
+    const uint64_t maxt = std::max<uint64_t>(ntiles, (n + gt - 1) / gt);
+    DevMem dseg, dtiles, tcnt, ke0, ke1, kh0, vh0, kh1, vh1, hist, bsum, counts, coll, ncoll, pe, ph;
     dseg.alloc(segs.size() * sizeof(KSeg));
-    k0.alloc(n * 8);
-    v0.alloc(n * 4);
-    k1.alloc(n * 8);
-    v1.alloc(n * 4);
-    hist.alloc(radix_hist_words(n) * 4);
-    bsum.alloc(radix_bsum_words(n) * 4);
+    dtiles.alloc(tiles.size() * sizeof(uint2));
+    tcnt.alloc(2 * static_cast<size_t>(ntiles) * 4);
+    ke0.alloc(slots * 8);
+    ke1.alloc(n * 8);
+    kh0.alloc(slots * 8);
+    vh0.alloc(slots * 4);
+    kh1.alloc(n * 8);
+    vh1.alloc(n * 4);
+    hist.alloc(maxt * 256 * 4);
+    bsum.alloc(radix_bsum_words(maxt * gt) * 4);
     counts.alloc(std::max<size_t>(nj, 1) * 8);
     coll.alloc(n * 4);
     ncoll.alloc(4);
     if (!segs.empty()) HIP_OK(hipMemcpyAsync(dseg.p, segs.data(), segs.size() * sizeof(KSeg), hipMemcpyHostToDevice, st));
+    if (!tiles.empty())
+        HIP_OK(hipMemcpyAsync(dtiles.p, tiles.data(), tiles.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(counts.p, 0, counts.bytes, st));
     HIP_OK(hipMemsetAsync(ncoll.p, 0, 4, st));
     hipEvent_t e0, e1;
     HIP_OK(hipEventCreate(&e0));
     HIP_OK(hipEventCreate(&e1));
     HIP_OK(hipEventRecord(e0, st));
-    launch_dedup_gather(s.dk, dseg.as<KSeg>(), static_cast<uint32_t>(segs.size()), n, job_bits, mask,
-                        k0.as<uint64_t>(), v0.as<uint32_t>(), st);
-    launch_radix_sort(k0.as<uint64_t>(), v0.as<uint32_t>(), k1.as<uint64_t>(), v1.as<uint32_t>(), n,
-                      hist.as<uint32_t>(), bsum.as<uint32_t>(), st);
-    launch_dedup_unique(k0.as<uint64_t>(), v0.as<uint32_t>(), n, s.dk, job_bits, counts.as<unsigned long long>(),
-                        coll.as<uint32_t>(), ncoll.as<uint32_t>(), st);
+    launch_dedup_gather(s.dk, dseg.as<KSeg>(), dtiles.as<uint2>(), ntiles, pos_bits, exact_job_shift, job_bits, mask,
+                        ke0.as<uint64_t>(), kh0.as<uint64_t>(), vh0.as<uint32_t>(), tcnt.as<uint32_t>(), st);
+    std::vector<uint32_t> htc(2 * static_cast<size_t>(ntiles));
+    if (!htc.empty()) HIP_OK(hipMemcpyAsync(htc.data(), tcnt.p, htc.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    uint64_t ne = 0, nh = 0;
+    for (uint32_t t = 0; t < ntiles; ++t) {
+        ne += htc[t];
+        nh += htc[ntiles + t];
+    }
+    if (ne + nh != n) throw Error(SB_EHIP, "dedup gather lost keys");
+    const uint32_t be = dedup_unique_blocks(ne), bh = dedup_unique_blocks(nh);
+    pe.alloc(std::max<uint32_t>(be, 1) * sizeof(uint4));
+    ph.alloc(std::max<uint32_t>(bh, 1) * sizeof(uint4));
+    // exact stream: keys only, as many 8-bit passes as its words have bits;
+    // the first pass compacts the gather tiles
+    const int re = launch_radix_sort(ke0.as<uint64_t>(), nullptr, ke1.as<uint64_t>(), nullptr, ne,
+                                     job_bits + pos_bits + 6, hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
+                                     tcnt.as<uint32_t>(), ntiles);
+    launch_dedup_unique(re ? ke1.as<uint64_t>() : ke0.as<uint64_t>(), nullptr, ne, s.dk, exact_job_shift, false,
+                        counts.as<unsigned long long>(), pe.as<uint4>(), coll.as<uint32_t>(), ncoll.as<uint32_t>(), st);
+    // hashed stream: (job | hash, key id), 8 passes, equal words confirmed
+    const int rh = launch_radix_sort(kh0.as<uint64_t>(), vh0.as<uint32_t>(), kh1.as<uint64_t>(), vh1.as<uint32_t>(),
+                                     nh, 64, hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
+                                     tcnt.as<uint32_t>() + ntiles, ntiles);
+    DevMem &kh = rh ? kh1 : kh0;
+    DevMem &vh = rh ? vh1 : vh0;
+    launch_dedup_unique(kh.as<uint64_t>(), vh.as<uint32_t>(), nh, s.dk, job_bits ? 64 - job_bits : 64, true,
+                        counts.as<unsigned long long>(), ph.as<uint4>(), coll.as<uint32_t>(), ncoll.as<uint32_t>(), st);
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipGetLastError());
     std::vector<uint64_t> cnt(std::max<size_t>(nj, 1));
     uint32_t nc = 0;
     HIP_OK(hipMemcpyAsync(cnt.data(), counts.p, cnt.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(&nc, ncoll.p, 4, hipMemcpyDeviceToHost, st));
+    std::vector<uint4> hpe(be), hph(bh);
+    if (be) HIP_OK(hipMemcpyAsync(hpe.data(), pe.p, be * sizeof(uint4), hipMemcpyDeviceToHost, st));
+    if (bh) HIP_OK(hipMemcpyAsync(hph.data(), ph.p, bh * sizeof(uint4), hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
+    for (const auto *P : {&hpe, &hph})
+        for (const uint4 &q : *P) {  // per-block partials: first and last job of each block
+            cnt[q.x] += q.y;
+            if (q.z != q.x) cnt[q.z] += q.w;
+        }
     float ms = 0;
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
@@ -939,10 +1002,11 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
     if (nc) {
         // exact recount of every group holding a collision: the device counted
         // 1 + (adjacent string changes) for it; replace that by |distinct|
+        const uint64_t n = nh;  // collisions live in the hashed stream
         std::vector<uint64_t> hk(n);
         std::vector<uint32_t> hv(n), ci(nc);
-        HIP_OK(hipMemcpy(hk.data(), k0.p, n * 8, hipMemcpyDeviceToHost));
-        HIP_OK(hipMemcpy(hv.data(), v0.p, n * 4, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(hk.data(), kh.p, n * 8, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(hv.data(), vh.p, n * 4, hipMemcpyDeviceToHost));
         HIP_OK(hipMemcpy(ci.data(), coll.p, nc * 4, hipMemcpyDeviceToHost));
         std::sort(ci.begin(), ci.end());
         uint64_t done_to = 0;  // groups end before this index

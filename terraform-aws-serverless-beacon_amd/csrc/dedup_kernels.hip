@@ -6,16 +6,22 @@
 // answer is the set size.  Here the region keys already sit in HBM (one 64-bit
 // hash + a tail word per key, devtypes.hpp KStore), and a batch of jobs is
 // answered with
-//   1. gather:   the keys of every job's VCF ranges -> (job | hash, key id)
-//   2. LSD radix sort of the 64-bit words, 8 passes of 8 bits, each pass =
-//      tile histogram (upsweep) + exclusive scan + stable rank-and-scatter
-//      (downsweep: wave-level match via 8 ballots, per-wave LDS counters)
-//   3. unique:   adjacent compare; equal words are confirmed byte-for-byte on
-//      the key strings, and pairs whose strings differ (hash collisions) are
-//      listed for the host's exact recount of that group.
-// Sorting by (job, hash) keeps every job contiguous, so the whole batch is one
-// sort.  All passes are HBM-streaming integer work: 256-thread workgroups, one
-// tile of 4096 keys each, coalesced 64-lane loads.
+//   1. gather:   the keys of every job's VCF ranges, split into two streams
+//      (devtypes.hpp, exact dedup words): EXACT words (job | P - rangeStart |
+//      REF/ALT codes) for single-base REF/ALT keys, keys only; HASHED words
+//      (job | hash) with their key ids for everything else;
+//   2. LSD radix sort of each stream, 8-bit digits, only as many passes as
+//      the stream's words have bits (exact: job + window + 6 bits, typically
+//      5 passes; hashed: 8), each pass = tile histogram (upsweep) + exclusive
+//      scan + stable rank-and-scatter (downsweep: wave-level match via 8
+//      ballots, per-wave LDS counters, LDS-staged coalesced writes);
+//   3. unique:   adjacent compare per stream.  Exact words are the strings;
+//      equal hashed words are confirmed byte-for-byte on the key strings, and
+//      pairs whose strings differ (hash collisions) are listed for the host's
+//      exact recount of that group.
+// Sorting by (job, word) keeps every job contiguous, so the whole batch is one
+// sort per stream.  All passes are HBM-streaming integer work: 256-thread
+// workgroups, one tile of 4096 keys each, coalesced 64-lane loads.
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
@@ -35,37 +41,155 @@ __device__ __forceinline__ uint32_t popc_below(uint64_t m) {
 }
 
 // ------------------------------------------------------------------ gather
-__global__ __launch_bounds__(kThreads) void gather_kernel(KStore ks, const KSeg *segs, uint32_t nseg, uint64_t n,
-                                                          uint32_t job_bits, uint64_t mask, uint64_t *keys,
-                                                          uint32_t *vals) {
-    const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
-    if (i >= n) return;
-    uint32_t lo = 0, hi = nseg;  // last segment with out_lo <= i
-    while (hi - lo > 1) {
-        const uint32_t m = (lo + hi) >> 1;
-        if (segs[m].out_lo <= i) lo = m; else hi = m;
+// canonical exact code of a key (devtypes.hpp): 0 = hashed stream
+__device__ __forceinline__ uint32_t exact_word(const KBody &b, uint32_t rs, uint32_t pos_bits, uint64_t *rel) {
+    const uint64_t t = b.tail;
+    if ((t & kTailBlob) || b.pos == 0) return 0;
+    const uint32_t len = static_cast<uint32_t>(t >> 56);
+    uint64_t P = b.pos;
+    uint32_t d = 0;
+    while (d < len) {
+        const uint32_t c = static_cast<uint32_t>(t >> (8 * d)) & 0xffu;
+        if (c < '0' || c > '9') break;
+        P = P * 10 + (c - '0');
+        ++d;
     }
-    const KSeg g = segs[lo];
-    const uint64_t k = g.key_lo + (i - g.out_lo);
-    const uint64_t h = ks.hash[k] & mask;
-    keys[i] = job_bits ? ((static_cast<uint64_t>(g.job) << (64 - job_bits)) | (h >> job_bits)) : h;
-    vals[i] = static_cast<uint32_t>(k);
+    if (len - d != 3) return 0;
+    const uint32_t c1 = static_cast<uint32_t>(t >> (8 * d)) & 0xffu;
+    const uint32_t us = static_cast<uint32_t>(t >> (8 * d + 8)) & 0xffu;
+    const uint32_t c2 = static_cast<uint32_t>(t >> (8 * d + 16)) & 0xffu;
+    if (us != '_' || c1 < 1 || c1 > 7 || c2 < 1 || c2 > 7) return 0;
+    if (P < rs || ((P - rs) >> pos_bits) != 0) return 0;  // outside the window: hashed stream
+    *rel = P - rs;
+    return (c1 << 3) | c2;
+}
+
+// One workgroup per host-planned tile of kTile keys of ONE segment (no
+// per-key segment search): every body load is issued first, then the class of
+// each key, then the hash loads of the (rare) hashed keys.  Each tile writes
+// its exact words and its hashed (word, key id) pairs compacted at the start
+// of its OWN kTile-slot region of the two streams and its two counts into
+// tcnt[tile] / tcnt[ntiles + tile]: no cross-workgroup atomics.  The first
+// radix pass reads the streams tile by tile (tile_n = tcnt) and leaves them
+// dense.
+constexpr int kGItems = kItems;
+constexpr uint32_t kGTile = kThreads * kGItems;
+static_assert(kGTile == static_cast<uint32_t>(kTile), "gather tiles are radix tiles");
+__global__ __launch_bounds__(kThreads) void gather_kernel(KStore ks, const KSeg *segs, const uint2 *tiles,
+                                                          uint32_t ntiles, uint32_t pos_bits,
+                                                          uint32_t exact_job_shift, uint32_t job_bits, uint64_t mask,
+                                                          uint64_t *ke, uint64_t *kh, uint32_t *vh, uint32_t *tcnt) {
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint2 T = tiles[blockIdx.x];  // (segment, first key offset in it)
+    const KSeg g = segs[T.x];
+    // two halves of kGItems / 2 keys: their body loads are issued together,
+    // then classified; words are staged in LDS (slot r * kThreads + tid) so
+    // only two flag masks stay live across the phases
+    __shared__ uint64_t s_word[kGTile];
+    __shared__ uint32_t s_off[2][kGItems][kWaves];
+    constexpr int kHalf = kGItems / 2;
+    uint32_t exm = 0, okm = 0;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        KBody body[kHalf];
+#pragma unroll
+        for (int q = 0; q < kHalf; ++q) {
+            const uint32_t j = T.y + static_cast<uint32_t>(h * kHalf + q) * kThreads + threadIdx.x;
+            body[q] = j < g.n ? ks.body[g.key_lo + j] : KBody{0, 0, 0};
+        }
+#pragma unroll
+        for (int q = 0; q < kHalf; ++q) {
+            const int r = h * kHalf + q;
+            const uint32_t j = T.y + static_cast<uint32_t>(r) * kThreads + threadIdx.x;
+            if (j >= g.n) continue;
+            okm |= 1u << r;
+            uint64_t rel = 0;
+            const uint32_t code = pos_bits ? exact_word(body[q], g.range_start, pos_bits, &rel) : 0u;
+            if (code) {
+                exm |= 1u << r;
+                s_word[r * kThreads + threadIdx.x] =
+                    (static_cast<uint64_t>(g.job) << exact_job_shift) | (rel << 6) | code;
+            }
+        }
+    }
+    const uint32_t hm = okm & ~exm;
+    if (hm) {
+        uint64_t hv[kGItems];
+#pragma unroll
+        for (int r = 0; r < kGItems; ++r)
+            hv[r] = ((hm >> r) & 1u) ? ks.hash[g.key_lo + T.y + static_cast<uint32_t>(r) * kThreads + threadIdx.x] : 0;
+#pragma unroll
+        for (int r = 0; r < kGItems; ++r) {
+            if ((hm >> r) & 1u) {
+                const uint64_t x = hv[r] & mask;
+                s_word[r * kThreads + threadIdx.x] =
+                    job_bits ? ((static_cast<uint64_t>(g.job) << (64 - job_bits)) | (x >> job_bits)) : x;
+            }
+        }
+    }
+    // tile-local positions in (item, wave, lane) order so that every store
+    // instruction writes consecutive slots: per-(item, wave) counts from
+    // ballots, a serial exclusive scan over the 2 x kGItems x kWaves counts,
+    // popc_below inside the wave
+#pragma unroll
+    for (int r = 0; r < kGItems; ++r) {
+        const uint64_t me = __ballot((exm >> r) & 1u);
+        const uint64_t mh = __ballot((hm >> r) & 1u);
+        if (lane == 0) {
+            s_off[0][r][w] = static_cast<uint32_t>(__popcll(me));
+            s_off[1][r][w] = static_cast<uint32_t>(__popcll(mh));
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        uint32_t run = 0;
+        uint32_t *o = &s_off[threadIdx.x][0][0];
+        for (int x = 0; x < kGItems * kWaves; ++x) {
+            const uint32_t c = o[x];
+            o[x] = run;
+            run += c;
+        }
+        tcnt[threadIdx.x * ntiles + blockIdx.x] = run;
+    }
+    __syncthreads();
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kTile;
+#pragma unroll
+    for (int r = 0; r < kGItems; ++r) {
+        const bool e = (exm >> r) & 1u, hh = (hm >> r) & 1u;
+        const uint64_t me = __ballot(e), mh = __ballot(hh);
+        if (e) {
+            ke[t0 + s_off[0][r][w] + popc_below(me)] = s_word[r * kThreads + threadIdx.x];
+        } else if (hh) {
+            const uint64_t d = t0 + s_off[1][r][w] + popc_below(mh);
+            kh[d] = s_word[r * kThreads + threadIdx.x];
+            vh[d] = static_cast<uint32_t>(g.key_lo + T.y + static_cast<uint32_t>(r) * kThreads + threadIdx.x);
+        }
+    }
 }
 
 // ------------------------------------------------------------- radix sort
 // hist layout: digit-major, hist[d * ntiles + tile]
-__global__ __launch_bounds__(kThreads) void upsweep_kernel(const uint64_t *keys, uint64_t n, uint32_t shift,
-                                                           uint32_t *hist, uint32_t ntiles) {
+// keys of tile b: dense (tile_n == nullptr) = [b * kTile, min(n, ..+kTile));
+// sparse (the first pass after gather) = the first tile_n[b] slots of tile b
+__device__ __forceinline__ uint32_t tile_count(uint64_t n, const uint32_t *tile_n) {
+    if (tile_n) return tile_n[blockIdx.x];
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kTile;
+    return static_cast<uint32_t>(min(static_cast<uint64_t>(kTile), n - t0));
+}
+
+__global__ __launch_bounds__(kThreads) void upsweep_kernel(const uint64_t *keys, uint64_t n, const uint32_t *tile_n,
+                                                           uint32_t shift, uint32_t *hist, uint32_t ntiles) {
     __shared__ uint32_t h[kWaves][256];
     const int w = threadIdx.x >> 6;
     for (int i = threadIdx.x; i < kWaves * 256; i += kThreads) (&h[0][0])[i] = 0;
     __syncthreads();
     const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kTile;
+    const uint32_t tn = tile_count(n, tile_n);
     uint32_t dg[kItems];
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
-        const uint64_t i = base + static_cast<uint64_t>(r) * kThreads + threadIdx.x;
-        dg[r] = i < n ? static_cast<uint32_t>(keys[i] >> shift) & 255u : 256u;
+        const uint32_t j = static_cast<uint32_t>(r) * kThreads + threadIdx.x;
+        dg[r] = j < tn ? static_cast<uint32_t>(keys[base + j] >> shift) & 255u : 256u;
     }
 #pragma unroll
     for (int r = 0; r < kItems; ++r)
@@ -98,27 +222,32 @@ __device__ __forceinline__ uint32_t block_exclusive(uint32_t x, uint32_t *lds, u
     return wofs + inc - x;
 }
 
+template <bool VALS>
 __global__ __launch_bounds__(kThreads) void downsweep_kernel(const uint64_t *kin, const uint32_t *vin,
                                                              uint64_t *kout, uint32_t *vout, uint64_t n,
-                                                             uint32_t shift, const uint32_t *off, uint32_t ntiles) {
+                                                             const uint32_t *tile_n, uint32_t shift,
+                                                             const uint32_t *off, uint32_t ntiles) {
     __shared__ uint32_t cnt[kWaves][256];
     const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
     for (int i = threadIdx.x; i < kWaves * 256; i += kThreads) (&cnt[0][0])[i] = 0;
     __syncthreads();
-    const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kTile + static_cast<uint64_t>(w) * kWaveKeys;
+    const uint64_t tile0 = static_cast<uint64_t>(blockIdx.x) * kTile;
+    const uint32_t tn = tile_count(n, tile_n);
+    const uint32_t wbase = static_cast<uint32_t>(w) * kWaveKeys;  // tile-local
     uint64_t k[kItems];
     uint32_t v[kItems], rank[kItems];
     // all of the wave's loads in flight first, then rank in index order
     // (wave w owns a contiguous quarter of the tile)
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
-        const uint64_t i = base + static_cast<uint64_t>(r) * 64 + lane;
-        k[r] = i < n ? kin[i] : 0;
-        v[r] = i < n ? vin[i] : 0;
+        const uint32_t j = wbase + static_cast<uint32_t>(r) * 64 + lane;
+        k[r] = j < tn ? kin[tile0 + j] : 0;
+        v[r] = (VALS && j < tn) ? vin[tile0 + j] : 0;
     }
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
-        const bool ok = base + static_cast<uint64_t>(r) * 64 + lane < n;
+        if (wbase + static_cast<uint32_t>(r) * 64 >= tn) break;  // wave-uniform: the rest of the wave's slots are empty
+        const bool ok = wbase + static_cast<uint32_t>(r) * 64 + lane < tn;
         const uint32_t d = static_cast<uint32_t>(k[r] >> shift) & 255u;
         uint64_t peers = __ballot(ok);
 #pragma unroll
@@ -156,20 +285,17 @@ __global__ __launch_bounds__(kThreads) void downsweep_kernel(const uint64_t *kin
     // stage the tile in digit order, then write runs of equal digits
     // contiguously (avg. 16 keys = 128 B per digit run)
     __shared__ uint64_t sk[kTile];
-    __shared__ uint32_t sv[kTile];
+    __shared__ uint32_t sv[VALS ? kTile : 1];
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
-        const uint64_t i = base + static_cast<uint64_t>(r) * 64 + lane;
-        if (i < n) {
+        if (wbase + static_cast<uint32_t>(r) * 64 + lane < tn) {
             const uint32_t d = static_cast<uint32_t>(k[r] >> shift) & 255u;
             const uint32_t loc = cnt[w][d] + rank[r];
             sk[loc] = k[r];
-            sv[loc] = v[r];
+            if (VALS) sv[loc] = v[r];
         }
     }
     __syncthreads();
-    const uint64_t tile0 = static_cast<uint64_t>(blockIdx.x) * kTile;
-    const uint32_t tn = static_cast<uint32_t>(min(static_cast<uint64_t>(kTile), n - tile0));
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
         const uint32_t loc = static_cast<uint32_t>(r) * kThreads + threadIdx.x;
@@ -177,7 +303,7 @@ __global__ __launch_bounds__(kThreads) void downsweep_kernel(const uint64_t *kin
             const uint64_t key = sk[loc];
             const uint32_t dst = gbase[static_cast<uint32_t>(key >> shift) & 255u] + loc;
             kout[dst] = key;
-            vout[dst] = sv[loc];
+            if (VALS) vout[dst] = sv[loc];
         }
     }
 }
@@ -259,10 +385,7 @@ __device__ KeyStr key_str(const KStore &ks, const KBody &k) {
     return s;
 }
 
-__device__ bool key_equal(const KStore &ks, uint32_t a, uint32_t b) {
-    if (a == b) return true;
-    const KBody x = ks.body[a], y = ks.body[b];
-    if (x.pos == y.pos && x.tail == y.tail) return true;  // same pos and same inline bytes / same blob bytes
+__device__ __noinline__ bool key_equal_slow(const KStore &ks, const KBody &x, const KBody &y) {
     const KeyStr u = key_str(ks, x), v = key_str(ks, y);
     if (u.nd + u.tl != v.nd + v.tl) return false;
     for (uint32_t j = 0; j < u.nd + u.tl; ++j)
@@ -270,50 +393,88 @@ __device__ bool key_equal(const KStore &ks, uint32_t a, uint32_t b) {
     return true;
 }
 
+// equal key strings?  Same POS (the common case of an equal hashed word):
+// the tails must match — inline words directly, blob tails byte by byte;
+// different POS: the general decimal-concatenation comparison.
+__device__ bool key_equal(const KStore &ks, uint32_t a, uint32_t b) {
+    if (a == b) return true;
+    const KBody x = ks.body[a], y = ks.body[b];
+    if (x.pos == y.pos) {
+        if (x.tail == y.tail) return true;
+        if (!((x.tail & y.tail) & kTailBlob)) return false;  // inline vs other: different bytes or lengths
+        const uint32_t lx = static_cast<uint32_t>((x.tail >> 40) & 0xffff), ly = static_cast<uint32_t>((y.tail >> 40) & 0xffff);
+        if (lx != ly) return false;
+        const uint8_t *p = ks.blob + (x.tail & ((1ull << 40) - 1)), *q = ks.blob + (y.tail & ((1ull << 40) - 1));
+        for (uint32_t j = 0; j < lx; ++j)
+            if (p[j] != q[j]) return false;
+        return true;
+    }
+    return key_equal_slow(ks, x, y);
+}
+
 // kItems sorted positions per thread (coalesced: item r of the block is
 // r * kThreads + threadIdx.x); the block's distinct count goes out with one
 // atomic per job it touches (one in the common single-job block)
+// Per block: the fresh (distinct) keys of its first and last job go to
+// part[block] = {job_first, count_first, job_last, count_last} (the host sums
+// them: no same-address atomics across workgroups); jobs strictly inside a
+// block (a job with fewer keys than a tile) take a global atomic.
+template <bool VERIFY>
 __global__ __launch_bounds__(kThreads) void unique_kernel(const uint64_t *keys, const uint32_t *vals, uint64_t n,
-                                                          KStore ks, uint32_t job_bits, unsigned long long *counts,
-                                                          uint32_t *coll, uint32_t *ncoll) {
+                                                          KStore ks, uint32_t job_shift, unsigned long long *counts,
+                                                          uint4 *part, uint32_t *coll, uint32_t *ncoll) {
     __shared__ uint32_t s_job[2];
-    __shared__ unsigned int s_cnt;
+    __shared__ unsigned int s_cnt[2];
     const uint64_t base = static_cast<uint64_t>(blockIdx.x) * kTile;
+    const int lane = threadIdx.x & 63;
     if (threadIdx.x == 0) {
-        s_cnt = 0;
+        s_cnt[0] = s_cnt[1] = 0;
         const uint64_t last = min(n, base + kTile) - 1;
-        s_job[0] = job_bits ? static_cast<uint32_t>(keys[base] >> (64 - job_bits)) : 0u;
-        s_job[1] = job_bits ? static_cast<uint32_t>(keys[last] >> (64 - job_bits)) : 0u;
+        s_job[0] = job_shift < 64 ? static_cast<uint32_t>(keys[base] >> job_shift) : 0u;
+        s_job[1] = job_shift < 64 ? static_cast<uint32_t>(keys[last] >> job_shift) : 0u;
     }
-    __syncthreads();
-    const bool one_job = s_job[0] == s_job[1];
-    uint32_t mine = 0;
-#pragma unroll 4
+    // all loads in flight first: item r of the block is r * kThreads + tid;
+    // its predecessor is lane - 1's item (shuffle), lane 0 loads its own
+    uint64_t k[kItems], kp0[kItems];
+#pragma unroll
     for (int r = 0; r < kItems; ++r) {
         const uint64_t i = base + static_cast<uint64_t>(r) * kThreads + threadIdx.x;
-        if (i >= n) break;
-        const uint64_t k = keys[i];
+        k[r] = i < n ? keys[i] : 0ull;
+        kp0[r] = (lane == 0 && i > 0 && i < n) ? keys[i - 1] : 0ull;
+    }
+    __syncthreads();
+    const uint32_t jf = s_job[0], jl = s_job[1];
+    uint32_t cf = 0, cl = 0;
+#pragma unroll
+    for (int r = 0; r < kItems; ++r) {
+        const uint64_t i = base + static_cast<uint64_t>(r) * kThreads + threadIdx.x;
+        const uint32_t plo = __shfl_up(static_cast<uint32_t>(k[r]), 1, 64);
+        const uint32_t phi = __shfl_up(static_cast<uint32_t>(k[r] >> 32), 1, 64);
+        const uint64_t prev = lane ? ((static_cast<uint64_t>(phi) << 32) | plo) : kp0[r];
+        if (i >= n) continue;
         bool fresh = false;
-        if (i == 0 || keys[i - 1] != k) {
+        if (i == 0 || prev != k[r]) {
             fresh = true;
-        } else if (!key_equal(ks, vals[i - 1], vals[i])) {
+        } else if (VERIFY && !key_equal(ks, vals[i - 1], vals[i])) {
             fresh = true;  // a different string under the same word: the host recounts its group
             coll[atomicAdd(ncoll, 1u)] = static_cast<uint32_t>(i);
         }
         if (!fresh) continue;
-        if (one_job) {
-            ++mine;
-        } else {
-            atomicAdd(&counts[job_bits ? static_cast<uint32_t>(k >> (64 - job_bits)) : 0u], 1ull);
-        }
+        const uint32_t j = job_shift < 64 ? static_cast<uint32_t>(k[r] >> job_shift) : 0u;
+        if (j == jf) ++cf;
+        else if (j == jl) ++cl;
+        else atomicAdd(&counts[j], 1ull);
     }
-    if (one_job) {
-        // wave sum, then one LDS add per wave and one global atomic per block
-        for (int d = 32; d >= 1; d >>= 1) mine += __shfl_xor(mine, d, 64);
-        if ((threadIdx.x & 63) == 0 && mine) atomicAdd(&s_cnt, mine);
-        __syncthreads();
-        if (threadIdx.x == 0 && s_cnt) atomicAdd(&counts[s_job[0]], static_cast<unsigned long long>(s_cnt));
+    for (int d = 32; d >= 1; d >>= 1) {
+        cf += __shfl_xor(cf, d, 64);
+        cl += __shfl_xor(cl, d, 64);
     }
+    if (lane == 0) {
+        if (cf) atomicAdd(&s_cnt[0], cf);
+        if (cl) atomicAdd(&s_cnt[1], cl);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) part[blockIdx.x] = uint4{jf, s_cnt[0], jl, s_cnt[1]};
 }
 
 uint32_t tiles_of(uint64_t n) { return static_cast<uint32_t>((n + kTile - 1) / kTile); }
@@ -330,35 +491,48 @@ void exclusive_scan(uint32_t *a, uint64_t m, uint32_t *bsum, hipStream_t s) {
 size_t radix_hist_words(uint64_t n) { return static_cast<size_t>(tiles_of(n)) * 256; }
 size_t radix_bsum_words(uint64_t n) { return (radix_hist_words(n) + kTile - 1) / kTile + 1; }
 
-void launch_dedup_gather(const KStore &ks, const KSeg *segs, uint32_t nseg, uint64_t n, uint32_t job_bits,
-                         uint64_t mask, uint64_t *keys, uint32_t *vals, hipStream_t s) {
-    if (!n) return;
-    gather_kernel<<<static_cast<uint32_t>((n + kThreads - 1) / kThreads), kThreads, 0, s>>>(ks, segs, nseg, n,
-                                                                                           job_bits, mask, keys, vals);
+uint32_t dedup_gather_tile() { return kGTile; }
+
+void launch_dedup_gather(const KStore &ks, const KSeg *segs, const uint2 *tiles, uint32_t ntiles, uint32_t pos_bits,
+                         uint32_t exact_job_shift, uint32_t job_bits, uint64_t mask, uint64_t *ke, uint64_t *kh,
+                         uint32_t *vh, uint32_t *tcnt, hipStream_t s) {
+    if (!ntiles) return;
+    gather_kernel<<<ntiles, kThreads, 0, s>>>(ks, segs, tiles, ntiles, pos_bits, exact_job_shift, job_bits, mask, ke,
+                                              kh, vh, tcnt);
 }
 
-int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t *hist,
-                      uint32_t *bsum, hipStream_t s) {
-    if (n <= 1) return 0;
-    const uint32_t nt = tiles_of(n);
+int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t bits,
+                      uint32_t *hist, uint32_t *bsum, hipStream_t s, const uint32_t *tile_n, uint32_t sparse_tiles) {
+    if (n == 0) return 0;
+    if (n <= 1 && !tile_n) return 0;
     uint64_t *kin = k0, *kout = k1;
     uint32_t *vin = v0, *vout = v1;
-    for (uint32_t shift = 0; shift < 64; shift += 8) {
-        upsweep_kernel<<<nt, kThreads, 0, s>>>(kin, n, shift, hist, nt);
+    for (uint32_t shift = 0; shift < bits || (tile_n && shift == 0); shift += 8) {
+        const bool sparse = tile_n && shift == 0;  // the first pass compacts the gather tiles
+        const uint32_t nt = sparse ? sparse_tiles : tiles_of(n);
+        const uint32_t *tn = sparse ? tile_n : nullptr;
+        upsweep_kernel<<<nt, kThreads, 0, s>>>(kin, n, tn, shift, hist, nt);
         exclusive_scan(hist, static_cast<uint64_t>(nt) * 256, bsum, s);
-        downsweep_kernel<<<nt, kThreads, 0, s>>>(kin, vin, kout, vout, n, shift, hist, nt);
+        if (vin)
+            downsweep_kernel<true><<<nt, kThreads, 0, s>>>(kin, vin, kout, vout, n, tn, shift, hist, nt);
+        else
+            downsweep_kernel<false><<<nt, kThreads, 0, s>>>(kin, vin, kout, vout, n, tn, shift, hist, nt);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
-    return kin == k0 ? 0 : 1;  // 8 passes: the result is back in (k0, v0)
+    return kin == k0 ? 0 : 1;
 }
 
-void launch_dedup_unique(const uint64_t *keys, const uint32_t *vals, uint64_t n, const KStore &ks, uint32_t job_bits,
-                         unsigned long long *counts, uint32_t *coll, uint32_t *ncoll, hipStream_t s) {
+uint32_t dedup_unique_blocks(uint64_t n) { return n ? tiles_of(n) : 0; }
+
+void launch_dedup_unique(const uint64_t *keys, const uint32_t *vals, uint64_t n, const KStore &ks, uint32_t job_shift,
+                         bool verify, unsigned long long *counts, uint4 *part, uint32_t *coll, uint32_t *ncoll,
+                         hipStream_t s) {
     if (!n) return;
-    unique_kernel<<<tiles_of(n), kThreads, 0, s>>>(keys, vals, n, ks,
-                                                                                           job_bits, counts, coll,
-                                                                                           ncoll);
+    if (verify)
+        unique_kernel<true><<<tiles_of(n), kThreads, 0, s>>>(keys, vals, n, ks, job_shift, counts, part, coll, ncoll);
+    else
+        unique_kernel<false><<<tiles_of(n), kThreads, 0, s>>>(keys, vals, n, ks, job_shift, counts, part, coll, ncoll);
 }
 
 }  // namespace sb

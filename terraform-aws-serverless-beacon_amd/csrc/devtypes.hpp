@@ -190,6 +190,16 @@ struct alignas(16) SumHot {
 };
 inline constexpr uint32_t kSumUnsupported = 1u << 31;
 
+// The same contribution packed into one 8-byte word for the phase-A stream:
+// rem bits 0..23, numVariants bits 24..31, numCalls bits 32..62; bit 63 =
+// escape (a field does not fit, or the record is unsupported): read SumHot.
+inline constexpr uint64_t kSumEscape = 1ull << 63;
+inline uint64_t pack_sum(const SumHot &h) {
+    const uint64_t nv = h.nvf & ~kSumUnsupported;
+    if ((h.nvf & kSumUnsupported) || h.rem >= (1u << 24) || nv >= 256 || h.nc >= (1ull << 31)) return kSumEscape;
+    return static_cast<uint64_t>(h.rem) | (nv << 24) | (h.nc << 32);
+}
+
 inline constexpr uint32_t kSumChunk = 4096;  // records per phase-A workgroup
 
 struct SDev {  // one summariseSlice invocation after host planning
@@ -213,6 +223,7 @@ struct SRes {
 };
 
 struct SStore {  // summary columns
+    const uint64_t *sum8;   // pack_sum(sum[i]) — the phase-A stream
     const SumHot *sum;
     const uint64_t *start;  // line start, absolute offset in the VCF text stream
     const uint32_t *cur;    // cursor offset after addCounts, relative to start
@@ -244,9 +255,21 @@ struct KStore {
 
 struct KSeg {  // one run of store keys gathered for a job
     uint64_t key_lo;   // first store key
-    uint64_t out_lo;   // first output slot
+    uint64_t out_lo;   // first gather index of the run
     uint32_t n;
     uint32_t job;
+    uint32_t range_start;  // the job's rangeStart (exact words hold POS - rangeStart)
+    uint32_t pad;
 };
+
+// Exact dedup words.  A key string decimal(pos) ++ tail parses uniquely as
+// (P = its longest leading digit run read as a number, rest); when rest is
+// c1 '_' c2 with c1, c2 compressSeq codes 1..7 (single-base REF and ALT: the
+// bulk of every VCF) the string is determined by (P, c1, c2) and the word
+// (job | P - rangeStart | c1 c2) identifies it exactly — equal words need no
+// string comparison.  Every other key (and any P outside the job's window)
+// goes to the hashed stream, whose equal words are confirmed byte-for-byte.
+// Both streams partition the strings (a string's class is a function of the
+// string), so the job's distinct count is the sum of the two streams'.
 
 }  // namespace sb

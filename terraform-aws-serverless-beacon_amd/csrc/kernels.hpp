@@ -38,20 +38,33 @@ void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *
 void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,
                     uint64_t *out, hipStream_t s);
 
-// duplicateVariantSearch (dedup_kernels.hip).  gather writes (job | hash,
-// key id) for every key of every segment; mask trims the hash (tests force
-// collisions with it).  The radix sort ping-pongs (k0, v0) <-> (k1, v1) over
-// 8 passes, so the sorted result is back in (k0, v0); hist needs
-// radix_hist_words(n) and bsum radix_bsum_words(n) u32.  unique adds each
-// job's distinct count into counts[job] and lists (into coll, capacity n)
-// every sorted position whose string differs from its equal-word neighbour.
+// duplicateVariantSearch (dedup_kernels.hip).  gather takes host-planned
+// tiles (segment, key offset) of dedup_gather_tile() keys and splits each
+// tile's keys into the exact stream ke (words only) and the hashed stream
+// (kh, key ids vh), compacted at the start of the tile's own slot region;
+// tcnt[t] / tcnt[ntiles + t] = the tile's exact / hashed counts.  pos_bits = 0
+// disables the exact stream; mask trims the hash (tests force collisions).
+// The radix sort ping-pongs (k0, v0) <-> (k1, v1) over ceil(bits / 8) passes
+// (v0 = nullptr: keys only; tile_n = the per-tile counts of a gathered,
+// sparse input, made dense by the first pass) and returns 1 when the result
+// ends in (k1, v1); hist needs 256 words per tile of the largest pass and
+// bsum radix_bsum_words of that.  unique writes per-block partial counts
+// part[b] = {job_first, n_first, job_last, n_last} (jobs strictly inside a
+// block are added into counts[]); with verify it confirms equal words on the
+// key strings and lists (into coll, capacity n) every sorted position whose
+// string differs from its equal-word neighbour.
 size_t radix_hist_words(uint64_t n);
 size_t radix_bsum_words(uint64_t n);
-void launch_dedup_gather(const KStore &ks, const KSeg *segs, uint32_t nseg, uint64_t n, uint32_t job_bits,
-                         uint64_t mask, uint64_t *keys, uint32_t *vals, hipStream_t s);
-int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t *hist,
-                      uint32_t *bsum, hipStream_t s);
-void launch_dedup_unique(const uint64_t *keys, const uint32_t *vals, uint64_t n, const KStore &ks, uint32_t job_bits,
-                         unsigned long long *counts, uint32_t *coll, uint32_t *ncoll, hipStream_t s);
+uint32_t dedup_gather_tile();
+uint32_t dedup_unique_blocks(uint64_t n);
+void launch_dedup_gather(const KStore &ks, const KSeg *segs, const uint2 *tiles, uint32_t ntiles, uint32_t pos_bits,
+                         uint32_t exact_job_shift, uint32_t job_bits, uint64_t mask, uint64_t *ke, uint64_t *kh,
+                         uint32_t *vh, uint32_t *tcnt, hipStream_t s);
+int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t bits,
+                      uint32_t *hist, uint32_t *bsum, hipStream_t s, const uint32_t *tile_n = nullptr,
+                      uint32_t sparse_tiles = 0);
+void launch_dedup_unique(const uint64_t *keys, const uint32_t *vals, uint64_t n, const KStore &ks, uint32_t job_shift,
+                         bool verify, unsigned long long *counts, uint4 *part, uint32_t *coll, uint32_t *ncoll,
+                         hipStream_t s);
 
 }  // namespace sb

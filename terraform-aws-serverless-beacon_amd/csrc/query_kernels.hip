@@ -85,6 +85,16 @@ __device__ __forceinline__ uint32_t popc_below(uint64_t m) {
 
 __device__ __forceinline__ uint8_t up(uint8_t c) { return (c >= 'a' && c <= 'z') ? c - 32 : c; }
 
+// XCD-aware workgroup order (cdna_hip_programming.md T1, bijective form):
+// the dispatcher deals workgroups round-robin over the 8 XCDs, so block b
+// shares an L2 with b + 8.  Remapping gives each XCD one contiguous run of
+// the (position-sorted) query list: neighbouring slices scan overlapping or
+// adjacent records, which then hit the same XCD's L2.
+__device__ __forceinline__ uint32_t xcd_block(uint32_t b, uint32_t nb) {
+    const uint32_t q = nb / 8, r = nb % 8, x = b % 8;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + b / 8;
+}
+
 // ---------------------------------------------------------------- bounds
 // [lo, hi) = records of the segment with x1 <= POS < x2.  The bucket holding
 // x brackets lower_bound(x) in [bucket[b], bucket[b+1]]; both searches issue
@@ -428,7 +438,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(
     DStore st, const QDev *__restrict__ qs, const uint32_t *__restrict__ qidx, uint32_t nq,
     const uint8_t *__restrict__ qbytes, const uint64_t *__restrict__ subsets, QRes *__restrict__ res,
     uint64_t *__restrict__ hits, uint64_t *__restrict__ samples_out) {
-    const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint32_t w = uniform(xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + (threadIdx.x >> 6));
     if (w >= nq) return;
     const uint32_t q = qidx ? uniform(qidx[w]) : w;
     const int lane = lane_id();
@@ -514,7 +524,7 @@ template <bool NONNEG>
 __global__ __launch_bounds__(kBlock) void range_n_kernel(DStore st, const QDev *__restrict__ qs,
                                                          const uint32_t *__restrict__ qidx, uint32_t nq,
                                                          QRes *__restrict__ res, uint64_t *__restrict__ hits) {
-    const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint32_t w = uniform(xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + (threadIdx.x >> 6));
     if (w >= nq) return;
     const uint32_t q = qidx ? uniform(qidx[w]) : w;
     const int lane = lane_id();
@@ -582,7 +592,7 @@ template <bool NONNEG>
 __global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__restrict__ qs,
                                                     const uint32_t *__restrict__ qidx, uint32_t nq,
                                                     QRes *__restrict__ res, uint64_t *__restrict__ hits) {
-    const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint32_t w = uniform(xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + (threadIdx.x >> 6));
     if (w >= nq) return;
     const uint32_t q = qidx ? uniform(qidx[w]) : w;
     const int lane = lane_id();
@@ -714,20 +724,35 @@ __global__ __launch_bounds__(kBlock) void summarise_chunk_kernel(SStore ss, cons
     uint32_t bad = 0, ov = 0;
     uint64_t *bm = bitmap + S.bitmap_off;
     constexpr int kPer = kSumChunk / kBlock;
-    SumHot h[kPer];  // all loads in flight before any use
+    uint64_t h[kPer];  // all 8-byte loads in flight before any use
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const uint32_t r = c0 + k * kBlock + threadIdx.x;
-        h[k] = r < c1 ? ss.sum[r] : SumHot{0xffffffffu, 0, 0};
+        h[k] = r < c1 ? ss.sum8[r] : 0ull;
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const uint32_t base = c0 + k * kBlock;
         const uint32_t r = base + threadIdx.x;
-        nv += h[k].nvf & ~kSumUnsupported;
-        nc += h[k].nc;
-        bad += h[k].nvf >> 31;
-        const uint64_t m = __ballot(r < c1 && r > S.lo && skip >= h[k].rem);
+        uint64_t rem, vnv, vnc;
+        uint32_t vbad = 0;
+        if (h[k] & kSumEscape) {  // rare: the wide word
+            const SumHot w = ss.sum[r];
+            rem = w.rem;
+            vnv = w.nvf & ~kSumUnsupported;
+            vnc = w.nc;
+            vbad = w.nvf >> 31;
+        } else {
+            rem = h[k] & 0xffffffull;
+            vnv = (h[k] >> 24) & 0xffull;
+            vnc = h[k] >> 32;
+        }
+        if (r < c1) {
+            nv += vnv;
+            nc += vnc;
+            bad += vbad;
+        }
+        const uint64_t m = __ballot(r < c1 && r > S.lo && skip >= rem);
         ov += m != 0;
         if (lane == 0 && base + wave * kWave < c1) bm[(base - S.lo) / kWave + wave] = m;
     }
