@@ -191,6 +191,33 @@ int sb_store_contig_name(const sb_store *s, uint32_t vcf_id, uint32_t i, const c
 int sb_store_chunk_boundaries(const sb_store *s, uint32_t vcf_id, const char *contig, size_t contig_len,
                               uint32_t stride, uint64_t *voffs, size_t cap, size_t *n);
 
+/* ---- summariseSlice region files ---------------------------------------------
+ * What summariseSlice writes to S3 besides its counts
+ * (lambda/summariseSlice/source/write_data_to_s3.h:30-228): one entry
+ * {pos u64 LE, len u16 LE, ref' '_' alt'} per ALT of every record the reader
+ * visits (skip heuristic included), split into files at POS gaps above
+ * MAX_SLICE_GAP (100,000) and above VCF_S3_OUTPUT_SIZE_LIMIT (50,000,000)
+ * entries (main.tf:17,215-216).  A file's S3 key is
+ * vcf-summaries/contig/{CHROM}/{bucket%key}/regions/{first_pos}-{last_pos}-{bytes}
+ * (the caller formats it; contig = index into sb_store_contig_name).  With
+ * with_data the files' uncompressed bytes are concatenated in file order
+ * (the reference gzips them, level 9, per <= 50 MB buffer).  status[i] =
+ * SB_QERR_UNSUPPORTED for a slice the reference throws on (compressSeq of an
+ * IUPAC code, reads past a line) or that is not record-aligned. */
+typedef struct {
+    uint32_t slice;     /* index into the slices argument */
+    uint32_t contig;    /* contig index of the slice's VCF */
+    uint64_t first_pos, last_pos;
+    uint64_t bytes;     /* uncompressed file length */
+    uint64_t entries;
+} sb_region_file;
+typedef struct sb_region_files sb_region_files;
+int sb_slice_region_files(sb_store *s, const sb_slice *slices, size_t n, int with_data, int32_t *status,
+                          sb_region_files **out);
+int sb_region_files_get(const sb_region_files *r, const sb_region_file **files, size_t *n, const uint8_t **data,
+                        size_t *data_len);
+void sb_region_files_free(sb_region_files *r);
+
 /* ---- duplicateVariantSearch -------------------------------------------------
  * One sb_dedup_job = one duplicateVariantSearch SNS message {"rangeStart",
  * "rangeEnd", "contig", "targetFilepaths", "dataset"} (lambda/

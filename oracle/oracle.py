@@ -203,6 +203,9 @@ def _summ_lib():
                                           C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.orc_region_stats.argtypes = [C.c_char_p, C.c_int64, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                        C.POINTER(C.c_uint64)]
+        L.orc_slice_region_files.restype = C.c_int64
+        L.orc_slice_region_files.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.POINTER(C.c_uint64), C.c_int64,
+                                             C.c_char_p, C.c_int64, C.POINTER(C.c_int64)]
         L._summ_ready = True
     return L
 
@@ -246,6 +249,22 @@ class OracleBgzf:
         if _summ_lib().orc_bgzf_voff_to_u(self.h, voff, C.byref(u)):
             raise ValueError(voff)
         return u.value
+
+    def region_files(self, vstart, vend, with_data=False):
+        """The slice's region files [(first, last, bytes, entries)] (+ the
+        concatenated uncompressed bytes); ValueError where the reference
+        throws."""
+        L = _summ_lib()
+        cap = 4096
+        rows = (C.c_uint64 * (4 * cap))()
+        dcap = max(1 << 16, 2 * self.ulen) if with_data else 0
+        data = C.create_string_buffer(dcap) if with_data else None
+        dl = C.c_int64()
+        n = L.orc_slice_region_files(self.h, vstart, vend, rows, cap, data, dcap, C.byref(dl))
+        if n < 0:
+            raise ValueError(f'region files: oracle rc={n}')
+        files = [tuple(rows[4 * i:4 * i + 4]) for i in range(n)]
+        return (files, data.raw[:dl.value]) if with_data else files
 
     def summarise_slice(self, vstart, vend):
         nv, nc, rec = C.c_uint64(), C.c_uint64(), C.c_uint64()

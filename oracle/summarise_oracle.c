@@ -407,6 +407,115 @@ int orc_region_stats(const char *s, int64_t n, uint64_t *num_variants, uint64_t 
     return 0;
 }
 
+/* write_data_to_s3.h:150-228 (recordHeader), :93-101 (saveNewFile),
+ * :39-92 (saveOutputToS3) over the records getRegionStats visits
+ * (main.cpp:217-237): the slice's region files.  rows gets up to cap rows of
+ * {first_pos, last_pos, bytes, entries}; data (optional, capacity data_cap)
+ * the files' uncompressed bytes {pos u64, len u16, ref' '_' alt'}.  Returns
+ * the number of files, -1 where the reference throws, -2 on overflow. */
+#define ORC_MAX_SLICE_GAP 100000ULL       /* main.tf:215 */
+#define ORC_OUTPUT_SIZE_LIMIT 50000000ULL /* main.tf:17,216 */
+int64_t orc_region_files(const char *s, int64_t n, uint64_t *rows, int64_t cap, char *data, int64_t data_cap,
+                         int64_t *data_len) {
+    rd_t r = {s, n, 0};
+    int contig_set = 0;
+    int64_t nf = 0, dl = 0;
+    uint64_t first = 0, last = 0, bytes = 0, entries = 0;
+    uint64_t skip = 0;
+    int first_rec = 1;
+    while (first_rec || r.pos < r.n) {
+        keys_t one = {0};
+        uint64_t pos = 0, nv = 0, nc = 0;
+        /* recordHeader: the POS check (gap / unsorted) happens before this
+         * record's entries are pushed */
+        const int bad = record_header(&r, &contig_set, &one, &pos);
+        if (bad) {
+            keys_free(&one);
+            return -1;
+        }
+        if (entries) {
+            if (pos < last) {
+                keys_free(&one);
+                return -1; /* "unsorted file" */
+            }
+            if (pos > last + ORC_MAX_SLICE_GAP) {
+                if (nf < cap) {
+                    rows[4 * nf] = first;
+                    rows[4 * nf + 1] = last;
+                    rows[4 * nf + 2] = bytes;
+                    rows[4 * nf + 3] = entries;
+                }
+                nf++;
+                bytes = entries = 0;
+            }
+        }
+        for (int64_t i = 0; i < one.n; ++i) {
+            char d[24];
+            const int nd = snprintf(d, sizeof d, "%llu", (unsigned long long)one.pos[i]);
+            const int64_t tl = one.len[i] - nd;
+            if (!entries) first = one.pos[i];
+            last = one.pos[i];
+            bytes += 10 + (uint64_t)tl;
+            entries++;
+            if (data) {
+                if (dl + 10 + tl > data_cap) {
+                    keys_free(&one);
+                    return -2;
+                }
+                const uint64_t p = one.pos[i];
+                const uint16_t l16 = (uint16_t)tl;
+                memcpy(data + dl, &p, 8);
+                memcpy(data + dl + 8, &l16, 2);
+                memcpy(data + dl + 10, one.s[i] + nd, (size_t)tl);
+            }
+            dl += 10 + tl;
+        }
+        keys_free(&one);
+        if (add_counts(&r, &nv, &nc)) return -1;
+        if (entries > ORC_OUTPUT_SIZE_LIMIT) {
+            if (nf < cap) {
+                rows[4 * nf] = first;
+                rows[4 * nf + 1] = last;
+                rows[4 * nf + 2] = bytes;
+                rows[4 * nf + 3] = entries;
+            }
+            nf++;
+            bytes = entries = 0;
+        }
+        if (first_rec) {
+            skip = 2 * skip_count(&r, '\n');
+            first_rec = 0;
+        } else {
+            r.pos += (int64_t)skip; /* seek(skipSize) */
+            skip_past(&r, '\n', 1);
+        }
+        if (n == 0) break;
+    }
+    if (entries) {
+        if (nf < cap) {
+            rows[4 * nf] = first;
+            rows[4 * nf + 1] = last;
+            rows[4 * nf + 2] = bytes;
+            rows[4 * nf + 3] = entries;
+        }
+        nf++;
+    }
+    if (data_len) *data_len = dl;
+    return nf > cap ? -2 : nf;
+}
+
+int64_t orc_slice_region_files(void *h, uint64_t vstart, uint64_t vend, uint64_t *rows, int64_t cap, char *data,
+                               int64_t data_cap, int64_t *data_len) {
+    bgzf_t *b = (bgzf_t *)h;
+    uint64_t u0, u1;
+    if (orc_bgzf_voff_to_u(b, vstart, &u0) || orc_bgzf_voff_to_u(b, vend, &u1)) return -3;
+    if (u1 <= u0) {
+        if (data_len) *data_len = 0;
+        return 0;
+    }
+    return orc_region_files((const char *)b->u + u0, (int64_t)(u1 - u0), rows, cap, data, data_cap, data_len);
+}
+
 int orc_summarise_slice(void *h, uint64_t vstart, uint64_t vend, uint64_t *num_variants, uint64_t *num_calls,
                         uint64_t *records) {
     bgzf_t *b = (bgzf_t *)h;

@@ -53,7 +53,10 @@ T *dev_upload(sb_store &s, const std::vector<T> &v) {
     DeviceBuffer b;
     b.bytes = std::max<size_t>(v.size() * sizeof(T), 16);
     HIP_OK(hipMalloc(&b.p, b.bytes));
-    if (!v.empty()) HIP_OK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s.stream));
+    if (!v.empty()) {
+        HIP_OK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s.stream));
+        HIP_OK(hipStreamSynchronize(s.stream));  // callers free pageable temporaries right after
+    }
     s.bufs.push_back(b);
     s.device_bytes += b.bytes;
     return static_cast<T *>(b.p);
@@ -387,6 +390,14 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.h_dk_tail = std::move(dk_tail);
     s.h_dk_blob = std::move(dk_blob);
     s.h_start = std::move(start);
+    s.h_rem.resize(sum.size());
+    s.h_sum_bad.resize(sum.size());
+    for (size_t i = 0; i < sum.size(); ++i) {
+        s.h_rem[i] = sum[i].rem;
+        s.h_sum_bad[i] = (sum[i].nvf & kSumUnsupported) ? 1 : 0;
+    }
+    s.h_cur = std::move(cur);
+    s.h_dcount = std::move(dcount);
     // host copies for output planning and result formatting
     s.h_pos = std::move(pos);
     s.h_end.resize(rec.size());
@@ -848,6 +859,111 @@ void summarise(sb_store &s, const sb_slice *sl, size_t n, sb_slice_stats *out, d
     }
 }
 
+// ---------------------------------------------------------- region files
+// summariseSlice's region files (lambda/summariseSlice/source/
+// write_data_to_s3.h): the reader visits the records of the slice exactly as
+// main.cpp:217-237 does (first record; then per record addCounts, seek
+// (skipSize), skipPast('\n') — the walk the device summarise kernels
+// reproduce), and recordHeader (:150-228) pushes one entry {pos, ref', alt'}
+// per ALT of every visited record; a file is closed when a record's POS is
+// more than MAX_SLICE_GAP past the buffer's last entry (:191-194) or when the
+// buffer holds more than VCF_S3_OUTPUT_SIZE_LIMIT entries (:224-227), and at
+// the end of the slice (~writeDataToS3).  File length = sum over entries of
+// pos u64 + len u16 + |ref'| + 1 + |alt'| (saveOutputToS3, :39-92).
+constexpr uint64_t kMaxSliceGap = 100000;        // main.tf:215 MAX_SLICE_GAP
+constexpr uint64_t kOutputSizeLimit = 50000000;  // main.tf:17,216 VCF_S3_OUTPUT_SIZE_LIMIT
+
+uint32_t key_tail_len(const sb_store &s, uint64_t k) {
+    const uint64_t t = s.h_dk_tail[k];
+    return (t & kTailBlob) ? static_cast<uint32_t>((t >> 40) & 0xffff) : static_cast<uint32_t>(t >> 56);
+}
+
+void append_key_entry(const sb_store &s, uint64_t k, std::vector<uint8_t> &out) {
+    const uint64_t pos = s.h_dk_pos[k];
+    const uint32_t tl = key_tail_len(s, k);
+    const uint16_t len = static_cast<uint16_t>(tl);
+    const size_t o = out.size();
+    out.resize(o + 10 + tl);
+    memcpy(out.data() + o, &pos, 8);
+    memcpy(out.data() + o + 8, &len, 2);
+    const uint64_t t = s.h_dk_tail[k];
+    if (t & kTailBlob)
+        memcpy(out.data() + o + 10, s.h_dk_blob.data() + (t & ((1ull << 40) - 1)), tl);
+    else
+        for (uint32_t j = 0; j < tl; ++j) out[o + 10 + j] = static_cast<uint8_t>(t >> (8 * j));
+}
+
+// one slice: status (0 / SB_QERR_UNSUPPORTED), files appended to `files`,
+// file bytes appended to `data` when non-null
+int32_t slice_region_files(const sb_store &s, uint32_t si, const sb_slice &sl, std::vector<sb_region_file> &files,
+                           std::vector<uint8_t> *data) {
+    if (sl.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "slice " + std::to_string(si) + ": unknown vcf id");
+    const VcfData &v = s.vcfs[sl.vcf_id];
+    if (v.blk_coff.empty()) throw Error(SB_EINVAL, "region files need a VCF ingested from a BGZF file (virtual offsets)");
+    uint64_t u0, u1;
+    if (!voff_to_stream(v, sl.virtual_start, &u0) || !voff_to_stream(v, sl.virtual_end, &u1)) return SB_QERR_UNSUPPORTED;
+    if (u1 < u0) u1 = u0;
+    const uint32_t rb = v.rec_base;
+    uint32_t re = rb;
+    for (const auto &sg : v.segments) re = std::max(re, sg.hi);
+    auto first = s.h_start.begin() + rb, last = s.h_start.begin() + re;
+    const uint32_t lo = rb + static_cast<uint32_t>(std::lower_bound(first, last, u0) - first);
+    const uint32_t hi = rb + static_cast<uint32_t>(std::lower_bound(first, last, u1) - first);
+    if (hi <= lo) return u1 > u0 ? SB_QERR_UNSUPPORTED : 0;
+    const uint64_t end_last = hi < re ? s.h_start[hi] : v.stream_len;
+    if (s.h_start[lo] != u0 || end_last > u1) return SB_QERR_UNSUPPORTED;
+    // contig of the slice (one contig per slice: index chunks never cross)
+    uint32_t contig = 0;
+    for (uint32_t g = 0; g < v.segments.size(); ++g)
+        if (lo >= v.segments[g].lo && lo < v.segments[g].hi) contig = g;
+    const size_t f0 = files.size();
+    const size_t d0 = data ? data->size() : 0;
+    sb_region_file cur{si, contig, 0, 0, 0, 0};
+    bool open = false;
+    auto close = [&]() {
+        if (open && cur.entries) files.push_back(cur);
+        cur = sb_region_file{si, contig, 0, 0, 0, 0};
+        open = false;
+    };
+    const uint64_t skip = 2ull * s.h_dcount[lo];
+    uint32_t r = lo;
+    while (r < hi) {
+        if (s.h_sum_bad[r]) {  // the reference throws / reads past the line
+            files.resize(f0);
+            if (data) data->resize(d0);
+            return SB_QERR_UNSUPPORTED;
+        }
+        const uint64_t pos = s.h_pos[r];
+        if (open && cur.entries) {
+            if (pos < cur.last_pos) throw Error(SB_EINVAL, "unsorted file");  // write_data_to_s3.h:184-188
+            if (pos > cur.last_pos + kMaxSliceGap) close();
+        }
+        for (uint32_t k = s.h_dk_lo[r]; k < s.h_dk_lo[r + 1]; ++k) {
+            if (!open || !cur.entries) {
+                cur.first_pos = s.h_dk_pos[k];
+                open = true;
+            }
+            cur.last_pos = s.h_dk_pos[k];
+            cur.bytes += 10 + key_tail_len(s, k);
+            ++cur.entries;
+            if (data) append_key_entry(s, k, *data);
+        }
+        if (cur.entries > kOutputSizeLimit) close();
+        // next visited record
+        if (r == lo) {
+            r = lo + 1;  // skipPastAndCountChars('\n') ends the first record's line
+        } else if (skip >= s.h_rem[r]) {  // seek(skipSize) lands past this line
+            const uint64_t P = s.h_start[r] + s.h_cur[r] + skip;
+            r = static_cast<uint32_t>(std::upper_bound(s.h_start.begin() + r + 1, s.h_start.begin() + hi, P) -
+                                      s.h_start.begin());
+        } else {
+            ++r;
+        }
+    }
+    close();
+    return 0;
+}
+
 // the key string of store key k: decimal(pos) ++ ref'_alt'
 std::string key_string(const sb_store &s, uint32_t k) {
     std::string out = std::to_string(s.h_dk_pos[k]);
@@ -1045,6 +1161,35 @@ int sb_summarise_slices(sb_store *s, const sb_slice *slices, size_t n, sb_slice_
         summarise(*s, slices, n, out, device_ms);
     });
 }
+
+struct sb_region_files {
+    std::vector<sb_region_file> files;
+    std::vector<uint8_t> data;
+};
+
+int sb_slice_region_files(sb_store *s, const sb_slice *slices, size_t n, int with_data, int32_t *status,
+                          sb_region_files **out) {
+    return guard([&] {
+        if (!s || (!slices && n) || (!status && n) || !out) throw Error(SB_EINVAL, "NULL argument");
+        auto R = std::make_unique<sb_region_files>();
+        for (size_t i = 0; i < n; ++i)
+            status[i] = slice_region_files(*s, static_cast<uint32_t>(i), slices[i], R->files,
+                                           with_data ? &R->data : nullptr);
+        *out = R.release();
+    });
+}
+
+int sb_region_files_get(const sb_region_files *r, const sb_region_file **files, size_t *n, const uint8_t **data,
+                        size_t *data_len) {
+    if (!r || !files || !n) return SB_EINVAL;
+    *files = r->files.data();
+    *n = r->files.size();
+    if (data) *data = r->data.data();
+    if (data_len) *data_len = r->data.size();
+    return SB_OK;
+}
+
+void sb_region_files_free(sb_region_files *r) { delete r; }
 
 int sb_dedup_count(sb_store *s, const sb_dedup_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,
                    sb_dedup_stats *stats) {

@@ -124,6 +124,10 @@ struct sb_store {
     std::vector<uint64_t> h_ref_off, h_a0_off, h_x_off;
     std::vector<uint8_t> h_blob;
     std::vector<uint64_t> h_start;  // line start in the VCF text stream (summariseSlice planning)
+    // the summariseSlice reader walk on the host (region files): rem, cursor,
+    // delimiter count and the unsupported flag of every record
+    std::vector<uint32_t> h_rem, h_cur, h_dcount;
+    std::vector<uint8_t> h_sum_bad;
     // duplicateVariantSearch keys (global indexing): planning + collision fixup
     uint64_t n_keys = 0;
     std::vector<uint32_t> h_dk_pos, h_dk_lo, h_dk_bad;

@@ -68,6 +68,11 @@ class SliceStats(C.Structure):
                 ('num_calls', C.c_uint64), ('records', C.c_uint64)]
 
 
+class RegionFile(C.Structure):
+    _fields_ = [('slice', C.c_uint32), ('contig', C.c_uint32), ('first_pos', C.c_uint64), ('last_pos', C.c_uint64),
+                ('bytes', C.c_uint64), ('entries', C.c_uint64)]
+
+
 class DedupJob(C.Structure):
     _fields_ = [('vcf_ids', C.POINTER(C.c_uint32)), ('n_vcf', C.c_uint32), ('contig_len', C.c_uint32),
                 ('contig', C.c_char_p), ('range_start', C.c_uint64), ('range_end', C.c_uint64)]
@@ -111,6 +116,11 @@ SIGNATURES = {
     'sb_batch_reduce_requests': (C.c_int, [P, C.c_void_p]),
     'sb_summarise_slices': (C.c_int, [P, C.POINTER(Slice), C.c_size_t, C.POINTER(SliceStats),
                                       C.POINTER(C.c_double)]),
+    'sb_slice_region_files': (C.c_int, [P, C.POINTER(Slice), C.c_size_t, C.c_int, C.POINTER(C.c_int32),
+                                        C.POINTER(P)]),
+    'sb_region_files_get': (C.c_int, [P, C.POINTER(C.POINTER(RegionFile)), C.POINTER(C.c_size_t),
+                                      C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    'sb_region_files_free': (None, [P]),
     'sb_dedup_count': (C.c_int, [P, C.POINTER(DedupJob), C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_int32),
                                  C.POINTER(DedupStats)]),
     'sb_store_n_contigs': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),

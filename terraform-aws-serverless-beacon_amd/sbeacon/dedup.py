@@ -21,8 +21,13 @@ duplicateVariantSearch.cpp:76-84,86-200).
 from __future__ import annotations
 
 import json
+import os
+from dataclasses import dataclass, field
 
 from . import engine
+
+# main.tf:16,128 (maximum_load_file_size -> ABS_MAX_DATA_SPLIT)
+ABS_MAX_DATA_SPLIT = int(os.environ.get('ABS_MAX_DATA_SPLIT', 750_000_000))
 
 
 def bucket_key(location: str) -> str:
@@ -39,6 +44,116 @@ def region_path_bucket_key(path: str) -> str:
     if len(parts) < 6 or parts[0] != 'vcf-summaries' or parts[1] != 'contig' or parts[-2] != 'regions':
         raise ValueError(f'not a region-file key: {path!r}')
     return parts[-3]
+
+
+# ------------------------------------------------ initDuplicateVariantSearch
+# lambda/summariseDataset/initDuplicateVariantSearch.py: the (contig, range,
+# region files) jobs a dataset's duplicate search fans out, planned from the
+# region-file keys summariseSlice wrote (sbeacon.summarise.region_file_keys).
+@dataclass
+class VcfRegionData:  # :21-27
+    filepath: str
+    filename: str
+    filesize: int
+    startRange: int
+    endRange: int
+
+
+@dataclass
+class BasePairRange:  # :30-34
+    start: int
+    end: int
+    filePaths: list = field(default_factory=list)
+
+
+def get_file_name_info(filepath: str) -> VcfRegionData:
+    """:77-89 — .../{filename}/regions/{first}-{last}-{bytes}."""
+    parts = filepath.split('/')
+    rng = parts[-1].split('-')
+    return VcfRegionData(filepath, parts[-3], int(rng[2]), int(rng[0]), int(rng[1]))
+
+
+def filter_range(region_data, start, end):
+    """:92-99 — the files overlapping [start, end] and their summed size."""
+    files = [rd for rd in region_data if rd.startRange <= end and rd.endRange >= start]
+    return sum(rd.filesize for rd in files), files
+
+
+def add_range(region_data, start_range, end_range, range_slices, abs_max=None):
+    """:103-125 — shrink the range end to a file end until the overlapping
+    files fit abs_max (or nothing smaller exists), record it, and return the
+    next start and the index after its last file."""
+    abs_max = ABS_MAX_DATA_SPLIT if abs_max is None else abs_max
+    size, files = filter_range(region_data, start_range, end_range)
+    while size > abs_max:
+        try:
+            new_end = max(f.endRange for f in files if f.endRange < end_range)
+            size, files = filter_range(files, start_range, new_end)
+        except ValueError:  # no smaller end: keep the range (the reference prints and continues)
+            new_end = end_range
+        if end_range == new_end:
+            break
+        end_range = new_end
+    range_slices.append(BasePairRange(start_range, end_range, [f.filepath for f in files]))
+    return end_range + 1, region_data.index(files[-1]) + 1
+
+
+def calc_range_splits(region_data, abs_max=None, max_iterations=10_000_000):
+    """:171-191 — greedy ranges of region files whose summed size stays under
+    abs_max.  The reference loops until the range start passes the last
+    file's end; inputs on which it never does (it would spin until the
+    Lambda times out) raise RuntimeError after max_iterations."""
+    abs_max = ABS_MAX_DATA_SPLIT if abs_max is None else abs_max
+    range_slices = []
+    running_total = 0
+    start_range = region_data[0].startRange
+    item_inc = 0
+    min_data_split = abs_max - region_data[0].filesize * 2
+    it = 0
+    while start_range - 1 != region_data[-1].endRange:
+        it += 1
+        if it > max_iterations:
+            raise RuntimeError('calcRangeSplits does not terminate on this input (the reference spins)')
+        element = region_data[item_inc]
+        if running_total < min_data_split:
+            running_total += element.filesize
+            item_inc = item_inc + 1 if item_inc + 1 < len(region_data) else item_inc
+        else:
+            start_range, item_inc = add_range(region_data, start_range, element.endRange, range_slices, abs_max)
+            running_total = 0
+    if running_total != 0:
+        add_range(region_data, start_range, max(r.endRange for r in region_data), range_slices, abs_max)
+    return range_slices
+
+
+def init_duplicate_variant_search(dataset, filepaths, region_keys, *, bucket='variants', tally=None,
+                                  abs_max=None):
+    """:235-255 — for every contig with region files of the dataset's VCFs
+    (``region_keys``: every region-file key of the variants bucket, the
+    listing retrieveS3Objects does), the range splits as
+    duplicateVariantSearch SNS messages; with a DuplicateTally, the
+    mark_updating / clearDatasetVariantCount writes too."""
+    filenames = ['/' + fn[5:-7].replace('/', '%') + '/' for fn in filepaths]
+    by_contig = {}
+    for k in region_keys:
+        parts = k.split('/')
+        if len(parts) >= 6 and parts[0] == 'vcf-summaries' and parts[1] == 'contig':
+            by_contig.setdefault(parts[2], []).append(k)
+    if tally is not None:
+        tally.dataset_counts[dataset] = 0
+    messages = []
+    for contig, keys in by_contig.items():
+        region = [get_file_name_info(k) for k in keys if any(fn in k for fn in filenames)]
+        if not region:
+            continue
+        region.sort(key=lambda x: x.startRange)
+        splits = calc_range_splits(region, abs_max)
+        if tally is not None:
+            tally.expect(contig, dataset, [(s.start, s.end) for s in splits])
+        for s in splits:
+            messages.append({'bucket': bucket, 'rangeStart': s.start, 'rangeEnd': s.end, 'contig': contig,
+                             'targetFilepaths': s.filePaths, 'dataset': dataset})
+    return messages
 
 
 def message_job(msg: dict, locations):

@@ -178,6 +178,47 @@ class Store:
                              'records': out[i].records})
         return (res, ms.value) if with_timing else res
 
+    def region_files(self, slices, *, with_data=False):
+        """summariseSlice's region files of each slice (write_data_to_s3.h):
+        per slice a list of {contig, first_pos, last_pos, bytes, entries}
+        dicts (+ 'data': the file's uncompressed bytes with_data), or the
+        exception for a slice the reference throws on."""
+        slices = list(slices)
+        n = len(slices)
+        arr = (Slice * max(n, 1))()
+        for i, (loc, vs, ve) in enumerate(slices):
+            arr[i].vcf_id = self.vcf_id(loc)
+            arr[i].virtual_start = int(vs)
+            arr[i].virtual_end = int(ve)
+        status = (C.c_int32 * max(n, 1))()
+        h = C.c_void_p()
+        check(lib().sb_slice_region_files(self._h, arr, n, 1 if with_data else 0, status, C.byref(h)))
+        try:
+            fp = C.POINTER(_lib.RegionFile)()
+            nf = C.c_size_t()
+            dp = C.c_void_p()
+            dl = C.c_size_t()
+            check(lib().sb_region_files_get(h, C.byref(fp), C.byref(nf), C.byref(dp), C.byref(dl)))
+            data = C.string_at(dp, dl.value) if with_data and dl.value else b''
+            contig_names = {}
+            out = [[] for _ in range(n)]
+            off = 0
+            for k in range(nf.value):
+                f = fp[k]
+                loc = slices[f.slice][0]
+                if loc not in contig_names:
+                    contig_names[loc] = self.contigs(loc)
+                d = {'contig': contig_names[loc][f.contig], 'first_pos': f.first_pos, 'last_pos': f.last_pos,
+                     'bytes': f.bytes, 'entries': f.entries}
+                if with_data:
+                    d['data'] = data[off:off + f.bytes]
+                    off += f.bytes
+                out[f.slice].append(d)
+        finally:
+            lib().sb_region_files_free(h)
+        return [NotImplementedError(f'slice {slices[i]}: the reference summariseSlice throws / slice not record-'
+                                    'aligned') if status[i] else out[i] for i in range(n)]
+
     def dedup_counts(self, jobs, *, with_stats=False):
         """jobs: iterable of (vcf_locations, contig, range_start, range_end).
         Returns the unique region-key count per job (duplicateVariantSearch's

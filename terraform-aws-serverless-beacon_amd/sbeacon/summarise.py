@@ -47,3 +47,56 @@ def lambda_handler(event, context=None):
     except (KeyError, IndexError, TypeError):
         pass
     return summarise_slice(msg['location'], int(msg['virtual_start']), int(msg['virtual_end']))
+
+
+def region_file_keys(store, location, slices):
+    """The S3 keys summariseSlice writes for these slices of one VCF
+    (write_data_to_s3.h:93-101: vcf-summaries/contig/{CHROM}/{bucket%key}/
+    regions/{first}-{last}-{bytes}), in slice then file order."""
+    from .dedup import bucket_key
+    bk = bucket_key(location)
+    keys = []
+    for sl, files in zip(slices, store.region_files([(location, a, b) for a, b in slices])):
+        if isinstance(files, Exception):
+            raise files
+        for f in files:
+            keys.append(f"vcf-summaries/contig/{f['contig']}/{bk}/regions/{f['first_pos']}-{f['last_pos']}-{f['bytes']}")
+    return keys
+
+
+def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None):
+    """The ingest pipeline of one dataset on the device: summariseVcf's slice
+    plan + summariseSlice counts for every VCF (lambda/summariseVcf,
+    lambda/summariseSlice), the region-file keys those slices write, then
+    initDuplicateVariantSearch's range splits (lambda/summariseDataset/
+    initDuplicateVariantSearch.py:235-255) answered by duplicateVariantSearch
+    (one batched sb_dedup_count).  Returns the dataset's counts:
+    variantCount / callCount from the summaries (summariseDataset
+    lambda_function.py:102-125) and uniqueVariants = the sum of the ranges'
+    distinct counts (the DATASETS_TABLE variantCount duplicateVariantSearch
+    leaves, duplicateVariantSearch.cpp:76-84)."""
+    from .dedup import DuplicateTally, dedup_batch, init_duplicate_variant_search
+    from .summarise_vcf import summarise_vcf
+    tally = tally or DuplicateTally()
+    counts = {'variantCount': 0, 'callCount': 0}
+    keys = []
+    for loc in locations:
+        slices, _, tot = summarise_vcf(store, loc)
+        counts['variantCount'] += tot['variantCount']
+        counts['callCount'] += tot['callCount']
+        keys += region_file_keys(store, loc, slices)
+    messages = init_duplicate_variant_search(dataset, locations, keys, tally=tally, abs_max=abs_max)
+    per_range = dedup_batch(messages, tally=tally, registry=_single_store_registry(store)) if messages else []
+    for r in per_range:
+        if isinstance(r, Exception):
+            raise r
+    counts['uniqueVariants'] = tally.dataset_counts.get(dataset, 0)
+    counts['ranges'] = len(messages)
+    return counts, messages, per_range
+
+
+def _single_store_registry(store):
+    from .engine import Registry
+    reg = Registry()
+    reg.register(store)
+    return reg

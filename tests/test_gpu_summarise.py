@@ -33,6 +33,20 @@ def skip_quirk_vcf(n=3000, seed=5):
     return b''.join(out)
 
 
+def gap_vcf(n=2500, seed=9):
+    """Records with occasional POS jumps above MAX_SLICE_GAP (region-file
+    splits), multiallelic and indel ALTs."""
+    rng = random.Random(seed)
+    out = [b'##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tA\n']
+    pos = 500
+    for i in range(n):
+        pos += rng.choice([1, 5, 40, 300, 99999, 100000, 100001, 250000]) if rng.random() < 0.05 else rng.randrange(0, 60)
+        ref = rng.choice(['A', 'C', 'GT', 'TTA'])
+        alt = rng.choice(['G', 'T,C', 'A', '<DEL>', 'GTT'])
+        out.append(f'3\t{pos}\t.\t{ref}\t{alt}\t.\tPASS\tAC=1;AN=2;DP=9\tGT\t0|1\n'.encode())
+    return b''.join(out)
+
+
 @pytest.fixture(scope='module')
 def bgzf_files(tmp_path_factory):
     from sbeacon.workload import SyntheticVcf, write_bgzf
@@ -41,6 +55,7 @@ def bgzf_files(tmp_path_factory):
     for name in ('tiny22', 'quirk22'):
         files[name] = write_bgzf(str(d / f'{name}.vcf.gz'), [open(os.path.join(FIXTURES, name + '.vcf'), 'rb').read()])
     files['skip7'] = write_bgzf(str(d / 'skip7.vcf.gz'), [skip_quirk_vcf()])
+    files['gaps3'] = write_bgzf(str(d / 'gaps3.vcf.gz'), [gap_vcf()])
     g = SyntheticVcf(n_records=30000, n_samples=24, seed=99)
     files['synth'] = write_bgzf(str(d / 'synth.vcf.gz'), g.chunks(threads=4), threads=4)
     return files
@@ -138,3 +153,31 @@ def test_summarise_vcf_partition(bgzf_files, bgzf_store):
         assert tot['variantCount'] == sum(e['numVariants'] for e in exp)
     # a small stride still covers every record
     assert plan_slices(bgzf_store, 'synth.vcf.gz', stride=7)
+
+
+@pytest.mark.parametrize('name', ['tiny22', 'skip7', 'gaps3', 'synth'])
+def test_region_files_vs_oracle(bgzf_files, bgzf_store, name):
+    """summariseSlice's region files (write_data_to_s3.h): visited records
+    only, gap splits, file lengths and bytes, against the C restatement."""
+    from oracle.oracle import OracleBgzf
+    path = bgzf_files[name]
+    o = OracleBgzf(path)
+    blk, txt = blocks(path), text(path)
+    rng = random.Random(3 + len(name))
+    slices = random_slices(txt, blk, rng, 120, max_records=3000)
+    starts = record_starts(txt)
+    slices.append(((blk[0][0] << 16) | starts[0], blk[-1][0] << 16))
+    got = bgzf_store.region_files([(name + '.vcf.gz', vs, ve) for vs, ve in slices], with_data=True)
+    n_files = 0
+    for (vs, ve), g in zip(slices, got):
+        try:
+            exp, data = o.region_files(vs, ve, with_data=True)
+        except ValueError:
+            assert isinstance(g, Exception), (name, vs, ve)
+            continue
+        assert not isinstance(g, Exception), (name, vs, ve, g)
+        assert [(f['first_pos'], f['last_pos'], f['bytes'], f['entries']) for f in g] == exp, (name, vs, ve)
+        assert b''.join(f['data'] for f in g) == data
+        n_files += len(g)
+    if name == 'gaps3':
+        assert n_files > len(slices)  # the fixture really splits files on gaps

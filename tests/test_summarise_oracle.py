@@ -100,3 +100,29 @@ def test_partition_chunks_and_split_model():
     # the Newton model converges to a positive size that grows with the file
     s1, s2 = find_best_split(1e7, 1000), find_best_split(5e9, 1000)
     assert 0 < s1 < s2
+
+
+def test_region_files_split_on_gaps_and_count_bytes(tmp_path):
+    """write_data_to_s3.h: one entry {pos u64, len u16, ref'_alt'} per ALT,
+    a new file when POS jumps more than MAX_SLICE_GAP (100,000) past the last
+    entry; file length = sum of 8 + 2 + |ref'| + 1 + |alt'|."""
+    import struct
+
+    from bgzf_util import blocks, record_starts, text
+    from oracle.oracle import OracleBgzf
+    from sbeacon.workload import write_bgzf
+    hdr = b'##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\n'
+    recs = [(100, 'A', 'G'), (200, 'C', 'T,G'), (100200, 'GA', 'G'), (200300, 'A', '<DEL>'), (300301, 'T', 'C')]
+    body = b''.join(f'5\t{p}\t.\t{r}\t{a}\t.\tPASS\tAC=1;AN=2;DP=5\n'.encode() for p, r, a in recs)
+    path = write_bgzf(str(tmp_path / 'gaps.vcf.gz'), [hdr + body])
+    o = OracleBgzf(path)
+    blk, txt = blocks(path), text(path)
+    starts = record_starts(txt)
+    vs, ve = (blk[0][0] << 16) | starts[0], blk[-1][0] << 16
+    files, data = o.region_files(vs, ve, with_data=True)
+    # 100, 200 (x2) | 100200 (gap 100000: same file) ... 200300 (gap 100100: new) | 300301 (gap 100001: new)
+    assert [(f[0], f[1], f[3]) for f in files] == [(100, 100200, 4), (200300, 200300, 1), (300301, 300301, 1)]
+    # entry bytes: SNV 10+3; GA->G: ref' 1 packed byte + '_' + 1 = 13; <DEL> -> 'DEL' : 10+1+1+3
+    assert [f[2] for f in files] == [13 * 4, 15, 13]
+    p, ln = struct.unpack_from('<QH', data, 0)
+    assert (p, ln) == (100, 3) and data[10:13] == b'\x01_\x03'
