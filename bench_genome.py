@@ -129,7 +129,7 @@ def main_genome(args):
                                'query_kernels_max': round(max(v[1] for v in allv), 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(allv[0][5], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(allv[0][5] / HBM_PEAK_GBS, 4), 'traffic': None,
-                     'kernel': 'rank 0 query step (scan_kernel<GENERAL> launches, HIP events)',
+                     'kernel': 'rank 0 query step (vt_kernel launches, HIP events)',
                      'algorithmic_bytes_per_launch': 32.0 * allv[0][3] + 8.0 * allv[0][4]},
         'cpu_baseline': cpu,
         'parity_sample': parity,

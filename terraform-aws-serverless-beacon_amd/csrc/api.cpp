@@ -338,13 +338,25 @@ void upload_store(sb_builder &b, sb_store &s) {
     std::vector<RangeHot>().swap(rng);
     {
         std::vector<VtHot> vth(rec.size());
+        std::vector<uint32_t> xvt(std::max<size_t>(x_cls.size(), 1), 0);
         for (size_t i = 0; i < rec.size(); ++i) {
-            const uint64_t rl = static_cast<uint64_t>(rec[i].end) - pos[i] + 1, al = a0_len[i];
-            vth[i] = VtHot{rec[i].end, rec[i].hot,
-                           static_cast<uint32_t>(std::min<uint64_t>(rl, 0xffff) | (std::min<uint64_t>(al, 0xffff) << 16)),
-                           rec[i].ac0};
+            const RecHot &h = rec[i];
+            const uint64_t rl = static_cast<uint64_t>(h.end) - pos[i] + 1;
+            uint32_t w = 0;
+            bool ok = !(h.hot & (H_AC_BAD | H_AN_BAD)) && (h.hot & H_HAS_AC) && vt_alt_word(h.hot, rl, a0_len[i], &w);
+            if (ok && (h.hot & H_MULTI)) {
+                const uint32_t nx = x_lo[i + 1] - x_lo[i];
+                ok = nx <= VT_MAX_NX;
+                for (uint32_t k = 0; ok && k < nx; ++k) {
+                    const uint32_t x = x_lo[i] + k;
+                    ok = vt_alt_word(x_cls[x], rl, x_len[x], &xvt[x]);
+                }
+                w |= nx << VT_NX_SHIFT;
+            }
+            vth[i] = VtHot{h.end, ok ? w : VT_SLOW};
         }
         s.d.vth = dev_upload(s, vth);
+        s.d.xvt = dev_upload(s, xvt);
     }
     s.d.pos = dev_upload(s, pos);
     s.d.ref_key = dev_upload(s, ref_key);

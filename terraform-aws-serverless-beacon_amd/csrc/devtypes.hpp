@@ -54,18 +54,54 @@ struct alignas(16) RangeHot {
 };
 enum : uint32_t { RH_EMIT_MASK = 0xffu, RH_HIT = 1u << 8, RH_SLOW = 1u << 9 };
 
+enum : uint32_t { VT_DEL = 0, VT_INS = 1, VT_DUP = 2, VT_DUPT = 3, VT_CNV = 4, VT_OTHER = 5 };
 // What a referenceBases='N' / alternateBases=None variantType query
-// (MODE_VTYPE) reads of a record: the first ALT's class and lengths sit next
-// to END, so the predicate of search_variants.py:100-183 needs one 16-byte
-// load; AN is fetched for hit lanes only.  Built at upload from RecHot, POS
-// and len(ALT0); lens saturate at 0xffff (those records take eval_record, as
-// do multiallelic / AC-less / int()-failing ones).
-struct alignas(16) VtHot {
+// (MODE_VTYPE) reads of a record: END and everything the predicate of
+// search_variants.py:100-183 needs about the first ALT, packed into 8 bytes
+// (one global_load_dwordx2 per lane); AC / AN are fetched from RecHot and the
+// extra rows for hit lanes only.  The non-symbolic predicates depend on an ALT
+// only through (len(ALT) vs len(REF), the REF*k class, ALT == '.'), so that
+// triple is stored as a 5-bit class index and each variantType becomes a
+// 24-bit mask over it (vt_class_mask): the per-ALT test is one shift.
+// ALTs 2..n of a multiallelic record (at most 7) have the same 32-bit word in
+// DStore::xvt.  Built at upload.  Records the packing cannot represent (AC-less,
+// int() failures, a missing AC entry, more than 8 ALTs, lengths or symbolic
+// ids >= 255) carry VT_SLOW and take eval_record.
+struct alignas(8) VtHot {
     uint32_t end;
-    uint32_t hot;   // RecHot::hot
-    uint32_t lens;  // len(REF) | len(ALT0) << 16
-    int32_t ac0;
+    uint32_t w;  // len(ALT0):8 | class:5 << 8 | VT_SYM | sym id:8 << 16 | VT_SLOW | n extra ALTs:3 << 29
 };
+enum : uint32_t {
+    VT_CLASS_SHIFT = 8,  // class = cmp * 8 + rep * 2 + dot; cmp 0/1/2: len(ALT) <, ==, > len(REF);
+                         // rep 0: ALT is not REF*k, 1: k in {0, 1}, 2: k == 2, 3: k > 2
+    VT_SYM = 1u << 13,   // symbolic ALT (sym id in bits 16..23)
+    VT_SLOW = 1u << 28,
+    VT_NX_SHIFT = 29,
+    VT_MAX_NX = 7,
+};
+// bit c set = an ALT of class c satisfies variantType `kind` (vtype_hit)
+__host__ __device__ constexpr uint32_t vt_class_mask(uint32_t kind) {
+    uint32_t m = 0;
+    for (uint32_t c = 0; c < 24; ++c) {
+        const uint32_t cmp = c >> 3, rep = (c >> 1) & 3u, dot = c & 1u;
+        if (kind == VT_DEL ? cmp == 0 : kind == VT_INS ? cmp == 2 : kind == VT_DUP ? rep >= 2
+            : kind == VT_DUPT ? rep == 2 : kind == VT_CNV ? (dot != 0 || rep != 0) : false)
+            m |= 1u << c;
+    }
+    return m;
+}
+// the 32-bit word of one ALT with class bits `cls` (C_*); false = not representable
+inline bool vt_alt_word(uint32_t cls, uint64_t ref_len, uint64_t alt_len, uint32_t *w) {
+    const uint32_t sym = cls >> C_SYM_SHIFT;
+    const uint32_t rep = (cls >> C_REP_SHIFT) & 63u;
+    if ((cls & C_AC_MISSING) || ref_len >= 255 || alt_len >= 255 || ((cls & C_SYMBOLIC) && sym >= 255)) return false;
+    const uint32_t rc = rep == C_REP_NONE ? 0u : rep < 2 ? 1u : rep == 2 ? 2u : 3u;
+    const uint32_t cmp = alt_len < ref_len ? 0u : alt_len == ref_len ? 1u : 2u;
+    const uint32_t c = cmp * 8 + rc * 2 + ((cls & C_DOT) ? 1u : 0u);
+    *w = static_cast<uint32_t>(alt_len) | (c << VT_CLASS_SHIFT);
+    if (cls & C_SYMBOLIC) *w |= VT_SYM | (sym << 16);
+    return true;
+}
 
 // ---- query modes -----------------------------------------------------------
 enum : uint32_t {
@@ -78,7 +114,6 @@ enum : uint32_t {
 enum : uint32_t { ALT_N = 0, ALT_EXACT = 1, ALT_VTYPE = 2 };
 // scan-kernel specialisations (query classes launched separately)
 enum : int { MODE_GENERAL = 0, MODE_RANGE_N = 1, MODE_EXACT = 2, MODE_VTYPE = 3 };
-enum : uint32_t { VT_DEL = 0, VT_INS = 1, VT_DUP = 2, VT_DUPT = 3, VT_CNV = 4, VT_OTHER = 5 };
 enum : uint32_t {
     F_DETAILS = 1u << 0,         // include_details
     F_BOOL_BREAK = 1u << 1,      // granularity boolean in search_variants (:253)
@@ -99,6 +134,7 @@ struct DStore {
     const RecHot *rec;
     const RangeHot *rng;      // MODE_RANGE_N view of the same records
     const VtHot *vth;         // MODE_VTYPE view of the same records
+    const uint32_t *xvt;      // MODE_VTYPE word of each extra row
     const uint32_t *pos;
     const uint64_t *ref_key;  // key(REF.upper())
     const uint64_t *a0_key;   // key(ALT0.upper())

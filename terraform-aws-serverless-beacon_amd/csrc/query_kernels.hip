@@ -363,6 +363,10 @@ __device__ __forceinline__ int chunk_tail(ScanState &S, const LaneOut &o, uint32
     const bool hit = o.hm != 0;
     const uint64_t errm = __ballot(o.err != 0);
     const uint64_t hitm = __ballot(hit);
+    if (!(errm | hitm)) {  // nothing to emit, count or stop on: state unchanged
+        *collectm = 0;
+        return kWave;
+    }
     int64_t cum = 0;
     uint64_t trigm;  // hit lanes where the running call_count is non-zero
     if constexpr (NONNEG) {
@@ -581,13 +585,13 @@ __global__ __launch_bounds__(kBlock) void range_n_kernel(DStore st, const QDev *
 
 // MODE_VTYPE: referenceBases 'N' + alternateBases None + variantType queries
 // (search_variants.py:100-166, the patched-oracle branch selector; strict
-// mode goes to MODE_GENERAL).  One 16-byte VtHot word per record carries END,
-// the first ALT's class bits and len(REF) | len(ALT0); the predicate, the
-// length bounds (:177-183) and the AC contribution (:205-214) of a clean
-// biallelic record need no other load, and AN is gathered for hit lanes only
-// (hits are rare: most records are SNVs no variantType matches).  Records
-// that are multiallelic, lack AC, carry int() failures or missing AC entries,
-// or have lengths >= 0xffff take eval_record.
+// mode goes to MODE_GENERAL).  One 8-byte VtHot word per record carries END,
+// the first ALT's class (symbolic id, '.', REF*k class) and len(REF),
+// len(ALT0); the predicate and the length bounds (:177-183) of a clean
+// biallelic record need no other load, and AC0 / AN (:205-214) are gathered
+// for hit lanes only (hits are rare: most records are SNVs no variantType
+// matches).  Records flagged VT_SLOW (multiallelic, no AC, int() failures,
+// missing AC entries, lengths or symbolic ids >= 255) take eval_record.
 template <bool NONNEG>
 __global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__restrict__ qs,
                                                     const uint32_t *__restrict__ qidx, uint32_t nq,
@@ -603,49 +607,101 @@ __global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__res
     uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
     if (!(flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
     ScanState S;
-    const uint32_t emin = Q.end_min < 0 ? 0u : Q.end_min > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_min);
-    const uint32_t emax = Q.end_max < 0 ? 0u : Q.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_max);
     const bool end_void = Q.end_max < 0 || Q.end_min > 0xffffffffll || Q.end_min > Q.end_max;
-    constexpr uint32_t kSlowBits = H_MULTI | H_AC_BAD | H_AN_BAD | C_AC_MISSING;
+    // END in [e0, e0 + espan] and len(ALT0) in [vlo, vlo + vspan] as one
+    // unsigned compare each; an empty length range never matches (vlo = 256)
+    const uint32_t e0 = Q.end_min < 0 ? 0u : static_cast<uint32_t>(Q.end_min);
+    const uint32_t espan = (Q.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_max)) - e0;
+    const int64_t vl = Q.vmin < 0 ? 0 : Q.vmin, vh = Q.vmax > 255 ? 255 : Q.vmax;
+    const uint32_t vlo = vh < vl ? 256u : static_cast<uint32_t>(vl);
+    const uint32_t vspan = vh < vl ? 0u : static_cast<uint32_t>(vh - vl);
+    const uint32_t vk = Q.vt_kind;
+    constexpr uint32_t kDel = vt_class_mask(VT_DEL), kIns = vt_class_mask(VT_INS), kDup = vt_class_mask(VT_DUP),
+                       kDupT = vt_class_mask(VT_DUPT), kCnv = vt_class_mask(VT_CNV);
+    const uint32_t cmask = vk == VT_DEL ? kDel : vk == VT_INS ? kIns : vk == VT_DUP ? kDup : vk == VT_DUPT ? kDupT
+                         : vk == VT_CNV ? kCnv : 0u;
+    const uint32_t *lut = st.sym_lut + Q.lut_off;
     uint64_t *out = hits + Q.hit_off;
-    QView V{flags, REF_ANY, ALT_VTYPE, false, false, nullptr, nullptr, nullptr};
+    const QView V{flags, REF_ANY, ALT_VTYPE, false, false, nullptr, nullptr, nullptr};
+    const uint32_t ul = static_cast<uint32_t>(lane);
+    const uint32_t shi = end_void ? lo : hi;  // no END can match: nothing to scan
 
-    auto chunk = [&](uint32_t base, const VtHot h) -> bool {  // true = keep going
-        const uint32_t r = base + static_cast<uint32_t>(lane);
-        const bool cand = !end_void && r < hi && h.end >= emin && h.end <= emax;
-        const uint32_t rl = h.lens & 0xffffu, al = h.lens >> 16;
-        const bool slow = (h.hot & kSlowBits) || !(h.hot & H_HAS_AC) || rl == 0xffffu || al == 0xffffu;
-        LaneOut o{0, 0, 0, 0, 0};
-        if (cand && !slow) {
-            const int64_t len = al;
-            if (vtype_hit(Q, st, h.hot, len, rl) && len >= Q.vmin && len <= Q.vmax) {
-                o.hm = 1;
-                o.c = h.ac0;
-                o.em = h.ac0 != 0 ? 1ull : 0ull;
-                o.anv = st.rec[r].an;
-            }
+    auto alt_ok = [&](uint32_t aw) -> bool {  // one ALT word: predicate + length bounds
+        if ((aw & 0xffu) - vlo > vspan) return false;
+        if (aw & VT_SYM) {
+            const uint32_t sym = (aw >> 16) & 0xffu;
+            return (lut[sym >> 5] >> (sym & 31)) & 1u;
         }
-        if (__ballot(cand && slow)) {
-            if (cand && slow) o = eval_record(st, Q, V, r, st.rec[r]);
-        }
-        uint64_t cm;
-        return chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) >= kWave;
+        return (cmask >> ((aw >> VT_CLASS_SHIFT) & 31u)) & 1u;
     };
-    const uint32_t l0 = lo + static_cast<uint32_t>(lane);
-    VtHot a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
-    if (l0 < hi) a = st.vth[l0];
-    if (l0 + kWave < hi) b = st.vth[l0 + kWave];
-    for (uint32_t base = lo; base < hi; base += 2 * kWave) {
-        const uint32_t r = base + static_cast<uint32_t>(lane);
-        VtHot c2 = {0, 0, 0, 0};
-        if (r + 2 * kWave < hi) c2 = st.vth[r + 2 * kWave];
-        if (!chunk(base, a)) break;
-        if (base + kWave >= hi) break;
-        VtHot d2 = {0, 0, 0, 0};
-        if (r + 3 * kWave < hi) d2 = st.vth[r + 3 * kWave];
-        if (!chunk(base + kWave, b)) break;
-        a = c2;
-        b = d2;
+    // a lane whose word is not VT_SLOW (cand false: nothing)
+    auto lane_eval = [&](const VtHot h, uint32_t r, bool cand) -> LaneOut {
+        LaneOut o{0, 0, 0, 0, 0};
+        uint64_t hm = (cand && alt_ok(h.w)) ? 1ull : 0ull;
+        const uint32_t nx = cand ? h.w >> VT_NX_SHIFT : 0u;
+        uint32_t x0 = 0;
+        if (__ballot(nx != 0) && nx) {  // ALTs 2..n (:124 loop)
+            x0 = st.x_lo[r];
+            for (uint32_t k = 0; k < nx; ++k)
+                if (alt_ok(st.xvt[x0 + k])) hm |= 2ull << k;
+        }
+        if (hm) {  // :205-214, AC of each matching ALT
+            const RecHot rh = st.rec[r];
+            for (uint64_t b = hm; b; b &= b - 1) {
+                const int k = ffs64(b);
+                const int64_t v = k ? st.xrow[x0 + k - 1].ac : rh.ac0;
+                o.c += v;
+                if (v != 0) o.em |= 1ull << k;
+            }
+            o.hm = hm;
+            o.anv = rh.an;
+        }
+        return o;
+    };
+    auto fast_chunk = [&](uint32_t base, const VtHot h) -> int {  // 0 go on, 1 stop, 2 has VT_SLOW lanes
+        const uint32_t r = base + ul;
+        const bool cand = r < shi && h.end - e0 <= espan;
+        if (__ballot(cand && (h.w & VT_SLOW))) return 2;
+        const LaneOut o = lane_eval(h, r, cand);
+        uint64_t cm;
+        return chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) >= kWave ? 0 : 1;
+    };
+    // four chunks in flight per trip (8-byte words: 2 VGPRs each); a slice
+    // of a 1000G-shape store is ~4 chunks, so its whole range is requested
+    // before the first record is evaluated
+    auto ld = [&](uint32_t i) -> VtHot { return i < shi ? st.vth[i] : VtHot{0, 0}; };
+    uint32_t base = lo;
+    int status = 0;
+    {
+        const uint32_t l0 = lo + ul;
+        VtHot a0 = ld(l0), a1 = ld(l0 + kWave), a2 = ld(l0 + 2 * kWave), a3 = ld(l0 + 3 * kWave);
+        while (base < shi) {
+            const uint32_t r = base + ul;
+            const VtHot n0 = ld(r + 4 * kWave), n1 = ld(r + 5 * kWave), n2 = ld(r + 6 * kWave), n3 = ld(r + 7 * kWave);
+            if ((status = fast_chunk(base, a0)) != 0 || (base += kWave) >= shi) break;
+            if ((status = fast_chunk(base, a1)) != 0 || (base += kWave) >= shi) break;
+            if ((status = fast_chunk(base, a2)) != 0 || (base += kWave) >= shi) break;
+            if ((status = fast_chunk(base, a3)) != 0) break;
+            base += kWave;
+            a0 = n0;
+            a1 = n1;
+            a2 = n2;
+            a3 = n3;
+        }
+    }
+    if (status == 2) {  // the rest of the slice one chunk at a time, eval_record for VT_SLOW lanes
+        VtHot h = ld(base + ul);
+        for (; base < shi; base += kWave) {
+            const uint32_t r = base + ul;
+            const VtHot nh = ld(r + kWave);
+            const bool cand = r < shi && h.end - e0 <= espan;
+            const bool slow = cand && (h.w & VT_SLOW);
+            LaneOut o = lane_eval(h, r, cand && !slow);
+            if (__ballot(slow) && slow) o = eval_record(st, Q, V, r, st.rec[r]);
+            uint64_t cm;
+            if (chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) < kWave) break;
+            h = nh;
+        }
     }
     finish_query<NONNEG>(S, q, hi - lo, res);
 }
