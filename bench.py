@@ -168,7 +168,7 @@ def main():
         'device_ms_per_step': {'scan_kernel': round(timing['scan_ms'], 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                     'kernel': 'query step: range_n_kernel + scan_kernel<EXACT> (HIP events around both launches)',
+                     'kernel': 'query step: fused_kernel (range_n + exact groups in one launch; HIP events around it)',
                      'algorithmic_bytes_per_launch': scan_bytes},
         'cpu_baseline': cpu,
         'parity_sample': parity,

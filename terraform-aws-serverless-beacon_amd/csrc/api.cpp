@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <array>
 #include <cstdio>
+#include <cstdlib>
 #include <memory>
 #include <thread>
 
@@ -335,6 +336,39 @@ void upload_store(sb_builder &b, sb_store &s) {
 
     s.d.rec = dev_upload(s, rec);
     s.d.rng = dev_upload(s, rng);
+    {  // RangeHot8 per VCF: its most common AN, and whether the 8-byte words cover it
+        std::vector<RangeHot8> rng8(rng.size());
+        for (size_t vi = 0; vi < b.vcfs.size(); ++vi) {
+            VcfData &v = b.vcfs[vi];
+            const size_t r0 = v.rec_base, r1 = vi + 1 < b.vcfs.size() ? b.vcfs[vi + 1].rec_base : rng.size();
+            std::unordered_map<int32_t, uint64_t> freq;
+            for (size_t r = r0; r < r1; ++r) ++freq[rng[r].an];
+            int32_t mode = 0;
+            uint64_t best = 0;
+            for (const auto &kv : freq)
+                if (kv.second > best || (kv.second == best && kv.first < mode)) {
+                    best = kv.second;
+                    mode = kv.first;
+                }
+            uint64_t hit = 0, slow = 0;
+            for (size_t r = r0; r < r1; ++r) {
+                const RangeHot &h = rng[r];
+                uint32_t info = h.info & (RH_EMIT_MASK | RH_HIT | RH_SLOW);
+                if (h.an != mode || h.c < 0 || static_cast<uint32_t>(h.c) > RH8_C_MAX) info |= RH_SLOW;
+                rng8[r] = RangeHot8{h.end, (info & RH_SLOW) ? info : (info | (static_cast<uint32_t>(h.c) << RH8_C_SHIFT))};
+                if (info & RH_HIT) {
+                    ++hit;
+                    if ((info & RH_SLOW) && !(h.info & RH_SLOW)) ++slow;
+                }
+            }
+            v.an_default = mode;
+            // SBEACON_NO_RANGE8=1 keeps every VCF on RangeHot (tests cover both paths)
+            const char *no8e = std::getenv("SBEACON_NO_RANGE8");
+            const bool no8 = no8e && no8e[0] == '1';
+            v.range8 = !no8 && slow * 50 <= hit;
+        }
+        s.d.rng8 = dev_upload(s, rng8);
+    }
     std::vector<RangeHot>().swap(rng);
     {
         std::vector<VtHot> vth(rec.size());
@@ -350,10 +384,11 @@ void upload_store(sb_builder &b, sb_store &s) {
                 for (uint32_t k = 0; ok && k < nx; ++k) {
                     const uint32_t x = x_lo[i] + k;
                     ok = vt_alt_word(x_cls[x], rl, x_len[x], &xvt[x]);
+                    w |= vt_xk_bits(xvt[x]);
                 }
                 w |= nx << VT_NX_SHIFT;
             }
-            vth[i] = VtHot{h.end, ok ? w : VT_SLOW};
+            vth[i] = VtHot{h.end, ok ? w : VT_SLOW, h.ac0, h.an};
         }
         s.d.vth = dev_upload(s, vth);
         s.d.xvt = dev_upload(s, xvt);
@@ -496,6 +531,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         d.n_samples = n_samples;
         d.rec_base = v.rec_base;
         d.x_base = v.x_base;
+        d.an_default = v.an_default;
         d.plane0_base = v.plane0_base;
         d.planex_base = v.planex_base;
         if (v.nonneg) d.flags |= F_NONNEG;
@@ -613,9 +649,9 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         // collect -> general kernel with the sample path; otherwise the
         // narrowest specialisation whose predicates cover the query
         B.groups.clear();
-        // groups 0..3 = MODE_GENERAL/RANGE_N/EXACT/VTYPE without the sample
-        // path; group 4 = MODE_GENERAL with the sample planes compiled in
-        constexpr int kCollect = 4;
+        // groups 0..4 = MODE_GENERAL/RANGE_N/EXACT/VTYPE/RANGE_N8 without the
+        // sample path; group 5 = MODE_GENERAL with the sample planes compiled in
+        constexpr int kCollect = 5;
         for (int g = 0; g <= kCollect; ++g)
             B.groups.push_back(sb_batch::Group{g == kCollect ? MODE_GENERAL : g, g == kCollect ? s.max_words : 0u, {}, {}});
         for (uint32_t i = 0; i < B.nq; ++i) {
@@ -627,7 +663,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
             } else if (d.flags & (F_STRICT_UNBOUND | F_SAMPLES_VARIANT)) {
                 g = MODE_GENERAL;
             } else if (d.ref_mode == REF_ANY && d.alt_mode == ALT_N) {
-                g = MODE_RANGE_N;
+                g = s.vcfs[B.vcf[i]].range8 ? MODE_RANGE_N8 : MODE_RANGE_N;
             } else if (d.ref_mode == REF_EXACT && d.alt_mode == ALT_EXACT) {
                 g = MODE_EXACT;
             } else if (d.ref_mode == REF_ANY && d.alt_mode == ALT_VTYPE) {
@@ -650,7 +686,9 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
                 return x.seg_lo != y.seg_lo ? x.seg_lo < y.seg_lo : x.first_bp < y.first_bp;
             });
     }
-    if (lut_all.empty()) lut_all.push_back(0);
+    // 8 words of slack: vt_kernel reads words 0..7 of its LUT unconditionally
+    // (packed symbolic ids are < 255; words past a LUT's end are never consulted)
+    lut_all.insert(lut_all.end(), 8, 0u);
     // ---- device buffers
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
@@ -685,11 +723,20 @@ void run(sb_batch &B) {
     }
     const auto &E = B.ev[B.runs_pending++];
     HIP_OK(hipEventRecord(E[0], st));
+    // sample-free groups: one fused launch, long scans first (range, variantType,
+    // general) and point lookups last, so the short waves fill the tail
+    std::vector<FusedGroup> fg;
+    for (int mode : {MODE_RANGE_N8, MODE_RANGE_N, MODE_VTYPE, MODE_GENERAL, MODE_EXACT})
+        for (const auto &g : B.groups)
+            if (g.max_words == 0 && g.mode == mode)
+                fg.push_back(FusedGroup{g.d_idx.as<uint32_t>(), static_cast<uint32_t>(g.idx.size()), g.mode});
+    launch_fused(d, B.q.as<QDev>(), fg.data(), static_cast<int>(fg.size()), B.nonneg, B.qbytes.as<uint8_t>(),
+                 B.subsets.as<uint64_t>(), B.res.as<QRes>(), B.hits.as<uint64_t>(), st);
     for (const auto &g : B.groups)
-        launch_scan(d, B.q.as<QDev>(), g.d_idx.as<uint32_t>(),
-                    static_cast<uint32_t>(g.idx.size()), B.nonneg, g.max_words, g.mode, B.qbytes.as<uint8_t>(),
-                    B.subsets.as<uint64_t>(), B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(),
-                    st);
+        if (g.max_words != 0)
+            launch_scan(d, B.q.as<QDev>(), g.d_idx.as<uint32_t>(), static_cast<uint32_t>(g.idx.size()), B.nonneg,
+                        g.max_words, g.mode, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(), B.res.as<QRes>(),
+                        B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), st);
     HIP_OK(hipEventRecord(E[1], st));
     HIP_OK(hipGetLastError());
 }

@@ -53,28 +53,51 @@ struct alignas(16) RangeHot {
     int32_t c;
 };
 enum : uint32_t { RH_EMIT_MASK = 0xffu, RH_HIT = 1u << 8, RH_SLOW = 1u << 9 };
+// The same in 8 bytes for a VCF whose records (almost) all carry one AN (the
+// 1000 Genomes shape: AN = 2 x samples at every site): w = info bits 0..9 as
+// above | c << RH8_C_SHIFT (21 bits), AN = the VCF's common value
+// (QDev::an_default).  A record whose AN differs, or whose c is negative or
+// >= 2^21, is RH_SLOW here.  Halves the bytes a range scan streams.
+struct alignas(8) RangeHot8 {
+    uint32_t end;
+    uint32_t w;
+};
+enum : uint32_t { RH8_C_SHIFT = 11, RH8_C_MAX = (1u << 21) - 1 };
 
 enum : uint32_t { VT_DEL = 0, VT_INS = 1, VT_DUP = 2, VT_DUPT = 3, VT_CNV = 4, VT_OTHER = 5 };
 // What a referenceBases='N' / alternateBases=None variantType query
 // (MODE_VTYPE) reads of a record: END and everything the predicate of
-// search_variants.py:100-183 needs about the first ALT, packed into 8 bytes
-// (one global_load_dwordx2 per lane); AC / AN are fetched from RecHot and the
-// extra rows for hit lanes only.  The non-symbolic predicates depend on an ALT
+// search_variants.py:100-183 needs about the first ALT, plus AC0 and AN, in
+// 16 bytes (one global_load_dwordx4 per lane): a biallelic hit needs no other
+// load, which matters because vmcnt retires in order, so a dependent load in
+// a chunk would drain the whole stream window behind it.  Only multiallelic
+// lanes read their extra rows.  The non-symbolic predicates depend on an ALT
 // only through (len(ALT) vs len(REF), the REF*k class, ALT == '.'), so that
 // triple is stored as a 5-bit class index and each variantType becomes a
 // 24-bit mask over it (vt_class_mask): the per-ALT test is one shift.
 // ALTs 2..n of a multiallelic record (at most 7) have the same 32-bit word in
-// DStore::xvt.  Built at upload.  Records the packing cannot represent (AC-less,
+// DStore::xvt; the record's own word says, per variantType, whether any of
+// them could match (VT_XK_*, length bounds aside), so a lane reads its extra
+// rows only then (a typical multiallelic SNV never does).  Built at upload.  Records the packing cannot represent (AC-less,
 // int() failures, a missing AC entry, more than 8 ALTs, lengths or symbolic
 // ids >= 255) carry VT_SLOW and take eval_record.
-struct alignas(8) VtHot {
+struct alignas(16) VtHot {
     uint32_t end;
     uint32_t w;  // len(ALT0):8 | class:5 << 8 | VT_SYM | sym id:8 << 16 | VT_SLOW | n extra ALTs:3 << 29
+    int32_t ac0;
+    int32_t an;
 };
 enum : uint32_t {
     VT_CLASS_SHIFT = 8,  // class = cmp * 8 + rep * 2 + dot; cmp 0/1/2: len(ALT) <, ==, > len(REF);
                          // rep 0: ALT is not REF*k, 1: k in {0, 1}, 2: k == 2, 3: k > 2
     VT_SYM = 1u << 13,   // symbolic ALT (sym id in bits 16..23)
+    // some extra ALT is of a class DEL / INS / DUP / DUP:TANDEM / CNV accepts, or symbolic
+    VT_XK_DEL = 1u << 14,
+    VT_XK_INS = 1u << 15,
+    VT_XK_DUP = 1u << 24,
+    VT_XK_DUPT = 1u << 25,
+    VT_XK_CNV = 1u << 26,
+    VT_XK_SYM = 1u << 27,
     VT_SLOW = 1u << 28,
     VT_NX_SHIFT = 29,
     VT_MAX_NX = 7,
@@ -89,6 +112,19 @@ __host__ __device__ constexpr uint32_t vt_class_mask(uint32_t kind) {
             m |= 1u << c;
     }
     return m;
+}
+__host__ __device__ constexpr uint32_t vt_xk_bit(uint32_t kind) {
+    return kind == VT_DEL ? VT_XK_DEL : kind == VT_INS ? VT_XK_INS : kind == VT_DUP ? VT_XK_DUP
+         : kind == VT_DUPT ? VT_XK_DUPT : kind == VT_CNV ? VT_XK_CNV : 0u;
+}
+// the VT_XK_* bits one extra-ALT word contributes to its record's word
+inline uint32_t vt_xk_bits(uint32_t xw) {
+    if (xw & VT_SYM) return VT_XK_SYM;
+    const uint32_t c = (xw >> VT_CLASS_SHIFT) & 31u;
+    uint32_t b = 0;
+    for (uint32_t k = VT_DEL; k <= VT_CNV; ++k)
+        if ((vt_class_mask(k) >> c) & 1u) b |= vt_xk_bit(k);
+    return b;
 }
 // the 32-bit word of one ALT with class bits `cls` (C_*); false = not representable
 inline bool vt_alt_word(uint32_t cls, uint64_t ref_len, uint64_t alt_len, uint32_t *w) {
@@ -113,7 +149,7 @@ enum : uint32_t {
 };
 enum : uint32_t { ALT_N = 0, ALT_EXACT = 1, ALT_VTYPE = 2 };
 // scan-kernel specialisations (query classes launched separately)
-enum : int { MODE_GENERAL = 0, MODE_RANGE_N = 1, MODE_EXACT = 2, MODE_VTYPE = 3 };
+enum : int { MODE_GENERAL = 0, MODE_RANGE_N = 1, MODE_EXACT = 2, MODE_VTYPE = 3, MODE_RANGE_N8 = 4 };
 enum : uint32_t {
     F_DETAILS = 1u << 0,         // include_details
     F_BOOL_BREAK = 1u << 1,      // granularity boolean in search_variants (:253)
@@ -133,6 +169,7 @@ struct DStore {
     // record-indexed
     const RecHot *rec;
     const RangeHot *rng;      // MODE_RANGE_N view of the same records
+    const RangeHot8 *rng8;    // MODE_RANGE_N8 view (VCFs with a common AN)
     const VtHot *vth;         // MODE_VTYPE view of the same records
     const uint32_t *xvt;      // MODE_VTYPE word of each extra row
     const uint32_t *pos;
@@ -182,6 +219,7 @@ struct QDev {
     uint64_t subset_off;       // word offset of subset mask (samples variant), ~0 = none
     uint64_t samples_out_off;  // word offset of the per-query sample bitset, ~0 = none
     uint64_t hit_off;          // this query's output region (host-planned upper bound)
+    int64_t an_default;        // the VCF's common AN (MODE_RANGE_N8)
 };
 
 struct QRes {

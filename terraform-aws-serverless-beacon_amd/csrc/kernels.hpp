@@ -21,6 +21,17 @@ void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t
                  int mode, const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits,
                  uint64_t *samples_out, hipStream_t s);
 
+// Several sample-free groups (each a list of queries fitting one MODE_*) in
+// one launch, in the order given (put the longest-running first).
+constexpr int kFusedMax = 5;
+struct FusedGroup {
+    const uint32_t *qidx;
+    uint32_t n;
+    int mode;
+};
+void launch_fused(const DStore &st, const QDev *q, const FusedGroup *groups, int count, bool nonneg,
+                  const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, hipStream_t s);
+
 // summariseSlice: phase A = one workgroup per chunk of kSumChunk records
 // (chunk_slice[c] = its slice), reducing the records' (numVariants, numCalls)
 // contributions into part[c] and writing the overshoot bitmap; phase B = one

@@ -19,6 +19,8 @@
 // bandwidth on the RecHot stream.
 #include <hip/hip_runtime.h>
 
+#include <stdexcept>
+
 #include "../../include/sbeacon.h"
 #include "devtypes.hpp"
 #include "kernels.hpp"
@@ -30,10 +32,24 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
+// chunks in flight per wave in the streaming kernels (stream_window)
+constexpr int kRangeWindow = 8;  // 16-byte RangeHot: 32 VGPRs
+constexpr int kRange8Window = 8;  // 8-byte RangeHot8: 16 VGPRs
+constexpr int kVtWindow = 4;     // 16-byte VtHot: 16 VGPRs (a 1000G-shape slice is ~4 chunks)
 
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// lane k's value, k wave-uniform (v_readlane into an SGPR)
+__device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t k) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(k)));
+}
+__device__ __forceinline__ int64_t rdl64(int64_t v, uint32_t k) {
+    const uint64_t u = static_cast<uint64_t>(v);
+    return static_cast<int64_t>((static_cast<uint64_t>(rdl(static_cast<uint32_t>(u >> 32), k)) << 32) |
+                                rdl(static_cast<uint32_t>(u), k));
+}
 
 __device__ __forceinline__ int ffs64(uint64_t m) { return __ffsll(static_cast<unsigned long long>(m)) - 1; }
 
@@ -432,19 +448,64 @@ __device__ __forceinline__ void finish_query(const ScanState &S, uint32_t q, uin
     }
 }
 
+// Sliding-window stream over the chunks of [lo, hi): D chunks of packed words
+// are in flight per wave, and chunk base + D*64 is requested as soon as chunk
+// base is consumed (the window rotates by register name in the unrolled body,
+// never by copy, so no load is waited on early).  `ld` must load
+// unconditionally (clamped index, no exec-masked branch): a load under a
+// divergent branch makes the waitcnt pass fall back to vmcnt(0).  `fast(base, word)` evaluates
+// one chunk: 0 = go on, 1 = the query is done, 2 = the chunk holds lanes only
+// the general path can decide (not consumed).  Returns that status; *at = the
+// base of the chunk it stopped on.
+template <int D, typename W, typename Load, typename Fast>
+__device__ __forceinline__ int stream_window(uint32_t lo, uint32_t hi, uint32_t *at, Load ld, Fast fast) {
+    const uint32_t ul = static_cast<uint32_t>(lane_id());
+    uint32_t base = lo;
+    int status = 0;
+    if (lo >= hi) {
+        *at = lo;
+        return 0;
+    }
+    W a[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) a[k] = ld(lo + ul + static_cast<uint32_t>(k) * kWave);
+    // The first D chunks are straight-line code: the waitcnt pass counts the
+    // loads in flight exactly there (vmcnt(D-1-k)), while at a loop header it
+    // falls back to vmcnt(0).  Most slices end inside this block; longer ones
+    // continue in the loop, whose header drains once per D chunks.
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        status = fast(base, a[k]);
+        if (status) goto done;
+        if (base + static_cast<uint32_t>(D) * kWave < hi) a[k] = ld(base + ul + static_cast<uint32_t>(D) * kWave);
+        base += kWave;
+        if (base >= hi) goto done;
+    }
+    for (;;) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            status = fast(base, a[k]);
+            if (status) goto done;
+            a[k] = ld(base + ul + static_cast<uint32_t>(D) * kWave);
+            base += kWave;
+            if (base >= hi) goto done;
+        }
+    }
+done:
+    *at = base;
+    return status;
+}
+
 // NACC: 64-bit sample-bitset words per lane (0 = no query in this launch
 // collects samples); NONNEG: every AC in the store is >= 0, so the running
 // call_count is monotone and `if call_count:` reduces to ballots.  MODE_EXACT
 // specialises the predicates for REF/ALT point queries; MODE_GENERAL handles
 // every payload (variantType, samples variant, strict mode, wildcards).
 template <int NACC, bool NONNEG, int MODE>
-__global__ __launch_bounds__(kBlock) void scan_kernel(
-    DStore st, const QDev *__restrict__ qs, const uint32_t *__restrict__ qidx, uint32_t nq,
+__device__ __forceinline__ void scan_slice(
+    DStore st, const QDev *__restrict__ qs, 
     const uint8_t *__restrict__ qbytes, const uint64_t *__restrict__ subsets, QRes *__restrict__ res,
-    uint64_t *__restrict__ hits, uint64_t *__restrict__ samples_out) {
-    const uint32_t w = uniform(xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + (threadIdx.x >> 6));
-    if (w >= nq) return;
-    const uint32_t q = qidx ? uniform(qidx[w]) : w;
+    uint64_t *__restrict__ hits, uint64_t *__restrict__ samples_out, uint32_t q, uint32_t lo, uint32_t hi) {
     const int lane = lane_id();
     const QDev &Q = qs[q];
     constexpr bool kGeneral = MODE == MODE_GENERAL;
@@ -461,8 +522,6 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(
     const bool collect = NACC > 0 && (V.flags & F_COLLECT) && details;
     const bool stop_on_exists = !details || (V.flags & F_BOOL_BREAK);
 
-    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;  // a <= POS <= b (:84-85)
-    if (!(V.flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
 
     ScanState S;
     uint64_t acc[NACC > 0 ? NACC : 1];
@@ -517,95 +576,115 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(
     }
 }
 
-// MODE_RANGE_N: referenceBases 'N' + alternateBases 'N' range queries (the
-// bulk of Beacon traffic).  Every per-record quantity such a query needs is
-// query-independent and sits in one 16-byte RangeHot word (devtypes.hpp), so
-// a record costs one coalesced dwordx4 load and a handful of VALU ops; records
-// flagged RH_SLOW (no AC, int() failures, > 8 ALTs ...) take eval_record.
-// The stream is unrolled two chunks per trip so the prefetched words rotate
-// by register name, never by copy (a copy of an in-flight load would wait).
-template <bool NONNEG>
-__global__ __launch_bounds__(kBlock) void range_n_kernel(DStore st, const QDev *__restrict__ qs,
-                                                         const uint32_t *__restrict__ qidx, uint32_t nq,
-                                                         QRes *__restrict__ res, uint64_t *__restrict__ hits) {
-    const uint32_t w = uniform(xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + (threadIdx.x >> 6));
-    if (w >= nq) return;
-    const uint32_t q = qidx ? uniform(qidx[w]) : w;
+// MODE_RANGE_N / MODE_RANGE_N8: referenceBases 'N' + alternateBases 'N'
+// range queries (the bulk of Beacon traffic).  Every per-record quantity such
+// a query needs is query-independent and sits in one RangeHot word (16 bytes)
+// or, for a VCF with a common AN, one RangeHot8 word (8 bytes; devtypes.hpp),
+// so a record costs one coalesced load and a handful of VALU ops, streamed
+// through a stream_window; chunks with RH_SLOW lanes (no AC, int() failures,
+// > 8 ALTs, an uncommon AN in RangeHot8 ...) go to a tail loop with
+// eval_record.
+// the two record words of MODE_RANGE_N / MODE_RANGE_N8
+template <typename W>
+struct RangeWord;
+template <>
+struct RangeWord<RangeHot> {
+    static constexpr int kWindow = kRangeWindow;
+    static __device__ __forceinline__ const RangeHot *col(const DStore &st) { return st.rng; }
+    static __device__ __forceinline__ uint32_t info(const RangeHot &h) { return h.info; }
+    static __device__ __forceinline__ int64_t c(const RangeHot &h) { return h.c; }
+    static __device__ __forceinline__ int64_t an(const RangeHot &h, int64_t) { return h.an; }
+};
+template <>
+struct RangeWord<RangeHot8> {
+    static constexpr int kWindow = kRange8Window;
+    static __device__ __forceinline__ const RangeHot8 *col(const DStore &st) { return st.rng8; }
+    static __device__ __forceinline__ uint32_t info(const RangeHot8 &h) { return h.w; }
+    static __device__ __forceinline__ int64_t c(const RangeHot8 &h) { return h.w >> RH8_C_SHIFT; }
+    static __device__ __forceinline__ int64_t an(const RangeHot8 &, int64_t an_default) { return an_default; }
+};
+
+template <bool NONNEG, typename W>
+__device__ __forceinline__ void range_n_slice(DStore st, const QDev *__restrict__ qs,
+                                                         
+                                                         QRes *__restrict__ res, uint64_t *__restrict__ hits, uint32_t q, uint32_t lo, uint32_t hi) {
     const int lane = lane_id();
     const QDev &Q = qs[q];
     const uint32_t flags = Q.flags;
     const bool details = flags & F_DETAILS;
     const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
-    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
-    if (!(flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
     ScanState S;
     // len(alt) = 1 for every ALT an 'N' query can hit (:174)
     const bool len_ok = Q.vmin <= 1 && Q.vmax >= 1;
-    const uint32_t emin = Q.end_min < 0 ? 0u : Q.end_min > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_min);
-    const uint32_t emax = Q.end_max < 0 ? 0u : Q.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_max);
     const bool end_void = Q.end_max < 0 || Q.end_min > 0xffffffffll || Q.end_min > Q.end_max;
-    const uint32_t hit_bits = (len_ok && !end_void) ? RH_HIT : 0u;
+    const uint32_t e0 = Q.end_min < 0 ? 0u : static_cast<uint32_t>(Q.end_min);  // END in [e0, e0 + espan]
+    const uint32_t espan = (Q.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_max)) - e0;
+    const uint32_t shi = (len_ok && !end_void) ? hi : lo;  // nothing can hit: nothing to scan
     uint64_t *out = hits + Q.hit_off;
-    QView V{flags, REF_ANY, ALT_N, false, false, nullptr, nullptr, nullptr};
+    const QView V{flags, REF_ANY, ALT_N, false, false, nullptr, nullptr, nullptr};
+    const uint32_t ul = static_cast<uint32_t>(lane);
 
-    auto chunk = [&](uint32_t base, const RangeHot h) -> bool {  // true = keep going
-        const uint32_t r = base + static_cast<uint32_t>(lane);
-        const bool cand = r < hi && (h.info & hit_bits) && h.end >= emin && h.end <= emax;
+    using RW = RangeWord<W>;
+    const int64_t an_default = Q.an_default;
+    const W *col = RW::col(st);
+    auto lane_eval = [&](const W h, bool cand) -> LaneOut {
         LaneOut o{0, 0, 0, 0, 0};
         if (cand) {
             o.hm = 1;
-            o.em = h.info & RH_EMIT_MASK;
-            o.c = h.c;
-            o.anv = h.an;
+            o.em = RW::info(h) & RH_EMIT_MASK;
+            o.c = RW::c(h);
+            o.anv = RW::an(h, an_default);
         }
-        if (__ballot(cand && (h.info & RH_SLOW))) {
-            if (cand && (h.info & RH_SLOW)) o = eval_record(st, Q, V, r, st.rec[r]);
-        }
-        uint64_t cm;
-        return chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) >= kWave;
+        return o;
     };
-    const uint32_t l0 = lo + static_cast<uint32_t>(lane);
-    RangeHot a = {0, 0, 0, 0}, b = {0, 0, 0, 0};
-    if (l0 < hi) a = st.rng[l0];
-    if (l0 + kWave < hi) b = st.rng[l0 + kWave];
-    for (uint32_t base = lo; base < hi; base += 2 * kWave) {
-        const uint32_t r = base + static_cast<uint32_t>(lane);
-        RangeHot c2 = {0, 0, 0, 0};
-        if (r + 2 * kWave < hi) c2 = st.rng[r + 2 * kWave];
-        if (!chunk(base, a)) break;
-        if (base + kWave >= hi) break;
-        RangeHot d2 = {0, 0, 0, 0};
-        if (r + 3 * kWave < hi) d2 = st.rng[r + 3 * kWave];
-        if (!chunk(base + kWave, b)) break;
-        a = c2;
-        b = d2;
+    auto fast = [&](uint32_t base, const W h) -> int {
+        const uint32_t r = base + ul;
+        const bool cand = r < shi && (RW::info(h) & RH_HIT) && h.end - e0 <= espan;
+        if (__ballot(cand && (RW::info(h) & RH_SLOW))) return 2;
+        uint64_t cm;
+        return chunk_tail<NONNEG>(S, lane_eval(h, cand), r, stop_on_exists, details, out, &cm) >= kWave ? 0 : 1;
+    };
+    // clamped, unconditional (used only when lo < shi); lanes past shi fail `cand`
+    auto ld = [&](uint32_t i) -> W { return col[min(i, shi - 1)]; };
+    uint32_t base = lo;
+    if (lo < shi && stream_window<RW::kWindow, W>(lo, shi, &base, ld, fast) == 2) {
+        // the rest one chunk at a time, eval_record for RH_SLOW lanes
+        W h = ld(base + ul);
+        for (; base < shi; base += kWave) {
+            const uint32_t r = base + ul;
+            const W nh = ld(r + kWave);
+            const bool cand = r < shi && (RW::info(h) & RH_HIT) && h.end - e0 <= espan;
+            const bool slow = cand && (RW::info(h) & RH_SLOW);
+            LaneOut o = lane_eval(h, cand && !slow);
+            if (__ballot(slow) && slow) o = eval_record(st, Q, V, r, st.rec[r]);
+            uint64_t cm;
+            if (chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) < kWave) break;
+            h = nh;
+        }
     }
     finish_query<NONNEG>(S, q, hi - lo, res);
 }
 
 // MODE_VTYPE: referenceBases 'N' + alternateBases None + variantType queries
 // (search_variants.py:100-166, the patched-oracle branch selector; strict
-// mode goes to MODE_GENERAL).  One 8-byte VtHot word per record carries END,
-// the first ALT's class (symbolic id, '.', REF*k class) and len(REF),
-// len(ALT0); the predicate and the length bounds (:177-183) of a clean
-// biallelic record need no other load, and AC0 / AN (:205-214) are gathered
-// for hit lanes only (hits are rare: most records are SNVs no variantType
-// matches).  Records flagged VT_SLOW (multiallelic, no AC, int() failures,
-// missing AC entries, lengths or symbolic ids >= 255) take eval_record.
+// mode goes to MODE_GENERAL).  One 16-byte VtHot word per record carries END,
+// the first ALT's class index (len(ALT0) vs len(REF), REF*k class, '.') or
+// symbolic id, len(ALT0), AC0 and AN: the predicate, the length bounds
+// (:177-183) and the AC / AN contributions (:205-214) of a biallelic record
+// need no other load.  Multiallelic lanes read their extra rows' words
+// (DStore::xvt) and AC; records flagged VT_SLOW (no AC, int() failures,
+// missing AC entries, > 8 ALTs, lengths or symbolic ids >= 255) go to a
+// one-chunk-at-a-time tail loop with eval_record.  The record stream is a
+// stream_window of kVtWindow chunks.
 template <bool NONNEG>
-__global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__restrict__ qs,
-                                                    const uint32_t *__restrict__ qidx, uint32_t nq,
-                                                    QRes *__restrict__ res, uint64_t *__restrict__ hits) {
-    const uint32_t w = uniform(xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + (threadIdx.x >> 6));
-    if (w >= nq) return;
-    const uint32_t q = qidx ? uniform(qidx[w]) : w;
+__device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
+                                                    
+                                                    QRes *__restrict__ res, uint64_t *__restrict__ hits, uint32_t q, uint32_t lo, uint32_t hi) {
     const int lane = lane_id();
     const QDev &Q = qs[q];
     const uint32_t flags = Q.flags;
     const bool details = flags & F_DETAILS;
     const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
-    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
-    if (!(flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
     ScanState S;
     const bool end_void = Q.end_max < 0 || Q.end_min > 0xffffffffll || Q.end_min > Q.end_max;
     // END in [e0, e0 + espan] and len(ALT0) in [vlo, vlo + vspan] as one
@@ -620,41 +699,51 @@ __global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__res
                        kDupT = vt_class_mask(VT_DUPT), kCnv = vt_class_mask(VT_CNV);
     const uint32_t cmask = vk == VT_DEL ? kDel : vk == VT_INS ? kIns : vk == VT_DUP ? kDup : vk == VT_DUPT ? kDupT
                          : vk == VT_CNV ? kCnv : 0u;
+    const uint32_t xneed = vt_xk_bit(vk) | VT_XK_SYM;  // an extra ALT might match
     const uint32_t *lut = st.sym_lut + Q.lut_off;
     uint64_t *out = hits + Q.hit_off;
     const QView V{flags, REF_ANY, ALT_VTYPE, false, false, nullptr, nullptr, nullptr};
     const uint32_t ul = static_cast<uint32_t>(lane);
     const uint32_t shi = end_void ? lo : hi;  // no END can match: nothing to scan
 
-    auto alt_ok = [&](uint32_t aw) -> bool {  // one ALT word: predicate + length bounds
+    // lanes 0..7 hold LUT words 0..7 (symbolic ids in the words are < 255);
+    // ALT0 lanes fetch theirs with ds_bpermute: no vector-memory load inside
+    // a chunk, so the stream window is never drained for a symbolic ALT
+    const uint32_t lutv = lut[min(ul, 7u)];
+    // one ALT word + the LUT word its symbolic id falls in: predicate + length bounds
+    auto alt_ok = [&](uint32_t aw, uint32_t lw) -> bool {
         if ((aw & 0xffu) - vlo > vspan) return false;
-        if (aw & VT_SYM) {
-            const uint32_t sym = (aw >> 16) & 0xffu;
-            return (lut[sym >> 5] >> (sym & 31)) & 1u;
-        }
+        if (aw & VT_SYM) return (lw >> ((aw >> 16) & 31u)) & 1u;
         return (cmask >> ((aw >> VT_CLASS_SHIFT) & 31u)) & 1u;
     };
     // a lane whose word is not VT_SLOW (cand false: nothing)
     auto lane_eval = [&](const VtHot h, uint32_t r, bool cand) -> LaneOut {
         LaneOut o{0, 0, 0, 0, 0};
-        uint64_t hm = (cand && alt_ok(h.w)) ? 1ull : 0ull;
-        const uint32_t nx = cand ? h.w >> VT_NX_SHIFT : 0u;
+        const uint32_t lw0 = __shfl(lutv, static_cast<int>((h.w >> 21) & 7u), kWave);  // all lanes active here
+        uint64_t hm = (cand && alt_ok(h.w, lw0)) ? 1ull : 0ull;
+        const uint32_t nx = (cand && (h.w & xneed)) ? h.w >> VT_NX_SHIFT : 0u;
         uint32_t x0 = 0;
         if (__ballot(nx != 0) && nx) {  // ALTs 2..n (:124 loop)
             x0 = st.x_lo[r];
-            for (uint32_t k = 0; k < nx; ++k)
-                if (alt_ok(st.xvt[x0 + k])) hm |= 2ull << k;
+            for (uint32_t k = 0; k < nx; ++k) {
+                const uint32_t xw = st.xvt[x0 + k];
+                if (alt_ok(xw, (xw & VT_SYM) ? lut[(xw >> 21) & 7u] : 0u)) hm |= 2ull << k;
+            }
         }
         if (hm) {  // :205-214, AC of each matching ALT
-            const RecHot rh = st.rec[r];
-            for (uint64_t b = hm; b; b &= b - 1) {
-                const int k = ffs64(b);
-                const int64_t v = k ? st.xrow[x0 + k - 1].ac : rh.ac0;
-                o.c += v;
-                if (v != 0) o.em |= 1ull << k;
+            if (hm == 1ull) {
+                o.c = h.ac0;
+                o.em = h.ac0 != 0 ? 1ull : 0ull;
+            } else {
+                for (uint64_t b = hm; b; b &= b - 1) {
+                    const int k = ffs64(b);
+                    const int64_t v = k ? st.xrow[x0 + k - 1].ac : h.ac0;
+                    o.c += v;
+                    if (v != 0) o.em |= 1ull << k;
+                }
             }
             o.hm = hm;
-            o.anv = rh.an;
+            o.anv = h.an;
         }
         return o;
     };
@@ -666,29 +755,10 @@ __global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__res
         uint64_t cm;
         return chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) >= kWave ? 0 : 1;
     };
-    // four chunks in flight per trip (8-byte words: 2 VGPRs each); a slice
-    // of a 1000G-shape store is ~4 chunks, so its whole range is requested
-    // before the first record is evaluated
-    auto ld = [&](uint32_t i) -> VtHot { return i < shi ? st.vth[i] : VtHot{0, 0}; };
+    // clamped, unconditional (used only when lo < shi); lanes past shi fail `cand`
+    auto ld = [&](uint32_t i) -> VtHot { return st.vth[min(i, shi - 1)]; };
     uint32_t base = lo;
-    int status = 0;
-    {
-        const uint32_t l0 = lo + ul;
-        VtHot a0 = ld(l0), a1 = ld(l0 + kWave), a2 = ld(l0 + 2 * kWave), a3 = ld(l0 + 3 * kWave);
-        while (base < shi) {
-            const uint32_t r = base + ul;
-            const VtHot n0 = ld(r + 4 * kWave), n1 = ld(r + 5 * kWave), n2 = ld(r + 6 * kWave), n3 = ld(r + 7 * kWave);
-            if ((status = fast_chunk(base, a0)) != 0 || (base += kWave) >= shi) break;
-            if ((status = fast_chunk(base, a1)) != 0 || (base += kWave) >= shi) break;
-            if ((status = fast_chunk(base, a2)) != 0 || (base += kWave) >= shi) break;
-            if ((status = fast_chunk(base, a3)) != 0) break;
-            base += kWave;
-            a0 = n0;
-            a1 = n1;
-            a2 = n2;
-            a3 = n3;
-        }
-    }
+    const int status = lo < shi ? stream_window<kVtWindow, VtHot>(lo, shi, &base, ld, fast_chunk) : 0;
     if (status == 2) {  // the rest of the slice one chunk at a time, eval_record for VT_SLOW lanes
         VtHot h = ld(base + ul);
         for (; base < shi; base += kWave) {
@@ -708,6 +778,175 @@ __global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__res
 
 // Gather each query's hits from its planned region into a dense array
 // (result shipping at fetch time; not part of the timed query step).
+// ---------------------------------------------------------------- slice runs
+// A wave answers `run` (<= kRun) consecutive entries of the (position-sorted)
+// launch list; the host picks run per launch (run_for) so that a small batch
+// still spreads over every SIMD.  One slice is only a few chunks of records, so a wave per slice would
+// spend most of its life on dependent setup rounds (query, index bucket, POS
+// probe) before its few data loads.  Here lanes 2j / 2j+1 fetch slice j's
+// parameters and bracket its lower / upper bound together, the 64-wide POS
+// probes of all 2*run bounds are issued at once, and the slices are then
+// evaluated in order with their [lo, hi) already known: the setup latency is
+// paid once per run.  Bounds are those of slice_bounds.
+constexpr uint32_t kRun = 8;
+
+template <class Body>
+__device__ __forceinline__ void run_slices(const DStore &st, const QDev *__restrict__ qs,
+                                           const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run, uint32_t w,
+                                           Body body) {
+    const uint32_t first = w * run;
+    if (first >= nq) return;
+    const uint32_t n = min(run, nq - first);
+    const uint32_t lane = static_cast<uint32_t>(lane_id());
+    const uint32_t j = lane >> 1;
+    const bool upper = lane & 1u;
+    uint32_t q = 0, L = 0, H = 0, done = 1;
+    int64_t x = 0;
+    if (j < n) {
+        q = qidx ? qidx[first + j] : first + j;
+        const QDev &Q = qs[q];
+        if ((Q.flags & F_EMPTY) || Q.first_bp > Q.last_bp) {  // a <= POS <= b (:84-85)
+            L = H = Q.seg_lo;
+        } else {
+            x = upper ? Q.last_bp + 1 : Q.first_bp;
+            const Bracket k = bracket(st, Q, x);
+            L = k.L;
+            H = k.H;
+            done = k.done ? 1u : 0u;
+        }
+    }
+    const uint32_t nb = 2 * n;
+    uint32_t v[2 * kRun];
+#pragma unroll
+    for (uint32_t k = 0; k < 2 * kRun; ++k) {
+        v[k] = 0xffffffffu;
+        if (k < nb) {
+            const uint32_t i = rdl(L, k) + lane;
+            if (!rdl(done, k) && i < rdl(H, k)) v[k] = st.pos[i];
+        }
+    }
+    uint32_t bound = 0;  // lane k: bound k (record index)
+#pragma unroll
+    for (uint32_t k = 0; k < 2 * kRun; ++k) {
+        if (k < nb) {
+            const uint32_t Lk = rdl(L, k);
+            const uint32_t b = rdl(done, k) ? Lk : finish_bound(st, Bracket{Lk, rdl(H, k), false}, rdl64(x, k), v[k]);
+            if (lane == k) bound = b;
+        }
+    }
+    for (uint32_t sj = 0; sj < n; ++sj) {
+        const uint32_t lo = rdl(bound, 2 * sj);
+        body(rdl(q, 2 * sj), lo, max(lo, rdl(bound, 2 * sj + 1)));
+    }
+}
+
+// one slice per wave (run == 1): fewer registers than run_slices, which
+// matters when a launch has too few slices to amortise setup over runs
+template <class Body>
+__device__ __forceinline__ void one_slice(const DStore &st, const QDev *__restrict__ qs,
+                                          const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t w, Body body) {
+    if (w >= nq) return;
+    const uint32_t q = qidx ? uniform(qidx[w]) : w;
+    const QDev &Q = qs[q];
+    uint32_t lo = Q.seg_lo, hi = Q.seg_lo;  // a <= POS <= b (:84-85)
+    if (!(Q.flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
+    body(q, lo, hi);
+}
+
+template <bool RUN, class Body>
+__device__ __forceinline__ void slices(const DStore &st, const QDev *__restrict__ qs,
+                                       const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run, uint32_t w,
+                                       Body body) {
+    if constexpr (RUN)
+        run_slices(st, qs, qidx, nq, run, w, body);
+    else
+        one_slice(st, qs, qidx, nq, w, body);
+}
+
+// ---------------------------------------------------------------- launches
+// wave index of this wave in a launch, XCD-aware (xcd_block)
+__device__ __forceinline__ uint32_t launch_wave() {
+    return uniform(xcd_block(blockIdx.x, gridDim.x) * kWavesPerBlock + (threadIdx.x >> 6));
+}
+
+template <int NACC, bool NONNEG, int MODE, bool RUN>
+__global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__restrict__ qs,
+                                                      const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run,
+                                                      const uint8_t *__restrict__ qbytes,
+                                                      const uint64_t *__restrict__ subsets, QRes *__restrict__ res,
+                                                      uint64_t *__restrict__ hits, uint64_t *__restrict__ samples_out) {
+    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi) {
+        scan_slice<NACC, NONNEG, MODE>(st, qs, qbytes, subsets, res, hits, samples_out, q, lo, hi);
+    });
+}
+
+// one specialisation per launch (a batch with a single sample-free group)
+template <bool NONNEG, bool RUN>
+__global__ __launch_bounds__(kBlock) void range_n_kernel(DStore st, const QDev *__restrict__ qs,
+                                                         const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run,
+                                                         QRes *__restrict__ res, uint64_t *__restrict__ hits) {
+    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi) {
+        range_n_slice<NONNEG, RangeHot>(st, qs, res, hits, q, lo, hi);
+    });
+}
+
+template <bool NONNEG, bool RUN>
+__global__ __launch_bounds__(kBlock) void range_n8_kernel(DStore st, const QDev *__restrict__ qs,
+                                                          const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run,
+                                                          QRes *__restrict__ res, uint64_t *__restrict__ hits) {
+    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi) {
+        range_n_slice<NONNEG, RangeHot8>(st, qs, res, hits, q, lo, hi);
+    });
+}
+
+template <bool NONNEG, bool RUN>
+__global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__restrict__ qs,
+                                                    const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run,
+                                                    QRes *__restrict__ res, uint64_t *__restrict__ hits) {
+    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi) {
+        vt_slice<NONNEG>(st, qs, res, hits, q, lo, hi);
+    });
+}
+
+// All sample-free groups of a batch in one launch: group g owns waves
+// [wave_begin[g], wave_begin[g+1]), rounded to whole workgroups so a block
+// runs one specialisation.  Longest-running groups come first in the grid, so
+// the short ones (point lookups) fill the others' tail instead of running
+// after it in a second launch.
+struct FusedGroups {
+    const uint32_t *idx[kFusedMax];
+    uint32_t n[kFusedMax];
+    uint32_t run[kFusedMax];
+    uint32_t wave_begin[kFusedMax + 1];
+    int mode[kFusedMax];
+    int count;
+};
+
+template <bool NONNEG, bool RUN>
+__global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, const QDev *__restrict__ qs, FusedGroups G,
+                                                       const uint8_t *__restrict__ qbytes,
+                                                       const uint64_t *__restrict__ subsets, QRes *__restrict__ res,
+                                                       uint64_t *__restrict__ hits) {
+    const uint32_t gw = launch_wave();
+    int g = 0;
+    while (g + 1 < G.count && gw >= G.wave_begin[g + 1]) ++g;
+    const uint32_t w = gw - G.wave_begin[g];
+    const int mode = G.mode[g];
+    slices<RUN>(st, qs, G.idx[g], G.n[g], G.run[g], w, [&](uint32_t q, uint32_t lo, uint32_t hi) {
+        switch (mode) {
+            case MODE_RANGE_N: range_n_slice<NONNEG, RangeHot>(st, qs, res, hits, q, lo, hi); break;
+            case MODE_RANGE_N8: range_n_slice<NONNEG, RangeHot8>(st, qs, res, hits, q, lo, hi); break;
+            case MODE_VTYPE: vt_slice<NONNEG>(st, qs, res, hits, q, lo, hi); break;
+            case MODE_EXACT:
+                scan_slice<0, NONNEG, MODE_EXACT>(st, qs, qbytes, subsets, res, hits, nullptr, q, lo, hi);
+                break;
+            default:
+                scan_slice<0, NONNEG, MODE_GENERAL>(st, qs, qbytes, subsets, res, hits, nullptr, q, lo, hi);
+                break;
+        }
+    });
+}
+
 __global__ __launch_bounds__(kBlock) void compact_kernel(const QDev *__restrict__ qs,
                                                          const uint64_t *__restrict__ dense_off,
                                                          const QRes *__restrict__ res, uint32_t nq,
@@ -749,7 +988,11 @@ __global__ __launch_bounds__(kBlock) void request_reduce_kernel(const QRes *__re
     out[w] = P;
 }
 
-inline uint32_t blocks_for(uint32_t nq) { return (nq + kWavesPerBlock - 1) / kWavesPerBlock; }
+inline uint32_t blocks_for(uint32_t nwaves) { return (nwaves + kWavesPerBlock - 1) / kWavesPerBlock; }
+// slices per wave for a launch of nq slices: up to kRun while the launch
+// still has >= 4 waves per slot of a full chip (256 CUs x 4 SIMDs x 8)
+inline uint32_t run_for(uint32_t nq) { return std::max(1u, std::min(kRun, nq / 32768u)); }
+inline uint32_t run_waves(uint32_t nq, uint32_t run) { return (nq + run - 1) / run; }
 
 // ------------------------------------------------------------ summariseSlice
 // lambda/summariseSlice/source/main.cpp:195-245.  The reader visits the first
@@ -949,19 +1192,11 @@ void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, u
 
 template <bool NONNEG>
 void launch_variant(int nacc, int mode, dim3 g, const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t n,
+                    uint32_t run,
                     const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out,
                     hipStream_t s) {
     const dim3 b(kBlock);
-    if (nacc == 0 && mode == MODE_RANGE_N) {
-        hipLaunchKernelGGL((range_n_kernel<NONNEG>), g, b, 0, s, st, q, qidx, n, res, hits);
-        return;
-    }
-    if (nacc == 0 && mode == MODE_VTYPE) {
-        hipLaunchKernelGGL((vt_kernel<NONNEG>), g, b, 0, s, st, q, qidx, n, res, hits);
-        return;
-    }
-#define SB_SCAN(NA, MO) hipLaunchKernelGGL((scan_kernel<NA, NONNEG, MO>), g, b, 0, s, st, q, qidx, n, qbytes, subsets, res, hits, samples_out)
-    if (nacc == 0 && mode == MODE_EXACT) { SB_SCAN(0, MODE_EXACT); return; }
+#define SB_SCAN(NA, MO) hipLaunchKernelGGL((scan_kernel<NA, NONNEG, MO, false>), g, b, 0, s, st, q, qidx, n, run, qbytes, subsets, res, hits, samples_out)
     switch (nacc) {
         case 0: SB_SCAN(0, MODE_GENERAL); break;
         case 1: SB_SCAN(1, MODE_GENERAL); break;
@@ -976,11 +1211,75 @@ void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t
                  uint64_t *samples_out, hipStream_t s) {
     if (!n) return;
     const int nacc = max_words == 0 ? 0 : max_words <= 64 ? 1 : max_words <= 256 ? 4 : 16;
+    if (nacc == 0) {  // every sample-free specialisation goes through the fused kernel
+        const FusedGroup one{qidx, n, mode};
+        launch_fused(st, q, &one, 1, nonneg, qbytes, subsets, res, hits, s);
+        return;
+    }
+    const uint32_t run = 1;  // the sample path keeps one slice per wave
     const dim3 g(blocks_for(n));
     if (nonneg)
-        launch_variant<true>(nacc, mode, g, st, q, qidx, n, qbytes, subsets, res, hits, samples_out, s);
+        launch_variant<true>(nacc, mode, g, st, q, qidx, n, run, qbytes, subsets, res, hits, samples_out, s);
     else
-        launch_variant<false>(nacc, mode, g, st, q, qidx, n, qbytes, subsets, res, hits, samples_out, s);
+        launch_variant<false>(nacc, mode, g, st, q, qidx, n, run, qbytes, subsets, res, hits, samples_out, s);
+}
+
+void launch_fused(const DStore &st, const QDev *q, const FusedGroup *groups, int count, bool nonneg,
+                  const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, hipStream_t s) {
+    FusedGroups G{};
+    uint32_t waves = 0;
+    int c = 0;
+    for (int i = 0; i < count; ++i) {
+        if (!groups[i].n) continue;
+        if (c == kFusedMax) throw std::runtime_error("launch_fused: too many groups");
+        G.idx[c] = groups[i].qidx;
+        G.n[c] = groups[i].n;
+        G.mode[c] = groups[i].mode;
+        G.run[c] = run_for(groups[i].n);
+        ++c;
+    }
+    // slice runs only when some group is large enough to use them (run_slices
+    // costs registers); otherwise every group runs one slice per wave
+    bool run = false;
+    for (int i = 0; i < c; ++i) run = run || G.run[i] > 1;
+    for (int i = 0; i < c; ++i) {
+        G.wave_begin[i] = waves;
+        waves += blocks_for(run_waves(G.n[i], G.run[i])) * kWavesPerBlock;
+    }
+    if (!c) return;
+    G.count = c;
+    G.wave_begin[c] = waves;
+    const dim3 g(waves / kWavesPerBlock), b(kBlock);
+    if (c == 1) {  // a single group: its own specialisation (smaller code, no group dispatch)
+        const uint32_t *qi = G.idx[0];
+        const uint32_t n = G.n[0], rn = G.run[0];
+#define SB_ONE(NN, RR)                                                                                         \
+        switch (G.mode[0]) {                                                                                   \
+            case MODE_RANGE_N: hipLaunchKernelGGL((range_n_kernel<NN, RR>), g, b, 0, s, st, q, qi, n, rn, res, hits); break; \
+            case MODE_RANGE_N8: hipLaunchKernelGGL((range_n8_kernel<NN, RR>), g, b, 0, s, st, q, qi, n, rn, res, hits); break; \
+            case MODE_VTYPE: hipLaunchKernelGGL((vt_kernel<NN, RR>), g, b, 0, s, st, q, qi, n, rn, res, hits); break;        \
+            case MODE_EXACT:                                                                                   \
+                hipLaunchKernelGGL((scan_kernel<0, NN, MODE_EXACT, RR>), g, b, 0, s, st, q, qi, n, rn, qbytes, subsets, res, hits, nullptr); \
+                break;                                                                                         \
+            default:                                                                                           \
+                hipLaunchKernelGGL((scan_kernel<0, NN, MODE_GENERAL, RR>), g, b, 0, s, st, q, qi, n, rn, qbytes, subsets, res, hits, nullptr); \
+                break;                                                                                         \
+        }
+        if (nonneg) {
+            if (run) { SB_ONE(true, true) } else { SB_ONE(true, false) }
+        } else {
+            if (run) { SB_ONE(false, true) } else { SB_ONE(false, false) }
+        }
+#undef SB_ONE
+        return;
+    }
+    if (nonneg) {
+        if (run) hipLaunchKernelGGL((fused_kernel<true, true>), g, b, 0, s, st, q, G, qbytes, subsets, res, hits);
+        else hipLaunchKernelGGL((fused_kernel<true, false>), g, b, 0, s, st, q, G, qbytes, subsets, res, hits);
+    } else {
+        if (run) hipLaunchKernelGGL((fused_kernel<false, true>), g, b, 0, s, st, q, G, qbytes, subsets, res, hits);
+        else hipLaunchKernelGGL((fused_kernel<false, false>), g, b, 0, s, st, q, G, qbytes, subsets, res, hits);
+    }
 }
 
 }  // namespace sb

@@ -80,6 +80,9 @@ struct VcfData {
     uint64_t plane0_base = 0, planex_base = 0;
     bool nonneg = true;
     bool has_planes = false;
+    // RangeHot8 usable (>= 98 % of the single-base-ALT records fit it), AN value
+    bool range8 = false;
+    int32_t an_default = 0;
 };
 
 struct Dict {

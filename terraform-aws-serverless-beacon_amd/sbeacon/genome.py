@@ -299,3 +299,26 @@ def prepare_shard_batch(store, sl: ShardSlices):
     batch = Batch(h, None, store)
     batch.set_owners(sl.req, sl.n_rows)
     return batch
+
+
+def union_rows(shape: GenomeShape, sl: ShardSlices) -> int:
+    """Records inside the union of the slices' [a, b] windows (each record
+    counted once however many slices scan it): the unique rows a step must
+    bring in from HBM at least once."""
+    total = 0
+    for ci in np.unique(sl.ci):
+        m = sl.ci == ci
+        a, b = sl.a[m].astype(np.int64), sl.b[m].astype(np.int64)
+        o = np.argsort(a, kind='stable')
+        a, b = a[o], b[o]
+        # merge overlapping windows
+        reach = np.maximum.accumulate(b)
+        start = np.ones(len(a), dtype=bool)
+        start[1:] = a[1:] > reach[:-1] + 1
+        ids = np.cumsum(start) - 1
+        ua = a[start]
+        ub = np.zeros(len(ua), dtype=np.int64)
+        np.maximum.at(ub, ids, b)
+        pos = shape.gen(int(ci)).positions().astype(np.int64)
+        total += int((np.searchsorted(pos, ub, side='right') - np.searchsorted(pos, ua, side='left')).sum())
+    return total

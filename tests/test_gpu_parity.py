@@ -135,3 +135,26 @@ def test_handlers_through_registry():
     r = perform_query.lambda_handler(ev, None)
     assert r['exists'] and r['call_count'] > 0 and r['variants']
     engine.registry.clear()
+
+
+@pytest.mark.parametrize('no_range8', ['0', '1'])
+def test_range_words_vs_oracle(tmp_path, monkeypatch, no_range8):
+    """ref=alt='N' range requests over a 1000G-shape VCF (one AN at every
+    site): RangeHot8 words by default, RangeHot with SBEACON_NO_RANGE8=1;
+    both must match the oracle.  Boolean / count granularities exercise the
+    early exits, record granularity the hit lists."""
+    from oracle.oracle import OracleVcf
+    from sbeacon.engine import Store
+    from sbeacon.workload import SyntheticVcf, config2_requests, requests_to_payloads
+    monkeypatch.setenv('SBEACON_NO_RANGE8', no_range8)
+    gen = SyntheticVcf(seed=31, n_records=40000, n_samples=8, mean_gap=60.0)
+    path = str(tmp_path / 'shape.vcf')
+    gen.write(path, sites_only=False)
+    store = Store.build([('s.vcf', path)], device=0)
+    reqs = config2_requests(gen, n_range=300, n_point=0, seed=77)
+    payloads, _ = requests_to_payloads(reqs, vcf_location='s.vcf', chrom='22')
+    rng = random.Random(5)
+    for p in payloads:
+        p['requested_granularity'] = rng.choice(['record', 'record', 'count', 'boolean'])
+        p['include_details'] = p['requested_granularity'] == 'record' or rng.random() < 0.3
+    _vs_oracle(store, OracleVcf(path), payloads)
