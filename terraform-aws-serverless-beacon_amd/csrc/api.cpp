@@ -392,6 +392,34 @@ void upload_store(sb_builder &b, sb_store &s) {
         }
         s.d.vth = dev_upload(s, vth);
         s.d.xvt = dev_upload(s, xvt);
+        // per-kind candidate lists + block tables (VcBlock)
+        const size_t n = vth.size(), nblk = n / 64 + 1;
+        std::vector<VcBlock> blk(kVtKinds * nblk, VcBlock{0, 0, 0});
+        std::vector<VtHot> cw;
+        std::vector<uint32_t> ci;
+        constexpr uint32_t kXk[kVtKinds] = {VT_XK_DEL, VT_XK_INS, VT_XK_DUP, VT_XK_DUPT, VT_XK_CNV, 0u};
+        for (uint32_t k = 0; k < kVtKinds; ++k) {
+            const uint32_t cm = vt_class_mask(k), xk = kXk[k] | VT_XK_SYM;
+            for (size_t i = 0; i < n; ++i) {
+                VcBlock &b = blk[k * nblk + i / 64];
+                if (i % 64 == 0) b.pre = static_cast<uint32_t>(cw.size());
+                const uint32_t w = vth[i].w;
+                const bool cand = (w & (VT_SLOW | VT_SYM | xk)) ||
+                                  ((cm >> ((w >> VT_CLASS_SHIFT) & 31u)) & 1u);
+                if (!cand) continue;
+                b.mask |= 1ull << (i % 64);
+                cw.push_back(vth[i]);
+                ci.push_back(static_cast<uint32_t>(i));
+            }
+            if (n % 64 == 0) blk[k * nblk + n / 64].pre = static_cast<uint32_t>(cw.size());
+        }
+        if (cw.size() > 0xffffffffull) throw Error(SB_EINVAL, "variantType candidate index exceeds 2^32 entries");
+        cw.push_back(VtHot{0, 0, 0, 0});  // clamp target of an empty candidate range
+        ci.push_back(0);
+        s.d.vc_word = dev_upload(s, cw);
+        s.d.vc_idx = dev_upload(s, ci);
+        s.d.vc_blk = dev_upload(s, blk);
+        s.d.vc_nblk = nblk;
     }
     s.d.pos = dev_upload(s, pos);
     s.d.ref_key = dev_upload(s, ref_key);

@@ -102,6 +102,21 @@ enum : uint32_t {
     VT_NX_SHIFT = 29,
     VT_MAX_NX = 7,
 };
+// Candidate index of MODE_VTYPE (built at upload): for each variantType kind
+// k in 0..5 (VT_DEL .. VT_OTHER) the records that could satisfy it for some
+// length bounds / END window -- ALT0 of an accepted class, a symbolic ALT0,
+// an extra ALT that might (VT_XK_*), or VT_SLOW -- in record order, with
+// their VtHot words copied alongside (vc_word / vc_idx, kind k at
+// vc_off[k]).  Every other record can neither hit nor raise for that kind,
+// so a slice scans only its candidates: [lo, hi) maps to candidate positions
+// through a per-64-record block table (prefix count + bitmask).  In a
+// 1000G-shape store a kind has a few % of the records as candidates.
+constexpr int kVtKinds = 6;
+struct alignas(16) VcBlock {
+    uint64_t mask;  // bit i: record 64 b + i is a candidate
+    uint32_t pre;   // candidates of this kind before record 64 b (+ vc_off[k])
+    uint32_t pad;
+};
 // bit c set = an ALT of class c satisfies variantType `kind` (vtype_hit)
 __host__ __device__ constexpr uint32_t vt_class_mask(uint32_t kind) {
     uint32_t m = 0;
@@ -172,6 +187,10 @@ struct DStore {
     const RangeHot8 *rng8;    // MODE_RANGE_N8 view (VCFs with a common AN)
     const VtHot *vth;         // MODE_VTYPE view of the same records
     const uint32_t *xvt;      // MODE_VTYPE word of each extra row
+    const VtHot *vc_word;     // MODE_VTYPE candidates (see VcBlock)
+    const uint32_t *vc_idx;
+    const VcBlock *vc_blk;    // [kVtKinds][vc_nblk]
+    uint64_t vc_nblk;
     const uint32_t *pos;
     const uint64_t *ref_key;  // key(REF.upper())
     const uint64_t *a0_key;   // key(ALT0.upper())

@@ -19,6 +19,7 @@
 // bandwidth on the RecHot stream.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <stdexcept>
 
 #include "../../include/sbeacon.h"
@@ -676,10 +677,23 @@ __device__ __forceinline__ void range_n_slice(DStore st, const QDev *__restrict_
 // missing AC entries, > 8 ALTs, lengths or symbolic ids >= 255) go to a
 // one-chunk-at-a-time tail loop with eval_record.  The record stream is a
 // stream_window of kVtWindow chunks.
+// candidate word + its record index (MODE_VTYPE stream element)
+struct VcWord {
+    VtHot h;
+    uint32_t r;
+};
+
+// candidates of variantType kind k among records [0, r): the VcBlock table
+__device__ __forceinline__ uint32_t vc_count(const DStore &st, uint32_t k, uint32_t r) {
+    const VcBlock b = st.vc_blk[k * st.vc_nblk + (r >> 6)];
+    const uint32_t o = r & 63u;
+    return b.pre + static_cast<uint32_t>(__popcll(o ? (b.mask & ((1ull << o) - 1ull)) : 0ull));
+}
+
 template <bool NONNEG>
-__device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
-                                                    
-                                                    QRes *__restrict__ res, uint64_t *__restrict__ hits, uint32_t q, uint32_t lo, uint32_t hi) {
+__device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs, QRes *__restrict__ res,
+                                         uint64_t *__restrict__ hits, uint32_t q, uint32_t lo, uint32_t hi,
+                                         uint32_t c_lo, uint32_t c_hi_all) {
     const int lane = lane_id();
     const QDev &Q = qs[q];
     const uint32_t flags = Q.flags;
@@ -747,30 +761,35 @@ __device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
         }
         return o;
     };
-    auto fast_chunk = [&](uint32_t base, const VtHot h) -> int {  // 0 go on, 1 stop, 2 has VT_SLOW lanes
-        const uint32_t r = base + ul;
-        const bool cand = r < shi && h.end - e0 <= espan;
-        if (__ballot(cand && (h.w & VT_SLOW))) return 2;
-        const LaneOut o = lane_eval(h, r, cand);
+    // the slice's candidates of this variantType (VcBlock): positions [c_lo, c_hi),
+    // mapped from [lo, hi) by the slice driver (VcAux); none if no END can match
+    const uint32_t c_hi = shi > lo ? c_hi_all : c_lo;
+    auto fast_chunk = [&](uint32_t base, const VcWord x) -> int {  // 0 go on, 1 stop, 2 has VT_SLOW lanes
+        const bool cand = base + ul < c_hi && x.h.end - e0 <= espan;
+        if (__ballot(cand && (x.h.w & VT_SLOW))) return 2;
+        const LaneOut o = lane_eval(x.h, x.r, cand);
         uint64_t cm;
-        return chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) >= kWave ? 0 : 1;
+        return chunk_tail<NONNEG>(S, o, x.r, stop_on_exists, details, out, &cm) >= kWave ? 0 : 1;
     };
-    // clamped, unconditional (used only when lo < shi); lanes past shi fail `cand`
-    auto ld = [&](uint32_t i) -> VtHot { return st.vth[min(i, shi - 1)]; };
-    uint32_t base = lo;
-    const int status = lo < shi ? stream_window<kVtWindow, VtHot>(lo, shi, &base, ld, fast_chunk) : 0;
-    if (status == 2) {  // the rest of the slice one chunk at a time, eval_record for VT_SLOW lanes
-        VtHot h = ld(base + ul);
-        for (; base < shi; base += kWave) {
-            const uint32_t r = base + ul;
-            const VtHot nh = ld(r + kWave);
-            const bool cand = r < shi && h.end - e0 <= espan;
-            const bool slow = cand && (h.w & VT_SLOW);
-            LaneOut o = lane_eval(h, r, cand && !slow);
+    // clamped, unconditional (used only when c_lo < c_hi); lanes past c_hi fail `cand`
+    auto ld = [&](uint32_t i) -> VcWord {
+        const uint32_t j = min(i, c_hi - 1);
+        return VcWord{st.vc_word[j], st.vc_idx[j]};
+    };
+    uint32_t base = c_lo;
+    const int status = c_lo < c_hi ? stream_window<kVtWindow, VcWord>(c_lo, c_hi, &base, ld, fast_chunk) : 0;
+    if (status == 2) {  // the rest of the candidates one chunk at a time, eval_record for VT_SLOW lanes
+        VcWord x = ld(base + ul);
+        for (; base < c_hi; base += kWave) {
+            const VcWord nx = ld(base + ul + kWave);
+            const uint32_t r = x.r;
+            const bool cand = base + ul < c_hi && x.h.end - e0 <= espan;
+            const bool slow = cand && (x.h.w & VT_SLOW);
+            LaneOut o = lane_eval(x.h, r, cand && !slow);
             if (__ballot(slow) && slow) o = eval_record(st, Q, V, r, st.rec[r]);
             uint64_t cm;
             if (chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm) < kWave) break;
-            h = nh;
+            x = nx;
         }
     }
     finish_query<NONNEG>(S, q, hi - lo, res);
@@ -790,10 +809,10 @@ __device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
 // paid once per run.  Bounds are those of slice_bounds.
 constexpr uint32_t kRun = 8;
 
-template <class Body>
+template <class Body, class Aux>
 __device__ __forceinline__ void run_slices(const DStore &st, const QDev *__restrict__ qs,
                                            const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run, uint32_t w,
-                                           Body body) {
+                                           Body body, Aux aux) {
     const uint32_t first = w * run;
     if (first >= nq) return;
     const uint32_t n = min(run, nq - first);
@@ -834,34 +853,53 @@ __device__ __forceinline__ void run_slices(const DStore &st, const QDev *__restr
             if (lane == k) bound = b;
         }
     }
+    // a per-bound companion value (aux(Q, bound), e.g. a candidate-list
+    // position), computed by all bound lanes at once
+    const uint32_t other = __shfl(bound, static_cast<int>(lane ^ 1u), kWave);  // the slice's other bound
+    uint32_t abound = 0;
+    if (lane < nb) abound = aux(qs[q], upper ? max(bound, other) : bound);
     for (uint32_t sj = 0; sj < n; ++sj) {
         const uint32_t lo = rdl(bound, 2 * sj);
-        body(rdl(q, 2 * sj), lo, max(lo, rdl(bound, 2 * sj + 1)));
+        body(rdl(q, 2 * sj), lo, max(lo, rdl(bound, 2 * sj + 1)), rdl(abound, 2 * sj), rdl(abound, 2 * sj + 1));
     }
 }
 
 // one slice per wave (run == 1): fewer registers than run_slices, which
 // matters when a launch has too few slices to amortise setup over runs
-template <class Body>
+template <class Body, class Aux>
 __device__ __forceinline__ void one_slice(const DStore &st, const QDev *__restrict__ qs,
-                                          const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t w, Body body) {
+                                          const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t w, Body body,
+                                          Aux aux) {
     if (w >= nq) return;
     const uint32_t q = qidx ? uniform(qidx[w]) : w;
     const QDev &Q = qs[q];
     uint32_t lo = Q.seg_lo, hi = Q.seg_lo;  // a <= POS <= b (:84-85)
     if (!(Q.flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
-    body(q, lo, hi);
+    body(q, lo, hi, aux(Q, lo), aux(Q, hi));
 }
 
-template <bool RUN, class Body>
+// no companion value
+struct NoAux {
+    __device__ __forceinline__ uint32_t operator()(const QDev &, uint32_t) const { return 0; }
+};
+
+template <bool RUN, class Body, class Aux = NoAux>
 __device__ __forceinline__ void slices(const DStore &st, const QDev *__restrict__ qs,
                                        const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run, uint32_t w,
-                                       Body body) {
+                                       Body body, Aux aux = Aux()) {
     if constexpr (RUN)
-        run_slices(st, qs, qidx, nq, run, w, body);
+        run_slices(st, qs, qidx, nq, run, w, body, aux);
     else
-        one_slice(st, qs, qidx, nq, w, body);
+        one_slice(st, qs, qidx, nq, w, body, aux);
 }
+
+// MODE_VTYPE companion: a bound's position in the slice kind's candidate list
+struct VcAux {
+    const DStore *st;
+    __device__ __forceinline__ uint32_t operator()(const QDev &Q, uint32_t r) const {
+        return vc_count(*st, Q.vt_kind, r);
+    }
+};
 
 // ---------------------------------------------------------------- launches
 // wave index of this wave in a launch, XCD-aware (xcd_block)
@@ -875,7 +913,7 @@ __global__ __launch_bounds__(kBlock) void scan_kernel(DStore st, const QDev *__r
                                                       const uint8_t *__restrict__ qbytes,
                                                       const uint64_t *__restrict__ subsets, QRes *__restrict__ res,
                                                       uint64_t *__restrict__ hits, uint64_t *__restrict__ samples_out) {
-    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi) {
+    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi, uint32_t alo, uint32_t ahi) {
         scan_slice<NACC, NONNEG, MODE>(st, qs, qbytes, subsets, res, hits, samples_out, q, lo, hi);
     });
 }
@@ -885,7 +923,7 @@ template <bool NONNEG, bool RUN>
 __global__ __launch_bounds__(kBlock) void range_n_kernel(DStore st, const QDev *__restrict__ qs,
                                                          const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run,
                                                          QRes *__restrict__ res, uint64_t *__restrict__ hits) {
-    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi) {
+    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi, uint32_t alo, uint32_t ahi) {
         range_n_slice<NONNEG, RangeHot>(st, qs, res, hits, q, lo, hi);
     });
 }
@@ -894,7 +932,7 @@ template <bool NONNEG, bool RUN>
 __global__ __launch_bounds__(kBlock) void range_n8_kernel(DStore st, const QDev *__restrict__ qs,
                                                           const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run,
                                                           QRes *__restrict__ res, uint64_t *__restrict__ hits) {
-    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi) {
+    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi, uint32_t alo, uint32_t ahi) {
         range_n_slice<NONNEG, RangeHot8>(st, qs, res, hits, q, lo, hi);
     });
 }
@@ -903,9 +941,9 @@ template <bool NONNEG, bool RUN>
 __global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__restrict__ qs,
                                                     const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run,
                                                     QRes *__restrict__ res, uint64_t *__restrict__ hits) {
-    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi) {
-        vt_slice<NONNEG>(st, qs, res, hits, q, lo, hi);
-    });
+    slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi, uint32_t alo, uint32_t ahi) {
+        vt_slice<NONNEG>(st, qs, res, hits, q, lo, hi, alo, ahi);
+    }, VcAux{&st});
 }
 
 // All sample-free groups of a batch in one launch: group g owns waves
@@ -932,11 +970,14 @@ __global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, const QDev *__
     while (g + 1 < G.count && gw >= G.wave_begin[g + 1]) ++g;
     const uint32_t w = gw - G.wave_begin[g];
     const int mode = G.mode[g];
-    slices<RUN>(st, qs, G.idx[g], G.n[g], G.run[g], w, [&](uint32_t q, uint32_t lo, uint32_t hi) {
+    const auto aux = [&](const QDev &Q, uint32_t r) -> uint32_t {
+        return mode == MODE_VTYPE ? vc_count(st, Q.vt_kind, r) : 0u;
+    };
+    slices<RUN>(st, qs, G.idx[g], G.n[g], G.run[g], w, [&](uint32_t q, uint32_t lo, uint32_t hi, uint32_t alo, uint32_t ahi) {
         switch (mode) {
             case MODE_RANGE_N: range_n_slice<NONNEG, RangeHot>(st, qs, res, hits, q, lo, hi); break;
             case MODE_RANGE_N8: range_n_slice<NONNEG, RangeHot8>(st, qs, res, hits, q, lo, hi); break;
-            case MODE_VTYPE: vt_slice<NONNEG>(st, qs, res, hits, q, lo, hi); break;
+            case MODE_VTYPE: vt_slice<NONNEG>(st, qs, res, hits, q, lo, hi, alo, ahi); break;
             case MODE_EXACT:
                 scan_slice<0, NONNEG, MODE_EXACT>(st, qs, qbytes, subsets, res, hits, nullptr, q, lo, hi);
                 break;
@@ -944,7 +985,7 @@ __global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, const QDev *__
                 scan_slice<0, NONNEG, MODE_GENERAL>(st, qs, qbytes, subsets, res, hits, nullptr, q, lo, hi);
                 break;
         }
-    });
+    }, aux);
 }
 
 __global__ __launch_bounds__(kBlock) void compact_kernel(const QDev *__restrict__ qs,
@@ -991,7 +1032,14 @@ __global__ __launch_bounds__(kBlock) void request_reduce_kernel(const QRes *__re
 inline uint32_t blocks_for(uint32_t nwaves) { return (nwaves + kWavesPerBlock - 1) / kWavesPerBlock; }
 // slices per wave for a launch of nq slices: up to kRun while the launch
 // still has >= 4 waves per slot of a full chip (256 CUs x 4 SIMDs x 8)
-inline uint32_t run_for(uint32_t nq) { return std::max(1u, std::min(kRun, nq / 32768u)); }
+// (SBEACON_SLICES_PER_WAVE=k forces k, 1..kRun: tests drive run_slices with small batches)
+inline uint32_t run_for(uint32_t nq) {
+    if (const char *e = std::getenv("SBEACON_SLICES_PER_WAVE")) {
+        const long k = std::strtol(e, nullptr, 10);
+        if (k >= 1) return std::min<uint32_t>(kRun, static_cast<uint32_t>(k));
+    }
+    return std::max(1u, std::min(kRun, nq / 32768u));
+}
 inline uint32_t run_waves(uint32_t nq, uint32_t run) { return (nq + run - 1) / run; }
 
 // ------------------------------------------------------------ summariseSlice

@@ -32,7 +32,12 @@ def _rows(batch, n_rows):
     return out.cpu().numpy()[:n_rows]
 
 
-def test_shards_match_oracle_and_unsharded(genome):
+@pytest.mark.parametrize('spw', ['0', '8'])
+def test_shards_match_oracle_and_unsharded(genome, monkeypatch, spw):
+    """spw '8': slice runs (8 slices per wave, candidate positions mapped in
+    the run prologue) on a batch small enough to default to one per wave."""
+    if spw != '0':
+        monkeypatch.setenv('SBEACON_SLICES_PER_WAVE', spw)
     from oracle.oracle import OracleVcf
     from sbeacon.genome import prepare_shard_batch, shard_slices, slice_payloads
     from sbeacon.shard import combine_host, request_rows_from_responses

@@ -56,9 +56,14 @@ def _vs_oracle(store, orc, payloads):
             assert normalise(g.dump()) == normalise(e), p
 
 
-@pytest.mark.parametrize('seed,quirks,n_rec,n_samp', [(11, False, 20000, 40), (12, True, 6000, 70),
-                                                        (13, False, 3000, 130)])
-def test_random_vs_oracle(tmp_path, seed, quirks, n_rec, n_samp):
+@pytest.mark.parametrize('seed,quirks,n_rec,n_samp,spw', [(11, False, 20000, 40, '0'), (12, True, 6000, 70, '0'),
+                                                            (13, False, 3000, 130, '0'), (11, False, 20000, 40, '8'),
+                                                            (12, True, 6000, 70, '3')])
+def test_random_vs_oracle(tmp_path, monkeypatch, seed, quirks, n_rec, n_samp, spw):
+    """spw: slices per wave ('0' = the launch's own choice, one per wave for
+    batches this small; '8' / '3' = slice runs with lane-parallel bounds)."""
+    if spw != '0':
+        monkeypatch.setenv('SBEACON_SLICES_PER_WAVE', spw)
     from oracle.oracle import OracleVcf
     from sbeacon import synth
     from sbeacon.engine import Store
@@ -137,8 +142,8 @@ def test_handlers_through_registry():
     engine.registry.clear()
 
 
-@pytest.mark.parametrize('no_range8', ['0', '1'])
-def test_range_words_vs_oracle(tmp_path, monkeypatch, no_range8):
+@pytest.mark.parametrize('no_range8,spw', [('0', '0'), ('1', '0'), ('0', '8')])
+def test_range_words_vs_oracle(tmp_path, monkeypatch, no_range8, spw):
     """ref=alt='N' range requests over a 1000G-shape VCF (one AN at every
     site): RangeHot8 words by default, RangeHot with SBEACON_NO_RANGE8=1;
     both must match the oracle.  Boolean / count granularities exercise the
@@ -147,6 +152,8 @@ def test_range_words_vs_oracle(tmp_path, monkeypatch, no_range8):
     from sbeacon.engine import Store
     from sbeacon.workload import SyntheticVcf, config2_requests, requests_to_payloads
     monkeypatch.setenv('SBEACON_NO_RANGE8', no_range8)
+    if spw != '0':
+        monkeypatch.setenv('SBEACON_SLICES_PER_WAVE', spw)
     gen = SyntheticVcf(seed=31, n_records=40000, n_samples=8, mean_gap=60.0)
     path = str(tmp_path / 'shape.vcf')
     gen.write(path, sites_only=False)
