@@ -78,16 +78,6 @@ __device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v) {
     return v;
 }
 
-__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
-    const int lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const uint32_t t = __shfl_up(v, d, kWave);
-        if (lane >= d) v += t;
-    }
-    return v;
-}
-
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += shfl_i64(v, lane_id() ^ d);
@@ -409,10 +399,15 @@ __device__ __forceinline__ int chunk_tail(ScanState &S, const LaneOut &o, uint32
         const uint64_t one = __ballot(cnt == 1);
         pos0 = popc_below(one);
         total = static_cast<uint32_t>(__popcll(one));
-    } else {
-        const uint32_t incl = wave_incl_scan_u32(cnt);
-        pos0 = incl - cnt;
-        total = __shfl(incl, kWave - 1, kWave);
+    } else {  // bit-sliced exclusive prefix of cnt: one ballot + mbcnt per bit, no LDS traffic
+        pos0 = 0;
+        total = 0;
+        for (uint32_t b = 0; b < 7; ++b) {
+            const uint64_t m = __ballot((cnt >> b) & 1u);
+            pos0 += popc_below(m) << b;
+            total += static_cast<uint32_t>(__popcll(m)) << b;
+            if (!__ballot(cnt >> (b + 1))) break;
+        }
     }
     if (cnt) {
         uint64_t *dst = out + S.n_out + pos0;
