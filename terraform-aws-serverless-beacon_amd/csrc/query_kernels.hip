@@ -78,10 +78,29 @@ __device__ __forceinline__ int64_t wave_incl_scan_i64(int64_t v) {
     return v;
 }
 
+// v of lane (DPP pattern CTRL); lanes the row / bank masks or the row edge
+// exclude read 0
+template <int CTRL, int ROW, int BANK>
+__device__ __forceinline__ int64_t dpp_i64(int64_t v) {
+    const uint64_t u = static_cast<uint64_t>(v);
+    const uint32_t lo = static_cast<uint32_t>(
+        __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(u)), CTRL, ROW, BANK, false));
+    const uint32_t hi = static_cast<uint32_t>(
+        __builtin_amdgcn_update_dpp(0, static_cast<int>(static_cast<uint32_t>(u >> 32)), CTRL, ROW, BANK, false));
+    return static_cast<int64_t>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// sum over the wave, returned in every lane: DPP row reductions (quad_perm,
+// row_shr 4 / 8, row_bcast 15 / 31) into lane 63, then one readlane -- no
+// LDS round trips (ds_bpermute) on the per-slice path
 __device__ __forceinline__ int64_t wave_sum_i64(int64_t v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += shfl_i64(v, lane_id() ^ d);
-    return v;
+    v += dpp_i64<0xb1, 0xf, 0xf>(v);   // quad_perm [1,0,3,2]
+    v += dpp_i64<0x4e, 0xf, 0xf>(v);   // quad_perm [2,3,0,1]: quad sums
+    v += dpp_i64<0x114, 0xf, 0xe>(v);  // row_shr:4 into banks 1..3
+    v += dpp_i64<0x118, 0xf, 0xc>(v);  // row_shr:8 into banks 2..3: lane 15 of a row = row sum
+    v += dpp_i64<0x142, 0xa, 0xf>(v);  // row_bcast:15 into rows 1, 3
+    v += dpp_i64<0x143, 0xc, 0xf>(v);  // row_bcast:31 into rows 2, 3: lane 63 = total
+    return rdl64(v, 63);
 }
 
 // number of lanes strictly below this one whose bit is set in m
