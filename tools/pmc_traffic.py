@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Fold two rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE) of a short
 bench.py run into profiles/traffic.json: HBM-side bytes per step of the
-timed query phase (range_n_kernel + scan_kernel launches).
+timed query phase (the fused query launch: range_n + exact groups).
 
 Corrections (MI355X_MICROARCH.md, HBM section): FETCH_SIZE/WRITE_SIZE are
 reported in KiB; on gfx950 FETCH_SIZE counts half the bytes of a wide
@@ -20,7 +20,7 @@ import os
 import re
 import sys
 
-PHASE = re.compile(r'(range_n_kernel|scan_kernel)')
+PHASE = re.compile(r'(fused_kernel|range_n8?_kernel|vt_kernel|scan_kernel)')
 
 
 def load(d, counter):
@@ -68,7 +68,7 @@ def main():
     out = {
         'records': a.records,
         'requests': a.requests,
-        'phase': 'query step = one launch of each kernel below (range_n_kernel + scan_kernel<EXACT>)',
+        'phase': 'query step = one launch of each kernel below (fused_kernel: range_n8 + exact groups)',
         'kernels': kernels,
         'scan_kernel_hbm_bytes_per_launch': step_bytes,
         'method': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, kernel trace only), '
