@@ -110,7 +110,7 @@ def main():
     elapsed = time.perf_counter() - t1
     if dist:
         dist.barrier()
-    timing = batch.timing()  # per-launch averages over the timed steps (HIP events)
+    timing = batch.timing()  # HIP events spanning the K back-to-back timed launches, / K
     rs = batch.fetch()
     st = rs.stats()
     n_req, n_slice = len(reqs), len(payloads)
@@ -168,7 +168,7 @@ def main():
         'device_ms_per_step': {'scan_kernel': round(timing['scan_ms'], 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                     'kernel': 'query step: fused_kernel (range_n + exact groups in one launch; HIP events around it)',
+                     'kernel': 'query step: fused_kernel (range_n + exact groups in one launch); HIP events spanning the K timed launches / K',
                      'algorithmic_bytes_per_launch': scan_bytes},
         'cpu_baseline': cpu,
         'parity_sample': parity,

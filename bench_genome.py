@@ -133,7 +133,7 @@ def main_genome(args):
                                'query_kernels_max': round(max(v[1] for v in allv), 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(allv[0][5], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(allv[0][5] / HBM_PEAK_GBS, 4), 'traffic': None,
-                     'kernel': 'rank 0 query step: vt_kernel launch (the batch is one variantType group), HIP events',
+                     'kernel': 'rank 0 query step: vt_kernel (the batch is one variantType group) + request_reduce_kernel; HIP events spanning the step',
                      'algorithmic_bytes_per_launch': 32.0 * allv[0][6] + 8.0 * allv[0][4],
                      'unique_rows_per_launch': int(allv[0][6]),
                      'rows_scanned_per_launch': int(allv[0][3]),

@@ -256,9 +256,12 @@ typedef struct sb_batch sb_batch;
 int sb_batch_prepare(sb_store *s, const sb_query *q, size_t nq, sb_batch **out);
 int sb_batch_run(sb_batch *b);               /* enqueue only (async) */
 int sb_batch_sync(sb_batch *b);              /* wait for the store stream */
-/* average per-launch device times (ms) over every sb_batch_run since the
- * previous sync, measured with hipEvents on the launch stream: whole
- * sequence, bounds + capacity prefix sum, range-scan kernel */
+/* average device time (ms) per sb_batch_run since the previous sync: one
+ * hipEvent before the first of those runs and one at the sync, on the launch
+ * stream, divided by the run count (back-to-back runs, no marker between
+ * them; work enqueued on the store stream in between is included).
+ * total_ms = scan_ms = that time; bounds_ms = 0 (bounds are found inside the
+ * scan kernels) */
 int sb_batch_last_timing(const sb_batch *b, double *total_ms, double *scan_ms, double *bounds_ms);
 int sb_batch_get_stats(const sb_batch *b, sb_batch_stats *out);
 int sb_batch_fetch(sb_batch *b, sb_result_set **out); /* D2H + host views */
