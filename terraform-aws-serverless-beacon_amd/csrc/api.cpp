@@ -88,6 +88,13 @@ struct DevMem {  // RAII device allocation for batches (move-only)
         bytes = std::max<size_t>(n, 16);
         HIP_OK(hipMalloc(&p, bytes));
     }
+    // keep the allocation when it is large enough (per-store scratch reused
+    // across calls: hipMalloc / hipFree of ~1 GB per call cost more than the
+    // kernels)
+    void reserve(size_t n) {
+        if (p && bytes >= n) return;
+        alloc(n + n / 4);
+    }
     void release() {
         if (p) (void)hipFree(p);
         p = nullptr;
@@ -862,6 +869,11 @@ bool voff_to_stream(const VcfData &v, uint64_t voff, uint64_t *u) {
     return *u <= v.stream_len;
 }
 
+// summariseSlice scratch, kept per store (sb_store::summarise_ws)
+struct SumWs {
+    DevMem dsl, dbm, dres, dcs, dpart;
+};
+
 void summarise(sb_store &s, const sb_slice *sl, size_t n, sb_slice_stats *out, double *device_ms) {
     std::vector<SDev> hs(n);
     std::vector<uint32_t> chunk_slice;  // phase-A chunk -> slice
@@ -906,12 +918,15 @@ void summarise(sb_store &s, const sb_slice *sl, size_t n, sb_slice_stats *out, d
     }
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
-    DevMem dsl, dbm, dres, dcs, dpart;
-    dsl.alloc(n * sizeof(SDev));
-    dbm.alloc(words * 8);
-    dres.alloc(n * sizeof(SRes));
-    dcs.alloc(chunk_slice.size() * 4);
-    dpart.alloc(chunk_slice.size() * sizeof(SPart));
+    if (!s.summarise_ws)
+        s.summarise_ws = std::shared_ptr<void>(new SumWs, [](void *w) { delete static_cast<SumWs *>(w); });
+    SumWs &W = *static_cast<SumWs *>(s.summarise_ws.get());
+    DevMem &dsl = W.dsl, &dbm = W.dbm, &dres = W.dres, &dcs = W.dcs, &dpart = W.dpart;
+    dsl.reserve(n * sizeof(SDev));
+    dbm.reserve(words * 8);  // every word is written by the chunk kernel
+    dres.reserve(n * sizeof(SRes));
+    dcs.reserve(chunk_slice.size() * 4);
+    dpart.reserve(chunk_slice.size() * sizeof(SPart));
     if (n) HIP_OK(hipMemcpyAsync(dsl.p, hs.data(), n * sizeof(SDev), hipMemcpyHostToDevice, st));
     if (!chunk_slice.empty())
         HIP_OK(hipMemcpyAsync(dcs.p, chunk_slice.data(), chunk_slice.size() * 4, hipMemcpyHostToDevice, st));
@@ -1059,6 +1074,11 @@ std::string key_string(const sb_store &s, uint32_t k) {
     return out;
 }
 
+// dedup scratch, kept per store (sb_store::dedup_ws) and grown on demand
+struct DedupWs {
+    DevMem dseg, dtiles, tcnt, ke0, ke1, kh0, vh0, kh1, vh1, hist, bsum, counts, coll, ncoll, pe, ph;
+};
+
 void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, int32_t *status,
            sb_dedup_stats *stats) {
     if (nj > (1u << 20)) throw Error(SB_EINVAL, "more than 2^20 dedup jobs in one call");
@@ -1125,25 +1145,29 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
     const uint32_t ntiles = static_cast<uint32_t>(tiles.size());
     const uint64_t slots = static_cast<uint64_t>(ntiles) * gt;  // sparse gather layout
     const uint64_t maxt = std::max<uint64_t>(ntiles, (n + gt - 1) / gt);
-    DevMem dseg, dtiles, tcnt, ke0, ke1, kh0, vh0, kh1, vh1, hist, bsum, counts, coll, ncoll, pe, ph;
-    dseg.alloc(segs.size() * sizeof(KSeg));
-    dtiles.alloc(tiles.size() * sizeof(uint2));
-    tcnt.alloc(2 * static_cast<size_t>(ntiles) * 4);
-    ke0.alloc(slots * 8);
-    ke1.alloc(n * 8);
-    kh0.alloc(slots * 8);
-    vh0.alloc(slots * 4);
-    kh1.alloc(n * 8);
-    vh1.alloc(n * 4);
-    hist.alloc(maxt * 256 * 4);
-    bsum.alloc(radix_bsum_words(maxt * gt) * 4);
-    counts.alloc(std::max<size_t>(nj, 1) * 8);
-    coll.alloc(n * 4);
-    ncoll.alloc(4);
+    if (!s.dedup_ws) s.dedup_ws = std::shared_ptr<void>(new DedupWs, [](void *w) { delete static_cast<DedupWs *>(w); });
+    DedupWs &W = *static_cast<DedupWs *>(s.dedup_ws.get());
+    DevMem &dseg = W.dseg, &dtiles = W.dtiles, &tcnt = W.tcnt, &ke0 = W.ke0, &ke1 = W.ke1, &kh0 = W.kh0, &vh0 = W.vh0,
+           &kh1 = W.kh1, &vh1 = W.vh1, &hist = W.hist, &bsum = W.bsum, &counts = W.counts, &coll = W.coll,
+           &ncoll = W.ncoll, &pe = W.pe, &ph = W.ph;
+    dseg.reserve(segs.size() * sizeof(KSeg));
+    dtiles.reserve(tiles.size() * sizeof(uint2));
+    tcnt.reserve(2 * static_cast<size_t>(ntiles) * 4);
+    ke0.reserve(slots * 8);
+    ke1.reserve(n * 8);
+    kh0.reserve(slots * 8);
+    vh0.reserve(slots * 4);
+    kh1.reserve(n * 8);
+    vh1.reserve(n * 4);
+    hist.reserve(maxt * 256 * 4);
+    bsum.reserve(radix_bsum_words(maxt * gt) * 4);
+    counts.reserve(std::max<size_t>(nj, 1) * 8);
+    coll.reserve(n * 4);
+    ncoll.reserve(4);
     if (!segs.empty()) HIP_OK(hipMemcpyAsync(dseg.p, segs.data(), segs.size() * sizeof(KSeg), hipMemcpyHostToDevice, st));
     if (!tiles.empty())
         HIP_OK(hipMemcpyAsync(dtiles.p, tiles.data(), tiles.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemsetAsync(counts.p, 0, counts.bytes, st));
+    HIP_OK(hipMemsetAsync(counts.p, 0, std::max<size_t>(nj, 1) * 8, st));
     HIP_OK(hipMemsetAsync(ncoll.p, 0, 4, st));
     hipEvent_t e0, e1;
     HIP_OK(hipEventCreate(&e0));
@@ -1161,8 +1185,8 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
     }
     if (ne + nh != n) throw Error(SB_EHIP, "dedup gather lost keys");
     const uint32_t be = dedup_unique_blocks(ne), bh = dedup_unique_blocks(nh);
-    pe.alloc(std::max<uint32_t>(be, 1) * sizeof(uint4));
-    ph.alloc(std::max<uint32_t>(bh, 1) * sizeof(uint4));
+    pe.reserve(std::max<uint32_t>(be, 1) * sizeof(uint4));
+    ph.reserve(std::max<uint32_t>(bh, 1) * sizeof(uint4));
     // exact stream: keys only, as many 8-bit passes as its words have bits;
     // the first pass compacts the gather tiles
     const int re = launch_radix_sort(ke0.as<uint64_t>(), nullptr, ke1.as<uint64_t>(), nullptr, ne,

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -116,6 +117,8 @@ struct sb_store {
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;  // serialises batches on this device
+    std::shared_ptr<void> dedup_ws;      // dedup scratch (api.cpp DedupWs), reused across calls
+    std::shared_ptr<void> summarise_ws;  // summariseSlice scratch (api.cpp SumWs)
     std::vector<sb::VcfData> vcfs;  // metadata (columns are moved to the globals below)
     std::unordered_map<std::string, uint32_t> vcf_by_location;
     sb::Dict vt, sym;
