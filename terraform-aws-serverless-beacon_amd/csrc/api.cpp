@@ -172,14 +172,14 @@ struct sb_batch {
     std::vector<uint8_t> samples_variant;
     std::vector<uint32_t> vcf;
     uint64_t cap_total = 0, samples_words = 0;
-    DevMem q, qbytes, subsets, lut, res, hits, samples_out;
+    DevMem q, hoff, qbytes, subsets, lut, res, hits, samples_out;
     // queries split by kernel variant: the sample path compiled in or out
     // queries grouped by kernel specialisation: one launch per non-empty group
     struct Group {
         int mode;
         uint32_t max_words;  // 0 = sample path compiled out
         std::vector<uint32_t> idx;
-        DevMem d_idx;
+        uint32_t base;  // first entry of the group in the launch-ordered device array
     };
     std::vector<Group> groups;
     bool nonneg = true;
@@ -687,7 +687,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         // sample path; group 5 = MODE_GENERAL with the sample planes compiled in
         constexpr int kCollect = 5;
         for (int g = 0; g <= kCollect; ++g)
-            B.groups.push_back(sb_batch::Group{g == kCollect ? MODE_GENERAL : g, g == kCollect ? s.max_words : 0u, {}, {}});
+            B.groups.push_back(sb_batch::Group{g == kCollect ? MODE_GENERAL : g, g == kCollect ? s.max_words : 0u, {}, 0});
         for (uint32_t i = 0; i < B.nq; ++i) {
             const QDev &d = B.hq[i];
             if (!(d.flags & F_NONNEG)) B.nonneg = false;
@@ -726,18 +726,29 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     // ---- device buffers
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
+    // device query array in launch order (groups back to back, each sorted by
+    // segment and first base): a wave reads its query at qs + w, with no index
+    // load in front; QDev::orig names the QRes row
+    std::vector<QDev> lq;
+    lq.reserve(nq);
+    for (uint32_t i = 0; i < nq; ++i) B.hq[i].orig = i;
+    for (auto &g : B.groups) {
+        g.base = static_cast<uint32_t>(lq.size());
+        for (uint32_t i : g.idx) lq.push_back(B.hq[i]);
+    }
+    std::vector<uint64_t> hoff(nq);
+    for (uint32_t i = 0; i < nq; ++i) hoff[i] = B.hq[i].hit_off;
     B.q.alloc(nq * sizeof(QDev));
+    B.hoff.alloc(nq * 8);
     B.qbytes.alloc(qbytes.size());
     B.subsets.alloc(subsets.size() * 8);
     B.lut.alloc(lut_all.size() * 4);
-    if (nq) HIP_OK(hipMemcpyAsync(B.q.p, B.hq.data(), nq * sizeof(QDev), hipMemcpyHostToDevice, st));
+    if (nq) HIP_OK(hipMemcpyAsync(B.q.p, lq.data(), nq * sizeof(QDev), hipMemcpyHostToDevice, st));
+    if (nq) HIP_OK(hipMemcpyAsync(B.hoff.p, hoff.data(), nq * 8, hipMemcpyHostToDevice, st));
     if (!qbytes.empty()) HIP_OK(hipMemcpyAsync(B.qbytes.p, qbytes.data(), qbytes.size(), hipMemcpyHostToDevice, st));
     if (!subsets.empty()) HIP_OK(hipMemcpyAsync(B.subsets.p, subsets.data(), subsets.size() * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(B.lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
-    for (auto &g : B.groups) {
-        g.d_idx.alloc(g.idx.size() * 4);
-        HIP_OK(hipMemcpyAsync(g.d_idx.p, g.idx.data(), g.idx.size() * 4, hipMemcpyHostToDevice, st));
-    }
+
     B.res.alloc(size_t(nq) * sizeof(QRes));
     B.hits.alloc(cap_total * 8);
     B.samples_out.alloc(samples_words * 8);
@@ -763,12 +774,12 @@ void run(sb_batch &B) {
     for (int mode : {MODE_RANGE_N8, MODE_RANGE_N, MODE_VTYPE, MODE_GENERAL, MODE_EXACT})
         for (const auto &g : B.groups)
             if (g.max_words == 0 && g.mode == mode)
-                fg.push_back(FusedGroup{g.d_idx.as<uint32_t>(), static_cast<uint32_t>(g.idx.size()), g.mode});
-    launch_fused(d, B.q.as<QDev>(), fg.data(), static_cast<int>(fg.size()), B.nonneg, B.qbytes.as<uint8_t>(),
-                 B.subsets.as<uint64_t>(), B.res.as<QRes>(), B.hits.as<uint64_t>(), st);
+                fg.push_back(FusedGroup{B.q.as<QDev>() + g.base, static_cast<uint32_t>(g.idx.size()), g.mode});
+    launch_fused(d, fg.data(), static_cast<int>(fg.size()), B.nonneg, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(),
+                 B.res.as<QRes>(), B.hits.as<uint64_t>(), st);
     for (const auto &g : B.groups)
         if (g.max_words != 0)
-            launch_scan(d, B.q.as<QDev>(), g.d_idx.as<uint32_t>(), static_cast<uint32_t>(g.idx.size()), B.nonneg,
+            launch_scan(d, B.q.as<QDev>() + g.base, nullptr, static_cast<uint32_t>(g.idx.size()), B.nonneg,
                         g.max_words, g.mode, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(), B.res.as<QRes>(),
                         B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), st);
     HIP_OK(hipGetLastError());
@@ -811,7 +822,7 @@ sb_result_set *fetch(sb_batch &B) {
         dense.alloc(total * 8);
         HIP_OK(hipMemcpyAsync(doff.p, R->dense_off.data(), (size_t(nq) + 1) * 8, hipMemcpyHostToDevice, st));
         // queries with an error report n_hits = 0 on the device (host errors are F_EMPTY)
-        launch_compact(B.q.as<QDev>(), doff.as<uint64_t>(), B.res.as<QRes>(), nq, B.hits.as<uint64_t>(),
+        launch_compact(B.hoff.as<uint64_t>(), doff.as<uint64_t>(), B.res.as<QRes>(), nq, B.hits.as<uint64_t>(),
                        dense.as<uint64_t>(), st);
         HIP_OK(hipGetLastError());
         HIP_OK(hipMemcpyAsync(R->hit.data(), dense.p, total * 8, hipMemcpyDeviceToHost, st));

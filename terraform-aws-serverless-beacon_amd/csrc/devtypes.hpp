@@ -239,6 +239,8 @@ struct QDev {
     uint64_t samples_out_off;  // word offset of the per-query sample bitset, ~0 = none
     uint64_t hit_off;          // this query's output region (host-planned upper bound)
     int64_t an_default;        // the VCF's common AN (MODE_RANGE_N8)
+    uint32_t orig;             // the query's index in the batch (its QRes row); the device
+    uint32_t pad_;             //   array is in launch order, so waves index it directly
 };
 
 struct QRes {

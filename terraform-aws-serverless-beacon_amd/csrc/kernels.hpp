@@ -25,11 +25,11 @@ void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t
 // one launch, in the order given (put the longest-running first).
 constexpr int kFusedMax = 5;
 struct FusedGroup {
-    const uint32_t *qidx;
+    const QDev *q;  // the group's n queries, contiguous in launch order
     uint32_t n;
     int mode;
 };
-void launch_fused(const DStore &st, const QDev *q, const FusedGroup *groups, int count, bool nonneg,
+void launch_fused(const DStore &st, const FusedGroup *groups, int count, bool nonneg,
                   const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, hipStream_t s);
 
 // summariseSlice: phase A = one workgroup per chunk of kSumChunk records
@@ -46,8 +46,8 @@ void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *
                            ReqPartial *out, hipStream_t s);
 
 // Fetch-time gather of every query's hits into one dense array.
-void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,
-                    uint64_t *out, hipStream_t s);
+void launch_compact(const uint64_t *hit_off, const uint64_t *dense_off, const QRes *res, uint32_t nq,
+                    const uint64_t *hits, uint64_t *out, hipStream_t s);
 
 // duplicateVariantSearch (dedup_kernels.hip).  gather takes host-planned
 // tiles (segment, key offset) of dedup_gather_tile() keys and splits each

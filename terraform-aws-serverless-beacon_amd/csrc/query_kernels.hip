@@ -577,7 +577,7 @@ __device__ __forceinline__ void scan_slice(
         cur = nxt;
         if (s < kWave) break;
     }
-    finish_query<NONNEG>(S, q, hi - lo, res);
+    finish_query<NONNEG>(S, Q.orig, hi - lo, res);
     if constexpr (NACC > 0) if (collect && Q.samples_out_off != ~0ull) {
 #pragma unroll
         for (int j = 0; j < NACC; ++j) {
@@ -677,7 +677,7 @@ __device__ __forceinline__ void range_n_slice(DStore st, const QDev *__restrict_
             h = nh;
         }
     }
-    finish_query<NONNEG>(S, q, hi - lo, res);
+    finish_query<NONNEG>(S, Q.orig, hi - lo, res);
 }
 
 // MODE_VTYPE: referenceBases 'N' + alternateBases None + variantType queries
@@ -806,7 +806,7 @@ __device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
             x = nx;
         }
     }
-    finish_query<NONNEG>(S, q, hi - lo, res);
+    finish_query<NONNEG>(S, Q.orig, hi - lo, res);
 }
 
 // Gather each query's hits from its planned region into a dense array
@@ -966,7 +966,7 @@ __global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__res
 // the short ones (point lookups) fill the others' tail instead of running
 // after it in a second launch.
 struct FusedGroups {
-    const uint32_t *idx[kFusedMax];
+    const QDev *q[kFusedMax];  // group g's queries, in launch order
     uint32_t n[kFusedMax];
     uint32_t run[kFusedMax];
     uint32_t wave_begin[kFusedMax + 1];
@@ -975,8 +975,7 @@ struct FusedGroups {
 };
 
 template <bool NONNEG, bool RUN>
-__global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, const QDev *__restrict__ qs, FusedGroups G,
-                                                       const uint8_t *__restrict__ qbytes,
+__global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, FusedGroups G, const uint8_t *__restrict__ qbytes,
                                                        const uint64_t *__restrict__ subsets, QRes *__restrict__ res,
                                                        uint64_t *__restrict__ hits) {
     const uint32_t gw = launch_wave();
@@ -984,10 +983,11 @@ __global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, const QDev *__
     while (g + 1 < G.count && gw >= G.wave_begin[g + 1]) ++g;
     const uint32_t w = gw - G.wave_begin[g];
     const int mode = G.mode[g];
+    const QDev *qs = G.q[g];
     const auto aux = [&](const QDev &Q, uint32_t r) -> uint32_t {
         return mode == MODE_VTYPE ? vc_count(st, Q.vt_kind, r) : 0u;
     };
-    slices<RUN>(st, qs, G.idx[g], G.n[g], G.run[g], w, [&](uint32_t q, uint32_t lo, uint32_t hi, uint32_t alo, uint32_t ahi) {
+    slices<RUN>(st, qs, nullptr, G.n[g], G.run[g], w, [&](uint32_t q, uint32_t lo, uint32_t hi, uint32_t alo, uint32_t ahi) {
         switch (mode) {
             case MODE_RANGE_N: range_n_slice<NONNEG, RangeHot>(st, qs, res, hits, q, lo, hi); break;
             case MODE_RANGE_N8: range_n_slice<NONNEG, RangeHot8>(st, qs, res, hits, q, lo, hi); break;
@@ -1002,14 +1002,14 @@ __global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, const QDev *__
     }, aux);
 }
 
-__global__ __launch_bounds__(kBlock) void compact_kernel(const QDev *__restrict__ qs,
+__global__ __launch_bounds__(kBlock) void compact_kernel(const uint64_t *__restrict__ hit_off,
                                                          const uint64_t *__restrict__ dense_off,
                                                          const QRes *__restrict__ res, uint32_t nq,
                                                          const uint64_t *__restrict__ hits,
                                                          uint64_t *__restrict__ out) {
     const uint32_t q = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     if (q >= nq) return;
-    const uint64_t src = qs[q].hit_off, dst = dense_off[q];
+    const uint64_t src = hit_off[q], dst = dense_off[q];
     const uint32_t n = res[q].n_hits;
     for (uint32_t i = static_cast<uint32_t>(lane_id()); i < n; i += kWave) out[dst + i] = hits[src + i];
 }
@@ -1246,10 +1246,11 @@ void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *
                        host_err, n_rows, out);
 }
 
-void launch_compact(const QDev *q, const uint64_t *dense_off, const QRes *res, uint32_t nq, const uint64_t *hits,
-                    uint64_t *out, hipStream_t s) {
+void launch_compact(const uint64_t *hit_off, const uint64_t *dense_off, const QRes *res, uint32_t nq,
+                    const uint64_t *hits, uint64_t *out, hipStream_t s) {
     if (!nq) return;
-    hipLaunchKernelGGL(compact_kernel, dim3(blocks_for(nq)), dim3(kBlock), 0, s, q, dense_off, res, nq, hits, out);
+    hipLaunchKernelGGL(compact_kernel, dim3(blocks_for(nq)), dim3(kBlock), 0, s, hit_off, dense_off, res, nq, hits,
+                       out);
 }
 
 template <bool NONNEG>
@@ -1274,8 +1275,9 @@ void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t
     if (!n) return;
     const int nacc = max_words == 0 ? 0 : max_words <= 64 ? 1 : max_words <= 256 ? 4 : 16;
     if (nacc == 0) {  // every sample-free specialisation goes through the fused kernel
-        const FusedGroup one{qidx, n, mode};
-        launch_fused(st, q, &one, 1, nonneg, qbytes, subsets, res, hits, s);
+        if (qidx) throw std::runtime_error("launch_scan: sample-free queries must be contiguous (qidx = null)");
+        const FusedGroup one{q, n, mode};
+        launch_fused(st, &one, 1, nonneg, qbytes, subsets, res, hits, s);
         return;
     }
     const uint32_t run = 1;  // the sample path keeps one slice per wave
@@ -1286,15 +1288,15 @@ void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t
         launch_variant<false>(nacc, mode, g, st, q, qidx, n, run, qbytes, subsets, res, hits, samples_out, s);
 }
 
-void launch_fused(const DStore &st, const QDev *q, const FusedGroup *groups, int count, bool nonneg,
-                  const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, hipStream_t s) {
+void launch_fused(const DStore &st, const FusedGroup *groups, int count, bool nonneg, const uint8_t *qbytes,
+                  const uint64_t *subsets, QRes *res, uint64_t *hits, hipStream_t s) {
     FusedGroups G{};
     uint32_t waves = 0;
     int c = 0;
     for (int i = 0; i < count; ++i) {
         if (!groups[i].n) continue;
         if (c == kFusedMax) throw std::runtime_error("launch_fused: too many groups");
-        G.idx[c] = groups[i].qidx;
+        G.q[c] = groups[i].q;
         G.n[c] = groups[i].n;
         G.mode[c] = groups[i].mode;
         G.run[c] = run_for(groups[i].n);
@@ -1313,7 +1315,8 @@ void launch_fused(const DStore &st, const QDev *q, const FusedGroup *groups, int
     G.wave_begin[c] = waves;
     const dim3 g(waves / kWavesPerBlock), b(kBlock);
     if (c == 1) {  // a single group: its own specialisation (smaller code, no group dispatch)
-        const uint32_t *qi = G.idx[0];
+        const QDev *q = G.q[0];
+        const uint32_t *qi = nullptr;  // the group's queries are contiguous in launch order
         const uint32_t n = G.n[0], rn = G.run[0];
 #define SB_ONE(NN, RR)                                                                                         \
         switch (G.mode[0]) {                                                                                   \
@@ -1336,11 +1339,11 @@ void launch_fused(const DStore &st, const QDev *q, const FusedGroup *groups, int
         return;
     }
     if (nonneg) {
-        if (run) hipLaunchKernelGGL((fused_kernel<true, true>), g, b, 0, s, st, q, G, qbytes, subsets, res, hits);
-        else hipLaunchKernelGGL((fused_kernel<true, false>), g, b, 0, s, st, q, G, qbytes, subsets, res, hits);
+        if (run) hipLaunchKernelGGL((fused_kernel<true, true>), g, b, 0, s, st, G, qbytes, subsets, res, hits);
+        else hipLaunchKernelGGL((fused_kernel<true, false>), g, b, 0, s, st, G, qbytes, subsets, res, hits);
     } else {
-        if (run) hipLaunchKernelGGL((fused_kernel<false, true>), g, b, 0, s, st, q, G, qbytes, subsets, res, hits);
-        else hipLaunchKernelGGL((fused_kernel<false, false>), g, b, 0, s, st, q, G, qbytes, subsets, res, hits);
+        if (run) hipLaunchKernelGGL((fused_kernel<false, true>), g, b, 0, s, st, G, qbytes, subsets, res, hits);
+        else hipLaunchKernelGGL((fused_kernel<false, false>), g, b, 0, s, st, G, qbytes, subsets, res, hits);
     }
 }
 
