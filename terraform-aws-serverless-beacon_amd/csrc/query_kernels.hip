@@ -375,6 +375,7 @@ struct ScanState {
     uint32_t n_out = 0;
     bool exists = false;
     int err_out = 0;
+    bool touched = false;  // some chunk had a hit or an error (else every total is 0)
 };
 
 // The reference loop's order-dependent state over one 64-record chunk
@@ -393,6 +394,7 @@ __device__ __forceinline__ int chunk_tail(ScanState &S, const LaneOut &o, uint32
         *collectm = 0;
         return kWave;
     }
+    S.touched = true;
     int64_t cum = 0;
     uint64_t trigm;  // hit lanes where the running call_count is non-zero
     if constexpr (NONNEG) {
@@ -449,6 +451,10 @@ __device__ __forceinline__ int chunk_tail(ScanState &S, const LaneOut &o, uint32
 
 template <bool NONNEG>
 __device__ __forceinline__ void finish_query(const ScanState &S, uint32_t q, uint32_t n_scanned, QRes *res) {
+    if (!S.touched) {  // no hit and no error in the whole slice (most variantType slices)
+        if (lane_id() == 0) res[q] = QRes{0, 0, 0, 0, 0, n_scanned};
+        return;
+    }
     const int64_t call_count = NONNEG ? wave_sum_i64(S.cc_acc) : S.carry;
     const int64_t an_sum = wave_sum_i64(S.an_acc);
     if (lane_id() == 0) {
