@@ -716,6 +716,10 @@ __device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
                                          uint32_t c_lo, uint32_t c_hi_all) {
     const int lane = lane_id();
     const QDev &Q = qs[q];
+    if (c_hi_all <= c_lo) {  // no candidate of this kind in the slice: nothing can hit or raise
+        if (lane == 0) res[Q.orig] = QRes{0, 0, 0, 0, 0, hi - lo};
+        return;
+    }
     const uint32_t flags = Q.flags;
     const bool details = flags & F_DETAILS;
     const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
