@@ -11,7 +11,7 @@ step() {  # name, limit, command...
   case $rc in 0|1) return 0;; *) exit $rc;; esac
 }
 step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
-step gpu_tests 900 python3 -m pytest tests -m gpu -q -x
+step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread
 step bench 900 python3 $R/bench.py --steps $STEPS --warmup 3
 cp $R/gpurun_out/bench.log $R/gpurun_out/bench_full.log
 cd /tmp && step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o bench -- python3 $R/bench.py --steps $STEPS --warmup 3 --no-cpu-baseline
