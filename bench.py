@@ -56,11 +56,14 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--parity-requests', type=int, default=300,
                     help='requests re-checked against the C oracle after timing (rank 0)')
-    ap.add_argument('--workload', choices=['chr22', 'genome'], default='chr22',
+    ap.add_argument('--workload', choices=['chr22', 'genome', 'gnomad'], default='chr22',
                     help='chr22: config 2 (default; replicas across GPUs). genome: config 3 (whole-genome store '
-                         'sharded by contig across the GPUs, request rows gathered to rank 0 over RCCL)')
+                         'sharded by contig across the GPUs, request rows gathered to rank 0 over RCCL). '
+                         'gnomad: config 5 (gnomAD-shape sites + carrier bit-matrix, shard r of 8 per GPU)')
     ap.add_argument('--genome-records', type=int, default=85_000_000)
     ap.add_argument('--genome-requests', type=int, default=1_000_000)
+    ap.add_argument('--gnomad-records', type=int, default=750_000_000)
+    ap.add_argument('--gnomad-requests', type=int, default=50_000, help='config-5 requests per GPU')
     return ap.parse_args()
 
 
@@ -69,6 +72,9 @@ def main():
     if args.workload == 'genome':
         from bench_genome import main_genome
         return main_genome(args)
+    if args.workload == 'gnomad':
+        from bench_gnomad import main_gnomad
+        return main_gnomad(args)
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))

@@ -74,6 +74,16 @@ int sb_builder_begin_vcf(sb_builder *b, const char *location, size_t location_le
 int sb_builder_add_text(sb_builder *b, uint32_t vcf_id, const char *text, size_t len);
 /* convenience: plain or gzip/BGZF file from disk (zlib) */
 int sb_builder_add_file(sb_builder *b, uint32_t vcf_id, const char *path);
+/* genotypes of a sites-only VCF from a separate carrier bit-matrix (config 5,
+ * gnomAD-shape sites + a cohort's genotypes): one row of ceil(n_samples/64)
+ * u64 words per ALT in record-then-ALT order, bit s of ALT k = sample s has
+ * a GT token equal to str(k+1) -- the set search_variants.py:233-236 collects
+ * from GT text.  Call after the VCF's last text; every record needs AC and AN
+ * (else SB_EINVAL: the reference's GT-count fallbacks, :215-226,:244-250,
+ * need the GT text itself).  Replaces the `[%GT,]` columns bcftools would emit
+ * (search_variants.py:45). */
+int sb_builder_attach_carriers(sb_builder *b, uint32_t vcf_id, const char *const *names, const uint32_t *name_len,
+                               uint32_t n_samples, const uint64_t *planes, uint64_t n_rows);
 /* upload to device `device` (HIP ordinal) and return an immutable store */
 int sb_builder_finish(sb_builder *b, int device, sb_store **out);
 void sb_builder_free(sb_builder *b);

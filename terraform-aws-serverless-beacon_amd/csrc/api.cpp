@@ -21,6 +21,8 @@ namespace sb {
 void builder_add_text(sb_builder &b, uint32_t vcf_id, const char *text, size_t len);
 void builder_add_file(sb_builder &b, uint32_t vcf_id, const char *path);
 void builder_flush(sb_builder &b, uint32_t vcf_id);
+void builder_attach_carriers(sb_builder &b, uint32_t vcf_id, const char *const *names, const uint32_t *name_len,
+                             uint32_t n_samples, const uint64_t *planes, uint64_t n_rows);
 
 namespace {
 thread_local std::string g_last_error;
@@ -286,10 +288,14 @@ void upload_store(sb_builder &b, sb_store &s) {
         v.x_base = x_base;
         v.nonneg = !c.any_negative;
         v.has_planes = !c.planes0.empty();
+        v.sample_pos.clear();
+        for (uint32_t k = 0; k < v.samples.size(); ++k) v.sample_pos[v.samples[k]].push_back(k);
         v.plane0_base = planes.size();
         planes.insert(planes.end(), c.planes0.begin(), c.planes0.end());
         v.planex_base = planes.size();
         planes.insert(planes.end(), c.planesx.begin(), c.planesx.end());
+        std::vector<uint64_t>().swap(c.planes0);  // the device copy is the only one used after upload
+        std::vector<uint64_t>().swap(c.planesx);
         rec.insert(rec.end(), c.rec.begin(), c.rec.end());
         rng.insert(rng.end(), c.rng.begin(), c.rng.end());
         pos.insert(pos.end(), c.pos.begin(), c.pos.end());
@@ -519,6 +525,12 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     B.host_err.assign(nq, 0);
     B.chrom.assign(nq, std::string());
     B.emitted.assign(nq, std::vector<uint32_t>());
+    struct SubsetEntry {
+        uint64_t off = 0;
+        bool empty = false;
+        std::vector<uint32_t> emitted;
+    };
+    std::unordered_map<std::string, SubsetEntry> subset_cache;
     B.samples_variant.assign(nq, 0);
     B.vcf.assign(nq, 0);
     std::vector<uint8_t> qbytes;
@@ -571,28 +583,37 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         if (v.nonneg) d.flags |= F_NONNEG;
         if (samples_variant) {  // bcftools --samples (svs:36-42), header order
             const std::string names = x.sample_names ? std::string(x.sample_names, x.sample_names_len) : std::string("_");
-            std::vector<uint8_t> sel(n_samples, 0);
-            size_t p = 0;
-            for (;;) {
-                const size_t c = names.find(',', p);
-                const std::string nm = names.substr(p, c == std::string::npos ? std::string::npos : c - p);
-                bool found = false;
-                for (uint32_t k = 0; k < n_samples; ++k)
-                    if (v.samples[k] == nm) {
-                        sel[k] = 1;
-                        found = true;
-                    }
-                if (!found) d.flags |= F_EMPTY;  // unknown sample: bcftools exits, no output
-                if (c == std::string::npos) break;
-                p = c + 1;
-            }
-            d.subset_off = subsets.size();
-            subsets.resize(subsets.size() + std::max(1u, v.words), 0ull);
-            for (uint32_t k = 0; k < n_samples; ++k)
-                if (sel[k]) {
-                    B.emitted[i].push_back(k);
-                    subsets[d.subset_off + (k >> 6)] |= 1ull << (k & 63);
+            // requests of one batch often share a sampleNames list: one mask each
+            const std::string ck = std::to_string(x.vcf_id) + '\n' + names;
+            auto hit = subset_cache.find(ck);
+            if (hit == subset_cache.end()) {
+                std::vector<uint8_t> sel(n_samples, 0);
+                bool empty = false;
+                size_t p = 0;
+                for (;;) {
+                    const size_t c = names.find(',', p);
+                    const std::string nm = names.substr(p, c == std::string::npos ? std::string::npos : c - p);
+                    auto f = v.sample_pos.find(nm);
+                    if (f == v.sample_pos.end()) empty = true;  // unknown sample: bcftools exits, no output
+                    else
+                        for (uint32_t k : f->second) sel[k] = 1;
+                    if (c == std::string::npos) break;
+                    p = c + 1;
                 }
+                SubsetEntry e;
+                e.off = subsets.size();
+                e.empty = empty;
+                subsets.resize(subsets.size() + std::max(1u, v.words), 0ull);
+                for (uint32_t k = 0; k < n_samples; ++k)
+                    if (sel[k]) {
+                        e.emitted.push_back(k);
+                        subsets[e.off + (k >> 6)] |= 1ull << (k & 63);
+                    }
+                hit = subset_cache.emplace(ck, std::move(e)).first;
+            }
+            if (hit->second.empty) d.flags |= F_EMPTY;
+            d.subset_off = hit->second.off;
+            B.emitted[i] = hit->second.emitted;
         }
         // REF predicate (:59, :94 / svs:87-91)
         d.qbytes_off = static_cast<uint32_t>(qbytes.size());
@@ -1412,6 +1433,14 @@ int sb_builder_add_file(sb_builder *b, uint32_t vcf_id, const char *path) {
     return guard([&] {
         if (!b || !path) throw Error(SB_EINVAL, "NULL argument");
         builder_add_file(*b, vcf_id, path);
+    });
+}
+
+int sb_builder_attach_carriers(sb_builder *b, uint32_t vcf_id, const char *const *names, const uint32_t *name_len,
+                               uint32_t n_samples, const uint64_t *planes, uint64_t n_rows) {
+    return guard([&] {
+        if (!b) throw Error(SB_EINVAL, "NULL argument");
+        builder_attach_carriers(*b, vcf_id, names, name_len, n_samples, planes, n_rows);
     });
 }
 

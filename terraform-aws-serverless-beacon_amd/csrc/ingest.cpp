@@ -15,6 +15,7 @@
 //     1-based allele number (the regex at :233-236)
 #include <algorithm>
 #include <atomic>
+#include <cstring>
 #include <thread>
 #include <zlib.h>
 
@@ -915,6 +916,53 @@ void builder_add_file(sb_builder &b, uint32_t vcf_id, const char *path) {
     }
     gzclose(f);
     builder_flush(b, vcf_id);
+}
+
+// Carrier matrix for a sites-only VCF (config 5: gnomAD-shape sites with a
+// separately held 2,504-sample genotype bit-matrix).  `planes` holds one row
+// of ceil(n_samples/64) words per ALT, in record-then-ALT order: bit s of
+// ALT k's row = sample s has a GT token equal to str(k + 1) -- exactly the
+// set the reference's regex at search_variants.py:233-236 collects, and what
+// the text path builds from GT columns above.  Every record must carry AC and
+// a valid AN: without them the reference counts GT tokens (:215-226,
+// :244-250), which a carrier matrix does not determine.
+void builder_attach_carriers(sb_builder &b, uint32_t vcf_id, const char *const *names, const uint32_t *name_len,
+                             uint32_t n_samples, const uint64_t *planes, uint64_t n_rows) {
+    if (vcf_id >= b.vcfs.size()) throw Error(SB_ENOSTORE, "unknown vcf id");
+    builder_flush(b, vcf_id);
+    VcfData &v = b.vcfs[vcf_id];
+    VcfCols &c = v.c;
+    if (!v.samples.empty()) throw Error(SB_EINVAL, "VCF already has sample columns");
+    if (n_samples == 0 || !planes || !names || !name_len) throw Error(SB_EINVAL, "empty carrier matrix");
+    const size_t nr = c.pos.size(), nx = c.x_key.size();
+    if (n_rows != nr + nx) throw Error(SB_EINVAL, "carrier matrix rows != ALT rows of the VCF");
+    for (size_t i = 0; i < nr; ++i) {
+        const uint32_t h = c.rec[i].hot;
+        if ((h & (H_HAS_AC | H_HAS_AN)) != (H_HAS_AC | H_HAS_AN) || (h & H_AN_BAD))
+            throw Error(SB_EINVAL, "carrier matrix needs AC and AN on every record");
+    }
+    v.samples.resize(n_samples);
+    for (uint32_t s = 0; s < n_samples; ++s) v.samples[s].assign(names[s], name_len[s]);
+    const uint32_t words = static_cast<uint32_t>((n_samples + 63) / 64);
+    v.words = words;
+    c.planes0.resize(nr * words);
+    c.planesx.resize(nx * words);
+    unsigned nt = b.opts.n_threads > 0 ? static_cast<unsigned>(b.opts.n_threads) : std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min<unsigned>(nt, static_cast<unsigned>(nr / 4096 + 1)));
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            const size_t a = nr * t / nt, e = nr * (t + 1) / nt;
+            for (size_t i = a; i < e; ++i) {
+                const size_t row = i + c.x_lo[i];  // rows before record i
+                const size_t nalt = 1 + c.x_lo[i + 1] - c.x_lo[i];
+                memcpy(&c.planes0[i * words], planes + row * words, words * 8);
+                if (nalt > 1)
+                    memcpy(&c.planesx[static_cast<size_t>(c.x_lo[i]) * words], planes + (row + 1) * words,
+                           (nalt - 1) * words * 8);
+            }
+        });
+    for (auto &x : th) x.join();
 }
 
 }  // namespace sb

@@ -64,6 +64,8 @@ struct BucketIndex {  // coarse POS index of one segment
 struct VcfData {
     std::string location;
     std::vector<std::string> samples;
+    // name -> header indices (built at upload; bcftools --samples lookups)
+    std::unordered_map<std::string, std::vector<uint32_t>> sample_pos;
     uint32_t words = 0;  // ceil(n_samples / 64)
     bool header_seen = false;
     std::vector<Segment> segments;

@@ -53,6 +53,10 @@ struct Gen {
     // probability `share`, otherwise from this member's own seed
     uint64_t own_seed = 0;
     double share = 1.0;
+    // config 5 (gnomAD-shape sites): INFO AC/AN over a cohort of an_sites
+    // alleles (0 = 2 x n_samples), genotypes over n_samples with carriers
+    // scaled by 2 n_samples / an_sites
+    uint32_t an_sites = 0;
     double multi_frac = 0.015;  // multiallelic share of all records (SBS_MULTI_FRAC overrides; experiments)
     uint64_t rec_seed(uint64_t i) const {
         if (share >= 1.0) return seed;
@@ -76,7 +80,7 @@ void make_record(const Gen &g, uint64_t i, Rec &r) {
     r.ac.clear();
     r.sym = false;
     const uint32_t hap = 2 * g.n_samples;
-    const uint32_t N = hap ? hap : 5008;
+    const uint32_t N = g.an_sites ? g.an_sites : (hap ? hap : 5008);
     auto draw_ac = [&](uint32_t cap) {
         // P(k) ~ 1/k on [1, cap]: k = floor((cap+1)^u)
         const double x = std::pow(static_cast<double>(cap) + 1.0, rng.uni());
@@ -135,6 +139,39 @@ size_t write_u(char *p, uint64_t v) {
     return static_cast<size_t>(n);
 }
 
+// Carrier haplotypes of record i, drawn from rng stream 2 after the INFO
+// draws render() makes (DP, five population AFs per ALT, END of a symbolic
+// record): f(k, h) for each haplotype h carrying ALT k (0-based).  Distinct
+// haplotypes per record; AC carriers per ALT, or AC scaled to the sample
+// cohort for an_sites VCFs.
+template <typename F>
+void draw_carriers(const Gen &g, const Rec &r, Rng &rng, std::vector<uint8_t> &taken, F f) {
+    const uint32_t hap = 2 * g.n_samples;
+    std::fill(taken.begin(), taken.end(), 0);
+    uint32_t free_h = hap;
+    for (size_t k = 0; k < r.ac.size(); ++k) {
+        uint32_t n = r.ac[k];
+        if (g.an_sites) n = static_cast<uint32_t>((static_cast<uint64_t>(n) * hap + g.an_sites - 1) / g.an_sites);
+        n = std::min(n, free_h);
+        free_h -= n;
+        for (uint32_t c = 0; c < n; ++c) {
+            uint32_t h;
+            do h = rng.below(hap);
+            while (taken[h]);
+            taken[h] = 1;
+            f(k, h);
+        }
+    }
+}
+
+// The stream-2 draws render() makes before the genotypes.
+void skip_site_draws(const Rec &r, Rng &rng) {
+    rng.below(30000);
+    for (int p = 0; p < 5; ++p)
+        for (size_t k = 0; k < r.ac.size(); ++k) rng.uni();
+    if (r.sym) rng.below(5000);
+}
+
 // Render records [lo, hi) into out (appends).
 void render(const Gen &g, uint64_t lo, uint64_t hi, bool sites_only, std::string &out) {
     Rec r;
@@ -181,7 +218,7 @@ void render(const Gen &g, uint64_t lo, uint64_t hi, bool sites_only, std::string
             if (k) putc_(',');
             putu(r.ac[k]);
         }
-        const uint32_t an = hap ? hap : 5008;
+        const uint32_t an = g.an_sites ? g.an_sites : (hap ? hap : 5008);
         put(";AF=", 4);
         for (size_t k = 0; k < r.ac.size(); ++k) {
             if (k) putc_(',');
@@ -221,17 +258,8 @@ void render(const Gen &g, uint64_t lo, uint64_t hi, bool sites_only, std::string
         // genotypes consistent with AC: distinct carrier haplotypes per allele
         const size_t g0 = out.size();
         out.append(gt);
-        std::fill(taken.begin(), taken.end(), 0);
-        for (size_t k = 0; k < r.ac.size(); ++k) {
-            const char digit = static_cast<char>('1' + k);
-            for (uint32_t c = 0; c < r.ac[k]; ++c) {
-                uint32_t h;
-                do h = rng.below(hap);
-                while (taken[h]);
-                taken[h] = 1;
-                out[g0 + 4 * (h >> 1) + 2 * (h & 1)] = digit;
-            }
-        }
+        draw_carriers(g, r, rng, taken,
+                      [&](size_t k, uint32_t h) { out[g0 + 4 * (h >> 1) + 2 * (h & 1)] = static_cast<char>('1' + k); });
     }
 }
 
@@ -346,6 +374,79 @@ char *sbs_records(void *h, uint64_t lo, uint64_t hi, int sites_only, int n_threa
     }
     *len = total;
     return o;
+}
+
+// config 5: INFO AN of every record (and the AC scale); 0 = 2 x n_samples
+void sbs_set_an_sites(void *h, uint32_t an) { static_cast<Gen *>(h)->an_sites = an; }
+
+// ALT rows (records + extra ALTs) of records [lo, hi)
+uint64_t sbs_alt_rows(void *h, uint64_t lo, uint64_t hi, int n_threads) {
+    auto *g = static_cast<Gen *>(h);
+    hi = std::min<uint64_t>(hi, g->n);
+    if (lo >= hi) return 0;
+    unsigned nt = n_threads > 0 ? static_cast<unsigned>(n_threads) : std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min<unsigned>(nt, static_cast<unsigned>((hi - lo + 1023) / 1024)));
+    std::vector<uint64_t> cnt(nt, 0);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            Rec r;
+            const uint64_t a = lo + (hi - lo) * t / nt, b = lo + (hi - lo) * (t + 1) / nt;
+            for (uint64_t i = a; i < b; ++i) {
+                make_record(*g, i, r);
+                cnt[t] += r.alts.size();
+            }
+        });
+    for (auto &x : th) x.join();
+    uint64_t n = 0;
+    for (auto c : cnt) n += c;
+    return n;
+}
+
+// Carrier bit-matrix of records [lo, hi): one row of ceil(n_samples/64)
+// words per ALT, record-then-ALT order (sb_builder_attach_carriers), the
+// same genotypes sbs_records renders as GT text.  out: n_rows x words u64.
+int sbs_carrier_planes(void *h, uint64_t lo, uint64_t hi, int n_threads, uint64_t *out, uint64_t n_rows) {
+    auto *g = static_cast<Gen *>(h);
+    hi = std::min<uint64_t>(hi, g->n);
+    if (lo >= hi) return n_rows == 0 ? 0 : -1;
+    const uint32_t words = (g->n_samples + 63) / 64;
+    unsigned nt = n_threads > 0 ? static_cast<unsigned>(n_threads) : std::thread::hardware_concurrency();
+    nt = std::max(1u, std::min<unsigned>(nt, static_cast<unsigned>((hi - lo + 1023) / 1024)));
+    std::vector<uint64_t> cnt(nt + 1, 0);
+    auto run = [&](bool fill) {
+        std::vector<std::thread> th;
+        for (unsigned t = 0; t < nt; ++t)
+            th.emplace_back([&, t, fill] {
+                Rec r;
+                std::vector<uint8_t> taken(2 * g->n_samples + 1);
+                const uint64_t a = lo + (hi - lo) * t / nt, b = lo + (hi - lo) * (t + 1) / nt;
+                uint64_t row = fill ? cnt[t] : 0;
+                for (uint64_t i = a; i < b; ++i) {
+                    make_record(*g, i, r);
+                    if (!fill) {
+                        row += r.alts.size();
+                        continue;
+                    }
+                    uint64_t *base = out + row * words;
+                    memset(base, 0, r.alts.size() * words * 8);
+                    Rng rng(g->rec_seed(i), i, 2);
+                    skip_site_draws(r, rng);
+                    draw_carriers(*g, r, rng, taken, [&](size_t k, uint32_t hp) {
+                        const uint32_t s = hp >> 1;
+                        base[k * words + (s >> 6)] |= 1ull << (s & 63);
+                    });
+                    row += r.alts.size();
+                }
+                if (!fill) cnt[t + 1] = row;
+            });
+        for (auto &x : th) x.join();
+    };
+    run(false);
+    for (unsigned t = 0; t < nt; ++t) cnt[t + 1] += cnt[t];
+    if (cnt[nt] != n_rows) return -1;
+    run(true);
+    return 0;
 }
 
 void sbs_free_text(char *p) { free(p); }

@@ -91,6 +91,8 @@ SIGNATURES = {
     'sb_builder_begin_vcf': (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(C.c_uint32)]),
     'sb_builder_add_text': (C.c_int, [P, C.c_uint32, C.c_char_p, C.c_size_t]),
     'sb_builder_add_file': (C.c_int, [P, C.c_uint32, C.c_char_p]),
+    'sb_builder_attach_carriers': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_uint32),
+                                             C.c_uint32, C.c_void_p, C.c_uint64]),
     'sb_builder_finish': (C.c_int, [P, C.c_int, C.POINTER(P)]),
     'sb_builder_free': (None, [P]),
     'sb_store_close': (None, [P]),

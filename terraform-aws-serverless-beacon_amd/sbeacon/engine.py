@@ -18,6 +18,8 @@ import ctypes as C
 import os
 from typing import Iterable
 
+import numpy as np
+
 from . import _lib
 from ._lib import (BatchStats, BuildOpts, DedupJob, DedupStats, Query, ResultView, Slice, SliceStats, StoreInfo,
                    check, lib)
@@ -89,14 +91,19 @@ class Store:
     def build(cls, sources, *, device: int = 0, keep_genotypes: bool = True, n_threads: int = 0):
         """``sources``: iterable of ``(vcf_location, path_or_text)``; a value
         that is an existing path is read (plain or gzip), otherwise it is
-        VCF text (``str``/``bytes``) or an iterable of text chunks."""
+        VCF text (``str``/``bytes``) or an iterable of text chunks.  A
+        3-tuple ``(vcf_location, source, (sample_names, planes))`` attaches a
+        carrier bit-matrix to a sites-only VCF (``planes``: uint64
+        ``[alt rows, ceil(n/64)]``, record-then-ALT order; sb_builder_attach_carriers)."""
         L = lib()
         b = C.c_void_p()
         opts = BuildOpts(1 if keep_genotypes else 0, int(n_threads))
         check(L.sb_builder_new(C.byref(opts), C.byref(b)))
         locs = []
         try:
-            for loc, src in sources:
+            for item in sources:
+                loc, src = item[0], item[1]
+                carriers = item[2] if len(item) > 2 else None
                 vid = C.c_uint32()
                 lb = _b(loc)
                 check(L.sb_builder_begin_vcf(b, lb, len(lb), C.byref(vid)))
@@ -110,6 +117,19 @@ class Store:
                     for chunk in src:
                         t = _b(chunk)
                         check(L.sb_builder_add_text(b, vid.value, t, len(t)))
+                if carriers is not None:
+                    names, planes = carriers[0], carriers[1]
+                    if isinstance(carriers, list):
+                        carriers.clear()  # a list hands over the only reference: freed after the copy
+                    nb = [_b(n) for n in names]
+                    arr = (C.c_char_p * len(nb))(*nb)
+                    lens = (C.c_uint32 * len(nb))(*[len(x) for x in nb])
+                    planes = np.ascontiguousarray(planes, dtype=np.uint64)
+                    if planes.ndim != 2 or planes.shape[1] != (len(nb) + 63) // 64:
+                        raise ValueError('carrier planes must be [alt rows, ceil(n_samples / 64)] uint64')
+                    check(L.sb_builder_attach_carriers(b, vid.value, arr, lens, len(nb), planes.ctypes.data,
+                                                       planes.shape[0]))
+                    del planes
             s = C.c_void_p()
             check(L.sb_builder_finish(b, int(device), C.byref(s)))
         finally:

@@ -42,6 +42,11 @@ def synth_lib():
         L.sbs_free_text.argtypes = [C.c_void_p]
         L.sbs_new_member.restype = C.c_void_p
         L.sbs_new_member.argtypes = [C.c_void_p, C.c_uint64, C.c_double, C.c_uint32]
+        L.sbs_set_an_sites.argtypes = [C.c_void_p, C.c_uint32]
+        L.sbs_alt_rows.restype = C.c_uint64
+        L.sbs_alt_rows.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int]
+        L.sbs_carrier_planes.restype = C.c_int
+        L.sbs_carrier_planes.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_int, C.c_void_p, C.c_uint64]
         L.sbs_bgzf_compress.restype = C.c_void_p
         L.sbs_bgzf_compress.argtypes = [C.c_char_p, C.c_size_t, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_size_t)]
         _syn = L
@@ -130,6 +135,33 @@ class SyntheticVcf:
         m._h = synth_lib().sbs_new_member(self._h, own_seed, float(share), m.n_samples)
         m._pos = self._pos
         return m
+
+    def set_an_sites(self, an: int):
+        """Config 5: every record's INFO AN = an (AC drawn over it); GT
+        carriers over the n_samples cohort scale with 2 n_samples / an."""
+        synth_lib().sbs_set_an_sites(self._h, int(an))
+        return self
+
+    def sample_names(self) -> list[str]:
+        return [f'HG{i + 96:05d}' for i in range(self.n_samples)]
+
+    def alt_rows(self, lo=0, hi=None, threads=0) -> int:
+        hi = self.n_records if hi is None else hi
+        return int(synth_lib().sbs_alt_rows(self._h, lo, hi, threads))
+
+    def carrier_planes(self, lo=0, hi=None, threads=0, out=None) -> np.ndarray:
+        """Carrier bit-matrix of records [lo, hi), the genotypes records()
+        renders as GT text: uint64 [alt rows, ceil(n_samples / 64)]."""
+        hi = self.n_records if hi is None else hi
+        words = (self.n_samples + 63) // 64
+        if out is None:
+            out = np.empty((self.alt_rows(lo, hi, threads), words), dtype=np.uint64)
+        n = out.shape[0]
+        if out.shape[1] != words or not out.flags['C_CONTIGUOUS']:
+            raise ValueError('out must be a C-contiguous [alt rows, words] uint64 array')
+        if synth_lib().sbs_carrier_planes(self._h, lo, hi, threads, out.ctypes.data, n) != 0:
+            raise RuntimeError('carrier plane generation failed')
+        return out
 
     def alleles(self, i):
         ref = C.create_string_buffer(256)
