@@ -96,6 +96,15 @@ def main_gnomad(args):
     # row (words x 8 B) per hit ALT of a sample-subset query
     alg = 32.0 * scanned + 8.0 * hits + 8.0 * words * samp_hits
     achieved = alg / (timing['scan_ms'] * 1e-3) / 1e9 if timing['scan_ms'] > 0 else 0.0
+    traffic = None  # HBM bytes per step from the PMC passes (tools/gpu_pmc_gnomad.sh)
+    tf = os.path.join(REPO, 'profiles', 'traffic_gnomad.json')
+    if os.path.exists(tf):
+        try:
+            tj = json.load(open(tf))
+            if tj.get('records') == shape.n_total and tj.get('requests') == args.gnomad_requests:
+                traffic = tj.get('scan_kernel_hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
     vals = [elapsed, timing['scan_ms'], float(sl.n_requests), float(len(sl)), float(scanned), float(hits),
             achieved, alg, float(samp_hits)]
     if dist:
@@ -136,7 +145,7 @@ def main_gnomad(args):
         'device_ms_per_step': {'query_kernels_rank0': round(timing['scan_ms'], 4),
                                'query_kernels_max': round(max(v[1] for v in allv), 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(allv[0][6], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(allv[0][6] / HBM_PEAK_GBS, 4), 'traffic': None,
+                     'frac': round(allv[0][6] / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'kernel': 'rank 0 query step (range_n + sample-path scan launches); HIP events spanning the step',
                      'algorithmic_bytes_per_launch': allv[0][7],
                      'note': f'32 B/row scanned + 8 B/hit + {8 * words} B carrier row per sample-path hit ALT'},

@@ -522,7 +522,7 @@ done:
 // call_count is monotone and `if call_count:` reduces to ballots.  MODE_EXACT
 // specialises the predicates for REF/ALT point queries; MODE_GENERAL handles
 // every payload (variantType, samples variant, strict mode, wildcards).
-constexpr int kRowBatch = 8;  // carrier rows in flight per wave (sample path)
+constexpr int kRowBatch = 16;  // carrier rows in flight per wave (sample path)
 
 template <int NACC, bool NONNEG, int MODE>
 __device__ __forceinline__ void scan_slice(
@@ -567,7 +567,8 @@ __device__ __forceinline__ void scan_slice(
         // eight independent loads in flight per wave instead of one
         // dependent round trip per hit; other lanes take the per-allele loop.
         if constexpr (NACC > 0) if (collect) {
-            const uint64_t row0 = Q.plane0_base + static_cast<uint64_t>(r - Q.rec_base) * Q.words;
+            // hit lane L scanned record base + L: its ALT-0 row is wave-uniform arithmetic
+            const uint64_t row_base = Q.plane0_base + static_cast<uint64_t>(base - Q.rec_base) * Q.words;
             uint64_t m1 = cm & __ballot(o.hm == 1ull);
             cm &= ~m1;
             while (m1) {
@@ -579,7 +580,7 @@ __device__ __forceinline__ void scan_slice(
                     if (m1) {
                         const int L = ffs64(m1);
                         m1 &= m1 - 1;
-                        rows[u] = static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(row0), L));
+                        rows[u] = row_base + static_cast<uint64_t>(L) * Q.words;
                         nb = u + 1;
                     }
                 }
