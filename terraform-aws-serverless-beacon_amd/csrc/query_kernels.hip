@@ -182,9 +182,8 @@ __device__ __forceinline__ bool wild_char(uint8_t c, uint8_t p) {
 }
 
 __device__ bool ref_wild_match(const DStore &st, uint32_t r, uint32_t ref_len, const uint8_t *__restrict__ pat,
-                               uint32_t plen) {
+                               uint32_t plen, uint64_t key) {
     if (ref_len != plen) return false;
-    const uint64_t key = st.ref_key[r];
     if (!(key >> 63)) {
         for (uint32_t i = 0; i < plen; ++i)
             if (!wild_char(static_cast<uint8_t>(key >> (8 * i)), pat[i])) return false;
@@ -256,8 +255,11 @@ struct QView {  // per-wave query constants, specialised by MODE
 
 // General evaluation of record r (RecHot h already loaded); extra ALTs and
 // hashed-key confirmations are loaded on demand.
+// pre_pos / pre_key: POS and ref_key of record r when the caller streamed
+// them ahead with the record word (have_pre), so REF_WILD costs no dependent load
 __device__ __forceinline__ LaneOut eval_record(const DStore &st, const QDev &Q, const QView &V, uint32_t r,
-                                            const RecHot h0) {
+                                            const RecHot h0, bool have_pre = false, uint32_t pre_pos = 0,
+                                            uint64_t pre_key = 0) {
     LaneOut o{0, 0, 0, 0, 0};
     const uint32_t e = h0.end;
     const uint32_t h = h0.hot;
@@ -273,7 +275,8 @@ __device__ __forceinline__ LaneOut eval_record(const DStore &st, const QDev &Q, 
                 break;
             }
             case REF_WILD:
-                pass = ref_wild_match(st, r, e - st.pos[r] + 1, V.qref, Q.ref_len);
+                pass = have_pre ? ref_wild_match(st, r, e - pre_pos + 1, V.qref, Q.ref_len, pre_key)
+                                : ref_wild_match(st, r, e - st.pos[r] + 1, V.qref, Q.ref_len, st.ref_key[r]);
                 break;
             case REF_NEVER:
                 pass = false;
@@ -553,12 +556,29 @@ __device__ __forceinline__ void scan_slice(
     uint64_t *out = hits + Q.hit_off;
 
     RecHot cur = {0, 0, 0, 0}, nxt = {0, 0, 0, 0};
-    if (lo + static_cast<uint32_t>(lane) < hi) cur = st.rec[lo + lane];
+    // samples variant with a wildcard REF (svs:88-91): POS and ref_key are
+    // streamed one chunk ahead with the record word
+    const bool pre = kGeneral && V.ref_mode == REF_WILD;
+    uint32_t cpos = 0, npos = 0;
+    uint64_t ckey = 0, nkey = 0;
+    if (lo + static_cast<uint32_t>(lane) < hi) {
+        cur = st.rec[lo + lane];
+        if (pre) {
+            cpos = st.pos[lo + lane];
+            ckey = st.ref_key[lo + lane];
+        }
+    }
     for (uint32_t base = lo; base < hi; base += kWave) {
         const uint32_t r = base + static_cast<uint32_t>(lane);
-        if (r + kWave < hi) nxt = st.rec[r + kWave];
+        if (r + kWave < hi) {
+            nxt = st.rec[r + kWave];
+            if (pre) {
+                npos = st.pos[r + kWave];
+                nkey = st.ref_key[r + kWave];
+            }
+        }
         LaneOut o{0, 0, 0, 0, 0};
-        if (r < hi) o = eval_record(st, Q, V, r, cur);
+        if (r < hi) o = eval_record(st, Q, V, r, cur, pre, cpos, ckey);
         uint64_t cm;
         const int s = chunk_tail<NONNEG>(S, o, r, stop_on_exists, details, out, &cm);
         if (s < kWave && S.err_out) break;
@@ -615,6 +635,8 @@ __device__ __forceinline__ void scan_slice(
             }
         }
         cur = nxt;
+        cpos = npos;
+        ckey = nkey;
         if (s < kWave) break;
     }
     finish_query<NONNEG>(S, Q.orig, hi - lo, res);
