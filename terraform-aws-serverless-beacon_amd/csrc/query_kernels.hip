@@ -875,6 +875,189 @@ __device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
     finish_query<NONNEG>(S, Q.orig, hi - lo, res);
 }
 
+// ---------------------------------------------------------------- packed variantType slices
+// A variantType slice has a few candidates (about 3 % of its records), so a
+// wave spent on one slice leaves most lanes idle and pays the chunk_tail /
+// finish_query reductions per slice.  Here four slices of a run share one
+// 64-lane pass, 16 lanes (candidates) each, with segmented sums and prefix
+// counts over each 16-lane group.  A slice is packed only when its answer
+// needs none of the order-dependent machinery: <= 16 candidates in its END
+// window, include_details and no boolean break (nothing stops the loop,
+// :229-232 / :253-254), a non-negative-AC store and no VT_SLOW candidate (no
+// exception can occur).  Then exists = some hit has AC > 0 (the cumulative
+// call_count of :229), call_count / all_alleles_count are sums over the hit
+// records (:214, :244) and hits are written in record-then-ALT order --
+// exactly what vt_slice + chunk_tail produce for it.  Other slices of the
+// run go through vt_slice.
+constexpr uint32_t kPackLanes = 16;
+constexpr uint32_t kPackPasses = 2;  // a run's slices (kRun = 8) / 4 per pass
+
+__device__ __forceinline__ int64_t seg16_sum_i64(int64_t v) {
+#pragma unroll
+    for (int m = 1; m < static_cast<int>(kPackLanes); m <<= 1) {
+        const int lo = __shfl_xor(static_cast<int>(static_cast<uint64_t>(v) & 0xffffffffu), m, kWave);
+        const int hi = __shfl_xor(static_cast<int>(static_cast<uint64_t>(v) >> 32), m, kWave);
+        v += static_cast<int64_t>((static_cast<uint64_t>(static_cast<uint32_t>(hi)) << 32) | static_cast<uint32_t>(lo));
+    }
+    return v;
+}
+
+template <bool NONNEG>
+struct VtPack {
+    const DStore *st;
+    const QDev *qs;
+    QRes *res;
+    uint64_t *hits;
+    // q / bound / abound as run_slices holds them (lanes 2j, 2j+1 = slice j);
+    // returns the mask of run slices answered here (wave-uniform)
+    __device__ __forceinline__ uint32_t operator()(uint32_t n, uint32_t q, uint32_t bound, uint32_t abound) const {
+        if constexpr (!NONNEG) {
+            return 0u;
+        } else {
+            const DStore &D = *st;
+            const uint32_t lane = static_cast<uint32_t>(lane_id());
+            const uint32_t g = lane / kPackLanes, k = lane % kPackLanes;
+            const uint64_t gm = 0xffffull << (kPackLanes * g);
+            uint32_t handled = 0;
+            // every load of both passes first (query fields, candidate words:
+            // their addresses come from shuffles only), then the evaluation
+            uint32_t a_lo[kPackPasses], a_hi[kPackPasses], a_alo[kPackPasses], a_ahi[kPackPasses];
+            VcWord a_x[kPackPasses];
+            QDev a_Q[kPackPasses];
+#pragma unroll
+            for (uint32_t p = 0; p < kPackPasses; ++p) {
+                const uint32_t j = p * 4 + g;
+                const bool vs = j < n;
+                const int src = vs ? static_cast<int>(2 * j) : 0;
+                const uint32_t qj = __shfl(q, src, kWave);
+                a_lo[p] = __shfl(bound, src, kWave);
+                a_hi[p] = max(a_lo[p], __shfl(bound, src + 1, kWave));
+                a_alo[p] = __shfl(abound, src, kWave);
+                a_ahi[p] = __shfl(abound, src + 1, kWave);
+                const uint32_t span = a_ahi[p] > a_alo[p] ? a_ahi[p] - a_alo[p] : 0u;
+                a_x[p] = VcWord{VtHot{0, 0, 0, 0}, 0};
+                if (vs && k < span && span <= kPackLanes)  // inside the kind's list: safe to load early
+                    a_x[p] = VcWord{D.vc_word[a_alo[p] + k], D.vc_idx[a_alo[p] + k]};
+                const QDev &G = qs[qj];
+                a_Q[p].flags = G.flags;
+                a_Q[p].end_min = G.end_min;
+                a_Q[p].end_max = G.end_max;
+                a_Q[p].vmin = G.vmin;
+                a_Q[p].vmax = G.vmax;
+                a_Q[p].vt_kind = G.vt_kind;
+                a_Q[p].lut_off = G.lut_off;
+                a_Q[p].hit_off = G.hit_off;
+                a_Q[p].orig = G.orig;
+            }
+#pragma unroll
+            for (uint32_t p = 0; p < kPackPasses; ++p) {
+                if (p * 4 >= n) break;
+                const uint32_t j = p * 4 + g;
+                const bool vs = j < n;
+                const uint32_t lo = a_lo[p], hi = a_hi[p], alo = a_alo[p], ahi = a_ahi[p];
+                const QDev &Q = a_Q[p];
+                const uint32_t flags = Q.flags;
+                const bool end_void = Q.end_max < 0 || Q.end_min > 0xffffffffll || Q.end_min > Q.end_max;
+                // vt_slice: shi = end_void ? lo : hi; c_hi = shi > lo ? c_hi_all : c_lo
+                const uint32_t c_hi = (!end_void && hi > lo) ? ahi : alo;
+                const uint32_t ncand = c_hi > alo ? c_hi - alo : 0u;
+                bool ok = vs && ncand <= kPackLanes && (flags & F_DETAILS) && !(flags & F_BOOL_BREAK);
+                const bool has = ok && k < ncand;
+                const VcWord x = a_x[p];
+                const uint32_t e0 = Q.end_min < 0 ? 0u : static_cast<uint32_t>(Q.end_min);
+                const uint32_t espan = (Q.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_max)) - e0;
+                const bool cand = has && x.h.end - e0 <= espan;
+                const uint64_t slowm = __ballot(cand && (x.h.w & VT_SLOW));
+                ok = ok && !(slowm & gm);
+                const uint64_t okm = __ballot(ok && k == 0);
+                if (!okm) continue;
+                // lane_eval of vt_slice with this lane's slice parameters
+                LaneOut o{0, 0, 0, 0, 0};
+                const int64_t vl = Q.vmin < 0 ? 0 : Q.vmin, vh = Q.vmax > 255 ? 255 : Q.vmax;
+                const uint32_t vlo = vh < vl ? 256u : static_cast<uint32_t>(vl);
+                const uint32_t vspan = vh < vl ? 0u : static_cast<uint32_t>(vh - vl);
+                const uint32_t vk = Q.vt_kind;
+                constexpr uint32_t kDel = vt_class_mask(VT_DEL), kIns = vt_class_mask(VT_INS),
+                                   kDup = vt_class_mask(VT_DUP), kDupT = vt_class_mask(VT_DUPT),
+                                   kCnv = vt_class_mask(VT_CNV);
+                const uint32_t cmask = vk == VT_DEL ? kDel : vk == VT_INS ? kIns : vk == VT_DUP ? kDup
+                                     : vk == VT_DUPT ? kDupT : vk == VT_CNV ? kCnv : 0u;
+                const uint32_t xneed = vt_xk_bit(vk) | VT_XK_SYM;
+                const uint32_t *lut = D.sym_lut + Q.lut_off;
+                auto alt_ok = [&](uint32_t aw, uint32_t lw) -> bool {
+                    if ((aw & 0xffu) - vlo > vspan) return false;
+                    if (aw & VT_SYM) return (lw >> ((aw >> 16) & 31u)) & 1u;
+                    return (cmask >> ((aw >> VT_CLASS_SHIFT) & 31u)) & 1u;
+                };
+                const bool ev = ok && cand;
+                if (ev) {
+                    const uint32_t lw0 = (x.h.w & VT_SYM) ? lut[(x.h.w >> 21) & 7u] : 0u;
+                    uint64_t hm = alt_ok(x.h.w, lw0) ? 1ull : 0ull;
+                    const uint32_t nx = (x.h.w & xneed) ? x.h.w >> VT_NX_SHIFT : 0u;
+                    uint32_t x0 = 0;
+                    if (nx) {  // ALTs 2..n (:124 loop)
+                        x0 = D.x_lo[x.r];
+                        for (uint32_t t = 0; t < nx; ++t) {
+                            const uint32_t xw = D.xvt[x0 + t];
+                            if (alt_ok(xw, (xw & VT_SYM) ? lut[(xw >> 21) & 7u] : 0u)) hm |= 2ull << t;
+                        }
+                    }
+                    if (hm) {  // :205-214
+                        if (hm == 1ull) {
+                            o.c = x.h.ac0;
+                            o.em = x.h.ac0 != 0 ? 1ull : 0ull;
+                        } else {
+                            for (uint64_t b = hm; b; b &= b - 1) {
+                                const int a = ffs64(b);
+                                const int64_t v = a ? D.xrow[x0 + a - 1].ac : x.h.ac0;
+                                o.c += v;
+                                if (v != 0) o.em |= 1ull << a;
+                            }
+                        }
+                        o.hm = hm;
+                        o.anv = x.h.an;
+                    }
+                }
+                const bool hit = o.hm != 0;
+                const uint32_t cnt = hit ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
+                uint32_t pos0, total;
+                if (!__ballot(cnt > 1)) {
+                    const uint64_t one = __ballot(cnt == 1) & gm;
+                    pos0 = popc_below(one);
+                    total = static_cast<uint32_t>(__popcll(one));
+                } else {  // bit-sliced exclusive prefix within the 16-lane group
+                    pos0 = 0;
+                    total = 0;
+                    for (uint32_t b = 0; b < 7; ++b) {
+                        const uint64_t m = __ballot((cnt >> b) & 1u) & gm;
+                        pos0 += popc_below(m) << b;
+                        total += static_cast<uint32_t>(__popcll(m)) << b;
+                        if (!__ballot(cnt >> (b + 1))) break;
+                    }
+                }
+                if (cnt) {
+                    uint64_t *dst = hits + Q.hit_off + pos0;
+                    for (uint64_t b = o.em; b; b &= b - 1)
+                        *dst++ = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
+                }
+                const int64_t cc = seg16_sum_i64(hit ? o.c : 0);
+                const int64_t an = seg16_sum_i64(hit ? o.anv : 0);
+                const bool ex = (__ballot(hit && o.c > 0) & gm) != 0ull;
+                if (ok && k == 0) res[Q.orig] = QRes{0, ex ? 1 : 0, cc, an, total, hi - lo};
+#pragma unroll
+                for (uint32_t t = 0; t < 4; ++t)
+                    if ((okm >> (kPackLanes * t)) & 1ull) handled |= 1u << (p * 4 + t);
+            }
+            return handled;
+        }
+    }
+};
+
+// no packed path
+struct NoPack {
+    __device__ __forceinline__ uint32_t operator()(uint32_t, uint32_t, uint32_t, uint32_t) const { return 0u; }
+};
+
 // Gather each query's hits from its planned region into a dense array
 // (result shipping at fetch time; not part of the timed query step).
 // ---------------------------------------------------------------- slice runs
@@ -888,11 +1071,12 @@ __device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
 // evaluated in order with their [lo, hi) already known: the setup latency is
 // paid once per run.  Bounds are those of slice_bounds.
 constexpr uint32_t kRun = 8;
+static_assert(kPackPasses * (kWave / kPackLanes) == kRun, "packed passes cover a whole run");
 
-template <class Body, class Aux>
+template <class Body, class Aux, class Pack>
 __device__ __forceinline__ void run_slices(const DStore &st, const QDev *__restrict__ qs,
                                            const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run, uint32_t w,
-                                           Body body, Aux aux) {
+                                           Body body, Aux aux, Pack pack) {
     const uint32_t first = w * run;
     if (first >= nq) return;
     const uint32_t n = min(run, nq - first);
@@ -938,7 +1122,9 @@ __device__ __forceinline__ void run_slices(const DStore &st, const QDev *__restr
     const uint32_t other = __shfl(bound, static_cast<int>(lane ^ 1u), kWave);  // the slice's other bound
     uint32_t abound = 0;
     if (lane < nb) abound = aux(qs[q], upper ? max(bound, other) : bound);
+    const uint32_t packed = pack(n, q, bound, abound);  // run slices answered in packed passes
     for (uint32_t sj = 0; sj < n; ++sj) {
+        if ((packed >> sj) & 1u) continue;
         const uint32_t lo = rdl(bound, 2 * sj);
         body(rdl(q, 2 * sj), lo, max(lo, rdl(bound, 2 * sj + 1)), rdl(abound, 2 * sj), rdl(abound, 2 * sj + 1));
     }
@@ -963,12 +1149,12 @@ struct NoAux {
     __device__ __forceinline__ uint32_t operator()(const QDev &, uint32_t) const { return 0; }
 };
 
-template <bool RUN, class Body, class Aux = NoAux>
+template <bool RUN, class Body, class Aux = NoAux, class Pack = NoPack>
 __device__ __forceinline__ void slices(const DStore &st, const QDev *__restrict__ qs,
                                        const uint32_t *__restrict__ qidx, uint32_t nq, uint32_t run, uint32_t w,
-                                       Body body, Aux aux = Aux()) {
+                                       Body body, Aux aux = Aux(), Pack pack = Pack()) {
     if constexpr (RUN)
-        run_slices(st, qs, qidx, nq, run, w, body, aux);
+        run_slices(st, qs, qidx, nq, run, w, body, aux, pack);
     else
         one_slice(st, qs, qidx, nq, w, body, aux);
 }
@@ -1023,7 +1209,7 @@ __global__ __launch_bounds__(kBlock) void vt_kernel(DStore st, const QDev *__res
                                                     QRes *__restrict__ res, uint64_t *__restrict__ hits) {
     slices<RUN>(st, qs, qidx, nq, run, launch_wave(), [&](uint32_t q, uint32_t lo, uint32_t hi, uint32_t alo, uint32_t ahi) {
         vt_slice<NONNEG>(st, qs, res, hits, q, lo, hi, alo, ahi);
-    }, VcAux{&st});
+    }, VcAux{&st}, VtPack<NONNEG>{&st, qs, res, hits});
 }
 
 // All sample-free groups of a batch in one launch: group g owns waves
