@@ -96,6 +96,15 @@ def main_genome(args):
     uniq = union_rows(shape, sl)
     scan_bytes = 32.0 * uniq + 8.0 * hits
     achieved = scan_bytes / (timing['scan_ms'] * 1e-3) / 1e9 if timing['scan_ms'] > 0 else 0.0
+    traffic = None  # HBM bytes per step from the PMC passes (tools/gpu_pmc_genome_traffic.sh)
+    tf = os.path.join(REPO, 'profiles', 'traffic_genome.json')
+    if world == 1 and os.path.exists(tf):
+        try:
+            tj = json.load(open(tf))
+            if tj.get('records') == shape.n_total and tj.get('requests') == len(reqs):
+                traffic = tj.get('scan_kernel_hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
     vals = [elapsed, timing['scan_ms'], float(len(sl)), float(scanned), float(hits), achieved, float(uniq)]
     if dist:
         t = torch.tensor(vals, dtype=torch.float64, device='cuda')
@@ -132,7 +141,7 @@ def main_genome(args):
         'device_ms_per_step': {'query_kernels_rank0': round(timing['scan_ms'], 4),
                                'query_kernels_max': round(max(v[1] for v in allv), 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(allv[0][5], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(allv[0][5] / HBM_PEAK_GBS, 4), 'traffic': None,
+                     'frac': round(allv[0][5] / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'kernel': 'rank 0 query step: vt_kernel (the batch is one variantType group) + request_reduce_kernel; HIP events spanning the step',
                      'algorithmic_bytes_per_launch': 32.0 * allv[0][6] + 8.0 * allv[0][4],
                      'unique_rows_per_launch': int(allv[0][6]),

@@ -20,7 +20,7 @@ import os
 import re
 import sys
 
-PHASE = re.compile(r'(fused_kernel|range_n8?_kernel|vt_kernel|scan_kernel)')
+PHASE = re.compile(r'(fused_kernel|range_n8?_kernel|vt_kernel|scan_kernel|request_reduce_kernel)')
 
 
 def load(d, counter):
