@@ -143,3 +143,39 @@ def test_attached_carriers_match_oracle_and_gt_store(small_gnomad):
         assert normalise(rs2.response(i).dump()) == got
         n_samp += bool(got['sample_indices'])
     assert n_samp > 150  # the sample-subset path was exercised
+
+
+@pytest.mark.gpu
+def test_flat_carrier_rows_2504_samples(tmp_path):
+    """40-word carrier rows (2,504 samples) take the flattened sample path
+    (8 rows = 5 full-wave loads, query_kernels.hip scan_slice); every
+    includeSamples / sample-subset response equals the oracle's on the GT text."""
+    import random
+
+    from oracle.oracle import OracleVcf
+    from sbeacon.engine import Store
+    from sbeacon.workload import SyntheticVcf, config2_requests, requests_to_payloads
+    gen = SyntheticVcf(seed=41, n_records=3000, n_samples=2504, mean_gap=60.0)
+    path = str(tmp_path / 'wide.vcf')
+    gen.write(path, sites_only=False)
+    store = Store.build([('w.vcf', path)], device=0)
+    reqs = config2_requests(gen, n_range=200, n_point=0, seed=78)
+    payloads, _ = requests_to_payloads(reqs, vcf_location='w.vcf', chrom='22')
+    names = gen.sample_names()
+    rng = random.Random(9)
+    for p in payloads:
+        if rng.random() < 0.5:
+            p['passthrough'] = {'includeSamples': True}
+        else:
+            pick = rng.sample(names, rng.choice([10, 300, 2504]))
+            p['passthrough'] = {'sampleNames': pick, 'selectedSamplesOnly': True, 'includeSamples': True}
+        p['requested_granularity'] = 'record'
+        p['include_details'] = True
+    exp = OracleVcf(path).perform_query_batch(payloads)
+    rs = store.query(payloads)
+    n_samp = 0
+    for i, (p, e) in enumerate(zip(payloads, exp)):
+        got = normalise(rs.response(i).dump())
+        assert got == normalise(e), (p['region'], p['passthrough'].keys())
+        n_samp += len(got['sample_indices']) > 64
+    assert n_samp > 20  # rows past the first 64 samples were collected
