@@ -158,6 +158,7 @@ typedef struct {
     uint64_t records_scanned; /* records with POS inside each slice, summed */
     uint64_t hits;
     double device_ms;         /* HIP-event time of the kernel sequence */
+    uint64_t chained_slices;  /* slices answered by the chain kernel (one wave per request) */
 } sb_batch_stats;
 int sb_result_stats(const sb_result_set *r, sb_batch_stats *out);
 void sb_result_free(sb_result_set *r);

@@ -184,6 +184,14 @@ struct sb_batch {
         uint32_t base;  // first entry of the group in the launch-ordered device array
     };
     std::vector<Group> groups;
+    // slice chains (ChainDev): their slices sit after the groups in the
+    // launch-ordered array; n_scanned of a chained slice is known on the host
+    std::vector<ChainDev> hchains;
+    DevMem chains;
+    std::vector<uint8_t> chained;
+    std::vector<uint32_t> nscan;
+    std::vector<uint32_t> chain_members;  // chained queries, chain by chain
+    uint32_t chain_base = 0;              // first chained slice in the launch-ordered array
     bool nonneg = true;
     // per-request rows (sb_batch_set_owners): seg = n_rows + 1 query offsets
     uint32_t n_rows = 0;
@@ -426,12 +434,63 @@ void upload_store(sb_builder &b, sb_store &s) {
             if (n % 64 == 0) blk[k * nblk + n / 64].pre = static_cast<uint32_t>(cw.size());
         }
         if (cw.size() > 0xffffffffull) throw Error(SB_EINVAL, "variantType candidate index exceeds 2^32 entries");
+        // candidate POS column + the coarse candidate index of every (segment,
+        // kind) pair, aiming at ~8 candidates per bucket (chain_kernel)
+        std::vector<uint32_t> cpos(cw.size() + 1, 0u);
+        for (size_t j = 0; j < ci.size(); ++j) cpos[j] = pos[ci[j]];
+        auto cand_before = [&](uint32_t k, uint64_t r) -> uint32_t {  // global list index
+            const VcBlock &b = blk[k * nblk + r / 64];
+            const uint32_t o = static_cast<uint32_t>(r % 64);
+            return b.pre + static_cast<uint32_t>(__builtin_popcountll(o ? (b.mask & ((1ull << o) - 1ull)) : 0ull));
+        };
+        std::vector<uint32_t> vcb;
+        for (auto &v : b.vcfs) {
+            v.vc_index.assign(v.segments.size(), std::array<VcIndex, kVtKinds>{});
+            for (size_t g = 0; g < v.segments.size(); ++g) {
+                const Segment &sg = v.segments[g];
+                for (uint32_t k = 0; k < kVtKinds; ++k) {
+                    VcIndex &x = v.vc_index[g][k];
+                    x.c_lo = cand_before(k, sg.lo);
+                    x.c_hi = cand_before(k, sg.hi);
+                    x.off = vcb.size();
+                    const uint32_t nc = x.c_hi - x.c_lo;
+                    if (nc == 0) {
+                        x.base = 0;
+                        x.shift = 31;
+                        x.n = 1;
+                        vcb.push_back(x.c_lo);
+                        vcb.push_back(x.c_hi);
+                        continue;
+                    }
+                    x.base = cpos[x.c_lo];
+                    const uint64_t span = static_cast<uint64_t>(cpos[x.c_hi - 1]) - x.base;
+                    const double gap = nc > 1 ? static_cast<double>(span) / static_cast<double>(nc - 1) : 1.0;
+                    uint32_t shift = 0;
+                    while (shift < 31 && static_cast<double>(1ull << (shift + 1)) <= gap * 8.0) ++shift;
+                    const uint64_t nb = (span >> shift) + 1;
+                    x.shift = shift;
+                    x.n = static_cast<uint32_t>(nb);
+                    uint32_t j = x.c_lo;
+                    for (uint64_t bb = 0; bb <= nb; ++bb) {
+                        const uint64_t at = static_cast<uint64_t>(x.base) + (bb << shift);
+                        while (j < x.c_hi && cpos[j] < at) ++j;
+                        vcb.push_back(j);
+                    }
+                    vcb.back() = x.c_hi;
+                }
+            }
+        }
+        s.h_vt_slow.clear();
+        for (size_t i = 0; i < n; ++i)
+            if (vth[i].w & VT_SLOW) s.h_vt_slow.push_back(static_cast<uint32_t>(i));
         cw.push_back(VtHot{0, 0, 0, 0});  // clamp target of an empty candidate range
         ci.push_back(0);
         s.d.vc_word = dev_upload(s, cw);
         s.d.vc_idx = dev_upload(s, ci);
         s.d.vc_blk = dev_upload(s, blk);
         s.d.vc_nblk = nblk;
+        s.d.vc_pos = dev_upload(s, cpos);
+        s.d.vc_bucket = dev_upload(s, vcb);
     }
     s.d.pos = dev_upload(s, pos);
     s.d.ref_key = dev_upload(s, ref_key);
@@ -517,10 +576,145 @@ uint32_t bucket_ceil(const sb_store &s, const QDev &d, int64_t x) {
     return s.h_bucket[d.bucket_off + b + 1];
 }
 
+// run fn(i) for i in [0, n) on up to `threads` host threads
+template <class F>
+void parallel_for(size_t n, F fn, unsigned threads = 16) {
+    const unsigned t = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, n / 4096)));
+    if (t <= 1) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < t; ++k)
+        th.emplace_back([&, k] {
+            for (size_t i = n * k / t, e = n * (k + 1) / t; i < e; ++i) fn(i);
+        });
+    for (auto &x : th) x.join();
+}
+
+// Chains of consecutive variantType slices (devtypes.hpp ChainDev).  vt =
+// the MODE_VTYPE queries in input order; returns those left to vt_slice.
+// Slices chain when they share the VCF segment and every filter, each starts
+// one base past the previous one, the chain's first slice sets the width and
+// only its last may be shorter (splitQuery's [a, min(a + 9999, start_max)]),
+// interleaved with other VCFs' slices or not; a slice qualifies only without
+// order-dependent semantics (include_details, no boolean break, a VCF without
+// negative AC) and a chain is dissolved when a VT_SLOW record lies in its window.
+std::vector<uint32_t> plan_chains(sb_batch &B, const std::vector<uint32_t> &segi, const std::vector<uint32_t> &vt) {
+    sb_store &s = *B.s;
+    std::vector<uint32_t> rest;
+    const char *off = std::getenv("SBEACON_NO_CHAINS");
+    if (off && off[0] == '1') return vt;
+    struct Ch {
+        std::vector<uint32_t> m;
+        int64_t first = 0, last = 0, width = 0;
+    };
+    std::vector<Ch> ch;
+    std::unordered_map<std::string, uint32_t> open;  // filter signature + next first_bp -> chain
+    auto key = [&](const QDev &d, uint32_t i, int64_t next) {
+        struct {
+            uint32_t vcf, seg;
+            int64_t emin, emax, vmin, vmax, next;
+            uint32_t kind, lut, flags;
+        } k{B.vcf[i], d.seg_lo, d.end_min, d.end_max, d.vmin, d.vmax, next, d.vt_kind, d.lut_off, d.flags};
+        return std::string(reinterpret_cast<const char *>(&k), sizeof k);
+    };
+    for (uint32_t i : vt) {
+        const QDev &d = B.hq[i];
+        const bool ok = (d.flags & F_DETAILS) && (d.flags & F_NONNEG) &&
+                        !(d.flags & (F_BOOL_BREAK | F_EMPTY | F_STRICT_UNBOUND | F_SAMPLES_VARIANT)) &&
+                        d.samples_out_off == ~0ull && segi[i] != UINT32_MAX && d.first_bp >= 0 &&
+                        d.first_bp <= d.last_bp && d.last_bp <= 0xfffffffell;
+        if (!ok) {
+            rest.push_back(i);
+            continue;
+        }
+        const int64_t w = d.last_bp - d.first_bp + 1;
+        uint32_t c = UINT32_MAX;
+        auto it = open.find(key(d, i, d.first_bp));
+        if (it != open.end()) {
+            c = it->second;
+            open.erase(it);
+            if (w > ch[c].width) c = UINT32_MAX;  // wider than the chain's slices: a new chain
+        }
+        if (c == UINT32_MAX) {
+            c = static_cast<uint32_t>(ch.size());
+            ch.push_back(Ch{{}, d.first_bp, d.last_bp, w});
+        }
+        ch[c].m.push_back(i);
+        ch[c].last = d.last_bp;
+        if (w == ch[c].width && ch[c].m.size() < kChainMax) open[key(d, i, d.last_bp + 1)] = c;
+    }
+    // exact record range of every chained slice (n_scanned) and the VT_SLOW check
+    B.chained.assign(B.nq, 0);
+    B.nscan.assign(B.nq, 0);
+    std::vector<uint8_t> dissolve(ch.size(), 0);
+    parallel_for(ch.size(), [&](size_t c) {
+        const Ch &x = ch[c];
+        const QDev &d0 = B.hq[x.m[0]];
+        auto pb = s.h_pos.begin();
+        auto lb = [&](int64_t p) {
+            return static_cast<uint32_t>(std::lower_bound(pb + d0.seg_lo, pb + d0.seg_hi, static_cast<uint64_t>(p),
+                                                          [](uint32_t a, uint64_t b) { return a < b; }) - pb);
+        };
+        const uint32_t lo = lb(x.first), hi = lb(x.last + 1);
+        auto sl = std::lower_bound(s.h_vt_slow.begin(), s.h_vt_slow.end(), lo);
+        if (sl != s.h_vt_slow.end() && *sl < hi) {
+            dissolve[c] = 1;
+            return;
+        }
+        uint32_t a = lo;
+        for (uint32_t i : x.m) {
+            const uint32_t e = lb(B.hq[i].last_bp + 1);
+            B.nscan[i] = e - a;
+            a = e;
+        }
+    });
+    // chains in (segment, first base) order; ChainDev.q0 is set at upload
+    std::vector<uint32_t> order;
+    for (uint32_t c = 0; c < ch.size(); ++c) {
+        if (dissolve[c])
+            rest.insert(rest.end(), ch[c].m.begin(), ch[c].m.end());
+        else
+            order.push_back(c);
+    }
+    std::sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) {
+        const QDev &x = B.hq[ch[a].m[0]], &y = B.hq[ch[b].m[0]];
+        return x.seg_lo != y.seg_lo ? x.seg_lo < y.seg_lo : ch[a].first < ch[b].first;
+    });
+    B.hchains.clear();
+    B.chain_members.clear();
+    for (uint32_t c : order) {
+        const Ch &x = ch[c];
+        const uint32_t i0 = x.m[0];
+        const QDev &d = B.hq[i0];
+        const VcIndex &vi = s.vcfs[B.vcf[i0]].vc_index[segi[i0]][d.vt_kind];
+        ChainDev cd{};
+        cd.n = static_cast<uint32_t>(x.m.size());
+        cd.first = static_cast<uint32_t>(x.first);
+        cd.last = static_cast<uint32_t>(x.last);
+        cd.width = static_cast<uint32_t>(x.width);
+        cd.c_lo = vi.c_lo;
+        cd.c_hi = vi.c_hi;
+        cd.cb_base = vi.base;
+        cd.cb_off = vi.off;
+        cd.cb_shift = vi.shift;
+        cd.cb_n = vi.n;
+        B.hchains.push_back(cd);
+        for (uint32_t i : x.m) {
+            B.chained[i] = 1;
+            B.chain_members.push_back(i);
+        }
+    }
+    std::sort(rest.begin(), rest.end());
+    return rest;
+}
+
 void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     sb_store &s = *B.s;
     if (nq >= (1u << 31)) throw Error(SB_EINVAL, "batch too large");
     B.nq = static_cast<uint32_t>(nq);
+    std::vector<uint32_t> segi(nq, UINT32_MAX);  // segment index of each query in its VCF
     B.hq.assign(nq, QDev{});
     B.host_err.assign(nq, 0);
     B.chrom.assign(nq, std::string());
@@ -561,6 +755,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         } else {
             const Segment &sg = v.segments[it->second];
             const BucketIndex &bi = v.buckets[it->second];
+            segi[i] = it->second;
             d.seg_lo = sg.lo;
             d.seg_hi = sg.hi;
             d.bucket_off = bi.off;
@@ -728,6 +923,10 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
             }
             B.groups[static_cast<size_t>(g)].idx.push_back(i);
         }
+        {  // variantType slices of one request -> chains (chain_kernel); the rest stay with vt_slice
+            auto &vg = B.groups[MODE_VTYPE].idx;
+            vg = plan_chains(B, segi, vg);
+        }
         std::vector<sb_batch::Group> keep;
         for (auto &g : B.groups)
             if (!g.idx.empty()) keep.push_back(std::move(g));
@@ -757,6 +956,19 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         g.base = static_cast<uint32_t>(lq.size());
         for (uint32_t i : g.idx) lq.push_back(B.hq[i]);
     }
+    B.chain_base = static_cast<uint32_t>(lq.size());
+    {
+        uint32_t at = B.chain_base;
+        for (ChainDev &c : B.hchains) {
+            c.q0 = at;
+            at += c.n;
+        }
+        for (uint32_t i : B.chain_members) lq.push_back(B.hq[i]);
+    }
+    B.chains.alloc(B.hchains.size() * sizeof(ChainDev));
+    if (!B.hchains.empty())
+        HIP_OK(hipMemcpyAsync(B.chains.p, B.hchains.data(), B.hchains.size() * sizeof(ChainDev), hipMemcpyHostToDevice,
+                              st));
     std::vector<uint64_t> hoff(nq);
     for (uint32_t i = 0; i < nq; ++i) hoff[i] = B.hq[i].hit_off;
     B.q.alloc(nq * sizeof(QDev));
@@ -789,6 +1001,9 @@ void run(sb_batch &B) {
         for (auto &e : B.ev) HIP_OK(hipEventCreate(&e));
     }
     if (B.runs_pending++ == 0) HIP_OK(hipEventRecord(B.ev[0], st));
+    // chains of variantType slices (one wave per request's slices)
+    launch_chains(d, B.q.as<QDev>(), B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()),
+                  B.res.as<QRes>(), B.hits.as<uint64_t>(), st);
     // sample-free groups: one fused launch, long scans first (range, variantType,
     // general) and point lookups last, so the short waves fill the tail
     std::vector<FusedGroup> fg;
@@ -830,8 +1045,10 @@ sb_result_set *fetch(sb_batch &B) {
     std::vector<uint64_t> sout(B.samples_words);
     if (!sout.empty()) HIP_OK(hipMemcpyAsync(sout.data(), B.samples_out.p, sout.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    for (uint32_t i = 0; i < nq; ++i)
+    for (uint32_t i = 0; i < nq; ++i) {
         if (B.host_err[i]) R->res[i].error = B.host_err[i];
+        if (!B.chained.empty() && B.chained[i]) R->res[i].n_scanned = B.nscan[i];
+    }
     // dense offsets on the host, gather on the device, one D2H
     R->dense_off.assign(size_t(nq) + 1, 0);
     for (uint32_t i = 0; i < nq; ++i) R->dense_off[i + 1] = R->dense_off[i] + (R->res[i].error ? 0 : R->res[i].n_hits);
@@ -882,6 +1099,7 @@ sb_result_set *fetch(sb_batch &B) {
     }
     R->stats.n_queries = nq;
     R->stats.records_scanned = scanned;
+    R->stats.chained_slices = B.chain_members.size();
     R->stats.hits = total;
     R->stats.device_ms = B.last_total_ms;
     return R.release();
@@ -1549,6 +1767,7 @@ int sb_batch_get_stats(const sb_batch *b, sb_batch_stats *out) {
     if (!b || !out) return SB_EINVAL;
     out->n_queries = b->nq;
     out->records_scanned = 0;
+    out->chained_slices = b->chain_members.size();
     out->hits = b->cap_total;
     out->device_ms = b->last_total_ms;
     return SB_OK;

@@ -117,6 +117,30 @@ struct alignas(16) VcBlock {
     uint32_t pre;   // candidates of this kind before record 64 b (+ vc_off[k])
     uint32_t pad;
 };
+// Slice chains (MODE_VTYPE): splitQuery cuts one request into consecutive
+// 10 kb slices that share every filter (lambda/splitQuery/lambda_function.py:
+// 82-106).  When none of them needs the order-dependent machinery
+// (include_details, no boolean break, non-negative AC, no VT_SLOW record in
+// the window) a chain of up to kChainMax such slices is answered by ONE wave:
+// the chain's candidate range comes from a per-(kind, segment) coarse index
+// over candidate POS (vc_bucket: entry b = first candidate of the pair with
+// POS >= base + (b << shift)), each candidate lane filters POS against the
+// chain window and finds its slice as (POS - first) / width, and per-slice
+// sums / hit positions are kept in LDS.  Per-slice QRes and hit regions are
+// exactly what vt_slice writes for each slice alone.
+constexpr uint32_t kChainMax = 32;
+struct alignas(16) ChainDev {
+    uint32_t q0;        // first slice in the launch-ordered QDev array (slices q0 .. q0 + n - 1)
+    uint32_t n;         // slices, 1 .. kChainMax
+    uint32_t first;     // first_bp of slice 0
+    uint32_t last;      // last_bp of slice n - 1
+    uint32_t width;     // slices 0 .. n-2 span exactly `width` bp; the last at most that
+    uint32_t c_lo, c_hi;  // the (kind, segment) pair's candidates
+    uint32_t cb_base;   // coarse candidate index of the pair (vc_bucket)
+    uint64_t cb_off;
+    uint32_t cb_shift, cb_n;
+};
+
 // bit c set = an ALT of class c satisfies variantType `kind` (vtype_hit)
 __host__ __device__ constexpr uint32_t vt_class_mask(uint32_t kind) {
     uint32_t m = 0;
@@ -191,6 +215,8 @@ struct DStore {
     const uint32_t *vc_idx;
     const VcBlock *vc_blk;    // [kVtKinds][vc_nblk]
     uint64_t vc_nblk;
+    const uint32_t *vc_pos;   // POS of each candidate (parallel to vc_word)
+    const uint32_t *vc_bucket;  // coarse POS index per (kind, segment) over candidates (ChainDev)
     const uint32_t *pos;
     const uint64_t *ref_key;  // key(REF.upper())
     const uint64_t *a0_key;   // key(ALT0.upper())

@@ -32,6 +32,11 @@ struct FusedGroup {
 void launch_fused(const DStore &st, const FusedGroup *groups, int count, bool nonneg,
                   const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, hipStream_t s);
 
+// Slice chains (devtypes.hpp ChainDev): one wave per chain of consecutive
+// variantType slices of one request; q = the launch-ordered QDev array.
+void launch_chains(const DStore &st, const QDev *q, const ChainDev *chains, uint32_t n_chains, QRes *res,
+                   uint64_t *hits, hipStream_t s);
+
 // summariseSlice: phase A = one workgroup per chunk of kSumChunk records
 // (chunk_slice[c] = its slice), reducing the records' (numVariants, numCalls)
 // contributions into part[c] and writing the overshoot bitmap; phase B = one

@@ -766,54 +766,46 @@ __device__ __forceinline__ uint32_t vc_count(const DStore &st, uint32_t k, uint3
     return b.pre + static_cast<uint32_t>(__popcll(o ? (b.mask & ((1ull << o) - 1ull)) : 0ull));
 }
 
-template <bool NONNEG>
-__device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs, QRes *__restrict__ res,
-                                         uint64_t *__restrict__ hits, uint32_t q, uint32_t lo, uint32_t hi,
-                                         uint32_t c_lo, uint32_t c_hi_all) {
-    const int lane = lane_id();
-    const QDev &Q = qs[q];
-    if (c_hi_all <= c_lo) {  // no candidate of this kind in the slice: nothing can hit or raise
-        if (lane == 0) res[Q.orig] = QRes{0, 0, 0, 0, 0, hi - lo};
-        return;
-    }
-    const uint32_t flags = Q.flags;
-    const bool details = flags & F_DETAILS;
-    const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
-    ScanState S;
-    const bool end_void = Q.end_max < 0 || Q.end_min > 0xffffffffll || Q.end_min > Q.end_max;
-    // END in [e0, e0 + espan] and len(ALT0) in [vlo, vlo + vspan] as one
-    // unsigned compare each; an empty length range never matches (vlo = 256)
-    const uint32_t e0 = Q.end_min < 0 ? 0u : static_cast<uint32_t>(Q.end_min);
-    const uint32_t espan = (Q.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_max)) - e0;
-    const int64_t vl = Q.vmin < 0 ? 0 : Q.vmin, vh = Q.vmax > 255 ? 255 : Q.vmax;
-    const uint32_t vlo = vh < vl ? 256u : static_cast<uint32_t>(vl);
-    const uint32_t vspan = vh < vl ? 0u : static_cast<uint32_t>(vh - vl);
-    const uint32_t vk = Q.vt_kind;
-    constexpr uint32_t kDel = vt_class_mask(VT_DEL), kIns = vt_class_mask(VT_INS), kDup = vt_class_mask(VT_DUP),
-                       kDupT = vt_class_mask(VT_DUPT), kCnv = vt_class_mask(VT_CNV);
-    const uint32_t cmask = vk == VT_DEL ? kDel : vk == VT_INS ? kIns : vk == VT_DUP ? kDup : vk == VT_DUPT ? kDupT
-                         : vk == VT_CNV ? kCnv : 0u;
-    const uint32_t xneed = vt_xk_bit(vk) | VT_XK_SYM;  // an extra ALT might match
-    const uint32_t *lut = st.sym_lut + Q.lut_off;
-    uint64_t *out = hits + Q.hit_off;
-    const QView V{flags, REF_ANY, ALT_VTYPE, false, false, nullptr, nullptr, nullptr};
-    const uint32_t ul = static_cast<uint32_t>(lane);
-    const uint32_t shi = end_void ? lo : hi;  // no END can match: nothing to scan
+// The variantType predicate of one query over packed VtHot words
+// (search_variants.py:100-183 + :205-214 for records that are not VT_SLOW):
+// END in [e0, e0 + espan] and len(ALT) in [vlo, vlo + vspan] as one unsigned
+// compare each (an empty length range never matches: vlo = 256), the class
+// mask of the kind, and the symbolic-ALT LUT held in lanes 0..7.
+struct VtPred {
+    uint32_t e0, espan, vlo, vspan, cmask, xneed;
+    bool end_void;  // no END can match
+    const uint32_t *lut;
+    uint32_t lutv;  // lane k < 8: LUT word k (symbolic ids in the words are < 255)
 
-    // lanes 0..7 hold LUT words 0..7 (symbolic ids in the words are < 255);
-    // ALT0 lanes fetch theirs with ds_bpermute: no vector-memory load inside
-    // a chunk, so the stream window is never drained for a symbolic ALT
-    const uint32_t lutv = lut[min(ul, 7u)];
+    __device__ __forceinline__ VtPred(const DStore &st, const QDev &Q) {
+        end_void = Q.end_max < 0 || Q.end_min > 0xffffffffll || Q.end_min > Q.end_max;
+        e0 = Q.end_min < 0 ? 0u : static_cast<uint32_t>(Q.end_min);
+        espan = (Q.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(Q.end_max)) - e0;
+        const int64_t vl = Q.vmin < 0 ? 0 : Q.vmin, vh = Q.vmax > 255 ? 255 : Q.vmax;
+        vlo = vh < vl ? 256u : static_cast<uint32_t>(vl);
+        vspan = vh < vl ? 0u : static_cast<uint32_t>(vh - vl);
+        const uint32_t vk = Q.vt_kind;
+        constexpr uint32_t kDel = vt_class_mask(VT_DEL), kIns = vt_class_mask(VT_INS), kDup = vt_class_mask(VT_DUP),
+                           kDupT = vt_class_mask(VT_DUPT), kCnv = vt_class_mask(VT_CNV);
+        cmask = vk == VT_DEL ? kDel : vk == VT_INS ? kIns : vk == VT_DUP ? kDup : vk == VT_DUPT ? kDupT
+              : vk == VT_CNV ? kCnv : 0u;
+        xneed = vt_xk_bit(vk) | VT_XK_SYM;  // an extra ALT might match
+        lut = st.sym_lut + Q.lut_off;
+        // ALT0 lanes fetch their LUT word with ds_bpermute: no vector-memory
+        // load inside a chunk, so a stream window is never drained for a symbolic ALT
+        lutv = lut[min(static_cast<uint32_t>(lane_id()), 7u)];
+    }
+    __device__ __forceinline__ bool end_ok(uint32_t end) const { return !end_void && end - e0 <= espan; }
     // one ALT word + the LUT word its symbolic id falls in: predicate + length bounds
-    auto alt_ok = [&](uint32_t aw, uint32_t lw) -> bool {
+    __device__ __forceinline__ bool alt_ok(uint32_t aw, uint32_t lw) const {
         if ((aw & 0xffu) - vlo > vspan) return false;
         if (aw & VT_SYM) return (lw >> ((aw >> 16) & 31u)) & 1u;
         return (cmask >> ((aw >> VT_CLASS_SHIFT) & 31u)) & 1u;
-    };
-    // a lane whose word is not VT_SLOW (cand false: nothing)
-    auto lane_eval = [&](const VtHot h, uint32_t r, bool cand) -> LaneOut {
+    }
+    // a lane whose word is not VT_SLOW (cand false: nothing); call with every lane active
+    __device__ __forceinline__ LaneOut eval(const DStore &st, const VtHot h, uint32_t r, bool cand) const {
         LaneOut o{0, 0, 0, 0, 0};
-        const uint32_t lw0 = __shfl(lutv, static_cast<int>((h.w >> 21) & 7u), kWave);  // all lanes active here
+        const uint32_t lw0 = __shfl(lutv, static_cast<int>((h.w >> 21) & 7u), kWave);
         uint64_t hm = (cand && alt_ok(h.w, lw0)) ? 1ull : 0ull;
         const uint32_t nx = (cand && (h.w & xneed)) ? h.w >> VT_NX_SHIFT : 0u;
         uint32_t x0 = 0;
@@ -840,12 +832,34 @@ __device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
             o.anv = h.an;
         }
         return o;
-    };
+    }
+};
+
+template <bool NONNEG>
+__device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs, QRes *__restrict__ res,
+                                         uint64_t *__restrict__ hits, uint32_t q, uint32_t lo, uint32_t hi,
+                                         uint32_t c_lo, uint32_t c_hi_all) {
+    const int lane = lane_id();
+    const QDev &Q = qs[q];
+    if (c_hi_all <= c_lo) {  // no candidate of this kind in the slice: nothing can hit or raise
+        if (lane == 0) res[Q.orig] = QRes{0, 0, 0, 0, 0, hi - lo};
+        return;
+    }
+    const uint32_t flags = Q.flags;
+    const bool details = flags & F_DETAILS;
+    const bool stop_on_exists = !details || (flags & F_BOOL_BREAK);
+    ScanState S;
+    const VtPred P(st, Q);
+    uint64_t *out = hits + Q.hit_off;
+    const QView V{flags, REF_ANY, ALT_VTYPE, false, false, nullptr, nullptr, nullptr};
+    const uint32_t ul = static_cast<uint32_t>(lane);
+    const uint32_t shi = P.end_void ? lo : hi;  // no END can match: nothing to scan
+    auto lane_eval = [&](const VtHot h, uint32_t r, bool cand) -> LaneOut { return P.eval(st, h, r, cand); };
     // the slice's candidates of this variantType (VcBlock): positions [c_lo, c_hi),
     // mapped from [lo, hi) by the slice driver (VcAux); none if no END can match
     const uint32_t c_hi = shi > lo ? c_hi_all : c_lo;
     auto fast_chunk = [&](uint32_t base, const VcWord x) -> int {  // 0 go on, 1 stop, 2 has VT_SLOW lanes
-        const bool cand = base + ul < c_hi && x.h.end - e0 <= espan;
+        const bool cand = base + ul < c_hi && x.h.end - P.e0 <= P.espan;
         if (__ballot(cand && (x.h.w & VT_SLOW))) return 2;
         const LaneOut o = lane_eval(x.h, x.r, cand);
         uint64_t cm;
@@ -863,7 +877,7 @@ __device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
         for (; base < c_hi; base += kWave) {
             const VcWord nx = ld(base + ul + kWave);
             const uint32_t r = x.r;
-            const bool cand = base + ul < c_hi && x.h.end - e0 <= espan;
+            const bool cand = base + ul < c_hi && x.h.end - P.e0 <= P.espan;
             const bool slow = cand && (x.h.w & VT_SLOW);
             LaneOut o = lane_eval(x.h, r, cand && !slow);
             if (__ballot(slow) && slow) o = eval_record(st, Q, V, r, st.rec[r]);
@@ -1254,6 +1268,121 @@ __global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, FusedGroups G,
     }, aux);
 }
 
+// ---------------------------------------------------------------- slice chains
+// One wave answers one chain (ChainDev): the consecutive 10 kb slices one
+// request was cut into by splitQuery, all with the same filters, none needing
+// the order-dependent machinery (host-checked at prepare: include_details, no
+// boolean break, non-negative AC, no VT_SLOW record in the window).  For such
+// slices vt_slice's answer is: exists = some hit with AC > 0, call_count /
+// all_alleles_count = sums over the hit records, hits in record-then-ALT order
+// -- each a sum (or an ordered concatenation) over the slice's candidates.
+// So the chain needs ONE candidate range, [C0, C1) from two entries of the
+// (kind, segment) coarse POS index (one scalar memory round instead of the
+// bucket -> POS probe -> VcBlock rounds per slice bound), every candidate lane
+// tests POS against the chain window and takes slice (POS - first) / width,
+// and the per-slice state lives in LDS: sums by LDS atomics, hit positions by
+// a wave prefix count minus the count at the first emitting lane of the same
+// slice, plus the slice's running total.  Per-slice QRes rows and hit regions
+// are bit-identical to vt_slice's (n_scanned is filled on the host).
+struct ChainLds {
+    unsigned long long cc[kChainMax], an[kChainMax], hoff[kChainMax];
+    unsigned int nh[kChainMax], ex[kChainMax];
+};
+
+__global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const QDev *__restrict__ qs,
+                                                       const ChainDev *__restrict__ chains, uint32_t n_chains,
+                                                       QRes *__restrict__ res, uint64_t *__restrict__ hits) {
+    __shared__ ChainLds lds_all[kWavesPerBlock];
+    const uint32_t c = launch_wave();
+    if (c >= n_chains) return;
+    ChainLds &L = lds_all[threadIdx.x >> 6];
+    const int lane = lane_id();
+    const uint32_t ul = static_cast<uint32_t>(lane);
+    const ChainDev C = chains[c];
+    const QDev &Q = qs[C.q0];  // the chain's common filters
+    const VtPred P(st, Q);
+    // candidate superset of [first, last] from the coarse index (both loads in one round)
+    auto cbound = [&](uint64_t x, uint32_t up) -> uint32_t {
+        if (x <= C.cb_base) return C.c_lo;
+        const uint64_t b = (x - C.cb_base) >> C.cb_shift;
+        if (b >= C.cb_n) return C.c_hi;
+        return st.vc_bucket[C.cb_off + b + up];
+    };
+    const uint32_t C0 = cbound(C.first, 0u);
+    const uint32_t C1 = P.end_void ? C0 : max(C0, cbound(static_cast<uint64_t>(C.last) + 1, 1u));
+    // slice lanes: lane j < n holds slice j's result row; LDS its running state
+    uint32_t orig = 0;
+    if (ul < C.n) {
+        const QDev &G = qs[C.q0 + ul];
+        orig = G.orig;
+        L.hoff[ul] = G.hit_off;
+        L.cc[ul] = 0;
+        L.an[ul] = 0;
+        L.nh[ul] = 0;
+        L.ex[ul] = 0;
+    }
+    uint32_t slow = 0;
+    for (uint32_t base = C0; base < C1; base += kWave) {
+        const uint32_t i = min(base + ul, C1 - 1);  // clamped, unconditional loads
+        const uint32_t p = st.vc_pos[i];
+        const VtHot h = st.vc_word[i];
+        const uint32_t r = st.vc_idx[i];
+        const bool inwin = base + ul < C1 && p >= C.first && p <= C.last;
+        const bool cand = inwin && P.end_ok(h.end);
+        slow |= static_cast<uint32_t>(__ballot(cand && (h.w & VT_SLOW)) != 0ull);  // excluded at prepare
+        const LaneOut o = P.eval(st, h, r, cand && !(h.w & VT_SLOW));
+        const bool hit = o.hm != 0;
+        if (!__ballot(hit)) continue;
+        uint32_t sid = inwin ? (p - C.first) / C.width : 0u;
+        sid = min(sid, C.n - 1);
+        const uint32_t cnt = hit ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
+        // exclusive prefix of the emitted counts over the wave
+        uint32_t pre;
+        if (!__ballot(cnt > 1)) {
+            pre = popc_below(__ballot(cnt == 1));
+        } else {  // bit-sliced (multi-ALT hit lanes)
+            pre = 0;
+            for (uint32_t b = 0; b < 7; ++b) {
+                pre += popc_below(__ballot((cnt >> b) & 1u)) << b;
+                if (!__ballot(cnt >> (b + 1))) break;
+            }
+        }
+        // first emitting lane of each slice run (slices are non-decreasing over the lanes)
+        const uint64_t emm = __ballot(cnt > 0);
+        const uint64_t below = emm & ((1ull << ul) - 1ull);
+        const int prev = below ? 63 - __clzll(static_cast<long long>(below)) : lane;
+        const uint32_t sid_prev = static_cast<uint32_t>(__shfl(static_cast<int>(sid), prev, kWave));
+        const uint64_t firstm = __ballot(cnt > 0 && (!below || sid_prev != sid));
+        const uint64_t upto = firstm & (ul == 63 ? ~0ull : ((2ull << ul) - 1ull));
+        const int f = upto ? 63 - __clzll(static_cast<long long>(upto)) : lane;
+        const uint32_t pre_f = static_cast<uint32_t>(__shfl(static_cast<int>(pre), f, kWave));
+        if (cnt) {
+            const uint32_t at = L.nh[sid] + pre - pre_f;
+            uint64_t *dst = hits + L.hoff[sid] + at;
+            for (uint64_t b = o.em; b; b &= b - 1)
+                *dst++ = static_cast<uint64_t>(r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
+            atomicAdd(&L.nh[sid], cnt);
+        }
+        if (hit) {
+            atomicAdd(&L.cc[sid], static_cast<unsigned long long>(o.c));
+            atomicAdd(&L.an[sid], static_cast<unsigned long long>(o.anv));
+            if (o.c > 0) L.ex[sid] = 1u;
+        }
+    }
+    if (ul < C.n) {
+        QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host (prepare knows each slice's record range)
+        if (slow) {
+            o.error = SB_QERR_UNSUPPORTED;  // never: prepare routes chains with a VT_SLOW record to vt_slice
+        } else {
+            o.exists = L.ex[ul] ? 1 : 0;
+            o.call_count = static_cast<int64_t>(L.cc[ul]);
+            o.all_alleles_count = static_cast<int64_t>(L.an[ul]);
+            o.n_hits = L.nh[ul];
+        }
+        res[orig] = o;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void compact_kernel(const uint64_t *__restrict__ hit_off,
                                                          const uint64_t *__restrict__ dense_off,
                                                          const QRes *__restrict__ res, uint32_t nq,
@@ -1489,6 +1618,13 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const u
                            bitmap, part);
     hipLaunchKernelGGL(summarise_finish_kernel, dim3((ns + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, s,
                        ss, slices, ns, bitmap, part, out);
+}
+
+void launch_chains(const DStore &st, const QDev *q, const ChainDev *chains, uint32_t n_chains, QRes *res,
+                   uint64_t *hits, hipStream_t s) {
+    if (!n_chains) return;
+    hipLaunchKernelGGL(chain_kernel, dim3(blocks_for(n_chains)), dim3(kBlock), 0, s, st, q, chains, n_chains, res,
+                       hits);
 }
 
 void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, uint32_t n_rows,

@@ -6,6 +6,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -61,6 +62,14 @@ struct BucketIndex {  // coarse POS index of one segment
     uint32_t n = 0;      // buckets; bucket[off + n] = segment end
 };
 
+// coarse POS index of the variantType candidates of one (segment, kind):
+// vc_bucket[off + b] = first candidate with POS >= base + (b << shift), b <= n
+struct VcIndex {
+    uint64_t off = 0;
+    uint32_t base = 0, shift = 31, n = 1;
+    uint32_t c_lo = 0, c_hi = 0;  // the pair's candidates in the kind's list
+};
+
 struct VcfData {
     std::string location;
     std::vector<std::string> samples;
@@ -71,6 +80,7 @@ struct VcfData {
     std::vector<Segment> segments;
     std::unordered_map<std::string, uint32_t> seg_index;
     std::vector<BucketIndex> buckets;  // parallel to segments (set by finish)
+    std::vector<std::array<VcIndex, kVtKinds>> vc_index;  // parallel to segments (set by finish)
     VcfCols c;
     std::string carry;  // partial line kept between add_text calls
     uint64_t stream_off = 0;  // text bytes consumed so far (incl. carry)
@@ -129,6 +139,7 @@ struct sb_store {
     // host copies needed to plan outputs and format results (global indexing)
     std::vector<uint32_t> h_pos, h_end, h_a0_len, h_x_lo, h_x_len, h_bucket;
     std::vector<uint16_t> h_vt;
+    std::vector<uint32_t> h_vt_slow;  // records whose VtHot word is VT_SLOW (sorted; chain planning)
     std::vector<uint64_t> h_ref_off, h_a0_off, h_x_off;
     std::vector<uint8_t> h_blob;
     std::vector<uint64_t> h_start;  // line start in the VCF text stream (summariseSlice planning)

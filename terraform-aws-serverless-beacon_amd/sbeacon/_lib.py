@@ -55,7 +55,7 @@ class ResultView(C.Structure):
 
 class BatchStats(C.Structure):
     _fields_ = [('n_queries', C.c_uint64), ('records_scanned', C.c_uint64), ('hits', C.c_uint64),
-                ('device_ms', C.c_double)]
+                ('device_ms', C.c_double), ('chained_slices', C.c_uint64)]
 
 
 class Slice(C.Structure):
