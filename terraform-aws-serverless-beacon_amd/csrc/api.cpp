@@ -190,8 +190,9 @@ struct sb_batch {
     DevMem chains;
     std::vector<uint8_t> chained;
     std::vector<uint32_t> nscan;
-    std::vector<uint32_t> chain_members;  // chained queries, chain by chain
+    std::vector<uint32_t> chain_members;  // chained queries, chain by chain (device copy: corig)
     uint32_t chain_base = 0;              // first chained slice in the launch-ordered array
+    DevMem corig;
     bool nonneg = true;
     // per-request rows (sb_batch_set_owners): seg = n_rows + 1 query offsets
     uint32_t n_rows = 0;
@@ -690,6 +691,7 @@ std::vector<uint32_t> plan_chains(sb_batch &B, const std::vector<uint32_t> &segi
         const QDev &d = B.hq[i0];
         const VcIndex &vi = s.vcfs[B.vcf[i0]].vc_index[segi[i0]][d.vt_kind];
         ChainDev cd{};
+        cd.s0 = static_cast<uint32_t>(B.chain_members.size());
         cd.n = static_cast<uint32_t>(x.m.size());
         cd.first = static_cast<uint32_t>(x.first);
         cd.last = static_cast<uint32_t>(x.last);
@@ -700,6 +702,16 @@ std::vector<uint32_t> plan_chains(sb_batch &B, const std::vector<uint32_t> &segi
         cd.cb_off = vi.off;
         cd.cb_shift = vi.shift;
         cd.cb_n = vi.n;
+        // VtPred's compare constants (query_kernels.hip), from the chain's common filters
+        const bool end_void = d.end_max < 0 || d.end_min > 0xffffffffll || d.end_min > d.end_max;
+        cd.e0 = d.end_min < 0 ? 0u : static_cast<uint32_t>(d.end_min);
+        cd.espan = (d.end_max > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(d.end_max)) - cd.e0;
+        const int64_t vl = d.vmin < 0 ? 0 : d.vmin, vh = d.vmax > 255 ? 255 : d.vmax;
+        cd.vlo = vh < vl ? 256u : static_cast<uint32_t>(vl);
+        cd.vspan = vh < vl ? 0u : static_cast<uint32_t>(vh - vl);
+        cd.kind = d.vt_kind | (end_void ? kChainEndVoid : 0u);
+        cd.lut_off = d.lut_off;
+        cd.out = 0;  // set with the hit regions
         B.hchains.push_back(cd);
         for (uint32_t i : x.m) {
             B.chained[i] = 1;
@@ -715,6 +727,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     if (nq >= (1u << 31)) throw Error(SB_EINVAL, "batch too large");
     B.nq = static_cast<uint32_t>(nq);
     std::vector<uint32_t> segi(nq, UINT32_MAX);  // segment index of each query in its VCF
+    std::vector<uint64_t> cap(nq, 0);           // hit-region capacity of each query
     B.hq.assign(nq, QDev{});
     B.host_err.assign(nq, 0);
     B.chrom.assign(nq, std::string());
@@ -731,7 +744,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     std::vector<uint64_t> subsets;
     std::vector<uint32_t> lut_all;
     std::unordered_map<std::string, uint32_t> lut_cache;
-    uint64_t samples_words = 0, cap_total = 0;
+    uint64_t samples_words = 0;
     for (size_t i = 0; i < nq; ++i) {
         const sb_query &x = qs[i];
         QDev &d = B.hq[i];
@@ -886,15 +899,14 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
             }
         }
         // output region: every ALT row of the records in the coarse bracket
-        d.hit_off = cap_total;
+        // (offsets assigned below, once the chains are known)
         if (!(d.flags & F_EMPTY) && d.first_bp <= d.last_bp) {
             const uint32_t lo = bucket_floor(s, d, d.first_bp);
             const uint32_t hi = std::max(lo, bucket_ceil(s, d, d.last_bp + 1));
-            cap_total += static_cast<uint64_t>(hi - lo) + (s.h_x_lo[hi] - s.h_x_lo[lo]);
+            cap[i] = static_cast<uint64_t>(hi - lo) + (s.h_x_lo[hi] - s.h_x_lo[lo]);
         }
     }
     B.samples_words = samples_words;
-    B.cap_total = cap_total;
     {
         // collect -> general kernel with the sample path; otherwise the
         // narrowest specialisation whose predicates cover the query
@@ -940,6 +952,25 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
                 return x.seg_lo != y.seg_lo ? x.seg_lo < y.seg_lo : x.first_bp < y.first_bp;
             });
     }
+    {  // hit regions: unchained queries in batch order, then each chain's slices
+        // back to back (a chain writes its hits densely from its first slot)
+        uint64_t at = 0;
+        for (uint32_t i = 0; i < nq; ++i)
+            if (B.chained.empty() || !B.chained[i]) {
+                B.hq[i].hit_off = at;
+                at += cap[i];
+            }
+        size_t m = 0;
+        for (ChainDev &c : B.hchains) {
+            c.out = at;
+            for (uint32_t j = 0; j < c.n; ++j, ++m) {
+                const uint32_t i = B.chain_members[m];
+                B.hq[i].hit_off = at;
+                at += cap[i];
+            }
+        }
+        B.cap_total = at;
+    }
     // 8 words of slack: vt_kernel reads words 0..7 of its LUT unconditionally
     // (packed symbolic ids are < 255; words past a LUT's end are never consulted)
     lut_all.insert(lut_all.end(), 8, 0u);
@@ -957,18 +988,15 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         for (uint32_t i : g.idx) lq.push_back(B.hq[i]);
     }
     B.chain_base = static_cast<uint32_t>(lq.size());
-    {
-        uint32_t at = B.chain_base;
-        for (ChainDev &c : B.hchains) {
-            c.q0 = at;
-            at += c.n;
-        }
-        for (uint32_t i : B.chain_members) lq.push_back(B.hq[i]);
-    }
+    for (uint32_t i : B.chain_members) lq.push_back(B.hq[i]);
     B.chains.alloc(B.hchains.size() * sizeof(ChainDev));
-    if (!B.hchains.empty())
+    B.corig.alloc(B.chain_members.size() * 4);
+    if (!B.hchains.empty()) {
         HIP_OK(hipMemcpyAsync(B.chains.p, B.hchains.data(), B.hchains.size() * sizeof(ChainDev), hipMemcpyHostToDevice,
                               st));
+        HIP_OK(hipMemcpyAsync(B.corig.p, B.chain_members.data(), B.chain_members.size() * 4, hipMemcpyHostToDevice,
+                              st));
+    }
     std::vector<uint64_t> hoff(nq);
     for (uint32_t i = 0; i < nq; ++i) hoff[i] = B.hq[i].hit_off;
     B.q.alloc(nq * sizeof(QDev));
@@ -983,7 +1011,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     HIP_OK(hipMemcpyAsync(B.lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
 
     B.res.alloc(size_t(nq) * sizeof(QRes));
-    B.hits.alloc(cap_total * 8);
+    B.hits.alloc(B.cap_total * 8);
     B.samples_out.alloc(samples_words * 8);
     HIP_OK(hipStreamSynchronize(st));
 }
@@ -1002,7 +1030,7 @@ void run(sb_batch &B) {
     }
     if (B.runs_pending++ == 0) HIP_OK(hipEventRecord(B.ev[0], st));
     // chains of variantType slices (one wave per request's slices)
-    launch_chains(d, B.q.as<QDev>(), B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()),
+    launch_chains(d, B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()), B.corig.as<uint32_t>(),
                   B.res.as<QRes>(), B.hits.as<uint64_t>(), st);
     // sample-free groups: one fused launch, long scans first (range, variantType,
     // general) and point lookups last, so the short waves fill the tail
@@ -1059,9 +1087,19 @@ sb_result_set *fetch(sb_batch &B) {
         doff.alloc((size_t(nq) + 1) * 8);
         dense.alloc(total * 8);
         HIP_OK(hipMemcpyAsync(doff.p, R->dense_off.data(), (size_t(nq) + 1) * 8, hipMemcpyHostToDevice, st));
+        // chained slices' hits are dense per chain: their region offsets follow
+        // from the n_hits of the chain's earlier slices
+        DevMem src;
+        const uint64_t *hoff = B.hoff.as<uint64_t>();
+        if (!B.hchains.empty()) {
+            src.alloc(size_t(nq) * 8);
+            HIP_OK(hipMemcpyAsync(src.p, B.hoff.p, size_t(nq) * 8, hipMemcpyDeviceToDevice, st));
+            launch_chain_src(B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()), B.corig.as<uint32_t>(),
+                             B.res.as<QRes>(), src.as<uint64_t>(), st);
+            hoff = src.as<uint64_t>();
+        }
         // queries with an error report n_hits = 0 on the device (host errors are F_EMPTY)
-        launch_compact(B.hoff.as<uint64_t>(), doff.as<uint64_t>(), B.res.as<QRes>(), nq, B.hits.as<uint64_t>(),
-                       dense.as<uint64_t>(), st);
+        launch_compact(hoff, doff.as<uint64_t>(), B.res.as<QRes>(), nq, B.hits.as<uint64_t>(), dense.as<uint64_t>(), st);
         HIP_OK(hipGetLastError());
         HIP_OK(hipMemcpyAsync(R->hit.data(), dense.p, total * 8, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));

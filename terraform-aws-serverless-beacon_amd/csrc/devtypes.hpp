@@ -126,11 +126,15 @@ struct alignas(16) VcBlock {
 // over candidate POS (vc_bucket: entry b = first candidate of the pair with
 // POS >= base + (b << shift)), each candidate lane filters POS against the
 // chain window and finds its slice as (POS - first) / width, and per-slice
-// sums / hit positions are kept in LDS.  Per-slice QRes and hit regions are
-// exactly what vt_slice writes for each slice alone.
+// sums are kept in LDS.  Per-slice QRes rows are exactly what vt_slice
+// writes for each slice alone; the chain's hits are written densely in slice
+// order from `out` (slice j's hits start after slices 0..j-1's n_hits).  The
+// descriptor carries the chain's filters already reduced to the compare
+// constants vt_slice derives from its QDev (VtPred), so a wave reads nothing
+// else before the index.
 constexpr uint32_t kChainMax = 32;
 struct alignas(16) ChainDev {
-    uint32_t q0;        // first slice in the launch-ordered QDev array (slices q0 .. q0 + n - 1)
+    uint32_t s0;        // first slice in the chain-ordered arrays (chain_orig)
     uint32_t n;         // slices, 1 .. kChainMax
     uint32_t first;     // first_bp of slice 0
     uint32_t last;      // last_bp of slice n - 1
@@ -139,7 +143,14 @@ struct alignas(16) ChainDev {
     uint32_t cb_base;   // coarse candidate index of the pair (vc_bucket)
     uint64_t cb_off;
     uint32_t cb_shift, cb_n;
+    uint32_t e0, espan;   // END in [e0, e0 + espan]
+    uint32_t vlo, vspan;  // len(ALT) in [vlo, vlo + vspan] (vlo = 256: empty)
+    uint32_t kind;        // vt_kind | kChainEndVoid
+    uint32_t lut_off;     // symbolic-ALT LUT of the chain's variantType
+    uint64_t out;         // first hit slot of the chain
 };
+static_assert(sizeof(ChainDev) == 80, "ChainDev is five 16-byte words");
+constexpr uint32_t kChainEndVoid = 1u << 8;  // no END can match
 
 // bit c set = an ALT of class c satisfies variantType `kind` (vtype_hit)
 __host__ __device__ constexpr uint32_t vt_class_mask(uint32_t kind) {

@@ -32,10 +32,14 @@ struct FusedGroup {
 void launch_fused(const DStore &st, const FusedGroup *groups, int count, bool nonneg,
                   const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits, hipStream_t s);
 
-// Slice chains (devtypes.hpp ChainDev): one wave per chain of consecutive
-// variantType slices of one request; q = the launch-ordered QDev array.
-void launch_chains(const DStore &st, const QDev *q, const ChainDev *chains, uint32_t n_chains, QRes *res,
+// Slice chains (devtypes.hpp ChainDev): runs of chains of consecutive
+// variantType slices of one request per wave; corig[s] = batch index of the
+// chain-ordered slice s.  launch_chain_src writes the hit-region offset of
+// every chained slice (dense per chain) into src[batch index].
+void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, QRes *res,
                    uint64_t *hits, hipStream_t s);
+void launch_chain_src(const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, const QRes *res,
+                      uint64_t *src, hipStream_t s);
 
 // summariseSlice: phase A = one workgroup per chunk of kSumChunk records
 // (chunk_slice[c] = its slice), reducing the records' (numVariants, numCalls)

@@ -775,8 +775,16 @@ struct VtPred {
     uint32_t e0, espan, vlo, vspan, cmask, xneed;
     bool end_void;  // no END can match
     const uint32_t *lut;
-    uint32_t lutv;  // lane k < 8: LUT word k (symbolic ids in the words are < 255)
+    uint32_t lutv;      // lane lut_lane + k (k < 8): LUT word k (symbolic ids in the words are < 255)
+    uint32_t lut_lane;
 
+    __device__ __forceinline__ void set_kind(uint32_t vk) {
+        constexpr uint32_t kDel = vt_class_mask(VT_DEL), kIns = vt_class_mask(VT_INS), kDup = vt_class_mask(VT_DUP),
+                           kDupT = vt_class_mask(VT_DUPT), kCnv = vt_class_mask(VT_CNV);
+        cmask = vk == VT_DEL ? kDel : vk == VT_INS ? kIns : vk == VT_DUP ? kDup : vk == VT_DUPT ? kDupT
+              : vk == VT_CNV ? kCnv : 0u;
+        xneed = vt_xk_bit(vk) | VT_XK_SYM;  // an extra ALT might match
+    }
     __device__ __forceinline__ VtPred(const DStore &st, const QDev &Q) {
         end_void = Q.end_max < 0 || Q.end_min > 0xffffffffll || Q.end_min > Q.end_max;
         e0 = Q.end_min < 0 ? 0u : static_cast<uint32_t>(Q.end_min);
@@ -784,16 +792,26 @@ struct VtPred {
         const int64_t vl = Q.vmin < 0 ? 0 : Q.vmin, vh = Q.vmax > 255 ? 255 : Q.vmax;
         vlo = vh < vl ? 256u : static_cast<uint32_t>(vl);
         vspan = vh < vl ? 0u : static_cast<uint32_t>(vh - vl);
-        const uint32_t vk = Q.vt_kind;
-        constexpr uint32_t kDel = vt_class_mask(VT_DEL), kIns = vt_class_mask(VT_INS), kDup = vt_class_mask(VT_DUP),
-                           kDupT = vt_class_mask(VT_DUPT), kCnv = vt_class_mask(VT_CNV);
-        cmask = vk == VT_DEL ? kDel : vk == VT_INS ? kIns : vk == VT_DUP ? kDup : vk == VT_DUPT ? kDupT
-              : vk == VT_CNV ? kCnv : 0u;
-        xneed = vt_xk_bit(vk) | VT_XK_SYM;  // an extra ALT might match
+        set_kind(Q.vt_kind);
         lut = st.sym_lut + Q.lut_off;
         // ALT0 lanes fetch their LUT word with ds_bpermute: no vector-memory
         // load inside a chunk, so a stream window is never drained for a symbolic ALT
         lutv = lut[min(static_cast<uint32_t>(lane_id()), 7u)];
+        lut_lane = 0;
+    }
+    // the same from a chain descriptor's constants (ChainDev, computed on the
+    // host exactly as above); LUT words already held in lanes lane0 .. lane0 + 7
+    __device__ __forceinline__ VtPred(const DStore &st, uint32_t e0_, uint32_t espan_, uint32_t vlo_, uint32_t vspan_,
+                                      uint32_t kind, uint32_t lut_off, uint32_t lutv_, uint32_t lane0) {
+        e0 = e0_;
+        espan = espan_;
+        vlo = vlo_;
+        vspan = vspan_;
+        end_void = (kind & kChainEndVoid) != 0;
+        set_kind(kind & 0xffu);
+        lut = st.sym_lut + lut_off;
+        lutv = lutv_;
+        lut_lane = lane0;
     }
     __device__ __forceinline__ bool end_ok(uint32_t end) const { return !end_void && end - e0 <= espan; }
     // one ALT word + the LUT word its symbolic id falls in: predicate + length bounds
@@ -805,7 +823,7 @@ struct VtPred {
     // a lane whose word is not VT_SLOW (cand false: nothing); call with every lane active
     __device__ __forceinline__ LaneOut eval(const DStore &st, const VtHot h, uint32_t r, bool cand) const {
         LaneOut o{0, 0, 0, 0, 0};
-        const uint32_t lw0 = __shfl(lutv, static_cast<int>((h.w >> 21) & 7u), kWave);
+        const uint32_t lw0 = __shfl(lutv, static_cast<int>(lut_lane + ((h.w >> 21) & 7u)), kWave);
         uint64_t hm = (cand && alt_ok(h.w, lw0)) ? 1ull : 0ull;
         const uint32_t nx = (cand && (h.w & xneed)) ? h.w >> VT_NX_SHIFT : 0u;
         uint32_t x0 = 0;
@@ -1269,98 +1287,126 @@ __global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, FusedGroups G,
 }
 
 // ---------------------------------------------------------------- slice chains
-// One wave answers one chain (ChainDev): the consecutive 10 kb slices one
-// request was cut into by splitQuery, all with the same filters, none needing
-// the order-dependent machinery (host-checked at prepare: include_details, no
-// boolean break, non-negative AC, no VT_SLOW record in the window).  For such
-// slices vt_slice's answer is: exists = some hit with AC > 0, call_count /
-// all_alleles_count = sums over the hit records, hits in record-then-ALT order
-// -- each a sum (or an ordered concatenation) over the slice's candidates.
-// So the chain needs ONE candidate range, [C0, C1) from two entries of the
-// (kind, segment) coarse POS index (one scalar memory round instead of the
-// bucket -> POS probe -> VcBlock rounds per slice bound), every candidate lane
-// tests POS against the chain window and takes slice (POS - first) / width,
-// and the per-slice state lives in LDS: sums by LDS atomics, hit positions by
-// a wave prefix count minus the count at the first emitting lane of the same
-// slice, plus the slice's running total.  Per-slice QRes rows and hit regions
-// are bit-identical to vt_slice's (n_scanned is filled on the host).
+// One wave answers a run of up to kChainRun chains (ChainDev): each chain is
+// the consecutive 10 kb slices one request was cut into by splitQuery, all
+// with the same filters, none needing the order-dependent machinery
+// (host-checked at prepare: include_details, no boolean break, non-negative
+// AC, no VT_SLOW record in the window).  For such slices vt_slice's answer is:
+// exists = some hit with AC > 0, call_count / all_alleles_count = sums over
+// the hit records, hits in record-then-ALT order -- each a sum (or an ordered
+// concatenation) over the slice's candidates.  So a chain needs ONE candidate
+// range, [C0, C1) from two entries of the (kind, segment) coarse POS index,
+// every candidate lane tests POS against the chain window and takes slice
+// (POS - first) / width, per-slice sums go to LDS by atomics and the chain's
+// hits are written densely in record order.  Memory rounds per wave: the
+// run's descriptors (lane k = chain k), then every chain's two index entries
+// and LUT words at once (lanes 2k / 2k+1, lanes 8k..8k+7), then candidate
+// chunks, chain k+1's first chunk issued before chain k is evaluated.
+constexpr uint32_t kChainRun = 8;  // chains per wave (lanes 8k..8k+7 hold chain k's LUT words)
+
 struct ChainLds {
-    unsigned long long cc[kChainMax], an[kChainMax], hoff[kChainMax];
+    unsigned long long cc[kChainMax], an[kChainMax];
     unsigned int nh[kChainMax], ex[kChainMax];
 };
 
-__global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const QDev *__restrict__ qs,
-                                                       const ChainDev *__restrict__ chains, uint32_t n_chains,
-                                                       QRes *__restrict__ res, uint64_t *__restrict__ hits) {
+struct ChainChunk {
+    uint32_t p;  // candidate POS
+    VtHot h;
+    uint32_t r;  // candidate record
+};
+
+__global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const ChainDev *__restrict__ chains,
+                                                       uint32_t n_chains, uint32_t run,
+                                                       const uint32_t *__restrict__ corig, QRes *__restrict__ res,
+                                                       uint64_t *__restrict__ hits) {
     __shared__ ChainLds lds_all[kWavesPerBlock];
-    const uint32_t c = launch_wave();
-    if (c >= n_chains) return;
+    const uint32_t c_first = launch_wave() * run;
+    if (c_first >= n_chains) return;
+    const uint32_t R = min(run, n_chains - c_first);
     ChainLds &L = lds_all[threadIdx.x >> 6];
     const int lane = lane_id();
     const uint32_t ul = static_cast<uint32_t>(lane);
-    const ChainDev C = chains[c];
-    const QDev &Q = qs[C.q0];  // the chain's common filters
-    const VtPred P(st, Q);
-    // candidate superset of [first, last] from the coarse index (both loads in one round)
-    auto cbound = [&](uint64_t x, uint32_t up) -> uint32_t {
-        if (x <= C.cb_base) return C.c_lo;
-        const uint64_t b = (x - C.cb_base) >> C.cb_shift;
-        if (b >= C.cb_n) return C.c_hi;
-        return st.vc_bucket[C.cb_off + b + up];
-    };
-    const uint32_t C0 = cbound(C.first, 0u);
-    const uint32_t C1 = P.end_void ? C0 : max(C0, cbound(static_cast<uint64_t>(C.last) + 1, 1u));
-    // slice lanes: lane j < n holds slice j's result row; LDS its running state
-    uint32_t orig = 0;
-    if (ul < C.n) {
-        const QDev &G = qs[C.q0 + ul];
-        orig = G.orig;
-        L.hoff[ul] = G.hit_off;
-        L.cc[ul] = 0;
-        L.an[ul] = 0;
-        L.nh[ul] = 0;
-        L.ex[ul] = 0;
+    // round 1: lane k < R holds chain k's descriptor
+    const uint4 *cd = reinterpret_cast<const uint4 *>(chains + c_first);
+    uint4 d0{0, 0, 0, 0}, d1{0, 0, 0, 0}, d2{0, 0, 0, 0}, d3{0, 0, 0, 0}, d4{0, 0, 0, 0};
+    if (ul < R) {
+        d0 = cd[5 * ul];
+        d1 = cd[5 * ul + 1];
+        d2 = cd[5 * ul + 2];
+        d3 = cd[5 * ul + 3];
+        d4 = cd[5 * ul + 4];
     }
-    uint32_t slow = 0;
-    for (uint32_t base = C0; base < C1; base += kWave) {
-        const uint32_t i = min(base + ul, C1 - 1);  // clamped, unconditional loads
-        const uint32_t p = st.vc_pos[i];
-        const VtHot h = st.vc_word[i];
-        const uint32_t r = st.vc_idx[i];
-        const bool inwin = base + ul < C1 && p >= C.first && p <= C.last;
-        const bool cand = inwin && P.end_ok(h.end);
-        slow |= static_cast<uint32_t>(__ballot(cand && (h.w & VT_SLOW)) != 0ull);  // excluded at prepare
-        const LaneOut o = P.eval(st, h, r, cand && !(h.w & VT_SLOW));
+    // round 2: lanes 2k / 2k+1 = chain k's candidate bounds from the coarse
+    // index (a superset of [first, last]); lanes 8k + t = LUT word t of chain k
+    uint32_t bound = 0, lutv = 0;
+    {
+        const int src = static_cast<int>(ul >> 1);
+        const uint32_t first = __shfl(d0.z, src, kWave), last = __shfl(d0.w, src, kWave);
+        const uint32_t c_lo = __shfl(d1.y, src, kWave), c_hi = __shfl(d1.z, src, kWave);
+        const uint32_t cb_base = __shfl(d1.w, src, kWave);
+        const uint64_t cb_off = static_cast<uint64_t>(static_cast<uint32_t>(__shfl(d2.x, src, kWave))) |
+                                (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(d2.y, src, kWave))) << 32);
+        const uint32_t cb_shift = __shfl(d2.z, src, kWave), cb_n = __shfl(d2.w, src, kWave);
+        const uint32_t lut_off = __shfl(d4.y, static_cast<int>(ul >> 3), kWave);
+        if (ul < 2 * R) {
+            const uint32_t up = ul & 1u;
+            const uint64_t x = up ? static_cast<uint64_t>(last) + 1 : first;
+            if (x <= cb_base) {
+                bound = c_lo;
+            } else {
+                const uint64_t b = (x - cb_base) >> cb_shift;
+                bound = b >= cb_n ? c_hi : st.vc_bucket[cb_off + b + up];
+            }
+        }
+        if (ul < 8 * R) lutv = st.sym_lut[lut_off + (ul & 7u)];
+    }
+    // clamped and unconditional (an empty range reads slot C0, inside the
+    // kind lists + sentinel): no load sits under a branch, so the waitcnt pass
+    // keeps the next chain's chunk in flight while this one is evaluated
+    auto load_chunk = [&](uint32_t C1, uint32_t base) -> ChainChunk {
+        const uint32_t i = min(base + ul, max(C1, base + 1) - 1);
+        return ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]};
+    };
+    auto range_of = [&](uint32_t k, uint32_t *C0, uint32_t *C1) {
+        *C0 = rdl(bound, 2 * k);
+        *C1 = (rdl(d4.x, k) & kChainEndVoid) ? *C0 : max(*C0, rdl(bound, 2 * k + 1));
+    };
+    // one chunk of chain candidates at positions [base, base + 64) of [C0, C1)
+    struct ChainCtx {
+        uint32_t first, last, width, n;
+        uint64_t out;
+        uint64_t nout;
+        uint32_t slow;
+    };
+    auto eval_chunk = [&](ChainCtx &X, const VtPred &P, const ChainChunk &x, uint32_t base, uint32_t C1) {
+        const bool inwin = base + ul < C1 && x.p >= X.first && x.p <= X.last;
+        const bool cand = inwin && P.end_ok(x.h.end);
+        X.slow |= static_cast<uint32_t>(__ballot(cand && (x.h.w & VT_SLOW)) != 0ull);  // excluded at prepare
+        const LaneOut o = P.eval(st, x.h, x.r, cand && !(x.h.w & VT_SLOW));
         const bool hit = o.hm != 0;
-        if (!__ballot(hit)) continue;
-        uint32_t sid = inwin ? (p - C.first) / C.width : 0u;
-        sid = min(sid, C.n - 1);
+        if (!__ballot(hit)) return;
+        const uint32_t sid = inwin ? min((x.p - X.first) / X.width, X.n - 1) : 0u;
         const uint32_t cnt = hit ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
-        // exclusive prefix of the emitted counts over the wave
-        uint32_t pre;
+        // exclusive prefix / total of the emitted counts over the wave
+        uint32_t pre, total;
         if (!__ballot(cnt > 1)) {
-            pre = popc_below(__ballot(cnt == 1));
+            const uint64_t one = __ballot(cnt == 1);
+            pre = popc_below(one);
+            total = static_cast<uint32_t>(__popcll(one));
         } else {  // bit-sliced (multi-ALT hit lanes)
             pre = 0;
+            total = 0;
             for (uint32_t b = 0; b < 7; ++b) {
-                pre += popc_below(__ballot((cnt >> b) & 1u)) << b;
+                const uint64_t m = __ballot((cnt >> b) & 1u);
+                pre += popc_below(m) << b;
+                total += static_cast<uint32_t>(__popcll(m)) << b;
                 if (!__ballot(cnt >> (b + 1))) break;
             }
         }
-        // first emitting lane of each slice run (slices are non-decreasing over the lanes)
-        const uint64_t emm = __ballot(cnt > 0);
-        const uint64_t below = emm & ((1ull << ul) - 1ull);
-        const int prev = below ? 63 - __clzll(static_cast<long long>(below)) : lane;
-        const uint32_t sid_prev = static_cast<uint32_t>(__shfl(static_cast<int>(sid), prev, kWave));
-        const uint64_t firstm = __ballot(cnt > 0 && (!below || sid_prev != sid));
-        const uint64_t upto = firstm & (ul == 63 ? ~0ull : ((2ull << ul) - 1ull));
-        const int f = upto ? 63 - __clzll(static_cast<long long>(upto)) : lane;
-        const uint32_t pre_f = static_cast<uint32_t>(__shfl(static_cast<int>(pre), f, kWave));
         if (cnt) {
-            const uint32_t at = L.nh[sid] + pre - pre_f;
-            uint64_t *dst = hits + L.hoff[sid] + at;
+            uint64_t *dst = hits + X.out + X.nout + pre;
             for (uint64_t b = o.em; b; b &= b - 1)
-                *dst++ = static_cast<uint64_t>(r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
+                *dst++ = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
             atomicAdd(&L.nh[sid], cnt);
         }
         if (hit) {
@@ -1368,18 +1414,76 @@ __global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const QDev *__
             atomicAdd(&L.an[sid], static_cast<unsigned long long>(o.anv));
             if (o.c > 0) L.ex[sid] = 1u;
         }
-    }
-    if (ul < C.n) {
-        QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host (prepare knows each slice's record range)
-        if (slow) {
-            o.error = SB_QERR_UNSUPPORTED;  // never: prepare routes chains with a VT_SLOW record to vt_slice
-        } else {
-            o.exists = L.ex[ul] ? 1 : 0;
-            o.call_count = static_cast<int64_t>(L.cc[ul]);
-            o.all_alleles_count = static_cast<int64_t>(L.an[ul]);
-            o.n_hits = L.nh[ul];
+        X.nout += total;
+    };
+    // chain k with its first chunk in `cur`; issues chain k+1's first chunk
+    // (into the returned value) before evaluating anything of chain k
+    auto process = [&](uint32_t k, const ChainChunk &cur) -> ChainChunk {
+        ChainChunk nxt{0, VtHot{0, 0, 0, 0}, 0};
+        if (k + 1 < R) {
+            uint32_t C0n, C1n;
+            range_of(k + 1, &C0n, &C1n);
+            nxt = load_chunk(C1n, C0n);
         }
-        res[orig] = o;
+        ChainCtx X{rdl(d0.z, k), rdl(d0.w, k), rdl(d1.x, k), rdl(d0.y, k),
+                   static_cast<uint64_t>(rdl(d4.z, k)) | (static_cast<uint64_t>(rdl(d4.w, k)) << 32), 0, 0};
+        const uint32_t s0 = rdl(d0.x, k);
+        const VtPred P(st, rdl(d3.x, k), rdl(d3.y, k), rdl(d3.z, k), rdl(d3.w, k), rdl(d4.x, k), rdl(d4.y, k),
+                       lutv, 8 * k);
+        uint32_t C0, C1;
+        range_of(k, &C0, &C1);
+        const uint32_t orig = corig[s0 + min(ul, X.n - 1)];
+        if (ul < X.n) {
+            L.cc[ul] = 0;
+            L.an[ul] = 0;
+            L.nh[ul] = 0;
+            L.ex[ul] = 0;
+        }
+        if (C0 < C1) {
+            eval_chunk(X, P, cur, C0, C1);
+            for (uint32_t base = C0 + kWave; base < C1; base += kWave)  // chains longer than one chunk
+                eval_chunk(X, P, load_chunk(C1, base), base, C1);
+        }
+        if (ul < X.n) {
+            QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host (prepare knows each slice's record range)
+            if (X.slow) {
+                o.error = SB_QERR_UNSUPPORTED;  // never: prepare routes chains with a VT_SLOW record to vt_slice
+            } else {
+                o.exists = L.ex[ul] ? 1 : 0;
+                o.call_count = static_cast<int64_t>(L.cc[ul]);
+                o.all_alleles_count = static_cast<int64_t>(L.an[ul]);
+                o.n_hits = L.nh[ul];
+            }
+            res[orig] = o;
+        }
+        return nxt;
+    };
+    ChainChunk x;
+    {
+        uint32_t C0, C1;
+        range_of(0, &C0, &C1);
+        x = load_chunk(C1, C0);
+    }
+    // unrolled: no loop-carried chunk registers, so the waitcnt pass keeps
+    // chain k+1's loads in flight (exact vmcnt) while chain k is evaluated
+#pragma unroll
+    for (uint32_t k = 0; k < kChainRun; ++k)
+        if (k < R) x = process(k, x);
+}
+
+// Hit-region offsets of chained slices (their hits are dense per chain, in
+// slice order): src[orig] = chain out + the n_hits of the chain's earlier slices.
+__global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__restrict__ chains, uint32_t n_chains,
+                                                           const uint32_t *__restrict__ corig,
+                                                           const QRes *__restrict__ res, uint64_t *__restrict__ src) {
+    const uint32_t c = blockIdx.x * kBlock + threadIdx.x;
+    if (c >= n_chains) return;
+    const ChainDev C = chains[c];
+    uint64_t at = C.out;
+    for (uint32_t j = 0; j < C.n; ++j) {
+        const uint32_t q = corig[C.s0 + j];
+        src[q] = at;
+        at += res[q].error ? 0u : res[q].n_hits;
     }
 }
 
@@ -1401,27 +1505,46 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(const uint64_t *__restr
 // number of slices that exist, so shard partials combine by sum), n_variants,
 // call_count and all_alleles_count are summed; a slice that raised (device
 // error or host-detected error flag) counts in `errors` and contributes
-// nothing else.  One thread per row; rows of a shard are few (10^5-10^6) and
-// each reads ~5 QRes, so this is a small streaming pass.
+// nothing else.  A workgroup owns kBlock consecutive rows, whose queries are
+// one contiguous QRes range: it stages that range through LDS in tiles with
+// coalesced 16-byte loads (a thread-per-row walk of QRes directly would read
+// 32-byte records at a ~5-record stride across the lanes), then each thread
+// sums its row's part of the tile.
+constexpr uint32_t kReduceTile = 1024;  // QRes per LDS tile (32 KiB)
+
 __global__ __launch_bounds__(kBlock) void request_reduce_kernel(const QRes *__restrict__ res,
                                                                 const uint32_t *__restrict__ seg,
                                                                 const uint8_t *__restrict__ host_err,
                                                                 uint32_t n_rows, ReqPartial *__restrict__ out) {
-    const uint32_t w = blockIdx.x * kBlock + threadIdx.x;
-    if (w >= n_rows) return;
+    __shared__ uint4 tile[kReduceTile * (sizeof(QRes) / 16)];
+    __shared__ uint8_t terr[kReduceTile];
+    static_assert(sizeof(QRes) == 32, "QRes is two 16-byte words");
+    const uint32_t r0 = blockIdx.x * kBlock, r1 = min(n_rows, r0 + kBlock);
+    const uint32_t w = r0 + threadIdx.x;
+    const uint32_t q_lo = seg[r0], q_hi = seg[r1];
+    const uint32_t a = w < r1 ? seg[w] : 0u, e = w < r1 ? seg[w + 1] : 0u;
     ReqPartial P{0, 0, 0, 0, 0};
-    for (uint32_t q = seg[w], e = seg[w + 1]; q < e; ++q) {
-        const QRes r = res[q];
-        if (r.error || host_err[q]) {
-            ++P.errors;
-            continue;
+    const uint4 *src = reinterpret_cast<const uint4 *>(res);
+    for (uint32_t t0 = q_lo; t0 < q_hi; t0 += kReduceTile) {
+        const uint32_t t1 = min(q_hi, t0 + kReduceTile);
+        for (uint32_t k = threadIdx.x; k < 2 * (t1 - t0); k += kBlock) tile[k] = src[2 * static_cast<size_t>(t0) + k];
+        for (uint32_t k = threadIdx.x; k < t1 - t0; k += kBlock) terr[k] = host_err[t0 + k];
+        __syncthreads();
+        const QRes *T = reinterpret_cast<const QRes *>(tile);
+        for (uint32_t q = max(a, t0), qe = min(e, t1); q < qe; ++q) {
+            const QRes &r = T[q - t0];
+            if (r.error || terr[q - t0]) {
+                ++P.errors;
+                continue;
+            }
+            P.exists += r.exists != 0;
+            P.n_variants += r.n_hits;
+            P.call_count += r.call_count;
+            P.all_alleles_count += r.all_alleles_count;
         }
-        P.exists += r.exists != 0;
-        P.n_variants += r.n_hits;
-        P.call_count += r.call_count;
-        P.all_alleles_count += r.all_alleles_count;
+        __syncthreads();
     }
-    out[w] = P;
+    if (w < r1) out[w] = P;
 }
 
 inline uint32_t blocks_for(uint32_t nwaves) { return (nwaves + kWavesPerBlock - 1) / kWavesPerBlock; }
@@ -1620,11 +1743,27 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const u
                        ss, slices, ns, bitmap, part, out);
 }
 
-void launch_chains(const DStore &st, const QDev *q, const ChainDev *chains, uint32_t n_chains, QRes *res,
+void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, QRes *res,
                    uint64_t *hits, hipStream_t s) {
     if (!n_chains) return;
-    hipLaunchKernelGGL(chain_kernel, dim3(blocks_for(n_chains)), dim3(kBlock), 0, s, st, q, chains, n_chains, res,
-                       hits);
+    // runs of kChainRun chains per wave while the launch still fills the chip
+    // (256 CUs x 4 SIMDs x 8 waves, 4 deep)
+    uint32_t run = kChainRun;
+    if (const char *e = std::getenv("SBEACON_CHAIN_RUN")) {
+        const long k = std::strtol(e, nullptr, 10);
+        if (k >= 1) run = std::min<uint32_t>(kChainRun, static_cast<uint32_t>(k));
+    } else {
+        while (run > 1 && (n_chains + run - 1) / run < 32768u) run >>= 1;
+    }
+    hipLaunchKernelGGL(chain_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st, chains,
+                       n_chains, run, corig, res, hits);
+}
+
+void launch_chain_src(const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, const QRes *res,
+                      uint64_t *src, hipStream_t s) {
+    if (!n_chains) return;
+    hipLaunchKernelGGL(chain_src_kernel, dim3((n_chains + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chains, n_chains,
+                       corig, res, src);
 }
 
 void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, uint32_t n_rows,
