@@ -1,24 +1,19 @@
 #!/usr/bin/env python3
-"""Benchmark: batched Beacon g_variants slice queries on an HBM-resident store.
+"""Benchmark: batched Beacon g_variants requests on an HBM-resident store.
 
-Workload (BASELINE.json configs[1]): a 1000G chr22-
-shape store — 1,103,547 records x 2,504 samples, seed 22 — and 10,000 Beacon
-requests (5,000 range + 5,000 point ref/alt, seed 1022 + rank), sliced into
-PerformQueryPayloads exactly as splitQuery does.  One step = one device pass
-of the whole batch with the queries already resident in HBM: the host plans
-each slice query's private output region once (sb_batch_prepare), and a step
-launches one range-scan kernel per query class (range_n_kernel for ref=alt='N'
-range requests, scan_kernel<EXACT> for point ref/alt requests), each doing the
-coarse-index lower_bound, interval/ref/alt filters, wave-prefix-sum call
-counts and ballot compaction of hits in a single pass.
+Default workload (BASELINE.json configs[2], SURVEY.md §8d config 3,
+``bench_genome.py``): the whole-genome 1000G-shape store (85 M records)
+sharded by contig across the GPUs, 1 M variantType requests per GPU; a step
+answers every request's 10 kb slices (chain_kernel), reduces them into
+request rows, compacts the hit lists and delivers rows + hits to each
+request's host-facing rank over RCCL.  ``--workload chr22`` is config 2
+(1000G chr22 shape, 10 k range / point requests, replicas), ``--workload
+gnomad`` config 5 (gnomAD-shape sites + carrier bit-matrix).
 
-Multi-GPU (`torch.distributed.run`, one rank per GPU): every rank holds its
-own store replica and answers its own 10k requests — the slices are
-independent (the reference fans them out as separate Lambdas), so there is
-no data-path collective; `value` = all ranks' requests / max-over-ranks time
-(weak scaling).  The barrier and the timing reduction use torch.distributed.
-
-Prints ONE JSON line on rank 0.
+``--gpus N`` without torch.distributed's environment starts
+``torch.distributed.run`` with N ranks (one per GPU) as a child process
+before anything touches a GPU, and exits with its code.  Every rank prints
+its log to stderr; rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -56,19 +51,40 @@ def parse():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--parity-requests', type=int, default=300,
                     help='requests re-checked against the C oracle after timing (rank 0)')
-    ap.add_argument('--workload', choices=['chr22', 'genome', 'gnomad'], default='chr22',
-                    help='chr22: config 2 (default; replicas across GPUs). genome: config 3 (whole-genome store '
-                         'sharded by contig across the GPUs, request rows gathered to rank 0 over RCCL). '
+    ap.add_argument('--workload', choices=['chr22', 'genome', 'gnomad'], default='genome',
+                    help='genome: config 3 (default; whole-genome store sharded by contig across the GPUs, '
+                         'request rows + hit lists delivered over RCCL). chr22: config 2 (replicas across GPUs). '
                          'gnomad: config 5 (gnomAD-shape sites + carrier bit-matrix, shard r of 8 per GPU)')
     ap.add_argument('--genome-records', type=int, default=85_000_000)
-    ap.add_argument('--genome-requests', type=int, default=1_000_000)
+    ap.add_argument('--genome-requests', type=int, default=1_000_000,
+                    help='config-3 requests per GPU (weak scaling) or in total (strong)')
+    ap.add_argument('--scaling', choices=['weak', 'strong'], default='weak')
+    ap.add_argument('--deliver', choices=['first', 'rank0'], default='first',
+                    help="config 3: each request's rows + hits go to the rank of its first slice, or all to rank 0")
     ap.add_argument('--gnomad-records', type=int, default=750_000_000)
     ap.add_argument('--gnomad-requests', type=int, default=50_000, help='config-5 requests per GPU')
     return ap.parse_args()
 
 
+def spawn_ranks(args) -> int:
+    """`--gpus N` outside torch.distributed: run N ranks under
+    torch.distributed.run as a child (nothing here has touched a GPU)."""
+    import socket
+    import subprocess
+    sk = socket.socket()
+    sk.bind(('127.0.0.1', 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.gpus}',
+           '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    log('launching: ' + ' '.join(cmd))
+    return subprocess.call(cmd)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and 'WORLD_SIZE' not in os.environ:
+        sys.exit(spawn_ranks(args))
     if args.workload == 'genome':
         from bench_genome import main_genome
         return main_genome(args)

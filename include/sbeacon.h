@@ -158,7 +158,12 @@ typedef struct {
     uint64_t records_scanned; /* records with POS inside each slice, summed */
     uint64_t hits;
     double device_ms;         /* HIP-event time of the kernel sequence */
-    uint64_t chained_slices;  /* slices answered by the chain kernel (one wave per request) */
+    uint64_t chained_slices;  /* slices answered by the chain kernel (one chain = one request's slices) */
+    uint64_t chains;
+    /* variantType candidates of the chains: read from the coarse-index superset
+     * (cand_loaded), inside the chain windows (cand_window), and in the union
+     * of the windows (cand_unique: each candidate counted once) */
+    uint64_t cand_loaded, cand_window, cand_unique;
 } sb_batch_stats;
 int sb_result_stats(const sb_result_set *r, sb_batch_stats *out);
 void sb_result_free(sb_result_set *r);
@@ -297,6 +302,25 @@ typedef struct {
 } sb_request_partial;
 int sb_batch_set_owners(sb_batch *b, const uint32_t *owner, size_t nq, uint32_t n_rows);
 int sb_batch_reduce_requests(sb_batch *b, void *dev_out);
+/* The hit lists that go with the rows (the `variants` of each request's
+ * responses, route_g_variants.py:159-171): enqueues, after the preceding run,
+ * dev_hits[row_off[w] .. row_off[w+1]) = row w's hits, each
+ * (record + rec_base) | alt << 32 (rec_base: the shard's first global record,
+ * so rows from several shards name records alike); dev_row_off = n_rows + 1
+ * u64.  dev_rows (optional) = this run's sb_batch_reduce_requests output on
+ * the same stream.  A row lists its queries' hits query by query, except that
+ * when every chain of slices (one request's 10 kb slices answered together)
+ * lies in one row the chain's hits come as one block at its first slice --
+ * the same multiset; the route treats it as a set (route_g_variants.py:160).
+ * Device pointers on the batch's device; dev_hits must hold
+ * sb_batch_get_stats().hits (the planned capacity) entries. */
+int sb_batch_compact_hits(sb_batch *b, const void *dev_rows, void *dev_hits, void *dev_row_off, uint64_t rec_base);
+/* Enqueue this batch's work (run, reduce, compact, and the timing events) on
+ * `stream` -- a hipStream_t of the store's device, e.g. the caller's current
+ * torch stream -- instead of the store's own stream, so it is ordered with the
+ * caller's reads and writes of dev_out / dev_hits and with its collectives;
+ * NULL restores the store's stream.  sb_batch_sync then waits for `stream`. */
+int sb_batch_set_stream(sb_batch *b, void *stream);
 void sb_batch_free(sb_batch *b);
 
 #ifdef __cplusplus

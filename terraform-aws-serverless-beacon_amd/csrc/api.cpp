@@ -193,6 +193,16 @@ struct sb_batch {
     std::vector<uint32_t> chain_members;  // chained queries, chain by chain (device copy: corig)
     uint32_t chain_base = 0;              // first chained slice in the launch-ordered array
     DevMem corig;
+    DevMem srcoff;  // each query's hit-region offset (chained slices: rewritten by chain_src_kernel)
+    DevMem tsum, dense;  // dense hit lists (sb_batch_compact_hits)
+    DevMem cpart;        // per-chain request-row partials (chain_kernel)
+    std::vector<uint64_t> chain_cap;  // hit capacity of each chain (ALTs of its coarse candidate range)
+    // request rows as pieces (sb_batch_set_owners, when every chain lies in one row)
+    bool row_pieces = false;
+    DevMem poff, piece, rows_scratch, rowsrc;
+    uint64_t cand_loaded = 0, cand_window = 0, cand_unique = 0;  // chain candidate statistics
+    hipStream_t stream = nullptr;  // sb_batch_set_stream (nullptr: the store's stream)
+    hipStream_t strm() const { return stream ? stream : s->stream; }
     bool nonneg = true;
     // per-request rows (sb_batch_set_owners): seg = n_rows + 1 query offsets
     uint32_t n_rows = 0;
@@ -439,6 +449,10 @@ void upload_store(sb_builder &b, sb_store &s) {
         // kind) pair, aiming at ~8 candidates per bucket (chain_kernel)
         std::vector<uint32_t> cpos(cw.size() + 1, 0u);
         for (size_t j = 0; j < ci.size(); ++j) cpos[j] = pos[ci[j]];
+        // ALTs of the candidates, as a prefix (a chain's hit capacity: every
+        // ALT of every candidate its coarse-index range can load)
+        s.h_vc_altpre.assign(ci.size() + 1, 0);
+        for (size_t j = 0; j < ci.size(); ++j) s.h_vc_altpre[j + 1] = s.h_vc_altpre[j] + 1 + (x_lo[ci[j] + 1] - x_lo[ci[j]]);
         auto cand_before = [&](uint32_t k, uint64_t r) -> uint32_t {  // global list index
             const VcBlock &b = blk[k * nblk + r / 64];
             const uint32_t o = static_cast<uint32_t>(r % 64);
@@ -492,6 +506,8 @@ void upload_store(sb_builder &b, sb_store &s) {
         s.d.vc_nblk = nblk;
         s.d.vc_pos = dev_upload(s, cpos);
         s.d.vc_bucket = dev_upload(s, vcb);
+        s.h_vc_pos = std::move(cpos);
+        s.h_vc_bucket = std::move(vcb);
     }
     s.d.pos = dev_upload(s, pos);
     s.d.ref_key = dev_upload(s, ref_key);
@@ -612,13 +628,21 @@ std::vector<uint32_t> plan_chains(sb_batch &B, const std::vector<uint32_t> &segi
     };
     std::vector<Ch> ch;
     std::unordered_map<std::string, uint32_t> open;  // filter signature + next first_bp -> chain
-    auto key = [&](const QDev &d, uint32_t i, int64_t next) {
-        struct {
-            uint32_t vcf, seg;
-            int64_t emin, emax, vmin, vmax, next;
-            uint32_t kind, lut, flags;
-        } k{B.vcf[i], d.seg_lo, d.end_min, d.end_max, d.vmin, d.vmax, next, d.vt_kind, d.lut_off, d.flags};
-        return std::string(reinterpret_cast<const char *>(&k), sizeof k);
+    auto key = [&](const QDev &d, uint32_t i, int64_t next) {  // field bytes only (no struct padding)
+        std::string k;
+        k.reserve(60);
+        auto put = [&](const auto &v) { k.append(reinterpret_cast<const char *>(&v), sizeof v); };
+        put(B.vcf[i]);
+        put(d.seg_lo);
+        put(d.end_min);
+        put(d.end_max);
+        put(d.vmin);
+        put(d.vmax);
+        put(next);
+        put(d.vt_kind);
+        put(d.lut_off);
+        put(d.flags);
+        return k;
     };
     for (uint32_t i : vt) {
         const QDev &d = B.hq[i];
@@ -717,6 +741,39 @@ std::vector<uint32_t> plan_chains(sb_batch &B, const std::vector<uint32_t> &segi
             B.chained[i] = 1;
             B.chain_members.push_back(i);
         }
+    }
+    // candidate statistics (roofline pricing of the chain kernel): the
+    // coarse-index superset each chain loads, its exact window, and the union
+    // of the windows (the candidates a step must bring in at least once)
+    std::vector<std::pair<uint32_t, uint32_t>> win(B.hchains.size());
+    std::vector<uint64_t> loaded(B.hchains.size());
+    B.chain_cap.assign(B.hchains.size(), 0);
+    parallel_for(B.hchains.size(), [&](size_t c) {
+        const ChainDev &d = B.hchains[c];
+        auto cb = [&](uint64_t x, uint32_t up) -> uint32_t {
+            if (x <= d.cb_base) return d.c_lo;
+            const uint64_t b = (x - d.cb_base) >> d.cb_shift;
+            return b >= d.cb_n ? d.c_hi : s.h_vc_bucket[d.cb_off + b + up];
+        };
+        const uint32_t C0 = cb(d.first, 0), C1 = (d.kind & kChainEndVoid) ? C0 : std::max(C0, cb(uint64_t(d.last) + 1, 1));
+        loaded[c] = C1 - C0;
+        B.chain_cap[c] = s.h_vc_altpre[C1] - s.h_vc_altpre[C0];
+        auto pb = s.h_vc_pos.begin();
+        const uint32_t a = static_cast<uint32_t>(std::lower_bound(pb + d.c_lo, pb + d.c_hi, d.first) - pb);
+        const uint32_t e = static_cast<uint32_t>(std::upper_bound(pb + d.c_lo, pb + d.c_hi, d.last) - pb);
+        win[c] = {a, std::max(a, e)};
+    });
+    B.cand_loaded = B.cand_window = B.cand_unique = 0;
+    for (size_t c = 0; c < win.size(); ++c) {
+        B.cand_loaded += loaded[c];
+        B.cand_window += win[c].second - win[c].first;
+    }
+    std::sort(win.begin(), win.end());
+    uint64_t reach = 0;
+    for (const auto &w : win) {  // kinds' lists are disjoint ranges of one index space
+        const uint64_t a = std::max<uint64_t>(w.first, reach);
+        if (w.second > a) B.cand_unique += w.second - a;
+        reach = std::max<uint64_t>(reach, w.second);
     }
     std::sort(rest.begin(), rest.end());
     return rest;
@@ -961,13 +1018,11 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
                 at += cap[i];
             }
         size_t m = 0;
-        for (ChainDev &c : B.hchains) {
+        for (size_t k = 0; k < B.hchains.size(); ++k) {
+            ChainDev &c = B.hchains[k];
             c.out = at;
-            for (uint32_t j = 0; j < c.n; ++j, ++m) {
-                const uint32_t i = B.chain_members[m];
-                B.hq[i].hit_off = at;
-                at += cap[i];
-            }
+            for (uint32_t j = 0; j < c.n; ++j, ++m) B.hq[B.chain_members[m]].hit_off = at;
+            at += B.chain_cap[k];
         }
         B.cap_total = at;
     }
@@ -991,6 +1046,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     for (uint32_t i : B.chain_members) lq.push_back(B.hq[i]);
     B.chains.alloc(B.hchains.size() * sizeof(ChainDev));
     B.corig.alloc(B.chain_members.size() * 4);
+    B.cpart.alloc(B.hchains.size() * sizeof(ReqPartial));
     if (!B.hchains.empty()) {
         HIP_OK(hipMemcpyAsync(B.chains.p, B.hchains.data(), B.hchains.size() * sizeof(ChainDev), hipMemcpyHostToDevice,
                               st));
@@ -1006,6 +1062,10 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     B.lut.alloc(lut_all.size() * 4);
     if (nq) HIP_OK(hipMemcpyAsync(B.q.p, lq.data(), nq * sizeof(QDev), hipMemcpyHostToDevice, st));
     if (nq) HIP_OK(hipMemcpyAsync(B.hoff.p, hoff.data(), nq * 8, hipMemcpyHostToDevice, st));
+    if (!B.hchains.empty()) {
+        B.srcoff.alloc(nq * 8);
+        HIP_OK(hipMemcpyAsync(B.srcoff.p, hoff.data(), nq * 8, hipMemcpyHostToDevice, st));
+    }
     if (!qbytes.empty()) HIP_OK(hipMemcpyAsync(B.qbytes.p, qbytes.data(), qbytes.size(), hipMemcpyHostToDevice, st));
     if (!subsets.empty()) HIP_OK(hipMemcpyAsync(B.subsets.p, subsets.data(), subsets.size() * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(B.lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
@@ -1019,7 +1079,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
 void run(sb_batch &B) {
     sb_store &s = *B.s;
     HIP_OK(hipSetDevice(s.device));
-    hipStream_t st = s.stream;
+    hipStream_t st = B.strm();
     DStore d = s.d;
     d.sym_lut = B.lut.as<uint32_t>();
     // timing: one event before the first run since the last sync and one at
@@ -1031,7 +1091,7 @@ void run(sb_batch &B) {
     if (B.runs_pending++ == 0) HIP_OK(hipEventRecord(B.ev[0], st));
     // chains of variantType slices (one wave per request's slices)
     launch_chains(d, B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()), B.corig.as<uint32_t>(),
-                  B.res.as<QRes>(), B.hits.as<uint64_t>(), st);
+                  B.res.as<QRes>(), B.hits.as<uint64_t>(), B.cpart.as<ReqPartial>(), st);
     // sample-free groups: one fused launch, long scans first (range, variantType,
     // general) and point lookups last, so the short waves fill the tail
     std::vector<FusedGroup> fg;
@@ -1051,8 +1111,8 @@ void run(sb_batch &B) {
 
 void sync(sb_batch &B) {
     HIP_OK(hipSetDevice(B.s->device));
-    if (B.runs_pending) HIP_OK(hipEventRecord(B.ev[1], B.s->stream));
-    HIP_OK(hipStreamSynchronize(B.s->stream));
+    if (B.runs_pending) HIP_OK(hipEventRecord(B.ev[1], B.strm()));
+    HIP_OK(hipStreamSynchronize(B.strm()));
     if (B.runs_pending) {  // device time per run = the span / runs (back-to-back launches)
         float x;
         HIP_OK(hipEventElapsedTime(&x, B.ev[0], B.ev[1]));
@@ -1061,10 +1121,19 @@ void sync(sb_batch &B) {
     }
 }
 
+// each query's hit-region offset: chained slices' hits are dense per chain,
+// so theirs follow from the n_hits of the chain's earlier slices
+const uint64_t *src_offsets(sb_batch &B, hipStream_t st) {
+    if (B.hchains.empty()) return B.hoff.as<uint64_t>();
+    launch_chain_src(B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()), B.corig.as<uint32_t>(),
+                     B.res.as<QRes>(), B.srcoff.as<uint64_t>(), st);
+    return B.srcoff.as<uint64_t>();
+}
+
 sb_result_set *fetch(sb_batch &B) {
     sync(B);
     sb_store &s = *B.s;
-    hipStream_t st = s.stream;
+    hipStream_t st = B.strm();
     auto R = std::make_unique<sb_result_set>();
     R->s = &s;
     const uint32_t nq = B.nq;
@@ -1087,17 +1156,7 @@ sb_result_set *fetch(sb_batch &B) {
         doff.alloc((size_t(nq) + 1) * 8);
         dense.alloc(total * 8);
         HIP_OK(hipMemcpyAsync(doff.p, R->dense_off.data(), (size_t(nq) + 1) * 8, hipMemcpyHostToDevice, st));
-        // chained slices' hits are dense per chain: their region offsets follow
-        // from the n_hits of the chain's earlier slices
-        DevMem src;
-        const uint64_t *hoff = B.hoff.as<uint64_t>();
-        if (!B.hchains.empty()) {
-            src.alloc(size_t(nq) * 8);
-            HIP_OK(hipMemcpyAsync(src.p, B.hoff.p, size_t(nq) * 8, hipMemcpyDeviceToDevice, st));
-            launch_chain_src(B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()), B.corig.as<uint32_t>(),
-                             B.res.as<QRes>(), src.as<uint64_t>(), st);
-            hoff = src.as<uint64_t>();
-        }
+        const uint64_t *hoff = src_offsets(B, st);
         // queries with an error report n_hits = 0 on the device (host errors are F_EMPTY)
         launch_compact(hoff, doff.as<uint64_t>(), B.res.as<QRes>(), nq, B.hits.as<uint64_t>(), dense.as<uint64_t>(), st);
         HIP_OK(hipGetLastError());
@@ -1138,6 +1197,10 @@ sb_result_set *fetch(sb_batch &B) {
     R->stats.n_queries = nq;
     R->stats.records_scanned = scanned;
     R->stats.chained_slices = B.chain_members.size();
+    R->stats.chains = B.hchains.size();
+    R->stats.cand_loaded = B.cand_loaded;
+    R->stats.cand_window = B.cand_window;
+    R->stats.cand_unique = B.cand_unique;
     R->stats.hits = total;
     R->stats.device_ms = B.last_total_ms;
     return R.release();
@@ -1805,7 +1868,13 @@ int sb_batch_get_stats(const sb_batch *b, sb_batch_stats *out) {
     if (!b || !out) return SB_EINVAL;
     out->n_queries = b->nq;
     out->records_scanned = 0;
+    for (uint32_t i = 0; i < b->nq && !b->chained.empty(); ++i)
+        if (b->chained[i]) out->records_scanned += b->nscan[i];
     out->chained_slices = b->chain_members.size();
+    out->chains = b->hchains.size();
+    out->cand_loaded = b->cand_loaded;
+    out->cand_window = b->cand_window;
+    out->cand_unique = b->cand_unique;
     out->hits = b->cap_total;
     out->device_ms = b->last_total_ms;
     return SB_OK;
@@ -1824,6 +1893,36 @@ int sb_batch_set_owners(sb_batch *b, const uint32_t *owner, size_t nq, uint32_t 
             ++seg[owner[i] + 1];
         }
         for (uint32_t w = 0; w < n_rows; ++w) seg[w + 1] += seg[w];
+        // rows as pieces when every chain lies in one row: a chain is listed at
+        // its first slice, unchained queries one by one, in query order
+        std::vector<uint32_t> chain_of(b->chained.empty() ? 0 : nq, UINT32_MAX);
+        bool pieces_ok = true;
+        {
+            size_t m = 0;
+            for (uint32_t c = 0; c < b->hchains.size(); ++c)
+                for (uint32_t j = 0; j < b->hchains[c].n; ++j, ++m) {
+                    const uint32_t i = b->chain_members[m];
+                    chain_of[i] = c;
+                    if (owner[i] != owner[b->chain_members[m - j]]) pieces_ok = false;
+                }
+        }
+        std::vector<uint32_t> poff(size_t(n_rows) + 1, 0), piece;
+        if (pieces_ok) {
+            std::vector<uint8_t> listed(b->hchains.size(), 0);
+            for (size_t i = 0; i < nq; ++i) {
+                const uint32_t c = chain_of.empty() ? UINT32_MAX : chain_of[i];
+                if (c == UINT32_MAX) {
+                    piece.push_back(static_cast<uint32_t>(i));
+                } else if (!listed[c]) {
+                    listed[c] = 1;
+                    piece.push_back(c | (1u << 31));
+                } else {
+                    continue;
+                }
+                ++poff[owner[i] + 1];
+            }
+            for (uint32_t w = 0; w < n_rows; ++w) poff[w + 1] += poff[w];
+        }
         std::vector<uint8_t> he(std::max<size_t>(nq, 1), 0);
         for (size_t i = 0; i < nq; ++i) he[i] = b->host_err[i] ? 1 : 0;
         std::lock_guard<std::mutex> lk(b->s->mu);
@@ -1833,6 +1932,15 @@ int sb_batch_set_owners(sb_batch *b, const uint32_t *owner, size_t nq, uint32_t 
         b->herr.alloc(he.size());
         HIP_OK(hipMemcpyAsync(b->seg.p, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, st));
         HIP_OK(hipMemcpyAsync(b->herr.p, he.data(), he.size(), hipMemcpyHostToDevice, st));
+        b->row_pieces = pieces_ok;
+        if (pieces_ok) {
+            b->rowsrc.alloc(std::max<size_t>(n_rows, 1) * 16);
+            b->poff.alloc(poff.size() * 4);
+            b->piece.alloc(std::max<size_t>(piece.size(), 1) * 4);
+            HIP_OK(hipMemcpyAsync(b->poff.p, poff.data(), poff.size() * 4, hipMemcpyHostToDevice, st));
+            if (!piece.empty())
+                HIP_OK(hipMemcpyAsync(b->piece.p, piece.data(), piece.size() * 4, hipMemcpyHostToDevice, st));
+        }
         HIP_OK(hipStreamSynchronize(st));
         b->n_rows = n_rows;
     });
@@ -1844,8 +1952,57 @@ int sb_batch_reduce_requests(sb_batch *b, void *dev_out) {
         if (!b->seg.p && b->n_rows) throw Error(SB_EINVAL, "sb_batch_set_owners was not called");
         std::lock_guard<std::mutex> lk(b->s->mu);
         HIP_OK(hipSetDevice(b->s->device));
-        launch_request_reduce(b->res.as<QRes>(), b->seg.as<uint32_t>(), b->herr.as<uint8_t>(), b->n_rows,
-                              static_cast<ReqPartial *>(dev_out), b->s->stream);
+        if (b->row_pieces)
+            launch_row_reduce(b->cpart.as<ReqPartial>(), b->chains.as<ChainDev>(), b->hoff.as<uint64_t>(),
+                              b->res.as<QRes>(), b->herr.as<uint8_t>(), b->poff.as<uint32_t>(),
+                              b->piece.as<uint32_t>(), b->n_rows, static_cast<ReqPartial *>(dev_out),
+                              b->rowsrc.as<ulonglong2>(), b->strm());
+        else
+            launch_request_reduce(b->res.as<QRes>(), b->seg.as<uint32_t>(), b->herr.as<uint8_t>(), b->n_rows,
+                                  static_cast<ReqPartial *>(dev_out), b->strm());
+        HIP_OK(hipGetLastError());
+    });
+}
+
+int sb_batch_set_stream(sb_batch *b, void *stream) {
+    return guard([&] {
+        if (!b) throw Error(SB_EINVAL, "NULL batch");
+        std::lock_guard<std::mutex> lk(b->s->mu);
+        if (b->runs_pending) throw Error(SB_EINVAL, "sb_batch_set_stream between a run and its sync");
+        b->stream = static_cast<hipStream_t>(stream);
+    });
+}
+
+int sb_batch_compact_hits(sb_batch *b, const void *dev_rows, void *dev_hits, void *dev_row_off, uint64_t rec_base) {
+    return guard([&] {
+        if (!b || (!dev_hits && b->cap_total) || !dev_row_off) throw Error(SB_EINVAL, "NULL argument");
+        if (!b->seg.p) throw Error(SB_EINVAL, "sb_batch_set_owners was not called");
+        std::lock_guard<std::mutex> lk(b->s->mu);
+        HIP_OK(hipSetDevice(b->s->device));
+        hipStream_t st = b->strm();
+        if (b->row_pieces) {  // over rows and pieces (chains as one contiguous copy each)
+            const ReqPartial *rows = static_cast<const ReqPartial *>(dev_rows);
+            if (!rows) {  // (the reduction also leaves rowsrc for the gather)
+                b->rows_scratch.reserve(std::max<size_t>(b->n_rows, 1) * sizeof(ReqPartial));
+                launch_row_reduce(b->cpart.as<ReqPartial>(), b->chains.as<ChainDev>(), b->hoff.as<uint64_t>(),
+                                  b->res.as<QRes>(), b->herr.as<uint8_t>(), b->poff.as<uint32_t>(),
+                                  b->piece.as<uint32_t>(), b->n_rows, b->rows_scratch.as<ReqPartial>(),
+                                  b->rowsrc.as<ulonglong2>(), st);
+                rows = b->rows_scratch.as<ReqPartial>();
+            }
+            b->tsum.reserve(hit_scan_words(b->n_rows) * 8);
+            launch_row_hit_lists(rows, b->rowsrc.as<ulonglong2>(), b->poff.as<uint32_t>(), b->piece.as<uint32_t>(),
+                                 b->n_rows, b->chains.as<ChainDev>(), b->cpart.as<ReqPartial>(), b->res.as<QRes>(),
+                                 b->hoff.as<uint64_t>(), b->hits.as<uint64_t>(), rec_base, b->tsum.as<uint64_t>(),
+                                 static_cast<uint64_t *>(dev_row_off), static_cast<uint64_t *>(dev_hits), st);
+        } else {  // over queries
+            b->tsum.reserve(hit_scan_words(b->nq) * 8);
+            b->dense.reserve((size_t(b->nq) + 1) * 8);
+            const uint64_t *src = src_offsets(*b, st);
+            launch_hit_lists(b->res.as<QRes>(), b->nq, src, b->hits.as<uint64_t>(), rec_base, b->seg.as<uint32_t>(),
+                             b->n_rows, b->tsum.as<uint64_t>(), b->dense.as<uint64_t>(),
+                             static_cast<uint64_t *>(dev_hits), static_cast<uint64_t *>(dev_row_off), st);
+        }
         HIP_OK(hipGetLastError());
     });
 }

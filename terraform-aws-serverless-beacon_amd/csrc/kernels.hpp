@@ -37,7 +37,7 @@ void launch_fused(const DStore &st, const FusedGroup *groups, int count, bool no
 // chain-ordered slice s.  launch_chain_src writes the hit-region offset of
 // every chained slice (dense per chain) into src[batch index].
 void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, QRes *res,
-                   uint64_t *hits, hipStream_t s);
+                   uint64_t *hits, ReqPartial *cpart, hipStream_t s);
 void launch_chain_src(const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, const QRes *res,
                       uint64_t *src, hipStream_t s);
 
@@ -53,6 +53,30 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const u
 // the answers of queries [seg[w], seg[w+1]).
 void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, uint32_t n_rows,
                            ReqPartial *out, hipStream_t s);
+
+// Dense per-query hit lists on the device: dense[q] = exclusive prefix of the
+// queries' hit counts (dense[nq] = total), out[dense[q] ..] = query q's hits
+// (from its region at src[q]) + rec_base; row_off[w] = dense[seg[w]] for
+// w <= n_rows when seg is given.  tsum needs hit_scan_words(nq) words.
+size_t hit_scan_words(uint32_t nq);
+void launch_hit_lists(const QRes *res, uint32_t nq, const uint64_t *src, const uint64_t *hits, uint64_t rec_base,
+                      const uint32_t *seg, uint32_t n_rows, uint64_t *tsum, uint64_t *dense, uint64_t *out,
+                      uint64_t *row_off, hipStream_t s);
+
+// Request rows by pieces (chains + unchained queries; piece bit 31 = chain):
+// row_reduce sums each row's pieces (chain partials from chain_kernel's
+// cpart, QRes otherwise); row_hit_lists scans the rows' n_variants into
+// row_off (n_rows + 1) and copies each row's pieces' hits to out[row_off[w]..]
+// with rec_base added.  tsum needs hit_scan_words(n_rows) words.
+// rowsrc (n_rows x {hit region, count}; {~0, 0} = several pieces) is written
+// by row_reduce and read by row_hit_lists.
+void launch_row_reduce(const ReqPartial *cpart, const ChainDev *chains, const uint64_t *hoff, const QRes *res,
+                       const uint8_t *host_err, const uint32_t *poff, const uint32_t *piece, uint32_t n_rows,
+                       ReqPartial *out, ulonglong2 *rowsrc, hipStream_t s);
+void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, const uint32_t *poff,
+                          const uint32_t *piece, uint32_t n_rows, const ChainDev *chains, const ReqPartial *cpart,
+                          const QRes *res, const uint64_t *hoff, const uint64_t *hits, uint64_t rec_base,
+                          uint64_t *tsum, uint64_t *row_off, uint64_t *out, hipStream_t s);
 
 // Fetch-time gather of every query's hits into one dense array.
 void launch_compact(const uint64_t *hit_off, const uint64_t *dense_off, const QRes *res, uint32_t nq,

@@ -1307,6 +1307,7 @@ constexpr uint32_t kChainRun = 8;  // chains per wave (lanes 8k..8k+7 hold chain
 struct ChainLds {
     unsigned long long cc[kChainMax], an[kChainMax];
     unsigned int nh[kChainMax], ex[kChainMax];
+    unsigned long long tcc, tan;  // chain totals (cpart)
 };
 
 struct ChainChunk {
@@ -1318,7 +1319,7 @@ struct ChainChunk {
 __global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const ChainDev *__restrict__ chains,
                                                        uint32_t n_chains, uint32_t run,
                                                        const uint32_t *__restrict__ corig, QRes *__restrict__ res,
-                                                       uint64_t *__restrict__ hits) {
+                                                       uint64_t *__restrict__ hits, ReqPartial *__restrict__ cpart) {
     __shared__ ChainLds lds_all[kWavesPerBlock];
     const uint32_t c_first = launch_wave() * run;
     if (c_first >= n_chains) return;
@@ -1412,6 +1413,8 @@ __global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const ChainDev
         if (hit) {
             atomicAdd(&L.cc[sid], static_cast<unsigned long long>(o.c));
             atomicAdd(&L.an[sid], static_cast<unsigned long long>(o.anv));
+            atomicAdd(&L.tcc, static_cast<unsigned long long>(o.c));
+            atomicAdd(&L.tan, static_cast<unsigned long long>(o.anv));
             if (o.c > 0) L.ex[sid] = 1u;
         }
         X.nout += total;
@@ -1439,22 +1442,37 @@ __global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const ChainDev
             L.nh[ul] = 0;
             L.ex[ul] = 0;
         }
+        if (lane == 0) {
+            L.tcc = 0;
+            L.tan = 0;
+        }
         if (C0 < C1) {
             eval_chunk(X, P, cur, C0, C1);
             for (uint32_t base = C0 + kWave; base < C1; base += kWave)  // chains longer than one chunk
                 eval_chunk(X, P, load_chunk(C1, base), base, C1);
         }
-        if (ul < X.n) {
+        const bool sl = ul < X.n;
+        const bool ex = sl && L.ex[ul];
+        const int64_t cc = sl ? static_cast<int64_t>(L.cc[ul]) : 0, an = sl ? static_cast<int64_t>(L.an[ul]) : 0;
+        if (sl) {
             QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host (prepare knows each slice's record range)
             if (X.slow) {
                 o.error = SB_QERR_UNSUPPORTED;  // never: prepare routes chains with a VT_SLOW record to vt_slice
             } else {
-                o.exists = L.ex[ul] ? 1 : 0;
-                o.call_count = static_cast<int64_t>(L.cc[ul]);
-                o.all_alleles_count = static_cast<int64_t>(L.an[ul]);
+                o.exists = ex ? 1 : 0;
+                o.call_count = cc;
+                o.all_alleles_count = an;
                 o.n_hits = L.nh[ul];
             }
             res[orig] = o;
+        }
+        if (cpart) {  // the chain's request-row partial (sb_batch_reduce_requests of its slices)
+            const uint64_t exm = __ballot(ex);
+            if (lane == 0)
+                cpart[c_first + k] =
+                    X.slow ? ReqPartial{0, 0, 0, 0, static_cast<int64_t>(X.n)}
+                           : ReqPartial{__popcll(exm), static_cast<int64_t>(X.nout), static_cast<int64_t>(L.tcc),
+                                        static_cast<int64_t>(L.tan), 0};
         }
         return nxt;
     };
@@ -1484,6 +1502,235 @@ __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__res
         const uint32_t q = corig[C.s0 + j];
         src[q] = at;
         at += res[q].error ? 0u : res[q].n_hits;
+    }
+}
+
+// ---------------------------------------------------------------- dense hit lists
+// Device-side result delivery for a sharded fan-out (sb_batch_compact_hits):
+// dense[q] = exclusive prefix over queries of their emitted hit counts (0 for
+// a query that raised), in three launches (tile sums, one-block scan of the
+// tile sums, tile scans); then every query's hits are copied from its region
+// to dense[q] with the shard's global record base added, and each request
+// row's first dense offset is read off at its first query.
+constexpr uint32_t kScanPer = 4;                    // items per thread
+constexpr uint32_t kScanTile = kBlock * kScanPer;  // items per workgroup
+
+__device__ __forceinline__ uint64_t hit_count(const QRes &r) { return r.error ? 0u : r.n_hits; }
+
+// inclusive sum over the workgroup of one value per thread (LDS of the wave totals)
+__device__ __forceinline__ uint64_t block_incl_scan(uint64_t v, uint64_t *wsum) {
+    const int wave = threadIdx.x >> 6;
+    const uint64_t incl = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(v)));
+    if (lane_id() == kWave - 1) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t before = 0;
+    for (int w = 0; w < wave; ++w) before += wsum[w];
+    __syncthreads();
+    return incl + before;
+}
+
+__global__ __launch_bounds__(kBlock) void hit_tile_sum_kernel(const QRes *__restrict__ res, uint32_t nq,
+                                                              uint64_t *__restrict__ tsum) {
+    __shared__ uint64_t wsum[kWavesPerBlock];
+    const uint32_t i0 = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    uint64_t v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k)
+        if (i0 + k < nq) v += hit_count(res[i0 + k]);
+    const uint64_t t = block_incl_scan(v, wsum);
+    if (threadIdx.x == kBlock - 1) tsum[blockIdx.x] = t;
+}
+
+// exclusive scan of tsum[0 .. nt) in place by one workgroup; tsum[nt] = total
+__global__ __launch_bounds__(kBlock) void tile_scan_kernel(uint64_t *__restrict__ tsum, uint32_t nt) {
+    __shared__ uint64_t wsum[kWavesPerBlock];
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < nt; base += kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        const uint64_t v = i < nt ? tsum[i] : 0u;
+        const uint64_t incl = block_incl_scan(v, wsum);
+        if (i < nt) tsum[i] = carry + incl - v;
+        if (threadIdx.x == kBlock - 1) wsum[0] = incl;  // block_incl_scan's LDS is free again here
+        __syncthreads();
+        carry += wsum[0];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) tsum[nt] = carry;
+}
+
+__global__ __launch_bounds__(kBlock) void hit_tile_scan_kernel(const QRes *__restrict__ res, uint32_t nq,
+                                                               const uint64_t *__restrict__ tsum,
+                                                               uint64_t *__restrict__ dense) {
+    __shared__ uint64_t wsum[kWavesPerBlock];
+    const uint32_t i0 = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    uint64_t c[kScanPer], v = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        c[k] = i0 + k < nq ? hit_count(res[i0 + k]) : 0u;
+        v += c[k];
+    }
+    uint64_t at = tsum[blockIdx.x] + block_incl_scan(v, wsum) - v;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        if (i0 + k < nq) dense[i0 + k] = at;
+        at += c[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) dense[nq] = tsum[gridDim.x];
+}
+
+// thread per query (most queries emit 0-3 hits)
+__global__ __launch_bounds__(kBlock) void hit_gather_kernel(const QRes *__restrict__ res, uint32_t nq,
+                                                            const uint64_t *__restrict__ src,
+                                                            const uint64_t *__restrict__ dense,
+                                                            const uint64_t *__restrict__ hits, uint64_t rec_base,
+                                                            uint64_t *__restrict__ out) {
+    const uint32_t q = blockIdx.x * kBlock + threadIdx.x;
+    if (q >= nq) return;
+    const uint64_t n = hit_count(res[q]), a = src[q], d = dense[q];
+    for (uint64_t k = 0; k < n; ++k) out[d + k] = hits[a + k] + rec_base;
+}
+
+__global__ __launch_bounds__(kBlock) void row_off_kernel(const uint32_t *__restrict__ seg, uint32_t n_rows,
+                                                         const uint64_t *__restrict__ dense,
+                                                         uint64_t *__restrict__ row_off) {
+    const uint32_t w = blockIdx.x * kBlock + threadIdx.x;
+    if (w <= n_rows) row_off[w] = dense[seg[w]];
+}
+
+// ---------------------------------------------------------------- request rows by pieces
+// When every chain lies in one request row (sb_batch_set_owners checks), a
+// row is a list of pieces -- chains (their partial rows come from
+// chain_kernel) and unchained queries (QRes) -- so the reduction, the scan of
+// the rows' hit counts and the hit gather run over rows and pieces (10^6)
+// instead of slices (5 x 10^6), and a chain's hits are one contiguous copy.
+// piece p: bit 31 set = chain (p & 0x7fffffff), else a query index.
+constexpr uint32_t kPieceChain = 1u << 31;
+
+// rowsrc[w] = {hit region, count} of a single-piece row ({~0, 0} otherwise):
+// the gather then needs no piece lookups for it
+__global__ __launch_bounds__(kBlock) void row_reduce_kernel(const ReqPartial *__restrict__ cpart,
+                                                            const ChainDev *__restrict__ chains,
+                                                            const uint64_t *__restrict__ hoff,
+                                                            const QRes *__restrict__ res,
+                                                            const uint8_t *__restrict__ host_err,
+                                                            const uint32_t *__restrict__ poff,
+                                                            const uint32_t *__restrict__ piece, uint32_t n_rows,
+                                                            ReqPartial *__restrict__ out, ulonglong2 *__restrict__ rowsrc) {
+    const uint32_t w = blockIdx.x * kBlock + threadIdx.x;
+    if (w >= n_rows) return;
+    ReqPartial P{0, 0, 0, 0, 0};
+    const uint32_t k0 = poff[w], k1 = poff[w + 1];
+    if (rowsrc) {
+        ulonglong2 rs{~0ull, 0ull};
+        if (k1 == k0 + 1) {
+            const uint32_t p = piece[k0];
+            if (p & kPieceChain) {
+                rs.x = chains[p & ~kPieceChain].out;
+                rs.y = static_cast<uint64_t>(cpart[p & ~kPieceChain].n_variants);
+            } else {
+                rs.x = hoff[p];
+                rs.y = hit_count(res[p]);
+            }
+        } else if (k1 == k0) {
+            rs.x = 0;
+        }
+        rowsrc[w] = rs;
+    }
+    for (uint32_t k = k0; k < k1; ++k) {
+        const uint32_t p = piece[k];
+        if (p & kPieceChain) {
+            const ReqPartial c = cpart[p & ~kPieceChain];
+            P.exists += c.exists;
+            P.n_variants += c.n_variants;
+            P.call_count += c.call_count;
+            P.all_alleles_count += c.all_alleles_count;
+            P.errors += c.errors;
+        } else {
+            const QRes r = res[p];
+            if (r.error || host_err[p]) {
+                ++P.errors;
+                continue;
+            }
+            P.exists += r.exists != 0;
+            P.n_variants += r.n_hits;
+            P.call_count += r.call_count;
+            P.all_alleles_count += r.all_alleles_count;
+        }
+    }
+    out[w] = P;
+}
+
+// tile sums / tile scans of one int64 field of a strided array (ReqPartial rows)
+__global__ __launch_bounds__(kBlock) void field_tile_sum_kernel(const int64_t *__restrict__ v, uint32_t stride,
+                                                                uint32_t n, uint64_t *__restrict__ tsum) {
+    __shared__ uint64_t wsum[kWavesPerBlock];
+    const uint32_t i0 = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    uint64_t x = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k)
+        if (i0 + k < n) x += static_cast<uint64_t>(v[static_cast<size_t>(i0 + k) * stride]);
+    const uint64_t t = block_incl_scan(x, wsum);
+    if (threadIdx.x == kBlock - 1) tsum[blockIdx.x] = t;
+}
+
+__global__ __launch_bounds__(kBlock) void field_tile_scan_kernel(const int64_t *__restrict__ v, uint32_t stride,
+                                                                 uint32_t n, const uint64_t *__restrict__ tsum,
+                                                                 uint64_t *__restrict__ out) {
+    __shared__ uint64_t wsum[kWavesPerBlock];
+    const uint32_t i0 = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    uint64_t c[kScanPer], x = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        c[k] = i0 + k < n ? static_cast<uint64_t>(v[static_cast<size_t>(i0 + k) * stride]) : 0u;
+        x += c[k];
+    }
+    uint64_t at = tsum[blockIdx.x] + block_incl_scan(x, wsum) - x;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        if (i0 + k < n) out[i0 + k] = at;
+        at += c[k];
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = tsum[gridDim.x];
+}
+
+// a team of kGatherTeam lanes per row: its pieces' hits, in piece order,
+// from row_off[w], the team's lanes striding over each piece (a row holds a
+// handful of hits: a lane per row would issue one scattered 8-byte access per
+// hit, a team moves up to 64 contiguous bytes per access)
+constexpr uint32_t kGatherTeam = 8;
+
+__global__ __launch_bounds__(kBlock) void row_gather_kernel(const uint32_t *__restrict__ poff,
+                                                            const uint32_t *__restrict__ piece, uint32_t n_rows,
+                                                            const ChainDev *__restrict__ chains,
+                                                            const ReqPartial *__restrict__ cpart,
+                                                            const QRes *__restrict__ res,
+                                                            const uint64_t *__restrict__ hoff,
+                                                            const uint64_t *__restrict__ hits, uint64_t rec_base,
+                                                            const uint64_t *__restrict__ row_off,
+                                                            const ulonglong2 *__restrict__ rowsrc,
+                                                            uint64_t *__restrict__ out) {
+    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t w = t / kGatherTeam, m = t % kGatherTeam;
+    if (w >= n_rows) return;
+    uint64_t d = row_off[w];
+    const ulonglong2 rs = rowsrc[w];
+    if (rs.x != ~0ull) {  // a single piece (or none): one contiguous copy
+        for (uint64_t j = m; j < rs.y; j += kGatherTeam) out[d + j] = hits[rs.x + j] + rec_base;
+        return;
+    }
+    for (uint32_t k = poff[w], e = poff[w + 1]; k < e; ++k) {
+        const uint32_t p = piece[k];
+        uint64_t a, n;
+        if (p & kPieceChain) {
+            const uint32_t c = p & ~kPieceChain;
+            a = chains[c].out;
+            n = static_cast<uint64_t>(cpart[c].n_variants);
+        } else {
+            a = hoff[p];
+            n = hit_count(res[p]);
+        }
+        for (uint64_t j = m; j < n; j += kGatherTeam) out[d + j] = hits[a + j] + rec_base;
+        d += n;
     }
 }
 
@@ -1744,7 +1991,7 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const u
 }
 
 void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, QRes *res,
-                   uint64_t *hits, hipStream_t s) {
+                   uint64_t *hits, ReqPartial *cpart, hipStream_t s) {
     if (!n_chains) return;
     // runs of kChainRun chains per wave while the launch still fills the chip
     // (256 CUs x 4 SIMDs x 8 waves, 4 deep)
@@ -1756,7 +2003,7 @@ void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, 
         while (run > 1 && (n_chains + run - 1) / run < 32768u) run >>= 1;
     }
     hipLaunchKernelGGL(chain_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st, chains,
-                       n_chains, run, corig, res, hits);
+                       n_chains, run, corig, res, hits, cpart);
 }
 
 void launch_chain_src(const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, const QRes *res,
@@ -1764,6 +2011,53 @@ void launch_chain_src(const ChainDev *chains, uint32_t n_chains, const uint32_t 
     if (!n_chains) return;
     hipLaunchKernelGGL(chain_src_kernel, dim3((n_chains + kBlock - 1) / kBlock), dim3(kBlock), 0, s, chains, n_chains,
                        corig, res, src);
+}
+
+size_t hit_scan_words(uint32_t nq) { return (nq + kScanTile - 1) / kScanTile + 1; }
+
+void launch_hit_lists(const QRes *res, uint32_t nq, const uint64_t *src, const uint64_t *hits, uint64_t rec_base,
+                      const uint32_t *seg, uint32_t n_rows, uint64_t *tsum, uint64_t *dense, uint64_t *out,
+                      uint64_t *row_off, hipStream_t s) {
+    const uint32_t nt = (nq + kScanTile - 1) / kScanTile;
+    if (nt) hipLaunchKernelGGL(hit_tile_sum_kernel, dim3(nt), dim3(kBlock), 0, s, res, nq, tsum);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kBlock), 0, s, tsum, nt);
+    if (nt) {
+        hipLaunchKernelGGL(hit_tile_scan_kernel, dim3(nt), dim3(kBlock), 0, s, res, nq, tsum, dense);
+        hipLaunchKernelGGL(hit_gather_kernel, dim3((nq + kBlock - 1) / kBlock), dim3(kBlock), 0, s, res, nq, src, dense,
+                           hits, rec_base, out);
+    } else {
+        (void)hipMemsetAsync(dense, 0, 8, s);
+    }
+    if (seg && row_off)
+        hipLaunchKernelGGL(row_off_kernel, dim3((n_rows + 1 + kBlock - 1) / kBlock), dim3(kBlock), 0, s, seg, n_rows,
+                           dense, row_off);
+}
+
+void launch_row_reduce(const ReqPartial *cpart, const ChainDev *chains, const uint64_t *hoff, const QRes *res,
+                       const uint8_t *host_err, const uint32_t *poff, const uint32_t *piece, uint32_t n_rows,
+                       ReqPartial *out, ulonglong2 *rowsrc, hipStream_t s) {
+    if (!n_rows) return;
+    hipLaunchKernelGGL(row_reduce_kernel, dim3((n_rows + kBlock - 1) / kBlock), dim3(kBlock), 0, s, cpart, chains,
+                       hoff, res, host_err, poff, piece, n_rows, out, rowsrc);
+}
+
+void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, const uint32_t *poff,
+                          const uint32_t *piece, uint32_t n_rows, const ChainDev *chains, const ReqPartial *cpart,
+                          const QRes *res, const uint64_t *hoff, const uint64_t *hits, uint64_t rec_base,
+                          uint64_t *tsum, uint64_t *row_off, uint64_t *out, hipStream_t s) {
+    const uint32_t nt = (n_rows + kScanTile - 1) / kScanTile;
+    const int64_t *nv = reinterpret_cast<const int64_t *>(rows) + 1;  // ReqPartial::n_variants
+    constexpr uint32_t stride = sizeof(ReqPartial) / sizeof(int64_t);
+    if (nt) hipLaunchKernelGGL(field_tile_sum_kernel, dim3(nt), dim3(kBlock), 0, s, nv, stride, n_rows, tsum);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kBlock), 0, s, tsum, nt);
+    if (!nt) {
+        (void)hipMemsetAsync(row_off, 0, 8, s);
+        return;
+    }
+    hipLaunchKernelGGL(field_tile_scan_kernel, dim3(nt), dim3(kBlock), 0, s, nv, stride, n_rows, tsum, row_off);
+    const uint64_t threads = static_cast<uint64_t>(n_rows) * kGatherTeam;
+    hipLaunchKernelGGL(row_gather_kernel, dim3(static_cast<uint32_t>((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+                       s, poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
 }
 
 void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, uint32_t n_rows,

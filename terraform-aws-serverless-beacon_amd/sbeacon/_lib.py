@@ -55,7 +55,8 @@ class ResultView(C.Structure):
 
 class BatchStats(C.Structure):
     _fields_ = [('n_queries', C.c_uint64), ('records_scanned', C.c_uint64), ('hits', C.c_uint64),
-                ('device_ms', C.c_double), ('chained_slices', C.c_uint64)]
+                ('device_ms', C.c_double), ('chained_slices', C.c_uint64), ('chains', C.c_uint64),
+                ('cand_loaded', C.c_uint64), ('cand_window', C.c_uint64), ('cand_unique', C.c_uint64)]
 
 
 class Slice(C.Structure):
@@ -116,6 +117,8 @@ SIGNATURES = {
     'sb_batch_free': (None, [P]),
     'sb_batch_set_owners': (C.c_int, [P, C.POINTER(C.c_uint32), C.c_size_t, C.c_uint32]),
     'sb_batch_reduce_requests': (C.c_int, [P, C.c_void_p]),
+    'sb_batch_compact_hits': (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    'sb_batch_set_stream': (C.c_int, [P, C.c_void_p]),
     'sb_summarise_slices': (C.c_int, [P, C.POINTER(Slice), C.c_size_t, C.POINTER(SliceStats),
                                       C.POINTER(C.c_double)]),
     'sb_slice_region_files': (C.c_int, [P, C.POINTER(Slice), C.c_size_t, C.c_int, C.POINTER(C.c_int32),

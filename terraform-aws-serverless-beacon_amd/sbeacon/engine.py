@@ -348,6 +348,25 @@ class Batch:
         all_alleles_count, errors)."""
         check(lib().sb_batch_reduce_requests(self._h, C.c_void_p(dev_ptr)))
 
+    def compact_hits(self, hits_ptr: int, row_off_ptr: int, rec_base: int = 0, rows_ptr: int = 0):
+        """Enqueue the rows' dense hit lists (sb_batch_compact_hits): hits
+        (capacity ``stats()['hits']`` u64 on the device) and n_rows + 1 row
+        offsets; records numbered from ``rec_base``; ``rows_ptr`` = this run's
+        reduce_requests output (optional)."""
+        check(lib().sb_batch_compact_hits(self._h, C.c_void_p(rows_ptr) if rows_ptr else None, C.c_void_p(hits_ptr),
+                                          C.c_void_p(row_off_ptr), int(rec_base)))
+
+    def set_stream(self, stream_ptr):
+        """Run this batch's work on a caller stream (e.g.
+        ``torch.cuda.current_stream().cuda_stream``); None = the store's."""
+        check(lib().sb_batch_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def stats(self) -> dict:
+        """Planning statistics (hits = the planned hit capacity)."""
+        s = BatchStats()
+        check(lib().sb_batch_get_stats(self._h, C.byref(s)))
+        return {f: getattr(s, f) for f, _ in BatchStats._fields_}
+
     def fetch(self) -> 'ResultSet':
         r = C.c_void_p()
         check(lib().sb_batch_fetch(self._h, C.byref(r)))

@@ -203,7 +203,14 @@ def rank_of_slices(shape: GenomeShape, world: int, ci: np.ndarray, a: np.ndarray
 
 
 def shard_slices(shape: GenomeShape, reqs: Requests, world: int, rank: int) -> ShardSlices:
-    req, a, b, emin, emax = request_slices(reqs)
+    # only requests whose [start_min, start_max] reaches this rank's core are expanded
+    smin = reqs.start + 1
+    smax = reqs.start + reqs.width + 1
+    near = (rank_of_slices(shape, world, reqs.ci, smin) <= rank) & (rank_of_slices(shape, world, reqs.ci, smax) >= rank)
+    idx = np.flatnonzero(near)
+    sub = Requests(reqs.ci[idx], reqs.start[idx], reqs.width[idx], reqs.vt[idx], reqs.vmin[idx], reqs.vmax[idx])
+    req, a, b, emin, emax = request_slices(sub)
+    req = idx[req] if len(idx) else req
     ci = reqs.ci[req]
     mine = rank_of_slices(shape, world, ci, a) == rank
     req, a, b, emin, emax, ci = req[mine], a[mine], b[mine], emin[mine], emax[mine], ci[mine]
@@ -322,3 +329,21 @@ def union_rows(shape: GenomeShape, sl: ShardSlices) -> int:
         pos = shape.gen(int(ci)).positions().astype(np.int64)
         total += int((np.searchsorted(pos, ub, side='right') - np.searchsorted(pos, ua, side='left')).sum())
     return total
+
+
+def first_rank_of_rows(shape: GenomeShape, reqs: Requests, world: int, sl: ShardSlices) -> np.ndarray:
+    """Rank holding the first slice of each of the window's request rows (the
+    request's host-facing rank in ResultExchange 'first' mode)."""
+    rows = sl.row_lo + np.arange(sl.n_rows)
+    return rank_of_slices(shape, world, reqs.ci[rows], reqs.start[rows] + 1)
+
+
+def shard_record_base(shape: GenomeShape, world: int, rank: int) -> int:
+    """Global record index (contig order) of the first record of rank's shard
+    store: shard record i is global record base + i (its pieces are
+    consecutive in that order)."""
+    pieces = shape.shard_pieces(world, rank)
+    if not pieces:
+        return 0
+    ci, lo, _ = pieces[0]
+    return int(shape.offsets[ci]) + lo

@@ -17,6 +17,14 @@ lies in its core.  Per step:
 
 The per-slice semantics never cross GPUs (halo, see genome.py), so the only
 exchange is this gather of per-request rows: 40 B x the rank's requests.
+
+:class:`ResultExchange` delivers rows AND hit lists (the ``variants`` of the
+responses) to each request's host-facing rank: 'first' = the rank holding the
+request's first slice (only requests that straddle a shard cut move, so the
+exchange stays a few KB whatever N), 'rank0' = one host-facing rank for all.
+Per step: an all_gather of every rank's per-destination (row, hit) counts,
+then point-to-point sends of those row / hit ranges (a gatherv; RCCL
+send / recv over xGMI, gloo on CPU), then the receiver sums the rows.
 """
 from __future__ import annotations
 
@@ -87,3 +95,142 @@ def request_rows_from_responses(owner, responses, n_rows):
         out[o, 2] += d['call_count']
         out[o, 3] += d['all_alleles_count']
     return out
+
+
+MODES = ('first', 'rank0')
+
+
+class ResultExchange:
+    """Per-step delivery of request rows + dense hit lists (sb_batch_compact_hits
+    layout) to their host-facing ranks.
+
+    ``owners``: owner rank of each of this rank's window rows (non-decreasing;
+    ``owner_ranks`` builds them).  After :meth:`exchange`, :attr:`rows` holds
+    the combined rows of the requests this rank owns (global request rows
+    ``[own_lo, own_lo + n_own)``) and :meth:`hit_lists` yields each owned
+    request's hits: its own slices' first, then each sender's in rank order
+    (= position order: shards are cut in (contig, POS) order)."""
+
+    def __init__(self, dist, rank: int, world: int, row_lo: int, n_rows: int, owners, device):
+        import torch
+        self.dist, self.rank, self.world, self.device = dist, rank, world, device
+        owners = np.asarray(owners, dtype=np.int64)
+        assert len(owners) == n_rows and (np.diff(owners) >= 0).all()
+        self.row_lo, self.n_rows = row_lo, n_rows
+        # my rows per destination: [a, b) window rows
+        self.sends = []
+        for d in range(world):
+            idx = np.flatnonzero(owners == d)
+            if len(idx):
+                assert idx[-1] - idx[0] + 1 == len(idx)
+                self.sends.append((d, int(idx[0]), int(idx[-1]) + 1))
+        own = [(a, b) for d, a, b in self.sends if d == rank]
+        self.own_a, self.own_b = own[0] if own else (0, 0)
+        self.sends = [x for x in self.sends if x[0] != rank]
+        # everyone's plan: plan[s, d] = (global first row, rows) s sends to d
+        plan = torch.zeros((world, 2), dtype=torch.int64)
+        for d, a, b in self.sends:
+            plan[d] = torch.tensor([row_lo + a, b - a])
+        if world > 1:
+            allp = [torch.zeros_like(plan) for _ in range(world)]
+            dist.all_gather(allp, plan.to(device))
+            allp = [x.cpu() for x in allp]
+        else:
+            allp = [plan]
+        self.recvs = [(s_, int(allp[s_][rank, 0]), int(allp[s_][rank, 1])) for s_ in range(world)
+                      if s_ != rank and int(allp[s_][rank, 1]) > 0]
+        # owned global rows: my own window rows plus every received range
+        lo = [row_lo + self.own_a] if self.own_b > self.own_a else []
+        hi = [row_lo + self.own_b] if self.own_b > self.own_a else []
+        for _, g, n in self.recvs:
+            lo.append(g)
+            hi.append(g + n)
+        self.own_lo = min(lo) if lo else 0
+        self.n_own = (max(hi) - self.own_lo) if hi else 0
+        # 'first' mode: what a rank owns lies in its own window (a request's
+        # first slice is on its owner), so the received rows are added into
+        # `part` in place and the owned rows are a view of it
+        self.inplace = self.n_own == 0 or (row_lo + self.own_a <= self.own_lo and
+                                           self.own_lo + self.n_own <= row_lo + self.own_b)
+        self.rows = None if self.inplace else torch.zeros((max(self.n_own, 1), NF), dtype=torch.int64, device=device)
+        self.recv_rows = [torch.zeros((n, NF), dtype=torch.int64, device=device) for _, _, n in self.recvs]
+        self.recv_hits = [None] * len(self.recvs)
+        self.recv_hits_n = {}
+        self._my_hits = None
+
+    def exchange(self, part, hits, row_off):
+        """part: [n_rows, 5] rows; hits / row_off: sb_batch_compact_hits output
+        (int64 tensors on the device, ``row_off`` n_rows + 1)."""
+        import torch
+        dist = self.dist
+        if self.world > 1:
+            # this step's hit range per destination: (first dense hit, count)
+            cnt = torch.zeros((self.world, 2), dtype=torch.int64, device=self.device)
+            for d, a, b in self.sends:
+                cnt[d, 0] = row_off[a]
+                cnt[d, 1] = row_off[b] - row_off[a]
+            allc = [torch.zeros_like(cnt) for _ in range(self.world)]
+            dist.all_gather(allc, cnt)
+            allc = torch.stack(allc).cpu()  # [src, dst, (start, n)]
+            ops = []
+            for d, a, b in self.sends:
+                st, n = int(allc[self.rank, d, 0]), int(allc[self.rank, d, 1])
+                ops.append((dist.isend, part[a:b], d))
+                if n:
+                    ops.append((dist.isend, hits[st:st + n], d))
+            for k, (s_, g, n) in enumerate(self.recvs):
+                nh = int(allc[s_, self.rank, 1])
+                if self.recv_hits[k] is None or self.recv_hits[k].numel() < nh:
+                    self.recv_hits[k] = torch.zeros(nh + nh // 4 + 64, dtype=torch.int64, device=self.device)
+                self.recv_hits_n[k] = nh
+                ops.append((dist.irecv, self.recv_rows[k], s_))
+                if nh:
+                    ops.append((dist.irecv, self.recv_hits[k][:nh], s_))
+            if ops:
+                if dist.get_backend() == 'nccl':  # one RCCL group: sends and receives together
+                    works = dist.batch_isend_irecv([dist.P2POp(f, t, p) for f, t, p in ops])
+                else:
+                    works = [f(t, p) for f, t, p in ops]
+                for w in works:
+                    w.wait()
+        # combine: my own rows, then each received range added in
+        self._my_hits = (hits, row_off)
+        if self.inplace:
+            for k, (_, g, n) in enumerate(self.recvs):
+                part[g - self.row_lo:g - self.row_lo + n] += self.recv_rows[k]
+            return part[self.own_a:self.own_b] if self.n_own else part[:0]
+        self.rows.zero_()
+        if self.own_b > self.own_a:
+            o = self.row_lo + self.own_a - self.own_lo
+            self.rows[o:o + self.own_b - self.own_a] += part[self.own_a:self.own_b]
+        for k, (_, g, n) in enumerate(self.recvs):
+            self.rows[g - self.own_lo:g - self.own_lo + n] += self.recv_rows[k]
+        return self.rows
+
+    def hit_lists(self):
+        """{global request row: [hit, ...]} of the owned requests (host; tests)."""
+        hits, row_off = self._my_hits
+        ro = row_off.cpu().numpy()
+        h = hits[:int(ro[-1])].cpu().numpy().astype(np.uint64)
+        out = {}
+        for w in range(self.own_a, self.own_b):
+            out[self.row_lo + w] = list(h[ro[w]:ro[w + 1]])
+        for k, (s_, g, n) in enumerate(self.recvs):
+            rows = self.recv_rows[k].cpu().numpy()
+            nh = self.recv_hits_n.get(k, 0)
+            rh = self.recv_hits[k][:nh].cpu().numpy().astype(np.uint64) if nh else np.zeros(0, np.uint64)
+            at = 0
+            for j in range(n):
+                c = int(rows[j, 1])
+                out.setdefault(g + j, []).extend(rh[at:at + c])
+                at += c
+        return out
+
+
+def owner_ranks(first_rank_of_rows, mode: str, rank: int):
+    """Owner rank of each window row: 'first' = the rank of the request's
+    first slice, 'rank0' = 0."""
+    if mode not in MODES:
+        raise ValueError(f'delivery mode {mode!r} not in {MODES}')
+    f = np.asarray(first_rank_of_rows, dtype=np.int64)
+    return np.zeros_like(f) if mode == 'rank0' else f

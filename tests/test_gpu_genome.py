@@ -73,3 +73,42 @@ def test_shards_match_oracle_and_unsharded(genome, monkeypatch, spw):
             windows.append((sl.row_lo, sl.n_rows))
             parts.append(rows)
         np.testing.assert_array_equal(combine_host(windows, parts, len(reqs)), exp)
+
+
+@pytest.mark.parametrize('chains', ['1', '0'])
+def test_compact_hits_match_fetch(genome, monkeypatch, chains):
+    """sb_batch_compact_hits (device scan + gather, chain-dense regions) gives
+    each request row the concatenation of its slices' fetched hits, with the
+    shard's global record base added, on the caller's torch stream."""
+    import torch
+    if chains == '0':
+        monkeypatch.setenv('SBEACON_NO_CHAINS', '1')
+    from sbeacon.genome import prepare_shard_batch, shard_record_base, shard_slices, slice_payloads
+    shape, reqs = genome
+    world, rank = 2, 1
+    store = shape.build_shard_store(world, rank, device=0)
+    sl = shard_slices(shape, reqs, world, rank)
+    b = prepare_shard_batch(store, sl)
+    b.set_stream(torch.cuda.current_stream().cuda_stream)
+    cap = b.stats()['hits']
+    hits = torch.full((max(cap, 1),), -1, dtype=torch.int64, device='cuda:0')
+    row_off = torch.zeros(sl.n_rows + 1, dtype=torch.int64, device='cuda:0')
+    part = torch.zeros((sl.n_rows, 5), dtype=torch.int64, device='cuda:0')
+    base = shard_record_base(shape, world, rank)
+    for k in range(2):  # with and without the reduced rows handed over
+        b.run()
+        b.reduce_requests(part.data_ptr())
+        b.compact_hits(hits.data_ptr(), row_off.data_ptr(), base, rows_ptr=part.data_ptr() if k else 0)
+    b.sync()
+    torch.cuda.synchronize()
+    ro = row_off.cpu().numpy()
+    h = hits.cpu().numpy().view(np.uint64)
+    np.testing.assert_array_equal(np.diff(ro), part.cpu().numpy()[:, 1])
+    b.payloads = slice_payloads(sl)
+    rs = b.fetch()
+    per_row = [[] for _ in range(sl.n_rows)]
+    for j, o in enumerate(sl.req):
+        per_row[o].extend((base + r) | (a << 32) for r, a in rs.hits(j))
+    assert ro[-1] == sum(len(x) for x in per_row) > 0
+    for w in range(sl.n_rows):
+        assert [int(x) for x in h[ro[w]:ro[w + 1]]] == per_row[w], w

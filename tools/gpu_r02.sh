@@ -19,7 +19,7 @@ if [ -n "${BENCH:-}" ]; then
 fi
 if [ -n "${PROF:-}" ]; then
   cd /tmp
-  step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 -u $R/bench.py --workload genome --steps 5 --warmup 1 --no-cpu-baseline ${EXTRA:-}
+  step prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 -u $R/bench.py --workload genome --steps ${STEPS:-10} --warmup 2 --no-cpu-baseline ${EXTRA:-}
   find $OUT/prof -name '*kernel_stats.csv' -exec cp {} $OUT/kernel_stats.csv \;
   cat $OUT/kernel_stats.csv | cut -c1-220 | head -12
 fi
