@@ -48,6 +48,7 @@ enum {
     SB_QERR_INDEX = 2,         /* search_variants.py:207 / :223 */
     SB_QERR_VALUE = 3,         /* search_variants.py:199 int(AN) / :206 int(AC) */
     SB_QERR_ATTRIBUTE = 4,     /* search_variants_in_samples.py:89 None.replace */
+    SB_QERR_RUNTIME = 5,       /* a C++ runtime_error of the reference (readVcfData.cpp:35,50; gzip.cpp:85) */
     SB_QERR_UNSUPPORTED = 9,   /* regex metacharacters in referenceBases */
 };
 
@@ -215,17 +216,22 @@ int sb_store_chunk_boundaries(const sb_store *s, uint32_t vcf_id, const char *co
  * MAX_SLICE_GAP (100,000) and above VCF_S3_OUTPUT_SIZE_LIMIT (50,000,000)
  * entries (main.tf:17,215-216).  A file's S3 key is
  * vcf-summaries/contig/{CHROM}/{bucket%key}/regions/{first_pos}-{last_pos}-{bytes}
- * (the caller formats it; contig = index into sb_store_contig_name).  With
- * with_data the files' uncompressed bytes are concatenated in file order
- * (the reference gzips them, level 9, per <= 50 MB buffer).  status[i] =
+ * (the caller formats it; contig = index into sb_store_contig_name).
+ * with_data = 1: the files' uncompressed bytes are concatenated in file order;
+ * with_data = 2: the bytes of each file as the reference stores it -- one
+ * gzip member (level 9, header name "c", write_data_to_s3.h:49-67 /
+ * gzip.cpp:19-59) per buffer, a buffer closed when the next entry's
+ * pos + ref' + alt' bytes would take it past VCF_S3_OUTPUT_SIZE_LIMIT.
+ * data_bytes = the file's length in the data buffer.  status[i] =
  * SB_QERR_UNSUPPORTED for a slice the reference throws on (compressSeq of an
  * IUPAC code, reads past a line) or that is not record-aligned. */
 typedef struct {
     uint32_t slice;     /* index into the slices argument */
     uint32_t contig;    /* contig index of the slice's VCF */
     uint64_t first_pos, last_pos;
-    uint64_t bytes;     /* uncompressed file length */
+    uint64_t bytes;     /* uncompressed file length (the S3 key's last field) */
     uint64_t entries;
+    uint64_t data_bytes; /* this file's bytes in the data buffer (0 without data) */
 } sb_region_file;
 typedef struct sb_region_files sb_region_files;
 int sb_slice_region_files(sb_store *s, const sb_slice *slices, size_t n, int with_data, int32_t *status,
@@ -264,6 +270,36 @@ typedef struct {
 /* unique[i] / status[i] per job; stats optional */
 int sb_dedup_count(sb_store *s, const sb_dedup_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,
                    sb_dedup_stats *stats);
+
+/* Reference-exact duplicateVariantSearch over region FILES (the message's
+ * targetFilepaths, duplicateVariantSearch/source/main.cpp:31-43): unique[i] =
+ * |union over the job's files of ReadVcfData::getVcfData(file, rangeStart,
+ * rangeEnd)| (duplicateVariantSearch.cpp:31-84, readVcfData.cpp:3-71): per
+ * file, every entry with pos >= rangeStart that the reader reaches -- it
+ * keeps reading while the gzip stream has more data, and only in the last
+ * decompressed 1 KiB window stops after the first entry past rangeEnd, so
+ * entries past rangeEnd are counted as the reference counts them.  A file is
+ * named by the summariseSlice message that wrote it (vcf, virtual offsets)
+ * and its index among that slice's region files (sb_slice_region_files
+ * order); its bytes are the ones sb_slice_region_files(with_data = 2) emits.
+ * status[i] = SB_QERR_RUNTIME where the reference's getVcfData throws (an
+ * entry skipped below rangeStart straddling a 1 KiB window, a truncated
+ * entry), SB_QERR_UNSUPPORTED where that summariseSlice throws. */
+typedef struct {
+    uint32_t vcf_id;
+    uint32_t file;       /* index among the slice's region files */
+    uint64_t virtual_start, virtual_end;
+} sb_region_ref;
+
+typedef struct {
+    const sb_region_ref *files;
+    uint32_t n_files;
+    uint32_t _pad;
+    uint64_t range_start, range_end;
+} sb_dedup_file_job;
+
+int sb_dedup_count_files(sb_store *s, const sb_dedup_file_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,
+                         sb_dedup_stats *stats);
 
 /* ---- device-resident batch (benchmarks / fused pipelines) ----------------
  * Upload a batch once, then launch the query kernels repeatedly on the

@@ -13,10 +13,15 @@
  * final block's blockChars = endUncompressed cuts it (vcf_chunk_reader.h:172,
  * :223-231), keepReading() is "cursor < |S|", and seek() may overshoot.
  *
- * The reference C++ cannot be compiled here (AWS SDK C++ and
- * aws-lambda-runtime are absent), so this restatement is
- * "parity unpinned": it is checked against hand-derived cases in
- * tests/test_summarise_oracle.py, not against reference output.
+ * The reference summariseSlice / duplicateVariantSearch programs cannot be
+ * built here (AWS SDK C++ and aws-lambda-runtime are absent).
+ * Their AWS-free pieces are: oracle/_ref (Makefile.ref) compiles
+ * lambda/shared/gzip/gzip.cpp, lambda/shared/source/generalutils.* and
+ * lambda/summariseSlice/source/fast_atoi.h where they lie, and
+ * tests/test_ref_pinned.py pins this file's sequenceToBinary table
+ * (seq_code), atoui64 (atoui64_len) and the region-file gzip round trip to
+ * them; the reader walk and the skip heuristic remain checked against
+ * hand-derived cases (tests/test_summarise_oracle.py).
  */
 #include <stdint.h>
 #include <stdio.h>
@@ -228,6 +233,9 @@ static int seq_code(char c) {
         default: return -1;
     }
 }
+
+int orc_seq_code(int c) { return seq_code((char)c); }
+int orc_atoui64_len(const char *s, uint8_t len, uint64_t *out) { return atoui64_len(s, len, out); }
 
 /* write_data_to_s3.h:103-134 compressSeq into out (returns length, -1 where
  * the reference throws).  Each packed byte is appended once (the reference's

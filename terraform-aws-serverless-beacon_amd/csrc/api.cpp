@@ -11,8 +11,12 @@
 #include <array>
 #include <cstdio>
 #include <cstdlib>
+#include <map>
 #include <memory>
 #include <thread>
+#include <tuple>
+
+#include <zlib.h>
 
 #include "kernels.hpp"
 #include "store.hpp"
@@ -1341,10 +1345,39 @@ void append_key_entry(const sb_store &s, uint64_t k, std::vector<uint8_t> &out) 
         for (uint32_t j = 0; j < tl; ++j) out[o + 10 + j] = static_cast<uint8_t>(t >> (8 * j));
 }
 
+// One gzip member of buf (write_data_to_s3.h:51-52,64-65 -> gzip.cpp:19-59):
+// deflateInit2(level 9, 16 + MAX_WBITS, memLevel 9), a header named "c"; the
+// reference leaves the header's other fields uninitialised, here they are 0.
+void gzip_member(const uint8_t *buf, size_t n, std::vector<uint8_t> &out) {
+    z_stream zs{};
+    if (deflateInit2(&zs, Z_BEST_COMPRESSION, Z_DEFLATED, 16 + MAX_WBITS, 9, Z_DEFAULT_STRATEGY) != Z_OK)
+        throw Error(SB_EIO, "deflateInit2 failed");
+    gz_header h{};
+    static char name[] = "c";
+    h.name = reinterpret_cast<Bytef *>(name);
+    deflateSetHeader(&zs, &h);
+    zs.next_in = const_cast<Bytef *>(buf);
+    zs.avail_in = static_cast<uInt>(n);
+    uint8_t chunk[1 << 16];
+    int ret;
+    do {
+        zs.next_out = chunk;
+        zs.avail_out = sizeof chunk;
+        ret = deflate(&zs, Z_FINISH);
+        if (ret == Z_STREAM_ERROR) {
+            deflateEnd(&zs);
+            throw Error(SB_EIO, "deflate failed");
+        }
+        out.insert(out.end(), chunk, chunk + (sizeof chunk - zs.avail_out));
+    } while (zs.avail_out == 0);
+    deflateEnd(&zs);
+}
+
 // one slice: status (0 / SB_QERR_UNSUPPORTED), files appended to `files`,
-// file bytes appended to `data` when non-null
+// file bytes appended to `data` when non-null (gz: as gzip members)
 int32_t slice_region_files(const sb_store &s, uint32_t si, const sb_slice &sl, std::vector<sb_region_file> &files,
-                           std::vector<uint8_t> *data) {
+                           std::vector<uint8_t> *data, bool gz = false,
+                           std::vector<std::vector<uint32_t>> *file_keys = nullptr) {
     if (sl.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "slice " + std::to_string(si) + ": unknown vcf id");
     const VcfData &v = s.vcfs[sl.vcf_id];
     if (v.blk_coff.empty()) throw Error(SB_EINVAL, "region files need a VCF ingested from a BGZF file (virtual offsets)");
@@ -1366,12 +1399,41 @@ int32_t slice_region_files(const sb_store &s, uint32_t si, const sb_slice &sl, s
         if (lo >= v.segments[g].lo && lo < v.segments[g].hi) contig = g;
     const size_t f0 = files.size();
     const size_t d0 = data ? data->size() : 0;
-    sb_region_file cur{si, contig, 0, 0, 0, 0};
+    sb_region_file cur{si, contig, 0, 0, 0, 0, 0};
     bool open = false;
+    // the open file's bytes and, for gzip output, where saveOutputToS3 cuts
+    // members: before an entry when bufferLength + ref' + alt' + sizeof(pos)
+    // > VCF_S3_OUTPUT_SIZE_LIMIT (write_data_to_s3.h:49)
+    std::vector<uint8_t> fbuf;
+    std::vector<size_t> cuts;
+    size_t member_len = 0;
+    std::vector<uint32_t> fkeys;  // the open file's store keys, in entry order (file_keys)
+    const size_t k0 = file_keys ? file_keys->size() : 0;
     auto close = [&]() {
-        if (open && cur.entries) files.push_back(cur);
-        cur = sb_region_file{si, contig, 0, 0, 0, 0};
+        if (open && cur.entries) {
+            if (file_keys) file_keys->push_back(fkeys);
+            if (data) {
+                const size_t at = data->size();
+                if (gz) {
+                    size_t a = 0;
+                    cuts.push_back(fbuf.size());
+                    for (size_t c : cuts) {
+                        if (c > a) gzip_member(fbuf.data() + a, c - a, *data);
+                        a = c;
+                    }
+                } else {
+                    data->insert(data->end(), fbuf.begin(), fbuf.end());
+                }
+                cur.data_bytes = data->size() - at;
+            }
+            files.push_back(cur);
+        }
+        cur = sb_region_file{si, contig, 0, 0, 0, 0, 0};
         open = false;
+        fbuf.clear();
+        cuts.clear();
+        member_len = 0;
+        fkeys.clear();
     };
     const uint64_t skip = 2ull * s.h_dcount[lo];
     uint32_t r = lo;
@@ -1379,6 +1441,7 @@ int32_t slice_region_files(const sb_store &s, uint32_t si, const sb_slice &sl, s
         if (s.h_sum_bad[r]) {  // the reference throws / reads past the line
             files.resize(f0);
             if (data) data->resize(d0);
+            if (file_keys) file_keys->resize(k0);
             return SB_QERR_UNSUPPORTED;
         }
         const uint64_t pos = s.h_pos[r];
@@ -1392,9 +1455,18 @@ int32_t slice_region_files(const sb_store &s, uint32_t si, const sb_slice &sl, s
                 open = true;
             }
             cur.last_pos = s.h_dk_pos[k];
-            cur.bytes += 10 + key_tail_len(s, k);
+            const uint32_t tl = key_tail_len(s, k);
+            cur.bytes += 10 + tl;
             ++cur.entries;
-            if (data) append_key_entry(s, k, *data);
+            if (data) {
+                if (gz && member_len + (tl - 1) + 8 > kOutputSizeLimit) {  // ref' + alt' = tail - '_'
+                    cuts.push_back(fbuf.size());
+                    member_len = 0;
+                }
+                append_key_entry(s, k, fbuf);
+                member_len += 10 + tl;
+            }
+            if (file_keys) fkeys.push_back(k);
         }
         if (cur.entries > kOutputSizeLimit) close();
         // next visited record
@@ -1429,6 +1501,9 @@ std::string key_string(const sb_store &s, uint32_t k) {
 struct DedupWs {
     DevMem dseg, dtiles, tcnt, ke0, ke1, kh0, vh0, kh1, vh1, hist, bsum, counts, coll, ncoll, pe, ph;
 };
+
+void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique, int32_t *status,
+               sb_dedup_stats *stats);
 
 void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, int32_t *status,
            sb_dedup_stats *stats) {
@@ -1472,6 +1547,13 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
             segs.resize(seg0);
         }
     }
+    dedup_run(s, segs, n, nj, unique, status, stats);
+}
+
+// the device part of duplicateVariantSearch over planned key runs: gather,
+// radix sort, adjacent-unique (+ host recount of 64-bit word collisions)
+void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique, int32_t *status,
+               sb_dedup_stats *stats) {
     if (n >= 0xffffffffull) throw Error(SB_EINVAL, "dedup batch exceeds 2^32 keys; split it");
     uint32_t job_bits = 0;
     while ((1ull << job_bits) < nj) ++job_bits;
@@ -1607,6 +1689,186 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
     }
 }
 
+// ------------------------------------------------ reference-exact duplicateVariantSearch
+// What ReadVcfData::getVcfData (lambda/duplicateVariantSearch/source/
+// readVcfData.cpp:3-71) inserts from one region file depends on when its
+// gzip reader (lambda/shared/gzip/gzip.cpp:61-144) reports the end of the
+// stream: the loop keeps reading while hasMoreData(), whatever the POS, and
+// only inside the last decompressed window stops after the first entry past
+// rangeEnd.  So the strict mode reads the region files exactly that way, over
+// the gzip members this library writes (sb_slice_region_files with_data = 2):
+// a multi-member stream inflated with Z_BLOCK through a 1 KiB input window
+// into the reader's 1 KiB buffer, the buffer's unread tail moved to its front
+// at every refill.  The entries it would insert are then deduplicated on the
+// device like the intended-range mode's.
+struct RefThrow {};  // a runtime_error of the reference (the Lambda fails)
+
+class RegionReader {  // gzip.cpp:4-17 (constructor), 61-79, 81-144 (proccesData)
+  public:
+    RegionReader(const uint8_t *file, uint64_t size, char *buf, uint32_t buf_size)
+        : file_(file), size_(static_cast<uint32_t>(size)), buf_(buf), buf_size_(buf_size) {
+        if (size > 0xffffffffull) throw RefThrow{};  // gzip.cpp:16
+    }
+    ~RegionReader() {
+        if (live_) inflateEnd(&zs_);
+    }
+    int start() {
+        const int err = inflateInit2(&zs_, 16 + MAX_WBITS);
+        live_ = err == Z_OK;
+        if (err >= 0) more_ = true;
+        return err;
+    }
+    bool more() const { return more_; }
+    uint32_t fill(uint32_t beg, uint32_t end) {
+        if (beg > end) throw RefThrow{};  // "gzip Error: proccesData input invalid"
+        if (beg < end) memmove(buf_, buf_ + beg, end - beg);
+        zs_.avail_out = buf_size_ - (end - beg);
+        zs_.next_out = reinterpret_cast<Bytef *>(buf_ + (end - beg));
+        for (;;) {
+            if (zs_.avail_out == 0) return buf_size_;
+            if (zs_.avail_in == 0) {
+                zs_.avail_in = std::min<uint32_t>(sizeof window_, size_ - read_);
+                zs_.next_in = window_;
+                memcpy(window_, file_ + read_, zs_.avail_in);
+                read_ += zs_.avail_in;
+            }
+            int err = inflate(&zs_, Z_BLOCK);
+            if (err == Z_STREAM_END) {
+                if (zs_.avail_in == 0 && size_ == read_) break;  // end of the file
+                stop();  // another member: start the decompression again
+                if (start() < 0) break;
+            } else if (err < 0 || size_ - read_ + zs_.avail_in <= 8) {
+                break;  // an error, or only the gzip footer left
+            }
+        }
+        stop();
+        return buf_size_ - zs_.avail_out;
+    }
+
+  private:
+    void stop() {
+        more_ = false;
+        if (live_) inflateEnd(&zs_);
+        live_ = false;
+    }
+    const uint8_t *file_;
+    uint32_t size_, read_ = 0;
+    char *buf_;
+    uint32_t buf_size_;
+    z_stream zs_{};
+    bool more_ = false, live_ = false;
+    Bytef window_[1024];
+};
+
+// readVcfData.cpp:3-71 over one region file: the file positions (entry
+// indices) of the entries getVcfData returns.  false = the reference throws.
+bool strict_region_entries(const uint8_t *file, uint64_t size, uint64_t rs, uint64_t re, std::vector<uint32_t> &incl) {
+    constexpr size_t kMin = sizeof(uint64_t) + sizeof(uint16_t);  // readVcfData.hpp:8 MIN_DATA_SIZE
+    char buf[1024];                                               // readVcfData.hpp:7 BUFFER_SIZE
+    size_t pos = 0, len = 0;
+    uint64_t vpos = 0;
+    uint32_t entry = 0;
+    try {
+        RegionReader in(file, size, buf, sizeof buf);
+        in.start();
+        auto avail = [&](size_t need) -> bool {  // checkForAvailableData
+            if (len >= pos + need) return true;
+            if (!in.more()) return false;
+            len = in.fill(static_cast<uint32_t>(pos), static_cast<uint32_t>(len));
+            if (len > 0) {
+                pos = 0;
+                return true;
+            }
+            return false;
+        };
+        do {
+            if (!avail(kMin)) return false;  // "Invalid File Read - getVcfData()"
+            memcpy(&vpos, buf + pos, sizeof vpos);
+            pos += sizeof vpos;
+            uint16_t sl;
+            memcpy(&sl, buf + pos, sizeof sl);
+            if (rs <= vpos) {  // readString
+                pos += sizeof sl;
+                if (!avail(sl)) return false;  // "Invalid File Read - readString()"
+                pos += sl;
+                incl.push_back(entry);
+            } else {
+                pos += sl + sizeof sl;  // skipped with no availability check (:27-30)
+            }
+            ++entry;
+        } while ((len != pos && vpos <= re) || in.more());
+    } catch (const RefThrow &) {
+        return false;
+    }
+    return true;
+}
+
+void dedup_files(sb_store &s, const sb_dedup_file_job *jobs, size_t nj, uint64_t *unique, int32_t *status,
+                 sb_dedup_stats *stats) {
+    if (nj > (1u << 20)) throw Error(SB_EINVAL, "more than 2^20 dedup jobs in one call");
+    struct SliceFiles {
+        int32_t status = 0;
+        std::vector<sb_region_file> files;
+        std::vector<uint8_t> data;
+        std::vector<uint64_t> at;  // each file's first byte in data
+        std::vector<std::vector<uint32_t>> keys;
+    };
+    std::map<std::tuple<uint32_t, uint64_t, uint64_t>, SliceFiles> cache;
+    std::vector<KSeg> segs;
+    uint64_t n = 0;
+    for (size_t j = 0; j < nj; ++j) {
+        const sb_dedup_file_job &J = jobs[j];
+        status[j] = 0;
+        unique[j] = 0;
+        if (!J.files && J.n_files) throw Error(SB_EINVAL, "dedup job: NULL file list");
+        const uint32_t rs = static_cast<uint32_t>(std::min<uint64_t>(J.range_start, 0xffffffffull));
+        const size_t seg0 = segs.size();
+        for (uint32_t t = 0; t < J.n_files && !status[j]; ++t) {
+            const sb_region_ref &F = J.files[t];
+            if (F.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "dedup job " + std::to_string(j) + ": unknown vcf id");
+            auto key = std::make_tuple(F.vcf_id, F.virtual_start, F.virtual_end);
+            auto it = cache.find(key);
+            if (it == cache.end()) {
+                SliceFiles sf;
+                const sb_slice sl{F.vcf_id, 0, F.virtual_start, F.virtual_end};
+                sf.status = slice_region_files(s, 0, sl, sf.files, &sf.data, true, &sf.keys);
+                uint64_t a = 0;
+                for (const auto &f : sf.files) {
+                    sf.at.push_back(a);
+                    a += f.data_bytes;
+                }
+                it = cache.emplace(key, std::move(sf)).first;
+            }
+            const SliceFiles &sf = it->second;
+            if (sf.status) {  // that summariseSlice never wrote its files
+                status[j] = sf.status;
+                break;
+            }
+            if (F.file >= sf.files.size()) throw Error(SB_EINVAL, "dedup job " + std::to_string(j) + ": no region file " +
+                                                                      std::to_string(F.file) + " in that slice");
+            std::vector<uint32_t> incl;
+            if (!strict_region_entries(sf.data.data() + sf.at[F.file], sf.files[F.file].data_bytes, J.range_start,
+                                       J.range_end, incl)) {
+                status[j] = SB_QERR_RUNTIME;
+                break;
+            }
+            const auto &fk = sf.keys[F.file];
+            for (size_t a = 0; a < incl.size();) {  // runs of consecutive store keys
+                size_t b = a + 1;
+                while (b < incl.size() && fk[incl[b]] == fk[incl[b - 1]] + 1) ++b;
+                segs.push_back(KSeg{fk[incl[a]], n, static_cast<uint32_t>(b - a), static_cast<uint32_t>(j), rs, 0});
+                n += b - a;
+                a = b;
+            }
+        }
+        if (status[j]) {
+            for (size_t g = seg0; g < segs.size(); ++g) n -= segs[g].n;
+            segs.resize(seg0);
+        }
+    }
+    dedup_run(s, segs, n, nj, unique, status, stats);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1629,9 +1891,10 @@ int sb_slice_region_files(sb_store *s, const sb_slice *slices, size_t n, int wit
     return guard([&] {
         if (!s || (!slices && n) || (!status && n) || !out) throw Error(SB_EINVAL, "NULL argument");
         auto R = std::make_unique<sb_region_files>();
+        if (with_data < 0 || with_data > 2) throw Error(SB_EINVAL, "with_data must be 0, 1 or 2");
         for (size_t i = 0; i < n; ++i)
             status[i] = slice_region_files(*s, static_cast<uint32_t>(i), slices[i], R->files,
-                                           with_data ? &R->data : nullptr);
+                                           with_data ? &R->data : nullptr, with_data == 2);
         *out = R.release();
     });
 }
@@ -1654,6 +1917,15 @@ int sb_dedup_count(sb_store *s, const sb_dedup_job *jobs, size_t n_jobs, uint64_
         if (!s || (n_jobs && (!jobs || !unique || !status))) throw Error(SB_EINVAL, "NULL argument");
         std::lock_guard<std::mutex> lk(s->mu);
         dedup(*s, jobs, n_jobs, unique, status, stats);
+    });
+}
+
+int sb_dedup_count_files(sb_store *s, const sb_dedup_file_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,
+                         sb_dedup_stats *stats) {
+    return guard([&] {
+        if (!s || (n_jobs && (!jobs || !unique || !status))) throw Error(SB_EINVAL, "NULL argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        dedup_files(*s, jobs, n_jobs, unique, status, stats);
     });
 }
 

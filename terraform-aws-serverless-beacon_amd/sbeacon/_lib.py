@@ -71,12 +71,22 @@ class SliceStats(C.Structure):
 
 class RegionFile(C.Structure):
     _fields_ = [('slice', C.c_uint32), ('contig', C.c_uint32), ('first_pos', C.c_uint64), ('last_pos', C.c_uint64),
-                ('bytes', C.c_uint64), ('entries', C.c_uint64)]
+                ('bytes', C.c_uint64), ('entries', C.c_uint64), ('data_bytes', C.c_uint64)]
 
 
 class DedupJob(C.Structure):
     _fields_ = [('vcf_ids', C.POINTER(C.c_uint32)), ('n_vcf', C.c_uint32), ('contig_len', C.c_uint32),
                 ('contig', C.c_char_p), ('range_start', C.c_uint64), ('range_end', C.c_uint64)]
+
+
+class RegionRef(C.Structure):
+    _fields_ = [('vcf_id', C.c_uint32), ('file', C.c_uint32), ('virtual_start', C.c_uint64),
+                ('virtual_end', C.c_uint64)]
+
+
+class DedupFileJob(C.Structure):
+    _fields_ = [('files', C.POINTER(RegionRef)), ('n_files', C.c_uint32), ('_pad', C.c_uint32),
+                ('range_start', C.c_uint64), ('range_end', C.c_uint64)]
 
 
 class DedupStats(C.Structure):
@@ -128,6 +138,8 @@ SIGNATURES = {
     'sb_region_files_free': (None, [P]),
     'sb_dedup_count': (C.c_int, [P, C.POINTER(DedupJob), C.c_size_t, C.POINTER(C.c_uint64), C.POINTER(C.c_int32),
                                  C.POINTER(DedupStats)]),
+    'sb_dedup_count_files': (C.c_int, [P, C.POINTER(DedupFileJob), C.c_size_t, C.POINTER(C.c_uint64),
+                                       C.POINTER(C.c_int32), C.POINTER(DedupStats)]),
     'sb_store_n_contigs': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),
     'sb_store_contig_name': (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t)]),
     'sb_store_chunk_boundaries': (C.c_int, [P, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint32,

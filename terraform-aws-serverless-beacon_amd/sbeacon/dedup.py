@@ -198,9 +198,13 @@ class DuplicateTally:
         self.dataset_counts[dataset] = self.dataset_counts.get(dataset, 0) + final_tally
 
 
-def dedup_batch(messages, *, tally: DuplicateTally | None = None, registry=None):
+def dedup_batch(messages, *, tally: DuplicateTally | None = None, registry=None, file_refs=None):
     """Answer many duplicateVariantSearch messages with one device call per
-    store.  Returns the unique count per message (or the exception)."""
+    store.  Returns the unique count per message (or the exception).
+    file_refs (region-file key -> (location, virtual_start, virtual_end, file
+    index), summarise.region_file_keys) selects the reference-exact mode: each
+    target file is read as ReadVcfData::getVcfData reads it
+    (sb_dedup_count_files) instead of counting the intended inclusive range."""
     reg = registry or engine.registry
     known = reg.locations()
     jobs = [message_job(m, known) for m in messages]
@@ -217,7 +221,11 @@ def dedup_batch(messages, *, tally: DuplicateTally | None = None, registry=None)
             for i in idx:
                 out[i] = 0
             continue
-        res = st.dedup_counts([jobs[i] for i in idx])
+        if file_refs is not None:
+            res = st.dedup_counts_files([([file_refs[p] for p in messages[i]['targetFilepaths']], jobs[i][2],
+                                          jobs[i][3]) for i in idx])
+        else:
+            res = st.dedup_counts([jobs[i] for i in idx])
         for i, r in zip(idx, res):
             out[i] = r
     if tally is not None:

@@ -201,8 +201,10 @@ class Store:
     def region_files(self, slices, *, with_data=False):
         """summariseSlice's region files of each slice (write_data_to_s3.h):
         per slice a list of {contig, first_pos, last_pos, bytes, entries}
-        dicts (+ 'data': the file's uncompressed bytes with_data), or the
-        exception for a slice the reference throws on."""
+        dicts (+ 'data': the file's bytes -- uncompressed with
+        ``with_data=True``, the reference's gzip members with
+        ``with_data='gzip'``), or the exception for a slice the reference
+        throws on."""
         slices = list(slices)
         n = len(slices)
         arr = (Slice * max(n, 1))()
@@ -212,14 +214,15 @@ class Store:
             arr[i].virtual_end = int(ve)
         status = (C.c_int32 * max(n, 1))()
         h = C.c_void_p()
-        check(lib().sb_slice_region_files(self._h, arr, n, 1 if with_data else 0, status, C.byref(h)))
+        mode = 2 if with_data == 'gzip' else (1 if with_data else 0)
+        check(lib().sb_slice_region_files(self._h, arr, n, mode, status, C.byref(h)))
         try:
             fp = C.POINTER(_lib.RegionFile)()
             nf = C.c_size_t()
             dp = C.c_void_p()
             dl = C.c_size_t()
             check(lib().sb_region_files_get(h, C.byref(fp), C.byref(nf), C.byref(dp), C.byref(dl)))
-            data = C.string_at(dp, dl.value) if with_data and dl.value else b''
+            data = C.string_at(dp, dl.value) if mode and dl.value else b''
             contig_names = {}
             out = [[] for _ in range(n)]
             off = 0
@@ -230,9 +233,9 @@ class Store:
                     contig_names[loc] = self.contigs(loc)
                 d = {'contig': contig_names[loc][f.contig], 'first_pos': f.first_pos, 'last_pos': f.last_pos,
                      'bytes': f.bytes, 'entries': f.entries}
-                if with_data:
-                    d['data'] = data[off:off + f.bytes]
-                    off += f.bytes
+                if mode:
+                    d['data'] = data[off:off + f.data_bytes]
+                    off += f.data_bytes
                 out[f.slice].append(d)
         finally:
             lib().sb_region_files_free(h)
@@ -265,6 +268,46 @@ class Store:
         res = [NotImplementedError(f'dedup job {jobs[i][1:]}: a record in range has an allele compressSeq '
                                    'rejects (the reference summariseSlice throws)') if status[i] else uniq[i]
                for i in range(n)]
+        if with_stats:
+            return res, {'keys': st.keys, 'collisions': st.collisions, 'device_ms': st.device_ms}
+        return res
+
+    def dedup_counts_files(self, jobs, *, with_stats=False):
+        """Reference-exact duplicateVariantSearch (sb_dedup_count_files).
+        jobs: iterable of (files, range_start, range_end), files = list of
+        (vcf_location, virtual_start, virtual_end, file index) naming region
+        files by the summariseSlice slice that wrote them.  Returns the unique
+        count per job, or the exception the reference raises (RuntimeError:
+        its getVcfData throws; NotImplementedError: its summariseSlice throws)."""
+        jobs = list(jobs)
+        n = len(jobs)
+        arr = (_lib.DedupFileJob * max(n, 1))()
+        keep = []
+        for i, (files, rs, re_) in enumerate(jobs):
+            fa = (_lib.RegionRef * max(len(files), 1))()
+            for k, (loc, vs, ve, fi) in enumerate(files):
+                fa[k].vcf_id = self.vcf_id(loc)
+                fa[k].file = int(fi)
+                fa[k].virtual_start = int(vs)
+                fa[k].virtual_end = int(ve)
+            keep.append(fa)
+            arr[i].files = fa
+            arr[i].n_files = len(files)
+            arr[i].range_start = int(rs)
+            arr[i].range_end = int(re_)
+        uniq = (C.c_uint64 * max(n, 1))()
+        status = (C.c_int32 * max(n, 1))()
+        st = DedupStats()
+        check(lib().sb_dedup_count_files(self._h, arr, n, uniq, status, C.byref(st)))
+        res = []
+        for i in range(n):
+            if status[i] == 5:
+                res.append(RuntimeError('Invalid File Read (the reference getVcfData throws)'))
+            elif status[i]:
+                res.append(NotImplementedError('a region file of this job comes from a slice the reference '
+                                               'summariseSlice throws on'))
+            else:
+                res.append(uniq[i])
         if with_stats:
             return res, {'keys': st.keys, 'collisions': st.collisions, 'device_ms': st.device_ms}
         return res

@@ -14,6 +14,7 @@ call (``summarise_batch``) — the analogue of summariseVcf's SNS fan-out
 from __future__ import annotations
 
 import json
+import os
 
 from .engine import registry
 
@@ -49,44 +50,61 @@ def lambda_handler(event, context=None):
     return summarise_slice(msg['location'], int(msg['virtual_start']), int(msg['virtual_end']))
 
 
-def region_file_keys(store, location, slices):
+def region_file_keys(store, location, slices, refs=None):
     """The S3 keys summariseSlice writes for these slices of one VCF
     (write_data_to_s3.h:93-101: vcf-summaries/contig/{CHROM}/{bucket%key}/
-    regions/{first}-{last}-{bytes}), in slice then file order."""
+    regions/{first}-{last}-{bytes}), in slice then file order.  ``refs``
+    (optional dict) receives key -> (location, virtual_start, virtual_end,
+    file index): the file a strict duplicateVariantSearch reads (a later
+    file with the same key replaces it, as an S3 PUT does)."""
     from .dedup import bucket_key
     bk = bucket_key(location)
     keys = []
     for sl, files in zip(slices, store.region_files([(location, a, b) for a, b in slices])):
         if isinstance(files, Exception):
             raise files
-        for f in files:
-            keys.append(f"vcf-summaries/contig/{f['contig']}/{bk}/regions/{f['first_pos']}-{f['last_pos']}-{f['bytes']}")
+        for i, f in enumerate(files):
+            k = f"vcf-summaries/contig/{f['contig']}/{bk}/regions/{f['first_pos']}-{f['last_pos']}-{f['bytes']}"
+            keys.append(k)
+            if refs is not None:
+                refs[k] = (location, sl[0], sl[1], i)
     return keys
 
 
-def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None):
+def strict_dedup_default() -> bool:
+    """SBEACON_STRICT_DEDUP=1: duplicateVariantSearch reads the region files
+    exactly as the reference does (sb_dedup_count_files) instead of counting
+    the intended inclusive range (sb_dedup_count)."""
+    return os.environ.get('SBEACON_STRICT_DEDUP', '0') == '1'
+
+
+def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None, strict=None):
     """The ingest pipeline of one dataset on the device: summariseVcf's slice
     plan + summariseSlice counts for every VCF (lambda/summariseVcf,
     lambda/summariseSlice), the region-file keys those slices write, then
     initDuplicateVariantSearch's range splits (lambda/summariseDataset/
     initDuplicateVariantSearch.py:235-255) answered by duplicateVariantSearch
-    (one batched sb_dedup_count).  Returns the dataset's counts:
+    (one batched device call).  Returns the dataset's counts:
     variantCount / callCount from the summaries (summariseDataset
     lambda_function.py:102-125) and uniqueVariants = the sum of the ranges'
     distinct counts (the DATASETS_TABLE variantCount duplicateVariantSearch
-    leaves, duplicateVariantSearch.cpp:76-84)."""
+    leaves, duplicateVariantSearch.cpp:76-84).  strict (default
+    SBEACON_STRICT_DEDUP): the reference's file-reading semantics."""
     from .dedup import DuplicateTally, dedup_batch, init_duplicate_variant_search
     from .summarise_vcf import summarise_vcf
+    strict = strict_dedup_default() if strict is None else strict
     tally = tally or DuplicateTally()
     counts = {'variantCount': 0, 'callCount': 0}
     keys = []
+    refs = {}
     for loc in locations:
         slices, _, tot = summarise_vcf(store, loc)
         counts['variantCount'] += tot['variantCount']
         counts['callCount'] += tot['callCount']
-        keys += region_file_keys(store, loc, slices)
+        keys += region_file_keys(store, loc, slices, refs)
     messages = init_duplicate_variant_search(dataset, locations, keys, tally=tally, abs_max=abs_max)
-    per_range = dedup_batch(messages, tally=tally, registry=_single_store_registry(store)) if messages else []
+    per_range = dedup_batch(messages, tally=tally, registry=_single_store_registry(store),
+                            file_refs=refs if strict else None) if messages else []
     for r in per_range:
         if isinstance(r, Exception):
             raise r

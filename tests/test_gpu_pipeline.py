@@ -45,3 +45,67 @@ def test_summarise_dataset_pipeline(tmp_path):
         for m, got in zip(messages, per_range):
             assert got == dedup_count(texts, m['contig'], m['rangeStart'], m['rangeEnd']), m
         assert counts['uniqueVariants'] == sum(per_range)
+
+
+def test_region_files_gzip_and_strict_dedup(tmp_path):
+    """Region files as the reference stores them (gzip members, level 9) and
+    duplicateVariantSearch in the reference-exact mode: every target file is
+    read by ReadVcfData::getVcfData's loop over the REFERENCE gzip reader
+    (oracle/_ref, built from lambda/shared/gzip/gzip.cpp); the device count of
+    each range must equal |union of those key sets|, reference throws included."""
+    import zlib
+    from oracle import ref
+    from test_ref_pinned import deflate9, gzip_payload
+    if ref.lib() is None:
+        pytest.skip('oracle/_ref missing')
+    from sbeacon.dedup import dedup_batch, init_duplicate_variant_search
+    from sbeacon.engine import Store
+    from sbeacon.summarise import _single_store_registry, region_file_keys, summarise_dataset
+    from sbeacon.summarise_vcf import plan_slices
+    from sbeacon.workload import SyntheticVcf, write_bgzf
+    pool = SyntheticVcf(seed=8, n_records=6000, n_samples=4, mean_gap=25000)
+    parts = [(f's3://bkt/dsS/p{k}.vcf.gz', pool.member(800 + k, share=0.6)) for k in (0, 1)]
+    paths = []
+    for loc, gen in parts:
+        path = str(tmp_path / (loc.replace('/', '_') + '.gz'))
+        write_bgzf(path, gen.chunks(threads=4), threads=4)
+        paths.append((loc, path))
+    locs = [l for l, _ in paths]
+    store = Store.build(paths, device=0)
+    gz_files, refs, keys = {}, {}, []
+    for loc in locs:
+        slices = plan_slices(store, loc)
+        keys += region_file_keys(store, loc, slices, refs)
+        raw = store.region_files([(loc, a, b) for a, b in slices], with_data=True)
+        gz = store.region_files([(loc, a, b) for a, b in slices], with_data='gzip')
+        for (a, b), fr, fg in zip(slices, raw, gz):
+            assert len(fr) == len(fg)
+            for i, (x, y) in enumerate(zip(fr, fg)):
+                assert zlib.decompress(y['data'], 16 + zlib.MAX_WBITS) == x['data']
+                assert gzip_payload(y['data']) == gzip_payload(ref.gzip_deflate(x['data'], 9)) \
+                    == gzip_payload(deflate9(x['data']))
+                gz_files[(loc, a, b, i)] = y['data']
+    assert all(r in gz_files for r in refs.values())
+    reg = _single_store_registry(store)
+    for abs_max in (10_000, 10**9):  # many ranges (files overlap range starts) / one range per contig
+        messages = init_duplicate_variant_search('dsS', locs, keys, abs_max=abs_max)
+        assert messages
+        per_range = dedup_batch(messages, registry=reg, file_refs=refs)
+        n_throw = 0
+        for m, got in zip(messages, per_range):
+            exp = set()
+            for p in m['targetFilepaths']:
+                kf = ref.region_keys(gz_files[refs[p]], m['rangeStart'], m['rangeEnd'])
+                if isinstance(kf, Exception):
+                    exp = kf
+                    break
+                exp |= set(kf)
+            if isinstance(exp, Exception):
+                n_throw += 1
+                assert isinstance(got, RuntimeError), m
+            else:
+                assert got == len(exp), m
+        if abs_max == 10**9:
+            assert n_throw == 0
+            counts, _, pr = summarise_dataset(store, 'dsS', locs, abs_max=abs_max, strict=True)
+            assert counts['uniqueVariants'] == sum(pr) == sum(per_range)
