@@ -301,6 +301,19 @@ typedef struct {
 int sb_dedup_count_files(sb_store *s, const sb_dedup_file_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,
                          sb_dedup_stats *stats);
 
+/* ---- CSI / TBI index of a BGZF VCF (host only, no device) -----------------
+ * The index summariseVcf reads its chunk boundaries from
+ * (lambda/summariseVcf/lambda_function.py:90-104 get_chunk_boundaries,
+ * :144-156 get_vcf_index; index_reader.py:4-125 Csi / Tbi), as
+ * `bcftools index` / `tabix -p vcf` would write it next to the VCF.
+ * min_shift <= 0 -> 14; depth <= 0 -> 5 for TBI, and for CSI the smallest
+ * depth >= 5 covering the longest record.  *out = the BGZF-compressed index
+ * (release with sb_free).  SB_EINVAL for an unsorted VCF or a position past
+ * the index's range. */
+enum { SB_INDEX_CSI = 0, SB_INDEX_TBI = 1 };
+int sb_index_vcf(const char *path, int fmt, int min_shift, int depth, uint8_t **out, size_t *out_len);
+void sb_free(void *p);
+
 /* ---- device-resident batch (benchmarks / fused pipelines) ----------------
  * Upload a batch once, then launch the query kernels repeatedly on the
  * store's stream with inputs already resident in HBM. */

@@ -145,6 +145,9 @@ SIGNATURES = {
     'sb_store_chunk_boundaries': (C.c_int, [P, C.c_uint32, C.c_char_p, C.c_size_t, C.c_uint32,
                                             C.POINTER(C.c_uint64), C.c_size_t, C.POINTER(C.c_size_t)]),
     'sb_store_vcf_stream': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    'sb_index_vcf': (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p),
+                               C.POINTER(C.c_size_t)]),
+    'sb_free': (None, [P]),
 }
 
 _lib = None

@@ -82,9 +82,10 @@ def queries_from_payloads(payloads: list[dict], vcf_id, *, strict_variant_type: 
 class Store:
     """An immutable HBM store built from VCF files or text."""
 
-    def __init__(self, handle, locations):
+    def __init__(self, handle, locations, paths=None):
         self._h = handle
         self.locations = list(locations)
+        self.paths = dict(paths or {})  # location -> source file (summariseVcf looks for its index there)
 
     # ---------------------------------------------------------------- build
     @classmethod
@@ -100,6 +101,7 @@ class Store:
         opts = BuildOpts(1 if keep_genotypes else 0, int(n_threads))
         check(L.sb_builder_new(C.byref(opts), C.byref(b)))
         locs = []
+        paths = {}
         try:
             for item in sources:
                 loc, src = item[0], item[1]
@@ -110,6 +112,7 @@ class Store:
                 locs.append(loc)
                 if isinstance(src, (str, os.PathLike)) and os.path.exists(src):
                     check(L.sb_builder_add_file(b, vid.value, os.fsencode(src)))
+                    paths[loc] = os.fspath(src)
                 elif isinstance(src, (str, bytes)):
                     t = _b(src)
                     check(L.sb_builder_add_text(b, vid.value, t, len(t)))
@@ -134,7 +137,7 @@ class Store:
             check(L.sb_builder_finish(b, int(device), C.byref(s)))
         finally:
             L.sb_builder_free(b)
-        return cls(s, locs)
+        return cls(s, locs, paths)
 
     def close(self):
         if self._h:

@@ -78,7 +78,7 @@ def strict_dedup_default() -> bool:
     return os.environ.get('SBEACON_STRICT_DEDUP', '0') == '1'
 
 
-def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None, strict=None):
+def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None, strict=None, vcf_groups=None):
     """The ingest pipeline of one dataset on the device: summariseVcf's slice
     plan + summariseSlice counts for every VCF (lambda/summariseVcf,
     lambda/summariseSlice), the region-file keys those slices write, then
@@ -89,7 +89,10 @@ def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None, st
     lambda_function.py:102-125) and uniqueVariants = the sum of the ranges'
     distinct counts (the DATASETS_TABLE variantCount duplicateVariantSearch
     leaves, duplicateVariantSearch.cpp:76-84).  strict (default
-    SBEACON_STRICT_DEDUP): the reference's file-reading semantics."""
+    SBEACON_STRICT_DEDUP): the reference's file-reading semantics.
+    sampleCount is counted once per VCF group (summariseDataset
+    lambda_function.py:118-124; vcf_groups defaults to one group of all the
+    locations, submitDataset lambda_function.py:93)."""
     from .dedup import DuplicateTally, dedup_batch, init_duplicate_variant_search
     from .summarise_vcf import summarise_vcf
     strict = strict_dedup_default() if strict is None else strict
@@ -97,10 +100,15 @@ def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None, st
     counts = {'variantCount': 0, 'callCount': 0}
     keys = []
     refs = {}
+    group_of = {loc: i for i, grp in enumerate(vcf_groups or [list(locations)]) for loc in grp}
+    counted = set()
     for loc in locations:
         slices, _, tot = summarise_vcf(store, loc)
         counts['variantCount'] += tot['variantCount']
         counts['callCount'] += tot['callCount']
+        if 'sampleCount' in tot and group_of[loc] not in counted:
+            counts['sampleCount'] = counts.get('sampleCount', 0) + tot['sampleCount']
+            counted.add(group_of[loc])
         keys += region_file_keys(store, loc, slices, refs)
     messages = init_duplicate_variant_search(dataset, locations, keys, tally=tally, abs_max=abs_max)
     per_range = dedup_batch(messages, tally=tally, registry=_single_store_registry(store),

@@ -2,13 +2,15 @@
 BGZF files: random record-aligned slices (both spellings of a block-boundary
 virtual offset), including a fixture built so the reference's skip heuristic
 swallows records."""
+import json
 import os
+import sys
 import random
 
 import pytest
 
 from bgzf_util import blocks, random_slices, record_starts, text
-from conftest import FIXTURES
+from conftest import FIXTURES, REPO
 from payload_gen import random_payload, read_records
 
 pytestmark = pytest.mark.gpu
@@ -181,3 +183,40 @@ def test_region_files_vs_oracle(bgzf_files, bgzf_store, name):
         n_files += len(g)
     if name == 'gaps3':
         assert n_files > len(slices)  # the fixture really splits files on gaps
+
+
+@pytest.fixture(scope='module')
+def index_files(tmp_path_factory):
+    sys.path.insert(0, os.path.join(REPO, 'tests', 'golden'))
+    from index_fixtures import FIXTURES, write_fixture
+    d = tmp_path_factory.mktemp('idxvcf')
+    return {name: write_fixture(name, str(d)) for name in FIXTURES}
+
+
+def test_summarise_vcf_over_reference_index_slices(index_files):
+    """summariseVcf over the CSI / TBI index (tests/golden/index_golden.json,
+    the reference handler's own slices): the plan equals the reference's, and
+    every slice's counts -- also at the finer partitions -- equal the
+    oracle's summariseSlice; sampleCount equals get_sample_count's."""
+    from oracle.oracle import OracleBgzf
+    from sbeacon.engine import Store
+    from sbeacon.summarise_vcf import index_chunk_boundaries, partition_chunks, summarise_vcf
+    gold = json.load(open(os.path.join(REPO, 'tests', 'golden', 'index_golden.json')))['cases']
+    store = Store.build([(n + '.vcf.gz', p) for n, p in index_files.items()], device=0)
+    for c in gold:
+        loc = c['fixture'] + '.vcf.gz'
+        idx = open(os.path.join(REPO, 'tests', 'golden', 'index', f'{c["fixture"]}.{c["format"]}'), 'rb').read()
+        slices, stats, tot = summarise_vcf(store, loc, index=idx)
+        assert [list(s) for s in slices] == c['slices']
+        assert tot['sampleCount'] == c['sample_count']
+        o = OracleBgzf(index_files[c['fixture']])
+        assert stats == [o.summarise_slice(a, b) for a, b in slices]
+        fine = partition_chunks(index_chunk_boundaries(idx), 20000)
+        assert [list(s) for s in fine] == c['partitions']['20000']
+        got = store.summarise_slices([(loc, a, b) for a, b in fine])
+        assert got == [o.summarise_slice(a, b) for a, b in fine]
+        assert sum(s['numVariants'] for s in got) == tot['variantCount']
+    # 'auto': no index next to the file, so the ingest writes one (CSI)
+    slices, _, _ = summarise_vcf(store, 'multi3.vcf.gz')
+    assert [list(s) for s in slices] == next(c['slices'] for c in gold if c['fixture'] == 'multi3'
+                                                 and c['format'] == 'csi')
