@@ -1105,6 +1105,12 @@ void run(sb_batch &B) {
                 fg.push_back(FusedGroup{B.q.as<QDev>() + g.base, static_cast<uint32_t>(g.idx.size()), g.mode});
     launch_fused(d, fg.data(), static_cast<int>(fg.size()), B.nonneg, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(),
                  B.res.as<QRes>(), B.hits.as<uint64_t>(), st);
+    // the sample path ORs words past its register window into samples_out
+    // (> 65,536-sample VCFs): start every run from zero
+    if (B.samples_out.bytes && std::any_of(B.groups.begin(), B.groups.end(), [](const sb_batch::Group &g) {
+            return g.max_words != 0;
+        }))
+        HIP_OK(hipMemsetAsync(B.samples_out.p, 0, B.samples_out.bytes, st));
     for (const auto &g : B.groups)
         if (g.max_words != 0)
             launch_scan(d, B.q.as<QDev>() + g.base, nullptr, static_cast<uint32_t>(g.idx.size()), B.nonneg,

@@ -615,6 +615,12 @@ __device__ __forceinline__ void scan_slice(
                         for (int u = 0; u < kRowBatch; ++u) acc[j] |= v[u];
                     }
                 }
+                if (Q.words > 64u * NACC && Q.samples_out_off != ~0ull)  // beyond the register window
+                    for (uint32_t wd = static_cast<uint32_t>(lane) + 64u * NACC; wd < Q.words; wd += 64u) {
+                        uint64_t v = 0;
+                        for (int u = 0; u < nb; ++u) v |= st.planes[rows[u] + wd];
+                        samples_out[Q.samples_out_off + wd] |= v;
+                    }
             }
             while (cm) {
                 const int L = ffs64(cm);
@@ -631,6 +637,9 @@ __device__ __forceinline__ void scan_slice(
                         const uint32_t wd = static_cast<uint32_t>(lane) + 64u * j;
                         if (wd < Q.words) acc[j] |= st.planes[row + wd];
                     }
+                    if (Q.words > 64u * NACC && Q.samples_out_off != ~0ull)
+                        for (uint32_t wd = static_cast<uint32_t>(lane) + 64u * NACC; wd < Q.words; wd += 64u)
+                            samples_out[Q.samples_out_off + wd] |= st.planes[row + wd];
                 }
             }
         }
@@ -649,6 +658,13 @@ __device__ __forceinline__ void scan_slice(
                 if (V.subset) v &= V.subset[wd];
                 samples_out[Q.samples_out_off + wd] = v;
             }
+        }
+        // words past the register window were OR-ed into samples_out (zeroed
+        // by the host) by the lane that owns them: mask them the same way
+        for (uint32_t wd = static_cast<uint32_t>(lane) + 64u * NACC; wd < Q.words; wd += 64u) {
+            uint64_t v = S.err_out ? 0ull : samples_out[Q.samples_out_off + wd];
+            if (V.subset) v &= V.subset[wd];
+            samples_out[Q.samples_out_off + wd] = v;
         }
     }
 }
@@ -2094,7 +2110,12 @@ void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t
                  int mode, const uint8_t *qbytes, const uint64_t *subsets, QRes *res, uint64_t *hits,
                  uint64_t *samples_out, hipStream_t s) {
     if (!n) return;
-    const int nacc = max_words == 0 ? 0 : max_words <= 64 ? 1 : max_words <= 256 ? 4 : 16;
+    int nacc = max_words == 0 ? 0 : max_words <= 64 ? 1 : max_words <= 256 ? 4 : 16;
+    // SBEACON_MAX_NACC (tests): shrink the register window so small cohorts
+    // exercise the words-beyond-the-window path of >65,536-sample VCFs
+    const char *cap_env = std::getenv("SBEACON_MAX_NACC");
+    const int cap = cap_env ? std::atoi(cap_env) : 16;
+    if (nacc > 0 && cap >= 1) nacc = std::min(nacc, cap >= 16 ? 16 : cap >= 4 ? 4 : 1);
     if (nacc == 0) {  // every sample-free specialisation goes through the fused kernel
         if (qidx) throw std::runtime_error("launch_scan: sample-free queries must be contiguous (qidx = null)");
         const FusedGroup one{q, n, mode};

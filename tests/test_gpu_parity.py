@@ -45,6 +45,34 @@ def test_patched_variant_type_goldens(goldens, fixture_stores, fixture):
         _cmp(g, c)
 
 
+@pytest.mark.parametrize('fixture', ['tiny22', 'quirk22'])
+@pytest.mark.parametrize('wrap', ['sync', 'sns'])
+def test_handler_goldens(goldens, fixture_stores, fixture, wrap, monkeypatch):
+    """performQuery lambda_handler (lambda/performQuery/lambda_function.py:
+    23-49) against the reference goldens, invoked directly and as an SNS
+    record (the payload JSON in Records[0].Sns.Message): the returned dict
+    equals the reference response.dump(), and the reference's exception class
+    is raised where it raised one (strict variantType, as generated)."""
+    import json
+    from sbeacon import engine, perform_query
+    monkeypatch.setattr(perform_query, 'STRICT_VARIANT_TYPE', True)
+    engine.registry.register(fixture_stores[fixture])
+    try:
+        for c in [c for c in goldens if c['fixture'] == fixture and c['oracle'] == 'reference']:
+            ev = c['payload'] if wrap == 'sync' else {'Records': [{'Sns': {'Message': json.dumps(c['payload'])}}]}
+            try:
+                got = perform_query.lambda_handler(ev, None)
+            except Exception as e:  # noqa: BLE001
+                got = e
+            if c['error']:
+                assert type(got).__name__ == c['error'], (c['payload'], got)
+            else:
+                assert not isinstance(got, Exception), (c['payload'], got)
+                assert normalise(got) == normalise(c['response']), c['payload']
+    finally:
+        engine.registry.clear()
+
+
 def _vs_oracle(store, orc, payloads):
     got = store.query(payloads).responses()
     exp = orc.perform_query_batch(payloads, patched=True)
@@ -58,11 +86,18 @@ def _vs_oracle(store, orc, payloads):
 
 @pytest.mark.parametrize('seed,quirks,n_rec,n_samp,spw', [(11, False, 20000, 40, '0'), (12, True, 6000, 70, '0'),
                                                             (13, False, 3000, 130, '0'), (11, False, 20000, 40, '8'),
-                                                            (12, True, 6000, 70, '3')])
+                                                            (12, True, 6000, 70, '3'),
+                                                            (14, False, 1500, 4500, 'nacc1'),
+                                                            (15, True, 40, 66000, '0')])
 def test_random_vs_oracle(tmp_path, monkeypatch, seed, quirks, n_rec, n_samp, spw):
     """spw: slices per wave ('0' = the launch's own choice, one per wave for
-    batches this small; '8' / '3' = slice runs with lane-parallel bounds)."""
-    if spw != '0':
+    batches this small; '8' / '3' = slice runs with lane-parallel bounds;
+    'nacc1' = a 64-word sample register window, so 4,500 samples (71 words)
+    take the words-beyond-the-window path).  66,000 samples (1,032 words) is
+    past the largest register window (1,024 words) on its own."""
+    if spw == 'nacc1':
+        monkeypatch.setenv('SBEACON_MAX_NACC', '1')
+    elif spw != '0':
         monkeypatch.setenv('SBEACON_SLICES_PER_WAVE', spw)
     from oracle.oracle import OracleVcf
     from sbeacon import synth
@@ -73,7 +108,7 @@ def test_random_vs_oracle(tmp_path, monkeypatch, seed, quirks, n_rec, n_samp, sp
     orc = OracleVcf(path)
     recs, names = read_records(path)
     rng = random.Random(seed)
-    payloads = [random_payload(rng, recs, names, 'r.vcf') for _ in range(3000)]
+    payloads = [random_payload(rng, recs, names, 'r.vcf') for _ in range(3000 if n_samp < 10000 else 300)]
     _vs_oracle(store, orc, payloads)
 
 
