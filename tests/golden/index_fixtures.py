@@ -48,12 +48,13 @@ def vcf_text(name: str) -> bytes:
             else:
                 ref = rng.choice('ACGT')
             alt = rng.choice('ACGT')
-            info = f'AC={rng.randint(0, 5)}'
+            info = f'AC={rng.randint(0, 5)};AN=10'
             if r > 0.985:  # a structural variant: END far past POS (upper-level bins)
                 alt = '<DEL>'
                 info += f';END={pos + rng.randint(1000, 3_000_000)}'
             elif r > 0.98:  # END= not past POS: ignored by the tabix VCF preset
                 info = f'END={pos - 5};' + info
+            info += ';DP=5'  # INFO does not end in AC/AN: a sites-only line would read on into the next one
             line = f'{contig}\t{pos}\t.\t{ref}\t{alt}\t50\tPASS\t{info}'
             if n_samples is not None:
                 line += '\tGT' + ''.join(f'\t{rng.randint(0, 1)}|{rng.randint(0, 1)}' for _ in range(n_samples))
