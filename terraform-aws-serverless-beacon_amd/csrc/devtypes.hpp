@@ -10,6 +10,7 @@
 // record-indexed columns, so biallelic records (98.5 % of a 1000G VCF) need
 // no dependent load.  ALTs 2..n live in "extra" rows reached through x_lo[].
 #pragma once
+#include <climits>
 #include <cstdint>
 
 namespace sb {
@@ -31,6 +32,10 @@ enum : uint32_t {
     C_REP_NONE = 63,
     C_SYM_SHIFT = 16,         // symbolic-ALT dictionary id
 };
+
+// RecHot::an of a record the store cannot represent (H_AN_BAD is set too):
+// a query that reaches it raises SB_QERR_UNSUPPORTED (ingest.cpp unrep)
+constexpr int32_t kAnUnrepresentable = INT32_MIN;
 
 struct alignas(16) RecHot {
     uint32_t end;  // POS + len(REF) - 1 (:90)

@@ -330,6 +330,12 @@ struct Parser {
         c.ref_off.push_back(c.blob.size());
         c.blob.insert(c.blob.end(), ref, ref + ref_len);
         // ALT split on ',' (:97)
+        // unrep: the record is beyond what the device words represent (> 64
+        // ALTs, AC / AN / called alleles beyond int32, a GT fallback row
+        // with ploidy > 3 or allele >= 255).  It is stored as a placeholder
+        // (REF, end, ALT 0) whose evaluation raises SB_QERR_UNSUPPORTED for
+        // any query that reaches it, instead of failing the whole VCF.
+        bool unrep = false;
         const char *alts[64];
         size_t alens[64];
         uint32_t na = 0;
@@ -338,10 +344,13 @@ struct Parser {
             for (;;) {
                 const char *cm = static_cast<const char *>(memchr(a, ',', static_cast<size_t>(ae - a)));
                 if (!cm) cm = ae;
-                if (na == 64) return fail(L, "more than 64 ALT alleles");
-                alts[na] = a;
-                alens[na] = static_cast<size_t>(cm - a);
-                ++na;
+                if (na == 64) {
+                    unrep = true;  // ALTs past the 64th are not stored
+                } else {
+                    alts[na] = a;
+                    alens[na] = static_cast<size_t>(cm - a);
+                    ++na;
+                }
                 if (cm == ae) break;
                 a = cm + 1;
             }
@@ -386,7 +395,7 @@ struct Parser {
         }
         L.vt_off.push_back(vt_off);
         L.vt_len.push_back(vt_len);
-        if (has_an && (an_val > INT32_MAX || an_val < INT32_MIN)) return fail(L, "AN beyond int32");
+        if (has_an && (an_val > INT32_MAX || an_val < INT32_MIN)) unrep = true;
         // AC values (:206)
         int64_t acv[64];
         uint32_t n_ac = 0;
@@ -400,7 +409,7 @@ struct Parser {
                 if (!py_int(a, static_cast<size_t>(cm - a), &v)) {
                     ac_bad = true;
                 } else {
-                    if (v > INT32_MAX || v < INT32_MIN) return fail(L, "AC beyond int32");
+                    if (v > INT32_MAX || v < INT32_MIN) unrep = true;
                     if (n_ac < 64) acv[n_ac] = v;
                     ++n_ac;
                 }
@@ -476,8 +485,10 @@ struct Parser {
                             ++gt_an;
                             if (v >= 1 && v <= na) gtcount[v - 1]++;
                             if (need_fb) {
-                                if (nrun >= 3 || v > 254) return fail(L, "genotype fallback row needs ploidy <= 3 and allele < 255");
-                                vals[nrun] = static_cast<uint32_t>(v);
+                                if (nrun >= 3 || v > 254)
+                                    unrep = true;
+                                else
+                                    vals[nrun] = static_cast<uint32_t>(v);
                             }
                             ++nrun;
                             i = j;
@@ -518,7 +529,17 @@ struct Parser {
         if (need_fb) hot |= H_HAS_FB;
         if (na > 1) hot |= H_MULTI;
         const int64_t anv = has_an ? an_val : gt_an;
-        if (anv > INT32_MAX) return fail(L, "called-allele count beyond int32");
+        if (anv > INT32_MAX || anv < INT32_MIN) unrep = true;
+        if (unrep) {
+            // placeholder: ALT 0 only, no extra rows / fallback row / carriers
+            hot = H_HAS_AN | H_AN_BAD;
+            na = 1;
+            fb_row = -1;
+            if (keep_gt && n_samples) {
+                c.planesx.resize(planex);
+                std::fill(c.planes0.begin() + static_cast<std::ptrdiff_t>(plane0), c.planes0.end(), 0ull);
+            }
+        }
         int32_t ac0 = 0;
         uint32_t rh_info = 0;  // RangeHot (MODE_RANGE_N) view
         int64_t rh_c = 0;
@@ -572,9 +593,14 @@ struct Parser {
             }
             c.blob.insert(c.blob.end(), ap, ap + al);
         }
-        c.rec.push_back(RecHot{static_cast<uint32_t>(end), hot, static_cast<int32_t>(anv), ac0});
+        if (unrep) {
+            ac0 = 0;
+            rh_info = RH_HIT | RH_SLOW;  // every range query evaluates it (and raises)
+        }
+        const int32_t an32 = unrep ? kAnUnrepresentable : static_cast<int32_t>(anv);
+        c.rec.push_back(RecHot{static_cast<uint32_t>(end), hot, an32, ac0});
         if (an_bad || ac_bad || rh_c > INT32_MAX || rh_c < INT32_MIN) rh_info |= RH_SLOW;
-        c.rng.push_back(RangeHot{static_cast<uint32_t>(end), rh_info, static_cast<int32_t>(anv),
+        c.rng.push_back(RangeHot{static_cast<uint32_t>(end), rh_info, an32,
                                  static_cast<int32_t>((rh_info & RH_SLOW) ? 0 : rh_c)});
         c.fb_off.push_back(fb_row);
         c.x_lo.push_back(static_cast<uint32_t>(c.x_key.size()));

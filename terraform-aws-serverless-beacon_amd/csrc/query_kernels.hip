@@ -292,6 +292,10 @@ __device__ __forceinline__ LaneOut eval_record(const DStore &st, const QDev &Q, 
         pass = false;
     }
     if (!pass) return o;
+    if ((h & H_AN_BAD) && h0.an == kAnUnrepresentable) {  // a placeholder record (ingest.cpp unrep)
+        o.err = SB_QERR_UNSUPPORTED;
+        return o;
+    }
     uint32_t x0 = 0, nx = 0;
     const int64_t ref_len = (V.alt_mode == ALT_VTYPE) ? static_cast<int64_t>(e) - st.pos[r] + 1 : 0;
     {  // ALT 0: class bits live in RecHot::hot

@@ -248,3 +248,41 @@ def test_range_words_vs_oracle(tmp_path, monkeypatch, no_range8, spw):
         p['requested_granularity'] = rng.choice(['record', 'record', 'count', 'boolean'])
         p['include_details'] = p['requested_granularity'] == 'record' or rng.random() < 0.3
     _vs_oracle(store, OracleVcf(path), payloads)
+
+
+def test_unrepresentable_records_are_placeholders(tmp_path):
+    """Records beyond the device words (> 64 ALTs, AC beyond int32, a GT
+    fallback row with ploidy 4) no longer fail the store build:
+    each is a placeholder that raises NotImplementedError (SB_QERR_UNSUPPORTED)
+    for a query reaching it, and queries elsewhere still match the oracle."""
+    from oracle.oracle import OracleVcf
+    from sbeacon.engine import Store
+    alts70 = ','.join('A' + 'C' * i for i in range(1, 71))
+    lines = ['##fileformat=VCFv4.2', '#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFORMAT\tS0\tS1',
+             '22\t1000\t.\tA\tG\t50\tPASS\tAC=1;AN=4\tGT\t0|1\t0|0',
+             f'22\t2000\t.\tA\t{alts70}\t50\tPASS\tAC={",".join(["1"] * 70)};AN=4\tGT\t0|1\t0|70',
+             '22\t3000\t.\tC\tT\t50\tPASS\tAC=3000000000;AN=4\tGT\t0|1\t1|1',
+             '22\t4000\t.\tG\tA\t50\tPASS\tAN=8\tGT\t0/1/1/1\t0/0/0/1',
+             '22\t5000\t.\tT\tC\t50\tPASS\tAC=1;AN=4\tGT\t0|1\t0|0']
+    path = str(tmp_path / 'lim.vcf')
+    open(path, 'w').write('\n'.join(lines) + '\n')
+    store = Store.build([('lim.vcf', path)], device=0)
+    orc = OracleVcf(path)
+    base = dict(passthrough={'includeSamples': True}, dataset_id='d', query_id='q', reference_bases='N', end_min=0,
+                end_max=10**9, variant_type=None, include_details=True, requested_granularity='record',
+                variant_min_length=0, variant_max_length=-1, vcf_location='lim.vcf')
+    placeholders = (2000, 3000, 4000)
+    payloads = []
+    for a, b in [(900, 1500), (1500, 2500), (2500, 3500), (3500, 4500), (4500, 5500), (1, 10000), (1, 1999)]:
+        for alt in ('N', 'G', 'T', None):
+            payloads.append(dict(base, region=f'22:{a}-{b}', alternate_bases=alt or 'N',
+                                 variant_type=None if alt else 'INS', **({} if alt else {'alternate_bases': None})))
+    got = store.query(payloads).responses()
+    for p, g in zip(payloads, got):
+        a, b = map(int, p['region'].split(':')[1].split('-'))
+        if any(a <= x <= b for x in placeholders):
+            assert isinstance(g, NotImplementedError), (p, g)
+        else:
+            e = orc.perform_query(p, patched=True)
+            assert not isinstance(g, Exception), (p, g)
+            assert normalise(g.dump()) == normalise(e), p
