@@ -153,6 +153,13 @@ int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out);
  * sample names ','-joined.  Pointers valid until sb_result_free. */
 int sb_result_variants_text(sb_result_set *r, size_t i, const char **p, size_t *len);
 int sb_result_sample_names_text(sb_result_set *r, size_t i, const char **p, size_t *len);
+/* The g_variants route aggregation (lambda/getGenomicVariants/
+ * route_g_variants.py:153-171: variants.update(...) over the responses) in
+ * the library: the distinct variant strings of the listed queries (errored
+ * queries skipped), '\n'-joined in first-seen order, *count of them.
+ * Pointer valid until the next call on r or sb_result_free. */
+int sb_result_distinct_variants(sb_result_set *r, const uint32_t *queries, size_t n, const char **p, size_t *len,
+                                uint64_t *count);
 
 typedef struct {
     uint64_t n_queries;

@@ -15,6 +15,7 @@
 #include <memory>
 #include <thread>
 #include <tuple>
+#include <unordered_set>
 
 #include <zlib.h>
 
@@ -233,6 +234,7 @@ struct sb_result_set {
     std::vector<std::string> chrom;
     std::vector<std::string> vtext, ntext;
     std::vector<uint8_t> vbuilt, nbuilt;
+    std::string distinct;                       // sb_result_distinct_variants
     std::vector<uint32_t> tmp_rec, tmp_alt;     // views for sb_result_get
     sb_batch_stats stats{};
 };
@@ -2328,38 +2330,79 @@ int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out) {
     return SB_OK;
 }
 
+namespace {
+// f'{chrom}\t{position}\t{reference}\t{alts[i]}\t{variant_type}' (search_variants.py:210)
+void append_variant(std::string &o, const sb_store &s, const std::string &chrom, uint64_t hit) {
+    const uint32_t rec = static_cast<uint32_t>(hit);
+    const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
+    char num[16];
+    o += chrom;
+    o.push_back('\t');
+    const int nn = snprintf(num, sizeof num, "%u", s.h_pos[rec]);
+    o.append(num, static_cast<size_t>(nn));
+    o.push_back('\t');
+    o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_ref_off[rec]), s.h_end[rec] - s.h_pos[rec] + 1);
+    o.push_back('\t');
+    if (k == 0) {
+        o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_a0_off[rec]), s.h_a0_len[rec]);
+    } else {
+        const uint32_t x = s.h_x_lo[rec] + k - 1;
+        o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_x_off[x]), s.h_x_len[x]);
+    }
+    o.push_back('\t');
+    o += s.vt.items[s.h_vt[rec]];
+}
+}  // namespace
+
 int sb_result_variants_text(sb_result_set *r, size_t i, const char **p, size_t *len) {
     if (!r || !p || !len || i >= r->res.size()) return SB_EINVAL;
     if (!r->vbuilt[i]) {
-        const sb_store &s = *r->s;
         std::string &o = r->vtext[i];
         const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
-        char num[16];
         for (uint64_t h = a; h < b; ++h) {
-            const uint32_t rec = static_cast<uint32_t>(r->hit[h]);
-            const uint32_t k = static_cast<uint32_t>(r->hit[h] >> kHitAltShift);
             if (h > a) o.push_back('\n');
-            o += r->chrom[i];  // f'{chrom}\t{position}\t{reference}\t{alts[i]}\t{variant_type}' (:210)
-            o.push_back('\t');
-            const int nn = snprintf(num, sizeof num, "%u", s.h_pos[rec]);
-            o.append(num, static_cast<size_t>(nn));
-            o.push_back('\t');
-            o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_ref_off[rec]), s.h_end[rec] - s.h_pos[rec] + 1);
-            o.push_back('\t');
-            if (k == 0) {
-                o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_a0_off[rec]), s.h_a0_len[rec]);
-            } else {
-                const uint32_t x = s.h_x_lo[rec] + k - 1;
-                o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_x_off[x]), s.h_x_len[x]);
-            }
-            o.push_back('\t');
-            o += s.vt.items[s.h_vt[rec]];
+            append_variant(o, *r->s, r->chrom[i], r->hit[h]);
         }
         r->vbuilt[i] = 1;
     }
     *p = r->vtext[i].data();
     *len = r->vtext[i].size();
     return SB_OK;
+}
+
+int sb_result_distinct_variants(sb_result_set *r, const uint32_t *queries, size_t n, const char **p, size_t *len,
+                                uint64_t *count) {
+    return guard([&] {
+        if (!r || !p || !len || !count || (n && !queries)) throw Error(SB_EINVAL, "NULL argument");
+        // (chrom string, record, alt) first, then the formatted strings: two
+        // records (or two VCFs naming the contig alike) can print the same line
+        std::unordered_map<std::string, uint32_t> chrom_id;
+        std::unordered_set<uint64_t> seen_hit;
+        std::unordered_set<std::string> seen_text;
+        std::string &o = r->distinct;
+        o.clear();
+        uint64_t c = 0;
+        std::string line;
+        for (size_t j = 0; j < n; ++j) {
+            const uint32_t i = queries[j];
+            if (i >= r->res.size()) throw Error(SB_EINVAL, "query index out of range");
+            if (r->res[i].error) continue;
+            const uint32_t cid = chrom_id.emplace(r->chrom[i], static_cast<uint32_t>(chrom_id.size())).first->second;
+            for (uint64_t h = r->dense_off[i]; h < r->dense_off[i + 1]; ++h) {
+                // hit = rec | alt << kHitAltShift; rec < 2^32, alt < 64: fold the chrom id above both
+                const uint64_t key = r->hit[h] ^ (static_cast<uint64_t>(cid) << 40);
+                if (!seen_hit.insert(key).second) continue;
+                line.clear();
+                append_variant(line, *r->s, r->chrom[i], r->hit[h]);
+                if (!seen_text.insert(line).second) continue;
+                if (c++) o.push_back('\n');
+                o += line;
+            }
+        }
+        *p = o.data();
+        *len = o.size();
+        *count = c;
+    });
 }
 
 int sb_result_sample_names_text(sb_result_set *r, size_t i, const char **p, size_t *len) {

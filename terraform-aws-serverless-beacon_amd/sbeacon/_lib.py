@@ -148,6 +148,8 @@ SIGNATURES = {
     'sb_index_vcf': (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int, C.POINTER(C.c_void_p),
                                C.POINTER(C.c_size_t)]),
     'sb_free': (None, [P]),
+    'sb_result_distinct_variants': (C.c_int, [P, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_void_p),
+                                              C.POINTER(C.c_size_t), C.POINTER(C.c_uint64)]),
 }
 
 _lib = None

@@ -47,6 +47,27 @@ class Catalog:
         self.filter_resolver = None
         self.job_status = lambda query_id: JobStatus.NEW
         self.cache: dict[str, dict] = {}  # fetch_from_cache stand-in (query-responses/{id}.json)
+        self._entities: dict[str, dict] = {}  # kind -> dataset_id -> sample name -> [rows]
+        self.entity_provider = None
+
+    def add_entities(self, kind: str, dataset_id: str, rows: dict):
+        """Metadata rows of one dataset (``kind`` = 'individuals' /
+        'biosamples'), keyed by the VCF sample name that analyses map them
+        from (``ANALYSES_TABLE._vcfsampleid``).  A value is one row or a list
+        of rows (a sample with several analyses)."""
+        tab = self._entities.setdefault(kind, {}).setdefault(dataset_id, {})
+        for name, row in rows.items():
+            tab.setdefault(name, []).extend(row if isinstance(row, list) else [row])
+
+    def entities(self, kind: str, dataset_id: str, sample_names) -> list:
+        """get_record_query(dataset_id, sample_names) of the sample routes
+        (route_g_variants_id_individuals.py:64-83, _biosamples.py:95-113):
+        the rows joined to the analyses of those samples.  A custom store is
+        plugged in through ``entity_provider(kind, dataset_id, names)``."""
+        if self.entity_provider is not None:
+            return list(self.entity_provider(kind, dataset_id, list(sample_names)))
+        tab = self._entities.get(kind, {}).get(dataset_id, {})
+        return [dict(r) for n in sample_names for r in tab.get(n, [])]
 
     def add(self, dataset: Dataset):
         self._datasets = [d for d in self._datasets if d.id != dataset.id] + [dataset]
@@ -55,7 +76,9 @@ class Catalog:
     def clear(self):
         self._datasets.clear()
         self.filter_resolver = None
+        self.entity_provider = None
         self.cache.clear()
+        self._entities.clear()
 
     def datasets_fast(self, assembly_id):
         """datasets_query_fast: every dataset of the assembly, no samples."""

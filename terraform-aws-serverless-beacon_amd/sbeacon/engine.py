@@ -15,6 +15,7 @@ to an S3 object.
 from __future__ import annotations
 
 import ctypes as C
+from collections.abc import Sequence
 import os
 from typing import Iterable
 
@@ -430,6 +431,34 @@ class Batch:
             pass
 
 
+class LazyVariants(Sequence):
+    """A response's variant strings, formatted by the library on first use."""
+
+    def __init__(self, rs, i, n):
+        self._rs, self._i, self._n, self._v = rs, i, n, None
+
+    def _load(self):
+        if self._v is None:
+            t = self._rs._text(lib().sb_result_variants_text, self._i)
+            self._v = t.split('\n') if self._n else []
+        return self._v
+
+    def __len__(self):
+        return self._n
+
+    def __getitem__(self, k):
+        return self._load()[k]
+
+    def __iter__(self):
+        return iter(self._load())
+
+    def __eq__(self, other):
+        return list(self._load()) == list(other)
+
+    def __repr__(self):
+        return repr(self._load())
+
+
 class ResultSet:
     def __init__(self, handle, payloads, store):
         self._h = handle
@@ -467,9 +496,20 @@ class ResultSet:
         check(fn(self._h, i, C.byref(p), C.byref(n)))
         return C.string_at(p, n.value).decode() if n.value else ''
 
-    def response(self, i: int) -> PerformQueryResponse:
+    def distinct_variants(self, indices) -> list[str]:
+        """The distinct variant strings of the listed queries, first-seen
+        order (sb_result_distinct_variants: the route aggregation)."""
+        idx = np.ascontiguousarray(np.asarray(list(indices), dtype=np.uint32))
+        p, n, cnt = C.c_void_p(), C.c_size_t(), C.c_uint64()
+        check(lib().sb_result_distinct_variants(self._h, idx.ctypes.data_as(C.POINTER(C.c_uint32)), idx.size,
+                                                C.byref(p), C.byref(n), C.byref(cnt)))
+        return C.string_at(p, n.value).decode().split('\n') if cnt.value else []
+
+    def response(self, i: int, *, lazy_variants: bool = False) -> PerformQueryResponse:
         """The reference PerformQueryResponse for query i, or raise the
-        exception the reference would raise (search_variants.py:262-271)."""
+        exception the reference would raise (search_variants.py:262-271).
+        lazy_variants: the variant strings are formatted on first use (the
+        routes aggregate them in the library instead)."""
         p = self.payloads[i]
         v = self.view(i)
         if v.error:
@@ -477,8 +517,11 @@ class ResultSet:
         pt = p.get('passthrough') or {}
         samples_variant = bool(pt.get('selectedSamplesOnly', False))
         include_samples = bool(pt.get('includeSamples', False))
-        vt = self._text(lib().sb_result_variants_text, i)
-        variants = vt.split('\n') if v.n_variants else []
+        if lazy_variants:
+            variants = LazyVariants(self, i, int(v.n_variants))
+        else:
+            vt = self._text(lib().sb_result_variants_text, i)
+            variants = vt.split('\n') if v.n_variants else []
         names_t = self._text(lib().sb_result_sample_names_text, i)
         names = names_t.split(',') if v.n_sample_indices else []
         if samples_variant:
@@ -487,18 +530,20 @@ class ResultSet:
         else:
             sample_indices = []
             sample_names = names if include_samples else []
-        return PerformQueryResponse(
+        r = PerformQueryResponse(
             exists=bool(v.exists), dataset_id=p.get('dataset_id'), vcf_location=p.get('vcf_location'),
             all_alleles_count=int(v.all_alleles_count), variants=variants, call_count=int(v.call_count),
             sample_indices=sample_indices, sample_names=sample_names)
+        r._src = (self, i)
+        return r
 
-    def responses(self) -> list:
+    def responses(self, *, lazy_variants: bool = False) -> list:
         """All responses; an entry is the exception instance where the
         reference would have raised."""
         out = []
         for i in range(len(self.payloads)):
             try:
-                out.append(self.response(i))
+                out.append(self.response(i, lazy_variants=lazy_variants))
             except (UnboundLocalError, IndexError, ValueError, AttributeError, NotImplementedError) as e:
                 out.append(e)
         return out
@@ -539,7 +584,7 @@ class Registry:
 registry = Registry()
 
 
-def query_payloads(payloads: list[dict], *, strict_variant_type: bool = False) -> list:
+def query_payloads(payloads: list[dict], *, strict_variant_type: bool = False, lazy_variants: bool = False) -> list:
     """Answer PerformQueryPayload dicts through the registry in as few
     device batches as there are stores.  Returns responses/exceptions in
     payload order."""
@@ -547,6 +592,6 @@ def query_payloads(payloads: list[dict], *, strict_variant_type: bool = False) -
     for store, idx in registry.group(payloads):
         sub = [payloads[i] for i in idx]
         rs = store.query(sub, strict_variant_type=strict_variant_type)
-        for j, r in zip(idx, rs.responses()):
+        for j, r in zip(idx, rs.responses(lazy_variants=lazy_variants)):
             out[j] = r
     return out

@@ -85,4 +85,7 @@ class PerformQueryResponse(_Serializable):
     sample_names: list = field(default_factory=list)
 
     def dump(self) -> dict:
-        return {f.name: getattr(self, f.name) for f in fields(self)}
+        d = {f.name: getattr(self, f.name) for f in fields(self)}
+        if not isinstance(d['variants'], list):  # engine.LazyVariants
+            d['variants'] = list(d['variants'])
+        return d

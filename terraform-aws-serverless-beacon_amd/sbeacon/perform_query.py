@@ -39,10 +39,11 @@ def perform_query(payload, is_async=False) -> PerformQueryResponse:
     return res
 
 
-def perform_query_batch(payloads) -> list:
+def perform_query_batch(payloads, *, lazy_variants=False) -> list:
     """Batched entry: one device pass for many PerformQueryPayloads.
     Entries are responses or the exception the reference would raise."""
-    return query_payloads([_as_dict(p) for p in payloads], strict_variant_type=STRICT_VARIANT_TYPE)
+    return query_payloads([_as_dict(p) for p in payloads], strict_variant_type=STRICT_VARIANT_TYPE,
+                          lazy_variants=lazy_variants)
 
 
 def lambda_handler(event, context):

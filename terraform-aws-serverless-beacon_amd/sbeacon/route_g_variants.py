@@ -69,26 +69,43 @@ def _params(event):
 
 
 def aggregate(query_responses, *, granularity, check_all, assembly_id):
-    """route_g_variants.py:144-171: returns (exists, variants, results)."""
+    """route_g_variants.py:144-171: returns (exists, variants, results).
+
+    Responses answered by the device carry their result set (``_src``): their
+    variant strings are deduplicated in the library
+    (sb_result_distinct_variants) and only the distinct strings reach
+    Python.  ``results`` follows first-seen order per result set (the
+    reference's is thread-completion order)."""
     variants = set()
     results = []
     found = set()
     exists = False
+    by_set = {}  # id(result set) -> (result set, [query indices])
+
+    def add(strings):
+        variants.update(strings)
+        for variant in strings:
+            chrom, pos, ref, alt, typ = variant.split('\t')
+            internal_id = f'{assembly_id}\t{chrom}\t{pos}\t{ref}\t{alt}'
+            if internal_id not in found:
+                results.append(responses.get_variant_entry(
+                    base64.b64encode(internal_id.encode()).decode(), assembly_id, ref, alt,
+                    int(pos), int(pos) + len(alt), typ))
+                found.add(internal_id)
+
     for query_response in query_responses:
         exists = exists or query_response.exists
         if exists:
             if granularity == 'boolean':
                 break
             if check_all:
-                variants.update(query_response.variants)
-                for variant in query_response.variants:
-                    chrom, pos, ref, alt, typ = variant.split('\t')
-                    internal_id = f'{assembly_id}\t{chrom}\t{pos}\t{ref}\t{alt}'
-                    if internal_id not in found:
-                        results.append(responses.get_variant_entry(
-                            base64.b64encode(internal_id.encode()).decode(), assembly_id, ref, alt,
-                            int(pos), int(pos) + len(alt), typ))
-                        found.add(internal_id)
+                src = getattr(query_response, '_src', None)
+                if src is not None:
+                    by_set.setdefault(id(src[0]), (src[0], []))[1].append(src[1])
+                else:
+                    add(query_response.variants)
+    for rs, idx in by_set.values():
+        add(rs.distinct_variants(idx))
     return exists, variants, results
 
 
@@ -183,4 +200,8 @@ def lambda_handler(event, context=None, *, catalog=None):
         return route(event, event_hash, catalog=catalog)
     if event['resource'] == '/g_variants/{id}':
         return route_id(event, event_hash, catalog=catalog)
+    if event['resource'] in ('/g_variants/{id}/individuals', '/g_variants/{id}/biosamples'):
+        from .route_g_variants_samples import route_biosamples, route_individuals
+        fn = route_individuals if event['resource'].endswith('individuals') else route_biosamples
+        return fn(event, event_hash, catalog=catalog)
     return None

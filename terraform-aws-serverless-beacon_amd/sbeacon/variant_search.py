@@ -61,7 +61,7 @@ def perform_variant_search_sync(*, datasets, referenceName, referenceBases, alte
     if not payloads:
         return []
     out = []
-    for r in perform_query_batch(payloads):
+    for r in perform_query_batch(payloads, lazy_variants=True):
         if isinstance(r, Exception):
             raise r  # the reference fails loading a Lambda error payload here (:244)
         out.append(r)

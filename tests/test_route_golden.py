@@ -80,7 +80,7 @@ def test_route_goldens_host_logic_with_oracle(route_golden, monkeypatch):
     import sbeacon.variant_search as vs
     orcs = {n: OracleVcf(os.path.join(FIXTURES, n)) for n in ('tiny22.vcf', 'quirk22.vcf')}
 
-    def oracle_batch(payloads):
+    def oracle_batch(payloads, **kw):
         out = []
         for p in payloads:
             r = orcs[p['vcf_location']].perform_query(p, patched=False)
@@ -108,3 +108,41 @@ def test_route_goldens_device(route_golden, monkeypatch):
     finally:
         engine.registry.clear()
     assert n >= 150
+
+
+@pytest.mark.gpu
+def test_library_aggregation_matches_python():
+    """aggregate() over device responses deduplicates the variant strings in
+    the library (sb_result_distinct_variants); the same responses without
+    their result-set link take the Python set path.  Wide requests over both
+    fixtures, several datasets sharing VCFs: identical exists / variants /
+    results."""
+    import random
+    from sbeacon import engine
+    from sbeacon.engine import Store
+    from sbeacon.route_g_variants import aggregate
+    from sbeacon.catalog import Dataset
+    from sbeacon.variant_search import perform_variant_search_sync
+    store = Store.build([(n, os.path.join(FIXTURES, n)) for n in ('tiny22.vcf', 'quirk22.vcf')], device=0)
+    engine.registry.register(store)
+    try:
+        ds = [Dataset(id='a', assemblyId='G', vcfLocations=['tiny22.vcf'],
+                      vcfChromosomeMap=[{'vcf': 'tiny22.vcf', 'chromosomes': ['22']}]),
+              Dataset(id='b', assemblyId='G', vcfLocations=['tiny22.vcf', 'quirk22.vcf'],
+                      vcfChromosomeMap=[{'vcf': v, 'chromosomes': ['22']} for v in ('tiny22.vcf', 'quirk22.vcf')])]
+        rng = random.Random(4)
+        for _ in range(40):
+            a = rng.randrange(16050000, 16100000)
+            rs = perform_variant_search_sync(
+                datasets=ds, referenceName='22', referenceBases='N', alternateBases=rng.choice(['N', 'A', 'T']),
+                start=[a], end=[a + rng.choice([100, 5000, 60000])], variantType=None, variantMinLength=0,
+                variantMaxLength=-1, requestedGranularity='record', includeResultsetResponses='ALL')
+            lib_side = aggregate(rs, granularity='record', check_all=True, assembly_id='G')
+            for r in rs:
+                r._src = None
+            py_side = aggregate(rs, granularity='record', check_all=True, assembly_id='G')
+            assert lib_side[0] == py_side[0] and lib_side[1] == py_side[1]
+            key = lambda e: e['variantInternalId']  # noqa: E731
+            assert sorted(lib_side[2], key=key) == sorted(py_side[2], key=key)
+    finally:
+        engine.registry.clear()
