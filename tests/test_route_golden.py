@@ -114,22 +114,23 @@ def test_route_goldens_device(route_golden, monkeypatch):
 def test_library_aggregation_matches_python():
     """aggregate() over device responses deduplicates the variant strings in
     the library (sb_result_distinct_variants); the same responses without
-    their result-set link take the Python set path.  Wide requests over both
-    fixtures, several datasets sharing VCFs: identical exists / variants /
-    results."""
+    their result-set link take the Python set path.  Wide requests, two
+    datasets sharing a VCF and a second VCF with the same lines (equal
+    strings from different records): identical exists / variants / results."""
     import random
     from sbeacon import engine
     from sbeacon.engine import Store
     from sbeacon.route_g_variants import aggregate
     from sbeacon.catalog import Dataset
     from sbeacon.variant_search import perform_variant_search_sync
-    store = Store.build([(n, os.path.join(FIXTURES, n)) for n in ('tiny22.vcf', 'quirk22.vcf')], device=0)
+    tiny = os.path.join(FIXTURES, 'tiny22.vcf')
+    store = Store.build([('tiny22.vcf', tiny), ('copy22.vcf', tiny)], device=0)  # same lines in two VCFs
     engine.registry.register(store)
     try:
         ds = [Dataset(id='a', assemblyId='G', vcfLocations=['tiny22.vcf'],
                       vcfChromosomeMap=[{'vcf': 'tiny22.vcf', 'chromosomes': ['22']}]),
-              Dataset(id='b', assemblyId='G', vcfLocations=['tiny22.vcf', 'quirk22.vcf'],
-                      vcfChromosomeMap=[{'vcf': v, 'chromosomes': ['22']} for v in ('tiny22.vcf', 'quirk22.vcf')])]
+              Dataset(id='b', assemblyId='G', vcfLocations=['tiny22.vcf', 'copy22.vcf'],
+                      vcfChromosomeMap=[{'vcf': v, 'chromosomes': ['22']} for v in ('tiny22.vcf', 'copy22.vcf')])]
         rng = random.Random(4)
         for _ in range(40):
             a = rng.randrange(16050000, 16100000)
