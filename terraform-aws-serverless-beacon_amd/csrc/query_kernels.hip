@@ -1509,6 +1509,278 @@ __global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const ChainDev
         if (k < R) x = process(k, x);
 }
 
+// Packed variant of chain_kernel: the run's chains share the wave's lanes.
+// After the descriptor round (staged in LDS) and the bounds / LUT / corig
+// round, the candidate ranges [C0_k, C1_k) of the run's chains are laid end
+// to end (prefix P_k); lane L of chunk c takes global candidate
+// g = 64 c + L, i.e. chain k with P_k <= g < P_{k+1}.  A run's ~150
+// candidates are then ~3 chunks instead of 8 chain-sequential ones, and every
+// chunk load of the run is issued before the first is evaluated (kPackAhead
+// in flight).  Per-slice sums live in LDS at slot 32 k + slice; each chain's
+// hits stay dense and in record order: its lanes are contiguous within a
+// chunk, so the in-chain prefix is a masked popcount and the chain's running
+// count advances by the popcount over its lane range.  exists = call_count >
+// 0 (chains need a non-negative-AC store).
+constexpr int kPackAhead = 4;  // candidate chunks issued before the first is evaluated
+
+struct PackLds {
+    uint4 desc[kChainRun * 5];  // the run's ChainDev descriptors
+    unsigned long long cc[kChainRun * kChainMax], an[kChainRun * kChainMax];
+    unsigned int nh[kChainRun * kChainMax];
+    unsigned long long tcc[kChainRun], tan[kChainRun];
+    unsigned int slow[kChainRun];
+};
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+struct PackChunk {
+    ChainChunk x;
+    uint32_t k;  // the lane's chain
+};
+
+__global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const ChainDev *__restrict__ chains,
+                                                            uint32_t n_chains, uint32_t run,
+                                                            const uint32_t *__restrict__ corig,
+                                                            QRes *__restrict__ res, uint64_t *__restrict__ hits,
+                                                            ReqPartial *__restrict__ cpart) {
+    __shared__ PackLds lds_all[kWavesPerBlock];
+    const uint32_t c_first = launch_wave() * run;
+    if (c_first >= n_chains) return;
+    const uint32_t R = min(run, n_chains - c_first);
+    PackLds &L = lds_all[threadIdx.x >> 6];
+    const uint32_t ul = static_cast<uint32_t>(lane_id());
+    // round 1: the run's descriptors, one 16-byte word per lane, staged in LDS
+    {
+        const uint4 *cd = reinterpret_cast<const uint4 *>(chains + c_first);
+        uint4 w{0, 0, 0, 0};
+        if (ul < 5 * R) w = cd[ul];
+        if (ul < 5 * R) L.desc[ul] = w;
+        if (ul < kChainRun) {
+            L.tcc[ul] = 0;
+            L.tan[ul] = 0;
+            L.slow[ul] = 0;
+        }
+    }
+    wave_lds_sync();
+    // lane j < R: chain j's slice count and its slots' prefix (sex / sin)
+    uint32_t nv = 0, sin = 0, sex = 0;
+    {
+        nv = ul < R ? L.desc[5 * ul].y : 0u;
+        sin = nv;
+#pragma unroll
+        for (int d = 1; d < static_cast<int>(kChainRun); d <<= 1) {
+            const uint32_t t = __shfl_up(sin, d, kWave);
+            if (ul >= static_cast<uint32_t>(d)) sin += t;
+        }
+        sex = sin - nv;
+    }
+    const uint32_t S = rdl(sin, kChainRun - 1);  // slots in use (<= kChainRun * kChainMax)
+    // slot t (flattened over the run) -> chain, slice
+    auto slot_of = [&](uint32_t t, uint32_t *j_out) -> uint32_t {
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t j = 1; j < kChainRun; ++j) k += (j < R && t >= rdl(sex, j)) ? 1u : 0u;
+        *j_out = t - __shfl(sex, static_cast<int>(k), kWave);
+        return k;
+    };
+    // round 2: lanes 2k / 2k+1 = chain k's candidate bounds, lanes 8k + t =
+    // LUT word t of chain k, lane t = corig of slot t; zero the used slots
+    uint32_t bound = 0, lutv = 0;
+    {
+        const uint32_t kb = min(ul >> 1, R - 1);
+        const uint4 b0 = L.desc[5 * kb], b1 = L.desc[5 * kb + 1], b2 = L.desc[5 * kb + 2];
+        if (ul < 2 * R) {
+            const uint32_t up = ul & 1u;
+            const uint64_t x = up ? static_cast<uint64_t>(b0.w) + 1 : b0.z;  // last + 1 / first
+            const uint32_t c_lo = b1.y, c_hi = b1.z, cb_base = b1.w;
+            const uint64_t cb_off = static_cast<uint64_t>(b2.x) | (static_cast<uint64_t>(b2.y) << 32);
+            if (x <= cb_base) {
+                bound = c_lo;
+            } else {
+                const uint64_t b = (x - cb_base) >> b2.z;
+                bound = b >= b2.w ? c_hi : st.vc_bucket[cb_off + b + up];
+            }
+        }
+        const uint32_t kl = min(ul >> 3, R - 1);
+        if (ul < 8 * R) lutv = st.sym_lut[L.desc[5 * kl + 4].y + (ul & 7u)];
+    }
+    uint32_t orig[kChainRun * kChainMax / kWave];  // slot ul + 64 t
+#pragma unroll
+    for (uint32_t t = 0; t < kChainRun * kChainMax / kWave; ++t) {
+        orig[t] = 0;
+        const uint32_t slot = ul + kWave * t;
+        if (kWave * t < S) {
+            uint32_t j;
+            const uint32_t k = slot_of(min(slot, S - 1), &j);
+            if (slot < S) {
+                orig[t] = corig[L.desc[5 * k].x + j];
+                L.cc[k * kChainMax + j] = 0;
+                L.an[k * kChainMax + j] = 0;
+                L.nh[k * kChainMax + j] = 0;
+            }
+        }
+    }
+    // the chains' candidate ranges laid end to end; lane j < R holds chain
+    // j's first candidate (c0v), its prefix (pex: exclusive, pin: inclusive)
+    uint32_t c0v = 0, pex = 0, pin = 0;
+    {
+        const uint32_t j = min(ul, R - 1);
+        const uint32_t lo = __shfl(bound, static_cast<int>(2 * j), kWave);
+        const uint32_t hi = __shfl(bound, static_cast<int>(2 * j + 1), kWave);
+        const bool void_end = (L.desc[5 * j + 4].x & kChainEndVoid) != 0;
+        c0v = lo;
+        const uint32_t cnt = (ul < R && !void_end) ? max(lo, hi) - lo : 0u;
+        pin = cnt;
+#pragma unroll
+        for (int d = 1; d < static_cast<int>(kChainRun); d <<= 1) {
+            const uint32_t t = __shfl_up(pin, d, kWave);
+            if (ul >= static_cast<uint32_t>(d)) pin += t;
+        }
+        pex = pin - cnt;
+    }
+    wave_lds_sync();
+    const uint32_t T = rdl(pin, kChainRun - 1);
+    const uint32_t i_safe = rdl(c0v, 0);  // a valid slot (inside the kind lists + sentinel)
+    // global candidate g -> chain k (count of chains j >= 1 starting at or before g)
+    auto chain_of = [&](uint32_t g) -> uint32_t {
+        uint32_t k = 0;
+#pragma unroll
+        for (uint32_t j = 1; j < kChainRun; ++j) k += (j < R && g >= rdl(pex, j)) ? 1u : 0u;
+        return k;
+    };
+    auto load = [&](uint32_t base) -> PackChunk {
+        const uint32_t g = base + ul;
+        const uint32_t k = chain_of(g);
+        const uint32_t c0 = __shfl(c0v, static_cast<int>(k), kWave), p = __shfl(pex, static_cast<int>(k), kWave);
+        const uint32_t i = g < T ? c0 + (g - p) : i_safe;
+        return PackChunk{ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]}, k};
+    };
+    uint32_t noutv = 0;  // lane j: hits chain j has written so far
+    auto lanes_from = [](uint32_t a) -> uint64_t { return a >= 64 ? 0ull : (~0ull << a); };
+    auto lanes_below = [](uint32_t b) -> uint64_t { return b >= 64 ? ~0ull : ((1ull << b) - 1ull); };
+    auto eval = [&](const PackChunk &c, uint32_t base) {
+        const ChainChunk &x = c.x;
+        const uint32_t k = c.k;
+        const uint32_t g = base + ul;
+        const bool valid = g < T;
+        const uint4 e0 = L.desc[5 * k], e1 = L.desc[5 * k + 1], e3 = L.desc[5 * k + 3], e4 = L.desc[5 * k + 4];
+        const uint32_t first = e0.z, last = e0.w, n = e0.y, width = e1.x;
+        const VtPred Pd(st, e3.x, e3.y, e3.z, e3.w, e4.x, e4.y, lutv, 8 * k);
+        const bool inwin = valid && x.p >= first && x.p <= last;
+        const bool cand = inwin && Pd.end_ok(x.h.end);
+        if (cand && (x.h.w & VT_SLOW)) L.slow[k] = 1u;  // never: prepare dissolves such chains
+        const LaneOut o = Pd.eval(st, x.h, x.r, cand && !(x.h.w & VT_SLOW));
+        const bool hit = o.hm != 0;
+        if (!__ballot(hit)) return;
+        // slice = (POS - first) / width: float reciprocal, then one exact correction
+        uint32_t sid = 0;
+        if (inwin) {
+            const uint32_t d = x.p - first;
+            uint32_t q;
+            if (d < (1u << 24)) {  // exact in f32: the estimate is within one of the quotient
+                q = static_cast<uint32_t>(static_cast<float>(d) * __frcp_rn(static_cast<float>(width)));
+                if (static_cast<uint64_t>(q) * width > d) --q;
+                else if (static_cast<uint64_t>(q + 1) * width <= d) ++q;
+            } else {
+                q = d / width;
+            }
+            sid = min(q, n - 1);
+        }
+        const uint32_t cnt = hit ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
+        const uint32_t pk = __shfl(pex, static_cast<int>(k), kWave);
+        const uint32_t before = __shfl(noutv, static_cast<int>(k), kWave);
+        const uint64_t mine = lanes_from(pk > base ? pk - base : 0u) & ((1ull << ul) - 1ull);  // chain k's lanes below
+        // lane j < R: chain j's lanes in this chunk
+        const uint64_t mj = lanes_from(pex > base ? pex - base : 0u) & lanes_below(pin > base ? pin - base : 0u);
+        uint32_t pre = 0, add = 0;
+        if (!__ballot(cnt > 1)) {
+            const uint64_t one = __ballot(cnt == 1);
+            pre = static_cast<uint32_t>(__popcll(one & mine));
+            add = static_cast<uint32_t>(__popcll(one & mj));
+        } else {  // bit-sliced (multi-ALT hit lanes)
+            for (uint32_t bb = 0; bb < 7; ++bb) {
+                const uint64_t m = __ballot((cnt >> bb) & 1u);
+                pre += static_cast<uint32_t>(__popcll(m & mine)) << bb;
+                add += static_cast<uint32_t>(__popcll(m & mj)) << bb;
+                if (!__ballot(cnt >> (bb + 1))) break;
+            }
+        }
+        if (ul < R) noutv += add;
+        if (cnt) {
+            const uint64_t out = static_cast<uint64_t>(e4.z) | (static_cast<uint64_t>(e4.w) << 32);
+            uint64_t *dst = hits + out + before + pre;
+            for (uint64_t b = o.em; b; b &= b - 1)
+                *dst++ = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
+            atomicAdd(&L.nh[k * kChainMax + sid], cnt);
+        }
+        if (hit) {
+            atomicAdd(&L.cc[k * kChainMax + sid], static_cast<unsigned long long>(o.c));
+            atomicAdd(&L.an[k * kChainMax + sid], static_cast<unsigned long long>(o.anv));
+        }
+    };
+    // every chunk of the run issued before the first is evaluated
+    PackChunk buf[kPackAhead];
+#pragma unroll
+    for (int a = 0; a < kPackAhead; ++a) buf[a] = load(64u * a);
+#pragma unroll
+    for (int a = 0; a < kPackAhead; ++a)
+        if (64u * a < T) eval(buf[a], 64u * a);
+    for (uint32_t base = 64u * kPackAhead; base < T; base += 64u) eval(load(base), base);  // long runs
+    wave_lds_sync();
+    // results: lane ul + 64 t = slot; chain totals by slot atomics
+    uint64_t exm_all[kChainRun * kChainMax / kWave];
+#pragma unroll
+    for (uint32_t t = 0; t < kChainRun * kChainMax / kWave; ++t) {
+        exm_all[t] = 0;
+        if (kWave * t < S) {
+            const uint32_t slot = ul + kWave * t;
+            uint32_t j;
+            const uint32_t k = slot_of(min(slot, S - 1), &j);
+            const bool sl = slot < S;
+            const uint32_t ls = k * kChainMax + j;
+            const int64_t cc = sl ? static_cast<int64_t>(L.cc[ls]) : 0;
+            const int64_t an = sl ? static_cast<int64_t>(L.an[ls]) : 0;
+            const uint32_t nh = sl ? L.nh[ls] : 0u;
+            exm_all[t] = __ballot(sl && cc > 0);
+            if (sl) {
+                QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host
+                if (L.slow[k]) {
+                    o.error = SB_QERR_UNSUPPORTED;
+                } else {
+                    o.exists = cc > 0 ? 1 : 0;
+                    o.call_count = cc;
+                    o.all_alleles_count = an;
+                    o.n_hits = nh;
+                }
+                res[orig[t]] = o;
+                if (cpart) {
+                    atomicAdd(&L.tcc[k], static_cast<unsigned long long>(cc));
+                    atomicAdd(&L.tan[k], static_cast<unsigned long long>(an));
+                }
+            }
+        }
+    }
+    if (cpart) {
+        wave_lds_sync();
+        if (ul < R) {
+            // exists count of chain ul: its slots [sex, sin) in the flattened order
+            int64_t ex = 0;
+#pragma unroll
+            for (uint32_t t = 0; t < kChainRun * kChainMax / kWave; ++t) {
+                const uint32_t a = sex > kWave * t ? sex - kWave * t : 0u, b = sin > kWave * t ? sin - kWave * t : 0u;
+                ex += __popcll(exm_all[t] & lanes_from(a) & lanes_below(b));
+            }
+            cpart[c_first + ul] = L.slow[ul] ? ReqPartial{0, 0, 0, 0, static_cast<int64_t>(nv)}
+                                             : ReqPartial{ex, static_cast<int64_t>(noutv),
+                                                          static_cast<int64_t>(L.tcc[ul]),
+                                                          static_cast<int64_t>(L.tan[ul]), 0};
+        }
+    }
+}
+
 // Hit-region offsets of chained slices (their hits are dense per chain, in
 // slice order): src[orig] = chain out + the n_hits of the chain's earlier slices.
 __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__restrict__ chains, uint32_t n_chains,
@@ -2022,8 +2294,13 @@ void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, 
     } else {
         while (run > 1 && (n_chains + run - 1) / run < 32768u) run >>= 1;
     }
-    hipLaunchKernelGGL(chain_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st, chains,
-                       n_chains, run, corig, res, hits, cpart);
+    const char *kern = std::getenv("SBEACON_CHAIN_KERNEL");  // "seq": one chain at a time per wave
+    if (kern && kern[0] == 's')
+        hipLaunchKernelGGL(chain_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st, chains,
+                           n_chains, run, corig, res, hits, cpart);
+    else
+        hipLaunchKernelGGL(chain_pack_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st,
+                           chains, n_chains, run, corig, res, hits, cpart);
 }
 
 void launch_chain_src(const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, const QRes *res,

@@ -53,7 +53,7 @@ HDR = b'##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFOR
     (b'22\t0100\t.\tA\tG\t.\t.\tAC=1;AN=2\tGT\t0|1\n', False),
     (b'22\t100\t.\t\tG\t.\t.\tAC=1;AN=2\tGT\t0|1\n', False),
     (b'22\t100\t.\tA\tG\t.\t.\tAC=1;AN=2\tGT\n', False),
-    (b'22\t100\t.\tA\tG\t.\t.\tAC=1\tGT\t0|1|1|1\n', False),  # fallback row needs ploidy <= 3
+    (b'22\t100\t.\tA\tG\t.\t.\tAC=1\tGT\t0|1|1|1\n', True),  # ploidy 4 fallback: a placeholder record
 ])
 def test_ingest_validation(body, ok):
     from sbeacon import _lib

@@ -62,7 +62,7 @@ class _DS:
 def test_variant_search_coordinates(monkeypatch):
     seen = []
 
-    def fake_batch(payloads):
+    def fake_batch(payloads, **kw):
         seen.extend(payloads)
         return [P.PerformQueryResponse(exists=False, vcf_location=p['vcf_location'], dataset_id=p['dataset_id'],
                                        all_alleles_count=0, variants=[], call_count=0) for p in payloads]

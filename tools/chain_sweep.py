@@ -27,13 +27,16 @@ def main():
     sl = shard_slices(shape, reqs, 1, 0)
     out = torch.zeros((max(sl.n_rows, 1), 5), dtype=torch.int64, device='cuda')
     base = None
-    for setting in os.environ.get('SETTINGS', 'run8,run4,run2,run1,nochain').split(','):
+    for setting in os.environ.get('SETTINGS', 'seq8,run8,run4,run2').split(','):
         env = {}
-        if setting.startswith('run'):
+        if setting.startswith('run'):  # packed kernel, k chains per wave
             env['SBEACON_CHAIN_RUN'] = setting[3:]
+        elif setting.startswith('seq'):  # chain-sequential kernel
+            env['SBEACON_CHAIN_RUN'] = setting[3:]
+            env['SBEACON_CHAIN_KERNEL'] = 'seq'
         elif setting == 'nochain':
             env['SBEACON_NO_CHAINS'] = '1'
-        for k in ('SBEACON_CHAIN_RUN', 'SBEACON_NO_CHAINS'):
+        for k in ('SBEACON_CHAIN_RUN', 'SBEACON_NO_CHAINS', 'SBEACON_CHAIN_KERNEL'):
             os.environ.pop(k, None)
         os.environ.update(env)
         t1 = time.perf_counter()

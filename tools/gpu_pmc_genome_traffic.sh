@@ -13,5 +13,5 @@ step() {  # name, limit, command...
 cd /tmp
 step pmc_fetch_w 400 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_fetch_w -o run -- python3 $R/bench.py $ARGS
 step pmc_write_w 400 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $R/gpurun_out/pmc_write_w -o run -- python3 $R/bench.py $ARGS
-cd $R && python3 tools/pmc_traffic.py gpurun_out/pmc_fetch_w gpurun_out/pmc_write_w --records 85000000 --requests 1000000 --out gpurun_out/traffic_genome.json > /dev/null && echo folded
+cd $R && python3 tools/pmc_traffic.py gpurun_out/pmc_fetch_w gpurun_out/pmc_write_w --records 85000000 --requests 1000000 --kernel chain_kernel --out gpurun_out/traffic_genome.json > /dev/null && echo folded
 exit 0

@@ -20,7 +20,7 @@ import os
 import re
 import sys
 
-PHASE = re.compile(r'(fused_kernel|range_n8?_kernel|vt_kernel|scan_kernel|request_reduce_kernel)')
+PHASE = re.compile(r'(fused_kernel|range_n8?_kernel|vt_kernel|scan_kernel|request_reduce_kernel|chain_kernel|row_reduce_kernel|row_gather_kernel|field_tile_\w+_kernel|tile_scan_kernel|hit_\w+_kernel|compact_kernel|dedup\w*|radix\w*|summ\w*)')
 
 
 def load(d, counter):
@@ -52,6 +52,7 @@ def main():
     ap.add_argument('--out', default='profiles/traffic.json')
     ap.add_argument('--records', type=int, default=1103547)
     ap.add_argument('--requests', type=int, default=10000)
+    ap.add_argument('--kernel', default=None, help='the dominant kernel the bench line prices (top-level entry)')
     a = ap.parse_args()
     fetch = load(a.fetch_dir, 'FETCH_SIZE')
     write = load(a.write_dir, 'WRITE_SIZE')
@@ -74,6 +75,13 @@ def main():
         'method': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, kernel trace only), '
                   'FETCH_SIZE x2 (gfx950 16B/lane streaming correction), KiB->B; includes Infinity-Cache hits',
     }
+    if a.kernel:
+        hit = [k for k in kernels if k.startswith(a.kernel)]
+        if hit:
+            out['kernel'] = a.kernel
+            out['hbm_bytes_per_launch'] = kernels[hit[0]]['hbm_bytes_per_launch']
+            out['fetch_bytes_per_launch'] = kernels[hit[0]]['fetch_bytes_per_launch']
+            out['write_bytes_per_launch'] = kernels[hit[0]]['write_bytes_per_launch']
     with open(a.out, 'w') as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
