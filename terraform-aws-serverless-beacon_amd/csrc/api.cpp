@@ -193,6 +193,8 @@ struct sb_batch {
     // launch-ordered array; n_scanned of a chained slice is known on the host
     std::vector<ChainDev> hchains;
     DevMem chains;
+    std::vector<uint32_t> hruns;  // first chain of each chain_pack_kernel wave (+ end)
+    DevMem runs;
     std::vector<uint8_t> chained;
     std::vector<uint32_t> nscan;
     std::vector<uint32_t> chain_members;  // chained queries, chain by chain (device copy: corig)
@@ -452,7 +454,7 @@ void upload_store(sb_builder &b, sb_store &s) {
         }
         if (cw.size() > 0xffffffffull) throw Error(SB_EINVAL, "variantType candidate index exceeds 2^32 entries");
         // candidate POS column + the coarse candidate index of every (segment,
-        // kind) pair, aiming at ~8 candidates per bucket (chain_kernel)
+        // kind) pair, aiming at ~2 candidates per bucket (chain_pack_kernel)
         std::vector<uint32_t> cpos(cw.size() + 1, 0u);
         for (size_t j = 0; j < ci.size(); ++j) cpos[j] = pos[ci[j]];
         // ALTs of the candidates, as a prefix (a chain's hit capacity: every
@@ -465,6 +467,10 @@ void upload_store(sb_builder &b, sb_store &s) {
             return b.pre + static_cast<uint32_t>(__builtin_popcountll(o ? (b.mask & ((1ull << o) - 1ull)) : 0ull));
         };
         std::vector<uint32_t> vcb;
+        // candidates per bucket: a chain loads about this many outside its
+        // window at each end (SBEACON_VC_BUCKET overrides)
+        double per_bucket = 2.0;
+        if (const char *e = std::getenv("SBEACON_VC_BUCKET")) per_bucket = std::max(1.0, std::atof(e));
         for (auto &v : b.vcfs) {
             v.vc_index.assign(v.segments.size(), std::array<VcIndex, kVtKinds>{});
             for (size_t g = 0; g < v.segments.size(); ++g) {
@@ -487,7 +493,7 @@ void upload_store(sb_builder &b, sb_store &s) {
                     const uint64_t span = static_cast<uint64_t>(cpos[x.c_hi - 1]) - x.base;
                     const double gap = nc > 1 ? static_cast<double>(span) / static_cast<double>(nc - 1) : 1.0;
                     uint32_t shift = 0;
-                    while (shift < 31 && static_cast<double>(1ull << (shift + 1)) <= gap * 8.0) ++shift;
+                    while (shift < 31 && static_cast<double>(1ull << (shift + 1)) <= gap * per_bucket) ++shift;
                     const uint64_t nb = (span >> shift) + 1;
                     x.shift = shift;
                     x.n = static_cast<uint32_t>(nb);
@@ -1050,6 +1056,25 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     }
     B.chain_base = static_cast<uint32_t>(lq.size());
     for (uint32_t i : B.chain_members) lq.push_back(B.hq[i]);
+    // chain runs: consecutive chains, at most pack_run_max() per wave and
+    // pack_slots_max() slices (the wave's LDS slots)
+    B.hruns.clear();
+    {
+        uint32_t slots = 0, cnt = 0;
+        for (uint32_t c = 0; c < B.hchains.size(); ++c) {
+            const uint32_t n = B.hchains[c].n;
+            if (cnt == 0 || cnt == pack_run_max() || slots + n > pack_slots_max()) {
+                B.hruns.push_back(c);
+                slots = 0;
+                cnt = 0;
+            }
+            slots += n;
+            ++cnt;
+        }
+        B.hruns.push_back(static_cast<uint32_t>(B.hchains.size()));
+    }
+    B.runs.alloc(B.hruns.size() * 4);
+    HIP_OK(hipMemcpyAsync(B.runs.p, B.hruns.data(), B.hruns.size() * 4, hipMemcpyHostToDevice, st));
     B.chains.alloc(B.hchains.size() * sizeof(ChainDev));
     B.corig.alloc(B.chain_members.size() * 4);
     B.cpart.alloc(B.hchains.size() * sizeof(ReqPartial));
@@ -1096,8 +1121,9 @@ void run(sb_batch &B) {
     }
     if (B.runs_pending++ == 0) HIP_OK(hipEventRecord(B.ev[0], st));
     // chains of variantType slices (one wave per request's slices)
-    launch_chains(d, B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()), B.corig.as<uint32_t>(),
-                  B.res.as<QRes>(), B.hits.as<uint64_t>(), B.cpart.as<ReqPartial>(), st);
+    launch_chains(d, B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()), B.runs.as<uint32_t>(),
+                  static_cast<uint32_t>(B.hruns.size() - 1), B.corig.as<uint32_t>(), B.res.as<QRes>(),
+                  B.hits.as<uint64_t>(), B.cpart.as<ReqPartial>(), st);
     // sample-free groups: one fused launch, long scans first (range, variantType,
     // general) and point lookups last, so the short waves fill the tail
     std::vector<FusedGroup> fg;

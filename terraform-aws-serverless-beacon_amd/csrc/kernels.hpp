@@ -36,8 +36,11 @@ void launch_fused(const DStore &st, const FusedGroup *groups, int count, bool no
 // variantType slices of one request per wave; corig[s] = batch index of the
 // chain-ordered slice s.  launch_chain_src writes the hit-region offset of
 // every chained slice (dense per chain) into src[batch index].
-void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, QRes *res,
-                   uint64_t *hits, ReqPartial *cpart, hipStream_t s);
+void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *runs, uint32_t n_runs,
+                   const uint32_t *corig, QRes *res, uint64_t *hits, ReqPartial *cpart, hipStream_t s);
+// chain runs (one wave each): at most pack_run_max() chains and pack_slots_max() slices per run
+uint32_t pack_run_max();
+uint32_t pack_slots_max();
 void launch_chain_src(const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, const QRes *res,
                       uint64_t *src, hipStream_t s);
 

@@ -797,6 +797,7 @@ struct VtPred {
     const uint32_t *lut;
     uint32_t lutv;      // lane lut_lane + k (k < 8): LUT word k (symbolic ids in the words are < 255)
     uint32_t lut_lane;
+    const uint32_t *llut = nullptr;  // the 8 LUT words in LDS (chain_pack_kernel) instead of lanes
 
     __device__ __forceinline__ void set_kind(uint32_t vk) {
         constexpr uint32_t kDel = vt_class_mask(VT_DEL), kIns = vt_class_mask(VT_INS), kDup = vt_class_mask(VT_DUP),
@@ -843,7 +844,8 @@ struct VtPred {
     // a lane whose word is not VT_SLOW (cand false: nothing); call with every lane active
     __device__ __forceinline__ LaneOut eval(const DStore &st, const VtHot h, uint32_t r, bool cand) const {
         LaneOut o{0, 0, 0, 0, 0};
-        const uint32_t lw0 = __shfl(lutv, static_cast<int>(lut_lane + ((h.w >> 21) & 7u)), kWave);
+        const uint32_t lw0 = llut ? llut[(h.w >> 21) & 7u]
+                                  : static_cast<uint32_t>(__shfl(lutv, static_cast<int>(lut_lane + ((h.w >> 21) & 7u)), kWave));
         uint64_t hm = (cand && alt_ok(h.w, lw0)) ? 1ull : 0ull;
         const uint32_t nx = (cand && (h.w & xneed)) ? h.w >> VT_NX_SHIFT : 0u;
         uint32_t x0 = 0;
@@ -1509,26 +1511,32 @@ __global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const ChainDev
         if (k < R) x = process(k, x);
 }
 
-// Packed variant of chain_kernel: the run's chains share the wave's lanes.
+// Packed chain kernel: a run of up to kPackRun chains shares the wave's lanes
+// (runs built on the host so a run's slices fit kPackSlots LDS slots).
 // After the descriptor round (staged in LDS) and the bounds / LUT / corig
 // round, the candidate ranges [C0_k, C1_k) of the run's chains are laid end
-// to end (prefix P_k); lane L of chunk c takes global candidate
-// g = 64 c + L, i.e. chain k with P_k <= g < P_{k+1}.  A run's ~150
-// candidates are then ~3 chunks instead of 8 chain-sequential ones, and every
-// chunk load of the run is issued before the first is evaluated (kPackAhead
-// in flight).  Per-slice sums live in LDS at slot 32 k + slice; each chain's
-// hits stay dense and in record order: its lanes are contiguous within a
-// chunk, so the in-chain prefix is a masked popcount and the chain's running
-// count advances by the popcount over its lane range.  exists = call_count >
-// 0 (chains need a non-negative-AC store).
-constexpr int kPackAhead = 4;  // candidate chunks issued before the first is evaluated
+// to end (prefix pex); lane L of chunk c takes global candidate g = 64 c + L,
+// i.e. the last chain k with pex_k <= g.  A run's candidates then fill few
+// chunks, and every chunk load of the run is issued before the first is
+// evaluated (kPackAhead in flight).  Per-slice sums live in LDS at the
+// run-flattened slot of (chain, slice); each chain's hits stay dense and in
+// record order: its lanes are contiguous within a chunk, so the in-chain
+// prefix is a masked popcount and the chain's running count (lane k of
+// noutv) advances by the popcount over its lane range.  exists =
+// call_count > 0 (chains need a non-negative-AC store).  The slot and LUT
+// tables keep the per-chain work off the VALU: the kernel is issue-bound
+// (SQ counters, profiles/r02_pmc_chain).
+constexpr int kPackAhead = 4;     // candidate chunks issued before the first is evaluated
+constexpr uint32_t kPackRun = 16;  // chains per wave at most
+constexpr uint32_t kPackSlots = 256;  // slices per run at most (host-enforced)
 
 struct PackLds {
-    uint4 desc[kChainRun * 5];  // the run's ChainDev descriptors
-    unsigned long long cc[kChainRun * kChainMax], an[kChainRun * kChainMax];
-    unsigned int nh[kChainRun * kChainMax];
-    unsigned long long tcc[kChainRun], tan[kChainRun];
-    unsigned int slow[kChainRun];
+    uint4 desc[kPackRun * 5];  // the run's ChainDev descriptors
+    unsigned long long cc[kPackSlots], an[kPackSlots];
+    unsigned int nh[kPackSlots];
+    uint32_t lut[kPackRun * 8];  // each chain's symbolic-ALT LUT words
+    unsigned long long tcc[kPackRun], tan[kPackRun];
+    unsigned int slow[kPackRun];
 };
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1541,54 +1549,61 @@ struct PackChunk {
     uint32_t k;  // the lane's chain
 };
 
+// last lane j < R (lanes hold a nondecreasing prefix v) with v_j <= g
+__device__ __forceinline__ uint32_t last_le(uint32_t v, uint32_t R, uint32_t g) {
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t step = kPackRun / 2; step >= 1; step >>= 1) {
+        const uint32_t t = lo + step;
+        const uint32_t vt = static_cast<uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(min(t, kPackRun - 1)), kWave));
+        if (t < R && vt <= g) lo = t;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const ChainDev *__restrict__ chains,
-                                                            uint32_t n_chains, uint32_t run,
+                                                            const uint32_t *__restrict__ runs, uint32_t n_runs,
                                                             const uint32_t *__restrict__ corig,
                                                             QRes *__restrict__ res, uint64_t *__restrict__ hits,
                                                             ReqPartial *__restrict__ cpart) {
     __shared__ PackLds lds_all[kWavesPerBlock];
-    const uint32_t c_first = launch_wave() * run;
-    if (c_first >= n_chains) return;
-    const uint32_t R = min(run, n_chains - c_first);
+    const uint32_t w = launch_wave();
+    if (w >= n_runs) return;
+    const uint32_t c_first = uniform(runs[w]);
+    const uint32_t R = uniform(runs[w + 1]) - c_first;  // 1 .. kPackRun
     PackLds &L = lds_all[threadIdx.x >> 6];
     const uint32_t ul = static_cast<uint32_t>(lane_id());
-    // round 1: the run's descriptors, one 16-byte word per lane, staged in LDS
+    // round 1: the run's descriptors (5 x 16 B per chain), staged in LDS
     {
         const uint4 *cd = reinterpret_cast<const uint4 *>(chains + c_first);
-        uint4 w{0, 0, 0, 0};
-        if (ul < 5 * R) w = cd[ul];
-        if (ul < 5 * R) L.desc[ul] = w;
-        if (ul < kChainRun) {
+        uint4 w0{0, 0, 0, 0}, w1{0, 0, 0, 0};
+        if (ul < 5 * R) w0 = cd[ul];
+        if (ul + kWave < 5 * R) w1 = cd[ul + kWave];
+        if (ul < 5 * R) L.desc[ul] = w0;
+        if (ul + kWave < 5 * R) L.desc[ul + kWave] = w1;
+        if (ul < kPackRun) {
             L.tcc[ul] = 0;
             L.tan[ul] = 0;
             L.slow[ul] = 0;
         }
     }
     wave_lds_sync();
-    // lane j < R: chain j's slice count and its slots' prefix (sex / sin)
+    // lane j < R: chain j's slice count and slot prefix (sex / sin)
     uint32_t nv = 0, sin = 0, sex = 0;
     {
         nv = ul < R ? L.desc[5 * ul].y : 0u;
         sin = nv;
 #pragma unroll
-        for (int d = 1; d < static_cast<int>(kChainRun); d <<= 1) {
+        for (int d = 1; d < static_cast<int>(kPackRun); d <<= 1) {
             const uint32_t t = __shfl_up(sin, d, kWave);
             if (ul >= static_cast<uint32_t>(d)) sin += t;
         }
         sex = sin - nv;
     }
-    const uint32_t S = rdl(sin, kChainRun - 1);  // slots in use (<= kChainRun * kChainMax)
-    // slot t (flattened over the run) -> chain, slice
-    auto slot_of = [&](uint32_t t, uint32_t *j_out) -> uint32_t {
-        uint32_t k = 0;
-#pragma unroll
-        for (uint32_t j = 1; j < kChainRun; ++j) k += (j < R && t >= rdl(sex, j)) ? 1u : 0u;
-        *j_out = t - __shfl(sex, static_cast<int>(k), kWave);
-        return k;
-    };
-    // round 2: lanes 2k / 2k+1 = chain k's candidate bounds, lanes 8k + t =
-    // LUT word t of chain k, lane t = corig of slot t; zero the used slots
-    uint32_t bound = 0, lutv = 0;
+    const uint32_t S = rdl(sin, kPackRun - 1);  // slots in use (<= kPackSlots, host-enforced)
+    // round 2: lanes 2k / 2k+1 = chain k's candidate bounds; every chain's
+    // LUT words into LDS; lane t = corig of slot t; zero the used slots
+    uint32_t bound = 0;
     {
         const uint32_t kb = min(ul >> 1, R - 1);
         const uint4 b0 = L.desc[5 * kb], b1 = L.desc[5 * kb + 1], b2 = L.desc[5 * kb + 2];
@@ -1604,22 +1619,26 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
                 bound = b >= b2.w ? c_hi : st.vc_bucket[cb_off + b + up];
             }
         }
-        const uint32_t kl = min(ul >> 3, R - 1);
-        if (ul < 8 * R) lutv = st.sym_lut[L.desc[5 * kl + 4].y + (ul & 7u)];
-    }
-    uint32_t orig[kChainRun * kChainMax / kWave];  // slot ul + 64 t
 #pragma unroll
-    for (uint32_t t = 0; t < kChainRun * kChainMax / kWave; ++t) {
+        for (uint32_t h = 0; h < kPackRun * 8 / kWave; ++h) {
+            const uint32_t t = ul + kWave * h;  // word t & 7 of chain t >> 3
+            const uint32_t kl = min(t >> 3, R - 1);
+            L.lut[t] = st.sym_lut[L.desc[5 * kl + 4].y + (t & 7u)];
+        }
+    }
+    uint32_t orig[kPackSlots / kWave];  // slot ul + 64 t
+#pragma unroll
+    for (uint32_t t = 0; t < kPackSlots / kWave; ++t) {
         orig[t] = 0;
-        const uint32_t slot = ul + kWave * t;
         if (kWave * t < S) {
-            uint32_t j;
-            const uint32_t k = slot_of(min(slot, S - 1), &j);
-            if (slot < S) {
-                orig[t] = corig[L.desc[5 * k].x + j];
-                L.cc[k * kChainMax + j] = 0;
-                L.an[k * kChainMax + j] = 0;
-                L.nh[k * kChainMax + j] = 0;
+            const uint32_t slot = min(ul + kWave * t, S - 1);
+            const uint32_t k = last_le(sex, R, slot);
+            const uint32_t sk = __shfl(sex, static_cast<int>(k), kWave);  // every lane active
+            if (ul + kWave * t < S) {
+                orig[t] = corig[L.desc[5 * k].x + (slot - sk)];
+                L.cc[slot] = 0;
+                L.an[slot] = 0;
+                L.nh[slot] = 0;
             }
         }
     }
@@ -1635,27 +1654,23 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
         const uint32_t cnt = (ul < R && !void_end) ? max(lo, hi) - lo : 0u;
         pin = cnt;
 #pragma unroll
-        for (int d = 1; d < static_cast<int>(kChainRun); d <<= 1) {
+        for (int d = 1; d < static_cast<int>(kPackRun); d <<= 1) {
             const uint32_t t = __shfl_up(pin, d, kWave);
             if (ul >= static_cast<uint32_t>(d)) pin += t;
         }
         pex = pin - cnt;
     }
     wave_lds_sync();
-    const uint32_t T = rdl(pin, kChainRun - 1);
+    const uint32_t T = rdl(pin, kPackRun - 1);
     const uint32_t i_safe = rdl(c0v, 0);  // a valid slot (inside the kind lists + sentinel)
-    // global candidate g -> chain k (count of chains j >= 1 starting at or before g)
-    auto chain_of = [&](uint32_t g) -> uint32_t {
-        uint32_t k = 0;
-#pragma unroll
-        for (uint32_t j = 1; j < kChainRun; ++j) k += (j < R && g >= rdl(pex, j)) ? 1u : 0u;
-        return k;
-    };
     auto load = [&](uint32_t base) -> PackChunk {
         const uint32_t g = base + ul;
-        const uint32_t k = chain_of(g);
-        const uint32_t c0 = __shfl(c0v, static_cast<int>(k), kWave), p = __shfl(pex, static_cast<int>(k), kWave);
-        const uint32_t i = g < T ? c0 + (g - p) : i_safe;
+        uint32_t k = 0, i = i_safe;
+        if (base < T) {  // wave-uniform; the load itself is issued either way
+            k = last_le(pex, R, g);
+            const uint32_t c0 = __shfl(c0v, static_cast<int>(k), kWave), p = __shfl(pex, static_cast<int>(k), kWave);
+            if (g < T) i = c0 + (g - p);
+        }
         return PackChunk{ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]}, k};
     };
     uint32_t noutv = 0;  // lane j: hits chain j has written so far
@@ -1668,19 +1683,20 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
         const bool valid = g < T;
         const uint4 e0 = L.desc[5 * k], e1 = L.desc[5 * k + 1], e3 = L.desc[5 * k + 3], e4 = L.desc[5 * k + 4];
         const uint32_t first = e0.z, last = e0.w, n = e0.y, width = e1.x;
-        const VtPred Pd(st, e3.x, e3.y, e3.z, e3.w, e4.x, e4.y, lutv, 8 * k);
+        VtPred Pd(st, e3.x, e3.y, e3.z, e3.w, e4.x, e4.y, 0u, 0u);
+        Pd.llut = &L.lut[8 * k];
         const bool inwin = valid && x.p >= first && x.p <= last;
         const bool cand = inwin && Pd.end_ok(x.h.end);
         if (cand && (x.h.w & VT_SLOW)) L.slow[k] = 1u;  // never: prepare dissolves such chains
         const LaneOut o = Pd.eval(st, x.h, x.r, cand && !(x.h.w & VT_SLOW));
         const bool hit = o.hm != 0;
         if (!__ballot(hit)) return;
-        // slice = (POS - first) / width: float reciprocal, then one exact correction
+        // slice = (POS - first) / width: f32 estimate within one of the quotient, then exact
         uint32_t sid = 0;
         if (inwin) {
             const uint32_t d = x.p - first;
             uint32_t q;
-            if (d < (1u << 24)) {  // exact in f32: the estimate is within one of the quotient
+            if (d < (1u << 24)) {
                 q = static_cast<uint32_t>(static_cast<float>(d) * __frcp_rn(static_cast<float>(width)));
                 if (static_cast<uint64_t>(q) * width > d) --q;
                 else if (static_cast<uint64_t>(q + 1) * width <= d) ++q;
@@ -1692,6 +1708,7 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
         const uint32_t cnt = hit ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
         const uint32_t pk = __shfl(pex, static_cast<int>(k), kWave);
         const uint32_t before = __shfl(noutv, static_cast<int>(k), kWave);
+        const uint32_t slot = __shfl(sex, static_cast<int>(k), kWave) + sid;
         const uint64_t mine = lanes_from(pk > base ? pk - base : 0u) & ((1ull << ul) - 1ull);  // chain k's lanes below
         // lane j < R: chain j's lanes in this chunk
         const uint64_t mj = lanes_from(pex > base ? pex - base : 0u) & lanes_below(pin > base ? pin - base : 0u);
@@ -1714,11 +1731,11 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
             uint64_t *dst = hits + out + before + pre;
             for (uint64_t b = o.em; b; b &= b - 1)
                 *dst++ = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
-            atomicAdd(&L.nh[k * kChainMax + sid], cnt);
+            atomicAdd(&L.nh[slot], cnt);
         }
         if (hit) {
-            atomicAdd(&L.cc[k * kChainMax + sid], static_cast<unsigned long long>(o.c));
-            atomicAdd(&L.an[k * kChainMax + sid], static_cast<unsigned long long>(o.anv));
+            atomicAdd(&L.cc[slot], static_cast<unsigned long long>(o.c));
+            atomicAdd(&L.an[slot], static_cast<unsigned long long>(o.anv));
         }
     };
     // every chunk of the run issued before the first is evaluated
@@ -1731,19 +1748,17 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
     for (uint32_t base = 64u * kPackAhead; base < T; base += 64u) eval(load(base), base);  // long runs
     wave_lds_sync();
     // results: lane ul + 64 t = slot; chain totals by slot atomics
-    uint64_t exm_all[kChainRun * kChainMax / kWave];
+    uint64_t exm_all[kPackSlots / kWave];
 #pragma unroll
-    for (uint32_t t = 0; t < kChainRun * kChainMax / kWave; ++t) {
+    for (uint32_t t = 0; t < kPackSlots / kWave; ++t) {
         exm_all[t] = 0;
         if (kWave * t < S) {
-            const uint32_t slot = ul + kWave * t;
-            uint32_t j;
-            const uint32_t k = slot_of(min(slot, S - 1), &j);
-            const bool sl = slot < S;
-            const uint32_t ls = k * kChainMax + j;
-            const int64_t cc = sl ? static_cast<int64_t>(L.cc[ls]) : 0;
-            const int64_t an = sl ? static_cast<int64_t>(L.an[ls]) : 0;
-            const uint32_t nh = sl ? L.nh[ls] : 0u;
+            const uint32_t slot = min(ul + kWave * t, S - 1);
+            const bool sl = ul + kWave * t < S;
+            const uint32_t k = last_le(sex, R, slot);
+            const int64_t cc = sl ? static_cast<int64_t>(L.cc[slot]) : 0;
+            const int64_t an = sl ? static_cast<int64_t>(L.an[slot]) : 0;
+            const uint32_t nh = sl ? L.nh[slot] : 0u;
             exm_all[t] = __ballot(sl && cc > 0);
             if (sl) {
                 QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host
@@ -1769,7 +1784,7 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
             // exists count of chain ul: its slots [sex, sin) in the flattened order
             int64_t ex = 0;
 #pragma unroll
-            for (uint32_t t = 0; t < kChainRun * kChainMax / kWave; ++t) {
+            for (uint32_t t = 0; t < kPackSlots / kWave; ++t) {
                 const uint32_t a = sex > kWave * t ? sex - kWave * t : 0u, b = sin > kWave * t ? sin - kWave * t : 0u;
                 ex += __popcll(exm_all[t] & lanes_from(a) & lanes_below(b));
             }
@@ -2282,9 +2297,15 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const u
                        ss, slices, ns, bitmap, part, out);
 }
 
-void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, QRes *res,
-                   uint64_t *hits, ReqPartial *cpart, hipStream_t s) {
+void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *runs, uint32_t n_runs,
+                   const uint32_t *corig, QRes *res, uint64_t *hits, ReqPartial *cpart, hipStream_t s) {
     if (!n_chains) return;
+    const char *kern = std::getenv("SBEACON_CHAIN_KERNEL");  // "seq": the chain-sequential kernel
+    if (!(kern && kern[0] == 's')) {
+        hipLaunchKernelGGL(chain_pack_kernel, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs, n_runs,
+                           corig, res, hits, cpart);
+        return;
+    }
     // runs of kChainRun chains per wave while the launch still fills the chip
     // (256 CUs x 4 SIMDs x 8 waves, 4 deep)
     uint32_t run = kChainRun;
@@ -2294,14 +2315,12 @@ void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, 
     } else {
         while (run > 1 && (n_chains + run - 1) / run < 32768u) run >>= 1;
     }
-    const char *kern = std::getenv("SBEACON_CHAIN_KERNEL");  // "seq": one chain at a time per wave
-    if (kern && kern[0] == 's')
-        hipLaunchKernelGGL(chain_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st, chains,
-                           n_chains, run, corig, res, hits, cpart);
-    else
-        hipLaunchKernelGGL(chain_pack_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st,
-                           chains, n_chains, run, corig, res, hits, cpart);
+    hipLaunchKernelGGL(chain_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st, chains,
+                       n_chains, run, corig, res, hits, cpart);
 }
+
+uint32_t pack_run_max() { return kPackRun; }
+uint32_t pack_slots_max() { return kPackSlots; }
 
 void launch_chain_src(const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, const QRes *res,
                       uint64_t *src, hipStream_t s) {

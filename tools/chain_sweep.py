@@ -27,10 +27,10 @@ def main():
     sl = shard_slices(shape, reqs, 1, 0)
     out = torch.zeros((max(sl.n_rows, 1), 5), dtype=torch.int64, device='cuda')
     base = None
-    for setting in os.environ.get('SETTINGS', 'seq8,run8,run4,run2').split(','):
+    for setting in os.environ.get('SETTINGS', 'seq8,pack').split(','):
         env = {}
-        if setting.startswith('run'):  # packed kernel, k chains per wave
-            env['SBEACON_CHAIN_RUN'] = setting[3:]
+        if setting == 'pack':  # packed kernel (host-built runs of up to 16 chains)
+            pass
         elif setting.startswith('seq'):  # chain-sequential kernel
             env['SBEACON_CHAIN_RUN'] = setting[3:]
             env['SBEACON_CHAIN_KERNEL'] = 'seq'
