@@ -75,6 +75,9 @@ def main_genome(args):
     sl = shard_slices(shape, reqs, world, rank)
     batch = prepare_shard_batch(store, sl)
     batch.set_stream(torch.cuda.current_stream().cuda_stream)  # one stream: kernels, torch ops, RCCL
+    # the step delivers request rows + hit lists: chained slices skip their
+    # per-slice QRes rows (turned back on below for the per-slice fetch)
+    batch.set_slice_results(False)
     pst = batch.stats()
     part = torch.zeros((max(sl.n_rows, 1), 5), dtype=torch.int64, device=dev)
     hits = torch.zeros(max(int(pst['hits']), 1), dtype=torch.int64, device=dev)
@@ -112,18 +115,21 @@ def main_genome(args):
         batch.run()
     batch.sync()
     kern_ms = batch.timing()['scan_ms']
+    batch.set_slice_results(True)
+    batch.run()
+    batch.sync()
     rs = batch.fetch()
     st = rs.stats()
     scanned, nhits = st['records_scanned'], st['hits']
-    # Roofline of chain_kernel, priced on the bytes one launch must move at
-    # least once: chain descriptors (80 B), their two coarse-
-    # index entries (8 B), slice ids (4 B / slice), the candidate words in the
-    # union of the chain windows (POS 4 + VtHot 16 + record 4 = 24 B, each
-    # candidate once however many overlapping requests read it), QRes rows
-    # (32 B / slice) and hits (8 B).  Beside it the SURVEY §8d contract figure:
+    # Roofline of chain_pack_kernel, priced on the bytes one launch must move
+    # at least once: chain descriptors (80 B), their two
+    # coarse-index entries (8 B), the request-row partial (40 B), the
+    # candidate words in the union of the chain windows (POS 4 + VtHot 16 +
+    # record 4 = 24 B, each candidate once however many overlapping requests
+    # read it) and hits (8 B).  Beside it the SURVEY §8d contract figure:
     # 32 B x unique records in the slice windows + 8 B / hit.
     chains, cslices = st['chains'], st['chained_slices']
-    comp = 80.0 * chains + 8.0 * chains + 4.0 * cslices + 24.0 * st['cand_unique'] + 32.0 * cslices + 8.0 * nhits
+    comp = 80.0 * chains + 8.0 * chains + 40.0 * chains + 24.0 * st['cand_unique'] + 8.0 * nhits
     achieved = comp / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     uniq = union_rows(shape, sl)
     contract = 32.0 * uniq + 8.0 * nhits
@@ -173,8 +179,9 @@ def main_genome(args):
                    'parallelism': f'contig shards x{world} (+10 kb halo); request rows + hit lists delivered to '
                                   f'the {"first slice" if args.deliver == "first" else "rank 0"} rank over '
                                   f'{"RCCL" if world > 1 else "(no peer)"}'},
-        'step': 'chain_kernel + request_reduce + dense hit lists (scan, gather) + exchange (all_gather of counts, '
-                'send/recv of straddling rows and hits)',
+        'step': 'chain_pack_kernel (request-row partials + dense chain hits; per-slice rows off) + request rows '
+                '+ dense hit lists (scan, gather) + exchange (all_gather of counts, send/recv of straddling rows and '
+                'hits)',
         'records_scanned_per_s': round(tot_scanned * args.steps / elapsed, 1),
         'hits_per_step': int(tot_hits),
         'device_ms_per_step': {'step_rank0': round(r0[9], 4), 'chain_kernel_rank0': round(r0[1], 4),
@@ -183,9 +190,9 @@ def main_genome(args):
                      'frac': round(r0[5] / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'kernel': 'chain_kernel (rank 0), HIP events around K back-to-back launches on its stream',
                      'algorithmic_bytes_per_launch': r0[7],
-                     'pricing': 'bytes one launch must move at least once: 88 B/chain (descriptor + 2 index '
-                                'entries) + 36 B/slice (slice id + QRes) + 24 B per candidate in the union of the '
-                                'chain windows + 8 B/hit',
+                     'pricing': 'bytes one launch must move at least once: 128 B/chain (80 B descriptor + 2 '
+                                'index entries + 40 B request-row partial) + 24 B per candidate in the union of the '
+                                'chain windows + 8 B/hit (the step keeps request rows, not per-slice rows)',
                      'candidates': {'unique': int(st['cand_unique']), 'in_windows': int(st['cand_window']),
                                     'loaded': int(st['cand_loaded'])},
                      'contract_bytes_per_launch': r0[8],

@@ -370,6 +370,13 @@ int sb_batch_reduce_requests(sb_batch *b, void *dev_out);
  * the same multiset; the route treats it as a set (route_g_variants.py:160).
  * Device pointers on the batch's device; dev_hits must hold
  * sb_batch_get_stats().hits (the planned capacity) entries. */
+/* Per-slice QRes rows of chained slices on (default) or off.  Off: a run
+ * leaves only what the request rows and their hit lists need (per-chain
+ * partials and dense chain hits; sb_batch_reduce_requests /
+ * sb_batch_compact_hits), which requires every chain to lie in one request
+ * row (sb_batch_set_owners); sb_batch_fetch then refuses until a run with
+ * them on.  Not between a run and its sync. */
+int sb_batch_set_slice_results(sb_batch *b, int on);
 int sb_batch_compact_hits(sb_batch *b, const void *dev_rows, void *dev_hits, void *dev_row_off, uint64_t rec_base);
 /* Enqueue this batch's work (run, reduce, compact, and the timing events) on
  * `stream` -- a hipStream_t of the store's device, e.g. the caller's current

@@ -195,6 +195,10 @@ struct sb_batch {
     DevMem chains;
     std::vector<uint32_t> hruns;  // first chain of each chain_pack_kernel wave (+ end)
     DevMem runs;
+    // chained slices also write their per-slice QRes rows (sb_batch_set_slice_results);
+    // off = request rows + hit lists only (row pieces), fetch refused
+    bool slice_rows = true;
+    bool slice_rows_stale = false;  // a run without them since the last run with them
     std::vector<uint8_t> chained;
     std::vector<uint32_t> nscan;
     std::vector<uint32_t> chain_members;  // chained queries, chain by chain (device copy: corig)
@@ -1122,8 +1126,9 @@ void run(sb_batch &B) {
     if (B.runs_pending++ == 0) HIP_OK(hipEventRecord(B.ev[0], st));
     // chains of variantType slices (one wave per request's slices)
     launch_chains(d, B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()), B.runs.as<uint32_t>(),
-                  static_cast<uint32_t>(B.hruns.size() - 1), B.corig.as<uint32_t>(), B.res.as<QRes>(),
-                  B.hits.as<uint64_t>(), B.cpart.as<ReqPartial>(), st);
+                  static_cast<uint32_t>(B.hruns.size() - 1), B.corig.as<uint32_t>(),
+                  B.slice_rows ? B.res.as<QRes>() : nullptr, B.hits.as<uint64_t>(), B.cpart.as<ReqPartial>(), st);
+    B.slice_rows_stale = !B.slice_rows && !B.hchains.empty();
     // sample-free groups: one fused launch, long scans first (range, variantType,
     // general) and point lookups last, so the short waves fill the tail
     std::vector<FusedGroup> fg;
@@ -1169,6 +1174,8 @@ const uint64_t *src_offsets(sb_batch &B, hipStream_t st) {
 }
 
 sb_result_set *fetch(sb_batch &B) {
+    if (B.slice_rows_stale)
+        throw Error(SB_EINVAL, "the last run skipped per-slice results (sb_batch_set_slice_results): enable them and run");
     sync(B);
     sb_store &s = *B.s;
     hipStream_t st = B.strm();
@@ -2276,6 +2283,18 @@ int sb_batch_set_stream(sb_batch *b, void *stream) {
         std::lock_guard<std::mutex> lk(b->s->mu);
         if (b->runs_pending) throw Error(SB_EINVAL, "sb_batch_set_stream between a run and its sync");
         b->stream = static_cast<hipStream_t>(stream);
+    });
+}
+
+int sb_batch_set_slice_results(sb_batch *b, int on) {
+    return guard([&] {
+        if (!b) throw Error(SB_EINVAL, "NULL batch");
+        std::lock_guard<std::mutex> lk(b->s->mu);
+        if (b->runs_pending) throw Error(SB_EINVAL, "sb_batch_set_slice_results between a run and its sync");
+        if (!on && !b->hchains.empty() && !b->row_pieces)
+            throw Error(SB_EINVAL, "per-slice results are needed unless every chain lies in one request row "
+                                   "(sb_batch_set_owners)");
+        b->slice_rows = on != 0;
     });
 }
 

@@ -1565,7 +1565,7 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
                                                             const uint32_t *__restrict__ runs, uint32_t n_runs,
                                                             const uint32_t *__restrict__ corig,
                                                             QRes *__restrict__ res, uint64_t *__restrict__ hits,
-                                                            ReqPartial *__restrict__ cpart) {
+                                                            ReqPartial *__restrict__ cpart, uint32_t dbg) {
     __shared__ PackLds lds_all[kWavesPerBlock];
     const uint32_t w = launch_wave();
     if (w >= n_runs) return;
@@ -1626,16 +1626,18 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
             L.lut[t] = st.sym_lut[L.desc[5 * kl + 4].y + (t & 7u)];
         }
     }
-    uint32_t orig[kPackSlots / kWave];  // slot ul + 64 t
+    uint32_t orig[kPackSlots / kWave];  // slot ul + 64 t (res == nullptr: request rows only, no per-slice QRes)
 #pragma unroll
     for (uint32_t t = 0; t < kPackSlots / kWave; ++t) {
         orig[t] = 0;
         if (kWave * t < S) {
             const uint32_t slot = min(ul + kWave * t, S - 1);
-            const uint32_t k = last_le(sex, R, slot);
-            const uint32_t sk = __shfl(sex, static_cast<int>(k), kWave);  // every lane active
+            if (res) {
+                const uint32_t k = last_le(sex, R, slot);
+                const uint32_t sk = __shfl(sex, static_cast<int>(k), kWave);  // every lane active
+                if (ul + kWave * t < S) orig[t] = corig[L.desc[5 * k].x + (slot - sk)];
+            }
             if (ul + kWave * t < S) {
-                orig[t] = corig[L.desc[5 * k].x + (slot - sk)];
                 L.cc[slot] = 0;
                 L.an[slot] = 0;
                 L.nh[slot] = 0;
@@ -1739,13 +1741,17 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
         }
     };
     // every chunk of the run issued before the first is evaluated
-    PackChunk buf[kPackAhead];
+    // (dbg: timing ablations of SBEACON_PACK_DBG; 0 in production)
+    if (!(dbg & 1u)) {
+        PackChunk buf[kPackAhead];
 #pragma unroll
-    for (int a = 0; a < kPackAhead; ++a) buf[a] = load(64u * a);
+        for (int a = 0; a < kPackAhead; ++a) buf[a] = load(64u * a);
 #pragma unroll
-    for (int a = 0; a < kPackAhead; ++a)
-        if (64u * a < T) eval(buf[a], 64u * a);
-    for (uint32_t base = 64u * kPackAhead; base < T; base += 64u) eval(load(base), base);  // long runs
+        for (int a = 0; a < kPackAhead; ++a)
+            if (64u * a < T) eval(buf[a], 64u * a);
+        for (uint32_t base = 64u * kPackAhead; base < T; base += 64u) eval(load(base), base);  // long runs
+    }
+    if (dbg & 2u) return;
     wave_lds_sync();
     // results: lane ul + 64 t = slot; chain totals by slot atomics
     uint64_t exm_all[kPackSlots / kWave];
@@ -1760,7 +1766,7 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
             const int64_t an = sl ? static_cast<int64_t>(L.an[slot]) : 0;
             const uint32_t nh = sl ? L.nh[slot] : 0u;
             exm_all[t] = __ballot(sl && cc > 0);
-            if (sl) {
+            if (sl && res) {
                 QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host
                 if (L.slow[k]) {
                     o.error = SB_QERR_UNSUPPORTED;
@@ -1771,10 +1777,10 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
                     o.n_hits = nh;
                 }
                 res[orig[t]] = o;
-                if (cpart) {
-                    atomicAdd(&L.tcc[k], static_cast<unsigned long long>(cc));
-                    atomicAdd(&L.tan[k], static_cast<unsigned long long>(an));
-                }
+            }
+            if (sl && cpart && (cc | an)) {
+                atomicAdd(&L.tcc[k], static_cast<unsigned long long>(cc));
+                atomicAdd(&L.tan[k], static_cast<unsigned long long>(an));
             }
         }
     }
@@ -2302,8 +2308,9 @@ void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, 
     if (!n_chains) return;
     const char *kern = std::getenv("SBEACON_CHAIN_KERNEL");  // "seq": the chain-sequential kernel
     if (!(kern && kern[0] == 's')) {
+        const char *dbg = std::getenv("SBEACON_PACK_DBG");
         hipLaunchKernelGGL(chain_pack_kernel, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs, n_runs,
-                           corig, res, hits, cpart);
+                           corig, res, hits, cpart, dbg ? static_cast<uint32_t>(std::atoi(dbg)) : 0u);
         return;
     }
     // runs of kChainRun chains per wave while the launch still fills the chip

@@ -408,6 +408,12 @@ class Batch:
         ``torch.cuda.current_stream().cuda_stream``); None = the store's."""
         check(lib().sb_batch_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def set_slice_results(self, on: bool):
+        """Per-slice results of chained slices on (default) / off: off keeps
+        only the request rows and hit lists (needs set_owners with every
+        chain in one row); fetch() then needs a run with them on."""
+        check(lib().sb_batch_set_slice_results(self._h, 1 if on else 0))
+
     def stats(self) -> dict:
         """Planning statistics (hits = the planned hit capacity)."""
         s = BatchStats()

@@ -34,9 +34,11 @@ def main():
         elif setting.startswith('seq'):  # chain-sequential kernel
             env['SBEACON_CHAIN_RUN'] = setting[3:]
             env['SBEACON_CHAIN_KERNEL'] = 'seq'
+        elif setting.startswith('dbg'):  # packed kernel timing ablation (results invalid)
+            env['SBEACON_PACK_DBG'] = setting[3:]
         elif setting == 'nochain':
             env['SBEACON_NO_CHAINS'] = '1'
-        for k in ('SBEACON_CHAIN_RUN', 'SBEACON_NO_CHAINS', 'SBEACON_CHAIN_KERNEL'):
+        for k in ('SBEACON_CHAIN_RUN', 'SBEACON_NO_CHAINS', 'SBEACON_CHAIN_KERNEL', 'SBEACON_PACK_DBG'):
             os.environ.pop(k, None)
         os.environ.update(env)
         t1 = time.perf_counter()
