@@ -2047,6 +2047,68 @@ __global__ __launch_bounds__(kBlock) void row_gather_kernel(const uint32_t *__re
     }
 }
 
+// The same copy, one wave per 64 consecutive rows: their outputs are one
+// contiguous range [row_off[r0], row_off[r0 + 64]) of the dense list, so
+// lane j of each pass writes output base + j (coalesced) and finds its row
+// by a binary search over the lanes' row starts.  Rows of one piece (or
+// none) read their hits from rowsrc.x; rows of several pieces (rowsrc.x =
+// ~0) are copied afterwards by their own lane, piece by piece.
+__global__ __launch_bounds__(kBlock) void row_gather_seg_kernel(const uint32_t *__restrict__ poff,
+                                                                const uint32_t *__restrict__ piece, uint32_t n_rows,
+                                                                const ChainDev *__restrict__ chains,
+                                                                const ReqPartial *__restrict__ cpart,
+                                                                const QRes *__restrict__ res,
+                                                                const uint64_t *__restrict__ hoff,
+                                                                const uint64_t *__restrict__ hits, uint64_t rec_base,
+                                                                const uint64_t *__restrict__ row_off,
+                                                                const ulonglong2 *__restrict__ rowsrc,
+                                                                uint64_t *__restrict__ out) {
+    const uint32_t r0 = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kWave;
+    if (r0 >= n_rows) return;
+    const uint32_t ul = static_cast<uint32_t>(lane_id());
+    const uint32_t r = min(r0 + ul, n_rows - 1);
+    const bool live = r0 + ul < n_rows;
+    const uint64_t base = row_off[r0];
+    const uint64_t end = row_off[min(r0 + kWave, n_rows)];
+    const uint64_t my0 = row_off[r];
+    const ulonglong2 rs = live ? rowsrc[r] : ulonglong2{0ull, 0ull};
+    const uint32_t e = static_cast<uint32_t>(live ? my0 - base : end - base);  // row start within the range
+    const bool single = live && rs.x != ~0ull;
+    const uint64_t total = end - base;
+    for (uint64_t j0 = 0; j0 < total; j0 += kWave) {
+        const uint32_t j = static_cast<uint32_t>(j0) + ul;
+        // last lane l with e_l <= j (e is nondecreasing over the lanes)
+        uint32_t l = 0;
+#pragma unroll
+        for (uint32_t step = kWave / 2; step >= 1; step >>= 1) {
+            const uint32_t t = l + step;
+            const uint32_t et = static_cast<uint32_t>(__shfl(static_cast<int>(e), static_cast<int>(t), kWave));
+            if (et <= j) l = t;
+        }
+        const uint32_t el = static_cast<uint32_t>(__shfl(static_cast<int>(e), static_cast<int>(l), kWave));
+        const uint64_t src = static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(rs.x), static_cast<int>(l)));
+        const bool sl = __shfl(static_cast<int>(single), static_cast<int>(l), kWave) != 0;
+        if (j < total && sl) out[base + j] = hits[src + (j - el)] + rec_base;
+    }
+    if (live && !single) {  // several pieces: this lane copies its row
+        uint64_t d = my0;
+        for (uint32_t k = poff[r], ke = poff[r + 1]; k < ke; ++k) {
+            const uint32_t p = piece[k];
+            uint64_t a, n;
+            if (p & kPieceChain) {
+                const uint32_t c = p & ~kPieceChain;
+                a = chains[c].out;
+                n = static_cast<uint64_t>(cpart[c].n_variants);
+            } else {
+                a = hoff[p];
+                n = hit_count(res[p]);
+            }
+            for (uint64_t jj = 0; jj < n; ++jj) out[d + jj] = hits[a + jj] + rec_base;
+            d += n;
+        }
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void compact_kernel(const uint64_t *__restrict__ hit_off,
                                                          const uint64_t *__restrict__ dense_off,
                                                          const QRes *__restrict__ res, uint32_t nq,
@@ -2378,9 +2440,15 @@ void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, cons
         return;
     }
     hipLaunchKernelGGL(field_tile_scan_kernel, dim3(nt), dim3(kBlock), 0, s, nv, stride, n_rows, tsum, row_off);
-    const uint64_t threads = static_cast<uint64_t>(n_rows) * kGatherTeam;
-    hipLaunchKernelGGL(row_gather_kernel, dim3(static_cast<uint32_t>((threads + kBlock - 1) / kBlock)), dim3(kBlock), 0,
-                       s, poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
+    const char *g = std::getenv("SBEACON_ROW_GATHER");  // "team": 8 lanes per row
+    if (g && g[0] == 't') {
+        const uint64_t threads = static_cast<uint64_t>(n_rows) * kGatherTeam;
+        hipLaunchKernelGGL(row_gather_kernel, dim3(static_cast<uint32_t>((threads + kBlock - 1) / kBlock)), dim3(kBlock),
+                           0, s, poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
+    } else {
+        hipLaunchKernelGGL(row_gather_seg_kernel, dim3(blocks_for((n_rows + kWave - 1) / kWave)), dim3(kBlock), 0, s,
+                           poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
+    }
 }
 
 void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, uint32_t n_rows,

@@ -43,6 +43,8 @@ def main():
         os.environ.update(env)
         t1 = time.perf_counter()
         batch = prepare_shard_batch(store, sl)
+        if os.environ.get('ROWS_ONLY', '1') == '1':
+            batch.set_slice_results(False)
         tp = time.perf_counter() - t1
         batch.run()
         batch.sync()
@@ -61,6 +63,9 @@ def main():
             base = rows
         else:
             same = bool((rows == base).all())
+        batch.set_slice_results(True)
+        batch.run()
+        batch.sync()
         st = batch.fetch().stats()
         print(json.dumps({'setting': setting, 'run_ms': round(run_ms, 4), 'run_plus_reduce_ms': round(step_ms, 4),
                           'prepare_s': round(tp, 2), 'chained_slices': st['chained_slices'], 'hits': st['hits'],
