@@ -91,8 +91,7 @@ def main_genome(args):
 
     def step():  # answer + deliver: chain kernel, request rows, dense hit lists, exchange
         batch.run()
-        batch.reduce_requests(part.data_ptr())
-        batch.compact_hits(hits.data_ptr(), row_off.data_ptr(), base, rows_ptr=part.data_ptr())
+        batch.deliver(part.data_ptr(), hits.data_ptr(), row_off.data_ptr(), base)  # request rows + hit lists
         ex.exchange(part, hits, row_off)
 
     for _ in range(args.warmup):

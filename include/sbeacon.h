@@ -370,6 +370,10 @@ int sb_batch_reduce_requests(sb_batch *b, void *dev_out);
  * the same multiset; the route treats it as a set (route_g_variants.py:160).
  * Device pointers on the batch's device; dev_hits must hold
  * sb_batch_get_stats().hits (the planned capacity) entries. */
+/* sb_batch_reduce_requests + sb_batch_compact_hits(rows = dev_rows) in one
+ * call: with every chain in one request row the reduction also leaves each
+ * row's n_variants densely, so the offset scan reads 8 B per row. */
+int sb_batch_deliver(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_off, uint64_t rec_base);
 /* Per-slice QRes rows of chained slices on (default) or off.  Off: a run
  * leaves only what the request rows and their hit lists need (per-chain
  * partials and dense chain hits; sb_batch_reduce_requests /

@@ -211,6 +211,7 @@ struct sb_batch {
     // request rows as pieces (sb_batch_set_owners, when every chain lies in one row)
     bool row_pieces = false;
     DevMem poff, piece, rows_scratch, rowsrc;
+    DevMem nvs;  // sb_batch_deliver: each row's n_variants (8 B / row) for the offset scan
     uint64_t cand_loaded = 0, cand_window = 0, cand_unique = 0;  // chain candidate statistics
     hipStream_t stream = nullptr;  // sb_batch_set_stream (nullptr: the store's stream)
     hipStream_t strm() const { return stream ? stream : s->stream; }
@@ -2275,6 +2276,28 @@ int sb_batch_reduce_requests(sb_batch *b, void *dev_out) {
                                   static_cast<ReqPartial *>(dev_out), b->strm());
         HIP_OK(hipGetLastError());
     });
+}
+
+int sb_batch_deliver(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_off, uint64_t rec_base) {
+    if (b && b->row_pieces) {
+        return guard([&] {
+            if ((!dev_rows && b->n_rows) || (!dev_hits && b->cap_total) || !dev_row_off)
+                throw Error(SB_EINVAL, "NULL argument");
+            std::lock_guard<std::mutex> lk(b->s->mu);
+            HIP_OK(hipSetDevice(b->s->device));
+            b->tsum.reserve(hit_scan_words(b->n_rows) * 8);
+            b->nvs.reserve(std::max<size_t>(b->n_rows, 1) * 8);
+            launch_row_deliver(b->cpart.as<ReqPartial>(), b->chains.as<ChainDev>(), b->hoff.as<uint64_t>(),
+                               b->res.as<QRes>(), b->herr.as<uint8_t>(), b->poff.as<uint32_t>(),
+                               b->piece.as<uint32_t>(), b->n_rows, static_cast<ReqPartial *>(dev_rows),
+                               b->rowsrc.as<ulonglong2>(), b->nvs.as<int64_t>(), b->tsum.as<uint64_t>(),
+                               b->hits.as<uint64_t>(), rec_base, static_cast<uint64_t *>(dev_row_off),
+                               static_cast<uint64_t *>(dev_hits), b->strm());
+            HIP_OK(hipGetLastError());
+        });
+    }
+    const int rc = sb_batch_reduce_requests(b, dev_rows);
+    return rc != SB_OK ? rc : sb_batch_compact_hits(b, dev_rows, dev_hits, dev_row_off, rec_base);
 }
 
 int sb_batch_set_stream(sb_batch *b, void *stream) {

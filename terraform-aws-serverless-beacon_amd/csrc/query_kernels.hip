@@ -1921,16 +1921,13 @@ constexpr uint32_t kPieceChain = 1u << 31;
 
 // rowsrc[w] = {hit region, count} of a single-piece row ({~0, 0} otherwise):
 // the gather then needs no piece lookups for it
-__global__ __launch_bounds__(kBlock) void row_reduce_kernel(const ReqPartial *__restrict__ cpart,
-                                                            const ChainDev *__restrict__ chains,
-                                                            const uint64_t *__restrict__ hoff,
-                                                            const QRes *__restrict__ res,
-                                                            const uint8_t *__restrict__ host_err,
-                                                            const uint32_t *__restrict__ poff,
-                                                            const uint32_t *__restrict__ piece, uint32_t n_rows,
-                                                            ReqPartial *__restrict__ out, ulonglong2 *__restrict__ rowsrc) {
-    const uint32_t w = blockIdx.x * kBlock + threadIdx.x;
-    if (w >= n_rows) return;
+// one request row from its pieces (chains: their partial; slices: their QRes)
+__device__ __forceinline__ ReqPartial reduce_row(uint32_t w, const ReqPartial *__restrict__ cpart,
+                                                 const ChainDev *__restrict__ chains,
+                                                 const uint64_t *__restrict__ hoff, const QRes *__restrict__ res,
+                                                 const uint8_t *__restrict__ host_err,
+                                                 const uint32_t *__restrict__ poff,
+                                                 const uint32_t *__restrict__ piece, ulonglong2 *__restrict__ rowsrc) {
     ReqPartial P{0, 0, 0, 0, 0};
     const uint32_t k0 = poff[w], k1 = poff[w + 1];
     if (rowsrc) {
@@ -1970,7 +1967,49 @@ __global__ __launch_bounds__(kBlock) void row_reduce_kernel(const ReqPartial *__
             P.all_alleles_count += r.all_alleles_count;
         }
     }
-    out[w] = P;
+    return P;
+}
+
+__global__ __launch_bounds__(kBlock) void row_reduce_kernel(const ReqPartial *__restrict__ cpart,
+                                                            const ChainDev *__restrict__ chains,
+                                                            const uint64_t *__restrict__ hoff,
+                                                            const QRes *__restrict__ res,
+                                                            const uint8_t *__restrict__ host_err,
+                                                            const uint32_t *__restrict__ poff,
+                                                            const uint32_t *__restrict__ piece, uint32_t n_rows,
+                                                            ReqPartial *__restrict__ out, ulonglong2 *__restrict__ rowsrc) {
+    const uint32_t w = blockIdx.x * kBlock + threadIdx.x;
+    if (w >= n_rows) return;
+    out[w] = reduce_row(w, cpart, chains, hoff, res, host_err, poff, piece, rowsrc);
+}
+
+// sb_batch_deliver: the rows as above plus, for the hit-list offsets, each
+// row's n_variants in a dense array and the per-tile sums of it (one tile =
+// kScanTile rows = this block's rows), so the offset scan reads 8 B / row
+__global__ __launch_bounds__(kBlock) void row_reduce_tiles_kernel(const ReqPartial *__restrict__ cpart,
+                                                                  const ChainDev *__restrict__ chains,
+                                                                  const uint64_t *__restrict__ hoff,
+                                                                  const QRes *__restrict__ res,
+                                                                  const uint8_t *__restrict__ host_err,
+                                                                  const uint32_t *__restrict__ poff,
+                                                                  const uint32_t *__restrict__ piece, uint32_t n_rows,
+                                                                  ReqPartial *__restrict__ out,
+                                                                  ulonglong2 *__restrict__ rowsrc,
+                                                                  int64_t *__restrict__ nv, uint64_t *__restrict__ tsum) {
+    __shared__ uint64_t wsum[kWavesPerBlock];
+    uint64_t x = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        const uint32_t w = blockIdx.x * kScanTile + k * kBlock + threadIdx.x;  // coalesced per k
+        if (w < n_rows) {
+            const ReqPartial P = reduce_row(w, cpart, chains, hoff, res, host_err, poff, piece, rowsrc);
+            out[w] = P;
+            nv[w] = P.n_variants;
+            x += static_cast<uint64_t>(P.n_variants);
+        }
+    }
+    const uint64_t t = block_incl_scan(x, wsum);
+    if (threadIdx.x == kBlock - 1) tsum[blockIdx.x] = t;
 }
 
 // tile sums / tile scans of one int64 field of a strided array (ReqPartial rows)
@@ -2424,6 +2463,23 @@ void launch_row_reduce(const ReqPartial *cpart, const ChainDev *chains, const ui
     if (!n_rows) return;
     hipLaunchKernelGGL(row_reduce_kernel, dim3((n_rows + kBlock - 1) / kBlock), dim3(kBlock), 0, s, cpart, chains,
                        hoff, res, host_err, poff, piece, n_rows, out, rowsrc);
+}
+
+void launch_row_deliver(const ReqPartial *cpart, const ChainDev *chains, const uint64_t *hoff, const QRes *res,
+                        const uint8_t *host_err, const uint32_t *poff, const uint32_t *piece, uint32_t n_rows,
+                        ReqPartial *rows, ulonglong2 *rowsrc, int64_t *nv, uint64_t *tsum, const uint64_t *hits,
+                        uint64_t rec_base, uint64_t *row_off, uint64_t *out, hipStream_t s) {
+    const uint32_t nt = (n_rows + kScanTile - 1) / kScanTile;
+    if (!nt) {
+        (void)hipMemsetAsync(row_off, 0, 8, s);
+        return;
+    }
+    hipLaunchKernelGGL(row_reduce_tiles_kernel, dim3(nt), dim3(kBlock), 0, s, cpart, chains, hoff, res, host_err, poff,
+                       piece, n_rows, rows, rowsrc, nv, tsum);
+    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kBlock), 0, s, tsum, nt);
+    hipLaunchKernelGGL(field_tile_scan_kernel, dim3(nt), dim3(kBlock), 0, s, nv, 1u, n_rows, tsum, row_off);
+    hipLaunchKernelGGL(row_gather_seg_kernel, dim3(blocks_for((n_rows + kWave - 1) / kWave)), dim3(kBlock), 0, s, poff,
+                       piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
 }
 
 void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, const uint32_t *poff,

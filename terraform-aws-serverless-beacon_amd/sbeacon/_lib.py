@@ -130,6 +130,7 @@ SIGNATURES = {
     'sb_batch_compact_hits': (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     'sb_batch_set_stream': (C.c_int, [P, C.c_void_p]),
     'sb_batch_set_slice_results': (C.c_int, [P, C.c_int]),
+    'sb_batch_deliver': (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     'sb_summarise_slices': (C.c_int, [P, C.POINTER(Slice), C.c_size_t, C.POINTER(SliceStats),
                                       C.POINTER(C.c_double)]),
     'sb_slice_region_files': (C.c_int, [P, C.POINTER(Slice), C.c_size_t, C.c_int, C.POINTER(C.c_int32),

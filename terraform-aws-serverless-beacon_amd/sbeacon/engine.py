@@ -408,6 +408,12 @@ class Batch:
         ``torch.cuda.current_stream().cuda_stream``); None = the store's."""
         check(lib().sb_batch_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def deliver(self, rows_ptr, hits_ptr, row_off_ptr, rec_base=0):
+        """reduce_requests(rows_ptr) + compact_hits(hits_ptr, row_off_ptr,
+        rec_base, rows_ptr) in one call (sb_batch_deliver)."""
+        check(lib().sb_batch_deliver(self._h, C.c_void_p(rows_ptr), C.c_void_p(hits_ptr), C.c_void_p(row_off_ptr),
+                                     int(rec_base)))
+
     def set_slice_results(self, on: bool):
         """Per-slice results of chained slices on (default) / off: off keeps
         only the request rows and hit lists (needs set_owners with every

@@ -77,9 +77,10 @@ def test_shards_match_oracle_and_unsharded(genome, monkeypatch, spw):
 
 @pytest.mark.parametrize('chains', ['1', '0'])
 def test_compact_hits_match_fetch(genome, monkeypatch, chains):
-    """sb_batch_compact_hits (device scan + gather, chain-dense regions) gives
-    each request row the concatenation of its slices' fetched hits, with the
-    shard's global record base added, on the caller's torch stream."""
+    """sb_batch_compact_hits (device scan + gather, chain-dense regions) and
+    the fused sb_batch_deliver give each request row the concatenation of its
+    slices' fetched hits, with the shard's global record base added, on the
+    caller's torch stream."""
     import torch
     if chains == '0':
         monkeypatch.setenv('SBEACON_NO_CHAINS', '1')
@@ -95,10 +96,16 @@ def test_compact_hits_match_fetch(genome, monkeypatch, chains):
     row_off = torch.zeros(sl.n_rows + 1, dtype=torch.int64, device='cuda:0')
     part = torch.zeros((sl.n_rows, 5), dtype=torch.int64, device='cuda:0')
     base = shard_record_base(shape, world, rank)
-    for k in range(2):  # with and without the reduced rows handed over
+    for k in range(3):  # without / with the reduced rows handed over, then the fused deliver
         b.run()
-        b.reduce_requests(part.data_ptr())
-        b.compact_hits(hits.data_ptr(), row_off.data_ptr(), base, rows_ptr=part.data_ptr() if k else 0)
+        if k < 2:
+            b.reduce_requests(part.data_ptr())
+            b.compact_hits(hits.data_ptr(), row_off.data_ptr(), base, rows_ptr=part.data_ptr() if k else 0)
+        else:
+            hits.fill_(-1)
+            row_off.zero_()
+            part.zero_()
+            b.deliver(part.data_ptr(), hits.data_ptr(), row_off.data_ptr(), base)
     b.sync()
     torch.cuda.synchronize()
     ro = row_off.cpu().numpy()
