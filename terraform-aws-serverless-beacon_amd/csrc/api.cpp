@@ -1541,11 +1541,11 @@ std::string key_string(const sb_store &s, uint32_t k) {
 
 // dedup scratch, kept per store (sb_store::dedup_ws) and grown on demand
 struct DedupWs {
-    DevMem dseg, dtiles, tcnt, ke0, ke1, kh0, vh0, kh1, vh1, hist, bsum, counts, coll, ncoll, pe, ph;
+    DevMem dseg, dtiles, tcnt, ke0, ke1, kh0, vh0, kh1, vh1, hist, bsum, counts, coll, ncoll, pe, ph, overflow;
 };
 
 void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique, int32_t *status,
-               sb_dedup_stats *stats);
+               sb_dedup_stats *stats, bool force_radix = false);
 
 void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, int32_t *status,
            sb_dedup_stats *stats) {
@@ -1595,7 +1595,7 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
 // the device part of duplicateVariantSearch over planned key runs: gather,
 // radix sort, adjacent-unique (+ host recount of 64-bit word collisions)
 void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique, int32_t *status,
-               sb_dedup_stats *stats) {
+               sb_dedup_stats *stats, bool force_radix) {
     if (n >= 0xffffffffull) throw Error(SB_EINVAL, "dedup batch exceeds 2^32 keys; split it");
     uint32_t job_bits = 0;
     while ((1ull << job_bits) < nj) ++job_bits;
@@ -1659,16 +1659,29 @@ void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj
         nh += htc[ntiles + t];
     }
     if (ne + nh != n) throw Error(SB_EHIP, "dedup gather lost keys");
-    const uint32_t be = dedup_unique_blocks(ne), bh = dedup_unique_blocks(nh);
+    // exact stream: hash buckets (two radix passes on a mix of the word +
+    // an LDS hash set per workgroup; SBEACON_DEDUP_EXACT=radix forces the
+    // full sort) or as many 8-bit radix passes as its words have bits + an
+    // adjacent-unique pass; the first pass compacts the gather tiles
+    const char *exm = std::getenv("SBEACON_DEDUP_EXACT");
+    const bool bucket = !force_radix && !(exm && exm[0] == 'r') && ne > 0;
+    const uint32_t be = bucket ? 0u : dedup_unique_blocks(ne), bh = dedup_unique_blocks(nh);
     pe.reserve(std::max<uint32_t>(be, 1) * sizeof(uint4));
     ph.reserve(std::max<uint32_t>(bh, 1) * sizeof(uint4));
-    // exact stream: keys only, as many 8-bit passes as its words have bits;
-    // the first pass compacts the gather tiles
-    const int re = launch_radix_sort(ke0.as<uint64_t>(), nullptr, ke1.as<uint64_t>(), nullptr, ne,
-                                     job_bits + pos_bits + 6, hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
-                                     tcnt.as<uint32_t>(), ntiles);
-    launch_dedup_unique(re ? ke1.as<uint64_t>() : ke0.as<uint64_t>(), nullptr, ne, s.dk, exact_job_shift, false,
-                        counts.as<unsigned long long>(), pe.as<uint4>(), coll.as<uint32_t>(), ncoll.as<uint32_t>(), st);
+    W.overflow.reserve(4);
+    HIP_OK(hipMemsetAsync(W.overflow.p, 0, 4, st));
+    if (bucket) {
+        launch_bucket_dedupe(ke0.as<uint64_t>(), ke1.as<uint64_t>(), ne, exact_job_shift, static_cast<uint32_t>(nj),
+                             counts.as<unsigned long long>(), W.overflow.as<uint32_t>(), hist.as<uint32_t>(),
+                             bsum.as<uint32_t>(), st, tcnt.as<uint32_t>(), ntiles);
+    } else {
+        const int re = launch_radix_sort(ke0.as<uint64_t>(), nullptr, ke1.as<uint64_t>(), nullptr, ne,
+                                         job_bits + pos_bits + 6, hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
+                                         tcnt.as<uint32_t>(), ntiles);
+        launch_dedup_unique(re ? ke1.as<uint64_t>() : ke0.as<uint64_t>(), nullptr, ne, s.dk, exact_job_shift, false,
+                            counts.as<unsigned long long>(), pe.as<uint4>(), coll.as<uint32_t>(), ncoll.as<uint32_t>(),
+                            st);
+    }
     // hashed stream: (job | hash, key id), 8 passes, equal words confirmed
     const int rh = launch_radix_sort(kh0.as<uint64_t>(), vh0.as<uint32_t>(), kh1.as<uint64_t>(), vh1.as<uint32_t>(),
                                      nh, 64, hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
@@ -1680,9 +1693,10 @@ void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipGetLastError());
     std::vector<uint64_t> cnt(std::max<size_t>(nj, 1));
-    uint32_t nc = 0;
+    uint32_t nc = 0, ovf = 0;
     HIP_OK(hipMemcpyAsync(cnt.data(), counts.p, cnt.size() * 8, hipMemcpyDeviceToHost, st));
     HIP_OK(hipMemcpyAsync(&nc, ncoll.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(&ovf, W.overflow.p, 4, hipMemcpyDeviceToHost, st));
     std::vector<uint4> hpe(be), hph(bh);
     if (be) HIP_OK(hipMemcpyAsync(hpe.data(), pe.p, be * sizeof(uint4), hipMemcpyDeviceToHost, st));
     if (bh) HIP_OK(hipMemcpyAsync(hph.data(), ph.p, bh * sizeof(uint4), hipMemcpyDeviceToHost, st));
@@ -1696,6 +1710,10 @@ void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    if (ovf) {  // a workgroup's buckets outgrew its hash set: recount with the full sort
+        dedup_run(s, segs, n, nj, unique, status, stats, true);
+        return;
+    }
     if (nc) {
         // exact recount of every group holding a collision: the device counted
         // 1 + (adjacent string changes) for it; replace that by |distinct|

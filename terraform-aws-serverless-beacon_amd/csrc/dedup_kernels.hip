@@ -24,6 +24,9 @@
 // workgroups, one tile of 4096 keys each, coalesced 64-lane loads.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "kernels.hpp"
 
 namespace sb {
@@ -168,6 +171,22 @@ __global__ __launch_bounds__(kThreads) void gather_kernel(KStore ks, const KSeg 
 }
 
 // ------------------------------------------------------------- radix sort
+// splitmix64 finalizer: the bucket partition of the exact stream sorts on
+// bits of mix(word) (a bijection), so buckets are uniform whatever the words
+__device__ __forceinline__ uint64_t mix64(uint64_t x) {
+    x ^= x >> 30;
+    x *= 0xbf58476d1ce4e5b9ull;
+    x ^= x >> 27;
+    x *= 0x94d049bb133111ebull;
+    x ^= x >> 31;
+    return x;
+}
+
+template <bool MIX>
+__device__ __forceinline__ uint32_t digit_of(uint64_t k, uint32_t shift) {
+    return static_cast<uint32_t>((MIX ? mix64(k) : k) >> shift) & 255u;
+}
+
 // hist layout: digit-major, hist[d * ntiles + tile]
 // keys of tile b: dense (tile_n == nullptr) = [b * kTile, min(n, ..+kTile));
 // sparse (the first pass after gather) = the first tile_n[b] slots of tile b
@@ -177,6 +196,7 @@ __device__ __forceinline__ uint32_t tile_count(uint64_t n, const uint32_t *tile_
     return static_cast<uint32_t>(min(static_cast<uint64_t>(kTile), n - t0));
 }
 
+template <bool MIX>
 __global__ __launch_bounds__(kThreads) void upsweep_kernel(const uint64_t *keys, uint64_t n, const uint32_t *tile_n,
                                                            uint32_t shift, uint32_t *hist, uint32_t ntiles) {
     __shared__ uint32_t h[kWaves][256];
@@ -189,7 +209,7 @@ __global__ __launch_bounds__(kThreads) void upsweep_kernel(const uint64_t *keys,
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
         const uint32_t j = static_cast<uint32_t>(r) * kThreads + threadIdx.x;
-        dg[r] = j < tn ? static_cast<uint32_t>(keys[base + j] >> shift) & 255u : 256u;
+        dg[r] = j < tn ? digit_of<MIX>(keys[base + j], shift) : 256u;
     }
 #pragma unroll
     for (int r = 0; r < kItems; ++r)
@@ -222,7 +242,7 @@ __device__ __forceinline__ uint32_t block_exclusive(uint32_t x, uint32_t *lds, u
     return wofs + inc - x;
 }
 
-template <bool VALS>
+template <bool VALS, bool MIX>
 __global__ __launch_bounds__(kThreads) void downsweep_kernel(const uint64_t *kin, const uint32_t *vin,
                                                              uint64_t *kout, uint32_t *vout, uint64_t n,
                                                              const uint32_t *tile_n, uint32_t shift,
@@ -248,7 +268,7 @@ __global__ __launch_bounds__(kThreads) void downsweep_kernel(const uint64_t *kin
     for (int r = 0; r < kItems; ++r) {
         if (wbase + static_cast<uint32_t>(r) * 64 >= tn) break;  // wave-uniform: the rest of the wave's slots are empty
         const bool ok = wbase + static_cast<uint32_t>(r) * 64 + lane < tn;
-        const uint32_t d = static_cast<uint32_t>(k[r] >> shift) & 255u;
+        const uint32_t d = digit_of<MIX>(k[r], shift);
         uint64_t peers = __ballot(ok);
 #pragma unroll
         for (int b = 0; b < 8; ++b) {
@@ -289,7 +309,7 @@ __global__ __launch_bounds__(kThreads) void downsweep_kernel(const uint64_t *kin
 #pragma unroll
     for (int r = 0; r < kItems; ++r) {
         if (wbase + static_cast<uint32_t>(r) * 64 + lane < tn) {
-            const uint32_t d = static_cast<uint32_t>(k[r] >> shift) & 255u;
+            const uint32_t d = digit_of<MIX>(k[r], shift);
             const uint32_t loc = cnt[w][d] + rank[r];
             sk[loc] = k[r];
             if (VALS) sv[loc] = v[r];
@@ -301,7 +321,7 @@ __global__ __launch_bounds__(kThreads) void downsweep_kernel(const uint64_t *kin
         const uint32_t loc = static_cast<uint32_t>(r) * kThreads + threadIdx.x;
         if (loc < tn) {
             const uint64_t key = sk[loc];
-            const uint32_t dst = gbase[static_cast<uint32_t>(key >> shift) & 255u] + loc;
+            const uint32_t dst = gbase[digit_of<MIX>(key, shift)] + loc;
             kout[dst] = key;
             if (VALS) vout[dst] = sv[loc];
         }
@@ -477,6 +497,75 @@ __global__ __launch_bounds__(kThreads) void unique_kernel(const uint64_t *keys, 
     if (threadIdx.x == 0) part[blockIdx.x] = uint4{jf, s_cnt[0], jl, s_cnt[1]};
 }
 
+// ------------------------------------------------------------- bucket dedupe
+// The exact stream after two radix passes on the top 16 bits of mix(word):
+// equal words are in one bucket and buckets are contiguous.  Workgroup w owns
+// the buckets that start in [w * kBTile, (w + 1) * kBTile) and counts their
+// distinct words with an LDS hash set (one successful insert per distinct
+// word), adding each to its job.  A set that would overflow raises *overflow
+// (the host then takes the radix path).  8 B / key after the partition.
+constexpr uint32_t kBTile = 2048;          // keys per workgroup (nominal)
+constexpr uint32_t kBSlots = 8192;         // LDS hash set (64 KB)
+constexpr uint64_t kBEmpty = ~0ull;        // exact words never reach all ones (job | window | 6 bits < 64 bits)
+
+__device__ __forceinline__ uint32_t bucket_of(uint64_t k) { return static_cast<uint32_t>(mix64(k) >> 48); }
+
+// first index >= at whose bucket differs from its predecessor's (n if none)
+__device__ uint64_t bucket_start_at(const uint64_t *keys, uint64_t n, uint64_t at, uint32_t *lds) {
+    if (at == 0) return 0;
+    if (at >= n) return n;
+    const uint32_t prevb = bucket_of(keys[at - 1]);
+    // scan forward in block-wide windows until a boundary is seen
+    for (uint64_t w0 = at; w0 < n; w0 += kThreads) {
+        const uint64_t i = w0 + threadIdx.x;
+        const bool edge = i < n && bucket_of(keys[i]) != (i == at ? prevb : bucket_of(keys[i - 1]));
+        if (threadIdx.x == 0) lds[0] = 0xffffffffu;
+        __syncthreads();
+        if (edge) atomicMin(&lds[0], static_cast<uint32_t>(i - w0));
+        __syncthreads();
+        const uint32_t f = lds[0];
+        __syncthreads();
+        if (f != 0xffffffffu) return w0 + f;
+    }
+    return n;
+}
+
+__global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t *keys, uint64_t n, uint32_t job_shift,
+                                                                 uint32_t nj_lds, unsigned long long *counts,
+                                                                 uint32_t *overflow, uint32_t cap) {
+    __shared__ unsigned long long set[kBSlots];
+    __shared__ unsigned int jc[256];
+    __shared__ uint32_t tmp[1];
+    for (uint32_t i = threadIdx.x; i < kBSlots; i += kThreads) set[i] = kBEmpty;
+    for (uint32_t i = threadIdx.x; i < 256; i += kThreads) jc[i] = 0;
+    const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kBTile;
+    const uint64_t s0 = bucket_start_at(keys, n, t0, tmp);
+    const uint64_t s1 = bucket_start_at(keys, n, t0 + kBTile, tmp);
+    __syncthreads();
+    if (s1 > s0 && s1 - s0 > cap) {  // cannot hold them: radix path
+        if (threadIdx.x == 0) atomicOr(overflow, 1u);
+        return;
+    }
+    for (uint64_t i = s0 + threadIdx.x; i < s1; i += kThreads) {
+        const uint64_t k = keys[i];
+        uint32_t h = static_cast<uint32_t>(mix64(k ^ 0x9e3779b97f4a7c15ull)) & (kBSlots - 1);
+        for (uint32_t probe = 0; probe < kBSlots; ++probe) {
+            const unsigned long long was = atomicCAS(&set[h], kBEmpty, static_cast<unsigned long long>(k));
+            if (was == kBEmpty) {  // first copy of this word: a distinct key of its job
+                const uint32_t j = job_shift < 64 ? static_cast<uint32_t>(k >> job_shift) : 0u;
+                if (j < nj_lds) atomicAdd(&jc[j], 1u);
+                else atomicAdd(&counts[j], 1ull);
+                break;
+            }
+            if (was == k) break;
+            h = (h + 1) & (kBSlots - 1);
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nj_lds; j += kThreads)
+        if (jc[j]) atomicAdd(&counts[j], static_cast<unsigned long long>(jc[j]));
+}
+
 uint32_t tiles_of(uint64_t n) { return static_cast<uint32_t>((n + kTile - 1) / kTile); }
 
 void exclusive_scan(uint32_t *a, uint64_t m, uint32_t *bsum, hipStream_t s) {
@@ -501,26 +590,49 @@ void launch_dedup_gather(const KStore &ks, const KSeg *segs, const uint2 *tiles,
                                               kh, vh, tcnt);
 }
 
-int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t bits,
-                      uint32_t *hist, uint32_t *bsum, hipStream_t s, const uint32_t *tile_n, uint32_t sparse_tiles) {
-    if (n == 0) return 0;
-    if (n <= 1 && !tile_n) return 0;
+namespace {
+template <bool MIX>
+int radix_passes(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t shift0, uint32_t bits,
+                 uint32_t *hist, uint32_t *bsum, hipStream_t s, const uint32_t *tile_n, uint32_t sparse_tiles) {
     uint64_t *kin = k0, *kout = k1;
     uint32_t *vin = v0, *vout = v1;
-    for (uint32_t shift = 0; shift < bits || (tile_n && shift == 0); shift += 8) {
-        const bool sparse = tile_n && shift == 0;  // the first pass compacts the gather tiles
+    for (uint32_t shift = shift0; shift < bits || (tile_n && shift == shift0); shift += 8) {
+        const bool sparse = tile_n && shift == shift0;  // the first pass compacts the gather tiles
         const uint32_t nt = sparse ? sparse_tiles : tiles_of(n);
         const uint32_t *tn = sparse ? tile_n : nullptr;
-        upsweep_kernel<<<nt, kThreads, 0, s>>>(kin, n, tn, shift, hist, nt);
+        upsweep_kernel<MIX><<<nt, kThreads, 0, s>>>(kin, n, tn, shift, hist, nt);
         exclusive_scan(hist, static_cast<uint64_t>(nt) * 256, bsum, s);
         if (vin)
-            downsweep_kernel<true><<<nt, kThreads, 0, s>>>(kin, vin, kout, vout, n, tn, shift, hist, nt);
+            downsweep_kernel<true, MIX><<<nt, kThreads, 0, s>>>(kin, vin, kout, vout, n, tn, shift, hist, nt);
         else
-            downsweep_kernel<false><<<nt, kThreads, 0, s>>>(kin, vin, kout, vout, n, tn, shift, hist, nt);
+            downsweep_kernel<false, MIX><<<nt, kThreads, 0, s>>>(kin, vin, kout, vout, n, tn, shift, hist, nt);
         std::swap(kin, kout);
         std::swap(vin, vout);
     }
     return kin == k0 ? 0 : 1;
+}
+}  // namespace
+
+int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t bits,
+                      uint32_t *hist, uint32_t *bsum, hipStream_t s, const uint32_t *tile_n, uint32_t sparse_tiles) {
+    if (n == 0) return 0;
+    if (n <= 1 && !tile_n) return 0;
+    return radix_passes<false>(k0, v0, k1, v1, n, 0, bits, hist, bsum, s, tile_n, sparse_tiles);
+}
+
+int launch_bucket_dedupe(uint64_t *k0, uint64_t *k1, uint64_t n, uint32_t job_shift, uint32_t nj,
+                         unsigned long long *counts, uint32_t *overflow, uint32_t *hist, uint32_t *bsum, hipStream_t s,
+                         const uint32_t *tile_n, uint32_t sparse_tiles) {
+    if (n == 0) return 0;
+    // two stable passes on bits 48..63 of mix(word): buckets contiguous
+    const int r = radix_passes<true>(k0, nullptr, k1, nullptr, n, 48, 64, hist, bsum, s, tile_n, sparse_tiles);
+    const uint64_t *keys = r ? k1 : k0;
+    const uint32_t nb = static_cast<uint32_t>((n + kBTile - 1) / kBTile);
+    // SBEACON_DEDUP_BUCKET_CAP (tests): a smaller cap forces the overflow fallback
+    uint32_t cap = kBSlots * 3 / 4;
+    if (const char *e = std::getenv("SBEACON_DEDUP_BUCKET_CAP")) cap = std::min<uint32_t>(cap, static_cast<uint32_t>(std::atoi(e)));
+    bucket_dedupe_kernel<<<nb, kThreads, 0, s>>>(keys, n, job_shift, nj < 256 ? nj : 256u, counts, overflow, cap);
+    return r;
 }
 
 uint32_t dedup_unique_blocks(uint64_t n) { return n ? tiles_of(n) : 0; }

@@ -1530,10 +1530,15 @@ constexpr int kPackAhead = 4;     // candidate chunks issued before the first is
 constexpr uint32_t kPackRun = 16;  // chains per wave at most
 constexpr uint32_t kPackSlots = 256;  // slices per run at most (host-enforced)
 
+// SLICES: per-slice sums (the per-slice QRes rows); without them (request
+// rows only) a slice keeps one "exists" bit and the chain its totals, which
+// frees the LDS for occupancy
+template <bool SLICES>
 struct PackLds {
     uint4 desc[kPackRun * 5];  // the run's ChainDev descriptors
-    unsigned long long cc[kPackSlots], an[kPackSlots];
-    unsigned int nh[kPackSlots];
+    unsigned long long cc[SLICES ? kPackSlots : 1], an[SLICES ? kPackSlots : 1];
+    unsigned int nh[SLICES ? kPackSlots : 1];
+    unsigned int exw[kPackSlots / 32];  // !SLICES: bit = the slot's slice exists
     uint32_t lut[kPackRun * 8];  // each chain's symbolic-ALT LUT words
     unsigned long long tcc[kPackRun], tan[kPackRun];
     unsigned int slow[kPackRun];
@@ -1561,17 +1566,18 @@ __device__ __forceinline__ uint32_t last_le(uint32_t v, uint32_t R, uint32_t g) 
     return lo;
 }
 
+template <bool SLICES>
 __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const ChainDev *__restrict__ chains,
                                                             const uint32_t *__restrict__ runs, uint32_t n_runs,
                                                             const uint32_t *__restrict__ corig,
                                                             QRes *__restrict__ res, uint64_t *__restrict__ hits,
                                                             ReqPartial *__restrict__ cpart, uint32_t dbg) {
-    __shared__ PackLds lds_all[kWavesPerBlock];
+    __shared__ PackLds<SLICES> lds_all[kWavesPerBlock];
     const uint32_t w = launch_wave();
     if (w >= n_runs) return;
     const uint32_t c_first = uniform(runs[w]);
     const uint32_t R = uniform(runs[w + 1]) - c_first;  // 1 .. kPackRun
-    PackLds &L = lds_all[threadIdx.x >> 6];
+    PackLds<SLICES> &L = lds_all[threadIdx.x >> 6];
     const uint32_t ul = static_cast<uint32_t>(lane_id());
     // round 1: the run's descriptors (5 x 16 B per chain), staged in LDS
     {
@@ -1586,6 +1592,7 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
             L.tan[ul] = 0;
             L.slow[ul] = 0;
         }
+        if (ul < kPackSlots / 32) L.exw[ul] = 0;
     }
     wave_lds_sync();
     // lane j < R: chain j's slice count and slot prefix (sex / sin)
@@ -1632,15 +1639,15 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
         orig[t] = 0;
         if (kWave * t < S) {
             const uint32_t slot = min(ul + kWave * t, S - 1);
-            if (res) {
+            if constexpr (SLICES) {
                 const uint32_t k = last_le(sex, R, slot);
                 const uint32_t sk = __shfl(sex, static_cast<int>(k), kWave);  // every lane active
-                if (ul + kWave * t < S) orig[t] = corig[L.desc[5 * k].x + (slot - sk)];
-            }
-            if (ul + kWave * t < S) {
-                L.cc[slot] = 0;
-                L.an[slot] = 0;
-                L.nh[slot] = 0;
+                if (ul + kWave * t < S) {
+                    orig[t] = corig[L.desc[5 * k].x + (slot - sk)];
+                    L.cc[slot] = 0;
+                    L.an[slot] = 0;
+                    L.nh[slot] = 0;
+                }
             }
         }
     }
@@ -1733,11 +1740,17 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
             uint64_t *dst = hits + out + before + pre;
             for (uint64_t b = o.em; b; b &= b - 1)
                 *dst++ = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
-            atomicAdd(&L.nh[slot], cnt);
+            if constexpr (SLICES) atomicAdd(&L.nh[slot], cnt);
         }
         if (hit) {
-            atomicAdd(&L.cc[slot], static_cast<unsigned long long>(o.c));
-            atomicAdd(&L.an[slot], static_cast<unsigned long long>(o.anv));
+            if constexpr (SLICES) {
+                atomicAdd(&L.cc[slot], static_cast<unsigned long long>(o.c));
+                atomicAdd(&L.an[slot], static_cast<unsigned long long>(o.anv));
+            } else {
+                if (o.c > 0) atomicOr(&L.exw[slot >> 5], 1u << (slot & 31u));
+                atomicAdd(&L.tcc[k], static_cast<unsigned long long>(o.c));
+                atomicAdd(&L.tan[k], static_cast<unsigned long long>(o.anv));
+            }
         }
     };
     // every chunk of the run issued before the first is evaluated
@@ -1753,52 +1766,65 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
     }
     if (dbg & 2u) return;
     wave_lds_sync();
-    // results: lane ul + 64 t = slot; chain totals by slot atomics
-    uint64_t exm_all[kPackSlots / kWave];
+    if constexpr (SLICES) {
+        // results: lane ul + 64 t = slot; chain totals by slot atomics
+        uint64_t exm_all[kPackSlots / kWave];
 #pragma unroll
-    for (uint32_t t = 0; t < kPackSlots / kWave; ++t) {
-        exm_all[t] = 0;
-        if (kWave * t < S) {
-            const uint32_t slot = min(ul + kWave * t, S - 1);
-            const bool sl = ul + kWave * t < S;
-            const uint32_t k = last_le(sex, R, slot);
-            const int64_t cc = sl ? static_cast<int64_t>(L.cc[slot]) : 0;
-            const int64_t an = sl ? static_cast<int64_t>(L.an[slot]) : 0;
-            const uint32_t nh = sl ? L.nh[slot] : 0u;
-            exm_all[t] = __ballot(sl && cc > 0);
-            if (sl && res) {
-                QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host
-                if (L.slow[k]) {
-                    o.error = SB_QERR_UNSUPPORTED;
-                } else {
-                    o.exists = cc > 0 ? 1 : 0;
-                    o.call_count = cc;
-                    o.all_alleles_count = an;
-                    o.n_hits = nh;
+        for (uint32_t t = 0; t < kPackSlots / kWave; ++t) {
+            exm_all[t] = 0;
+            if (kWave * t < S) {
+                const uint32_t slot = min(ul + kWave * t, S - 1);
+                const bool sl = ul + kWave * t < S;
+                const uint32_t k = last_le(sex, R, slot);
+                const int64_t cc = sl ? static_cast<int64_t>(L.cc[slot]) : 0;
+                const int64_t an = sl ? static_cast<int64_t>(L.an[slot]) : 0;
+                const uint32_t nh = sl ? L.nh[slot] : 0u;
+                exm_all[t] = __ballot(sl && cc > 0);
+                if (sl && res) {
+                    QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host
+                    if (L.slow[k]) {
+                        o.error = SB_QERR_UNSUPPORTED;
+                    } else {
+                        o.exists = cc > 0 ? 1 : 0;
+                        o.call_count = cc;
+                        o.all_alleles_count = an;
+                        o.n_hits = nh;
+                    }
+                    res[orig[t]] = o;
                 }
-                res[orig[t]] = o;
-            }
-            if (sl && cpart && (cc | an)) {
-                atomicAdd(&L.tcc[k], static_cast<unsigned long long>(cc));
-                atomicAdd(&L.tan[k], static_cast<unsigned long long>(an));
+                if (sl && cpart && (cc | an)) {
+                    atomicAdd(&L.tcc[k], static_cast<unsigned long long>(cc));
+                    atomicAdd(&L.tan[k], static_cast<unsigned long long>(an));
+                }
             }
         }
-    }
-    if (cpart) {
-        wave_lds_sync();
-        if (ul < R) {
-            // exists count of chain ul: its slots [sex, sin) in the flattened order
-            int64_t ex = 0;
+        if (cpart) {
+            wave_lds_sync();
+            if (ul < R) {
+                // exists count of chain ul: its slots [sex, sin) in the flattened order
+                int64_t ex = 0;
 #pragma unroll
-            for (uint32_t t = 0; t < kPackSlots / kWave; ++t) {
-                const uint32_t a = sex > kWave * t ? sex - kWave * t : 0u, b = sin > kWave * t ? sin - kWave * t : 0u;
-                ex += __popcll(exm_all[t] & lanes_from(a) & lanes_below(b));
+                for (uint32_t t = 0; t < kPackSlots / kWave; ++t) {
+                    const uint32_t a = sex > kWave * t ? sex - kWave * t : 0u, b = sin > kWave * t ? sin - kWave * t : 0u;
+                    ex += __popcll(exm_all[t] & lanes_from(a) & lanes_below(b));
+                }
+                cpart[c_first + ul] = L.slow[ul] ? ReqPartial{0, 0, 0, 0, static_cast<int64_t>(nv)}
+                                                 : ReqPartial{ex, static_cast<int64_t>(noutv),
+                                                              static_cast<int64_t>(L.tcc[ul]),
+                                                              static_cast<int64_t>(L.tan[ul]), 0};
             }
-            cpart[c_first + ul] = L.slow[ul] ? ReqPartial{0, 0, 0, 0, static_cast<int64_t>(nv)}
-                                             : ReqPartial{ex, static_cast<int64_t>(noutv),
-                                                          static_cast<int64_t>(L.tcc[ul]),
-                                                          static_cast<int64_t>(L.tan[ul]), 0};
         }
+    } else if (ul < R) {  // request rows only: chain ul's partial from its exists bits and totals
+        int64_t ex = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kPackSlots / 32; ++q) {
+            const uint32_t a = sex > 32 * q ? min(sex - 32 * q, 32u) : 0u, b = sin > 32 * q ? min(sin - 32 * q, 32u) : 0u;
+            const uint32_t m = (b >= 32 ? ~0u : ((1u << b) - 1u)) & (a >= 32 ? 0u : (~0u << a));
+            ex += __popc(L.exw[q] & m);
+        }
+        cpart[c_first + ul] = L.slow[ul] ? ReqPartial{0, 0, 0, 0, static_cast<int64_t>(nv)}
+                                         : ReqPartial{ex, static_cast<int64_t>(noutv), static_cast<int64_t>(L.tcc[ul]),
+                                                      static_cast<int64_t>(L.tan[ul]), 0};
     }
 }
 
@@ -2410,8 +2436,13 @@ void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, 
     const char *kern = std::getenv("SBEACON_CHAIN_KERNEL");  // "seq": the chain-sequential kernel
     if (!(kern && kern[0] == 's')) {
         const char *dbg = std::getenv("SBEACON_PACK_DBG");
-        hipLaunchKernelGGL(chain_pack_kernel, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs, n_runs,
-                           corig, res, hits, cpart, dbg ? static_cast<uint32_t>(std::atoi(dbg)) : 0u);
+        const uint32_t dbgv = dbg ? static_cast<uint32_t>(std::atoi(dbg)) : 0u;
+        if (res || !cpart)
+            hipLaunchKernelGGL(chain_pack_kernel<true>, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs,
+                               n_runs, corig, res, hits, cpart, dbgv);
+        else
+            hipLaunchKernelGGL(chain_pack_kernel<false>, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs,
+                               n_runs, corig, res, hits, cpart, dbgv);
         return;
     }
     // runs of kChainRun chains per wave while the launch still fills the chip

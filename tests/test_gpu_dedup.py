@@ -103,7 +103,15 @@ def check(texts, jobs, got):
             assert g == e, (j, g, e)
 
 
-def test_dedup_batch_vs_oracle(texts, store):
+@pytest.mark.parametrize('exact', ['bucket', 'radix', 'overflow'])
+def test_dedup_batch_vs_oracle(texts, store, monkeypatch, exact):
+    """exact stream by hash buckets (default), by the full radix sort, and
+    by buckets whose hash sets 'overflow' (a cap of 4 keys per workgroup):
+    the radix recount must give the same answers."""
+    if exact == 'radix':
+        monkeypatch.setenv('SBEACON_DEDUP_EXACT', 'radix')
+    elif exact == 'overflow':
+        monkeypatch.setenv('SBEACON_DEDUP_BUCKET_CAP', '4')
     rng = random.Random(11)
     jobs = random_jobs(texts, rng, 300)
     got, st = store.dedup_counts(jobs, with_stats=True)
