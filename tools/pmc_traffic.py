@@ -63,8 +63,12 @@ def main():
         w = write.get(name, [])
         fb = 2.0 * 1024.0 * sum(f) / max(1, len(f))   # gfx950 streaming-read correction, KiB -> B
         wb = 1024.0 * sum(w) / max(1, len(w))
+        # profiles/r02_fetch_calib: x2 for coalesced streams (any lane width), x1
+        # for scattered 64 B lines; x2 is the upper bound, x1 the lower
         kernels[short(name)] = {'dispatches': [len(f), len(w)], 'fetch_bytes_per_launch': fb,
-                                'write_bytes_per_launch': wb, 'hbm_bytes_per_launch': fb + wb}
+                                'fetch_bytes_per_launch_x1': fb / 2.0,
+                                'write_bytes_per_launch': wb, 'hbm_bytes_per_launch': fb + wb,
+                                'hbm_bytes_per_launch_x1': fb / 2.0 + wb}
         step_bytes += fb + wb
     out = {
         'records': a.records,
@@ -73,7 +77,9 @@ def main():
         'kernels': kernels,
         'scan_kernel_hbm_bytes_per_launch': step_bytes,
         'method': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, kernel trace only), '
-                  'FETCH_SIZE x2 (gfx950 16B/lane streaming correction), KiB->B; includes Infinity-Cache hits',
+                  'FETCH_SIZE x2 (gfx950 streaming correction, calibrated at 4/8/16 B per lane in '
+                  'profiles/r02_fetch_calib; scattered 64 B lines need x1: *_x1 is that lower bound), KiB->B; '
+                  'includes Infinity-Cache hits',
     }
     if a.kernel:
         hit = [k for k in kernels if k.startswith(a.kernel)]
@@ -82,6 +88,7 @@ def main():
             out['hbm_bytes_per_launch'] = kernels[hit[0]]['hbm_bytes_per_launch']
             out['fetch_bytes_per_launch'] = kernels[hit[0]]['fetch_bytes_per_launch']
             out['write_bytes_per_launch'] = kernels[hit[0]]['write_bytes_per_launch']
+            out['hbm_bytes_per_launch_x1'] = kernels[hit[0]]['hbm_bytes_per_launch_x1']
     with open(a.out, 'w') as fh:
         json.dump(out, fh, indent=1)
     print(json.dumps(out, indent=1))
