@@ -1665,15 +1665,15 @@ void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj
     // adjacent-unique pass; the first pass compacts the gather tiles
     const char *exm = std::getenv("SBEACON_DEDUP_EXACT");
     const bool bucket = !force_radix && !(exm && exm[0] == 'r') && ne > 0;
-    const uint32_t be = bucket ? 0u : dedup_unique_blocks(ne), bh = dedup_unique_blocks(nh);
+    const uint32_t be = bucket ? 0u : dedup_unique_blocks(ne), bh = bucket ? 0u : dedup_unique_blocks(nh);
     pe.reserve(std::max<uint32_t>(be, 1) * sizeof(uint4));
     ph.reserve(std::max<uint32_t>(bh, 1) * sizeof(uint4));
     W.overflow.reserve(4);
     HIP_OK(hipMemsetAsync(W.overflow.p, 0, 4, st));
     if (bucket) {
-        launch_bucket_dedupe(ke0.as<uint64_t>(), ke1.as<uint64_t>(), ne, exact_job_shift, static_cast<uint32_t>(nj),
-                             counts.as<unsigned long long>(), W.overflow.as<uint32_t>(), hist.as<uint32_t>(),
-                             bsum.as<uint32_t>(), st, tcnt.as<uint32_t>(), ntiles);
+        launch_bucket_dedupe(ke0.as<uint64_t>(), nullptr, ke1.as<uint64_t>(), nullptr, ne, s.dk, exact_job_shift,
+                             static_cast<uint32_t>(nj), counts.as<unsigned long long>(), W.overflow.as<uint32_t>(),
+                             hist.as<uint32_t>(), bsum.as<uint32_t>(), st, tcnt.as<uint32_t>(), ntiles);
     } else {
         const int re = launch_radix_sort(ke0.as<uint64_t>(), nullptr, ke1.as<uint64_t>(), nullptr, ne,
                                          job_bits + pos_bits + 6, hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
@@ -1682,14 +1682,26 @@ void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj
                             counts.as<unsigned long long>(), pe.as<uint4>(), coll.as<uint32_t>(), ncoll.as<uint32_t>(),
                             st);
     }
-    // hashed stream: (job | hash, key id), 8 passes, equal words confirmed
-    const int rh = launch_radix_sort(kh0.as<uint64_t>(), vh0.as<uint32_t>(), kh1.as<uint64_t>(), vh1.as<uint32_t>(),
-                                     nh, 64, hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
-                                     tcnt.as<uint32_t>() + ntiles, ntiles);
+    // hashed stream: (job | hash, key id); hash buckets with equal words
+    // confirmed on the strings (any collision: the sorted path below via the
+    // overflow rerun), or 8 radix passes + adjacent unique with the exact
+    // host recount of collided groups
+    const uint32_t hjob_shift = job_bits ? 64 - job_bits : 64;
+    int rh = 0;
+    if (bucket && nh) {
+        rh = launch_bucket_dedupe(kh0.as<uint64_t>(), vh0.as<uint32_t>(), kh1.as<uint64_t>(), vh1.as<uint32_t>(), nh, s.dk,
+                                  hjob_shift, static_cast<uint32_t>(nj), counts.as<unsigned long long>(),
+                                  W.overflow.as<uint32_t>(), hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
+                                  tcnt.as<uint32_t>() + ntiles, ntiles);
+    } else {
+        rh = launch_radix_sort(kh0.as<uint64_t>(), vh0.as<uint32_t>(), kh1.as<uint64_t>(), vh1.as<uint32_t>(), nh, 64,
+                               hist.as<uint32_t>(), bsum.as<uint32_t>(), st, tcnt.as<uint32_t>() + ntiles, ntiles);
+        launch_dedup_unique((rh ? kh1 : kh0).as<uint64_t>(), (rh ? vh1 : vh0).as<uint32_t>(), nh, s.dk, hjob_shift,
+                            true, counts.as<unsigned long long>(), ph.as<uint4>(), coll.as<uint32_t>(),
+                            ncoll.as<uint32_t>(), st);
+    }
     DevMem &kh = rh ? kh1 : kh0;
     DevMem &vh = rh ? vh1 : vh0;
-    launch_dedup_unique(kh.as<uint64_t>(), vh.as<uint32_t>(), nh, s.dk, job_bits ? 64 - job_bits : 64, true,
-                        counts.as<unsigned long long>(), ph.as<uint4>(), coll.as<uint32_t>(), ncoll.as<uint32_t>(), st);
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipGetLastError());
     std::vector<uint64_t> cnt(std::max<size_t>(nj, 1));

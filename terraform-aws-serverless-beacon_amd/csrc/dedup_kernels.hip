@@ -530,35 +530,81 @@ __device__ uint64_t bucket_start_at(const uint64_t *keys, uint64_t n, uint64_t a
     return n;
 }
 
-__global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t *keys, uint64_t n, uint32_t job_shift,
-                                                                 uint32_t nj_lds, unsigned long long *counts,
-                                                                 uint32_t *overflow, uint32_t cap) {
-    __shared__ unsigned long long set[kBSlots];
+// VALS (the hashed stream: words are job | 64-bit hash, vals the key ids):
+// a word already in the set is confirmed on the key strings; two different
+// strings under one word (a 64-bit collision, or the SBEACON_DEDUP_HASH_BITS
+// test hook) raise *overflow so the host recounts with the sorted path,
+// whose exact collision recount needs adjacent groups.  Keys are handled in
+// rounds of kBPer per thread, every load of a round issued first.
+constexpr uint32_t kBPer = 8;
+
+template <bool VALS, uint32_t SLOTS>
+__global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t *keys, const uint32_t *vals, uint64_t n,
+                                                                 KStore ks, uint32_t job_shift, uint32_t nj_lds,
+                                                                 unsigned long long *counts, uint32_t *overflow,
+                                                                 uint32_t cap) {
+    __shared__ unsigned long long set[SLOTS];
+    __shared__ uint32_t ids[VALS ? SLOTS : 1];
     __shared__ unsigned int jc[256];
     __shared__ uint32_t tmp[1];
-    for (uint32_t i = threadIdx.x; i < kBSlots; i += kThreads) set[i] = kBEmpty;
+    for (uint32_t i = threadIdx.x; i < SLOTS; i += kThreads) set[i] = kBEmpty;
     for (uint32_t i = threadIdx.x; i < 256; i += kThreads) jc[i] = 0;
     const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kBTile;
     const uint64_t s0 = bucket_start_at(keys, n, t0, tmp);
     const uint64_t s1 = bucket_start_at(keys, n, t0 + kBTile, tmp);
     __syncthreads();
-    if (s1 > s0 && s1 - s0 > cap) {  // cannot hold them: radix path
+    if (s1 <= s0) return;
+    if (s1 - s0 > cap) {  // cannot hold them: the sorted path
         if (threadIdx.x == 0) atomicOr(overflow, 1u);
         return;
     }
-    for (uint64_t i = s0 + threadIdx.x; i < s1; i += kThreads) {
-        const uint64_t k = keys[i];
-        uint32_t h = static_cast<uint32_t>(mix64(k ^ 0x9e3779b97f4a7c15ull)) & (kBSlots - 1);
-        for (uint32_t probe = 0; probe < kBSlots; ++probe) {
-            const unsigned long long was = atomicCAS(&set[h], kBEmpty, static_cast<unsigned long long>(k));
-            if (was == kBEmpty) {  // first copy of this word: a distinct key of its job
-                const uint32_t j = job_shift < 64 ? static_cast<uint32_t>(k >> job_shift) : 0u;
+    const uint32_t m = static_cast<uint32_t>(s1 - s0);
+    for (uint32_t r0 = 0; r0 < m; r0 += kThreads * kBPer) {  // uniform trip count
+        uint64_t k[kBPer];
+        uint32_t v[kBPer], slot[kBPer];
+        bool mine[kBPer], ok[kBPer];
+#pragma unroll
+        for (uint32_t u = 0; u < kBPer; ++u) {
+            const uint32_t j = r0 + u * kThreads + threadIdx.x;
+            ok[u] = j < m;
+            k[u] = ok[u] ? keys[s0 + j] : 0ull;
+            v[u] = (VALS && ok[u]) ? vals[s0 + j] : 0u;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kBPer; ++u) {
+            mine[u] = false;
+            slot[u] = 0;
+            if (!ok[u]) continue;
+            if (k[u] == kBEmpty) {  // the set's empty marker (a hashed word of all ones): the sorted path
+                atomicOr(overflow, 1u);
+                ok[u] = false;
+                continue;
+            }
+            uint32_t h = static_cast<uint32_t>(mix64(k[u] ^ 0x9e3779b97f4a7c15ull)) & (SLOTS - 1);
+            for (uint32_t probe = 0; probe < SLOTS; ++probe) {
+                const unsigned long long was = atomicCAS(&set[h], kBEmpty, static_cast<unsigned long long>(k[u]));
+                if (was == kBEmpty || was == k[u]) {
+                    mine[u] = was == kBEmpty;  // first copy of this word
+                    slot[u] = h;
+                    break;
+                }
+                h = (h + 1) & (SLOTS - 1);
+            }
+            if (mine[u]) {
+                const uint32_t j = job_shift < 64 ? static_cast<uint32_t>(k[u] >> job_shift) : 0u;
                 if (j < nj_lds) atomicAdd(&jc[j], 1u);
                 else atomicAdd(&counts[j], 1ull);
-                break;
             }
-            if (was == k) break;
-            h = (h + 1) & (kBSlots - 1);
+        }
+        if constexpr (VALS) {  // the inserters publish their key ids, the rest compare strings
+            __syncthreads();
+#pragma unroll
+            for (uint32_t u = 0; u < kBPer; ++u)
+                if (mine[u]) ids[slot[u]] = v[u];
+            __syncthreads();
+#pragma unroll
+            for (uint32_t u = 0; u < kBPer; ++u)
+                if (ok[u] && !mine[u] && !key_equal(ks, ids[slot[u]], v[u])) atomicOr(overflow, 1u);
         }
     }
     __syncthreads();
@@ -620,18 +666,25 @@ int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, ui
     return radix_passes<false>(k0, v0, k1, v1, n, 0, bits, hist, bsum, s, tile_n, sparse_tiles);
 }
 
-int launch_bucket_dedupe(uint64_t *k0, uint64_t *k1, uint64_t n, uint32_t job_shift, uint32_t nj,
-                         unsigned long long *counts, uint32_t *overflow, uint32_t *hist, uint32_t *bsum, hipStream_t s,
-                         const uint32_t *tile_n, uint32_t sparse_tiles) {
+int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, const KStore &ks,
+                         uint32_t job_shift, uint32_t nj, unsigned long long *counts, uint32_t *overflow,
+                         uint32_t *hist, uint32_t *bsum, hipStream_t s, const uint32_t *tile_n, uint32_t sparse_tiles) {
     if (n == 0) return 0;
     // two stable passes on bits 48..63 of mix(word): buckets contiguous
-    const int r = radix_passes<true>(k0, nullptr, k1, nullptr, n, 48, 64, hist, bsum, s, tile_n, sparse_tiles);
+    const int r = radix_passes<true>(k0, v0, k1, v1, n, 48, 64, hist, bsum, s, tile_n, sparse_tiles);
     const uint64_t *keys = r ? k1 : k0;
+    const uint32_t *vals = v0 ? (r ? v1 : v0) : nullptr;
     const uint32_t nb = static_cast<uint32_t>((n + kBTile - 1) / kBTile);
     // SBEACON_DEDUP_BUCKET_CAP (tests): a smaller cap forces the overflow fallback
-    uint32_t cap = kBSlots * 3 / 4;
+    const uint32_t slots = v0 ? 4096u : kBSlots;
+    uint32_t cap = slots * 3 / 4;
     if (const char *e = std::getenv("SBEACON_DEDUP_BUCKET_CAP")) cap = std::min<uint32_t>(cap, static_cast<uint32_t>(std::atoi(e)));
-    bucket_dedupe_kernel<<<nb, kThreads, 0, s>>>(keys, n, job_shift, nj < 256 ? nj : 256u, counts, overflow, cap);
+    const uint32_t njl = nj < 256 ? nj : 256u;
+    if (v0)
+        bucket_dedupe_kernel<true, 4096><<<nb, kThreads, 0, s>>>(keys, vals, n, ks, job_shift, njl, counts, overflow, cap);
+    else
+        bucket_dedupe_kernel<false, kBSlots><<<nb, kThreads, 0, s>>>(keys, nullptr, n, ks, job_shift, njl, counts, overflow,
+                                                                     cap);
     return r;
 }
 

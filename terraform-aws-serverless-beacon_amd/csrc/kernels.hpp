@@ -116,14 +116,16 @@ void launch_dedup_gather(const KStore &ks, const KSeg *segs, const uint2 *tiles,
 int launch_radix_sort(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, uint32_t bits,
                       uint32_t *hist, uint32_t *bsum, hipStream_t s, const uint32_t *tile_n = nullptr,
                       uint32_t sparse_tiles = 0);
-// exact stream by hash buckets instead of a full sort: two radix passes on
+// a stream by hash buckets instead of a full sort (exact words; or, with
+// vals = key ids, the hashed stream, equal words confirmed on the strings and
+// any collision raising *overflow): two radix passes on
 // the top 16 bits of a mix of the word, then an LDS hash set per workgroup
 // of buckets adds each job's distinct words to counts[job].  Sets
 // *overflow (leaving counts partial) when a workgroup's buckets outgrow its
 // set: the caller then recounts the stream with the radix path.
-int launch_bucket_dedupe(uint64_t *k0, uint64_t *k1, uint64_t n, uint32_t job_shift, uint32_t nj,
-                         unsigned long long *counts, uint32_t *overflow, uint32_t *hist, uint32_t *bsum, hipStream_t s,
-                         const uint32_t *tile_n, uint32_t sparse_tiles);
+int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1, uint64_t n, const KStore &ks,
+                         uint32_t job_shift, uint32_t nj, unsigned long long *counts, uint32_t *overflow,
+                         uint32_t *hist, uint32_t *bsum, hipStream_t s, const uint32_t *tile_n, uint32_t sparse_tiles);
 void launch_dedup_unique(const uint64_t *keys, const uint32_t *vals, uint64_t n, const KStore &ks, uint32_t job_shift,
                          bool verify, unsigned long long *counts, uint4 *part, uint32_t *coll, uint32_t *ncoll,
                          hipStream_t s);
