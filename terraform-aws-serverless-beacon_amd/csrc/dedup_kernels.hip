@@ -510,26 +510,6 @@ constexpr uint64_t kBEmpty = ~0ull;        // exact words never reach all ones (
 
 __device__ __forceinline__ uint32_t bucket_of(uint64_t k) { return static_cast<uint32_t>(mix64(k) >> 48); }
 
-// first index >= at whose bucket differs from its predecessor's (n if none)
-__device__ uint64_t bucket_start_at(const uint64_t *keys, uint64_t n, uint64_t at, uint32_t *lds) {
-    if (at == 0) return 0;
-    if (at >= n) return n;
-    const uint32_t prevb = bucket_of(keys[at - 1]);
-    // scan forward in block-wide windows until a boundary is seen
-    for (uint64_t w0 = at; w0 < n; w0 += kThreads) {
-        const uint64_t i = w0 + threadIdx.x;
-        const bool edge = i < n && bucket_of(keys[i]) != (i == at ? prevb : bucket_of(keys[i - 1]));
-        if (threadIdx.x == 0) lds[0] = 0xffffffffu;
-        __syncthreads();
-        if (edge) atomicMin(&lds[0], static_cast<uint32_t>(i - w0));
-        __syncthreads();
-        const uint32_t f = lds[0];
-        __syncthreads();
-        if (f != 0xffffffffu) return w0 + f;
-    }
-    return n;
-}
-
 // VALS (the hashed stream: words are job | 64-bit hash, vals the key ids):
 // a word already in the set is confirmed on the key strings; two different
 // strings under one word (a 64-bit collision, or the SBEACON_DEDUP_HASH_BITS
@@ -546,29 +526,53 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
     __shared__ unsigned long long set[SLOTS];
     __shared__ uint32_t ids[VALS ? SLOTS : 1];
     __shared__ unsigned int jc[256];
-    __shared__ uint32_t tmp[1];
+    __shared__ uint32_t s_more, s_ins;
+    if (threadIdx.x == 0) s_ins = 0;
     for (uint32_t i = threadIdx.x; i < SLOTS; i += kThreads) set[i] = kBEmpty;
     for (uint32_t i = threadIdx.x; i < 256; i += kThreads) jc[i] = 0;
+    // this workgroup owns tile [t0, t0 + kBTile) minus the leading keys of the
+    // bucket that started in an earlier tile, plus the rest of its last bucket
+    // beyond the tile's end
     const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kBTile;
-    const uint64_t s0 = bucket_start_at(keys, n, t0, tmp);
-    const uint64_t s1 = bucket_start_at(keys, n, t0 + kBTile, tmp);
+    const uint64_t te = min(n, t0 + kBTile);
+    const uint32_t b_prev = t0 ? bucket_of(keys[t0 - 1]) : 0xffffffffu;
+    const uint32_t b_last = bucket_of(keys[te - 1]);
     __syncthreads();
-    if (s1 <= s0) return;
-    if (s1 - s0 > cap) {  // cannot hold them: the sorted path
-        if (threadIdx.x == 0) atomicOr(overflow, 1u);
-        return;
-    }
-    const uint32_t m = static_cast<uint32_t>(s1 - s0);
-    for (uint32_t r0 = 0; r0 < m; r0 += kThreads * kBPer) {  // uniform trip count
+    for (uint64_t r0 = t0;; r0 += kThreads * kBPer) {  // uniform trip count (s_more)
         uint64_t k[kBPer];
         uint32_t v[kBPer], slot[kBPer];
         bool mine[kBPer], ok[kBPer];
 #pragma unroll
         for (uint32_t u = 0; u < kBPer; ++u) {
-            const uint32_t j = r0 + u * kThreads + threadIdx.x;
-            ok[u] = j < m;
-            k[u] = ok[u] ? keys[s0 + j] : 0ull;
-            v[u] = (VALS && ok[u]) ? vals[s0 + j] : 0u;
+            const uint64_t j = r0 + u * kThreads + threadIdx.x;
+            k[u] = j < n ? keys[j] : 0ull;
+            v[u] = (VALS && j < n) ? vals[j] : 0u;
+            ok[u] = j < n;
+        }
+        bool any_beyond = false;
+#pragma unroll
+        for (uint32_t u = 0; u < kBPer; ++u) {
+            const uint64_t j = r0 + u * kThreads + threadIdx.x;
+            if (!ok[u]) continue;
+            const uint32_t b = bucket_of(k[u]);
+            if (j < te) {
+                ok[u] = b != b_prev || b_prev == 0xffffffffu;  // leading keys of an earlier bucket: not ours
+            } else {
+                ok[u] = b == b_last && b_last != b_prev;       // the rest of our last bucket
+                any_beyond |= ok[u];
+            }
+        }
+        uint32_t nok = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < kBPer; ++u) nok += ok[u] ? 1u : 0u;
+        if (threadIdx.x == 0) s_more = 0;
+        __syncthreads();
+        if (any_beyond) s_more = 1;
+        if (nok) atomicAdd(&s_ins, nok);
+        __syncthreads();
+        if (s_ins > cap) {  // the set cannot hold this workgroup's keys: the sorted path
+            if (threadIdx.x == 0) atomicOr(overflow, 1u);
+            return;
         }
 #pragma unroll
         for (uint32_t u = 0; u < kBPer; ++u) {
@@ -606,8 +610,10 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
             for (uint32_t u = 0; u < kBPer; ++u)
                 if (ok[u] && !mine[u] && !key_equal(ks, ids[slot[u]], v[u])) atomicOr(overflow, 1u);
         }
+        __syncthreads();
+        const bool more = r0 + kThreads * kBPer < te || s_more;
+        if (!more) break;
     }
-    __syncthreads();
     for (uint32_t j = threadIdx.x; j < nj_lds; j += kThreads)
         if (jc[j]) atomicAdd(&counts[j], static_cast<unsigned long long>(jc[j]));
 }
