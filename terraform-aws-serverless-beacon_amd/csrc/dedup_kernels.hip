@@ -565,6 +565,7 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
         uint32_t nok = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kBPer; ++u) nok += ok[u] ? 1u : 0u;
+        __syncthreads();  // every thread has read the previous round's s_more
         if (threadIdx.x == 0) s_more = 0;
         __syncthreads();
         if (any_beyond) s_more = 1;
@@ -611,7 +612,10 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
                 if (ok[u] && !mine[u] && !key_equal(ks, ids[slot[u]], v[u])) atomicOr(overflow, 1u);
         }
         __syncthreads();
-        const bool more = r0 + kThreads * kBPer < te || s_more;
+        // go on: inside the tile; or this round reached its end and the last
+        // bucket may continue past it; or this round found more of that bucket
+        const bool reached_end = r0 < te && r0 + kThreads * kBPer >= te;
+        const bool more = r0 + kThreads * kBPer < te || s_more || (reached_end && te < n && b_last != b_prev);
         if (!more) break;
     }
     for (uint32_t j = threadIdx.x; j < nj_lds; j += kThreads)
