@@ -522,7 +522,7 @@ template <bool VALS, uint32_t SLOTS>
 __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t *keys, const uint32_t *vals, uint64_t n,
                                                                  KStore ks, uint32_t job_shift, uint32_t nj_lds,
                                                                  unsigned long long *counts, uint32_t *overflow,
-                                                                 uint32_t cap) {
+                                                                 uint32_t cap, uint32_t dbg) {
     __shared__ unsigned long long set[SLOTS];
     __shared__ uint32_t ids[VALS ? SLOTS : 1];
     __shared__ unsigned int jc[256];
@@ -550,11 +550,13 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
             ok[u] = j < n;
         }
         bool any_beyond = false;
+        uint64_t mx[kBPer];  // mix(word): top 16 bits = bucket, low bits = set slot
 #pragma unroll
         for (uint32_t u = 0; u < kBPer; ++u) {
             const uint64_t j = r0 + u * kThreads + threadIdx.x;
+            mx[u] = mix64(k[u]);
             if (!ok[u]) continue;
-            const uint32_t b = bucket_of(k[u]);
+            const uint32_t b = static_cast<uint32_t>(mx[u] >> 48);
             if (j < te) {
                 ok[u] = b != b_prev || b_prev == 0xffffffffu;  // leading keys of an earlier bucket: not ours
             } else {
@@ -575,26 +577,31 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
             if (threadIdx.x == 0) atomicOr(overflow, 1u);
             return;
         }
+        // first probe of every key issued back to back (independent slots),
+        // then the (rare) keys whose slot held another word probe on
+        uint32_t h[kBPer];
+        unsigned long long was[kBPer];
 #pragma unroll
         for (uint32_t u = 0; u < kBPer; ++u) {
             mine[u] = false;
             slot[u] = 0;
-            if (!ok[u]) continue;
-            if (k[u] == kBEmpty) {  // the set's empty marker (a hashed word of all ones): the sorted path
+            h[u] = static_cast<uint32_t>(mx[u]) & (SLOTS - 1);
+            if (ok[u] && k[u] == kBEmpty) {  // the set's empty marker (a hashed word of all ones): the sorted path
                 atomicOr(overflow, 1u);
                 ok[u] = false;
-                continue;
             }
-            uint32_t h = static_cast<uint32_t>(mix64(k[u] ^ 0x9e3779b97f4a7c15ull)) & (SLOTS - 1);
-            for (uint32_t probe = 0; probe < SLOTS; ++probe) {
-                const unsigned long long was = atomicCAS(&set[h], kBEmpty, static_cast<unsigned long long>(k[u]));
-                if (was == kBEmpty || was == k[u]) {
-                    mine[u] = was == kBEmpty;  // first copy of this word
-                    slot[u] = h;
-                    break;
-                }
-                h = (h + 1) & (SLOTS - 1);
+            if (dbg) ok[u] = false;  // timing ablation (SBEACON_DEDUP_BUCKET_DBG): no inserts
+            was[u] = ok[u] ? atomicCAS(&set[h[u]], kBEmpty, static_cast<unsigned long long>(k[u])) : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kBPer; ++u) {
+            if (!ok[u]) continue;
+            for (uint32_t probe = 1; was[u] != kBEmpty && was[u] != k[u] && probe < SLOTS; ++probe) {
+                h[u] = (h[u] + 1) & (SLOTS - 1);
+                was[u] = atomicCAS(&set[h[u]], kBEmpty, static_cast<unsigned long long>(k[u]));
             }
+            mine[u] = was[u] == kBEmpty;  // first copy of this word
+            slot[u] = h[u];
             if (mine[u]) {
                 const uint32_t j = job_shift < 64 ? static_cast<uint32_t>(k[u] >> job_shift) : 0u;
                 if (j < nj_lds) atomicAdd(&jc[j], 1u);
@@ -690,11 +697,14 @@ int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1,
     uint32_t cap = slots * 3 / 4;
     if (const char *e = std::getenv("SBEACON_DEDUP_BUCKET_CAP")) cap = std::min<uint32_t>(cap, static_cast<uint32_t>(std::atoi(e)));
     const uint32_t njl = nj < 256 ? nj : 256u;
+    const char *dbge = std::getenv("SBEACON_DEDUP_BUCKET_DBG");
+    const uint32_t dbg = dbge ? static_cast<uint32_t>(std::atoi(dbge)) : 0u;
     if (v0)
-        bucket_dedupe_kernel<true, 4096><<<nb, kThreads, 0, s>>>(keys, vals, n, ks, job_shift, njl, counts, overflow, cap);
+        bucket_dedupe_kernel<true, 4096><<<nb, kThreads, 0, s>>>(keys, vals, n, ks, job_shift, njl, counts, overflow, cap,
+                                                                 dbg);
     else
         bucket_dedupe_kernel<false, kBSlots><<<nb, kThreads, 0, s>>>(keys, nullptr, n, ks, job_shift, njl, counts, overflow,
-                                                                     cap);
+                                                                     cap, dbg);
     return r;
 }
 
