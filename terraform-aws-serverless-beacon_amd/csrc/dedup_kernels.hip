@@ -510,6 +510,36 @@ constexpr uint64_t kBEmpty = ~0ull;        // exact words never reach all ones (
 
 __device__ __forceinline__ uint32_t bucket_of(uint64_t k) { return static_cast<uint32_t>(mix64(k) >> 48); }
 
+// first index in [at, n) whose bucket is above b (buckets are nondecreasing):
+// two rounds of block-wide loads, 256 samples 16 apart then the 16 keys of
+// the span that holds the boundary; a bucket longer than 4096 keys takes
+// further rounds.  Every thread gets the answer.
+__device__ uint64_t bucket_end(const uint64_t *keys, uint64_t n, uint64_t at, uint32_t b, uint32_t *lds) {
+    for (uint64_t base = at; base < n; base += kThreads * 16) {
+        const uint64_t i = base + threadIdx.x * 16;
+        const bool past = i < n && bucket_of(keys[i]) > b;
+        if (threadIdx.x == 0) lds[0] = 0xffffffffu;
+        __syncthreads();
+        if (past) atomicMin(&lds[0], threadIdx.x);
+        __syncthreads();
+        const uint32_t f = lds[0];
+        __syncthreads();
+        if (f == 0xffffffffu) continue;  // not in this 4096-key span
+        // the boundary lies in (base + 16 (f - 1), base + 16 f]
+        const uint64_t lo = f ? base + 16 * static_cast<uint64_t>(f - 1) + 1 : base;
+        const uint64_t j = lo + threadIdx.x;
+        const bool past2 = threadIdx.x < 16 && j < n && bucket_of(keys[j]) > b;
+        if (threadIdx.x == 0) lds[0] = 0xffffffffu;
+        __syncthreads();
+        if (past2) atomicMin(&lds[0], threadIdx.x);
+        __syncthreads();
+        const uint32_t g = lds[0];
+        __syncthreads();
+        return g == 0xffffffffu ? base + 16 * static_cast<uint64_t>(f) : lo + g;
+    }
+    return n;
+}
+
 // VALS (the hashed stream: words are job | 64-bit hash, vals the key ids):
 // a word already in the set is confirmed on the key strings; two different
 // strings under one word (a 64-bit collision, or the SBEACON_DEDUP_HASH_BITS
@@ -526,51 +556,42 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
     __shared__ unsigned long long set[SLOTS];
     __shared__ uint32_t ids[VALS ? SLOTS : 1];
     __shared__ unsigned int jc[256];
-    __shared__ uint32_t s_more, s_ins;
+    __shared__ uint32_t s_ins;
     if (threadIdx.x == 0) s_ins = 0;
     for (uint32_t i = threadIdx.x; i < SLOTS; i += kThreads) set[i] = kBEmpty;
     for (uint32_t i = threadIdx.x; i < 256; i += kThreads) jc[i] = 0;
     // this workgroup owns tile [t0, t0 + kBTile) minus the leading keys of the
     // bucket that started in an earlier tile, plus the rest of its last bucket
-    // beyond the tile's end
+    // beyond the tile's end (both ends found by bucket_end)
     const uint64_t t0 = static_cast<uint64_t>(blockIdx.x) * kBTile;
     const uint64_t te = min(n, t0 + kBTile);
     const uint32_t b_prev = t0 ? bucket_of(keys[t0 - 1]) : 0xffffffffu;
     const uint32_t b_last = bucket_of(keys[te - 1]);
     __syncthreads();
-    for (uint64_t r0 = t0;; r0 += kThreads * kBPer) {  // uniform trip count (s_more)
+    // owned range [s0, s1): from the end of the bucket running into the tile
+    // (if any) to the end of the tile's last bucket
+    __shared__ uint32_t s_tmp[1];
+    if (b_prev == b_last && t0) return;  // the whole tile lies in a bucket owned by an earlier workgroup
+    const uint64_t s0 = t0 && b_prev != 0xffffffffu ? bucket_end(keys, n, t0, b_prev, s_tmp) : t0;
+    const uint64_t s1 = te < n ? bucket_end(keys, n, te, b_last, s_tmp) : n;
+    for (uint64_t r0 = s0; r0 < s1; r0 += kThreads * kBPer) {  // uniform trip count
         uint64_t k[kBPer];
         uint32_t v[kBPer], slot[kBPer];
         bool mine[kBPer], ok[kBPer];
 #pragma unroll
         for (uint32_t u = 0; u < kBPer; ++u) {
             const uint64_t j = r0 + u * kThreads + threadIdx.x;
-            k[u] = j < n ? keys[j] : 0ull;
-            v[u] = (VALS && j < n) ? vals[j] : 0u;
-            ok[u] = j < n;
+            ok[u] = j < s1;
+            k[u] = ok[u] ? keys[j] : 0ull;
+            v[u] = (VALS && ok[u]) ? vals[j] : 0u;
         }
-        bool any_beyond = false;
-        uint64_t mx[kBPer];  // mix(word): top 16 bits = bucket, low bits = set slot
-#pragma unroll
-        for (uint32_t u = 0; u < kBPer; ++u) {
-            const uint64_t j = r0 + u * kThreads + threadIdx.x;
-            mx[u] = mix64(k[u]);
-            if (!ok[u]) continue;
-            const uint32_t b = static_cast<uint32_t>(mx[u] >> 48);
-            if (j < te) {
-                ok[u] = b != b_prev || b_prev == 0xffffffffu;  // leading keys of an earlier bucket: not ours
-            } else {
-                ok[u] = b == b_last && b_last != b_prev;       // the rest of our last bucket
-                any_beyond |= ok[u];
-            }
-        }
+        uint64_t mx[kBPer];  // mix(word): low bits = set slot
         uint32_t nok = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < kBPer; ++u) nok += ok[u] ? 1u : 0u;
-        __syncthreads();  // every thread has read the previous round's s_more
-        if (threadIdx.x == 0) s_more = 0;
-        __syncthreads();
-        if (any_beyond) s_more = 1;
+        for (uint32_t u = 0; u < kBPer; ++u) {
+            mx[u] = mix64(k[u]);
+            nok += ok[u] ? 1u : 0u;
+        }
         if (nok) atomicAdd(&s_ins, nok);
         __syncthreads();
         if (s_ins > cap) {  // the set cannot hold this workgroup's keys: the sorted path
@@ -619,11 +640,6 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
                 if (ok[u] && !mine[u] && !key_equal(ks, ids[slot[u]], v[u])) atomicOr(overflow, 1u);
         }
         __syncthreads();
-        // go on: inside the tile; or this round reached its end and the last
-        // bucket may continue past it; or this round found more of that bucket
-        const bool reached_end = r0 < te && r0 + kThreads * kBPer >= te;
-        const bool more = r0 + kThreads * kBPer < te || s_more || (reached_end && te < n && b_last != b_prev);
-        if (!more) break;
     }
     for (uint32_t j = threadIdx.x; j < nj_lds; j += kThreads)
         if (jc[j]) atomicAdd(&counts[j], static_cast<unsigned long long>(jc[j]));
