@@ -271,8 +271,11 @@ typedef struct {
 typedef struct {
     uint64_t keys;        /* keys gathered and sorted (all jobs) */
     uint64_t collisions;  /* equal 64-bit words holding different strings (recounted on the host) */
-    double device_ms;     /* HIP-event time: gather + radix sort + unique */
+    double device_ms;     /* HIP-event time of the device part */
+    uint32_t path;        /* SB_DEDUP_WINDOWS (one read per key), SB_DEDUP_BUCKETS, SB_DEDUP_RADIX */
+    uint32_t windows;     /* window workgroups launched (window path) */
 } sb_dedup_stats;
+enum { SB_DEDUP_WINDOWS = 0, SB_DEDUP_BUCKETS = 1, SB_DEDUP_RADIX = 2 };
 
 /* unique[i] / status[i] per job; stats optional */
 int sb_dedup_count(sb_store *s, const sb_dedup_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,

@@ -558,7 +558,19 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.dk.hash = dev_upload(s, dk_hash);
     {
         std::vector<KBody> body(dk_hash.size());
-        for (size_t k = 0; k < body.size(); ++k) body[k] = KBody{dk_tail[k], dk_pos[k], 0};
+        s.h_dk_disp.clear();
+        for (size_t k = 0; k < body.size(); ++k) {
+            const uint64_t t = dk_tail[k];
+            uint32_t c0 = 0x100;  // first tail byte (none: 0x100)
+            if (t & kTailBlob) {
+                if ((t >> 40) & 0xffff) c0 = dk_blob[t & ((1ull << 40) - 1)];
+            } else if (t >> 56) {
+                c0 = static_cast<uint32_t>(t & 0xff);
+            }
+            const bool disp = c0 >= '0' && c0 <= '9';
+            body[k] = KBody{t, dk_pos[k], disp ? kKeyDisplaced : 0u};
+            if (disp) s.h_dk_disp.push_back(static_cast<uint32_t>(k));
+        }
         s.dk.body = dev_upload(s, body);
     }
     s.dk.blob = dev_upload(s, dk_blob);
@@ -1592,11 +1604,192 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
     dedup_run(s, segs, n, nj, unique, status, stats);
 }
 
-// the device part of duplicateVariantSearch over planned key runs: gather,
-// radix sort, adjacent-unique (+ host recount of 64-bit word collisions)
+// ---- window dedup planning (devtypes.hpp KWin)
+// A key string's leading decimal run P is a function of the string, so equal
+// strings share P.  For a key whose tail does not start with a digit P is its
+// POS, and every key run of a job is POS-sorted: cutting the job's runs at
+// POS boundaries into windows of about kWinTarget keys partitions its
+// distinct strings.  Displaced keys (tail starts with a digit, P > POS) join
+// the window holding P as one-key side pieces; one whose P lies in no window
+// (or starts with '0', or exceeds 32 bits) can only equal other such keys
+// (no run key has that POS) and is counted on the host by its string.
+struct WinPlan {
+    std::vector<KWin> wins;
+    std::vector<KPiece> pieces;
+    std::vector<uint64_t> far;  // per job: distinct keys outside every window
+};
+
+bool key_effective_pos(const sb_store &s, uint32_t k, uint64_t &P) {
+    const std::string str = key_string(s, k);
+    if (str.empty() || str[0] == '0') return false;
+    uint64_t v = 0;
+    for (char c : str) {
+        if (c < '0' || c > '9') break;
+        v = v * 10 + static_cast<uint64_t>(c - '0');
+        if (v > 0xffffffffull) return false;
+    }
+    P = v;
+    return true;
+}
+
+bool plan_windows(const sb_store &s, const std::vector<KSeg> &segs, size_t nj, WinPlan &P) {
+    uint32_t kTarget = 2048;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
+    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) kTarget = std::max(1, std::min(2048, std::atoi(e)));
+    constexpr uint64_t kSpan = (1ull << kWinSpanBits) - 2;
+    if (s.n_keys >= 0x80000000ull) return false;
+    P.far.assign(nj, 0);
+    std::vector<char> seen(nj, 0);
+    const std::vector<uint32_t> &pos = s.h_dk_pos;
+    for (size_t g0 = 0; g0 < segs.size();) {
+        const uint32_t job = segs[g0].job;
+        size_t g1 = g0 + 1;
+        while (g1 < segs.size() && segs[g1].job == job) ++g1;
+        if (seen[job]) return false;  // a job's runs are not contiguous
+        seen[job] = 1;
+        const size_t m = g1 - g0;
+        if (m > kWinPieces / 2) return false;  // many short runs (strict-mode region files): the sorted path
+        std::vector<uint32_t> cur(m), end(m);
+        for (size_t r = 0; r < m; ++r) {
+            cur[r] = static_cast<uint32_t>(segs[g0 + r].key_lo);
+            end[r] = static_cast<uint32_t>(segs[g0 + r].key_lo + segs[g0 + r].n);
+        }
+        std::vector<std::pair<uint64_t, uint32_t>> side;
+        std::vector<std::string> far;
+        for (size_t r = 0; r < m; ++r)
+            for (auto it = std::lower_bound(s.h_dk_disp.begin(), s.h_dk_disp.end(), cur[r]);
+                 it != s.h_dk_disp.end() && *it < end[r]; ++it) {
+                uint64_t p = 0;
+                if (key_effective_pos(s, *it, p)) side.emplace_back(p, *it);
+                else far.push_back(key_string(s, *it));
+            }
+        std::sort(side.begin(), side.end());
+        size_t si = 0;
+        auto lb = [&](size_t r, uint64_t p) -> uint32_t {
+            if (p > 0xffffffffull) return end[r];
+            return static_cast<uint32_t>(
+                std::lower_bound(pos.begin() + cur[r], pos.begin() + end[r], static_cast<uint32_t>(p)) - pos.begin());
+        };
+        for (;;) {
+            uint64_t p0 = ~0ull;
+            uint32_t act = 0;
+            for (size_t r = 0; r < m; ++r)
+                if (cur[r] < end[r]) {
+                    p0 = std::min<uint64_t>(p0, pos[cur[r]]);
+                    ++act;
+                }
+            if (!act) break;
+            while (si < side.size() && side[si].first < p0) far.push_back(key_string(s, side[si++].second));
+            // grow [p0, p1) in up to three steps: each run may add budget / act keys
+            uint64_t p1 = p0;
+            uint32_t budget = kTarget;
+            for (int it = 0; it < 3 && budget >= std::min<uint32_t>(64, kTarget); ++it) {
+                const uint32_t per = std::max<uint32_t>(1, budget / act);
+                uint64_t cand = p0 + kSpan;
+                for (size_t r = 0; r < m; ++r) {
+                    if (cur[r] >= end[r]) continue;
+                    const uint64_t idx = static_cast<uint64_t>(lb(r, p1)) + per;
+                    if (idx < end[r]) cand = std::min<uint64_t>(cand, pos[idx]);
+                }
+                if (cand <= p1) break;
+                p1 = cand;
+                uint64_t cnt = 0;
+                for (size_t r = 0; r < m; ++r) cnt += lb(r, p1) - cur[r];
+                budget = cnt < kTarget ? kTarget - static_cast<uint32_t>(cnt) : 0;
+            }
+            if (p1 == p0) p1 = p0 + 1;  // one POS holds more than a share of the window
+            KWin w{static_cast<uint32_t>(P.pieces.size()), 0, job, static_cast<uint32_t>(p0)};
+            uint64_t total = 0;
+            for (size_t r = 0; r < m; ++r) {
+                const uint32_t e = lb(r, p1);
+                if (e > cur[r]) {
+                    P.pieces.push_back(KPiece{cur[r], e - cur[r]});
+                    total += e - cur[r];
+                    cur[r] = e;
+                }
+            }
+            for (; si < side.size() && side[si].first < p1; ++si) {
+                P.pieces.push_back(KPiece{side[si].second, 1u | 0x80000000u});
+                ++total;
+            }
+            w.npieces = static_cast<uint32_t>(P.pieces.size()) - w.piece_lo;
+            if (total > kWinCap || w.npieces > kWinPieces) return false;  // a pile-up: the sorted path
+            P.wins.push_back(w);
+        }
+        for (; si < side.size(); ++si) far.push_back(key_string(s, side[si].second));
+        std::sort(far.begin(), far.end());
+        P.far[job] = static_cast<uint64_t>(std::unique(far.begin(), far.end()) - far.begin());
+        g0 = g1;
+    }
+    return true;
+}
+
+struct WinWs {
+    DevMem wins, pieces, counts, overflow;
+};
+
+// the window path: true when it answered every job (counts in unique[])
+bool dedup_window_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique,
+                      const int32_t *status, sb_dedup_stats *stats) {
+    WinPlan P;
+    if (!plan_windows(s, segs, nj, P)) return false;
+    HIP_OK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    if (!s.win_ws) s.win_ws = std::shared_ptr<void>(new WinWs, [](void *w) { delete static_cast<WinWs *>(w); });
+    WinWs &W = *static_cast<WinWs *>(s.win_ws.get());
+    const uint32_t nw = static_cast<uint32_t>(P.wins.size());
+    W.wins.reserve(std::max<size_t>(nw, 1) * sizeof(KWin));
+    W.pieces.reserve(std::max<size_t>(P.pieces.size(), 1) * sizeof(KPiece));
+    W.counts.reserve(std::max<size_t>(nj, 1) * 8);
+    W.overflow.reserve(4);
+    if (nw) {
+        HIP_OK(hipMemcpyAsync(W.wins.p, P.wins.data(), nw * sizeof(KWin), hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(W.pieces.p, P.pieces.data(), P.pieces.size() * sizeof(KPiece), hipMemcpyHostToDevice, st));
+    }
+    HIP_OK(hipMemsetAsync(W.counts.p, 0, std::max<size_t>(nj, 1) * 8, st));
+    HIP_OK(hipMemsetAsync(W.overflow.p, 0, 4, st));
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipEventRecord(e0, st));
+    launch_window_dedupe(s.dk, W.wins.as<KWin>(), nw, W.pieces.as<KPiece>(), W.counts.as<unsigned long long>(),
+                         W.overflow.as<uint32_t>(), st);
+    HIP_OK(hipEventRecord(e1, st));
+    HIP_OK(hipGetLastError());
+    std::vector<uint64_t> cnt(std::max<size_t>(nj, 1));
+    uint32_t ovf = 0;
+    HIP_OK(hipMemcpyAsync(cnt.data(), W.counts.p, cnt.size() * 8, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(&ovf, W.overflow.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    float ms = 0;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (ovf) return false;
+    for (size_t j = 0; j < nj; ++j) unique[j] = status[j] ? 0 : cnt[j] + P.far[j];
+    if (stats) {
+        stats->keys = n;
+        stats->collisions = 0;
+        stats->device_ms = ms;
+        stats->path = SB_DEDUP_WINDOWS;
+        stats->windows = nw;
+    }
+    return true;
+}
+
+// the device part of duplicateVariantSearch over planned key runs: windows
+// (one read of every key), else gather, radix sort, adjacent-unique (+ host
+// recount of 64-bit word collisions)
 void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique, int32_t *status,
                sb_dedup_stats *stats, bool force_radix) {
     if (n >= 0xffffffffull) throw Error(SB_EINVAL, "dedup batch exceeds 2^32 keys; split it");
+    {
+        // SBEACON_DEDUP_EXACT=bucket / radix (tests, A/B) skip the window path
+        const char *exm = std::getenv("SBEACON_DEDUP_EXACT");
+        const bool hash_hook = std::getenv("SBEACON_DEDUP_HASH_BITS") != nullptr;
+        if (!force_radix && !hash_hook && !(exm && (exm[0] == 'r' || exm[0] == 'b')) &&
+            dedup_window_run(s, segs, n, nj, unique, status, stats))
+            return;
+    }
     uint32_t job_bits = 0;
     while ((1ull << job_bits) < nj) ++job_bits;
     uint64_t mask = ~0ull;
@@ -1758,6 +1951,8 @@ void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj
         stats->keys = n;
         stats->collisions = nc;
         stats->device_ms = ms;
+        stats->path = bucket ? SB_DEDUP_BUCKETS : SB_DEDUP_RADIX;
+        stats->windows = 0;
     }
 }
 

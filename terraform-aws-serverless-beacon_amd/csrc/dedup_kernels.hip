@@ -645,6 +645,165 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
         if (jc[j]) atomicAdd(&counts[j], static_cast<unsigned long long>(jc[j]));
 }
 
+// ------------------------------------------------------------- window dedupe
+// One workgroup per host-planned window (devtypes.hpp KWin): its keys are
+// read ONCE from the store (16 B body; the 8 B hash only for keys outside
+// the exact class) and counted with two LDS hash sets — 32-bit exact words
+// (P - p0) << 6 | c1 c2, and 64-bit string hashes whose repeats are confirmed
+// on the key strings.  No gather stream, no radix pass: 16 B/key + 8 B per
+// hashed key.  Any condition the sets cannot take (more hashed keys than
+// their set holds, a hash equal to the empty marker, two strings under one
+// hash) raises *overflow and the host recounts the call on the sorted path.
+constexpr uint32_t kXSlots = 4096;  // exact set (16 KB), kWinCap keys at most
+constexpr uint32_t kHSlots = 1024;  // hashed set (8 KB + 4 KB ids)
+constexpr uint32_t kHCap = 768;
+constexpr uint32_t kWPer = kWinCap / kThreads;
+static_assert(kWPer * kThreads == kWinCap, "window keys per thread");
+static_assert(kWinPieces == 64, "one wave scans the pieces");
+
+__global__ __launch_bounds__(kThreads) void window_dedupe_kernel(KStore ks, const KWin *wins, const KPiece *pieces,
+                                                                 unsigned long long *counts, uint32_t *overflow) {
+    __shared__ uint32_t xset[kXSlots];
+    __shared__ unsigned long long hset[kHSlots];
+    __shared__ uint32_t hid[kHSlots];
+    __shared__ uint32_t s_pre[kWinPieces + 1], s_klo[kWinPieces];
+    __shared__ unsigned long long s_side;
+    __shared__ uint32_t s_fresh, s_nh;
+    const KWin W = wins[blockIdx.x];
+    const int lane = threadIdx.x & 63;
+    for (uint32_t i = threadIdx.x; i < kXSlots; i += kThreads) xset[i] = ~0u;
+    for (uint32_t i = threadIdx.x; i < kHSlots; i += kThreads) hset[i] = ~0ull;
+    if (threadIdx.x < 64) {  // wave 0: the pieces' inclusive prefix
+        uint32_t len = 0, klo = 0;
+        bool side = false;
+        if (static_cast<uint32_t>(lane) < W.npieces) {
+            const KPiece p = pieces[W.piece_lo + lane];
+            klo = p.key_lo;
+            len = p.n & 0x7fffffffu;
+            side = (p.n >> 31) != 0;
+        }
+        uint32_t inc = len;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        const uint64_t sm = __ballot(side);
+        s_pre[lane + 1] = inc;
+        s_klo[lane] = klo;
+        if (lane == 0) {
+            s_pre[0] = 0;
+            s_side = sm;
+            s_fresh = 0;
+            s_nh = 0;
+        }
+    }
+    __syncthreads();
+    const uint32_t np = W.npieces, total = s_pre[np];
+    const uint64_t sidem = s_side;
+    // every body load of the window first (key u = u * kThreads + tid)
+    KBody b[kWPer];
+    uint32_t kid[kWPer];
+    uint32_t okm = 0, sdm = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kWPer; ++u) {
+        const uint32_t f = u * kThreads + threadIdx.x;
+        kid[u] = 0;
+        b[u] = KBody{0, 0, 0};
+        if (f < total) {
+            uint32_t p = 0;  // the last piece starting at or before f
+#pragma unroll
+            for (uint32_t st = 32; st; st >>= 1)
+                if (p + st < np && s_pre[p + st] <= f) p += st;
+            kid[u] = s_klo[p] + (f - s_pre[p]);
+            b[u] = ks.body[kid[u]];
+            okm |= 1u << u;
+            if ((sidem >> p) & 1ull) sdm |= 1u << u;
+        }
+    }
+    // classes: displaced keys read from a run are counted in their P window
+    // (as a side piece) instead; exact words; the rest hashed
+    uint32_t xw[kWPer];
+    uint32_t em = 0, hm = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kWPer; ++u) {
+        xw[u] = 0;
+        if (!((okm >> u) & 1u)) continue;
+        if ((b[u].flags & kKeyDisplaced) && !((sdm >> u) & 1u)) continue;
+        uint64_t rel = 0;
+        const uint32_t code = exact_word(b[u], W.p0, kWinSpanBits, &rel);
+        if (code) {
+            xw[u] = (static_cast<uint32_t>(rel) << 6) | code;
+            em |= 1u << u;
+        } else {
+            hm |= 1u << u;
+        }
+    }
+    unsigned long long hv[kWPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kWPer; ++u) hv[u] = ((hm >> u) & 1u) ? ks.hash[kid[u]] : 0ull;
+    uint32_t fresh = 0;
+#pragma unroll
+    for (uint32_t u = 0; u < kWPer; ++u) {
+        if (!((em >> u) & 1u)) continue;
+        uint32_t h = (xw[u] * 0x9E3779B1u) >> (32 - 12);
+        static_assert(kXSlots == 1u << 12, "exact set slots");
+        for (uint32_t probe = 0; probe < kXSlots; ++probe) {
+            const uint32_t was = atomicCAS(&xset[h], ~0u, xw[u]);
+            if (was == ~0u) {
+                ++fresh;
+                break;
+            }
+            if (was == xw[u]) break;
+            h = (h + 1) & (kXSlots - 1);
+        }
+    }
+    const uint32_t nh = static_cast<uint32_t>(__popc(hm));
+    if (nh) atomicAdd(&s_nh, nh);
+    __syncthreads();
+    if (s_nh) {  // workgroup-uniform
+        if (s_nh > kHCap) {
+            if (threadIdx.x == 0) atomicOr(overflow, 1u);
+            return;
+        }
+        uint32_t mine = 0, slot[kWPer];
+#pragma unroll
+        for (uint32_t u = 0; u < kWPer; ++u) {
+            slot[u] = 0;
+            if (!((hm >> u) & 1u)) continue;
+            if (hv[u] == ~0ull) {
+                atomicOr(overflow, 1u);
+                continue;
+            }
+            uint32_t h = static_cast<uint32_t>(hv[u]) & (kHSlots - 1);
+            unsigned long long was = 0;
+            for (uint32_t probe = 0; probe < kHSlots; ++probe) {
+                was = atomicCAS(&hset[h], ~0ull, hv[u]);
+                if (was == ~0ull || was == hv[u]) break;
+                h = (h + 1) & (kHSlots - 1);
+            }
+            slot[u] = h;
+            if (was == ~0ull) {
+                mine |= 1u << u;
+                ++fresh;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kWPer; ++u)
+            if ((mine >> u) & 1u) hid[slot[u]] = kid[u];
+        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kWPer; ++u)
+            if (((hm & ~mine) >> u) & 1u && hv[u] != ~0ull && !key_equal(ks, hid[slot[u]], kid[u]))
+                atomicOr(overflow, 1u);
+    }
+    for (int d = 32; d >= 1; d >>= 1) fresh += __shfl_xor(fresh, d, 64);
+    if (lane == 0 && fresh) atomicAdd(&s_fresh, fresh);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_fresh) atomicAdd(&counts[W.job], static_cast<unsigned long long>(s_fresh));
+}
+
 uint32_t tiles_of(uint64_t n) { return static_cast<uint32_t>((n + kTile - 1) / kTile); }
 
 void exclusive_scan(uint32_t *a, uint64_t m, uint32_t *bsum, hipStream_t s) {
@@ -722,6 +881,12 @@ int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1,
         bucket_dedupe_kernel<false, kBSlots><<<nb, kThreads, 0, s>>>(keys, nullptr, n, ks, job_shift, njl, counts, overflow,
                                                                      cap, dbg);
     return r;
+}
+
+void launch_window_dedupe(const KStore &ks, const KWin *wins, uint32_t nw, const KPiece *pieces,
+                          unsigned long long *counts, uint32_t *overflow, hipStream_t s) {
+    if (!nw) return;
+    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, wins, pieces, counts, overflow);
 }
 
 uint32_t dedup_unique_blocks(uint64_t n) { return n ? tiles_of(n) : 0; }

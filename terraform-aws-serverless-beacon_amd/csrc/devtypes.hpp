@@ -381,8 +381,27 @@ inline constexpr int kTailInlineMax = 7;
 struct alignas(16) KBody {  // what the equality check reads: one 16-byte load
     uint64_t tail;
     uint32_t pos;
-    uint32_t pad;
+    uint32_t flags;  // kKeyDisplaced
 };
+// the tail starts with a decimal digit: the string's leading digit run (its
+// "effective position" P) is longer than decimal(pos), so the key is counted
+// in the window of P, not of pos (window dedup)
+inline constexpr uint32_t kKeyDisplaced = 1u;
+
+// Window dedup (sb_dedup_count): a job's keys partitioned by effective
+// position P into windows [p0, p1) of at most kWinCap keys.  Keys with equal
+// strings have equal P, so each window is deduplicated on its own.  A window
+// = pieces of store keys; a piece is a POS-sorted run's part inside the window
+// or (n bit 31) one displaced key whose P lies in it.
+struct KWin {
+    uint32_t piece_lo, npieces, job, p0;
+};
+struct KPiece {
+    uint32_t key_lo, n;
+};
+inline constexpr uint32_t kWinCap = 3072;    // keys per window (LDS sets sized for it)
+inline constexpr uint32_t kWinPieces = 64;   // pieces per window
+inline constexpr uint32_t kWinSpanBits = 26; // p1 - p0 < 2^26 - 1: exact words fit 32 bits
 
 struct KStore {
     const uint64_t *hash;

@@ -130,6 +130,7 @@ struct sb_store {
     hipStream_t stream = nullptr;
     std::mutex mu;  // serialises batches on this device
     std::shared_ptr<void> dedup_ws;      // dedup scratch (api.cpp DedupWs), reused across calls
+    std::shared_ptr<void> win_ws;        // window-dedup scratch (api.cpp WinWs)
     std::shared_ptr<void> summarise_ws;  // summariseSlice scratch (api.cpp SumWs)
     std::vector<sb::VcfData> vcfs;  // metadata (columns are moved to the globals below)
     std::unordered_map<std::string, uint32_t> vcf_by_location;
@@ -152,6 +153,7 @@ struct sb_store {
     // duplicateVariantSearch keys (global indexing): planning + collision fixup
     uint64_t n_keys = 0;
     std::vector<uint32_t> h_dk_pos, h_dk_lo, h_dk_bad;
+    std::vector<uint32_t> h_dk_disp;  // displaced keys (tail starts with a digit), sorted
     std::vector<uint64_t> h_dk_tail;
     std::vector<uint8_t> h_dk_blob;
     // device image

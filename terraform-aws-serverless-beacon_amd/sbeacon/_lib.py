@@ -90,7 +90,11 @@ class DedupFileJob(C.Structure):
 
 
 class DedupStats(C.Structure):
-    _fields_ = [('keys', C.c_uint64), ('collisions', C.c_uint64), ('device_ms', C.c_double)]
+    _fields_ = [('keys', C.c_uint64), ('collisions', C.c_uint64), ('device_ms', C.c_double),
+                ('path', C.c_uint32), ('windows', C.c_uint32)]
+
+
+DEDUP_PATHS = ('windows', 'buckets', 'radix')
 
 
 # every exported symbol of include/sbeacon.h: name -> (restype, argtypes)

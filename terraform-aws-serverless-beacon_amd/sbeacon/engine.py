@@ -273,7 +273,8 @@ class Store:
                                    'rejects (the reference summariseSlice throws)') if status[i] else uniq[i]
                for i in range(n)]
         if with_stats:
-            return res, {'keys': st.keys, 'collisions': st.collisions, 'device_ms': st.device_ms}
+            return res, {'keys': st.keys, 'collisions': st.collisions, 'device_ms': st.device_ms,
+                         'path': _lib.DEDUP_PATHS[st.path], 'windows': st.windows}
         return res
 
     def dedup_counts_files(self, jobs, *, with_stats=False):
@@ -313,7 +314,8 @@ class Store:
             else:
                 res.append(uniq[i])
         if with_stats:
-            return res, {'keys': st.keys, 'collisions': st.collisions, 'device_ms': st.device_ms}
+            return res, {'keys': st.keys, 'collisions': st.collisions, 'device_ms': st.device_ms,
+                         'path': _lib.DEDUP_PATHS[st.path], 'windows': st.windows}
         return res
 
     def contigs(self, location) -> list[str]:

@@ -103,23 +103,50 @@ def check(texts, jobs, got):
             assert g == e, (j, g, e)
 
 
-@pytest.mark.parametrize('exact', ['bucket', 'radix', 'overflow'])
+@pytest.mark.parametrize('exact', ['window', 'window_small', 'bucket', 'radix', 'overflow'])
 def test_dedup_batch_vs_oracle(texts, store, monkeypatch, exact):
-    """exact stream by hash buckets (default), by the full radix sort, and
-    by buckets whose hash sets 'overflow' (a cap of 4 keys per workgroup):
-    the radix recount must give the same answers."""
+    """windows (default: each job's runs cut by effective position, one read
+    of every key; window_small: windows of ~3 keys, so displaced keys land in
+    other windows than their POS and in the gaps between them), the exact
+    stream by hash buckets, by the full radix sort, and by buckets whose hash
+    sets 'overflow' (a cap of 4 keys per workgroup): the same answers."""
     if exact == 'radix':
         monkeypatch.setenv('SBEACON_DEDUP_EXACT', 'radix')
+    elif exact == 'bucket':
+        monkeypatch.setenv('SBEACON_DEDUP_EXACT', 'bucket')
     elif exact == 'overflow':
+        monkeypatch.setenv('SBEACON_DEDUP_EXACT', 'bucket')
         monkeypatch.setenv('SBEACON_DEDUP_BUCKET_CAP', '4')
+    elif exact == 'window_small':
+        monkeypatch.setenv('SBEACON_DEDUP_WIN_TARGET', '3')
     rng = random.Random(11)
     jobs = random_jobs(texts, rng, 300)
     got, st = store.dedup_counts(jobs, with_stats=True)
     check(texts, jobs, got)
     assert st['keys'] > 0
-    # a single-job call agrees with the batched sort
+    assert st['path'] == {'radix': 'radix', 'bucket': 'buckets', 'overflow': 'radix'}.get(exact, 'windows')
+    if exact == 'window_small':
+        assert st['windows'] > st['keys'] // 8
+    # a single-job call agrees with the batched call
     for j, g in list(zip(jobs, got))[:20]:
         assert store.dedup_counts([j]) == [g]
+
+
+def test_window_pileup_takes_the_sorted_path(monkeypatch):
+    """One POS holding more keys than a window (3,072) cannot be cut: the
+    call is answered by the bucket / radix path, with the same count."""
+    from oracle.oracle import dedup_count
+    from sbeacon.engine import Store
+    rows = []
+    for i in range(3200):  # 3,200 distinct multi-base REFs at one POS
+        ref = ''.join('ACGT'[(i >> (2 * k)) & 3] for k in range(6))
+        rows.append(f'22\t500\t.\t{ref}\tA\t.\t.\tAC=1;AN=2\tGT\t0|1\t0|0\n')
+    t = HEADER + ''.join(rows).encode() + b'22\t501\t.\tA\tC\t.\t.\tAC=1;AN=2\tGT\t0|1\t0|0\n'
+    st = Store.build([('pile.vcf.gz', t)], device=0)
+    got, stats = st.dedup_counts([(['pile.vcf.gz'], '22', 0, 10**9), (['pile.vcf.gz'], '22', 501, 501)],
+                                 with_stats=True)
+    assert stats['path'] != 'windows'
+    assert got == [dedup_count([t], '22', 0, 10**9), 1]
 
 
 def test_decimal_concat_collisions_are_counted_as_the_reference_does(texts, store):
