@@ -47,6 +47,7 @@ def main():
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--threads', type=int, default=16)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--only', choices=['summarise', 'dedup'], default=None)
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -75,8 +76,10 @@ def main():
         info = store.info()
         log(f'{len(files)} VCFs, {info["n_records"]} records, {info["device_bytes"] / 2**20:.0f} MiB HBM; '
             f'generate {t_gen:.1f} s, ingest {t_ingest:.1f} s')
-        summarise_line(args, store, files, plan_slices)
-        dedup_line(args, store, datasets, files)
+        if args.only != 'dedup':
+            summarise_line(args, store, files, plan_slices)
+        if args.only != 'summarise':
+            dedup_line(args, store, datasets, files)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -152,7 +155,10 @@ def dedup_line(args, store, datasets, files):
     dev, keys = [], 0
     t = time.perf_counter()
     for _ in range(args.steps):
+        t1 = time.perf_counter()
         res, st = store.dedup_counts(jobs, with_stats=True)
+        if os.environ.get('SBEACON_DEDUP_DEBUG'):
+            log(f'dedup call {1e3 * (time.perf_counter() - t1):.3f} ms')
         dev.append(st['device_ms'])
         keys = st['keys']
     wall = (time.perf_counter() - t) / args.steps
@@ -160,11 +166,19 @@ def dedup_line(args, store, datasets, files):
     ures, ust = store.dedup_counts(union, with_stats=True)
     ures, ust = store.dedup_counts(union, with_stats=True)
     alg = 8.0 * keys  # compulsory: one read of the 64-bit key stream
-    # implementation bytes (exact stream, ~97 % of keys, bucket path): gather
-    # (20 B/key) + two radix passes on the word's mix (24 B/key each: histogram
-    # read, rank read, scatter write) + the bucket hash-set pass (8 B/key); the
-    # hashed stream's 8 passes of 28 B/key over its ~3 % of keys on top
-    impl = 20.0 * keys + 2 * 24.0 * keys + 8.0 * keys + 0.03 * 8 * 28.0 * keys
+    if st['path'] == 'windows':
+        # implementation bytes: one 16 B body read per key + the 8 B hash of
+        # keys outside the exact class (~5 %) + 16 B per window descriptor;
+        # deferred displaced keys are noise
+        impl = 16.0 * keys + 8.0 * 0.05 * keys + 16.0 * st['windows']
+        kern = ('window_dedupe_kernel (one workgroup per POS window: one read of every key, LDS hash set) + '
+                'deferred_dedupe_kernel (displaced keys with a possible copy at a larger POS)')
+    else:
+        # exact stream, ~97 % of keys, bucket path: gather (20 B/key) + two
+        # radix passes on the word's mix (24 B/key each) + the bucket hash-set
+        # pass (8 B/key); the hashed stream's 8 passes of 28 B/key on top
+        impl = 20.0 * keys + 2 * 24.0 * keys + 8.0 * keys + 0.03 * 8 * 28.0 * keys
+        kern = 'gather + 2 mix-digit radix passes + bucket hash sets (exact stream); radix sort + unique (hashed stream)'
     achieved = alg / (dev_ms * 1e-3) / 1e9
     cpu = parity = None
     if not args.no_cpu_baseline:
@@ -186,12 +200,11 @@ def dedup_line(args, store, datasets, files):
         'dtype': 'uint64', 'data': 'synthetic config-4 cohort, sites-only BGZF',
         'config': {'workload': f'config4-dedup-{args.datasets}ds', 'jobs': len(jobs), 'keys': keys,
                    'unique_per_dataset_mean': sum(r for r in res if isinstance(r, int)) / max(len(res), 1)},
-        'device_ms_per_step': round(dev_ms, 4),
+        'device_ms_per_step': round(dev_ms, 4), 'path': st['path'], 'windows': st['windows'],
         'union': {'vcfs': len(files), 'keys': ust['keys'], 'unique': ures[0], 'device_ms': round(ust['device_ms'], 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
-                     'kernel': 'gather + 2 mix-digit radix passes + bucket hash sets (exact stream); radix sort + '
-                               'unique (hashed stream)', 'algorithmic_bytes_per_launch': alg,
+                     'kernel': kern, 'algorithmic_bytes_per_launch': alg,
                      'implementation_bytes_per_launch_upper_bound': impl,
                      'implementation_GBs': round(impl / (dev_ms * 1e-3) / 1e9, 1)},
         'cpu_baseline': cpu, 'parity_sample': parity}), flush=True)

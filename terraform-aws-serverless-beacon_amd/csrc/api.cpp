@@ -8,7 +8,9 @@
 // are formatted on the host from the store's allele blob in the reference's
 // exact format.
 #include <algorithm>
+#include <atomic>
 #include <array>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -558,7 +560,6 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.dk.hash = dev_upload(s, dk_hash);
     {
         std::vector<KBody> body(dk_hash.size());
-        s.h_dk_disp.clear();
         for (size_t k = 0; k < body.size(); ++k) {
             const uint64_t t = dk_tail[k];
             uint32_t c0 = 0x100;  // first tail byte (none: 0x100)
@@ -569,11 +570,14 @@ void upload_store(sb_builder &b, sb_store &s) {
             }
             const bool disp = c0 >= '0' && c0 <= '9';
             body[k] = KBody{t, dk_pos[k], disp ? kKeyDisplaced : 0u};
-            if (disp) s.h_dk_disp.push_back(static_cast<uint32_t>(k));
         }
         s.dk.body = dev_upload(s, body);
     }
+    dk_blob.resize(dk_blob.size() + 16, 0);  // padding: the device compares blob tails by aligned words
     s.dk.blob = dev_upload(s, dk_blob);
+    s.dk.lo = dev_upload(s, dk_lo);
+    s.dk.rpos = s.d.pos;
+    s.dk.bucket = s.d.bucket;
     s.n_keys = dk_hash.size();
     HIP_OK(hipStreamSynchronize(s.stream));
     s.h_dk_pos = std::move(dk_pos);
@@ -1557,12 +1561,13 @@ struct DedupWs {
 };
 
 void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique, int32_t *status,
-               sb_dedup_stats *stats, bool force_radix = false);
+               sb_dedup_stats *stats, bool force_radix = false, std::vector<KRun> *runs = nullptr);
 
 void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, int32_t *status,
            sb_dedup_stats *stats) {
     if (nj > (1u << 20)) throw Error(SB_EINVAL, "more than 2^20 dedup jobs in one call");
     std::vector<KSeg> segs;
+    std::vector<KRun> runs;  // parallel to segs (window path)
     uint64_t n = 0;
     for (size_t j = 0; j < nj; ++j) {
         const sb_dedup_job &J = jobs[j];
@@ -1593,145 +1598,188 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
             const uint32_t e = static_cast<uint32_t>(std::upper_bound(kb + klo, kb + khi, re) - kb);
             if (e > a) {
                 segs.push_back(KSeg{a, n, e - a, static_cast<uint32_t>(j), rs, 0});
+                const BucketIndex &bi = v.buckets[it->second];
+                runs.push_back(KRun{a, e, s.h_dk_pos[a], s.h_dk_pos[e - 1], sg.lo, sg.hi, bi.base, bi.shift, bi.off,
+                                    bi.n, static_cast<uint32_t>(j), 0, 0, {0, 0}});
                 n += e - a;
             }
         }
         if (status[j]) {  // drop the job's keys
             for (size_t g = seg0; g < segs.size(); ++g) n -= segs[g].n;
             segs.resize(seg0);
+            runs.resize(seg0);
         }
     }
-    dedup_run(s, segs, n, nj, unique, status, stats);
+    dedup_run(s, segs, n, nj, unique, status, stats, false, &runs);
 }
 
 // ---- window dedup planning (devtypes.hpp KWin)
-// A key string's leading decimal run P is a function of the string, so equal
-// strings share P.  For a key whose tail does not start with a digit P is its
-// POS, and every key run of a job is POS-sorted: cutting the job's runs at
-// POS boundaries into windows of about kWinTarget keys partitions its
-// distinct strings.  Displaced keys (tail starts with a digit, P > POS) join
-// the window holding P as one-key side pieces; one whose P lies in no window
-// (or starts with '0', or exceeds 32 bits) can only equal other such keys
-// (no run key has that POS) and is counted on the host by its string.
+// Every key run of a job is POS-sorted: cutting the job's runs at POS
+// boundaries into windows of about kWinTarget keys puts all keys of one
+// (string, POS) in one window.  runs[g] = segs[g]'s KRun (key range, POS
+// span, its segment's coarse POS index for the twin lookups).
 struct WinPlan {
     std::vector<KWin> wins;
     std::vector<KPiece> pieces;
-    std::vector<uint64_t> far;  // per job: distinct keys outside every window
+    const char *why = "";  // why the plan was declined (SBEACON_DEDUP_DEBUG)
 };
 
-bool key_effective_pos(const sb_store &s, uint32_t k, uint64_t &P) {
-    const std::string str = key_string(s, k);
-    if (str.empty() || str[0] == '0') return false;
-    uint64_t v = 0;
-    for (char c : str) {
-        if (c < '0' || c > '9') break;
-        v = v * 10 + static_cast<uint64_t>(c - '0');
-        if (v > 0xffffffffull) return false;
+// one job's windows (runs [g0, g1) of the call)
+bool plan_job_windows(const sb_store &s, const std::vector<KRun> &runs, size_t g0, size_t g1, uint32_t target,
+                      std::vector<KWin> &wins, std::vector<KPiece> &pieces, const char **why) {
+    constexpr uint64_t kSpan = (1ull << kWinSpanBits) - 2;
+    const std::vector<uint32_t> &pos = s.h_dk_pos;
+    const size_t m = g1 - g0;
+    if (m > kWinPieces) return *why = "runs", false;
+    const uint32_t job = runs[g0].job;
+    std::vector<uint32_t> cur(m), end(m), e(m);
+    uint32_t pmax = 0;
+    for (size_t r = 0; r < m; ++r) {
+        cur[r] = runs[g0 + r].key_lo;
+        end[r] = runs[g0 + r].key_hi;
+        pmax = std::max(pmax, runs[g0 + r].pos_hi);
     }
-    P = v;
+    // lower bound of x in run r at or after a, searched outward from the
+    // hint h (the runs of a job have similar densities, so the answer is
+    // usually a few keys from a + the window's share): galloping steps, then
+    // a binary search over the last one
+    auto lb = [&](size_t r, uint32_t a, uint64_t p, uint32_t h) -> uint32_t {
+        if (p > 0xffffffffull) return end[r];
+        const uint32_t x = static_cast<uint32_t>(p);
+        h = std::min(std::max(h, a), end[r]);
+        uint32_t lo, hi;  // answer in [lo, hi]
+        if (h > a && pos[h - 1] >= x) {  // at or before h - 1: gallop down
+            hi = h - 1;
+            uint32_t step = 8;
+            while (hi - a > step && pos[hi - step] >= x) {
+                hi -= step;
+                step *= 2;
+            }
+            lo = hi - a > step ? hi - step : a;
+        } else {  // at or after h: gallop up
+            lo = h;
+            uint32_t step = 8;
+            while (lo + step < end[r] && pos[lo + step] < x) {
+                lo += step;
+                step *= 2;
+            }
+            hi = static_cast<uint32_t>(std::min<uint64_t>(end[r], static_cast<uint64_t>(lo) + step));
+        }
+        return static_cast<uint32_t>(std::lower_bound(pos.begin() + lo, pos.begin() + hi, x) - pos.begin());
+    };
+    for (;;) {
+        uint64_t p0 = ~0ull;
+        uint32_t act = 0;
+        for (size_t r = 0; r < m; ++r)
+            if (cur[r] < end[r]) {
+                p0 = std::min<uint64_t>(p0, pos[cur[r]]);
+                ++act;
+            }
+        if (!act) break;
+        // grow [p0, p1) in up to three steps: each run may add budget / act
+        // keys; e[r] = lower bound of p1 in run r
+        uint64_t p1 = p0;
+        for (size_t r = 0; r < m; ++r) e[r] = cur[r];
+        uint32_t budget = target;
+        for (int it = 0; it < 3 && budget >= std::min<uint32_t>(64, target); ++it) {
+            const uint32_t per = std::max<uint32_t>(1, budget / act);
+            uint64_t cand = p0 + kSpan;
+            for (size_t r = 0; r < m; ++r) {
+                const uint64_t idx = static_cast<uint64_t>(e[r]) + per;
+                if (cur[r] < end[r] && idx < end[r]) cand = std::min<uint64_t>(cand, pos[idx]);
+            }
+            if (cand <= p1) break;
+            p1 = cand;
+            uint64_t cnt = 0;
+            for (size_t r = 0; r < m; ++r) {
+                e[r] = lb(r, e[r], p1, e[r] + per);
+                cnt += e[r] - cur[r];
+            }
+            budget = cnt < target ? target - static_cast<uint32_t>(cnt) : 0;
+        }
+        if (p1 == p0) {  // one POS holds more than a share of the window
+            p1 = p0 + 1;
+            for (size_t r = 0; r < m; ++r) e[r] = lb(r, cur[r], p1, cur[r]);
+        }
+        KWin w{static_cast<uint32_t>(pieces.size()), 0, job, static_cast<uint32_t>(p0), static_cast<uint32_t>(g0), pmax,
+               {0, 0}};
+        uint64_t total = 0;
+        for (size_t r = 0; r < m; ++r) {
+            if (e[r] > cur[r]) {
+                pieces.push_back(KPiece{cur[r], (e[r] - cur[r]) | (static_cast<uint32_t>(r) << 16)});
+                total += e[r] - cur[r];
+                cur[r] = e[r];
+            }
+        }
+        w.npieces = static_cast<uint32_t>(pieces.size()) - w.piece_lo;
+        if (total > kWinCap) return *why = "pile-up", false;  // the sorted path
+        wins.push_back(w);
+    }
     return true;
 }
 
-bool plan_windows(const sb_store &s, const std::vector<KSeg> &segs, size_t nj, WinPlan &P) {
-    uint32_t kTarget = 2048;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
-    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) kTarget = std::max(1, std::min(2048, std::atoi(e)));
-    constexpr uint64_t kSpan = (1ull << kWinSpanBits) - 2;
-    if (s.n_keys >= 0x80000000ull) return false;
-    P.far.assign(nj, 0);
+// Every job's windows; jobs planned on host threads.  runs[g] = segs[g]'s KRun.
+bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan &P) {
+    uint32_t target = 2048;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
+    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) target = std::max(1, std::min(2048, std::atoi(e)));
+    if (s.n_keys >= 0x80000000ull) return P.why = "2^31 keys", false;
+    std::vector<std::pair<size_t, size_t>> groups;  // each job's runs
     std::vector<char> seen(nj, 0);
-    const std::vector<uint32_t> &pos = s.h_dk_pos;
-    for (size_t g0 = 0; g0 < segs.size();) {
-        const uint32_t job = segs[g0].job;
+    for (size_t g0 = 0; g0 < runs.size();) {
         size_t g1 = g0 + 1;
-        while (g1 < segs.size() && segs[g1].job == job) ++g1;
-        if (seen[job]) return false;  // a job's runs are not contiguous
-        seen[job] = 1;
-        const size_t m = g1 - g0;
-        if (m > kWinPieces / 2) return false;  // many short runs (strict-mode region files): the sorted path
-        std::vector<uint32_t> cur(m), end(m);
-        for (size_t r = 0; r < m; ++r) {
-            cur[r] = static_cast<uint32_t>(segs[g0 + r].key_lo);
-            end[r] = static_cast<uint32_t>(segs[g0 + r].key_lo + segs[g0 + r].n);
+        while (g1 < runs.size() && runs[g1].job == runs[g0].job) ++g1;
+        if (seen[runs[g0].job]) return P.why = "job runs not contiguous", false;
+        seen[runs[g0].job] = 1;
+        for (size_t g = g0; g < g1; ++g) {
+            runs[g].run_lo = static_cast<uint32_t>(g0);
+            runs[g].nruns = static_cast<uint32_t>(g1 - g0);
         }
-        std::vector<std::pair<uint64_t, uint32_t>> side;
-        std::vector<std::string> far;
-        for (size_t r = 0; r < m; ++r)
-            for (auto it = std::lower_bound(s.h_dk_disp.begin(), s.h_dk_disp.end(), cur[r]);
-                 it != s.h_dk_disp.end() && *it < end[r]; ++it) {
-                uint64_t p = 0;
-                if (key_effective_pos(s, *it, p)) side.emplace_back(p, *it);
-                else far.push_back(key_string(s, *it));
-            }
-        std::sort(side.begin(), side.end());
-        size_t si = 0;
-        auto lb = [&](size_t r, uint64_t p) -> uint32_t {
-            if (p > 0xffffffffull) return end[r];
-            return static_cast<uint32_t>(
-                std::lower_bound(pos.begin() + cur[r], pos.begin() + end[r], static_cast<uint32_t>(p)) - pos.begin());
-        };
-        for (;;) {
-            uint64_t p0 = ~0ull;
-            uint32_t act = 0;
-            for (size_t r = 0; r < m; ++r)
-                if (cur[r] < end[r]) {
-                    p0 = std::min<uint64_t>(p0, pos[cur[r]]);
-                    ++act;
-                }
-            if (!act) break;
-            while (si < side.size() && side[si].first < p0) far.push_back(key_string(s, side[si++].second));
-            // grow [p0, p1) in up to three steps: each run may add budget / act keys
-            uint64_t p1 = p0;
-            uint32_t budget = kTarget;
-            for (int it = 0; it < 3 && budget >= std::min<uint32_t>(64, kTarget); ++it) {
-                const uint32_t per = std::max<uint32_t>(1, budget / act);
-                uint64_t cand = p0 + kSpan;
-                for (size_t r = 0; r < m; ++r) {
-                    if (cur[r] >= end[r]) continue;
-                    const uint64_t idx = static_cast<uint64_t>(lb(r, p1)) + per;
-                    if (idx < end[r]) cand = std::min<uint64_t>(cand, pos[idx]);
-                }
-                if (cand <= p1) break;
-                p1 = cand;
-                uint64_t cnt = 0;
-                for (size_t r = 0; r < m; ++r) cnt += lb(r, p1) - cur[r];
-                budget = cnt < kTarget ? kTarget - static_cast<uint32_t>(cnt) : 0;
-            }
-            if (p1 == p0) p1 = p0 + 1;  // one POS holds more than a share of the window
-            KWin w{static_cast<uint32_t>(P.pieces.size()), 0, job, static_cast<uint32_t>(p0)};
-            uint64_t total = 0;
-            for (size_t r = 0; r < m; ++r) {
-                const uint32_t e = lb(r, p1);
-                if (e > cur[r]) {
-                    P.pieces.push_back(KPiece{cur[r], e - cur[r]});
-                    total += e - cur[r];
-                    cur[r] = e;
-                }
-            }
-            for (; si < side.size() && side[si].first < p1; ++si) {
-                P.pieces.push_back(KPiece{side[si].second, 1u | 0x80000000u});
-                ++total;
-            }
-            w.npieces = static_cast<uint32_t>(P.pieces.size()) - w.piece_lo;
-            if (total > kWinCap || w.npieces > kWinPieces) return false;  // a pile-up: the sorted path
+        groups.emplace_back(g0, g1);
+        g0 = g1;
+    }
+    const size_t nt = std::min<size_t>(groups.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
+    std::vector<std::vector<KWin>> tw(groups.size());
+    std::vector<std::vector<KPiece>> tp(groups.size());
+    std::vector<const char *> why(groups.size(), nullptr);
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+        for (size_t q; (q = next.fetch_add(1)) < groups.size();) {
+            const char *w = nullptr;
+            if (!plan_job_windows(s, runs, groups[q].first, groups[q].second, target, tw[q], tp[q], &w)) why[q] = w;
+        }
+    };
+    std::vector<std::thread> th;
+    for (size_t t = 1; t < nt; ++t) th.emplace_back(work);
+    work();
+    for (auto &t : th) t.join();
+    for (size_t q = 0; q < groups.size(); ++q) {
+        if (why[q]) return P.why = why[q], false;
+        const uint32_t base = static_cast<uint32_t>(P.pieces.size());
+        for (KWin w : tw[q]) {
+            w.piece_lo += base;
             P.wins.push_back(w);
         }
-        for (; si < side.size(); ++si) far.push_back(key_string(s, side[si].second));
-        std::sort(far.begin(), far.end());
-        P.far[job] = static_cast<uint64_t>(std::unique(far.begin(), far.end()) - far.begin());
-        g0 = g1;
+        P.pieces.insert(P.pieces.end(), tp[q].begin(), tp[q].end());
     }
     return true;
 }
 
 struct WinWs {
-    DevMem wins, pieces, counts, overflow;
+    DevMem wins, pieces, runs, counts, overflow, list, n_list;
 };
 
 // the window path: true when it answered every job (counts in unique[])
-bool dedup_window_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique,
+bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t nj, uint64_t *unique,
                       const int32_t *status, sb_dedup_stats *stats) {
     WinPlan P;
-    if (!plan_windows(s, segs, nj, P)) return false;
+    const bool dbg = std::getenv("SBEACON_DEDUP_DEBUG") != nullptr;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
+    if (!plan_windows(s, runs, nj, P)) {
+        if (dbg) std::fprintf(stderr, "[sbeacon] dedup windows: plan declined (%s; %zu windows so far)\n", P.why, P.wins.size());
+        return false;
+    }
+    const double t_plan = since();
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
     if (!s.win_ws) s.win_ws = std::shared_ptr<void>(new WinWs, [](void *w) { delete static_cast<WinWs *>(w); });
@@ -1739,11 +1787,19 @@ bool dedup_window_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, si
     const uint32_t nw = static_cast<uint32_t>(P.wins.size());
     W.wins.reserve(std::max<size_t>(nw, 1) * sizeof(KWin));
     W.pieces.reserve(std::max<size_t>(P.pieces.size(), 1) * sizeof(KPiece));
+    W.runs.reserve(std::max<size_t>(runs.size(), 1) * sizeof(KRun));
     W.counts.reserve(std::max<size_t>(nj, 1) * 8);
     W.overflow.reserve(4);
+    // deferred displaced keys (10 POS <= the job's largest POS): a list of a
+    // quarter of the keys; a fuller list is an overflow (the sorted path)
+    const uint32_t cap = static_cast<uint32_t>(std::min<uint64_t>(n / 4 + 65536, 0xffffffffull));
+    W.list.reserve(static_cast<size_t>(cap) * 8);
+    W.n_list.reserve(4);
+    HIP_OK(hipMemsetAsync(W.n_list.p, 0, 4, st));
     if (nw) {
         HIP_OK(hipMemcpyAsync(W.wins.p, P.wins.data(), nw * sizeof(KWin), hipMemcpyHostToDevice, st));
         HIP_OK(hipMemcpyAsync(W.pieces.p, P.pieces.data(), P.pieces.size() * sizeof(KPiece), hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(W.runs.p, runs.data(), runs.size() * sizeof(KRun), hipMemcpyHostToDevice, st));
     }
     HIP_OK(hipMemsetAsync(W.counts.p, 0, std::max<size_t>(nj, 1) * 8, st));
     HIP_OK(hipMemsetAsync(W.overflow.p, 0, 4, st));
@@ -1751,7 +1807,8 @@ bool dedup_window_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, si
     HIP_OK(hipEventCreate(&e0));
     HIP_OK(hipEventCreate(&e1));
     HIP_OK(hipEventRecord(e0, st));
-    launch_window_dedupe(s.dk, W.wins.as<KWin>(), nw, W.pieces.as<KPiece>(), W.counts.as<unsigned long long>(),
+    launch_window_dedupe(s.dk, W.wins.as<KWin>(), nw, W.pieces.as<KPiece>(), W.runs.as<KRun>(),
+                         W.counts.as<unsigned long long>(), W.list.as<uint2>(), W.n_list.as<uint32_t>(), cap,
                          W.overflow.as<uint32_t>(), st);
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipGetLastError());
@@ -1764,8 +1821,14 @@ bool dedup_window_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, si
     HIP_OK(hipEventElapsedTime(&ms, e0, e1));
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    if (ovf) return false;
-    for (size_t j = 0; j < nj; ++j) unique[j] = status[j] ? 0 : cnt[j] + P.far[j];
+    if (dbg)
+        std::fprintf(stderr, "[sbeacon] dedup windows: %u windows, plan %.3f ms, all %.3f ms (device %.3f ms)\n", nw,
+                     t_plan, since(), ms);
+    if (ovf) {
+        if (dbg) std::fprintf(stderr, "[sbeacon] dedup windows: device overflow over %u windows\n", nw);
+        return false;
+    }
+    for (size_t j = 0; j < nj; ++j) unique[j] = status[j] ? 0 : cnt[j];
     if (stats) {
         stats->keys = n;
         stats->collisions = 0;
@@ -1780,14 +1843,14 @@ bool dedup_window_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, si
 // (one read of every key), else gather, radix sort, adjacent-unique (+ host
 // recount of 64-bit word collisions)
 void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique, int32_t *status,
-               sb_dedup_stats *stats, bool force_radix) {
+               sb_dedup_stats *stats, bool force_radix, std::vector<KRun> *runs) {
     if (n >= 0xffffffffull) throw Error(SB_EINVAL, "dedup batch exceeds 2^32 keys; split it");
     {
         // SBEACON_DEDUP_EXACT=bucket / radix (tests, A/B) skip the window path
         const char *exm = std::getenv("SBEACON_DEDUP_EXACT");
         const bool hash_hook = std::getenv("SBEACON_DEDUP_HASH_BITS") != nullptr;
-        if (!force_radix && !hash_hook && !(exm && (exm[0] == 'r' || exm[0] == 'b')) &&
-            dedup_window_run(s, segs, n, nj, unique, status, stats))
+        if (runs && !force_radix && !hash_hook && !(exm && (exm[0] == 'r' || exm[0] == 'b')) &&
+            dedup_window_run(s, *runs, n, nj, unique, status, stats))
             return;
     }
     uint32_t job_bits = 0;

@@ -648,39 +648,141 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
 // ------------------------------------------------------------- window dedupe
 // One workgroup per host-planned window (devtypes.hpp KWin): its keys are
 // read ONCE from the store (16 B body; the 8 B hash only for keys outside
-// the exact class) and counted with two LDS hash sets — 32-bit exact words
-// (P - p0) << 6 | c1 c2, and 64-bit string hashes whose repeats are confirmed
-// on the key strings.  No gather stream, no radix pass: 16 B/key + 8 B per
-// hashed key.  Any condition the sets cannot take (more hashed keys than
-// their set holds, a hash equal to the empty marker, two strings under one
-// hash) raises *overflow and the host recounts the call on the sorted path.
-constexpr uint32_t kXSlots = 4096;  // exact set (16 KB), kWinCap keys at most
-constexpr uint32_t kHSlots = 1024;  // hashed set (8 KB + 4 KB ids)
-constexpr uint32_t kHCap = 768;
+// the exact class) and counted in one LDS hash set of 64-bit entries:
+//   exact keys   (POS - p0) << 6 | c1 c2          (< 2^32: the string itself)
+//   hashed keys  1 << 63 | hash bits 13..62 << 12 | window-local key index
+// A hashed key meeting an entry with its hash bits is confirmed on the key
+// strings against the inserter (named by the entry's index).  Displaced keys
+// with 10 POS > the job's largest POS are hashed like any key; the other
+// displaced keys are deferred to deferred_dedupe_kernel (a list of (key, run)
+// pairs).  Two strings under one hash, or a full deferred list, raise
+// *overflow and the host recounts the call on the sorted path.  No gather
+// stream, no radix pass: 16 B/key + 8 B per hashed key.
+constexpr uint32_t kWSlots = 4096;  // 32 KB; kWinCap keys at most (load <= 0.75)
 constexpr uint32_t kWPer = kWinCap / kThreads;
 static_assert(kWPer * kThreads == kWinCap, "window keys per thread");
+static_assert(kWinCap < kWSlots, "window set load");
 static_assert(kWinPieces == 64, "one wave scans the pieces");
 
+// len bytes at blob offsets oa and ob equal?  Aligned 8-byte words (every
+// load of a 32-byte round issued first) funnel-shifted into place; the blob
+// is padded by 16 bytes, so the word past the last byte is readable.
+__device__ bool blob_equal(const uint8_t *__restrict__ blob, uint64_t oa, uint64_t ob, uint32_t len) {
+    const uint64_t *w = reinterpret_cast<const uint64_t *>(blob);
+    auto word_at = [&](uint64_t lo_w, uint64_t hi_w, uint32_t sh) {
+        return sh ? (lo_w >> (8 * sh)) | (hi_w << (64 - 8 * sh)) : lo_w;
+    };
+    for (uint32_t j = 0; j < len; j += 32) {
+        uint64_t wa[5], wb[5];
+        const uint64_t ia = (oa + j) >> 3, ib = (ob + j) >> 3;
+        const uint32_t nw = min(len - j, 32u);
+        const uint32_t na = static_cast<uint32_t>((((oa + j) & 7) + nw + 7) >> 3);
+        const uint32_t nb = static_cast<uint32_t>((((ob + j) & 7) + nw + 7) >> 3);
+#pragma unroll
+        for (uint32_t q = 0; q < 5; ++q) {
+            wa[q] = q < na ? w[ia + q] : 0ull;
+            wb[q] = q < nb ? w[ib + q] : 0ull;
+        }
+        const uint32_t sa = static_cast<uint32_t>((oa + j) & 7), sb = static_cast<uint32_t>((ob + j) & 7);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; ++q) {
+            if (8 * q >= nw) break;
+            uint64_t d = word_at(wa[q], wa[q + 1], sa) ^ word_at(wb[q], wb[q + 1], sb);
+            const uint32_t rem = nw - 8 * q;
+            if (rem < 8) d &= (1ull << (8 * rem)) - 1ull;
+            if (d) return false;
+        }
+    }
+    return true;
+}
+
+// two key bodies' strings equal (same POS: the tails; else the general
+// decimal-concatenation comparison)
+__device__ bool body_equal(const KStore &ks, const KBody &x, const KBody &y) {
+    if (x.pos == y.pos) {
+        if (x.tail == y.tail) return true;
+        if (!((x.tail & y.tail) & kTailBlob)) return false;  // inline vs other: different bytes or lengths
+        const uint32_t lx = static_cast<uint32_t>((x.tail >> 40) & 0xffff), ly = static_cast<uint32_t>((y.tail >> 40) & 0xffff);
+        return lx == ly && blob_equal(ks.blob, x.tail & ((1ull << 40) - 1), y.tail & ((1ull << 40) - 1), lx);
+    }
+    return key_equal_slow(ks, x, y);
+}
+
+__device__ bool key_equal_body(const KStore &ks, uint32_t a, const KBody &y) { return body_equal(ks, ks.body[a], y); }
+
+// byte j of a key's tail (j < its length)
+__device__ __forceinline__ uint32_t tail_byte(const KStore &ks, uint64_t t, uint32_t j) {
+    if (t & kTailBlob) return ks.blob[(t & ((1ull << 40) - 1)) + j];
+    return static_cast<uint32_t>(t >> (8 * j)) & 0xffu;
+}
+
+// a key of run R at POS X, with index below klim, holding y's string?
+__device__ bool run_has_equal(const KStore &ks, const KRun &R, uint64_t X, const KBody &y, uint32_t klim) {
+    if (X < R.pos_lo || X > R.pos_hi) return false;
+    // records of the segment with POS == X: bucket bracket + binary search
+    const uint64_t b = (X - R.b_base) >> R.b_shift;
+    uint32_t lo = b >= R.b_n ? R.seg_hi : ks.bucket[R.b_off + b];
+    uint32_t hi = b >= R.b_n ? R.seg_hi : ks.bucket[R.b_off + b + 1];
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ks.rpos[mid] < X) lo = mid + 1;
+        else hi = mid;
+    }
+    for (uint32_t rec = lo; rec < R.seg_hi && ks.rpos[rec] == X; ++rec) {
+        const uint32_t k0 = max(ks.lo[rec], R.key_lo), k1 = min(min(ks.lo[rec + 1], R.key_hi), klim);
+        for (uint32_t k = k0; k < k1; ++k)
+            if (key_equal_body(ks, k, y)) return true;
+    }
+    return false;
+}
+
+// One lane per deferred key (kid, run): it counts for its job when no key of
+// the job's runs holds its string at a larger POS (decimal(POS) ++ the first
+// j >= 1 tail digits) and no earlier key of the job's runs equals it.
+// Grid-stride over the list length the window kernel left in *n_list.
+__global__ __launch_bounds__(kThreads) void deferred_dedupe_kernel(KStore ks, const KRun *runs, const uint2 *list,
+                                                                   const uint32_t *n_list, uint32_t cap,
+                                                                   unsigned long long *counts) {
+    const uint32_t n = min(*n_list, cap);
+    for (uint32_t i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        const uint2 e = list[i];
+        const KRun R = runs[e.y];
+        const KBody y = ks.body[e.x];
+        bool skip = false;
+        // a copy at a larger POS
+        const uint64_t t = y.tail;
+        const uint32_t len = (t & kTailBlob) ? static_cast<uint32_t>((t >> 40) & 0xffff) : static_cast<uint32_t>(t >> 56);
+        uint64_t P = y.pos;
+        for (uint32_t j = 0; j < len && !skip; ++j) {
+            const uint32_t c = tail_byte(ks, t, j);
+            if (c < '0' || c > '9') break;
+            P = P * 10 + (c - '0');
+            if (P > 0xffffffffull) break;
+            for (uint32_t r = 0; r < R.nruns && !skip; ++r) skip = run_has_equal(ks, runs[R.run_lo + r], P, y, ~0u);
+        }
+        // an earlier copy at this POS: earlier runs of the job, or earlier in this run
+        for (uint32_t r = R.run_lo; r <= e.y && !skip; ++r) skip = run_has_equal(ks, runs[r], y.pos, y, r == e.y ? e.x : ~0u);
+        if (!skip) atomicAdd(&counts[R.job], 1ull);
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void window_dedupe_kernel(KStore ks, const KWin *wins, const KPiece *pieces,
-                                                                 unsigned long long *counts, uint32_t *overflow) {
-    __shared__ uint32_t xset[kXSlots];
-    __shared__ unsigned long long hset[kHSlots];
-    __shared__ uint32_t hid[kHSlots];
-    __shared__ uint32_t s_pre[kWinPieces + 1], s_klo[kWinPieces];
-    __shared__ unsigned long long s_side;
-    __shared__ uint32_t s_fresh, s_nh;
+                                                                 unsigned long long *counts, uint2 *list,
+                                                                 uint32_t *n_list, uint32_t cap, uint32_t *overflow,
+                                                                 uint32_t dbg) {
+    __shared__ unsigned long long set[kWSlots];
+    __shared__ uint32_t s_pre[kWinPieces + 1], s_klo[kWinPieces], s_run[kWinPieces];
+    __shared__ uint32_t s_fresh, s_def, s_def0;
     const KWin W = wins[blockIdx.x];
     const int lane = threadIdx.x & 63;
-    for (uint32_t i = threadIdx.x; i < kXSlots; i += kThreads) xset[i] = ~0u;
-    for (uint32_t i = threadIdx.x; i < kHSlots; i += kThreads) hset[i] = ~0ull;
+    for (uint32_t i = threadIdx.x; i < kWSlots; i += kThreads) set[i] = ~0ull;
     if (threadIdx.x < 64) {  // wave 0: the pieces' inclusive prefix
-        uint32_t len = 0, klo = 0;
-        bool side = false;
+        uint32_t len = 0, klo = 0, run = 0;
         if (static_cast<uint32_t>(lane) < W.npieces) {
             const KPiece p = pieces[W.piece_lo + lane];
             klo = p.key_lo;
-            len = p.n & 0x7fffffffu;
-            side = (p.n >> 31) != 0;
+            len = p.n & 0xffffu;
+            run = W.run_lo + (p.n >> 16);
         }
         uint32_t inc = len;
 #pragma unroll
@@ -688,48 +790,63 @@ __global__ __launch_bounds__(kThreads) void window_dedupe_kernel(KStore ks, cons
             const uint32_t y = __shfl_up(inc, o, 64);
             if (lane >= o) inc += y;
         }
-        const uint64_t sm = __ballot(side);
         s_pre[lane + 1] = inc;
         s_klo[lane] = klo;
+        s_run[lane] = run;
         if (lane == 0) {
             s_pre[0] = 0;
-            s_side = sm;
             s_fresh = 0;
-            s_nh = 0;
+            s_def = 0;
         }
     }
     __syncthreads();
     const uint32_t np = W.npieces, total = s_pre[np];
-    const uint64_t sidem = s_side;
+    auto piece_of = [&](uint32_t f) {
+        uint32_t p = 0;
+#pragma unroll
+        for (uint32_t st = 32; st; st >>= 1)
+            if (p + st < np && s_pre[p + st] <= f) p += st;
+        return p;
+    };
+    auto key_of = [&](uint32_t f) {  // window-local index -> store key
+        const uint32_t p = piece_of(f);
+        return s_klo[p] + (f - s_pre[p]);
+    };
     // every body load of the window first (key u = u * kThreads + tid)
     KBody b[kWPer];
     uint32_t kid[kWPer];
-    uint32_t okm = 0, sdm = 0;
+    uint32_t okm = 0;
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) {
         const uint32_t f = u * kThreads + threadIdx.x;
         kid[u] = 0;
         b[u] = KBody{0, 0, 0};
         if (f < total) {
-            uint32_t p = 0;  // the last piece starting at or before f
-#pragma unroll
-            for (uint32_t st = 32; st; st >>= 1)
-                if (p + st < np && s_pre[p + st] <= f) p += st;
-            kid[u] = s_klo[p] + (f - s_pre[p]);
+            kid[u] = key_of(f);
             b[u] = ks.body[kid[u]];
             okm |= 1u << u;
-            if ((sidem >> p) & 1ull) sdm |= 1u << u;
         }
     }
-    // classes: displaced keys read from a run are counted in their P window
-    // (as a side piece) instead; exact words; the rest hashed
+    if (dbg & 4u) {  // timing ablation (SBEACON_DEDUP_WIN_DBG): loads only
+        uint32_t x = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < kWPer; ++u) x += b[u].pos;
+        if (x == 0xdeadbeefu) atomicOr(overflow, x);
+        return;
+    }
+    // classes: exact words, hashed, deferred (displaced keys that may have a
+    // copy at a larger POS of the job)
     uint32_t xw[kWPer];
-    uint32_t em = 0, hm = 0;
+    uint32_t em = 0, hm = 0, dm = 0;
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) {
         xw[u] = 0;
         if (!((okm >> u) & 1u)) continue;
-        if ((b[u].flags & kKeyDisplaced) && !((sdm >> u) & 1u)) continue;
+        if (b[u].flags & kKeyDisplaced) {
+            if (static_cast<uint64_t>(b[u].pos) * 10 > W.pmax) hm |= 1u << u;
+            else dm |= 1u << u;
+            continue;
+        }
         uint64_t rel = 0;
         const uint32_t code = exact_word(b[u], W.p0, kWinSpanBits, &rel);
         if (code) {
@@ -742,62 +859,87 @@ __global__ __launch_bounds__(kThreads) void window_dedupe_kernel(KStore ks, cons
     unsigned long long hv[kWPer];
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) hv[u] = ((hm >> u) & 1u) ? ks.hash[kid[u]] : 0ull;
+    // deferred keys: one reservation per workgroup in the global list
+    const uint32_t nd = static_cast<uint32_t>(__popc(dm));
+    uint32_t dofs = 0;
+    if (nd) dofs = atomicAdd(&s_def, nd);
+    __syncthreads();
+    if (threadIdx.x == 0 && s_def) {
+        const uint32_t at = atomicAdd(n_list, s_def);
+        s_def0 = at;
+        if (at + s_def > cap) atomicOr(overflow, 1u);
+    }
+    __syncthreads();
+    if (nd) {
+        uint32_t at = s_def0 + dofs;
+#pragma unroll
+        for (uint32_t u = 0; u < kWPer; ++u)
+            if ((dm >> u) & 1u) {
+                if (at < cap) list[at] = uint2{kid[u], s_run[piece_of(u * kThreads + threadIdx.x)]};
+                ++at;
+            }
+    }
     uint32_t fresh = 0;
+    uint32_t pend = 0;      // hashed keys that met an entry with their hash bits
+    uint32_t ins[kWPer];    // ... and that entry's window-local key index
+    auto insert = [&](uint32_t u, bool ex) {
+        const uint32_t f = u * kThreads + threadIdx.x;
+        const unsigned long long e =
+            ex ? static_cast<unsigned long long>(xw[u]) : ((1ull << 63) | ((hv[u] >> 13) << 12) | f);
+        uint32_t h = ex ? (xw[u] * 0x9E3779B1u) >> 20 : static_cast<uint32_t>(hv[u]) & (kWSlots - 1);
+        static_assert(kWSlots == 1u << 12, "set slots");
+        for (uint32_t probe = 0; probe < kWSlots; ++probe) {
+            const unsigned long long was = atomicCAS(&set[h], ~0ull, e);
+            if (was == ~0ull) {
+                ++fresh;
+                return;
+            }
+            if (ex ? was == e : (was >> 12) == (e >> 12)) {
+                if (!ex) {
+                    pend |= 1u << u;
+                    ins[u] = static_cast<uint32_t>(was & 0xfff);
+                }
+                return;
+            }
+            h = (h + 1) & (kWSlots - 1);
+        }
+    };
+    if (dbg & 1u) em = 0;  // timing ablation: no exact inserts
+    if (dbg & 2u) hm = 0;  // no hashed inserts
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) {
-        if (!((em >> u) & 1u)) continue;
-        uint32_t h = (xw[u] * 0x9E3779B1u) >> (32 - 12);
-        static_assert(kXSlots == 1u << 12, "exact set slots");
-        for (uint32_t probe = 0; probe < kXSlots; ++probe) {
-            const uint32_t was = atomicCAS(&xset[h], ~0u, xw[u]);
-            if (was == ~0u) {
-                ++fresh;
-                break;
-            }
-            if (was == xw[u]) break;
-            h = (h + 1) & (kXSlots - 1);
-        }
+        ins[u] = 0;
+        if ((em >> u) & 1u) insert(u, true);
     }
-    const uint32_t nh = static_cast<uint32_t>(__popc(hm));
-    if (nh) atomicAdd(&s_nh, nh);
-    __syncthreads();
-    if (s_nh) {  // workgroup-uniform
-        if (s_nh > kHCap) {
-            if (threadIdx.x == 0) atomicOr(overflow, 1u);
-            return;
-        }
-        uint32_t mine = 0, slot[kWPer];
+#pragma unroll
+    for (uint32_t u = 0; u < kWPer; ++u)
+        if ((hm >> u) & 1u) insert(u, false);
+    // the strings of a repeated hash must match the inserter's: every
+    // inserter body load issued together, then the comparisons (the general
+    // decimal-concatenation one only for different POS or two blob tails)
+    bool bad = false;
+    if (pend) {
+        KBody xb[kWPer];
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u) {
-            slot[u] = 0;
-            if (!((hm >> u) & 1u)) continue;
-            if (hv[u] == ~0ull) {
-                atomicOr(overflow, 1u);
-                continue;
-            }
-            uint32_t h = static_cast<uint32_t>(hv[u]) & (kHSlots - 1);
-            unsigned long long was = 0;
-            for (uint32_t probe = 0; probe < kHSlots; ++probe) {
-                was = atomicCAS(&hset[h], ~0ull, hv[u]);
-                if (was == ~0ull || was == hv[u]) break;
-                h = (h + 1) & (kHSlots - 1);
-            }
-            slot[u] = h;
-            if (was == ~0ull) {
-                mine |= 1u << u;
-                ++fresh;
-            }
+            ins[u] = ((pend >> u) & 1u) ? key_of(ins[u]) : 0u;
+            xb[u] = ((pend >> u) & 1u) ? ks.body[ins[u]] : KBody{0, 0, 0};
         }
-        __syncthreads();
+        uint32_t slow = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < kWPer; ++u)
-            if ((mine >> u) & 1u) hid[slot[u]] = kid[u];
-        __syncthreads();
+        for (uint32_t u = 0; u < kWPer; ++u) {
+            if (!((pend >> u) & 1u)) continue;
+            if (xb[u].pos == b[u].pos && xb[u].tail == b[u].tail) continue;
+            if (xb[u].pos == b[u].pos && !((xb[u].tail & b[u].tail) & kTailBlob)) bad = true;
+            else slow |= 1u << u;  // two blob tails (or different POS)
+        }
+        if (slow) {
 #pragma unroll
-        for (uint32_t u = 0; u < kWPer; ++u)
-            if (((hm & ~mine) >> u) & 1u && hv[u] != ~0ull && !key_equal(ks, hid[slot[u]], kid[u]))
-                atomicOr(overflow, 1u);
+            for (uint32_t u = 0; u < kWPer; ++u)
+                if (((slow >> u) & 1u) && !body_equal(ks, xb[u], b[u])) bad = true;
+        }
     }
+    if (bad) atomicOr(overflow, 1u);
     for (int d = 32; d >= 1; d >>= 1) fresh += __shfl_xor(fresh, d, 64);
     if (lane == 0 && fresh) atomicAdd(&s_fresh, fresh);
     __syncthreads();
@@ -883,10 +1025,14 @@ int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1,
     return r;
 }
 
-void launch_window_dedupe(const KStore &ks, const KWin *wins, uint32_t nw, const KPiece *pieces,
-                          unsigned long long *counts, uint32_t *overflow, hipStream_t s) {
+void launch_window_dedupe(const KStore &ks, const KWin *wins, uint32_t nw, const KPiece *pieces, const KRun *runs,
+                          unsigned long long *counts, uint2 *list, uint32_t *n_list, uint32_t cap, uint32_t *overflow,
+                          hipStream_t s) {
     if (!nw) return;
-    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, wins, pieces, counts, overflow);
+    const char *dbge = std::getenv("SBEACON_DEDUP_WIN_DBG");  // timing ablations (never set by the benches)
+    const uint32_t dbg = dbge ? static_cast<uint32_t>(std::atoi(dbge)) : 0u;
+    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, wins, pieces, counts, list, n_list, cap, overflow, dbg);
+    deferred_dedupe_kernel<<<1024, kThreads, 0, s>>>(ks, runs, list, n_list, cap, counts);
 }
 
 uint32_t dedup_unique_blocks(uint64_t n) { return n ? tiles_of(n) : 0; }

@@ -384,29 +384,51 @@ struct alignas(16) KBody {  // what the equality check reads: one 16-byte load
     uint32_t flags;  // kKeyDisplaced
 };
 // the tail starts with a decimal digit: the string's leading digit run (its
-// "effective position" P) is longer than decimal(pos), so the key is counted
-// in the window of P, not of pos (window dedup)
+// "effective position" P) is longer than decimal(pos) and the same string
+// may also be stored at a larger POS (a prefix of P's digits, or P itself)
 inline constexpr uint32_t kKeyDisplaced = 1u;
 
-// Window dedup (sb_dedup_count): a job's keys partitioned by effective
-// position P into windows [p0, p1) of at most kWinCap keys.  Keys with equal
-// strings have equal P, so each window is deduplicated on its own.  A window
-// = pieces of store keys; a piece is a POS-sorted run's part inside the window
-// or (n bit 31) one displaced key whose P lies in it.
+// Window dedup (sb_dedup_count): a job's key runs (POS-sorted) cut at POS
+// boundaries into windows [p0, p1) of at most kWinCap keys, each
+// deduplicated on its own in LDS.  Equal strings at one POS meet in one
+// window.  A string stored at several POS (displaced keys) counts only at its
+// largest POS: a displaced key y with 10 POS > the job's largest POS can have
+// no copy at a larger POS and is counted in its window like any key; the
+// others (deferred keys) are listed and counted by a second kernel, one lane
+// per key: y counts when no key of the job's runs holds its string at a
+// larger POS (its twin, found through the record POS index) and no earlier
+// key of the job's runs (earlier run, or earlier in its run) equals it.
 struct KWin {
     uint32_t piece_lo, npieces, job, p0;
+    uint32_t run_lo;  // the job's first KRun
+    uint32_t pmax;    // largest POS of the job's runs
+    uint32_t pad[2];
 };
-struct KPiece {
+struct KPiece {  // keys [key_lo, key_lo + (n & 0xffff)) of run (n >> 16) of the job
     uint32_t key_lo, n;
 };
+struct KRun {  // one POS-sorted key run of a job + its segment's POS index
+    uint32_t key_lo, key_hi, pos_lo, pos_hi;  // keys, POS of the first / last
+    uint32_t seg_lo, seg_hi, b_base, b_shift;  // segment records, bucket base / width
+    uint64_t b_off;
+    uint32_t b_n;
+    uint32_t job;
+    uint32_t run_lo, nruns;  // the job's runs [run_lo, run_lo + nruns)
+    uint32_t pad[2];
+};
 inline constexpr uint32_t kWinCap = 3072;    // keys per window (LDS sets sized for it)
-inline constexpr uint32_t kWinPieces = 64;   // pieces per window
+inline constexpr uint32_t kWinPieces = 64;   // pieces (= runs) per window
 inline constexpr uint32_t kWinSpanBits = 26; // p1 - p0 < 2^26 - 1: exact words fit 32 bits
 
 struct KStore {
     const uint64_t *hash;
     const KBody *body;
     const uint8_t *blob;
+    // twin lookups of the window dedup: first key of each record (+ end), the
+    // records' POS and the segments' coarse POS index (DStore::pos / bucket)
+    const uint32_t *lo;
+    const uint32_t *rpos;
+    const uint32_t *bucket;
 };
 
 struct KSeg {  // one run of store keys gathered for a job

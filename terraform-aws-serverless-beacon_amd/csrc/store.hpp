@@ -153,7 +153,6 @@ struct sb_store {
     // duplicateVariantSearch keys (global indexing): planning + collision fixup
     uint64_t n_keys = 0;
     std::vector<uint32_t> h_dk_pos, h_dk_lo, h_dk_bad;
-    std::vector<uint32_t> h_dk_disp;  // displaced keys (tail starts with a digit), sorted
     std::vector<uint64_t> h_dk_tail;
     std::vector<uint8_t> h_dk_blob;
     // device image
