@@ -1720,8 +1720,8 @@ bool plan_job_windows(const sb_store &s, const std::vector<KRun> &runs, size_t g
 
 // Every job's windows; jobs planned on host threads.  runs[g] = segs[g]'s KRun.
 bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan &P) {
-    uint32_t target = 2048;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
-    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) target = std::max(1, std::min(2048, std::atoi(e)));
+    uint32_t target = 1536;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
+    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) target = std::max(1, std::min(1536, std::atoi(e)));
     if (s.n_keys >= 0x80000000ull) return P.why = "2^31 keys", false;
     std::vector<std::pair<size_t, size_t>> groups;  // each job's runs
     std::vector<char> seen(nj, 0);

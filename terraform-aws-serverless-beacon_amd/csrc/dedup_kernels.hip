@@ -658,7 +658,7 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
 // pairs).  Two strings under one hash, or a full deferred list, raise
 // *overflow and the host recounts the call on the sorted path.  No gather
 // stream, no radix pass: 16 B/key + 8 B per hashed key.
-constexpr uint32_t kWSlots = 4096;  // 32 KB; kWinCap keys at most (load <= 0.75)
+constexpr uint32_t kWSlots = 3072;  // 24 KB; kWinCap keys at most (load <= 0.67); slot = multiply-shift range reduction
 constexpr uint32_t kWPer = kWinCap / kThreads;
 static_assert(kWPer * kThreads == kWinCap, "window keys per thread");
 static_assert(kWinCap < kWSlots, "window set load");
@@ -766,7 +766,7 @@ __global__ __launch_bounds__(kThreads) void deferred_dedupe_kernel(KStore ks, co
     }
 }
 
-__global__ __launch_bounds__(kThreads) void window_dedupe_kernel(KStore ks, const KWin *wins, const KPiece *pieces,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void window_dedupe_kernel(KStore ks, const KWin *wins, const KPiece *pieces,
                                                                  unsigned long long *counts, uint2 *list,
                                                                  uint32_t *n_list, uint32_t cap, uint32_t *overflow,
                                                                  uint32_t dbg) {
@@ -886,8 +886,9 @@ __global__ __launch_bounds__(kThreads) void window_dedupe_kernel(KStore ks, cons
         const uint32_t f = u * kThreads + threadIdx.x;
         const unsigned long long e =
             ex ? static_cast<unsigned long long>(xw[u]) : ((1ull << 63) | ((hv[u] >> 13) << 12) | f);
-        uint32_t h = ex ? (xw[u] * 0x9E3779B1u) >> 20 : static_cast<uint32_t>(hv[u]) & (kWSlots - 1);
-        static_assert(kWSlots == 1u << 12, "set slots");
+        const uint32_t hr = ex ? xw[u] * 0x9E3779B1u : static_cast<uint32_t>(hv[u]);
+        uint32_t h = static_cast<uint32_t>((static_cast<uint64_t>(hr) * kWSlots) >> 32);
+        static_assert(kWinCap <= 4096, "window-local index in 12 bits");
         for (uint32_t probe = 0; probe < kWSlots; ++probe) {
             const unsigned long long was = atomicCAS(&set[h], ~0ull, e);
             if (was == ~0ull) {
@@ -901,7 +902,7 @@ __global__ __launch_bounds__(kThreads) void window_dedupe_kernel(KStore ks, cons
                 }
                 return;
             }
-            h = (h + 1) & (kWSlots - 1);
+            h = h + 1 == kWSlots ? 0u : h + 1;
         }
     };
     if (dbg & 1u) em = 0;  // timing ablation: no exact inserts
