@@ -137,7 +137,7 @@ def main_genome(args):
     if world == 1 and os.path.exists(tf):
         try:
             tj = json.load(open(tf))
-            if tj.get('records') == shape.n_total and tj.get('requests') == len(reqs) and tj.get('kernel') == 'chain_kernel':
+            if tj.get('records') == shape.n_total and tj.get('requests') == len(reqs) and tj.get('kernel') == 'chain_pack_kernel<false>':
                 traffic = tj.get('hbm_bytes_per_launch')
         except Exception:
             traffic = None

@@ -84,6 +84,23 @@ def main():
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def pmc_traffic(records, kernels):
+    """HBM bytes per launch of the named kernels from the committed PMC passes
+    (tools/gpu_pmc_r02.sh -> profiles/traffic_paths.json), when they were
+    measured on this workload; else None."""
+    tf = os.path.join(REPO, 'profiles', 'traffic_paths.json')
+    try:
+        tj = json.load(open(tf))
+    except (OSError, ValueError):
+        return None
+    if tj.get('records') != records:
+        return None
+    ks = tj.get('kernels', {})
+    if not all(k in ks for k in kernels):
+        return None
+    return sum(ks[k]['hbm_bytes_per_launch'] for k in kernels)
+
+
 def summarise_line(args, store, files, plan_slices):
     # summariseVcf's plan per VCF from its CSI index (written by the ingest
     # side, sb_index_vcf; one host thread per VCF)
@@ -125,7 +142,8 @@ def summarise_line(args, store, files, plan_slices):
                    'slices': len(slices), 'records_visited': recs},
         'device_ms_per_step': round(dev_ms, 4),
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                     'frac': round(achieved / HBM_PEAK_GBS, 4),
+                     'traffic': pmc_traffic(n_records, ['summarise_chunk_kernel', 'summarise_finish_kernel']),
                      'kernel': 'summarise_chunk_kernel + summarise_finish_kernel',
                      'algorithmic_bytes_per_launch': alg},
         'cpu_baseline': cpu, 'parity_sample': parity}), flush=True)
@@ -203,7 +221,9 @@ def dedup_line(args, store, datasets, files):
         'device_ms_per_step': round(dev_ms, 4), 'path': st['path'], 'windows': st['windows'],
         'union': {'vcfs': len(files), 'keys': ust['keys'], 'unique': ures[0], 'device_ms': round(ust['device_ms'], 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                     'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': None,
+                     'frac': round(achieved / HBM_PEAK_GBS, 4),
+                     'traffic': (pmc_traffic(store.info()['n_records'], ['window_dedupe_kernel', 'deferred_dedupe_kernel'])
+                                 if st['path'] == 'windows' else None),
                      'kernel': kern, 'algorithmic_bytes_per_launch': alg,
                      'implementation_bytes_per_launch_upper_bound': impl,
                      'implementation_GBs': round(impl / (dev_ms * 1e-3) / 1e9, 1)},
