@@ -11,6 +11,8 @@
 #include <atomic>
 #include <array>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -1081,10 +1083,12 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     // pack_slots_max() slices (the wave's LDS slots)
     B.hruns.clear();
     {
-        uint32_t slots = 0, cnt = 0;
+        uint32_t slots = 0, cnt = 0, run_max = pack_run_max();
+        if (const char *e = std::getenv("SBEACON_PACK_RUN"))  // A/B: shorter runs
+            run_max = std::max(1u, std::min(run_max, static_cast<uint32_t>(std::atoi(e))));
         for (uint32_t c = 0; c < B.hchains.size(); ++c) {
             const uint32_t n = B.hchains[c].n;
-            if (cnt == 0 || cnt == pack_run_max() || slots + n > pack_slots_max()) {
+            if (cnt == 0 || cnt == run_max || slots + n > pack_slots_max()) {
                 B.hruns.push_back(c);
                 slots = 0;
                 cnt = 0;
@@ -1718,7 +1722,76 @@ bool plan_job_windows(const sb_store &s, const std::vector<KRun> &runs, size_t g
     return true;
 }
 
-// Every job's windows; jobs planned on host threads.  runs[g] = segs[g]'s KRun.
+// A persistent host worker pool (planning runs once per call: spawning
+// threads per call cost a few hundred microseconds).  run(n, fn) calls fn(i)
+// for i < n on the pool and the calling thread; one run at a time.
+class WorkerPool {
+  public:
+    static WorkerPool &get() {
+        static WorkerPool pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+        return pool;
+    }
+    template <class F>
+    void run(size_t n, F fn) {
+        std::lock_guard<std::mutex> one(run_mu_);
+        std::function<void(size_t)> f = fn;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &f;
+            n_ = n;
+            next_ = 0;
+            busy_ = workers_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+
+  private:
+    explicit WorkerPool(unsigned k) {
+        for (unsigned i = 0; i < k; ++i) workers_.emplace_back([this] { loop(); });
+    }
+    void drain() {
+        for (size_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            drain();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--busy_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_, done_;
+    std::function<void(size_t)> *fn_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    size_t busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// Every job's windows; jobs planned on the worker pool.  runs[g] = segs[g]'s KRun.
 bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan &P) {
     uint32_t target = 1536;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
     if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) target = std::max(1, std::min(1536, std::atoi(e)));
@@ -1737,21 +1810,19 @@ bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan
         groups.emplace_back(g0, g1);
         g0 = g1;
     }
-    const size_t nt = std::min<size_t>(groups.size(), std::max(1u, std::min(16u, std::thread::hardware_concurrency())));
     std::vector<std::vector<KWin>> tw(groups.size());
     std::vector<std::vector<KPiece>> tp(groups.size());
     std::vector<const char *> why(groups.size(), nullptr);
-    std::atomic<size_t> next{0};
-    auto work = [&]() {
-        for (size_t q; (q = next.fetch_add(1)) < groups.size();) {
-            const char *w = nullptr;
-            if (!plan_job_windows(s, runs, groups[q].first, groups[q].second, target, tw[q], tp[q], &w)) why[q] = w;
-        }
+    auto work = [&](size_t q) {
+        const char *w = nullptr;
+        uint64_t keys = 0;
+        for (size_t g = groups[q].first; g < groups[q].second; ++g) keys += runs[g].key_hi - runs[g].key_lo;
+        tw[q].reserve(keys / (target / 2 + 1) + 4);
+        tp[q].reserve(2 * (keys / (target / 2 + 1) + 4) * (groups[q].second - groups[q].first));
+        if (!plan_job_windows(s, runs, groups[q].first, groups[q].second, target, tw[q], tp[q], &w)) why[q] = w;
     };
-    std::vector<std::thread> th;
-    for (size_t t = 1; t < nt; ++t) th.emplace_back(work);
-    work();
-    for (auto &t : th) t.join();
+    if (groups.size() > 1) WorkerPool::get().run(groups.size(), work);
+    else if (!groups.empty()) work(0);
     for (size_t q = 0; q < groups.size(); ++q) {
         if (why[q]) return P.why = why[q], false;
         const uint32_t base = static_cast<uint32_t>(P.pieces.size());

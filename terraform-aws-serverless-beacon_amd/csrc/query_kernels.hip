@@ -1526,8 +1526,8 @@ __global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const ChainDev
 // call_count > 0 (chains need a non-negative-AC store).  The slot and LUT
 // tables keep the per-chain work off the VALU: the kernel is issue-bound
 // (SQ counters, profiles/r02_pmc_chain).
-constexpr int kPackAhead = 4;     // candidate chunks issued before the first is evaluated
-constexpr uint32_t kPackRun = 16;  // chains per wave at most
+constexpr int kPackAhead = 3;     // candidate chunks in flight (a chunk's load is issued kPackAhead chunks ahead)
+constexpr uint32_t kPackRun = 32;  // chains per wave at most
 constexpr uint32_t kPackSlots = 256;  // slices per run at most (host-enforced)
 
 // SLICES: per-slice sums (the per-slice QRes rows); without them (request
@@ -1567,7 +1567,7 @@ __device__ __forceinline__ uint32_t last_le(uint32_t v, uint32_t R, uint32_t g) 
 }
 
 template <bool SLICES>
-__global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const ChainDev *__restrict__ chains,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SLICES ? 4 : 8, 8))) void chain_pack_kernel(DStore st, const ChainDev *__restrict__ chains,
                                                             const uint32_t *__restrict__ runs, uint32_t n_runs,
                                                             const uint32_t *__restrict__ corig,
                                                             QRes *__restrict__ res, uint64_t *__restrict__ hits,
@@ -1582,11 +1582,13 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
     // round 1: the run's descriptors (5 x 16 B per chain), staged in LDS
     {
         const uint4 *cd = reinterpret_cast<const uint4 *>(chains + c_first);
-        uint4 w0{0, 0, 0, 0}, w1{0, 0, 0, 0};
-        if (ul < 5 * R) w0 = cd[ul];
-        if (ul + kWave < 5 * R) w1 = cd[ul + kWave];
-        if (ul < 5 * R) L.desc[ul] = w0;
-        if (ul + kWave < 5 * R) L.desc[ul + kWave] = w1;
+        constexpr uint32_t kDw = (kPackRun * 5 + kWave - 1) / kWave;  // descriptor words per lane
+        uint4 dw[kDw];
+#pragma unroll
+        for (uint32_t q = 0; q < kDw; ++q) dw[q] = ul + kWave * q < 5 * R ? cd[ul + kWave * q] : uint4{0, 0, 0, 0};
+#pragma unroll
+        for (uint32_t q = 0; q < kDw; ++q)
+            if (ul + kWave * q < 5 * R) L.desc[ul + kWave * q] = dw[q];
         if (ul < kPackRun) {
             L.tcc[ul] = 0;
             L.tan[ul] = 0;
@@ -1756,13 +1758,21 @@ __global__ __launch_bounds__(kBlock) void chain_pack_kernel(DStore st, const Cha
     // every chunk of the run issued before the first is evaluated
     // (dbg: timing ablations of SBEACON_PACK_DBG; 0 in production)
     if (!(dbg & 1u)) {
+        // software pipeline: chunk c + kPackAhead's loads are issued right
+        // after chunk c is evaluated (static buffer slots: unrolled by kPackAhead)
         PackChunk buf[kPackAhead];
 #pragma unroll
         for (int a = 0; a < kPackAhead; ++a) buf[a] = load(64u * a);
+        for (uint32_t base = 0; base < T; base += 64u * kPackAhead) {
 #pragma unroll
-        for (int a = 0; a < kPackAhead; ++a)
-            if (64u * a < T) eval(buf[a], 64u * a);
-        for (uint32_t base = 64u * kPackAhead; base < T; base += 64u) eval(load(base), base);  // long runs
+            for (int a = 0; a < kPackAhead; ++a) {
+                const uint32_t b = base + 64u * a;
+                if (b < T) {
+                    eval(buf[a], b);
+                    if (b + 64u * kPackAhead < T) buf[a] = load(b + 64u * kPackAhead);
+                }
+            }
+        }
     }
     if (dbg & 2u) return;
     wave_lds_sync();

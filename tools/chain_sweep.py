@@ -29,8 +29,10 @@ def main():
     base = None
     for setting in os.environ.get('SETTINGS', 'seq8,pack').split(','):
         env = {}
-        if setting == 'pack':  # packed kernel (host-built runs of up to 16 chains)
+        if setting == 'pack':  # packed kernel (host-built runs of up to pack_run_max() chains)
             pass
+        elif setting.startswith('pack'):  # packed kernel, runs of at most N chains
+            env['SBEACON_PACK_RUN'] = setting[4:]
         elif setting.startswith('seq'):  # chain-sequential kernel
             env['SBEACON_CHAIN_RUN'] = setting[3:]
             env['SBEACON_CHAIN_KERNEL'] = 'seq'
@@ -38,7 +40,7 @@ def main():
             env['SBEACON_PACK_DBG'] = setting[3:]
         elif setting == 'nochain':
             env['SBEACON_NO_CHAINS'] = '1'
-        for k in ('SBEACON_CHAIN_RUN', 'SBEACON_NO_CHAINS', 'SBEACON_CHAIN_KERNEL', 'SBEACON_PACK_DBG'):
+        for k in ('SBEACON_CHAIN_RUN', 'SBEACON_NO_CHAINS', 'SBEACON_CHAIN_KERNEL', 'SBEACON_PACK_DBG', 'SBEACON_PACK_RUN'):
             os.environ.pop(k, None)
         os.environ.update(env)
         t1 = time.perf_counter()
