@@ -214,7 +214,7 @@ struct sb_batch {
     std::vector<uint64_t> chain_cap;  // hit capacity of each chain (ALTs of its coarse candidate range)
     // request rows as pieces (sb_batch_set_owners, when every chain lies in one row)
     bool row_pieces = false;
-    DevMem poff, piece, rows_scratch, rowsrc;
+    DevMem poff, piece, rows_scratch, rowsrc, rowout;
     DevMem nvs;  // sb_batch_deliver: each row's n_variants (8 B / row) for the offset scan
     uint64_t cand_loaded = 0, cand_window = 0, cand_unique = 0;  // chain candidate statistics
     hipStream_t stream = nullptr;  // sb_batch_set_stream (nullptr: the store's stream)
@@ -2613,6 +2613,17 @@ int sb_batch_set_owners(sb_batch *b, const uint32_t *owner, size_t nq, uint32_t 
             HIP_OK(hipMemcpyAsync(b->poff.p, poff.data(), poff.size() * 4, hipMemcpyHostToDevice, st));
             if (!piece.empty())
                 HIP_OK(hipMemcpyAsync(b->piece.p, piece.data(), piece.size() * 4, hipMemcpyHostToDevice, st));
+            // each single-piece row's hit region (static for the batch): the
+            // deliver gather reads it instead of a per-run rowsrc
+            std::vector<uint64_t> rowout(std::max<size_t>(n_rows, 1), ~0ull);
+            for (uint32_t w = 0; w < n_rows; ++w) {
+                if (poff[w + 1] == poff[w]) rowout[w] = 0;
+                if (poff[w + 1] != poff[w] + 1) continue;
+                const uint32_t p = piece[poff[w]];
+                rowout[w] = (p & (1u << 31)) ? b->hchains[p & ~(1u << 31)].out : b->hq[p].hit_off;
+            }
+            b->rowout.alloc(rowout.size() * 8);
+            HIP_OK(hipMemcpyAsync(b->rowout.p, rowout.data(), rowout.size() * 8, hipMemcpyHostToDevice, st));
         }
         HIP_OK(hipStreamSynchronize(st));
         b->n_rows = n_rows;
@@ -2649,7 +2660,9 @@ int sb_batch_deliver(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_
             launch_row_deliver(b->cpart.as<ReqPartial>(), b->chains.as<ChainDev>(), b->hoff.as<uint64_t>(),
                                b->res.as<QRes>(), b->herr.as<uint8_t>(), b->poff.as<uint32_t>(),
                                b->piece.as<uint32_t>(), b->n_rows, static_cast<ReqPartial *>(dev_rows),
-                               b->rowsrc.as<ulonglong2>(), b->nvs.as<int64_t>(), b->tsum.as<uint64_t>(),
+                               b->rowsrc.as<ulonglong2>(),
+                               std::getenv("SBEACON_NO_ROWOUT") ? nullptr : b->rowout.as<uint64_t>(),  // A/B knob
+                               b->nvs.as<int64_t>(), b->tsum.as<uint64_t>(),
                                b->hits.as<uint64_t>(), rec_base, static_cast<uint64_t *>(dev_row_off),
                                static_cast<uint64_t *>(dev_hits), b->strm());
             HIP_OK(hipGetLastError());

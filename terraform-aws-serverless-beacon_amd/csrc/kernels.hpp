@@ -76,12 +76,14 @@ void launch_hit_lists(const QRes *res, uint32_t nq, const uint64_t *src, const u
 void launch_row_reduce(const ReqPartial *cpart, const ChainDev *chains, const uint64_t *hoff, const QRes *res,
                        const uint8_t *host_err, const uint32_t *poff, const uint32_t *piece, uint32_t n_rows,
                        ReqPartial *out, ulonglong2 *rowsrc, hipStream_t s);
-// sb_batch_deliver (row pieces): rows + rowsrc + dense n_variants / tile
-// sums, the offset scan over them, then the segmented gather
+// sb_batch_deliver (row pieces): rows + dense n_variants / tile sums, the
+// offset scan over them, then the segmented gather; rowout (optional, built
+// at sb_batch_set_owners) = each single-piece row's hit region (~0: several
+// pieces) in place of the rowsrc the reduction would write
 void launch_row_deliver(const ReqPartial *cpart, const ChainDev *chains, const uint64_t *hoff, const QRes *res,
                         const uint8_t *host_err, const uint32_t *poff, const uint32_t *piece, uint32_t n_rows,
-                        ReqPartial *rows, ulonglong2 *rowsrc, int64_t *nv, uint64_t *tsum, const uint64_t *hits,
-                        uint64_t rec_base, uint64_t *row_off, uint64_t *out, hipStream_t s);
+                        ReqPartial *rows, ulonglong2 *rowsrc, const uint64_t *rowout, int64_t *nv, uint64_t *tsum,
+                        const uint64_t *hits, uint64_t rec_base, uint64_t *row_off, uint64_t *out, hipStream_t s);
 void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, const uint32_t *poff,
                           const uint32_t *piece, uint32_t n_rows, const ChainDev *chains, const ReqPartial *cpart,
                           const QRes *res, const uint64_t *hoff, const uint64_t *hits, uint64_t rec_base,

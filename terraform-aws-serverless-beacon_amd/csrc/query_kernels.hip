@@ -2136,7 +2136,7 @@ __global__ __launch_bounds__(kBlock) void row_gather_seg_kernel(const uint32_t *
                                                                 const uint64_t *__restrict__ hoff,
                                                                 const uint64_t *__restrict__ hits, uint64_t rec_base,
                                                                 const uint64_t *__restrict__ row_off,
-                                                                const ulonglong2 *__restrict__ rowsrc,
+                                                                const uint64_t *__restrict__ srcx, uint32_t sstride,
                                                                 uint64_t *__restrict__ out) {
     const uint32_t r0 = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kWave;
     if (r0 >= n_rows) return;
@@ -2146,7 +2146,7 @@ __global__ __launch_bounds__(kBlock) void row_gather_seg_kernel(const uint32_t *
     const uint64_t base = row_off[r0];
     const uint64_t end = row_off[min(r0 + kWave, n_rows)];
     const uint64_t my0 = row_off[r];
-    const ulonglong2 rs = live ? rowsrc[r] : ulonglong2{0ull, 0ull};
+    const ulonglong2 rs{live ? srcx[static_cast<size_t>(r) * sstride] : 0ull, 0ull};  // x: the row's hit region
     const uint32_t e = static_cast<uint32_t>(live ? my0 - base : end - base);  // row start within the range
     const bool single = live && rs.x != ~0ull;
     const uint64_t total = end - base;
@@ -2508,19 +2508,23 @@ void launch_row_reduce(const ReqPartial *cpart, const ChainDev *chains, const ui
 
 void launch_row_deliver(const ReqPartial *cpart, const ChainDev *chains, const uint64_t *hoff, const QRes *res,
                         const uint8_t *host_err, const uint32_t *poff, const uint32_t *piece, uint32_t n_rows,
-                        ReqPartial *rows, ulonglong2 *rowsrc, int64_t *nv, uint64_t *tsum, const uint64_t *hits,
-                        uint64_t rec_base, uint64_t *row_off, uint64_t *out, hipStream_t s) {
+                        ReqPartial *rows, ulonglong2 *rowsrc, const uint64_t *rowout, int64_t *nv, uint64_t *tsum,
+                        const uint64_t *hits, uint64_t rec_base, uint64_t *row_off, uint64_t *out, hipStream_t s) {
     const uint32_t nt = (n_rows + kScanTile - 1) / kScanTile;
     if (!nt) {
         (void)hipMemsetAsync(row_off, 0, 8, s);
         return;
     }
+    // rowout (static hit region of each single-piece row, ~0 for several
+    // pieces): the reduction skips the scattered chain-descriptor reads and the
+    // rowsrc writes
     hipLaunchKernelGGL(row_reduce_tiles_kernel, dim3(nt), dim3(kBlock), 0, s, cpart, chains, hoff, res, host_err, poff,
-                       piece, n_rows, rows, rowsrc, nv, tsum);
+                       piece, n_rows, rows, rowout ? nullptr : rowsrc, nv, tsum);
     hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kBlock), 0, s, tsum, nt);
     hipLaunchKernelGGL(field_tile_scan_kernel, dim3(nt), dim3(kBlock), 0, s, nv, 1u, n_rows, tsum, row_off);
     hipLaunchKernelGGL(row_gather_seg_kernel, dim3(blocks_for((n_rows + kWave - 1) / kWave)), dim3(kBlock), 0, s, poff,
-                       piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
+                       piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off,
+                       rowout ? rowout : reinterpret_cast<const uint64_t *>(rowsrc), rowout ? 1u : 2u, out);
 }
 
 void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, const uint32_t *poff,
@@ -2544,7 +2548,8 @@ void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, cons
                            0, s, poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
     } else {
         hipLaunchKernelGGL(row_gather_seg_kernel, dim3(blocks_for((n_rows + kWave - 1) / kWave)), dim3(kBlock), 0, s,
-                           poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
+                           poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off,
+                           reinterpret_cast<const uint64_t *>(rowsrc), 2u, out);
     }
 }
 

@@ -220,3 +220,22 @@ def test_synthetic_store_properties():
     assert whole == dedup_count([a], '22', 0, 2**32)
     assert union == whole
     assert left + right == whole
+
+
+def test_many_vcfs_in_one_job_fall_back_to_the_sorted_path():
+    """A job over more VCFs than a window holds runs (64) is declined by the
+    window planner and answered by the sorted path with the same count; a
+    job over fewer takes the windows."""
+    from oracle.oracle import dedup_count
+    from sbeacon.engine import Store
+    pool = make_pool(seed=9)
+    texts = {f'm{i}.vcf.gz': gen_vcf(500 + i, pool, share=0.3, n_own=40) for i in range(70)}
+    st = Store.build(list(texts.items()), device=0)
+    names = list(texts)
+    got, stats = st.dedup_counts([(names, '22', 0, 10**9)], with_stats=True)
+    assert stats['path'] != 'windows'
+    assert got == [dedup_count([texts[n] for n in names], '22', 0, 10**9)]
+    got, stats = st.dedup_counts([(names[:40], '22', 0, 10**9)], with_stats=True)
+    assert stats['path'] == 'windows'
+    assert got == [dedup_count([texts[n] for n in names[:40]], '22', 0, 10**9)]
+
