@@ -15,6 +15,7 @@
 #include <functional>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <map>
 #include <memory>
 #include <thread>
@@ -1623,9 +1624,26 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
 // (string, POS) in one window.  runs[g] = segs[g]'s KRun (key range, POS
 // span, its segment's coarse POS index for the twin lookups).
 struct WinPlan {
-    std::vector<KWin> wins;
-    std::vector<KPiece> pieces;
+    std::vector<std::vector<KWin>> wins;      // per job group (piece_lo local to the group)
+    std::vector<std::vector<KPiece>> pieces;  // per job group
+    size_t n_wins = 0, n_pieces = 0;
     const char *why = "";  // why the plan was declined (SBEACON_DEDUP_DEBUG)
+};
+
+struct PinnedHost {  // grow-only pinned host staging (hipHostMalloc)
+    void *p = nullptr;
+    size_t bytes = 0;
+    void reserve(size_t n) {
+        if (n <= bytes) return;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        bytes = 0;
+        HIP_OK(hipHostMalloc(&p, n, hipHostMallocDefault));
+        bytes = n;
+    }
+    ~PinnedHost() {
+        if (p) (void)hipHostFree(p);
+    }
 };
 
 // one job's windows (runs [g0, g1) of the call)
@@ -1810,8 +1828,10 @@ bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan
         groups.emplace_back(g0, g1);
         g0 = g1;
     }
-    std::vector<std::vector<KWin>> tw(groups.size());
-    std::vector<std::vector<KPiece>> tp(groups.size());
+    std::vector<std::vector<KWin>> &tw = P.wins;
+    std::vector<std::vector<KPiece>> &tp = P.pieces;
+    tw.assign(groups.size(), {});
+    tp.assign(groups.size(), {});
     std::vector<const char *> why(groups.size(), nullptr);
     auto work = [&](size_t q) {
         const char *w = nullptr;
@@ -1825,18 +1845,15 @@ bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan
     else if (!groups.empty()) work(0);
     for (size_t q = 0; q < groups.size(); ++q) {
         if (why[q]) return P.why = why[q], false;
-        const uint32_t base = static_cast<uint32_t>(P.pieces.size());
-        for (KWin w : tw[q]) {
-            w.piece_lo += base;
-            P.wins.push_back(w);
-        }
-        P.pieces.insert(P.pieces.end(), tp[q].begin(), tp[q].end());
+        P.n_wins += tw[q].size();
+        P.n_pieces += tp[q].size();
     }
     return true;
 }
 
 struct WinWs {
     DevMem wins, pieces, runs, counts, overflow, list, n_list;
+    PinnedHost stage;  // windows | pieces | runs for one H2D copy; counts + overflow back
 };
 
 // the window path: true when it answered every job (counts in unique[])
@@ -1847,7 +1864,7 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     const auto t0 = std::chrono::steady_clock::now();
     auto since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     if (!plan_windows(s, runs, nj, P)) {
-        if (dbg) std::fprintf(stderr, "[sbeacon] dedup windows: plan declined (%s; %zu windows so far)\n", P.why, P.wins.size());
+        if (dbg) std::fprintf(stderr, "[sbeacon] dedup windows: plan declined (%s)\n", P.why);
         return false;
     }
     const double t_plan = since();
@@ -1855,9 +1872,9 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     hipStream_t st = s.stream;
     if (!s.win_ws) s.win_ws = std::shared_ptr<void>(new WinWs, [](void *w) { delete static_cast<WinWs *>(w); });
     WinWs &W = *static_cast<WinWs *>(s.win_ws.get());
-    const uint32_t nw = static_cast<uint32_t>(P.wins.size());
+    const uint32_t nw = static_cast<uint32_t>(P.n_wins);
     W.wins.reserve(std::max<size_t>(nw, 1) * sizeof(KWin));
-    W.pieces.reserve(std::max<size_t>(P.pieces.size(), 1) * sizeof(KPiece));
+    W.pieces.reserve(std::max<size_t>(P.n_pieces, 1) * sizeof(KPiece));
     W.runs.reserve(std::max<size_t>(runs.size(), 1) * sizeof(KRun));
     W.counts.reserve(std::max<size_t>(nj, 1) * 8);
     W.overflow.reserve(4);
@@ -1867,10 +1884,28 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     W.list.reserve(static_cast<size_t>(cap) * 8);
     W.n_list.reserve(4);
     HIP_OK(hipMemsetAsync(W.n_list.p, 0, 4, st));
+    // the plan staged in pinned memory (the groups' windows with their piece
+    // offsets made global, pieces, runs): DMA without a pageable bounce; the
+    // previous call's copies have completed (it synchronised)
+    const size_t bw = size_t(nw) * sizeof(KWin), bp = P.n_pieces * sizeof(KPiece), br = runs.size() * sizeof(KRun);
+    W.stage.reserve(bw + bp + br + 64 + std::max<size_t>(nj, 1) * 8);
     if (nw) {
-        HIP_OK(hipMemcpyAsync(W.wins.p, P.wins.data(), nw * sizeof(KWin), hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemcpyAsync(W.pieces.p, P.pieces.data(), P.pieces.size() * sizeof(KPiece), hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemcpyAsync(W.runs.p, runs.data(), runs.size() * sizeof(KRun), hipMemcpyHostToDevice, st));
+        KWin *hw = static_cast<KWin *>(W.stage.p);
+        KPiece *hp = reinterpret_cast<KPiece *>(static_cast<uint8_t *>(W.stage.p) + bw);
+        uint32_t pbase = 0;
+        for (size_t q = 0; q < P.wins.size(); ++q) {
+            for (const KWin &w : P.wins[q]) {
+                *hw = w;
+                hw->piece_lo += pbase;
+                ++hw;
+            }
+            std::copy(P.pieces[q].begin(), P.pieces[q].end(), hp + pbase);
+            pbase += static_cast<uint32_t>(P.pieces[q].size());
+        }
+        std::memcpy(static_cast<uint8_t *>(W.stage.p) + bw + bp, runs.data(), br);
+        HIP_OK(hipMemcpyAsync(W.wins.p, W.stage.p, bw, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(W.pieces.p, static_cast<uint8_t *>(W.stage.p) + bw, bp, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(W.runs.p, static_cast<uint8_t *>(W.stage.p) + bw + bp, br, hipMemcpyHostToDevice, st));
     }
     HIP_OK(hipMemsetAsync(W.counts.p, 0, std::max<size_t>(nj, 1) * 8, st));
     HIP_OK(hipMemsetAsync(W.overflow.p, 0, 4, st));
