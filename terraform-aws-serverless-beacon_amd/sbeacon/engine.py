@@ -40,44 +40,99 @@ def _b(s):
     return None if s is None else (s if isinstance(s, bytes) else str(s).encode())
 
 
+_QUERY_FIELDS = ['vcf_id', 'region', 'region_len', 'end_min', 'end_max', 'reference_bases', 'reference_len',
+                 'alternate_bases', 'alternate_len', 'variant_type', 'variant_type_len', 'variant_min_length',
+                 'variant_max_length', 'granularity', 'include_details', 'include_samples', 'selected_samples_only',
+                 'strict_variant_type', 'sample_names', 'sample_names_len']
+_QUERY_FORMATS = ['u4', 'u8', 'u8', 'i8', 'i8', 'u8', 'u8', 'u8', 'u8', 'u8', 'u8', 'i8', 'i8',
+                  'u1', 'u1', 'u1', 'u1', 'u1', 'u8', 'u8']
+_QUERY_DTYPE = None
+
+
+def _query_dtype():
+    global _QUERY_DTYPE
+    if _QUERY_DTYPE is None:
+        _QUERY_DTYPE = np.dtype({'names': _QUERY_FIELDS, 'formats': _QUERY_FORMATS,
+                                 'offsets': [getattr(Query, f).offset for f in _QUERY_FIELDS],
+                                 'itemsize': C.sizeof(Query)})
+    return _QUERY_DTYPE
+
+
 def queries_from_payloads(payloads: list[dict], vcf_id, *, strict_variant_type: bool = False):
     """PerformQueryPayload dicts -> (ctypes Query array, keep-alive list);
-    vcf_id(location) -> the store's vcf id."""
+    vcf_id(location) -> the store's vcf id.  Column-wise: every string goes
+    into one pooled buffer (repeated values stored once) and the fields are
+    filled through a numpy view of the array, so a batch of 10^5 payloads
+    costs list comprehensions, not 10^6 ctypes attribute stores."""
     n = len(payloads)
-    arr = (Query * n)()
-    keep = []
+    arr = (Query * max(n, 1))()
+    if n == 0:
+        return arr, []
     vid_cache = {}
-    for i, p in enumerate(payloads):
-        loc = p['vcf_location']
-        vid = vid_cache.get(loc)
-        if vid is None:
-            vid = vid_cache[loc] = vcf_id(loc)
-        pt = p.get('passthrough') or {}
-        region = _b(p['region'])
-        ref = _b(p.get('reference_bases'))
-        alt = _b(p.get('alternate_bases'))
-        vt = _b(p.get('variant_type'))
-        names = pt.get('sampleNames', None)
-        sn = _b(','.join(names)) if names is not None else None
-        keep.append((region, ref, alt, vt, sn))
-        if p.get('end_min') is None or p.get('end_max') is None:
-            raise TypeError("'<=' not supported between instances of 'NoneType' and 'int'")
-        q = arr[i]
-        q.vcf_id = vid
-        q.region, q.region_len = region, len(region)
-        q.end_min, q.end_max = int(p['end_min']), int(p['end_max'])
-        q.reference_bases, q.reference_len = ref, len(ref) if ref is not None else 0
-        q.alternate_bases, q.alternate_len = alt, len(alt) if alt is not None else 0
-        q.variant_type, q.variant_type_len = vt, len(vt) if vt is not None else 0
-        q.variant_min_length = int(p['variant_min_length'])
-        q.variant_max_length = int(p['variant_max_length'])
-        q.granularity = _lib.SB_GRAN.get(p.get('requested_granularity'), 255)
-        q.include_details = 1 if p.get('include_details') else 0
-        q.include_samples = 1 if pt.get('includeSamples', False) else 0
-        q.selected_samples_only = 1 if pt.get('selectedSamplesOnly', False) else 0
-        q.strict_variant_type = 1 if strict_variant_type else 0
-        q.sample_names, q.sample_names_len = sn, len(sn) if sn is not None else 0
-    return arr, keep
+
+    def vid_of(loc):
+        v = vid_cache.get(loc)
+        if v is None:
+            v = vid_cache[loc] = vcf_id(loc)
+        return v
+
+    pts = [p.get('passthrough') or {} for p in payloads]
+    em = [p.get('end_min') for p in payloads]
+    ex = [p.get('end_max') for p in payloads]
+    if any(x is None for x in em) or any(x is None for x in ex):
+        raise TypeError("'<=' not supported between instances of 'NoneType' and 'int'")
+    # pooled strings (NUL-terminated, as the bytes objects ctypes would
+    # pass): offset (-1 = NULL) and length per payload; a column of few
+    # distinct values (REF / ALT / variantType) stores each value once
+    pool = bytearray()
+
+    def col(vals):
+        strs = [v for v in vals if v is not None]
+        if len(strs) == len(vals) and all(type(v) is str for v in vals):
+            joined = '\0'.join(vals)
+            if joined.isascii() and len(set(vals)) * 4 > len(vals):  # mostly unique (regions): one join
+                ln = np.fromiter((len(v) for v in vals), dtype=np.uint64, count=len(vals))
+                off = len(pool) + np.concatenate([[0], np.cumsum(ln[:-1] + 1)]).astype(np.int64)
+                pool.extend(joined.encode())
+                pool.append(0)
+                return off, ln
+        at = {}
+        for v in set(strs):
+            bv = _b(v)
+            at[v] = (len(pool), len(bv))
+            pool.extend(bv)
+            pool.append(0)
+        off = np.array([at[v][0] if v is not None else -1 for v in vals], dtype=np.int64)
+        ln = np.array([at[v][1] if v is not None else 0 for v in vals], dtype=np.uint64)
+        return off, ln
+
+    names = [pt.get('sampleNames', None) for pt in pts]
+    cols = {
+        'region': col([p['region'] for p in payloads]),
+        'reference_bases': col([p.get('reference_bases') for p in payloads]),
+        'alternate_bases': col([p.get('alternate_bases') for p in payloads]),
+        'variant_type': col([p.get('variant_type') for p in payloads]),
+        'sample_names': col([','.join(x) if x is not None else None for x in names]),
+    }
+    buf = C.create_string_buffer(bytes(pool), max(len(pool), 1))
+    base = C.addressof(buf)
+    v = np.frombuffer((C.c_char * (C.sizeof(Query) * n)).from_address(C.addressof(arr)), dtype=_query_dtype())
+    lens = {'region': 'region_len', 'reference_bases': 'reference_len', 'alternate_bases': 'alternate_len',
+            'variant_type': 'variant_type_len', 'sample_names': 'sample_names_len'}
+    for f, (off, ln) in cols.items():
+        v[f] = np.where(off >= 0, base + np.maximum(off, 0), 0).astype(np.uint64)
+        v[lens[f]] = ln
+    v['vcf_id'] = [vid_of(p['vcf_location']) for p in payloads]
+    v['end_min'] = [int(x) for x in em]
+    v['end_max'] = [int(x) for x in ex]
+    v['variant_min_length'] = [int(p['variant_min_length']) for p in payloads]
+    v['variant_max_length'] = [int(p['variant_max_length']) for p in payloads]
+    v['granularity'] = [_lib.SB_GRAN.get(p.get('requested_granularity'), 255) for p in payloads]
+    v['include_details'] = [1 if p.get('include_details') else 0 for p in payloads]
+    v['include_samples'] = [1 if pt.get('includeSamples', False) else 0 for pt in pts]
+    v['selected_samples_only'] = [1 if pt.get('selectedSamplesOnly', False) else 0 for pt in pts]
+    v['strict_variant_type'] = 1 if strict_variant_type else 0
+    return arr, [buf]
 
 
 class Store:
