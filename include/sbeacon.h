@@ -148,6 +148,8 @@ typedef struct {
 } sb_result_view;
 
 int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out);
+/* views of queries 0 .. n-1 in one call (n <= the batch's queries) */
+int sb_result_get_all(const sb_result_set *r, sb_result_view *out, size_t n);
 /* Reference-format strings for query i: variants '\n'-joined
  * (f'{chrom}\t{POS}\t{REF}\t{ALT}\t{VT}', search_variants.py:210) and
  * sample names ','-joined.  Pointers valid until sb_result_free. */

@@ -2805,6 +2805,12 @@ int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out) {
     return SB_OK;
 }
 
+int sb_result_get_all(const sb_result_set *r, sb_result_view *out, size_t n) {
+    if (!r || (!out && n) || n > r->res.size()) return SB_EINVAL;
+    for (size_t i = 0; i < n; ++i) sb_result_get(r, i, out + i);
+    return SB_OK;
+}
+
 namespace {
 // f'{chrom}\t{position}\t{reference}\t{alts[i]}\t{variant_type}' (search_variants.py:210)
 void append_variant(std::string &o, const sb_store &s, const std::string &chrom, uint64_t hit) {

@@ -118,6 +118,7 @@ SIGNATURES = {
                                        C.POINTER(C.c_size_t)]),
     'sb_query_batch': (C.c_int, [P, C.POINTER(Query), C.c_size_t, C.c_uint32, C.POINTER(P)]),
     'sb_result_get': (C.c_int, [P, C.c_size_t, C.POINTER(ResultView)]),
+    'sb_result_get_all': (C.c_int, [P, C.POINTER(ResultView), C.c_size_t]),
     'sb_result_variants_text': (C.c_int, [P, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     'sb_result_sample_names_text': (C.c_int, [P, C.c_size_t, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     'sb_result_stats': (C.c_int, [P, C.POINTER(BatchStats)]),

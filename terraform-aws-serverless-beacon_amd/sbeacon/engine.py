@@ -608,13 +608,42 @@ class ResultSet:
 
     def responses(self, *, lazy_variants: bool = False) -> list:
         """All responses; an entry is the exception instance where the
-        reference would have raised."""
+        reference would have raised.  The views of every query come from one
+        library call (sb_result_get_all); the per-query text calls happen only
+        where there is text (variants when not lazy, sample names)."""
+        n = len(self.payloads)
+        if n == 0:
+            return []
+        views = (ResultView * n)()
+        check(lib().sb_result_get_all(self._h, views, n))
         out = []
-        for i in range(len(self.payloads)):
-            try:
-                out.append(self.response(i, lazy_variants=lazy_variants))
-            except (UnboundLocalError, IndexError, ValueError, AttributeError, NotImplementedError) as e:
+        vtext, ntext = lib().sb_result_variants_text, lib().sb_result_sample_names_text
+        for i, (p, v) in enumerate(zip(self.payloads, views)):
+            if v.error:
+                e = QERR.get(v.error, RuntimeError)(QERR_MSG.get(v.error, 'error'))
+                if not isinstance(e, (UnboundLocalError, IndexError, ValueError, AttributeError, NotImplementedError)):
+                    raise e
                 out.append(e)
+                continue
+            pt = p.get('passthrough') or {}
+            nv, ns = int(v.n_variants), int(v.n_sample_indices)
+            if lazy_variants:
+                variants = LazyVariants(self, i, nv)
+            else:
+                variants = self._text(vtext, i).split('\n') if nv else []
+            names = self._text(ntext, i).split(',') if ns else []
+            if pt.get('selectedSamplesOnly', False):
+                sample_indices = v.sample_indices[:ns] if ns else []
+                sample_names = names
+            else:
+                sample_indices = []
+                sample_names = names if pt.get('includeSamples', False) else []
+            r = PerformQueryResponse(
+                exists=bool(v.exists), dataset_id=p.get('dataset_id'), vcf_location=p.get('vcf_location'),
+                all_alleles_count=int(v.all_alleles_count), variants=variants, call_count=int(v.call_count),
+                sample_indices=sample_indices, sample_names=sample_names)
+            r._src = (self, i)
+            out.append(r)
         return out
 
 
