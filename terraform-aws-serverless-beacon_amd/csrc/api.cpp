@@ -1811,8 +1811,8 @@ class WorkerPool {
 
 // Every job's windows; jobs planned on the worker pool.  runs[g] = segs[g]'s KRun.
 bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan &P) {
-    uint32_t target = 1536;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
-    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) target = std::max(1, std::min(1536, std::atoi(e)));
+    uint32_t target = kWinCap;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
+    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) target = std::max(1, std::min(static_cast<int>(kWinCap), std::atoi(e)));
     if (s.n_keys >= 0x80000000ull) return P.why = "2^31 keys", false;
     std::vector<std::pair<size_t, size_t>> groups;  // each job's runs
     std::vector<char> seen(nj, 0);
