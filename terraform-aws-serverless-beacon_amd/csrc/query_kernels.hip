@@ -834,6 +834,21 @@ struct VtPred {
         lutv = lutv_;
         lut_lane = lane0;
     }
+    // chain_pack_kernel: the constants precomputed per chain at setup, LUT words in LDS
+    __device__ __forceinline__ VtPred(uint32_t e0_, uint32_t espan_, uint32_t vlo_, uint32_t vspan_, uint32_t cmask_,
+                                      uint32_t xneed_, bool end_void_, const uint32_t *llut_) {
+        e0 = e0_;
+        espan = espan_;
+        vlo = vlo_;
+        vspan = vspan_;
+        cmask = cmask_;
+        xneed = xneed_;
+        end_void = end_void_;
+        lut = nullptr;
+        lutv = 0;
+        lut_lane = 0;
+        llut = llut_;
+    }
     __device__ __forceinline__ bool end_ok(uint32_t end) const { return !end_void && end - e0 <= espan; }
     // one ALT word + the LUT word its symbolic id falls in: predicate + length bounds
     __device__ __forceinline__ bool alt_ok(uint32_t aw, uint32_t lw) const {
@@ -853,7 +868,8 @@ struct VtPred {
             x0 = st.x_lo[r];
             for (uint32_t k = 0; k < nx; ++k) {
                 const uint32_t xw = st.xvt[x0 + k];
-                if (alt_ok(xw, (xw & VT_SYM) ? lut[(xw >> 21) & 7u] : 0u)) hm |= 2ull << k;
+                if (alt_ok(xw, (xw & VT_SYM) ? (llut ? llut[(xw >> 21) & 7u] : lut[(xw >> 21) & 7u]) : 0u))
+                    hm |= 2ull << k;
             }
         }
         if (hm) {  // :205-214, AC of each matching ALT
@@ -1670,6 +1686,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SLICES ?
             if (ul >= static_cast<uint32_t>(d)) pin += t;
         }
         pex = pin - cnt;
+        // lane j < R: chain j's per-candidate constants in its descriptor's
+        // setup-only words (read above, in program order): word 1.y = 1 /
+        // width (f32), word 4.x = the kind's class mask, word 4.y = the
+        // extra-ALT bits | end_void << 31 (the LUT offset is not needed: the
+        // LUT words are in LDS)
+        if (ul < R) {
+            const uint32_t kind = L.desc[5 * ul + 4].x;
+            VtPred q(st, 0u, 0u, 0u, 0u, kind, 0u, 0u, 0u);
+            L.desc[5 * ul + 1].y = __float_as_uint(__frcp_rn(static_cast<float>(L.desc[5 * ul + 1].x)));
+            L.desc[5 * ul + 4].x = q.cmask;
+            L.desc[5 * ul + 4].y = q.xneed | (q.end_void ? 0x80000000u : 0u);
+        }
     }
     wave_lds_sync();
     const uint32_t T = rdl(pin, kPackRun - 1);
@@ -1694,8 +1722,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SLICES ?
         const bool valid = g < T;
         const uint4 e0 = L.desc[5 * k], e1 = L.desc[5 * k + 1], e3 = L.desc[5 * k + 3], e4 = L.desc[5 * k + 4];
         const uint32_t first = e0.z, last = e0.w, n = e0.y, width = e1.x;
-        VtPred Pd(st, e3.x, e3.y, e3.z, e3.w, e4.x, e4.y, 0u, 0u);
-        Pd.llut = &L.lut[8 * k];
+        VtPred Pd(e3.x, e3.y, e3.z, e3.w, e4.x, e4.y & 0x7fffffffu, (e4.y >> 31) != 0, &L.lut[8 * k]);
         const bool inwin = valid && x.p >= first && x.p <= last;
         const bool cand = inwin && Pd.end_ok(x.h.end);
         if (cand && (x.h.w & VT_SLOW)) L.slow[k] = 1u;  // never: prepare dissolves such chains
@@ -1708,7 +1735,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SLICES ?
             const uint32_t d = x.p - first;
             uint32_t q;
             if (d < (1u << 24)) {
-                q = static_cast<uint32_t>(static_cast<float>(d) * __frcp_rn(static_cast<float>(width)));
+                q = static_cast<uint32_t>(static_cast<float>(d) * __uint_as_float(e1.y));  // 1 / width (setup)
                 if (static_cast<uint64_t>(q) * width > d) --q;
                 else if (static_cast<uint64_t>(q + 1) * width <= d) ++q;
             } else {
