@@ -2177,20 +2177,38 @@ __global__ __launch_bounds__(kBlock) void row_gather_seg_kernel(const uint32_t *
     const uint32_t e = static_cast<uint32_t>(live ? my0 - base : end - base);  // row start within the range
     const bool single = live && rs.x != ~0ull;
     const uint64_t total = end - base;
-    for (uint64_t j0 = 0; j0 < total; j0 += kWave) {
-        const uint32_t j = static_cast<uint32_t>(j0) + ul;
-        // last lane l with e_l <= j (e is nondecreasing over the lanes)
-        uint32_t l = 0;
+    // lane r's source offset of output slot j is off_r + j - 2^63 (its hit
+    // region minus its row start, biased so it is never 0); 0 = a
+    // several-piece row (copied below)
+    constexpr uint64_t kBias = 1ull << 63;
+    const uint64_t offr = single ? rs.x - e + kBias : 0ull;
+    auto src_of = [&](uint32_t j) -> uint64_t {  // call with every lane active
+        uint32_t l = 0;  // last lane l with e_l <= j (e is nondecreasing over the lanes)
 #pragma unroll
         for (uint32_t step = kWave / 2; step >= 1; step >>= 1) {
             const uint32_t t = l + step;
             const uint32_t et = static_cast<uint32_t>(__shfl(static_cast<int>(e), static_cast<int>(t), kWave));
             if (et <= j) l = t;
         }
-        const uint32_t el = static_cast<uint32_t>(__shfl(static_cast<int>(e), static_cast<int>(l), kWave));
-        const uint64_t src = static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(rs.x), static_cast<int>(l)));
-        const bool sl = __shfl(static_cast<int>(single), static_cast<int>(l), kWave) != 0;
-        if (j < total && sl) out[base + j] = hits[src + (j - el)] + rec_base;
+        return static_cast<uint64_t>(shfl_i64(static_cast<int64_t>(offr), static_cast<int>(l)));
+    };
+    // four output passes per round: their searches, then every load, then the stores
+    constexpr uint32_t kGU = 4;
+    for (uint64_t j0 = 0; j0 < total; j0 += kGU * kWave) {
+        uint64_t so[kGU], hv[kGU];
+#pragma unroll
+        for (uint32_t q = 0; q < kGU; ++q)
+            so[q] = j0 + q * kWave < total ? src_of(static_cast<uint32_t>(j0) + q * kWave + ul) : 0ull;
+#pragma unroll
+        for (uint32_t q = 0; q < kGU; ++q) {
+            const uint64_t j = j0 + q * kWave + ul;
+            hv[q] = (j < total && so[q] != 0ull) ? hits[so[q] - kBias + j] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kGU; ++q) {
+            const uint64_t j = j0 + q * kWave + ul;
+            if (j < total && so[q] != 0ull) out[base + j] = hv[q] + rec_base;
+        }
     }
     if (live && !single) {  // several pieces: this lane copies its row
         uint64_t d = my0;
