@@ -2108,6 +2108,37 @@ __global__ __launch_bounds__(kBlock) void field_tile_scan_kernel(const int64_t *
     if (blockIdx.x == 0 && threadIdx.x == 0) out[n] = tsum[gridDim.x];
 }
 
+// The same scan without the one-block tile_scan launch in front: block b
+// sums the raw tile sums of the blocks before it itself (L2-resident, a few
+// KB), and the last block writes the total at out[n]
+__global__ __launch_bounds__(kBlock) void field_scan_fused_kernel(const int64_t *__restrict__ v, uint32_t n,
+                                                                  const uint64_t *__restrict__ tsum,
+                                                                  uint64_t *__restrict__ out) {
+    __shared__ uint64_t wsum[kWavesPerBlock];
+    __shared__ uint64_t s_pre;
+    uint64_t part = 0;
+    for (uint32_t i = threadIdx.x; i < blockIdx.x; i += kBlock) part += tsum[i];
+    const uint64_t pincl = block_incl_scan(part, wsum);
+    if (threadIdx.x == kBlock - 1) s_pre = pincl;
+    __syncthreads();
+    const uint64_t pre = s_pre;
+    const uint32_t i0 = blockIdx.x * kScanTile + threadIdx.x * kScanPer;
+    uint64_t c[kScanPer], x = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        c[k] = i0 + k < n ? static_cast<uint64_t>(v[i0 + k]) : 0u;
+        x += c[k];
+    }
+    const uint64_t incl = block_incl_scan(x, wsum);
+    uint64_t at = pre + incl - x;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; ++k) {
+        if (i0 + k < n) out[i0 + k] = at;
+        at += c[k];
+    }
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = pre + incl;
+}
+
 // a team of kGatherTeam lanes per row: its pieces' hits, in piece order,
 // from row_off[w], the team's lanes striding over each piece (a row holds a
 // handful of hits: a lane per row would issue one scattered 8-byte access per
@@ -2565,8 +2596,7 @@ void launch_row_deliver(const ReqPartial *cpart, const ChainDev *chains, const u
     // rowsrc writes
     hipLaunchKernelGGL(row_reduce_tiles_kernel, dim3(nt), dim3(kBlock), 0, s, cpart, chains, hoff, res, host_err, poff,
                        piece, n_rows, rows, rowout ? nullptr : rowsrc, nv, tsum);
-    hipLaunchKernelGGL(tile_scan_kernel, dim3(1), dim3(kBlock), 0, s, tsum, nt);
-    hipLaunchKernelGGL(field_tile_scan_kernel, dim3(nt), dim3(kBlock), 0, s, nv, 1u, n_rows, tsum, row_off);
+    hipLaunchKernelGGL(field_scan_fused_kernel, dim3(nt), dim3(kBlock), 0, s, nv, n_rows, tsum, row_off);
     hipLaunchKernelGGL(row_gather_seg_kernel, dim3(blocks_for((n_rows + kWave - 1) / kWave)), dim3(kBlock), 0, s, poff,
                        piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off,
                        rowout ? rowout : reinterpret_cast<const uint64_t *>(rowsrc), rowout ? 1u : 2u, out);
