@@ -36,7 +36,8 @@ class OrcResult(C.Structure):
                 ('all_alleles_count', C.c_int64), ('variants', C.c_void_p),
                 ('n_variants', C.c_int64), ('sample_indices', C.POINTER(C.c_int32)),
                 ('n_sample_indices', C.c_int64), ('sample_names', C.c_void_p),
-                ('n_sample_names', C.c_int64)]
+                ('n_sample_names', C.c_int64), ('call_count_hex', C.c_char_p),
+                ('all_alleles_count_hex', C.c_char_p)]
 
 
 _lib = None
@@ -97,9 +98,9 @@ def _result_dict(r: OrcResult, p: dict):
         'exists': bool(r.exists),
         'vcf_location': p.get('vcf_location'),
         'dataset_id': p.get('dataset_id'),
-        'all_alleles_count': int(r.all_alleles_count),
+        'all_alleles_count': int(r.all_alleles_count_hex, 16) if r.all_alleles_count_hex else int(r.all_alleles_count),
         'variants': variants.split('\n') if r.n_variants else [],
-        'call_count': int(r.call_count),
+        'call_count': int(r.call_count_hex, 16) if r.call_count_hex else int(r.call_count),
         'sample_indices': [r.sample_indices[i] for i in range(r.n_sample_indices)] if samples_variant else [],
         'sample_names': names.split(',') if r.n_sample_names else [],
     }

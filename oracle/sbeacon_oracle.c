@@ -98,6 +98,278 @@ static int py_int(const char *p, int64_t n, int64_t *out) {
     return 0;
 }
 
+/* ----------------------------------------------------------- Python ints
+ * int(str) is unbounded in the reference (sv:199, :206, :218) up to
+ * CPython's 4300-digit str->int limit (ValueError past it; Python >= 3.10.7 /
+ * 3.9.14, the Lambda python3.9 runtime included).  Values are kept as int64
+ * while they fit and as two's complement bignums (BN_LIMBS x 32 bits) past
+ * that. */
+#define PY_MAX_STR_DIGITS 4300
+#define BN_LIMBS 480 /* 15360 bits: a 4300-digit value (14284 bits) + sum headroom */
+
+typedef struct {
+    uint32_t l[BN_LIMBS];
+} bn_t;
+
+static void bn_from_i64(bn_t *b, int64_t v) {
+    uint64_t u = (uint64_t)v;
+    b->l[0] = (uint32_t)u;
+    b->l[1] = (uint32_t)(u >> 32);
+    uint32_t s = v < 0 ? 0xffffffffu : 0u;
+    for (int i = 2; i < BN_LIMBS; i++) b->l[i] = s;
+}
+static void bn_add(bn_t *a, const bn_t *b) {
+    uint64_t c = 0;
+    for (int i = 0; i < BN_LIMBS; i++) {
+        c += (uint64_t)a->l[i] + b->l[i];
+        a->l[i] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+static void bn_neg(bn_t *a) {
+    uint64_t c = 1;
+    for (int i = 0; i < BN_LIMBS; i++) {
+        c += (uint64_t)(uint32_t)~a->l[i];
+        a->l[i] = (uint32_t)c;
+        c >>= 32;
+    }
+}
+static int bn_is_zero(const bn_t *a) {
+    for (int i = 0; i < BN_LIMBS; i++)
+        if (a->l[i]) return 0;
+    return 1;
+}
+static int bn_fits_i64(const bn_t *a, int64_t *v) {
+    uint32_t s = (a->l[1] >> 31) ? 0xffffffffu : 0u;
+    for (int i = 2; i < BN_LIMBS; i++)
+        if (a->l[i] != s) return 0;
+    *v = (int64_t)(((uint64_t)a->l[1] << 32) | a->l[0]);
+    return 1;
+}
+static char *bn_to_hex(const bn_t *a) { /* "0x.." / "-0x.." (malloc) */
+    bn_t m = *a;
+    int neg = (m.l[BN_LIMBS - 1] >> 31) != 0;
+    if (neg) bn_neg(&m);
+    char *s = (char *)malloc(BN_LIMBS * 8 + 4), *p = s;
+    if (neg) *p++ = '-';
+    *p++ = '0';
+    *p++ = 'x';
+    int top = BN_LIMBS - 1;
+    while (top > 0 && !m.l[top]) top--;
+    p += sprintf(p, "%x", m.l[top]);
+    for (int i = top - 1; i >= 0; i--) p += sprintf(p, "%08x", m.l[i]);
+    return s;
+}
+
+/* Python int(str) for the ASCII forms VCF text carries: strip whitespace,
+ * optional sign, digits with single '_' between digits, at most 4300 digits.
+ * small = |v| < 10^18; otherwise *big (caller frees). 0 ok, -1 ValueError. */
+typedef struct {
+    int64_t v;
+    bn_t *big; /* NULL = small */
+} pyint_t;
+
+static int py_int_big(const char *p, int64_t n, pyint_t *out) {
+    int64_t i = 0, j = n;
+    out->v = 0;
+    out->big = NULL;
+    while (i < j && isspace((unsigned char)p[i])) i++;
+    while (j > i && isspace((unsigned char)p[j - 1])) j--;
+    if (i == j) return -1;
+    int neg = 0;
+    if (p[i] == '+' || p[i] == '-') {
+        neg = p[i] == '-';
+        i++;
+    }
+    if (i == j || !isdigit((unsigned char)p[i])) return -1;
+    int64_t digits = 0, sig = 0; /* all digits / digits after leading zeros */
+    for (int64_t k = i; k < j; k++) {
+        if (p[k] == '_') {
+            if (k + 1 >= j || !isdigit((unsigned char)p[k + 1]) || !isdigit((unsigned char)p[k - 1])) return -1;
+            continue;
+        }
+        if (!isdigit((unsigned char)p[k])) return -1;
+        digits++;
+        if (sig || p[k] != '0') sig++;
+    }
+    if (digits > PY_MAX_STR_DIGITS) return -1;
+    if (sig <= 18) {
+        int64_t v = 0;
+        for (int64_t k = i; k < j; k++)
+            if (p[k] != '_') v = v * 10 + (p[k] - '0');
+        out->v = neg ? -v : v;
+        return 0;
+    }
+    bn_t *b = (bn_t *)calloc(1, sizeof(bn_t));
+    for (int64_t k = i; k < j; k++) {
+        if (p[k] == '_') continue;
+        uint64_t c = (uint64_t)(p[k] - '0');
+        for (int t = 0; t < BN_LIMBS; t++) {
+            c += (uint64_t)b->l[t] * 10u;
+            b->l[t] = (uint32_t)c;
+            c >>= 32;
+        }
+    }
+    if (neg) bn_neg(b);
+    out->big = b;
+    return 0;
+}
+static int py_is_zero(const pyint_t *x) { return x->big ? bn_is_zero(x->big) : x->v == 0; }
+
+/* running Python-int sum: v + (b ? *b : 0) */
+typedef struct {
+    int64_t v;
+    bn_t *b;
+} acc_t;
+
+static void acc_spill(acc_t *a) {
+    if (!a->b) {
+        a->b = (bn_t *)calloc(1, sizeof(bn_t));
+    }
+    bn_t t;
+    bn_from_i64(&t, a->v);
+    bn_add(a->b, &t);
+    a->v = 0;
+}
+static void acc_add_i64(acc_t *a, int64_t x) {
+    int64_t r;
+    if (__builtin_add_overflow(a->v, x, &r)) {
+        acc_spill(a);
+        a->v = x;
+    } else {
+        a->v = r;
+    }
+}
+static void acc_add(acc_t *a, const pyint_t *x) {
+    if (!x->big) {
+        acc_add_i64(a, x->v);
+        return;
+    }
+    if (!a->b) a->b = (bn_t *)calloc(1, sizeof(bn_t));
+    bn_add(a->b, x->big);
+}
+static int acc_nonzero(acc_t *a) {
+    if (!a->b) return a->v != 0;
+    acc_spill(a);
+    return !bn_is_zero(a->b);
+}
+static void acc_out(acc_t *a, int64_t *v, char **hex) {
+    *hex = NULL;
+    if (!a->b) {
+        *v = a->v;
+        return;
+    }
+    acc_spill(a);
+    if (!bn_fits_i64(a->b, v)) {
+        *v = (int64_t)(((uint64_t)a->b->l[1] << 32) | a->b->l[0]);
+        *hex = bn_to_hex(a->b);
+    }
+}
+static void acc_free(acc_t *a) {
+    free(a->b);
+    a->b = NULL;
+}
+
+/* --------------------------------------------- CPython set emulation
+ * sv:223 emits `alts[i] for i in set(all_calls) & hit_set`: the variant
+ * order is CPython's iteration order of that set (Objects/setobject.c,
+ * 3.10: set_add_entry / set_insert_clean / set_table_resize /
+ * set_intersection; LINEAR_PROBES 9, PERTURB_SHIFT 5, PySet_MINSIZE 8, growth
+ * at fill*5 >= mask*3 to 4*used).  An int's hash is its value mod 2**61 - 1.
+ * Keys index a table of call values compared by value. */
+typedef struct {
+    uint64_t hash;
+    int64_t v;      /* small value (sig digits <= 18) */
+    const char *d;  /* big: significant digits */
+    int64_t dl;     /* big: their count (0 = small) */
+} pyval_t;
+
+static int pyval_eq(const pyval_t *a, const pyval_t *b) {
+    if (a->dl != b->dl) return 0;
+    if (!a->dl) return a->v == b->v;
+    return !memcmp(a->d, b->d, (size_t)a->dl);
+}
+
+typedef struct {
+    uint64_t hash;
+    int64_t key;
+    int used;
+} sent_t;
+typedef struct {
+    sent_t *t;
+    uint64_t mask, fill, used;
+} pset_t;
+
+static void pset_init(pset_t *s) {
+    s->mask = 7;
+    s->t = (sent_t *)calloc(8, sizeof(sent_t));
+    s->fill = s->used = 0;
+}
+static void pset_insert_clean(sent_t *t, uint64_t mask, uint64_t hash, int64_t key) {
+    uint64_t perturb = hash, i = hash & mask;
+    sent_t *e;
+    for (;;) {
+        e = &t[i];
+        if (!e->used) goto found;
+        if (i + 9 <= mask)
+            for (int j = 0; j < 9; j++) {
+                e++;
+                if (!e->used) goto found;
+            }
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+found:
+    e->used = 1;
+    e->hash = hash;
+    e->key = key;
+}
+static void pset_add(pset_t *s, const pyval_t *vals, uint64_t hash, int64_t key) {
+    uint64_t mask = s->mask, i = hash & mask, perturb = hash;
+    sent_t *e;
+    for (;;) {
+        e = &s->t[i];
+        int probes = (i + 9 <= mask) ? 9 : 0;
+        do {
+            if (!e->used) goto unused;
+            if (e->hash == hash && pyval_eq(&vals[e->key], &vals[key])) return;
+            e++;
+        } while (probes--);
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+unused:
+    e->used = 1;
+    e->hash = hash;
+    e->key = key;
+    s->fill++;
+    s->used++;
+    if (s->fill * 5 < mask * 3) return;
+    uint64_t minused = s->used > 50000 ? s->used * 2 : s->used * 4, newsize = 8;
+    while (newsize <= minused) newsize <<= 1;
+    sent_t *nt = (sent_t *)calloc(newsize, sizeof(sent_t));
+    for (uint64_t k = 0; k <= mask; k++)
+        if (s->t[k].used) pset_insert_clean(nt, newsize - 1, s->t[k].hash, s->t[k].key);
+    free(s->t);
+    s->t = nt;
+    s->mask = newsize - 1;
+    s->fill = s->used;
+}
+static int pset_contains(const pset_t *s, const pyval_t *vals, uint64_t hash, int64_t key) {
+    uint64_t mask = s->mask, i = hash & mask, perturb = hash;
+    for (;;) {
+        const sent_t *e = &s->t[i];
+        int probes = (i + 9 <= mask) ? 9 : 0;
+        do {
+            if (!e->used) return 0;
+            if (e->hash == hash && pyval_eq(&vals[e->key], &vals[key])) return 1;
+            e++;
+        } while (probes--);
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
 /* ------------------------------------------------------------------ load */
 static char *slurp(const char *path, int64_t *len) {
     gzFile f = gzopen(path, "rb");
@@ -231,6 +503,8 @@ void orc_result_free(orc_result *r) {
     free(r->variants);
     free(r->sample_indices);
     free(r->sample_names);
+    free(r->call_count_hex);
+    free(r->all_alleles_count_hex);
     memset(r, 0, sizeof *r);
 }
 
@@ -418,7 +692,7 @@ int orc_query_one(void *h, const orc_query *q, orc_result *res) {
 
     const int approx = q->reference_bases && !strcmp(q->reference_bases, "N"); /* sv:59 */
     int exists = 0;
-    int64_t call_count = 0, all_alleles_count = 0;
+    acc_t call_count = {0, NULL}, all_alleles_count = {0, NULL};
     dbuf variants = {0};
     int64_t n_variants = 0;
     char *sample_hit = (char *)calloc((size_t)n_sel + 1, 1);
@@ -426,10 +700,13 @@ int orc_query_one(void *h, const orc_query *q, orc_result *res) {
     int err = ORC_OK;
     sv_t *alts = (sv_t *)malloc(sizeof(sv_t) * MAX_ALTS);
     int *hits = (int *)malloc(sizeof(int) * MAX_ALTS);
+    char *is_hit = (char *)malloc(MAX_ALTS + 1);
     sv_t *cols = (sv_t *)malloc(sizeof(sv_t) * (size_t)(v->n_samples + 1));
-    int64_t *ac = (int64_t *)malloc(sizeof(int64_t) * MAX_ALTS);
-    int64_t *calls = NULL;
+    pyint_t *ac = (pyint_t *)calloc(MAX_ALTS, sizeof(pyint_t));
+    int n_ac_alloc = 0; /* entries of ac[] holding a bignum to free */
+    pyval_t *calls = NULL; /* all_calls (sv:218), then the hit_set values */
     int64_t calls_cap = 0;
+    int calls_huge = 0;    /* a digit run int() rejects (> 4300 digits) */
 
     int64_t hi = 0;
     int64_t i0 = bcftools_failed ? 0 : lower_bound(v, rg.chrom, rg.first_bp, &hi);
@@ -482,7 +759,7 @@ int orc_query_one(void *h, const orc_query *q, orc_result *res) {
         /* sv:191-201 INFO scan: last AC=, last AN= (int), last VT= */
         sv_t ac_s = {0, -1};
         int have_an = 0;
-        int64_t an = 0;
+        pyint_t an = {0, NULL};
         sv_t vt = {"N/A", 3};
         {
             const char *p = r->info.p, *end = r->info.p + r->info.n;
@@ -494,7 +771,8 @@ int orc_query_one(void *h, const orc_query *q, orc_result *res) {
                     ac_s.p = p + 3;
                     ac_s.n = f.n - 3;
                 } else if (sv_starts(f, "AN=")) {
-                    if (py_int(p + 3, f.n - 3, &an)) {
+                    free(an.big);
+                    if (py_int_big(p + 3, f.n - 3, &an)) {
                         err = ORC_VALUE_ERROR;
                         break;
                     }
@@ -507,111 +785,155 @@ int orc_query_one(void *h, const orc_query *q, orc_result *res) {
                 p = c + 1;
             }
         }
-        if (err) break;
+        if (err) {
+            free(an.big);
+            break;
+        }
 
         /* genotypes of the emitted samples (needed by the GT fallbacks / sample regex) */
         int64_t ncols = 0;
         int have_calls = 0;
         int64_t n_calls = 0;
         if (r->gt) ncols = gt_columns(r, cols, v->n_samples);
+        /* all_calls = digit runs of the subset's GT text (sv:218, :249): value
+         * identity and hash of int(run) (hash(int) = value mod 2**61 - 1) */
 #define GATHER_CALLS()                                                                          \
     do {                                                                                        \
         n_calls = 0;                                                                            \
+        calls_huge = 0;                                                                         \
         for (int32_t si = 0; si < n_sel; si++) {                                                \
             if (sel[si] >= ncols) continue;                                                     \
             sv_t g = cols[sel[si]];                                                             \
             for (int64_t k = 0; k < g.n;) {                                                     \
                 if (isdigit((unsigned char)g.p[k])) {                                           \
-                    int64_t val = 0;                                                            \
-                    while (k < g.n && isdigit((unsigned char)g.p[k])) val = val * 10 + (g.p[k++] - '0'); \
-                    if (n_calls == calls_cap) {                                                 \
+                    int64_t k0 = k;                                                             \
+                    while (k < g.n && isdigit((unsigned char)g.p[k])) k++;                      \
+                    if (n_calls + nh + 1 >= calls_cap) {                                        \
                         calls_cap = calls_cap ? calls_cap * 2 : 1024;                          \
-                        calls = (int64_t *)realloc(calls, sizeof(int64_t) * (size_t)calls_cap); \
+                        while (calls_cap <= n_calls + nh + 1) calls_cap *= 2;                   \
+                        calls = (pyval_t *)realloc(calls, sizeof(pyval_t) * (size_t)calls_cap); \
                     }                                                                           \
-                    calls[n_calls++] = val;                                                     \
+                    if (k - k0 > PY_MAX_STR_DIGITS) calls_huge = 1;                             \
+                    while (k0 < k - 1 && g.p[k0] == '0') k0++;                                  \
+                    pyval_t *pv = &calls[n_calls++];                                            \
+                    pv->v = 0;                                                                  \
+                    pv->hash = 0;                                                               \
+                    pv->d = g.p + k0;                                                           \
+                    pv->dl = (k - k0 > 18) ? k - k0 : 0;                                        \
+                    for (int64_t t = k0; t < k; t++) {                                          \
+                        unsigned __int128 h = (unsigned __int128)pv->hash * 10u + (unsigned)(g.p[t] - '0'); \
+                        pv->hash = (uint64_t)(h % 2305843009213693951ull);                      \
+                        if (!pv->dl) pv->v = pv->v * 10 + (g.p[t] - '0');                       \
+                    }                                                                           \
                 } else                                                                          \
                     k++;                                                                        \
             }                                                                                   \
         }                                                                                       \
         have_calls = 1;                                                                         \
     } while (0)
+#define EMIT_VARIANT(ALT)                                  \
+    do {                                                   \
+        if (n_variants) db_putc(&variants, '\n');          \
+        db_put(&variants, rg.chrom.p, rg.chrom.n);         \
+        db_putc(&variants, '\t');                          \
+        db_put(&variants, r->pos_txt.p, r->pos_txt.n);     \
+        db_putc(&variants, '\t');                          \
+        db_put(&variants, r->ref.p, r->ref.n);             \
+        db_putc(&variants, '\t');                          \
+        db_put(&variants, (ALT).p, (ALT).n);               \
+        db_putc(&variants, '\t');                          \
+        db_put(&variants, vt.p, vt.n);                     \
+        n_variants++;                                      \
+    } while (0)
 
         if (ac_s.n >= 0) { /* sv:205-214 */
             int n_ac = 0;
+            for (int k = 0; k < n_ac_alloc; k++) {
+                free(ac[k].big);
+                ac[k].big = NULL;
+            }
             const char *p = ac_s.p, *end = ac_s.p + ac_s.n;
             for (;;) {
                 const char *c = memchr(p, ',', (size_t)(end - p));
                 if (!c) c = end;
-                int64_t val;
-                if (py_int(p, c - p, &val)) {
+                pyint_t val;
+                if (py_int_big(p, c - p, &val)) {
                     err = ORC_VALUE_ERROR;
                     break;
                 }
                 if (n_ac < MAX_ALTS) ac[n_ac++] = val;
+                else free(val.big);
+                n_ac_alloc = n_ac;
                 if (c == end) break;
                 p = c + 1;
             }
-            if (err) break;
-            for (int k = 0; k < nh; k++)
-                if (hits[k] >= n_ac) err = ORC_INDEX_ERROR; /* sv:207 */
-            if (err) break;
+            if (!err)
+                for (int k = 0; k < nh; k++)
+                    if (hits[k] >= n_ac) err = ORC_INDEX_ERROR; /* sv:207 */
+            if (err) {
+                free(an.big);
+                break;
+            }
             for (int k = 0; k < nh; k++) {
                 int i = hits[k];
-                if (ac[i] != 0) { /* sv:209-213 */
-                    if (n_variants) db_putc(&variants, '\n');
-                    db_put(&variants, rg.chrom.p, rg.chrom.n);
-                    db_putc(&variants, '\t');
-                    db_put(&variants, r->pos_txt.p, r->pos_txt.n);
-                    db_putc(&variants, '\t');
-                    db_put(&variants, r->ref.p, r->ref.n);
-                    db_putc(&variants, '\t');
-                    db_put(&variants, alts[i].p, alts[i].n);
-                    db_putc(&variants, '\t');
-                    db_put(&variants, vt.p, vt.n);
-                    n_variants++;
-                }
-                call_count += ac[i]; /* sv:214 */
+                if (!py_is_zero(&ac[i])) EMIT_VARIANT(alts[i]); /* sv:209-213 */
+                acc_add(&call_count, &ac[i]);                   /* sv:214 */
             }
         } else { /* sv:215-226 genotype fallback */
             GATHER_CALLS();
-            /* set(all_calls) & {i+1}: iterated ascending (CPython small-int set order) */
-            for (int k = 0; k < nh && !err; k++) {
-                int64_t want = hits[k] + 1;
-                int present = 0;
-                for (int64_t c = 0; c < n_calls; c++)
-                    if (calls[c] == want) {
-                        present = 1;
-                        break;
-                    }
-                if (!present) continue;
-                if (want >= n_alt) {
-                    err = ORC_INDEX_ERROR; /* sv:223 alts[i] with 1-based i */
-                    break;
-                }
-                if (n_variants) db_putc(&variants, '\n');
-                db_put(&variants, rg.chrom.p, rg.chrom.n);
-                db_putc(&variants, '\t');
-                db_put(&variants, r->pos_txt.p, r->pos_txt.n);
-                db_putc(&variants, '\t');
-                db_put(&variants, r->ref.p, r->ref.n);
-                db_putc(&variants, '\t');
-                db_put(&variants, alts[want].p, alts[want].n);
-                db_putc(&variants, '\t');
-                db_put(&variants, vt.p, vt.n);
-                n_variants++;
+            if (calls_huge) { /* int(g) of a run past 4300 digits */
+                err = ORC_VALUE_ERROR;
+                free(an.big);
+                break;
             }
-            if (err) break;
+            /* set(all_calls) & {i + 1 for i in hit_indexes}, iterated in CPython order */
+            pset_t sc, hs, res;
+            pset_init(&sc);
+            pset_init(&hs);
+            pset_init(&res);
+            for (int64_t c = 0; c < n_calls; c++) pset_add(&sc, calls, calls[c].hash, c);
+            for (int k = 0; k < nh; k++) {
+                pyval_t *hv = &calls[n_calls + k];
+                hv->v = hits[k] + 1;
+                hv->hash = (uint64_t)hv->v;
+                hv->d = NULL;
+                hv->dl = 0;
+                pset_add(&hs, calls, hv->hash, n_calls + k);
+            }
+            const pset_t *so = &sc, *other = &hs; /* set_intersection(so, other) */
+            if (hs.used > sc.used) {
+                so = &hs;
+                other = &sc;
+            }
+            for (uint64_t k = 0; k <= other->mask; k++)
+                if (other->t[k].used && pset_contains(so, calls, other->t[k].hash, other->t[k].key))
+                    pset_add(&res, calls, other->t[k].hash, other->t[k].key);
+            for (uint64_t k = 0; k <= res.mask && !err; k++)
+                if (res.t[k].used && calls[res.t[k].key].v >= n_alt) err = ORC_INDEX_ERROR; /* sv:223 alts[i], 1-based i */
+            if (!err)
+                for (uint64_t k = 0; k <= res.mask; k++)
+                    if (res.t[k].used) EMIT_VARIANT(alts[calls[res.t[k].key].v]);
+            free(sc.t);
+            free(hs.t);
+            free(res.t);
+            if (err) {
+                free(an.big);
+                break;
+            }
+            memset(is_hit, 0, (size_t)n_alt + 1);
+            for (int k = 0; k < nh; k++) is_hit[hits[k] + 1] = 1;
+            int64_t cnt = 0;
             for (int64_t c = 0; c < n_calls; c++)
-                for (int k = 0; k < nh; k++)
-                    if (calls[c] == hits[k] + 1) {
-                        call_count++; /* sv:226 */
-                        break;
-                    }
+                if (!calls[c].dl && calls[c].v >= 1 && calls[c].v <= n_alt && is_hit[calls[c].v]) cnt++; /* sv:226 */
+            acc_add_i64(&call_count, cnt);
         }
 
-        if (call_count) { /* sv:229 cumulative */
+        if (acc_nonzero(&call_count)) { /* sv:229 cumulative */
             exists = 1;
-            if (!q->include_details) break; /* sv:231-232 (before AN is added) */
+            if (!q->include_details) { /* sv:231-232 (before AN is added) */
+                free(an.big);
+                break;
+            }
             int collect = (q->granularity == ORC_RECORD || q->granularity == ORC_AGGREGATED) &&
                           (samples_variant || include_samples); /* sv:235, svs:231 */
             if (collect) {
@@ -639,21 +961,27 @@ int orc_query_one(void *h, const orc_query *q, orc_result *res) {
         }
         /* sv:244-250 */
         if (have_an) {
-            all_alleles_count += an;
+            acc_add(&all_alleles_count, &an);
         } else {
-            if (!have_calls) GATHER_CALLS();
-            all_alleles_count += n_calls;
+            if (!have_calls) GATHER_CALLS(); /* get_all_calls: strings, no int() */
+            acc_add_i64(&all_alleles_count, n_calls);
         }
+        free(an.big);
         if (!samples_variant && q->granularity == ORC_BOOLEAN && exists) break; /* sv:253-254 */
     }
 #undef GATHER_CALLS
+#undef EMIT_VARIANT
 
     free(alts);
     free(hits);
+    free(is_hit);
     free(cols);
+    for (int k = 0; k < n_ac_alloc; k++) free(ac[k].big);
     free(ac);
     free(calls);
     if (err) {
+        acc_free(&call_count);
+        acc_free(&all_alleles_count);
         free(sel);
         free(sample_hit);
         free(variants.p);
@@ -661,8 +989,10 @@ int orc_query_one(void *h, const orc_query *q, orc_result *res) {
         return err;
     }
     res->exists = exists;
-    res->call_count = call_count;
-    res->all_alleles_count = all_alleles_count;
+    acc_out(&call_count, &res->call_count, &res->call_count_hex);
+    acc_out(&all_alleles_count, &res->all_alleles_count, &res->all_alleles_count_hex);
+    acc_free(&call_count);
+    acc_free(&all_alleles_count);
     res->variants = variants.p ? variants.p : (char *)calloc(1, 1);
     res->n_variants = n_variants;
     /* sv:257-258 / svs:248-249 sample names; all_sample_names comes from the first

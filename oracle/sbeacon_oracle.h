@@ -59,6 +59,11 @@ typedef struct {
     int64_t n_sample_indices;
     char *sample_names;      /* ','-joined (malloc) */
     int64_t n_sample_names;
+    /* Python ints are unbounded: when call_count / all_alleles_count does not
+     * fit int64 the exact value is here as "0x.." / "-0x.." text (malloc;
+     * NULL when the int64 field is exact) */
+    char *call_count_hex;
+    char *all_alleles_count_hex;
 } orc_result;
 
 void *orc_load_vcf(const char *path, int load_gt);

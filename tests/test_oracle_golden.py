@@ -43,6 +43,28 @@ def test_oracle_matches_reference_goldens(goldens, oracles):
     assert not bad, bad[:5]
 
 
+def test_oracle_matches_general_goldens(general_goldens):
+    """General records (> 64 ALTs, AC / AN past int32 / int64 up to 4300
+    digits, GT fallbacks with ploidy > 3, alleles >= 8 whose variants come in
+    CPython set order, huge GT tokens): the oracle against the reference."""
+    from oracle.oracle import OracleVcf
+    o = OracleVcf(os.path.join(FIXTURES, 'general22.vcf'))
+    kinds = {c['error'] for c in general_goldens}
+    assert {None, 'IndexError', 'ValueError'} <= kinds
+    assert any(isinstance((c['response'] or {}).get('call_count'), dict) for c in general_goldens)
+    bad = []
+    for i, c in enumerate(general_goldens):
+        try:
+            got, err = o.perform_query(c['payload'], patched=c['oracle'] == 'patched-oracle'), None
+        except Exception as e:  # noqa: BLE001
+            got, err = None, type(e).__name__
+        if err != c['error']:
+            bad.append((i, 'error', err, c['error']))
+        elif got is not None and normalise(got) != normalise(c['response']):
+            bad.append((i, 'response'))
+    assert not bad, bad[:5]
+
+
 def test_oracle_region_count(oracles):
     o = oracles['tiny22']
     assert o.records_in_region('22:1-10') == 0
