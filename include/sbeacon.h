@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SB_ABI_VERSION 1
+#define SB_ABI_VERSION 2
 
 /* ---- error codes ------------------------------------------------------- */
 enum {
@@ -145,6 +145,15 @@ typedef struct {
     const uint32_t *hit_alt;    /* alt index used for the label (0-based) */
     uint64_t n_sample_indices;  /* indices into the emitted sample list */
     const uint32_t *sample_indices;
+    /* Python ints are unbounded (search_variants.py:199,206,214,245): when
+     * call_count or all_alleles_count needs more than 64 bits, both exact
+     * values are here as big_limbs 32-bit limbs each, two's complement,
+     * little-endian (the int64 fields then hold their low 64 bits);
+     * big_limbs = 0 otherwise */
+    uint32_t big_limbs;
+    uint32_t _pad;
+    const uint32_t *big_call_count;
+    const uint32_t *big_all_alleles_count;
 } sb_result_view;
 
 int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out);
@@ -316,8 +325,10 @@ int sb_dedup_count_files(sb_store *s, const sb_dedup_file_job *jobs, size_t n_jo
 /* ---- CSI / TBI index of a BGZF VCF (host only, no device) -----------------
  * The index summariseVcf reads its chunk boundaries from
  * (lambda/summariseVcf/lambda_function.py:90-104 get_chunk_boundaries,
- * :144-156 get_vcf_index; index_reader.py:4-125 Csi / Tbi), as
- * `bcftools index` / `tabix -p vcf` would write it next to the VCF.
+ * :144-156 get_vcf_index; index_reader.py:4-125 Csi / Tbi), in the place of
+ * the one `bcftools index` / `tabix -p vcf` writes next to the VCF: the same
+ * binning and chunk boundaries, not byte-identical to htslib's file (linear
+ * index fill and bin loff differ; see csrc/index.cpp).
  * min_shift <= 0 -> 14; depth <= 0 -> 5 for TBI, and for CSI the smallest
  * depth >= 5 covering the longest record.  *out = the BGZF-compressed index
  * (release with sb_free).  SB_EINVAL for an unsorted VCF or a position past

@@ -881,6 +881,10 @@ int orc_query_one(void *h, const orc_query *q, orc_result *res) {
             }
         } else { /* sv:215-226 genotype fallback */
             GATHER_CALLS();
+            if (n_calls + nh + 1 >= calls_cap) { /* room for the hit_set values after the calls */
+                calls_cap = n_calls + nh + 1024;
+                calls = (pyval_t *)realloc(calls, sizeof(pyval_t) * (size_t)calls_cap);
+            }
             if (calls_huge) { /* int(g) of a run past 4300 digits */
                 err = ORC_VALUE_ERROR;
                 free(an.big);

@@ -224,6 +224,10 @@ struct sb_batch {
     // per-request rows (sb_batch_set_owners): seg = n_rows + 1 query offsets
     uint32_t n_rows = 0;
     DevMem seg, herr;
+    // general records (general_slice_kernel): work list [count, launch
+    // indices], per-wave scratch, slices with counts past 64 bits
+    DevMem gen_work, gen_scratch, gen_big_n, gen_big, gen_limbs;
+    uint32_t gen_grid = 0, gen_big_cap = 0;
     // events around the runs since the last sync (run() records [0], sync() [1])
     std::array<hipEvent_t, 2> ev{};
     size_t runs_pending = 0;
@@ -248,6 +252,9 @@ struct sb_result_set {
     std::vector<uint8_t> vbuilt, nbuilt;
     std::string distinct;                       // sb_result_distinct_variants
     std::vector<uint32_t> tmp_rec, tmp_alt;     // views for sb_result_get
+    // queries whose counts need more than 64 bits: 2 x big_limbs limbs each
+    uint32_t big_limbs = 0;
+    std::unordered_map<uint32_t, std::vector<uint32_t>> big;
     sb_batch_stats stats{};
 };
 
@@ -302,6 +309,11 @@ void upload_store(sb_builder &b, sb_store &s) {
     std::vector<uint32_t> dk_pos, dk_lo, dk_bad;
     std::vector<uint64_t> dk_hash, dk_tail;
     std::vector<uint8_t> dk_blob;
+    // general records (GenRec side table), global indexing
+    std::vector<GenRec> gen;
+    std::vector<uint64_t> gnum_off{0}, gtok_off;
+    std::vector<uint32_t> gnum, gtok;
+    std::vector<GenVal> gval;
     uint64_t nr = 0, nx = 0, np = 0, nk = 0;
     for (auto &v : b.vcfs) {
         nr += v.c.pos.size();
@@ -334,6 +346,29 @@ void upload_store(sb_builder &b, sb_store &s) {
         std::vector<uint64_t>().swap(c.planes0);  // the device copy is the only one used after upload
         std::vector<uint64_t>().swap(c.planesx);
         rec.insert(rec.end(), c.rec.begin(), c.rec.end());
+        {  // general records: global record / number / token / value indices
+            const uint32_t gen0 = static_cast<uint32_t>(gen.size());
+            const uint64_t num0 = gnum_off.size() - 1, tok0 = gtok_off.size(), gt0 = gtok.size();
+            const uint32_t val0 = static_cast<uint32_t>(gval.size());
+            const uint64_t limb0 = gnum.size();
+            for (size_t k = 0; k < c.gen.size(); ++k) {
+                GenRec g = c.gen[k];
+                rec[rec_base + g.rec].ac0 = static_cast<int32_t>(gen0 + k);
+                g.rec += rec_base;
+                g.ac_num += num0;
+                g.an_num += num0;
+                if (g.flags & GR_FB) {
+                    g.tok_off += tok0;
+                    g.val_off += val0;
+                }
+                gen.push_back(g);
+            }
+            for (size_t k = 1; k < c.gnum_off.size(); ++k) gnum_off.push_back(c.gnum_off[k] + limb0);
+            gnum.insert(gnum.end(), c.gnum.begin(), c.gnum.end());
+            for (uint64_t o : c.gtok_off) gtok_off.push_back(o + gt0);
+            gtok.insert(gtok.end(), c.gtok.begin(), c.gtok.end());
+            gval.insert(gval.end(), c.gval.begin(), c.gval.end());
+        }
         rng.insert(rng.end(), c.rng.begin(), c.rng.end());
         pos.insert(pos.end(), c.pos.begin(), c.pos.end());
         a0_len.insert(a0_len.end(), c.a0_len.begin(), c.a0_len.end());
@@ -382,6 +417,33 @@ void upload_store(sb_builder &b, sb_store &s) {
     }
     s.n_records = pos.size();
     s.n_extra = x_key.size();
+    if (gen.size() > 0xffffffffull) throw Error(SB_EINVAL, "more than 2^32 general records");
+    {  // general records: numbers repacked to one limb count (sign-extended)
+        uint32_t L = 2;
+        for (size_t k = 0; k + 1 < gnum_off.size(); ++k)
+            L = std::max<uint32_t>(L, static_cast<uint32_t>(gnum_off[k + 1] - gnum_off[k]));
+        if (L + 2 > kGenAccMax) throw Error(SB_EPARSE, "an INFO integer beyond the general path's width");
+        const size_t nn = gnum_off.size() - 1;
+        std::vector<uint32_t> num(nn * L);
+        for (size_t k = 0; k < nn; ++k) {
+            const uint64_t a = gnum_off[k], e = gnum_off[k + 1];
+            const uint32_t sgn = (gnum[e - 1] >> 31) ? 0xffffffffu : 0u;
+            for (uint32_t j = 0; j < L; ++j) num[k * L + j] = a + j < e ? gnum[a + j] : sgn;
+        }
+        s.g.n = static_cast<uint32_t>(gen.size());
+        s.g.limbs = L;
+        s.g.acc_limbs = std::max<uint32_t>(L + 2, 4);
+        s.g.max_alt = s.g.max_vals = 0;
+        for (const GenRec &g : gen) {
+            s.g.max_alt = std::max(s.g.max_alt, g.n_alt);
+            s.g.max_vals = std::max(s.g.max_vals, g.n_vals);
+        }
+        s.g.rec = dev_upload(s, gen);
+        s.g.num = dev_upload(s, num);
+        s.g.tok_off = dev_upload(s, gtok_off);
+        s.g.tok = dev_upload(s, gtok);
+        s.g.val = dev_upload(s, gval);
+    }
 
     s.d.rec = dev_upload(s, rec);
     s.d.rng = dev_upload(s, rng);
@@ -1130,6 +1192,18 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     B.res.alloc(size_t(nq) * sizeof(QRes));
     B.hits.alloc(B.cap_total * 8);
     B.samples_out.alloc(samples_words * 8);
+    if (s.g.n && nq) {  // general records: work list + scratch (general_slice_kernel)
+        uint32_t hw, tc;
+        const uint64_t wb = general_wave_bytes(s.g, &hw, &tc);
+        const uint64_t budget = uint64_t(256) << 20;
+        B.gen_grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>({nq, 1024, budget / wb})));
+        B.gen_work.alloc((size_t(nq) + 1) * 4);
+        B.gen_scratch.alloc(size_t(B.gen_grid) * wb);
+        B.gen_big_cap = std::min<uint32_t>(nq, 4096);
+        B.gen_big_n.alloc(4);
+        B.gen_big.alloc(size_t(B.gen_big_cap) * sizeof(GenBig));
+        B.gen_limbs.alloc(size_t(B.gen_big_cap) * 2 * kGenAccMax * 4);
+    }
     HIP_OK(hipStreamSynchronize(st));
 }
 
@@ -1139,6 +1213,8 @@ void run(sb_batch &B) {
     hipStream_t st = B.strm();
     DStore d = s.d;
     d.sym_lut = B.lut.as<uint32_t>();
+    d.q_all = B.q.as<QDev>();
+    d.gen_work = B.gen_grid ? B.gen_work.as<uint32_t>() : nullptr;
     // timing: one event before the first run since the last sync and one at
     // the sync (sync()); no marker between back-to-back runs (a marker pair
     // per run measured ~8 us of stream gap per run on MI355X)
@@ -1146,6 +1222,10 @@ void run(sb_batch &B) {
         for (auto &e : B.ev) HIP_OK(hipEventCreate(&e));
     }
     if (B.runs_pending++ == 0) HIP_OK(hipEventRecord(B.ev[0], st));
+    if (B.gen_grid) {
+        HIP_OK(hipMemsetAsync(B.gen_work.p, 0, 4, st));
+        HIP_OK(hipMemsetAsync(B.gen_big_n.p, 0, 4, st));
+    }
     // chains of variantType slices (one wave per request's slices)
     launch_chains(d, B.chains.as<ChainDev>(), static_cast<uint32_t>(B.hchains.size()), B.runs.as<uint32_t>(),
                   static_cast<uint32_t>(B.hruns.size() - 1), B.corig.as<uint32_t>(),
@@ -1171,6 +1251,10 @@ void run(sb_batch &B) {
             launch_scan(d, B.q.as<QDev>() + g.base, nullptr, static_cast<uint32_t>(g.idx.size()), B.nonneg,
                         g.max_words, g.mode, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(), B.res.as<QRes>(),
                         B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), st);
+    // slices whose scan reached a general record (work list filled above)
+    launch_general(d, s.g, B.gen_work.as<uint32_t>(), B.gen_grid, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(),
+                   B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), B.gen_scratch.as<uint8_t>(),
+                   B.gen_big_n.as<uint32_t>(), B.gen_big.as<GenBig>(), B.gen_limbs.as<uint32_t>(), B.gen_big_cap, st);
     HIP_OK(hipGetLastError());
 }
 
@@ -1212,6 +1296,27 @@ sb_result_set *fetch(sb_batch &B) {
     for (uint32_t i = 0; i < nq; ++i) {
         if (B.host_err[i]) R->res[i].error = B.host_err[i];
         if (!B.chained.empty() && B.chained[i]) R->res[i].n_scanned = B.nscan[i];
+    }
+    if (B.gen_grid) {  // general slices whose counts need more than 64 bits
+        uint32_t nb = 0;
+        HIP_OK(hipMemcpy(&nb, B.gen_big_n.p, 4, hipMemcpyDeviceToHost));
+        if (nb > B.gen_big_cap)
+            throw Error(SB_ENOMEM, "more than " + std::to_string(B.gen_big_cap) +
+                                       " slices of one batch have counts past 64 bits: split the batch");
+        if (nb) {
+            std::vector<GenBig> bl(nb);
+            std::vector<uint32_t> limbs(size_t(nb) * 2 * kGenAccMax);
+            HIP_OK(hipMemcpy(bl.data(), B.gen_big.p, nb * sizeof(GenBig), hipMemcpyDeviceToHost));
+            HIP_OK(hipMemcpy(limbs.data(), B.gen_limbs.p, limbs.size() * 4, hipMemcpyDeviceToHost));
+            const uint32_t W = (s.g.acc_limbs + 63) / 64 * 64;
+            R->big_limbs = W;
+            for (uint32_t k = 0; k < nb; ++k) {
+                const uint32_t *p = limbs.data() + size_t(k) * 2 * kGenAccMax;
+                std::vector<uint32_t> v(p, p + W);
+                v.insert(v.end(), p + kGenAccMax, p + kGenAccMax + W);
+                R->big[bl[k].orig] = std::move(v);
+            }
+        }
     }
     // dense offsets on the host, gather on the device, one D2H
     R->dense_off.assign(size_t(nq) + 1, 0);
@@ -2634,6 +2739,11 @@ int sb_batch_set_owners(sb_batch *b, const uint32_t *owner, size_t nq, uint32_t 
         std::vector<uint8_t> he(std::max<size_t>(nq, 1), 0);
         for (size_t i = 0; i < nq; ++i) he[i] = b->host_err[i] ? 1 : 0;
         std::lock_guard<std::mutex> lk(b->s->mu);
+        // per-slice rows off (sb_batch_set_slice_results(0)) needs every chain in
+        // one row: a split chain's slices would have no QRes rows to reduce
+        if (!pieces_ok && !b->slice_rows)
+            throw Error(SB_EINVAL, "a chain of slices spans request rows while per-slice results are off "
+                                   "(sb_batch_set_slice_results(b, 1) first)");
         HIP_OK(hipSetDevice(b->s->device));
         hipStream_t st = b->s->stream;
         b->seg.alloc(seg.size() * 4);
@@ -2670,6 +2780,8 @@ int sb_batch_reduce_requests(sb_batch *b, void *dev_out) {
         if (!b || (!dev_out && b->n_rows)) throw Error(SB_EINVAL, "NULL argument");
         if (!b->seg.p && b->n_rows) throw Error(SB_EINVAL, "sb_batch_set_owners was not called");
         std::lock_guard<std::mutex> lk(b->s->mu);
+        if (!b->row_pieces && b->slice_rows_stale)
+            throw Error(SB_EINVAL, "the last run skipped per-slice results that a per-query reduction needs");
         HIP_OK(hipSetDevice(b->s->device));
         if (b->row_pieces)
             launch_row_reduce(b->cpart.as<ReqPartial>(), b->chains.as<ChainDev>(), b->hoff.as<uint64_t>(),
@@ -2733,6 +2845,8 @@ int sb_batch_compact_hits(sb_batch *b, const void *dev_rows, void *dev_hits, voi
         if (!b || (!dev_hits && b->cap_total) || !dev_row_off) throw Error(SB_EINVAL, "NULL argument");
         if (!b->seg.p) throw Error(SB_EINVAL, "sb_batch_set_owners was not called");
         std::lock_guard<std::mutex> lk(b->s->mu);
+        if (!b->row_pieces && b->slice_rows_stale)
+            throw Error(SB_EINVAL, "the last run skipped per-slice results that per-query hit lists need");
         HIP_OK(hipSetDevice(b->s->device));
         hipStream_t st = b->strm();
         if (b->row_pieces) {  // over rows and pieces (chains as one contiguous copy each)
@@ -2802,6 +2916,17 @@ int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out) {
     out->hit_alt = r->tmp_alt.data() + a;
     out->n_sample_indices = r->sidx[i].size();
     out->sample_indices = r->sidx[i].data();
+    out->big_limbs = 0;
+    out->_pad = 0;
+    out->big_call_count = out->big_all_alleles_count = nullptr;
+    if (!r->big.empty()) {
+        auto it = r->big.find(static_cast<uint32_t>(i));
+        if (it != r->big.end() && !q.error) {
+            out->big_limbs = r->big_limbs;
+            out->big_call_count = it->second.data();
+            out->big_all_alleles_count = it->second.data() + r->big_limbs;
+        }
+    }
     return SB_OK;
 }
 

@@ -33,9 +33,61 @@ enum : uint32_t {
     C_SYM_SHIFT = 16,         // symbolic-ALT dictionary id
 };
 
-// RecHot::an of a record the store cannot represent (H_AN_BAD is set too):
-// a query that reaches it raises SB_QERR_UNSUPPORTED (ingest.cpp unrep)
+// RecHot::an of a *general record* (H_AN_BAD is set too; RecHot::ac0 = its
+// GenRec index): one the packed words cannot hold -- more than 64 ALTs, an
+// AC / AN integer outside int32 (Python ints are unbounded below CPython's
+// 4300-digit int() limit), a GT fallback with ploidy > 3 or allele numbers >=
+// 255, or a GT fallback over >= 8 ALTs (the variant order is then CPython's
+// set iteration order, search_variants.py:223).  Every scan kernel stops at a
+// general record it reaches and hands the slice (SB_QERR_GENERAL, internal)
+// to general_slice_kernel, which answers it from the GenRec side table.
 constexpr int32_t kAnUnrepresentable = INT32_MIN;
+constexpr int32_t SB_QERR_GENERAL = 10;  // internal: never leaves the library
+
+enum : uint32_t {
+    GR_HAS_AC = 1u << 0,    // INFO has an AC= tag
+    GR_HAS_AN = 1u << 1,    // INFO has an AN= tag
+    GR_AC_BAD = 1u << 2,    // an entry of the last AC= fails int() -> ValueError (:206)
+    GR_AN_BAD = 1u << 3,    // an AN= fails int() -> ValueError (:199)
+    GR_FB = 1u << 4,        // no AC or no AN, and samples: GT digit runs kept (tok / val)
+};
+struct alignas(16) GenRec {
+    uint32_t rec;       // global record index
+    uint32_t flags;     // GR_*
+    uint32_t n_alt;     // len(ALT.split(','))
+    uint32_t n_ac;      // entries of the last AC= (GR_HAS_AC, not GR_AC_BAD)
+    uint64_t ac_num;    // first of its n_ac numbers (GStore::num)
+    uint64_t an_num;    // its AN (GR_HAS_AN, not GR_AN_BAD)
+    uint64_t tok_off;   // GR_FB: n_samples + 1 offsets into GStore::tok (per header sample)
+    uint32_t n_vals;    // GR_FB: distinct digit-run values, numbered in first-occurrence order
+    uint32_t val_off;   //   (over all samples) from GStore::val + val_off
+    uint32_t a0_cls;    // C_* class bits of ALT 0 (+ symbolic id); ALTs >= 1 are extra rows
+    uint32_t pad[3];
+};
+static_assert(sizeof(GenRec) == 64, "GenRec is four 16-byte words");
+// one distinct GT digit-run value of a GR_FB record (int(run), :218)
+struct alignas(16) GenVal {
+    uint64_t hash;    // CPython hash(int): value mod 2**61 - 1
+    uint32_t allele;  // the value when it is an allele number 1 .. n_alt, else 0
+    uint32_t huge;    // run longer than 4300 digits: int() raises ValueError
+};
+struct GStore {
+    const GenRec *rec;
+    const uint32_t *num;      // numbers as `limbs` u32 limbs each, two's complement, little-endian
+    const uint64_t *tok_off;  // per GR_FB record: n_samples + 1 offsets into tok
+    const uint32_t *tok;      // digit-run value ids, sample by sample, in GT text order
+    const GenVal *val;
+    uint32_t n, limbs;        // records; limbs per number
+    uint32_t acc_limbs;       // limbs of a running sum (limbs + 2, <= kGenAccMax)
+    uint32_t max_alt, max_vals;  // over the records (scratch sizing)
+};
+constexpr uint32_t kGenAccGroups = 8;                 // 64-limb groups a sum may span
+constexpr uint32_t kGenAccMax = 64 * kGenAccGroups;   // 16384 bits > a 4300-digit value + headroom
+// a general slice whose call_count or all_alleles_count needs more than 64 bits
+struct GenBig {
+    uint32_t orig;  // QRes row
+    uint32_t pad;
+};
 
 struct alignas(16) RecHot {
     uint32_t end;  // POS + len(REF) - 1 (:90)
@@ -220,6 +272,8 @@ struct alignas(8) XRow {
     int32_t ac;    // INFO AC entry, or its GT count when AC is absent
 };
 
+struct QDev;
+
 struct DStore {
     // record-indexed
     const RecHot *rec;
@@ -252,6 +306,11 @@ struct DStore {
     const uint32_t *fb;       // fallback rows: per sample [n:8][v0:8][v1:8][v2:8]
     const uint32_t *bucket;   // coarse POS index of every segment
     const uint32_t *sym_lut;  // per query-distinct variantType: bitset over sym ids
+    // per run: the batch's launch-ordered queries and the general-slice work
+    // list ([0] = count, then launch indices); nullptr = the store has no
+    // general record
+    const QDev *q_all;
+    uint32_t *gen_work;
 };
 
 struct QDev {

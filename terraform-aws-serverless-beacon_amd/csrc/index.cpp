@@ -7,6 +7,14 @@
 // `bcftools index` / `tabix -p vcf`; the ingest writes one here so a VCF
 // arriving without an index still gets the reference's slices.
 //
+// The file is a valid SAMv1 §5 index that index_reader.py (and htslib)
+// parse, with the chunk boundaries summariseVcf reads; it is NOT claimed to
+// be byte-identical to what htslib writes (htslib is absent here, so that is
+// unpinned): empty linear-index windows take the NEXT window's offset (htslib
+// forward-fills from the previous one), a bin's loff is its smallest record
+// offset (htslib: the linear-index entry of its bottom bin) and the CSI
+// default depth is 5 (bcftools' tbx path uses 6).
+//
 // Layout: SAMv1 §5 (binning scheme, CSI v1 and tabix formats).  A record
 // covers [POS-1, POS-1+len(REF)), or [POS-1, END) when INFO carries END= past
 // POS (the tabix VCF preset).  Chunks are built as htslib's hts_idx_push does:

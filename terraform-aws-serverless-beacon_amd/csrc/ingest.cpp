@@ -16,7 +16,9 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <string_view>
 #include <thread>
+#include <unordered_map>
 #include <zlib.h>
 
 #include "store.hpp"
@@ -34,6 +36,12 @@ struct Local {  // one thread's parse of a run of lines
     int err = 0;
     std::string msg;
     size_t err_line = 0;
+    // per-record scratch, reused record to record
+    std::vector<const char *> alt_p, ac_p;
+    std::vector<size_t> alt_n, ac_n;
+    std::vector<int64_t> acv, gtcount;
+    std::vector<uint32_t> limbs;
+    std::unordered_map<std::string_view, uint32_t> val_id;
 };
 
 inline bool is_digit(char c) { return c >= '0' && c <= '9'; }
@@ -329,36 +337,32 @@ struct Parser {
         c.ref_key.push_back(ref_key);
         c.ref_off.push_back(c.blob.size());
         c.blob.insert(c.blob.end(), ref, ref + ref_len);
-        // ALT split on ',' (:97)
-        // unrep: the record is beyond what the device words represent (> 64
-        // ALTs, AC / AN / called alleles beyond int32, a GT fallback row
-        // with ploidy > 3 or allele >= 255).  It is stored as a placeholder
-        // (REF, end, ALT 0) whose evaluation raises SB_QERR_UNSUPPORTED for
-        // any query that reaches it, instead of failing the whole VCF.
-        bool unrep = false;
-        const char *alts[64];
-        size_t alens[64];
-        uint32_t na = 0;
+        // ALT split on ',' (:97): any number of ALTs
+        auto &alt_p = L.alt_p;
+        auto &alt_n = L.alt_n;
+        alt_p.clear();
+        alt_n.clear();
         {
             const char *a = f[4], *ae = f[4] + n[4];
             for (;;) {
                 const char *cm = static_cast<const char *>(memchr(a, ',', static_cast<size_t>(ae - a)));
                 if (!cm) cm = ae;
-                if (na == 64) {
-                    unrep = true;  // ALTs past the 64th are not stored
-                } else {
-                    alts[na] = a;
-                    alens[na] = static_cast<size_t>(cm - a);
-                    ++na;
-                }
+                alt_p.push_back(a);
+                alt_n.push_back(static_cast<size_t>(cm - a));
                 if (cm == ae) break;
                 a = cm + 1;
             }
         }
+        if (alt_p.size() > 0xfffffffull) return fail(L, "more than 2^28 ALTs in one record");
+        uint32_t na = static_cast<uint32_t>(alt_p.size());
+        // general: the packed words cannot hold this record (devtypes.hpp GenRec)
+        bool general = na > 64;
         // ---- INFO (:195-201): last AC= string, every AN= parsed, last VT=
-        const char *ac_p = nullptr;
-        size_t ac_n = 0;
-        bool has_ac = false, has_an = false, an_bad = false;
+        const char *ac_s = nullptr;
+        size_t ac_sn = 0;
+        const char *an_s = nullptr;  // text of the last AN= (general records re-parse it)
+        size_t an_sn = 0;
+        bool has_ac = false, has_an = false, an_bad = false, an_big = false;
         int64_t an_val = 0;
         int64_t vt_off = -1;
         uint32_t vt_len = 0;
@@ -371,16 +375,20 @@ struct Parser {
                 if (fl >= 3 && a[2] == '=') {
                     if (a[0] == 'A' && a[1] == 'C') {
                         has_ac = true;
-                        ac_p = a + 3;
-                        ac_n = fl - 3;
+                        ac_s = a + 3;
+                        ac_sn = fl - 3;
                     } else if (a[0] == 'A' && a[1] == 'N') {
-                        int64_t v;
+                        int64_t v = 0;
                         if (!an_bad) {
-                            if (py_int(a + 3, fl - 3, &v)) {
-                                an_val = v;
-                                has_an = true;
-                            } else {
+                            const int st = py_int_ex(a + 3, fl - 3, &v);
+                            if (st < 0) {
                                 an_bad = true;
+                            } else {
+                                an_val = v;
+                                an_big = st == 1;
+                                an_s = a + 3;
+                                an_sn = fl - 3;
+                                has_an = true;
                             }
                         }
                     } else if (a[0] == 'V' && a[1] == 'T') {
@@ -395,31 +403,38 @@ struct Parser {
         }
         L.vt_off.push_back(vt_off);
         L.vt_len.push_back(vt_len);
-        if (has_an && (an_val > INT32_MAX || an_val < INT32_MIN)) unrep = true;
+        if (has_an && (an_big || an_val > INT32_MAX || an_val < INT32_MIN)) general = true;
         // AC values (:206)
-        int64_t acv[64];
-        uint32_t n_ac = 0;
+        auto &acv = L.acv;
+        acv.clear();
+        L.ac_p.clear();
+        L.ac_n.clear();
         bool ac_bad = false;
         if (has_ac) {
-            const char *a = ac_p, *ae = ac_p + ac_n;
+            const char *a = ac_s, *ae = ac_s + ac_sn;
             for (;;) {
                 const char *cm = static_cast<const char *>(memchr(a, ',', static_cast<size_t>(ae - a)));
                 if (!cm) cm = ae;
-                int64_t v;
-                if (!py_int(a, static_cast<size_t>(cm - a), &v)) {
+                int64_t v = 0;
+                const int st = py_int_ex(a, static_cast<size_t>(cm - a), &v);
+                if (st < 0) {
                     ac_bad = true;
                 } else {
-                    if (v > INT32_MAX || v < INT32_MIN) unrep = true;
-                    if (n_ac < 64) acv[n_ac] = v;
-                    ++n_ac;
+                    if (st == 1 || v > INT32_MAX || v < INT32_MIN) general = true;
+                    acv.push_back(st == 1 ? 0 : v);
+                    L.ac_p.push_back(a);
+                    L.ac_n.push_back(static_cast<size_t>(cm - a));
                 }
                 if (cm == ae) break;
                 a = cm + 1;
             }
         }
+        const uint32_t n_ac = static_cast<uint32_t>(acv.size());
+        // a GT fallback over >= 8 ALTs emits variants in CPython set order (:223)
+        if (!has_ac && n_samples > 0 && na >= 8) general = true;
         // ---- genotypes
-        int64_t gtcount[64];
-        for (uint32_t i = 0; i < na; ++i) gtcount[i] = 0;
+        auto &gtcount = L.gtcount;
+        gtcount.assign(na, 0);
         int64_t gt_an = 0;
         const bool need_fb = (!has_ac || !has_an || an_bad) && n_samples > 0;
         const size_t plane0 = c.planes0.size(), planex = c.planesx.size();
@@ -427,15 +442,16 @@ struct Parser {
             c.planes0.resize(plane0 + words, 0ull);
             c.planesx.resize(planex + static_cast<size_t>(na - 1) * words, 0ull);
         }
+        const size_t fb0 = c.fb.size();
         int64_t fb_row = -1;
-        if (need_fb) {
+        if (need_fb && !general) {
             fb_row = static_cast<int64_t>(c.fb.size());
             c.fb.resize(c.fb.size() + n_samples, 0u);
         }
+        int gt_idx = -1;
         if (n_samples) {
             if (col < 9) return fail(L, "missing FORMAT/sample columns");
             // FORMAT: index of GT
-            int gt_idx = -1;
             {
                 int k = 0;
                 const char *a = f[8], *ae = f[8] + n[8];
@@ -454,23 +470,12 @@ struct Parser {
                 if (a > e) return fail(L, "fewer sample columns than header samples");
                 const char *t = static_cast<const char *>(memchr(a, '\t', static_cast<size_t>(e - a)));
                 if (!t) t = e;
-                // GT subfield
-                const char *g = a, *ge = t;
-                if (gt_idx < 0) {
-                    g = ".";
-                    ge = g + 1;  // no GT key: bcftools prints '.'  (unpinned)
-                } else {
-                    for (int k = 0; k < gt_idx && g < ge; ++k) {
-                        const char *cl = static_cast<const char *>(memchr(g, ':', static_cast<size_t>(ge - g)));
-                        g = cl ? cl + 1 : ge;
-                    }
-                    const char *cl = static_cast<const char *>(memchr(g, ':', static_cast<size_t>(ge - g)));
-                    if (cl) ge = cl;
-                }
+                const char *g, *ge;
+                gt_field(a, t, gt_idx, &g, &ge);
                 const size_t gl = static_cast<size_t>(ge - g);
                 if (gl == 3 && g[0] == '0' && g[2] == '0' && (g[1] == '|' || g[1] == '/')) {
                     gt_an += 2;  // hot path: homozygous REF
-                    if (need_fb) c.fb[static_cast<size_t>(fb_row) + s] = 2u;
+                    if (fb_row >= 0) c.fb[static_cast<size_t>(fb_row) + s] = 2u;
                 } else {
                     // digit runs (re '[0-9]+'): calls for counts / AN fallback
                     uint32_t nrun = 0, vals[3] = {0, 0, 0};
@@ -486,7 +491,7 @@ struct Parser {
                             if (v >= 1 && v <= na) gtcount[v - 1]++;
                             if (need_fb) {
                                 if (nrun >= 3 || v > 254)
-                                    unrep = true;
+                                    general = true;  // beyond the packed fallback row
                                 else
                                     vals[nrun] = static_cast<uint32_t>(v);
                             }
@@ -496,21 +501,25 @@ struct Parser {
                             ++i;
                         }
                     }
-                    if (need_fb) c.fb[static_cast<size_t>(fb_row) + s] = nrun | (vals[0] << 8) | (vals[1] << 16) | (vals[2] << 24);
+                    if (fb_row >= 0) c.fb[static_cast<size_t>(fb_row) + s] = nrun | (vals[0] << 8) | (vals[1] << 16) | (vals[2] << 24);
                     // carrier: a token (split on | and /) equal to str(allele number)
+                    // (the regex at :233-236: canonical decimal, no leading zero)
                     if (keep_gt) {
                         size_t i = 0;
                         while (i <= gl) {
                             size_t j = i;
                             while (j < gl && g[j] != '|' && g[j] != '/') ++j;
                             const size_t tl = j - i;
-                            if (tl >= 1 && tl <= 2 && is_digit(g[i]) && (tl == 1 || (g[i] != '0' && is_digit(g[i + 1])))) {
-                                const uint32_t v = tl == 1 ? static_cast<uint32_t>(g[i] - '0')
-                                                           : static_cast<uint32_t>((g[i] - '0') * 10 + (g[i + 1] - '0'));
-                                if (v == 1)
-                                    c.planes0[plane0 + (s >> 6)] |= 1ull << (s & 63);
-                                else if (v >= 2 && v <= na)
-                                    c.planesx[planex + static_cast<size_t>(v - 2) * words + (s >> 6)] |= 1ull << (s & 63);
+                            if (tl >= 1 && tl <= 10 && g[i] != '0') {
+                                uint64_t v = 0;
+                                size_t k = i;
+                                while (k < j && is_digit(g[k])) v = v * 10 + static_cast<uint64_t>(g[k++] - '0');
+                                if (k == j) {
+                                    if (v == 1)
+                                        c.planes0[plane0 + (s >> 6)] |= 1ull << (s & 63);
+                                    else if (v >= 2 && v <= na)
+                                        c.planesx[planex + static_cast<size_t>(v - 2) * words + (s >> 6)] |= 1ull << (s & 63);
+                                }
                             }
                             i = j + 1;
                         }
@@ -520,6 +529,8 @@ struct Parser {
                 a = t + 1;
             }
         }
+        const int64_t anv = has_an ? an_val : gt_an;
+        if (!an_big && (anv > INT32_MAX || anv < INT32_MIN)) general = true;
         // ---- per-ALT class words (symbolic ids are resolved at merge)
         uint32_t hot = 0;
         if (has_ac) hot |= H_HAS_AC;
@@ -528,24 +539,96 @@ struct Parser {
         if (an_bad) hot |= H_AN_BAD;
         if (need_fb) hot |= H_HAS_FB;
         if (na > 1) hot |= H_MULTI;
-        const int64_t anv = has_an ? an_val : gt_an;
-        if (anv > INT32_MAX || anv < INT32_MIN) unrep = true;
-        if (unrep) {
-            // placeholder: ALT 0 only, no extra rows / fallback row / carriers
-            hot = H_HAS_AN | H_AN_BAD;
-            na = 1;
+        uint32_t gen_idx = 0;
+        if (general) {
+            // the GenRec side table answers it (general_slice_kernel); the
+            // packed words mark it (H_AN_BAD + kAnUnrepresentable, ac0 = index)
+            hot = H_HAS_AN | H_AN_BAD | (na > 1 ? H_MULTI : 0u);
+            if (fb_row >= 0) c.fb.resize(fb0);
             fb_row = -1;
-            if (keep_gt && n_samples) {
-                c.planesx.resize(planex);
-                std::fill(c.planes0.begin() + static_cast<std::ptrdiff_t>(plane0), c.planes0.end(), 0ull);
+            gen_idx = static_cast<uint32_t>(c.gen.size());
+            GenRec gr{};
+            gr.rec = static_cast<uint32_t>(c.pos.size() - 1);
+            gr.flags = (has_ac ? GR_HAS_AC : 0u) | (has_an ? GR_HAS_AN : 0u) | (ac_bad ? GR_AC_BAD : 0u) |
+                       (an_bad ? GR_AN_BAD : 0u);
+            gr.n_alt = na;
+            gr.n_ac = ac_bad ? 0u : n_ac;
+            auto put_num = [&](const char *p, size_t len, int64_t small, bool big) {
+                if (big) py_int_limbs(p, len, L.limbs);
+                else i64_limbs(small, L.limbs);
+                c.gnum.insert(c.gnum.end(), L.limbs.begin(), L.limbs.end());
+                c.gnum_off.push_back(c.gnum.size());
+            };
+            gr.ac_num = c.gnum_off.size() - 1;
+            if (has_ac && !ac_bad)
+                for (uint32_t k = 0; k < n_ac; ++k) {
+                    int64_t v = 0;
+                    const bool big = py_int_ex(L.ac_p[k], L.ac_n[k], &v) == 1;
+                    put_num(L.ac_p[k], L.ac_n[k], acv[k], big);
+                }
+            gr.an_num = c.gnum_off.size() - 1;
+            if (has_an && !an_bad) put_num(an_s, an_sn, an_val, an_big);
+            if ((!has_ac || !has_an) && n_samples > 0) {
+                // every GT digit run of every sample, as value ids numbered in
+                // first-occurrence order (:218 int(g), :249 len(all_calls))
+                gr.flags |= GR_FB;
+                gr.tok_off = c.gtok_off.size();
+                gr.val_off = static_cast<uint32_t>(c.gval.size());
+                L.val_id.clear();
+                const char *a = q;
+                for (uint32_t s = 0; s < n_samples; ++s) {
+                    const char *t = static_cast<const char *>(memchr(a, '\t', static_cast<size_t>(e - a)));
+                    if (!t) t = e;
+                    const char *g, *ge;
+                    gt_field(a, t, gt_idx, &g, &ge);
+                    c.gtok_off.push_back(c.gtok.size());
+                    for (const char *x = g; x < ge;) {
+                        if (!is_digit(*x)) {
+                            ++x;
+                            continue;
+                        }
+                        const char *x0 = x;
+                        while (x < ge && is_digit(*x)) ++x;
+                        const size_t raw = static_cast<size_t>(x - x0);
+                        const char *d = x0;
+                        while (d < x - 1 && *d == '0') ++d;  // the value's significant digits
+                        const std::string_view key(d, static_cast<size_t>(x - d));
+                        auto it = L.val_id.find(key);
+                        uint32_t id;
+                        if (it == L.val_id.end()) {
+                            id = static_cast<uint32_t>(L.val_id.size());
+                            L.val_id.emplace(key, id);
+                            GenVal gv{0, 0, 0};
+                            unsigned __int128 h = 0;
+                            for (const char *y = d; y < x; ++y)
+                                h = (h * 10u + static_cast<unsigned>(*y - '0')) % 2305843009213693951ull;
+                            gv.hash = static_cast<uint64_t>(h);
+                            if (key.size() <= 10) {
+                                uint64_t v = 0;
+                                for (char ch : key) v = v * 10 + static_cast<uint64_t>(ch - '0');
+                                if (v >= 1 && v <= na) gv.allele = static_cast<uint32_t>(v);
+                            }
+                            gv.huge = raw > kPyMaxStrDigits ? 1u : 0u;
+                            c.gval.push_back(gv);
+                        } else {
+                            id = it->second;
+                            if (raw > kPyMaxStrDigits) c.gval[gr.val_off + id].huge = 1u;
+                        }
+                        c.gtok.push_back(id);
+                    }
+                    a = t + 1;
+                }
+                c.gtok_off.push_back(c.gtok.size());
+                gr.n_vals = static_cast<uint32_t>(L.val_id.size());
             }
+            c.gen.push_back(gr);
         }
         int32_t ac0 = 0;
         uint32_t rh_info = 0;  // RangeHot (MODE_RANGE_N) view
         int64_t rh_c = 0;
         for (uint32_t i = 0; i < na; ++i) {
-            const uint8_t *ap = reinterpret_cast<const uint8_t *>(alts[i]);
-            const size_t al = alens[i];
+            const uint8_t *ap = reinterpret_cast<const uint8_t *>(alt_p[i]);
+            const size_t al = alt_n[i];
             bool hashed;
             const uint64_t key = allele_key(ap, al, true, &hashed);
             uint32_t cls = 0;
@@ -564,22 +647,24 @@ struct Parser {
                 if (ok) rep = k >= 62 ? 62u : static_cast<uint32_t>(k);
             }
             cls |= rep << C_REP_SHIFT;
-            int64_t acval;
-            if (has_ac) {
+            int64_t acval = 0;
+            if (general) {
+                if (i == 0) c.gen.back().a0_cls = cls;
+            } else if (has_ac) {
                 if (i >= n_ac) cls |= C_AC_MISSING;
-                acval = (!ac_bad && i < n_ac && i < 64) ? acv[i] : 0;
+                acval = (!ac_bad && i < n_ac) ? acv[i] : 0;
                 if (acval < 0) c.any_negative = true;
             } else {
                 acval = gtcount[i];
             }
-            if (cls & C_SINGLE_BASE) {
+            if (!general && (cls & C_SINGLE_BASE)) {
                 rh_info |= RH_HIT;
                 if (!has_ac || (cls & C_AC_MISSING)) rh_info |= RH_SLOW;
                 rh_c += acval;
                 if (acval != 0) rh_info |= i < 8 ? (1u << i) : RH_SLOW;
             }
             if (i == 0) {
-                hot |= cls;
+                if (!general) hot |= cls;
                 ac0 = static_cast<int32_t>(acval);
                 c.a0_key.push_back(key);
                 c.a0_len.push_back(static_cast<uint32_t>(al));
@@ -593,11 +678,11 @@ struct Parser {
             }
             c.blob.insert(c.blob.end(), ap, ap + al);
         }
-        if (unrep) {
-            ac0 = 0;
-            rh_info = RH_HIT | RH_SLOW;  // every range query evaluates it (and raises)
+        if (general) {
+            ac0 = static_cast<int32_t>(gen_idx);  // GenRec index (vcf-local until merge)
+            rh_info = RH_HIT | RH_SLOW;           // every range query evaluates it
         }
-        const int32_t an32 = unrep ? kAnUnrepresentable : static_cast<int32_t>(anv);
+        const int32_t an32 = general ? kAnUnrepresentable : static_cast<int32_t>(anv);
         c.rec.push_back(RecHot{static_cast<uint32_t>(end), hot, an32, ac0});
         if (an_bad || ac_bad || rh_c > INT32_MAX || rh_c < INT32_MIN) rh_info |= RH_SLOW;
         c.rng.push_back(RangeHot{static_cast<uint32_t>(end), rh_info, an32,
@@ -605,6 +690,24 @@ struct Parser {
         c.fb_off.push_back(fb_row);
         c.x_lo.push_back(static_cast<uint32_t>(c.x_key.size()));
         return true;
+    }
+
+    // the GT subfield of one sample column [a, t) (FORMAT index gt_idx; none: '.')
+    static void gt_field(const char *a, const char *t, int gt_idx, const char **g, const char **ge) {
+        if (gt_idx < 0) {
+            *g = ".";
+            *ge = *g + 1;  // no GT key: bcftools prints '.'  (unpinned)
+            return;
+        }
+        const char *x = a, *xe = t;
+        for (int k = 0; k < gt_idx && x < xe; ++k) {
+            const char *cl = static_cast<const char *>(memchr(x, ':', static_cast<size_t>(xe - x)));
+            x = cl ? cl + 1 : xe;
+        }
+        const char *cl = static_cast<const char *>(memchr(x, ':', static_cast<size_t>(xe - x)));
+        if (cl) xe = cl;
+        *g = x;
+        *ge = xe;
     }
 
     static bool fail(Local &L, const char *m) {
@@ -696,7 +799,30 @@ void merge(sb_builder &b, VcfData &v, Local &L) {
         d.vt.push_back(static_cast<uint16_t>(id));
         RecHot h = s.rec[i];
         if (h.hot & C_SYMBOLIC) h.hot |= sym_id(b, s.blob.data() + s.a0_off[i], s.a0_len[i]) << C_SYM_SHIFT;
+        if ((h.hot & H_AN_BAD) && h.an == kAnUnrepresentable) h.ac0 += static_cast<int32_t>(d.gen.size());
         d.rec.push_back(h);
+    }
+    {  // general records: indices into the merged side table
+        const uint64_t num0 = d.gnum_off.size() - 1, tok0 = d.gtok_off.size(), gt0 = d.gtok.size();
+        const uint32_t val0 = static_cast<uint32_t>(d.gval.size());
+        const uint64_t limb0 = d.gnum.size();
+        for (GenRec g : s.gen) {
+            if (g.a0_cls & C_SYMBOLIC)
+                g.a0_cls |= sym_id(b, s.blob.data() + s.a0_off[g.rec], s.a0_len[g.rec]) << C_SYM_SHIFT;
+            g.rec += rec0;
+            g.ac_num += num0;
+            g.an_num += num0;
+            if (g.flags & GR_FB) {
+                g.tok_off += tok0;
+                g.val_off += val0;
+            }
+            d.gen.push_back(g);
+        }
+        for (size_t k = 1; k < s.gnum_off.size(); ++k) d.gnum_off.push_back(s.gnum_off[k] + limb0);
+        app(d.gnum, s.gnum);
+        for (uint64_t o : s.gtok_off) d.gtok_off.push_back(o + gt0);
+        app(d.gtok, s.gtok);
+        app(d.gval, s.gval);
     }
     for (size_t i = 0; i < nr; ++i) d.ref_off.push_back(s.ref_off[i] + blob0);
     for (size_t i = 0; i < nr; ++i) d.a0_off.push_back(s.a0_off[i] + blob0);
@@ -963,9 +1089,14 @@ void builder_attach_carriers(sb_builder &b, uint32_t vcf_id, const char *const *
     const size_t nr = c.pos.size(), nx = c.x_key.size();
     if (n_rows != nr + nx) throw Error(SB_EINVAL, "carrier matrix rows != ALT rows of the VCF");
     for (size_t i = 0; i < nr; ++i) {
-        const uint32_t h = c.rec[i].hot;
-        if ((h & (H_HAS_AC | H_HAS_AN)) != (H_HAS_AC | H_HAS_AN) || (h & H_AN_BAD))
-            throw Error(SB_EINVAL, "carrier matrix needs AC and AN on every record");
+        const RecHot &r = c.rec[i];
+        const uint32_t h = r.hot;
+        bool ok = (h & (H_HAS_AC | H_HAS_AN)) == (H_HAS_AC | H_HAS_AN) && !(h & H_AN_BAD);
+        if ((h & H_AN_BAD) && r.an == kAnUnrepresentable) {  // a general record: its own flags
+            const uint32_t gf = c.gen[static_cast<size_t>(r.ac0)].flags;
+            ok = (gf & (GR_HAS_AC | GR_HAS_AN)) == (GR_HAS_AC | GR_HAS_AN) && !(gf & GR_AN_BAD);
+        }
+        if (!ok) throw Error(SB_EINVAL, "carrier matrix needs AC and AN on every record");
     }
     v.samples.resize(n_samples);
     for (uint32_t s = 0; s < n_samples; ++s) v.samples[s].assign(names[s], name_len[s]);

@@ -89,6 +89,17 @@ void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, cons
                           const QRes *res, const uint64_t *hoff, const uint64_t *hits, uint64_t rec_base,
                           uint64_t *tsum, uint64_t *row_off, uint64_t *out, hipStream_t s);
 
+// General records (devtypes.hpp GenRec): one wave per slice of the work list
+// (work[0] = count, then launch indices into st.q_all) written by the scan
+// kernels; `grid` single-wave workgroups loop over it, each with
+// general_wave_bytes() of scratch.  Slices whose counts need more than 64
+// bits append {orig} to big (count in *big_n, at most big_cap) and their
+// limbs to big_limbs (2 x kGenAccMax u32 per entry: call_count, all_alleles_count).
+uint64_t general_wave_bytes(const GStore &gs, uint32_t *hwords, uint32_t *tcap);
+void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, uint32_t grid, const uint8_t *qbytes,
+                    const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out, uint8_t *scratch,
+                    uint32_t *big_n, GenBig *big, uint32_t *big_limbs, uint32_t big_cap, hipStream_t s);
+
 // Fetch-time gather of every query's hits into one dense array.
 void launch_compact(const uint64_t *hit_off, const uint64_t *dense_off, const QRes *res, uint32_t nq,
                     const uint64_t *hits, uint64_t *out, hipStream_t s);

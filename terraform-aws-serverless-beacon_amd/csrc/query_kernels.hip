@@ -292,8 +292,8 @@ __device__ __forceinline__ LaneOut eval_record(const DStore &st, const QDev &Q, 
         pass = false;
     }
     if (!pass) return o;
-    if ((h & H_AN_BAD) && h0.an == kAnUnrepresentable) {  // a placeholder record (ingest.cpp unrep)
-        o.err = SB_QERR_UNSUPPORTED;
+    if ((h & H_AN_BAD) && h0.an == kAnUnrepresentable) {  // a general record: general_slice_kernel answers the slice
+        o.err = SB_QERR_GENERAL;
         return o;
     }
     uint32_t x0 = 0, nx = 0;
@@ -457,10 +457,16 @@ __device__ __forceinline__ int chunk_tail(ScanState &S, const LaneOut &o, uint32
 }
 
 template <bool NONNEG>
-__device__ __forceinline__ void finish_query(const ScanState &S, uint32_t q, uint32_t n_scanned, QRes *res) {
+__device__ __forceinline__ void finish_query(const ScanState &S, const DStore &st, const QDev &Q, uint32_t n_scanned,
+                                             QRes *res) {
+    const uint32_t q = Q.orig;
     if (!S.touched) {  // no hit and no error in the whole slice (most variantType slices)
         if (lane_id() == 0) res[q] = QRes{0, 0, 0, 0, 0, n_scanned};
         return;
+    }
+    if (S.err_out == SB_QERR_GENERAL && lane_id() == 0) {  // the scan reached a general record
+        const uint32_t k = atomicAdd(st.gen_work, 1u);
+        st.gen_work[1 + k] = static_cast<uint32_t>(&Q - st.q_all);
     }
     const int64_t call_count = NONNEG ? wave_sum_i64(S.cc_acc) : S.carry;
     const int64_t an_sum = wave_sum_i64(S.an_acc);
@@ -652,7 +658,7 @@ __device__ __forceinline__ void scan_slice(
         ckey = nkey;
         if (s < kWave) break;
     }
-    finish_query<NONNEG>(S, Q.orig, hi - lo, res);
+    finish_query<NONNEG>(S, st, Q, hi - lo, res);
     if constexpr (NACC > 0) if (collect && Q.samples_out_off != ~0ull) {
 #pragma unroll
         for (int j = 0; j < NACC; ++j) {
@@ -759,7 +765,7 @@ __device__ __forceinline__ void range_n_slice(DStore st, const QDev *__restrict_
             h = nh;
         }
     }
-    finish_query<NONNEG>(S, Q.orig, hi - lo, res);
+    finish_query<NONNEG>(S, st, Q, hi - lo, res);
 }
 
 // MODE_VTYPE: referenceBases 'N' + alternateBases None + variantType queries
@@ -942,7 +948,7 @@ __device__ __forceinline__ void vt_slice(DStore st, const QDev *__restrict__ qs,
             x = nx;
         }
     }
-    finish_query<NONNEG>(S, Q.orig, hi - lo, res);
+    finish_query<NONNEG>(S, st, Q, hi - lo, res);
 }
 
 // ---------------------------------------------------------------- packed variantType slices
@@ -2504,6 +2510,472 @@ __global__ __launch_bounds__(kBlock) void summarise_finish_kernel(SStore ss, con
     }
 }
 
+// ---------------------------------------------------------------- general records
+// A slice whose scan reached a general record (devtypes.hpp GenRec) is
+// answered here, one wave per slice, record by record in file order
+// (search_variants.py:70-254 / search_variants_in_samples.py:63-245): the
+// ordinary records of each 64-record chunk through eval_record in parallel,
+// then the reference loop's state machine over the chunk's lanes in order; a
+// general record is evaluated by the whole wave:
+//   * ALT predicates over any number of ALTs, 64 per round (hit bitmap);
+//   * AC / AN as Python ints: running sums are two's complement numbers of up
+//     to kGenAccMax 32-bit limbs, limb j in lane j % 64 of group j / 64, added
+//     with a carry-lookahead over the wave (generate / propagate ballots:
+//     carry-in = (G + (G|P)) ^ (G|P) ^ G);
+//   * the GT fallback (:215-226): token counts over the (subset) samples in
+//     parallel; the variant order is CPython's iteration order of
+//     set(all_calls) & hit_set (:223), emulated by one lane over scratch
+//     tables exactly as Objects/setobject.c (3.10) builds them.
+
+// per-lane limbs of a wave-wide number
+using BigLimbs = uint32_t[kGenAccGroups];
+
+__device__ __forceinline__ void big_zero(BigLimbs &a) {
+#pragma unroll
+    for (uint32_t t = 0; t < kGenAccGroups; ++t) a[t] = 0u;
+}
+
+// a += x over `groups` 64-limb groups (both sign-extended to the full width)
+__device__ __forceinline__ void big_add(BigLimbs &a, const BigLimbs &x, uint32_t groups) {
+    const uint32_t lane = static_cast<uint32_t>(lane_id());
+    uint32_t cg = 0;  // carry into limb 0 of the group
+#pragma unroll
+    for (uint32_t t = 0; t < kGenAccGroups; ++t) {
+        if (t < groups) {
+            const uint64_t s = static_cast<uint64_t>(a[t]) + x[t] + (lane == 0 ? cg : 0u);
+            const uint64_t G = __ballot((s >> 32) != 0);
+            const uint64_t P = __ballot(static_cast<uint32_t>(s) == 0xffffffffu);
+            const uint64_t X = G | P, sum = G + X;
+            const uint64_t cin = sum ^ X ^ G;  // bit i: carry into limb i
+            a[t] = static_cast<uint32_t>(s) + static_cast<uint32_t>((cin >> lane) & 1u);
+            cg = sum < X ? 1u : 0u;  // out of the group's top limb
+        }
+    }
+}
+
+__device__ __forceinline__ void big_add_i64(BigLimbs &a, int64_t v, uint32_t groups) {
+    const uint32_t lane = static_cast<uint32_t>(lane_id());
+    const uint32_t sgn = v < 0 ? 0xffffffffu : 0u;
+    BigLimbs x;
+#pragma unroll
+    for (uint32_t t = 0; t < kGenAccGroups; ++t) x[t] = sgn;
+    const uint64_t u = static_cast<uint64_t>(v);
+    if (lane == 0) x[0] = static_cast<uint32_t>(u);
+    if (lane == 1) x[0] = static_cast<uint32_t>(u >> 32);
+    big_add(a, x, groups);
+}
+
+// GStore number k (limbs of it past gs.limbs: its sign)
+__device__ __forceinline__ void big_add_num(BigLimbs &a, const GStore &gs, uint64_t k, uint32_t groups) {
+    const uint32_t lane = static_cast<uint32_t>(lane_id());
+    const uint32_t *p = gs.num + k * gs.limbs;
+    const uint32_t sgn = (p[gs.limbs - 1] >> 31) ? 0xffffffffu : 0u;
+    BigLimbs x;
+#pragma unroll
+    for (uint32_t t = 0; t < kGenAccGroups; ++t) {
+        const uint32_t j = t * kWave + lane;
+        x[t] = (t < groups && j < gs.limbs) ? p[j] : sgn;
+    }
+    big_add(a, x, groups);
+}
+
+__device__ __forceinline__ bool big_nonzero(const BigLimbs &a, uint32_t groups) {
+    bool nz = false;
+#pragma unroll
+    for (uint32_t t = 0; t < kGenAccGroups; ++t)
+        if (t < groups) nz = nz || __ballot(a[t] != 0u);
+    return nz;
+}
+
+__device__ __forceinline__ int64_t big_low64(const BigLimbs &a) {
+    return static_cast<int64_t>((static_cast<uint64_t>(rdl(a[0], 1)) << 32) | rdl(a[0], 0));
+}
+
+__device__ __forceinline__ bool big_fits64(const BigLimbs &a, uint32_t groups) {
+    const uint32_t lane = static_cast<uint32_t>(lane_id());
+    const uint32_t sgn = (rdl(a[0], 1) >> 31) ? 0xffffffffu : 0u;
+    bool bad = false;
+#pragma unroll
+    for (uint32_t t = 0; t < kGenAccGroups; ++t)
+        if (t < groups) bad = bad || __ballot((t > 0 || lane >= 2) && a[t] != sgn);
+    return !bad;
+}
+
+// one slot of an emulated CPython set: key bit 31 = a hit allele number
+// (hit_set), else a value id of the record's GT digit runs (set(all_calls))
+struct SetEnt {
+    uint64_t hash;
+    uint32_t key;
+    uint32_t used;
+};
+struct PySetD {
+    SetEnt *t;
+    uint64_t mask, fill, used;
+};
+constexpr uint32_t kHitKey = 0x80000000u;
+
+__device__ __forceinline__ bool set_key_eq(const GenVal *val, uint32_t a, uint32_t b) {
+    if (a == b) return true;
+    if ((a ^ b) < kHitKey) return false;  // same domain, different keys
+    const uint32_t vid = (a & kHitKey) ? b : a, al = ((a & kHitKey) ? a : b) & ~kHitKey;
+    return val[vid].allele == al;
+}
+
+__device__ void set_init(PySetD &s, SetEnt *t) {
+    s.t = t;
+    s.mask = 7;
+    s.fill = s.used = 0;
+    for (int i = 0; i < 8; ++i) t[i] = SetEnt{0, 0, 0};
+}
+
+__device__ void set_insert_clean(SetEnt *t, uint64_t mask, uint64_t hash, uint32_t key) {
+    uint64_t perturb = hash, i = hash & mask;
+    SetEnt *e;
+    for (;;) {
+        e = &t[i];
+        if (!e->used) break;
+        bool found = false;
+        if (i + 9 <= mask)
+            for (int j = 0; j < 9; ++j) {
+                ++e;
+                if (!e->used) {
+                    found = true;
+                    break;
+                }
+            }
+        if (found) break;
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+    *e = SetEnt{hash, key, 1u};
+}
+
+// set_add_entry (with set_table_resize through `tmp`, tcap entries)
+__device__ void set_add(PySetD &s, SetEnt *tmp, const GenVal *val, uint64_t hash, uint32_t key) {
+    uint64_t mask = s.mask, i = hash & mask, perturb = hash;
+    SetEnt *e = nullptr;
+    for (;;) {
+        e = &s.t[i];
+        int probes = (i + 9 <= mask) ? 9 : 0;
+        bool unused = false;
+        do {
+            if (!e->used) {
+                unused = true;
+                break;
+            }
+            if (e->hash == hash && set_key_eq(val, e->key, key)) return;
+            ++e;
+        } while (probes--);
+        if (unused) break;
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+    *e = SetEnt{hash, key, 1u};
+    ++s.fill;
+    ++s.used;
+    if (s.fill * 5 < mask * 3) return;
+    const uint64_t minused = s.used > 50000 ? s.used * 2 : s.used * 4;
+    uint64_t newsize = 8;
+    while (newsize <= minused) newsize <<= 1;
+    for (uint64_t k = 0; k < newsize; ++k) tmp[k] = SetEnt{0, 0, 0};
+    for (uint64_t k = 0; k <= mask; ++k)
+        if (s.t[k].used) set_insert_clean(tmp, newsize - 1, s.t[k].hash, s.t[k].key);
+    for (uint64_t k = 0; k < newsize; ++k) s.t[k] = tmp[k];
+    s.mask = newsize - 1;
+    s.fill = s.used;
+}
+
+__device__ bool set_contains(const PySetD &s, const GenVal *val, uint64_t hash, uint32_t key) {
+    uint64_t mask = s.mask, i = hash & mask, perturb = hash;
+    for (;;) {
+        const SetEnt *e = &s.t[i];
+        int probes = (i + 9 <= mask) ? 9 : 0;
+        do {
+            if (!e->used) return false;
+            if (e->hash == hash && set_key_eq(val, e->key, key)) return true;
+            ++e;
+        } while (probes--);
+        perturb >>= 5;
+        i = (i * 5 + 1 + perturb) & mask;
+    }
+}
+
+// ALT k of record r against the query's ALT predicate + length bounds
+// (search_variants.py:100-183; the ALT half of eval_record)
+__device__ __forceinline__ bool gen_alt_ok(const DStore &st, const QDev &Q, const QView &V, uint32_t r, uint32_t k,
+                                           uint32_t x0, uint32_t a0_cls, int64_t ref_len) {
+    const uint32_t x = x0 + k - 1;
+    const uint32_t cls = k ? st.xrow[x].cls : a0_cls;
+    int64_t len = 1;
+    bool ok;
+    if (V.alt_mode == ALT_N) {
+        ok = cls & C_SINGLE_BASE;
+    } else if (V.alt_mode == ALT_EXACT) {
+        const uint64_t key = k ? st.x_key[x] : st.a0_key[r];
+        ok = key == Q.alt_key;
+        len = Q.alt_len;
+        if (ok && (key >> 63))
+            ok = k ? blob_eq_upper(st.blob, st.x_off[x], st.x_len[x], V.qalt, Q.alt_len)
+                   : blob_eq_upper(st.blob, st.a0_off[r], st.a0_len[r], V.qalt, Q.alt_len);
+    } else {
+        len = k ? st.x_len[x] : st.a0_len[r];
+        ok = vtype_hit(Q, st, cls, len, ref_len);
+    }
+    return ok && len >= Q.vmin && len <= Q.vmax;
+}
+
+struct GenSlice {  // one wave's state over one slice
+    BigLimbs cc, an;
+    uint32_t n_out;
+    bool exists;
+};
+
+enum : int { GEN_GO = 0, GEN_STOP = -1 };  // > 0: the SB_QERR_* the reference raises
+
+__device__ __forceinline__ void or_planes(const DStore &st, const QDev &Q, uint64_t row, uint64_t *samples_out) {
+    for (uint32_t w = static_cast<uint32_t>(lane_id()); w < Q.words; w += kWave)
+        samples_out[Q.samples_out_off + w] |= st.planes[row + w];
+}
+
+// one general record reached by the slice's loop
+__device__ int general_record(const DStore &st, const GStore &gs, const QDev &Q, const QView &V, uint32_t r,
+                              GenSlice &S, uint64_t *out, uint64_t *samples_out, bool collect, uint32_t groups,
+                              uint64_t *hbits, SetEnt *tabs, uint32_t tcap) {
+    const uint32_t lane = static_cast<uint32_t>(lane_id());
+    const GenRec G = gs.rec[static_cast<uint32_t>(st.rec[r].ac0)];
+    const uint32_t n_alt = G.n_alt, x0 = st.x_lo[r];
+    const int64_t ref_len = static_cast<int64_t>(st.rec[r].end) - st.pos[r] + 1;
+    // ---- hit_indexes (:100-183)
+    uint32_t nh = 0, maxhit = 0;
+    for (uint32_t k0 = 0; k0 < n_alt; k0 += kWave) {
+        const uint32_t k = k0 + lane;
+        const bool ok = k < n_alt && gen_alt_ok(st, Q, V, r, k, x0, G.a0_cls, ref_len);
+        const uint64_t m = __ballot(ok);
+        if (lane == 0) hbits[k0 / kWave] = m;
+        if (m) {
+            nh += static_cast<uint32_t>(__popcll(m));
+            maxhit = k0 + 63u - static_cast<uint32_t>(__clzll(m));
+        }
+    }
+    if (!nh) return GEN_GO;  // :184
+    __threadfence();  // hbits: lane 0's stores, every lane's loads
+    auto is_hit = [&](uint32_t k) -> bool { return (hbits[k / kWave] >> (k % kWave)) & 1ull; };
+    if (G.flags & GR_AN_BAD) return SB_QERR_VALUE;  // :199
+    const uint64_t *subset = V.subset;
+    if (G.flags & GR_HAS_AC) {  // :205-214
+        if (G.flags & GR_AC_BAD) return SB_QERR_VALUE;
+        if (maxhit >= G.n_ac) return SB_QERR_INDEX;  // :207
+        for (uint32_t k0 = 0; k0 < n_alt; k0 += kWave) {
+            const uint64_t m = static_cast<uint64_t>(rdl64(static_cast<int64_t>(hbits[k0 / kWave]), 0));
+            if (!m) continue;
+            const uint32_t k = k0 + lane;
+            bool nz = false;
+            if ((m >> lane) & 1ull) {
+                const uint32_t *p = gs.num + (G.ac_num + k) * gs.limbs;
+                for (uint32_t j = 0; j < gs.limbs; ++j) nz = nz || p[j] != 0u;
+            }
+            const uint64_t nzm = __ballot(nz);
+            if (nz) out[S.n_out + popc_below(nzm)] = static_cast<uint64_t>(r) | (static_cast<uint64_t>(k) << kHitAltShift);
+            S.n_out += static_cast<uint32_t>(__popcll(nzm));
+            for (uint64_t b = m; b; b &= b - 1) big_add_num(S.cc, gs, G.ac_num + k0 + ffs64(b), groups);
+        }
+    } else if (G.flags & GR_FB) {  // :215-226 genotype fallback over the (subset) samples
+        const uint64_t *toff = gs.tok_off + G.tok_off;
+        const GenVal *val = gs.val + G.val_off;
+        int64_t cnt = 0;
+        bool huge = false, last = false;  // last: the value n_alt occurs (alts[n_alt] -> IndexError)
+        for (uint32_t s = lane; s < Q.n_samples; s += kWave) {
+            if (subset && !((subset[s >> 6] >> (s & 63)) & 1ull)) continue;
+            for (uint64_t t = toff[s]; t < toff[s + 1]; ++t) {
+                const GenVal v = val[gs.tok[t]];
+                huge = huge || v.huge;
+                if (v.allele && is_hit(v.allele - 1)) {
+                    ++cnt;
+                    last = last || v.allele == n_alt;
+                }
+            }
+        }
+        if (__ballot(huge)) return SB_QERR_VALUE;  // :218 int(g) past 4300 digits
+        if (__ballot(last)) return SB_QERR_INDEX;  // :223 alts[i] with 1-based i
+        const int64_t cc = wave_sum_i64(cnt);
+        uint32_t ne = 0;
+        if (lane == 0) {  // variants in the iteration order of set(all_calls) & hit_set
+            SetEnt *tmp = tabs + 3ull * tcap;
+            PySetD sc, hs, rs;
+            set_init(sc, tabs);
+            set_init(hs, tabs + tcap);
+            set_init(rs, tabs + 2ull * tcap);
+            if (!subset) {  // value ids are numbered in first-occurrence order over all samples
+                for (uint32_t v = 0; v < G.n_vals; ++v) set_add(sc, tmp, val, val[v].hash, v);
+            } else {
+                for (uint32_t s = 0; s < Q.n_samples; ++s)
+                    if ((subset[s >> 6] >> (s & 63)) & 1ull)
+                        for (uint64_t t = toff[s]; t < toff[s + 1]; ++t) {
+                            const uint32_t v = gs.tok[t];
+                            set_add(sc, tmp, val, val[v].hash, v);
+                        }
+            }
+            for (uint32_t k = 0; k < n_alt; ++k)
+                if (is_hit(k)) set_add(hs, tmp, val, k + 1, kHitKey | (k + 1));
+            const PySetD *so = &sc, *other = &hs;  // set_intersection: iterate the smaller
+            if (hs.used > sc.used) {
+                so = &hs;
+                other = &sc;
+            }
+            for (uint64_t i = 0; i <= other->mask; ++i) {
+                const SetEnt e = other->t[i];
+                if (e.used && set_contains(*so, val, e.hash, e.key)) set_add(rs, tmp, val, e.hash, e.key);
+            }
+            for (uint64_t i = 0; i <= rs.mask; ++i)
+                if (rs.t[i].used) {
+                    const uint32_t key = rs.t[i].key;
+                    const uint32_t a = (key & kHitKey) ? key & ~kHitKey : val[key].allele;
+                    out[S.n_out + ne++] = static_cast<uint64_t>(r) | (static_cast<uint64_t>(a) << kHitAltShift);
+                }
+        }
+        S.n_out += rdl(ne, 0);
+        big_add_i64(S.cc, cc, groups);
+    }
+    // :229-236
+    if (big_nonzero(S.cc, groups)) {
+        S.exists = true;
+        if (!(V.flags & F_DETAILS)) return GEN_STOP;  // :231-232, before AN
+        if (collect)
+            for (uint32_t k = 0; k < n_alt; ++k)
+                if (is_hit(k))
+                    or_planes(st, Q,
+                              k ? Q.planex_base + static_cast<uint64_t>(x0 + k - 1 - Q.x_base) * Q.words
+                                : Q.plane0_base + static_cast<uint64_t>(r - Q.rec_base) * Q.words,
+                              samples_out);
+    }
+    // :244-250
+    if (G.flags & GR_HAS_AN) {
+        big_add_num(S.an, gs, G.an_num, groups);
+    } else if (G.flags & GR_FB) {  // len(get_all_calls(genotypes))
+        const uint64_t *toff = gs.tok_off + G.tok_off;
+        int64_t n = 0;
+        for (uint32_t s = lane; s < Q.n_samples; s += kWave)
+            if (!subset || ((subset[s >> 6] >> (s & 63)) & 1ull)) n += static_cast<int64_t>(toff[s + 1] - toff[s]);
+        big_add_i64(S.an, wave_sum_i64(n), groups);
+    }
+    if ((V.flags & F_BOOL_BREAK) && S.exists) return GEN_STOP;  // :253-254
+    return GEN_GO;
+}
+
+__global__ __launch_bounds__(kWave) void general_slice_kernel(
+    DStore st, GStore gs, const uint32_t *__restrict__ work, const uint8_t *__restrict__ qbytes,
+    const uint64_t *__restrict__ subsets, QRes *__restrict__ res, uint64_t *__restrict__ hits,
+    uint64_t *__restrict__ samples_out, uint8_t *__restrict__ scratch, uint64_t wave_bytes, uint32_t hwords,
+    uint32_t tcap, uint32_t *__restrict__ big_n, GenBig *__restrict__ big, uint32_t *__restrict__ big_limbs,
+    uint32_t big_cap) {
+    const uint32_t lane = static_cast<uint32_t>(lane_id());
+    const uint32_t n_work = work[0];
+    uint64_t *hbits = reinterpret_cast<uint64_t *>(scratch + blockIdx.x * wave_bytes);
+    SetEnt *tabs = reinterpret_cast<SetEnt *>(hbits + hwords);
+    const uint32_t groups = (gs.acc_limbs + kWave - 1) / kWave;
+    for (uint32_t w = blockIdx.x; w < n_work; w += gridDim.x) {
+        const QDev &Q = st.q_all[work[1 + w]];
+        QView V;
+        V.flags = Q.flags;
+        V.ref_mode = Q.ref_mode;
+        V.alt_mode = Q.alt_mode;
+        V.samples_variant = (V.flags & F_SAMPLES_VARIANT) != 0;
+        V.strict_unbound = (V.flags & F_STRICT_UNBOUND) != 0;
+        V.qref = qbytes + Q.qbytes_off;
+        V.qalt = V.qref + Q.ref_len;
+        V.subset = (Q.subset_off != ~0ull) ? subsets + Q.subset_off : nullptr;
+        const bool collect = (V.flags & F_COLLECT) && (V.flags & F_DETAILS) && Q.samples_out_off != ~0ull;
+        uint32_t lo = Q.seg_lo, hi = Q.seg_lo;
+        if (!(Q.flags & F_EMPTY) && Q.first_bp <= Q.last_bp) slice_bounds(st, Q, &lo, &hi);
+        if (collect)
+            for (uint32_t wd = lane; wd < Q.words; wd += kWave) samples_out[Q.samples_out_off + wd] = 0ull;
+        GenSlice S;
+        big_zero(S.cc);
+        big_zero(S.an);
+        S.n_out = 0;
+        S.exists = false;
+        uint64_t *out = hits + Q.hit_off;
+        int err = 0;
+        bool stop = false;
+        for (uint32_t base = lo; base < hi && !stop; base += kWave) {
+            const uint32_t r = base + lane;
+            LaneOut o{0, 0, 0, 0, 0};
+            if (r < hi) o = eval_record(st, Q, V, r, st.rec[r]);
+            const uint32_t nin = min(static_cast<uint32_t>(kWave), hi - base);
+            for (uint32_t L = 0; L < nin && !stop; ++L) {
+                const int e = static_cast<int>(rdl(static_cast<uint32_t>(o.err), L));
+                const uint32_t rr = base + L;
+                if (e == SB_QERR_GENERAL) {
+                    const int g = general_record(st, gs, Q, V, rr, S, out, samples_out, collect, groups, hbits, tabs,
+                                                 tcap);
+                    if (g > 0) err = g;
+                    if (g != GEN_GO) stop = true;
+                    continue;
+                }
+                if (e) {
+                    err = e;
+                    stop = true;
+                    continue;
+                }
+                const uint64_t hm = static_cast<uint64_t>(rdl64(static_cast<int64_t>(o.hm), L));
+                if (!hm) continue;
+                const uint64_t em = static_cast<uint64_t>(rdl64(static_cast<int64_t>(o.em), L));
+                if (lane == 0) {
+                    uint32_t k = 0;
+                    for (uint64_t b = em; b; b &= b - 1)
+                        out[S.n_out + k++] = static_cast<uint64_t>(rr) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
+                }
+                S.n_out += static_cast<uint32_t>(__popcll(em));
+                big_add_i64(S.cc, rdl64(o.c, L), groups);
+                if (big_nonzero(S.cc, groups)) {
+                    S.exists = true;
+                    if (!(V.flags & F_DETAILS)) {
+                        stop = true;
+                        continue;
+                    }
+                    if (collect) {
+                        const uint32_t xl = (hm >> 1) ? st.x_lo[rr] : 0u;
+                        for (uint64_t b = hm; b; b &= b - 1) {
+                            const int k = ffs64(b);
+                            or_planes(st, Q,
+                                      k ? Q.planex_base + static_cast<uint64_t>(xl + k - 1 - Q.x_base) * Q.words
+                                        : Q.plane0_base + static_cast<uint64_t>(rr - Q.rec_base) * Q.words,
+                                      samples_out);
+                        }
+                    }
+                }
+                big_add_i64(S.an, rdl64(o.anv, L), groups);
+                if ((V.flags & F_BOOL_BREAK) && S.exists) stop = true;
+            }
+        }
+        const int64_t cc = big_low64(S.cc), an = big_low64(S.an);
+        const bool wide = !err && !(big_fits64(S.cc, groups) && big_fits64(S.an, groups));
+        if (lane == 0)
+            res[Q.orig] = QRes{err, (!err && S.exists) ? 1 : 0, err ? 0 : cc, err ? 0 : an, err ? 0u : S.n_out, hi - lo};
+        if (wide) {  // Python ints past 64 bits: the exact limbs beside the row
+            uint32_t slot = 0;
+            if (lane == 0) slot = atomicAdd(big_n, 1u);
+            slot = rdl(slot, 0);
+            if (slot < big_cap) {
+                if (lane == 0) big[slot] = GenBig{Q.orig, 0u};
+                uint32_t *dst = big_limbs + static_cast<uint64_t>(slot) * 2u * kGenAccMax;
+#pragma unroll
+                for (uint32_t t = 0; t < kGenAccGroups; ++t)
+                    if (t < groups) {
+                        dst[t * kWave + lane] = S.cc[t];
+                        dst[kGenAccMax + t * kWave + lane] = S.an[t];
+                    }
+            }
+        }
+        if (collect)
+            for (uint32_t wd = lane; wd < Q.words; wd += kWave) {
+                uint64_t v = err ? 0ull : samples_out[Q.samples_out_off + wd];
+                if (V.subset) v &= V.subset[wd];
+                samples_out[Q.samples_out_off + wd] = v;
+            }
+    }
+}
+
 }  // namespace
 
 void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const uint32_t *chunk_slice, uint32_t nchunks,
@@ -2521,8 +2993,14 @@ void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, 
     if (!n_chains) return;
     const char *kern = std::getenv("SBEACON_CHAIN_KERNEL");  // "seq": the chain-sequential kernel
     if (!(kern && kern[0] == 's')) {
+        // timing ablations (skip evaluation / results) exist only in a bench
+        // build (-DSBEACON_ABLATION): the product library always runs the full kernel
+#ifdef SBEACON_ABLATION
         const char *dbg = std::getenv("SBEACON_PACK_DBG");
         const uint32_t dbgv = dbg ? static_cast<uint32_t>(std::atoi(dbg)) : 0u;
+#else
+        const uint32_t dbgv = 0u;
+#endif
         if (res || !cpart)
             hipLaunchKernelGGL(chain_pack_kernel<true>, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs,
                                n_runs, corig, res, hits, cpart, dbgv);
@@ -2542,6 +3020,25 @@ void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, 
     }
     hipLaunchKernelGGL(chain_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st, chains,
                        n_chains, run, corig, res, hits, cpart);
+}
+
+uint64_t general_wave_bytes(const GStore &gs, uint32_t *hwords, uint32_t *tcap) {
+    *hwords = std::max<uint32_t>(1u, (gs.max_alt + kWave - 1) / kWave);
+    uint64_t t = 8;
+    while (t <= 4ull * std::max(gs.max_vals, gs.max_alt)) t <<= 1;
+    *tcap = static_cast<uint32_t>(t);
+    const uint64_t b = 8ull * *hwords + 4ull * t * sizeof(SetEnt);
+    return (b + 255) & ~255ull;
+}
+
+void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, uint32_t grid, const uint8_t *qbytes,
+                    const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out, uint8_t *scratch,
+                    uint32_t *big_n, GenBig *big, uint32_t *big_limbs, uint32_t big_cap, hipStream_t s) {
+    if (!grid) return;
+    uint32_t hwords, tcap;
+    const uint64_t wb = general_wave_bytes(gs, &hwords, &tcap);
+    hipLaunchKernelGGL(general_slice_kernel, dim3(grid), dim3(kWave), 0, s, st, gs, work, qbytes, subsets, res, hits,
+                       samples_out, scratch, wb, hwords, tcap, big_n, big, big_limbs, big_cap);
 }
 
 uint32_t pack_run_max() { return kPackRun; }

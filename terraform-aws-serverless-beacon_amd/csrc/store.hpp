@@ -53,6 +53,15 @@ struct VcfCols {
     std::vector<uint64_t> dk_hash, dk_tail;   // hash of the key string; tail word (devtypes.hpp)
     std::vector<uint8_t> dk_blob;             // tails longer than 7 bytes
     std::vector<uint32_t> dk_bad;             // records where compressSeq would throw
+    // general records (devtypes.hpp GenRec; vcf-local rec / number / token /
+    // value indices until upload): numbers are variable-length two's
+    // complement limbs here (gnum_off[k] .. gnum_off[k + 1])
+    std::vector<GenRec> gen;
+    std::vector<uint64_t> gnum_off{0};
+    std::vector<uint32_t> gnum;
+    std::vector<uint64_t> gtok_off;
+    std::vector<uint32_t> gtok;
+    std::vector<GenVal> gval;
 };
 
 struct BucketIndex {  // coarse POS index of one segment
@@ -155,6 +164,8 @@ struct sb_store {
     std::vector<uint32_t> h_dk_pos, h_dk_lo, h_dk_bad;
     std::vector<uint64_t> h_dk_tail;
     std::vector<uint8_t> h_dk_blob;
+    // general records (GenRec side table): device image + sizes
+    sb::GStore g{};
     // device image
     sb::DStore d{};
     sb::SStore ds{};

@@ -50,7 +50,21 @@ class ResultView(C.Structure):
     _fields_ = [('error', C.c_int32), ('exists', C.c_int32), ('call_count', C.c_int64),
                 ('all_alleles_count', C.c_int64), ('n_variants', C.c_uint64),
                 ('hit_record', C.POINTER(C.c_uint32)), ('hit_alt', C.POINTER(C.c_uint32)),
-                ('n_sample_indices', C.c_uint64), ('sample_indices', C.POINTER(C.c_uint32))]
+                ('n_sample_indices', C.c_uint64), ('sample_indices', C.POINTER(C.c_uint32)),
+                ('big_limbs', C.c_uint32), ('_pad', C.c_uint32),
+                ('big_call_count', C.POINTER(C.c_uint32)), ('big_all_alleles_count', C.POINTER(C.c_uint32))]
+
+
+def big_int(limbs, n: int) -> int:
+    """n 32-bit two's complement limbs (little-endian) -> Python int."""
+    return int.from_bytes(C.string_at(limbs, 4 * n), 'little', signed=True)
+
+
+def view_counts(v) -> tuple[int, int]:
+    """(call_count, all_alleles_count) of a ResultView, exact past 64 bits."""
+    if v.big_limbs:
+        return big_int(v.big_call_count, v.big_limbs), big_int(v.big_all_alleles_count, v.big_limbs)
+    return int(v.call_count), int(v.all_alleles_count)
 
 
 class BatchStats(C.Structure):

@@ -27,6 +27,7 @@ from ._lib import (BatchStats, BuildOpts, DedupJob, DedupStats, Query, ResultVie
 from .payloads import PerformQueryResponse
 
 QERR = {1: UnboundLocalError, 2: IndexError, 3: ValueError, 4: AttributeError, 9: NotImplementedError}
+assert 10 not in QERR  # SB_QERR_GENERAL is internal to the library (general_slice_kernel resolves it)
 QERR_MSG = {
     1: "local variable 'variant_type' referenced before assignment",
     2: 'list index out of range',
@@ -599,9 +600,10 @@ class ResultSet:
         else:
             sample_indices = []
             sample_names = names if include_samples else []
+        cc, an = _lib.view_counts(v)
         r = PerformQueryResponse(
             exists=bool(v.exists), dataset_id=p.get('dataset_id'), vcf_location=p.get('vcf_location'),
-            all_alleles_count=int(v.all_alleles_count), variants=variants, call_count=int(v.call_count),
+            all_alleles_count=an, variants=variants, call_count=cc,
             sample_indices=sample_indices, sample_names=sample_names)
         r._src = (self, i)
         return r
@@ -638,9 +640,10 @@ class ResultSet:
             else:
                 sample_indices = []
                 sample_names = names if pt.get('includeSamples', False) else []
+            cc, an = _lib.view_counts(v)
             r = PerformQueryResponse(
                 exists=bool(v.exists), dataset_id=p.get('dataset_id'), vcf_location=p.get('vcf_location'),
-                all_alleles_count=int(v.all_alleles_count), variants=variants, call_count=int(v.call_count),
+                all_alleles_count=an, variants=variants, call_count=cc,
                 sample_indices=sample_indices, sample_names=sample_names)
             r._src = (self, i)
             out.append(r)

@@ -222,17 +222,24 @@ def header_sample_count(head: bytes):
     before #CHROM; None when the bytes end first."""
     d = zlib.decompressobj(16 + zlib.MAX_WBITS)
     buf, rest = b'', head
+    complete = True  # every gzip member of the bytes ended (else GzipFile hits EOFError at the cut)
     while rest:
         try:
             buf += d.decompress(rest)
         except zlib.error:
+            complete = False
             break
         rest = d.unused_data
         if d.eof and rest:
             d = zlib.decompressobj(16 + zlib.MAX_WBITS)
         elif not d.eof:
+            complete = False
             break
-    for line in buf.split(b'\n'):
+    lines = buf.split(b'\n')
+    tail = lines.pop()  # after the last '\n': a line only when the stream ended cleanly
+    if complete and tail:
+        lines.append(tail)
+    for line in lines:
         if not line.startswith(b'#'):
             raise ValueError('Incorrectly formatted file')
         if line.startswith(b'#CHROM'):
@@ -249,7 +256,8 @@ def summarise_vcf(store, location, stride=1, index='auto'):
     """All slices of one VCF summarised on the device; returns
     (slices, per-slice RegionStats, the VCF's totals: variantCount,
     callCount and, for a VCF held as a file, sampleCount)."""
-    slices = plan_slices(store, location, stride, index)
+    cb = chunk_boundaries(store, location, stride, index)
+    slices = slices_from_boundaries(cb)
     stats = store.summarise_slices([(location, a, b) for a, b in slices])
     tot = {'variantCount': 0, 'callCount': 0}
     for s in stats:
@@ -258,6 +266,6 @@ def summarise_vcf(store, location, stride=1, index='auto'):
         tot['variantCount'] += s['numVariants']
         tot['callCount'] += s['numCalls']
     path = getattr(store, 'paths', {}).get(location)
-    if path is not None and slices:
-        tot['sampleCount'] = vcf_sample_count(path, min(a for a, _ in slices) >> 16)
+    if path is not None and cb:  # get_sample_count(location, first_chunk_start) (:256, :272)
+        tot['sampleCount'] = vcf_sample_count(path, min(b[0] for b in cb.values()) >> 16)
     return slices, stats, tot

@@ -30,9 +30,11 @@ import tempfile
 import threading
 import types
 
-if os.environ.get('PYTHONHASHSEED') != '0':
-    os.environ['PYTHONHASHSEED'] = '0'
-    os.execv(sys.executable, [sys.executable] + sys.argv)
+if __name__ == '__main__' and os.environ.get('PYTHONHASHSEED') != '0':
+    # set iteration order must be reproducible: rerun as a child with the
+    # seed fixed (a child process, never an exec of this one)
+    import subprocess
+    sys.exit(subprocess.run([sys.executable] + sys.argv, env=dict(os.environ, PYTHONHASHSEED='0')).returncode)
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)

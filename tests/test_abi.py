@@ -24,7 +24,7 @@ def test_library_exports_every_header_symbol():
     missing = [n for n in names if not hasattr(L, n)]
     assert not missing, missing
     assert set(names) == set(_lib.SIGNATURES), set(names) ^ set(_lib.SIGNATURES)
-    assert L.sb_abi_version() == 1
+    assert L.sb_abi_version() == 2
 
 
 def test_library_is_gfx950_code_object():
@@ -53,7 +53,9 @@ HDR = b'##fileformat=VCFv4.2\n#CHROM\tPOS\tID\tREF\tALT\tQUAL\tFILTER\tINFO\tFOR
     (b'22\t0100\t.\tA\tG\t.\t.\tAC=1;AN=2\tGT\t0|1\n', False),
     (b'22\t100\t.\t\tG\t.\t.\tAC=1;AN=2\tGT\t0|1\n', False),
     (b'22\t100\t.\tA\tG\t.\t.\tAC=1;AN=2\tGT\n', False),
-    (b'22\t100\t.\tA\tG\t.\t.\tAC=1\tGT\t0|1|1|1\n', True),  # ploidy 4 fallback: a placeholder record
+    (b'22\t100\t.\tA\tG\t.\t.\tAC=1\tGT\t0|1|1|1\n', True),  # ploidy 4 fallback: a general record
+    (b'22\t100\t.\tA\tG\t.\t.\tAC=1;AN=' + b'9' * 4300 + b'\tGT\t0|1\n', True),  # AN past int64: general
+    (b'22\t100\t.\tA\t' + b','.join([b'C'] * 300) + b'\t.\t.\tAN=2\tGT\t0|299\n', True),  # 300 ALTs, no AC
 ])
 def test_ingest_validation(body, ok):
     from sbeacon import _lib
