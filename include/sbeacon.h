@@ -337,10 +337,51 @@ enum { SB_INDEX_CSI = 0, SB_INDEX_TBI = 1 };
 int sb_index_vcf(const char *path, int fmt, int min_shift, int depth, uint8_t **out, size_t *out_len);
 void sb_free(void *p);
 
+typedef struct sb_batch sb_batch;
+
+/* ---- split-query requests (the splitQuery fan-out in the library) ---------
+ * One sb_request = one SplitQueryPayload (shared_resources/payloads/
+ * lambda_payloads.py:8-44) for ONE of its vcf_locations: the VCF and the
+ * contig (index into sb_store_contig_name) its chrom maps to.  The library
+ * cuts it into splitQuery's 10 kb slices (lambda/splitQuery/
+ * lambda_function.py:74-110: [s, min(s + 9999, start_max)] for s =
+ * start_min, start_min + 10000, ...) and answers each as performQuery would;
+ * include_details = check_all (include_datasets in {HIT, ALL}).  A contig
+ * index the VCF lacks, or start_min > start_max, gives a row with no slices.
+ * Every request is one ROW (sb_request_partial: the route-level sums of its
+ * slices' responses, route_g_variants.py:144-171) with its hit list. */
+typedef struct {
+    uint32_t vcf_id;
+    uint32_t contig;
+    int64_t start_min, start_max; /* split_payload.start_min / start_max (inclusive) */
+    int64_t end_min, end_max;
+    const char *reference_bases; size_t reference_len;
+    const char *alternate_bases; size_t alternate_len; /* NULL = None (variantType query) */
+    const char *variant_type; size_t variant_type_len; /* NULL = None */
+    int64_t variant_min_length, variant_max_length;    /* max < 0 = infinity */
+    uint8_t granularity;           /* SB_GRAN_* */
+    uint8_t include_details;       /* check_all */
+    uint8_t include_samples;       /* passthrough.includeSamples */
+    uint8_t selected_samples_only; /* passthrough.selectedSamplesOnly */
+    uint8_t strict_variant_type;
+    uint8_t _pad[3];
+    const char *sample_names; size_t sample_names_len; /* ','-joined passthrough.sampleNames, NULL = ['_'] */
+} sb_request;
+
+/* Plan and upload a request batch (sb_batch_free releases it); its
+ * sb_batch_get_stats().hits is the output capacity (hits). */
+int sb_requests_prepare(sb_store *s, const sb_request *r, size_t n, sb_batch **out);
+/* Enqueue one pass: answer every request, then write dev_rows[n]
+ * (sb_request_partial), dev_row_off[n + 1] and the rows' hit lists densely
+ * in request order: row w's hits ((record + rec_base) | alt << 32, the
+ * reference's variant order) are dev_hits[row_off[w] .. row_off[w + 1]).
+ * Device pointers on the store's device; sb_batch_sync waits, and
+ * sb_batch_last_timing reports the passes' device time. */
+int sb_requests_run(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_off, uint64_t rec_base);
+
 /* ---- device-resident batch (benchmarks / fused pipelines) ----------------
  * Upload a batch once, then launch the query kernels repeatedly on the
  * store's stream with inputs already resident in HBM. */
-typedef struct sb_batch sb_batch;
 int sb_batch_prepare(sb_store *s, const sb_query *q, size_t nq, sb_batch **out);
 int sb_batch_run(sb_batch *b);               /* enqueue only (async) */
 int sb_batch_sync(sb_batch *b);              /* wait for the store stream */

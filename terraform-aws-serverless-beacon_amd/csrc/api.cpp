@@ -8,6 +8,7 @@
 // are formatted on the host from the store's allele blob in the reference's
 // exact format.
 #include <algorithm>
+#include <deque>
 #include <atomic>
 #include <array>
 #include <chrono>
@@ -224,6 +225,18 @@ struct sb_batch {
     // per-request rows (sb_batch_set_owners): seg = n_rows + 1 query offsets
     uint32_t n_rows = 0;
     DevMem seg, herr;
+    bool no_chains = false;  // the slice part of a request batch: every slice answered on its own
+    // request batches (sb_requests_prepare): rows = requests
+    struct Req {
+        uint32_t n_rows = 0;
+        std::vector<ChainDev> chains;  // one per chain-answered request (s0 = its row)
+        std::vector<RowRun> runs;
+        uint64_t cap = 0;              // output hit capacity
+        uint64_t n_chain_slices = 0;
+        DevMem dchains, druns, status, ticket, spill, lut, sseg, sherr;
+        bool slices = false;           // some rows answered per slice (the batch's query part)
+    };
+    std::unique_ptr<Req> req;
     // general records (general_slice_kernel): work list [count, launch
     // indices], per-wave scratch, slices with counts past 64 bits
     DevMem gen_work, gen_scratch, gen_big_n, gen_big, gen_limbs;
@@ -582,6 +595,16 @@ void upload_store(sb_builder &b, sb_store &s) {
         s.h_vt_slow.clear();
         for (size_t i = 0; i < n; ++i)
             if (vth[i].w & VT_SLOW) s.h_vt_slow.push_back(static_cast<uint32_t>(i));
+        s.seg_slow_pos.assign(b.vcfs.size(), {});
+        for (size_t vi = 0; vi < b.vcfs.size(); ++vi) {
+            const auto &segs = b.vcfs[vi].segments;
+            auto &out = s.seg_slow_pos[vi];
+            out.assign(segs.size(), {});
+            for (size_t g = 0; g < segs.size(); ++g) {
+                auto a = std::lower_bound(s.h_vt_slow.begin(), s.h_vt_slow.end(), segs[g].lo);
+                for (; a != s.h_vt_slow.end() && *a < segs[g].hi; ++a) out[g].push_back(pos[*a]);
+            }
+        }
         cw.push_back(VtHot{0, 0, 0, 0});  // clamp target of an empty candidate range
         ci.push_back(0);
         s.d.vc_word = dev_upload(s, cw);
@@ -719,7 +742,7 @@ std::vector<uint32_t> plan_chains(sb_batch &B, const std::vector<uint32_t> &segi
     sb_store &s = *B.s;
     std::vector<uint32_t> rest;
     const char *off = std::getenv("SBEACON_NO_CHAINS");
-    if (off && off[0] == '1') return vt;
+    if ((off && off[0] == '1') || B.no_chains) return vt;
     struct Ch {
         std::vector<uint32_t> m;
         int64_t first = 0, last = 0, width = 0;
@@ -1207,7 +1230,25 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     HIP_OK(hipStreamSynchronize(st));
 }
 
+// timing: one event before the first run since the last sync and one at the
+// sync (sync()); no marker between back-to-back runs (a marker pair per run
+// measured ~8 us of stream gap per run on MI355X)
+void mark_run(sb_batch &B) {
+    if (!B.ev[0]) {
+        for (auto &e : B.ev) HIP_OK(hipEventCreate(&e));
+    }
+    if (B.runs_pending++ == 0) HIP_OK(hipEventRecord(B.ev[0], B.strm()));
+}
+
+void run_kernels(sb_batch &B);
+
 void run(sb_batch &B) {
+    HIP_OK(hipSetDevice(B.s->device));
+    mark_run(B);
+    run_kernels(B);
+}
+
+void run_kernels(sb_batch &B) {
     sb_store &s = *B.s;
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = B.strm();
@@ -1215,13 +1256,6 @@ void run(sb_batch &B) {
     d.sym_lut = B.lut.as<uint32_t>();
     d.q_all = B.q.as<QDev>();
     d.gen_work = B.gen_grid ? B.gen_work.as<uint32_t>() : nullptr;
-    // timing: one event before the first run since the last sync and one at
-    // the sync (sync()); no marker between back-to-back runs (a marker pair
-    // per run measured ~8 us of stream gap per run on MI355X)
-    if (!B.ev[0]) {
-        for (auto &e : B.ev) HIP_OK(hipEventCreate(&e));
-    }
-    if (B.runs_pending++ == 0) HIP_OK(hipEventRecord(B.ev[0], st));
     if (B.gen_grid) {
         HIP_OK(hipMemsetAsync(B.gen_work.p, 0, 4, st));
         HIP_OK(hipMemsetAsync(B.gen_big_n.p, 0, 4, st));
@@ -2642,6 +2676,291 @@ int sb_store_sample_name(const sb_store *s, uint32_t vcf_id, uint32_t i, const c
     return SB_OK;
 }
 
+namespace {
+
+constexpr int64_t kSplitSize = 10000;  // lambda/splitQuery/lambda_function.py:12
+
+// Request batch (sb_requests_prepare): rows = requests.  A request whose
+// slices need none of the order-dependent machinery (variantType query with
+// referenceBases 'N', include_details, no boolean break, a non-negative-AC
+// VCF, no samples, at most kChainMax slices, no VT_SLOW / general record in
+// its window) becomes ONE chain answered by request_rows_kernel; every other
+// request is cut into its splitQuery slices (split_query_sync,
+// lambda/splitQuery/lambda_function.py:74-110) and answered per slice by the
+// query kernels (the batch's query part), its row reduced and gathered by
+// request_reduce + request_rows_kernel.
+void prepare_requests(sb_batch &B, const sb_request *rq, size_t n) {
+    sb_store &s = *B.s;
+    if (n >= (1u << 31)) throw Error(SB_EINVAL, "too many requests");
+    auto R = std::make_unique<sb_batch::Req>();
+    R->n_rows = static_cast<uint32_t>(n);
+    // variantType strings: a handful of distinct values (pointer cache, then by value)
+    struct VtEnt {
+        const char *p;
+        size_t len;
+        uint32_t kind, lut;
+    };
+    std::vector<VtEnt> vt_seen;
+    std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> vt_map;
+    std::vector<uint32_t> lut_all;
+    std::vector<uint32_t> vt_of(n, 0u), lut_of(n, 0u);
+    for (size_t i = 0; i < n; ++i) {
+        const sb_request &x = rq[i];
+        if (x.alternate_bases) continue;
+        const VtEnt *hit = nullptr;
+        for (const VtEnt &e : vt_seen)
+            if (e.p == x.variant_type && e.len == x.variant_type_len) {
+                hit = &e;
+                break;
+            }
+        if (!hit) {
+            const std::string vt = x.variant_type ? std::string(x.variant_type, x.variant_type_len) : std::string("None");
+            auto it = vt_map.find(vt);
+            if (it == vt_map.end()) {
+                const uint32_t kind = !x.variant_type ? VT_OTHER
+                                      : vt == "DEL"        ? VT_DEL
+                                      : vt == "INS"        ? VT_INS
+                                      : vt == "DUP"        ? VT_DUP
+                                      : vt == "DUP:TANDEM" ? VT_DUPT
+                                      : vt == "CNV"        ? VT_CNV
+                                                           : VT_OTHER;
+                const auto lut = sym_lut(s, kind, "<" + vt);
+                const uint32_t off = static_cast<uint32_t>(lut_all.size());
+                lut_all.insert(lut_all.end(), lut.begin(), lut.end());
+                it = vt_map.emplace(vt, std::make_pair(kind, off)).first;
+            }
+            if (vt_seen.size() < 16) vt_seen.push_back(VtEnt{x.variant_type, x.variant_type_len, it->second.first,
+                                                             it->second.second});
+            vt_of[i] = it->second.first;
+            lut_of[i] = it->second.second;
+        } else {
+            vt_of[i] = hit->kind;
+            lut_of[i] = hit->lut;
+        }
+    }
+    lut_all.insert(lut_all.end(), 8, 0u);
+    // classify: 0 = no slices, 1 = one chain, 2 = per slice
+    std::vector<uint8_t> cls(n, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const sb_request &x = rq[i];
+        if (x.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "request " + std::to_string(i) + ": unknown vcf id");
+        if (!x.reference_bases && x.reference_len) throw Error(SB_EINVAL, "request " + std::to_string(i) + ": bad REF");
+    }
+    parallel_for(n, [&](size_t i) {
+        const sb_request &x = rq[i];
+        const VcfData &v = s.vcfs[x.vcf_id];
+        if (x.contig >= v.segments.size() || x.start_min > x.start_max) return;  // bcftools emits nothing / no slice
+        const int64_t nsl = (x.start_max - x.start_min) / kSplitSize + 1;
+        const bool collect = (x.granularity == SB_GRAN_RECORD || x.granularity == SB_GRAN_AGGREGATED) &&
+                             (x.selected_samples_only || x.include_samples);
+        bool chain = !x.alternate_bases && x.reference_bases && x.reference_len == 1 && x.reference_bases[0] == 'N' &&
+                     x.include_details && x.granularity != SB_GRAN_BOOLEAN && !x.selected_samples_only &&
+                     !x.strict_variant_type && !(collect && v.words) && v.nonneg && nsl <= kChainMax &&
+                     x.start_min >= 1 && x.start_max <= 0xfffffffell;
+        if (chain) {  // a VT_SLOW / general record in the window: per slice
+            const auto &sp = s.seg_slow_pos[x.vcf_id][x.contig];
+            auto a = std::lower_bound(sp.begin(), sp.end(), static_cast<uint32_t>(x.start_min));
+            if (a != sp.end() && *a <= static_cast<uint64_t>(x.start_max)) chain = false;
+        }
+        cls[i] = chain ? 1 : 2;
+    });
+    // chains in row order
+    std::vector<uint32_t> chain_of(n, UINT32_MAX);
+    uint32_t nc = 0;
+    for (size_t i = 0; i < n; ++i)
+        if (cls[i] == 1) chain_of[i] = nc++;
+    R->chains.resize(nc);
+    std::vector<uint64_t> ccap(nc, 0);
+    parallel_for(n, [&](size_t i) {
+        if (cls[i] != 1) return;
+        const sb_request &x = rq[i];
+        const VcIndex &vi = s.vcfs[x.vcf_id].vc_index[x.contig][vt_of[i]];
+        ChainDev &cd = R->chains[chain_of[i]];
+        cd = ChainDev{};
+        cd.s0 = static_cast<uint32_t>(i);
+        cd.n = static_cast<uint32_t>((x.start_max - x.start_min) / kSplitSize + 1);
+        cd.first = static_cast<uint32_t>(x.start_min);
+        cd.last = static_cast<uint32_t>(x.start_max);
+        cd.width = static_cast<uint32_t>(kSplitSize);
+        cd.c_lo = vi.c_lo;
+        cd.c_hi = vi.c_hi;
+        cd.cb_base = vi.base;
+        cd.cb_off = vi.off;
+        cd.cb_shift = vi.shift;
+        cd.cb_n = vi.n;
+        const int64_t emin = x.end_min, emax = x.end_max;
+        const bool end_void = emax < 0 || emin > 0xffffffffll || emin > emax;
+        cd.e0 = emin < 0 ? 0u : static_cast<uint32_t>(emin);
+        cd.espan = (emax > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(emax)) - cd.e0;
+        const int64_t vmax = x.variant_max_length < 0 ? INT64_MAX : x.variant_max_length;
+        const int64_t vl = x.variant_min_length < 0 ? 0 : x.variant_min_length, vh = vmax > 255 ? 255 : vmax;
+        cd.vlo = vh < vl ? 256u : static_cast<uint32_t>(vl);
+        cd.vspan = vh < vl ? 0u : static_cast<uint32_t>(vh - vl);
+        cd.kind = vt_of[i] | (end_void ? kChainEndVoid : 0u);
+        cd.lut_off = lut_of[i];
+        cd.out = 0;
+        // hit capacity: every ALT of the coarse-index candidate range
+        auto cb = [&](uint64_t xx, uint32_t up) -> uint32_t {
+            if (xx <= cd.cb_base) return cd.c_lo;
+            const uint64_t b = (xx - cd.cb_base) >> cd.cb_shift;
+            return b >= cd.cb_n ? cd.c_hi : s.h_vc_bucket[cd.cb_off + b + up];
+        };
+        const uint32_t C0 = cb(cd.first, 0), C1 = end_void ? C0 : std::max(C0, cb(uint64_t(cd.last) + 1, 1));
+        ccap[chain_of[i]] = s.h_vc_altpre[C1] - s.h_vc_altpre[C0];
+    });
+    for (const ChainDev &c : R->chains) R->n_chain_slices += c.n;
+    // the per-slice part: splitQuery's slices of the other requests, in row order
+    std::vector<sb_query> qs;
+    std::vector<uint32_t> owner;
+    std::deque<std::string> regions;  // stable storage for the region strings
+    for (size_t i = 0; i < n; ++i) {
+        if (cls[i] != 2) continue;
+        const sb_request &x = rq[i];
+        const std::string &chrom = s.vcfs[x.vcf_id].segments[x.contig].contig;
+        for (int64_t a = x.start_min; a <= x.start_max; a += kSplitSize) {
+            const int64_t b = std::min(a + kSplitSize - 1, x.start_max);
+            regions.push_back(chrom + ":" + std::to_string(a) + "-" + std::to_string(b));
+            sb_query q{};
+            q.vcf_id = x.vcf_id;
+            q.region = regions.back().data();
+            q.region_len = regions.back().size();
+            q.end_min = x.end_min;
+            q.end_max = x.end_max;
+            q.reference_bases = x.reference_bases;
+            q.reference_len = x.reference_len;
+            q.alternate_bases = x.alternate_bases;
+            q.alternate_len = x.alternate_len;
+            q.variant_type = x.variant_type;
+            q.variant_type_len = x.variant_type_len;
+            q.variant_min_length = x.variant_min_length;
+            q.variant_max_length = x.variant_max_length;
+            q.granularity = x.granularity;
+            q.include_details = x.include_details;
+            q.include_samples = x.include_samples;
+            q.selected_samples_only = x.selected_samples_only;
+            q.strict_variant_type = x.strict_variant_type;
+            q.sample_names = x.sample_names;
+            q.sample_names_len = x.sample_names_len;
+            qs.push_back(q);
+            owner.push_back(static_cast<uint32_t>(i));
+            if (a > INT64_MAX - kSplitSize) break;
+        }
+    }
+    B.no_chains = true;
+    if (!qs.empty()) {
+        prepare(B, qs.data(), qs.size());
+        R->slices = true;
+    }
+    // rows -> their per-slice queries, host errors
+    std::vector<uint32_t> seg(n + 1, 0);
+    for (uint32_t o : owner) ++seg[o + 1];
+    for (size_t w = 0; w < n; ++w) seg[w + 1] += seg[w];
+    // runs of consecutive rows (<= kRunRows rows, kPackRun chains, kPackSlots slots)
+    uint64_t spill_total = 0;
+    {
+        RowRun cur{0, 0, 0, 0, 0, 0, 0};
+        uint64_t cap = 0;
+        auto close = [&](uint32_t row_hi) {
+            cur.row_hi = row_hi;
+            cur.spill = spill_total;
+            if (cap > kRowHitBuf) spill_total += cap - kRowHitBuf;
+            R->runs.push_back(cur);
+        };
+        uint32_t c = 0;
+        for (uint32_t i = 0; i < n; ++i) {
+            const bool ch = cls[i] == 1;
+            const uint32_t need = ch ? R->chains[c].n : 0u;
+            if (i > cur.row_lo && (i - cur.row_lo == kRunRows || (ch && (cur.c_hi - cur.c_lo == pack_run_max() ||
+                                                                           cur.n_slots + need > pack_slots_max())))) {
+                close(i);
+                cur = RowRun{i, i, c, c, 0, 0, 0};
+                cap = 0;
+            }
+            if (ch) {
+                cur.c_hi = ++c;
+                cur.n_slots += need;
+                cap += ccap[c - 1];
+            }
+        }
+        if (n) close(static_cast<uint32_t>(n));
+    }
+    R->cap = B.cap_total;
+    for (uint64_t x : ccap) R->cap += x;
+    // device buffers
+    HIP_OK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    R->dchains.alloc(R->chains.size() * sizeof(ChainDev));
+    R->druns.alloc(R->runs.size() * sizeof(RowRun));
+    R->status.alloc(R->runs.size() * 8);
+    R->ticket.alloc(4);
+    R->spill.alloc(spill_total * 8);
+    R->lut.alloc(lut_all.size() * 4);
+    if (!R->chains.empty())
+        HIP_OK(hipMemcpyAsync(R->dchains.p, R->chains.data(), R->chains.size() * sizeof(ChainDev),
+                              hipMemcpyHostToDevice, st));
+    if (!R->runs.empty())
+        HIP_OK(hipMemcpyAsync(R->druns.p, R->runs.data(), R->runs.size() * sizeof(RowRun), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(R->lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
+    if (R->slices) {
+        std::vector<uint8_t> he(std::max<size_t>(B.nq, 1), 0);
+        for (uint32_t q = 0; q < B.nq; ++q) he[q] = B.host_err[q] ? 1 : 0;
+        R->sseg.alloc(seg.size() * 4);
+        R->sherr.alloc(he.size());
+        HIP_OK(hipMemcpyAsync(R->sseg.p, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(R->sherr.p, he.data(), he.size(), hipMemcpyHostToDevice, st));
+    }
+    HIP_OK(hipStreamSynchronize(st));
+    B.req = std::move(R);
+}
+
+void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t rec_base) {
+    sb_store &s = *B.s;
+    sb_batch::Req &R = *B.req;
+    HIP_OK(hipSetDevice(s.device));
+    hipStream_t st = B.strm();
+    mark_run(B);
+    HIP_OK(hipMemsetAsync(R.ticket.p, 0, 4, st));
+    if (!R.runs.empty()) HIP_OK(hipMemsetAsync(R.status.p, 0, R.runs.size() * 8, st));
+    if (R.slices) {  // the per-slice part, then its rows (chain rows come out zero; the row kernel writes them)
+        run_kernels(B);
+        launch_request_reduce(B.res.as<QRes>(), R.sseg.as<uint32_t>(), R.sherr.as<uint8_t>(), R.n_rows,
+                              static_cast<ReqPartial *>(rows), st);
+    }
+    DStore d = s.d;
+    d.sym_lut = R.lut.as<uint32_t>();
+    launch_request_rows(d, R.dchains.as<ChainDev>(), R.druns.as<RowRun>(), static_cast<uint32_t>(R.runs.size()),
+                        R.ticket.as<uint32_t>(), R.status.as<unsigned long long>(),
+                        R.slices ? B.res.as<QRes>() : nullptr, R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(),
+                        R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(), static_cast<ReqPartial *>(rows),
+                        static_cast<uint64_t *>(row_off), static_cast<uint64_t *>(hits), R.spill.as<uint64_t>(),
+                        R.n_rows, rec_base, st);
+    HIP_OK(hipGetLastError());
+}
+
+}  // namespace
+
+int sb_requests_prepare(sb_store *s, const sb_request *r, size_t n, sb_batch **out) {
+    return guard([&] {
+        if (!s || (!r && n) || !out) throw Error(SB_EINVAL, "NULL argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        auto B = std::make_unique<sb_batch>();
+        B->s = s;
+        prepare_requests(*B, r, n);
+        *out = B.release();
+    });
+}
+
+int sb_requests_run(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_off, uint64_t rec_base) {
+    return guard([&] {
+        if (!b) throw Error(SB_EINVAL, "NULL batch");
+        if (!b->req) throw Error(SB_EINVAL, "not a request batch (sb_requests_prepare)");
+        if ((!dev_rows && b->req->n_rows) || (!dev_hits && b->req->cap) || !dev_row_off)
+            throw Error(SB_EINVAL, "NULL argument");
+        std::lock_guard<std::mutex> lk(b->s->mu);
+        run_requests(*b, dev_rows, dev_hits, dev_row_off, rec_base);
+    });
+}
+
 int sb_batch_prepare(sb_store *s, const sb_query *q, size_t nq, sb_batch **out) {
     return guard([&] {
         if (!s || (!q && nq) || !out) throw Error(SB_EINVAL, "NULL argument");
@@ -2656,6 +2975,7 @@ int sb_batch_prepare(sb_store *s, const sb_query *q, size_t nq, sb_batch **out) 
 int sb_batch_run(sb_batch *b) {
     return guard([&] {
         if (!b) throw Error(SB_EINVAL, "NULL batch");
+        if (b->req) throw Error(SB_EINVAL, "a request batch runs through sb_requests_run");
         std::lock_guard<std::mutex> lk(b->s->mu);
         run(*b);
     });
@@ -2690,6 +3010,11 @@ int sb_batch_get_stats(const sb_batch *b, sb_batch_stats *out) {
     out->cand_unique = b->cand_unique;
     out->hits = b->cap_total;
     out->device_ms = b->last_total_ms;
+    if (b->req) {  // request batch: the rows' output capacity and its chains
+        out->hits = b->req->cap;
+        out->chains = b->req->chains.size();
+        out->chained_slices = b->req->n_chain_slices;
+    }
     return SB_OK;
 }
 

@@ -209,6 +209,24 @@ struct alignas(16) ChainDev {
 static_assert(sizeof(ChainDev) == 80, "ChainDev is five 16-byte words");
 constexpr uint32_t kChainEndVoid = 1u << 8;  // no END can match
 
+// Request batches (sb_requests_prepare / sb_requests_run): every request is a
+// row; request_rows_kernel answers one run of consecutive rows per wave --
+// the rows' chains (ChainDev::s0 = the chain's row) evaluated as
+// chain_pack_kernel does, the other rows' hits (per-slice queries answered
+// before) gathered -- and writes the rows, their offsets and their hits
+// densely in row order at the run's offset, found by a decoupled look-back
+// over the runs (status words, one ticket counter).
+constexpr uint32_t kRunRows = 64;    // rows per run at most (one lane each)
+constexpr uint32_t kRowHitBuf = 320; // chain hits a wave stages in LDS; the rest spill to global
+struct alignas(16) RowRun {
+    uint32_t row_lo, row_hi;  // rows [row_lo, row_hi)
+    uint32_t c_lo, c_hi;      // the run's chains, rows increasing
+    uint64_t spill;           // first spill slot of the run (hits past kRowHitBuf)
+    uint32_t n_slots;         // slices of its chains (<= 256)
+    uint32_t pad;
+};
+static_assert(sizeof(RowRun) == 32, "RowRun is two 16-byte words");
+
 // bit c set = an ALT of class c satisfies variantType `kind` (vtype_hit)
 __host__ __device__ constexpr uint32_t vt_class_mask(uint32_t kind) {
     uint32_t m = 0;

@@ -100,6 +100,16 @@ void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, ui
                     const uint64_t *subsets, QRes *res, uint64_t *hits, uint64_t *samples_out, uint8_t *scratch,
                     uint32_t *big_n, GenBig *big, uint32_t *big_limbs, uint32_t big_cap, hipStream_t s);
 
+// Request batches (devtypes.hpp RowRun): rows + row offsets + dense hits in
+// row order, one wave per run, offsets by decoupled look-back (ticket and
+// status zeroed by the caller; status n_runs words).  sres..shits: the
+// batch's per-slice part (rows of it already reduced into `rows`), or null.
+void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun *runs, uint32_t n_runs,
+                         uint32_t *ticket, unsigned long long *status, const QRes *sres, const uint32_t *sseg,
+                         const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits, ReqPartial *rows,
+                         uint64_t *row_off, uint64_t *out, uint64_t *spill, uint32_t n_rows, uint64_t rec_base,
+                         hipStream_t s);
+
 // Fetch-time gather of every query's hits into one dense array.
 void launch_compact(const uint64_t *hit_off, const uint64_t *dense_off, const QRes *res, uint32_t nq,
                     const uint64_t *hits, uint64_t *out, hipStream_t s);

@@ -1887,6 +1887,295 @@ __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__res
     }
 }
 
+// ---------------------------------------------------------------- request rows
+// Request batches (sb_requests_run, devtypes.hpp RowRun): one wave per run of
+// consecutive request rows (ticket order, so a wave only ever waits on runs
+// whose waves already started).  The run's chains are evaluated as in
+// chain_pack_kernel (rows only: per-slice exists bits + chain totals), with
+// two changes: each candidate lane finds its chain by a wave-uniform walk over
+// the few chains that start inside its chunk (v_readlane of the lane-held
+// prefixes: no binary search, no ds_bpermute), and hits are appended to an
+// LDS buffer in candidate order -- which is chain order, which is row order
+// -- instead of scattered into per-chain regions.  Once the run's hit count
+// is known its output offset comes from a decoupled look-back over the
+// runs' status words (aggregate / inclusive prefix), and the wave writes its
+// rows, row offsets and hits densely at that offset: no capacity-sized hit
+// regions, no gather kernel.  Rows answered per slice (queries of the batch's
+// slice part, reduced into `rows` by request_reduce before this kernel) are
+// gathered from their hit regions in row order.
+struct ReqLds {
+    uint4 pred[kPackRun * 3];  // per chain: {first, last, n, width}, {e0, espan, vlo, vspan},
+                               // {class mask, extra-ALT bits | end_void << 31, 1/width (f32), LUT offset}
+    unsigned long long tcc[kPackRun], tan[kPackRun];
+    unsigned int exw[kPackSlots / 32];  // bit = the slot's slice exists
+    unsigned int slow[kPackRun];
+    unsigned int cstart[kPackRun + 1];  // buffer position of each chain's first candidate (~0: none)
+    unsigned int ccount[kPackRun];
+    uint8_t rowchain[kRunRows];         // row (run-relative) -> its chain (0xff: not a chain row)
+    unsigned long long hbuf[kRowHitBuf];
+};
+
+struct RowChunk {
+    ChainChunk x;
+    uint32_t k, so;  // the lane's chain and its first slot
+    bool first;      // the lane holds its chain's first candidate
+};
+
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_rows_kernel(
+    DStore st, const ChainDev *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
+    uint32_t *__restrict__ ticket, unsigned long long *__restrict__ status, const QRes *__restrict__ sres,
+    const uint32_t *__restrict__ sseg, const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr,
+    const uint64_t *__restrict__ shits, ReqPartial *__restrict__ rows, uint64_t *__restrict__ row_off,
+    uint64_t *__restrict__ out, uint64_t *__restrict__ spill, uint32_t n_rows, uint64_t rec_base) {
+    __shared__ ReqLds lds_all[kWavesPerBlock];
+    ReqLds &L = lds_all[threadIdx.x >> 6];
+    const uint32_t ul = static_cast<uint32_t>(lane_id());
+    uint32_t w = 0;
+    if (ul == 0) w = atomicAdd(ticket, 1u);
+    w = rdl(w, 0);
+    if (w >= n_runs) return;
+    const uint32_t row_lo = uniform(runs[w].row_lo), row_hi = uniform(runs[w].row_hi);
+    const uint32_t c_lo = uniform(runs[w].c_lo), R = uniform(runs[w].c_hi) - c_lo;
+    const uint64_t spill_at = (static_cast<uint64_t>(uniform(static_cast<uint32_t>(runs[w].spill >> 32))) << 32) |
+                              uniform(static_cast<uint32_t>(runs[w].spill));
+    const uint32_t nrows = row_hi - row_lo;
+    // ---- setup: lane k < R = chain k (descriptor, predicate constants, candidate bounds)
+    uint32_t rowk = 0, c0 = 0, cnt = 0, nsl = 0;
+    if (ul < R) {
+        const ChainDev C = chains[c_lo + ul];
+        rowk = C.s0;
+        VtPred q(st, 0u, 0u, 0u, 0u, C.kind, 0u, 0u, 0u);
+        L.pred[3 * ul] = uint4{C.first, C.last, C.n, C.width};
+        L.pred[3 * ul + 1] = uint4{C.e0, C.espan, C.vlo, C.vspan};
+        L.pred[3 * ul + 2] = uint4{q.cmask, q.xneed | (q.end_void ? 0x80000000u : 0u),
+                                   __float_as_uint(__frcp_rn(static_cast<float>(C.width))), C.lut_off};
+        auto cb = [&](uint64_t x, uint32_t up) -> uint32_t {
+            if (x <= C.cb_base) return C.c_lo;
+            const uint64_t b = (x - C.cb_base) >> C.cb_shift;
+            return b >= C.cb_n ? C.c_hi : st.vc_bucket[C.cb_off + b + up];
+        };
+        const uint32_t lo = cb(C.first, 0u);
+        const uint32_t hi = q.end_void ? lo : max(lo, cb(static_cast<uint64_t>(C.last) + 1, 1u));
+        c0 = lo;
+        cnt = hi - lo;
+        nsl = C.n;
+        L.tcc[ul] = 0;
+        L.tan[ul] = 0;
+        L.slow[ul] = 0;
+    }
+    if (ul < kPackSlots / 32) L.exw[ul] = 0;
+    if (ul < kRunRows) L.rowchain[ul] = 0xffu;
+    if (ul <= kPackRun) L.cstart[ul] = 0xffffffffu;
+    wave_lds_sync();
+    if (ul < R) L.rowchain[rowk - row_lo] = static_cast<uint8_t>(ul);
+    // candidate ranges end to end (pex / pin), slots (sex / sin); delta = c0 - pex
+    uint32_t pin = cnt, sin = nsl;
+#pragma unroll
+    for (int d = 1; d < static_cast<int>(kPackRun); d <<= 1) {
+        const uint32_t t = __shfl_up(pin, d, kWave), u = __shfl_up(sin, d, kWave);
+        if (ul >= static_cast<uint32_t>(d)) {
+            pin += t;
+            sin += u;
+        }
+    }
+    const uint32_t pex = pin - cnt, sex = sin - nsl, delta = c0 - pex;
+    const uint32_t T = rdl(pin, kPackRun - 1);
+    const uint32_t i_safe = rdl(c0, 0);
+    wave_lds_sync();
+    // ---- candidates: chunk c covers run positions [64 c, 64 c + 64)
+    uint32_t kc = 0;  // chain at the current chunk's first position (wave-uniform)
+    auto load = [&](uint32_t base) -> RowChunk {
+        const uint32_t g = base + ul;
+        RowChunk c;
+        c.k = kc;
+        uint32_t dl = rdl(delta, kc);
+        c.so = rdl(sex, kc);
+        c.first = rdl(pex, kc) == g;
+        uint32_t next = kc;
+        for (uint32_t j = kc + 1; j < R; ++j) {  // chains starting inside this chunk (usually a few)
+            const uint32_t pj = rdl(pex, j);
+            if (pj > base + kWave) break;
+            if (pj <= g) {
+                c.k = j;
+                dl = rdl(delta, j);
+                c.so = rdl(sex, j);
+                c.first = pj == g;
+            }
+            next = j;
+        }
+        kc = next;
+        const uint32_t i = (base < T && g < T) ? g + dl : i_safe;
+        c.x = ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]};
+        return c;
+    };
+    uint32_t hpos = 0;  // hits appended so far (wave-uniform)
+    auto put_hit = [&](uint32_t at, uint64_t v) {
+        if (at < kRowHitBuf) L.hbuf[at] = v;
+        else spill[spill_at + (at - kRowHitBuf)] = v;
+    };
+    auto eval = [&](const RowChunk &c, uint32_t base) {
+        const ChainChunk &x = c.x;
+        const uint32_t k = c.k;
+        const uint32_t g = base + ul;
+        const bool valid = g < T;
+        const uint4 p0 = L.pred[3 * k], p1 = L.pred[3 * k + 1], p2 = L.pred[3 * k + 2];
+        const uint32_t first = p0.x, last = p0.y, n = p0.z, width = p0.w;
+        VtPred Pd(p1.x, p1.y, p1.z, p1.w, p2.x, p2.y & 0x7fffffffu, (p2.y >> 31) != 0, st.sym_lut + p2.w);
+        const bool inwin = valid && x.p >= first && x.p <= last;
+        const bool cand = inwin && Pd.end_ok(x.h.end);
+        if (cand && (x.h.w & VT_SLOW)) L.slow[k] = 1u;  // never: prepare sends such requests per slice
+        const LaneOut o = Pd.eval(st, x.h, x.r, cand && !(x.h.w & VT_SLOW));
+        const bool hit = o.hm != 0;
+        if (!__ballot(hit)) {
+            if (valid && c.first) L.cstart[k] = hpos;
+            return;
+        }
+        const uint32_t cn = hit ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
+        uint32_t pre, tot;
+        if (!__ballot(cn > 1)) {
+            const uint64_t one = __ballot(cn == 1);
+            pre = popc_below(one);
+            tot = static_cast<uint32_t>(__popcll(one));
+        } else {  // bit-sliced (multi-ALT hit lanes)
+            pre = 0;
+            tot = 0;
+            for (uint32_t bb = 0; bb < 7; ++bb) {
+                const uint64_t m = __ballot((cn >> bb) & 1u);
+                pre += popc_below(m) << bb;
+                tot += static_cast<uint32_t>(__popcll(m)) << bb;
+                if (!__ballot(cn >> (bb + 1))) break;
+            }
+        }
+        if (valid && c.first) L.cstart[k] = hpos + pre;
+        if (cn) {
+            uint32_t at = hpos + pre;
+            for (uint64_t b = o.em; b; b &= b - 1)
+                put_hit(at++, static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift));
+        }
+        hpos += tot;
+        if (hit) {
+            // slice = (POS - first) / width: f32 estimate within one of the quotient, then exact
+            const uint32_t d = x.p - first;
+            uint32_t qt;
+            if (d < (1u << 24)) {
+                qt = static_cast<uint32_t>(static_cast<float>(d) * __uint_as_float(p2.z));
+                if (static_cast<uint64_t>(qt) * width > d) --qt;
+                else if (static_cast<uint64_t>(qt + 1) * width <= d) ++qt;
+            } else {
+                qt = d / width;
+            }
+            const uint32_t slot = c.so + min(qt, n - 1);
+            if (o.c > 0) atomicOr(&L.exw[slot >> 5], 1u << (slot & 31u));
+            atomicAdd(&L.tcc[k], static_cast<unsigned long long>(o.c));
+            atomicAdd(&L.tan[k], static_cast<unsigned long long>(o.anv));
+        }
+    };
+    {
+        RowChunk buf[kPackAhead];
+#pragma unroll
+        for (int a = 0; a < kPackAhead; ++a) buf[a] = load(64u * a);
+        for (uint32_t base = 0; base < T; base += 64u * kPackAhead) {
+#pragma unroll
+            for (int a = 0; a < kPackAhead; ++a) {
+                const uint32_t b = base + 64u * a;
+                if (b < T) {
+                    eval(buf[a], b);
+                    if (b + 64u * kPackAhead < T) buf[a] = load(b + 64u * kPackAhead);
+                }
+            }
+        }
+    }
+    wave_lds_sync();
+    // ---- per chain (lane k < R): hit count, exists count, partial
+    uint32_t cs = ul <= R ? L.cstart[ul] : 0xffffffffu;
+    if (ul == R) cs = hpos;
+#pragma unroll
+    for (int d = 1; d < static_cast<int>(kPackRun) * 2; d <<= 1) {  // suffix min: a chain without candidates starts where the next does
+        const uint32_t t = __shfl_down(cs, d, kWave);
+        if (ul + static_cast<uint32_t>(d) <= R) cs = min(cs, t);
+    }
+    const uint32_t cs_next = __shfl_down(cs, 1, kWave);
+    bool bad = false;  // a VT_SLOW candidate in some chain's window (its row raises; never for prepared chains)
+    ReqPartial part{0, 0, 0, 0, 0};
+    if (ul < R) {
+        const bool slow = L.slow[ul] != 0;
+        bad = slow;
+        int64_t ex = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kPackSlots / 32; ++q) {
+            const uint32_t a = sex > 32 * q ? min(sex - 32 * q, 32u) : 0u, b = sin > 32 * q ? min(sin - 32 * q, 32u) : 0u;
+            const uint32_t m = (b >= 32 ? ~0u : ((1u << b) - 1u)) & (a >= 32 ? 0u : (~0u << a));
+            ex += __popc(L.exw[q] & m);
+        }
+        const uint32_t nv = slow ? 0u : cs_next - cs;
+        L.ccount[ul] = nv;
+        L.cstart[ul] = cs;
+        part = slow ? ReqPartial{0, 0, 0, 0, static_cast<int64_t>(nsl)}
+                    : ReqPartial{ex, static_cast<int64_t>(nv), static_cast<int64_t>(L.tcc[ul]),
+                                 static_cast<int64_t>(L.tan[ul]), 0};
+    }
+    const bool any_slow = __ballot(bad) != 0;
+    wave_lds_sync();
+    // ---- rows (lane i < nrows = row row_lo + i): hit counts -> run-local offsets
+    const uint32_t row = row_lo + ul;
+    const uint32_t ch = ul < nrows ? L.rowchain[ul] : 0xffu;
+    uint64_t nvr = 0;
+    if (ul < nrows) nvr = ch != 0xffu ? L.ccount[ch] : (sres ? static_cast<uint64_t>(rows[row].n_variants) : 0ull);
+    const bool slice_hits = ul < nrows && ch == 0xffu && nvr != 0;
+    const bool simple = !any_slow && !__ballot(slice_hits);  // buffer order = row order
+    const uint64_t linc = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(nvr)));
+    const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(linc), kWave - 1));
+    // ---- decoupled look-back: this run's offset = the hits of every earlier run
+    uint64_t O = 0;
+    if (ul == 0) {
+        constexpr unsigned long long kAgg = 1ull << 62, kPre = 2ull << 62, kVal = (1ull << 62) - 1;
+        __hip_atomic_store(&status[w], kAgg | H, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t excl = 0;
+        for (int64_t j = static_cast<int64_t>(w) - 1; j >= 0; --j) {
+            unsigned long long sj;
+            while (((sj = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0)
+                __builtin_amdgcn_s_sleep(1);
+            excl += sj & kVal;
+            if ((sj >> 62) == 2) break;
+        }
+        __hip_atomic_store(&status[w], kPre | (excl + H), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        O = excl;
+    }
+    O = static_cast<uint64_t>(rdl64(static_cast<int64_t>(O), 0));
+    // ---- outputs
+    if (ul < nrows) row_off[row] = O + linc - nvr;
+    if (row_hi == n_rows && ul == 0) row_off[n_rows] = O + H;
+    if (ul < R) rows[rowk] = part;
+    if (!sres && ul < nrows && ch == 0xffu) rows[row] = ReqPartial{0, 0, 0, 0, 0};
+    if (simple) {  // chain rows (and empty rows) only: the buffer is the output
+        for (uint64_t j = ul; j < H; j += kWave)
+            out[O + j] = (j < kRowHitBuf ? L.hbuf[j] : spill[spill_at + (j - kRowHitBuf)]) + rec_base;
+        return;
+    }
+    for (uint32_t i = 0; i < nrows; ++i) {  // row by row (some rows answered per slice)
+        const uint64_t nv = static_cast<uint64_t>(rdl64(static_cast<int64_t>(nvr), i));
+        if (!nv) continue;
+        const uint64_t at = O + static_cast<uint64_t>(rdl64(static_cast<int64_t>(linc), i)) - nv;
+        const uint32_t k = L.rowchain[i];
+        if (k != 0xffu) {
+            const uint32_t s0 = L.cstart[k];
+            for (uint64_t j = ul; j < nv; j += kWave) {
+                const uint64_t p = s0 + j;
+                out[at + j] = (p < kRowHitBuf ? L.hbuf[p] : spill[spill_at + (p - kRowHitBuf)]) + rec_base;
+            }
+        } else {
+            uint64_t dst = at;
+            for (uint32_t q = sseg[row_lo + i], qe = sseg[row_lo + i + 1]; q < qe; ++q) {
+                const QRes r = sres[q];
+                if (r.error || sherr[q]) continue;
+                const uint64_t src = shoff[q];
+                for (uint32_t j = ul; j < r.n_hits; j += kWave) out[dst + j] = shits[src + j] + rec_base;
+                dst += r.n_hits;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------- dense hit lists
 // Device-side result delivery for a sharded fan-out (sb_batch_compact_hits):
 // dense[q] = exclusive prefix over queries of their emitted hit counts (0 for
@@ -3039,6 +3328,19 @@ void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, ui
     const uint64_t wb = general_wave_bytes(gs, &hwords, &tcap);
     hipLaunchKernelGGL(general_slice_kernel, dim3(grid), dim3(kWave), 0, s, st, gs, work, qbytes, subsets, res, hits,
                        samples_out, scratch, wb, hwords, tcap, big_n, big, big_limbs, big_cap);
+}
+
+void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun *runs, uint32_t n_runs,
+                         uint32_t *ticket, unsigned long long *status, const QRes *sres, const uint32_t *sseg,
+                         const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits, ReqPartial *rows,
+                         uint64_t *row_off, uint64_t *out, uint64_t *spill, uint32_t n_rows, uint64_t rec_base,
+                         hipStream_t s) {
+    if (!n_runs) {
+        (void)hipMemsetAsync(row_off, 0, 8, s);
+        return;
+    }
+    hipLaunchKernelGGL(request_rows_kernel, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs, n_runs,
+                       ticket, status, sres, sseg, shoff, sherr, shits, rows, row_off, out, spill, n_rows, rec_base);
 }
 
 uint32_t pack_run_max() { return kPackRun; }

@@ -150,6 +150,9 @@ struct sb_store {
     std::vector<uint32_t> h_pos, h_end, h_a0_len, h_x_lo, h_x_len, h_bucket;
     std::vector<uint16_t> h_vt;
     std::vector<uint32_t> h_vt_slow;  // records whose VtHot word is VT_SLOW (sorted; chain planning)
+    // per (vcf, segment): POS of its VT_SLOW records, sorted (request batches:
+    // a request whose window holds one is answered per slice)
+    std::vector<std::vector<std::vector<uint32_t>>> seg_slow_pos;
     std::vector<uint32_t> h_vc_pos, h_vc_bucket;  // candidate POS + coarse candidate index (chain statistics)
     std::vector<uint64_t> h_vc_altpre;  // ALTs of candidates [0, j) (chain hit capacity)
     std::vector<uint64_t> h_ref_off, h_a0_off, h_x_off;

@@ -46,6 +46,19 @@ class Query(C.Structure):
                 ('sample_names', C.c_char_p), ('sample_names_len', C.c_size_t)]
 
 
+class Request(C.Structure):
+    """sb_request: one SplitQueryPayload x one of its VCFs (include/sbeacon.h)."""
+    _fields_ = [('vcf_id', C.c_uint32), ('contig', C.c_uint32),
+                ('start_min', C.c_int64), ('start_max', C.c_int64), ('end_min', C.c_int64), ('end_max', C.c_int64),
+                ('reference_bases', C.c_char_p), ('reference_len', C.c_size_t),
+                ('alternate_bases', C.c_char_p), ('alternate_len', C.c_size_t),
+                ('variant_type', C.c_char_p), ('variant_type_len', C.c_size_t),
+                ('variant_min_length', C.c_int64), ('variant_max_length', C.c_int64),
+                ('granularity', C.c_uint8), ('include_details', C.c_uint8), ('include_samples', C.c_uint8),
+                ('selected_samples_only', C.c_uint8), ('strict_variant_type', C.c_uint8), ('_pad', C.c_uint8 * 3),
+                ('sample_names', C.c_char_p), ('sample_names_len', C.c_size_t)]
+
+
 class ResultView(C.Structure):
     _fields_ = [('error', C.c_int32), ('exists', C.c_int32), ('call_count', C.c_int64),
                 ('all_alleles_count', C.c_int64), ('n_variants', C.c_uint64),
@@ -171,6 +184,8 @@ SIGNATURES = {
     'sb_free': (None, [P]),
     'sb_result_distinct_variants': (C.c_int, [P, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_void_p),
                                               C.POINTER(C.c_size_t), C.POINTER(C.c_uint64)]),
+    'sb_requests_prepare': (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(P)]),
+    'sb_requests_run': (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
 }
 
 _lib = None

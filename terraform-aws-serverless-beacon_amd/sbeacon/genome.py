@@ -347,3 +347,67 @@ def shard_record_base(shape: GenomeShape, world: int, rank: int) -> int:
         return 0
     ci, lo, _ = pieces[0]
     return int(shape.offsets[ci]) + lo
+
+
+@dataclass
+class ShardRequests:
+    """The sub-requests one rank answers (request batch): row w = request
+    row_lo + w; its slices on this rank are slice indices [k0, k1) of the
+    request's splitQuery slices, i.e. the sub-request [start_min + 10000 k0,
+    min(start_max, start_min + 10000 k1 - 1)] (end bounds unchanged)."""
+    row_lo: int
+    n_rows: int
+    ci: np.ndarray
+    start_min: np.ndarray
+    start_max: np.ndarray   # < start_min: no slice of the request on this rank
+    end_min: np.ndarray
+    end_max: np.ndarray
+    vt: np.ndarray
+    vmin: np.ndarray
+    vmax: np.ndarray
+
+    def __len__(self):
+        return self.n_rows
+
+
+def shard_requests(shape: GenomeShape, reqs: Requests, world: int, rank: int) -> ShardRequests:
+    """Vectorised: each request's slices whose first base is in rank's core
+    [cuts[rank], cuts[rank + 1]) form one run of slice indices."""
+    cuts = shape.cuts(world)
+    (c0, p0), (c1, p1) = cuts[rank], cuts[rank + 1]
+    smin = reqs.start.astype(np.int64) + 1
+    smax = reqs.start.astype(np.int64) + reqs.width + 1
+    nsl = (smax - smin) // SPLIT_SIZE + 1
+    ci = reqs.ci.astype(np.int64)
+    ceil_div = lambda a: -((-a) // SPLIT_SIZE)  # noqa: E731
+    k0 = np.where(ci > c0, 0, np.where(ci == c0, np.clip(ceil_div(p0 - smin), 0, None), nsl))
+    k1 = np.where(ci < c1, nsl, np.where(ci == c1, np.clip(ceil_div(p1 - smin), 0, None), 0))
+    k0 = np.minimum(k0, nsl)
+    k1 = np.clip(k1, k0, nsl)
+    has = k1 > k0
+    idx = np.flatnonzero(has)
+    if len(idx) == 0:
+        e = np.zeros(0, dtype=np.int64)
+        return ShardRequests(0, 0, e, e, e, e, e, e, e, e)
+    lo, hi = int(idx[0]), int(idx[-1]) + 1
+    w = slice(lo, hi)
+    a = smin[w] + SPLIT_SIZE * k0[w]
+    b = np.minimum(smax[w], smin[w] + SPLIT_SIZE * k1[w] - 1)
+    b = np.where(has[w], b, a - 1)
+    return ShardRequests(lo, hi - lo, ci[w], a, b, smin[w], smax[w], reqs.vt[w], reqs.vmin[w], reqs.vmax[w])
+
+
+def prepare_shard_requests(store, sr: ShardRequests):
+    """The rank's request batch (sbeacon.requests.RequestBatch)."""
+    from .requests import RequestBatch, requests_array
+    names = store.contigs(LOCATION)
+    at = {c: i for i, c in enumerate(names)}
+    cmap = np.array([at.get(c, 0xffffffff) for c in CONTIGS], dtype=np.int64)
+    arr, keep = requests_array(
+        sr.n_rows, vcf_id=store.vcf_id(LOCATION), contig=cmap[sr.ci] if sr.n_rows else 0,
+        start_min=sr.start_min, start_max=sr.start_max, end_min=sr.end_min, end_max=sr.end_max,
+        reference=('N',), alternate=(None,), variant_type=VARIANT_TYPES, variant_type_code=sr.vt,
+        variant_min_length=sr.vmin, variant_max_length=sr.vmax, granularity='record', include_details=1)
+    batch = RequestBatch(store, arr, sr.n_rows)
+    del keep
+    return batch

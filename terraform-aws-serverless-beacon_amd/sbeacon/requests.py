@@ -1,0 +1,213 @@
+"""Request batches: the splitQuery fan-out inside the library.
+
+One *request* is one ``SplitQueryPayload``
+(``shared_resources/payloads/lambda_payloads.py:8-44``) restricted to one of
+its ``vcf_locations`` -- what ``split_query_sync``
+(``lambda/splitQuery/lambda_function.py:74-110``) would cut into 10 kb
+``PerformQueryPayload`` slices.  ``sb_requests_prepare`` takes the requests
+as a columnar array (no per-slice payload objects, no region strings) and
+``sb_requests_run`` answers all of them on the device, leaving one row per
+request -- the route-level sums of its slices' responses
+(``route_g_variants.py:144-171``: exists count, variants, call_count,
+all_alleles_count, errors) -- and the rows' hit lists densely in request
+order.  ``requests_array`` builds the ``sb_request`` array from numpy
+columns; string columns are small dictionaries of distinct values plus a
+code per request.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import Request, check, lib
+
+_FIELDS = [f for f, _ in Request._fields_ if f != '_pad']
+
+
+def request_dtype() -> np.dtype:
+    """numpy view of one sb_request (the C layout, padding kept)."""
+    fmt = {C.c_uint32: 'u4', C.c_int64: 'i8', C.c_char_p: 'u8', C.c_size_t: 'u8', C.c_uint8: 'u1'}
+    names, formats, offsets = [], [], []
+    for f, t in Request._fields_:
+        if f == '_pad':
+            continue
+        names.append(f)
+        formats.append(fmt[t])
+        offsets.append(getattr(Request, f).offset)
+    return np.dtype({'names': names, 'formats': formats, 'offsets': offsets, 'itemsize': C.sizeof(Request)})
+
+
+class _Pool:
+    """Distinct strings in one ctypes buffer: value -> (address, length)."""
+
+    def __init__(self):
+        self.bufs = []
+
+    def column(self, values: Sequence, codes, n: int):
+        """values: distinct strings (None = NULL); codes: index per request
+        (scalar = the same for all).  Returns (address array, length array)."""
+        addr = np.zeros(len(values), dtype=np.uint64)
+        ln = np.zeros(len(values), dtype=np.uint64)
+        for k, v in enumerate(values):
+            if v is None:
+                continue
+            b = v.encode() if isinstance(v, str) else bytes(v)
+            buf = C.create_string_buffer(b, len(b) + 1)
+            self.bufs.append(buf)
+            addr[k] = C.addressof(buf)
+            ln[k] = len(b)
+        codes = np.broadcast_to(np.asarray(codes, dtype=np.int64), (n,))
+        return addr[codes], ln[codes]
+
+
+def requests_array(n: int, *, vcf_id, contig, start_min, start_max, end_min, end_max,
+                   reference=('N',), reference_code=0, alternate=(None,), alternate_code=0,
+                   variant_type=(None,), variant_type_code=0, variant_min_length=0, variant_max_length=-1,
+                   granularity='record', include_details=True, include_samples=False,
+                   selected_samples_only=False, strict_variant_type=False, sample_names=(None,),
+                   sample_names_code=0):
+    """sb_request array of n requests from columns (scalars broadcast).
+    Returns (ctypes array, keep-alive)."""
+    arr = (Request * max(n, 1))()
+    keep = _Pool()
+    if n == 0:
+        return arr, keep
+    v = np.frombuffer((C.c_char * (C.sizeof(Request) * n)).from_address(C.addressof(arr)), dtype=request_dtype())
+    v['vcf_id'] = vcf_id
+    v['contig'] = contig
+    v['start_min'] = start_min
+    v['start_max'] = start_max
+    v['end_min'] = end_min
+    v['end_max'] = end_max
+    for f, vals, codes in (('reference_bases', reference, reference_code),
+                           ('alternate_bases', alternate, alternate_code),
+                           ('variant_type', variant_type, variant_type_code),
+                           ('sample_names', sample_names, sample_names_code)):
+        a, ln = keep.column(vals, codes, n)
+        v[f] = a
+        v[{'reference_bases': 'reference_len', 'alternate_bases': 'alternate_len',
+           'variant_type': 'variant_type_len', 'sample_names': 'sample_names_len'}[f]] = ln
+    v['variant_min_length'] = variant_min_length
+    v['variant_max_length'] = variant_max_length
+    g = granularity
+    v['granularity'] = _lib.SB_GRAN[g] if isinstance(g, str) else g
+    v['include_details'] = np.asarray(include_details, dtype=np.uint8)
+    v['include_samples'] = np.asarray(include_samples, dtype=np.uint8)
+    v['selected_samples_only'] = np.asarray(selected_samples_only, dtype=np.uint8)
+    v['strict_variant_type'] = np.asarray(strict_variant_type, dtype=np.uint8)
+    return arr, keep
+
+
+def requests_from_split_payloads(store, payloads: list[dict], *, strict_variant_type: bool = False):
+    """SplitQueryPayload dicts -> (sb_request array, keep-alive, owners):
+    one request per (payload, vcf_location) pair, owners[k] = (payload
+    index, vcf_location).  The chrom string each vcf_location maps to is
+    looked up among the VCF's contigs (absent: a request with no slices, as
+    bcftools emits nothing for it)."""
+    rows = []
+    for i, p in enumerate(payloads):
+        for loc, chrom in p['vcf_locations'].items():
+            rows.append((i, loc, chrom))
+    n = len(rows)
+    contig_idx = {}
+
+    def cidx(loc, chrom):
+        key = (loc, chrom)
+        if key not in contig_idx:
+            names = store.contigs(loc)
+            contig_idx[key] = names.index(chrom) if chrom in names else 0xffffffff
+        return contig_idx[key]
+
+    def codes(vals):
+        d = {}
+        out = np.empty(len(vals), dtype=np.int64)
+        for k, x in enumerate(vals):
+            out[k] = d.setdefault(x, len(d))
+        return list(d), out
+
+    P = [payloads[i] for i, _, _ in rows]
+    ref_v, ref_c = codes([p.get('reference_bases') for p in P])
+    alt_v, alt_c = codes([p.get('alternate_bases') for p in P])
+    vt_v, vt_c = codes([p.get('variant_type') for p in P])
+    pts = [p.get('passthrough') or {} for p in P]
+    sn_v, sn_c = codes([','.join(pt['sampleNames']) if pt.get('sampleNames') is not None else None for pt in pts])
+    arr, keep = requests_array(
+        n, vcf_id=[store.vcf_id(loc) for _, loc, _ in rows], contig=[cidx(loc, c) for _, loc, c in rows],
+        start_min=[int(p['start_min']) for p in P], start_max=[int(p['start_max']) for p in P],
+        end_min=[int(p['end_min']) for p in P], end_max=[int(p['end_max']) for p in P],
+        reference=ref_v, reference_code=ref_c, alternate=alt_v, alternate_code=alt_c,
+        variant_type=vt_v, variant_type_code=vt_c,
+        variant_min_length=[int(p['variant_min_length']) for p in P],
+        variant_max_length=[int(p['variant_max_length']) for p in P],
+        granularity=[_lib.SB_GRAN.get(p.get('requested_granularity'), 255) for p in P],
+        include_details=[1 if p.get('include_datasets') in ('HIT', 'ALL') else 0 for p in P],
+        include_samples=[1 if pt.get('includeSamples', False) else 0 for pt in pts],
+        selected_samples_only=[1 if pt.get('selectedSamplesOnly', False) else 0 for pt in pts],
+        strict_variant_type=1 if strict_variant_type else 0, sample_names=sn_v, sample_names_code=sn_c)
+    return arr, keep, [(i, loc) for i, loc, _ in rows]
+
+
+class RequestBatch:
+    """A prepared request batch (sb_requests_prepare) on the store's device."""
+
+    def __init__(self, store, arr, n: int):
+        self.store = store
+        self.n = n
+        h = C.c_void_p()
+        check(lib().sb_requests_prepare(store.handle, C.cast(arr, C.c_void_p), n, C.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self):
+        return self._h
+
+    def run(self, rows_ptr: int, hits_ptr: int, row_off_ptr: int, rec_base: int = 0):
+        """Enqueue one pass: rows (n x 5 int64: exists, n_variants, call_count,
+        all_alleles_count, errors), dense hits, n + 1 row offsets."""
+        check(lib().sb_requests_run(self._h, C.c_void_p(rows_ptr), C.c_void_p(hits_ptr), C.c_void_p(row_off_ptr),
+                                    int(rec_base)))
+
+    def sync(self):
+        check(lib().sb_batch_sync(self._h))
+
+    def timing(self):
+        t, s, b = C.c_double(), C.c_double(), C.c_double()
+        check(lib().sb_batch_last_timing(self._h, C.byref(t), C.byref(s), C.byref(b)))
+        return {'total_ms': t.value, 'scan_ms': s.value}
+
+    def stats(self) -> dict:
+        st = _lib.BatchStats()
+        check(lib().sb_batch_get_stats(self._h, C.byref(st)))
+        return {f: getattr(st, f) for f, _ in _lib.BatchStats._fields_}
+
+    def set_stream(self, stream_ptr):
+        check(lib().sb_batch_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def free(self):
+        if self._h:
+            lib().sb_batch_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def answer(self, rec_base: int = 0, device=None):
+        """One pass, rows + hit lists copied to the host (torch tensors on
+        the store's device as staging): (rows [n, 5] int64, hits uint64,
+        row_off [n + 1] int64)."""
+        import torch
+        dev = device if device is not None else torch.device('cuda', self.store.info()['device'])
+        rows = torch.zeros((max(self.n, 1), 5), dtype=torch.int64, device=dev)
+        hits = torch.zeros(max(int(self.stats()['hits']), 1), dtype=torch.int64, device=dev)
+        row_off = torch.zeros(self.n + 1, dtype=torch.int64, device=dev)
+        self.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+        self.run(rows.data_ptr(), hits.data_ptr(), row_off.data_ptr(), rec_base)
+        self.sync()
+        ro = row_off.cpu().numpy()
+        return rows[:self.n].cpu().numpy(), hits[:int(ro[-1])].cpu().numpy().view(np.uint64), ro

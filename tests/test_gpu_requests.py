@@ -1,0 +1,181 @@
+"""Request batches (sb_requests_prepare / sb_requests_run: the splitQuery
+fan-out in the library, rows + dense hit lists in request order) against the
+per-slice path: every request's row equals the route-level reduction of its
+splitQuery slices' responses and its hit list the concatenation of theirs;
+on the config-3 genome shape also against the C oracle."""
+import os
+import random
+import tempfile
+
+import numpy as np
+import pytest
+
+from conftest import FIXTURES
+
+pytestmark = pytest.mark.gpu
+
+
+def _split_payload(rng, recs, names, loc, chrom='22'):
+    pos = recs[rng.randrange(len(recs))][1]
+    width = rng.choice([0, 1, 50, 5000, 9999, 10000, 25000, 100000, 330000])
+    smin = max(1, pos - rng.randrange(0, width + 1))
+    smax = smin + width
+    u = rng.random()
+    ref, alt, vt = 'N', None, rng.choice(['DEL', 'INS', 'DUP', 'DUP:TANDEM', 'CNV', 'INV', None])
+    if u < 0.25:
+        alt = 'N'
+    elif u < 0.35:
+        alt, ref = 'A', rng.choice(['N', 'C', 'G'])
+    gran = rng.choice(['record', 'record', 'aggregated', 'count', 'boolean'])
+    pt = {}
+    r = rng.random()
+    if r < 0.1:
+        pt = {'includeSamples': True}
+    elif r < 0.15 and names:
+        pt = {'sampleNames': rng.sample(names, rng.randrange(1, len(names) + 1)), 'selectedSamplesOnly': True}
+    emin, emax = (smin, smax + rng.choice([0, 10, 10**6])) if rng.random() < 0.7 else (0, 10**9)
+    vmin, vmax = (0, -1) if rng.random() < 0.6 else (rng.choice([0, 1, 2]), rng.choice([-1, 1, 3, 10]))
+    return dict(passthrough=pt, dataset_id='d', query_id='q', reference_bases=ref, start_min=smin, start_max=smax,
+                end_min=emin, end_max=emax, alternate_bases=alt, variant_type=vt,
+                include_datasets=rng.choice(['HIT', 'HIT', 'ALL', 'NONE']), vcf_locations={loc: chrom},
+                vcf_groups=[], requested_granularity=gran, variant_min_length=vmin, variant_max_length=vmax)
+
+
+def _expected(store, split_payloads):
+    """Per-slice path: splitQuery's payloads through store.query, reduced per
+    request row (route-level sums) + concatenated hit lists."""
+    pls, owner = [], []
+    for i, sp in enumerate(split_payloads):
+        for p in split_payloads_of(sp):
+            pls.append(p)
+            owner.append(i)
+    rs = store.query(pls)
+    res = rs.responses()
+    # route-level sums per row (sb_request_partial), Python ints wrapped to int64 as the device rows hold them
+    acc = [[0, 0, 0, 0, 0] for _ in split_payloads]
+    for o, r in zip(owner, res):
+        if isinstance(r, Exception):
+            acc[o][4] += 1
+            continue
+        d = r.dump()
+        acc[o][0] += 1 if d['exists'] else 0
+        acc[o][1] += len(d['variants'])
+        acc[o][2] += d['call_count']
+        acc[o][3] += d['all_alleles_count']
+    wrap = lambda x: ((x + 2**63) % 2**64) - 2**63  # noqa: E731
+    rows = np.array([[wrap(x) for x in a] for a in acc], dtype=np.int64).reshape(len(split_payloads), 5)
+    hits = [[] for _ in split_payloads]
+    for j, o in enumerate(owner):
+        if not isinstance(res[j], Exception):
+            hits[o].extend(int(r) | (int(a) << 32) for r, a in rs.hits(j))
+    return rows, hits
+
+
+def split_payloads_of(sp):
+    from sbeacon.split_query import split_payloads
+    return split_payloads(sp)
+
+
+@pytest.mark.parametrize('fixture', ['tiny22', 'quirk22', 'general22'])
+def test_requests_match_slices(fixture):
+    from payload_gen import read_records
+    from sbeacon.engine import Store
+    from sbeacon.requests import RequestBatch, requests_from_split_payloads
+    path = os.path.join(FIXTURES, fixture + '.vcf')
+    store = Store.build([(fixture + '.vcf', path)], device=0)
+    recs, names = read_records(path)
+    rng = random.Random(hash(fixture) % 1000)
+    sps = [_split_payload(rng, recs, names, fixture + '.vcf') for _ in range(400)]
+    sps.append(dict(sps[0], vcf_locations={fixture + '.vcf': 'chrUnknown'}))  # contig the VCF lacks
+    sps.append(dict(sps[1], start_min=sps[1]['start_max'] + 1))               # no slices
+    arr, keep, owners = requests_from_split_payloads(store, sps)
+    b = RequestBatch(store, arr, len(owners))
+    rows, hits, ro = b.answer()
+    exp_rows, exp_hits = _expected(store, sps)
+    np.testing.assert_array_equal(rows, exp_rows)
+    assert np.all(np.diff(ro) == rows[:, 1])
+    for w in range(len(sps)):
+        assert [int(x) for x in hits[ro[w]:ro[w + 1]]] == exp_hits[w], (w, sps[w])
+    st = b.stats()
+    assert st['chains'] > 0  # some requests took the chain path
+
+
+def test_genome_requests_match_oracle_and_slices():
+    """Config-3 shape (small): shard request batches at world 1 and 2 vs the
+    per-slice shard batches (rows + hit lists) and the C oracle (rows)."""
+    from oracle.oracle import OracleVcf
+    from sbeacon.genome import (GenomeShape, config3_requests, prepare_shard_batch, prepare_shard_requests,
+                                shard_record_base, shard_requests, shard_slices, slice_payloads)
+    from sbeacon.shard import request_rows_from_responses
+    import torch
+    shape = GenomeShape(n_total=240_000, seed=3, n_samples=0)
+    reqs = config3_requests(shape, n=2000, seed=1003)
+    with tempfile.TemporaryDirectory() as tmp:
+        full = os.path.join(tmp, 'full.vcf')
+        with open(full, 'wb') as f:
+            for c in shape.shard_chunks(1, 0):
+                f.write(c)
+        orc = OracleVcf(full, load_gt=False)
+        whole = shard_slices(shape, reqs, 1, 0)
+        exp = request_rows_from_responses(whole.req, orc.perform_query_batch(slice_payloads(whole), patched=True),
+                                          whole.n_rows)
+    for world in (1, 2):
+        total = np.zeros((len(reqs), 5), dtype=np.int64)
+        for rank in range(world):
+            store = shape.build_shard_store(world, rank, device=0)
+            sr = shard_requests(shape, reqs, world, rank)
+            sl = shard_slices(shape, reqs, world, rank)
+            assert (sr.row_lo, sr.n_rows) == (sl.row_lo, sl.n_rows)
+            base = shard_record_base(shape, world, rank)
+            b = prepare_shard_requests(store, sr)
+            rows, hits, ro = b.answer(rec_base=base)
+            # the per-slice shard batch (rows + hit lists by sb_batch_deliver)
+            sb = prepare_shard_batch(store, sl)
+            part = torch.zeros((sl.n_rows, 5), dtype=torch.int64, device='cuda:0')
+            h2 = torch.zeros(max(sb.stats()['hits'], 1), dtype=torch.int64, device='cuda:0')
+            ro2 = torch.zeros(sl.n_rows + 1, dtype=torch.int64, device='cuda:0')
+            sb.set_stream(torch.cuda.current_stream().cuda_stream)
+            sb.run()
+            sb.deliver(part.data_ptr(), h2.data_ptr(), ro2.data_ptr(), base)
+            sb.sync()
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(rows, part.cpu().numpy())
+            ro2 = ro2.cpu().numpy()
+            h2 = h2.cpu().numpy().view(np.uint64)
+            for w in range(sr.n_rows):
+                assert sorted(hits[ro[w]:ro[w + 1]].tolist()) == sorted(h2[ro2[w]:ro2[w + 1]].tolist()), w
+            total[sr.row_lo:sr.row_lo + sr.n_rows] += rows
+        np.testing.assert_array_equal(total, exp)
+
+
+def test_request_batch_is_repeatable():
+    """Back-to-back passes (ticket / status re-zeroed per pass) give the same
+    rows and hits; the spill path (more hits per run than the LDS buffer)
+    is exercised by a dense fixture."""
+    from payload_gen import read_records
+    from sbeacon.engine import Store
+    from sbeacon.requests import RequestBatch, requests_from_split_payloads
+    path = os.path.join(FIXTURES, 'tiny22.vcf')
+    store = Store.build([('tiny22.vcf', path)], device=0)
+    recs, names = read_records(path)
+    lo, hi = recs[0][1], recs[-1][1]
+    sps = []
+    for k in range(64):  # wide variantType requests over the whole fixture: many hits per run
+        sps.append(dict(passthrough={}, dataset_id='d', query_id='q', reference_bases='N', start_min=lo + k,
+                        start_max=min(hi, lo + k + 300000), end_min=0, end_max=10**9, alternate_bases=None,
+                        variant_type=['DEL', 'INS', 'CNV', 'DUP'][k % 4], include_datasets='HIT',
+                        vcf_locations={'tiny22.vcf': '22'}, vcf_groups=[], requested_granularity='record',
+                        variant_min_length=0, variant_max_length=-1))
+    arr, keep, owners = requests_from_split_payloads(store, sps)
+    b = RequestBatch(store, arr, len(owners))
+    first = b.answer()
+    for _ in range(3):
+        again = b.answer()
+        for x, y in zip(first, again):
+            np.testing.assert_array_equal(x, y)
+    exp_rows, exp_hits = _expected(store, sps)
+    rows, hits, ro = first
+    np.testing.assert_array_equal(rows, exp_rows)
+    for w in range(len(sps)):
+        assert [int(x) for x in hits[ro[w]:ro[w + 1]]] == exp_hits[w], w
+    assert ro[-1] > 320  # more than one LDS buffer of hits in some run
