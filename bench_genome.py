@@ -48,8 +48,8 @@ def main_genome(args):
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group('nccl', device_id=dev)
-    from sbeacon.genome import (GenomeShape, config3_requests, first_rank_of_rows, prepare_shard_batch,
-                                shard_record_base, shard_slices, union_rows)
+    from sbeacon.genome import (GenomeShape, config3_requests, first_rank_of_rows, prepare_shard_requests,
+                                shard_record_base, shard_requests, union_rows, shard_slices)
     from sbeacon.shard import ResultExchange, owner_ranks
 
     t0 = time.perf_counter()
@@ -67,31 +67,29 @@ def main_genome(args):
     t_ingest = time.perf_counter() - t0
     log(f'[rank {rank}] shard: {info["n_records"]} records, {info["device_bytes"] / 2**20:.0f} MiB HBM, '
         f'ingest {t_ingest:.1f} s')
-    t0 = time.perf_counter()
     # weak scaling (default): genome-wide requests, args.genome_requests per GPU, routed
     # to the shards by position; strong: args.genome_requests in total
     n_req = args.genome_requests * (world if args.scaling == 'weak' else 1)
     reqs = config3_requests(shape, n=n_req, seed=1003)
-    sl = shard_slices(shape, reqs, world, rank)
-    batch = prepare_shard_batch(store, sl)
+    t0 = time.perf_counter()
+    sr = shard_requests(shape, reqs, world, rank)  # the splitQuery slices on this rank, per request
+    batch = prepare_shard_requests(store, sr)      # request batch: planning + upload (C++)
+    t_prepare = time.perf_counter() - t0
     batch.set_stream(torch.cuda.current_stream().cuda_stream)  # one stream: kernels, torch ops, RCCL
-    # the step delivers request rows + hit lists: chained slices skip their
-    # per-slice QRes rows (turned back on below for the per-slice fetch)
-    batch.set_slice_results(False)
     pst = batch.stats()
-    part = torch.zeros((max(sl.n_rows, 1), 5), dtype=torch.int64, device=dev)
+    part = torch.zeros((max(sr.n_rows, 1), 5), dtype=torch.int64, device=dev)
     hits = torch.zeros(max(int(pst['hits']), 1), dtype=torch.int64, device=dev)
-    row_off = torch.zeros(sl.n_rows + 1, dtype=torch.int64, device=dev)
+    row_off = torch.zeros(sr.n_rows + 1, dtype=torch.int64, device=dev)
     base = shard_record_base(shape, world, rank)
+    sl = shard_slices(shape, reqs, world, rank)  # slice view (statistics / roofline pricing only)
     owners = owner_ranks(first_rank_of_rows(shape, reqs, world, sl), args.deliver, rank)
-    ex = ResultExchange(dist, rank, world, sl.row_lo, sl.n_rows, owners, dev)
-    log(f'[rank {rank}] {n_req} requests, {len(sl)} slices on this rank (rows {sl.row_lo}+{sl.n_rows}, '
+    ex = ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, dev)
+    log(f'[rank {rank}] {n_req} requests, {len(sl)} slices on this rank (rows {sr.row_lo}+{sr.n_rows}, '
         f'{pst["chains"]} chains), delivery {args.deliver}: owns {ex.n_own} rows, receives {len(ex.recvs)} '
-        f'range(s), prepare {time.perf_counter() - t0:.1f} s')
+        f'range(s), prepare {t_prepare:.2f} s')
 
-    def step():  # answer + deliver: chain kernel, request rows, dense hit lists, exchange
-        batch.run()
-        batch.deliver(part.data_ptr(), hits.data_ptr(), row_off.data_ptr(), base)  # request rows + hit lists
+    def step():  # answer + deliver: request rows + dense hit lists (one kernel), exchange
+        batch.run(part.data_ptr(), hits.data_ptr(), row_off.data_ptr(), base)
         ex.exchange(part, hits, row_off)
 
     for _ in range(args.warmup):
@@ -109,40 +107,47 @@ def main_genome(args):
     if dist:
         dist.barrier()
     step_dev_ms = batch.timing()['scan_ms']  # HIP events on the stream: first run -> sync, / steps
-    # the dominant kernel alone (chain_kernel): K back-to-back runs between two events
+    # the dominant kernel alone: K back-to-back passes between two events on its stream
     for _ in range(args.steps):
-        batch.run()
+        batch.run(part.data_ptr(), hits.data_ptr(), row_off.data_ptr(), base)
     batch.sync()
     kern_ms = batch.timing()['scan_ms']
-    batch.set_slice_results(True)
-    batch.run()
-    batch.sync()
-    rs = batch.fetch()
-    st = rs.stats()
-    scanned, nhits = st['records_scanned'], st['hits']
-    # Roofline of chain_pack_kernel, priced on the bytes one launch must move
-    # at least once: chain descriptors (80 B), their two
-    # coarse-index entries (8 B), the request-row partial (40 B), the
-    # candidate words in the union of the chain windows (POS 4 + VtHot 16 +
-    # record 4 = 24 B, each candidate once however many overlapping requests
-    # read it) and hits (8 B).  Beside it the SURVEY §8d contract figure:
-    # 32 B x unique records in the slice windows + 8 B / hit.
-    chains, cslices = st['chains'], st['chained_slices']
-    comp = 80.0 * chains + 8.0 * chains + 40.0 * chains + 24.0 * st['cand_unique'] + 8.0 * nhits
+    nhits = int(row_off[-1].item())
+    # candidate statistics of the rank's chains (the slice view of the same requests)
+    from sbeacon.genome import prepare_shard_batch
+    sbat = prepare_shard_batch(store, sl)
+    st = sbat.stats()
+    sbat.free()
+    # Roofline of request_rows_kernel, priced on the bytes one launch must move
+    # at least once: per chain its 80 B descriptor, two
+    # coarse-index entries (8 B), its row (40 B) and row offset (8 B); 24 B per
+    # candidate in the union of the chain windows (POS 4 + VtHot 16 + record
+    # 4, each once however many overlapping requests read it); 8 B per hit
+    # written.  Beside it the SURVEY §8d contract: 32 B x unique records in
+    # the slice windows + 8 B / hit.
+    chains = int(pst['chains'])
+    comp = (80.0 + 8.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * nhits
     achieved = comp / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     uniq = union_rows(shape, sl)
     contract = 32.0 * uniq + 8.0 * nhits
-    traffic = None  # HBM bytes per launch from the PMC passes (tools/gpu_pmc_genome_traffic.sh)
+    traffic = None  # HBM bytes per launch from the PMC passes (tools/gpu_pmc_r03.sh)
     tf = os.path.join(REPO, 'profiles', 'traffic_genome.json')
     if world == 1 and os.path.exists(tf):
         try:
             tj = json.load(open(tf))
-            if tj.get('records') == shape.n_total and tj.get('requests') == len(reqs) and tj.get('kernel') == 'chain_pack_kernel<false>':
+            if tj.get('records') == shape.n_total and tj.get('requests') == len(reqs) and \
+                    tj.get('kernel') == 'request_rows_kernel':
                 traffic = tj.get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
-    vals = [elapsed, kern_ms, float(len(sl)), float(scanned), float(nhits), achieved, float(uniq), comp, contract,
-            step_dev_ms]
+    # delivered: requests in host memory -> rows + hit lists in host memory,
+    # everything inside the timed region (routing to the rank, planning,
+    # upload, the pass, D2H); rank-local (no exchange)
+    delivered = None
+    if world == 1:
+        delivered = delivered_passes(args, store, shape, reqs, world, rank, base, dev)
+    vals = [elapsed, kern_ms, float(len(sl)), float(st['cand_loaded']), float(nhits), achieved, float(uniq), comp,
+            contract, step_dev_ms]
     if dist:
         t = torch.tensor(vals, dtype=torch.float64, device=dev)
         allv = [torch.zeros_like(t) for _ in range(world)]
@@ -152,7 +157,7 @@ def main_genome(args):
         allv = [vals]
     elapsed = max(v[0] for v in allv)
     tot_slices = sum(v[2] for v in allv)
-    tot_scanned = sum(v[3] for v in allv)
+    tot_cand = sum(v[3] for v in allv)
     tot_hits = sum(v[4] for v in allv)
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -178,34 +183,94 @@ def main_genome(args):
                    'parallelism': f'contig shards x{world} (+10 kb halo); request rows + hit lists delivered to '
                                   f'the {"first slice" if args.deliver == "first" else "rank 0"} rank over '
                                   f'{"RCCL" if world > 1 else "(no peer)"}'},
-        'step': 'chain_pack_kernel (request-row partials + dense chain hits; per-slice rows off) + request rows '
-                '+ dense hit lists (scan, gather) + exchange (all_gather of counts, send/recv of straddling rows and '
-                'hits)',
-        'records_scanned_per_s': round(tot_scanned * args.steps / elapsed, 1),
+        'step': 'request batch pass (request_rows_kernel: every request = one chain of its 10 kb slices, rows + '
+                'dense hit lists in request order, offsets by decoupled look-back) + exchange (all_gather of '
+                'counts, send/recv of straddling rows and hits); inputs resident in HBM',
+        'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
+        'candidates_loaded_per_s': round(tot_cand * args.steps / elapsed, 1),
         'hits_per_step': int(tot_hits),
-        'device_ms_per_step': {'step_rank0': round(r0[9], 4), 'chain_kernel_rank0': round(r0[1], 4),
-                               'chain_kernel_max': round(max(v[1] for v in allv), 4)},
+        'device_ms_per_step': {'step_rank0': round(r0[9], 4), 'kernel_rank0': round(r0[1], 4),
+                               'kernel_max': round(max(v[1] for v in allv), 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(r0[5], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(r0[5] / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                     'kernel': 'chain_kernel (rank 0), HIP events around K back-to-back launches on its stream',
+                     'kernel': 'request_rows_kernel (rank 0): HIP events around K back-to-back launches on its '
+                               'stream, / K',
                      'algorithmic_bytes_per_launch': r0[7],
-                     'pricing': 'bytes one launch must move at least once: 128 B/chain (80 B descriptor + 2 '
-                                'index entries + 40 B request-row partial) + 24 B per candidate in the union of the '
-                                'chain windows + 8 B/hit (the step keeps request rows, not per-slice rows)',
+                     'pricing': 'bytes one launch must move at least once: 136 B/request (80 B chain descriptor + 2 '
+                                'index entries + 40 B row + 8 B row offset) + 24 B per candidate in the union of the '
+                                'chain windows + 8 B/hit written',
                      'candidates': {'unique': int(st['cand_unique']), 'in_windows': int(st['cand_window']),
                                     'loaded': int(st['cand_loaded'])},
                      'contract_bytes_per_launch': r0[8],
                      'contract_frac': round(r0[8] / (r0[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if r0[1] > 0 else None,
-                     'contract_note': 'SURVEY 8d: 32 B x unique records in the slice windows (a full scan of them) '
-                                      '+ 8 B/hit; the candidate index reads a few % of those records'},
+                     'contract_note': 'SURVEY 8d prices a full scan of every record in the slice windows (32 B x '
+                                      'unique records + 8 B/hit); the candidate index never reads most of them, so '
+                                      'this is records covered per second, not bytes moved'},
+        'delivered': delivered,
         'cpu_baseline': cpu,
         'parity_sample': parity,
         'ingest_s': round(t_ingest, 2),
+        'prepare_s': round(t_prepare, 3),
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5):
+    """End to end on one GPU: requests (numpy, host) -> routing to the rank
+    (shard_requests, numpy) -> request batch planning + upload
+    (sb_requests_prepare, C++) -> one pass -> rows, row offsets and the hit
+    lists copied back into pinned host memory.  Every part inside the timed
+    region; a fresh batch each pass."""
+    import numpy as np
+    import torch
+    from sbeacon.genome import prepare_shard_requests, shard_requests
+    t_route = t_prep = t_dev = 0.0
+    best = None
+    rows_h = hits_h = ro_h = None
+    for k in range(passes + 1):  # pass 0 warms the allocator / pinned buffers (untimed)
+        torch.cuda.synchronize()
+        a = time.perf_counter()
+        sr = shard_requests(shape, reqs, world, rank)
+        b0 = time.perf_counter()
+        batch = prepare_shard_requests(store, sr)
+        batch.set_stream(torch.cuda.current_stream().cuda_stream)
+        cap = int(batch.stats()['hits'])
+        c0 = time.perf_counter()
+        if rows_h is None or rows_h.shape[0] < sr.n_rows or hits_h.shape[0] < cap:
+            rows_d = torch.empty((max(sr.n_rows, 1), 5), dtype=torch.int64, device=dev)
+            ro_d = torch.empty(sr.n_rows + 1, dtype=torch.int64, device=dev)
+            hits_d = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+            rows_h = torch.empty(rows_d.shape, dtype=torch.int64, pin_memory=True)
+            ro_h = torch.empty(ro_d.shape, dtype=torch.int64, pin_memory=True)
+            hits_h = torch.empty(hits_d.shape, dtype=torch.int64, pin_memory=True)
+        batch.run(rows_d.data_ptr(), hits_d.data_ptr(), ro_d.data_ptr(), base)
+        rows_h[:sr.n_rows].copy_(rows_d[:sr.n_rows], non_blocking=True)
+        ro_h.copy_(ro_d, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        total = int(ro_h[-1])
+        hits_h[:total].copy_(hits_d[:total], non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        d0 = time.perf_counter()
+        batch.free()
+        if k == 0:
+            continue
+        t_route += b0 - a
+        t_prep += c0 - b0
+        t_dev += d0 - c0
+        best = (d0 - a) if best is None else min(best, d0 - a)
+    dt = (t_route + t_prep + t_dev) / passes
+    n = len(reqs)
+    return {'requests_per_s': round(n / dt, 1), 'ms_per_pass': round(dt * 1e3, 2),
+            'best_ms': round(best * 1e3, 2), 'passes': passes,
+            'split_ms': {'route_numpy': round(t_route / passes * 1e3, 2),
+                         'prepare_upload': round(t_prep / passes * 1e3, 2),
+                         'device_pass_and_d2h': round(t_dev / passes * 1e3, 2)},
+            'hits_returned': int(ro_h[-1]),
+            'note': 'requests as numpy columns in host memory -> rows + row offsets + dense hit lists in pinned host '
+                    'memory; routing, planning, upload, the pass and both D2H copies inside the timed region'}
 
 
 def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20000, seed=7):

@@ -85,6 +85,18 @@ int sb_builder_add_file(sb_builder *b, uint32_t vcf_id, const char *path);
  * (search_variants.py:45). */
 int sb_builder_attach_carriers(sb_builder *b, uint32_t vcf_id, const char *const *names, const uint32_t *name_len,
                                uint32_t n_samples, const uint64_t *planes, uint64_t n_rows);
+/* Shard builds (one rank's part of a VCF, sbeacon/sharding.py): keep only
+ * records [lo, hi) of the file (0-based, file order); call before any text
+ * of that VCF. */
+int sb_builder_set_record_range(sb_builder *b, uint32_t vcf_id, uint64_t lo, uint64_t hi);
+/* CHROM / POS of every record of a VCF file (plain, gzip or BGZF) without
+ * building a store: the input of a shard plan.  Contigs in file order with
+ * their record ranges [lo, hi); pos[r] = POS of record r. */
+typedef struct sb_vcf_scan sb_vcf_scan;
+int sb_vcf_scan_file(const char *path, sb_vcf_scan **out);
+int sb_vcf_scan_info(const sb_vcf_scan *s, uint64_t *n_records, uint32_t *n_contigs, const uint32_t **pos);
+int sb_vcf_scan_contig(const sb_vcf_scan *s, uint32_t i, const char **name, size_t *len, uint64_t *lo, uint64_t *hi);
+void sb_vcf_scan_free(sb_vcf_scan *s);
 /* upload to device `device` (HIP ordinal) and return an immutable store */
 int sb_builder_finish(sb_builder *b, int device, sb_store **out);
 void sb_builder_free(sb_builder *b);

@@ -32,6 +32,7 @@ namespace sb {
 void builder_add_text(sb_builder &b, uint32_t vcf_id, const char *text, size_t len);
 void builder_add_file(sb_builder &b, uint32_t vcf_id, const char *path);
 void builder_flush(sb_builder &b, uint32_t vcf_id);
+void vcf_scan_file(const char *path, VcfScan &out);
 void builder_attach_carriers(sb_builder &b, uint32_t vcf_id, const char *const *names, const uint32_t *name_len,
                              uint32_t n_samples, const uint64_t *planes, uint64_t n_rows);
 
@@ -2599,6 +2600,51 @@ int sb_builder_add_file(sb_builder *b, uint32_t vcf_id, const char *path) {
     return guard([&] {
         if (!b || !path) throw Error(SB_EINVAL, "NULL argument");
         builder_add_file(*b, vcf_id, path);
+    });
+}
+
+struct sb_vcf_scan {
+    VcfScan s;
+};
+
+int sb_vcf_scan_file(const char *path, sb_vcf_scan **out) {
+    return guard([&] {
+        if (!path || !out) throw Error(SB_EINVAL, "NULL argument");
+        auto r = std::make_unique<sb_vcf_scan>();
+        vcf_scan_file(path, r->s);
+        *out = r.release();
+    });
+}
+
+int sb_vcf_scan_info(const sb_vcf_scan *s, uint64_t *n_records, uint32_t *n_contigs, const uint32_t **pos) {
+    if (!s || !n_records || !n_contigs || !pos) return SB_EINVAL;
+    *n_records = s->s.pos.size();
+    *n_contigs = static_cast<uint32_t>(s->s.contigs.size());
+    *pos = s->s.pos.data();
+    return SB_OK;
+}
+
+int sb_vcf_scan_contig(const sb_vcf_scan *s, uint32_t i, const char **name, size_t *len, uint64_t *lo, uint64_t *hi) {
+    if (!s || !name || !len || !lo || !hi || i >= s->s.contigs.size()) return SB_EINVAL;
+    const auto &c = s->s.contigs[i];
+    *name = c.name.data();
+    *len = c.name.size();
+    *lo = c.lo;
+    *hi = c.hi;
+    return SB_OK;
+}
+
+void sb_vcf_scan_free(sb_vcf_scan *s) { delete s; }
+
+int sb_builder_set_record_range(sb_builder *b, uint32_t vcf_id, uint64_t lo, uint64_t hi) {
+    return guard([&] {
+        if (!b) throw Error(SB_EINVAL, "NULL builder");
+        if (vcf_id >= b->vcfs.size()) throw Error(SB_ENOSTORE, "unknown vcf id");
+        VcfData &v = b->vcfs[vcf_id];
+        if (v.lines_seen || v.stream_off) throw Error(SB_EINVAL, "set the record range before adding text");
+        if (lo > hi) throw Error(SB_EINVAL, "record range lo > hi");
+        v.rec_lo = lo;
+        v.rec_hi = hi;
     });
 }
 

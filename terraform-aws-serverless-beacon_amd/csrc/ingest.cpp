@@ -875,6 +875,17 @@ void parse_records(sb_builder &b, VcfData &v, const char *p, size_t len, uint64_
     for (const char *s : starts)
         if (*s == '#') throw Error(SB_EPARSE, "header line after records");
     if (!v.header_seen) throw Error(SB_EPARSE, "records before the #CHROM header line");
+    {  // a shard build keeps the records [rec_lo, rec_hi) of the file
+        const uint64_t o0 = v.lines_seen;
+        v.lines_seen += starts.size();
+        if (v.rec_lo > o0 || v.rec_hi < v.lines_seen) {
+            const uint64_t a = std::min<uint64_t>(std::max(v.rec_lo, o0) - o0, starts.size());
+            const uint64_t b = std::max<uint64_t>(std::min(v.rec_hi, v.lines_seen), o0 + a) - o0;
+            starts = std::vector<const char *>(starts.begin() + static_cast<std::ptrdiff_t>(a),
+                                               starts.begin() + static_cast<std::ptrdiff_t>(std::min<uint64_t>(b, starts.size())));
+            if (starts.empty()) return;
+        }
+    }
     const size_t nl = starts.size();
     unsigned nt = b.opts.n_threads > 0 ? static_cast<unsigned>(b.opts.n_threads) : std::thread::hardware_concurrency();
     nt = std::max(1u, std::min<unsigned>(nt, static_cast<unsigned>((nl + 4095) / 4096)));
@@ -968,15 +979,14 @@ void builder_flush(sb_builder &b, uint32_t vcf_id) {
     }
 }
 
-// BGZF ingest: block table for virtual offsets, blocks inflated in parallel
-// in ~64 MiB batches that are fed to the text parser in order.
-void add_bgzf(sb_builder &b, VcfData &v, const std::vector<uint8_t> &c, const char *path) {
-    if (v.stream_off != 0 || !v.carry.empty()) throw Error(SB_EINVAL, "a BGZF file must be the only text source of its VCF");
-    struct Blk {
-        size_t coff, bsize;
-        uint32_t isize;
-        uint64_t ustart;
-    };
+// BGZF blocks of a file image: (compressed offset, size, uncompressed size, uncompressed start)
+struct Blk {
+    size_t coff, bsize;
+    uint32_t isize;
+    uint64_t ustart;
+};
+
+std::vector<Blk> bgzf_blocks(const std::vector<uint8_t> &c, const char *path) {
     std::vector<Blk> blks;
     uint64_t u = 0;
     for (size_t p = 0; p < c.size();) {
@@ -986,14 +996,16 @@ void add_bgzf(sb_builder &b, VcfData &v, const std::vector<uint8_t> &c, const ch
         const uint8_t *t = c.data() + p + bs - 4;
         const uint32_t is = t[0] | (t[1] << 8) | (t[2] << 16) | (static_cast<uint32_t>(t[3]) << 24);
         blks.push_back(Blk{p, bs, is, u});
-        v.blk_coff.push_back(p);
-        v.blk_ustart.push_back(u);
         u += is;
         p += bs;
     }
-    v.stream_len = u;
-    const unsigned nt = std::max(1u, std::min(16u, b.opts.n_threads > 0 ? static_cast<unsigned>(b.opts.n_threads)
-                                                                          : std::thread::hardware_concurrency()));
+    return blks;
+}
+
+// blocks inflated in parallel (nt threads) in ~64 MiB batches, handed to
+// `feed` in file order
+template <class F>
+void bgzf_inflate(const std::vector<uint8_t> &c, const std::vector<Blk> &blks, const char *path, unsigned nt, F feed) {
     std::vector<char> buf;
     for (size_t i = 0; i < blks.size();) {
         size_t j = i;
@@ -1025,8 +1037,112 @@ void add_bgzf(sb_builder &b, VcfData &v, const std::vector<uint8_t> &c, const ch
         for (unsigned t = 0; t < nt; ++t) th.emplace_back(work);
         for (auto &t : th) t.join();
         if (bad) throw Error(SB_EIO, std::string("BGZF inflate failed in ") + path);
-        add_text(b, v, buf.data(), buf.size());
+        feed(buf.data(), buf.size());
         i = j;
+    }
+}
+
+// BGZF ingest: block table for virtual offsets, blocks inflated in parallel
+// in ~64 MiB batches that are fed to the text parser in order.
+void add_bgzf(sb_builder &b, VcfData &v, const std::vector<uint8_t> &c, const char *path) {
+    if (v.stream_off != 0 || !v.carry.empty()) throw Error(SB_EINVAL, "a BGZF file must be the only text source of its VCF");
+    const std::vector<Blk> blks = bgzf_blocks(c, path);
+    for (const Blk &bk : blks) {
+        v.blk_coff.push_back(bk.coff);
+        v.blk_ustart.push_back(bk.ustart);
+    }
+    v.stream_len = blks.empty() ? 0 : blks.back().ustart + blks.back().isize;
+    const unsigned nt = std::max(1u, std::min(16u, b.opts.n_threads > 0 ? static_cast<unsigned>(b.opts.n_threads)
+                                                                          : std::thread::hardware_concurrency()));
+    bgzf_inflate(c, blks, path, nt, [&](const char *t, size_t n) { add_text(b, v, t, n); });
+}
+
+// the text of a plain, gzip or BGZF file, in order, in chunks
+template <class F>
+void read_vcf_file(const char *path, unsigned nt, F feed) {
+    FILE *fp = fopen(path, "rb");
+    if (!fp) throw Error(SB_EIO, std::string("cannot open ") + path);
+    uint8_t hdr[18];
+    const size_t got = fread(hdr, 1, sizeof hdr, fp);
+    size_t bs;
+    if (got == sizeof hdr && bgzf_block_size(hdr, got, &bs)) {
+        fseek(fp, 0, SEEK_END);
+        const long n = ftell(fp);
+        fseek(fp, 0, SEEK_SET);
+        std::vector<uint8_t> c(static_cast<size_t>(n));
+        const size_t rd = fread(c.data(), 1, c.size(), fp);
+        fclose(fp);
+        if (rd != c.size()) throw Error(SB_EIO, std::string("short read: ") + path);
+        bgzf_inflate(c, bgzf_blocks(c, path), path, nt, feed);
+        return;
+    }
+    fclose(fp);
+    gzFile f = gzopen(path, "rb");
+    if (!f) throw Error(SB_EIO, std::string("cannot open ") + path);
+    gzbuffer(f, 1 << 20);
+    const size_t chunk = size_t(64) << 20;
+    std::vector<char> buf(chunk);
+    for (;;) {
+        const int r = gzread(f, buf.data(), static_cast<unsigned>(chunk));
+        if (r < 0) {
+            gzclose(f);
+            throw Error(SB_EIO, std::string("decompression failed: ") + path);
+        }
+        if (r == 0) break;
+        feed(buf.data(), static_cast<size_t>(r));
+    }
+    gzclose(f);
+}
+
+// CHROM / POS of every record of a VCF file (shard planning): contigs in
+// file order with their record ranges, POS per record.  Text from the same
+// readers as the builder (BGZF in parallel, gzip, plain).
+struct ScanState {
+    std::string carry;
+    VcfScan *out;
+    void feed(const char *t, size_t n) {
+        std::string joined;
+        if (!carry.empty()) {
+            joined = carry;
+            joined.append(t, n);
+            carry.clear();
+            t = joined.data();
+            n = joined.size();
+        }
+        size_t upto = n;
+        while (upto > 0 && t[upto - 1] != '\n') --upto;
+        if (upto < n) carry.assign(t + upto, n - upto);
+        line_loop(t, upto);
+    }
+    void line_loop(const char *p, size_t n) {
+        const char *e = p + n;
+        while (p < e) {
+            const char *nl = static_cast<const char *>(memchr(p, '\n', static_cast<size_t>(e - p)));
+            if (!nl) nl = e;
+            if (nl > p && *p != '#' && !(nl - p == 1 && *p == '\r')) {
+                const char *t = static_cast<const char *>(memchr(p, '\t', static_cast<size_t>(nl - p)));
+                if (!t) throw Error(SB_EPARSE, "record without a tab");
+                const std::string chrom(p, static_cast<size_t>(t - p));
+                uint64_t pos = 0;
+                for (const char *q = t + 1; q < nl && is_digit(*q); ++q) pos = pos * 10 + static_cast<uint64_t>(*q - '0');
+                if (pos > 0xffffffffull) throw Error(SB_EPARSE, "POS beyond 32 bits");
+                const uint64_t r = out->pos.size();
+                if (out->contigs.empty() || out->contigs.back().name != chrom)
+                    out->contigs.push_back(VcfScan::Contig{chrom, r, r});
+                out->pos.push_back(static_cast<uint32_t>(pos));
+                out->contigs.back().hi = r + 1;
+            }
+            p = nl + 1;
+        }
+    }
+};
+
+void vcf_scan_file(const char *path, VcfScan &out) {
+    ScanState st{{}, &out};
+    read_vcf_file(path, 16, [&](const char *t, size_t n) { st.feed(t, n); });
+    if (!st.carry.empty()) {
+        st.carry.push_back('\n');
+        st.line_loop(st.carry.data(), st.carry.size());
     }
 }
 

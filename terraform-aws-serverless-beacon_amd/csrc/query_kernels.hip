@@ -2133,7 +2133,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         uint64_t excl = 0;
         for (int64_t j = static_cast<int64_t>(w) - 1; j >= 0; --j) {
             unsigned long long sj;
-            while (((sj = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0)
+            uint32_t spins = 0;  // bounded: a predecessor takes microseconds; never hang the queue
+            while (((sj = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0 &&
+                   ++spins < (1u << 24))
                 __builtin_amdgcn_s_sleep(1);
             excl += sj & kVal;
             if ((sj >> 62) == 2) break;

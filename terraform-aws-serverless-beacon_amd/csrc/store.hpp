@@ -81,6 +81,8 @@ struct VcIndex {
 
 struct VcfData {
     std::string location;
+    // shard builds (sb_builder_set_record_range): keep records [rec_lo, rec_hi) of the file
+    uint64_t rec_lo = 0, rec_hi = UINT64_MAX, lines_seen = 0;
     std::vector<std::string> samples;
     // name -> header indices (built at upload; bcftools --samples lookups)
     std::unordered_map<std::string, std::vector<uint32_t>> sample_pos;
@@ -105,6 +107,16 @@ struct VcfData {
     // RangeHot8 usable (>= 98 % of the single-base-ALT records fit it), AN value
     bool range8 = false;
     int32_t an_default = 0;
+};
+
+// CHROM / POS of a VCF's records without a store (shard planning)
+struct VcfScan {
+    struct Contig {
+        std::string name;
+        uint64_t lo, hi;  // records [lo, hi) in file order
+    };
+    std::vector<Contig> contigs;
+    std::vector<uint32_t> pos;
 };
 
 struct Dict {

@@ -184,6 +184,12 @@ SIGNATURES = {
     'sb_free': (None, [P]),
     'sb_result_distinct_variants': (C.c_int, [P, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_void_p),
                                               C.POINTER(C.c_size_t), C.POINTER(C.c_uint64)]),
+    'sb_builder_set_record_range': (C.c_int, [P, C.c_uint32, C.c_uint64, C.c_uint64]),
+    'sb_vcf_scan_file': (C.c_int, [C.c_char_p, C.POINTER(P)]),
+    'sb_vcf_scan_info': (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint32), C.POINTER(C.c_void_p)]),
+    'sb_vcf_scan_contig': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_char_p), C.POINTER(C.c_size_t),
+                                     C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    'sb_vcf_scan_free': (None, [P]),
     'sb_requests_prepare': (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(P)]),
     'sb_requests_run': (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
 }

@@ -157,21 +157,28 @@ class ResultExchange:
         self.recv_hits = [None] * len(self.recvs)
         self.recv_hits_n = {}
         self._my_hits = None
+        self._allc = None  # hit ranges [src, dst, (start, n)], fixed per batch (exchange)
 
     def exchange(self, part, hits, row_off):
-        """part: [n_rows, 5] rows; hits / row_off: sb_batch_compact_hits output
-        (int64 tensors on the device, ``row_off`` n_rows + 1)."""
+        """part: [n_rows, 5] rows; hits / row_off: sb_batch_compact_hits /
+        sb_requests_run output (int64 tensors on the device, ``row_off``
+        n_rows + 1) of ONE batch (its hit counts are fixed: see below)."""
         import torch
         dist = self.dist
         if self.world > 1:
-            # this step's hit range per destination: (first dense hit, count)
-            cnt = torch.zeros((self.world, 2), dtype=torch.int64, device=self.device)
-            for d, a, b in self.sends:
-                cnt[d, 0] = row_off[a]
-                cnt[d, 1] = row_off[b] - row_off[a]
-            allc = [torch.zeros_like(cnt) for _ in range(self.world)]
-            dist.all_gather(allc, cnt)
-            allc = torch.stack(allc).cpu()  # [src, dst, (start, n)]
+            # hit range per destination: (first dense hit, count).  A batch's
+            # rows and hit counts are the same on every pass, so the sizes are
+            # gathered once (one host sync, first exchange) and reused: later
+            # steps enqueue RCCL send/recv only, with no host round trip
+            if self._allc is None:
+                cnt = torch.zeros((self.world, 2), dtype=torch.int64, device=self.device)
+                for d, a, b in self.sends:
+                    cnt[d, 0] = row_off[a]
+                    cnt[d, 1] = row_off[b] - row_off[a]
+                allc = [torch.zeros_like(cnt) for _ in range(self.world)]
+                dist.all_gather(allc, cnt)
+                self._allc = torch.stack(allc).cpu()  # [src, dst, (start, n)]
+            allc = self._allc
             ops = []
             for d, a, b in self.sends:
                 st, n = int(allc[self.rank, d, 0]), int(allc[self.rank, d, 1])
