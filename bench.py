@@ -49,7 +49,7 @@ def parse():
     ap.add_argument('--threads', type=int, default=16, help='host ingest / CPU-baseline threads')
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='target CPU-baseline sample duration')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--parity-requests', type=int, default=300,
+    ap.add_argument('--parity-requests', type=int, default=2000,
                     help='requests re-checked against the C oracle after timing (rank 0)')
     ap.add_argument('--workload', choices=['chr22', 'genome', 'gnomad'], default='genome',
                     help='genome: config 3 (default; whole-genome store sharded by contig across the GPUs, '

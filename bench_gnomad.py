@@ -92,9 +92,20 @@ def main_gnomad(args):
     samp_idx = np.flatnonzero(sl.kind == 1)
     samp_hits = int(sum(rs.view(int(j)).n_variants for j in samp_idx))
     words = (shape.n_samples + 63) // 64
-    # algorithmic bytes: 32 B/row scanned + 8 B/hit + one carrier
-    # row (words x 8 B) per hit ALT of a sample-subset query
-    alg = 32.0 * scanned + 8.0 * hits + 8.0 * words * samp_hits
+    # rows inside the slices, per kind (host count over the generator's POS)
+    rows_kind = [0, 0]
+    for ci in np.unique(sl.ci).tolist():
+        pos = shape.gen(int(ci)).positions()
+        m = sl.ci == ci
+        n_in = np.searchsorted(pos, sl.b[m], side='right') - np.searchsorted(pos, sl.a[m], side='left')
+        for k in (0, 1):
+            rows_kind[k] += int(n_in[sl.kind[m] == k].sum())
+    # algorithmic bytes = what the kernels must read at least once: the 8 B
+    # RangeHot8 word per aggregation row, the 16 B RecHot word per sample-path
+    # row, one carrier row (words x 8 B) per hit ALT of a sample-subset query,
+    # 8 B per hit written.  SURVEY §8d's 32 B/row contract is reported beside it.
+    alg = 8.0 * rows_kind[0] + 16.0 * rows_kind[1] + 8.0 * words * samp_hits + 8.0 * hits
+    contract = 32.0 * scanned + 8.0 * hits + 8.0 * words * samp_hits
     achieved = alg / (timing['scan_ms'] * 1e-3) / 1e9 if timing['scan_ms'] > 0 else 0.0
     traffic = None  # HBM bytes per step from the PMC passes (tools/gpu_pmc_gnomad.sh)
     tf = os.path.join(REPO, 'profiles', 'traffic_gnomad.json')
@@ -106,7 +117,7 @@ def main_gnomad(args):
         except Exception:
             traffic = None
     vals = [elapsed, timing['scan_ms'], float(sl.n_requests), float(len(sl)), float(scanned), float(hits),
-            achieved, alg, float(samp_hits)]
+            achieved, alg, float(samp_hits), contract]
     if dist:
         t = torch.tensor(vals, dtype=torch.float64, device='cuda')
         allv = [torch.zeros_like(t) for _ in range(world)]
@@ -146,9 +157,14 @@ def main_gnomad(args):
                                'query_kernels_max': round(max(v[1] for v in allv), 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(allv[0][6], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(allv[0][6] / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                     'kernel': 'rank 0 query step (range_n + sample-path scan launches); HIP events spanning the step',
+                     'kernel': 'rank 0 query step (range_n + sample-path scan launches); HIP events spanning the step (not a rocprof average)',
                      'algorithmic_bytes_per_launch': allv[0][7],
-                     'note': f'32 B/row scanned + 8 B/hit + {8 * words} B carrier row per sample-path hit ALT'},
+                     'pricing': f'8 B/aggregation row (RangeHot8) + 16 B/sample-path row (RecHot) + {8 * words} B '
+                                f'carrier row per sample-path hit ALT + 8 B/hit written',
+                     'rows_in_slices': {'aggregation': rows_kind[0], 'sample_subset': rows_kind[1]},
+                     'contract_bytes_per_launch': allv[0][9],
+                     'contract_note': 'SURVEY 8d prices 32 B per row scanned; the packed words are 8-16 B, so that '
+                                      'figure is rows covered, not bytes moved'},
         'cpu_baseline': cpu,
         'parity_sample': parity,
         'ingest_s': round(t_ingest, 2),
@@ -185,7 +201,7 @@ def _write_vcf(path, shape, sl, idx, sites_only, threads):
                     cur = hi
 
 
-def cpu_baseline_and_parity(args, shape, sl, subsets, rs, n_agg=2000, n_samp=48, seed=9):
+def cpu_baseline_and_parity(args, shape, sl, subsets, rs, n_agg=2000, n_samp=1000, seed=9):
     """C oracle (OpenMP) on samples of both request kinds: aggregation slices
     over a sites-only VCF, sample-subset slices over a VCF with the 2,504 GT
     columns (the oracle's regex-equivalent token match per sample, :233-236).

@@ -383,6 +383,41 @@ typedef struct {
 /* Plan and upload a request batch (sb_batch_free releases it); its
  * sb_batch_get_stats().hits is the output capacity (hits). */
 int sb_requests_prepare(sb_store *s, const sb_request *r, size_t n, sb_batch **out);
+
+/* The same requests as columns -- no per-request struct, no per-request
+ * string: what a batched caller holds (numpy columns, a parsed event
+ * batch).  A numeric / flag column is an array of n values, or NULL to give
+ * every request the `*_all` scalar after it.  A string column is a
+ * dictionary of distinct values (sb_str, p == NULL = None) and a uint32 code
+ * per request into it (codes NULL = every request takes dict[0]); a NULL
+ * dictionary = None for every request.  start_min / start_max are required.
+ * Replaces the per-SplitQueryPayload fan-out of split_query_sync
+ * (lambda/splitQuery/lambda_function.py:74-110) for a whole batch. */
+typedef struct {
+    const char *p;
+    size_t len;
+} sb_str;
+
+typedef struct {
+    const uint32_t *vcf_id;  uint32_t vcf_id_all;
+    const uint32_t *contig;  uint32_t contig_all;
+    const int64_t *start_min, *start_max;
+    const int64_t *end_min;  int64_t end_min_all;
+    const int64_t *end_max;  int64_t end_max_all;
+    const int64_t *variant_min_length;  int64_t variant_min_length_all;
+    const int64_t *variant_max_length;  int64_t variant_max_length_all;
+    const sb_str *reference_dict;    const uint32_t *reference_code;    uint32_t n_reference;
+    const sb_str *alternate_dict;    const uint32_t *alternate_code;    uint32_t n_alternate;
+    const sb_str *variant_type_dict; const uint32_t *variant_type_code; uint32_t n_variant_type;
+    const sb_str *sample_names_dict; const uint32_t *sample_names_code; uint32_t n_sample_names;
+    const uint8_t *granularity;           uint8_t granularity_all;
+    const uint8_t *include_details;       uint8_t include_details_all;
+    const uint8_t *include_samples;       uint8_t include_samples_all;
+    const uint8_t *selected_samples_only; uint8_t selected_samples_only_all;
+    uint8_t strict_variant_type;
+} sb_request_columns;
+
+int sb_requests_prepare_columns(sb_store *s, const sb_request_columns *c, size_t n, sb_batch **out);
 /* Enqueue one pass: answer every request, then write dev_rows[n]
  * (sb_request_partial), dev_row_off[n + 1] and the rows' hit lists densely
  * in request order: row w's hits ((record + rec_base) | alt << 32, the

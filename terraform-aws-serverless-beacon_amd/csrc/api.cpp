@@ -2735,65 +2735,173 @@ constexpr int64_t kSplitSize = 10000;  // lambda/splitQuery/lambda_function.py:1
 // lambda/splitQuery/lambda_function.py:74-110) and answered per slice by the
 // query kernels (the batch's query part), its row reduced and gathered by
 // request_reduce + request_rows_kernel.
-void prepare_requests(sb_batch &B, const sb_request *rq, size_t n) {
-    sb_store &s = *B.s;
-    if (n >= (1u << 31)) throw Error(SB_EINVAL, "too many requests");
-    auto R = std::make_unique<sb_batch::Req>();
-    R->n_rows = static_cast<uint32_t>(n);
-    // variantType strings: a handful of distinct values (pointer cache, then by value)
+extern "C++" {  // overloads and templates inside the extern "C" block
+
+// Request sources: the sb_request array, or the same requests as columns
+// (sb_request_columns: numeric arrays or scalars, string columns as a
+// dictionary + a code per request).  src(i) is request i as an sb_request.
+struct AosSrc {
+    const sb_request *rq;
+    sb_request operator()(size_t i) const { return rq[i]; }
+};
+
+struct ColSrc {
+    const sb_request_columns &c;
+    static sb_str pick(const sb_str *dict, const uint32_t *code, size_t i) {
+        return dict ? dict[code ? code[i] : 0u] : sb_str{nullptr, 0};
+    }
+    sb_request operator()(size_t i) const {
+        sb_request r{};
+        r.vcf_id = c.vcf_id ? c.vcf_id[i] : c.vcf_id_all;
+        r.contig = c.contig ? c.contig[i] : c.contig_all;
+        r.start_min = c.start_min[i];
+        r.start_max = c.start_max[i];
+        r.end_min = c.end_min ? c.end_min[i] : c.end_min_all;
+        r.end_max = c.end_max ? c.end_max[i] : c.end_max_all;
+        const sb_str ref = pick(c.reference_dict, c.reference_code, i), alt = pick(c.alternate_dict, c.alternate_code, i),
+                     vt = pick(c.variant_type_dict, c.variant_type_code, i),
+                     sn = pick(c.sample_names_dict, c.sample_names_code, i);
+        r.reference_bases = ref.p;
+        r.reference_len = ref.len;
+        r.alternate_bases = alt.p;
+        r.alternate_len = alt.len;
+        r.variant_type = vt.p;
+        r.variant_type_len = vt.len;
+        r.variant_min_length = c.variant_min_length ? c.variant_min_length[i] : c.variant_min_length_all;
+        r.variant_max_length = c.variant_max_length ? c.variant_max_length[i] : c.variant_max_length_all;
+        r.granularity = c.granularity ? c.granularity[i] : c.granularity_all;
+        r.include_details = c.include_details ? c.include_details[i] : c.include_details_all;
+        r.include_samples = c.include_samples ? c.include_samples[i] : c.include_samples_all;
+        r.selected_samples_only = c.selected_samples_only ? c.selected_samples_only[i] : c.selected_samples_only_all;
+        r.strict_variant_type = c.strict_variant_type;
+        r.sample_names = sn.p;
+        r.sample_names_len = sn.len;
+        return r;
+    }
+};
+
+// variantType strings -> (kind, symbolic-ALT LUT offset), each distinct value once
+struct VtResolver {
+    sb_store &s;
+    std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> map;
+    std::vector<uint32_t> lut_all;
+    std::pair<uint32_t, uint32_t> get(const char *p, size_t len) {
+        const std::string vt = p ? std::string(p, len) : std::string("None");
+        auto it = map.find(vt);
+        if (it == map.end()) {
+            const uint32_t kind = !p                    ? VT_OTHER
+                                  : vt == "DEL"        ? VT_DEL
+                                  : vt == "INS"        ? VT_INS
+                                  : vt == "DUP"        ? VT_DUP
+                                  : vt == "DUP:TANDEM" ? VT_DUPT
+                                  : vt == "CNV"        ? VT_CNV
+                                                       : VT_OTHER;
+            const auto lut = sym_lut(s, kind, "<" + vt);
+            const uint32_t off = static_cast<uint32_t>(lut_all.size());
+            lut_all.insert(lut_all.end(), lut.begin(), lut.end());
+            it = map.emplace(vt, std::make_pair(kind, off)).first;
+        }
+        return it->second;
+    }
+};
+
+// a handful of distinct values in practice: a pointer cache in front of the map
+void resolve_vtypes(VtResolver &V, const AosSrc &src, size_t n, std::vector<uint32_t> &vt_of,
+                    std::vector<uint32_t> &lut_of) {
     struct VtEnt {
         const char *p;
         size_t len;
         uint32_t kind, lut;
     };
-    std::vector<VtEnt> vt_seen;
-    std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> vt_map;
-    std::vector<uint32_t> lut_all;
-    std::vector<uint32_t> vt_of(n, 0u), lut_of(n, 0u);
+    std::vector<VtEnt> seen;
     for (size_t i = 0; i < n; ++i) {
-        const sb_request &x = rq[i];
+        const sb_request &x = src.rq[i];
         if (x.alternate_bases) continue;
         const VtEnt *hit = nullptr;
-        for (const VtEnt &e : vt_seen)
+        for (const VtEnt &e : seen)
             if (e.p == x.variant_type && e.len == x.variant_type_len) {
                 hit = &e;
                 break;
             }
         if (!hit) {
-            const std::string vt = x.variant_type ? std::string(x.variant_type, x.variant_type_len) : std::string("None");
-            auto it = vt_map.find(vt);
-            if (it == vt_map.end()) {
-                const uint32_t kind = !x.variant_type ? VT_OTHER
-                                      : vt == "DEL"        ? VT_DEL
-                                      : vt == "INS"        ? VT_INS
-                                      : vt == "DUP"        ? VT_DUP
-                                      : vt == "DUP:TANDEM" ? VT_DUPT
-                                      : vt == "CNV"        ? VT_CNV
-                                                           : VT_OTHER;
-                const auto lut = sym_lut(s, kind, "<" + vt);
-                const uint32_t off = static_cast<uint32_t>(lut_all.size());
-                lut_all.insert(lut_all.end(), lut.begin(), lut.end());
-                it = vt_map.emplace(vt, std::make_pair(kind, off)).first;
-            }
-            if (vt_seen.size() < 16) vt_seen.push_back(VtEnt{x.variant_type, x.variant_type_len, it->second.first,
-                                                             it->second.second});
-            vt_of[i] = it->second.first;
-            lut_of[i] = it->second.second;
+            const auto kl = V.get(x.variant_type, x.variant_type_len);
+            if (seen.size() < 16) seen.push_back(VtEnt{x.variant_type, x.variant_type_len, kl.first, kl.second});
+            vt_of[i] = kl.first;
+            lut_of[i] = kl.second;
         } else {
             vt_of[i] = hit->kind;
             lut_of[i] = hit->lut;
         }
     }
+}
+
+// columns: per dictionary entry, then a table lookup per request
+void resolve_vtypes(VtResolver &V, const ColSrc &src, size_t n, std::vector<uint32_t> &vt_of,
+                    std::vector<uint32_t> &lut_of) {
+    const sb_request_columns &c = src.c;
+    std::vector<std::pair<uint32_t, uint32_t>> tab;
+    if (c.variant_type_dict)
+        for (uint32_t d = 0; d < c.n_variant_type; ++d) tab.push_back(V.get(c.variant_type_dict[d].p, c.variant_type_dict[d].len));
+    else
+        tab.push_back(V.get(nullptr, 0));
+    parallel_for(n, [&](size_t i) {
+        const auto &kl = tab[c.variant_type_dict && c.variant_type_code ? c.variant_type_code[i] : 0u];
+        vt_of[i] = kl.first;
+        lut_of[i] = kl.second;
+    });
+}
+
+void check_columns(const sb_request_columns &c, size_t n) {
+    if (n && (!c.start_min || !c.start_max)) throw Error(SB_EINVAL, "start_min / start_max columns are required");
+    auto codes = [&](const char *what, const sb_str *dict, const uint32_t *code, uint32_t nd) {
+        if (!dict) {
+            if (code) throw Error(SB_EINVAL, std::string(what) + ": codes without a dictionary");
+            return;
+        }
+        if (!nd) throw Error(SB_EINVAL, std::string(what) + ": empty dictionary");
+        for (uint32_t d = 0; d < nd; ++d)
+            if (!dict[d].p && dict[d].len) throw Error(SB_EINVAL, std::string(what) + ": NULL string with a length");
+        if (code)
+            for (size_t i = 0; i < n; ++i)
+                if (code[i] >= nd) throw Error(SB_EINVAL, std::string(what) + ": code out of range at request " + std::to_string(i));
+    };
+    codes("reference_bases", c.reference_dict, c.reference_code, c.n_reference);
+    codes("alternate_bases", c.alternate_dict, c.alternate_code, c.n_alternate);
+    codes("variant_type", c.variant_type_dict, c.variant_type_code, c.n_variant_type);
+    codes("sample_names", c.sample_names_dict, c.sample_names_code, c.n_sample_names);
+}
+
+template <class Src>
+void prepare_requests(sb_batch &B, const Src &src, size_t n) {
+    sb_store &s = *B.s;
+    if (n >= (1u << 31)) throw Error(SB_EINVAL, "too many requests");
+    auto R = std::make_unique<sb_batch::Req>();
+    R->n_rows = static_cast<uint32_t>(n);
+    // SBEACON_PREP_TRACE=1: host phase times to stderr (bench diagnostics)
+    const bool trace = std::getenv("SBEACON_PREP_TRACE") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto tick = [&](const char *what) {
+        if (!trace) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[prep] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
+    // variantType strings -> kind + LUT
+    VtResolver V{s, {}, {}};
+    std::vector<uint32_t> vt_of(n, 0u), lut_of(n, 0u);
+    resolve_vtypes(V, src, n, vt_of, lut_of);
+    std::vector<uint32_t> &lut_all = V.lut_all;
     lut_all.insert(lut_all.end(), 8, 0u);
+    tick("vtypes");
     // classify: 0 = no slices, 1 = one chain, 2 = per slice
     std::vector<uint8_t> cls(n, 0);
     for (size_t i = 0; i < n; ++i) {
-        const sb_request &x = rq[i];
+        const sb_request x = src(i);
         if (x.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "request " + std::to_string(i) + ": unknown vcf id");
         if (!x.reference_bases && x.reference_len) throw Error(SB_EINVAL, "request " + std::to_string(i) + ": bad REF");
     }
     parallel_for(n, [&](size_t i) {
-        const sb_request &x = rq[i];
+        const sb_request x = src(i);
         const VcfData &v = s.vcfs[x.vcf_id];
         if (x.contig >= v.segments.size() || x.start_min > x.start_max) return;  // bcftools emits nothing / no slice
         const int64_t nsl = (x.start_max - x.start_min) / kSplitSize + 1;
@@ -2810,6 +2918,7 @@ void prepare_requests(sb_batch &B, const sb_request *rq, size_t n) {
         }
         cls[i] = chain ? 1 : 2;
     });
+    tick("classify");
     // chains in row order
     std::vector<uint32_t> chain_of(n, UINT32_MAX);
     uint32_t nc = 0;
@@ -2819,7 +2928,7 @@ void prepare_requests(sb_batch &B, const sb_request *rq, size_t n) {
     std::vector<uint64_t> ccap(nc, 0);
     parallel_for(n, [&](size_t i) {
         if (cls[i] != 1) return;
-        const sb_request &x = rq[i];
+        const sb_request x = src(i);
         const VcIndex &vi = s.vcfs[x.vcf_id].vc_index[x.contig][vt_of[i]];
         ChainDev &cd = R->chains[chain_of[i]];
         cd = ChainDev{};
@@ -2855,13 +2964,14 @@ void prepare_requests(sb_batch &B, const sb_request *rq, size_t n) {
         ccap[chain_of[i]] = s.h_vc_altpre[C1] - s.h_vc_altpre[C0];
     });
     for (const ChainDev &c : R->chains) R->n_chain_slices += c.n;
+    tick("chains");
     // the per-slice part: splitQuery's slices of the other requests, in row order
     std::vector<sb_query> qs;
     std::vector<uint32_t> owner;
     std::deque<std::string> regions;  // stable storage for the region strings
     for (size_t i = 0; i < n; ++i) {
         if (cls[i] != 2) continue;
-        const sb_request &x = rq[i];
+        const sb_request x = src(i);
         const std::string &chrom = s.vcfs[x.vcf_id].segments[x.contig].contig;
         for (int64_t a = x.start_min; a <= x.start_max; a += kSplitSize) {
             const int64_t b = std::min(a + kSplitSize - 1, x.start_max);
@@ -2897,6 +3007,7 @@ void prepare_requests(sb_batch &B, const sb_request *rq, size_t n) {
         prepare(B, qs.data(), qs.size());
         R->slices = true;
     }
+    tick("slices");
     // rows -> their per-slice queries, host errors
     std::vector<uint32_t> seg(n + 1, 0);
     for (uint32_t o : owner) ++seg[o + 1];
@@ -2932,6 +3043,7 @@ void prepare_requests(sb_batch &B, const sb_request *rq, size_t n) {
     }
     R->cap = B.cap_total;
     for (uint64_t x : ccap) R->cap += x;
+    tick("runs");
     // device buffers
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
@@ -2956,8 +3068,11 @@ void prepare_requests(sb_batch &B, const sb_request *rq, size_t n) {
         HIP_OK(hipMemcpyAsync(R->sherr.p, he.data(), he.size(), hipMemcpyHostToDevice, st));
     }
     HIP_OK(hipStreamSynchronize(st));
+    tick("upload");
     B.req = std::move(R);
 }
+
+}  // extern "C++"
 
 void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t rec_base) {
     sb_store &s = *B.s;
@@ -2991,7 +3106,21 @@ int sb_requests_prepare(sb_store *s, const sb_request *r, size_t n, sb_batch **o
         std::lock_guard<std::mutex> lk(s->mu);
         auto B = std::make_unique<sb_batch>();
         B->s = s;
-        prepare_requests(*B, r, n);
+        prepare_requests(*B, AosSrc{r}, n);
+        *out = B.release();
+    });
+}
+
+int sb_requests_prepare_columns(sb_store *s, const sb_request_columns *c, size_t n, sb_batch **out) {
+    return guard([&] {
+        if (!s || (!c && n) || !out) throw Error(SB_EINVAL, "NULL argument");
+        static const sb_request_columns kNone{};
+        const sb_request_columns &cc = c ? *c : kNone;
+        check_columns(cc, n);
+        std::lock_guard<std::mutex> lk(s->mu);
+        auto B = std::make_unique<sb_batch>();
+        B->s = s;
+        prepare_requests(*B, ColSrc{cc}, n);
         *out = B.release();
     });
 }

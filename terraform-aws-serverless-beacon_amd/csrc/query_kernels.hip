@@ -1915,6 +1915,44 @@ struct ReqLds {
     unsigned long long hbuf[kRowHitBuf];
 };
 
+// Decoupled look-back over one 64-bit status word per run {flag : 2 | value :
+// 62}: flag 1 = the run's own total, 2 = its inclusive prefix, 0 = not yet
+// published.  A word carries its value, so relaxed agent-scope (sc1) stores and
+// loads are enough -- no release / acquire fences, which on gfx950 are an XCD
+// L2 write-back / an L1 invalidate of microseconds EACH (one per poll made the
+// serial form of this loop ~0.9 us per run).  The wave reads 64 predecessors per
+// round (lane j: run top - j) and stops at the nearest inclusive prefix.  A run
+// only waits on runs with earlier tickets, which are resident: no deadlock.
+// Returns the exclusive prefix (wave-uniform) and publishes excl + H.
+__device__ __forceinline__ uint64_t lookback_exclusive(unsigned long long *__restrict__ status, uint32_t w,
+                                                       uint64_t H) {
+    constexpr unsigned long long kAgg = 1ull << 62, kPre = 2ull << 62, kVal = (1ull << 62) - 1;
+    const uint32_t ul = static_cast<uint32_t>(lane_id());
+    if (ul == 0) __hip_atomic_store(&status[w], kAgg | H, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t excl = 0;
+    int64_t top = static_cast<int64_t>(w) - 1;
+    uint32_t spins = 0;  // bounded: a predecessor takes microseconds; never hang the queue
+    while (top >= 0) {
+        const int64_t j = top - static_cast<int64_t>(ul);
+        const unsigned long long s =
+            j >= 0 ? __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kPre;
+        const uint64_t pre = __ballot((s >> 62) == 2);
+        const uint64_t low = pre & (~pre + 1);                      // the nearest prefix (lowest lane)
+        const uint64_t need = pre ? (low | (low - 1)) : ~0ull;      // lanes up to and including it
+        if (__ballot((s >> 62) == 0) & need) {
+            if (++spins >= (1u << 22)) break;
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        const int64_t v = ((need >> ul) & 1ull) ? static_cast<int64_t>(s & kVal) : 0;
+        excl += static_cast<uint64_t>(rdl64(wave_incl_scan_i64(v), kWave - 1));
+        if (pre) break;
+        top -= kWave;
+    }
+    if (ul == 0) __hip_atomic_store(&status[w], kPre | (excl + H), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return excl;
+}
+
 struct RowChunk {
     ChainChunk x;
     uint32_t k, so;  // the lane's chain and its first slot
@@ -2126,24 +2164,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const uint64_t linc = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(nvr)));
     const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(linc), kWave - 1));
     // ---- decoupled look-back: this run's offset = the hits of every earlier run
-    uint64_t O = 0;
-    if (ul == 0) {
-        constexpr unsigned long long kAgg = 1ull << 62, kPre = 2ull << 62, kVal = (1ull << 62) - 1;
-        __hip_atomic_store(&status[w], kAgg | H, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t excl = 0;
-        for (int64_t j = static_cast<int64_t>(w) - 1; j >= 0; --j) {
-            unsigned long long sj;
-            uint32_t spins = 0;  // bounded: a predecessor takes microseconds; never hang the queue
-            while (((sj = __hip_atomic_load(&status[j], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 62) == 0 &&
-                   ++spins < (1u << 24))
-                __builtin_amdgcn_s_sleep(1);
-            excl += sj & kVal;
-            if ((sj >> 62) == 2) break;
-        }
-        __hip_atomic_store(&status[w], kPre | (excl + H), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-        O = excl;
-    }
-    O = static_cast<uint64_t>(rdl64(static_cast<int64_t>(O), 0));
+    const uint64_t O = lookback_exclusive(status, w, H);
     // ---- outputs
     if (ul < nrows) row_off[row] = O + linc - nvr;
     if (row_hi == n_rows && ul == 0) row_off[n_rows] = O + H;

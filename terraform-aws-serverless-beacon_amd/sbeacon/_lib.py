@@ -59,6 +59,31 @@ class Request(C.Structure):
                 ('sample_names', C.c_char_p), ('sample_names_len', C.c_size_t)]
 
 
+class Str(C.Structure):
+    """sb_str: p == NULL is None."""
+    _fields_ = [('p', C.c_void_p), ('len', C.c_size_t)]
+
+
+class RequestColumns(C.Structure):
+    """sb_request_columns (include/sbeacon.h): requests as columns."""
+    _fields_ = [('vcf_id', C.c_void_p), ('vcf_id_all', C.c_uint32),
+                ('contig', C.c_void_p), ('contig_all', C.c_uint32),
+                ('start_min', C.c_void_p), ('start_max', C.c_void_p),
+                ('end_min', C.c_void_p), ('end_min_all', C.c_int64),
+                ('end_max', C.c_void_p), ('end_max_all', C.c_int64),
+                ('variant_min_length', C.c_void_p), ('variant_min_length_all', C.c_int64),
+                ('variant_max_length', C.c_void_p), ('variant_max_length_all', C.c_int64),
+                ('reference_dict', C.c_void_p), ('reference_code', C.c_void_p), ('n_reference', C.c_uint32),
+                ('alternate_dict', C.c_void_p), ('alternate_code', C.c_void_p), ('n_alternate', C.c_uint32),
+                ('variant_type_dict', C.c_void_p), ('variant_type_code', C.c_void_p), ('n_variant_type', C.c_uint32),
+                ('sample_names_dict', C.c_void_p), ('sample_names_code', C.c_void_p), ('n_sample_names', C.c_uint32),
+                ('granularity', C.c_void_p), ('granularity_all', C.c_uint8),
+                ('include_details', C.c_void_p), ('include_details_all', C.c_uint8),
+                ('include_samples', C.c_void_p), ('include_samples_all', C.c_uint8),
+                ('selected_samples_only', C.c_void_p), ('selected_samples_only_all', C.c_uint8),
+                ('strict_variant_type', C.c_uint8)]
+
+
 class ResultView(C.Structure):
     _fields_ = [('error', C.c_int32), ('exists', C.c_int32), ('call_count', C.c_int64),
                 ('all_alleles_count', C.c_int64), ('n_variants', C.c_uint64),
@@ -192,6 +217,7 @@ SIGNATURES = {
     'sb_vcf_scan_free': (None, [P]),
     'sb_requests_prepare': (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(P)]),
     'sb_requests_run': (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
+    'sb_requests_prepare_columns': (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(P)]),
 }
 
 _lib = None

@@ -399,12 +399,12 @@ def shard_requests(shape: GenomeShape, reqs: Requests, world: int, rank: int) ->
 
 def prepare_shard_requests(store, sr: ShardRequests):
     """The rank's request batch (sbeacon.requests.RequestBatch)."""
-    from .requests import RequestBatch, requests_array
+    from .requests import RequestBatch, request_columns
     names = store.contigs(LOCATION)
     at = {c: i for i, c in enumerate(names)}
-    cmap = np.array([at.get(c, 0xffffffff) for c in CONTIGS], dtype=np.int64)
-    arr, keep = requests_array(
-        sr.n_rows, vcf_id=store.vcf_id(LOCATION), contig=cmap[sr.ci] if sr.n_rows else 0,
+    cmap = np.array([at.get(c, 0xffffffff) for c in CONTIGS], dtype=np.uint32)
+    arr, keep = request_columns(
+        sr.n_rows, vcf_id=store.vcf_id(LOCATION), contig=cmap[sr.ci] if sr.n_rows else np.zeros(0, np.uint32),
         start_min=sr.start_min, start_max=sr.start_max, end_min=sr.end_min, end_max=sr.end_max,
         reference=('N',), alternate=(None,), variant_type=VARIANT_TYPES, variant_type_code=sr.vt,
         variant_min_length=sr.vmin, variant_max_length=sr.vmax, granularity='record', include_details=1)

@@ -6,7 +6,9 @@ its ``vcf_locations`` -- what ``split_query_sync``
 (``lambda/splitQuery/lambda_function.py:74-110``) would cut into 10 kb
 ``PerformQueryPayload`` slices.  ``sb_requests_prepare`` takes the requests
 as a columnar array (no per-slice payload objects, no region strings) and
-``sb_requests_run`` answers all of them on the device, leaving one row per
+``sb_requests_prepare_columns`` takes the same requests as numpy-backed
+columns (``request_columns``: no per-request struct, string columns as
+dictionary codes); ``sb_requests_run`` answers all of them on the device, leaving one row per
 request -- the route-level sums of its slices' responses
 (``route_g_variants.py:144-171``: exists count, variants, call_count,
 all_alleles_count, errors) -- and the rows' hit lists densely in request
@@ -101,10 +103,79 @@ def requests_array(n: int, *, vcf_id, contig, start_min, start_max, end_min, end
     return arr, keep
 
 
-def requests_from_split_payloads(store, payloads: list[dict], *, strict_variant_type: bool = False):
+def request_columns(n: int, *, vcf_id, contig, start_min, start_max, end_min, end_max,
+                    reference=('N',), reference_code=None, alternate=(None,), alternate_code=None,
+                    variant_type=(None,), variant_type_code=None, variant_min_length=0, variant_max_length=-1,
+                    granularity='record', include_details=True, include_samples=False,
+                    selected_samples_only=False, strict_variant_type=False, sample_names=(None,),
+                    sample_names_code=None):
+    """sb_request_columns over numpy columns (no per-request struct): a
+    scalar gives every request that value; string columns are the distinct
+    values plus a code per request (None = every request takes values[0]).
+    Returns (RequestColumns, keep-alive)."""
+    c = _lib.RequestColumns()
+    keep = [c]
+
+    def arr(x, dt):
+        a = np.ascontiguousarray(x, dtype=dt)
+        keep.append(a)
+        return a.ctypes.data
+
+    def num(field, x, dt):
+        if np.ndim(x) == 0:
+            setattr(c, field + '_all', int(x))
+        else:
+            if len(x) != n:
+                raise ValueError(f'{field}: {len(x)} values for {n} requests')
+            setattr(c, field, arr(x, dt))
+
+    for f, x, dt in (('vcf_id', vcf_id, np.uint32), ('contig', contig, np.uint32), ('end_min', end_min, np.int64),
+                     ('end_max', end_max, np.int64), ('variant_min_length', variant_min_length, np.int64),
+                     ('variant_max_length', variant_max_length, np.int64)):
+        num(f, x, dt)
+    for f, x in (('start_min', start_min), ('start_max', start_max)):
+        x = np.broadcast_to(np.asarray(x, dtype=np.int64), (n,))
+        setattr(c, f, arr(x, np.int64))
+    g = granularity
+    if isinstance(g, str):
+        g = _lib.SB_GRAN[g]
+    for f, x in (('granularity', g), ('include_details', include_details), ('include_samples', include_samples),
+                 ('selected_samples_only', selected_samples_only)):
+        if np.ndim(x) == 0:
+            setattr(c, f + '_all', int(x))
+        else:
+            setattr(c, f, arr(x, np.uint8))
+    c.strict_variant_type = 1 if strict_variant_type else 0
+    for f, short, vals, codes in (('reference', 'reference', reference, reference_code),
+                                  ('alternate', 'alternate', alternate, alternate_code),
+                                  ('variant_type', 'variant_type', variant_type, variant_type_code),
+                                  ('sample_names', 'sample_names', sample_names, sample_names_code)):
+        vals = list(vals)
+        if all(v is None for v in vals):
+            continue  # None for every request
+        d = (_lib.Str * len(vals))()
+        for k, v in enumerate(vals):
+            if v is None:
+                continue
+            b = v.encode() if isinstance(v, str) else bytes(v)
+            buf = C.create_string_buffer(b, len(b) + 1)
+            keep.append(buf)
+            d[k].p = C.addressof(buf)
+            d[k].len = len(b)
+        keep.append(d)
+        setattr(c, f + '_dict', C.addressof(d))
+        setattr(c, 'n_' + short, len(vals))
+        if codes is not None:
+            setattr(c, f + '_code', arr(np.broadcast_to(np.asarray(codes), (n,)), np.uint32))
+    return c, keep
+
+
+def requests_from_split_payloads(store, payloads: list[dict], *, strict_variant_type: bool = False,
+                                 columns: bool = False):
     """SplitQueryPayload dicts -> (sb_request array, keep-alive, owners):
     one request per (payload, vcf_location) pair, owners[k] = (payload
-    index, vcf_location).  The chrom string each vcf_location maps to is
+    index, vcf_location); ``columns``: a RequestColumns (dictionary-coded
+    string columns) instead of the sb_request array.  The chrom string each vcf_location maps to is
     looked up among the VCF's contigs (absent: a request with no slices, as
     bcftools emits nothing for it)."""
     rows = []
@@ -134,7 +205,8 @@ def requests_from_split_payloads(store, payloads: list[dict], *, strict_variant_
     vt_v, vt_c = codes([p.get('variant_type') for p in P])
     pts = [p.get('passthrough') or {} for p in P]
     sn_v, sn_c = codes([','.join(pt['sampleNames']) if pt.get('sampleNames') is not None else None for pt in pts])
-    arr, keep = requests_array(
+    make = request_columns if columns else requests_array
+    arr, keep = make(
         n, vcf_id=[store.vcf_id(loc) for _, loc, _ in rows], contig=[cidx(loc, c) for _, loc, c in rows],
         start_min=[int(p['start_min']) for p in P], start_max=[int(p['start_max']) for p in P],
         end_min=[int(p['end_min']) for p in P], end_max=[int(p['end_max']) for p in P],
@@ -154,10 +226,15 @@ class RequestBatch:
     """A prepared request batch (sb_requests_prepare) on the store's device."""
 
     def __init__(self, store, arr, n: int):
+        """arr: an sb_request array (requests_array) or RequestColumns
+        (request_columns)."""
         self.store = store
         self.n = n
         h = C.c_void_p()
-        check(lib().sb_requests_prepare(store.handle, C.cast(arr, C.c_void_p), n, C.byref(h)))
+        if isinstance(arr, _lib.RequestColumns):
+            check(lib().sb_requests_prepare_columns(store.handle, C.byref(arr), n, C.byref(h)))
+        else:
+            check(lib().sb_requests_prepare(store.handle, C.cast(arr, C.c_void_p), n, C.byref(h)))
         self._h = h
 
     @property

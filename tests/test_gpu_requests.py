@@ -98,6 +98,13 @@ def test_requests_match_slices(fixture):
         assert [int(x) for x in hits[ro[w]:ro[w + 1]]] == exp_hits[w], (w, sps[w])
     st = b.stats()
     assert st['chains'] > 0  # some requests took the chain path
+    # the same requests as columns (sb_requests_prepare_columns): identical answers
+    cols, keep_c, owners_c = requests_from_split_payloads(store, sps, columns=True)
+    assert owners_c == owners
+    rows_c, hits_c, ro_c = RequestBatch(store, cols, len(owners)).answer()
+    np.testing.assert_array_equal(rows_c, rows)
+    np.testing.assert_array_equal(ro_c, ro)
+    np.testing.assert_array_equal(hits_c, hits)
 
 
 def test_genome_requests_match_oracle_and_slices():
