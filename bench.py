@@ -208,6 +208,21 @@ def main():
                          'ms_per_batch': round(dt * 1e3, 2), 'responses': len(resp),
                          'note': 'one batch of all requests\' payload dicts -> PerformQueryResponse objects '
                                  '(prepare + device pass + fetch + responses; host-bound, not the timed step)'}
+            # at the wire: the performQuery events as the Lambda runtime receives
+            # them (JSON text) -> the JSON text it would send back, for the whole
+            # batch in one library call (sbeacon/wire.py, csrc/wire.cpp)
+            from sbeacon.wire import pack_events, perform_query_events_packed
+            ebuf, eoff = pack_events([json.dumps(p) for p in payloads])
+            perform_query_events_packed(ebuf, eoff[:65])
+            t2 = time.perf_counter()
+            for _ in range(reps):
+                wout = perform_query_events_packed(ebuf, eoff)
+            dtw = (time.perf_counter() - t2) / reps
+            delivered['wire'] = {'requests_per_s': round(n_req / dtw, 1), 'slice_payloads_per_s': round(n_slice / dtw, 1),
+                                 'ms_per_batch': round(dtw * 1e3, 2), 'event_bytes': len(ebuf),
+                                 'response_bytes': len(wout.buf), 'python_fallbacks': int(wout.fallback.sum()),
+                                 'note': 'event JSON texts in -> response JSON texts out (json.dumps(response.dump()) '
+                                         'byte for byte): C++ parse + one device batch + C++ formatting'}
         finally:
             engine.registry.clear()
 

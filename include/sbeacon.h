@@ -349,6 +349,31 @@ enum { SB_INDEX_CSI = 0, SB_INDEX_TBI = 1 };
 int sb_index_vcf(const char *path, int fmt, int min_shift, int depth, uint8_t **out, size_t *out_len);
 void sb_free(void *p);
 
+/* ---- performQuery at the wire -------------------------------------------
+ * The performQuery Lambda (lambda/performQuery/lambda_function.py:23-49) for
+ * a batch of events: event i is the JSON text text[offsets[i] ..
+ * offsets[i + 1]) -- a PerformQueryPayload (shared_resources/payloads/
+ * lambda_payloads.py:46-77) or its SNS envelope (Records[0].Sns.Message).
+ * Each event's vcf_location picks the store that holds it; every store's
+ * events are answered by one sb_query_batch.  Response i is the JSON text of
+ * the handler's return value, json.dumps(response.dump())
+ * (lambda_responses.py:14-23; ensure_ascii escapes, ", " / ": "
+ * separators), or {"errorMessage", "errorType"} where the reference raises
+ * from the query.  status[i] = 1 (no text) marks an event outside the typed
+ * fast path -- a field of an unexpected JSON type, a key the payload does not
+ * take, a vcf_location no store holds, invalid UTF-8 -- for the caller to
+ * answer through the Python handler, which reproduces the reference's
+ * behaviour.  flags bit 0: strict variantType (the reference's
+ * UnboundLocalError).  Output: JSON lines -- response i is buf[offsets[i] ..
+ * offsets[i + 1] - 1), each followed by '\n' (empty for status 1); release it
+ * with sb_json_out_free. */
+typedef struct sb_json_out sb_json_out;
+int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char *text, const uint64_t *offsets,
+                            size_t n, uint32_t flags, sb_json_out **out);
+int sb_json_out_get(const sb_json_out *o, const char **buf, size_t *len, const uint64_t **offsets,
+                    const uint8_t **status);
+void sb_json_out_free(sb_json_out *o);
+
 typedef struct sb_batch sb_batch;
 
 /* ---- split-query requests (the splitQuery fan-out in the library) ---------

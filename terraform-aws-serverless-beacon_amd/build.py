@@ -20,7 +20,7 @@ INCLUDE = os.path.join(os.path.dirname(HERE), 'include')
 ARCH = os.environ.get('SBEACON_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 
-SOURCES = ['api.cpp', 'ingest.cpp', 'index.cpp', 'query_kernels.hip', 'dedup_kernels.hip']
+SOURCES = ['api.cpp', 'ingest.cpp', 'index.cpp', 'wire.cpp', 'query_kernels.hip', 'dedup_kernels.hip']
 FLAGS = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-Wall', '-Wextra', '-Wno-unused-parameter',
          f'-I{INCLUDE}']
 

@@ -217,7 +217,7 @@ constexpr uint32_t kChainEndVoid = 1u << 8;  // no END can match
 // densely in row order at the run's offset, found by a decoupled look-back
 // over the runs (status words, one ticket counter).
 constexpr uint32_t kRunRows = 64;    // rows per run at most (one lane each)
-constexpr uint32_t kRowHitBuf = 320; // chain hits a wave stages in LDS; the rest spill to global
+constexpr uint32_t kRowHitBuf = 256; // chain hits a wave stages in LDS; the rest spill to global
 struct alignas(16) RowRun {
     uint32_t row_lo, row_hi;  // rows [row_lo, row_hi)
     uint32_t c_lo, c_hi;      // the run's chains, rows increasing

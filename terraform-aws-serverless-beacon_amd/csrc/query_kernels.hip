@@ -1959,18 +1959,28 @@ struct RowChunk {
     bool first;      // the lane holds its chain's first candidate
 };
 
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_rows_kernel(
+// Eight waves per workgroup and ONE ticket per workgroup: a single device-scope
+// counter serves at most ~88 returning atomics per microsecond (guide,
+// `dequeue`), so a ticket per wave (31 k runs at config 3) cost ~0.35 ms of
+// the 0.47 ms launch.  Wave k of ticket t answers run 8 t + k; a run waits only
+// on lower runs, whose workgroups already hold their tickets (resident): no
+// assumption on dispatch order or placement.
+constexpr int kReqWaves = 8;
+constexpr int kReqBlock = kReqWaves * kWave;
+
+__global__ __launch_bounds__(kReqBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_rows_kernel(
     DStore st, const ChainDev *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
     uint32_t *__restrict__ ticket, unsigned long long *__restrict__ status, const QRes *__restrict__ sres,
     const uint32_t *__restrict__ sseg, const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr,
     const uint64_t *__restrict__ shits, ReqPartial *__restrict__ rows, uint64_t *__restrict__ row_off,
     uint64_t *__restrict__ out, uint64_t *__restrict__ spill, uint32_t n_rows, uint64_t rec_base) {
-    __shared__ ReqLds lds_all[kWavesPerBlock];
+    __shared__ ReqLds lds_all[kReqWaves];
+    __shared__ uint32_t blk_ticket;
     ReqLds &L = lds_all[threadIdx.x >> 6];
     const uint32_t ul = static_cast<uint32_t>(lane_id());
-    uint32_t w = 0;
-    if (ul == 0) w = atomicAdd(ticket, 1u);
-    w = rdl(w, 0);
+    if (threadIdx.x == 0) blk_ticket = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t w = uniform(blk_ticket) * kReqWaves + (threadIdx.x >> 6);
     if (w >= n_runs) return;
     const uint32_t row_lo = uniform(runs[w].row_lo), row_hi = uniform(runs[w].row_hi);
     const uint32_t c_lo = uniform(runs[w].c_lo), R = uniform(runs[w].c_hi) - c_lo;
@@ -3362,7 +3372,8 @@ void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun 
         (void)hipMemsetAsync(row_off, 0, 8, s);
         return;
     }
-    hipLaunchKernelGGL(request_rows_kernel, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs, n_runs,
+    hipLaunchKernelGGL(request_rows_kernel, dim3((n_runs + kReqWaves - 1) / kReqWaves), dim3(kReqBlock), 0, s, st,
+                       chains, runs, n_runs,
                        ticket, status, sres, sseg, shoff, sherr, shits, rows, row_off, out, spill, n_rows, rec_base);
 }
 

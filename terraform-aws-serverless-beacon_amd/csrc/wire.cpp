@@ -1,0 +1,787 @@
+// wire.cpp — the performQuery Lambda at the wire: event JSON in, response
+// JSON out, for a whole batch of events in one call.
+//
+// Reference: lambda/performQuery/lambda_function.py:23-49 — the event (a
+// PerformQueryPayload, or its SNS envelope whose Records[0].Sns.Message is
+// the payload's JSON text) is loaded with jsons.load into a
+// PerformQueryPayload (shared_resources/payloads/lambda_payloads.py:46-77),
+// answered by search_variants(.._in_samples).perform_query, and the handler
+// returns response.dump() (lambda_responses.py:14-23), which the Lambda
+// runtime serialises with json.dumps.  Here the events are parsed in C++,
+// every event of the batch is answered by ONE sb_query_batch per store, and
+// each response is written as the text json.dumps(response.dump()) gives
+// (ensure_ascii escapes, ", " / ": " separators, the dataclass field order).
+// An event outside the typed fast path (a field of an unexpected JSON type,
+// a key PerformQueryPayload does not take, a vcf_location no store holds,
+// invalid UTF-8 or a lone surrogate) is returned with status 1 and no text:
+// the caller answers it through the Python handler, which reproduces the
+// reference's behaviour (including the exception it raises).
+//
+// Only the public C ABI (include/sbeacon.h) is used below the parser.
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "common.hpp"
+
+struct sb_json_out {
+    std::string buf;
+    std::vector<uint64_t> off;   // n + 1
+    std::vector<uint8_t> status;  // 0 answered, 1 = answer through the Python handler
+};
+
+namespace sb {
+namespace {
+
+// ------------------------------------------------------------------ JSON DOM
+// What Python's json.loads accepts (strict mode: no raw control characters in
+// strings; NaN / Infinity literals are accepted and typed as floats).
+struct JVal {
+    enum Kind : uint8_t { NUL, BOOL, INT, FLOAT, STR, ARR, OBJ } kind = NUL;
+    bool b = false;
+    bool big = false;  // an integer beyond int64 (Python keeps it exactly; never a fast-path value)
+    int64_t i = 0;
+    std::string s;     // STR: UTF-8
+    std::vector<JVal> a;
+    std::vector<std::pair<std::string, JVal>> o;  // insertion order; duplicate keys: the last wins (dict semantics)
+
+    const JVal *get(const char *key) const {
+        const JVal *r = nullptr;
+        for (const auto &kv : o)
+            if (kv.first == key) r = &kv.second;
+        return r;
+    }
+};
+
+struct Parser {
+    const char *p, *e;
+    bool bad = false;  // not valid JSON, or outside what the fast path carries (lone surrogate, bad UTF-8)
+
+    void ws() {
+        while (p < e && (*p == ' ' || *p == '\t' || *p == '\n' || *p == '\r')) ++p;
+    }
+    bool lit(const char *w) {
+        const size_t n = strlen(w);
+        if (static_cast<size_t>(e - p) < n || memcmp(p, w, n) != 0) return false;
+        p += n;
+        return true;
+    }
+    static void put_utf8(std::string &o, uint32_t cp) {
+        if (cp < 0x80) {
+            o.push_back(static_cast<char>(cp));
+        } else if (cp < 0x800) {
+            o.push_back(static_cast<char>(0xc0 | (cp >> 6)));
+            o.push_back(static_cast<char>(0x80 | (cp & 0x3f)));
+        } else if (cp < 0x10000) {
+            o.push_back(static_cast<char>(0xe0 | (cp >> 12)));
+            o.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3f)));
+            o.push_back(static_cast<char>(0x80 | (cp & 0x3f)));
+        } else {
+            o.push_back(static_cast<char>(0xf0 | (cp >> 18)));
+            o.push_back(static_cast<char>(0x80 | ((cp >> 12) & 0x3f)));
+            o.push_back(static_cast<char>(0x80 | ((cp >> 6) & 0x3f)));
+            o.push_back(static_cast<char>(0x80 | (cp & 0x3f)));
+        }
+    }
+    int hex4() {
+        if (e - p < 4) return -1;
+        int v = 0;
+        for (int k = 0; k < 4; ++k) {
+            const char c = p[k];
+            v <<= 4;
+            if (c >= '0' && c <= '9') v |= c - '0';
+            else if (c >= 'a' && c <= 'f') v |= c - 'a' + 10;
+            else if (c >= 'A' && c <= 'F') v |= c - 'A' + 10;
+            else return -1;
+        }
+        p += 4;
+        return v;
+    }
+    bool str(std::string &o) {  // at the opening quote
+        ++p;
+        while (true) {
+            if (p >= e) return false;
+            const unsigned char c = static_cast<unsigned char>(*p);
+            if (c == '"') {
+                ++p;
+                return true;
+            }
+            if (c < 0x20) return false;  // strict json.loads
+            if (c == '\\') {
+                if (++p >= e) return false;
+                const char x = *p++;
+                switch (x) {
+                    case '"': o.push_back('"'); break;
+                    case '\\': o.push_back('\\'); break;
+                    case '/': o.push_back('/'); break;
+                    case 'b': o.push_back('\b'); break;
+                    case 'f': o.push_back('\f'); break;
+                    case 'n': o.push_back('\n'); break;
+                    case 'r': o.push_back('\r'); break;
+                    case 't': o.push_back('\t'); break;
+                    case 'u': {
+                        int u = hex4();
+                        if (u < 0) return false;
+                        uint32_t cp = static_cast<uint32_t>(u);
+                        if (cp >= 0xd800 && cp < 0xdc00) {  // a high surrogate needs its low half
+                            if (e - p >= 6 && p[0] == '\\' && p[1] == 'u') {
+                                p += 2;
+                                const int lo = hex4();
+                                if (lo < 0) return false;
+                                if (lo < 0xdc00 || lo >= 0xe000) {
+                                    bad = true;
+                                    return true;
+                                }
+                                cp = 0x10000 + ((cp - 0xd800) << 10) + (static_cast<uint32_t>(lo) - 0xdc00);
+                            } else {
+                                bad = true;  // lone surrogate: Python keeps it; not UTF-8 representable
+                                return true;
+                            }
+                        } else if (cp >= 0xdc00 && cp < 0xe000) {
+                            bad = true;
+                            return true;
+                        }
+                        put_utf8(o, cp);
+                        break;
+                    }
+                    default: return false;
+                }
+                continue;
+            }
+            // raw bytes: must be valid UTF-8 (the event text is decoded as UTF-8)
+            if (c < 0x80) {
+                o.push_back(static_cast<char>(c));
+                ++p;
+                continue;
+            }
+            const int n = (c & 0xe0) == 0xc0 ? 2 : (c & 0xf0) == 0xe0 ? 3 : (c & 0xf8) == 0xf0 ? 4 : 0;
+            if (!n || e - p < n) {
+                bad = true;
+                return true;
+            }
+            uint32_t cp = c & (0x7f >> n);
+            for (int k = 1; k < n; ++k) {
+                const unsigned char cc = static_cast<unsigned char>(p[k]);
+                if ((cc & 0xc0) != 0x80) {
+                    bad = true;
+                    return true;
+                }
+                cp = (cp << 6) | (cc & 0x3f);
+            }
+            if ((n == 2 && cp < 0x80) || (n == 3 && cp < 0x800) || (n == 4 && (cp < 0x10000 || cp > 0x10ffff)) ||
+                (cp >= 0xd800 && cp < 0xe000)) {
+                bad = true;
+                return true;
+            }
+            o.append(p, static_cast<size_t>(n));
+            p += n;
+        }
+    }
+    bool num(JVal &v) {
+        const char *s0 = p;
+        if (p < e && *p == '-') ++p;
+        if (p >= e) return false;
+        if (*p == '0') {
+            ++p;
+        } else if (*p >= '1' && *p <= '9') {
+            while (p < e && *p >= '0' && *p <= '9') ++p;
+        } else {
+            return false;
+        }
+        bool is_int = true;
+        if (p < e && *p == '.') {
+            is_int = false;
+            ++p;
+            if (p >= e || *p < '0' || *p > '9') return false;
+            while (p < e && *p >= '0' && *p <= '9') ++p;
+        }
+        if (p < e && (*p == 'e' || *p == 'E')) {
+            is_int = false;
+            ++p;
+            if (p < e && (*p == '+' || *p == '-')) ++p;
+            if (p >= e || *p < '0' || *p > '9') return false;
+            while (p < e && *p >= '0' && *p <= '9') ++p;
+        }
+        if (!is_int) {
+            v.kind = JVal::FLOAT;
+            return true;
+        }
+        v.kind = JVal::INT;
+        const bool neg = *s0 == '-';
+        uint64_t m = 0;
+        for (const char *q = s0 + (neg ? 1 : 0); q < p; ++q) {
+            const uint64_t d = static_cast<uint64_t>(*q - '0');
+            if (m > (UINT64_MAX - d) / 10) {
+                v.big = true;
+                return true;
+            }
+            m = m * 10 + d;
+        }
+        if (neg ? m > (1ull << 63) : m > static_cast<uint64_t>(INT64_MAX)) {
+            v.big = true;
+            return true;
+        }
+        v.i = neg ? static_cast<int64_t>(0 - m) : static_cast<int64_t>(m);
+        return true;
+    }
+    bool value(JVal &v, int depth) {
+        if (depth > 64) return false;
+        ws();
+        if (p >= e) return false;
+        const char c = *p;
+        if (c == '{') {
+            v.kind = JVal::OBJ;
+            ++p;
+            ws();
+            if (p < e && *p == '}') {
+                ++p;
+                return true;
+            }
+            while (true) {
+                ws();
+                if (p >= e || *p != '"') return false;
+                std::string k;
+                if (!str(k)) return false;
+                ws();
+                if (p >= e || *p != ':') return false;
+                ++p;
+                v.o.emplace_back(std::move(k), JVal{});
+                if (!value(v.o.back().second, depth + 1)) return false;
+                ws();
+                if (p < e && *p == ',') {
+                    ++p;
+                    continue;
+                }
+                if (p < e && *p == '}') {
+                    ++p;
+                    return true;
+                }
+                return false;
+            }
+        }
+        if (c == '[') {
+            v.kind = JVal::ARR;
+            ++p;
+            ws();
+            if (p < e && *p == ']') {
+                ++p;
+                return true;
+            }
+            while (true) {
+                v.a.emplace_back();
+                if (!value(v.a.back(), depth + 1)) return false;
+                ws();
+                if (p < e && *p == ',') {
+                    ++p;
+                    continue;
+                }
+                if (p < e && *p == ']') {
+                    ++p;
+                    return true;
+                }
+                return false;
+            }
+        }
+        if (c == '"') {
+            v.kind = JVal::STR;
+            return str(v.s);
+        }
+        if (lit("true")) {
+            v.kind = JVal::BOOL;
+            v.b = true;
+            return true;
+        }
+        if (lit("false")) {
+            v.kind = JVal::BOOL;
+            return true;
+        }
+        if (lit("null")) {
+            v.kind = JVal::NUL;
+            return true;
+        }
+        if (lit("NaN") || lit("Infinity") || lit("-Infinity")) {
+            v.kind = JVal::FLOAT;
+            return true;
+        }
+        return num(v);
+    }
+};
+
+bool parse_json(const char *p, size_t n, JVal &out, bool &bad) {
+    Parser P{p, p + n};
+    if (!P.value(out, 0)) return false;
+    P.ws();
+    bad = P.bad;
+    return P.p == P.e;
+}
+
+// ------------------------------------------------------------------ events
+// One event on the typed fast path: the sb_query fields plus the strings the
+// response echoes.  Strings are owned here (sb_query points into them).
+struct Event {
+    bool ok = false;
+    uint32_t store = 0;
+    sb_query q{};
+    std::string region, ref, alt, vt, names, location, dataset;
+    bool has_ref = false, has_alt = false, has_vt = false, has_names = false, dataset_null = true;
+};
+
+// PerformQueryPayload.__init__ keyword arguments (lambda_payloads.py:46-77)
+const char *const kPayloadKeys[] = {"passthrough",   "dataset_id",      "query_id",     "region",
+                                    "reference_bases", "end_min",       "end_max",      "alternate_bases",
+                                    "variant_type",  "include_details", "requested_granularity",
+                                    "variant_min_length", "variant_max_length", "vcf_location"};
+
+// Python truthiness of a JSON value limited to the kinds the fast path takes
+bool truthy(const JVal *v, bool &ok) {
+    if (!v || v->kind == JVal::NUL) return false;
+    if (v->kind == JVal::BOOL) return v->b;
+    if (v->kind == JVal::INT && !v->big) return v->i != 0;
+    ok = false;
+    return false;
+}
+
+bool opt_str(const JVal *v, std::string &out, bool &has) {
+    if (!v || v->kind == JVal::NUL) {
+        has = false;
+        return true;
+    }
+    if (v->kind != JVal::STR) return false;
+    out = v->s;
+    has = true;
+    return true;
+}
+
+bool req_int(const JVal *v, int64_t &out) {
+    if (!v || v->kind != JVal::INT || v->big) return false;
+    out = v->i;
+    return true;
+}
+
+// event text -> Event (ok = false: answer through the Python handler)
+void load_event(const char *text, size_t len, sb_store *const *stores, size_t n_stores, bool strict_vt, Event &E) {
+    JVal root;
+    bool bad = false;
+    if (!parse_json(text, len, root, bad) || bad) return;
+    // lambda_function.py:33-39: the SNS envelope, when Records[0].Sns.Message parses
+    const JVal *ev = &root;
+    JVal inner;
+    if (root.kind == JVal::OBJ) {
+        const JVal *rec = root.get("Records");
+        if (rec && (rec->kind == JVal::ARR || rec->kind == JVal::OBJ)) {
+            // Python: event['Records'][0] works on a list (and raises on a dict without key 0)
+            if (rec->kind == JVal::ARR && !rec->a.empty() && rec->a[0].kind == JVal::OBJ) {
+                const JVal *sns = rec->a[0].get("Sns");
+                const JVal *msg = sns && sns->kind == JVal::OBJ ? sns->get("Message") : nullptr;
+                if (msg && msg->kind == JVal::STR) {
+                    bool bad2 = false;
+                    if (parse_json(msg->s.data(), msg->s.size(), inner, bad2)) {
+                        if (bad2) return;
+                        ev = &inner;
+                    }
+                } else if (msg) {
+                    return;  // json.loads of a non-string raises TypeError: caught; keep it simple, use Python
+                }
+            } else if (rec->kind == JVal::OBJ || (rec->kind == JVal::ARR && !rec->a.empty())) {
+                return;  // indexing behaviour of odd envelopes: Python decides
+            }
+        }
+    }
+    if (ev->kind != JVal::OBJ) return;
+    for (const auto &kv : ev->o) {  // PerformQueryPayload(**event): unknown keyword -> TypeError
+        bool known = false;
+        for (const char *k : kPayloadKeys) known = known || kv.first == k;
+        if (!known) return;
+    }
+    const JVal *loc = ev->get("vcf_location");
+    if (!loc || loc->kind != JVal::STR) return;
+    E.location = loc->s;
+    bool found = false;
+    for (size_t k = 0; k < n_stores && !found; ++k) {
+        uint32_t vid = 0;
+        if (sb_store_find_vcf(stores[k], E.location.data(), E.location.size(), &vid) == SB_OK) {
+            E.store = static_cast<uint32_t>(k);
+            E.q.vcf_id = vid;
+            found = true;
+        }
+    }
+    if (!found) return;
+    const JVal *region = ev->get("region");
+    if (!region || region->kind != JVal::STR) return;
+    E.region = region->s;
+    bool ok = true;
+    int64_t emin = 0, emax = 0, vmin = 0, vmax = 0;
+    if (!req_int(ev->get("end_min"), emin) || !req_int(ev->get("end_max"), emax) ||
+        !req_int(ev->get("variant_min_length"), vmin) || !req_int(ev->get("variant_max_length"), vmax))
+        return;
+    if (!opt_str(ev->get("reference_bases"), E.ref, E.has_ref) || !opt_str(ev->get("alternate_bases"), E.alt, E.has_alt) ||
+        !opt_str(ev->get("variant_type"), E.vt, E.has_vt))
+        return;
+    const JVal *ds = ev->get("dataset_id");
+    if (ds && ds->kind == JVal::STR) {
+        E.dataset = ds->s;
+        E.dataset_null = false;
+    } else if (ds && ds->kind != JVal::NUL) {
+        return;
+    }
+    const bool details = truthy(ev->get("include_details"), ok);
+    uint8_t gran = 255;
+    if (const JVal *g = ev->get("requested_granularity")) {
+        if (g->kind == JVal::STR) {
+            gran = g->s == "boolean" ? SB_GRAN_BOOLEAN : g->s == "count" ? SB_GRAN_COUNT
+                 : g->s == "aggregated" ? SB_GRAN_AGGREGATED : g->s == "record" ? SB_GRAN_RECORD : 255;
+        } else if (g->kind != JVal::NUL) {
+            return;
+        }
+    }
+    bool inc = false, sel = false;
+    if (const JVal *pt = ev->get("passthrough")) {  // `payload.passthrough or {}`
+        if (pt->kind == JVal::OBJ) {
+            inc = truthy(pt->get("includeSamples"), ok);
+            sel = truthy(pt->get("selectedSamplesOnly"), ok);
+            if (const JVal *sn = pt->get("sampleNames")) {
+                if (sn->kind == JVal::ARR) {
+                    for (size_t k = 0; k < sn->a.size(); ++k) {
+                        if (sn->a[k].kind != JVal::STR) return;
+                        if (k) E.names.push_back(',');
+                        E.names += sn->a[k].s;
+                    }
+                    E.has_names = true;
+                } else if (sn->kind != JVal::NUL) {
+                    return;
+                }
+            }
+        } else if (pt->kind != JVal::NUL && !(pt->kind == JVal::BOOL && !pt->b)) {
+            return;
+        }
+    }
+    if (!ok) return;
+    sb_query &q = E.q;
+    q.end_min = emin;
+    q.end_max = emax;
+    q.variant_min_length = vmin;
+    q.variant_max_length = vmax;
+    q.granularity = gran;
+    q.include_details = details ? 1 : 0;
+    q.include_samples = inc ? 1 : 0;
+    q.selected_samples_only = sel ? 1 : 0;
+    q.strict_variant_type = strict_vt ? 1 : 0;
+    E.ok = true;
+}
+
+void bind_strings(Event &E) {  // after E is in its final place
+    sb_query &q = E.q;
+    q.region = E.region.c_str();
+    q.region_len = E.region.size();
+    q.reference_bases = E.has_ref ? E.ref.c_str() : nullptr;
+    q.reference_len = E.has_ref ? E.ref.size() : 0;
+    q.alternate_bases = E.has_alt ? E.alt.c_str() : nullptr;
+    q.alternate_len = E.has_alt ? E.alt.size() : 0;
+    q.variant_type = E.has_vt ? E.vt.c_str() : nullptr;
+    q.variant_type_len = E.has_vt ? E.vt.size() : 0;
+    q.sample_names = E.has_names ? E.names.c_str() : nullptr;
+    q.sample_names_len = E.has_names ? E.names.size() : 0;
+}
+
+// ------------------------------------------------------------------ output
+// json.dumps (ensure_ascii=True) of a Python str holding these UTF-8 bytes;
+// false on invalid UTF-8 (the Python path's .decode() raises there)
+bool put_jstr(std::string &o, const char *s, size_t n) {
+    static const char kHex[] = "0123456789abcdef";
+    auto u4 = [&](uint32_t v) {
+        o += "\\u";
+        o.push_back(kHex[(v >> 12) & 15]);
+        o.push_back(kHex[(v >> 8) & 15]);
+        o.push_back(kHex[(v >> 4) & 15]);
+        o.push_back(kHex[v & 15]);
+    };
+    o.push_back('"');
+    for (size_t i = 0; i < n;) {
+        const unsigned char c = static_cast<unsigned char>(s[i]);
+        if (c < 0x80) {
+            switch (c) {
+                case '"': o += "\\\""; break;
+                case '\\': o += "\\\\"; break;
+                case '\n': o += "\\n"; break;
+                case '\r': o += "\\r"; break;
+                case '\t': o += "\\t"; break;
+                case '\b': o += "\\b"; break;
+                case '\f': o += "\\f"; break;
+                default:
+                    if (c < 0x20 || c == 0x7f) u4(c);
+                    else o.push_back(static_cast<char>(c));
+            }
+            ++i;
+            continue;
+        }
+        const int len = (c & 0xe0) == 0xc0 ? 2 : (c & 0xf0) == 0xe0 ? 3 : (c & 0xf8) == 0xf0 ? 4 : 0;
+        if (!len || i + len > n) return false;
+        uint32_t cp = c & (0x7f >> len);
+        for (int k = 1; k < len; ++k) {
+            const unsigned char cc = static_cast<unsigned char>(s[i + k]);
+            if ((cc & 0xc0) != 0x80) return false;
+            cp = (cp << 6) | (cc & 0x3f);
+        }
+        if ((len == 2 && cp < 0x80) || (len == 3 && cp < 0x800) || (len == 4 && (cp < 0x10000 || cp > 0x10ffff)) ||
+            (cp >= 0xd800 && cp < 0xe000))
+            return false;
+        if (cp >= 0x10000) {
+            const uint32_t v = cp - 0x10000;
+            u4(0xd800 + (v >> 10));
+            u4(0xdc00 + (v & 0x3ff));
+        } else {
+            u4(cp);
+        }
+        i += static_cast<size_t>(len);
+    }
+    o.push_back('"');
+    return true;
+}
+
+void put_i64(std::string &o, int64_t v) {
+    char b[24];
+    const int n = snprintf(b, sizeof b, "%lld", static_cast<long long>(v));
+    o.append(b, static_cast<size_t>(n));
+}
+
+// decimal of a two's-complement little-endian 32-bit-limb integer; false
+// when it has more digits than CPython converts (json.dumps raises ValueError)
+bool put_limbs(std::string &o, const uint32_t *l, uint32_t n) {
+    std::vector<uint32_t> m(l, l + n);
+    const bool neg = n && (m[n - 1] >> 31);
+    if (neg) {  // magnitude = ~x + 1
+        uint64_t carry = 1;
+        for (auto &x : m) {
+            const uint64_t t = static_cast<uint64_t>(~x) + carry;
+            x = static_cast<uint32_t>(t);
+            carry = t >> 32;
+        }
+    }
+    std::string digits;
+    while (true) {
+        bool zero = true;
+        uint64_t rem = 0;
+        for (size_t k = m.size(); k-- > 0;) {
+            const uint64_t cur = (rem << 32) | m[k];
+            m[k] = static_cast<uint32_t>(cur / 1000000000u);
+            rem = cur % 1000000000u;
+            zero = zero && m[k] == 0;
+        }
+        char b[16];
+        if (zero) {
+            const int w = snprintf(b, sizeof b, "%llu", static_cast<unsigned long long>(rem));
+            digits.insert(0, b, static_cast<size_t>(w));
+            break;
+        }
+        snprintf(b, sizeof b, "%09llu", static_cast<unsigned long long>(rem));
+        digits.insert(0, b, 9);
+    }
+    if (digits.size() > kPyMaxStrDigits) return false;
+    if (neg) o.push_back('-');
+    o += digits;
+    return true;
+}
+
+// what json.dumps raises for an int past CPython's digit limit
+void put_digits_error(std::string &o) {
+    static const char kMsg[] =
+        "Exceeds the limit (4300) for integer string conversion; use sys.set_int_max_str_digits() to increase the limit";
+    o = "{\"errorMessage\": ";
+    put_jstr(o, kMsg, sizeof kMsg - 1);
+    o += ", \"errorType\": \"ValueError\"}";
+}
+
+// QERR -> the exception the reference raises (sbeacon/engine.py QERR / QERR_MSG)
+void put_error(std::string &o, int32_t err) {
+    const char *type = "RuntimeError", *msg = "error";
+    switch (err) {
+        case 1: type = "UnboundLocalError"; msg = "local variable 'variant_type' referenced before assignment"; break;
+        case 2: type = "IndexError"; msg = "list index out of range"; break;
+        case 3: type = "ValueError"; msg = "invalid literal for int() with base 10"; break;
+        case 4: type = "AttributeError"; msg = "'NoneType' object has no attribute 'replace'"; break;
+        case 9: type = "NotImplementedError"; msg = "referenceBases contains regex metacharacters (outside the restated contract)"; break;
+        default: break;
+    }
+    o += "{\"errorMessage\": ";
+    put_jstr(o, msg, strlen(msg));
+    o += ", \"errorType\": ";
+    put_jstr(o, type, strlen(type));
+    o += "}";
+}
+
+// json.dumps(PerformQueryResponse.dump()) for query i of rs (engine.py
+// ResultSet.responses); false = text the Python path could not decode
+bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
+    sb_result_view v;
+    if (sb_result_get(rs, i, &v) != SB_OK) return false;
+    if (v.error) {
+        put_error(o, v.error);
+        return true;
+    }
+    const char *tp = nullptr;
+    size_t tn = 0;
+    o += "{\"exists\": ";
+    o += v.exists ? "true" : "false";
+    o += ", \"vcf_location\": ";
+    if (!put_jstr(o, E.location.data(), E.location.size())) return false;
+    o += ", \"dataset_id\": ";
+    if (E.dataset_null) o += "null";
+    else if (!put_jstr(o, E.dataset.data(), E.dataset.size())) return false;
+    o += ", \"all_alleles_count\": ";
+    if (v.big_limbs) {
+        if (!put_limbs(o, v.big_all_alleles_count, v.big_limbs)) {
+            put_digits_error(o);
+            return true;
+        }
+    } else {
+        put_i64(o, v.all_alleles_count);
+    }
+    o += ", \"variants\": [";
+    if (v.n_variants) {
+        if (sb_result_variants_text(rs, i, &tp, &tn) != SB_OK) return false;
+        size_t a = 0;
+        for (size_t k = 0; k <= tn; ++k) {
+            if (k == tn || tp[k] == '\n') {
+                if (a) o += ", ";
+                if (!put_jstr(o, tp + a, k - a)) return false;
+                a = k + 1;
+            }
+        }
+    }
+    o += "], \"call_count\": ";
+    if (v.big_limbs) {
+        if (!put_limbs(o, v.big_call_count, v.big_limbs)) {
+            put_digits_error(o);
+            return true;
+        }
+    } else {
+        put_i64(o, v.call_count);
+    }
+    // sample_indices / sample_names (engine.py ResultSet.responses)
+    const bool sel = E.q.selected_samples_only, inc = E.q.include_samples;
+    o += ", \"sample_indices\": [";
+    if (sel)
+        for (uint64_t k = 0; k < v.n_sample_indices; ++k) {
+            if (k) o += ", ";
+            put_i64(o, v.sample_indices[k]);
+        }
+    o += "], \"sample_names\": [";
+    if ((sel || inc) && v.n_sample_indices) {
+        if (sb_result_sample_names_text(rs, i, &tp, &tn) != SB_OK) return false;
+        size_t a = 0;
+        bool first = true;
+        for (size_t k = 0; k <= tn; ++k) {
+            if (k == tn || tp[k] == ',') {
+                if (!first) o += ", ";
+                first = false;
+                if (!put_jstr(o, tp + a, k - a)) return false;
+                a = k + 1;
+            }
+        }
+    }
+    o += "]}";
+    return true;
+}
+
+template <class F>
+void par(size_t n, unsigned threads, F fn) {
+    const unsigned t = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, n / 256)));
+    if (t <= 1) {
+        for (size_t i = 0; i < n; ++i) fn(i, 0u);
+        return;
+    }
+    std::vector<std::thread> th;
+    for (unsigned k = 0; k < t; ++k)
+        th.emplace_back([&, k] {
+            for (size_t i = n * k / t, e = n * (k + 1) / t; i < e; ++i) fn(i, k);
+        });
+    for (auto &x : th) x.join();
+}
+
+}  // namespace
+}  // namespace sb
+
+extern "C" {
+
+int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char *text, const uint64_t *offsets,
+                            size_t n, uint32_t flags, sb_json_out **out) {
+    using namespace sb;
+    try {
+        if ((!stores && n_stores) || (!offsets && n) || (!text && n) || !out) throw Error(SB_EINVAL, "NULL argument");
+        for (size_t i = 0; i < n; ++i)
+            if (offsets[i + 1] < offsets[i]) throw Error(SB_EINVAL, "offsets not non-decreasing");
+        const unsigned threads = 16;
+        const bool strict_vt = (flags & 1u) != 0;
+        std::vector<Event> ev(n);
+        par(n, threads, [&](size_t i, unsigned) {
+            load_event(text + offsets[i], offsets[i + 1] - offsets[i], stores, n_stores, strict_vt, ev[i]);
+            if (ev[i].ok) bind_strings(ev[i]);
+        });
+        auto R = std::make_unique<sb_json_out>();
+        R->status.assign(n, 1);
+        std::vector<std::string> parts(n);
+        // one device batch per store, events in input order
+        for (size_t k = 0; k < n_stores; ++k) {
+            std::vector<uint32_t> idx;
+            for (size_t i = 0; i < n; ++i)
+                if (ev[i].ok && ev[i].store == k) idx.push_back(static_cast<uint32_t>(i));
+            if (idx.empty()) continue;
+            std::vector<sb_query> qs(idx.size());
+            for (size_t j = 0; j < idx.size(); ++j) qs[j] = ev[idx[j]].q;
+            sb_result_set *rs = nullptr;
+            const int rc = sb_query_batch(stores[k], qs.data(), qs.size(), 0, &rs);
+            if (rc != SB_OK) return rc;  // sb_last_error holds the message
+            std::unique_ptr<sb_result_set, void (*)(sb_result_set *)> keep(rs, sb_result_free);
+            par(idx.size(), threads, [&](size_t j, unsigned) {
+                const uint32_t i = idx[j];
+                std::string o;
+                o.reserve(256);
+                if (put_response(o, rs, j, ev[i])) {
+                    parts[i] = std::move(o);
+                    R->status[i] = 0;
+                }
+            });
+        }
+        size_t total = 0;
+        for (const auto &s : parts) total += s.size();
+        R->buf.reserve(total + n);
+        R->off.resize(n + 1);
+        for (size_t i = 0; i < n; ++i) {  // JSON lines: every response ends with '\n'
+            R->off[i] = R->buf.size();
+            R->buf += parts[i];
+            R->buf.push_back('\n');
+        }
+        R->off[n] = R->buf.size();
+        *out = R.release();
+        return SB_OK;
+    } catch (const Error &e) {
+        set_last_error(e.what());
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        set_last_error("out of host memory");
+        return SB_ENOMEM;
+    } catch (const std::exception &e) {
+        set_last_error(e.what());
+        return SB_EINVAL;
+    }
+}
+
+int sb_json_out_get(const sb_json_out *o, const char **buf, size_t *len, const uint64_t **offsets,
+                    const uint8_t **status) {
+    if (!o || !buf || !len || !offsets || !status) return SB_EINVAL;
+    *buf = o->buf.data();
+    *len = o->buf.size();
+    *offsets = o->off.data();
+    *status = o->status.data();
+    return SB_OK;
+}
+
+void sb_json_out_free(sb_json_out *o) { delete o; }
+
+}  // extern "C"
