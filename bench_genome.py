@@ -118,7 +118,7 @@ def main_genome(args):
     sbat = prepare_shard_batch(store, sl)
     st = sbat.stats()
     sbat.free()
-    # Roofline of request_rows_kernel, priced on the bytes one launch must move
+    # Roofline of the request pass (eval + deliver), priced on the bytes it must move
     # at least once: per chain its 80 B descriptor, two
     # coarse-index entries (8 B), its row (40 B) and row offset (8 B); 24 B per
     # candidate in the union of the chain windows (POS 4 + VtHot 16 + record
@@ -136,7 +136,7 @@ def main_genome(args):
         try:
             tj = json.load(open(tf))
             if tj.get('records') == shape.n_total and tj.get('requests') == len(reqs) and \
-                    tj.get('kernel') == 'request_rows_kernel':
+                    tj.get('kernel') == 'request_pass':
                 traffic = tj.get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
@@ -183,9 +183,10 @@ def main_genome(args):
                    'parallelism': f'contig shards x{world} (+10 kb halo); request rows + hit lists delivered to '
                                   f'the {"first slice" if args.deliver == "first" else "rank 0"} rank over '
                                   f'{"RCCL" if world > 1 else "(no peer)"}'},
-        'step': 'request batch pass (request_rows_kernel: every request = one chain of its 10 kb slices, rows + '
-                'dense hit lists in request order, offsets by decoupled look-back) + exchange (all_gather of '
-                'counts, send/recv of straddling rows and hits); inputs resident in HBM',
+        'step': 'request batch pass (request_eval_kernel: every request = one chain of its 10 kb slices, rows + '
+                'hits staged per run; request_deliver_kernel: offsets by a decoupled look-back over tiles of runs, '
+                'dense hit lists in request order) + exchange (send/recv of straddling rows and hits); inputs '
+                'resident in HBM',
         'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
         'candidates_loaded_per_s': round(tot_cand * args.steps / elapsed, 1),
         'hits_per_step': int(tot_hits),
@@ -193,8 +194,9 @@ def main_genome(args):
                                'kernel_max': round(max(v[1] for v in allv), 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(r0[5], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(r0[5] / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                     'kernel': 'request_rows_kernel (rank 0): HIP events around K back-to-back launches on its '
-                               'stream, / K',
+                     'kernel': 'request pass = request_eval_kernel + request_deliver_kernel (rank 0): HIP events '
+                               'around K back-to-back passes on their stream, / K (rocprof per-kernel averages: '
+                               'profiles/)',
                      'algorithmic_bytes_per_launch': r0[7],
                      'pricing': 'bytes one launch must move at least once: 136 B/request (80 B chain descriptor + 2 '
                                 'index entries + 40 B row + 8 B row offset) + 24 B per candidate in the union of the '

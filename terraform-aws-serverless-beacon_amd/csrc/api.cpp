@@ -234,7 +234,8 @@ struct sb_batch {
         std::vector<RowRun> runs;
         uint64_t cap = 0;              // output hit capacity
         uint64_t n_chain_slices = 0;
-        DevMem dchains, druns, status, ticket, spill, lut, sseg, sherr;
+        uint32_t n_lut = 0;            // LUT words (request_rows_kernel stages them in LDS when they fit)
+        DevMem dchains, druns, status, tstatus, stage, row_src, lut, sseg, sherr;
         bool slices = false;           // some rows answered per slice (the batch's query part)
     };
     std::unique_ptr<Req> req;
@@ -3013,14 +3014,14 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     for (uint32_t o : owner) ++seg[o + 1];
     for (size_t w = 0; w < n; ++w) seg[w + 1] += seg[w];
     // runs of consecutive rows (<= kRunRows rows, kPackRun chains, kPackSlots slots)
-    uint64_t spill_total = 0;
+    uint64_t stage_total = 0;  // staging slots: every run's chain hit capacity, back to back
     {
-        RowRun cur{0, 0, 0, 0, 0, 0, 0};
+        RowRun cur{0, 0, 0, 0, 0, 0, kRunSimple};
         uint64_t cap = 0;
         auto close = [&](uint32_t row_hi) {
             cur.row_hi = row_hi;
-            cur.spill = spill_total;
-            if (cap > kRowHitBuf) spill_total += cap - kRowHitBuf;
+            cur.stage = stage_total;
+            stage_total += cap;
             R->runs.push_back(cur);
         };
         uint32_t c = 0;
@@ -3030,9 +3031,10 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
             if (i > cur.row_lo && (i - cur.row_lo == kRunRows || (ch && (cur.c_hi - cur.c_lo == pack_run_max() ||
                                                                            cur.n_slots + need > pack_slots_max())))) {
                 close(i);
-                cur = RowRun{i, i, c, c, 0, 0, 0};
+                cur = RowRun{i, i, c, c, 0, 0, kRunSimple};
                 cap = 0;
             }
+            if (cls[i] == 2) cur.flags &= ~kRunSimple;  // a row answered per slice: gathered row by row
             if (ch) {
                 cur.c_hi = ++c;
                 cur.n_slots += need;
@@ -3050,9 +3052,13 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     R->dchains.alloc(R->chains.size() * sizeof(ChainDev));
     R->druns.alloc(R->runs.size() * sizeof(RowRun));
     R->status.alloc(R->runs.size() * 8);
-    R->ticket.alloc(4);
-    R->spill.alloc(spill_total * 8);
+    R->tstatus.alloc(size_t(request_tiles(static_cast<uint32_t>(R->runs.size()))) * 8);
+    R->stage.alloc(stage_total * 8);
+    R->row_src.alloc(R->slices || std::any_of(R->runs.begin(), R->runs.end(),
+                                              [](const RowRun &r) { return !(r.flags & kRunSimple); })
+                         ? size_t(n) * 8 : 0);
     R->lut.alloc(lut_all.size() * 4);
+    R->n_lut = static_cast<uint32_t>(lut_all.size());
     if (!R->chains.empty())
         HIP_OK(hipMemcpyAsync(R->dchains.p, R->chains.data(), R->chains.size() * sizeof(ChainDev),
                               hipMemcpyHostToDevice, st));
@@ -3080,8 +3086,6 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = B.strm();
     mark_run(B);
-    HIP_OK(hipMemsetAsync(R.ticket.p, 0, 4, st));
-    if (!R.runs.empty()) HIP_OK(hipMemsetAsync(R.status.p, 0, R.runs.size() * 8, st));
     if (R.slices) {  // the per-slice part, then its rows (chain rows come out zero; the row kernel writes them)
         run_kernels(B);
         launch_request_reduce(B.res.as<QRes>(), R.sseg.as<uint32_t>(), R.sherr.as<uint8_t>(), R.n_rows,
@@ -3090,11 +3094,11 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
     DStore d = s.d;
     d.sym_lut = R.lut.as<uint32_t>();
     launch_request_rows(d, R.dchains.as<ChainDev>(), R.druns.as<RowRun>(), static_cast<uint32_t>(R.runs.size()),
-                        R.ticket.as<uint32_t>(), R.status.as<unsigned long long>(),
-                        R.slices ? B.res.as<QRes>() : nullptr, R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(),
-                        R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(), static_cast<ReqPartial *>(rows),
-                        static_cast<uint64_t *>(row_off), static_cast<uint64_t *>(hits), R.spill.as<uint64_t>(),
-                        R.n_rows, rec_base, st);
+                        R.status.as<unsigned long long>(), R.tstatus.as<unsigned long long>(),
+                        R.slices ? B.res.as<QRes>() : nullptr,
+                        R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
+                        static_cast<ReqPartial *>(rows), static_cast<uint64_t *>(row_off), R.row_src.as<uint64_t>(),
+                        R.stage.as<uint64_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, st);
     HIP_OK(hipGetLastError());
 }
 
@@ -3444,8 +3448,15 @@ void append_variant(std::string &o, const sb_store &s, const std::string &chrom,
     char num[16];
     o += chrom;
     o.push_back('\t');
-    const int nn = snprintf(num, sizeof num, "%u", s.h_pos[rec]);
-    o.append(num, static_cast<size_t>(nn));
+    {  // decimal POS (no snprintf: millions of variant strings per batch)
+        uint32_t v = s.h_pos[rec];
+        char *e = num + sizeof num, *q = e;
+        do {
+            *--q = static_cast<char>('0' + v % 10);
+            v /= 10;
+        } while (v);
+        o.append(q, static_cast<size_t>(e - q));
+    }
     o.push_back('\t');
     o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_ref_off[rec]), s.h_end[rec] - s.h_pos[rec] + 1);
     o.push_back('\t');

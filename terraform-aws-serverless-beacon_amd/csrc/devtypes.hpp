@@ -210,20 +210,21 @@ static_assert(sizeof(ChainDev) == 80, "ChainDev is five 16-byte words");
 constexpr uint32_t kChainEndVoid = 1u << 8;  // no END can match
 
 // Request batches (sb_requests_prepare / sb_requests_run): every request is a
-// row; request_rows_kernel answers one run of consecutive rows per wave --
+// row; request_eval_kernel answers one run of consecutive rows per wave --
 // the rows' chains (ChainDev::s0 = the chain's row) evaluated as
-// chain_pack_kernel does, the other rows' hits (per-slice queries answered
-// before) gathered -- and writes the rows, their offsets and their hits
-// densely in row order at the run's offset, found by a decoupled look-back
-// over the runs (status words, one ticket counter).
-constexpr uint32_t kRunRows = 64;    // rows per run at most (one lane each)
-constexpr uint32_t kRowHitBuf = 256; // chain hits a wave stages in LDS; the rest spill to global
+// chain_pack_kernel does, their hits appended to the run's staging region --
+// and request_deliver_kernel writes the rows' offsets and hits densely in row
+// order at the run's offset, found by a decoupled look-back over the runs'
+// status words (the other rows' hits, from per-slice queries answered
+// before, gathered there too).
+constexpr uint32_t kRunRows = 64;     // rows per run at most (one lane each)
+constexpr uint32_t kRunSimple = 1u;   // RowRun::flags: no row of the run is answered per slice
 struct alignas(16) RowRun {
     uint32_t row_lo, row_hi;  // rows [row_lo, row_hi)
     uint32_t c_lo, c_hi;      // the run's chains, rows increasing
-    uint64_t spill;           // first spill slot of the run (hits past kRowHitBuf)
+    uint64_t stage;           // first staging slot of the run (its chains' hit capacity follows)
     uint32_t n_slots;         // slices of its chains (<= 256)
-    uint32_t pad;
+    uint32_t flags;           // kRunSimple
 };
 static_assert(sizeof(RowRun) == 32, "RowRun is two 16-byte words");
 

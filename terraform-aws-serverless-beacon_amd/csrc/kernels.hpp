@@ -105,10 +105,11 @@ void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, ui
 // status zeroed by the caller; status n_runs words).  sres..shits: the
 // batch's per-slice part (rows of it already reduced into `rows`), or null.
 void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun *runs, uint32_t n_runs,
-                         uint32_t *ticket, unsigned long long *status, const QRes *sres, const uint32_t *sseg,
-                         const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits, ReqPartial *rows,
-                         uint64_t *row_off, uint64_t *out, uint64_t *spill, uint32_t n_rows, uint64_t rec_base,
-                         hipStream_t s);
+                         unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
+                         const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
+                         ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,
+                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, hipStream_t s);
+uint32_t request_tiles(uint32_t n_runs);
 
 // Fetch-time gather of every query's hits into one dense array.
 void launch_compact(const uint64_t *hit_off, const uint64_t *dense_off, const QRes *res, uint32_t nq,

@@ -41,6 +41,9 @@ constexpr int kVtWindow = 4;     // 16-byte VtHot: 16 VGPRs (a 1000G-shape slice
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+    return (static_cast<uint64_t>(uniform(static_cast<uint32_t>(v >> 32))) << 32) | uniform(static_cast<uint32_t>(v));
+}
 
 // lane k's value, k wave-uniform (v_readlane into an SGPR)
 __device__ __forceinline__ uint32_t rdl(uint32_t v, uint32_t k) {
@@ -1888,31 +1891,38 @@ __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__res
 }
 
 // ---------------------------------------------------------------- request rows
-// Request batches (sb_requests_run, devtypes.hpp RowRun): one wave per run of
-// consecutive request rows (ticket order, so a wave only ever waits on runs
-// whose waves already started).  The run's chains are evaluated as in
-// chain_pack_kernel (rows only: per-slice exists bits + chain totals), with
-// two changes: each candidate lane finds its chain by a wave-uniform walk over
-// the few chains that start inside its chunk (v_readlane of the lane-held
-// prefixes: no binary search, no ds_bpermute), and hits are appended to an
-// LDS buffer in candidate order -- which is chain order, which is row order
-// -- instead of scattered into per-chain regions.  Once the run's hit count
-// is known its output offset comes from a decoupled look-back over the
-// runs' status words (aggregate / inclusive prefix), and the wave writes its
-// rows, row offsets and hits densely at that offset: no capacity-sized hit
-// regions, no gather kernel.  Rows answered per slice (queries of the batch's
-// slice part, reduced into `rows` by request_reduce before this kernel) are
-// gathered from their hit regions in row order.
+// Request batches (sb_requests_run, devtypes.hpp RowRun), two launches:
+//
+// request_eval_kernel -- one wave per run of consecutive request rows (XCD-
+// aware block order; no inter-wave dependency).  The run's chains are
+// evaluated as in chain_pack_kernel (rows only: per-slice exists bits + chain
+// totals), with two changes: each candidate lane finds its chain by a
+// wave-uniform walk over the few chains that start inside its chunk
+// (v_readlane of the lane-held prefixes: no binary search, no ds_bpermute),
+// and hits are appended in candidate order -- which is chain order, which is
+// row order -- to the run's staging region (capacity planned on the host).
+// The wave writes its rows, each row's hit count (into row_off) and the run's
+// total as an aggregate status word.
+//
+// request_deliver_kernel -- one wave per run: the run's output offset by a
+// decoupled look-back over the status words (every aggregate is already
+// published, so no wave ever waits), row offsets, and the hits copied to the
+// dense output: one contiguous copy for a run of chain rows only; row by row
+// where some rows were answered per slice (queries of the batch's slice part,
+// reduced into `rows` by request_reduce before the first kernel).
+//
+// A single-pass form (hits held in LDS until the look-back resolved) made
+// every wave wait for its slowest predecessor's evaluation: 0.27 ms vs the two
+// launches' sum.
 struct ReqLds {
     uint4 pred[kPackRun * 3];  // per chain: {first, last, n, width}, {e0, espan, vlo, vspan},
                                // {class mask, extra-ALT bits | end_void << 31, 1/width (f32), LUT offset}
     unsigned long long tcc[kPackRun], tan[kPackRun];
     unsigned int exw[kPackSlots / 32];  // bit = the slot's slice exists
     unsigned int slow[kPackRun];
-    unsigned int cstart[kPackRun + 1];  // buffer position of each chain's first candidate (~0: none)
+    unsigned int cstart[kPackRun + 1];  // staging position of each chain's first hit (~0: none)
     unsigned int ccount[kPackRun];
     uint8_t rowchain[kRunRows];         // row (run-relative) -> its chain (0xff: not a chain row)
-    unsigned long long hbuf[kRowHitBuf];
 };
 
 // Decoupled look-back over one 64-bit status word per run {flag : 2 | value :
@@ -1921,17 +1931,17 @@ struct ReqLds {
 // loads are enough -- no release / acquire fences, which on gfx950 are an XCD
 // L2 write-back / an L1 invalidate of microseconds EACH (one per poll made the
 // serial form of this loop ~0.9 us per run).  The wave reads 64 predecessors per
-// round (lane j: run top - j) and stops at the nearest inclusive prefix.  A run
-// only waits on runs with earlier tickets, which are resident: no deadlock.
+// round (lane j: run top - j) and stops at the nearest inclusive prefix.
 // Returns the exclusive prefix (wave-uniform) and publishes excl + H.
 __device__ __forceinline__ uint64_t lookback_exclusive(unsigned long long *__restrict__ status, uint32_t w,
                                                        uint64_t H) {
     constexpr unsigned long long kAgg = 1ull << 62, kPre = 2ull << 62, kVal = (1ull << 62) - 1;
     const uint32_t ul = static_cast<uint32_t>(lane_id());
+    // the aggregate first: successors sum it instead of waiting for this prefix
     if (ul == 0) __hip_atomic_store(&status[w], kAgg | H, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t excl = 0;
     int64_t top = static_cast<int64_t>(w) - 1;
-    uint32_t spins = 0;  // bounded: a predecessor takes microseconds; never hang the queue
+    uint32_t spins = 0;  // bounded: never hang the queue
     while (top >= 0) {
         const int64_t j = top - static_cast<int64_t>(ul);
         const unsigned long long s =
@@ -1959,33 +1969,34 @@ struct RowChunk {
     bool first;      // the lane holds its chain's first candidate
 };
 
-// Eight waves per workgroup and ONE ticket per workgroup: a single device-scope
-// counter serves at most ~88 returning atomics per microsecond (guide,
-// `dequeue`), so a ticket per wave (31 k runs at config 3) cost ~0.35 ms of
-// the 0.47 ms launch.  Wave k of ticket t answers run 8 t + k; a run waits only
-// on lower runs, whose workgroups already hold their tickets (resident): no
-// assumption on dispatch order or placement.
-constexpr int kReqWaves = 8;
-constexpr int kReqBlock = kReqWaves * kWave;
+// the batch's symbolic-ALT LUT words (8 per distinct variantType string) are
+// staged in LDS once per workgroup when they fit: a predicate's LUT word is
+// then an LDS read, not a dependent global load behind the candidate's load
+constexpr uint32_t kReqLut = 512;
+constexpr uint32_t kDeliverTile = 16;  // runs per request_deliver_kernel wave
 
-__global__ __launch_bounds__(kReqBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_rows_kernel(
+template <bool LDS_LUT>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_eval_kernel(
     DStore st, const ChainDev *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
-    uint32_t *__restrict__ ticket, unsigned long long *__restrict__ status, const QRes *__restrict__ sres,
-    const uint32_t *__restrict__ sseg, const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr,
-    const uint64_t *__restrict__ shits, ReqPartial *__restrict__ rows, uint64_t *__restrict__ row_off,
-    uint64_t *__restrict__ out, uint64_t *__restrict__ spill, uint32_t n_rows, uint64_t rec_base) {
-    __shared__ ReqLds lds_all[kReqWaves];
-    __shared__ uint32_t blk_ticket;
+    unsigned long long *__restrict__ status, unsigned long long *__restrict__ tstatus, const QRes *__restrict__ sres,
+    ReqPartial *__restrict__ rows, uint64_t *__restrict__ row_cnt, uint64_t *__restrict__ row_src,
+    uint64_t *__restrict__ stage, uint32_t n_lut, uint32_t n_tiles) {
+    __shared__ ReqLds lds_all[kWavesPerBlock];
+    __shared__ uint32_t slut[LDS_LUT ? kReqLut : 1];
     ReqLds &L = lds_all[threadIdx.x >> 6];
     const uint32_t ul = static_cast<uint32_t>(lane_id());
-    if (threadIdx.x == 0) blk_ticket = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const uint32_t w = uniform(blk_ticket) * kReqWaves + (threadIdx.x >> 6);
+    if constexpr (LDS_LUT) {
+        for (uint32_t i = threadIdx.x; i < n_lut; i += kBlock) slut[i] = st.sym_lut[i];
+        __syncthreads();
+    }
+    const uint32_t *lut_base = LDS_LUT ? slut : st.sym_lut;
+    const uint32_t w = launch_wave();
     if (w >= n_runs) return;
     const uint32_t row_lo = uniform(runs[w].row_lo), row_hi = uniform(runs[w].row_hi);
     const uint32_t c_lo = uniform(runs[w].c_lo), R = uniform(runs[w].c_hi) - c_lo;
-    const uint64_t spill_at = (static_cast<uint64_t>(uniform(static_cast<uint32_t>(runs[w].spill >> 32))) << 32) |
-                              uniform(static_cast<uint32_t>(runs[w].spill));
+    const uint64_t stage_at = (static_cast<uint64_t>(uniform(static_cast<uint32_t>(runs[w].stage >> 32))) << 32) |
+                              uniform(static_cast<uint32_t>(runs[w].stage));
+    const bool simple = (uniform(runs[w].flags) & kRunSimple) != 0;
     const uint32_t nrows = row_hi - row_lo;
     // ---- setup: lane k < R = chain k (descriptor, predicate constants, candidate bounds)
     uint32_t rowk = 0, c0 = 0, cnt = 0, nsl = 0;
@@ -2057,10 +2068,7 @@ __global__ __launch_bounds__(kReqBlock) __attribute__((amdgpu_waves_per_eu(8, 8)
         return c;
     };
     uint32_t hpos = 0;  // hits appended so far (wave-uniform)
-    auto put_hit = [&](uint32_t at, uint64_t v) {
-        if (at < kRowHitBuf) L.hbuf[at] = v;
-        else spill[spill_at + (at - kRowHitBuf)] = v;
-    };
+    uint64_t *const sdst = stage + stage_at;  // the run's staging region (capacity planned on the host)
     auto eval = [&](const RowChunk &c, uint32_t base) {
         const ChainChunk &x = c.x;
         const uint32_t k = c.k;
@@ -2068,7 +2076,7 @@ __global__ __launch_bounds__(kReqBlock) __attribute__((amdgpu_waves_per_eu(8, 8)
         const bool valid = g < T;
         const uint4 p0 = L.pred[3 * k], p1 = L.pred[3 * k + 1], p2 = L.pred[3 * k + 2];
         const uint32_t first = p0.x, last = p0.y, n = p0.z, width = p0.w;
-        VtPred Pd(p1.x, p1.y, p1.z, p1.w, p2.x, p2.y & 0x7fffffffu, (p2.y >> 31) != 0, st.sym_lut + p2.w);
+        VtPred Pd(p1.x, p1.y, p1.z, p1.w, p2.x, p2.y & 0x7fffffffu, (p2.y >> 31) != 0, lut_base + p2.w);
         const bool inwin = valid && x.p >= first && x.p <= last;
         const bool cand = inwin && Pd.end_ok(x.h.end);
         if (cand && (x.h.w & VT_SLOW)) L.slow[k] = 1u;  // never: prepare sends such requests per slice
@@ -2098,7 +2106,7 @@ __global__ __launch_bounds__(kReqBlock) __attribute__((amdgpu_waves_per_eu(8, 8)
         if (cn) {
             uint32_t at = hpos + pre;
             for (uint64_t b = o.em; b; b &= b - 1)
-                put_hit(at++, static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift));
+                sdst[at++] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
         }
         hpos += tot;
         if (hit) {
@@ -2143,11 +2151,9 @@ __global__ __launch_bounds__(kReqBlock) __attribute__((amdgpu_waves_per_eu(8, 8)
         if (ul + static_cast<uint32_t>(d) <= R) cs = min(cs, t);
     }
     const uint32_t cs_next = __shfl_down(cs, 1, kWave);
-    bool bad = false;  // a VT_SLOW candidate in some chain's window (its row raises; never for prepared chains)
     ReqPartial part{0, 0, 0, 0, 0};
     if (ul < R) {
-        const bool slow = L.slow[ul] != 0;
-        bad = slow;
+        const bool slow = L.slow[ul] != 0;  // a VT_SLOW candidate in the window: never for prepared chains
         int64_t ex = 0;
 #pragma unroll
         for (uint32_t q = 0; q < kPackSlots / 32; ++q) {
@@ -2162,49 +2168,140 @@ __global__ __launch_bounds__(kReqBlock) __attribute__((amdgpu_waves_per_eu(8, 8)
                     : ReqPartial{ex, static_cast<int64_t>(nv), static_cast<int64_t>(L.tcc[ul]),
                                  static_cast<int64_t>(L.tan[ul]), 0};
     }
-    const bool any_slow = __ballot(bad) != 0;
     wave_lds_sync();
-    // ---- rows (lane i < nrows = row row_lo + i): hit counts -> run-local offsets
+    // ---- rows (lane i < nrows = row row_lo + i): partials, hit counts, staging starts
     const uint32_t row = row_lo + ul;
     const uint32_t ch = ul < nrows ? L.rowchain[ul] : 0xffu;
     uint64_t nvr = 0;
     if (ul < nrows) nvr = ch != 0xffu ? L.ccount[ch] : (sres ? static_cast<uint64_t>(rows[row].n_variants) : 0ull);
-    const bool slice_hits = ul < nrows && ch == 0xffu && nvr != 0;
-    const bool simple = !any_slow && !__ballot(slice_hits);  // buffer order = row order
-    const uint64_t linc = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(nvr)));
-    const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(linc), kWave - 1));
-    // ---- decoupled look-back: this run's offset = the hits of every earlier run
-    const uint64_t O = lookback_exclusive(status, w, H);
-    // ---- outputs
-    if (ul < nrows) row_off[row] = O + linc - nvr;
-    if (row_hi == n_rows && ul == 0) row_off[n_rows] = O + H;
     if (ul < R) rows[rowk] = part;
     if (!sres && ul < nrows && ch == 0xffu) rows[row] = ReqPartial{0, 0, 0, 0, 0};
-    if (simple) {  // chain rows (and empty rows) only: the buffer is the output
-        for (uint64_t j = ul; j < H; j += kWave)
-            out[O + j] = (j < kRowHitBuf ? L.hbuf[j] : spill[spill_at + (j - kRowHitBuf)]) + rec_base;
-        return;
+    if (ul < nrows) {
+        row_cnt[row] = nvr;
+        if (!simple && ch != 0xffu) row_src[row] = stage_at + L.cstart[ch];
     }
-    for (uint32_t i = 0; i < nrows; ++i) {  // row by row (some rows answered per slice)
-        const uint64_t nv = static_cast<uint64_t>(rdl64(static_cast<int64_t>(nvr), i));
-        if (!nv) continue;
-        const uint64_t at = O + static_cast<uint64_t>(rdl64(static_cast<int64_t>(linc), i)) - nv;
-        const uint32_t k = L.rowchain[i];
-        if (k != 0xffu) {
-            const uint32_t s0 = L.cstart[k];
-            for (uint64_t j = ul; j < nv; j += kWave) {
-                const uint64_t p = s0 + j;
-                out[at + j] = (p < kRowHitBuf ? L.hbuf[p] : spill[spill_at + (p - kRowHitBuf)]) + rec_base;
+    const uint64_t H = static_cast<uint64_t>(rdl64(wave_incl_scan_i64(static_cast<int64_t>(nvr)), kWave - 1));
+    if (ul == 0) {  // read by request_deliver_kernel (kernel boundary)
+        status[w] = H;
+        // tile and super-tile totals (zeroed before this launch): tstatus[t] for
+        // tile t, tstatus[n_tiles + u] for tiles [64 u, 64 u + 64)
+        atomicAdd(&tstatus[w / kDeliverTile], static_cast<unsigned long long>(H));
+        atomicAdd(&tstatus[n_tiles + w / (kDeliverTile * kWave)], static_cast<unsigned long long>(H));
+    }
+}
+
+// request_deliver_kernel: one wave per TILE of kDeliverTile consecutive runs.
+// request_eval_kernel left every run's hit total and added it to its tile's
+// total, so a tile's output offset is the plain sum of the earlier tiles'
+// totals: the totals of the earlier super-tiles (64 tiles each) and of the
+// earlier tiles of its own super-tile, one load per lane each (an in-launch
+// look-back, or a strided loop over the tiles, is a chain of dependent
+// ~1-2 us loads: 0.1 ms for the launch),
+// and a tile of chain runs is copied as ONE contiguous range of ~4 k hits:
+// output position p belongs to the last run of the tile whose exclusive
+// offset is <= p (offsets held one per lane; a 15-step wave-uniform compare).
+__global__ __launch_bounds__(kBlock) void request_deliver_kernel(
+    const RowRun *__restrict__ runs, uint32_t n_runs, const unsigned long long *__restrict__ status,
+    const unsigned long long *__restrict__ tstatus, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
+    const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr, const uint64_t *__restrict__ shits,
+    uint64_t *__restrict__ row_off, const uint64_t *__restrict__ row_src, const uint64_t *__restrict__ stage,
+    uint64_t *__restrict__ out, uint32_t n_rows, uint64_t rec_base) {
+    const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    const uint32_t t0 = w * kDeliverTile;
+    if (t0 >= n_runs) return;
+    const uint32_t ul = static_cast<uint32_t>(lane_id());
+    const uint32_t nr = min(kDeliverTile, n_runs - t0);
+    // lane j < nr: run t0 + j
+    uint64_t Hj = 0, stj = 0;
+    uint32_t rlo = 0, rhi = 0;
+    bool simple = true;
+    if (ul < nr) {
+        const RowRun rr = runs[t0 + ul];
+        Hj = status[t0 + ul];
+        stj = rr.stage;
+        rlo = rr.row_lo;
+        rhi = rr.row_hi;
+        simple = (rr.flags & kRunSimple) != 0;
+    }
+    const uint64_t incl = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(Hj)));
+    const uint64_t T = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl), kWave - 1));
+    const uint64_t excl = incl - Hj;
+    // the tile's offset: every earlier tile's total (request_eval_kernel added
+    // them up), summed directly -- independent loads, no look-back chain
+    const uint32_t n_tiles = (n_runs + kDeliverTile - 1) / kDeliverTile, sup = w / kWave;
+    uint64_t part = 0;
+    for (uint32_t u = ul; u < sup; u += kWave) part += tstatus[n_tiles + u];  // earlier super-tiles (one load per lane
+                                                                             // below 65 k runs)
+    if (kWave * sup + ul < w) part += tstatus[kWave * sup + ul];             // earlier tiles of this super-tile
+    const uint64_t O = static_cast<uint64_t>(rdl64(wave_incl_scan_i64(static_cast<int64_t>(part)), kWave - 1));
+    const bool all_simple = !__ballot(!simple);
+    // every run's row counts (left in row_off) loaded up front: one round trip
+    // for the tile, not one per run
+    uint64_t cnt[kDeliverTile];
+#pragma unroll
+    for (uint32_t j = 0; j < kDeliverTile; ++j) {
+        const uint32_t a = rdl(rlo, j < nr ? j : 0u), b = j < nr ? rdl(rhi, j) : a;
+        cnt[j] = a + ul < b ? row_off[a + ul] : 0ull;
+    }
+    // row offsets, run by run: lane i = row rlo_j + i; a tile with rows
+    // answered per slice copies run by run here
+#pragma unroll
+    for (uint32_t j = 0; j < kDeliverTile; ++j) {
+        if (j >= nr) break;
+        const uint32_t a = rdl(rlo, j), b = rdl(rhi, j);
+        const uint64_t base = O + static_cast<uint64_t>(rdl64(static_cast<int64_t>(excl), j));
+        const uint32_t row = a + ul;
+        const uint64_t c = cnt[j];
+        const uint64_t off = base + static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(c))) - c;
+        if (row < b) row_off[row] = off;
+        if (all_simple) continue;
+        const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(Hj), j));
+        if (!H) continue;
+        if (__shfl(simple ? 1 : 0, static_cast<int>(j), kWave)) {  // chain rows only: one contiguous copy
+            const uint64_t st0 = static_cast<uint64_t>(rdl64(static_cast<int64_t>(stj), j));
+            for (uint64_t q = ul; q < H; q += kWave) out[base + q] = stage[st0 + q] + rec_base;
+            continue;
+        }
+        for (uint32_t i = 0; i < b - a; ++i) {  // row by row
+            const uint64_t nv = static_cast<uint64_t>(rdl64(static_cast<int64_t>(c), i));
+            if (!nv) continue;
+            const uint64_t at = static_cast<uint64_t>(rdl64(static_cast<int64_t>(off), i));
+            const uint32_t r = a + i;
+            const uint32_t q0 = uniform(sseg[r]), q1 = uniform(sseg[r + 1]);
+            if (q1 == q0) {  // a chain row: its hits are contiguous in the staging region
+                const uint64_t src = uniform64(row_src[r]);
+                for (uint64_t k = ul; k < nv; k += kWave) out[at + k] = stage[src + k] + rec_base;
+            } else {
+                uint64_t dst = at;
+                for (uint32_t q = q0; q < q1; ++q) {
+                    const QRes rq = sres[q];
+                    if (rq.error || sherr[q]) continue;
+                    const uint64_t src = shoff[q];
+                    for (uint32_t k = ul; k < rq.n_hits; k += kWave) out[dst + k] = shits[src + k] + rec_base;
+                    dst += rq.n_hits;
+                }
             }
-        } else {
-            uint64_t dst = at;
-            for (uint32_t q = sseg[row_lo + i], qe = sseg[row_lo + i + 1]; q < qe; ++q) {
-                const QRes r = sres[q];
-                if (r.error || sherr[q]) continue;
-                const uint64_t src = shoff[q];
-                for (uint32_t j = ul; j < r.n_hits; j += kWave) out[dst + j] = shits[src + j] + rec_base;
-                dst += r.n_hits;
-            }
+        }
+    }
+    if (t0 + nr == n_runs && ul == 0) row_off[n_rows] = O + T;
+    if (!all_simple) return;
+    // chain runs only: their staging regions hold the tile's hits in order
+    const int64_t delta = static_cast<int64_t>(stj - excl);  // staging slot = p + delta_j
+    constexpr uint32_t kU = 4;
+    for (uint64_t p0 = 0; p0 < T; p0 += kWave * kU) {
+        uint64_t v[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint64_t p = p0 + kWave * u + ul;
+            int64_t d = rdl64(delta, 0);
+            for (uint32_t k = 1; k < nr; ++k)
+                if (p >= static_cast<uint64_t>(rdl64(static_cast<int64_t>(excl), k))) d = rdl64(delta, k);
+            v[u] = p < T ? stage[static_cast<uint64_t>(static_cast<int64_t>(p) + d)] : 0ull;
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint64_t p = p0 + kWave * u + ul;
+            if (p < T) out[O + p] = v[u] + rec_base;
         }
     }
 }
@@ -3364,17 +3461,32 @@ void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, ui
 }
 
 void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun *runs, uint32_t n_runs,
-                         uint32_t *ticket, unsigned long long *status, const QRes *sres, const uint32_t *sseg,
-                         const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits, ReqPartial *rows,
-                         uint64_t *row_off, uint64_t *out, uint64_t *spill, uint32_t n_rows, uint64_t rec_base,
-                         hipStream_t s) {
+                         unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
+                         const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
+                         ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,
+                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, hipStream_t s) {
     if (!n_runs) {
         (void)hipMemsetAsync(row_off, 0, 8, s);
         return;
     }
-    hipLaunchKernelGGL(request_rows_kernel, dim3((n_runs + kReqWaves - 1) / kReqWaves), dim3(kReqBlock), 0, s, st,
-                       chains, runs, n_runs,
-                       ticket, status, sres, sseg, shoff, sherr, shits, rows, row_off, out, spill, n_rows, rec_base);
+    const dim3 grid(blocks_for(n_runs));
+    const uint32_t n_tiles = (n_runs + kDeliverTile - 1) / kDeliverTile;
+    (void)hipMemsetAsync(tstatus, 0, size_t(request_tiles(n_runs)) * 8, s);
+    if (n_lut <= kReqLut)
+        hipLaunchKernelGGL(request_eval_kernel<true>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status,
+                           tstatus, sres, rows, row_off, row_src, stage, n_lut, n_tiles);
+    else
+        hipLaunchKernelGGL(request_eval_kernel<false>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status,
+                           tstatus, sres, rows, row_off, row_src, stage, n_lut, n_tiles);
+    const uint32_t tiles = (n_runs + kDeliverTile - 1) / kDeliverTile;
+    hipLaunchKernelGGL(request_deliver_kernel, dim3(blocks_for(tiles)), dim3(kBlock), 0, s, runs, n_runs, status,
+                       tstatus, sres, sseg, shoff, sherr, shits, row_off, row_src, stage, out, n_rows, rec_base);
+}
+
+// words of tstatus: the tile totals, then the super-tile totals
+uint32_t request_tiles(uint32_t n_runs) {
+    const uint32_t t = (n_runs + kDeliverTile - 1) / kDeliverTile;
+    return t + (t + kWave - 1) / kWave;
 }
 
 uint32_t pack_run_max() { return kPackRun; }

@@ -19,6 +19,8 @@
 //
 // Only the public C ABI (include/sbeacon.h) is used below the parser.
 #include <algorithm>
+#include <chrono>
+#include <cstdlib>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -31,7 +33,8 @@
 #include "common.hpp"
 
 struct sb_json_out {
-    std::string buf;
+    std::unique_ptr<char[]> buf;  // n bytes (uninitialised storage: filled in parallel)
+    uint64_t n = 0;
     std::vector<uint64_t> off;   // n + 1
     std::vector<uint8_t> status;  // 0 answered, 1 = answer through the Python handler
 };
@@ -503,6 +506,17 @@ bool put_jstr(std::string &o, const char *s, size_t n) {
     };
     o.push_back('"');
     for (size_t i = 0; i < n;) {
+        size_t r = i;  // a run of printable ASCII other than '"' and '\\' is copied as is
+        while (r < n) {
+            const unsigned char x = static_cast<unsigned char>(s[r]);
+            if (x < 0x20 || x >= 0x7f || x == '"' || x == '\\') break;
+            ++r;
+        }
+        if (r > i) {
+            o.append(s + i, r - i);
+            i = r;
+            if (i >= n) break;
+        }
         const unsigned char c = static_cast<unsigned char>(s[i]);
         if (c < 0x80) {
             switch (c) {
@@ -589,10 +603,11 @@ bool put_limbs(std::string &o, const uint32_t *l, uint32_t n) {
 }
 
 // what json.dumps raises for an int past CPython's digit limit
-void put_digits_error(std::string &o) {
+void put_digits_error(std::string &o, size_t start) {
     static const char kMsg[] =
         "Exceeds the limit (4300) for integer string conversion; use sys.set_int_max_str_digits() to increase the limit";
-    o = "{\"errorMessage\": ";
+    o.resize(start);  // drop the response written so far
+    o += "{\"errorMessage\": ";
     put_jstr(o, kMsg, sizeof kMsg - 1);
     o += ", \"errorType\": \"ValueError\"}";
 }
@@ -618,6 +633,7 @@ void put_error(std::string &o, int32_t err) {
 // json.dumps(PerformQueryResponse.dump()) for query i of rs (engine.py
 // ResultSet.responses); false = text the Python path could not decode
 bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
+    const size_t start = o.size();  // o may already hold earlier responses
     sb_result_view v;
     if (sb_result_get(rs, i, &v) != SB_OK) return false;
     if (v.error) {
@@ -636,7 +652,7 @@ bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
     o += ", \"all_alleles_count\": ";
     if (v.big_limbs) {
         if (!put_limbs(o, v.big_all_alleles_count, v.big_limbs)) {
-            put_digits_error(o);
+            put_digits_error(o, start);
             return true;
         }
     } else {
@@ -645,6 +661,7 @@ bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
     o += ", \"variants\": [";
     if (v.n_variants) {
         if (sb_result_variants_text(rs, i, &tp, &tn) != SB_OK) return false;
+        o.reserve(o.size() + tn + 4 * v.n_variants + 256);
         size_t a = 0;
         for (size_t k = 0; k <= tn; ++k) {
             if (k == tn || tp[k] == '\n') {
@@ -657,7 +674,7 @@ bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
     o += "], \"call_count\": ";
     if (v.big_limbs) {
         if (!put_limbs(o, v.big_call_count, v.big_limbs)) {
-            put_digits_error(o);
+            put_digits_error(o, start);
             return true;
         }
     } else {
@@ -718,15 +735,30 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
             if (offsets[i + 1] < offsets[i]) throw Error(SB_EINVAL, "offsets not non-decreasing");
         const unsigned threads = 16;
         const bool strict_vt = (flags & 1u) != 0;
+        // SBEACON_WIRE_TRACE=1: phase times to stderr (bench diagnostics)
+        const bool trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;
+        auto t_last = std::chrono::steady_clock::now();
+        auto tick = [&](const char *what) {
+            if (!trace) return;
+            const auto t = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "[wire] %-8s %8.2f ms\n", what,
+                         std::chrono::duration<double, std::milli>(t - t_last).count());
+            t_last = t;
+        };
         std::vector<Event> ev(n);
         par(n, threads, [&](size_t i, unsigned) {
             load_event(text + offsets[i], offsets[i + 1] - offsets[i], stores, n_stores, strict_vt, ev[i]);
             if (ev[i].ok) bind_strings(ev[i]);
         });
+        tick("parse");
         auto R = std::make_unique<sb_json_out>();
         R->status.assign(n, 1);
-        std::vector<std::string> parts(n);
-        // one device batch per store, events in input order
+        // each event's text goes to the buffer of the thread that formats it
+        // (thread k formats a contiguous range of its store's events); the
+        // buffers are then copied once, in parallel, into the output in event order
+        std::vector<uint32_t> where(n, 0);   // formatting thread
+        std::vector<uint64_t> pos(n, 0), len(n, 0);
+        std::vector<std::string> tbuf(threads);
         for (size_t k = 0; k < n_stores; ++k) {
             std::vector<uint32_t> idx;
             for (size_t i = 0; i < n; ++i)
@@ -738,26 +770,34 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
             const int rc = sb_query_batch(stores[k], qs.data(), qs.size(), 0, &rs);
             if (rc != SB_OK) return rc;  // sb_last_error holds the message
             std::unique_ptr<sb_result_set, void (*)(sb_result_set *)> keep(rs, sb_result_free);
-            par(idx.size(), threads, [&](size_t j, unsigned) {
+            tick("query");
+            par(idx.size(), threads, [&](size_t j, unsigned t) {
                 const uint32_t i = idx[j];
-                std::string o;
-                o.reserve(256);
+                std::string &o = tbuf[t];
+                const size_t at = o.size();
                 if (put_response(o, rs, j, ev[i])) {
-                    parts[i] = std::move(o);
+                    o.push_back('\n');
+                    where[i] = t;
+                    pos[i] = at;
+                    len[i] = o.size() - at;
                     R->status[i] = 0;
+                } else {
+                    o.resize(at);
                 }
             });
+            tick("format");
         }
-        size_t total = 0;
-        for (const auto &s : parts) total += s.size();
-        R->buf.reserve(total + n);
+        // JSON lines: every response ends with '\n' (none for status 1)
         R->off.resize(n + 1);
-        for (size_t i = 0; i < n; ++i) {  // JSON lines: every response ends with '\n'
-            R->off[i] = R->buf.size();
-            R->buf += parts[i];
-            R->buf.push_back('\n');
-        }
-        R->off[n] = R->buf.size();
+        R->off[0] = 0;
+        for (size_t i = 0; i < n; ++i) R->off[i + 1] = R->off[i] + len[i];
+        R->n = R->off[n];
+        R->buf.reset(new char[std::max<uint64_t>(R->n, 1)]);
+        char *dst = R->buf.get();
+        par(n, threads, [&](size_t i, unsigned) {
+            if (len[i]) memcpy(dst + R->off[i], tbuf[where[i]].data() + pos[i], len[i]);
+        });
+        tick("concat");
         *out = R.release();
         return SB_OK;
     } catch (const Error &e) {
@@ -775,8 +815,8 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
 int sb_json_out_get(const sb_json_out *o, const char **buf, size_t *len, const uint64_t **offsets,
                     const uint8_t **status) {
     if (!o || !buf || !len || !offsets || !status) return SB_EINVAL;
-    *buf = o->buf.data();
-    *len = o->buf.size();
+    *buf = o->buf.get();
+    *len = o->n;
     *offsets = o->off.data();
     *status = o->status.data();
     return SB_OK;

@@ -40,19 +40,30 @@ def _python_handler(text: str) -> str:
 class EventResponses:
     """The response texts of one event batch as JSON lines: response i is
     ``buf[offsets[i]:offsets[i + 1] - 1]`` (each line ends with '\\n');
-    ``fallback`` marks the events the Python handler answered."""
+    ``fallback`` marks the events the Python handler answered.  ``buf`` is a
+    read-only view of the library's buffer (no copy), valid while this
+    object lives."""
 
-    def __init__(self, buf: bytes, offsets: np.ndarray, fallback: np.ndarray):
-        self.buf, self.offsets, self.fallback = buf, offsets, fallback
+    def __init__(self, buf, offsets: np.ndarray, fallback: np.ndarray, handle=None):
+        self.buf, self.offsets, self.fallback, self._h = buf, offsets, fallback, handle
+
+    def __del__(self):
+        h, self._h = getattr(self, '_h', None), None
+        if h:
+            try:
+                self.buf = None
+                lib().sb_json_out_free(h)
+            except Exception:
+                pass
 
     def __len__(self):
         return len(self.offsets) - 1
 
     def __getitem__(self, i: int) -> str:
-        return self.buf[int(self.offsets[i]):int(self.offsets[i + 1]) - 1].decode()
+        return bytes(self.buf[int(self.offsets[i]):int(self.offsets[i + 1]) - 1]).decode()
 
     def texts(self) -> list[str]:
-        return self.buf.decode().split('\n')[:-1] if len(self) else []
+        return bytes(self.buf).decode().split('\n')[:-1] if len(self) else []
 
 
 def pack_events(events) -> tuple[bytes, np.ndarray]:
@@ -80,27 +91,33 @@ def perform_query_events_packed(buf: bytes, offsets: np.ndarray, *, stores=None,
         return EventResponses(b'', np.zeros(1, dtype=np.uint64), np.zeros(0, dtype=np.uint8))
     offsets = np.ascontiguousarray(offsets, dtype=np.uint64)
     handles = (C.c_void_p * max(len(stores), 1))(*[s.handle for s in stores])
-    src = C.create_string_buffer(buf, len(buf) + 1)
+    src = C.c_char_p(bytes(buf))  # the bytes object's own storage (no copy for bytes input)
     out = C.c_void_p()
     check(lib().sb_perform_query_events(handles, len(stores), C.cast(src, C.c_void_p), offsets.ctypes.data, n,
                                         1 if strict else 0, C.byref(out)))
+    p, ln, po, ps = C.c_void_p(), C.c_size_t(), C.c_void_p(), C.c_void_p()
     try:
-        p, ln, po, ps = C.c_void_p(), C.c_size_t(), C.c_void_p(), C.c_void_p()
         check(lib().sb_json_out_get(out, C.byref(p), C.byref(ln), C.byref(po), C.byref(ps)))
-        text = C.string_at(p, ln.value) if ln.value else b''
-        roff = np.ctypeslib.as_array(C.cast(po, C.POINTER(C.c_uint64)), shape=(n + 1,)).copy()
-        status = np.ctypeslib.as_array(C.cast(ps, C.POINTER(C.c_uint8)), shape=(n,)).copy()
+    except Exception:
+        lib().sb_json_out_free(out)
+        raise
+    view = memoryview((C.c_char * max(ln.value, 1)).from_address(p.value)).cast('B')[:ln.value] if ln.value \
+        else memoryview(b'')
+    roff = np.ctypeslib.as_array(C.cast(po, C.POINTER(C.c_uint64)), shape=(n + 1,))
+    status = np.ctypeslib.as_array(C.cast(ps, C.POINTER(C.c_uint8)), shape=(n,)).copy()
+    fb = np.flatnonzero(status)
+    if not len(fb):  # zero copy: the view stays valid while the result object holds the handle
+        return EventResponses(view.toreadonly(), roff, status, out)
+    # events outside the typed fast path: the Python handler
+    try:
+        parts = [bytes(view[int(roff[i]):int(roff[i + 1])]) for i in range(n)]
     finally:
         lib().sb_json_out_free(out)
-    fb = np.flatnonzero(status)
-    if len(fb):  # events outside the typed fast path: the Python handler
-        parts = [text[int(roff[i]):int(roff[i + 1])] for i in range(n)]
-        for i in fb.tolist():
-            parts[i] = _python_handler(buf[int(offsets[i]):int(offsets[i + 1])].decode()).encode() + b'\n'
-        text = b''.join(parts)
-        roff = np.zeros(n + 1, dtype=np.uint64)
-        roff[1:] = np.cumsum([len(x) for x in parts])
-    return EventResponses(text, roff, status)
+    for i in fb.tolist():
+        parts[i] = _python_handler(buf[int(offsets[i]):int(offsets[i + 1])].decode()).encode() + b'\n'
+    roff = np.zeros(n + 1, dtype=np.uint64)
+    roff[1:] = np.cumsum([len(x) for x in parts])
+    return EventResponses(memoryview(b''.join(parts)), roff, status)
 
 
 def perform_query_events(events, *, stores=None, strict_variant_type=None) -> list[str]:
