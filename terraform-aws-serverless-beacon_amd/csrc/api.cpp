@@ -25,6 +25,7 @@
 
 #include <zlib.h>
 
+#include "jsonesc.hpp"
 #include "kernels.hpp"
 #include "store.hpp"
 
@@ -266,6 +267,7 @@ struct sb_result_set {
     std::vector<std::string> vtext, ntext;
     std::vector<uint8_t> vbuilt, nbuilt;
     std::string distinct;                       // sb_result_distinct_variants
+    std::vector<std::string> vt_json;           // escaped VT strings (sb::result_prepare_json)
     std::vector<uint32_t> tmp_rec, tmp_alt;     // views for sb_result_get
     // queries whose counts need more than 64 bits: 2 x big_limbs limbs each
     uint32_t big_limbs = 0;
@@ -650,6 +652,7 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.dk.hash = dev_upload(s, dk_hash);
     {
         std::vector<KBody> body(dk_hash.size());
+        std::vector<uint64_t> word(dk_hash.size());
         for (size_t k = 0; k < body.size(); ++k) {
             const uint64_t t = dk_tail[k];
             uint32_t c0 = 0x100;  // first tail byte (none: 0x100)
@@ -660,8 +663,16 @@ void upload_store(sb_builder &b, sb_store &s) {
             }
             const bool disp = c0 >= '0' && c0 <= '9';
             body[k] = KBody{t, dk_pos[k], disp ? kKeyDisplaced : 0u};
+            // the exact class (dedup_kernels.hip exact_word with no leading digit): tail = c1 '_' c2
+            uint64_t code = 0;
+            if (!disp && !(t & kTailBlob) && dk_pos[k] != 0 && (t >> 56) == 3) {
+                const uint32_t c1 = t & 0xff, us = (t >> 8) & 0xff, c2 = (t >> 16) & 0xff;
+                if (us == '_' && c1 >= 1 && c1 <= 7 && c2 >= 1 && c2 <= 7) code = (c1 << 3) | c2;
+            }
+            word[k] = dk_pos[k] | (code << 32) | (disp ? kWordDisplaced : 0ull);
         }
         s.dk.body = dev_upload(s, body);
+        s.dk.word = dev_upload(s, word);
     }
     dk_blob.resize(dk_blob.size() + 16, 0);  // padding: the device compares blob tails by aligned words
     s.dk.blob = dev_upload(s, dk_blob);
@@ -3470,6 +3481,62 @@ void append_variant(std::string &o, const sb_store &s, const std::string &chrom,
     o += s.vt.items[s.h_vt[rec]];
 }
 }  // namespace
+
+}  // extern "C"
+
+namespace sb {
+void result_prepare_json(sb_result_set *r) {
+    if (!r->vt_json.empty()) return;
+    const auto &items = r->s->vt.items;
+    r->vt_json.resize(items.size());
+    for (size_t k = 0; k < items.size(); ++k)
+        if (!json_escape_append(r->vt_json[k], items[k].data(), items[k].size())) r->vt_json[k] = std::string("\x01");
+}
+
+bool result_variants_json(const sb_result_set *r, size_t i, std::string &o) {
+    const sb_store &s = *r->s;
+    const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
+    std::string chrom;
+    if (!json_escape_append(chrom, r->chrom[i].data(), r->chrom[i].size())) return false;
+    const char *blob = reinterpret_cast<const char *>(s.h_blob.data());
+    char num[16];
+    for (uint64_t h = a; h < b; ++h) {
+        const uint64_t hit = r->hit[h];
+        const uint32_t rec = static_cast<uint32_t>(hit);
+        const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
+        if (h > a) o += ", ";
+        o.push_back('"');
+        o += chrom;
+        o += "\\t";
+        uint32_t v = s.h_pos[rec];
+        char *e = num + sizeof num, *q = e;
+        do {
+            *--q = static_cast<char>('0' + v % 10);
+            v /= 10;
+        } while (v);
+        o.append(q, static_cast<size_t>(e - q));
+        o += "\\t";
+        if (!json_escape_append(o, blob + s.h_ref_off[rec], s.h_end[rec] - s.h_pos[rec] + 1)) return false;
+        o += "\\t";
+        bool ok;
+        if (k == 0) {
+            ok = json_escape_append(o, blob + s.h_a0_off[rec], s.h_a0_len[rec]);
+        } else {
+            const uint32_t x = s.h_x_lo[rec] + k - 1;
+            ok = json_escape_append(o, blob + s.h_x_off[x], s.h_x_len[x]);
+        }
+        if (!ok) return false;
+        o += "\\t";
+        const std::string &vt = r->vt_json[s.h_vt[rec]];
+        if (vt.size() == 1 && vt[0] == '\x01') return false;  // a VT string that is not UTF-8
+        o += vt;
+        o.push_back('"');
+    }
+    return true;
+}
+}  // namespace sb
+
+extern "C" {
 
 int sb_result_variants_text(sb_result_set *r, size_t i, const char **p, size_t *len) {
     if (!r || !p || !len || i >= r->res.size()) return SB_EINVAL;

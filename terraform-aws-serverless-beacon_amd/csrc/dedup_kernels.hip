@@ -812,25 +812,27 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))
         const uint32_t p = piece_of(f);
         return s_klo[p] + (f - s_pre[p]);
     };
-    // every body load of the window first (key u = u * kThreads + tid)
-    KBody b[kWPer];
+    // every key's 8-byte class word first (key u = u * kThreads + tid): POS,
+    // exact code, displaced flag -- the 16-byte body only where a hashed key
+    // meets an entry with its hash bits (string confirmation, below)
+    uint64_t wd[kWPer];
     uint32_t kid[kWPer];
     uint32_t okm = 0;
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) {
         const uint32_t f = u * kThreads + threadIdx.x;
         kid[u] = 0;
-        b[u] = KBody{0, 0, 0};
+        wd[u] = 0;
         if (f < total) {
             kid[u] = key_of(f);
-            b[u] = ks.body[kid[u]];
+            wd[u] = ks.word[kid[u]];
             okm |= 1u << u;
         }
     }
     if (dbg & 4u) {  // timing ablation (SBEACON_DEDUP_WIN_DBG): loads only
         uint32_t x = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < kWPer; ++u) x += b[u].pos;
+        for (uint32_t u = 0; u < kWPer; ++u) x += static_cast<uint32_t>(wd[u]);
         if (x == 0xdeadbeefu) atomicOr(overflow, x);
         return;
     }
@@ -842,15 +844,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))
     for (uint32_t u = 0; u < kWPer; ++u) {
         xw[u] = 0;
         if (!((okm >> u) & 1u)) continue;
-        if (b[u].flags & kKeyDisplaced) {
-            if (static_cast<uint64_t>(b[u].pos) * 10 > W.pmax) hm |= 1u << u;
+        const uint32_t pos = static_cast<uint32_t>(wd[u]);
+        if (wd[u] & kWordDisplaced) {
+            if (static_cast<uint64_t>(pos) * 10 > W.pmax) hm |= 1u << u;
             else dm |= 1u << u;
             continue;
         }
-        uint64_t rel = 0;
-        const uint32_t code = exact_word(b[u], W.p0, kWinSpanBits, &rel);
-        if (code) {
-            xw[u] = (static_cast<uint32_t>(rel) << 6) | code;
+        const uint32_t code = static_cast<uint32_t>(wd[u] >> 32) & 63u;
+        if (code && pos >= W.p0 && ((pos - W.p0) >> kWinSpanBits) == 0) {
+            xw[u] = ((pos - W.p0) << 6) | code;
             em |= 1u << u;
         } else {
             hm |= 1u << u;
@@ -920,11 +922,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))
     // decimal-concatenation one only for different POS or two blob tails)
     bool bad = false;
     if (pend) {
-        KBody xb[kWPer];
+        KBody xb[kWPer], b[kWPer];
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u) {
             ins[u] = ((pend >> u) & 1u) ? key_of(ins[u]) : 0u;
             xb[u] = ((pend >> u) & 1u) ? ks.body[ins[u]] : KBody{0, 0, 0};
+            b[u] = ((pend >> u) & 1u) ? ks.body[kid[u]] : KBody{0, 0, 0};
         }
         uint32_t slow = 0;
 #pragma unroll

@@ -498,9 +498,15 @@ inline constexpr uint32_t kWinCap = 2048;    // keys per window (LDS sets sized 
 inline constexpr uint32_t kWinPieces = 64;   // pieces (= runs) per window
 inline constexpr uint32_t kWinSpanBits = 26; // p1 - p0 < 2^26 - 1: exact words fit 32 bits
 
+// one 8-byte class word per key (window dedup reads only this for most
+// keys): POS in bits 0..31, the exact code c1 c2 (compressSeq codes of a
+// single-base REF and ALT, 0 = the key is not of that class) in bits 32..37,
+// kWordDisplaced when the tail starts with a digit
+inline constexpr uint64_t kWordDisplaced = 1ull << 62;
 struct KStore {
     const uint64_t *hash;
     const KBody *body;
+    const uint64_t *word;
     const uint8_t *blob;
     // twin lookups of the window dedup: first key of each record (+ end), the
     // records' POS and the segments' coarse POS index (DStore::pos / bucket)

@@ -1920,7 +1920,7 @@ struct ReqLds {
     unsigned long long tcc[kPackRun], tan[kPackRun];
     unsigned int exw[kPackSlots / 32];  // bit = the slot's slice exists
     unsigned int slow[kPackRun];
-    unsigned int cstart[kPackRun + 1];  // staging position of each chain's first hit (~0: none)
+    unsigned int cstart[kPackRun + 2];  // staging position of each chain's first hit (~0: none); + a dummy slot
     unsigned int ccount[kPackRun];
     uint8_t rowchain[kRunRows];         // row (run-relative) -> its chain (0xff: not a chain row)
 };
@@ -2042,33 +2042,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const uint32_t i_safe = rdl(c0, 0);
     wave_lds_sync();
     // ---- candidates: chunk c covers run positions [64 c, 64 c + 64)
-    uint32_t kc = 0;  // chain at the current chunk's first position (wave-uniform)
+    // a candidate lane's chain: the last chain j < R whose first position
+    // pex_j <= g (binary search over the lane-held prefixes: VALU + ds_bpermute,
+    // no scalar loop -- SQ counters put a readlane walk at ~1.5 k SALU / wave)
     auto load = [&](uint32_t base) -> RowChunk {
         const uint32_t g = base + ul;
         RowChunk c;
-        c.k = kc;
-        uint32_t dl = rdl(delta, kc);
-        c.so = rdl(sex, kc);
-        c.first = rdl(pex, kc) == g;
-        uint32_t next = kc;
-        for (uint32_t j = kc + 1; j < R; ++j) {  // chains starting inside this chunk (usually a few)
-            const uint32_t pj = rdl(pex, j);
-            if (pj > base + kWave) break;
-            if (pj <= g) {
-                c.k = j;
-                dl = rdl(delta, j);
-                c.so = rdl(sex, j);
-                c.first = pj == g;
-            }
-            next = j;
-        }
-        kc = next;
+        const uint32_t k = last_le(pex, R, g);
+        c.k = k;
+        const uint32_t dl = static_cast<uint32_t>(__shfl(static_cast<int>(delta), static_cast<int>(k), kWave));
+        c.so = static_cast<uint32_t>(__shfl(static_cast<int>(sex), static_cast<int>(k), kWave));
+        c.first = static_cast<uint32_t>(__shfl(static_cast<int>(pex), static_cast<int>(k), kWave)) == g;
         const uint32_t i = (base < T && g < T) ? g + dl : i_safe;
         c.x = ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]};
         return c;
     };
     uint32_t hpos = 0;  // hits appended so far (wave-uniform)
     uint64_t *const sdst = stage + stage_at;  // the run's staging region (capacity planned on the host)
+    // few divergent regions per chunk (each costs exec-mask SALU): the chain-
+    // start marks go to a dummy LDS slot from the other lanes, the slice index
+    // is branch-free, multi-ALT lanes take a separate ballot-guarded path
     auto eval = [&](const RowChunk &c, uint32_t base) {
         const ChainChunk &x = c.x;
         const uint32_t k = c.k;
@@ -2079,16 +2072,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         VtPred Pd(p1.x, p1.y, p1.z, p1.w, p2.x, p2.y & 0x7fffffffu, (p2.y >> 31) != 0, lut_base + p2.w);
         const bool inwin = valid && x.p >= first && x.p <= last;
         const bool cand = inwin && Pd.end_ok(x.h.end);
-        if (cand && (x.h.w & VT_SLOW)) L.slow[k] = 1u;  // never: prepare sends such requests per slice
+        if (__ballot(cand && (x.h.w & VT_SLOW)))  // never: prepare sends such requests per slice
+            if (cand && (x.h.w & VT_SLOW)) L.slow[k] = 1u;
         const LaneOut o = Pd.eval(st, x.h, x.r, cand && !(x.h.w & VT_SLOW));
         const bool hit = o.hm != 0;
+        const uint32_t mark = (valid && c.first) ? k : kPackRun + 1;  // kPackRun + 1: the dummy slot
         if (!__ballot(hit)) {
-            if (valid && c.first) L.cstart[k] = hpos;
+            L.cstart[mark] = hpos;
             return;
         }
         const uint32_t cn = hit ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
         uint32_t pre, tot;
-        if (!__ballot(cn > 1)) {
+        const bool multi = __ballot(cn > 1) != 0;
+        if (!multi) {
             const uint64_t one = __ballot(cn == 1);
             pre = popc_below(one);
             tot = static_cast<uint32_t>(__popcll(one));
@@ -2102,26 +2098,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 if (!__ballot(cn >> (bb + 1))) break;
             }
         }
-        if (valid && c.first) L.cstart[k] = hpos + pre;
-        if (cn) {
+        L.cstart[mark] = hpos + pre;
+        if (cn == 1) sdst[hpos + pre] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(o.em)) << kHitAltShift);
+        if (multi && cn > 1) {
             uint32_t at = hpos + pre;
             for (uint64_t b = o.em; b; b &= b - 1)
                 sdst[at++] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
         }
         hpos += tot;
+        // slice = (POS - first) / width: an f32 estimate within one of the
+        // quotient, corrected (d < 2^24: a chain spans <= kChainMax 10 kb slices)
+        const uint32_t d = x.p - first;
+        uint32_t qt = static_cast<uint32_t>(static_cast<float>(d) * __uint_as_float(p2.z));
+        qt -= qt * width > d ? 1u : 0u;
+        qt += (qt + 1) * width <= d ? 1u : 0u;
+        const uint32_t slot = c.so + min(qt, n - 1);
         if (hit) {
-            // slice = (POS - first) / width: f32 estimate within one of the quotient, then exact
-            const uint32_t d = x.p - first;
-            uint32_t qt;
-            if (d < (1u << 24)) {
-                qt = static_cast<uint32_t>(static_cast<float>(d) * __uint_as_float(p2.z));
-                if (static_cast<uint64_t>(qt) * width > d) --qt;
-                else if (static_cast<uint64_t>(qt + 1) * width <= d) ++qt;
-            } else {
-                qt = d / width;
-            }
-            const uint32_t slot = c.so + min(qt, n - 1);
-            if (o.c > 0) atomicOr(&L.exw[slot >> 5], 1u << (slot & 31u));
+            atomicOr(&L.exw[slot >> 5], o.c > 0 ? 1u << (slot & 31u) : 0u);
             atomicAdd(&L.tcc[k], static_cast<unsigned long long>(o.c));
             atomicAdd(&L.tan[k], static_cast<unsigned long long>(o.anv));
         }
@@ -2183,125 +2176,102 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const uint64_t H = static_cast<uint64_t>(rdl64(wave_incl_scan_i64(static_cast<int64_t>(nvr)), kWave - 1));
     if (ul == 0) {  // read by request_deliver_kernel (kernel boundary)
         status[w] = H;
-        // tile and super-tile totals (zeroed before this launch): tstatus[t] for
-        // tile t, tstatus[n_tiles + u] for tiles [64 u, 64 u + 64)
+        // the tile's total (zeroed before this launch; 16 adds per address):
+        // request_tile_scan_kernel turns the tile totals into tile offsets
         atomicAdd(&tstatus[w / kDeliverTile], static_cast<unsigned long long>(H));
-        atomicAdd(&tstatus[n_tiles + w / (kDeliverTile * kWave)], static_cast<unsigned long long>(H));
     }
 }
 
-// request_deliver_kernel: one wave per TILE of kDeliverTile consecutive runs.
-// request_eval_kernel left every run's hit total and added it to its tile's
-// total, so a tile's output offset is the plain sum of the earlier tiles'
-// totals: the totals of the earlier super-tiles (64 tiles each) and of the
-// earlier tiles of its own super-tile, one load per lane each (an in-launch
-// look-back, or a strided loop over the tiles, is a chain of dependent
-// ~1-2 us loads: 0.1 ms for the launch),
-// and a tile of chain runs is copied as ONE contiguous range of ~4 k hits:
-// output position p belongs to the last run of the tile whose exclusive
-// offset is <= p (offsets held one per lane; a 15-step wave-uniform compare).
+// request_tile_scan_kernel: one workgroup turns the tile totals (tiles of
+// kDeliverTile runs, added up by request_eval_kernel) into exclusive tile
+// offsets in place.
+__global__ __launch_bounds__(1024) void request_tile_scan_kernel(unsigned long long *__restrict__ tsum, uint32_t nt) {
+    __shared__ unsigned long long wsum[16];
+    __shared__ unsigned long long carry_s;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
+    if (tid == 0) carry_s = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < nt; base += 1024) {
+        const uint32_t i = base + tid;
+        const uint64_t v = i < nt ? tsum[i] : 0ull;
+        const uint64_t incl = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(v)));
+        if (lane_id() == kWave - 1) wsum[wave] = incl;
+        __syncthreads();
+        uint64_t before = carry_s;
+        for (uint32_t k = 0; k < wave; ++k) before += wsum[k];
+        if (i < nt) tsum[i] = before + incl - v;
+        __syncthreads();
+        if (tid == 1023) carry_s = before + incl;
+        __syncthreads();
+    }
+}
+
+// request_deliver_kernel: one wave per run.  Its output offset = its tile's
+// offset + the totals of the earlier runs of its tile (<= 15 loads, one per
+// lane); row offsets by a wave scan of the row counts request_eval_kernel
+// left in row_off; the run's hits copied from its staging region (one
+// contiguous range for a run of chain rows; row by row where some rows were
+// answered per slice).  No inter-wave dependency.  (One wave per tile of 16
+// runs, or a look-back, left the chip mostly idle: ~2 k waves, 0.1 ms.)
 __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const RowRun *__restrict__ runs, uint32_t n_runs, const unsigned long long *__restrict__ status,
-    const unsigned long long *__restrict__ tstatus, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
+    const unsigned long long *__restrict__ toff, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
     const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr, const uint64_t *__restrict__ shits,
     uint64_t *__restrict__ row_off, const uint64_t *__restrict__ row_src, const uint64_t *__restrict__ stage,
     uint64_t *__restrict__ out, uint32_t n_rows, uint64_t rec_base) {
     const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    const uint32_t t0 = w * kDeliverTile;
-    if (t0 >= n_runs) return;
+    if (w >= n_runs) return;
     const uint32_t ul = static_cast<uint32_t>(lane_id());
-    const uint32_t nr = min(kDeliverTile, n_runs - t0);
-    // lane j < nr: run t0 + j
-    uint64_t Hj = 0, stj = 0;
-    uint32_t rlo = 0, rhi = 0;
-    bool simple = true;
-    if (ul < nr) {
-        const RowRun rr = runs[t0 + ul];
-        Hj = status[t0 + ul];
-        stj = rr.stage;
-        rlo = rr.row_lo;
-        rhi = rr.row_hi;
-        simple = (rr.flags & kRunSimple) != 0;
-    }
-    const uint64_t incl = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(Hj)));
-    const uint64_t T = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl), kWave - 1));
-    const uint64_t excl = incl - Hj;
-    // the tile's offset: every earlier tile's total (request_eval_kernel added
-    // them up), summed directly -- independent loads, no look-back chain
-    const uint32_t n_tiles = (n_runs + kDeliverTile - 1) / kDeliverTile, sup = w / kWave;
-    uint64_t part = 0;
-    for (uint32_t u = ul; u < sup; u += kWave) part += tstatus[n_tiles + u];  // earlier super-tiles (one load per lane
-                                                                             // below 65 k runs)
-    if (kWave * sup + ul < w) part += tstatus[kWave * sup + ul];             // earlier tiles of this super-tile
-    const uint64_t O = static_cast<uint64_t>(rdl64(wave_incl_scan_i64(static_cast<int64_t>(part)), kWave - 1));
-    const bool all_simple = !__ballot(!simple);
-    // every run's row counts (left in row_off) loaded up front: one round trip
-    // for the tile, not one per run
-    uint64_t cnt[kDeliverTile];
+    const uint32_t t0 = (w / kDeliverTile) * kDeliverTile;
+    const RowRun rr = runs[w];
+    const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
+    const uint64_t stage_at = uniform64(rr.stage);
+    const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
+    const uint32_t row = row_lo + ul;
+    const uint64_t c = row < row_hi ? row_off[row] : 0ull;  // the counts request_eval_kernel left
+    const uint64_t before = t0 + ul < w ? status[t0 + ul] : 0ull;
+    const uint64_t O = uniform64(toff[w / kDeliverTile]) +
+                       static_cast<uint64_t>(rdl64(wave_incl_scan_i64(static_cast<int64_t>(before)), kWave - 1));
+    const uint64_t linc = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(c)));
+    const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(linc), kWave - 1));
+    const uint64_t off = O + linc - c;
+    if (row < row_hi) row_off[row] = off;
+    if (row_hi == n_rows && ul == 0) row_off[n_rows] = O + H;
+    if (simple) {  // chain rows (and empty rows) only: the staging region is the output, in order
+        constexpr uint32_t kU = 4;
+        for (uint64_t j0 = 0; j0 < H; j0 += kWave * kU) {
+            uint64_t v[kU];
 #pragma unroll
-    for (uint32_t j = 0; j < kDeliverTile; ++j) {
-        const uint32_t a = rdl(rlo, j < nr ? j : 0u), b = j < nr ? rdl(rhi, j) : a;
-        cnt[j] = a + ul < b ? row_off[a + ul] : 0ull;
-    }
-    // row offsets, run by run: lane i = row rlo_j + i; a tile with rows
-    // answered per slice copies run by run here
+            for (uint32_t u = 0; u < kU; ++u) {
+                const uint64_t j = j0 + kWave * u + ul;
+                v[u] = j < H ? stage[stage_at + j] : 0ull;
+            }
 #pragma unroll
-    for (uint32_t j = 0; j < kDeliverTile; ++j) {
-        if (j >= nr) break;
-        const uint32_t a = rdl(rlo, j), b = rdl(rhi, j);
-        const uint64_t base = O + static_cast<uint64_t>(rdl64(static_cast<int64_t>(excl), j));
-        const uint32_t row = a + ul;
-        const uint64_t c = cnt[j];
-        const uint64_t off = base + static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(c))) - c;
-        if (row < b) row_off[row] = off;
-        if (all_simple) continue;
-        const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(Hj), j));
-        if (!H) continue;
-        if (__shfl(simple ? 1 : 0, static_cast<int>(j), kWave)) {  // chain rows only: one contiguous copy
-            const uint64_t st0 = static_cast<uint64_t>(rdl64(static_cast<int64_t>(stj), j));
-            for (uint64_t q = ul; q < H; q += kWave) out[base + q] = stage[st0 + q] + rec_base;
-            continue;
-        }
-        for (uint32_t i = 0; i < b - a; ++i) {  // row by row
-            const uint64_t nv = static_cast<uint64_t>(rdl64(static_cast<int64_t>(c), i));
-            if (!nv) continue;
-            const uint64_t at = static_cast<uint64_t>(rdl64(static_cast<int64_t>(off), i));
-            const uint32_t r = a + i;
-            const uint32_t q0 = uniform(sseg[r]), q1 = uniform(sseg[r + 1]);
-            if (q1 == q0) {  // a chain row: its hits are contiguous in the staging region
-                const uint64_t src = uniform64(row_src[r]);
-                for (uint64_t k = ul; k < nv; k += kWave) out[at + k] = stage[src + k] + rec_base;
-            } else {
-                uint64_t dst = at;
-                for (uint32_t q = q0; q < q1; ++q) {
-                    const QRes rq = sres[q];
-                    if (rq.error || sherr[q]) continue;
-                    const uint64_t src = shoff[q];
-                    for (uint32_t k = ul; k < rq.n_hits; k += kWave) out[dst + k] = shits[src + k] + rec_base;
-                    dst += rq.n_hits;
-                }
+            for (uint32_t u = 0; u < kU; ++u) {
+                const uint64_t j = j0 + kWave * u + ul;
+                if (j < H) out[O + j] = v[u] + rec_base;
             }
         }
+        return;
     }
-    if (t0 + nr == n_runs && ul == 0) row_off[n_rows] = O + T;
-    if (!all_simple) return;
-    // chain runs only: their staging regions hold the tile's hits in order
-    const int64_t delta = static_cast<int64_t>(stj - excl);  // staging slot = p + delta_j
-    constexpr uint32_t kU = 4;
-    for (uint64_t p0 = 0; p0 < T; p0 += kWave * kU) {
-        uint64_t v[kU];
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-            const uint64_t p = p0 + kWave * u + ul;
-            int64_t d = rdl64(delta, 0);
-            for (uint32_t k = 1; k < nr; ++k)
-                if (p >= static_cast<uint64_t>(rdl64(static_cast<int64_t>(excl), k))) d = rdl64(delta, k);
-            v[u] = p < T ? stage[static_cast<uint64_t>(static_cast<int64_t>(p) + d)] : 0ull;
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < kU; ++u) {
-            const uint64_t p = p0 + kWave * u + ul;
-            if (p < T) out[O + p] = v[u] + rec_base;
+    for (uint32_t i = 0; i < row_hi - row_lo; ++i) {  // row by row (some rows answered per slice)
+        const uint64_t nv = static_cast<uint64_t>(rdl64(static_cast<int64_t>(c), i));
+        if (!nv) continue;
+        const uint64_t at = static_cast<uint64_t>(rdl64(static_cast<int64_t>(off), i));
+        const uint32_t r = row_lo + i;
+        const uint32_t q0 = uniform(sseg[r]), q1 = uniform(sseg[r + 1]);
+        if (q1 == q0) {  // a chain row: its hits are contiguous in the staging region
+            const uint64_t src = uniform64(row_src[r]);
+            for (uint64_t k = ul; k < nv; k += kWave) out[at + k] = stage[src + k] + rec_base;
+        } else {
+            uint64_t dst = at;
+            for (uint32_t q = q0; q < q1; ++q) {
+                const QRes rq = sres[q];
+                if (rq.error || sherr[q]) continue;
+                const uint64_t src = shoff[q];
+                for (uint32_t k = ul; k < rq.n_hits; k += kWave) out[dst + k] = shits[src + k] + rec_base;
+                dst += rq.n_hits;
+            }
         }
     }
 }
@@ -3470,24 +3440,21 @@ void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun 
         return;
     }
     const dim3 grid(blocks_for(n_runs));
-    const uint32_t n_tiles = (n_runs + kDeliverTile - 1) / kDeliverTile;
-    (void)hipMemsetAsync(tstatus, 0, size_t(request_tiles(n_runs)) * 8, s);
+    const uint32_t n_tiles = request_tiles(n_runs);
+    (void)hipMemsetAsync(tstatus, 0, size_t(n_tiles) * 8, s);
     if (n_lut <= kReqLut)
         hipLaunchKernelGGL(request_eval_kernel<true>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status,
                            tstatus, sres, rows, row_off, row_src, stage, n_lut, n_tiles);
     else
         hipLaunchKernelGGL(request_eval_kernel<false>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status,
                            tstatus, sres, rows, row_off, row_src, stage, n_lut, n_tiles);
-    const uint32_t tiles = (n_runs + kDeliverTile - 1) / kDeliverTile;
-    hipLaunchKernelGGL(request_deliver_kernel, dim3(blocks_for(tiles)), dim3(kBlock), 0, s, runs, n_runs, status,
-                       tstatus, sres, sseg, shoff, sherr, shits, row_off, row_src, stage, out, n_rows, rec_base);
+    hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, tstatus, n_tiles);
+    hipLaunchKernelGGL(request_deliver_kernel, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg,
+                       shoff, sherr, shits, row_off, row_src, stage, out, n_rows, rec_base);
 }
 
-// words of tstatus: the tile totals, then the super-tile totals
-uint32_t request_tiles(uint32_t n_runs) {
-    const uint32_t t = (n_runs + kDeliverTile - 1) / kDeliverTile;
-    return t + (t + kWave - 1) / kWave;
-}
+// tile totals (request_eval_kernel) -> tile offsets (request_tile_scan_kernel)
+uint32_t request_tiles(uint32_t n_runs) { return (n_runs + kDeliverTile - 1) / kDeliverTile; }
 
 uint32_t pack_run_max() { return kPackRun; }
 uint32_t pack_slots_max() { return kPackSlots; }

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "common.hpp"
+#include "jsonesc.hpp"
 
 struct sb_json_out {
     std::unique_ptr<char[]> buf;  // n bytes (uninitialised storage: filled in parallel)
@@ -493,67 +494,11 @@ void bind_strings(Event &E) {  // after E is in its final place
 }
 
 // ------------------------------------------------------------------ output
-// json.dumps (ensure_ascii=True) of a Python str holding these UTF-8 bytes;
-// false on invalid UTF-8 (the Python path's .decode() raises there)
+// json.dumps (ensure_ascii=True) of a Python str holding these UTF-8 bytes
+// (jsonesc.hpp); false on invalid UTF-8 (the Python path's .decode() raises)
 bool put_jstr(std::string &o, const char *s, size_t n) {
-    static const char kHex[] = "0123456789abcdef";
-    auto u4 = [&](uint32_t v) {
-        o += "\\u";
-        o.push_back(kHex[(v >> 12) & 15]);
-        o.push_back(kHex[(v >> 8) & 15]);
-        o.push_back(kHex[(v >> 4) & 15]);
-        o.push_back(kHex[v & 15]);
-    };
     o.push_back('"');
-    for (size_t i = 0; i < n;) {
-        size_t r = i;  // a run of printable ASCII other than '"' and '\\' is copied as is
-        while (r < n) {
-            const unsigned char x = static_cast<unsigned char>(s[r]);
-            if (x < 0x20 || x >= 0x7f || x == '"' || x == '\\') break;
-            ++r;
-        }
-        if (r > i) {
-            o.append(s + i, r - i);
-            i = r;
-            if (i >= n) break;
-        }
-        const unsigned char c = static_cast<unsigned char>(s[i]);
-        if (c < 0x80) {
-            switch (c) {
-                case '"': o += "\\\""; break;
-                case '\\': o += "\\\\"; break;
-                case '\n': o += "\\n"; break;
-                case '\r': o += "\\r"; break;
-                case '\t': o += "\\t"; break;
-                case '\b': o += "\\b"; break;
-                case '\f': o += "\\f"; break;
-                default:
-                    if (c < 0x20 || c == 0x7f) u4(c);
-                    else o.push_back(static_cast<char>(c));
-            }
-            ++i;
-            continue;
-        }
-        const int len = (c & 0xe0) == 0xc0 ? 2 : (c & 0xf0) == 0xe0 ? 3 : (c & 0xf8) == 0xf0 ? 4 : 0;
-        if (!len || i + len > n) return false;
-        uint32_t cp = c & (0x7f >> len);
-        for (int k = 1; k < len; ++k) {
-            const unsigned char cc = static_cast<unsigned char>(s[i + k]);
-            if ((cc & 0xc0) != 0x80) return false;
-            cp = (cp << 6) | (cc & 0x3f);
-        }
-        if ((len == 2 && cp < 0x80) || (len == 3 && cp < 0x800) || (len == 4 && (cp < 0x10000 || cp > 0x10ffff)) ||
-            (cp >= 0xd800 && cp < 0xe000))
-            return false;
-        if (cp >= 0x10000) {
-            const uint32_t v = cp - 0x10000;
-            u4(0xd800 + (v >> 10));
-            u4(0xdc00 + (v & 0x3ff));
-        } else {
-            u4(cp);
-        }
-        i += static_cast<size_t>(len);
-    }
+    if (!json_escape_append(o, s, n)) return false;
     o.push_back('"');
     return true;
 }
@@ -659,18 +604,7 @@ bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
         put_i64(o, v.all_alleles_count);
     }
     o += ", \"variants\": [";
-    if (v.n_variants) {
-        if (sb_result_variants_text(rs, i, &tp, &tn) != SB_OK) return false;
-        o.reserve(o.size() + tn + 4 * v.n_variants + 256);
-        size_t a = 0;
-        for (size_t k = 0; k <= tn; ++k) {
-            if (k == tn || tp[k] == '\n') {
-                if (a) o += ", ";
-                if (!put_jstr(o, tp + a, k - a)) return false;
-                a = k + 1;
-            }
-        }
-    }
+    if (v.n_variants && !result_variants_json(rs, i, o)) return false;
     o += "], \"call_count\": ";
     if (v.big_limbs) {
         if (!put_limbs(o, v.big_call_count, v.big_limbs)) {
@@ -770,6 +704,7 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
             const int rc = sb_query_batch(stores[k], qs.data(), qs.size(), 0, &rs);
             if (rc != SB_OK) return rc;  // sb_last_error holds the message
             std::unique_ptr<sb_result_set, void (*)(sb_result_set *)> keep(rs, sb_result_free);
+            result_prepare_json(rs);
             tick("query");
             par(idx.size(), threads, [&](size_t j, unsigned t) {
                 const uint32_t i = idx[j];
