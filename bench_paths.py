@@ -48,6 +48,8 @@ def main():
     ap.add_argument('--threads', type=int, default=16)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--only', choices=['summarise', 'dedup'], default=None)
+    ap.add_argument('--strict-datasets', type=int, default=10,
+                    help='datasets whose messages also run in the reference-exact dedup mode (0: skip)')
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -146,7 +148,41 @@ def summarise_line(args, store, files, plan_slices):
                      'traffic': pmc_traffic(n_records, ['summarise_chunk_kernel', 'summarise_finish_kernel']),
                      'kernel': 'summarise_chunk_kernel + summarise_finish_kernel',
                      'algorithmic_bytes_per_launch': alg},
-        'cpu_baseline': cpu, 'parity_sample': parity}), flush=True)
+        'cpu_baseline': cpu, 'parity_sample': parity, 'strict_mode': strict}), flush=True)
+
+
+def strict_sample(args, store, datasets):
+    """The reference-exact duplicateVariantSearch (SBEACON_STRICT_DEDUP=1:
+    every region file a message names read as ReadVcfData::getVcfData reads
+    it, sb_dedup_count_files) beside the intended-range device path, over the
+    same initDuplicateVariantSearch messages of the first datasets: the
+    summariseVcf / summariseSlice / region-file steps run once, untimed; the
+    timed part is one dedup_batch call of all those messages per mode."""
+    from sbeacon.dedup import DuplicateTally, dedup_batch, init_duplicate_variant_search
+    from sbeacon.summarise import _single_store_registry, region_file_keys
+    from sbeacon.summarise_vcf import summarise_vcf
+    reg = _single_store_registry(store)
+    msgs, refs = [], {}
+    for ds, parts in datasets[:args.strict_datasets]:
+        keys = []
+        for loc, _ in parts:
+            slices, _, _ = summarise_vcf(store, loc)
+            keys += region_file_keys(store, loc, slices, refs)
+        msgs += init_duplicate_variant_search(ds, [loc for loc, _ in parts], keys, tally=DuplicateTally())
+    out = {'datasets': min(args.strict_datasets, len(datasets)), 'messages': len(msgs),
+           'region_files': len(refs)}
+    for mode, fr in (('strict', refs), ('intended', None)):
+        dedup_batch(msgs, registry=reg, file_refs=fr)
+        reps = 3
+        t = time.perf_counter()
+        for _ in range(reps):
+            res = dedup_batch(msgs, registry=reg, file_refs=fr)
+        dt = (time.perf_counter() - t) / reps
+        out[mode] = {'ms_per_call': round(dt * 1e3, 2), 'unique_sum': int(sum(r for r in res if isinstance(r, int))),
+                     'raised': int(sum(isinstance(r, Exception) for r in res))}
+    out['note'] = ('one dedup_batch call of every message of these datasets per mode; strict = the reference\'s '
+                   'reader over the region files (host walk + device keys), intended = the device window path')
+    return out
 
 
 def summarise_cpu(file, slices, got):
@@ -185,10 +221,10 @@ def dedup_line(args, store, datasets, files):
     ures, ust = store.dedup_counts(union, with_stats=True)
     alg = 8.0 * keys  # compulsory: one read of the 64-bit key stream
     if st['path'] == 'windows':
-        # implementation bytes: one 16 B body read per key + the 8 B hash of
+        # implementation bytes: one 8 B class word per key + the 8 B hash of
         # keys outside the exact class (~5 %) + 16 B per window descriptor;
-        # deferred displaced keys are noise
-        impl = 16.0 * keys + 8.0 * 0.05 * keys + 16.0 * st['windows']
+        # bodies of colliding hashed keys and deferred displaced keys are noise
+        impl = 8.0 * keys + 8.0 * 0.05 * keys + 16.0 * st['windows']
         kern = ('window_dedupe_kernel (one workgroup per POS window: one read of every key, LDS hash set) + '
                 'deferred_dedupe_kernel (displaced keys with a possible copy at a larger POS)')
     else:
@@ -210,6 +246,7 @@ def dedup_line(args, store, datasets, files):
                'sample': f'dataset {ds}: its 2 VCFs ({2 * args.records} records) through orc_dedup_count '
                          '(string keys, qsort + unique; text parse included)', 'seconds': round(dt, 3)}
         parity = {'jobs': 1, 'mismatches': int(res[0] != e), 'unique': e}
+    strict = strict_sample(args, store, datasets) if args.strict_datasets else None
     print(json.dumps({
         'metric': 'duplicateVariantSearch region keys/s (per-dataset unique counts, one batched call)',
         'value': round(keys / wall, 1) if wall > 0 else None,
@@ -227,7 +264,41 @@ def dedup_line(args, store, datasets, files):
                      'kernel': kern, 'algorithmic_bytes_per_launch': alg,
                      'implementation_bytes_per_launch_upper_bound': impl,
                      'implementation_GBs': round(impl / (dev_ms * 1e-3) / 1e9, 1)},
-        'cpu_baseline': cpu, 'parity_sample': parity}), flush=True)
+        'cpu_baseline': cpu, 'parity_sample': parity, 'strict_mode': strict}), flush=True)
+
+
+def strict_sample(args, store, datasets):
+    """The reference-exact duplicateVariantSearch (SBEACON_STRICT_DEDUP=1:
+    every region file a message names read as ReadVcfData::getVcfData reads
+    it, sb_dedup_count_files) beside the intended-range device path, over the
+    same initDuplicateVariantSearch messages of the first datasets: the
+    summariseVcf / summariseSlice / region-file steps run once, untimed; the
+    timed part is one dedup_batch call of all those messages per mode."""
+    from sbeacon.dedup import DuplicateTally, dedup_batch, init_duplicate_variant_search
+    from sbeacon.summarise import _single_store_registry, region_file_keys
+    from sbeacon.summarise_vcf import summarise_vcf
+    reg = _single_store_registry(store)
+    msgs, refs = [], {}
+    for ds, parts in datasets[:args.strict_datasets]:
+        keys = []
+        for loc, _ in parts:
+            slices, _, _ = summarise_vcf(store, loc)
+            keys += region_file_keys(store, loc, slices, refs)
+        msgs += init_duplicate_variant_search(ds, [loc for loc, _ in parts], keys, tally=DuplicateTally())
+    out = {'datasets': min(args.strict_datasets, len(datasets)), 'messages': len(msgs),
+           'region_files': len(refs)}
+    for mode, fr in (('strict', refs), ('intended', None)):
+        dedup_batch(msgs, registry=reg, file_refs=fr)
+        reps = 3
+        t = time.perf_counter()
+        for _ in range(reps):
+            res = dedup_batch(msgs, registry=reg, file_refs=fr)
+        dt = (time.perf_counter() - t) / reps
+        out[mode] = {'ms_per_call': round(dt * 1e3, 2), 'unique_sum': int(sum(r for r in res if isinstance(r, int))),
+                     'raised': int(sum(isinstance(r, Exception) for r in res))}
+    out['note'] = ('one dedup_batch call of every message of these datasets per mode; strict = the reference\'s '
+                   'reader over the region files (host walk + device keys), intended = the device window path')
+    return out
 
 
 if __name__ == '__main__':

@@ -2974,6 +2974,9 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
         };
         const uint32_t C0 = cb(cd.first, 0), C1 = end_void ? C0 : std::max(C0, cb(uint64_t(cd.last) + 1, 1));
         ccap[chain_of[i]] = s.h_vc_altpre[C1] - s.h_vc_altpre[C0];
+        // request chains carry their candidate range itself (request_eval_kernel)
+        cd.c_lo = C0;
+        cd.c_hi = C1;
     });
     for (const ChainDev &c : R->chains) R->n_chain_slices += c.n;
     tick("chains");

@@ -196,7 +196,7 @@ struct alignas(16) ChainDev {
     uint32_t first;     // first_bp of slice 0
     uint32_t last;      // last_bp of slice n - 1
     uint32_t width;     // slices 0 .. n-2 span exactly `width` bp; the last at most that
-    uint32_t c_lo, c_hi;  // the (kind, segment) pair's candidates
+    uint32_t c_lo, c_hi;  // the (kind, segment) pair's candidates; request chains: the chain's own range (host-resolved)
     uint32_t cb_base;   // coarse candidate index of the pair (vc_bucket)
     uint64_t cb_off;
     uint32_t cb_shift, cb_n;

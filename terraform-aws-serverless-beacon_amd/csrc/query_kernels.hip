@@ -2008,15 +2008,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         L.pred[3 * ul + 1] = uint4{C.e0, C.espan, C.vlo, C.vspan};
         L.pred[3 * ul + 2] = uint4{q.cmask, q.xneed | (q.end_void ? 0x80000000u : 0u),
                                    __float_as_uint(__frcp_rn(static_cast<float>(C.width))), C.lut_off};
-        auto cb = [&](uint64_t x, uint32_t up) -> uint32_t {
-            if (x <= C.cb_base) return C.c_lo;
-            const uint64_t b = (x - C.cb_base) >> C.cb_shift;
-            return b >= C.cb_n ? C.c_hi : st.vc_bucket[C.cb_off + b + up];
-        };
-        const uint32_t lo = cb(C.first, 0u);
-        const uint32_t hi = q.end_void ? lo : max(lo, cb(static_cast<uint64_t>(C.last) + 1, 1u));
-        c0 = lo;
-        cnt = hi - lo;
+        // the chain's candidate range [c_lo, c_hi): resolved on the host at
+        // prepare (the same coarse-index bounds it sizes the staging with), so
+        // the candidate loads follow the descriptor load directly
+        c0 = C.c_lo;
+        cnt = C.c_hi - C.c_lo;
         nsl = C.n;
         L.tcc[ul] = 0;
         L.tan[ul] = 0;

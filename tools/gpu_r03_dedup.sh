@@ -10,7 +10,8 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; grep '^{' $OUT/$name.log | cut -c1-300; tail -2 $OUT/$name.log | cut -c1-300
   case $rc in 0) return 0;; *) exit $rc;; esac
 }
-step tests 400 python3 -u -m pytest $R/tests -m gpu -x -q --timeout 120 --timeout-method thread -k "dedup or pipeline"
+step tests 400 python3 -u -m pytest $R/tests -m gpu -x -q --timeout 120 --timeout-method thread -k "dedup or pipeline or wire"
+SBEACON_WIRE_TRACE=1 step wire 300 python3 -u $R/tools/wire_split.py
 step paths 900 python3 -u $R/bench_paths.py --datasets 50 --only dedup --steps 10 --warmup 2 --no-cpu-baseline
 cd /tmp
 step prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python3 $R/bench_paths.py --datasets 50 --only dedup --steps 5 --warmup 1 --no-cpu-baseline
