@@ -235,7 +235,8 @@ struct sb_batch {
         std::vector<RowRun> runs;
         uint64_t cap = 0;              // output hit capacity
         uint64_t n_chain_slices = 0;
-        uint32_t n_lut = 0;            // LUT words (request_rows_kernel stages them in LDS when they fit)
+        uint32_t n_lut = 0;            // LUT words (request_eval_kernel stages them in LDS when they fit)
+        uint64_t n_chains = 0;         // chain-answered requests (chains holds them padded per run)
         DevMem dchains, druns, status, tstatus, stage, row_src, lut, sseg, sherr;
         bool slices = false;           // some rows answered per slice (the batch's query part)
     };
@@ -3063,6 +3064,17 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     // device buffers
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
+    // chain descriptors padded to kPackRun slots per run (request_eval_kernel
+    // loads a run's descriptors beside its RowRun, n == 0 marks an empty slot)
+    {
+        const uint32_t slots = pack_run_max();
+        std::vector<ChainDev> padded(R->runs.size() * slots, ChainDev{});
+        for (size_t r = 0; r < R->runs.size(); ++r)
+            std::copy(R->chains.begin() + R->runs[r].c_lo, R->chains.begin() + R->runs[r].c_hi,
+                      padded.begin() + r * slots);
+        R->n_chains = R->chains.size();
+        R->chains = std::move(padded);
+    }
     R->dchains.alloc(R->chains.size() * sizeof(ChainDev));
     R->druns.alloc(R->runs.size() * sizeof(RowRun));
     R->status.alloc(R->runs.size() * 8);
@@ -3205,7 +3217,7 @@ int sb_batch_get_stats(const sb_batch *b, sb_batch_stats *out) {
     out->device_ms = b->last_total_ms;
     if (b->req) {  // request batch: the rows' output capacity and its chains
         out->hits = b->req->cap;
-        out->chains = b->req->chains.size();
+        out->chains = b->req->n_chains;
         out->chained_slices = b->req->n_chain_slices;
     }
     return SB_OK;

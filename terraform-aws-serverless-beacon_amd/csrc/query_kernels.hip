@@ -1992,16 +1992,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const uint32_t *lut_base = LDS_LUT ? slut : st.sym_lut;
     const uint32_t w = launch_wave();
     if (w >= n_runs) return;
-    const uint32_t row_lo = uniform(runs[w].row_lo), row_hi = uniform(runs[w].row_hi);
-    const uint32_t c_lo = uniform(runs[w].c_lo), R = uniform(runs[w].c_hi) - c_lo;
-    const uint64_t stage_at = (static_cast<uint64_t>(uniform(static_cast<uint32_t>(runs[w].stage >> 32))) << 32) |
-                              uniform(static_cast<uint32_t>(runs[w].stage));
-    const bool simple = (uniform(runs[w].flags) & kRunSimple) != 0;
+    // the run record and the run's chain descriptors (kPackRun slots per run,
+    // n == 0 = an empty slot) are independent loads: one round trip for both
+    const RowRun rr = runs[w];
+    ChainDev C{};
+    if (ul < kPackRun) C = chains[static_cast<uint64_t>(w) * kPackRun + ul];
+    const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
+    const uint64_t stage_at = uniform64(rr.stage);
+    const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
+    const uint32_t R = static_cast<uint32_t>(__popcll(__ballot(ul < kPackRun && C.n != 0)));
     const uint32_t nrows = row_hi - row_lo;
     // ---- setup: lane k < R = chain k (descriptor, predicate constants, candidate bounds)
     uint32_t rowk = 0, c0 = 0, cnt = 0, nsl = 0;
     if (ul < R) {
-        const ChainDev C = chains[c_lo + ul];
         rowk = C.s0;
         VtPred q(st, 0u, 0u, 0u, 0u, C.kind, 0u, 0u, 0u);
         L.pred[3 * ul] = uint4{C.first, C.last, C.n, C.width};
