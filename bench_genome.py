@@ -106,12 +106,16 @@ def main_genome(args):
     elapsed = time.perf_counter() - t1
     if dist:
         dist.barrier()
-    step_dev_ms = batch.timing()['scan_ms']  # HIP events on the stream: first run -> sync, / steps
-    # the dominant kernel alone: K back-to-back passes between two events on its stream
+    step_dev_ms = batch.timing()['total_ms']  # HIP events on the stream: first run -> sync, / steps
+    # the dominant kernel (request_eval_kernel) alone: events around its launch
+    # in each of K passes on its stream (sb_requests_time_eval); the whole pass beside it
+    batch.time_eval(True)
     for _ in range(args.steps):
         batch.run(part.data_ptr(), hits.data_ptr(), row_off.data_ptr(), base)
     batch.sync()
-    kern_ms = batch.timing()['scan_ms']
+    tm = batch.timing()
+    kern_ms, pass_ms = tm['scan_ms'], tm['total_ms']
+    batch.time_eval(False)
     nhits = int(row_off[-1].item())
     # candidate statistics of the rank's chains (the slice view of the same requests)
     from sbeacon.genome import prepare_shard_batch
@@ -126,17 +130,24 @@ def main_genome(args):
     # written.  Beside it the SURVEY §8d contract: 32 B x unique records in
     # the slice windows + 8 B / hit.
     chains = int(pst['chains'])
-    comp = (80.0 + 8.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * nhits
+    # request_eval_kernel: its 80 B chain descriptor, 40 B row and 8 B row
+    # count per request, 24 B per candidate in the union of the windows, 8 B
+    # per hit staged
+    comp = (80.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * nhits
     achieved = comp / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    # the whole pass (eval + tile scan + delivery): + 8 B row offset per request
+    # and the hits' dense copy (8 B read + 8 B written per hit)
+    comp_pass = comp + 8.0 * chains + 16.0 * nhits
+    achieved_pass = comp_pass / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
     uniq = union_rows(shape, sl)
     contract = 32.0 * uniq + 8.0 * nhits
-    traffic = None  # HBM bytes per launch from the PMC passes (tools/gpu_pmc_r03.sh)
+    traffic = None  # HBM bytes per launch from the PMC passes (tools/gpu_r03_pmc.sh)
     tf = os.path.join(REPO, 'profiles', 'traffic_genome.json')
     if world == 1 and os.path.exists(tf):
         try:
             tj = json.load(open(tf))
             if tj.get('records') == shape.n_total and tj.get('requests') == len(reqs) and \
-                    tj.get('kernel') == 'request_pass':
+                    tj.get('kernel') == 'request_eval_kernel':
                 traffic = tj.get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
@@ -147,7 +158,7 @@ def main_genome(args):
     if world == 1:
         delivered = delivered_passes(args, store, shape, reqs, world, rank, base, dev)
     vals = [elapsed, kern_ms, float(len(sl)), float(st['cand_loaded']), float(nhits), achieved, float(uniq), comp,
-            contract, step_dev_ms]
+            contract, step_dev_ms, pass_ms, achieved_pass, comp_pass]
     if dist:
         t = torch.tensor(vals, dtype=torch.float64, device=dev)
         allv = [torch.zeros_like(t) for _ in range(world)]
@@ -190,17 +201,22 @@ def main_genome(args):
         'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
         'candidates_loaded_per_s': round(tot_cand * args.steps / elapsed, 1),
         'hits_per_step': int(tot_hits),
-        'device_ms_per_step': {'step_rank0': round(r0[9], 4), 'kernel_rank0': round(r0[1], 4),
-                               'kernel_max': round(max(v[1] for v in allv), 4)},
+        'device_ms_per_step': {'step_rank0': round(r0[9], 4), 'pass_rank0': round(r0[10], 4),
+                               'eval_kernel_rank0': round(r0[1], 4),
+                               'eval_kernel_max': round(max(v[1] for v in allv), 4)},
         'roofline': {'bound': 'hbm', 'achieved': round(r0[5], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(r0[5] / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                     'kernel': 'request pass = request_eval_kernel + request_deliver_kernel (rank 0): HIP events '
-                               'around K back-to-back passes on their stream, / K (rocprof per-kernel averages: '
+                     'kernel': 'request_eval_kernel (rank 0, the dominant kernel of the pass): HIP events around '
+                               'its launch in each of K passes on its stream, averaged (rocprof per-kernel averages: '
                                'profiles/)',
                      'algorithmic_bytes_per_launch': r0[7],
-                     'pricing': 'bytes one launch must move at least once: 136 B/request (80 B chain descriptor + 2 '
-                                'index entries + 40 B row + 8 B row offset) + 24 B per candidate in the union of the '
-                                'chain windows + 8 B/hit written',
+                     'pricing': 'bytes the launch must move at least once: 128 B/request (80 B chain descriptor + '
+                                '40 B row + 8 B row count) + 24 B per candidate in the union of the chain windows + '
+                                '8 B/hit staged',
+                     'pass': {'ms': round(r0[10], 4), 'achieved': round(r0[11], 1),
+                              'frac': round(r0[11] / HBM_PEAK_GBS, 4), 'bytes': r0[12],
+                              'note': 'eval + tile scan + delivery (row offsets, dense hit copy: +8 B/request, '
+                                      '+16 B/hit)'},
                      'candidates': {'unique': int(st['cand_unique']), 'in_windows': int(st['cand_window']),
                                     'loaded': int(st['cand_loaded'])},
                      'contract_bytes_per_launch': r0[8],

@@ -148,42 +148,7 @@ def summarise_line(args, store, files, plan_slices):
                      'traffic': pmc_traffic(n_records, ['summarise_chunk_kernel', 'summarise_finish_kernel']),
                      'kernel': 'summarise_chunk_kernel + summarise_finish_kernel',
                      'algorithmic_bytes_per_launch': alg},
-        'cpu_baseline': cpu, 'parity_sample': parity, 'strict_mode': strict}), flush=True)
-
-
-def strict_sample(args, store, datasets):
-    """The reference-exact duplicateVariantSearch (SBEACON_STRICT_DEDUP=1:
-    every region file a message names read as ReadVcfData::getVcfData reads
-    it, sb_dedup_count_files) beside the intended-range device path, over the
-    same initDuplicateVariantSearch messages of the first datasets: the
-    summariseVcf / summariseSlice / region-file steps run once, untimed; the
-    timed part is one dedup_batch call of all those messages per mode."""
-    from sbeacon.dedup import DuplicateTally, dedup_batch, init_duplicate_variant_search
-    from sbeacon.summarise import _single_store_registry, region_file_keys
-    from sbeacon.summarise_vcf import summarise_vcf
-    reg = _single_store_registry(store)
-    msgs, refs = [], {}
-    for ds, parts in datasets[:args.strict_datasets]:
-        keys = []
-        for loc, _ in parts:
-            slices, _, _ = summarise_vcf(store, loc)
-            keys += region_file_keys(store, loc, slices, refs)
-        msgs += init_duplicate_variant_search(ds, [loc for loc, _ in parts], keys, tally=DuplicateTally())
-    out = {'datasets': min(args.strict_datasets, len(datasets)), 'messages': len(msgs),
-           'region_files': len(refs)}
-    for mode, fr in (('strict', refs), ('intended', None)):
-        dedup_batch(msgs, registry=reg, file_refs=fr)
-        reps = 3
-        t = time.perf_counter()
-        for _ in range(reps):
-            res = dedup_batch(msgs, registry=reg, file_refs=fr)
-        dt = (time.perf_counter() - t) / reps
-        out[mode] = {'ms_per_call': round(dt * 1e3, 2), 'unique_sum': int(sum(r for r in res if isinstance(r, int))),
-                     'raised': int(sum(isinstance(r, Exception) for r in res))}
-    out['note'] = ('one dedup_batch call of every message of these datasets per mode; strict = the reference\'s '
-                   'reader over the region files (host walk + device keys), intended = the device window path')
-    return out
-
+        'cpu_baseline': cpu, 'parity_sample': parity}), flush=True)
 
 def summarise_cpu(file, slices, got):
     from oracle.oracle import OracleBgzf

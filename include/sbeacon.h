@@ -450,6 +450,12 @@ int sb_requests_prepare_columns(sb_store *s, const sb_request_columns *c, size_t
  * Device pointers on the store's device; sb_batch_sync waits, and
  * sb_batch_last_timing reports the passes' device time. */
 int sb_requests_run(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_off, uint64_t rec_base);
+/* Measurement: with on != 0 every pass also records events around its
+ * request_eval_kernel launch (the dominant kernel); sb_batch_last_timing's
+ * scan_ms then reports that kernel's average over the passes since the last
+ * sync (total_ms stays the whole pass).  Off by default: the markers add
+ * stream gaps. */
+int sb_requests_time_eval(sb_batch *b, int on);
 
 /* ---- device-resident batch (benchmarks / fused pipelines) ----------------
  * Upload a batch once, then launch the query kernels repeatedly on the

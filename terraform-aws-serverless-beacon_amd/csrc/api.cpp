@@ -237,6 +237,15 @@ struct sb_batch {
         uint64_t n_chain_slices = 0;
         uint32_t n_lut = 0;            // LUT words (request_eval_kernel stages them in LDS when they fit)
         uint64_t n_chains = 0;         // chain-answered requests (chains holds them padded per run)
+        // sb_requests_time_eval: events around every pass's request_eval_kernel
+        bool time_eval = false;
+        std::vector<std::array<hipEvent_t, 2>> eval_ev;
+        size_t eval_used = 0;
+        double last_eval_ms = 0;
+        ~Req() {
+            for (auto &p : eval_ev)
+                for (auto e : p) (void)hipEventDestroy(e);
+        }
         DevMem dchains, druns, status, tstatus, stage, row_src, lut, sseg, sherr;
         bool slices = false;           // some rows answered per slice (the batch's query part)
     };
@@ -1315,6 +1324,16 @@ void sync(sb_batch &B) {
         HIP_OK(hipEventElapsedTime(&x, B.ev[0], B.ev[1]));
         B.last_total_ms = x / static_cast<float>(B.runs_pending);
         B.runs_pending = 0;
+    }
+    if (B.req && B.req->eval_used) {  // request batches: request_eval_kernel alone, averaged over the passes
+        double sum = 0;
+        for (size_t k = 0; k < B.req->eval_used; ++k) {
+            float x;
+            HIP_OK(hipEventElapsedTime(&x, B.req->eval_ev[k][0], B.req->eval_ev[k][1]));
+            sum += x;
+        }
+        B.req->last_eval_ms = sum / static_cast<double>(B.req->eval_used);
+        B.req->eval_used = 0;
     }
 }
 
@@ -3119,12 +3138,22 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
     }
     DStore d = s.d;
     d.sym_lut = R.lut.as<uint32_t>();
+    std::array<hipEvent_t, 2> ev{nullptr, nullptr};
+    if (R.time_eval) {
+        if (R.eval_used == R.eval_ev.size()) {
+            std::array<hipEvent_t, 2> p{};
+            for (auto &e : p) HIP_OK(hipEventCreate(&e));
+            R.eval_ev.push_back(p);
+        }
+        ev = R.eval_ev[R.eval_used++];
+    }
     launch_request_rows(d, R.dchains.as<ChainDev>(), R.druns.as<RowRun>(), static_cast<uint32_t>(R.runs.size()),
                         R.status.as<unsigned long long>(), R.tstatus.as<unsigned long long>(),
                         R.slices ? B.res.as<QRes>() : nullptr,
                         R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
                         static_cast<ReqPartial *>(rows), static_cast<uint64_t *>(row_off), R.row_src.as<uint64_t>(),
-                        R.stage.as<uint64_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, st);
+                        R.stage.as<uint64_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, st,
+                        ev[0], ev[1]);
     HIP_OK(hipGetLastError());
 }
 
@@ -3166,6 +3195,15 @@ int sb_requests_run(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_o
     });
 }
 
+int sb_requests_time_eval(sb_batch *b, int on) {
+    return guard([&] {
+        if (!b || !b->req) throw Error(SB_EINVAL, "not a request batch");
+        sync(*b);
+        b->req->time_eval = on != 0;
+        b->req->last_eval_ms = 0;
+    });
+}
+
 int sb_batch_prepare(sb_store *s, const sb_query *q, size_t nq, sb_batch **out) {
     return guard([&] {
         if (!s || (!q && nq) || !out) throw Error(SB_EINVAL, "NULL argument");
@@ -3195,9 +3233,11 @@ int sb_batch_sync(sb_batch *b) {
 
 int sb_batch_last_timing(const sb_batch *b, double *total_ms, double *scan_ms, double *bounds_ms) {
     if (!b) return SB_EINVAL;
-    // the query step is one launch: bounds are found inside the scan kernel
+    // the query step is one launch: bounds are found inside the scan kernel;
+    // request batches with eval timing on: scan = request_eval_kernel alone
     if (total_ms) *total_ms = b->last_total_ms;
-    if (scan_ms) *scan_ms = b->last_total_ms;
+    if (scan_ms) *scan_ms = (b->req && b->req->time_eval && b->req->last_eval_ms > 0) ? b->req->last_eval_ms
+                                                                                      : b->last_total_ms;
     if (bounds_ms) *bounds_ms = 0.0;
     return SB_OK;
 }

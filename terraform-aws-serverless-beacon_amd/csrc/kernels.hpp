@@ -108,7 +108,8 @@ void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun 
                          unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,
-                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, hipStream_t s);
+                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, hipStream_t s, hipEvent_t ev0 = nullptr,
+                         hipEvent_t ev1 = nullptr);
 uint32_t request_tiles(uint32_t n_runs);
 
 // Fetch-time gather of every query's hits into one dense array.

@@ -3433,7 +3433,8 @@ void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun 
                          unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,
-                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, hipStream_t s) {
+                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, hipStream_t s, hipEvent_t ev0,
+                         hipEvent_t ev1) {
     if (!n_runs) {
         (void)hipMemsetAsync(row_off, 0, 8, s);
         return;
@@ -3441,12 +3442,14 @@ void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun 
     const dim3 grid(blocks_for(n_runs));
     const uint32_t n_tiles = request_tiles(n_runs);
     (void)hipMemsetAsync(tstatus, 0, size_t(n_tiles) * 8, s);
+    if (ev0) (void)hipEventRecord(ev0, s);
     if (n_lut <= kReqLut)
         hipLaunchKernelGGL(request_eval_kernel<true>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status,
                            tstatus, sres, rows, row_off, row_src, stage, n_lut, n_tiles);
     else
         hipLaunchKernelGGL(request_eval_kernel<false>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status,
                            tstatus, sres, rows, row_off, row_src, stage, n_lut, n_tiles);
+    if (ev1) (void)hipEventRecord(ev1, s);
     hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, tstatus, n_tiles);
     hipLaunchKernelGGL(request_deliver_kernel, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg,
                        shoff, sherr, shits, row_off, row_src, stage, out, n_rows, rec_base);

@@ -706,6 +706,22 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
             std::unique_ptr<sb_result_set, void (*)(sb_result_set *)> keep(rs, sb_result_free);
             result_prepare_json(rs);
             tick("query");
+            // each formatting thread's buffer sized once for its range of
+            // events (par's contiguous split): no reallocation while writing
+            {
+                const size_t m = idx.size();
+                const unsigned tt = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, m / 256)));
+                par(tt, tt, [&](size_t k, unsigned) {
+                    size_t need = 0;
+                    for (size_t j = m * k / tt, e = m * (k + 1) / tt; j < e; ++j) {
+                        sb_result_view v;
+                        if (sb_result_get(rs, j, &v) == SB_OK)
+                            need += 320 + ev[idx[j]].location.size() + ev[idx[j]].dataset.size() + 56 * v.n_variants +
+                                    12 * v.n_sample_indices;
+                    }
+                    tbuf[k].reserve(tbuf[k].size() + need);
+                });
+            }
             par(idx.size(), threads, [&](size_t j, unsigned t) {
                 const uint32_t i = idx[j];
                 std::string &o = tbuf[t];

@@ -255,6 +255,11 @@ class RequestBatch:
         check(lib().sb_batch_last_timing(self._h, C.byref(t), C.byref(s), C.byref(b)))
         return {'total_ms': t.value, 'scan_ms': s.value}
 
+    def time_eval(self, on: bool):
+        """Events around every pass's request_eval_kernel (measurement);
+        timing()['scan_ms'] then reports that kernel alone."""
+        check(lib().sb_requests_time_eval(self._h, 1 if on else 0))
+
     def stats(self) -> dict:
         st = _lib.BatchStats()
         check(lib().sb_batch_get_stats(self._h, C.byref(st)))

@@ -20,7 +20,7 @@ import os
 import re
 import sys
 
-PHASE = re.compile(r'(fused_kernel|range_n8?_kernel|vt_kernel|scan_kernel|request_reduce_kernel|chain_\w*kernel|upsweep_kernel|downsweep_kernel|gather_kernel|bucket_dedupe_kernel|unique_kernel|scan_reduce_kernel|scan_top_kernel|scan_down_kernel|summarise_\w+_kernel|row_reduce_kernel|row_gather_kernel|field_tile_\w+_kernel|tile_scan_kernel|hit_\w+_kernel|compact_kernel|dedup\w*|radix\w*|summ\w*)')
+PHASE = re.compile(r'(request_\w+_kernel|fused_kernel|range_n8?_kernel|vt_kernel|scan_kernel|request_reduce_kernel|chain_\w*kernel|upsweep_kernel|downsweep_kernel|gather_kernel|bucket_dedupe_kernel|unique_kernel|scan_reduce_kernel|scan_top_kernel|scan_down_kernel|summarise_\w+_kernel|row_reduce_kernel|row_gather_kernel|field_tile_\w+_kernel|tile_scan_kernel|hit_\w+_kernel|compact_kernel|dedup\w*|radix\w*|summ\w*)')
 
 
 def load(d, counter):
