@@ -15,7 +15,9 @@
  * (pointer, length) pairs — no NUL requirement.  The library owns everything
  * it returns until the matching *_free call.  Inputs are borrowed for the
  * duration of the call.  All entry points are re-entrant; concurrent queries
- * on one store are serialised per device internally.
+ * on one store are serialised per device internally, except request batches
+ * (sb_requests_*): each owns its device buffers, so passes of different
+ * batches on different streams overlap on the device.
  */
 #ifndef SBEACON_H
 #define SBEACON_H

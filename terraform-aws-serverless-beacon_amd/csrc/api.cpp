@@ -258,6 +258,7 @@ struct sb_batch {
     std::array<hipEvent_t, 2> ev{};
     size_t runs_pending = 0;
     float last_total_ms = 0;
+    std::mutex mu;  // request batches: one pass at a time per batch
     ~sb_batch() {
         for (auto e : ev)
             if (e) (void)hipEventDestroy(e);
@@ -3162,7 +3163,9 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
 int sb_requests_prepare(sb_store *s, const sb_request *r, size_t n, sb_batch **out) {
     return guard([&] {
         if (!s || (!r && n) || !out) throw Error(SB_EINVAL, "NULL argument");
-        std::lock_guard<std::mutex> lk(s->mu);
+        // request batches do not take the store lock: planning reads the
+        // store's host columns only, and each batch owns its device buffers
+        // (runs on separate streams overlap on the device)
         auto B = std::make_unique<sb_batch>();
         B->s = s;
         prepare_requests(*B, AosSrc{r}, n);
@@ -3176,7 +3179,6 @@ int sb_requests_prepare_columns(sb_store *s, const sb_request_columns *c, size_t
         static const sb_request_columns kNone{};
         const sb_request_columns &cc = c ? *c : kNone;
         check_columns(cc, n);
-        std::lock_guard<std::mutex> lk(s->mu);
         auto B = std::make_unique<sb_batch>();
         B->s = s;
         prepare_requests(*B, ColSrc{cc}, n);
@@ -3190,7 +3192,7 @@ int sb_requests_run(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_o
         if (!b->req) throw Error(SB_EINVAL, "not a request batch (sb_requests_prepare)");
         if ((!dev_rows && b->req->n_rows) || (!dev_hits && b->req->cap) || !dev_row_off)
             throw Error(SB_EINVAL, "NULL argument");
-        std::lock_guard<std::mutex> lk(b->s->mu);
+        std::lock_guard<std::mutex> lk(b->mu);  // this batch's buffers only (see sb_requests_prepare)
         run_requests(*b, dev_rows, dev_hits, dev_row_off, rec_base);
     });
 }

@@ -245,3 +245,47 @@ def test_shard_plan_stores_on_device():
     # record ids differ between the shard stores and the full store: compare
     # (POS, ALT index) through each store's records
     assert sum(len(h) for h in hits_by_row) == int(exp_ro[-1])
+
+
+def test_request_batches_concurrent_streams():
+    """Request batches take no store lock (sb_requests_prepare / _run): four
+    host threads, each preparing its own batch and running it on its own
+    stream, give the answers the batches give one at a time."""
+    import threading
+    import torch
+    from payload_gen import read_records
+    from sbeacon.engine import Store
+    from sbeacon.requests import RequestBatch, requests_from_split_payloads
+    path = os.path.join(FIXTURES, 'tiny22.vcf')
+    store = Store.build([('tiny22.vcf', path)], device=0)
+    recs, names = read_records(path)
+    sets = []
+    for t in range(4):
+        rng = random.Random(100 + t)
+        sets.append([_split_payload(rng, recs, names, 'tiny22.vcf') for _ in range(300)])
+    expect = []
+    for sps in sets:
+        arr, keep, owners = requests_from_split_payloads(store, sps, columns=True)
+        expect.append(RequestBatch(store, arr, len(owners)).answer())
+    got = [None] * 4
+    errors = []
+
+    def work(t):
+        try:
+            with torch.cuda.stream(torch.cuda.Stream(device=0)):
+                arr, keep, owners = requests_from_split_payloads(store, sets[t], columns=True)
+                b = RequestBatch(store, arr, len(owners))
+                for _ in range(3):
+                    got[t] = b.answer()
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors
+    for t in range(4):
+        for x, y in zip(got[t], expect[t]):
+            np.testing.assert_array_equal(x, y)
