@@ -122,18 +122,15 @@ def main_genome(args):
     sbat = prepare_shard_batch(store, sl)
     st = sbat.stats()
     sbat.free()
-    # Roofline of the request pass (eval + deliver), priced on the bytes it must move
-    # at least once: per chain its 80 B descriptor, two
-    # coarse-index entries (8 B), its row (40 B) and row offset (8 B); 24 B per
-    # candidate in the union of the chain windows (POS 4 + VtHot 16 + record
-    # 4, each once however many overlapping requests read it); 8 B per hit
-    # written.  Beside it the SURVEY §8d contract: 32 B x unique records in
-    # the slice windows + 8 B / hit.
+    # Roofline of the request pass, priced on the bytes it must move at least
+    # once.  request_eval_kernel: per request its 32 B chain
+    # descriptor (ReqChain), 40 B row and 8 B row count; 24 B per candidate in
+    # the union of the chain windows (POS 4 + VtHot 16 + record 4, each once
+    # however many overlapping requests read it); 8 B per hit staged.  Beside
+    # it the SURVEY §8d contract: 32 B x unique records in the slice windows +
+    # 8 B / hit.
     chains = int(pst['chains'])
-    # request_eval_kernel: its 80 B chain descriptor, 40 B row and 8 B row
-    # count per request, 24 B per candidate in the union of the windows, 8 B
-    # per hit staged
-    comp = (80.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * nhits
+    comp = (32.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * nhits
     achieved = comp / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     # the whole pass (eval + tile scan + delivery): + 8 B row offset per request
     # and the hits' dense copy (8 B read + 8 B written per hit)
@@ -195,7 +192,7 @@ def main_genome(args):
                                   f'the {"first slice" if args.deliver == "first" else "rank 0"} rank over '
                                   f'{"RCCL" if world > 1 else "(no peer)"}'},
         'step': 'request batch pass (request_eval_kernel: every request = one chain of its 10 kb slices, rows + '
-                'hits staged per run; request_deliver_kernel: offsets by a decoupled look-back over tiles of runs, '
+                'hits staged per run; request_tile_scan_kernel + request_deliver_kernel: offsets from run totals scanned over tiles of runs, '
                 'dense hit lists in request order) + exchange (send/recv of straddling rows and hits); inputs '
                 'resident in HBM',
         'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
@@ -210,7 +207,7 @@ def main_genome(args):
                                'its launch in each of K passes on its stream, averaged (rocprof per-kernel averages: '
                                'profiles/)',
                      'algorithmic_bytes_per_launch': r0[7],
-                     'pricing': 'bytes the launch must move at least once: 128 B/request (80 B chain descriptor + '
+                     'pricing': 'bytes the launch must move at least once: 80 B/request (32 B chain descriptor + '
                                 '40 B row + 8 B row count) + 24 B per candidate in the union of the chain windows + '
                                 '8 B/hit staged',
                      'pass': {'ms': round(r0[10], 4), 'achieved': round(r0[11], 1),

@@ -169,6 +169,7 @@ def summarise_cpu(file, slices, got):
 def dedup_line(args, store, datasets, files):
     jobs = [([loc for loc, _ in parts], '22', 0, 2**32 - 1) for _, parts in datasets]
     union = [([loc for loc, _ in files], '22', 0, 2**32 - 1)]
+    log(f'dedup: {len(jobs)} jobs, warmup')
     for _ in range(args.warmup):
         store.dedup_counts(jobs)
     dev, keys = [], 0
@@ -182,6 +183,7 @@ def dedup_line(args, store, datasets, files):
         keys = st['keys']
     wall = (time.perf_counter() - t) / args.steps
     dev_ms = sum(dev) / len(dev)
+    log(f'dedup: {wall * 1e3:.3f} ms per call, device {dev_ms:.3f} ms')
     ures, ust = store.dedup_counts(union, with_stats=True)
     ures, ust = store.dedup_counts(union, with_stats=True)
     alg = 8.0 * keys  # compulsory: one read of the 64-bit key stream
@@ -250,6 +252,7 @@ def strict_sample(args, store, datasets):
             slices, _, _ = summarise_vcf(store, loc)
             keys += region_file_keys(store, loc, slices, refs)
         msgs += init_duplicate_variant_search(ds, [loc for loc, _ in parts], keys, tally=DuplicateTally())
+        log(f'strict: dataset {ds} planned ({len(msgs)} messages, {len(refs)} region files)')
     out = {'datasets': min(args.strict_datasets, len(datasets)), 'messages': len(msgs),
            'region_files': len(refs)}
     for mode, fr in (('strict', refs), ('intended', None)):
@@ -259,6 +262,7 @@ def strict_sample(args, store, datasets):
         for _ in range(reps):
             res = dedup_batch(msgs, registry=reg, file_refs=fr)
         dt = (time.perf_counter() - t) / reps
+        log(f'strict: {mode} {dt * 1e3:.2f} ms per call')
         out[mode] = {'ms_per_call': round(dt * 1e3, 2), 'unique_sum': int(sum(r for r in res if isinstance(r, int))),
                      'raised': int(sum(isinstance(r, Exception) for r in res))}
     out['note'] = ('one dedup_batch call of every message of these datasets per mode; strict = the reference\'s '

@@ -177,6 +177,82 @@ sb_store::~sb_store() {
 }
 
 // ------------------------------------------------------------------ batch
+// Request batches' buffers, pooled per store (sb_store::req_pool): planning
+// stages descriptors in pinned host memory and a pass needs seven device
+// buffers; allocating them per batch (hipHostMalloc pins pages, hipFree
+// synchronises the device) cost more than the pass itself.  Best fit among
+// the free buffers no more than twice the size asked for; bounded.
+struct ReqPool {
+    struct Pinned {
+        void *p = nullptr;
+        size_t bytes = 0;
+    };
+    std::mutex mu;
+    std::vector<Pinned> pinned;
+    std::vector<DevMem> dev;
+    static constexpr size_t kKeep = 64;
+    ~ReqPool() {
+        for (Pinned &x : pinned) (void)hipHostFree(x.p);
+    }
+    template <class V>
+    static ptrdiff_t fit(const V &v, size_t n) {
+        ptrdiff_t best = -1;
+        for (size_t i = 0; i < v.size(); ++i)
+            if (v[i].bytes >= n && v[i].bytes <= 2 * n + (1u << 20) && (best < 0 || v[i].bytes < v[best].bytes))
+                best = static_cast<ptrdiff_t>(i);
+        return best;
+    }
+    Pinned get_pinned(size_t n) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            const ptrdiff_t i = fit(pinned, n);
+            if (i >= 0) {
+                Pinned x = pinned[i];
+                pinned.erase(pinned.begin() + i);
+                return x;
+            }
+        }
+        Pinned x;
+        x.bytes = std::max<size_t>(n + n / 4, 4096);
+        HIP_OK(hipHostMalloc(&x.p, x.bytes, hipHostMallocDefault));
+        return x;
+    }
+    void put_pinned(Pinned x) {
+        std::lock_guard<std::mutex> lk(mu);
+        pinned.push_back(x);
+        if (pinned.size() > kKeep) {
+            (void)hipHostFree(pinned.front().p);
+            pinned.erase(pinned.begin());
+        }
+    }
+    DevMem get_dev(size_t n) {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            const ptrdiff_t i = fit(dev, n);
+            if (i >= 0) {
+                DevMem x = std::move(dev[i]);
+                dev.erase(dev.begin() + i);
+                return x;
+            }
+        }
+        DevMem x;
+        x.alloc(n + n / 4);
+        return x;
+    }
+    void put_dev(DevMem &&x) {
+        std::lock_guard<std::mutex> lk(mu);
+        dev.push_back(std::move(x));
+        if (dev.size() > kKeep) dev.erase(dev.begin());
+    }
+};
+
+std::shared_ptr<ReqPool> req_pool(sb_store &s) {
+    std::call_once(s.req_pool_once, [&] {
+        s.req_pool = std::shared_ptr<void>(new ReqPool, [](void *w) { delete static_cast<ReqPool *>(w); });
+    });
+    return std::shared_ptr<ReqPool>(s.req_pool, static_cast<ReqPool *>(s.req_pool.get()));
+}
+
 struct sb_batch {
     sb_store *s = nullptr;
     uint32_t nq = 0;
@@ -231,12 +307,11 @@ struct sb_batch {
     // request batches (sb_requests_prepare): rows = requests
     struct Req {
         uint32_t n_rows = 0;
-        std::vector<ChainDev> chains;  // one per chain-answered request (s0 = its row)
         std::vector<RowRun> runs;
         uint64_t cap = 0;              // output hit capacity
         uint64_t n_chain_slices = 0;
         uint32_t n_lut = 0;            // LUT words (request_eval_kernel stages them in LDS when they fit)
-        uint64_t n_chains = 0;         // chain-answered requests (chains holds them padded per run)
+        uint64_t n_chains = 0;         // chain-answered requests (dchains holds them padded per run)
         // sb_requests_time_eval: events around every pass's request_eval_kernel
         bool time_eval = false;
         std::vector<std::array<hipEvent_t, 2>> eval_ev;
@@ -246,8 +321,15 @@ struct sb_batch {
             for (auto &p : eval_ev)
                 for (auto e : p) (void)hipEventDestroy(e);
         }
-        DevMem dchains, druns, status, tstatus, stage, row_src, lut, sseg, sherr;
+        // dchains: ReqChain slots (kPackRun per run), then the RowRuns at runs_at
+        DevMem dchains, status, tstatus, stage, row_src, lut, sseg, sherr;
+        size_t runs_at = 0;
+        std::shared_ptr<ReqPool> pool;  // where the device buffers go back when the batch is freed
         bool slices = false;           // some rows answered per slice (the batch's query part)
+        void give_back() {
+            for (DevMem *m : {&dchains, &status, &tstatus, &stage, &row_src, &lut, &sseg, &sherr})
+                if (m->p) pool->put_dev(std::move(*m));
+        }
     };
     std::unique_ptr<Req> req;
     // general records (general_slice_kernel): work list [count, launch
@@ -262,6 +344,10 @@ struct sb_batch {
     ~sb_batch() {
         for (auto e : ev)
             if (e) (void)hipEventDestroy(e);
+        if (req && req->pool) {  // the pass may still be in flight on the batch's stream
+            (void)hipStreamSynchronize(strm());
+            req->give_back();
+        }
     }
 };
 
@@ -279,6 +365,9 @@ struct sb_result_set {
     std::vector<uint8_t> vbuilt, nbuilt;
     std::string distinct;                       // sb_result_distinct_variants
     std::vector<std::string> vt_json;           // escaped VT strings (sb::result_prepare_json)
+    // per VCF of the set, per header sample: its name as JSON list items
+    // (sb::result_prepare_json; "\x01" = not UTF-8)
+    std::vector<std::vector<std::string>> names_json;
     std::vector<uint32_t> tmp_rec, tmp_alt;     // views for sb_result_get
     // queries whose counts need more than 64 bits: 2 x big_limbs limbs each
     uint32_t big_limbs = 0;
@@ -2926,15 +3015,18 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     std::vector<uint32_t> &lut_all = V.lut_all;
     lut_all.insert(lut_all.end(), 8, 0u);
     tick("vtypes");
-    // classify: 0 = no slices, 1 = one chain, 2 = per slice
-    std::vector<uint8_t> cls(n, 0);
-    for (size_t i = 0; i < n; ++i) {
-        const sb_request x = src(i);
-        if (x.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "request " + std::to_string(i) + ": unknown vcf id");
-        if (!x.reference_bases && x.reference_len) throw Error(SB_EINVAL, "request " + std::to_string(i) + ": bad REF");
-    }
+    // classify: 0 = no slices, 1 = one chain, 2 = per slice (and the slice
+    // count of a chain); the first bad request, if any, is reported
+    std::vector<uint8_t> cls(n, 0), nsl_of(n, 0);
+    std::atomic<size_t> bad{SIZE_MAX};
     parallel_for(n, [&](size_t i) {
         const sb_request x = src(i);
+        if (x.vcf_id >= s.vcfs.size() || (!x.reference_bases && x.reference_len)) {
+            size_t b = bad.load(std::memory_order_relaxed);
+            while (i < b && !bad.compare_exchange_weak(b, i, std::memory_order_relaxed)) {
+            }
+            return;
+        }
         const VcfData &v = s.vcfs[x.vcf_id];
         if (x.contig >= v.segments.size() || x.start_min > x.start_max) return;  // bcftools emits nothing / no slice
         const int64_t nsl = (x.start_max - x.start_min) / kSplitSize + 1;
@@ -2950,57 +3042,15 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
             if (a != sp.end() && *a <= static_cast<uint64_t>(x.start_max)) chain = false;
         }
         cls[i] = chain ? 1 : 2;
+        if (chain) nsl_of[i] = static_cast<uint8_t>(nsl);
     });
-    tick("classify");
-    // chains in row order
-    std::vector<uint32_t> chain_of(n, UINT32_MAX);
-    uint32_t nc = 0;
-    for (size_t i = 0; i < n; ++i)
-        if (cls[i] == 1) chain_of[i] = nc++;
-    R->chains.resize(nc);
-    std::vector<uint64_t> ccap(nc, 0);
-    parallel_for(n, [&](size_t i) {
-        if (cls[i] != 1) return;
+    if (bad.load() != SIZE_MAX) {
+        const size_t i = bad.load();
         const sb_request x = src(i);
-        const VcIndex &vi = s.vcfs[x.vcf_id].vc_index[x.contig][vt_of[i]];
-        ChainDev &cd = R->chains[chain_of[i]];
-        cd = ChainDev{};
-        cd.s0 = static_cast<uint32_t>(i);
-        cd.n = static_cast<uint32_t>((x.start_max - x.start_min) / kSplitSize + 1);
-        cd.first = static_cast<uint32_t>(x.start_min);
-        cd.last = static_cast<uint32_t>(x.start_max);
-        cd.width = static_cast<uint32_t>(kSplitSize);
-        cd.c_lo = vi.c_lo;
-        cd.c_hi = vi.c_hi;
-        cd.cb_base = vi.base;
-        cd.cb_off = vi.off;
-        cd.cb_shift = vi.shift;
-        cd.cb_n = vi.n;
-        const int64_t emin = x.end_min, emax = x.end_max;
-        const bool end_void = emax < 0 || emin > 0xffffffffll || emin > emax;
-        cd.e0 = emin < 0 ? 0u : static_cast<uint32_t>(emin);
-        cd.espan = (emax > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(emax)) - cd.e0;
-        const int64_t vmax = x.variant_max_length < 0 ? INT64_MAX : x.variant_max_length;
-        const int64_t vl = x.variant_min_length < 0 ? 0 : x.variant_min_length, vh = vmax > 255 ? 255 : vmax;
-        cd.vlo = vh < vl ? 256u : static_cast<uint32_t>(vl);
-        cd.vspan = vh < vl ? 0u : static_cast<uint32_t>(vh - vl);
-        cd.kind = vt_of[i] | (end_void ? kChainEndVoid : 0u);
-        cd.lut_off = lut_of[i];
-        cd.out = 0;
-        // hit capacity: every ALT of the coarse-index candidate range
-        auto cb = [&](uint64_t xx, uint32_t up) -> uint32_t {
-            if (xx <= cd.cb_base) return cd.c_lo;
-            const uint64_t b = (xx - cd.cb_base) >> cd.cb_shift;
-            return b >= cd.cb_n ? cd.c_hi : s.h_vc_bucket[cd.cb_off + b + up];
-        };
-        const uint32_t C0 = cb(cd.first, 0), C1 = end_void ? C0 : std::max(C0, cb(uint64_t(cd.last) + 1, 1));
-        ccap[chain_of[i]] = s.h_vc_altpre[C1] - s.h_vc_altpre[C0];
-        // request chains carry their candidate range itself (request_eval_kernel)
-        cd.c_lo = C0;
-        cd.c_hi = C1;
-    });
-    for (const ChainDev &c : R->chains) R->n_chain_slices += c.n;
-    tick("chains");
+        if (x.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "request " + std::to_string(i) + ": unknown vcf id");
+        throw Error(SB_EINVAL, "request " + std::to_string(i) + ": bad REF");
+    }
+    tick("classify");
     // the per-slice part: splitQuery's slices of the other requests, in row order
     std::vector<sb_query> qs;
     std::vector<uint32_t> owner;
@@ -3049,77 +3099,113 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     for (uint32_t o : owner) ++seg[o + 1];
     for (size_t w = 0; w < n; ++w) seg[w + 1] += seg[w];
     // runs of consecutive rows (<= kRunRows rows, kPackRun chains, kPackSlots slots)
-    uint64_t stage_total = 0;  // staging slots: every run's chain hit capacity, back to back
     {
         RowRun cur{0, 0, 0, 0, 0, 0, kRunSimple};
-        uint64_t cap = 0;
-        auto close = [&](uint32_t row_hi) {
-            cur.row_hi = row_hi;
-            cur.stage = stage_total;
-            stage_total += cap;
-            R->runs.push_back(cur);
-        };
         uint32_t c = 0;
         for (uint32_t i = 0; i < n; ++i) {
             const bool ch = cls[i] == 1;
-            const uint32_t need = ch ? R->chains[c].n : 0u;
+            const uint32_t need = nsl_of[i];
             if (i > cur.row_lo && (i - cur.row_lo == kRunRows || (ch && (cur.c_hi - cur.c_lo == pack_run_max() ||
                                                                            cur.n_slots + need > pack_slots_max())))) {
-                close(i);
+                cur.row_hi = i;
+                R->runs.push_back(cur);
                 cur = RowRun{i, i, c, c, 0, 0, kRunSimple};
-                cap = 0;
             }
             if (cls[i] == 2) cur.flags &= ~kRunSimple;  // a row answered per slice: gathered row by row
             if (ch) {
                 cur.c_hi = ++c;
                 cur.n_slots += need;
-                cap += ccap[c - 1];
+                R->n_chain_slices += need;
             }
         }
-        if (n) close(static_cast<uint32_t>(n));
+        if (n) {
+            cur.row_hi = static_cast<uint32_t>(n);
+            R->runs.push_back(cur);
+        }
+        R->n_chains = c;
     }
-    R->cap = B.cap_total;
-    for (uint64_t x : ccap) R->cap += x;
     tick("runs");
-    // device buffers
+    // chain descriptors straight into pinned staging, kPackRun slots per run
+    // (request_eval_kernel loads a run's slots beside its RowRun), the runs
+    // after them: one H2D copy from pinned memory
+    const size_t n_runs = R->runs.size(), slots = pack_run_max();
+    const size_t chain_bytes = n_runs * slots * sizeof(ReqChain), run_bytes = n_runs * sizeof(RowRun);
+    R->pool = req_pool(s);
+    ReqPool::Pinned pin = R->pool->get_pinned(chain_bytes + run_bytes);
+    ReqChain *hc = static_cast<ReqChain *>(pin.p);
+    RowRun *hr = reinterpret_cast<RowRun *>(static_cast<char *>(pin.p) + chain_bytes);
+    std::vector<uint64_t> rcap(n_runs, 0);  // each run's hit capacity (staging slots)
+    parallel_for(n_runs, [&](size_t r) {
+        const RowRun &run = R->runs[r];
+        ReqChain *out = hc + r * slots;
+        uint32_t j = 0;
+        uint64_t cap = 0;
+        for (uint32_t i = run.row_lo; i < run.row_hi; ++i) {
+            if (cls[i] != 1) continue;
+            const sb_request x = src(i);
+            const VcIndex &vi = s.vcfs[x.vcf_id].vc_index[x.contig][vt_of[i]];
+            ReqChain &cd = out[j++];
+            cd.first = static_cast<uint32_t>(x.start_min);
+            cd.last = static_cast<uint32_t>(x.start_max);
+            const int64_t emin = x.end_min, emax = x.end_max;
+            const bool end_void = emax < 0 || emin > 0xffffffffll || emin > emax;
+            cd.e0 = emin < 0 ? 0u : static_cast<uint32_t>(emin);
+            cd.espan = (emax > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(emax)) - cd.e0;
+            const int64_t vmax = x.variant_max_length < 0 ? INT64_MAX : x.variant_max_length;
+            const int64_t vl = x.variant_min_length < 0 ? 0 : x.variant_min_length, vh = vmax > 255 ? 255 : vmax;
+            cd.bits = req_bits(vh < vl ? 256u : static_cast<uint32_t>(vl), vh < vl ? 0u : static_cast<uint32_t>(vh - vl),
+                               i - run.row_lo, vt_of[i], end_void);
+            cd.lut_off = lut_of[i];
+            // the candidate range from the (kind, segment) coarse index; hit
+            // capacity: every ALT of it
+            auto cb = [&](uint64_t xx, uint32_t up) -> uint32_t {
+                if (xx <= vi.base) return vi.c_lo;
+                const uint64_t b = (xx - vi.base) >> vi.shift;
+                return b >= vi.n ? vi.c_hi : s.h_vc_bucket[vi.off + b + up];
+            };
+            const uint32_t C0 = cb(cd.first, 0), C1 = end_void ? C0 : std::max(C0, cb(uint64_t(cd.last) + 1, 1));
+            cd.c_lo = C0;
+            cd.c_hi = C1;
+            cap += s.h_vc_altpre[C1] - s.h_vc_altpre[C0];
+        }
+        std::memset(static_cast<void *>(out + j), 0, (slots - j) * sizeof(ReqChain));  // empty slots: first == 0
+        rcap[r] = cap;
+    });
+    uint64_t stage_total = 0;  // staging slots: every run's chain hit capacity, back to back
+    for (size_t r = 0; r < n_runs; ++r) {
+        R->runs[r].stage = stage_total;
+        stage_total += rcap[r];
+    }
+    std::memcpy(static_cast<void *>(hr), R->runs.data(), run_bytes);
+    R->cap = B.cap_total + stage_total;
+    tick("chains");
+    // device buffers (pooled per store: a batch returns them when freed)
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
-    // chain descriptors padded to kPackRun slots per run (request_eval_kernel
-    // loads a run's descriptors beside its RowRun, n == 0 marks an empty slot)
-    {
-        const uint32_t slots = pack_run_max();
-        std::vector<ChainDev> padded(R->runs.size() * slots, ChainDev{});
-        for (size_t r = 0; r < R->runs.size(); ++r)
-            std::copy(R->chains.begin() + R->runs[r].c_lo, R->chains.begin() + R->runs[r].c_hi,
-                      padded.begin() + r * slots);
-        R->n_chains = R->chains.size();
-        R->chains = std::move(padded);
-    }
-    R->dchains.alloc(R->chains.size() * sizeof(ChainDev));
-    R->druns.alloc(R->runs.size() * sizeof(RowRun));
-    R->status.alloc(R->runs.size() * 8);
-    R->tstatus.alloc(size_t(request_tiles(static_cast<uint32_t>(R->runs.size()))) * 8);
-    R->stage.alloc(stage_total * 8);
-    R->row_src.alloc(R->slices || std::any_of(R->runs.begin(), R->runs.end(),
-                                              [](const RowRun &r) { return !(r.flags & kRunSimple); })
-                         ? size_t(n) * 8 : 0);
-    R->lut.alloc(lut_all.size() * 4);
+    ReqPool &P = *R->pool;
+    R->dchains = P.get_dev(chain_bytes + run_bytes);
+    R->status = P.get_dev(n_runs * 8);
+    R->tstatus = P.get_dev(size_t(request_tiles(static_cast<uint32_t>(n_runs))) * 8);
+    R->stage = P.get_dev(stage_total * 8);
+    R->row_src = P.get_dev(R->slices || std::any_of(R->runs.begin(), R->runs.end(),
+                                                    [](const RowRun &r) { return !(r.flags & kRunSimple); })
+                               ? size_t(n) * 8 : 0);
+    R->lut = P.get_dev(lut_all.size() * 4);
     R->n_lut = static_cast<uint32_t>(lut_all.size());
-    if (!R->chains.empty())
-        HIP_OK(hipMemcpyAsync(R->dchains.p, R->chains.data(), R->chains.size() * sizeof(ChainDev),
-                              hipMemcpyHostToDevice, st));
-    if (!R->runs.empty())
-        HIP_OK(hipMemcpyAsync(R->druns.p, R->runs.data(), R->runs.size() * sizeof(RowRun), hipMemcpyHostToDevice, st));
+    if (chain_bytes + run_bytes)
+        HIP_OK(hipMemcpyAsync(R->dchains.p, pin.p, chain_bytes + run_bytes, hipMemcpyHostToDevice, st));
+    R->runs_at = chain_bytes;
     HIP_OK(hipMemcpyAsync(R->lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
     if (R->slices) {
         std::vector<uint8_t> he(std::max<size_t>(B.nq, 1), 0);
         for (uint32_t q = 0; q < B.nq; ++q) he[q] = B.host_err[q] ? 1 : 0;
-        R->sseg.alloc(seg.size() * 4);
-        R->sherr.alloc(he.size());
+        R->sseg = P.get_dev(seg.size() * 4);
+        R->sherr = P.get_dev(he.size());
         HIP_OK(hipMemcpyAsync(R->sseg.p, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, st));
         HIP_OK(hipMemcpyAsync(R->sherr.p, he.data(), he.size(), hipMemcpyHostToDevice, st));
     }
     HIP_OK(hipStreamSynchronize(st));
+    P.put_pinned(pin);
     tick("upload");
     B.req = std::move(R);
 }
@@ -3148,7 +3234,8 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
         }
         ev = R.eval_ev[R.eval_used++];
     }
-    launch_request_rows(d, R.dchains.as<ChainDev>(), R.druns.as<RowRun>(), static_cast<uint32_t>(R.runs.size()),
+    launch_request_rows(d, R.dchains.as<ReqChain>(), reinterpret_cast<const RowRun *>(R.dchains.as<char>() + R.runs_at),
+                        static_cast<uint32_t>(R.runs.size()),
                         R.status.as<unsigned long long>(), R.tstatus.as<unsigned long long>(),
                         R.slices ? B.res.as<QRes>() : nullptr,
                         R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
@@ -3548,6 +3635,48 @@ void result_prepare_json(sb_result_set *r) {
     r->vt_json.resize(items.size());
     for (size_t k = 0; k < items.size(); ++k)
         if (!json_escape_append(r->vt_json[k], items[k].data(), items[k].size())) r->vt_json[k] = std::string("\x01");
+    // sample names: the reference joins the selected names with ',' and the
+    // response lists the pieces of splitting that text on ',' -- per name,
+    // the pieces of the name split on ','
+    r->names_json.assign(r->s->vcfs.size(), {});
+    std::vector<uint8_t> need(r->s->vcfs.size(), 0);
+    for (size_t i = 0; i < r->res.size(); ++i)
+        if (!r->sidx[i].empty()) need[r->vcf_of[i]] = 1;
+    for (size_t f = 0; f < need.size(); ++f) {
+        if (!need[f]) continue;
+        const auto &names = r->s->vcfs[f].samples;
+        auto &out = r->names_json[f];
+        out.resize(names.size());
+        for (size_t h = 0; h < names.size(); ++h) {
+            const std::string &nm = names[h];
+            std::string &o = out[h];
+            size_t a = 0;
+            for (size_t k = 0; k <= nm.size(); ++k)
+                if (k == nm.size() || nm[k] == ',') {
+                    if (a) o += ", ";
+                    o.push_back('"');
+                    if (!json_escape_append(o, nm.data() + a, k - a)) {
+                        o = std::string("\x01");
+                        break;
+                    }
+                    o.push_back('"');
+                    a = k + 1;
+                }
+        }
+    }
+}
+
+bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o) {
+    const auto &ix = r->sidx[i];
+    const auto &nj = r->names_json[r->vcf_of[i]];
+    for (size_t j = 0; j < ix.size(); ++j) {
+        const uint32_t h = r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j];
+        const std::string &x = nj[h];
+        if (x.size() == 1 && x[0] == '\x01') return false;
+        if (j) o += ", ";
+        o += x;
+    }
+    return true;
 }
 
 bool result_variants_json(const sb_result_set *r, size_t i, std::string &o) {

@@ -211,12 +211,12 @@ constexpr uint32_t kChainEndVoid = 1u << 8;  // no END can match
 
 // Request batches (sb_requests_prepare / sb_requests_run): every request is a
 // row; request_eval_kernel answers one run of consecutive rows per wave --
-// the rows' chains (ChainDev::s0 = the chain's row) evaluated as
+// the rows' chains (ReqChain, below) evaluated as
 // chain_pack_kernel does, their hits appended to the run's staging region --
 // and request_deliver_kernel writes the rows' offsets and hits densely in row
-// order at the run's offset, found by a decoupled look-back over the runs'
-// status words (the other rows' hits, from per-slice queries answered
-// before, gathered there too).
+// order at the run's offset, from the runs' totals and a scan over tiles of
+// runs (the other rows' hits, from per-slice queries answered before,
+// gathered there too).
 constexpr uint32_t kRunRows = 64;     // rows per run at most (one lane each)
 constexpr uint32_t kRunSimple = 1u;   // RowRun::flags: no row of the run is answered per slice
 struct alignas(16) RowRun {
@@ -227,6 +227,23 @@ struct alignas(16) RowRun {
     uint32_t flags;           // kRunSimple
 };
 static_assert(sizeof(RowRun) == 32, "RowRun is two 16-byte words");
+
+// A request's chain as request_eval_kernel reads it (kPackRun slots per run,
+// first == 0 = an empty slot): splitQuery's slices are [first + j * kReqWidth,
+// ...] up to `last`, so width and slice count follow from the window; the
+// row, kind and length bounds share one word.  32 B, not ChainDev's 80.
+constexpr uint32_t kReqWidth = 10000;  // lambda/splitQuery/lambda_function.py:12
+struct alignas(16) ReqChain {
+    uint32_t first, last;  // the request's [start_min, start_max] (first >= 1)
+    uint32_t c_lo, c_hi;   // candidate range (host-resolved from the coarse index)
+    uint32_t e0, espan;    // END in [e0, e0 + espan]
+    uint32_t bits;         // vlo : 9 | vspan : 8 | row - run.row_lo : 6 | vt kind : 3 | end void : 1
+    uint32_t lut_off;      // symbolic-ALT LUT of the request's variantType
+};
+static_assert(sizeof(ReqChain) == 32, "ReqChain is two 16-byte words");
+__host__ __device__ constexpr uint32_t req_bits(uint32_t vlo, uint32_t vspan, uint32_t row, uint32_t kind, bool end_void) {
+    return vlo | vspan << 9 | row << 17 | kind << 23 | (end_void ? 1u << 26 : 0u);
+}
 
 // bit c set = an ALT of class c satisfies variantType `kind` (vtype_hit)
 __host__ __device__ constexpr uint32_t vt_class_mask(uint32_t kind) {

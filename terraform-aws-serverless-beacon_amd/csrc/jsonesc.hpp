@@ -78,5 +78,7 @@ inline bool json_escape_append(std::string &o, const char *s, size_t n) {
 // result_variants_json may run on many threads for different i.
 void result_prepare_json(sb_result_set *r);
 bool result_variants_json(const sb_result_set *r, size_t i, std::string &o);
+// the sample_names list items of query i (false: a name that is not UTF-8)
+bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o);
 
 }  // namespace sb

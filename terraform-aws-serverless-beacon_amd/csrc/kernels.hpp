@@ -104,7 +104,7 @@ void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, ui
 // row order, one wave per run, offsets by decoupled look-back (ticket and
 // status zeroed by the caller; status n_runs words).  sres..shits: the
 // batch's per-slice part (rows of it already reduced into `rows`), or null.
-void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun *runs, uint32_t n_runs,
+void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun *runs, uint32_t n_runs,
                          unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,

@@ -1904,16 +1904,18 @@ __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__res
 // The wave writes its rows, each row's hit count (into row_off) and the run's
 // total as an aggregate status word.
 //
-// request_deliver_kernel -- one wave per run: the run's output offset by a
-// decoupled look-back over the status words (every aggregate is already
-// published, so no wave ever waits), row offsets, and the hits copied to the
-// dense output: one contiguous copy for a run of chain rows only; row by row
-// where some rows were answered per slice (queries of the batch's slice part,
-// reduced into `rows` by request_reduce before the first kernel).
+// request_tile_scan_kernel -- the tile totals (16 runs a tile) into tile offsets.
 //
-// A single-pass form (hits held in LDS until the look-back resolved) made
-// every wave wait for its slowest predecessor's evaluation: 0.27 ms vs the two
-// launches' sum.
+// request_deliver_kernel -- one wave per run: the run's output offset (its
+// tile's offset + the earlier runs' totals of the tile), row offsets, and the
+// hits copied to the dense output: one contiguous copy for a run of chain rows
+// only; row by row where some rows were answered per slice (queries of the
+// batch's slice part, reduced into `rows` by request_reduce before the first
+// kernel).
+//
+// A single-pass form (hits held in LDS until a decoupled look-back over the
+// runs resolved) made every wave wait for its slowest predecessor's
+// evaluation: 0.27 ms vs the launches' sum.
 struct ReqLds {
     uint4 pred[kPackRun * 3];  // per chain: {first, last, n, width}, {e0, espan, vlo, vspan},
                                // {class mask, extra-ALT bits | end_void << 31, 1/width (f32), LUT offset}
@@ -1924,44 +1926,6 @@ struct ReqLds {
     unsigned int ccount[kPackRun];
     uint8_t rowchain[kRunRows];         // row (run-relative) -> its chain (0xff: not a chain row)
 };
-
-// Decoupled look-back over one 64-bit status word per run {flag : 2 | value :
-// 62}: flag 1 = the run's own total, 2 = its inclusive prefix, 0 = not yet
-// published.  A word carries its value, so relaxed agent-scope (sc1) stores and
-// loads are enough -- no release / acquire fences, which on gfx950 are an XCD
-// L2 write-back / an L1 invalidate of microseconds EACH (one per poll made the
-// serial form of this loop ~0.9 us per run).  The wave reads 64 predecessors per
-// round (lane j: run top - j) and stops at the nearest inclusive prefix.
-// Returns the exclusive prefix (wave-uniform) and publishes excl + H.
-__device__ __forceinline__ uint64_t lookback_exclusive(unsigned long long *__restrict__ status, uint32_t w,
-                                                       uint64_t H) {
-    constexpr unsigned long long kAgg = 1ull << 62, kPre = 2ull << 62, kVal = (1ull << 62) - 1;
-    const uint32_t ul = static_cast<uint32_t>(lane_id());
-    // the aggregate first: successors sum it instead of waiting for this prefix
-    if (ul == 0) __hip_atomic_store(&status[w], kAgg | H, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t excl = 0;
-    int64_t top = static_cast<int64_t>(w) - 1;
-    uint32_t spins = 0;  // bounded: never hang the queue
-    while (top >= 0) {
-        const int64_t j = top - static_cast<int64_t>(ul);
-        const unsigned long long s =
-            j >= 0 ? __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kPre;
-        const uint64_t pre = __ballot((s >> 62) == 2);
-        const uint64_t low = pre & (~pre + 1);                      // the nearest prefix (lowest lane)
-        const uint64_t need = pre ? (low | (low - 1)) : ~0ull;      // lanes up to and including it
-        if (__ballot((s >> 62) == 0) & need) {
-            if (++spins >= (1u << 22)) break;
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        const int64_t v = ((need >> ul) & 1ull) ? static_cast<int64_t>(s & kVal) : 0;
-        excl += static_cast<uint64_t>(rdl64(wave_incl_scan_i64(v), kWave - 1));
-        if (pre) break;
-        top -= kWave;
-    }
-    if (ul == 0) __hip_atomic_store(&status[w], kPre | (excl + H), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return excl;
-}
 
 struct RowChunk {
     ChainChunk x;
@@ -1977,7 +1941,7 @@ constexpr uint32_t kDeliverTile = 16;  // runs per request_deliver_kernel wave
 
 template <bool LDS_LUT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_eval_kernel(
-    DStore st, const ChainDev *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
+    DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
     unsigned long long *__restrict__ status, unsigned long long *__restrict__ tstatus, const QRes *__restrict__ sres,
     ReqPartial *__restrict__ rows, uint64_t *__restrict__ row_cnt, uint64_t *__restrict__ row_src,
     uint64_t *__restrict__ stage, uint32_t n_lut, uint32_t n_tiles) {
@@ -1993,30 +1957,30 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const uint32_t w = launch_wave();
     if (w >= n_runs) return;
     // the run record and the run's chain descriptors (kPackRun slots per run,
-    // n == 0 = an empty slot) are independent loads: one round trip for both
+    // first == 0 = an empty slot) are independent loads: one round trip for both
     const RowRun rr = runs[w];
-    ChainDev C{};
+    ReqChain C{};
     if (ul < kPackRun) C = chains[static_cast<uint64_t>(w) * kPackRun + ul];
     const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
     const uint64_t stage_at = uniform64(rr.stage);
     const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
-    const uint32_t R = static_cast<uint32_t>(__popcll(__ballot(ul < kPackRun && C.n != 0)));
+    const uint32_t R = static_cast<uint32_t>(__popcll(__ballot(ul < kPackRun && C.first != 0)));
     const uint32_t nrows = row_hi - row_lo;
     // ---- setup: lane k < R = chain k (descriptor, predicate constants, candidate bounds)
     uint32_t rowk = 0, c0 = 0, cnt = 0, nsl = 0;
     if (ul < R) {
-        rowk = C.s0;
-        VtPred q(st, 0u, 0u, 0u, 0u, C.kind, 0u, 0u, 0u);
-        L.pred[3 * ul] = uint4{C.first, C.last, C.n, C.width};
-        L.pred[3 * ul + 1] = uint4{C.e0, C.espan, C.vlo, C.vspan};
-        L.pred[3 * ul + 2] = uint4{q.cmask, q.xneed | (q.end_void ? 0x80000000u : 0u),
-                                   __float_as_uint(__frcp_rn(static_cast<float>(C.width))), C.lut_off};
+        rowk = row_lo + ((C.bits >> 17) & 63u);
+        const uint32_t kind = ((C.bits >> 23) & 7u) | ((C.bits >> 26) & 1u ? kChainEndVoid : 0u);
+        VtPred q(st, 0u, 0u, 0u, 0u, kind, 0u, 0u, 0u);
+        nsl = (C.last - C.first) / kReqWidth + 1;
+        L.pred[3 * ul] = uint4{C.first, C.last, nsl, 0u};
+        L.pred[3 * ul + 1] = uint4{C.e0, C.espan, C.bits & 511u, (C.bits >> 9) & 255u};
+        L.pred[3 * ul + 2] = uint4{q.cmask, q.xneed | (q.end_void ? 0x80000000u : 0u), 0u, C.lut_off};
         // the chain's candidate range [c_lo, c_hi): resolved on the host at
         // prepare (the same coarse-index bounds it sizes the staging with), so
         // the candidate loads follow the descriptor load directly
         c0 = C.c_lo;
         cnt = C.c_hi - C.c_lo;
-        nsl = C.n;
         L.tcc[ul] = 0;
         L.tan[ul] = 0;
         L.slow[ul] = 0;
@@ -2067,7 +2031,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint32_t g = base + ul;
         const bool valid = g < T;
         const uint4 p0 = L.pred[3 * k], p1 = L.pred[3 * k + 1], p2 = L.pred[3 * k + 2];
-        const uint32_t first = p0.x, last = p0.y, n = p0.z, width = p0.w;
+        const uint32_t first = p0.x, last = p0.y, n = p0.z;
         VtPred Pd(p1.x, p1.y, p1.z, p1.w, p2.x, p2.y & 0x7fffffffu, (p2.y >> 31) != 0, lut_base + p2.w);
         const bool inwin = valid && x.p >= first && x.p <= last;
         const bool cand = inwin && Pd.end_ok(x.h.end);
@@ -2105,13 +2069,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 sdst[at++] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
         }
         hpos += tot;
-        // slice = (POS - first) / width: an f32 estimate within one of the
-        // quotient, corrected (d < 2^24: a chain spans <= kChainMax 10 kb slices)
-        const uint32_t d = x.p - first;
-        uint32_t qt = static_cast<uint32_t>(static_cast<float>(d) * __uint_as_float(p2.z));
-        qt -= qt * width > d ? 1u : 0u;
-        qt += (qt + 1) * width <= d ? 1u : 0u;
-        const uint32_t slot = c.so + min(qt, n - 1);
+        // slice = (POS - first) / kReqWidth (a constant divisor: multiply-high + shift)
+        const uint32_t slot = c.so + min((x.p - first) / kReqWidth, n - 1);
         if (hit) {
             atomicOr(&L.exw[slot >> 5], o.c > 0 ? 1u << (slot & 31u) : 0u);
             atomicAdd(&L.tcc[k], static_cast<unsigned long long>(o.c));
@@ -3429,7 +3388,7 @@ void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, ui
                        samples_out, scratch, wb, hwords, tcap, big_n, big, big_limbs, big_cap);
 }
 
-void launch_request_rows(const DStore &st, const ChainDev *chains, const RowRun *runs, uint32_t n_runs,
+void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun *runs, uint32_t n_runs,
                          unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,

@@ -585,8 +585,6 @@ bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
         put_error(o, v.error);
         return true;
     }
-    const char *tp = nullptr;
-    size_t tn = 0;
     o += "{\"exists\": ";
     o += v.exists ? "true" : "false";
     o += ", \"vcf_location\": ";
@@ -623,19 +621,7 @@ bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
             put_i64(o, v.sample_indices[k]);
         }
     o += "], \"sample_names\": [";
-    if ((sel || inc) && v.n_sample_indices) {
-        if (sb_result_sample_names_text(rs, i, &tp, &tn) != SB_OK) return false;
-        size_t a = 0;
-        bool first = true;
-        for (size_t k = 0; k <= tn; ++k) {
-            if (k == tn || tp[k] == ',') {
-                if (!first) o += ", ";
-                first = false;
-                if (!put_jstr(o, tp + a, k - a)) return false;
-                a = k + 1;
-            }
-        }
-    }
+    if ((sel || inc) && v.n_sample_indices && !result_sample_names_json(rs, i, o)) return false;
     o += "]}";
     return true;
 }

@@ -372,29 +372,60 @@ class ShardRequests:
 
 def shard_requests(shape: GenomeShape, reqs: Requests, world: int, rank: int) -> ShardRequests:
     """Vectorised: each request's slices whose first base is in rank's core
-    [cuts[rank], cuts[rank + 1]) form one run of slice indices."""
+    [cuts[rank], cuts[rank + 1]) form one run of slice indices.  Requests are
+    ordered by (contig, start), so the rank's rows are one range and only the
+    rows of the two cut contigs can lose slices (the others keep every slice:
+    their columns are views)."""
     cuts = shape.cuts(world)
     (c0, p0), (c1, p1) = cuts[rank], cuts[rank + 1]
-    smin = reqs.start.astype(np.int64) + 1
-    smax = reqs.start.astype(np.int64) + reqs.width + 1
-    nsl = (smax - smin) // SPLIT_SIZE + 1
-    ci = reqs.ci.astype(np.int64)
+    r0 = int(np.searchsorted(reqs.ci, c0, side='left'))
+    r1 = int(np.searchsorted(reqs.ci, c1, side='right'))
+    ci = reqs.ci[r0:r1]
+    smin = reqs.start[r0:r1] + 1
+    smax = smin + reqs.width[r0:r1]
+    n = len(smin)
+    e0 = int(np.searchsorted(ci, c0, side='right'))  # rows [0, e0): contig c0
+    s1 = int(np.searchsorted(ci, c1, side='left'))   # rows [s1, n): contig c1
     ceil_div = lambda a: -((-a) // SPLIT_SIZE)  # noqa: E731
-    k0 = np.where(ci > c0, 0, np.where(ci == c0, np.clip(ceil_div(p0 - smin), 0, None), nsl))
-    k1 = np.where(ci < c1, nsl, np.where(ci == c1, np.clip(ceil_div(p1 - smin), 0, None), 0))
-    k0 = np.minimum(k0, nsl)
-    k1 = np.clip(k1, k0, nsl)
-    has = k1 > k0
-    idx = np.flatnonzero(has)
-    if len(idx) == 0:
+    # (first row, last row, the cut at the start applies, the cut at the end applies)
+    segs = [(0, n, True, True)] if c0 == c1 else [(0, e0, True, False), (s1, n, False, True)]
+    cut = []  # (x0, has, a, b) of each cut contig's rows
+    for x0, x1, at0, at1 in segs:
+        if x1 <= x0:
+            continue
+        sm, sx = smin[x0:x1], smax[x0:x1]
+        nsl = (sx - sm) // SPLIT_SIZE + 1
+        k0 = np.minimum(np.clip(ceil_div(p0 - sm), 0, None), nsl) if at0 else np.zeros_like(nsl)
+        k1 = np.clip(np.clip(ceil_div(p1 - sm), 0, None), k0, nsl) if at1 else nsl
+        has = k1 > k0
+        aa = sm + SPLIT_SIZE * k0
+        cut.append((x0, has, aa, np.where(has, np.minimum(sx, sm + SPLIT_SIZE * k1 - 1), aa - 1)))
+    # the first and last rows with a slice here (rows between the cut contigs have all of theirs)
+    firsts, lasts = [], []
+    for x0, has, _, _ in cut:
+        if has.any():
+            firsts.append(x0 + int(np.argmax(has)))
+            lasts.append(x0 + len(has) - int(np.argmax(has[::-1])))
+    if e0 < s1 and c0 != c1:
+        firsts.append(e0)
+        lasts.append(s1)
+    if not firsts:
         e = np.zeros(0, dtype=np.int64)
         return ShardRequests(0, 0, e, e, e, e, e, e, e, e)
-    lo, hi = int(idx[0]), int(idx[-1]) + 1
-    w = slice(lo, hi)
-    a = smin[w] + SPLIT_SIZE * k0[w]
-    b = np.minimum(smax[w], smin[w] + SPLIT_SIZE * k1[w] - 1)
-    b = np.where(has[w], b, a - 1)
-    return ShardRequests(lo, hi - lo, ci[w], a, b, smin[w], smax[w], reqs.vt[w], reqs.vmin[w], reqs.vmax[w])
+    lo, hi = min(firsts), max(lasts)
+    a, b = smin[lo:hi], smax[lo:hi]
+    changed = [(x0, aa, bb) for x0, _, aa, bb in cut
+               if not (np.array_equal(aa, smin[x0:x0 + len(aa)]) and np.array_equal(bb, smax[x0:x0 + len(bb)]))]
+    if changed:
+        a, b = a.copy(), b.copy()
+        for x0, aa, bb in changed:
+            y0, y1 = max(x0, lo), min(x0 + len(aa), hi)
+            if y1 > y0:
+                a[y0 - lo:y1 - lo] = aa[y0 - x0:y1 - x0]
+                b[y0 - lo:y1 - lo] = bb[y0 - x0:y1 - x0]
+    w = slice(r0 + lo, r0 + hi)
+    return ShardRequests(r0 + lo, hi - lo, ci[lo:hi], a, b, smin[lo:hi], smax[lo:hi], reqs.vt[w], reqs.vmin[w],
+                         reqs.vmax[w])
 
 
 def prepare_shard_requests(store, sr: ShardRequests):
