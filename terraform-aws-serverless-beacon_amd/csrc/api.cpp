@@ -827,14 +827,106 @@ uint32_t bucket_ceil(const sb_store &s, const QDev &d, int64_t x) {
     return s.h_bucket[d.bucket_off + b + 1];
 }
 
-// run fn(i) for i in [0, n) on up to `threads` host threads
+// A persistent host worker pool (planning runs once per call: spawning
+// threads per call cost a few hundred microseconds).  run(n, fn) calls fn(i)
+// for i < n on the pool and the calling thread; one run at a time (try_run:
+// parallel_for falls back to its own threads when the pool is taken).
+class WorkerPool {
+  public:
+    static WorkerPool &get() {
+        static WorkerPool pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
+        return pool;
+    }
+    template <class F>
+    void run(size_t n, F fn) {
+        std::unique_lock<std::mutex> one(run_mu_);
+        run_locked(n, fn);
+    }
+    // the same, or false at once when another run holds the pool (a
+    // concurrent caller, or a call from inside a task)
+    template <class F>
+    bool try_run(size_t n, F fn) {
+        std::unique_lock<std::mutex> one(run_mu_, std::try_to_lock);
+        if (!one.owns_lock()) return false;
+        run_locked(n, fn);
+        return true;
+    }
+
+  private:
+    template <class F>
+    void run_locked(size_t n, F fn) {
+        std::function<void(size_t)> f = fn;
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            fn_ = &f;
+            n_ = n;
+            next_ = 0;
+            busy_ = workers_.size();
+            ++gen_;
+        }
+        cv_.notify_all();
+        drain();
+        std::unique_lock<std::mutex> lk(mu_);
+        done_.wait(lk, [&] { return busy_ == 0; });
+        fn_ = nullptr;
+    }
+
+  public:
+    ~WorkerPool() {
+        {
+            std::lock_guard<std::mutex> lk(mu_);
+            stop_ = true;
+            ++gen_;
+        }
+        cv_.notify_all();
+        for (auto &t : workers_) t.join();
+    }
+
+  private:
+    explicit WorkerPool(unsigned k) {
+        for (unsigned i = 0; i < k; ++i) workers_.emplace_back([this] { loop(); });
+    }
+    void drain() {
+        for (size_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            {
+                std::unique_lock<std::mutex> lk(mu_);
+                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+                if (stop_) return;
+                seen = gen_;
+            }
+            drain();
+            std::lock_guard<std::mutex> lk(mu_);
+            if (--busy_ == 0) done_.notify_all();
+        }
+    }
+    std::vector<std::thread> workers_;
+    std::mutex mu_, run_mu_;
+    std::condition_variable cv_, done_;
+    std::function<void(size_t)> *fn_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> next_{0};
+    size_t busy_ = 0;
+    uint64_t gen_ = 0;
+    bool stop_ = false;
+};
+
+// run fn(i) for i in [0, n) on up to `threads` host threads (the worker
+// pool's when it is free)
 template <class F>
-void parallel_for(size_t n, F fn, unsigned threads = 16) {
-    const unsigned t = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, n / 4096)));
+void parallel_for(size_t n, F fn, unsigned threads = 16, size_t grain = 4096) {
+    const unsigned t = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, n / grain)));
     if (t <= 1) {
         for (size_t i = 0; i < n; ++i) fn(i);
         return;
     }
+    if (WorkerPool::get().try_run(t, [&](size_t k) {
+            for (size_t i = n * k / t, e = n * (k + 1) / t; i < e; ++i) fn(i);
+        }))
+        return;
     std::vector<std::thread> th;
     for (unsigned k = 0; k < t; ++k)
         th.emplace_back([&, k] {
@@ -2002,75 +2094,6 @@ bool plan_job_windows(const sb_store &s, const std::vector<KRun> &runs, size_t g
     return true;
 }
 
-// A persistent host worker pool (planning runs once per call: spawning
-// threads per call cost a few hundred microseconds).  run(n, fn) calls fn(i)
-// for i < n on the pool and the calling thread; one run at a time.
-class WorkerPool {
-  public:
-    static WorkerPool &get() {
-        static WorkerPool pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
-        return pool;
-    }
-    template <class F>
-    void run(size_t n, F fn) {
-        std::lock_guard<std::mutex> one(run_mu_);
-        std::function<void(size_t)> f = fn;
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            fn_ = &f;
-            n_ = n;
-            next_ = 0;
-            busy_ = workers_.size();
-            ++gen_;
-        }
-        cv_.notify_all();
-        drain();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return busy_ == 0; });
-        fn_ = nullptr;
-    }
-    ~WorkerPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-            ++gen_;
-        }
-        cv_.notify_all();
-        for (auto &t : workers_) t.join();
-    }
-
-  private:
-    explicit WorkerPool(unsigned k) {
-        for (unsigned i = 0; i < k; ++i) workers_.emplace_back([this] { loop(); });
-    }
-    void drain() {
-        for (size_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-            }
-            drain();
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--busy_ == 0) done_.notify_all();
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex mu_, run_mu_;
-    std::condition_variable cv_, done_;
-    std::function<void(size_t)> *fn_ = nullptr;
-    size_t n_ = 0;
-    std::atomic<size_t> next_{0};
-    size_t busy_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
-
 // Every job's windows; jobs planned on the worker pool.  runs[g] = segs[g]'s KRun.
 bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan &P) {
     uint32_t target = kWinCap;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
@@ -2501,60 +2524,147 @@ bool strict_region_entries(const uint8_t *file, uint64_t size, uint64_t rs, uint
     return true;
 }
 
+// A slice's region files as summariseSlice writes them (gzip members, the
+// store key of every entry), kept per store: the reference writes them once
+// and every duplicateVariantSearch message reads them, so strict mode
+// compresses each slice's files once (level 9 dominates: ~10 MB/s) and then
+// only inflates.  Bounded by bytes (cleared when full).
+struct SliceFiles {
+    int32_t status = 0;
+    std::vector<sb_region_file> files;
+    std::vector<uint8_t> data;
+    std::vector<uint64_t> at;  // each file's first byte in data
+    std::vector<std::vector<uint32_t>> keys;
+    size_t bytes() const {
+        size_t b = data.size() + files.size() * sizeof(sb_region_file);
+        for (const auto &k : keys) b += k.size() * 4;
+        return b;
+    }
+};
+struct RegionCache {
+    std::map<std::tuple<uint32_t, uint64_t, uint64_t>, std::shared_ptr<const SliceFiles>> m;
+    size_t bytes = 0;
+    static constexpr size_t kCap = size_t(8) << 30;
+};
+
 void dedup_files(sb_store &s, const sb_dedup_file_job *jobs, size_t nj, uint64_t *unique, int32_t *status,
                  sb_dedup_stats *stats) {
     if (nj > (1u << 20)) throw Error(SB_EINVAL, "more than 2^20 dedup jobs in one call");
-    struct SliceFiles {
-        int32_t status = 0;
-        std::vector<sb_region_file> files;
-        std::vector<uint8_t> data;
-        std::vector<uint64_t> at;  // each file's first byte in data
-        std::vector<std::vector<uint32_t>> keys;
+    if (!s.region_cache)  // under the store lock (sb_dedup_count_files)
+        s.region_cache = std::shared_ptr<void>(new RegionCache, [](void *w) { delete static_cast<RegionCache *>(w); });
+    RegionCache &C = *static_cast<RegionCache *>(s.region_cache.get());
+    using Key = std::tuple<uint32_t, uint64_t, uint64_t>;
+    // every (job, file) pair, and the slices not cached yet
+    struct Pair {
+        uint32_t job;
+        const SliceFiles *sf = nullptr;
+        uint32_t file;
+        bool ok = true;
+        std::vector<uint32_t> incl;
     };
-    std::map<std::tuple<uint32_t, uint64_t, uint64_t>, SliceFiles> cache;
-    std::vector<KSeg> segs;
-    uint64_t n = 0;
+    std::vector<Pair> pairs;
+    std::vector<Key> missing;
+    std::vector<Key> pkey;
     for (size_t j = 0; j < nj; ++j) {
         const sb_dedup_file_job &J = jobs[j];
         status[j] = 0;
         unique[j] = 0;
         if (!J.files && J.n_files) throw Error(SB_EINVAL, "dedup job: NULL file list");
-        const uint32_t rs = static_cast<uint32_t>(std::min<uint64_t>(J.range_start, 0xffffffffull));
-        const size_t seg0 = segs.size();
-        for (uint32_t t = 0; t < J.n_files && !status[j]; ++t) {
+        for (uint32_t t = 0; t < J.n_files; ++t) {
             const sb_region_ref &F = J.files[t];
             if (F.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "dedup job " + std::to_string(j) + ": unknown vcf id");
-            auto key = std::make_tuple(F.vcf_id, F.virtual_start, F.virtual_end);
-            auto it = cache.find(key);
-            if (it == cache.end()) {
-                SliceFiles sf;
-                const sb_slice sl{F.vcf_id, 0, F.virtual_start, F.virtual_end};
-                sf.status = slice_region_files(s, 0, sl, sf.files, &sf.data, true, &sf.keys);
-                uint64_t a = 0;
-                for (const auto &f : sf.files) {
-                    sf.at.push_back(a);
-                    a += f.data_bytes;
-                }
-                it = cache.emplace(key, std::move(sf)).first;
+            const Key key = std::make_tuple(F.vcf_id, F.virtual_start, F.virtual_end);
+            if (!C.m.count(key)) missing.push_back(key);
+            pairs.push_back(Pair{static_cast<uint32_t>(j), nullptr, F.file, true, {}});
+            pkey.push_back(key);
+        }
+    }
+    std::sort(missing.begin(), missing.end());
+    missing.erase(std::unique(missing.begin(), missing.end()), missing.end());
+    // the missing slices' files, in parallel (gzip level 9 is the cost)
+    std::vector<std::shared_ptr<SliceFiles>> made(missing.size());
+    std::vector<std::unique_ptr<Error>> errs(missing.size());  // raised when a job reaches that file
+    parallel_for(missing.size(), [&](size_t i) {
+        try {
+            auto sf = std::make_shared<SliceFiles>();
+            const sb_slice sl{std::get<0>(missing[i]), 0, std::get<1>(missing[i]), std::get<2>(missing[i])};
+            sf->status = slice_region_files(s, 0, sl, sf->files, &sf->data, true, &sf->keys);
+            uint64_t a = 0;
+            for (const auto &f : sf->files) {
+                sf->at.push_back(a);
+                a += f.data_bytes;
             }
-            const SliceFiles &sf = it->second;
+            made[i] = std::move(sf);
+        } catch (const Error &e) {
+            errs[i] = std::make_unique<Error>(e);
+        } catch (const std::exception &e) {
+            errs[i] = std::make_unique<Error>(SB_EINVAL, e.what());
+        }
+    }, 16, 1);
+    size_t add = 0;
+    for (const auto &m : made)
+        if (m) add += m->bytes();
+    if (C.bytes + add > RegionCache::kCap) {
+        C.m.clear();
+        C.bytes = 0;
+    }
+    // this call's slices stay referenced here even if the cache drops them
+    std::map<Key, std::shared_ptr<const SliceFiles>> use;
+    std::map<Key, const Error *> failed;
+    for (size_t i = 0; i < missing.size(); ++i) {
+        if (!made[i]) {
+            failed[missing[i]] = errs[i].get();
+            continue;
+        }
+        use[missing[i]] = made[i];
+        C.m[missing[i]] = made[i];
+        C.bytes += made[i]->bytes();
+    }
+    for (size_t p = 0; p < pairs.size(); ++p) {
+        if (failed.count(pkey[p])) continue;  // sf stays null
+        auto it = use.find(pkey[p]);
+        if (it == use.end()) it = use.emplace(pkey[p], C.m.at(pkey[p])).first;
+        pairs[p].sf = it->second.get();
+    }
+    // each pair's entries as the reference reader returns them, in parallel
+    parallel_for(pairs.size(), [&](size_t p) {
+        Pair &P = pairs[p];
+        if (!P.sf) return;
+        const SliceFiles &sf = *P.sf;
+        if (sf.status || P.file >= sf.files.size()) return;  // reported in job order below
+        const sb_dedup_file_job &J = jobs[P.job];
+        P.ok = strict_region_entries(sf.data.data() + sf.at[P.file], sf.files[P.file].data_bytes, J.range_start,
+                                     J.range_end, P.incl);
+    }, 16, 1);
+    // key runs in job order; a job stops at its first failing file
+    std::vector<KSeg> segs;
+    uint64_t n = 0;
+    for (size_t p = 0; p < pairs.size();) {
+        const uint32_t j = pairs[p].job;
+        const uint32_t rs = static_cast<uint32_t>(std::min<uint64_t>(jobs[j].range_start, 0xffffffffull));
+        const size_t seg0 = segs.size();
+        for (; p < pairs.size() && pairs[p].job == j; ++p) {
+            if (status[j]) continue;
+            const Pair &P = pairs[p];
+            if (!P.sf) throw *failed.at(pkey[p]);  // the error writing that slice's files raised
+            const SliceFiles &sf = *P.sf;
             if (sf.status) {  // that summariseSlice never wrote its files
                 status[j] = sf.status;
-                break;
+                continue;
             }
-            if (F.file >= sf.files.size()) throw Error(SB_EINVAL, "dedup job " + std::to_string(j) + ": no region file " +
-                                                                      std::to_string(F.file) + " in that slice");
-            std::vector<uint32_t> incl;
-            if (!strict_region_entries(sf.data.data() + sf.at[F.file], sf.files[F.file].data_bytes, J.range_start,
-                                       J.range_end, incl)) {
+            if (P.file >= sf.files.size())
+                throw Error(SB_EINVAL, "dedup job " + std::to_string(j) + ": no region file " + std::to_string(P.file) +
+                                           " in that slice");
+            if (!P.ok) {
                 status[j] = SB_QERR_RUNTIME;
-                break;
+                continue;
             }
-            const auto &fk = sf.keys[F.file];
+            const auto &fk = sf.keys[P.file];
+            const auto &incl = P.incl;
             for (size_t a = 0; a < incl.size();) {  // runs of consecutive store keys
                 size_t b = a + 1;
                 while (b < incl.size() && fk[incl[b]] == fk[incl[b - 1]] + 1) ++b;
-                segs.push_back(KSeg{fk[incl[a]], n, static_cast<uint32_t>(b - a), static_cast<uint32_t>(j), rs, 0});
+                segs.push_back(KSeg{fk[incl[a]], n, static_cast<uint32_t>(b - a), j, rs, 0});
                 n += b - a;
                 a = b;
             }
@@ -3098,31 +3208,57 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     std::vector<uint32_t> seg(n + 1, 0);
     for (uint32_t o : owner) ++seg[o + 1];
     for (size_t w = 0; w < n; ++w) seg[w + 1] += seg[w];
-    // runs of consecutive rows (<= kRunRows rows, kPackRun chains, kPackSlots slots)
+    // runs of consecutive rows (<= kRunRows rows, kPackRun chains, kPackSlots
+    // slots), formed greedily in blocks of rows on several threads (a block
+    // boundary also ends a run)
     {
-        RowRun cur{0, 0, 0, 0, 0, 0, kRunSimple};
-        uint32_t c = 0;
-        for (uint32_t i = 0; i < n; ++i) {
-            const bool ch = cls[i] == 1;
-            const uint32_t need = nsl_of[i];
-            if (i > cur.row_lo && (i - cur.row_lo == kRunRows || (ch && (cur.c_hi - cur.c_lo == pack_run_max() ||
-                                                                           cur.n_slots + need > pack_slots_max())))) {
-                cur.row_hi = i;
-                R->runs.push_back(cur);
-                cur = RowRun{i, i, c, c, 0, 0, kRunSimple};
+        const size_t nb = std::max<size_t>(1, std::min<size_t>(16, n / 65536));
+        std::vector<std::vector<RowRun>> part(nb);
+        std::vector<uint64_t> part_chains(nb, 0), part_slices(nb, 0);
+        parallel_for(nb, [&](size_t k) {
+            const uint32_t r0 = static_cast<uint32_t>(n * k / nb), r1 = static_cast<uint32_t>(n * (k + 1) / nb);
+            auto &out = part[k];
+            out.reserve((r1 - r0) / 16 + 1);
+            RowRun cur{r0, r0, 0, 0, 0, 0, kRunSimple};
+            uint32_t c = 0;
+            uint64_t sl = 0;
+            for (uint32_t i = r0; i < r1; ++i) {
+                const bool ch = cls[i] == 1;
+                const uint32_t need = nsl_of[i];
+                if (i > cur.row_lo && (i - cur.row_lo == kRunRows || (ch && (cur.c_hi - cur.c_lo == pack_run_max() ||
+                                                                               cur.n_slots + need > pack_slots_max())))) {
+                    cur.row_hi = i;
+                    out.push_back(cur);
+                    cur = RowRun{i, i, c, c, 0, 0, kRunSimple};
+                }
+                if (cls[i] == 2) cur.flags &= ~kRunSimple;  // a row answered per slice: gathered row by row
+                if (ch) {
+                    cur.c_hi = ++c;
+                    cur.n_slots += need;
+                    sl += need;
+                }
             }
-            if (cls[i] == 2) cur.flags &= ~kRunSimple;  // a row answered per slice: gathered row by row
-            if (ch) {
-                cur.c_hi = ++c;
-                cur.n_slots += need;
-                R->n_chain_slices += need;
+            if (r1 > r0) {
+                cur.row_hi = r1;
+                out.push_back(cur);
             }
+            part_chains[k] = c;
+            part_slices[k] = sl;
+        }, 16, 1);
+        size_t total = 0;
+        for (auto &p : part) total += p.size();
+        R->runs.reserve(total);
+        uint32_t cbase = 0;
+        for (size_t k = 0; k < nb; ++k) {  // chain ordinals made batch-wide
+            for (RowRun r : part[k]) {
+                r.c_lo += cbase;
+                r.c_hi += cbase;
+                R->runs.push_back(r);
+            }
+            cbase += static_cast<uint32_t>(part_chains[k]);
+            R->n_chain_slices += part_slices[k];
         }
-        if (n) {
-            cur.row_hi = static_cast<uint32_t>(n);
-            R->runs.push_back(cur);
-        }
-        R->n_chains = c;
+        R->n_chains = cbase;
     }
     tick("runs");
     // chain descriptors straight into pinned staging, kPackRun slots per run

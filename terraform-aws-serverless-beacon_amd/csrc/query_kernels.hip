@@ -1904,7 +1904,7 @@ __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__res
 // The wave writes its rows, each row's hit count (into row_off) and the run's
 // total as an aggregate status word.
 //
-// request_tile_scan_kernel -- the tile totals (16 runs a tile) into tile offsets.
+// request_tile_scan_kernel -- the runs' totals, summed per tile of 16 runs, into tile offsets.
 //
 // request_deliver_kernel -- one wave per run: the run's output offset (its
 // tile's offset + the earlier runs' totals of the tile), row offsets, and the
@@ -1942,9 +1942,8 @@ constexpr uint32_t kDeliverTile = 16;  // runs per request_deliver_kernel wave
 template <bool LDS_LUT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_eval_kernel(
     DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
-    unsigned long long *__restrict__ status, unsigned long long *__restrict__ tstatus, const QRes *__restrict__ sres,
-    ReqPartial *__restrict__ rows, uint64_t *__restrict__ row_cnt, uint64_t *__restrict__ row_src,
-    uint64_t *__restrict__ stage, uint32_t n_lut, uint32_t n_tiles) {
+    unsigned long long *__restrict__ status, const QRes *__restrict__ sres, ReqPartial *__restrict__ rows,
+    uint64_t *__restrict__ row_cnt, uint64_t *__restrict__ row_src, uint64_t *__restrict__ stage, uint32_t n_lut) {
     __shared__ ReqLds lds_all[kWavesPerBlock];
     __shared__ uint32_t slut[LDS_LUT ? kReqLut : 1];
     ReqLds &L = lds_all[threadIdx.x >> 6];
@@ -2132,18 +2131,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         if (!simple && ch != 0xffu) row_src[row] = stage_at + L.cstart[ch];
     }
     const uint64_t H = static_cast<uint64_t>(rdl64(wave_incl_scan_i64(static_cast<int64_t>(nvr)), kWave - 1));
-    if (ul == 0) {  // read by request_deliver_kernel (kernel boundary)
-        status[w] = H;
-        // the tile's total (zeroed before this launch; 16 adds per address):
-        // request_tile_scan_kernel turns the tile totals into tile offsets
-        atomicAdd(&tstatus[w / kDeliverTile], static_cast<unsigned long long>(H));
-    }
+    if (ul == 0) status[w] = H;  // read by the tile scan and request_deliver_kernel (kernel boundaries)
 }
 
-// request_tile_scan_kernel: one workgroup turns the tile totals (tiles of
-// kDeliverTile runs, added up by request_eval_kernel) into exclusive tile
-// offsets in place.
-__global__ __launch_bounds__(1024) void request_tile_scan_kernel(unsigned long long *__restrict__ tsum, uint32_t nt) {
+// request_tile_scan_kernel: one workgroup adds up each tile's run totals
+// (tiles of kDeliverTile runs) and scans them into exclusive tile offsets.
+// (Tile totals by device atomics in request_eval_kernel needed a memset
+// launch before every pass.)
+__global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned long long *__restrict__ status,
+                                                                 uint32_t n_runs, unsigned long long *__restrict__ tsum,
+                                                                 uint32_t nt) {
     __shared__ unsigned long long wsum[16];
     __shared__ unsigned long long carry_s;
     const uint32_t tid = threadIdx.x, wave = tid >> 6;
@@ -2151,7 +2148,20 @@ __global__ __launch_bounds__(1024) void request_tile_scan_kernel(unsigned long l
     __syncthreads();
     for (uint32_t base = 0; base < nt; base += 1024) {
         const uint32_t i = base + tid;
-        const uint64_t v = i < nt ? tsum[i] : 0ull;
+        uint64_t v = 0;
+        if (i < nt) {  // the tile's run totals: 16 words, 128 B aligned (8 x 16-byte loads when whole)
+            const uint32_t r0 = i * kDeliverTile;
+            if (r0 + kDeliverTile <= n_runs) {
+                const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(status + r0);
+                ulonglong2 x[kDeliverTile / 2];
+#pragma unroll
+                for (uint32_t k = 0; k < kDeliverTile / 2; ++k) x[k] = q[k];
+#pragma unroll
+                for (uint32_t k = 0; k < kDeliverTile / 2; ++k) v += x[k].x + x[k].y;
+            } else {
+                for (uint32_t r = r0; r < n_runs; ++r) v += status[r];
+            }
+        }
         const uint64_t incl = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(v)));
         if (lane_id() == kWave - 1) wsum[wave] = incl;
         __syncthreads();
@@ -3400,21 +3410,20 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
     }
     const dim3 grid(blocks_for(n_runs));
     const uint32_t n_tiles = request_tiles(n_runs);
-    (void)hipMemsetAsync(tstatus, 0, size_t(n_tiles) * 8, s);
     if (ev0) (void)hipEventRecord(ev0, s);
     if (n_lut <= kReqLut)
-        hipLaunchKernelGGL(request_eval_kernel<true>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status,
-                           tstatus, sres, rows, row_off, row_src, stage, n_lut, n_tiles);
+        hipLaunchKernelGGL(request_eval_kernel<true>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
+                           rows, row_off, row_src, stage, n_lut);
     else
-        hipLaunchKernelGGL(request_eval_kernel<false>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status,
-                           tstatus, sres, rows, row_off, row_src, stage, n_lut, n_tiles);
+        hipLaunchKernelGGL(request_eval_kernel<false>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
+                           rows, row_off, row_src, stage, n_lut);
     if (ev1) (void)hipEventRecord(ev1, s);
-    hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, tstatus, n_tiles);
+    hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, status, n_runs, tstatus, n_tiles);
     hipLaunchKernelGGL(request_deliver_kernel, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg,
                        shoff, sherr, shits, row_off, row_src, stage, out, n_rows, rec_base);
 }
 
-// tile totals (request_eval_kernel) -> tile offsets (request_tile_scan_kernel)
+// run totals (request_eval_kernel) -> tile offsets (request_tile_scan_kernel)
 uint32_t request_tiles(uint32_t n_runs) { return (n_runs + kDeliverTile - 1) / kDeliverTile; }
 
 uint32_t pack_run_max() { return kPackRun; }

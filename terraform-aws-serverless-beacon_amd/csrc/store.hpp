@@ -154,6 +154,7 @@ struct sb_store {
     std::shared_ptr<void> win_ws;        // window-dedup scratch (api.cpp WinWs)
     std::shared_ptr<void> summarise_ws;  // summariseSlice scratch (api.cpp SumWs)
     std::shared_ptr<void> req_pool;      // request batches' pinned / device buffers (api.cpp ReqPool)
+    std::shared_ptr<void> region_cache;  // strict dedup: slices' region files (api.cpp RegionCache)
     std::once_flag req_pool_once;
     std::vector<sb::VcfData> vcfs;  // metadata (columns are moved to the globals below)
     std::unordered_map<std::string, uint32_t> vcf_by_location;

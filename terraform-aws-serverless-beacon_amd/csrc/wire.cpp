@@ -708,7 +708,19 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
                     tbuf[k].reserve(tbuf[k].size() + need);
                 });
             }
+            std::vector<double> t_ms(threads, 0.0);
+            std::vector<uint64_t> t_n(threads, 0);
             par(idx.size(), threads, [&](size_t j, unsigned t) {
+                const auto t0 = trace ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
+                struct Acc {  // per-thread time in put_response (SBEACON_WIRE_TRACE)
+                    std::chrono::steady_clock::time_point t0;
+                    double *ms;
+                    bool on;
+                    ~Acc() {
+                        if (on) *ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                    }
+                } acc{t0, &t_ms[t], trace};
+                ++t_n[t];
                 const uint32_t i = idx[j];
                 std::string &o = tbuf[t];
                 const size_t at = o.size();
@@ -722,6 +734,16 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
                     o.resize(at);
                 }
             });
+            if (trace) {
+                double mx = 0, sum = 0;
+                size_t bytes = 0;
+                for (unsigned t = 0; t < threads; ++t) {
+                    mx = std::max(mx, t_ms[t]);
+                    sum += t_ms[t];
+                    bytes += tbuf[t].size();
+                }
+                std::fprintf(stderr, "[wire] format threads: max %.2f ms, sum %.2f ms, %zu bytes\n", mx, sum, bytes);
+            }
             tick("format");
         }
         // JSON lines: every response ends with '\n' (none for status 1)

@@ -91,6 +91,9 @@ def test_region_files_gzip_and_strict_dedup(tmp_path):
         messages = init_duplicate_variant_search('dsS', locs, keys, abs_max=abs_max)
         assert messages
         per_range = dedup_batch(messages, registry=reg, file_refs=refs)
+        again = dedup_batch(messages, registry=reg, file_refs=refs)  # the region files from the store's cache
+        norm = lambda rs: [r if isinstance(r, int) else type(r) for r in rs]  # noqa: E731
+        assert norm(again) == norm(per_range)
         n_throw = 0
         for m, got in zip(messages, per_range):
             exp = set()
