@@ -503,10 +503,32 @@ bool put_jstr(std::string &o, const char *s, size_t n) {
     return true;
 }
 
+// decimal int64 (no snprintf: sample index lists run to tens of millions of
+// numbers per batch); two digits per step from a table
 void put_i64(std::string &o, int64_t v) {
+    static const char kPairs[] =
+        "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+        "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+        "8081828384858687888990919293949596979899";
     char b[24];
-    const int n = snprintf(b, sizeof b, "%lld", static_cast<long long>(v));
-    o.append(b, static_cast<size_t>(n));
+    char *e = b + sizeof b, *q = e;
+    uint64_t u = v < 0 ? 0ull - static_cast<uint64_t>(v) : static_cast<uint64_t>(v);
+    while (u >= 100) {
+        const uint32_t r = static_cast<uint32_t>(u % 100);
+        u /= 100;
+        q -= 2;
+        q[0] = kPairs[2 * r];
+        q[1] = kPairs[2 * r + 1];
+    }
+    if (u >= 10) {
+        q -= 2;
+        q[0] = kPairs[2 * u];
+        q[1] = kPairs[2 * u + 1];
+    } else {
+        *--q = static_cast<char>('0' + u);
+    }
+    if (v < 0) *--q = '-';
+    o.append(q, static_cast<size_t>(e - q));
 }
 
 // decimal of a two's-complement little-endian 32-bit-limb integer; false
