@@ -324,6 +324,7 @@ struct sb_batch {
         // dchains: ReqChain slots (kPackRun per run), then the RowRuns at runs_at
         DevMem dchains, status, tstatus, stage, row_src, lut, sseg, sherr;
         size_t runs_at = 0;
+        uint32_t run = 32;             // chain slots per run (request_eval_kernel's RUN)
         std::shared_ptr<ReqPool> pool;  // where the device buffers go back when the batch is freed
         bool slices = false;           // some rows answered per slice (the batch's query part)
         void give_back() {
@@ -3208,9 +3209,11 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     std::vector<uint32_t> seg(n + 1, 0);
     for (uint32_t o : owner) ++seg[o + 1];
     for (size_t w = 0; w < n; ++w) seg[w + 1] += seg[w];
-    // runs of consecutive rows (<= kRunRows rows, kPackRun chains, kPackSlots
-    // slots), formed greedily in blocks of rows on several threads (a block
-    // boundary also ends a run)
+    // runs of consecutive rows (<= kRunRows rows, R->run chains, 8 slots per
+    // chain slot), formed greedily in blocks of rows on several threads (a
+    // block boundary also ends a run)
+    R->run = req_run_max();
+    const uint32_t run_max = R->run, slots_max = req_slots_max(R->run);
     {
         const size_t nb = std::max<size_t>(1, std::min<size_t>(16, n / 65536));
         std::vector<std::vector<RowRun>> part(nb);
@@ -3225,8 +3228,8 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
             for (uint32_t i = r0; i < r1; ++i) {
                 const bool ch = cls[i] == 1;
                 const uint32_t need = nsl_of[i];
-                if (i > cur.row_lo && (i - cur.row_lo == kRunRows || (ch && (cur.c_hi - cur.c_lo == pack_run_max() ||
-                                                                               cur.n_slots + need > pack_slots_max())))) {
+                if (i > cur.row_lo && (i - cur.row_lo == kRunRows || (ch && (cur.c_hi - cur.c_lo == run_max ||
+                                                                               cur.n_slots + need > slots_max)))) {
                     cur.row_hi = i;
                     out.push_back(cur);
                     cur = RowRun{i, i, c, c, 0, 0, kRunSimple};
@@ -3264,7 +3267,7 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     // chain descriptors straight into pinned staging, kPackRun slots per run
     // (request_eval_kernel loads a run's slots beside its RowRun), the runs
     // after them: one H2D copy from pinned memory
-    const size_t n_runs = R->runs.size(), slots = pack_run_max();
+    const size_t n_runs = R->runs.size(), slots = run_max;
     const size_t chain_bytes = n_runs * slots * sizeof(ReqChain), run_bytes = n_runs * sizeof(RowRun);
     R->pool = req_pool(s);
     ReqPool::Pinned pin = R->pool->get_pinned(chain_bytes + run_bytes);
@@ -3376,8 +3379,8 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
                         R.slices ? B.res.as<QRes>() : nullptr,
                         R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
                         static_cast<ReqPartial *>(rows), static_cast<uint64_t *>(row_off), R.row_src.as<uint64_t>(),
-                        R.stage.as<uint64_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, st,
-                        ev[0], ev[1]);
+                        R.stage.as<uint64_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
+                        st, ev[0], ev[1]);
     HIP_OK(hipGetLastError());
 }
 

@@ -233,6 +233,7 @@ static_assert(sizeof(RowRun) == 32, "RowRun is two 16-byte words");
 // ...] up to `last`, so width and slice count follow from the window; the
 // row, kind and length bounds share one word.  32 B, not ChainDev's 80.
 constexpr uint32_t kReqWidth = 10000;  // lambda/splitQuery/lambda_function.py:12
+constexpr uint32_t kReqRun = 32;       // ReqChain slots per run (request_eval_kernel's RUN)
 struct alignas(16) ReqChain {
     uint32_t first, last;  // the request's [start_min, start_max] (first >= 1)
     uint32_t c_lo, c_hi;   // candidate range (host-resolved from the coarse index)

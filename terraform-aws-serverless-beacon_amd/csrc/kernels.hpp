@@ -108,8 +108,11 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                          unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,
-                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, hipStream_t s, hipEvent_t ev0 = nullptr,
-                         hipEvent_t ev1 = nullptr);
+                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, hipStream_t s,
+                         hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+// slices per run of `run` chain slots (ReqLds<run>::kSlots); chain slots per run
+uint32_t req_slots_max(uint32_t run);
+uint32_t req_run_max();
 uint32_t request_tiles(uint32_t n_runs);
 
 // Fetch-time gather of every query's hits into one dense array.

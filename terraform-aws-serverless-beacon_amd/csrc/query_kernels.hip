@@ -1579,13 +1579,14 @@ struct PackChunk {
     uint32_t k;  // the lane's chain
 };
 
-// last lane j < R (lanes hold a nondecreasing prefix v) with v_j <= g
+// last lane j < R <= RUN (lanes hold a nondecreasing prefix v) with v_j <= g
+template <uint32_t RUN = kPackRun>
 __device__ __forceinline__ uint32_t last_le(uint32_t v, uint32_t R, uint32_t g) {
     uint32_t lo = 0;
 #pragma unroll
-    for (uint32_t step = kPackRun / 2; step >= 1; step >>= 1) {
+    for (uint32_t step = RUN / 2; step >= 1; step >>= 1) {
         const uint32_t t = lo + step;
-        const uint32_t vt = static_cast<uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(min(t, kPackRun - 1)), kWave));
+        const uint32_t vt = static_cast<uint32_t>(__shfl(static_cast<int>(v), static_cast<int>(min(t, RUN - 1)), kWave));
         if (t < R && vt <= g) lo = t;
     }
     return lo;
@@ -1916,21 +1917,24 @@ __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__res
 // A single-pass form (hits held in LDS until a decoupled look-back over the
 // runs resolved) made every wave wait for its slowest predecessor's
 // evaluation: 0.27 ms vs the launches' sum.
+// RUN = chain slots per run (kReqRun), 8 slices per chain slot
+template <uint32_t RUN>
 struct ReqLds {
-    uint4 pred[kPackRun * 3];  // per chain: {first, last, n, width}, {e0, espan, vlo, vspan},
-                               // {class mask, extra-ALT bits | end_void << 31, 1/width (f32), LUT offset}
-    unsigned long long tcc[kPackRun], tan[kPackRun];
-    unsigned int exw[kPackSlots / 32];  // bit = the slot's slice exists
-    unsigned int slow[kPackRun];
-    unsigned int cstart[kPackRun + 2];  // staging position of each chain's first hit (~0: none); + a dummy slot
-    unsigned int ccount[kPackRun];
-    uint8_t rowchain[kRunRows];         // row (run-relative) -> its chain (0xff: not a chain row)
+    static constexpr uint32_t kSlots = RUN * 8;
+    uint4 pred[RUN * 2];  // per chain: {first, last, class mask, extra-ALT bits | end_void << 31},
+                          // {e0, espan, vlo | vspan << 9 | (n - 1) << 17, LUT offset}
+    unsigned long long tcc[RUN], tan[RUN];
+    unsigned int exw[kSlots / 32];  // bit = the slot's slice exists
+    unsigned int slow[RUN / 32];    // bit = a VT_SLOW candidate in the chain's window
+    unsigned int cstart[RUN + 2];   // staging position of each chain's first hit (~0: none); + a dummy slot
+    unsigned int ccount[RUN];
+    uint8_t rowchain[kRunRows];     // row (run-relative) -> its chain (0xff: not a chain row)
 };
 
 struct RowChunk {
     ChainChunk x;
-    uint32_t k, so;  // the lane's chain and its first slot
-    bool first;      // the lane holds its chain's first candidate
+    uint32_t k;  // the lane's chain
+    bool first;  // the lane holds its chain's first candidate
 };
 
 // the batch's symbolic-ALT LUT words (8 per distinct variantType string) are
@@ -1939,14 +1943,15 @@ struct RowChunk {
 constexpr uint32_t kReqLut = 512;
 constexpr uint32_t kDeliverTile = 16;  // runs per request_deliver_kernel wave
 
-template <bool LDS_LUT>
+template <bool LDS_LUT, uint32_t RUN>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_eval_kernel(
     DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
     unsigned long long *__restrict__ status, const QRes *__restrict__ sres, ReqPartial *__restrict__ rows,
     uint64_t *__restrict__ row_cnt, uint64_t *__restrict__ row_src, uint64_t *__restrict__ stage, uint32_t n_lut) {
-    __shared__ ReqLds lds_all[kWavesPerBlock];
+    using Lds = ReqLds<RUN>;
+    __shared__ Lds lds_all[kWavesPerBlock];
     __shared__ uint32_t slut[LDS_LUT ? kReqLut : 1];
-    ReqLds &L = lds_all[threadIdx.x >> 6];
+    Lds &L = lds_all[threadIdx.x >> 6];
     const uint32_t ul = static_cast<uint32_t>(lane_id());
     if constexpr (LDS_LUT) {
         for (uint32_t i = threadIdx.x; i < n_lut; i += kBlock) slut[i] = st.sym_lut[i];
@@ -1955,15 +1960,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const uint32_t *lut_base = LDS_LUT ? slut : st.sym_lut;
     const uint32_t w = launch_wave();
     if (w >= n_runs) return;
-    // the run record and the run's chain descriptors (kPackRun slots per run,
+    // the run record and the run's chain descriptors (RUN slots per run,
     // first == 0 = an empty slot) are independent loads: one round trip for both
     const RowRun rr = runs[w];
     ReqChain C{};
-    if (ul < kPackRun) C = chains[static_cast<uint64_t>(w) * kPackRun + ul];
+    if (ul < RUN) C = chains[static_cast<uint64_t>(w) * RUN + ul];
     const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
     const uint64_t stage_at = uniform64(rr.stage);
     const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
-    const uint32_t R = static_cast<uint32_t>(__popcll(__ballot(ul < kPackRun && C.first != 0)));
+    const uint32_t R = static_cast<uint32_t>(__popcll(__ballot(ul < RUN && C.first != 0)));
     const uint32_t nrows = row_hi - row_lo;
     // ---- setup: lane k < R = chain k (descriptor, predicate constants, candidate bounds)
     uint32_t rowk = 0, c0 = 0, cnt = 0, nsl = 0;
@@ -1972,9 +1977,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint32_t kind = ((C.bits >> 23) & 7u) | ((C.bits >> 26) & 1u ? kChainEndVoid : 0u);
         VtPred q(st, 0u, 0u, 0u, 0u, kind, 0u, 0u, 0u);
         nsl = (C.last - C.first) / kReqWidth + 1;
-        L.pred[3 * ul] = uint4{C.first, C.last, nsl, 0u};
-        L.pred[3 * ul + 1] = uint4{C.e0, C.espan, C.bits & 511u, (C.bits >> 9) & 255u};
-        L.pred[3 * ul + 2] = uint4{q.cmask, q.xneed | (q.end_void ? 0x80000000u : 0u), 0u, C.lut_off};
+        L.pred[2 * ul] = uint4{C.first, C.last, q.cmask, q.xneed | (q.end_void ? 0x80000000u : 0u)};
+        L.pred[2 * ul + 1] = uint4{C.e0, C.espan, (C.bits & 0x1ffffu) | (nsl - 1) << 17, C.lut_off};
         // the chain's candidate range [c_lo, c_hi): resolved on the host at
         // prepare (the same coarse-index bounds it sizes the staging with), so
         // the candidate loads follow the descriptor load directly
@@ -1982,17 +1986,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         cnt = C.c_hi - C.c_lo;
         L.tcc[ul] = 0;
         L.tan[ul] = 0;
-        L.slow[ul] = 0;
     }
-    if (ul < kPackSlots / 32) L.exw[ul] = 0;
+    if (ul < RUN / 32) L.slow[ul] = 0;
+    if (ul < Lds::kSlots / 32) L.exw[ul] = 0;
     if (ul < kRunRows) L.rowchain[ul] = 0xffu;
-    if (ul <= kPackRun) L.cstart[ul] = 0xffffffffu;
+    if (ul < RUN + 2) L.cstart[ul] = 0xffffffffu;  // (the dummy slot RUN + 1 is never read)
     wave_lds_sync();
     if (ul < R) L.rowchain[rowk - row_lo] = static_cast<uint8_t>(ul);
     // candidate ranges end to end (pex / pin), slots (sex / sin); delta = c0 - pex
     uint32_t pin = cnt, sin = nsl;
 #pragma unroll
-    for (int d = 1; d < static_cast<int>(kPackRun); d <<= 1) {
+    for (int d = 1; d < static_cast<int>(RUN); d <<= 1) {
         const uint32_t t = __shfl_up(pin, d, kWave), u = __shfl_up(sin, d, kWave);
         if (ul >= static_cast<uint32_t>(d)) {
             pin += t;
@@ -2000,7 +2004,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         }
     }
     const uint32_t pex = pin - cnt, sex = sin - nsl, delta = c0 - pex;
-    const uint32_t T = rdl(pin, kPackRun - 1);
+    const uint32_t T = rdl(pin, RUN - 1);
     const uint32_t i_safe = rdl(c0, 0);
     wave_lds_sync();
     // ---- candidates: chunk c covers run positions [64 c, 64 c + 64)
@@ -2010,10 +2014,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     auto load = [&](uint32_t base) -> RowChunk {
         const uint32_t g = base + ul;
         RowChunk c;
-        const uint32_t k = last_le(pex, R, g);
+        const uint32_t k = last_le<RUN>(pex, R, g);
         c.k = k;
         const uint32_t dl = static_cast<uint32_t>(__shfl(static_cast<int>(delta), static_cast<int>(k), kWave));
-        c.so = static_cast<uint32_t>(__shfl(static_cast<int>(sex), static_cast<int>(k), kWave));
         c.first = static_cast<uint32_t>(__shfl(static_cast<int>(pex), static_cast<int>(k), kWave)) == g;
         const uint32_t i = (base < T && g < T) ? g + dl : i_safe;
         c.x = ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]};
@@ -2029,16 +2032,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint32_t k = c.k;
         const uint32_t g = base + ul;
         const bool valid = g < T;
-        const uint4 p0 = L.pred[3 * k], p1 = L.pred[3 * k + 1], p2 = L.pred[3 * k + 2];
-        const uint32_t first = p0.x, last = p0.y, n = p0.z;
-        VtPred Pd(p1.x, p1.y, p1.z, p1.w, p2.x, p2.y & 0x7fffffffu, (p2.y >> 31) != 0, lut_base + p2.w);
+        const uint4 p0 = L.pred[2 * k], p1 = L.pred[2 * k + 1];
+        const uint32_t first = p0.x, last = p0.y, nm1 = p1.z >> 17;
+        VtPred Pd(p1.x, p1.y, p1.z & 511u, (p1.z >> 9) & 255u, p0.z, p0.w & 0x7fffffffu, (p0.w >> 31) != 0,
+                  lut_base + p1.w);
         const bool inwin = valid && x.p >= first && x.p <= last;
         const bool cand = inwin && Pd.end_ok(x.h.end);
         if (__ballot(cand && (x.h.w & VT_SLOW)))  // never: prepare sends such requests per slice
-            if (cand && (x.h.w & VT_SLOW)) L.slow[k] = 1u;
+            if (cand && (x.h.w & VT_SLOW)) atomicOr(&L.slow[k >> 5], 1u << (k & 31u));
         const LaneOut o = Pd.eval(st, x.h, x.r, cand && !(x.h.w & VT_SLOW));
         const bool hit = o.hm != 0;
-        const uint32_t mark = (valid && c.first) ? k : kPackRun + 1;  // kPackRun + 1: the dummy slot
+        const uint32_t mark = (valid && c.first) ? k : RUN + 1;  // RUN + 1: the dummy slot
         if (!__ballot(hit)) {
             L.cstart[mark] = hpos;
             return;
@@ -2069,7 +2073,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         }
         hpos += tot;
         // slice = (POS - first) / kReqWidth (a constant divisor: multiply-high + shift)
-        const uint32_t slot = c.so + min((x.p - first) / kReqWidth, n - 1);
+        // the chain's first slot: fetched here, not carried in the chunk buffers (VGPRs)
+        const uint32_t so = static_cast<uint32_t>(__shfl(static_cast<int>(sex), static_cast<int>(k), kWave));
+        const uint32_t slot = so + min((x.p - first) / kReqWidth, nm1);
         if (hit) {
             atomicOr(&L.exw[slot >> 5], o.c > 0 ? 1u << (slot & 31u) : 0u);
             atomicAdd(&L.tcc[k], static_cast<unsigned long long>(o.c));
@@ -2093,20 +2099,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     }
     wave_lds_sync();
     // ---- per chain (lane k < R): hit count, exists count, partial
-    uint32_t cs = ul <= R ? L.cstart[ul] : 0xffffffffu;
-    if (ul == R) cs = hpos;
+    // suffix min (lanes >= R hold the end, hpos): a chain without candidates
+    // starts where the next does (shfl_down past lane 63 returns the lane's own)
+    uint32_t cs = ul < R ? L.cstart[ul] : hpos;
 #pragma unroll
-    for (int d = 1; d < static_cast<int>(kPackRun) * 2; d <<= 1) {  // suffix min: a chain without candidates starts where the next does
-        const uint32_t t = __shfl_down(cs, d, kWave);
-        if (ul + static_cast<uint32_t>(d) <= R) cs = min(cs, t);
-    }
-    const uint32_t cs_next = __shfl_down(cs, 1, kWave);
+    for (int d = 1; d < kWave; d <<= 1) cs = min(cs, static_cast<uint32_t>(__shfl_down(cs, d, kWave)));
+    // every lane takes part in the shuffle (a lane outside a divergent
+    // shuffle supplies no value: lane 62 would read 0 from lane 63 when R = 64)
+    const uint32_t cs_down = static_cast<uint32_t>(__shfl_down(cs, 1, kWave));
+    const uint32_t cs_next = ul + 1 < kWave ? cs_down : hpos;
     ReqPartial part{0, 0, 0, 0, 0};
     if (ul < R) {
-        const bool slow = L.slow[ul] != 0;  // a VT_SLOW candidate in the window: never for prepared chains
+        const bool slow = (L.slow[ul >> 5] >> (ul & 31u)) & 1u;  // a VT_SLOW candidate in the window: never for prepared chains
         int64_t ex = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < kPackSlots / 32; ++q) {
+        for (uint32_t q = sex >> 5; q < (sin + 31) >> 5; ++q) {  // the words the chain's slots [sex, sin) touch
             const uint32_t a = sex > 32 * q ? min(sex - 32 * q, 32u) : 0u, b = sin > 32 * q ? min(sin - 32 * q, 32u) : 0u;
             const uint32_t m = (b >= 32 ? ~0u : ((1u << b) - 1u)) & (a >= 32 ? 0u : (~0u << a));
             ex += __popc(L.exw[q] & m);
@@ -3402,8 +3408,8 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                          unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,
-                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, hipStream_t s, hipEvent_t ev0,
-                         hipEvent_t ev1) {
+                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, hipStream_t s,
+                         hipEvent_t ev0, hipEvent_t ev1) {
     if (!n_runs) {
         (void)hipMemsetAsync(row_off, 0, 8, s);
         return;
@@ -3411,12 +3417,16 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
     const dim3 grid(blocks_for(n_runs));
     const uint32_t n_tiles = request_tiles(n_runs);
     if (ev0) (void)hipEventRecord(ev0, s);
-    if (n_lut <= kReqLut)
-        hipLaunchKernelGGL(request_eval_kernel<true>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
-                           rows, row_off, row_src, stage, n_lut);
-    else
-        hipLaunchKernelGGL(request_eval_kernel<false>, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
-                           rows, row_off, row_src, stage, n_lut);
+    auto eval = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres, rows, row_off,
+                           row_src, stage, n_lut);
+    };
+    // RUN = 32 only: a 64-slot instantiation (8 slots per chain, 2-word
+    // predicates) faulted in the genome request test on MI355X (round 3, cause
+    // not found) and is not built
+    (void)run;
+    if (n_lut <= kReqLut) eval(request_eval_kernel<true, kReqRun>);
+    else eval(request_eval_kernel<false, kReqRun>);
     if (ev1) (void)hipEventRecord(ev1, s);
     hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, status, n_runs, tstatus, n_tiles);
     hipLaunchKernelGGL(request_deliver_kernel, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg,
@@ -3427,6 +3437,8 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
 uint32_t request_tiles(uint32_t n_runs) { return (n_runs + kDeliverTile - 1) / kDeliverTile; }
 
 uint32_t pack_run_max() { return kPackRun; }
+uint32_t req_slots_max(uint32_t run) { return run * 8; }
+uint32_t req_run_max() { return kReqRun; }
 uint32_t pack_slots_max() { return kPackSlots; }
 
 void launch_chain_src(const ChainDev *chains, uint32_t n_chains, const uint32_t *corig, const QRes *res,

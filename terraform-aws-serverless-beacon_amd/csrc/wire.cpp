@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <unordered_map>
@@ -599,6 +600,11 @@ void put_error(std::string &o, int32_t err) {
 
 // json.dumps(PerformQueryResponse.dump()) for query i of rs (engine.py
 // ResultSet.responses); false = text the Python path could not decode
+// SBEACON_WIRE_TRACE: time in the variant / sample-name writers, per thread
+thread_local double tl_var_ms = 0, tl_samp_ms = 0;
+thread_local uint64_t tl_var_n = 0, tl_samp_n = 0, tl_var_b = 0, tl_samp_b = 0;
+bool g_wire_trace = false;
+
 bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
     const size_t start = o.size();  // o may already hold earlier responses
     sb_result_view v;
@@ -624,7 +630,16 @@ bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
         put_i64(o, v.all_alleles_count);
     }
     o += ", \"variants\": [";
-    if (v.n_variants && !result_variants_json(rs, i, o)) return false;
+    if (v.n_variants) {
+        const auto t0 = g_wire_trace ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
+        const size_t b0 = o.size();
+        if (!result_variants_json(rs, i, o)) return false;
+        if (g_wire_trace) {
+            tl_var_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            tl_var_n += v.n_variants;
+            tl_var_b += o.size() - b0;
+        }
+    }
     o += "], \"call_count\": ";
     if (v.big_limbs) {
         if (!put_limbs(o, v.big_call_count, v.big_limbs)) {
@@ -643,7 +658,16 @@ bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
             put_i64(o, v.sample_indices[k]);
         }
     o += "], \"sample_names\": [";
-    if ((sel || inc) && v.n_sample_indices && !result_sample_names_json(rs, i, o)) return false;
+    if ((sel || inc) && v.n_sample_indices) {
+        const auto t0 = g_wire_trace ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
+        const size_t b0 = o.size();
+        if (!result_sample_names_json(rs, i, o)) return false;
+        if (g_wire_trace) {
+            tl_samp_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            tl_samp_n += v.n_sample_indices;
+            tl_samp_b += o.size() - b0;
+        }
+    }
     o += "]}";
     return true;
 }
@@ -731,6 +755,9 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
                 });
             }
             std::vector<double> t_ms(threads, 0.0);
+            std::mutex tot_mu;
+            double tot[6] = {0, 0, 0, 0, 0, 0};
+            g_wire_trace = trace;
             std::vector<uint64_t> t_n(threads, 0);
             par(idx.size(), threads, [&](size_t j, unsigned t) {
                 const auto t0 = trace ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
@@ -745,6 +772,23 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
                 ++t_n[t];
                 const uint32_t i = idx[j];
                 std::string &o = tbuf[t];
+                struct Flush {  // this thread's writer times into the call's totals
+                    bool on;
+                    std::mutex *mu;
+                    double *tot;
+                    ~Flush() {
+                        if (!on) return;
+                        std::lock_guard<std::mutex> lk(*mu);
+                        tot[0] += tl_var_ms;
+                        tot[1] += tl_samp_ms;
+                        tot[2] += static_cast<double>(tl_var_n);
+                        tot[3] += static_cast<double>(tl_samp_n);
+                        tot[4] += static_cast<double>(tl_var_b);
+                        tot[5] += static_cast<double>(tl_samp_b);
+                        tl_var_ms = tl_samp_ms = 0;
+                        tl_var_n = tl_samp_n = tl_var_b = tl_samp_b = 0;
+                    }
+                } flush{trace, &tot_mu, tot};
                 const size_t at = o.size();
                 if (put_response(o, rs, j, ev[i])) {
                     o.push_back('\n');
@@ -765,6 +809,10 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
                     bytes += tbuf[t].size();
                 }
                 std::fprintf(stderr, "[wire] format threads: max %.2f ms, sum %.2f ms, %zu bytes\n", mx, sum, bytes);
+                std::fprintf(stderr,
+                             "[wire] format parts: variants %.2f ms (%.0f strings, %.0f bytes), sample names %.2f ms "
+                             "(%.0f names, %.0f bytes)\n",
+                             tot[0], tot[2], tot[4], tot[1], tot[3], tot[5]);
             }
             tick("format");
         }
