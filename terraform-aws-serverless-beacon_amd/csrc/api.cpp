@@ -3805,57 +3805,111 @@ void result_prepare_json(sb_result_set *r) {
     }
 }
 
-bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o) {
-    const auto &ix = r->sidx[i];
-    const auto &nj = r->names_json[r->vcf_of[i]];
-    for (size_t j = 0; j < ix.size(); ++j) {
-        const uint32_t h = r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j];
-        const std::string &x = nj[h];
-        if (x.size() == 1 && x[0] == '\x01') return false;
-        if (j) o += ", ";
-        o += x;
-    }
-    return true;
-}
-
 bool result_variants_json(const sb_result_set *r, size_t i, std::string &o) {
     const sb_store &s = *r->s;
     const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
-    std::string chrom;
-    if (!json_escape_append(chrom, r->chrom[i].data(), r->chrom[i].size())) return false;
-    const char *blob = reinterpret_cast<const char *>(s.h_blob.data());
-    char num[16];
+    if (b == a) return true;
+    char cbuf[256];  // the chrom escaped (longer names: the string path)
+    std::string chrom_long;
+    const std::string &cs = r->chrom[i];
+    const char *chrom = cbuf;
+    size_t clen;
+    if (6 * cs.size() <= sizeof cbuf) {
+        char *e = json_escape_to(cbuf, cs.data(), cs.size());
+        if (!e) return false;
+        clen = static_cast<size_t>(e - cbuf);
+    } else {
+        if (!json_escape_append(chrom_long, cs.data(), cs.size())) return false;
+        chrom = chrom_long.data();
+        clen = chrom_long.size();
+    }
+    // an upper bound of the text (escapes at most 6x a string's bytes), one
+    // resize, raw writes, then the true length
+    size_t need = 0;
     for (uint64_t h = a; h < b; ++h) {
         const uint64_t hit = r->hit[h];
         const uint32_t rec = static_cast<uint32_t>(hit);
         const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
-        if (h > a) o += ", ";
-        o.push_back('"');
-        o += chrom;
-        o += "\\t";
-        uint32_t v = s.h_pos[rec];
-        char *e = num + sizeof num, *q = e;
-        do {
-            *--q = static_cast<char>('0' + v % 10);
-            v /= 10;
-        } while (v);
-        o.append(q, static_cast<size_t>(e - q));
-        o += "\\t";
-        if (!json_escape_append(o, blob + s.h_ref_off[rec], s.h_end[rec] - s.h_pos[rec] + 1)) return false;
-        o += "\\t";
-        bool ok;
+        const size_t al = k == 0 ? s.h_a0_len[rec] : s.h_x_len[s.h_x_lo[rec] + k - 1];
+        need += 2 + 2 + clen + 2 + 10 + 2 + 6 * (size_t(s.h_end[rec]) - s.h_pos[rec] + 1) + 2 + 6 * al + 2 +
+                r->vt_json[s.h_vt[rec]].size();
+    }
+    const size_t o0 = o.size();
+    o.resize(o0 + need);
+    char *p = &o[o0];
+    const char *blob = reinterpret_cast<const char *>(s.h_blob.data());
+    for (uint64_t h = a; h < b; ++h) {
+        const uint64_t hit = r->hit[h];
+        const uint32_t rec = static_cast<uint32_t>(hit);
+        const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
+        if (h > a) {
+            *p++ = ',';
+            *p++ = ' ';
+        }
+        *p++ = '"';
+        std::memcpy(p, chrom, clen);
+        p += clen;
+        *p++ = '\\';
+        *p++ = 't';
+        {
+            char num[16];
+            uint32_t v = s.h_pos[rec];
+            char *e = num + sizeof num, *q = e;
+            do {
+                *--q = static_cast<char>('0' + v % 10);
+                v /= 10;
+            } while (v);
+            std::memcpy(p, q, static_cast<size_t>(e - q));
+            p += e - q;
+        }
+        *p++ = '\\';
+        *p++ = 't';
+        p = json_escape_to(p, blob + s.h_ref_off[rec], s.h_end[rec] - s.h_pos[rec] + 1);
+        if (!p) return o.resize(o0), false;
+        *p++ = '\\';
+        *p++ = 't';
         if (k == 0) {
-            ok = json_escape_append(o, blob + s.h_a0_off[rec], s.h_a0_len[rec]);
+            p = json_escape_to(p, blob + s.h_a0_off[rec], s.h_a0_len[rec]);
         } else {
             const uint32_t x = s.h_x_lo[rec] + k - 1;
-            ok = json_escape_append(o, blob + s.h_x_off[x], s.h_x_len[x]);
+            p = json_escape_to(p, blob + s.h_x_off[x], s.h_x_len[x]);
         }
-        if (!ok) return false;
-        o += "\\t";
+        if (!p) return o.resize(o0), false;
+        *p++ = '\\';
+        *p++ = 't';
         const std::string &vt = r->vt_json[s.h_vt[rec]];
-        if (vt.size() == 1 && vt[0] == '\x01') return false;  // a VT string that is not UTF-8
-        o += vt;
-        o.push_back('"');
+        if (vt.size() == 1 && vt[0] == '\x01') return o.resize(o0), false;  // a VT string that is not UTF-8
+        std::memcpy(p, vt.data(), vt.size());
+        p += vt.size();
+        *p++ = '"';
+    }
+    o.resize(static_cast<size_t>(p - o.data()));
+    return true;
+}
+
+bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o) {
+    const auto &ix = r->sidx[i];
+    const auto &nj = r->names_json[r->vcf_of[i]];
+    auto name = [&](size_t j) -> const std::string & {
+        return nj[r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j]];
+    };
+    size_t need = ix.empty() ? 0 : 2 * (ix.size() - 1);
+    for (size_t j = 0; j < ix.size(); ++j) {
+        const std::string &x = name(j);
+        if (x.size() == 1 && x[0] == '\x01') return false;  // not UTF-8
+        need += x.size();
+    }
+    const size_t o0 = o.size();
+    o.resize(o0 + need);
+    char *p = &o[o0];
+    for (size_t j = 0; j < ix.size(); ++j) {
+        const std::string &x = name(j);
+        if (j) {
+            *p++ = ',';
+            *p++ = ' ';
+        }
+        std::memcpy(p, x.data(), x.size());
+        p += x.size();
     }
     return true;
 }

@@ -71,6 +71,63 @@ inline bool json_escape_append(std::string &o, const char *s, size_t n) {
     return true;
 }
 
+// the same into a raw buffer with room for 6 * n bytes (the worst case:
+// every byte a \uXXXX escape); returns the end, nullptr on invalid UTF-8
+inline char *json_escape_to(char *p, const char *s, size_t n) {
+    static const char kHex[] = "0123456789abcdef";
+    auto u4 = [&](uint32_t v) {
+        p[0] = '\\';
+        p[1] = 'u';
+        p[2] = kHex[(v >> 12) & 15];
+        p[3] = kHex[(v >> 8) & 15];
+        p[4] = kHex[(v >> 4) & 15];
+        p[5] = kHex[v & 15];
+        p += 6;
+    };
+    for (size_t i = 0; i < n;) {
+        const unsigned char c = static_cast<unsigned char>(s[i]);
+        if (c >= 0x20 && c < 0x7f && c != '"' && c != '\\') {
+            *p++ = static_cast<char>(c);
+            ++i;
+            continue;
+        }
+        if (c < 0x80) {
+            switch (c) {
+                case '"': *p++ = '\\'; *p++ = '"'; break;
+                case '\\': *p++ = '\\'; *p++ = '\\'; break;
+                case '\n': *p++ = '\\'; *p++ = 'n'; break;
+                case '\r': *p++ = '\\'; *p++ = 'r'; break;
+                case '\t': *p++ = '\\'; *p++ = 't'; break;
+                case '\b': *p++ = '\\'; *p++ = 'b'; break;
+                case '\f': *p++ = '\\'; *p++ = 'f'; break;
+                default: u4(c);  // other control characters and DEL
+            }
+            ++i;
+            continue;
+        }
+        const int len = (c & 0xe0) == 0xc0 ? 2 : (c & 0xf0) == 0xe0 ? 3 : (c & 0xf8) == 0xf0 ? 4 : 0;
+        if (!len || i + len > n) return nullptr;
+        uint32_t cp = c & (0x7f >> len);
+        for (int k = 1; k < len; ++k) {
+            const unsigned char cc = static_cast<unsigned char>(s[i + k]);
+            if ((cc & 0xc0) != 0x80) return nullptr;
+            cp = (cp << 6) | (cc & 0x3f);
+        }
+        if ((len == 2 && cp < 0x80) || (len == 3 && cp < 0x800) || (len == 4 && (cp < 0x10000 || cp > 0x10ffff)) ||
+            (cp >= 0xd800 && cp < 0xe000))
+            return nullptr;
+        if (cp >= 0x10000) {
+            const uint32_t v = cp - 0x10000;
+            u4(0xd800 + (v >> 10));
+            u4(0xdc00 + (v & 0x3ff));
+        } else {
+            u4(cp);
+        }
+        i += static_cast<size_t>(len);
+    }
+    return p;
+}
+
 // the result set's variant strings of query i as JSON strings joined by ", "
 // (f'{chrom}\\t{POS}\\t{REF}\\t{ALT}\\t{VT}', search_variants.py:210), written
 // straight from the store's columns; false on text Python could not decode.
