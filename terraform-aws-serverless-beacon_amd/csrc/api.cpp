@@ -2001,9 +2001,11 @@ struct PinnedHost {  // grow-only pinned host staging (hipHostMalloc)
     }
 };
 
-// one job's windows (runs [g0, g1) of the call)
+// one job's windows (runs [g0, g1) of the call) over its keys with POS in
+// [p_from, p_to) (a POS range of the job: windows never straddle it)
 bool plan_job_windows(const sb_store &s, const std::vector<KRun> &runs, size_t g0, size_t g1, uint32_t target,
-                      std::vector<KWin> &wins, std::vector<KPiece> &pieces, const char **why) {
+                      std::vector<KWin> &wins, std::vector<KPiece> &pieces, const char **why, uint64_t p_from = 0,
+                      uint64_t p_to = ~0ull) {
     constexpr uint64_t kSpan = (1ull << kWinSpanBits) - 2;
     const std::vector<uint32_t> &pos = s.h_dk_pos;
     const size_t m = g1 - g0;
@@ -2015,6 +2017,13 @@ bool plan_job_windows(const sb_store &s, const std::vector<KRun> &runs, size_t g
         cur[r] = runs[g0 + r].key_lo;
         end[r] = runs[g0 + r].key_hi;
         pmax = std::max(pmax, runs[g0 + r].pos_hi);
+        if (p_from > 0)
+            cur[r] = static_cast<uint32_t>(
+                std::lower_bound(pos.begin() + cur[r], pos.begin() + end[r], std::min<uint64_t>(p_from, 0xffffffffull)) -
+                pos.begin());
+        if (p_to <= 0xffffffffull)
+            end[r] = static_cast<uint32_t>(
+                std::lower_bound(pos.begin() + cur[r], pos.begin() + end[r], static_cast<uint32_t>(p_to)) - pos.begin());
     }
     // lower bound of x in run r at or after a, searched outward from the
     // hint h (the runs of a job have similar densities, so the answer is
@@ -2114,22 +2123,46 @@ bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan
         groups.emplace_back(g0, g1);
         g0 = g1;
     }
+    // tasks: each job cut into POS ranges at quantiles of its first run's
+    // keys (few jobs per call would leave the pool's threads idle: 50 equal
+    // jobs on 16 threads take 4 rounds)
+    struct Task {
+        size_t q;
+        uint64_t p_from, p_to;
+    };
+    std::vector<Task> tasks;
+    const size_t split = groups.size() >= 64 ? 1 : std::min<size_t>(8, (128 + groups.size() - 1) / std::max<size_t>(groups.size(), 1));
+    for (size_t q = 0; q < groups.size(); ++q) {
+        const KRun &r0 = runs[groups[q].first];
+        uint64_t prev = 0;
+        for (size_t k = 1; k < split; ++k) {
+            const uint64_t p = s.h_dk_pos[r0.key_lo + (uint64_t(r0.key_hi - r0.key_lo) * k) / split];
+            if (p > prev) {
+                tasks.push_back(Task{q, prev, p});
+                prev = p;
+            }
+        }
+        tasks.push_back(Task{q, prev, ~0ull});
+    }
     std::vector<std::vector<KWin>> &tw = P.wins;
     std::vector<std::vector<KPiece>> &tp = P.pieces;
-    tw.assign(groups.size(), {});
-    tp.assign(groups.size(), {});
-    std::vector<const char *> why(groups.size(), nullptr);
-    auto work = [&](size_t q) {
+    tw.assign(tasks.size(), {});
+    tp.assign(tasks.size(), {});
+    std::vector<const char *> why(tasks.size(), nullptr);
+    auto work = [&](size_t t) {
+        const Task &T = tasks[t];
+        const auto &G = groups[T.q];
         const char *w = nullptr;
         uint64_t keys = 0;
-        for (size_t g = groups[q].first; g < groups[q].second; ++g) keys += runs[g].key_hi - runs[g].key_lo;
-        tw[q].reserve(keys / (target / 2 + 1) + 4);
-        tp[q].reserve(2 * (keys / (target / 2 + 1) + 4) * (groups[q].second - groups[q].first));
-        if (!plan_job_windows(s, runs, groups[q].first, groups[q].second, target, tw[q], tp[q], &w)) why[q] = w;
+        for (size_t g = G.first; g < G.second; ++g) keys += runs[g].key_hi - runs[g].key_lo;
+        keys = keys / split + 1;
+        tw[t].reserve(keys / (target / 2 + 1) + 4);
+        tp[t].reserve(2 * (keys / (target / 2 + 1) + 4) * (G.second - G.first));
+        if (!plan_job_windows(s, runs, G.first, G.second, target, tw[t], tp[t], &w, T.p_from, T.p_to)) why[t] = w;
     };
-    if (groups.size() > 1) WorkerPool::get().run(groups.size(), work);
-    else if (!groups.empty()) work(0);
-    for (size_t q = 0; q < groups.size(); ++q) {
+    if (tasks.size() > 1) WorkerPool::get().run(tasks.size(), work);
+    else if (!tasks.empty()) work(0);
+    for (size_t q = 0; q < tasks.size(); ++q) {
         if (why[q]) return P.why = why[q], false;
         P.n_wins += tw[q].size();
         P.n_pieces += tp[q].size();
