@@ -627,7 +627,7 @@ void put_error(std::string &o, int32_t err) {
 // SBEACON_WIRE_TRACE: time in the variant / sample-name writers, per thread
 thread_local double tl_var_ms = 0, tl_samp_ms = 0;
 thread_local uint64_t tl_var_n = 0, tl_samp_n = 0, tl_var_b = 0, tl_samp_b = 0;
-bool g_wire_trace = false;
+const bool g_wire_trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;  // read once at load
 
 bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
     const size_t start = o.size();  // o may already hold earlier responses
@@ -785,7 +785,6 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
             std::vector<double> t_ms(threads, 0.0);
             std::mutex tot_mu;
             double tot[6] = {0, 0, 0, 0, 0, 0};
-            g_wire_trace = trace;
             std::vector<uint64_t> t_n(threads, 0);
             par(idx.size(), threads, [&](size_t j, unsigned t) {
                 const auto t0 = trace ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
