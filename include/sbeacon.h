@@ -103,6 +103,10 @@ void sb_vcf_scan_free(sb_vcf_scan *s);
 int sb_builder_finish(sb_builder *b, int device, sb_store **out);
 void sb_builder_free(sb_builder *b);
 void sb_store_close(sb_store *s);
+/* Free the device and pinned buffers a store keeps for reuse by request
+ * batches (at most 64 of each, 4 GiB device / 2 GiB pinned; batches in
+ * flight keep theirs). */
+int sb_store_trim(sb_store *s);
 
 typedef struct {
     uint64_t n_records;
@@ -458,6 +462,13 @@ int sb_requests_run(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_o
  * sync (total_ms stays the whole pass).  Off by default: the markers add
  * stream gaps. */
 int sb_requests_time_eval(sb_batch *b, int on);
+/* After a pass (waits for it): flags[w] = 1 when row w's call_count or
+ * all_alleles_count is not exact in int64 -- a slice's count past 64 bits
+ * (Python ints, records answered by the general path) or a sum that
+ * overflows; the row then holds the low 64 bits of the exact value (the
+ * per-slice results, sb_result_view.big_*, carry the exact limbs).
+ * Replaces nothing in the reference (its counts are Python ints). */
+int sb_requests_inexact_rows(sb_batch *b, uint8_t *flags);
 
 /* ---- device-resident batch (benchmarks / fused pipelines) ----------------
  * Upload a batch once, then launch the query kernels repeatedly on the

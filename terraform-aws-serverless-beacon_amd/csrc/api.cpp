@@ -190,9 +190,28 @@ struct ReqPool {
     std::mutex mu;
     std::vector<Pinned> pinned;
     std::vector<DevMem> dev;
-    static constexpr size_t kKeep = 64;
-    ~ReqPool() {
+    static constexpr size_t kKeep = 64;                      // buffers kept per kind at most
+    static constexpr size_t kKeepDevBytes = size_t(4) << 30;  // and bytes: the largest go first
+    static constexpr size_t kKeepPinnedBytes = size_t(2) << 30;
+    ~ReqPool() { trim(); }
+    template <class V>
+    static size_t total(const V &v) {
+        size_t t = 0;
+        for (const auto &x : v) t += x.bytes;
+        return t;
+    }
+    template <class V>
+    static size_t largest(const V &v) {
+        size_t b = 0;
+        for (size_t i = 1; i < v.size(); ++i)
+            if (v[i].bytes > v[b].bytes) b = i;
+        return b;
+    }
+    void trim() {  // free every cached buffer (sb_store_trim)
+        std::lock_guard<std::mutex> lk(mu);
         for (Pinned &x : pinned) (void)hipHostFree(x.p);
+        pinned.clear();
+        dev.clear();
     }
     template <class V>
     static ptrdiff_t fit(const V &v, size_t n) {
@@ -224,6 +243,11 @@ struct ReqPool {
             (void)hipHostFree(pinned.front().p);
             pinned.erase(pinned.begin());
         }
+        while (pinned.size() > 1 && total(pinned) > kKeepPinnedBytes) {
+            const size_t i = largest(pinned);
+            (void)hipHostFree(pinned[i].p);
+            pinned.erase(pinned.begin() + static_cast<ptrdiff_t>(i));
+        }
     }
     DevMem get_dev(size_t n) {
         {
@@ -243,6 +267,7 @@ struct ReqPool {
         std::lock_guard<std::mutex> lk(mu);
         dev.push_back(std::move(x));
         if (dev.size() > kKeep) dev.erase(dev.begin());
+        while (dev.size() > 1 && total(dev) > kKeepDevBytes) dev.erase(dev.begin() + static_cast<ptrdiff_t>(largest(dev)));
     }
 };
 
@@ -321,14 +346,17 @@ struct sb_batch {
             for (auto &p : eval_ev)
                 for (auto e : p) (void)hipEventDestroy(e);
         }
-        // dchains: ReqChain slots (kPackRun per run), then the RowRuns at runs_at
+        // dchains: ReqChain slots (kReqRun per run), then the RowRuns at runs_at
         DevMem dchains, status, tstatus, stage, row_src, lut, sseg, sherr;
+        // rows whose counts are not exact in int64 (sb_requests_inexact_rows):
+        // per-slice wide marks + one flag per row (batches with general records)
+        DevMem wide, row_flag;
         size_t runs_at = 0;
-        uint32_t run = 32;             // chain slots per run (request_eval_kernel's RUN)
+        uint32_t run = kReqRun;        // chain slots per run (request_eval_kernel: one lane each)
         std::shared_ptr<ReqPool> pool;  // where the device buffers go back when the batch is freed
         bool slices = false;           // some rows answered per slice (the batch's query part)
         void give_back() {
-            for (DevMem *m : {&dchains, &status, &tstatus, &stage, &row_src, &lut, &sseg, &sherr})
+            for (DevMem *m : {&dchains, &status, &tstatus, &stage, &row_src, &lut, &sseg, &sherr, &wide, &row_flag})
                 if (m->p) pool->put_dev(std::move(*m));
         }
     };
@@ -2949,6 +2977,13 @@ int sb_builder_finish(sb_builder *b, int device, sb_store **out) {
 void sb_builder_free(sb_builder *b) { delete b; }
 void sb_store_close(sb_store *s) { delete s; }
 
+int sb_store_trim(sb_store *s) {
+    return guard([&] {
+        if (!s) throw Error(SB_EINVAL, "NULL store");
+        if (s->req_pool) static_cast<ReqPool *>(s->req_pool.get())->trim();
+    });
+}
+
 int sb_store_get_info(const sb_store *s, sb_store_info *out) {
     return guard([&] {
         if (!s || !out) throw Error(SB_EINVAL, "NULL argument");
@@ -2995,12 +3030,12 @@ constexpr int64_t kSplitSize = 10000;  // lambda/splitQuery/lambda_function.py:1
 // Request batch (sb_requests_prepare): rows = requests.  A request whose
 // slices need none of the order-dependent machinery (variantType query with
 // referenceBases 'N', include_details, no boolean break, a non-negative-AC
-// VCF, no samples, at most kChainMax slices, no VT_SLOW / general record in
-// its window) becomes ONE chain answered by request_rows_kernel; every other
-// request is cut into its splitQuery slices (split_query_sync,
+// VCF, no samples, at most kReqChainSlices slices, no VT_SLOW / general
+// record in its window) becomes ONE chain answered by request_eval_kernel;
+// every other request is cut into its splitQuery slices (split_query_sync,
 // lambda/splitQuery/lambda_function.py:74-110) and answered per slice by the
-// query kernels (the batch's query part), its row reduced and gathered by
-// request_reduce + request_rows_kernel.
+// query kernels (the batch's query part), its row reduced by request_reduce
+// and gathered by request_deliver_kernel.
 extern "C++" {  // overloads and templates inside the extern "C" block
 
 // Request sources: the sb_request array, or the same requests as columns
@@ -3161,7 +3196,8 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     tick("vtypes");
     // classify: 0 = no slices, 1 = one chain, 2 = per slice (and the slice
     // count of a chain); the first bad request, if any, is reported
-    std::vector<uint8_t> cls(n, 0), nsl_of(n, 0);
+    std::vector<uint8_t> cls(n, 0);
+    std::vector<uint32_t> nsl_of(n, 0), clo_of(n, 0), chi_of(n, 0);
     std::atomic<size_t> bad{SIZE_MAX};
     parallel_for(n, [&](size_t i) {
         const sb_request x = src(i);
@@ -3178,7 +3214,7 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
                              (x.selected_samples_only || x.include_samples);
         bool chain = !x.alternate_bases && x.reference_bases && x.reference_len == 1 && x.reference_bases[0] == 'N' &&
                      x.include_details && x.granularity != SB_GRAN_BOOLEAN && !x.selected_samples_only &&
-                     !x.strict_variant_type && !(collect && v.words) && v.nonneg && nsl <= kChainMax &&
+                     !x.strict_variant_type && !(collect && v.words) && v.nonneg && nsl <= kReqChainSlices &&
                      x.start_min >= 1 && x.start_max <= 0xfffffffell;
         if (chain) {  // a VT_SLOW / general record in the window: per slice
             const auto &sp = s.seg_slow_pos[x.vcf_id][x.contig];
@@ -3186,7 +3222,22 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
             if (a != sp.end() && *a <= static_cast<uint64_t>(x.start_max)) chain = false;
         }
         cls[i] = chain ? 1 : 2;
-        if (chain) nsl_of[i] = static_cast<uint8_t>(nsl);
+        if (chain) {
+            nsl_of[i] = static_cast<uint32_t>(nsl);
+            // the candidate range from the (kind, segment) coarse index (no
+            // END can match: none)
+            const VcIndex &vi = v.vc_index[x.contig][vt_of[i]];
+            auto cb = [&](uint64_t xx, uint32_t up) -> uint32_t {
+                if (xx <= vi.base) return vi.c_lo;
+                const uint64_t b = (xx - vi.base) >> vi.shift;
+                return b >= vi.n ? vi.c_hi : s.h_vc_bucket[vi.off + b + up];
+            };
+            const int64_t emin = x.end_min, emax = x.end_max;
+            const bool end_void = emax < 0 || emin > 0xffffffffll || emin > emax;
+            const uint32_t C0 = cb(static_cast<uint64_t>(x.start_min), 0);
+            clo_of[i] = C0;
+            chi_of[i] = end_void ? C0 : std::max(C0, cb(static_cast<uint64_t>(x.start_max) + 1, 1));
+        }
     });
     if (bad.load() != SIZE_MAX) {
         const size_t i = bad.load();
@@ -3242,11 +3293,13 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     std::vector<uint32_t> seg(n + 1, 0);
     for (uint32_t o : owner) ++seg[o + 1];
     for (size_t w = 0; w < n; ++w) seg[w + 1] += seg[w];
-    // runs of consecutive rows (<= kRunRows rows, R->run chains, 8 slots per
-    // chain slot), formed greedily in blocks of rows on several threads (a
-    // block boundary also ends a run)
+    // runs of consecutive rows (<= kRunRows rows, R->run chains, every chain
+    // starting below position kReqStartPos of the run's candidates), formed
+    // greedily in blocks of rows on several threads (a block boundary also
+    // ends a run)
     R->run = req_run_max();
-    const uint32_t run_max = R->run, slots_max = req_slots_max(R->run);
+    const uint32_t run_max = R->run;
+    constexpr uint64_t kReqStartPos = 64ull * kReqStartChunks;
     {
         const size_t nb = std::max<size_t>(1, std::min<size_t>(16, n / 65536));
         std::vector<std::vector<RowRun>> part(nb);
@@ -3257,21 +3310,23 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
             out.reserve((r1 - r0) / 16 + 1);
             RowRun cur{r0, r0, 0, 0, 0, 0, kRunSimple};
             uint32_t c = 0;
-            uint64_t sl = 0;
+            uint64_t sl = 0, tpos = 0;  // the run's candidates so far
             for (uint32_t i = r0; i < r1; ++i) {
                 const bool ch = cls[i] == 1;
                 const uint32_t need = nsl_of[i];
-                if (i > cur.row_lo && (i - cur.row_lo == kRunRows || (ch && (cur.c_hi - cur.c_lo == run_max ||
-                                                                               cur.n_slots + need > slots_max)))) {
+                if (i > cur.row_lo && (i - cur.row_lo == kRunRows ||
+                                       (ch && (cur.c_hi - cur.c_lo == run_max || tpos >= kReqStartPos)))) {
                     cur.row_hi = i;
                     out.push_back(cur);
                     cur = RowRun{i, i, c, c, 0, 0, kRunSimple};
+                    tpos = 0;
                 }
                 if (cls[i] == 2) cur.flags &= ~kRunSimple;  // a row answered per slice: gathered row by row
                 if (ch) {
                     cur.c_hi = ++c;
                     cur.n_slots += need;
                     sl += need;
+                    tpos += chi_of[i] - clo_of[i];
                 }
             }
             if (r1 > r0) {
@@ -3297,7 +3352,7 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
         R->n_chains = cbase;
     }
     tick("runs");
-    // chain descriptors straight into pinned staging, kPackRun slots per run
+    // chain descriptors straight into pinned staging, kReqRun slots per run
     // (request_eval_kernel loads a run's slots beside its RowRun), the runs
     // after them: one H2D copy from pinned memory
     const size_t n_runs = R->runs.size(), slots = run_max;
@@ -3312,10 +3367,12 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
         ReqChain *out = hc + r * slots;
         uint32_t j = 0;
         uint64_t cap = 0;
+        // the chains with candidates first (row order: their hits are staged
+        // in slot order), then those without
+        for (int pass = 0; pass < 2; ++pass)
         for (uint32_t i = run.row_lo; i < run.row_hi; ++i) {
-            if (cls[i] != 1) continue;
+            if (cls[i] != 1 || (chi_of[i] > clo_of[i]) != (pass == 0)) continue;
             const sb_request x = src(i);
-            const VcIndex &vi = s.vcfs[x.vcf_id].vc_index[x.contig][vt_of[i]];
             ReqChain &cd = out[j++];
             cd.first = static_cast<uint32_t>(x.start_min);
             cd.last = static_cast<uint32_t>(x.start_max);
@@ -3328,17 +3385,10 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
             cd.bits = req_bits(vh < vl ? 256u : static_cast<uint32_t>(vl), vh < vl ? 0u : static_cast<uint32_t>(vh - vl),
                                i - run.row_lo, vt_of[i], end_void);
             cd.lut_off = lut_of[i];
-            // the candidate range from the (kind, segment) coarse index; hit
-            // capacity: every ALT of it
-            auto cb = [&](uint64_t xx, uint32_t up) -> uint32_t {
-                if (xx <= vi.base) return vi.c_lo;
-                const uint64_t b = (xx - vi.base) >> vi.shift;
-                return b >= vi.n ? vi.c_hi : s.h_vc_bucket[vi.off + b + up];
-            };
-            const uint32_t C0 = cb(cd.first, 0), C1 = end_void ? C0 : std::max(C0, cb(uint64_t(cd.last) + 1, 1));
-            cd.c_lo = C0;
-            cd.c_hi = C1;
-            cap += s.h_vc_altpre[C1] - s.h_vc_altpre[C0];
+            // the candidate range (classify); hit capacity: every ALT of it
+            cd.c_lo = clo_of[i];
+            cd.c_hi = chi_of[i];
+            cap += s.h_vc_altpre[cd.c_hi] - s.h_vc_altpre[cd.c_lo];
         }
         std::memset(static_cast<void *>(out + j), 0, (slots - j) * sizeof(ReqChain));  // empty slots: first == 0
         rcap[r] = cap;
@@ -3373,6 +3423,10 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
         for (uint32_t q = 0; q < B.nq; ++q) he[q] = B.host_err[q] ? 1 : 0;
         R->sseg = P.get_dev(seg.size() * 4);
         R->sherr = P.get_dev(he.size());
+        if (B.gen_grid) {  // general records can make a row's counts wider than int64
+            R->wide = P.get_dev(std::max<size_t>(B.nq, 1));
+            R->row_flag = P.get_dev(std::max<size_t>(n, 1));
+        }
         HIP_OK(hipMemcpyAsync(R->sseg.p, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, st));
         HIP_OK(hipMemcpyAsync(R->sherr.p, he.data(), he.size(), hipMemcpyHostToDevice, st));
     }
@@ -3392,8 +3446,12 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
     mark_run(B);
     if (R.slices) {  // the per-slice part, then its rows (chain rows come out zero; the row kernel writes them)
         run_kernels(B);
-        launch_request_reduce(B.res.as<QRes>(), R.sseg.as<uint32_t>(), R.sherr.as<uint8_t>(), R.n_rows,
-                              static_cast<ReqPartial *>(rows), st);
+        if (R.wide.p) {
+            HIP_OK(hipMemsetAsync(R.wide.p, 0, B.nq, st));
+            mark_wide(B.gen_big_n.as<uint32_t>(), B.gen_big.as<GenBig>(), B.gen_big_cap, R.wide.as<uint8_t>(), st);
+        }
+        launch_request_reduce(B.res.as<QRes>(), R.sseg.as<uint32_t>(), R.sherr.as<uint8_t>(), R.wide.as<uint8_t>(),
+                              R.n_rows, static_cast<ReqPartial *>(rows), R.row_flag.as<uint8_t>(), st);
     }
     DStore d = s.d;
     d.sym_lut = R.lut.as<uint32_t>();
@@ -3453,6 +3511,22 @@ int sb_requests_run(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_o
             throw Error(SB_EINVAL, "NULL argument");
         std::lock_guard<std::mutex> lk(b->mu);  // this batch's buffers only (see sb_requests_prepare)
         run_requests(*b, dev_rows, dev_hits, dev_row_off, rec_base);
+    });
+}
+
+int sb_requests_inexact_rows(sb_batch *b, uint8_t *flags) {
+    return guard([&] {
+        if (!b || (!flags && b->req && b->req->n_rows)) throw Error(SB_EINVAL, "NULL argument");
+        if (!b->req) throw Error(SB_EINVAL, "not a request batch (sb_requests_prepare)");
+        sb_batch::Req &R = *b->req;
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (!R.row_flag.p) {
+            std::memset(flags, 0, R.n_rows);
+            return;
+        }
+        HIP_OK(hipSetDevice(b->s->device));
+        HIP_OK(hipStreamSynchronize(b->strm()));
+        HIP_OK(hipMemcpy(flags, R.row_flag.p, R.n_rows, hipMemcpyDeviceToHost));
     });
 }
 
@@ -3620,8 +3694,8 @@ int sb_batch_reduce_requests(sb_batch *b, void *dev_out) {
                               b->piece.as<uint32_t>(), b->n_rows, static_cast<ReqPartial *>(dev_out),
                               b->rowsrc.as<ulonglong2>(), b->strm());
         else
-            launch_request_reduce(b->res.as<QRes>(), b->seg.as<uint32_t>(), b->herr.as<uint8_t>(), b->n_rows,
-                                  static_cast<ReqPartial *>(dev_out), b->strm());
+            launch_request_reduce(b->res.as<QRes>(), b->seg.as<uint32_t>(), b->herr.as<uint8_t>(), nullptr,
+                                  b->n_rows, static_cast<ReqPartial *>(dev_out), nullptr, b->strm());
         HIP_OK(hipGetLastError());
     });
 }

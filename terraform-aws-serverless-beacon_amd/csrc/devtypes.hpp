@@ -223,17 +223,25 @@ struct alignas(16) RowRun {
     uint32_t row_lo, row_hi;  // rows [row_lo, row_hi)
     uint32_t c_lo, c_hi;      // the run's chains, rows increasing
     uint64_t stage;           // first staging slot of the run (its chains' hit capacity follows)
-    uint32_t n_slots;         // slices of its chains (<= 256)
+    uint32_t n_slots;         // slices of its chains
     uint32_t flags;           // kRunSimple
 };
 static_assert(sizeof(RowRun) == 32, "RowRun is two 16-byte words");
 
-// A request's chain as request_eval_kernel reads it (kPackRun slots per run,
+// A request's chain as request_eval_kernel reads it (kReqRun slots per run:
+// the chains with candidates first, in row order, then those without, then
 // first == 0 = an empty slot): splitQuery's slices are [first + j * kReqWidth,
 // ...] up to `last`, so width and slice count follow from the window; the
 // row, kind and length bounds share one word.  32 B, not ChainDev's 80.
 constexpr uint32_t kReqWidth = 10000;  // lambda/splitQuery/lambda_function.py:12
-constexpr uint32_t kReqRun = 32;       // ReqChain slots per run (request_eval_kernel's RUN)
+constexpr uint32_t kReqRun = 64;       // ReqChain slots per run (one lane of request_eval_kernel each)
+// chain starts below position 64 * kReqStartChunks of a run's candidates
+// (laid end to end) are found through the wave's chain-start bitmap, later
+// ones by ballot (runs are cut there when they can be)
+constexpr uint32_t kReqStartChunks = 64;
+// slices of one request chain at most (slice keys of request_eval_kernel are
+// chain << 20 | slice)
+constexpr uint32_t kReqChainSlices = (1u << 20) - 1;
 struct alignas(16) ReqChain {
     uint32_t first, last;  // the request's [start_min, start_max] (first >= 1)
     uint32_t c_lo, c_hi;   // candidate range (host-resolved from the coarse index)

@@ -53,9 +53,13 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const u
                       uint64_t *bitmap, SPart *part, SRes *out, hipStream_t s);
 
 // Per-request partials of one shard (sb_batch_reduce_requests): row w sums
-// the answers of queries [seg[w], seg[w+1]).
-void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, uint32_t n_rows,
-                           ReqPartial *out, hipStream_t s);
+// the answers of queries [seg[w], seg[w+1]).  wide (optional, per query) =
+// the query's counts needed more than 64 bits (mark_wide, from the general
+// path's big list); row_flag (optional, per row) = 1 when the row's
+// call_count / all_alleles_count are not exact in int64 (low 64 bits kept).
+void mark_wide(const uint32_t *big_n, const GenBig *big, uint32_t cap, uint8_t *wide, hipStream_t s);
+void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, const uint8_t *wide,
+                           uint32_t n_rows, ReqPartial *out, uint8_t *row_flag, hipStream_t s);
 
 // Dense per-query hit lists on the device: dense[q] = exclusive prefix of the
 // queries' hit counts (dense[nq] = total), out[dense[q] ..] = query q's hits
@@ -110,8 +114,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, hipStream_t s,
                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
-// slices per run of `run` chain slots (ReqLds<run>::kSlots); chain slots per run
-uint32_t req_slots_max(uint32_t run);
+// chain slots per run (kReqRun)
 uint32_t req_run_max();
 uint32_t request_tiles(uint32_t n_runs);
 

@@ -1892,18 +1892,32 @@ __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__res
 }
 
 // ---------------------------------------------------------------- request rows
-// Request batches (sb_requests_run, devtypes.hpp RowRun), two launches:
+// Request batches (sb_requests_run, devtypes.hpp RowRun), three launches:
 //
-// request_eval_kernel -- one wave per run of consecutive request rows (XCD-
-// aware block order; no inter-wave dependency).  The run's chains are
-// evaluated as in chain_pack_kernel (rows only: per-slice exists bits + chain
-// totals), with two changes: each candidate lane finds its chain by a
-// wave-uniform walk over the few chains that start inside its chunk
-// (v_readlane of the lane-held prefixes: no binary search, no ds_bpermute),
-// and hits are appended in candidate order -- which is chain order, which is
-// row order -- to the run's staging region (capacity planned on the host).
-// The wave writes its rows, each row's hit count (into row_off) and the run's
-// total as an aggregate status word.
+// request_eval_kernel -- one wave per run of consecutive request rows with up
+// to kReqRun (64) chains (XCD-aware block order; no inter-wave dependency).
+// Lane k holds chain k: its candidate range laid end to end with the run's
+// other chains (positions [pex, pin) of the run's T positions).  A chunk of 64
+// positions is evaluated per step, lane L taking position 64 c + L:
+//   * its chain: the chain-start bitmap of the chunk (built once per wave in
+//     LDS, then held one word per lane; chunks past the 64th collect their
+//     few starts by ballot) read with v_readlane into SGPRs; the lane's chain
+//     = the chunk's first chain + v_mbcnt of the starts at or below it -- two
+//     VALU, no LDS round trip, no search;
+//   * its candidate: index = position + the chain's delta (one LDS read), the
+//     three candidate columns loaded PIPE chunks ahead;
+//   * the predicate of lambda/performQuery/search_variants.py:100-183 (the
+//     variantType branch, patched-oracle intent) with the chain's constants
+//     from two 16-byte LDS words; hits staged in candidate order = chain order
+//     = row order (ballot + mbcnt);
+//   * per-chain sums without atomics: inclusive DPP scans over the chunk of
+//     the hit count, the new-slice count (a positive hit whose 10 kb slice
+//     differs from the previous positive hit's: max-scan of slice keys), the
+//     call count and the AN sum; lane k then pulls the scans at its chain's
+//     last lane in the chunk (ds_bpermute) and subtracts chain k-1's (DPP
+//     wave_shr) -- chain k's part of the chunk, added to lane-held totals.
+// The wave writes its rows, each row's hit count (into row_cnt), the staging
+// start of rows answered row by row, and the run's total as a status word.
 //
 // request_tile_scan_kernel -- the runs' totals, summed per tile of 16 runs, into tile offsets.
 //
@@ -1914,44 +1928,83 @@ __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__res
 // batch's slice part, reduced into `rows` by request_reduce before the first
 // kernel).
 //
-// A single-pass form (hits held in LDS until a decoupled look-back over the
-// runs resolved) made every wave wait for its slowest predecessor's
-// evaluation: 0.27 ms vs the launches' sum.
-// RUN = chain slots per run (kReqRun), 8 slices per chain slot
-template <uint32_t RUN>
-struct ReqLds {
-    static constexpr uint32_t kSlots = RUN * 8;
-    uint4 pred[RUN * 2];  // per chain: {first, last, class mask, extra-ALT bits | end_void << 31},
-                          // {e0, espan, vlo | vspan << 9 | (n - 1) << 17, LUT offset}
-    unsigned long long tcc[RUN], tan[RUN];
-    unsigned int exw[kSlots / 32];  // bit = the slot's slice exists
-    unsigned int slow[RUN / 32];    // bit = a VT_SLOW candidate in the chain's window
-    unsigned int cstart[RUN + 2];   // staging position of each chain's first hit (~0: none); + a dummy slot
-    unsigned int ccount[RUN];
-    uint8_t rowchain[kRunRows];     // row (run-relative) -> its chain (0xff: not a chain row)
-};
-
-struct RowChunk {
-    ChainChunk x;
-    uint32_t k;  // the lane's chain
-    bool first;  // the lane holds its chain's first candidate
-};
+// Measured forms this replaces: chains found by a
+// binary search over lane-held prefixes (5 dependent ds_bpermutes per chunk)
+// and per-chain sums by contended 64-bit LDS atomics, 32 chains per run.
 
 // the batch's symbolic-ALT LUT words (8 per distinct variantType string) are
 // staged in LDS once per workgroup when they fit: a predicate's LUT word is
 // then an LDS read, not a dependent global load behind the candidate's load
 constexpr uint32_t kReqLut = 512;
 constexpr uint32_t kDeliverTile = 16;  // runs per request_deliver_kernel wave
+constexpr int kReqPipe = 2;            // candidate chunks in flight per wave
 
-template <bool LDS_LUT, uint32_t RUN>
+// DPP lane moves (GFX9 controls; lanes without a source read 0)
+template <int CTRL, int ROW = 0xf, int BANK = 0xf>
+__device__ __forceinline__ uint32_t dpp32(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROW, BANK, false));
+}
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v) { return dpp32<0x138>(v); }  // lane i <- lane i - 1 (lane 0: 0)
+__device__ __forceinline__ uint64_t wave_shr1_64(uint64_t v) {
+    return (static_cast<uint64_t>(wave_shr1(static_cast<uint32_t>(v >> 32))) << 32) | wave_shr1(static_cast<uint32_t>(v));
+}
+// inclusive scans over the wave: row_shr 1, 2, 4, 8 inside rows of 16, then
+// row_bcast 15 / 31 across rows (the GFX9 sequence; no LDS)
+__device__ __forceinline__ uint32_t incl_sum_u32(uint32_t v) {
+    v += dpp32<0x111>(v);
+    v += dpp32<0x112>(v);
+    v += dpp32<0x114>(v);
+    v += dpp32<0x118>(v);
+    v += dpp32<0x142, 0xa>(v);
+    v += dpp32<0x143, 0xc>(v);
+    return v;
+}
+__device__ __forceinline__ uint32_t incl_max_u32(uint32_t v) {
+    v = max(v, dpp32<0x111>(v));
+    v = max(v, dpp32<0x112>(v));
+    v = max(v, dpp32<0x114>(v));
+    v = max(v, dpp32<0x118>(v));
+    v = max(v, dpp32<0x142, 0xa>(v));
+    v = max(v, dpp32<0x143, 0xc>(v));
+    return v;
+}
+__device__ __forceinline__ uint64_t incl_sum_u64(uint64_t v) {
+    v += static_cast<uint64_t>(dpp_i64<0x111, 0xf, 0xf>(static_cast<int64_t>(v)));
+    v += static_cast<uint64_t>(dpp_i64<0x112, 0xf, 0xf>(static_cast<int64_t>(v)));
+    v += static_cast<uint64_t>(dpp_i64<0x114, 0xf, 0xf>(static_cast<int64_t>(v)));
+    v += static_cast<uint64_t>(dpp_i64<0x118, 0xf, 0xf>(static_cast<int64_t>(v)));
+    v += static_cast<uint64_t>(dpp_i64<0x142, 0xa, 0xf>(static_cast<int64_t>(v)));
+    v += static_cast<uint64_t>(dpp_i64<0x143, 0xc, 0xf>(static_cast<int64_t>(v)));
+    return v;
+}
+__device__ __forceinline__ uint32_t bperm(uint32_t v, uint32_t lane) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(static_cast<int>(lane << 2), static_cast<int>(v)));
+}
+__device__ __forceinline__ uint64_t bperm64(uint64_t v, uint32_t lane) {
+    return (static_cast<uint64_t>(bperm(static_cast<uint32_t>(v >> 32), lane)) << 32) | bperm(static_cast<uint32_t>(v), lane);
+}
+
+struct ReqLds {
+    uint4 a[kReqRun];  // chain k: {candidate index - run position, first, last - first, e0}
+    uint4 b[kReqRun];  // {espan, vlo | vspan << 9, class mask | kind << 24, LUT offset}
+    unsigned long long wch[kReqStartChunks];  // chunk c: bit j = a chain's first position is 64 c + j
+    unsigned int slow[kReqRun / 32];          // bit = a VT_SLOW candidate in the chain's window
+    uint8_t rowchain[kRunRows];               // row (run-relative) -> its chain (0xff: not a chain row)
+};
+
+struct ReqChunk {
+    ChainChunk x;
+    uint32_t k;  // the lane's chain
+};
+
+template <bool LDS_LUT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_eval_kernel(
     DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
     unsigned long long *__restrict__ status, const QRes *__restrict__ sres, ReqPartial *__restrict__ rows,
     uint64_t *__restrict__ row_cnt, uint64_t *__restrict__ row_src, uint64_t *__restrict__ stage, uint32_t n_lut) {
-    using Lds = ReqLds<RUN>;
-    __shared__ Lds lds_all[kWavesPerBlock];
+    __shared__ ReqLds lds_all[kWavesPerBlock];
     __shared__ uint32_t slut[LDS_LUT ? kReqLut : 1];
-    Lds &L = lds_all[threadIdx.x >> 6];
+    ReqLds &L = lds_all[threadIdx.x >> 6];
     const uint32_t ul = static_cast<uint32_t>(lane_id());
     if constexpr (LDS_LUT) {
         for (uint32_t i = threadIdx.x; i < n_lut; i += kBlock) slut[i] = st.sym_lut[i];
@@ -1960,101 +2013,150 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const uint32_t *lut_base = LDS_LUT ? slut : st.sym_lut;
     const uint32_t w = launch_wave();
     if (w >= n_runs) return;
-    // the run record and the run's chain descriptors (RUN slots per run,
-    // first == 0 = an empty slot) are independent loads: one round trip for both
+    // the run record and the run's chain descriptors (lane k = slot k; the
+    // non-empty chains first, then the empty ones, then first == 0 slots):
+    // independent loads, one round trip
     const RowRun rr = runs[w];
-    ReqChain C{};
-    if (ul < RUN) C = chains[static_cast<uint64_t>(w) * RUN + ul];
+    const ReqChain C = chains[static_cast<uint64_t>(w) * kReqRun + ul];
     const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
     const uint64_t stage_at = uniform64(rr.stage);
     const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
-    const uint32_t R = static_cast<uint32_t>(__popcll(__ballot(ul < RUN && C.first != 0)));
+    const bool slot = C.first != 0;
+    const uint32_t R = static_cast<uint32_t>(__popcll(__ballot(slot)));
+    const uint32_t cnt = slot ? C.c_hi - C.c_lo : 0u;
     const uint32_t nrows = row_hi - row_lo;
-    // ---- setup: lane k < R = chain k (descriptor, predicate constants, candidate bounds)
-    uint32_t rowk = 0, c0 = 0, cnt = 0, nsl = 0;
-    if (ul < R) {
-        rowk = row_lo + ((C.bits >> 17) & 63u);
-        const uint32_t kind = ((C.bits >> 23) & 7u) | ((C.bits >> 26) & 1u ? kChainEndVoid : 0u);
-        VtPred q(st, 0u, 0u, 0u, 0u, kind, 0u, 0u, 0u);
-        nsl = (C.last - C.first) / kReqWidth + 1;
-        L.pred[2 * ul] = uint4{C.first, C.last, q.cmask, q.xneed | (q.end_void ? 0x80000000u : 0u)};
-        L.pred[2 * ul + 1] = uint4{C.e0, C.espan, (C.bits & 0x1ffffu) | (nsl - 1) << 17, C.lut_off};
-        // the chain's candidate range [c_lo, c_hi): resolved on the host at
-        // prepare (the same coarse-index bounds it sizes the staging with), so
-        // the candidate loads follow the descriptor load directly
-        c0 = C.c_lo;
-        cnt = C.c_hi - C.c_lo;
-        L.tcc[ul] = 0;
-        L.tan[ul] = 0;
+    // ---- setup: candidate ranges end to end (lane k: [pex, pin))
+    const uint32_t pin = incl_sum_u32(cnt), pex = pin - cnt;
+    const uint32_t T = rdl(pin, kWave - 1);
+    const uint32_t Rn = static_cast<uint32_t>(__popcll(__ballot(cnt != 0)));  // non-empty chains = lanes 0 .. Rn-1
+    const uint32_t rowk = row_lo + ((C.bits >> 17) & 63u);
+    const uint32_t kind = (C.bits >> 23) & 7u;
+    const uint32_t nsl = slot ? (C.last - C.first) / kReqWidth + 1 : 0u;
+    {
+        constexpr uint32_t kDel = vt_class_mask(VT_DEL), kIns = vt_class_mask(VT_INS), kDup = vt_class_mask(VT_DUP),
+                           kDupT = vt_class_mask(VT_DUPT), kCnv = vt_class_mask(VT_CNV);
+        const uint32_t cm = kind == VT_DEL ? kDel : kind == VT_INS ? kIns : kind == VT_DUP ? kDup : kind == VT_DUPT ? kDupT
+                          : kind == VT_CNV ? kCnv : 0u;
+        L.a[ul] = uint4{C.c_lo - pex, C.first, C.last - C.first, C.e0};
+        L.b[ul] = uint4{C.espan, C.bits & 0x1ffffu, cm | kind << 24, C.lut_off};
     }
-    if (ul < RUN / 32) L.slow[ul] = 0;
-    if (ul < Lds::kSlots / 32) L.exw[ul] = 0;
-    if (ul < kRunRows) L.rowchain[ul] = 0xffu;
-    if (ul < RUN + 2) L.cstart[ul] = 0xffffffffu;  // (the dummy slot RUN + 1 is never read)
+    L.wch[ul] = 0ull;  // kReqStartChunks == kWave
+    L.rowchain[ul] = 0xffu;
+    if (ul < kReqRun / 32) L.slow[ul] = 0u;
     wave_lds_sync();
     if (ul < R) L.rowchain[rowk - row_lo] = static_cast<uint8_t>(ul);
-    // candidate ranges end to end (pex / pin), slots (sex / sin); delta = c0 - pex
-    uint32_t pin = cnt, sin = nsl;
-#pragma unroll
-    for (int d = 1; d < static_cast<int>(RUN); d <<= 1) {
-        const uint32_t t = __shfl_up(pin, d, kWave), u = __shfl_up(sin, d, kWave);
-        if (ul >= static_cast<uint32_t>(d)) {
-            pin += t;
-            sin += u;
-        }
-    }
-    const uint32_t pex = pin - cnt, sex = sin - nsl, delta = c0 - pex;
-    const uint32_t T = rdl(pin, RUN - 1);
-    const uint32_t i_safe = rdl(c0, 0);
+    // the chain-start bitmap of the first kReqStartChunks chunks (later chunks
+    // find their chains' starts one by one)
+    if (ul < Rn && pex < kWave * kReqStartChunks) atomicOr(&L.wch[pex >> 6], 1ull << (pex & 63u));
     wave_lds_sync();
-    // ---- candidates: chunk c covers run positions [64 c, 64 c + 64)
-    // a candidate lane's chain: the last chain j < R whose first position
-    // pex_j <= g (binary search over the lane-held prefixes: VALU + ds_bpermute,
-    // no scalar loop -- SQ counters put a readlane walk at ~1.5 k SALU / wave)
-    auto load = [&](uint32_t base) -> RowChunk {
-        const uint32_t g = base + ul;
-        RowChunk c;
-        const uint32_t k = last_le<RUN>(pex, R, g);
-        c.k = k;
-        const uint32_t dl = static_cast<uint32_t>(__shfl(static_cast<int>(delta), static_cast<int>(k), kWave));
-        c.first = static_cast<uint32_t>(__shfl(static_cast<int>(pex), static_cast<int>(k), kWave)) == g;
-        const uint32_t i = (base < T && g < T) ? g + dl : i_safe;
-        c.x = ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]};
-        return c;
-    };
-    uint32_t hpos = 0;  // hits appended so far (wave-uniform)
-    uint64_t *const sdst = stage + stage_at;  // the run's staging region (capacity planned on the host)
-    // few divergent regions per chunk (each costs exec-mask SALU): the chain-
-    // start marks go to a dummy LDS slot from the other lanes, the slice index
-    // is branch-free, multi-ALT lanes take a separate ballot-guarded path
-    auto eval = [&](const RowChunk &c, uint32_t base) {
-        const ChainChunk &x = c.x;
-        const uint32_t k = c.k;
-        const uint32_t g = base + ul;
-        const bool valid = g < T;
-        const uint4 p0 = L.pred[2 * k], p1 = L.pred[2 * k + 1];
-        const uint32_t first = p0.x, last = p0.y, nm1 = p1.z >> 17;
-        VtPred Pd(p1.x, p1.y, p1.z & 511u, (p1.z >> 9) & 255u, p0.z, p0.w & 0x7fffffffu, (p0.w >> 31) != 0,
-                  lut_base + p1.w);
-        const bool inwin = valid && x.p >= first && x.p <= last;
-        const bool cand = inwin && Pd.end_ok(x.h.end);
-        if (__ballot(cand && (x.h.w & VT_SLOW)))  // never: prepare sends such requests per slice
-            if (cand && (x.h.w & VT_SLOW)) atomicOr(&L.slow[k >> 5], 1u << (k & 31u));
-        const LaneOut o = Pd.eval(st, x.h, x.r, cand && !(x.h.w & VT_SLOW));
-        const bool hit = o.hm != 0;
-        const uint32_t mark = (valid && c.first) ? k : RUN + 1;  // RUN + 1: the dummy slot
-        if (!__ballot(hit)) {
-            L.cstart[mark] = hpos;
-            return;
+    const uint64_t wl = L.wch[ul];  // lane c: chunk c's chain starts
+    const uint32_t cumv = incl_sum_u32(static_cast<uint32_t>(__popcll(wl))) - static_cast<uint32_t>(__popcll(wl));
+    const uint32_t nch = (T + kWave - 1) / kWave;
+    const uint32_t i_safe = rdl(C.c_lo, 0);  // a valid candidate index (chain 0 is non-empty when T > 0)
+    uint64_t *const hdst = stage + stage_at;  // the run's staging region (capacity planned on the host)
+    // ---- candidates
+    auto load = [&](uint32_t c) -> ReqChunk {
+        const uint32_t g = kWave * c + ul;
+        uint64_t W;
+        uint32_t cum;
+        if (c < kReqStartChunks) {
+            W = (static_cast<uint64_t>(rdl(static_cast<uint32_t>(wl >> 32), c)) << 32) | rdl(static_cast<uint32_t>(wl), c);
+            cum = rdl(cumv, c);
+        } else {  // past the bitmap (a run with more than 4 k candidates): the chains starting here, one by one
+            const uint32_t b0 = kWave * c;
+            cum = static_cast<uint32_t>(__popcll(__ballot(ul < Rn && pex < b0)));
+            W = 0;
+            for (uint64_t m = __ballot(ul < Rn && pex >= b0 && pex - b0 < kWave); m; m &= m - 1)
+                W |= 1ull << (rdl(pex, static_cast<uint32_t>(ffs64(m))) - b0);
         }
-        const uint32_t cn = hit ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
+        // chain of position g: starts before the chunk + starts at chunk positions <= lane
+        const uint32_t s0 = cum + static_cast<uint32_t>(W & 1ull) - 1u;
+        const uint64_t W1 = W >> 1;
+        ReqChunk q;
+        q.k = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(W1 >> 32),
+                                        __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(W1), s0));
+        const uint32_t i = g < T ? g + L.a[q.k].x : i_safe;
+        q.x = ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]};
+        return q;
+    };
+    uint32_t hpos = 0;   // hits staged so far (wave-uniform)
+    uint32_t carry = 0;  // the last positive hit's slice key + 1 (keys grow with the position)
+    uint32_t acc_nv = 0, acc_ex = 0;
+    uint64_t acc_cc = 0, acc_an = 0;
+    auto eval = [&](const ReqChunk &q, uint32_t c) {
+        const ChainChunk &x = q.x;
+        const uint32_t k = q.k;
+        const uint32_t base = kWave * c;
+        const uint32_t g = base + ul;
+        const uint4 A = L.a[k], Bw = L.b[k];
+        const uint32_t first = A.y;
+        const uint32_t w = x.h.w;
+        bool cand = g < T && x.p - first <= A.z && x.h.end - A.w <= Bw.x;
+        if (__ballot(cand && (w & VT_SLOW))) {  // never: prepare sends such requests per slice
+            if (cand && (w & VT_SLOW)) atomicOr(&L.slow[k >> 5], 1u << (k & 31u));
+            cand = cand && !(w & VT_SLOW);
+        }
+        const uint32_t vlo = Bw.y & 511u, vspan = (Bw.y >> 9) & 255u;
+        // ALT0 (search_variants.py:100-183): length bounds, then the class
+        // mask of the kind or, for a symbolic ALT, the variantType's LUT bit
+        bool a0 = ((Bw.z >> ((w >> VT_CLASS_SHIFT) & 31u)) & 1u) != 0;
+        if (__ballot(cand && (w & VT_SYM))) {
+            const uint32_t lw = (w & VT_SYM) ? lut_base[Bw.w + ((w >> 21) & 7u)] : 0u;
+            if (w & VT_SYM) a0 = ((lw >> ((w >> 16) & 31u)) & 1u) != 0;
+        }
+        const bool h0 = cand && (w & 0xffu) - vlo <= vspan && a0;
+        // ALTs 2..n (:124 loop): only records whose word says an extra ALT might match
+        const uint32_t kd = Bw.z >> 24;
+        const uint32_t xneed = VT_XK_SYM | vt_xk_bit(kd);
+        const bool xl = cand && (w >> VT_NX_SHIFT) != 0 && (w & xneed) != 0;
+        bool hit;
+        uint32_t cn;      // variants emitted (ALTs with AC != 0)
+        uint64_t em = 0;  // their label indexes (multi-ALT lanes)
+        int64_t cv;       // call count contribution
+        uint32_t anv;     // AN contribution
+        const bool multi_rec = __ballot(xl) != 0;
+        if (!multi_rec) {
+            hit = h0;
+            cv = hit ? x.h.ac0 : 0;
+            cn = hit && x.h.ac0 != 0 ? 1u : 0u;
+            em = cn;
+            anv = hit ? static_cast<uint32_t>(x.h.an) : 0u;
+        } else {
+            uint64_t hm = h0 ? 1ull : 0ull;
+            uint32_t x0 = 0;
+            if (xl) {
+                x0 = st.x_lo[x.r];
+                const uint32_t nx = w >> VT_NX_SHIFT;
+                for (uint32_t j = 0; j < nx; ++j) {
+                    const uint32_t xw = st.xvt[x0 + j];
+                    bool ok = (xw & 0xffu) - vlo <= vspan;
+                    if (ok) {
+                        if (xw & VT_SYM) ok = ((lut_base[Bw.w + ((xw >> 21) & 7u)] >> ((xw >> 16) & 31u)) & 1u) != 0;
+                        else ok = ((Bw.z >> ((xw >> VT_CLASS_SHIFT) & 31u)) & 1u) != 0;
+                    }
+                    if (ok) hm |= 2ull << j;
+                }
+            }
+            hit = hm != 0;
+            cv = 0;
+            for (uint64_t b = hm; b; b &= b - 1) {  // :205-214, AC of each matching ALT
+                const int j = ffs64(b);
+                const int64_t v = j ? st.xrow[x0 + j - 1].ac : x.h.ac0;
+                cv += v;
+                if (v != 0) em |= 1ull << j;
+            }
+            cn = static_cast<uint32_t>(__popcll(em));
+            anv = hit ? static_cast<uint32_t>(x.h.an) : 0u;
+        }
+        // ---- staging: hits in candidate order, ALTs of a record in label order
         uint32_t pre, tot;
         const bool multi = __ballot(cn > 1) != 0;
         if (!multi) {
             const uint64_t one = __ballot(cn == 1);
             pre = popc_below(one);
             tot = static_cast<uint32_t>(__popcll(one));
-        } else {  // bit-sliced (multi-ALT hit lanes)
+            if (cn == 1) hdst[hpos + pre] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(em)) << kHitAltShift);
+        } else {  // bit-sliced prefix (multi-ALT hit lanes)
             pre = 0;
             tot = 0;
             for (uint32_t bb = 0; bb < 7; ++bb) {
@@ -2063,80 +2165,92 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 tot += static_cast<uint32_t>(__popcll(m)) << bb;
                 if (!__ballot(cn >> (bb + 1))) break;
             }
-        }
-        L.cstart[mark] = hpos + pre;
-        if (cn == 1) sdst[hpos + pre] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(o.em)) << kHitAltShift);
-        if (multi && cn > 1) {
             uint32_t at = hpos + pre;
-            for (uint64_t b = o.em; b; b &= b - 1)
-                sdst[at++] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
+            for (uint64_t b = em; b; b &= b - 1)
+                hdst[at++] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
         }
         hpos += tot;
-        // slice = (POS - first) / kReqWidth (a constant divisor: multiply-high + shift)
-        // the chain's first slot: fetched here, not carried in the chunk buffers (VGPRs)
-        const uint32_t so = static_cast<uint32_t>(__shfl(static_cast<int>(sex), static_cast<int>(k), kWave));
-        const uint32_t slot = so + min((x.p - first) / kReqWidth, nm1);
-        if (hit) {
-            atomicOr(&L.exw[slot >> 5], o.c > 0 ? 1u << (slot & 31u) : 0u);
-            atomicAdd(&L.tcc[k], static_cast<unsigned long long>(o.c));
-            atomicAdd(&L.tan[k], static_cast<unsigned long long>(o.anv));
+        // ---- slices with exists = True: a positive hit whose slice differs
+        // from the previous positive hit's (keys: chain << 20 | slice, growing
+        // with the position), the carry from the chunks before
+        const bool pos = hit && cv > 0;
+        const uint32_t key1 = pos ? (k << 20 | (x.p - first) / kReqWidth) + 1u : 0u;
+        const uint32_t mx = incl_max_u32(key1);
+        const uint32_t prev = max(wave_shr1(mx), carry);
+        const bool isnew = pos && key1 != prev;
+        carry = max(carry, rdl(mx, kWave - 1));
+        const uint64_t nb = __ballot(isnew);
+        // inclusive per-lane counts of the chunk: variants | new slices << 16
+        const uint32_t nvex = (pre + cn) | (popc_below(nb) + (isnew ? 1u : 0u)) << 16;
+        // ---- chain k's part of the chunk, pulled by lane k from its last lane
+        const uint32_t lim = min(base + kWave, T);
+        const bool inter = pex < lim && pin > base;
+        const uint32_t e = inter ? min(pin, base + kWave) - 1u - base : 0u;
+        const bool opens = pex <= base;  // no earlier chain in the chunk
+        const uint32_t pn = bperm(nvex, e);
+        const uint32_t qn = wave_shr1(pn);
+        const uint32_t dn = inter ? pn - (opens ? 0u : qn) : 0u;
+        acc_nv += dn & 0xffffu;
+        acc_ex += dn >> 16;
+        const bool big = __ballot(hit && (cv < 0 || cv >= (1ll << 25) || x.h.an < 0 || x.h.an >= (1 << 25))) != 0;
+        if (!big) {  // the chunk's sums fit 32 bits
+            const uint32_t scc = incl_sum_u32(static_cast<uint32_t>(cv)), san = incl_sum_u32(anv);
+            const uint32_t pc = bperm(scc, e), pa = bperm(san, e);
+            const uint32_t qc = wave_shr1(pc), qa = wave_shr1(pa);
+            if (inter) {
+                acc_cc += pc - (opens ? 0u : qc);
+                acc_an += pa - (opens ? 0u : qa);
+            }
+        } else {
+            const uint64_t scc = incl_sum_u64(static_cast<uint64_t>(cv)),
+                           san = incl_sum_u64(static_cast<uint64_t>(static_cast<int64_t>(static_cast<int32_t>(anv))));
+            const uint64_t pc = bperm64(scc, e), pa = bperm64(san, e);
+            const uint64_t qc = wave_shr1_64(pc), qa = wave_shr1_64(pa);
+            if (inter) {
+                acc_cc += pc - (opens ? 0ull : qc);
+                acc_an += pa - (opens ? 0ull : qa);
+            }
         }
     };
     {
-        RowChunk buf[kPackAhead];
+        ReqChunk buf[kReqPipe];
 #pragma unroll
-        for (int a = 0; a < kPackAhead; ++a) buf[a] = load(64u * a);
-        for (uint32_t base = 0; base < T; base += 64u * kPackAhead) {
+        for (int a = 0; a < kReqPipe; ++a)
+            if (static_cast<uint32_t>(a) < nch) buf[a] = load(a);
+        for (uint32_t c0 = 0; c0 < nch; c0 += kReqPipe) {
 #pragma unroll
-            for (int a = 0; a < kPackAhead; ++a) {
-                const uint32_t b = base + 64u * a;
-                if (b < T) {
-                    eval(buf[a], b);
-                    if (b + 64u * kPackAhead < T) buf[a] = load(b + 64u * kPackAhead);
+            for (int a = 0; a < kReqPipe; ++a) {
+                const uint32_t c = c0 + a;
+                if (c < nch) {
+                    eval(buf[a], c);
+                    if (c + kReqPipe < nch) buf[a] = load(c + kReqPipe);
                 }
             }
         }
     }
     wave_lds_sync();
-    // ---- per chain (lane k < R): hit count, exists count, partial
-    // suffix min (lanes >= R hold the end, hpos): a chain without candidates
-    // starts where the next does (shfl_down past lane 63 returns the lane's own)
-    uint32_t cs = ul < R ? L.cstart[ul] : hpos;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) cs = min(cs, static_cast<uint32_t>(__shfl_down(cs, d, kWave)));
-    // every lane takes part in the shuffle (a lane outside a divergent
-    // shuffle supplies no value: lane 62 would read 0 from lane 63 when R = 64)
-    const uint32_t cs_down = static_cast<uint32_t>(__shfl_down(cs, 1, kWave));
-    const uint32_t cs_next = ul + 1 < kWave ? cs_down : hpos;
+    // ---- per chain (lane k < R): staging start (scan of the hit counts), partial
+    const uint32_t cs = incl_sum_u32(acc_nv) - acc_nv;
     ReqPartial part{0, 0, 0, 0, 0};
     if (ul < R) {
-        const bool slow = (L.slow[ul >> 5] >> (ul & 31u)) & 1u;  // a VT_SLOW candidate in the window: never for prepared chains
-        int64_t ex = 0;
-        for (uint32_t q = sex >> 5; q < (sin + 31) >> 5; ++q) {  // the words the chain's slots [sex, sin) touch
-            const uint32_t a = sex > 32 * q ? min(sex - 32 * q, 32u) : 0u, b = sin > 32 * q ? min(sin - 32 * q, 32u) : 0u;
-            const uint32_t m = (b >= 32 ? ~0u : ((1u << b) - 1u)) & (a >= 32 ? 0u : (~0u << a));
-            ex += __popc(L.exw[q] & m);
-        }
-        const uint32_t nv = slow ? 0u : cs_next - cs;
-        L.ccount[ul] = nv;
-        L.cstart[ul] = cs;
-        part = slow ? ReqPartial{0, 0, 0, 0, static_cast<int64_t>(nsl)}
-                    : ReqPartial{ex, static_cast<int64_t>(nv), static_cast<int64_t>(L.tcc[ul]),
-                                 static_cast<int64_t>(L.tan[ul]), 0};
+        const bool slow = (L.slow[ul >> 5] >> (ul & 31u)) & 1u;  // never for prepared chains
+        part = slow ? ReqPartial{0, static_cast<int64_t>(acc_nv), 0, 0, static_cast<int64_t>(nsl)}
+                    : ReqPartial{static_cast<int64_t>(acc_ex), static_cast<int64_t>(acc_nv),
+                                 static_cast<int64_t>(acc_cc), static_cast<int64_t>(acc_an), 0};
+        rows[rowk] = part;
     }
-    wave_lds_sync();
-    // ---- rows (lane i < nrows = row row_lo + i): partials, hit counts, staging starts
+    // ---- rows (lane i < nrows = row row_lo + i): hit counts, staging starts
     const uint32_t row = row_lo + ul;
     const uint32_t ch = ul < nrows ? L.rowchain[ul] : 0xffu;
+    const uint32_t chn = bperm(acc_nv, ch & 63u), chs = bperm(cs, ch & 63u);
     uint64_t nvr = 0;
-    if (ul < nrows) nvr = ch != 0xffu ? L.ccount[ch] : (sres ? static_cast<uint64_t>(rows[row].n_variants) : 0ull);
-    if (ul < R) rows[rowk] = part;
+    if (ul < nrows) nvr = ch != 0xffu ? chn : (sres ? static_cast<uint64_t>(rows[row].n_variants) : 0ull);
     if (!sres && ul < nrows && ch == 0xffu) rows[row] = ReqPartial{0, 0, 0, 0, 0};
     if (ul < nrows) {
         row_cnt[row] = nvr;
-        if (!simple && ch != 0xffu) row_src[row] = stage_at + L.cstart[ch];
+        if (!simple && ch != 0xffu) row_src[row] = stage_at + chs;
     }
-    const uint64_t H = static_cast<uint64_t>(rdl64(wave_incl_scan_i64(static_cast<int64_t>(nvr)), kWave - 1));
+    const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(nvr)), kWave - 1));
     if (ul == 0) status[w] = H;  // read by the tile scan and request_deliver_kernel (kernel boundaries)
 }
 
@@ -2659,10 +2773,24 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(const uint64_t *__restr
 // sums its row's part of the tile.
 constexpr uint32_t kReduceTile = 1024;  // QRes per LDS tile (32 KiB)
 
+// wide[q] = 1 for every slice whose counts needed more than 64 bits (the
+// general path's big list; its QRes holds the low 64 bits)
+__global__ __launch_bounds__(kBlock) void mark_wide_kernel(const uint32_t *__restrict__ big_n,
+                                                           const GenBig *__restrict__ big, uint32_t cap,
+                                                           uint8_t *__restrict__ wide) {
+    const uint32_t n = min(*big_n, cap);
+    for (uint32_t i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock) wide[big[i].orig] = 1;
+}
+
+// row w = the sums of slices [seg[w], seg[w + 1]); row_flag[w] (optional) = 1
+// when a count is not exact in 64 bits (a wide slice, or the sum overflows):
+// the row then holds the low 64 bits of the exact sums
 __global__ __launch_bounds__(kBlock) void request_reduce_kernel(const QRes *__restrict__ res,
                                                                 const uint32_t *__restrict__ seg,
                                                                 const uint8_t *__restrict__ host_err,
-                                                                uint32_t n_rows, ReqPartial *__restrict__ out) {
+                                                                const uint8_t *__restrict__ wide, uint32_t n_rows,
+                                                                ReqPartial *__restrict__ out,
+                                                                uint8_t *__restrict__ row_flag) {
     __shared__ uint4 tile[kReduceTile * (sizeof(QRes) / 16)];
     __shared__ uint8_t terr[kReduceTile];
     static_assert(sizeof(QRes) == 32, "QRes is two 16-byte words");
@@ -2671,6 +2799,7 @@ __global__ __launch_bounds__(kBlock) void request_reduce_kernel(const QRes *__re
     const uint32_t q_lo = seg[r0], q_hi = seg[r1];
     const uint32_t a = w < r1 ? seg[w] : 0u, e = w < r1 ? seg[w + 1] : 0u;
     ReqPartial P{0, 0, 0, 0, 0};
+    bool inexact = false;
     const uint4 *src = reinterpret_cast<const uint4 *>(res);
     for (uint32_t t0 = q_lo; t0 < q_hi; t0 += kReduceTile) {
         const uint32_t t1 = min(q_hi, t0 + kReduceTile);
@@ -2686,12 +2815,20 @@ __global__ __launch_bounds__(kBlock) void request_reduce_kernel(const QRes *__re
             }
             P.exists += r.exists != 0;
             P.n_variants += r.n_hits;
-            P.call_count += r.call_count;
-            P.all_alleles_count += r.all_alleles_count;
+            long long cc, an;
+            inexact |= __builtin_add_overflow(static_cast<long long>(P.call_count), static_cast<long long>(r.call_count), &cc);
+            inexact |= __builtin_add_overflow(static_cast<long long>(P.all_alleles_count),
+                                              static_cast<long long>(r.all_alleles_count), &an);
+            P.call_count = cc;
+            P.all_alleles_count = an;
+            if (wide && wide[q]) inexact = true;
         }
         __syncthreads();
     }
-    if (w < r1) out[w] = P;
+    if (w < r1) {
+        out[w] = P;
+        if (row_flag) row_flag[w] = inexact ? 1 : 0;
+    }
 }
 
 inline uint32_t blocks_for(uint32_t nwaves) { return (nwaves + kWavesPerBlock - 1) / kWavesPerBlock; }
@@ -3426,12 +3563,9 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres, rows, row_off,
                            row_src, stage, n_lut);
     };
-    // RUN = 32 only: a 64-slot instantiation (8 slots per chain, 2-word
-    // predicates) faulted in the genome request test on MI355X (round 3, cause
-    // not found) and is not built
     (void)run;
-    if (n_lut <= kReqLut) eval(request_eval_kernel<true, kReqRun>);
-    else eval(request_eval_kernel<false, kReqRun>);
+    if (n_lut <= kReqLut) eval(request_eval_kernel<true>);
+    else eval(request_eval_kernel<false>);
     if (ev1) (void)hipEventRecord(ev1, s);
     hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, status, n_runs, tstatus, n_tiles);
     hipLaunchKernelGGL(request_deliver_kernel, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg,
@@ -3442,7 +3576,6 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
 uint32_t request_tiles(uint32_t n_runs) { return (n_runs + kDeliverTile - 1) / kDeliverTile; }
 
 uint32_t pack_run_max() { return kPackRun; }
-uint32_t req_slots_max(uint32_t run) { return run * 8; }
 uint32_t req_run_max() { return kReqRun; }
 uint32_t pack_slots_max() { return kPackSlots; }
 
@@ -3527,11 +3660,16 @@ void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, cons
     }
 }
 
-void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, uint32_t n_rows,
-                           ReqPartial *out, hipStream_t s) {
+void mark_wide(const uint32_t *big_n, const GenBig *big, uint32_t cap, uint8_t *wide, hipStream_t s) {
+    hipLaunchKernelGGL(mark_wide_kernel, dim3(std::max<uint32_t>(1, std::min<uint32_t>(64, (cap + kBlock - 1) / kBlock))),
+                       dim3(kBlock), 0, s, big_n, big, cap, wide);
+}
+
+void launch_request_reduce(const QRes *res, const uint32_t *seg, const uint8_t *host_err, const uint8_t *wide,
+                           uint32_t n_rows, ReqPartial *out, uint8_t *row_flag, hipStream_t s) {
     if (!n_rows) return;
     hipLaunchKernelGGL(request_reduce_kernel, dim3((n_rows + kBlock - 1) / kBlock), dim3(kBlock), 0, s, res, seg,
-                       host_err, n_rows, out);
+                       host_err, wide, n_rows, out, row_flag);
 }
 
 void launch_compact(const uint64_t *hit_off, const uint64_t *dense_off, const QRes *res, uint32_t nq,

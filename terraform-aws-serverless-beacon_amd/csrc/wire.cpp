@@ -470,7 +470,10 @@ void load_event(const char *text, size_t len, sb_store *const *stores, size_t n_
         }
     }
     bool inc = false, sel = false;
-    if (const JVal *pt = ev->get("passthrough")) {  // `payload.passthrough or {}`
+    // passthrough: an object, or absent (the payload default {}); anything
+    // else makes lambda_function.py:43 raise AttributeError -- the Python
+    // handler answers it
+    if (const JVal *pt = ev->get("passthrough")) {
         if (pt->kind == JVal::OBJ) {
             inc = truthy(pt->get("includeSamples"), ok);
             sel = truthy(pt->get("selectedSamplesOnly"), ok);
@@ -486,7 +489,7 @@ void load_event(const char *text, size_t len, sb_store *const *stores, size_t n_
                     return;
                 }
             }
-        } else if (pt->kind != JVal::NUL && !(pt->kind == JVal::BOOL && !pt->b)) {
+        } else {
             return;
         }
     }

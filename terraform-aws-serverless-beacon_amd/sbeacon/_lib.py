@@ -219,6 +219,8 @@ SIGNATURES = {
     'sb_requests_run': (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     'sb_requests_prepare_columns': (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(P)]),
     'sb_requests_time_eval': (C.c_int, [P, C.c_int]),
+    'sb_requests_inexact_rows': (C.c_int, [P, P]),
+    'sb_store_trim': (C.c_int, [P]),
     'sb_perform_query_events': (C.c_int, [C.POINTER(P), C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32,
                                           C.POINTER(P)]),
     'sb_json_out_get': (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),

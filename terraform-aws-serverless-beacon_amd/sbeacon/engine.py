@@ -77,7 +77,10 @@ def queries_from_payloads(payloads: list[dict], vcf_id, *, strict_variant_type: 
             v = vid_cache[loc] = vcf_id(loc)
         return v
 
-    pts = [p.get('passthrough') or {} for p in payloads]
+    pts = [p.get('passthrough', {}) for p in payloads]
+    for pt in pts:  # the reference calls payload.passthrough.get(...) (search_variants.py:37)
+        if not isinstance(pt, dict):
+            raise AttributeError(f"'{type(pt).__name__}' object has no attribute 'get'")
     em = [p.get('end_min') for p in payloads]
     ex = [p.get('end_max') for p in payloads]
     if any(x is None for x in em) or any(x is None for x in ex):
@@ -195,6 +198,10 @@ class Store:
         finally:
             L.sb_builder_free(b)
         return cls(s, locs, paths)
+
+    def trim(self):
+        """Free the buffers cached for request batches (sb_store_trim)."""
+        check(lib().sb_store_trim(self._h))
 
     def close(self):
         if self._h:

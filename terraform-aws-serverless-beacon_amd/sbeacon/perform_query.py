@@ -54,4 +54,6 @@ def lambda_handler(event, context):
     except Exception:
         is_async = False
     payload = PerformQueryPayload.load(event)
+    # lambda_function.py:43: a passthrough that is not an object raises here
+    payload.passthrough.get('selectedSamplesOnly', False)
     return perform_query(payload, is_async).dump()

@@ -260,6 +260,13 @@ class RequestBatch:
         timing()['scan_ms'] then reports that kernel alone."""
         check(lib().sb_requests_time_eval(self._h, 1 if on else 0))
 
+    def inexact_rows(self) -> np.ndarray:
+        """After a pass: True for rows whose call_count / all_alleles_count
+        are not exact in int64 (low 64 bits held; sb_requests_inexact_rows)."""
+        f = np.zeros(max(self.n, 1), dtype=np.uint8)
+        check(lib().sb_requests_inexact_rows(self._h, f.ctypes.data))
+        return f[:self.n].astype(bool)
+
     def stats(self) -> dict:
         st = _lib.BatchStats()
         check(lib().sb_batch_get_stats(self._h, C.byref(st)))

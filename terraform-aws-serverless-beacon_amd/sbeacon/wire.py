@@ -30,8 +30,12 @@ def _error_text(e: BaseException) -> str:
     return json.dumps({'errorMessage': str(e), 'errorType': type(e).__name__})
 
 
-def _python_handler(text: str) -> str:
+def _python_handler(text) -> str:
+    """One event through the Python handler; ``text`` is str or UTF-8 bytes
+    (decoded here, so an invalid event is its own error response)."""
     try:
+        if not isinstance(text, str):
+            text = bytes(text).decode()
         return json.dumps(perform_query.lambda_handler(json.loads(text), None))
     except Exception as e:  # the Lambda runtime reports the raised exception
         return _error_text(e)
@@ -113,8 +117,9 @@ def perform_query_events_packed(buf: bytes, offsets: np.ndarray, *, stores=None,
         parts = [bytes(view[int(roff[i]):int(roff[i + 1])]) for i in range(n)]
     finally:
         lib().sb_json_out_free(out)
+    raw = buf if isinstance(buf, bytes) else bytes(buf)
     for i in fb.tolist():
-        parts[i] = _python_handler(buf[int(offsets[i]):int(offsets[i + 1])].decode()).encode() + b'\n'
+        parts[i] = _python_handler(raw[int(offsets[i]):int(offsets[i + 1])]).encode() + b'\n'
     roff = np.zeros(n + 1, dtype=np.uint64)
     roff[1:] = np.cumsum([len(x) for x in parts])
     return EventResponses(memoryview(b''.join(parts)), roff, status)

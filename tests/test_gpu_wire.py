@@ -82,14 +82,16 @@ def test_wire_random_and_fallback_events(stores):
                dict(base, unexpected=1),                        # PerformQueryPayload(**event): TypeError
                dict(base, vcf_location='nowhere.vcf'),          # no store holds it: KeyError
                dict(base, dataset_id='dé\U0001F600"\\'),   # escapes + a non-BMP character (fast path)
-               dict(base, passthrough=None),                    # `passthrough or {}`
+               dict(base, passthrough=None),                    # passthrough.get: AttributeError (:43)
+               dict(base, passthrough=False),                   # the same
                {'Records': {'0': 1}}]                           # an envelope that does not unwrap
         evs.extend(odd)
         buf, off = pack_events([json.dumps(e) for e in evs])
         out = perform_query_events_packed(buf, off)
         fb = out.fallback.tolist()
-        assert fb[-7:] == [1, 1, 1, 1, 0, 0, 1]
-        assert not any(fb[:-7])
+        assert fb[-8:] == [1, 1, 1, 1, 0, 1, 1, 1]
+        assert not any(fb[:-8])
+        assert 'AttributeError' in out[len(evs) - 3] and 'AttributeError' in out[len(evs) - 2]
         for i, ev in enumerate(evs):
             assert out[i] == _python(ev), (ev, out[i])
         assert out.texts() == [out[i] for i in range(len(evs))]
