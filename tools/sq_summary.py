@@ -10,7 +10,7 @@ for d in sys.argv[1:]:
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     disp = collections.defaultdict(set)
     for r in csv.DictReader(open(f)):
-        k = r['Kernel_Name'].split('(')[0][-40:]
+        k = r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0][-48:]
         agg[k][r['Counter_Name']] += float(r['Counter_Value'])
         disp[k].add(r['Dispatch_Id'])
     print(d)
