@@ -99,7 +99,11 @@ int sb_vcf_scan_file(const char *path, sb_vcf_scan **out);
 int sb_vcf_scan_info(const sb_vcf_scan *s, uint64_t *n_records, uint32_t *n_contigs, const uint32_t **pos);
 int sb_vcf_scan_contig(const sb_vcf_scan *s, uint32_t i, const char **name, size_t *len, uint64_t *lo, uint64_t *hi);
 void sb_vcf_scan_free(sb_vcf_scan *s);
-/* upload to device `device` (HIP ordinal) and return an immutable store */
+/* upload to device `device` (HIP ordinal) and return an immutable store.
+ * device = SB_HOST_ONLY builds every host-side column without a device
+ * image (no HIP call): request planning, region files, CSI/TBI and
+ * sb_store_save work on it; a query or pass returns SB_EHIP. */
+#define SB_HOST_ONLY (-1)
 int sb_builder_finish(sb_builder *b, int device, sb_store **out);
 void sb_builder_free(sb_builder *b);
 void sb_store_close(sb_store *s);

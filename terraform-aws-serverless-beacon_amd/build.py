@@ -72,5 +72,58 @@ def build(verbose: bool = False) -> str:
     return LIB
 
 
+ASAN_DIR = os.path.join(BUILD, 'asan')
+ASAN_LIB = os.path.join(ASAN_DIR, 'libsbeacon_hip_asan.so')
+HOST_SOURCES = ['api.cpp', 'ingest.cpp', 'index.cpp', 'wire.cpp']
+# host code only (-Xarch_host): device code is never instrumented; the kernel
+# objects of build() are linked as they are.  SBEACON_CHECKS turns on the
+# request-plan invariant checks (api.cpp check_request_plan).
+SAN = ['-Xarch_host', '-fsanitize=address', '-Xarch_host', '-fsanitize=undefined', '-Xarch_host',
+       '-fno-sanitize-recover=undefined', '-Xarch_host', '-fno-omit-frame-pointer', '-DSBEACON_CHECKS', '-g1']
+
+
+def asan_runtime() -> str:
+    """The clang AddressSanitizer runtime a Python process preloads to load ASAN_LIB."""
+    import glob
+    hits = sorted(glob.glob('/opt/rocm/lib/llvm/lib/clang/*/lib/*/libclang_rt.asan-x86_64.so') +
+                  glob.glob('/opt/rocm/lib/llvm/lib/clang/*/lib/*/libclang_rt.asan.so'))
+    if not hits:
+        raise RuntimeError('no clang AddressSanitizer runtime under /opt/rocm/lib/llvm')
+    return hits[0]
+
+
+def build_sanitized(verbose: bool = False) -> str:
+    """libsbeacon_hip with its host code under AddressSanitizer + UBSan
+    (tests/test_host_sanitizers.py runs ingest, index writing, request planning
+    and the wire parser through it on the CPU)."""
+    build(verbose)
+    os.makedirs(ASAN_DIR, exist_ok=True)
+    deps = _deps()
+    jobs = []
+    for src in HOST_SOURCES:
+        s = os.path.join(CSRC, src)
+        o = os.path.join(ASAN_DIR, src + '.o')
+        if _stale(o, [s] + deps + [os.path.abspath(__file__)]):
+            jobs.append([HIPCC, '-x', 'hip'] + FLAGS + SAN + ['-c', s, '-o', o])
+
+    def run(cmd):
+        if verbose:
+            print(' '.join(cmd), file=sys.stderr)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode:
+            raise RuntimeError(f'compile failed: {" ".join(cmd)}\n{r.stdout}\n{r.stderr}')
+
+    with ThreadPoolExecutor(max_workers=min(4, max(1, len(jobs)))) as ex:
+        list(ex.map(run, jobs))
+    objs = [os.path.join(ASAN_DIR, s + '.o') for s in HOST_SOURCES] + \
+           [os.path.join(BUILD, s + '.o') for s in SOURCES if s.endswith('.hip')]
+    if _stale(ASAN_LIB, objs):
+        run([HIPCC, f'--offload-arch={ARCH}', '-shared', '-Xarch_host', '-fsanitize=address', '-Xarch_host',
+             '-fsanitize=undefined', '-shared-libasan', '-o', ASAN_LIB] + objs + ['-lz', '-lpthread'])
+    return ASAN_LIB
+
+
 if __name__ == '__main__':
     print(build(verbose=True))
+    if '--sanitized' in sys.argv:
+        print(build_sanitized(verbose=True))

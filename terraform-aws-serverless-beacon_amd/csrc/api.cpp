@@ -66,6 +66,7 @@ int guard(F &&f) {
 
 template <class T>
 T *dev_upload(sb_store &s, const std::vector<T> &v) {
+    if (s.device < 0) return nullptr;  // a host-only store (SB_HOST_ONLY): no device image
     DeviceBuffer b;
     b.bytes = std::max<size_t>(v.size() * sizeof(T), 16);
     HIP_OK(hipMalloc(&b.p, b.bytes));
@@ -169,6 +170,16 @@ const char *last_error_cstr() { return g_last_error.c_str(); }
 }  // namespace sb
 
 using namespace sb;
+
+namespace sb {
+sb_store *store_hold(sb_store *s) {
+    s->holders.fetch_add(1, std::memory_order_acq_rel);
+    return s;
+}
+void store_release(sb_store *s) {
+    if (s->holders.fetch_sub(1, std::memory_order_acq_rel) == 1) delete s;
+}
+}  // namespace sb
 
 sb_store::~sb_store() {
     if (device >= 0) (void)hipSetDevice(device);
@@ -337,6 +348,7 @@ struct sb_batch {
         uint64_t n_chain_slices = 0;
         uint32_t n_lut = 0;            // LUT words (request_eval_kernel stages them in LDS when they fit)
         uint64_t n_chains = 0;         // chain-answered requests (dchains holds them padded per run)
+        uint32_t n_runs = 0;           // runs (runs: their host copy when planned on the host)
         // sb_requests_time_eval: events around every pass's request_eval_kernel
         bool time_eval = false;
         std::vector<std::array<hipEvent_t, 2>> eval_ev;
@@ -351,6 +363,7 @@ struct sb_batch {
         // rows whose counts are not exact in int64 (sb_requests_inexact_rows):
         // per-slice wide marks + one flag per row (batches with general records)
         DevMem wide, row_flag;
+        std::vector<char> hplan;  // host-only stores: the descriptors + runs (as dchains would hold them)
         size_t runs_at = 0;
         uint32_t run = kReqRun;        // chain slots per run (request_eval_kernel: one lane each)
         std::shared_ptr<ReqPool> pool;  // where the device buffers go back when the batch is freed
@@ -381,7 +394,10 @@ struct sb_batch {
 };
 
 struct sb_result_set {
-    sb_store *s = nullptr;
+    sb_store *s = nullptr;  // held (store_hold) while the set lives
+    ~sb_result_set() {
+        if (s) store_release(s);
+    }
     std::vector<QRes> res;
     std::vector<uint64_t> dense_off;
     std::vector<uint64_t> hit;                  // rec | alt << 32
@@ -725,6 +741,16 @@ void upload_store(sb_builder &b, sb_store &s) {
                 }
             }
         }
+        {  // the (segment, kind) indexes and the ALT prefix on the device (request_plan_kernel)
+            std::vector<VcIndex> vcx;
+            for (auto &v : b.vcfs) {
+                v.seg_base = static_cast<uint32_t>(vcx.size() / kVtKinds);
+                for (const auto &a : v.vc_index) vcx.insert(vcx.end(), a.begin(), a.end());
+            }
+            if (vcx.empty()) vcx.resize(kVtKinds);
+            s.d.vcx = dev_upload(s, vcx);
+            s.d.vc_altpre = dev_upload(s, s.h_vc_altpre);
+        }
         s.h_vt_slow.clear();
         for (size_t i = 0; i < n; ++i)
             if (vth[i].w & VT_SLOW) s.h_vt_slow.push_back(static_cast<uint32_t>(i));
@@ -809,7 +835,7 @@ void upload_store(sb_builder &b, sb_store &s) {
     s.dk.rpos = s.d.pos;
     s.dk.bucket = s.d.bucket;
     s.n_keys = dk_hash.size();
-    HIP_OK(hipStreamSynchronize(s.stream));
+    if (s.stream) HIP_OK(hipStreamSynchronize(s.stream));
     s.h_dk_pos = std::move(dk_pos);
     s.h_dk_lo = std::move(dk_lo);
     s.h_dk_bad = std::move(dk_bad);
@@ -1385,6 +1411,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     // (packed symbolic ids are < 255; words past a LUT's end are never consulted)
     lut_all.insert(lut_all.end(), 8, 0u);
     // ---- device buffers
+    if (s.device < 0) return;  // a host-only store: the plan stays on the host
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
     // device query array in launch order (groups back to back, each sorted by
@@ -1564,7 +1591,7 @@ sb_result_set *fetch(sb_batch &B) {
     sb_store &s = *B.s;
     hipStream_t st = B.strm();
     auto R = std::make_unique<sb_result_set>();
-    R->s = &s;
+    R->s = store_hold(&s);
     const uint32_t nq = B.nq;
     R->res.resize(nq);
     if (nq) HIP_OK(hipMemcpyAsync(R->res.data(), B.res.p, nq * sizeof(QRes), hipMemcpyDeviceToHost, st));
@@ -2954,13 +2981,15 @@ int sb_builder_finish(sb_builder *b, int device, sb_store **out) {
     return guard([&] {
         if (!b || !out) throw Error(SB_EINVAL, "NULL argument");
         for (uint32_t i = 0; i < b->vcfs.size(); ++i) builder_flush(*b, i);
-        int n_dev = 0;
-        HIP_OK(hipGetDeviceCount(&n_dev));
-        if (device < 0 || device >= n_dev) throw Error(SB_EHIP, "device ordinal out of range");
         auto s = std::make_unique<sb_store>();
         s->device = device;
-        HIP_OK(hipSetDevice(device));
-        HIP_OK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        if (device != SB_HOST_ONLY) {
+            int n_dev = 0;
+            HIP_OK(hipGetDeviceCount(&n_dev));
+            if (device < 0 || device >= n_dev) throw Error(SB_EHIP, "device ordinal out of range");
+            HIP_OK(hipSetDevice(device));
+            HIP_OK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+        }
         upload_store(*b, *s);
         s->vcfs = std::move(b->vcfs);
         s->vt = std::move(b->vt);
@@ -2975,7 +3004,9 @@ int sb_builder_finish(sb_builder *b, int device, sb_store **out) {
 }
 
 void sb_builder_free(sb_builder *b) { delete b; }
-void sb_store_close(sb_store *s) { delete s; }
+void sb_store_close(sb_store *s) {
+    if (s) store_release(s);
+}
 
 int sb_store_trim(sb_store *s) {
     return guard([&] {
@@ -3172,6 +3203,257 @@ void check_columns(const sb_request_columns &c, size_t n) {
     codes("sample_names", c.sample_names_dict, c.sample_names_code, c.n_sample_names);
 }
 
+// The per-slice part of a request batch: splitQuery's slices of the rows
+// with cls[i] == 2, in row order (split_query_sync,
+// lambda/splitQuery/lambda_function.py:74-110), planned as one slice batch
+// (prepare); seg[w] .. seg[w + 1] = row w's queries.
+template <class Src>
+void slice_part(sb_batch &B, sb_batch::Req &R, const Src &src, size_t n, const std::vector<uint8_t> &cls,
+                std::vector<uint32_t> &seg) {
+    sb_store &s = *B.s;
+    std::vector<sb_query> qs;
+    std::vector<uint32_t> owner;
+    std::deque<std::string> regions;  // stable storage for the region strings
+    for (size_t i = 0; i < n; ++i) {
+        if (cls[i] != 2) continue;
+        const sb_request x = src(i);
+        const std::string &chrom = s.vcfs[x.vcf_id].segments[x.contig].contig;
+        for (int64_t a = x.start_min; a <= x.start_max; a += kSplitSize) {
+            const int64_t b = std::min(a + kSplitSize - 1, x.start_max);
+            regions.push_back(chrom + ":" + std::to_string(a) + "-" + std::to_string(b));
+            sb_query q{};
+            q.vcf_id = x.vcf_id;
+            q.region = regions.back().data();
+            q.region_len = regions.back().size();
+            q.end_min = x.end_min;
+            q.end_max = x.end_max;
+            q.reference_bases = x.reference_bases;
+            q.reference_len = x.reference_len;
+            q.alternate_bases = x.alternate_bases;
+            q.alternate_len = x.alternate_len;
+            q.variant_type = x.variant_type;
+            q.variant_type_len = x.variant_type_len;
+            q.variant_min_length = x.variant_min_length;
+            q.variant_max_length = x.variant_max_length;
+            q.granularity = x.granularity;
+            q.include_details = x.include_details;
+            q.include_samples = x.include_samples;
+            q.selected_samples_only = x.selected_samples_only;
+            q.strict_variant_type = x.strict_variant_type;
+            q.sample_names = x.sample_names;
+            q.sample_names_len = x.sample_names_len;
+            qs.push_back(q);
+            owner.push_back(static_cast<uint32_t>(i));
+            if (a > INT64_MAX - kSplitSize) break;
+        }
+    }
+    B.no_chains = true;
+    if (!qs.empty()) {
+        prepare(B, qs.data(), qs.size());
+        R.slices = true;
+    }
+    seg.assign(n + 1, 0);
+    for (uint32_t o : owner) ++seg[o + 1];
+    for (size_t w = 0; w < n; ++w) seg[w + 1] += seg[w];
+}
+
+// the per-slice part's row table, host errors and (general records) the
+// inexact-row marks on the device
+void upload_slice_part(sb_batch &B, sb_batch::Req &R, const std::vector<uint32_t> &seg, size_t n, hipStream_t st) {
+    if (!R.slices) return;
+    ReqPool &P = *R.pool;
+    std::vector<uint8_t> he(std::max<size_t>(B.nq, 1), 0);
+    for (uint32_t q = 0; q < B.nq; ++q) he[q] = B.host_err[q] ? 1 : 0;
+    R.sseg = P.get_dev(seg.size() * 4);
+    R.sherr = P.get_dev(he.size());
+    if (B.gen_grid) {  // general records can make a row's counts wider than int64
+        R.wide = P.get_dev(std::max<size_t>(B.nq, 1));
+        R.row_flag = P.get_dev(std::max<size_t>(n, 1));
+    }
+    HIP_OK(hipMemcpyAsync(R.sseg.p, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(R.sherr.p, he.data(), he.size(), hipMemcpyHostToDevice, st));
+    HIP_OK(hipStreamSynchronize(st));  // he / seg are freed by the caller
+}
+
+// sb_requests_prepare_columns, planned on the device: when the columns that
+// decide the chain test are batch-wide scalars (one VCF, referenceBases 'N',
+// alternateBases None, include_details, no boolean break, no samples) the
+// host only packs each request into a 32-byte ReqIn (one streaming pass on
+// 16 threads: window, END / length bounds, kind and LUT, class) and
+// request_plan_kernel forms the runs of 64 rows, resolves every chain's
+// candidate range from the coarse index and its hit capacity, and packs the
+// descriptors; request_stage_scan_kernel lays the runs' staging regions end
+// to end.  One readback (chains, slices, staging total) sizes the buffers.
+// Returns false when the columns do not qualify: prepare_requests plans on
+// the host.
+bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n) {
+    sb_store &s = *B.s;
+    if (s.device < 0 || n == 0 || n >= (1u << 31) || c.vcf_id || c.vcf_id_all >= s.vcfs.size()) return false;
+    const VcfData &v = s.vcfs[c.vcf_id_all];
+    auto single = [](const sb_str *d, const uint32_t *code, uint32_t nd) { return d && (!code || nd == 1); };
+    if (!v.nonneg || !single(c.reference_dict, c.reference_code, c.n_reference) ||
+        c.reference_dict[0].len != 1 || !c.reference_dict[0].p || c.reference_dict[0].p[0] != 'N')
+        return false;
+    if (c.alternate_dict && !(single(c.alternate_dict, c.alternate_code, c.n_alternate) && !c.alternate_dict[0].p))
+        return false;
+    if (c.granularity || c.granularity_all == SB_GRAN_BOOLEAN || c.include_details || !c.include_details_all ||
+        c.selected_samples_only || c.selected_samples_only_all || c.include_samples || c.strict_variant_type)
+        return false;
+    const bool collect = (c.granularity_all == SB_GRAN_RECORD || c.granularity_all == SB_GRAN_AGGREGATED) &&
+                         c.include_samples_all;
+    if (collect && v.words) return false;
+    const bool trace = std::getenv("SBEACON_PREP_TRACE") != nullptr;
+    auto t_last = std::chrono::steady_clock::now();
+    auto tick = [&](const char *what) {
+        if (!trace) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[prep-dev] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
+    auto R = std::make_unique<sb_batch::Req>();
+    R->n_rows = static_cast<uint32_t>(n);
+    R->run = kReqRun;
+    R->pool = req_pool(s);
+    ReqPool &P = *R->pool;
+    // variantType dictionary -> (kind, LUT offset)
+    VtResolver V{s, {}, {}};
+    std::vector<std::pair<uint32_t, uint32_t>> tab;
+    if (c.variant_type_dict)
+        for (uint32_t d = 0; d < c.n_variant_type; ++d) tab.push_back(V.get(c.variant_type_dict[d].p, c.variant_type_dict[d].len));
+    else
+        tab.push_back(V.get(nullptr, 0));
+    std::vector<uint32_t> &lut_all = V.lut_all;
+    lut_all.insert(lut_all.end(), 8, 0u);
+    // pack
+    const uint32_t vid = c.vcf_id_all;
+    const auto &slow_pos = s.seg_slow_pos[vid];
+    ReqPool::Pinned pin = P.get_pinned(n * sizeof(ReqIn));
+    ReqIn *pk = static_cast<ReqIn *>(pin.p);
+    std::vector<uint8_t> cls(n, 0);
+    std::atomic<bool> any_slices{false};
+    parallel_for(n, [&](size_t i) {
+        const uint32_t contig = c.contig ? c.contig[i] : c.contig_all;
+        const int64_t smin = c.start_min[i], smax = c.start_max[i];
+        ReqIn o{0, 0, 0, 0, 0, 0, 0, REQ_NONE};
+        if (contig < v.segments.size() && smin <= smax) {  // else bcftools emits nothing / no slice
+            const int64_t nsl = (smax - smin) / kSplitSize + 1;
+            bool chain = smin >= 1 && smax <= 0xfffffffell && nsl <= kReqChainSlices;
+            if (chain && !slow_pos[contig].empty()) {  // a VT_SLOW / general record in the window: per slice
+                const auto &sp = slow_pos[contig];
+                auto a = std::lower_bound(sp.begin(), sp.end(), static_cast<uint32_t>(smin));
+                if (a != sp.end() && *a <= static_cast<uint64_t>(smax)) chain = false;
+            }
+            if (!chain) {
+                o.cls = REQ_SLICES;
+                cls[i] = 2;
+                any_slices.store(true, std::memory_order_relaxed);
+            } else {
+                const int64_t emin = c.end_min ? c.end_min[i] : c.end_min_all, emax = c.end_max ? c.end_max[i] : c.end_max_all;
+                const bool end_void = emax < 0 || emin > 0xffffffffll || emin > emax;
+                o.first = static_cast<uint32_t>(smin);
+                o.last = static_cast<uint32_t>(smax);
+                o.e0 = emin < 0 ? 0u : static_cast<uint32_t>(emin);
+                o.espan = (emax > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(emax)) - o.e0;
+                const int64_t vmin = c.variant_min_length ? c.variant_min_length[i] : c.variant_min_length_all;
+                const int64_t vmax0 = c.variant_max_length ? c.variant_max_length[i] : c.variant_max_length_all;
+                const int64_t vmax = vmax0 < 0 ? INT64_MAX : vmax0;
+                const int64_t vl = vmin < 0 ? 0 : vmin, vh = vmax > 255 ? 255 : vmax;
+                const auto &kl = tab[c.variant_type_dict && c.variant_type_code ? c.variant_type_code[i] : 0u];
+                o.bits = req_bits(vh < vl ? 256u : static_cast<uint32_t>(vl), vh < vl ? 0u : static_cast<uint32_t>(vh - vl),
+                                  0u, kl.first, end_void);
+                o.seg = v.seg_base + contig;
+                o.lut_off = kl.second;
+                o.cls = REQ_CHAIN | static_cast<uint32_t>(nsl) << 2;
+            }
+        }
+        pk[i] = o;
+    });
+    tick("pack");
+    std::vector<uint32_t> seg;
+    if (any_slices.load()) slice_part(B, *R, ColSrc{c}, n, cls, seg);
+    tick("slices");
+    HIP_OK(hipSetDevice(s.device));
+    hipStream_t st = s.stream;
+    const uint32_t n_runs = static_cast<uint32_t>((n + kRunRows - 1) / kRunRows);
+    const size_t chain_bytes = size_t(n_runs) * kReqRun * sizeof(ReqChain), run_bytes = size_t(n_runs) * sizeof(RowRun);
+    DevMem din = P.get_dev(n * sizeof(ReqIn)), rc = P.get_dev(size_t(n_runs) * 8 + 32);
+    R->dchains = P.get_dev(chain_bytes + run_bytes);
+    R->runs_at = chain_bytes;
+    R->n_runs = n_runs;
+    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(rc.as<char>() + size_t(n_runs) * 8);
+    HIP_OK(hipMemcpyAsync(din.p, pk, n * sizeof(ReqIn), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemsetAsync(cnt, 0, 32, st));
+    launch_request_plan(s.d, din.as<ReqIn>(), static_cast<uint32_t>(n), R->dchains.as<ReqChain>(),
+                        reinterpret_cast<RowRun *>(R->dchains.as<char>() + chain_bytes), rc.as<unsigned long long>(),
+                        cnt, st);
+    HIP_OK(hipGetLastError());
+    unsigned long long *hc = reinterpret_cast<unsigned long long *>(static_cast<char *>(pin.p));
+    HIP_OK(hipStreamSynchronize(st));  // the packed requests are consumed: the pinned buffer carries the counters back
+    HIP_OK(hipMemcpyAsync(hc, cnt, 24, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    R->n_chains = hc[0];
+    R->n_chain_slices = hc[1];
+    const uint64_t stage_total = hc[2];
+    tick("plan");
+    P.put_pinned(pin);
+    P.put_dev(std::move(din));
+    P.put_dev(std::move(rc));
+    R->cap = B.cap_total + stage_total;
+    R->status = P.get_dev(size_t(n_runs) * 8);
+    R->tstatus = P.get_dev(size_t(request_tiles(n_runs)) * 8);
+    R->stage = P.get_dev(stage_total * 8);
+    R->row_src = P.get_dev(R->slices ? n * 8 : 0);
+    R->lut = P.get_dev(lut_all.size() * 4);
+    R->n_lut = static_cast<uint32_t>(lut_all.size());
+    HIP_OK(hipMemcpyAsync(R->lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
+    upload_slice_part(B, *R, seg, n, st);
+    HIP_OK(hipStreamSynchronize(st));
+    tick("upload");
+    B.req = std::move(R);
+    return true;
+}
+
+#ifdef SBEACON_CHECKS
+// Plan invariants (the sanitizer build, tests/test_host_sanitizers.py): a
+// run's slots hold its chain rows once each (those with candidates first,
+// each row field inside the run, each range the one planned for the row and
+// inside the (segment, kind) pair's candidates); the staging regions are laid
+// end to end and each covers every ALT of its chains' ranges.
+void check_request_plan(const sb_store &s, const sb_batch::Req &R, const ReqChain *hc, const std::vector<uint8_t> &cls,
+                        const std::vector<uint32_t> &clo, const std::vector<uint32_t> &chi, size_t n) {
+    auto fail = [](const std::string &m) { throw Error(SB_EINVAL, "request plan check: " + m); };
+    uint64_t stage = 0, chains = 0;
+    const uint64_t n_cand = s.h_vc_altpre.empty() ? 0 : s.h_vc_altpre.size() - 1;
+    for (size_t r = 0; r < R.runs.size(); ++r) {
+        const RowRun &run = R.runs[r];
+        if (run.row_hi <= run.row_lo || run.row_hi - run.row_lo > kRunRows || run.row_hi > n) fail("run rows");
+        if (run.stage != stage) fail("staging regions not end to end");
+        std::vector<uint8_t> seen(kRunRows, 0);
+        uint64_t cap = 0;
+        bool empty_seen = false;
+        uint32_t j = 0;
+        for (; j < R.run; ++j) {
+            const ReqChain &c = hc[r * R.run + j];
+            if (c.first == 0) break;
+            const uint32_t row = (c.bits >> 17) & 63u;
+            if (run.row_lo + row >= run.row_hi || seen[row]++ || cls[run.row_lo + row] != 1) fail("slot row");
+            const size_t i = run.row_lo + row;
+            if (c.c_lo != clo[i] || c.c_hi != chi[i] || c.c_hi < c.c_lo || c.c_hi > n_cand) fail("slot range");
+            if (c.c_hi > c.c_lo && empty_seen) fail("a chain with candidates after an empty one");
+            empty_seen |= c.c_hi == c.c_lo;
+            cap += s.h_vc_altpre[c.c_hi] - s.h_vc_altpre[c.c_lo];
+            ++chains;
+        }
+        for (uint32_t k = j; k < R.run; ++k)
+            if (hc[r * R.run + k].first != 0) fail("a used slot after an empty one");
+        for (uint32_t i = run.row_lo; i < run.row_hi; ++i)
+            if (cls[i] == 1 && !seen[i - run.row_lo]) fail("a chain row without a slot");
+        stage += cap;
+    }
+    if (chains != R.n_chains) fail("chain count");
+}
+#endif
+
 template <class Src>
 void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     sb_store &s = *B.s;
@@ -3247,52 +3529,9 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     }
     tick("classify");
     // the per-slice part: splitQuery's slices of the other requests, in row order
-    std::vector<sb_query> qs;
-    std::vector<uint32_t> owner;
-    std::deque<std::string> regions;  // stable storage for the region strings
-    for (size_t i = 0; i < n; ++i) {
-        if (cls[i] != 2) continue;
-        const sb_request x = src(i);
-        const std::string &chrom = s.vcfs[x.vcf_id].segments[x.contig].contig;
-        for (int64_t a = x.start_min; a <= x.start_max; a += kSplitSize) {
-            const int64_t b = std::min(a + kSplitSize - 1, x.start_max);
-            regions.push_back(chrom + ":" + std::to_string(a) + "-" + std::to_string(b));
-            sb_query q{};
-            q.vcf_id = x.vcf_id;
-            q.region = regions.back().data();
-            q.region_len = regions.back().size();
-            q.end_min = x.end_min;
-            q.end_max = x.end_max;
-            q.reference_bases = x.reference_bases;
-            q.reference_len = x.reference_len;
-            q.alternate_bases = x.alternate_bases;
-            q.alternate_len = x.alternate_len;
-            q.variant_type = x.variant_type;
-            q.variant_type_len = x.variant_type_len;
-            q.variant_min_length = x.variant_min_length;
-            q.variant_max_length = x.variant_max_length;
-            q.granularity = x.granularity;
-            q.include_details = x.include_details;
-            q.include_samples = x.include_samples;
-            q.selected_samples_only = x.selected_samples_only;
-            q.strict_variant_type = x.strict_variant_type;
-            q.sample_names = x.sample_names;
-            q.sample_names_len = x.sample_names_len;
-            qs.push_back(q);
-            owner.push_back(static_cast<uint32_t>(i));
-            if (a > INT64_MAX - kSplitSize) break;
-        }
-    }
-    B.no_chains = true;
-    if (!qs.empty()) {
-        prepare(B, qs.data(), qs.size());
-        R->slices = true;
-    }
+    std::vector<uint32_t> seg;
+    slice_part(B, *R, src, n, cls, seg);
     tick("slices");
-    // rows -> their per-slice queries, host errors
-    std::vector<uint32_t> seg(n + 1, 0);
-    for (uint32_t o : owner) ++seg[o + 1];
-    for (size_t w = 0; w < n; ++w) seg[w + 1] += seg[w];
     // runs of consecutive rows (<= kRunRows rows, R->run chains, every chain
     // starting below position kReqStartPos of the run's candidates), formed
     // greedily in blocks of rows on several threads (a block boundary also
@@ -3358,7 +3597,12 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     const size_t n_runs = R->runs.size(), slots = run_max;
     const size_t chain_bytes = n_runs * slots * sizeof(ReqChain), run_bytes = n_runs * sizeof(RowRun);
     R->pool = req_pool(s);
-    ReqPool::Pinned pin = R->pool->get_pinned(chain_bytes + run_bytes);
+    const bool host_only = s.device < 0;
+    ReqPool::Pinned pin = host_only ? ReqPool::Pinned{} : R->pool->get_pinned(chain_bytes + run_bytes);
+    if (host_only) {  // no device: the plan is kept in host memory (R->hplan)
+        R->hplan.resize(chain_bytes + run_bytes);
+        pin.p = R->hplan.data();
+    }
     ReqChain *hc = static_cast<ReqChain *>(pin.p);
     RowRun *hr = reinterpret_cast<RowRun *>(static_cast<char *>(pin.p) + chain_bytes);
     std::vector<uint64_t> rcap(n_runs, 0);  // each run's hit capacity (staging slots)
@@ -3400,7 +3644,16 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     }
     std::memcpy(static_cast<void *>(hr), R->runs.data(), run_bytes);
     R->cap = B.cap_total + stage_total;
+    R->n_runs = static_cast<uint32_t>(n_runs);
+    R->runs_at = chain_bytes;
     tick("chains");
+#ifdef SBEACON_CHECKS
+    check_request_plan(s, *R, hc, cls, clo_of, chi_of, n);
+#endif
+    if (host_only) {
+        B.req = std::move(R);
+        return;
+    }
     // device buffers (pooled per store: a batch returns them when freed)
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
@@ -3418,19 +3671,9 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
         HIP_OK(hipMemcpyAsync(R->dchains.p, pin.p, chain_bytes + run_bytes, hipMemcpyHostToDevice, st));
     R->runs_at = chain_bytes;
     HIP_OK(hipMemcpyAsync(R->lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
-    if (R->slices) {
-        std::vector<uint8_t> he(std::max<size_t>(B.nq, 1), 0);
-        for (uint32_t q = 0; q < B.nq; ++q) he[q] = B.host_err[q] ? 1 : 0;
-        R->sseg = P.get_dev(seg.size() * 4);
-        R->sherr = P.get_dev(he.size());
-        if (B.gen_grid) {  // general records can make a row's counts wider than int64
-            R->wide = P.get_dev(std::max<size_t>(B.nq, 1));
-            R->row_flag = P.get_dev(std::max<size_t>(n, 1));
-        }
-        HIP_OK(hipMemcpyAsync(R->sseg.p, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemcpyAsync(R->sherr.p, he.data(), he.size(), hipMemcpyHostToDevice, st));
-    }
+    upload_slice_part(B, *R, seg, n, st);
     HIP_OK(hipStreamSynchronize(st));
+    R->n_runs = static_cast<uint32_t>(n_runs);
     P.put_pinned(pin);
     tick("upload");
     B.req = std::move(R);
@@ -3441,6 +3684,7 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
 void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t rec_base) {
     sb_store &s = *B.s;
     sb_batch::Req &R = *B.req;
+    if (s.device < 0) throw Error(SB_EHIP, "the store has no device image (SB_HOST_ONLY)");
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = B.strm();
     mark_run(B);
@@ -3465,7 +3709,7 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
         ev = R.eval_ev[R.eval_used++];
     }
     launch_request_rows(d, R.dchains.as<ReqChain>(), reinterpret_cast<const RowRun *>(R.dchains.as<char>() + R.runs_at),
-                        static_cast<uint32_t>(R.runs.size()),
+                        R.n_runs,
                         R.status.as<unsigned long long>(), R.tstatus.as<unsigned long long>(),
                         R.slices ? B.res.as<QRes>() : nullptr,
                         R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
@@ -3486,6 +3730,7 @@ int sb_requests_prepare(sb_store *s, const sb_request *r, size_t n, sb_batch **o
         auto B = std::make_unique<sb_batch>();
         B->s = s;
         prepare_requests(*B, AosSrc{r}, n);
+        store_hold(s);
         *out = B.release();
     });
 }
@@ -3498,7 +3743,8 @@ int sb_requests_prepare_columns(sb_store *s, const sb_request_columns *c, size_t
         check_columns(cc, n);
         auto B = std::make_unique<sb_batch>();
         B->s = s;
-        prepare_requests(*B, ColSrc{cc}, n);
+        if (!prepare_requests_device(*B, cc, n)) prepare_requests(*B, ColSrc{cc}, n);
+        store_hold(s);
         *out = B.release();
     });
 }
@@ -3546,6 +3792,7 @@ int sb_batch_prepare(sb_store *s, const sb_query *q, size_t nq, sb_batch **out) 
         auto B = std::make_unique<sb_batch>();
         B->s = s;
         prepare(*B, q, nq);
+        store_hold(s);
         *out = B.release();
     });
 }
@@ -3791,8 +4038,10 @@ int sb_batch_fetch(sb_batch *b, sb_result_set **out) {
 
 void sb_batch_free(sb_batch *b) {
     if (!b) return;
-    (void)hipSetDevice(b->s->device);
+    sb_store *s = b->s;
+    if (s->device >= 0) (void)hipSetDevice(s->device);
     delete b;
+    store_release(s);  // every batch handed out holds its store
 }
 
 int sb_query_batch(sb_store *s, const sb_query *q, size_t nq, uint32_t flags, sb_result_set **out) {

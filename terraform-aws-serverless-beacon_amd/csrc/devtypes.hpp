@@ -190,6 +190,21 @@ struct alignas(16) VcBlock {
 // constants vt_slice derives from its QDev (VtPred), so a wave reads nothing
 // else before the index.
 constexpr uint32_t kChainMax = 32;
+// coarse POS index of the variantType candidates of one (segment, kind):
+// vc_bucket[off + b] = first candidate with POS >= base + (b << shift), b <= n
+// (host planning, and DStore::vcx for request planning on the device)
+struct VcIndex {
+    uint64_t off = 0;
+    uint32_t base = 0, shift = 31, n = 1;
+    uint32_t c_lo = 0, c_hi = 0;  // the pair's candidates in the kind's list
+};
+// first candidate of the pair with POS >= x (up = 0), or the end of the
+// bucket holding x - 1 (up = 1: a bound >= the exact upper bound of x - 1)
+__host__ __device__ inline uint32_t vc_bound(const VcIndex &vi, const uint32_t *bucket, uint64_t x, uint32_t up) {
+    if (x <= vi.base) return vi.c_lo;
+    const uint64_t b = (x - vi.base) >> vi.shift;
+    return b >= vi.n ? vi.c_hi : bucket[vi.off + b + up];
+}
 struct alignas(16) ChainDev {
     uint32_t s0;        // first slice in the chain-ordered arrays (chain_orig)
     uint32_t n;         // slices, 1 .. kChainMax
@@ -253,6 +268,22 @@ static_assert(sizeof(ReqChain) == 32, "ReqChain is two 16-byte words");
 __host__ __device__ constexpr uint32_t req_bits(uint32_t vlo, uint32_t vspan, uint32_t row, uint32_t kind, bool end_void) {
     return vlo | vspan << 9 | row << 17 | kind << 23 | (end_void ? 1u << 26 : 0u);
 }
+
+// One request as the host packs it for planning on the device
+// (sb_requests_prepare_columns when every varying column is numeric): the
+// ReqChain fields that do not depend on the store, its store-wide segment
+// and its class.  request_plan_kernel turns a run of 64 of them into the
+// run's ReqChain slots and RowRun.
+enum : uint32_t { REQ_CHAIN = 0, REQ_NONE = 1, REQ_SLICES = 2 };
+struct alignas(16) ReqIn {
+    uint32_t first, last;  // start_min, start_max (REQ_CHAIN: 1 <= first <= last <= 0xfffffffe)
+    uint32_t e0, espan;    // END in [e0, e0 + espan]
+    uint32_t bits;         // req_bits(vlo, vspan, 0, kind, end_void)
+    uint32_t seg;          // store-wide segment (DStore::vcx row)
+    uint32_t lut_off;      // symbolic-ALT LUT of the variantType
+    uint32_t cls;          // REQ_* | slices << 2
+};
+static_assert(sizeof(ReqIn) == 32, "ReqIn is two 16-byte words");
 
 // bit c set = an ALT of class c satisfies variantType `kind` (vtype_hit)
 __host__ __device__ constexpr uint32_t vt_class_mask(uint32_t kind) {
@@ -332,6 +363,8 @@ struct DStore {
     uint64_t vc_nblk;
     const uint32_t *vc_pos;   // POS of each candidate (parallel to vc_word)
     const uint32_t *vc_bucket;  // coarse POS index per (kind, segment) over candidates (ChainDev)
+    const VcIndex *vcx;         // [segment (store-wide) * kVtKinds + kind]: the pair's coarse index
+    const uint64_t *vc_altpre;  // ALTs of candidates [0, j) (a chain's hit capacity)
     const uint32_t *pos;
     const uint64_t *ref_key;  // key(REF.upper())
     const uint64_t *a0_key;   // key(ALT0.upper())

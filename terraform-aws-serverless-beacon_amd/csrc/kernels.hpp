@@ -116,6 +116,12 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                          hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
 // chain slots per run (kReqRun)
 uint32_t req_run_max();
+// Request planning on the device: rows in runs of kRunRows (n_runs =
+// ceil(n / 64)); chains gets kReqRun ReqChain slots per run, runs the RowRuns
+// with staging offsets, rcap one word per run; counters (3 words, zeroed by
+// the caller) = chain rows, their slices, the staging total.
+void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,
+                         unsigned long long *rcap, unsigned long long *counters, hipStream_t s);
 uint32_t request_tiles(uint32_t n_runs);
 
 // Fetch-time gather of every query's hits into one dense array.

@@ -2254,6 +2254,85 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     if (ul == 0) status[w] = H;  // read by the tile scan and request_deliver_kernel (kernel boundaries)
 }
 
+// ---- request planning on the device (sb_requests_prepare_columns)
+// request_plan_kernel: one wave per run of 64 consecutive rows (row = lane).
+// A chain row's candidate range is read from its (segment, kind) coarse
+// index -- two bucket entries, the batched lower / upper bound of
+// splitQuery's window -- and its hit capacity from the candidates' ALT
+// prefix; the run's chains are packed into its 64 slots (rows with
+// candidates first, in row order, then those without; first == 0 after),
+// its capacity summed for request_stage_scan_kernel.  Rows answered per
+// slice (REQ_SLICES) make the run non-simple; REQ_NONE rows have no slice.
+__global__ __launch_bounds__(kBlock) void request_plan_kernel(DStore st, const ReqIn *__restrict__ in, uint32_t n,
+                                                              uint32_t n_runs, ReqChain *__restrict__ chains,
+                                                              RowRun *__restrict__ runs,
+                                                              unsigned long long *__restrict__ rcap,
+                                                              unsigned long long *__restrict__ counters) {
+    const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
+    if (w >= n_runs) return;
+    const uint32_t ul = static_cast<uint32_t>(lane_id());
+    const uint32_t row = w * kRunRows + ul;
+    ReqIn q{};
+    if (row < n) q = in[row];
+    const uint32_t cls = row < n ? (q.cls & 3u) : static_cast<uint32_t>(REQ_NONE);
+    const bool chain = cls == REQ_CHAIN;
+    uint32_t c0 = 0, c1 = 0;
+    uint64_t cap = 0;
+    if (chain) {
+        const VcIndex vi = st.vcx[static_cast<uint64_t>(q.seg) * kVtKinds + ((q.bits >> 23) & 7u)];
+        c0 = vc_bound(vi, st.vc_bucket, q.first, 0);
+        c1 = (q.bits >> 26) & 1u ? c0 : max(c0, vc_bound(vi, st.vc_bucket, static_cast<uint64_t>(q.last) + 1, 1));
+        cap = st.vc_altpre[c1] - st.vc_altpre[c0];
+    }
+    const bool ne = chain && c1 > c0;
+    const uint64_t mne = __ballot(ne), mem = __ballot(chain && !ne);
+    const uint32_t nne = static_cast<uint32_t>(__popcll(mne)), nslots = nne + static_cast<uint32_t>(__popcll(mem));
+    ReqChain *out = chains + static_cast<uint64_t>(w) * kReqRun;
+    if (chain) {
+        const uint32_t slot = ne ? popc_below(mne) : nne + popc_below(mem);
+        out[slot] = ReqChain{q.first, q.last, c0, c1, q.e0, q.espan, q.bits | (ul << 17), q.lut_off};
+    }
+    if (ul >= nslots) out[ul] = ReqChain{0, 0, 0, 0, 0, 0, 0, 0};  // the unused slots (first == 0)
+    const uint64_t capsum = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(cap)), kWave - 1));
+    const uint32_t nsl = chain ? q.cls >> 2 : 0u;
+    const uint32_t slsum = rdl(incl_sum_u32(nsl), kWave - 1);
+    const bool simple = __ballot(cls == REQ_SLICES) == 0;
+    if (ul == 0) {
+        runs[w] = RowRun{w * kRunRows, min(w * kRunRows + kRunRows, n), 0u, nslots, 0ull, slsum,
+                         simple ? kRunSimple : 0u};
+        rcap[w] = capsum;
+        atomicAdd(&counters[0], static_cast<unsigned long long>(__popcll(mne | mem)));
+        atomicAdd(&counters[1], static_cast<unsigned long long>(slsum));
+    }
+}
+
+// request_stage_scan_kernel (one workgroup): each run's staging offset =
+// the exclusive prefix of the runs' capacities; counters[2] = the total
+__global__ __launch_bounds__(1024) void request_stage_scan_kernel(RowRun *__restrict__ runs,
+                                                                  const unsigned long long *__restrict__ rcap,
+                                                                  uint32_t n_runs,
+                                                                  unsigned long long *__restrict__ counters) {
+    __shared__ unsigned long long wsum[16];
+    __shared__ unsigned long long carry_s;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
+    if (tid == 0) carry_s = 0;
+    __syncthreads();
+    for (uint32_t base = 0; base < n_runs; base += 1024) {
+        const uint32_t i = base + tid;
+        const uint64_t v = i < n_runs ? rcap[i] : 0ull;
+        const uint64_t incl = incl_sum_u64(v);
+        if (lane_id() == kWave - 1) wsum[wave] = incl;
+        __syncthreads();
+        uint64_t before = carry_s;
+        for (uint32_t k = 0; k < wave; ++k) before += wsum[k];
+        if (i < n_runs) runs[i].stage = before + incl - v;
+        __syncthreads();
+        if (tid == 1023) carry_s = before + incl;
+        __syncthreads();
+    }
+    if (tid == 0) counters[2] = carry_s;
+}
+
 // request_tile_scan_kernel: one workgroup adds up each tile's run totals
 // (tiles of kDeliverTile runs) and scans them into exclusive tile offsets.
 // A thread takes two adjacent tiles per round (2,048 tiles: 32 k runs, 1 M
@@ -3570,6 +3649,15 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
     hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, status, n_runs, tstatus, n_tiles);
     hipLaunchKernelGGL(request_deliver_kernel, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg,
                        shoff, sherr, shits, row_off, row_src, stage, out, n_rows, rec_base);
+}
+
+void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,
+                         unsigned long long *rcap, unsigned long long *counters, hipStream_t s) {
+    const uint32_t n_runs = (n + kRunRows - 1) / kRunRows;
+    if (!n_runs) return;
+    hipLaunchKernelGGL(request_plan_kernel, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, in, n, n_runs, chains,
+                       runs, rcap, counters);
+    hipLaunchKernelGGL(request_stage_scan_kernel, dim3(1), dim3(1024), 0, s, runs, rcap, n_runs, counters);
 }
 
 // run totals (request_eval_kernel) -> tile offsets (request_tile_scan_kernel)

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <atomic>
 #include <cstdint>
 #include <memory>
 #include <mutex>
@@ -71,14 +72,6 @@ struct BucketIndex {  // coarse POS index of one segment
     uint32_t n = 0;      // buckets; bucket[off + n] = segment end
 };
 
-// coarse POS index of the variantType candidates of one (segment, kind):
-// vc_bucket[off + b] = first candidate with POS >= base + (b << shift), b <= n
-struct VcIndex {
-    uint64_t off = 0;
-    uint32_t base = 0, shift = 31, n = 1;
-    uint32_t c_lo = 0, c_hi = 0;  // the pair's candidates in the kind's list
-};
-
 struct VcfData {
     std::string location;
     // shard builds (sb_builder_set_record_range): keep records [rec_lo, rec_hi) of the file
@@ -92,6 +85,7 @@ struct VcfData {
     std::unordered_map<std::string, uint32_t> seg_index;
     std::vector<BucketIndex> buckets;  // parallel to segments (set by finish)
     std::vector<std::array<VcIndex, kVtKinds>> vc_index;  // parallel to segments (set by finish)
+    uint32_t seg_base = 0;  // store-wide index of segment 0 (DStore::vcx rows)
     VcfCols c;
     std::string carry;  // partial line kept between add_text calls
     uint64_t stream_off = 0;  // text bytes consumed so far (incl. carry)
@@ -147,6 +141,9 @@ struct sb_builder {
 };
 
 struct sb_store {
+    // the open handle + every live batch and result set (sb_store_close
+    // defers the teardown until the last of them is freed)
+    std::atomic<uint32_t> holders{1};
     int device = 0;
     hipStream_t stream = nullptr;
     std::mutex mu;  // serialises batches on this device

@@ -295,3 +295,58 @@ def test_request_batches_concurrent_streams():
     for t in range(4):
         for x, y in zip(got[t], expect[t]):
             np.testing.assert_array_equal(x, y)
+
+
+def test_device_planned_requests_match_host_planned():
+    """sb_requests_prepare_columns with batch-wide scalar filters plans on the
+    device (request_plan_kernel: runs of 64 rows, candidate ranges from the
+    coarse index); the same requests as an sb_request array plan on the host.
+    Wide requests (up to 5 Mb, hundreds of slices) put more than 4 k
+    candidates into some runs (chain starts found past the start bitmap).
+    Both must give identical rows, offsets and hit lists."""
+    from sbeacon.genome import (CONTIGS, LOCATION, VARIANT_TYPES, GenomeShape, Requests, config3_requests,
+                                prepare_shard_requests, shard_requests)
+    from sbeacon.requests import RequestBatch, requests_array
+    shape = GenomeShape(n_total=240_000, seed=3, n_samples=0)
+    base = config3_requests(shape, n=3000, seed=77)
+    rng = np.random.default_rng(5)
+    width = base.width.copy()
+    wide = rng.random(len(width)) < 0.1  # 1 - 250 Mb: up to ~25 k slices
+    width[wide] = rng.integers(1_000_000, 250_000_000, int(wide.sum()))
+    # 192 requests over the whole of contig 1, first in (contig, start)
+    # order: three runs of 64 whole-contig chains, each well past the
+    # chain-start bitmap's 4 k candidate positions
+    k = 192
+    ci = np.concatenate([np.zeros(k, dtype=base.ci.dtype), base.ci])
+    start = np.concatenate([np.arange(k, dtype=base.start.dtype), base.start])
+    width = np.concatenate([np.full(k, 248_000_000, dtype=width.dtype), width])
+    vt = np.concatenate([rng.integers(0, len(VARIANT_TYPES), k).astype(base.vt.dtype), base.vt])
+    vmin = np.concatenate([np.zeros(k, dtype=base.vmin.dtype), base.vmin])
+    vmax = np.concatenate([np.full(k, -1, dtype=base.vmax.dtype), base.vmax])
+    order = np.lexsort((start, ci))
+    reqs = Requests(ci[order], start[order], width[order], vt[order], vmin[order], vmax[order])
+    store = shape.build_shard_store(1, 0, device=0)
+    sr = shard_requests(shape, reqs, 1, 0)
+    dev_b = prepare_shard_requests(store, sr)  # scalar filters: planned on the device
+    names = store.contigs(LOCATION)
+    at = {c: i for i, c in enumerate(names)}
+    cmap = np.array([at.get(c, 0xffffffff) for c in CONTIGS], dtype=np.uint32)
+    arr, keep = requests_array(
+        sr.n_rows, vcf_id=store.vcf_id(LOCATION), contig=cmap[sr.ci], start_min=sr.start_min,
+        start_max=sr.start_max, end_min=sr.end_min, end_max=sr.end_max, reference=('N',), alternate=(None,),
+        variant_type=VARIANT_TYPES, variant_type_code=sr.vt, variant_min_length=sr.vmin,
+        variant_max_length=sr.vmax, granularity='record', include_details=1)
+    host_b = RequestBatch(store, arr, sr.n_rows)
+    sd, sh = dev_b.stats(), host_b.stats()
+    assert sd['chains'] == sh['chains'] > 0
+    assert sd['hits'] == sh['hits']  # the same staging capacity, however the runs are cut
+    rows_d, hits_d, ro_d = dev_b.answer()
+    rows_h, hits_h, ro_h = host_b.answer()
+    np.testing.assert_array_equal(rows_d, rows_h)
+    np.testing.assert_array_equal(ro_d, ro_h)
+    np.testing.assert_array_equal(hits_d, hits_h)
+    # the first runs of 64 rows (device plan) stage more than 4 k hits, so
+    # their candidates run past the chain-start bitmap's 4 k positions
+    runs = np.add.reduceat(rows_d[:, 1], np.arange(0, len(rows_d), 64))
+    assert runs[:3].min() > 4096, runs[:3]
+    del keep, dev_b, host_b
