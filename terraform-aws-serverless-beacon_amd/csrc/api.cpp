@@ -3337,7 +3337,8 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n)
         ReqIn o{0, 0, 0, 0, 0, 0, 0, REQ_NONE};
         if (contig < v.segments.size() && smin <= smax) {  // else bcftools emits nothing / no slice
             const int64_t nsl = (smax - smin) / kSplitSize + 1;
-            bool chain = smin >= 1 && smax <= 0xfffffffell && nsl <= kReqChainSlices;
+            const auto &kl = tab[c.variant_type_dict && c.variant_type_code ? c.variant_type_code[i] : 0u];
+            bool chain = smin >= 1 && smax <= 0xfffffffell && nsl <= kReqChainSlices && kl.second < kReqLutMax;
             if (chain && !slow_pos[contig].empty()) {  // a VT_SLOW / general record in the window: per slice
                 const auto &sp = slow_pos[contig];
                 auto a = std::lower_bound(sp.begin(), sp.end(), static_cast<uint32_t>(smin));
@@ -3358,7 +3359,6 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n)
                 const int64_t vmax0 = c.variant_max_length ? c.variant_max_length[i] : c.variant_max_length_all;
                 const int64_t vmax = vmax0 < 0 ? INT64_MAX : vmax0;
                 const int64_t vl = vmin < 0 ? 0 : vmin, vh = vmax > 255 ? 255 : vmax;
-                const auto &kl = tab[c.variant_type_dict && c.variant_type_code ? c.variant_type_code[i] : 0u];
                 o.bits = req_bits(vh < vl ? 256u : static_cast<uint32_t>(vl), vh < vl ? 0u : static_cast<uint32_t>(vh - vl),
                                   0u, kl.first, end_void);
                 o.seg = v.seg_base + contig;
@@ -3497,7 +3497,7 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
         bool chain = !x.alternate_bases && x.reference_bases && x.reference_len == 1 && x.reference_bases[0] == 'N' &&
                      x.include_details && x.granularity != SB_GRAN_BOOLEAN && !x.selected_samples_only &&
                      !x.strict_variant_type && !(collect && v.words) && v.nonneg && nsl <= kReqChainSlices &&
-                     x.start_min >= 1 && x.start_max <= 0xfffffffell;
+                     x.start_min >= 1 && x.start_max <= 0xfffffffell && lut_of[i] < kReqLutMax;
         if (chain) {  // a VT_SLOW / general record in the window: per slice
             const auto &sp = s.seg_slow_pos[x.vcf_id][x.contig];
             auto a = std::lower_bound(sp.begin(), sp.end(), static_cast<uint32_t>(x.start_min));

@@ -257,6 +257,10 @@ constexpr uint32_t kReqStartChunks = 64;
 // slices of one request chain at most (slice keys of request_eval_kernel are
 // chain << 20 | slice)
 constexpr uint32_t kReqChainSlices = (1u << 20) - 1;
+// LUT offsets a chain can carry (request_eval_kernel packs the offset into
+// 15 bits): a request whose variantType string's LUT lies past it is
+// answered per slice (only batches with > 4 k distinct variantType strings)
+constexpr uint32_t kReqLutMax = 1u << 15;
 struct alignas(16) ReqChain {
     uint32_t first, last;  // the request's [start_min, start_max] (first >= 1)
     uint32_t c_lo, c_hi;   // candidate range (host-resolved from the coarse index)

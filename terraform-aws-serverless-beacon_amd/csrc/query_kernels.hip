@@ -1986,7 +1986,7 @@ __device__ __forceinline__ uint64_t bperm64(uint64_t v, uint32_t lane) {
 
 struct ReqLds {
     uint4 a[kReqRun];  // chain k: {candidate index - run position, first, last - first, e0}
-    uint4 b[kReqRun];  // {espan, vlo | vspan << 9, class mask | kind << 24, LUT offset}
+    uint4 b[kReqRun];  // {espan, vlo | vspan << 9 | LUT offset << 17, class mask, extra-ALT bits that may match}
     unsigned long long wch[kReqStartChunks];  // chunk c: bit j = a chain's first position is 64 c + j
     unsigned int slow[kReqRun / 32];          // bit = a VT_SLOW candidate in the chain's window
     uint8_t rowchain[kRunRows];               // row (run-relative) -> its chain (0xff: not a chain row)
@@ -2006,18 +2006,23 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     __shared__ uint32_t slut[LDS_LUT ? kReqLut : 1];
     ReqLds &L = lds_all[threadIdx.x >> 6];
     const uint32_t ul = static_cast<uint32_t>(lane_id());
+    const uint32_t w = launch_wave();
+    // the run record and the run's chain descriptors (lane k = slot k; the
+    // non-empty chains first, then the empty ones, then first == 0 slots)
+    // and the workgroup's LUT words: independent loads, one round trip
+    const bool live = w < n_runs;
+    RowRun rr{};
+    ReqChain C{};
+    if (live) {
+        rr = runs[w];
+        C = chains[static_cast<uint64_t>(w) * kReqRun + ul];
+    }
     if constexpr (LDS_LUT) {
         for (uint32_t i = threadIdx.x; i < n_lut; i += kBlock) slut[i] = st.sym_lut[i];
         __syncthreads();
     }
     const uint32_t *lut_base = LDS_LUT ? slut : st.sym_lut;
-    const uint32_t w = launch_wave();
-    if (w >= n_runs) return;
-    // the run record and the run's chain descriptors (lane k = slot k; the
-    // non-empty chains first, then the empty ones, then first == 0 slots):
-    // independent loads, one round trip
-    const RowRun rr = runs[w];
-    const ReqChain C = chains[static_cast<uint64_t>(w) * kReqRun + ul];
+    if (!live) return;
     const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
     const uint64_t stage_at = uniform64(rr.stage);
     const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
@@ -2038,7 +2043,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint32_t cm = kind == VT_DEL ? kDel : kind == VT_INS ? kIns : kind == VT_DUP ? kDup : kind == VT_DUPT ? kDupT
                           : kind == VT_CNV ? kCnv : 0u;
         L.a[ul] = uint4{C.c_lo - pex, C.first, C.last - C.first, C.e0};
-        L.b[ul] = uint4{C.espan, C.bits & 0x1ffffu, cm | kind << 24, C.lut_off};
+        // lut_off < kReqLutMax (host-enforced) shares the length-bounds word
+        L.b[ul] = uint4{C.espan, (C.bits & 0x1ffffu) | C.lut_off << 17, cm, VT_XK_SYM | vt_xk_bit(kind)};
     }
     L.wch[ul] = 0ull;  // kReqStartChunks == kWave
     L.rowchain[ul] = 0xffu;
@@ -2091,38 +2097,40 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint4 A = L.a[k], Bw = L.b[k];
         const uint32_t first = A.y;
         const uint32_t w = x.h.w;
-        bool cand = g < T && x.p - first <= A.z && x.h.end - A.w <= Bw.x;
-        if (__ballot(cand && (w & VT_SLOW))) {  // never: prepare sends such requests per slice
-            if (cand && (w & VT_SLOW)) atomicOr(&L.slow[k >> 5], 1u << (k & 31u));
-            cand = cand && !(w & VT_SLOW);
+        // window, END bounds: every operand evaluated (bitwise, not
+        // short-circuit: no divergent LDS reads)
+        uint32_t cand = static_cast<uint32_t>(g < T) & static_cast<uint32_t>(x.p - first <= A.z) &
+                        static_cast<uint32_t>(x.h.end - A.w <= Bw.x);
+        if (__ballot(cand & (w >> 28))) {  // VT_SLOW: never (prepare sends such requests per slice)
+            if (cand & (w >> 28)) atomicOr(&L.slow[k >> 5], 1u << (k & 31u));
+            cand &= ~(w >> 28) & 1u;
         }
-        const uint32_t vlo = Bw.y & 511u, vspan = (Bw.y >> 9) & 255u;
+        const uint32_t vlo = Bw.y & 511u, vspan = (Bw.y >> 9) & 255u, lut_off = Bw.y >> 17;
         // ALT0 (search_variants.py:100-183): length bounds, then the class
         // mask of the kind or, for a symbolic ALT, the variantType's LUT bit
-        bool a0 = ((Bw.z >> ((w >> VT_CLASS_SHIFT) & 31u)) & 1u) != 0;
-        if (__ballot(cand && (w & VT_SYM))) {
-            const uint32_t lw = (w & VT_SYM) ? lut_base[Bw.w + ((w >> 21) & 7u)] : 0u;
-            if (w & VT_SYM) a0 = ((lw >> ((w >> 16) & 31u)) & 1u) != 0;
+        uint32_t a0 = (Bw.z >> ((w >> VT_CLASS_SHIFT) & 31u)) & 1u;
+        const uint32_t sym = (w >> 13) & 1u;  // VT_SYM
+        if (__ballot(cand & sym)) {
+            const uint32_t lw = sym ? lut_base[lut_off + ((w >> 21) & 7u)] : 0u;
+            if (sym) a0 = (lw >> ((w >> 16) & 31u)) & 1u;
         }
-        const bool h0 = cand && (w & 0xffu) - vlo <= vspan && a0;
-        // ALTs 2..n (:124 loop): only records whose word says an extra ALT might match
-        const uint32_t kd = Bw.z >> 24;
-        const uint32_t xneed = VT_XK_SYM | vt_xk_bit(kd);
-        const bool xl = cand && (w >> VT_NX_SHIFT) != 0 && (w & xneed) != 0;
+        const uint32_t h0 = cand & static_cast<uint32_t>((w & 0xffu) - vlo <= vspan) & a0;
+        // ALTs 2..n (:124 loop): only records whose word says an extra ALT
+        // of an accepted class (or a symbolic one) might match (Bw.w = xneed)
+        const uint32_t xl = cand & static_cast<uint32_t>((w >> VT_NX_SHIFT) != 0) & static_cast<uint32_t>((w & Bw.w) != 0);
         bool hit;
         uint32_t cn;      // variants emitted (ALTs with AC != 0)
-        uint64_t em = 0;  // their label indexes (multi-ALT lanes)
+        uint64_t em;      // their label indexes
         int64_t cv;       // call count contribution
         uint32_t anv;     // AN contribution
-        const bool multi_rec = __ballot(xl) != 0;
-        if (!multi_rec) {
-            hit = h0;
+        if (!__ballot(xl)) {  // every hit lane has one ALT
+            hit = h0 != 0;
             cv = hit ? x.h.ac0 : 0;
-            cn = hit && x.h.ac0 != 0 ? 1u : 0u;
+            cn = static_cast<uint32_t>(hit & (x.h.ac0 != 0));
             em = cn;
             anv = hit ? static_cast<uint32_t>(x.h.an) : 0u;
         } else {
-            uint64_t hm = h0 ? 1ull : 0ull;
+            uint64_t hm = h0;
             uint32_t x0 = 0;
             if (xl) {
                 x0 = st.x_lo[x.r];
@@ -2131,7 +2139,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                     const uint32_t xw = st.xvt[x0 + j];
                     bool ok = (xw & 0xffu) - vlo <= vspan;
                     if (ok) {
-                        if (xw & VT_SYM) ok = ((lut_base[Bw.w + ((xw >> 21) & 7u)] >> ((xw >> 16) & 31u)) & 1u) != 0;
+                        if (xw & VT_SYM) ok = ((lut_base[lut_off + ((xw >> 21) & 7u)] >> ((xw >> 16) & 31u)) & 1u) != 0;
                         else ok = ((Bw.z >> ((xw >> VT_CLASS_SHIFT) & 31u)) & 1u) != 0;
                     }
                     if (ok) hm |= 2ull << j;
@@ -2139,6 +2147,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             }
             hit = hm != 0;
             cv = 0;
+            em = 0;
             for (uint64_t b = hm; b; b &= b - 1) {  // :205-214, AC of each matching ALT
                 const int j = ffs64(b);
                 const int64_t v = j ? st.xrow[x0 + j - 1].ac : x.h.ac0;
