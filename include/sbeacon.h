@@ -40,6 +40,7 @@ enum {
     SB_EIO = -4,        /* file / decompression failure */
     SB_EPARSE = -5,     /* VCF text the store cannot represent exactly */
     SB_ENOMEM = -6,
+    SB_ESTALE = -7,     /* a persisted store's source VCF changed since it was saved */
 };
 
 /* per-query error: the Python exception the reference raises on this input
@@ -111,6 +112,18 @@ void sb_store_close(sb_store *s);
  * batches (at most 64 of each, 4 GiB device / 2 GiB pinned; batches in
  * flight keep theirs). */
 int sb_store_trim(sb_store *s);
+/* Persisted stores.  sb_store_save writes the finished store to directory
+ * `dir` (created if absent): manifest.json, host.bin (host columns, VCF
+ * metadata) and device.bin (the device image; empty for a host-only store).
+ * sb_store_open re-creates it on `device` (or SB_HOST_ONLY: the host side
+ * only) from `dir` or `dir`/manifest.json without re-reading any VCF;
+ * if a source file of the store (sb_builder_add_file) changed since the save
+ * it returns SB_ESTALE and sb_last_error() lists the changed paths, one per
+ * line -- re-ingest that store.  Replaces the reference's persisted ingest
+ * state (region files in S3, lambda/summariseSlice/source/
+ * write_data_to_s3.h:39-92; toUpdate in DynamoDB, main.cpp:360-438). */
+int sb_store_save(sb_store *s, const char *dir);
+int sb_store_open(const char *path, int device, sb_store **out);
 
 typedef struct {
     uint64_t n_records;

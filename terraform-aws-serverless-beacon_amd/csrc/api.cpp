@@ -172,6 +172,8 @@ const char *last_error_cstr() { return g_last_error.c_str(); }
 using namespace sb;
 
 namespace sb {
+void store_save(sb_store &s, const std::string &dir);                         // persist.cpp
+sb_store *store_open(const std::string &path, int device, std::string *stale);  // persist.cpp
 sb_store *store_hold(sb_store *s) {
     s->holders.fetch_add(1, std::memory_order_acq_rel);
     return s;
@@ -2028,17 +2030,58 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
     dedup_run(s, segs, n, nj, unique, status, stats, false, &runs);
 }
 
-// ---- window dedup planning (devtypes.hpp KWin)
-// Every key run of a job is POS-sorted: cutting the job's runs at POS
+// ---- window dedup planning (devtypes.hpp KWin / KJob)
+// Every key run of a job is POS-sorted: cutting the job's runs at common POS
 // boundaries into windows of about kWinTarget keys puts all keys of one
-// (string, POS) in one window.  runs[g] = segs[g]'s KRun (key range, POS
-// span, its segment's coarse POS index for the twin lookups).
+// (string, POS) in one window.  The host only sizes each job (windows =
+// its keys / kWinTarget, its leader run, its POS span); dedup_plan_kernel
+// finds the cuts.  runs[g] = segs[g]'s KRun (key range, POS span, its
+// segment's coarse POS index for the cuts and the twin lookups).
 struct WinPlan {
-    std::vector<std::vector<KWin>> wins;      // per job group (piece_lo local to the group)
-    std::vector<std::vector<KPiece>> pieces;  // per job group
-    size_t n_wins = 0, n_pieces = 0;
+    std::vector<KJob> jobs;
+    uint64_t n_wins = 0, n_e = 0;
     const char *why = "";  // why the plan was declined (SBEACON_DEDUP_DEBUG)
 };
+
+bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan &P) {
+    uint32_t target = kWinTarget;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
+    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) target = std::max(1, std::min(static_cast<int>(kWinCap), std::atoi(e)));
+    if (s.n_keys >= 0x80000000ull) return P.why = "2^31 keys", false;
+    std::vector<char> seen(nj, 0);
+    for (size_t g0 = 0; g0 < runs.size();) {
+        size_t g1 = g0 + 1;
+        while (g1 < runs.size() && runs[g1].job == runs[g0].job) ++g1;
+        if (seen[runs[g0].job]) return P.why = "job runs not contiguous", false;
+        seen[runs[g0].job] = 1;
+        if (g1 - g0 > kWinPieces) return P.why = "runs", false;
+        KJob J{};
+        uint64_t keys = 0;
+        size_t lead = g0;
+        J.pmin = UINT32_MAX;
+        for (size_t g = g0; g < g1; ++g) {
+            runs[g].run_lo = static_cast<uint32_t>(g0);
+            runs[g].nruns = static_cast<uint32_t>(g1 - g0);
+            const uint32_t k = runs[g].key_hi - runs[g].key_lo;
+            keys += k;
+            if (k > runs[lead].key_hi - runs[lead].key_lo) lead = g;
+            J.pmin = std::min(J.pmin, runs[g].pos_lo);
+            J.pmax = std::max(J.pmax, runs[g].pos_hi);
+        }
+        J.lead_lo = runs[lead].key_lo;
+        J.lead_n = runs[lead].key_hi - runs[lead].key_lo;
+        J.nw = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(1, (keys + target - 1) / target), J.lead_n));
+        J.w0 = static_cast<uint32_t>(P.n_wins);
+        J.run_lo = static_cast<uint32_t>(g0);
+        J.nruns = static_cast<uint32_t>(g1 - g0);
+        J.eoff = static_cast<uint32_t>(P.n_e);
+        P.n_wins += J.nw;
+        P.n_e += uint64_t(J.nruns) * (J.nw + 1);
+        if (P.n_wins >= 0x7fffffffull || P.n_e >= 0xffffffffull) return P.why = "windows", false;
+        P.jobs.push_back(J);
+        g0 = g1;
+    }
+    return true;
+}
 
 struct PinnedHost {  // grow-only pinned host staging (hipHostMalloc)
     void *p = nullptr;
@@ -2056,178 +2099,9 @@ struct PinnedHost {  // grow-only pinned host staging (hipHostMalloc)
     }
 };
 
-// one job's windows (runs [g0, g1) of the call) over its keys with POS in
-// [p_from, p_to) (a POS range of the job: windows never straddle it)
-bool plan_job_windows(const sb_store &s, const std::vector<KRun> &runs, size_t g0, size_t g1, uint32_t target,
-                      std::vector<KWin> &wins, std::vector<KPiece> &pieces, const char **why, uint64_t p_from = 0,
-                      uint64_t p_to = ~0ull) {
-    constexpr uint64_t kSpan = (1ull << kWinSpanBits) - 2;
-    const std::vector<uint32_t> &pos = s.h_dk_pos;
-    const size_t m = g1 - g0;
-    if (m > kWinPieces) return *why = "runs", false;
-    const uint32_t job = runs[g0].job;
-    std::vector<uint32_t> cur(m), end(m), e(m);
-    uint32_t pmax = 0;
-    for (size_t r = 0; r < m; ++r) {
-        cur[r] = runs[g0 + r].key_lo;
-        end[r] = runs[g0 + r].key_hi;
-        pmax = std::max(pmax, runs[g0 + r].pos_hi);
-        if (p_from > 0)
-            cur[r] = static_cast<uint32_t>(
-                std::lower_bound(pos.begin() + cur[r], pos.begin() + end[r], std::min<uint64_t>(p_from, 0xffffffffull)) -
-                pos.begin());
-        if (p_to <= 0xffffffffull)
-            end[r] = static_cast<uint32_t>(
-                std::lower_bound(pos.begin() + cur[r], pos.begin() + end[r], static_cast<uint32_t>(p_to)) - pos.begin());
-    }
-    // lower bound of x in run r at or after a, searched outward from the
-    // hint h (the runs of a job have similar densities, so the answer is
-    // usually a few keys from a + the window's share): galloping steps, then
-    // a binary search over the last one
-    auto lb = [&](size_t r, uint32_t a, uint64_t p, uint32_t h) -> uint32_t {
-        if (p > 0xffffffffull) return end[r];
-        const uint32_t x = static_cast<uint32_t>(p);
-        h = std::min(std::max(h, a), end[r]);
-        uint32_t lo, hi;  // answer in [lo, hi]
-        if (h > a && pos[h - 1] >= x) {  // at or before h - 1: gallop down
-            hi = h - 1;
-            uint32_t step = 8;
-            while (hi - a > step && pos[hi - step] >= x) {
-                hi -= step;
-                step *= 2;
-            }
-            lo = hi - a > step ? hi - step : a;
-        } else {  // at or after h: gallop up
-            lo = h;
-            uint32_t step = 8;
-            while (lo + step < end[r] && pos[lo + step] < x) {
-                lo += step;
-                step *= 2;
-            }
-            hi = static_cast<uint32_t>(std::min<uint64_t>(end[r], static_cast<uint64_t>(lo) + step));
-        }
-        return static_cast<uint32_t>(std::lower_bound(pos.begin() + lo, pos.begin() + hi, x) - pos.begin());
-    };
-    for (;;) {
-        uint64_t p0 = ~0ull;
-        uint32_t act = 0;
-        for (size_t r = 0; r < m; ++r)
-            if (cur[r] < end[r]) {
-                p0 = std::min<uint64_t>(p0, pos[cur[r]]);
-                ++act;
-            }
-        if (!act) break;
-        // grow [p0, p1) in up to three steps: each run may add budget / act
-        // keys; e[r] = lower bound of p1 in run r
-        uint64_t p1 = p0;
-        for (size_t r = 0; r < m; ++r) e[r] = cur[r];
-        uint32_t budget = target;
-        for (int it = 0; it < 3 && budget >= std::min<uint32_t>(64, target); ++it) {
-            const uint32_t per = std::max<uint32_t>(1, budget / act);
-            uint64_t cand = p0 + kSpan;
-            for (size_t r = 0; r < m; ++r) {
-                const uint64_t idx = static_cast<uint64_t>(e[r]) + per;
-                if (cur[r] < end[r] && idx < end[r]) cand = std::min<uint64_t>(cand, pos[idx]);
-            }
-            if (cand <= p1) break;
-            p1 = cand;
-            uint64_t cnt = 0;
-            for (size_t r = 0; r < m; ++r) {
-                e[r] = lb(r, e[r], p1, e[r] + per);
-                cnt += e[r] - cur[r];
-            }
-            budget = cnt < target ? target - static_cast<uint32_t>(cnt) : 0;
-        }
-        if (p1 == p0) {  // one POS holds more than a share of the window
-            p1 = p0 + 1;
-            for (size_t r = 0; r < m; ++r) e[r] = lb(r, cur[r], p1, cur[r]);
-        }
-        KWin w{static_cast<uint32_t>(pieces.size()), 0, job, static_cast<uint32_t>(p0), static_cast<uint32_t>(g0), pmax,
-               {0, 0}};
-        uint64_t total = 0;
-        for (size_t r = 0; r < m; ++r) {
-            if (e[r] > cur[r]) {
-                pieces.push_back(KPiece{cur[r], (e[r] - cur[r]) | (static_cast<uint32_t>(r) << 16)});
-                total += e[r] - cur[r];
-                cur[r] = e[r];
-            }
-        }
-        w.npieces = static_cast<uint32_t>(pieces.size()) - w.piece_lo;
-        if (total > kWinCap) return *why = "pile-up", false;  // the sorted path
-        wins.push_back(w);
-    }
-    return true;
-}
-
-// Every job's windows; jobs planned on the worker pool.  runs[g] = segs[g]'s KRun.
-bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan &P) {
-    uint32_t target = kWinCap;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
-    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) target = std::max(1, std::min(static_cast<int>(kWinCap), std::atoi(e)));
-    if (s.n_keys >= 0x80000000ull) return P.why = "2^31 keys", false;
-    std::vector<std::pair<size_t, size_t>> groups;  // each job's runs
-    std::vector<char> seen(nj, 0);
-    for (size_t g0 = 0; g0 < runs.size();) {
-        size_t g1 = g0 + 1;
-        while (g1 < runs.size() && runs[g1].job == runs[g0].job) ++g1;
-        if (seen[runs[g0].job]) return P.why = "job runs not contiguous", false;
-        seen[runs[g0].job] = 1;
-        for (size_t g = g0; g < g1; ++g) {
-            runs[g].run_lo = static_cast<uint32_t>(g0);
-            runs[g].nruns = static_cast<uint32_t>(g1 - g0);
-        }
-        groups.emplace_back(g0, g1);
-        g0 = g1;
-    }
-    // tasks: each job cut into POS ranges at quantiles of its first run's
-    // keys (few jobs per call would leave the pool's threads idle: 50 equal
-    // jobs on 16 threads take 4 rounds)
-    struct Task {
-        size_t q;
-        uint64_t p_from, p_to;
-    };
-    std::vector<Task> tasks;
-    const size_t split = groups.size() >= 64 ? 1 : std::min<size_t>(8, (128 + groups.size() - 1) / std::max<size_t>(groups.size(), 1));
-    for (size_t q = 0; q < groups.size(); ++q) {
-        const KRun &r0 = runs[groups[q].first];
-        uint64_t prev = 0;
-        for (size_t k = 1; k < split; ++k) {
-            const uint64_t p = s.h_dk_pos[r0.key_lo + (uint64_t(r0.key_hi - r0.key_lo) * k) / split];
-            if (p > prev) {
-                tasks.push_back(Task{q, prev, p});
-                prev = p;
-            }
-        }
-        tasks.push_back(Task{q, prev, ~0ull});
-    }
-    std::vector<std::vector<KWin>> &tw = P.wins;
-    std::vector<std::vector<KPiece>> &tp = P.pieces;
-    tw.assign(tasks.size(), {});
-    tp.assign(tasks.size(), {});
-    std::vector<const char *> why(tasks.size(), nullptr);
-    auto work = [&](size_t t) {
-        const Task &T = tasks[t];
-        const auto &G = groups[T.q];
-        const char *w = nullptr;
-        uint64_t keys = 0;
-        for (size_t g = G.first; g < G.second; ++g) keys += runs[g].key_hi - runs[g].key_lo;
-        keys = keys / split + 1;
-        tw[t].reserve(keys / (target / 2 + 1) + 4);
-        tp[t].reserve(2 * (keys / (target / 2 + 1) + 4) * (G.second - G.first));
-        if (!plan_job_windows(s, runs, G.first, G.second, target, tw[t], tp[t], &w, T.p_from, T.p_to)) why[t] = w;
-    };
-    if (tasks.size() > 1) WorkerPool::get().run(tasks.size(), work);
-    else if (!tasks.empty()) work(0);
-    for (size_t q = 0; q < tasks.size(); ++q) {
-        if (why[q]) return P.why = why[q], false;
-        P.n_wins += tw[q].size();
-        P.n_pieces += tp[q].size();
-    }
-    return true;
-}
-
 struct WinWs {
-    DevMem wins, pieces, runs, counts, overflow, list, n_list;
-    PinnedHost stage;  // windows | pieces | runs for one H2D copy; counts + overflow back
+    DevMem jobs, wins, e, runs, counts, overflow, list, n_list;
+    PinnedHost stage;  // jobs | runs for one H2D copy; counts + overflow back
 };
 
 // the window path: true when it answered every job (counts in unique[])
@@ -2247,8 +2121,9 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     if (!s.win_ws) s.win_ws = std::shared_ptr<void>(new WinWs, [](void *w) { delete static_cast<WinWs *>(w); });
     WinWs &W = *static_cast<WinWs *>(s.win_ws.get());
     const uint32_t nw = static_cast<uint32_t>(P.n_wins);
+    W.jobs.reserve(std::max<size_t>(P.jobs.size(), 1) * sizeof(KJob));
     W.wins.reserve(std::max<size_t>(nw, 1) * sizeof(KWin));
-    W.pieces.reserve(std::max<size_t>(P.n_pieces, 1) * sizeof(KPiece));
+    W.e.reserve(std::max<size_t>(P.n_e, 1) * 4);
     W.runs.reserve(std::max<size_t>(runs.size(), 1) * sizeof(KRun));
     W.counts.reserve(std::max<size_t>(nj, 1) * 8);
     W.overflow.reserve(4);
@@ -2258,28 +2133,15 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     W.list.reserve(static_cast<size_t>(cap) * 8);
     W.n_list.reserve(4);
     HIP_OK(hipMemsetAsync(W.n_list.p, 0, 4, st));
-    // the plan staged in pinned memory (the groups' windows with their piece
-    // offsets made global, pieces, runs): DMA without a pageable bounce; the
-    // previous call's copies have completed (it synchronised)
-    const size_t bw = size_t(nw) * sizeof(KWin), bp = P.n_pieces * sizeof(KPiece), br = runs.size() * sizeof(KRun);
-    W.stage.reserve(bw + bp + br + 64 + std::max<size_t>(nj, 1) * 8);
+    // jobs and runs staged in pinned memory: DMA without a pageable bounce;
+    // the previous call's copies have completed (it synchronised)
+    const size_t bj = P.jobs.size() * sizeof(KJob), br = runs.size() * sizeof(KRun);
+    W.stage.reserve(bj + br + 64 + std::max<size_t>(nj, 1) * 8);
     if (nw) {
-        KWin *hw = static_cast<KWin *>(W.stage.p);
-        KPiece *hp = reinterpret_cast<KPiece *>(static_cast<uint8_t *>(W.stage.p) + bw);
-        uint32_t pbase = 0;
-        for (size_t q = 0; q < P.wins.size(); ++q) {
-            for (const KWin &w : P.wins[q]) {
-                *hw = w;
-                hw->piece_lo += pbase;
-                ++hw;
-            }
-            std::copy(P.pieces[q].begin(), P.pieces[q].end(), hp + pbase);
-            pbase += static_cast<uint32_t>(P.pieces[q].size());
-        }
-        std::memcpy(static_cast<uint8_t *>(W.stage.p) + bw + bp, runs.data(), br);
-        HIP_OK(hipMemcpyAsync(W.wins.p, W.stage.p, bw, hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemcpyAsync(W.pieces.p, static_cast<uint8_t *>(W.stage.p) + bw, bp, hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemcpyAsync(W.runs.p, static_cast<uint8_t *>(W.stage.p) + bw + bp, br, hipMemcpyHostToDevice, st));
+        std::memcpy(W.stage.p, P.jobs.data(), bj);
+        std::memcpy(static_cast<uint8_t *>(W.stage.p) + bj, runs.data(), br);
+        HIP_OK(hipMemcpyAsync(W.jobs.p, W.stage.p, bj, hipMemcpyHostToDevice, st));
+        HIP_OK(hipMemcpyAsync(W.runs.p, static_cast<uint8_t *>(W.stage.p) + bj, br, hipMemcpyHostToDevice, st));
     }
     HIP_OK(hipMemsetAsync(W.counts.p, 0, std::max<size_t>(nj, 1) * 8, st));
     HIP_OK(hipMemsetAsync(W.overflow.p, 0, 4, st));
@@ -2287,9 +2149,9 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     HIP_OK(hipEventCreate(&e0));
     HIP_OK(hipEventCreate(&e1));
     HIP_OK(hipEventRecord(e0, st));
-    launch_window_dedupe(s.dk, W.wins.as<KWin>(), nw, W.pieces.as<KPiece>(), W.runs.as<KRun>(),
-                         W.counts.as<unsigned long long>(), W.list.as<uint2>(), W.n_list.as<uint32_t>(), cap,
-                         W.overflow.as<uint32_t>(), st);
+    launch_window_dedupe(s.dk, W.jobs.as<KJob>(), static_cast<uint32_t>(P.jobs.size()), W.wins.as<KWin>(), nw,
+                         W.e.as<uint32_t>(), W.runs.as<KRun>(), W.counts.as<unsigned long long>(), W.list.as<uint2>(),
+                         W.n_list.as<uint32_t>(), cap, W.overflow.as<uint32_t>(), st);
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipGetLastError());
     std::vector<uint64_t> cnt(std::max<size_t>(nj, 1));
@@ -2980,7 +2842,10 @@ int sb_builder_attach_carriers(sb_builder *b, uint32_t vcf_id, const char *const
 int sb_builder_finish(sb_builder *b, int device, sb_store **out) {
     return guard([&] {
         if (!b || !out) throw Error(SB_EINVAL, "NULL argument");
+        const bool trace = std::getenv("SBEACON_INGEST_TRACE") != nullptr;  // phase times to stderr
+        const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t i = 0; i < b->vcfs.size(); ++i) builder_flush(*b, i);
+        const auto t1 = std::chrono::steady_clock::now();
         auto s = std::make_unique<sb_store>();
         s->device = device;
         if (device != SB_HOST_ONLY) {
@@ -2991,6 +2856,10 @@ int sb_builder_finish(sb_builder *b, int device, sb_store **out) {
             HIP_OK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
         }
         upload_store(*b, *s);
+        if (trace)
+            std::fprintf(stderr, "[ingest] flush %.2f s, store columns + upload %.2f s\n",
+                         std::chrono::duration<double>(t1 - t0).count(),
+                         std::chrono::duration<double>(std::chrono::steady_clock::now() - t1).count());
         s->vcfs = std::move(b->vcfs);
         s->vt = std::move(b->vt);
         s->sym = std::move(b->sym);
@@ -3006,6 +2875,24 @@ int sb_builder_finish(sb_builder *b, int device, sb_store **out) {
 void sb_builder_free(sb_builder *b) { delete b; }
 void sb_store_close(sb_store *s) {
     if (s) store_release(s);
+}
+
+int sb_store_save(sb_store *s, const char *dir) {
+    return guard([&] {
+        if (!s || !dir) throw Error(SB_EINVAL, "NULL argument");
+        std::lock_guard<std::mutex> lk(s->mu);
+        store_save(*s, dir);
+    });
+}
+
+int sb_store_open(const char *path, int device, sb_store **out) {
+    return guard([&] {
+        if (!path || !out) throw Error(SB_EINVAL, "NULL argument");
+        std::string stale;
+        sb_store *s = store_open(path, device, &stale);
+        if (!s) throw Error(SB_ESTALE, stale);
+        *out = s;
+    });
 }
 
 int sb_store_trim(sb_store *s) {

@@ -766,7 +766,53 @@ __global__ __launch_bounds__(kThreads) void deferred_dedupe_kernel(KStore ks, co
     }
 }
 
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void window_dedupe_kernel(KStore ks, const KWin *wins, const KPiece *pieces,
+// first key of run R with POS >= x: the segment's coarse POS index
+// brackets the records (as run_has_equal), a binary search over their POS
+// names the record, its first key is the bound (keys are in record order)
+__device__ uint32_t key_lower_bound(const KStore &ks, const KRun &R, uint32_t x) {
+    if (x <= R.pos_lo) return R.key_lo;
+    if (x > R.pos_hi) return R.key_hi;
+    const uint64_t b = (static_cast<uint64_t>(x) - R.b_base) >> R.b_shift;
+    uint32_t lo = b >= R.b_n ? R.seg_hi : ks.bucket[R.b_off + b];
+    uint32_t hi = b >= R.b_n ? R.seg_hi : ks.bucket[R.b_off + b + 1];
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (ks.rpos[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return min(max(ks.lo[lo], R.key_lo), R.key_hi);
+}
+
+// Window planning on the device (replaces the host walk): one thread per
+// window.  Window i of job J starts at POS P_i = the POS of the leader
+// run's key i * lead_n / nw (P_0 = the job's smallest POS); every run of the
+// job starts it at its lower bound of P_i, so windows are POS ranges and the
+// keys of one POS meet in one window.
+__global__ __launch_bounds__(kThreads) void dedup_plan_kernel(KStore ks, const KJob *__restrict__ jobs, uint32_t nj,
+                                                              const KRun *__restrict__ runs, uint32_t nw_total,
+                                                              KWin *__restrict__ wins, uint32_t *__restrict__ E) {
+    const uint32_t w = blockIdx.x * kThreads + threadIdx.x;
+    if (w >= nw_total) return;
+    uint32_t lo = 0, hi = nj;  // the last job with w0 <= w
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (jobs[mid].w0 <= w) lo = mid;
+        else hi = mid;
+    }
+    const KJob J = jobs[lo];
+    const uint32_t i = w - J.w0;
+    const uint32_t P = i == 0 ? J.pmin
+                              : static_cast<uint32_t>(ks.word[J.lead_lo + static_cast<uint64_t>(i) * J.lead_n / J.nw]);
+    for (uint32_t r = 0; r < J.nruns; ++r) {
+        const KRun R = runs[J.run_lo + r];
+        uint32_t *e = E + J.eoff + static_cast<uint64_t>(r) * (J.nw + 1);
+        e[i] = i == 0 ? R.key_lo : key_lower_bound(ks, R, P);
+        if (i + 1 == J.nw) e[J.nw] = R.key_hi;
+    }
+    wins[w] = KWin{i, J.nruns, runs[J.run_lo].job, P, J.run_lo, J.pmax, J.eoff, J.nw};
+}
+
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void window_dedupe_kernel(KStore ks, const KWin *wins, const uint32_t *E,
                                                                  unsigned long long *counts, uint2 *list,
                                                                  uint32_t *n_list, uint32_t cap, uint32_t *overflow,
                                                                  uint32_t dbg) {
@@ -778,11 +824,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))
     for (uint32_t i = threadIdx.x; i < kWSlots; i += kThreads) set[i] = ~0ull;
     if (threadIdx.x < 64) {  // wave 0: the pieces' inclusive prefix
         uint32_t len = 0, klo = 0, run = 0;
-        if (static_cast<uint32_t>(lane) < W.npieces) {
-            const KPiece p = pieces[W.piece_lo + lane];
-            klo = p.key_lo;
-            len = p.n & 0xffffu;
-            run = W.run_lo + (p.n >> 16);
+        if (static_cast<uint32_t>(lane) < W.nruns) {  // run `lane`'s piece of the window
+            const uint32_t *e = E + W.eoff + static_cast<uint64_t>(lane) * (W.nw + 1) + W.i;
+            klo = e[0];
+            len = e[1] - e[0];
+            run = W.run_lo + lane;
         }
         uint32_t inc = len;
 #pragma unroll
@@ -800,7 +846,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))
         }
     }
     __syncthreads();
-    const uint32_t np = W.npieces, total = s_pre[np];
+    const uint32_t np = W.nruns, total = s_pre[np];
+    if (total > kWinCap) {  // a pile-up past the window's set (the host recounts on the sorted path)
+        if (threadIdx.x == 0) atomicOr(overflow, 1u);
+        return;
+    }
     auto piece_of = [&](uint32_t f) {
         uint32_t p = 0;
 #pragma unroll
@@ -1029,13 +1079,14 @@ int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1,
     return r;
 }
 
-void launch_window_dedupe(const KStore &ks, const KWin *wins, uint32_t nw, const KPiece *pieces, const KRun *runs,
-                          unsigned long long *counts, uint2 *list, uint32_t *n_list, uint32_t cap, uint32_t *overflow,
-                          hipStream_t s) {
+void launch_window_dedupe(const KStore &ks, const KJob *jobs, uint32_t nj, KWin *wins, uint32_t nw, uint32_t *E,
+                          const KRun *runs, unsigned long long *counts, uint2 *list, uint32_t *n_list, uint32_t cap,
+                          uint32_t *overflow, hipStream_t s) {
     if (!nw) return;
     const char *dbge = std::getenv("SBEACON_DEDUP_WIN_DBG");  // timing ablations (never set by the benches)
     const uint32_t dbg = dbge ? static_cast<uint32_t>(std::atoi(dbge)) : 0u;
-    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, wins, pieces, counts, list, n_list, cap, overflow, dbg);
+    dedup_plan_kernel<<<(nw + kThreads - 1) / kThreads, kThreads, 0, s>>>(ks, jobs, nj, runs, nw, wins, E);
+    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, wins, E, counts, list, n_list, cap, overflow, dbg);
     deferred_dedupe_kernel<<<1024, kThreads, 0, s>>>(ks, runs, list, n_list, cap, counts);
 }
 

@@ -539,14 +539,22 @@ inline constexpr uint32_t kKeyDisplaced = 1u;
 // per key: y counts when no key of the job's runs holds its string at a
 // larger POS (its twin, found through the record POS index) and no earlier
 // key of the job's runs (earlier run, or earlier in its run) equals it.
-struct KWin {
-    uint32_t piece_lo, npieces, job, p0;
+struct KWin {  // window w of a call (dedup_plan_kernel writes it)
+    uint32_t i, nruns, job, p0;  // window i of its job; the job's runs; POS where it starts
     uint32_t run_lo;  // the job's first KRun
     uint32_t pmax;    // largest POS of the job's runs
-    uint32_t pad[2];
+    uint32_t eoff;    // run r's window starts: E[eoff + r * (nw + 1) + i], ends at ... + i + 1
+    uint32_t nw;      // the job's windows
 };
-struct KPiece {  // keys [key_lo, key_lo + (n & 0xffff)) of run (n >> 16) of the job
-    uint32_t key_lo, n;
+// One job of a window-dedup call (host-built): its windows [w0, w0 + nw) cut
+// its POS axis at the leader run's key ranks i * lead_n / nw, every run of the
+// job split at the same POS (dedup_plan_kernel: a lower bound per run and cut)
+struct KJob {
+    uint32_t w0, nw, run_lo, nruns;
+    uint32_t lead_lo, lead_n;  // the leader run's (the job's longest) keys
+    uint32_t pmin, pmax;       // POS span of the job's runs
+    uint32_t eoff;             // first E entry of the job's runs (nruns x (nw + 1))
+    uint32_t pad[3];
 };
 struct KRun {  // one POS-sorted key run of a job + its segment's POS index
     uint32_t key_lo, key_hi, pos_lo, pos_hi;  // keys, POS of the first / last
@@ -558,6 +566,7 @@ struct KRun {  // one POS-sorted key run of a job + its segment's POS index
     uint32_t pad[2];
 };
 inline constexpr uint32_t kWinCap = 2048;    // keys per window (LDS sets sized for it)
+inline constexpr uint32_t kWinTarget = 1536; // keys a window is planned for (runs of a job differ in density)
 inline constexpr uint32_t kWinPieces = 64;   // pieces (= runs) per window
 inline constexpr uint32_t kWinSpanBits = 26; // p1 - p0 < 2^26 - 1: exact words fit 32 bits
 

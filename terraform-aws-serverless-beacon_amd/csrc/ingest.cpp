@@ -1148,6 +1148,7 @@ void vcf_scan_file(const char *path, VcfScan &out) {
 
 void builder_add_file(sb_builder &b, uint32_t vcf_id, const char *path) {
     if (vcf_id >= b.vcfs.size()) throw Error(SB_ENOSTORE, "unknown vcf id");
+    b.vcfs[vcf_id].sources.push_back(fingerprint(path));  // sb_store_save / sb_store_open
     {
         FILE *fp = fopen(path, "rb");
         if (!fp) throw Error(SB_EIO, std::string("cannot open ") + path);

@@ -1,0 +1,505 @@
+// persist.cpp — a store on disk: sb_store_save / sb_store_open.
+//
+// The reference keeps its ingest state between invocations: each VCF's
+// region files in S3 (lambda/summariseSlice/source/write_data_to_s3.h:39-92)
+// and the per-dataset toUpdate bookkeeping in DynamoDB
+// (lambda/summariseSlice/source/main.cpp:360-438), so a performQuery never
+// re-reads VCF text.  Here the finished store itself is saved: every device
+// buffer (copied back from HBM), the host columns the planners and
+// formatters read, and the VCF metadata, plus a fingerprint of every source
+// file (size, mtime, a hash of its first and last 64 KiB).  sb_store_open
+// re-allocates the buffers, streams them up from the file (no re-parse, no
+// column rebuild) and remaps the device pointers the store's kernel views
+// hold.  A source that changed since the save makes sb_store_open fail with
+// SB_ESTALE naming it; the caller re-ingests that store only (stores are per
+// VCF group: sbeacon.catalog.StoreCatalog rebuilds just the stale ones).
+//
+//   <dir>/manifest.json  version, sources with fingerprints, sizes (text)
+//   <dir>/host.bin       host columns + VCF metadata + kernel views
+//   <dir>/device.bin     the device buffers, back to back (4 KiB aligned)
+#include <hip/hip_runtime.h>
+#include <sys/stat.h>
+
+#include <array>
+#include <chrono>
+#include <memory>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <thread>
+#include <type_traits>
+#include <vector>
+
+#include "common.hpp"
+#include "jsonesc.hpp"
+#include "store.hpp"
+
+#define HIP_OK(x)                                                                                  \
+    do {                                                                                           \
+        hipError_t e_ = (x);                                                                       \
+        if (e_ != hipSuccess) throw sb::Error(SB_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+namespace sb {
+
+constexpr uint64_t kMagic = 0x3150544f5453424full;  // "OBSTOTP1"
+constexpr uint32_t kFormat = 1;
+
+// FNV-1a over the first and last 64 KiB (with the size and mtime, a change
+// detector -- not a content address)
+SourceFile fingerprint(const std::string &path) {
+    SourceFile f;
+    f.path = path;
+    struct stat st {};
+    if (stat(path.c_str(), &st) != 0) return f;
+    f.size = static_cast<uint64_t>(st.st_size);
+    f.mtime_ns = static_cast<int64_t>(st.st_mtim.tv_sec) * 1000000000ll + st.st_mtim.tv_nsec;
+    FILE *fp = fopen(path.c_str(), "rb");
+    if (!fp) return f;
+    uint64_t h = 1469598103934665603ull;
+    std::vector<uint8_t> buf(65536);
+    auto eat = [&](long at) {
+        if (fseek(fp, at, SEEK_SET) != 0) return;
+        const size_t n = fread(buf.data(), 1, buf.size(), fp);
+        for (size_t i = 0; i < n; ++i) h = (h ^ buf[i]) * 1099511628211ull;
+    };
+    eat(0);
+    if (f.size > buf.size()) eat(static_cast<long>(f.size - buf.size()));
+    fclose(fp);
+    f.sample_hash = h;
+    return f;
+}
+
+namespace {
+
+struct Writer {
+    FILE *f = nullptr;
+    uint64_t at = 0;
+    explicit Writer(const std::string &path) {
+        f = fopen(path.c_str(), "wb");
+        if (!f) throw Error(SB_EIO, "cannot write " + path);
+    }
+    ~Writer() {
+        if (f) fclose(f);
+    }
+    void raw(const void *p, size_t n) {
+        if (n && fwrite(p, 1, n, f) != n) throw Error(SB_EIO, "short write");
+        at += n;
+    }
+    template <class T>
+    void pod(const T &v) {
+        static_assert(std::is_trivially_copyable<T>::value, "pod");
+        raw(&v, sizeof v);
+    }
+    template <class T>
+    void vec(const std::vector<T> &v) {
+        static_assert(std::is_trivially_copyable<T>::value, "vec of pod");
+        pod<uint64_t>(v.size());
+        raw(v.data(), v.size() * sizeof(T));
+    }
+    void str(const std::string &s) {
+        pod<uint64_t>(s.size());
+        raw(s.data(), s.size());
+    }
+    void strs(const std::vector<std::string> &v) {
+        pod<uint64_t>(v.size());
+        for (const auto &s : v) str(s);
+    }
+    void pad(uint64_t align) {
+        static const uint8_t z[4096] = {};
+        while (at % align) raw(z, std::min<uint64_t>(align - at % align, sizeof z));
+    }
+};
+
+struct Reader {
+    std::vector<uint8_t> b;
+    size_t at = 0;
+    void need(size_t n) const {
+        if (at + n > b.size()) throw Error(SB_EIO, "persisted store: truncated host.bin");
+    }
+    void raw(void *p, size_t n) {
+        need(n);
+        if (n) std::memcpy(p, b.data() + at, n);
+        at += n;
+    }
+    template <class T>
+    T pod() {
+        T v;
+        raw(&v, sizeof v);
+        return v;
+    }
+    template <class T>
+    void vec(std::vector<T> &v) {
+        const uint64_t n = pod<uint64_t>();
+        need(n * sizeof(T));
+        v.resize(n);
+        raw(v.data(), n * sizeof(T));
+    }
+    std::string str() {
+        const uint64_t n = pod<uint64_t>();
+        need(n);
+        std::string s(reinterpret_cast<const char *>(b.data() + at), n);
+        at += n;
+        return s;
+    }
+    std::vector<std::string> strs() {
+        std::vector<std::string> v(pod<uint64_t>());
+        for (auto &s : v) s = str();
+        return v;
+    }
+};
+
+std::vector<uint8_t> read_file(const std::string &path) {
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) throw Error(SB_EIO, "cannot open " + path);
+    fseek(f, 0, SEEK_END);
+    const long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    std::vector<uint8_t> b(static_cast<size_t>(std::max(0l, n)));
+    const size_t got = fread(b.data(), 1, b.size(), f);
+    fclose(f);
+    if (got != b.size()) throw Error(SB_EIO, "short read " + path);
+    return b;
+}
+
+void put_sources(Writer &w, const std::vector<SourceFile> &v) {
+    w.pod<uint64_t>(v.size());
+    for (const SourceFile &f : v) {
+        w.str(f.path);
+        w.pod(f.size);
+        w.pod(f.mtime_ns);
+        w.pod(f.sample_hash);
+    }
+}
+
+std::vector<SourceFile> get_sources(Reader &r) {
+    std::vector<SourceFile> v(r.pod<uint64_t>());
+    for (SourceFile &f : v) {
+        f.path = r.str();
+        f.size = r.pod<uint64_t>();
+        f.mtime_ns = r.pod<int64_t>();
+        f.sample_hash = r.pod<uint64_t>();
+    }
+    return v;
+}
+
+// a finished store's VCF metadata (its columns were moved into the store)
+void put_vcf(Writer &w, const VcfData &v) {
+    w.str(v.location);
+    put_sources(w, v.sources);
+    w.pod(v.rec_lo);
+    w.pod(v.rec_hi);
+    w.pod(v.lines_seen);
+    w.strs(v.samples);
+    w.pod(v.words);
+    w.pod<uint8_t>(v.header_seen);
+    w.pod<uint64_t>(v.segments.size());
+    for (const Segment &g : v.segments) {
+        w.str(g.contig);
+        w.pod(g.lo);
+        w.pod(g.hi);
+    }
+    w.vec(v.buckets);
+    w.vec(v.vc_index);
+    w.pod(v.seg_base);
+    w.pod(v.stream_off);
+    w.vec(v.blk_coff);
+    w.vec(v.blk_ustart);
+    w.pod(v.stream_len);
+    w.pod(v.rec_base);
+    w.pod(v.x_base);
+    w.pod(v.plane0_base);
+    w.pod(v.planex_base);
+    w.pod<uint8_t>(v.nonneg);
+    w.pod<uint8_t>(v.has_planes);
+    w.pod<uint8_t>(v.range8);
+    w.pod(v.an_default);
+}
+
+void get_vcf(Reader &r, VcfData &v) {
+    v.location = r.str();
+    v.sources = get_sources(r);
+    v.rec_lo = r.pod<uint64_t>();
+    v.rec_hi = r.pod<uint64_t>();
+    v.lines_seen = r.pod<uint64_t>();
+    v.samples = r.strs();
+    v.words = r.pod<uint32_t>();
+    v.header_seen = r.pod<uint8_t>() != 0;
+    v.segments.resize(r.pod<uint64_t>());
+    for (Segment &g : v.segments) {
+        g.contig = r.str();
+        g.lo = r.pod<uint32_t>();
+        g.hi = r.pod<uint32_t>();
+    }
+    r.vec(v.buckets);
+    r.vec(v.vc_index);
+    v.seg_base = r.pod<uint32_t>();
+    v.stream_off = r.pod<uint64_t>();
+    r.vec(v.blk_coff);
+    r.vec(v.blk_ustart);
+    v.stream_len = r.pod<uint64_t>();
+    v.rec_base = r.pod<uint32_t>();
+    v.x_base = r.pod<uint32_t>();
+    v.plane0_base = r.pod<uint64_t>();
+    v.planex_base = r.pod<uint64_t>();
+    v.nonneg = r.pod<uint8_t>() != 0;
+    v.has_planes = r.pod<uint8_t>() != 0;
+    v.range8 = r.pod<uint8_t>() != 0;
+    v.an_default = r.pod<int32_t>();
+    v.seg_index.clear();
+    for (uint32_t i = 0; i < v.segments.size(); ++i) v.seg_index.emplace(v.segments[i].contig, i);
+    v.sample_pos.clear();
+    for (uint32_t k = 0; k < v.samples.size(); ++k) v.sample_pos[v.samples[k]].push_back(k);
+}
+
+// every host column of the store, in one order for save and open
+template <class F>
+void host_columns(sb_store &s, F &&f) {
+    f(s.h_pos), f(s.h_end), f(s.h_a0_len), f(s.h_x_lo), f(s.h_x_len), f(s.h_bucket);
+    f(s.h_vt), f(s.h_vt_slow), f(s.h_vc_pos), f(s.h_vc_bucket), f(s.h_vc_altpre);
+    f(s.h_ref_off), f(s.h_a0_off), f(s.h_x_off), f(s.h_blob), f(s.h_start);
+    f(s.h_rem), f(s.h_cur), f(s.h_dcount), f(s.h_sum_bad);
+    f(s.h_dk_pos), f(s.h_dk_lo), f(s.h_dk_bad), f(s.h_dk_tail), f(s.h_dk_blob);
+}
+
+// the store's kernel views, as 8-byte words (their pointers are remapped)
+template <class T>
+uint64_t *words(T &v) {
+    static_assert(sizeof(T) % 8 == 0, "views are 8-byte multiples");
+    return reinterpret_cast<uint64_t *>(&v);
+}
+
+std::string manifest_text(const sb_store &s, uint64_t host_bytes, uint64_t device_bytes) {
+    std::string o = "{\n  \"format\": " + std::to_string(kFormat) + ",\n  \"abi\": " + std::to_string(SB_ABI_VERSION) +
+                    ",\n  \"records\": " + std::to_string(s.n_records) + ",\n  \"host_bytes\": " +
+                    std::to_string(host_bytes) + ",\n  \"device_bytes\": " + std::to_string(device_bytes) +
+                    ",\n  \"vcfs\": [";
+    for (size_t i = 0; i < s.vcfs.size(); ++i) {
+        const VcfData &v = s.vcfs[i];
+        o += i ? ",\n    {" : "\n    {";
+        o += "\"location\": \"";
+        if (!json_escape_append(o, v.location.data(), v.location.size())) o += "?";
+        o += "\"";
+        o += ", \"sources\": [";
+        for (size_t k = 0; k < v.sources.size(); ++k) {
+            const SourceFile &f = v.sources[k];
+            if (k) o += ", ";
+            o += "{\"path\": \"";
+            if (!json_escape_append(o, f.path.data(), f.path.size())) o += "?";
+            o += "\", \"size\": " + std::to_string(f.size) + ", \"mtime_ns\": " + std::to_string(f.mtime_ns) +
+                 ", \"sample_hash\": \"" + std::to_string(f.sample_hash) + "\"}";
+        }
+        o += "]}";
+    }
+    o += "\n  ]\n}\n";
+    return o;
+}
+
+}  // namespace
+
+void store_save(sb_store &s, const std::string &dir) {
+    mkdir(dir.c_str(), 0755);
+    if (s.device >= 0) {
+        HIP_OK(hipSetDevice(s.device));
+        HIP_OK(hipStreamSynchronize(s.stream));
+    }
+    // device buffers, back to back: copied down through a pinned bounce (a
+    // host-only store (SB_HOST_ONLY) has none)
+    uint64_t dev_bytes = 0;
+    if (s.device >= 0) {
+        Writer w(dir + "/device.bin");
+        void *pin = nullptr;
+        const size_t chunk = size_t(64) << 20;
+        HIP_OK(hipHostMalloc(&pin, chunk, hipHostMallocDefault));
+        try {
+            for (const DeviceBuffer &b : s.bufs) {
+                for (size_t o = 0; o < b.bytes; o += chunk) {
+                    const size_t n = std::min(chunk, b.bytes - o);
+                    HIP_OK(hipMemcpy(pin, static_cast<const uint8_t *>(b.p) + o, n, hipMemcpyDeviceToHost));
+                    w.raw(pin, n);
+                }
+                w.pad(4096);
+            }
+        } catch (...) {
+            (void)hipHostFree(pin);
+            throw;
+        }
+        (void)hipHostFree(pin);
+        dev_bytes = w.at;
+    } else {
+        Writer w(dir + "/device.bin");  // empty: no device image
+    }
+    uint64_t host_bytes = 0;
+    {
+        Writer w(dir + "/host.bin");
+        w.pod(kMagic);
+        w.pod(kFormat);
+        w.pod<uint64_t>(s.n_records);
+        w.pod<uint64_t>(s.n_extra);
+        w.pod<uint32_t>(s.max_words);
+        w.pod<uint64_t>(s.n_keys);
+        host_columns(s, [&](auto &v) { w.vec(v); });
+        w.pod<uint64_t>(s.seg_slow_pos.size());
+        for (const auto &per_vcf : s.seg_slow_pos) {
+            w.pod<uint64_t>(per_vcf.size());
+            for (const auto &seg : per_vcf) w.vec(seg);
+        }
+        w.strs(s.vt.items);
+        w.strs(s.sym.items);
+        w.pod<uint64_t>(s.vcfs.size());
+        for (const VcfData &v : s.vcfs) put_vcf(w, v);
+        // kernel views and the buffers their pointers index
+        w.pod(s.d);
+        w.pod(s.ds);
+        w.pod(s.dk);
+        w.pod(s.g);
+        w.pod<uint64_t>(s.bufs.size());
+        for (const DeviceBuffer &b : s.bufs) {
+            w.pod<uint64_t>(reinterpret_cast<uint64_t>(b.p));
+            w.pod<uint64_t>(b.bytes);
+        }
+        w.pod(kMagic);
+        host_bytes = w.at;
+    }
+    const std::string m = manifest_text(s, host_bytes, dev_bytes);
+    FILE *f = fopen((dir + "/manifest.json").c_str(), "wb");
+    if (!f) throw Error(SB_EIO, "cannot write " + dir + "/manifest.json");
+    fwrite(m.data(), 1, m.size(), f);
+    fclose(f);
+}
+
+// dir of a manifest path (or the directory itself)
+std::string store_dir(const std::string &p) {
+    const std::string tail = "/manifest.json";
+    if (p.size() >= tail.size() && p.compare(p.size() - tail.size(), tail.size(), tail) == 0)
+        return p.substr(0, p.size() - tail.size());
+    if (p == "manifest.json") return ".";
+    return p;
+}
+
+sb_store *store_open(const std::string &path, int device, std::string *stale) {
+    const std::string dir = store_dir(path);
+    Reader r;
+    r.b = read_file(dir + "/host.bin");
+    if (r.pod<uint64_t>() != kMagic || r.pod<uint32_t>() != kFormat)
+        throw Error(SB_EIO, "persisted store: not a store file of this format (" + dir + ")");
+    auto s = std::make_unique<sb_store>();
+    s->n_records = r.pod<uint64_t>();
+    s->n_extra = r.pod<uint64_t>();
+    s->max_words = r.pod<uint32_t>();
+    s->n_keys = r.pod<uint64_t>();
+    host_columns(*s, [&](auto &v) { r.vec(v); });
+    s->seg_slow_pos.resize(r.pod<uint64_t>());
+    for (auto &per_vcf : s->seg_slow_pos) {
+        per_vcf.resize(r.pod<uint64_t>());
+        for (auto &seg : per_vcf) r.vec(seg);
+    }
+    for (const std::string &x : r.strs()) s->vt.get(x);
+    for (const std::string &x : r.strs()) s->sym.get(x);
+    s->vcfs.resize(r.pod<uint64_t>());
+    for (VcfData &v : s->vcfs) get_vcf(r, v);
+    // sources changed since the save: the caller re-ingests this store
+    for (const VcfData &v : s->vcfs)
+        for (const SourceFile &f : v.sources) {
+            const SourceFile now = fingerprint(f.path);
+            if (now.size != f.size || now.mtime_ns != f.mtime_ns || now.sample_hash != f.sample_hash) {
+                if (stale) *stale += (stale->empty() ? "" : "\n") + f.path;
+            }
+        }
+    if (stale && !stale->empty()) return nullptr;
+    s->d = r.pod<DStore>();
+    s->ds = r.pod<SStore>();
+    s->dk = r.pod<KStore>();
+    s->g = r.pod<GStore>();
+    std::vector<DeviceBuffer> old(r.pod<uint64_t>());
+    for (DeviceBuffer &b : old) {
+        b.p = reinterpret_cast<void *>(r.pod<uint64_t>());
+        b.bytes = r.pod<uint64_t>();
+    }
+    if (r.pod<uint64_t>() != kMagic) throw Error(SB_EIO, "persisted store: corrupt host.bin");
+    for (uint32_t i = 0; i < s->vcfs.size(); ++i) s->vcf_by_location.emplace(s->vcfs[i].location, i);
+    if (device == SB_HOST_ONLY) {  // the host side only (planning, region files, index)
+        s->device = SB_HOST_ONLY;
+        s->d = DStore{};
+        s->ds = SStore{};
+        s->dk = KStore{};
+        s->g = GStore{};
+        return s.release();
+    }
+    if (old.empty() && s->n_records)
+        throw Error(SB_EINVAL, "persisted store: saved from a host-only store (no device image); open it SB_HOST_ONLY");
+    // device image: the buffers re-allocated in order, streamed up
+    int n_dev = 0;
+    HIP_OK(hipGetDeviceCount(&n_dev));
+    if (device < 0 || device >= n_dev) throw Error(SB_EHIP, "device ordinal out of range");
+    s->device = device;
+    HIP_OK(hipSetDevice(device));
+    HIP_OK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    FILE *f = fopen((dir + "/device.bin").c_str(), "rb");
+    if (!f) throw Error(SB_EIO, "cannot open " + dir + "/device.bin");
+    const size_t chunk = size_t(64) << 20;
+    std::array<void *, 2> pin{nullptr, nullptr};
+    std::array<hipEvent_t, 2> done{nullptr, nullptr};
+    try {
+        for (int k = 0; k < 2; ++k) {
+            HIP_OK(hipHostMalloc(&pin[k], chunk, hipHostMallocDefault));
+            HIP_OK(hipEventCreate(&done[k]));
+        }
+        int k = 0;
+        uint64_t at = 0;
+        for (const DeviceBuffer &o : old) {
+            DeviceBuffer b;
+            b.bytes = o.bytes;
+            HIP_OK(hipMalloc(&b.p, b.bytes));
+            s->bufs.push_back(b);
+            s->device_bytes += b.bytes;
+            // double-buffered: the read of chunk n + 1 overlaps the copy of chunk n
+            for (size_t off = 0; off < b.bytes; off += chunk) {
+                const size_t n = std::min(chunk, b.bytes - off);
+                HIP_OK(hipEventSynchronize(done[k]));
+                if (fread(pin[k], 1, n, f) != n) throw Error(SB_EIO, "persisted store: truncated device.bin");
+                HIP_OK(hipMemcpyAsync(static_cast<uint8_t *>(b.p) + off, pin[k], n, hipMemcpyHostToDevice, s->stream));
+                HIP_OK(hipEventRecord(done[k], s->stream));
+                k ^= 1;
+                at += n;
+            }
+            const uint64_t padded = (at + 4095) / 4096 * 4096;
+            if (padded != at && fseek(f, static_cast<long>(padded - at), SEEK_CUR) != 0)
+                throw Error(SB_EIO, "persisted store: truncated device.bin");
+            at = padded;
+        }
+        HIP_OK(hipStreamSynchronize(s->stream));
+    } catch (...) {
+        fclose(f);
+        for (int k = 0; k < 2; ++k) {
+            if (pin[k]) (void)hipHostFree(pin[k]);
+            if (done[k]) (void)hipEventDestroy(done[k]);
+        }
+        throw;
+    }
+    fclose(f);
+    for (int k = 0; k < 2; ++k) {
+        (void)hipHostFree(pin[k]);
+        (void)hipEventDestroy(done[k]);
+    }
+    // remap: every view word inside an old buffer now points into its new copy
+    auto remap = [&](uint64_t *w, size_t n) {
+        for (size_t i = 0; i < n; ++i) {
+            if (!w[i]) continue;
+            for (size_t b = 0; b < old.size(); ++b) {
+                const uint64_t base = reinterpret_cast<uint64_t>(old[b].p);
+                if (w[i] >= base && w[i] < base + old[b].bytes) {
+                    w[i] = reinterpret_cast<uint64_t>(s->bufs[b].p) + (w[i] - base);
+                    break;
+                }
+            }
+        }
+    };
+    remap(words(s->d), sizeof(DStore) / 8);
+    remap(words(s->ds), sizeof(SStore) / 8);
+    remap(words(s->dk), sizeof(KStore) / 8);
+    remap(words(s->g), sizeof(GStore) / 8);
+    return s.release();
+}
+
+}  // namespace sb

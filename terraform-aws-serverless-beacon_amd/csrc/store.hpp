@@ -72,8 +72,19 @@ struct BucketIndex {  // coarse POS index of one segment
     uint32_t n = 0;      // buckets; bucket[off + n] = segment end
 };
 
+// a source file of a VCF (sb_builder_add_file): what sb_store_open checks
+// to tell whether the persisted store still describes it
+struct SourceFile {
+    std::string path;
+    uint64_t size = 0;
+    int64_t mtime_ns = 0;
+    uint64_t sample_hash = 0;  // of the first and last 64 KiB
+};
+SourceFile fingerprint(const std::string &path);  // persist.cpp
+
 struct VcfData {
     std::string location;
+    std::vector<SourceFile> sources;  // the files it was read from (none: text)
     // shard builds (sb_builder_set_record_range): keep records [rec_lo, rec_hi) of the file
     uint64_t rec_lo = 0, rec_hi = UINT64_MAX, lines_seen = 0;
     std::vector<std::string> samples;

@@ -16,6 +16,10 @@ SB_OK = 0
 SB_GRAN = {'boolean': 0, 'count': 1, 'aggregated': 2, 'record': 3}
 
 
+SB_ESTALE = -7  # sb_store_open: a source VCF changed since the save
+SB_HOST_ONLY = -1  # sb_builder_finish / sb_store_open: no device image
+
+
 class SbError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f'sbeacon error {code}: {msg}')
@@ -221,6 +225,8 @@ SIGNATURES = {
     'sb_requests_time_eval': (C.c_int, [P, C.c_int]),
     'sb_requests_inexact_rows': (C.c_int, [P, P]),
     'sb_store_trim': (C.c_int, [P]),
+    'sb_store_save': (C.c_int, [P, C.c_char_p]),
+    'sb_store_open': (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]),
     'sb_perform_query_events': (C.c_int, [C.POINTER(P), C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32,
                                           C.POINTER(P)]),
     'sb_json_out_get': (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),

@@ -139,6 +139,14 @@ def queries_from_payloads(payloads: list[dict], vcf_id, *, strict_variant_type: 
     return arr, [buf]
 
 
+class StaleStore(Exception):
+    """A persisted store whose source VCFs changed since it was saved."""
+
+    def __init__(self, paths):
+        super().__init__('stale store: ' + ', '.join(paths))
+        self.paths = list(paths)
+
+
 class Store:
     """An immutable HBM store built from VCF files or text."""
 
@@ -202,6 +210,30 @@ class Store:
     def trim(self):
         """Free the buffers cached for request batches (sb_store_trim)."""
         check(lib().sb_store_trim(self._h))
+
+    # ---------------------------------------------------------------- persist
+    def save(self, directory: str):
+        """Write the store to ``directory`` (sb_store_save) with a sidecar of
+        its locations and source paths."""
+        import json
+        check(lib().sb_store_save(self._h, os.fsencode(directory)))
+        with open(os.path.join(directory, 'sbeacon.json'), 'w') as f:
+            json.dump({'locations': self.locations, 'paths': self.paths}, f)
+
+    @classmethod
+    def open(cls, directory: str, *, device: int = 0):
+        """Re-create a saved store (sb_store_open) without re-reading any VCF.
+        Raises StaleStore (listing the changed source files) when a source
+        changed since the save."""
+        import json
+        s = C.c_void_p()
+        rc = lib().sb_store_open(os.fsencode(directory), int(device), C.byref(s))
+        if rc == _lib.SB_ESTALE:
+            raise StaleStore(lib().sb_last_error().decode().split('\n'))
+        check(rc)
+        with open(os.path.join(directory, 'sbeacon.json')) as f:
+            meta = json.load(f)
+        return cls(s, meta['locations'], meta['paths'])
 
     def close(self):
         if self._h:

@@ -10,7 +10,13 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; tail -2 $OUT/$name.log | cut -c1-300
   case $rc in 0) return 0;; *) exit $rc;; esac
 }
-step tests 400 python3 -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread -k "requests or genome or chains"
+step tests 400 python3 -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread -k "requests or genome or chains or dedup"
 step genome 600 python3 -u $R/bench.py --no-cpu-baseline
 grep -o '"device_ms_per_step[^}]*}' $OUT/genome.log
+SBEACON_DEDUP_DEBUG=1 step paths 500 python3 -u $R/bench_paths.py --datasets 50 --only dedup --no-cpu-baseline --strict-datasets 0
+cd /tmp
+step dsq1 500 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU --kernel-trace --output-format csv -d $OUT/dsq1 -o run -- python3 $R/bench_paths.py --datasets 50 --only dedup --steps 2 --warmup 1 --no-cpu-baseline --strict-datasets 0
+step dsq2 500 rocprofv3 --pmc SQ_WAVES SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS --kernel-trace --output-format csv -d $OUT/dsq2 -o run -- python3 $R/bench_paths.py --datasets 50 --only dedup --steps 2 --warmup 1 --no-cpu-baseline --strict-datasets 0
+cd $R
+python3 tools/sq_summary.py $OUT/dsq1 $OUT/dsq2 > $OUT/dsq_summary.txt 2>&1; grep "window_dedupe\|deferred" $OUT/dsq_summary.txt | cut -c1-600
 exit 0
