@@ -1,19 +1,22 @@
 #!/usr/bin/env python3
 """Config 3 bench (the default of ``python bench.py``): whole-genome
-1000G-shape store sharded by contig across the GPUs (sbeacon/genome.py) and
-variantType Beacon requests -- 1 M per GPU (weak scaling, the default: N M
-genome-wide requests routed to the shards by position) or 1 M in total
-(``--scaling strong``).
+1000G-shape store sharded across the GPUs by the product sharder
+(sbeacon.sharding.ShardPlan over the generated genome VCF: record-balanced
+(contig, POS) cores + 10 kb halo) and variantType Beacon requests -- 1 M per
+GPU (weak scaling, the default: N M genome-wide requests routed to the shards
+by ShardPlan.route / slice_runs) or 1 M in total (``--scaling strong``).
 
-One step = every rank answers the slices in its core (chain_kernel: one wave
-per request's slices), reduces them into per-request rows
-(sb_batch_reduce_requests), writes the rows' dense hit lists with global
-record ids (sb_batch_compact_hits), and delivers rows + hits to each
-request's host-facing rank (sbeacon.shard.ResultExchange: all_gather of
-counts, then RCCL send/recv over xGMI of the straddling requests' rows and
-hits; ``--deliver rank0`` sends everything to rank 0).  Barrier +
+One step = every rank runs its request batch (request_eval_kernel: each
+request's slices on this rank as one chain; request_tile_scan_kernel +
+request_deliver_kernel: request rows, row offsets and dense hit lists with
+global record ids), then delivers rows + hits to each request's host-facing
+rank (sbeacon.shard.ResultExchange: sizes gathered once per batch, then one
+RCCL send/recv group over xGMI per step for the straddling requests;
+``--deliver rank0`` sends everything to rank 0).  Barrier +
 torch.cuda.synchronize() bracket the K timed steps; the time is the max over
-ranks.  Prints one JSON line on rank 0.
+ranks.  Prints one JSON line on rank 0.  tests/test_bench_step_gloo.py runs
+this step (shard_setup + make_step) at world 2 over gloo against the
+unsharded oracle.
 """
 from __future__ import annotations
 
@@ -48,9 +51,8 @@ def main_genome(args):
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group('nccl', device_id=dev)
-    from sbeacon.genome import (GenomeShape, config3_requests, first_rank_of_rows, prepare_shard_requests,
-                                shard_record_base, shard_requests, union_rows, shard_slices)
-    from sbeacon.shard import ResultExchange, owner_ranks
+    from sbeacon.genome import GenomeShape, config3_requests, prepare_shard_requests, union_rows, shard_slices
+    from sbeacon.shard import ResultExchange
 
     t0 = time.perf_counter()
     shape = GenomeShape(n_total=args.genome_records, seed=3)
@@ -72,7 +74,7 @@ def main_genome(args):
     n_req = args.genome_requests * (world if args.scaling == 'weak' else 1)
     reqs = config3_requests(shape, n=n_req, seed=1003)
     t0 = time.perf_counter()
-    sr = shard_requests(shape, reqs, world, rank)  # the splitQuery slices on this rank, per request
+    sr, owners, base = shard_setup(shape, reqs, world, rank, args.deliver)  # ShardPlan routing
     batch = prepare_shard_requests(store, sr)      # request batch: planning + upload (C++)
     t_prepare = time.perf_counter() - t0
     batch.set_stream(torch.cuda.current_stream().cuda_stream)  # one stream: kernels, torch ops, RCCL
@@ -80,17 +82,15 @@ def main_genome(args):
     part = torch.zeros((max(sr.n_rows, 1), 5), dtype=torch.int64, device=dev)
     hits = torch.zeros(max(int(pst['hits']), 1), dtype=torch.int64, device=dev)
     row_off = torch.zeros(sr.n_rows + 1, dtype=torch.int64, device=dev)
-    base = shard_record_base(shape, world, rank)
     sl = shard_slices(shape, reqs, world, rank)  # slice view (statistics / roofline pricing only)
-    owners = owner_ranks(first_rank_of_rows(shape, reqs, world, sl), args.deliver, rank)
     ex = ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, dev)
     log(f'[rank {rank}] {n_req} requests, {len(sl)} slices on this rank (rows {sr.row_lo}+{sr.n_rows}, '
         f'{pst["chains"]} chains), delivery {args.deliver}: owns {ex.n_own} rows, receives {len(ex.recvs)} '
         f'range(s), prepare {t_prepare:.2f} s')
 
-    def step():  # answer + deliver: request rows + dense hit lists (one kernel), exchange
-        batch.run(part.data_ptr(), hits.data_ptr(), row_off.data_ptr(), base)
-        ex.exchange(part, hits, row_off)
+    # answer + deliver: request rows + dense hit lists (one pass), exchange
+    step = make_step(lambda p, h, o: batch.run(p.data_ptr(), h.data_ptr(), o.data_ptr(), base), ex, part, hits,
+                     row_off)
 
     for _ in range(args.warmup):
         step()
@@ -231,6 +231,32 @@ def main_genome(args):
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def shard_setup(shape, reqs, world, rank, deliver):
+    """One rank's routing, all through the product sharder
+    (sbeacon.sharding.ShardPlan over the genome's layout, GenomeShape.plan):
+    its sub-requests (ShardPlan.slice_runs: the splitQuery slices whose first
+    base its core holds), the host-facing rank of each of its rows
+    (ShardPlan.route of the request's first slice, or rank 0) and the first
+    record of its store (ShardPlan.record_range)."""
+    import numpy as np
+    from sbeacon.genome import rank_of_slices, shard_record_base, shard_requests
+    from sbeacon.shard import owner_ranks
+    sr = shard_requests(shape, reqs, world, rank)
+    rows = sr.row_lo + np.arange(sr.n_rows)
+    first = rank_of_slices(shape, world, reqs.ci[rows], reqs.start[rows] + 1)
+    return sr, owner_ranks(first, deliver, rank), shard_record_base(shape, world, rank)
+
+
+def make_step(run, ex, part, hits, row_off):
+    """The bench step: ``run(part, hits, row_off)`` answers the rank's
+    sub-requests into its rows / dense hit lists, then ResultExchange
+    delivers them to their host-facing ranks.  Returns the owned rows."""
+    def step():
+        run(part, hits, row_off)
+        return ex.exchange(part, hits, row_off)
+    return step
 
 
 def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5):

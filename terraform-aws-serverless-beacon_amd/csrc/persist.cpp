@@ -18,7 +18,9 @@
 //   <dir>/host.bin       host columns + VCF metadata + kernel views
 //   <dir>/device.bin     the device buffers, back to back (4 KiB aligned)
 #include <hip/hip_runtime.h>
+#include <fcntl.h>
 #include <sys/stat.h>
+#include <unistd.h>
 
 #include <array>
 #include <chrono>
@@ -435,17 +437,17 @@ sb_store *store_open(const std::string &path, int device, std::string *stale) {
     s->device = device;
     HIP_OK(hipSetDevice(device));
     HIP_OK(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    FILE *f = fopen((dir + "/device.bin").c_str(), "rb");
-    if (!f) throw Error(SB_EIO, "cannot open " + dir + "/device.bin");
-    const size_t chunk = size_t(64) << 20;
-    std::array<void *, 2> pin{nullptr, nullptr};
-    std::array<hipEvent_t, 2> done{nullptr, nullptr};
-    try {
-        for (int k = 0; k < 2; ++k) {
-            HIP_OK(hipHostMalloc(&pin[k], chunk, hipHostMallocDefault));
-            HIP_OK(hipEventCreate(&done[k]));
-        }
-        int k = 0;
+    // the buffers re-allocated in order; their bytes cut into 32 MiB pieces
+    // that 8 threads read (pread, page cache) into their own pinned pair and
+    // copy up on their own streams
+    struct Piece {
+        uint64_t file_off;
+        void *dst;
+        size_t n;
+    };
+    std::vector<Piece> pieces;
+    {
+        const size_t chunk = size_t(32) << 20;
         uint64_t at = 0;
         for (const DeviceBuffer &o : old) {
             DeviceBuffer b;
@@ -453,35 +455,58 @@ sb_store *store_open(const std::string &path, int device, std::string *stale) {
             HIP_OK(hipMalloc(&b.p, b.bytes));
             s->bufs.push_back(b);
             s->device_bytes += b.bytes;
-            // double-buffered: the read of chunk n + 1 overlaps the copy of chunk n
-            for (size_t off = 0; off < b.bytes; off += chunk) {
-                const size_t n = std::min(chunk, b.bytes - off);
-                HIP_OK(hipEventSynchronize(done[k]));
-                if (fread(pin[k], 1, n, f) != n) throw Error(SB_EIO, "persisted store: truncated device.bin");
-                HIP_OK(hipMemcpyAsync(static_cast<uint8_t *>(b.p) + off, pin[k], n, hipMemcpyHostToDevice, s->stream));
-                HIP_OK(hipEventRecord(done[k], s->stream));
-                k ^= 1;
-                at += n;
+            for (size_t off = 0; off < b.bytes; off += chunk)
+                pieces.push_back(Piece{at + off, static_cast<uint8_t *>(b.p) + off, std::min(chunk, b.bytes - off)});
+            at = (at + b.bytes + 4095) / 4096 * 4096;
+        }
+    }
+    const int fd = ::open((dir + "/device.bin").c_str(), O_RDONLY);
+    if (fd < 0) throw Error(SB_EIO, "cannot open " + dir + "/device.bin");
+    const unsigned nt = static_cast<unsigned>(std::min<size_t>(8, std::max<size_t>(1, pieces.size())));
+    std::vector<std::string> errs(nt);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            std::array<void *, 2> pin{nullptr, nullptr};
+            std::array<hipEvent_t, 2> done{nullptr, nullptr};
+            hipStream_t st = nullptr;
+            try {
+                HIP_OK(hipSetDevice(device));
+                HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+                for (int k = 0; k < 2; ++k) {
+                    HIP_OK(hipHostMalloc(&pin[k], size_t(32) << 20, hipHostMallocDefault));
+                    HIP_OK(hipEventCreate(&done[k]));
+                }
+                int k = 0;
+                for (size_t q = t; q < pieces.size(); q += nt) {  // double-buffered: read n + 1 while n copies
+                    const Piece &pc = pieces[q];
+                    HIP_OK(hipEventSynchronize(done[k]));
+                    size_t got = 0;
+                    while (got < pc.n) {
+                        const ssize_t r = pread(fd, static_cast<uint8_t *>(pin[k]) + got, pc.n - got,
+                                                static_cast<off_t>(pc.file_off + got));
+                        if (r <= 0) throw Error(SB_EIO, "persisted store: truncated device.bin");
+                        got += static_cast<size_t>(r);
+                    }
+                    HIP_OK(hipMemcpyAsync(pc.dst, pin[k], pc.n, hipMemcpyHostToDevice, st));
+                    HIP_OK(hipEventRecord(done[k], st));
+                    k ^= 1;
+                }
+                HIP_OK(hipStreamSynchronize(st));
+            } catch (const std::exception &e) {
+                errs[t] = e.what();
+                if (st) (void)hipStreamSynchronize(st);
             }
-            const uint64_t padded = (at + 4095) / 4096 * 4096;
-            if (padded != at && fseek(f, static_cast<long>(padded - at), SEEK_CUR) != 0)
-                throw Error(SB_EIO, "persisted store: truncated device.bin");
-            at = padded;
-        }
-        HIP_OK(hipStreamSynchronize(s->stream));
-    } catch (...) {
-        fclose(f);
-        for (int k = 0; k < 2; ++k) {
-            if (pin[k]) (void)hipHostFree(pin[k]);
-            if (done[k]) (void)hipEventDestroy(done[k]);
-        }
-        throw;
-    }
-    fclose(f);
-    for (int k = 0; k < 2; ++k) {
-        (void)hipHostFree(pin[k]);
-        (void)hipEventDestroy(done[k]);
-    }
+            for (int k = 0; k < 2; ++k) {
+                if (pin[k]) (void)hipHostFree(pin[k]);
+                if (done[k]) (void)hipEventDestroy(done[k]);
+            }
+            if (st) (void)hipStreamDestroy(st);
+        });
+    for (auto &x : th) x.join();
+    ::close(fd);
+    for (const std::string &e : errs)
+        if (!e.empty()) throw Error(SB_EIO, "persisted store: " + e);
     // remap: every view word inside an old buffer now points into its new copy
     auto remap = [&](uint64_t *w, size_t n) {
         for (size_t i = 0; i < n; ++i) {

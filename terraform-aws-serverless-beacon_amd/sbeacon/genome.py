@@ -47,6 +47,39 @@ VMIN = [0, 0, 1, 5]
 VMAX = [-1, -1, 10, 50, 1000]
 
 
+class _GenomePositions:
+    """POS of every genome record, in genome order, read from the contig
+    generators on demand (index or slice; a slice within one contig is a
+    view)."""
+
+    def __init__(self, shape):
+        self.shape = shape
+
+    def __len__(self):
+        return int(self.shape.n_total)
+
+    def _contig(self, g):
+        return int(np.searchsorted(self.shape.offsets, g, side='right') - 1)
+
+    def __getitem__(self, k):
+        off = self.shape.offsets
+        if isinstance(k, slice):
+            a, b, step = k.indices(len(self))
+            assert step == 1
+            if b <= a:
+                return np.zeros(0, dtype=np.uint32)
+            out = []
+            while a < b:
+                ci = self._contig(a)
+                e = min(b, int(off[ci + 1]))
+                out.append(self.shape.gen(ci).positions()[a - int(off[ci]):e - int(off[ci])])
+                a = e
+            return out[0] if len(out) == 1 else np.concatenate(out)
+        g = int(k)
+        ci = self._contig(g)
+        return self.shape.gen(ci).positions()[g - int(off[ci])]
+
+
 class GenomeShape:
     def __init__(self, *, n_total: int = 85_000_000, seed: int = 3, n_samples: int = 2504):
         self.seed, self.n_total, self.n_samples = seed, n_total, n_samples
@@ -73,57 +106,73 @@ class GenomeShape:
         return int(p[0]), int(p[-1])
 
     # ------------------------------------------------------------- sharding
+    # The genome is one VCF (LOCATION) of the contigs in order; it is cut by
+    # the product sharder, sbeacon.sharding.ShardPlan, over a layout whose POS
+    # column is read lazily from the generators (the plan only reads it at
+    # the cut contigs), so a deployment over real VCF files and this bench
+    # run the same cuts, routing, halo and sub-request split.
+    def layout(self):
+        from .sharding import VcfLayout
+        contigs = [(c, int(self.offsets[ci]), int(self.offsets[ci + 1])) for ci, c in enumerate(CONTIGS)]
+        return VcfLayout(LOCATION, LOCATION, contigs, _GenomePositions(self))
+
+    def plan(self, world: int):
+        """The ShardPlan of `world` ranks (cached)."""
+        plans = self.__dict__.setdefault('_plans', {})
+        p = plans.get(world)
+        if p is None:
+            from .sharding import ShardPlan
+            p = plans[world] = ShardPlan([self.layout()], world, HALO)
+        return p
+
     def cuts(self, world: int):
-        """world + 1 cut points (contig index, POS); rank r's core is
-        [cuts[r], cuts[r + 1]) in lexicographic order."""
-        out = [(0, 0)]
-        for r in range(1, world):
-            g = r * self.n_total // world
-            ci = int(np.searchsorted(self.offsets, g, side='right') - 1)
-            i = g - int(self.offsets[ci])
-            out.append((ci, int(self.gen(ci).positions()[i])))
-        out.append((len(CONTIGS), 0))
-        return out
+        """world + 1 cut points (contig index, POS): rank r's core is
+        [cuts[r], cuts[r + 1]) in lexicographic order (the plan's keys)."""
+        keys = self.plan(world).keys
+        return [(0, 0)] + [(int(k[1]), int(k[2])) for k in keys[1:]] + [(len(CONTIGS), 0)]
 
     def shard_pieces(self, world: int, rank: int):
         """[(contig index, record lo, record hi)] of rank's store: its core
-        plus the right halo (records of the cut contig with POS < P + HALO)."""
-        cuts = self.cuts(world)
-        (c0, p0), (c1, p1) = cuts[rank], cuts[rank + 1]
+        plus the right halo (ShardPlan.record_range)."""
+        lo, hi = self.plan(world).record_range(rank, 0)
         pieces = []
-        for ci in range(c0, min(c1, len(CONTIGS) - 1) + 1):
-            pos = self.gen(ci).positions()
-            lo = int(np.searchsorted(pos, p0, side='left')) if ci == c0 else 0
-            if ci == c1:
-                hi = int(np.searchsorted(pos, p1 + HALO, side='left'))  # halo into the next rank's core
-            else:
-                hi = len(pos)
-            if hi > lo:
-                pieces.append((ci, lo, hi))
+        for ci in range(len(CONTIGS)):
+            a, b = max(lo, int(self.offsets[ci])), min(hi, int(self.offsets[ci + 1]))
+            if b > a:
+                pieces.append((ci, a - int(self.offsets[ci]), b - int(self.offsets[ci])))
         return pieces
 
-    def shard_chunks(self, world: int, rank: int, chunk=1 << 20, threads=0, progress=None):
-        """VCF text of rank's shard (one VCF, contigs in order, sites only).
-        Large chunks: the builder parses each chunk with all its threads."""
-        pieces = self.shard_pieces(world, rank)
+    def text(self, lo: int, hi: int, chunk=1 << 20, threads=0, progress=None):
+        """VCF text (header + records [lo, hi) in genome order, sites only) in
+        large chunks: the builder parses each chunk with all its threads."""
         first = True
         done = 0
-        for ci, lo, hi in pieces:
-            g = self.gen(ci)
+        for ci in range(len(CONTIGS)):
+            a, b = max(lo, int(self.offsets[ci])), min(hi, int(self.offsets[ci + 1]))
             if first:
-                yield g.header(sites_only=True)
+                yield self.gen(ci).header(sites_only=True)
                 first = False
-            for a in range(lo, hi, chunk):
-                b = min(a + chunk, hi)
-                yield g.records(a, b, sites_only=True, threads=threads)
-                done += b - a
+            if b <= a:
+                continue
+            g = self.gen(ci)
+            a, b = a - int(self.offsets[ci]), b - int(self.offsets[ci])
+            for x in range(a, b, chunk):
+                y = min(x + chunk, b)
+                yield g.records(x, y, sites_only=True, threads=threads)
+                done += y - x
                 if progress:
                     progress(CONTIGS[ci], done)
 
+    def shard_chunks(self, world: int, rank: int, chunk=1 << 20, threads=0, progress=None):
+        """VCF text of rank's shard (one VCF, contigs in order, sites only)."""
+        lo, hi = self.plan(world).record_range(rank, 0)
+        return self.text(lo, hi, chunk, threads, progress)
+
     def build_shard_store(self, world: int, rank: int, *, device=0, threads=0, progress=None):
-        from .engine import Store
-        return Store.build([(LOCATION, self.shard_chunks(world, rank, threads=threads, progress=progress))],
-                           device=device, keep_genotypes=False, n_threads=threads)
+        """Rank's store, built by ShardPlan.build_store from the generated text."""
+        return self.plan(world).build_store(
+            rank, device=device, keep_genotypes=False, n_threads=threads,
+            text=lambda v, lo, hi: self.text(lo, hi, threads=threads, progress=progress))
 
     def shard_records(self, world: int, rank: int) -> int:
         return sum(hi - lo for _, lo, hi in self.shard_pieces(world, rank))
@@ -196,10 +245,9 @@ def request_slices(reqs: Requests):
 
 
 def rank_of_slices(shape: GenomeShape, world: int, ci: np.ndarray, a: np.ndarray) -> np.ndarray:
-    cuts = shape.cuts(world)
-    key = ci.astype(np.int64) * (1 << 32) + a
-    ck = np.array([c * (1 << 32) + p for c, p in cuts], dtype=np.int64)
-    return np.searchsorted(ck, key, side='right') - 1
+    """Rank answering slices with first base a on contig ci (ShardPlan.route)."""
+    ci = np.asarray(ci, dtype=np.int64)
+    return shape.plan(world).route(np.zeros_like(ci), ci, a)
 
 
 def shard_slices(shape: GenomeShape, reqs: Requests, world: int, rank: int) -> ShardSlices:
@@ -342,11 +390,7 @@ def shard_record_base(shape: GenomeShape, world: int, rank: int) -> int:
     """Global record index (contig order) of the first record of rank's shard
     store: shard record i is global record base + i (its pieces are
     consecutive in that order)."""
-    pieces = shape.shard_pieces(world, rank)
-    if not pieces:
-        return 0
-    ci, lo, _ = pieces[0]
-    return int(shape.offsets[ci]) + lo
+    return shape.plan(world).record_base(rank, 0)
 
 
 @dataclass
@@ -386,20 +430,14 @@ def shard_requests(shape: GenomeShape, reqs: Requests, world: int, rank: int) ->
     n = len(smin)
     e0 = int(np.searchsorted(ci, c0, side='right'))  # rows [0, e0): contig c0
     s1 = int(np.searchsorted(ci, c1, side='left'))   # rows [s1, n): contig c1
-    ceil_div = lambda a: -((-a) // SPLIT_SIZE)  # noqa: E731
-    # (first row, last row, the cut at the start applies, the cut at the end applies)
-    segs = [(0, n, True, True)] if c0 == c1 else [(0, e0, True, False), (s1, n, False, True)]
-    cut = []  # (x0, has, a, b) of each cut contig's rows
-    for x0, x1, at0, at1 in segs:
+    plan = shape.plan(world)
+    segs = [(0, n)] if c0 == c1 else [(0, e0), (s1, n)]
+    cut = []  # (x0, has, a, b) of each cut contig's rows: the plan's splitQuery cut
+    for x0, x1 in segs:
         if x1 <= x0:
             continue
-        sm, sx = smin[x0:x1], smax[x0:x1]
-        nsl = (sx - sm) // SPLIT_SIZE + 1
-        k0 = np.minimum(np.clip(ceil_div(p0 - sm), 0, None), nsl) if at0 else np.zeros_like(nsl)
-        k1 = np.clip(np.clip(ceil_div(p1 - sm), 0, None), k0, nsl) if at1 else nsl
-        has = k1 > k0
-        aa = sm + SPLIT_SIZE * k0
-        cut.append((x0, has, aa, np.where(has, np.minimum(sx, sm + SPLIT_SIZE * k1 - 1), aa - 1)))
+        aa, bb = plan.slice_runs(rank, 0, ci[x0:x1], smin[x0:x1], smax[x0:x1])
+        cut.append((x0, bb >= aa, aa, bb))
     # the first and last rows with a slice here (rows between the cut contigs have all of theirs)
     firsts, lasts = [], []
     for x0, has, _, _ in cut:

@@ -118,7 +118,7 @@ def config5_slices(shape: GnomadShape, rank: int, n_requests: int, seed: int = 1
     spans = []
     for ci in range(c0, min(c1, len(CONTIGS) - 1) + 1):
         lo_c, hi_c = shape.span(ci)
-        lo = p0 if ci == c0 else lo_c
+        lo = max(p0, lo_c) if ci == c0 else lo_c
         hi = (p1 - 1) if ci == c1 else hi_c
         if hi > lo:
             spans.append((ci, lo, hi))

@@ -160,8 +160,11 @@ class ShardPlan:
         return lo, hi
 
     # ---------------------------------------------------------------- stores
-    def build_store(self, rank: int, *, device: int = 0, keep_genotypes: bool = True, n_threads: int = 0):
-        """Rank r's store: every VCF of the plan restricted to its record range."""
+    def build_store(self, rank: int, *, device: int = 0, keep_genotypes: bool = True, n_threads: int = 0,
+                    text=None):
+        """Rank r's store: every VCF of the plan restricted to its record range.
+        ``text(v, lo, hi)``, when given, yields VCF v's header + records
+        [lo, hi) as text chunks (a generated VCF) instead of reading its file."""
         from ._lib import BuildOpts
         from .engine import Store
         L = lib()
@@ -173,13 +176,22 @@ class ShardPlan:
                 lb = lay.location.encode()
                 check(L.sb_builder_begin_vcf(b, lb, len(lb), C.byref(vid)))
                 lo, hi = self.record_range(rank, v)
-                check(L.sb_builder_set_record_range(b, vid.value, lo, hi))
-                check(L.sb_builder_add_file(b, vid.value, os.fsencode(lay.path)))
+                if text is None:
+                    check(L.sb_builder_set_record_range(b, vid.value, lo, hi))
+                    check(L.sb_builder_add_file(b, vid.value, os.fsencode(lay.path)))
+                else:
+                    for chunk in text(v, lo, hi):
+                        check(L.sb_builder_add_text(b, vid.value, chunk, len(chunk)))
             s = C.c_void_p()
             check(L.sb_builder_finish(b, int(device), C.byref(s)))
         finally:
             L.sb_builder_free(b)
-        return Store(s, [l.location for l in self.layouts], {l.location: l.path for l in self.layouts})
+        return Store(s, [l.location for l in self.layouts],
+                     {l.location: l.path for l in self.layouts if text is None})
+
+    def record_base(self, rank: int, v: int = 0) -> int:
+        """Ordinal within VCF v of the first record rank r's store holds."""
+        return self.record_range(rank, v)[0]
 
     # ---------------------------------------------------------------- routing
     def contig_index(self, v: int, chrom: str) -> int:
@@ -219,6 +231,34 @@ class ShardPlan:
             out[j] = r
         return out
 
+    def slice_runs(self, rank: int, v, c, smin, smax):
+        """Vectorised splitQuery cut (lambda/splitQuery/lambda_function.py:74-110)
+        of requests [smin, smax] on contig index c of VCF v: the sub-request
+        [a, b] of the slices (a = smin + 10000 k, k in [k0, k1)) whose first
+        base rank r's core holds; b < a when it holds none."""
+        v, c, smin, smax = (np.asarray(x, dtype=np.int64) for x in (v, c, smin, smax))
+        nsl = np.where(smax >= smin, (smax - smin) // SPLIT_SIZE + 1, 0)
+
+        # slice k's first base smin + 10000 k is routed monotonically in k: the
+        # run on rank r is [k0, k1) = slices routed >= r minus those routed > r
+        def first_k(rk):
+            """first slice index routed to rank >= rk (nsl if none)."""
+            if rk <= 0:
+                return np.zeros_like(nsl)
+            if rk >= self.world:
+                return nsl.copy()
+            kv, kc, kp = self.keys[rk]
+            out = np.where((v > kv) | ((v == kv) & (c > kc)), 0, nsl)
+            same = (v == kv) & (c == kc)
+            need = -((-(kp - smin)) // SPLIT_SIZE)  # ceil((kp - smin) / 10000)
+            return np.where(same, np.clip(need, 0, nsl), out)
+
+        k0, k1 = first_k(rank), first_k(rank + 1)
+        k1 = np.maximum(k1, k0)
+        a = smin + SPLIT_SIZE * k0
+        b = np.minimum(smax, smin + SPLIT_SIZE * k1 - 1)
+        return a, np.where(k1 > k0, b, a - 1)
+
     def split_requests(self, split_payloads: list[dict], rank: int):
         """The request-level fan-out on rank r: one sb_request per
         (SplitQueryPayload, vcf_location) pair -- every rank gets the same
@@ -233,27 +273,7 @@ class ShardPlan:
         c = np.array([self.contig_index(int(v[k]), chrom) for k, (_, _, chrom) in enumerate(rows)], dtype=np.int64)
         smin = np.array([int(p['start_min']) for p in P], dtype=np.int64)
         smax = np.array([int(p['start_max']) for p in P], dtype=np.int64)
-        nsl = np.where(smax >= smin, (smax - smin) // SPLIT_SIZE + 1, 0)
-        # slice k's first base smin + 10000 k is routed monotonically in k: the
-        # run on rank r is [k0, k1) = slices routed >= r minus those routed > r
-        def first_k(rk):
-            """first slice index routed to rank >= rk (nsl if none)."""
-            if rk <= 0:
-                return np.zeros(n, dtype=np.int64)
-            if rk >= self.world:
-                return nsl.copy()
-            kv, kc, kp = self.keys[rk]
-            out = np.where((v > kv) | ((v == kv) & (c > kc)), 0, nsl)
-            same = (v == kv) & (c == kc)
-            need = -((-(kp - smin)) // SPLIT_SIZE)  # ceil((kp - smin) / 10000)
-            out = np.where(same, np.clip(need, 0, nsl), out)
-            return out
-        k0, k1 = first_k(rank), first_k(rank + 1)
-        k1 = np.maximum(k1, k0)
-        a = smin + SPLIT_SIZE * k0
-        b = np.minimum(smax, smin + SPLIT_SIZE * k1 - 1)
-        b = np.where(k1 > k0, b, a - 1)
-        names = {}
+        a, b = self.slice_runs(rank, v, c, smin, smax)
 
         def codes(vals):
             d = {}
@@ -280,7 +300,6 @@ class ShardPlan:
             include_samples=[1 if pt.get('includeSamples', False) else 0 for pt in pts],
             selected_samples_only=[1 if pt.get('selectedSamplesOnly', False) else 0 for pt in pts],
             sample_names=sn_v, sample_names_code=sn_c)
-        del names
         return arr, keep, [(i, loc) for i, loc, _ in rows]
 
     # ---------------------------------------------------------------- text (tests)
