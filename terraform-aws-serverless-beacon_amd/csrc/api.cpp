@@ -2475,6 +2475,92 @@ bool strict_region_entries(const uint8_t *file, uint64_t size, uint64_t rs, uint
     return true;
 }
 
+// The same reader over a whole file, once (every entry read): what a call's
+// (rangeStart, rangeEnd) then selects follows in closed form.  Entries are
+// POS-sorted in a region file, so getVcfData skips a prefix [0, lo) (POS <
+// rangeStart) and reads on; the refills happen at the same entries on the
+// read and the skip path except where an entry's string crosses the end of
+// the buffer -- a skipped one leaves the read position past the data and the
+// next refill throws ("proccesData input invalid").  The loop stops after
+// the first entry at or past the final refill (`last`, more() false from
+// then on) whose POS exceeds rangeEnd; with no final refill before the last
+// entry it runs past the end and throws.
+struct FileProfile {
+    uint32_t n = 0;                   // entries
+    uint32_t last_fill = UINT32_MAX;  // entry during which the stream ended (more() false after it)
+    uint32_t fail_at = UINT32_MAX;    // entry at which the all-read walk failed (n: past the last)
+    bool sorted = true;               // POS non-decreasing (else: the walk per call)
+    bool consec = false;              // the entries' store keys are consecutive
+    std::vector<uint32_t> straddle;   // entries whose string crosses a refill
+    std::vector<uint64_t> vpos;
+};
+
+FileProfile profile_region_file(const uint8_t *file, uint64_t size) {
+    constexpr size_t kMin = sizeof(uint64_t) + sizeof(uint16_t);
+    char buf[1024];
+    size_t pos = 0, len = 0;
+    FileProfile P;
+    uint32_t entry = 0;
+    try {
+        RegionReader in(file, size, buf, sizeof buf);
+        in.start();
+        auto avail = [&](size_t need) -> bool {
+            if (len >= pos + need) return true;
+            if (!in.more()) return false;
+            len = in.fill(static_cast<uint32_t>(pos), static_cast<uint32_t>(len));
+            if (!in.more() && P.last_fill == UINT32_MAX) P.last_fill = entry;
+            if (len > 0) {
+                pos = 0;
+                return true;
+            }
+            return false;
+        };
+        do {
+            if (!avail(kMin)) {
+                P.fail_at = entry;
+                break;
+            }
+            uint64_t vpos;
+            uint16_t sl;
+            memcpy(&vpos, buf + pos, sizeof vpos);
+            pos += sizeof vpos;
+            memcpy(&sl, buf + pos, sizeof sl);
+            pos += sizeof sl;
+            if (len < pos + sl) P.straddle.push_back(entry);
+            if (!avail(sl)) {
+                P.fail_at = entry;
+                break;
+            }
+            pos += sl;
+            if (!P.vpos.empty() && vpos < P.vpos.back()) P.sorted = false;
+            P.vpos.push_back(vpos);
+            ++entry;
+        } while (len != pos || in.more());
+    } catch (const RefThrow &) {
+        P.fail_at = entry;
+    }
+    P.n = static_cast<uint32_t>(P.vpos.size());
+    return P;
+}
+
+// the entries [lo, last] getVcfData returns for (rs, re) (none when lo >
+// last); false = it throws
+bool profile_range(const FileProfile &P, uint64_t rs, uint64_t re, uint32_t &lo, uint32_t &last) {
+    const auto b = P.vpos.begin(), e = P.vpos.end();
+    lo = static_cast<uint32_t>(std::lower_bound(b, e, rs) - b);
+    const bool tail = !(P.last_fill < P.n);  // more() still true after the last entry
+    last = P.n ? P.n - 1 : 0;
+    if (!tail) {  // the first entry at or after the final refill with POS > re ends the loop
+        const uint32_t j = static_cast<uint32_t>(std::upper_bound(b + P.last_fill, e, re) - b);
+        if (j < P.n) last = j;
+    }
+    const uint32_t reach = tail ? P.n : last;  // the last entry the loop starts
+    if (P.fail_at != UINT32_MAX && P.fail_at <= reach) return false;
+    // a skipped entry whose string crosses the buffer end throws when the next entry starts
+    if (!P.straddle.empty() && P.straddle.front() < std::min(lo, reach)) return false;
+    return true;
+}
+
 // A slice's region files as summariseSlice writes them (gzip members, the
 // store key of every entry), kept per store: the reference writes them once
 // and every duplicateVariantSearch message reads them, so strict mode
@@ -2486,9 +2572,11 @@ struct SliceFiles {
     std::vector<uint8_t> data;
     std::vector<uint64_t> at;  // each file's first byte in data
     std::vector<std::vector<uint32_t>> keys;
+    std::vector<FileProfile> prof;  // per file (profile_region_file)
     size_t bytes() const {
         size_t b = data.size() + files.size() * sizeof(sb_region_file);
         for (const auto &k : keys) b += k.size() * 4;
+        for (const auto &f : prof) b += f.vpos.size() * 8 + f.straddle.size() * 4;
         return b;
     }
 };
@@ -2511,6 +2599,8 @@ void dedup_files(sb_store &s, const sb_dedup_file_job *jobs, size_t nj, uint64_t
         const SliceFiles *sf = nullptr;
         uint32_t file;
         bool ok = true;
+        bool walked = false;          // entries listed in incl (an unsorted file)
+        uint32_t e_lo = 0, e_hi = 0;  // else the entries [e_lo, e_hi)
         std::vector<uint32_t> incl;
     };
     std::vector<Pair> pairs;
@@ -2526,7 +2616,7 @@ void dedup_files(sb_store &s, const sb_dedup_file_job *jobs, size_t nj, uint64_t
             if (F.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "dedup job " + std::to_string(j) + ": unknown vcf id");
             const Key key = std::make_tuple(F.vcf_id, F.virtual_start, F.virtual_end);
             if (!C.m.count(key)) missing.push_back(key);
-            pairs.push_back(Pair{static_cast<uint32_t>(j), nullptr, F.file, true, {}});
+            pairs.push_back(Pair{static_cast<uint32_t>(j), nullptr, F.file, true, false, 0, 0, {}});
             pkey.push_back(key);
         }
     }
@@ -2544,6 +2634,13 @@ void dedup_files(sb_store &s, const sb_dedup_file_job *jobs, size_t nj, uint64_t
             for (const auto &f : sf->files) {
                 sf->at.push_back(a);
                 a += f.data_bytes;
+            }
+            for (size_t f = 0; f < sf->files.size(); ++f) {
+                sf->prof.push_back(profile_region_file(sf->data.data() + sf->at[f], sf->files[f].data_bytes));
+                const auto &fk = sf->keys[f];
+                bool c = fk.size() == sf->prof.back().n;
+                for (size_t k = 1; c && k < fk.size(); ++k) c = fk[k] == fk[k - 1] + 1;
+                sf->prof.back().consec = c;
             }
             made[i] = std::move(sf);
         } catch (const Error &e) {
@@ -2577,23 +2674,76 @@ void dedup_files(sb_store &s, const sb_dedup_file_job *jobs, size_t nj, uint64_t
         if (it == use.end()) it = use.emplace(pkey[p], C.m.at(pkey[p])).first;
         pairs[p].sf = it->second.get();
     }
-    // each pair's entries as the reference reader returns them, in parallel
+    // each pair's entries as the reference reader returns them: from the
+    // file's profile (two binary searches), or by the walk itself for an
+    // unsorted file; SBEACON_STRICT_CHECK=1 (tests) runs both and compares
+    const bool check = std::getenv("SBEACON_STRICT_CHECK") != nullptr;
+    std::atomic<bool> mismatch{false};
     parallel_for(pairs.size(), [&](size_t p) {
         Pair &P = pairs[p];
         if (!P.sf) return;
         const SliceFiles &sf = *P.sf;
         if (sf.status || P.file >= sf.files.size()) return;  // reported in job order below
         const sb_dedup_file_job &J = jobs[P.job];
-        P.ok = strict_region_entries(sf.data.data() + sf.at[P.file], sf.files[P.file].data_bytes, J.range_start,
-                                     J.range_end, P.incl);
+        const FileProfile &F = sf.prof[P.file];
+        if (F.sorted) {
+            uint32_t lo = 0, last = 0;
+            P.ok = profile_range(F, J.range_start, J.range_end, lo, last);
+            P.e_lo = std::min(lo, F.n);
+            P.e_hi = std::max(P.e_lo, std::min(last + 1, F.n));
+        }
+        if (!F.sorted || check) {
+            std::vector<uint32_t> incl;
+            const bool ok = strict_region_entries(sf.data.data() + sf.at[P.file], sf.files[P.file].data_bytes,
+                                                  J.range_start, J.range_end, incl);
+            if (F.sorted) {
+                bool same = ok == P.ok;
+                if (same && ok) {
+                    same = incl.size() == P.e_hi - P.e_lo;
+                    for (size_t k = 0; same && k < incl.size(); ++k) same = incl[k] == P.e_lo + k;
+                }
+                if (!same) mismatch = true;
+            } else {
+                P.ok = ok;
+                P.walked = true;
+                P.incl = std::move(incl);
+            }
+        }
     }, 16, 1);
-    // key runs in job order; a job stops at its first failing file
+    if (mismatch) throw Error(SB_EINVAL, "strict dedup: region-file profile disagrees with the reader walk");
+    // key runs in job order (consecutive store keys; KRun pieces of the
+    // window path: a run is cut where the keys stop being consecutive or
+    // leave their contig segment); a job stops at its first failing file
     std::vector<KSeg> segs;
+    std::vector<KRun> runs;
     uint64_t n = 0;
+    auto add_run = [&](uint32_t vcf, uint32_t a, uint32_t e, uint32_t j, uint32_t rs) {
+        const VcfData &v = s.vcfs[vcf];
+        while (a < e) {
+            uint32_t k = 0;  // the segment holding key a
+            while (k < v.segments.size() && !(s.h_dk_lo[v.segments[k].lo] <= a && a < s.h_dk_lo[v.segments[k].hi])) ++k;
+            if (k == v.segments.size()) throw Error(SB_EINVAL, "strict dedup: a region-file key outside its VCF");
+            const Segment &sg = v.segments[k];
+            const uint32_t b = std::min(e, s.h_dk_lo[sg.hi]);
+            if (!runs.empty() && runs.back().job == j && runs.back().key_hi == a && runs.back().seg_lo == sg.lo) {
+                runs.back().key_hi = b;  // continues the previous run
+                runs.back().pos_hi = s.h_dk_pos[b - 1];
+                segs.back().n += b - a;
+            } else {
+                const BucketIndex &bi = v.buckets[k];
+                segs.push_back(KSeg{a, n, b - a, j, rs, 0});
+                runs.push_back(KRun{a, b, s.h_dk_pos[a], s.h_dk_pos[b - 1], sg.lo, sg.hi, bi.base, bi.shift, bi.off,
+                                    bi.n, j, 0, 0, {0, 0}});
+            }
+            n += b - a;
+            a = b;
+        }
+    };
     for (size_t p = 0; p < pairs.size();) {
         const uint32_t j = pairs[p].job;
         const uint32_t rs = static_cast<uint32_t>(std::min<uint64_t>(jobs[j].range_start, 0xffffffffull));
         const size_t seg0 = segs.size();
+        const uint64_t n0 = n;
         for (; p < pairs.size() && pairs[p].job == j; ++p) {
             if (status[j]) continue;
             const Pair &P = pairs[p];
@@ -2611,21 +2761,25 @@ void dedup_files(sb_store &s, const sb_dedup_file_job *jobs, size_t nj, uint64_t
                 continue;
             }
             const auto &fk = sf.keys[P.file];
-            const auto &incl = P.incl;
-            for (size_t a = 0; a < incl.size();) {  // runs of consecutive store keys
-                size_t b = a + 1;
-                while (b < incl.size() && fk[incl[b]] == fk[incl[b - 1]] + 1) ++b;
-                segs.push_back(KSeg{fk[incl[a]], n, static_cast<uint32_t>(b - a), j, rs, 0});
-                n += b - a;
+            const uint32_t vcf = std::get<0>(pkey[p]);
+            auto key_of = [&](uint32_t k) { return P.walked ? fk[P.incl[k]] : fk[P.e_lo + k]; };
+            const uint32_t cnt = P.walked ? static_cast<uint32_t>(P.incl.size()) : P.e_hi - P.e_lo;
+            for (uint32_t a = 0; a < cnt;) {  // runs of consecutive store keys
+                uint32_t b = a + 1;
+                if (!P.walked && sf.prof[P.file].consec) b = cnt;  // every key of the file is consecutive
+                else
+                    while (b < cnt && key_of(b) == key_of(b - 1) + 1) ++b;
+                add_run(vcf, key_of(a), key_of(b - 1) + 1, j, rs);
                 a = b;
             }
         }
         if (status[j]) {
-            for (size_t g = seg0; g < segs.size(); ++g) n -= segs[g].n;
             segs.resize(seg0);
+            runs.resize(seg0);
+            n = n0;
         }
     }
-    dedup_run(s, segs, n, nj, unique, status, stats);
+    dedup_run(s, segs, n, nj, unique, status, stats, false, &runs);
 }
 
 }  // namespace

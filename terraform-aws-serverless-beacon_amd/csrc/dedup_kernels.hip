@@ -658,11 +658,32 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
 // pairs).  Two strings under one hash, or a full deferred list, raise
 // *overflow and the host recounts the call on the sorted path.  No gather
 // stream, no radix pass: 16 B/key + 8 B per hashed key.
-constexpr uint32_t kWSlots = 3072;  // 24 KB; kWinCap keys at most (load <= 0.67); slot = multiply-shift range reduction
+// the window's two sets share 24 KB: hashed keys get 64-bit slots at load
+// <= 2/3, exact keys the remaining 32-bit slots (kWinCap keys: load <= 1/3
+// with no hashed key); slot = multiply-shift range reduction
+constexpr uint32_t kWSetWords = 6144;
 constexpr uint32_t kWPer = kWinCap / kThreads;
 static_assert(kWPer * kThreads == kWinCap, "window keys per thread");
-static_assert(kWinCap < kWSlots, "window set load");
+static_assert(kWinCap < kWSetWords / 2 - 8, "hashed set of a window of hashed keys only");
 static_assert(kWinPieces == 64, "one wave scans the pieces");
+
+// wave-wide sums (DPP row shifts, then the row broadcasts)
+template <int CTRL, int ROW = 0xf>
+__device__ __forceinline__ uint32_t dppm(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), CTRL, ROW, 0xf, false));
+}
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += dppm<0x111>(v);
+    v += dppm<0x112>(v);
+    v += dppm<0x114>(v);
+    v += dppm<0x118>(v);
+    v += dppm<0x142, 0xa>(v);
+    v += dppm<0x143, 0xc>(v);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(wave_incl_sum(v)), 63));
+}
 
 // len bytes at blob offsets oa and ob equal?  Aligned 8-byte words (every
 // load of a 32-byte round issued first) funnel-shifted into place; the blob
@@ -812,71 +833,65 @@ __global__ __launch_bounds__(kThreads) void dedup_plan_kernel(KStore ks, const K
     wins[w] = KWin{i, J.nruns, runs[J.run_lo].job, P, J.run_lo, J.pmax, J.eoff, J.nw};
 }
 
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))) void window_dedupe_kernel(KStore ks, const KWin *wins, const uint32_t *E,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void window_dedupe_kernel(KStore ks, const KWin *wins, const uint32_t *E,
                                                                  unsigned long long *counts, uint2 *list,
                                                                  uint32_t *n_list, uint32_t cap, uint32_t *overflow,
                                                                  uint32_t dbg) {
-    __shared__ unsigned long long set[kWSlots];
-    __shared__ uint32_t s_pre[kWinPieces + 1], s_klo[kWinPieces], s_run[kWinPieces];
-    __shared__ uint32_t s_fresh, s_def, s_def0;
+    // one LDS buffer split per window: the exact set (32-bit words, the
+    // first X words) and the hashed set (64-bit entries, the last H)
+    __shared__ __attribute__((aligned(16))) uint32_t sets[kWSetWords];
+    __shared__ uint32_t s_pre[kWinPieces + 1], s_base[kWinPieces], s_run[kWinPieces];
+    __shared__ uint32_t s_fresh, s_def, s_def0, s_nh;
     const KWin W = wins[blockIdx.x];
-    const int lane = threadIdx.x & 63;
-    for (uint32_t i = threadIdx.x; i < kWSlots; i += kThreads) set[i] = ~0ull;
-    if (threadIdx.x < 64) {  // wave 0: the pieces' inclusive prefix
+    const uint32_t lane = threadIdx.x & 63u;
+    if (threadIdx.x < 64) {  // wave 0: the pieces' inclusive prefix (DPP scan)
         uint32_t len = 0, klo = 0, run = 0;
-        if (static_cast<uint32_t>(lane) < W.nruns) {  // run `lane`'s piece of the window
+        if (lane < W.nruns) {  // run `lane`'s piece of the window
             const uint32_t *e = E + W.eoff + static_cast<uint64_t>(lane) * (W.nw + 1) + W.i;
             klo = e[0];
             len = e[1] - e[0];
             run = W.run_lo + lane;
         }
-        uint32_t inc = len;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = __shfl_up(inc, o, 64);
-            if (lane >= o) inc += y;
-        }
+        const uint32_t inc = wave_incl_sum(len);
         s_pre[lane + 1] = inc;
-        s_klo[lane] = klo;
+        s_base[lane] = klo - (inc - len);  // key id = window-local index + base
         s_run[lane] = run;
         if (lane == 0) {
             s_pre[0] = 0;
             s_fresh = 0;
             s_def = 0;
+            s_nh = 0;
         }
     }
     __syncthreads();
     const uint32_t np = W.nruns, total = s_pre[np];
-    if (total > kWinCap) {  // a pile-up past the window's set (the host recounts on the sorted path)
+    if (total > kWinCap) {  // a pile-up past the window's sets (the host recounts on the sorted path)
         if (threadIdx.x == 0) atomicOr(overflow, 1u);
         return;
     }
-    auto piece_of = [&](uint32_t f) {
-        uint32_t p = 0;
-#pragma unroll
-        for (uint32_t st = 32; st; st >>= 1)
-            if (p + st < np && s_pre[p + st] <= f) p += st;
-        return p;
-    };
-    auto key_of = [&](uint32_t f) {  // window-local index -> store key
-        const uint32_t p = piece_of(f);
-        return s_klo[p] + (f - s_pre[p]);
-    };
-    // every key's 8-byte class word first (key u = u * kThreads + tid): POS,
-    // exact code, displaced flag -- the 16-byte body only where a hashed key
-    // meets an entry with its hash bits (string confirmation, below)
+    // every key's 8-byte class word (key u = u * kThreads + tid): POS, exact
+    // code, displaced flag -- the 8-byte hash only for hashed keys, the
+    // 16-byte body only where a hashed key meets an entry with its hash bits.
+    // The lane's piece only moves forward with u (f grows by kThreads): a
+    // short catch-up walk per key, the pieces kept 6 bits each for later
     uint64_t wd[kWPer];
     uint32_t kid[kWPer];
     uint32_t okm = 0;
+    uint64_t pk = 0;  // piece of key u in bits 6u..6u+5
+    {
+        uint32_t pc = 0;
 #pragma unroll
-    for (uint32_t u = 0; u < kWPer; ++u) {
-        const uint32_t f = u * kThreads + threadIdx.x;
-        kid[u] = 0;
-        wd[u] = 0;
-        if (f < total) {
-            kid[u] = key_of(f);
-            wd[u] = ks.word[kid[u]];
-            okm |= 1u << u;
+        for (uint32_t u = 0; u < kWPer; ++u) {
+            const uint32_t f = u * kThreads + threadIdx.x;
+            kid[u] = 0;
+            wd[u] = 0;
+            if (f < total) {
+                while (pc + 1 < np && s_pre[pc + 1] <= f) ++pc;
+                kid[u] = f + s_base[pc];
+                wd[u] = ks.word[kid[u]];
+                okm |= 1u << u;
+                pk |= static_cast<uint64_t>(pc) << (6 * u);
+            }
         }
     }
     if (dbg & 4u) {  // timing ablation (SBEACON_DEDUP_WIN_DBG): loads only
@@ -890,112 +905,117 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(5, 8))
     // copy at a larger POS of the job)
     uint32_t xw[kWPer];
     uint32_t em = 0, hm = 0, dm = 0;
+    const uint32_t pm10 = W.pmax / 10;
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) {
-        xw[u] = 0;
-        if (!((okm >> u) & 1u)) continue;
         const uint32_t pos = static_cast<uint32_t>(wd[u]);
-        if (wd[u] & kWordDisplaced) {
-            if (static_cast<uint64_t>(pos) * 10 > W.pmax) hm |= 1u << u;
-            else dm |= 1u << u;
-            continue;
-        }
         const uint32_t code = static_cast<uint32_t>(wd[u] >> 32) & 63u;
-        if (code && pos >= W.p0 && ((pos - W.p0) >> kWinSpanBits) == 0) {
-            xw[u] = ((pos - W.p0) << 6) | code;
-            em |= 1u << u;
-        } else {
-            hm |= 1u << u;
-        }
+        const bool ok = (okm >> u) & 1u;
+        const bool disp = (wd[u] & kWordDisplaced) != 0;
+        const bool big = pos > pm10;  // 10 POS > the job's largest POS
+        const bool ex = ok && !disp && code && pos >= W.p0 && ((pos - W.p0) >> kWinSpanBits) == 0;
+        xw[u] = ((pos - W.p0) << 6) | code;
+        em |= (ex ? 1u : 0u) << u;
+        hm |= ((ok && !ex && (!disp || big)) ? 1u : 0u) << u;
+        dm |= ((ok && disp && !big) ? 1u : 0u) << u;
     }
     unsigned long long hv[kWPer];
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) hv[u] = ((hm >> u) & 1u) ? ks.hash[kid[u]] : 0ull;
-    // deferred keys: one reservation per workgroup in the global list
+    // per workgroup: hashed keys (sizes the two sets) and deferred keys (one
+    // reservation in the global list)
     const uint32_t nd = static_cast<uint32_t>(__popc(dm));
     uint32_t dofs = 0;
     if (nd) dofs = atomicAdd(&s_def, nd);
+    {
+        const uint32_t nhw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
+            static_cast<int>(wave_sum_u32(static_cast<uint32_t>(__popc(hm))))));
+        if (lane == 0 && nhw) atomicAdd(&s_nh, nhw);
+    }
     __syncthreads();
     if (threadIdx.x == 0 && s_def) {
         const uint32_t at = atomicAdd(n_list, s_def);
         s_def0 = at;
         if (at + s_def > cap) atomicOr(overflow, 1u);
     }
+    // hashed set: H 64-bit slots (load <= 2/3); exact set: the rest
+    const uint32_t nh = s_nh;
+    const uint32_t H = nh ? min(nh + nh / 2 + 8u, kWSetWords / 2 - 8u) : 0u;
+    const uint32_t X = kWSetWords - 2u * H;
+    unsigned long long *hset = reinterpret_cast<unsigned long long *>(sets + X);
+    for (uint32_t i = threadIdx.x * 4; i < kWSetWords; i += kThreads * 4)
+        *reinterpret_cast<uint4 *>(sets + i) = uint4{~0u, ~0u, ~0u, ~0u};
     __syncthreads();
     if (nd) {
         uint32_t at = s_def0 + dofs;
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u)
             if ((dm >> u) & 1u) {
-                if (at < cap) list[at] = uint2{kid[u], s_run[piece_of(u * kThreads + threadIdx.x)]};
+                if (at < cap) list[at] = uint2{kid[u], s_run[(pk >> (6 * u)) & 63u]};
                 ++at;
             }
     }
-    uint32_t fresh = 0;
-    uint32_t pend = 0;      // hashed keys that met an entry with their hash bits
-    uint32_t ins[kWPer];    // ... and that entry's window-local key index
-    auto insert = [&](uint32_t u, bool ex) {
-        const uint32_t f = u * kThreads + threadIdx.x;
-        const unsigned long long e =
-            ex ? static_cast<unsigned long long>(xw[u]) : ((1ull << 63) | ((hv[u] >> 13) << 12) | f);
-        const uint32_t hr = ex ? xw[u] * 0x9E3779B1u : static_cast<uint32_t>(hv[u]);
-        uint32_t h = static_cast<uint32_t>((static_cast<uint64_t>(hr) * kWSlots) >> 32);
-        static_assert(kWinCap <= 4096, "window-local index in 12 bits");
-        for (uint32_t probe = 0; probe < kWSlots; ++probe) {
-            const unsigned long long was = atomicCAS(&set[h], ~0ull, e);
-            if (was == ~0ull) {
-                ++fresh;
-                return;
-            }
-            if (ex ? was == e : (was >> 12) == (e >> 12)) {
-                if (!ex) {
-                    pend |= 1u << u;
-                    ins[u] = static_cast<uint32_t>(was & 0xfff);
-                }
-                return;
-            }
-            h = h + 1 == kWSlots ? 0u : h + 1;
-        }
-    };
     if (dbg & 1u) em = 0;  // timing ablation: no exact inserts
     if (dbg & 2u) hm = 0;  // no hashed inserts
+    uint32_t fresh = 0;
+    // exact keys: 32-bit words; the probe loop runs while any lane of the
+    // wave still probes (linear probing, multiply-shift slot)
+#pragma unroll
+    for (uint32_t u = 0; u < kWPer; ++u) {
+        bool todo = (em >> u) & 1u;
+        uint32_t h = static_cast<uint32_t>((static_cast<uint64_t>(xw[u] * 0x9E3779B1u) * X) >> 32);
+        while (__ballot(todo)) {
+            if (todo) {
+                const uint32_t was = atomicCAS(&sets[h], ~0u, xw[u]);
+                fresh += was == ~0u ? 1u : 0u;
+                todo = was != ~0u && was != xw[u];
+                h = h + 1 == X ? 0u : h + 1;
+            }
+        }
+    }
+    // hashed keys: hash bits 13..63 << 12 | window-local index
+    uint32_t pend = 0;    // hashed keys that met an entry with their hash bits
+    uint32_t ins[kWPer];  // ... and that entry's window-local key index
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) {
         ins[u] = 0;
-        if ((em >> u) & 1u) insert(u, true);
+        bool todo = (hm >> u) & 1u;
+        if (!__ballot(todo)) continue;
+        const unsigned long long e = ((hv[u] >> 13) << 12) | (u * kThreads + threadIdx.x);
+        uint32_t h = static_cast<uint32_t>((static_cast<uint64_t>(static_cast<uint32_t>(hv[u])) * H) >> 32);
+        while (__ballot(todo)) {
+            if (todo) {
+                const unsigned long long was = atomicCAS(&hset[h], ~0ull, e);
+                fresh += was == ~0ull ? 1u : 0u;
+                if (was != ~0ull && (was >> 12) == (e >> 12)) {
+                    pend |= 1u << u;
+                    ins[u] = static_cast<uint32_t>(was & 0xfff);
+                }
+                todo = was != ~0ull && (was >> 12) != (e >> 12);
+                h = h + 1 == H ? 0u : h + 1;
+            }
+        }
     }
-#pragma unroll
-    for (uint32_t u = 0; u < kWPer; ++u)
-        if ((hm >> u) & 1u) insert(u, false);
-    // the strings of a repeated hash must match the inserter's: every
-    // inserter body load issued together, then the comparisons (the general
-    // decimal-concatenation one only for different POS or two blob tails)
+    // the strings of a repeated hash must match the inserter's (rare: key by
+    // key; the general decimal-concatenation comparison only for different
+    // POS or two blob tails)
     bool bad = false;
-    if (pend) {
-        KBody xb[kWPer], b[kWPer];
 #pragma unroll
-        for (uint32_t u = 0; u < kWPer; ++u) {
-            ins[u] = ((pend >> u) & 1u) ? key_of(ins[u]) : 0u;
-            xb[u] = ((pend >> u) & 1u) ? ks.body[ins[u]] : KBody{0, 0, 0};
-            b[u] = ((pend >> u) & 1u) ? ks.body[kid[u]] : KBody{0, 0, 0};
-        }
-        uint32_t slow = 0;
-#pragma unroll
-        for (uint32_t u = 0; u < kWPer; ++u) {
-            if (!((pend >> u) & 1u)) continue;
-            if (xb[u].pos == b[u].pos && xb[u].tail == b[u].tail) continue;
-            if (xb[u].pos == b[u].pos && !((xb[u].tail & b[u].tail) & kTailBlob)) bad = true;
-            else slow |= 1u << u;  // two blob tails (or different POS)
-        }
-        if (slow) {
-#pragma unroll
-            for (uint32_t u = 0; u < kWPer; ++u)
-                if (((slow >> u) & 1u) && !body_equal(ks, xb[u], b[u])) bad = true;
+    for (uint32_t u = 0; u < kWPer; ++u) {
+        if (!__ballot((pend >> u) & 1u)) continue;
+        if ((pend >> u) & 1u) {
+            uint32_t q = 0;  // the inserter's piece
+            while (q + 1 < np && s_pre[q + 1] <= ins[u]) ++q;
+            const KBody xb = ks.body[ins[u] + s_base[q]], b = ks.body[kid[u]];
+            if (!(xb.pos == b.pos && xb.tail == b.tail)) {
+                if (xb.pos == b.pos && !((xb.tail & b.tail) & kTailBlob)) bad = true;
+                else if (!body_equal(ks, xb, b)) bad = true;
+            }
         }
     }
     if (bad) atomicOr(overflow, 1u);
-    for (int d = 32; d >= 1; d >>= 1) fresh += __shfl_xor(fresh, d, 64);
-    if (lane == 0 && fresh) atomicAdd(&s_fresh, fresh);
+    const uint32_t fw = wave_sum_u32(fresh);
+    if (lane == 0 && fw) atomicAdd(&s_fresh, fw);
     __syncthreads();
     if (threadIdx.x == 0 && s_fresh) atomicAdd(&counts[W.job], static_cast<unsigned long long>(s_fresh));
 }

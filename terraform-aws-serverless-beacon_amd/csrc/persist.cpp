@@ -19,10 +19,14 @@
 //   <dir>/device.bin     the device buffers, back to back (4 KiB aligned)
 #include <hip/hip_runtime.h>
 #include <fcntl.h>
+#include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <array>
+#include <atomic>
+#include <functional>
 #include <chrono>
 #include <memory>
 #include <cstdio>
@@ -74,6 +78,34 @@ SourceFile fingerprint(const std::string &path) {
 
 namespace {
 
+void pread_all(int fd, void *dst, size_t n, uint64_t off, const char *what) {
+    size_t got = 0;
+    while (got < n) {
+        const ssize_t r = pread(fd, static_cast<uint8_t *>(dst) + got, n - got, static_cast<off_t>(off + got));
+        if (r <= 0) throw Error(SB_EIO, std::string("persisted store: truncated ") + what);
+        got += static_cast<size_t>(r);
+    }
+}
+
+// run jobs on up to nt threads, largest first; the first error is rethrown
+void run_jobs(std::vector<std::pair<size_t, std::function<void()>>> &jobs, unsigned nt) {
+    std::sort(jobs.begin(), jobs.end(), [](const auto &a, const auto &b) { return a.first > b.first; });
+    std::atomic<size_t> next{0};
+    std::vector<std::string> errs(nt);
+    std::vector<std::thread> th;
+    for (unsigned t = 0; t < nt; ++t)
+        th.emplace_back([&, t] {
+            try {
+                for (size_t q; (q = next.fetch_add(1)) < jobs.size();) jobs[q].second();
+            } catch (const std::exception &e) {
+                errs[t] = e.what();
+            }
+        });
+    for (auto &x : th) x.join();
+    for (const std::string &e : errs)
+        if (!e.empty()) throw Error(SB_EIO, e);
+}
+
 struct Writer {
     FILE *f = nullptr;
     uint64_t at = 0;
@@ -113,15 +145,20 @@ struct Writer {
     }
 };
 
+// host.bin is parsed from a read-only mapping; columns of 1 MiB or more are
+// not copied during the parse but become jobs (resize + pread into the
+// column) that threads run beside the device image upload
 struct Reader {
-    std::vector<uint8_t> b;
-    size_t at = 0;
+    const uint8_t *b = nullptr;
+    size_t size = 0, at = 0;
+    int fd = -1;
+    std::vector<std::pair<size_t, std::function<void()>>> *defer = nullptr;  // (bytes, job)
     void need(size_t n) const {
-        if (at + n > b.size()) throw Error(SB_EIO, "persisted store: truncated host.bin");
+        if (at + n > size) throw Error(SB_EIO, "persisted store: truncated host.bin");
     }
     void raw(void *p, size_t n) {
         need(n);
-        if (n) std::memcpy(p, b.data() + at, n);
+        if (n) std::memcpy(p, b + at, n);
         at += n;
     }
     template <class T>
@@ -133,14 +170,25 @@ struct Reader {
     template <class T>
     void vec(std::vector<T> &v) {
         const uint64_t n = pod<uint64_t>();
-        need(n * sizeof(T));
-        v.resize(n);
-        raw(v.data(), n * sizeof(T));
+        const size_t bytes = n * sizeof(T);
+        need(bytes);
+        if (defer && bytes >= (size_t(1) << 20)) {
+            const size_t off = at;
+            const int f = fd;
+            defer->emplace_back(bytes, [&v, n, off, f] {
+                v.resize(n);
+                pread_all(f, v.data(), n * sizeof(T), off, "host.bin");
+            });
+            at += bytes;
+        } else {
+            v.resize(n);
+            raw(v.data(), bytes);
+        }
     }
     std::string str() {
         const uint64_t n = pod<uint64_t>();
         need(n);
-        std::string s(reinterpret_cast<const char *>(b.data() + at), n);
+        std::string s(reinterpret_cast<const char *>(b + at), n);
         at += n;
         return s;
     }
@@ -151,18 +199,36 @@ struct Reader {
     }
 };
 
-std::vector<uint8_t> read_file(const std::string &path) {
-    FILE *f = fopen(path.c_str(), "rb");
-    if (!f) throw Error(SB_EIO, "cannot open " + path);
-    fseek(f, 0, SEEK_END);
-    const long n = ftell(f);
-    fseek(f, 0, SEEK_SET);
-    std::vector<uint8_t> b(static_cast<size_t>(std::max(0l, n)));
-    const size_t got = fread(b.data(), 1, b.size(), f);
-    fclose(f);
-    if (got != b.size()) throw Error(SB_EIO, "short read " + path);
-    return b;
-}
+// a read-only mapping of a whole file
+struct Mapped {
+    int fd = -1;
+    const uint8_t *p = nullptr;
+    size_t n = 0;
+    explicit Mapped(const std::string &path) {
+        fd = ::open(path.c_str(), O_RDONLY);
+        if (fd < 0) throw Error(SB_EIO, "cannot open " + path);
+        struct stat st{};
+        if (fstat(fd, &st) != 0) {
+            ::close(fd);
+            throw Error(SB_EIO, "cannot stat " + path);
+        }
+        n = static_cast<size_t>(st.st_size);
+        if (n) {
+            void *m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+            if (m == MAP_FAILED) {
+                ::close(fd);
+                throw Error(SB_EIO, "cannot map " + path);
+            }
+            p = static_cast<const uint8_t *>(m);
+        }
+    }
+    ~Mapped() {
+        if (p) munmap(const_cast<uint8_t *>(p), n);
+        if (fd >= 0) ::close(fd);
+    }
+    Mapped(const Mapped &) = delete;
+    Mapped &operator=(const Mapped &) = delete;
+};
 
 void put_sources(Writer &w, const std::vector<SourceFile> &v) {
     w.pod<uint64_t>(v.size());
@@ -381,8 +447,13 @@ std::string store_dir(const std::string &p) {
 
 sb_store *store_open(const std::string &path, int device, std::string *stale) {
     const std::string dir = store_dir(path);
+    Mapped hm(dir + "/host.bin");
+    std::vector<std::pair<size_t, std::function<void()>>> host_jobs;
     Reader r;
-    r.b = read_file(dir + "/host.bin");
+    r.b = hm.p;
+    r.size = hm.n;
+    r.fd = hm.fd;
+    r.defer = &host_jobs;
     if (r.pod<uint64_t>() != kMagic || r.pod<uint32_t>() != kFormat)
         throw Error(SB_EIO, "persisted store: not a store file of this format (" + dir + ")");
     auto s = std::make_unique<sb_store>();
@@ -426,6 +497,7 @@ sb_store *store_open(const std::string &path, int device, std::string *stale) {
         s->ds = SStore{};
         s->dk = KStore{};
         s->g = GStore{};
+        run_jobs(host_jobs, 8);
         return s.release();
     }
     if (old.empty() && s->n_records)
@@ -462,6 +534,15 @@ sb_store *store_open(const std::string &path, int device, std::string *stale) {
     }
     const int fd = ::open((dir + "/device.bin").c_str(), O_RDONLY);
     if (fd < 0) throw Error(SB_EIO, "cannot open " + dir + "/device.bin");
+    // the host columns load beside the device image
+    std::string host_err;
+    std::thread host_loader([&] {
+        try {
+            run_jobs(host_jobs, 6);
+        } catch (const std::exception &e) {
+            host_err = e.what();
+        }
+    });
     const unsigned nt = static_cast<unsigned>(std::min<size_t>(8, std::max<size_t>(1, pieces.size())));
     std::vector<std::string> errs(nt);
     std::vector<std::thread> th;
@@ -504,9 +585,11 @@ sb_store *store_open(const std::string &path, int device, std::string *stale) {
             if (st) (void)hipStreamDestroy(st);
         });
     for (auto &x : th) x.join();
+    host_loader.join();
     ::close(fd);
     for (const std::string &e : errs)
         if (!e.empty()) throw Error(SB_EIO, "persisted store: " + e);
+    if (!host_err.empty()) throw Error(SB_EIO, host_err);
     // remap: every view word inside an old buffer now points into its new copy
     auto remap = [&](uint64_t *w, size_t n) {
         for (size_t i = 0; i < n; ++i) {

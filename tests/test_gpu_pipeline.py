@@ -47,7 +47,7 @@ def test_summarise_dataset_pipeline(tmp_path):
         assert counts['uniqueVariants'] == sum(per_range)
 
 
-def test_region_files_gzip_and_strict_dedup(tmp_path):
+def test_region_files_gzip_and_strict_dedup(tmp_path, monkeypatch):
     """Region files as the reference stores them (gzip members, level 9) and
     duplicateVariantSearch in the reference-exact mode: every target file is
     read by ReadVcfData::getVcfData's loop over the REFERENCE gzip reader
@@ -58,6 +58,9 @@ def test_region_files_gzip_and_strict_dedup(tmp_path):
     from test_ref_pinned import deflate9, gzip_payload
     if ref.lib() is None:
         pytest.skip('oracle/_ref missing')
+    # every (job, file) pair's entries from the file profile are also read by
+    # the reader walk and compared (the library raises on a difference)
+    monkeypatch.setenv('SBEACON_STRICT_CHECK', '1')
     from sbeacon.dedup import dedup_batch, init_duplicate_variant_search
     from sbeacon.engine import Store
     from sbeacon.summarise import _single_store_registry, region_file_keys, summarise_dataset
