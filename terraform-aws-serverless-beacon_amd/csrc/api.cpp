@@ -21,6 +21,8 @@
 #include <memory>
 #include <thread>
 #include <tuple>
+#include <string_view>
+#include <unordered_map>
 #include <unordered_set>
 
 #include <zlib.h>
@@ -810,6 +812,14 @@ void upload_store(sb_builder &b, sb_store &s) {
     {
         std::vector<KBody> body(dk_hash.size());
         std::vector<uint64_t> word(dk_hash.size());
+        // every distinct tail string gets a store-wide id (kWordIdMask): the
+        // window dedup then compares keys as (POS, id) words, exactly, with
+        // no hash and no string confirmation (a displaced key's equal strings
+        // in its window are at its own POS too: the others are deferred).  Single-base REF/ALT tails
+        // c1 '_' c2 are ids c1 << 3 | c2 (< 64); the others are numbered from
+        // 64 in key order; past the id space a key stays hashed (id 0)
+        std::unordered_map<std::string_view, uint32_t> tail_id;
+        uint32_t next_id = 64;
         for (size_t k = 0; k < body.size(); ++k) {
             const uint64_t t = dk_tail[k];
             uint32_t c0 = 0x100;  // first tail byte (none: 0x100)
@@ -820,11 +830,26 @@ void upload_store(sb_builder &b, sb_store &s) {
             }
             const bool disp = c0 >= '0' && c0 <= '9';
             body[k] = KBody{t, dk_pos[k], disp ? kKeyDisplaced : 0u};
-            // the exact class (dedup_kernels.hip exact_word with no leading digit): tail = c1 '_' c2
             uint64_t code = 0;
-            if (!disp && !(t & kTailBlob) && dk_pos[k] != 0 && (t >> 56) == 3) {
-                const uint32_t c1 = t & 0xff, us = (t >> 8) & 0xff, c2 = (t >> 16) & 0xff;
-                if (us == '_' && c1 >= 1 && c1 <= 7 && c2 >= 1 && c2 <= 7) code = (c1 << 3) | c2;
+            if (dk_pos[k] != 0) {
+                if (!(t & kTailBlob) && (t >> 56) == 3 && ((t >> 8) & 0xff) == '_' && (t & 0xff) >= 1 && (t & 0xff) <= 7 &&
+                    ((t >> 16) & 0xff) >= 1 && ((t >> 16) & 0xff) <= 7) {
+                    code = ((t & 0xff) << 3) | ((t >> 16) & 0xff);
+                } else {
+                    std::string_view sv;
+                    if (t & kTailBlob)
+                        sv = std::string_view(reinterpret_cast<const char *>(dk_blob.data() + (t & ((1ull << 40) - 1))),
+                                              (t >> 40) & 0xffff);
+                    else
+                        sv = std::string_view(reinterpret_cast<const char *>(&dk_tail[k]), static_cast<size_t>(t >> 56));
+                    auto it = tail_id.find(sv);
+                    if (it != tail_id.end()) {
+                        code = it->second;
+                    } else if (next_id <= kWordIdMask) {
+                        tail_id.emplace(sv, next_id);
+                        code = next_id++;
+                    }
+                }
             }
             word[k] = dk_pos[k] | (code << 32) | (disp ? kWordDisplaced : 0ull);
         }

@@ -658,13 +658,22 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
 // pairs).  Two strings under one hash, or a full deferred list, raise
 // *overflow and the host recounts the call on the sorted path.  No gather
 // stream, no radix pass: 16 B/key + 8 B per hashed key.
-// the window's two sets share 24 KB: hashed keys get 64-bit slots at load
-// <= 2/3, exact keys the remaining 32-bit slots (kWinCap keys: load <= 1/3
-// with no hashed key); slot = multiply-shift range reduction
-constexpr uint32_t kWSetWords = 6144;
+// A window's keys are deduplicated without LDS atomics: every key's
+// identity word (identified: 1 << 63 | (POS - p0) << 29 | id, exact;
+// hashed: the 64-bit hash with bit 63 clear) is staged at its window-local
+// index, and in rounds every unresolved key writes its index to the slot of
+// its identity (a per-round salted hash; plain 16-bit stores, one of the
+// writers wins), then reads the winner back: the winner's identity equal to
+// its own resolves it (the winner counts itself, an equal key is a
+// duplicate -- for hashed identities after the strings are confirmed); a
+// different identity (a collision) leaves it for the next round.  Equal
+// identities always meet in one slot, so a value is counted once.
+constexpr uint32_t kWSlots = 4096;   // 8 KB of 16-bit winners, load <= 1/2
+constexpr uint32_t kWRounds = 24;    // unresolved after that: the sorted path
+constexpr uint32_t kWConfirm = 128;  // hashed duplicate pairs confirmed per window
 constexpr uint32_t kWPer = kWinCap / kThreads;
 static_assert(kWPer * kThreads == kWinCap, "window keys per thread");
-static_assert(kWinCap < kWSetWords / 2 - 8, "hashed set of a window of hashed keys only");
+static_assert(kWinCap <= kWSlots / 2 && kWinCap <= 65536, "window slot load / 16-bit winners");
 static_assert(kWinPieces == 64, "one wave scans the pieces");
 
 // wave-wide sums (DPP row shifts, then the row broadcasts)
@@ -837,11 +846,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
                                                                  unsigned long long *counts, uint2 *list,
                                                                  uint32_t *n_list, uint32_t cap, uint32_t *overflow,
                                                                  uint32_t dbg) {
-    // one LDS buffer split per window: the exact set (32-bit words, the
-    // first X words) and the hashed set (64-bit entries, the last H)
-    __shared__ __attribute__((aligned(16))) uint32_t sets[kWSetWords];
+    __shared__ __attribute__((aligned(16))) unsigned long long s_id[kWinCap];  // identity of window key f
+    __shared__ __attribute__((aligned(16))) uint16_t s_win[kWSlots];            // a round's winner per slot
     __shared__ uint32_t s_pre[kWinPieces + 1], s_base[kWinPieces], s_run[kWinPieces];
-    __shared__ uint32_t s_fresh, s_def, s_def0, s_nh;
+    __shared__ uint32_t s_conf[kWConfirm];  // hashed duplicate pairs (winner | key << 16) to confirm
+    __shared__ uint32_t s_fresh, s_def, s_def0, s_nconf;
     const KWin W = wins[blockIdx.x];
     const uint32_t lane = threadIdx.x & 63u;
     if (threadIdx.x < 64) {  // wave 0: the pieces' inclusive prefix (DPP scan)
@@ -860,22 +869,21 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
             s_pre[0] = 0;
             s_fresh = 0;
             s_def = 0;
-            s_nh = 0;
+            s_nconf = 0;
         }
     }
     __syncthreads();
     const uint32_t np = W.nruns, total = s_pre[np];
-    if (total > kWinCap) {  // a pile-up past the window's sets (the host recounts on the sorted path)
+    if (total > kWinCap) {  // a pile-up past the window (the host recounts on the sorted path)
         if (threadIdx.x == 0) atomicOr(overflow, 1u);
         return;
     }
-    // every key's 8-byte class word (key u = u * kThreads + tid): POS, exact
-    // code, displaced flag -- the 8-byte hash only for hashed keys, the
-    // 16-byte body only where a hashed key meets an entry with its hash bits.
-    // The lane's piece only moves forward with u (f grows by kThreads): a
-    // short catch-up walk per key, the pieces kept 6 bits each for later
-    uint64_t wd[kWPer];
-    uint32_t kid[kWPer];
+    // every key's 8-byte class word (key u = u * kThreads + tid): POS, the
+    // tail's id, displaced flag -- the 8-byte hash and 16-byte body only for
+    // the few keys without an id.  The lane's piece only moves forward with
+    // u (f grows by kThreads): a short catch-up walk per key, the pieces kept
+    // 6 bits each for later
+    uint32_t wlo[kWPer], whi[kWPer];  // the class words' halves
     uint32_t okm = 0;
     uint64_t pk = 0;  // piece of key u in bits 6u..6u+5
     {
@@ -883,12 +891,13 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u) {
             const uint32_t f = u * kThreads + threadIdx.x;
-            kid[u] = 0;
-            wd[u] = 0;
+            wlo[u] = 0;
+            whi[u] = 0;
             if (f < total) {
                 while (pc + 1 < np && s_pre[pc + 1] <= f) ++pc;
-                kid[u] = f + s_base[pc];
-                wd[u] = ks.word[kid[u]];
+                const uint64_t wv = ks.word[f + s_base[pc]];
+                wlo[u] = static_cast<uint32_t>(wv);
+                whi[u] = static_cast<uint32_t>(wv >> 32);
                 okm |= 1u << u;
                 pk |= static_cast<uint64_t>(pc) << (6 * u);
             }
@@ -897,121 +906,105 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     if (dbg & 4u) {  // timing ablation (SBEACON_DEDUP_WIN_DBG): loads only
         uint32_t x = 0;
 #pragma unroll
-        for (uint32_t u = 0; u < kWPer; ++u) x += static_cast<uint32_t>(wd[u]);
+        for (uint32_t u = 0; u < kWPer; ++u) x += wlo[u] ^ whi[u];
         if (x == 0xdeadbeefu) atomicOr(overflow, x);
         return;
     }
-    // classes: exact words, hashed, deferred (displaced keys that may have a
-    // copy at a larger POS of the job)
-    uint32_t xw[kWPer];
+    auto kid_of = [&](uint32_t u) { return u * kThreads + threadIdx.x + s_base[static_cast<uint32_t>(pk >> (6 * u)) & 63u]; };
+    // classes: identified (the tail has an id), hashed (no id), deferred
+    // (displaced keys that may have a copy at a larger POS of the job).  A
+    // displaced key with no such copy meets its equal strings at its own POS
     uint32_t em = 0, hm = 0, dm = 0;
     const uint32_t pm10 = W.pmax / 10;
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) {
-        const uint32_t pos = static_cast<uint32_t>(wd[u]);
-        const uint32_t code = static_cast<uint32_t>(wd[u] >> 32) & 63u;
+        const uint32_t pos = wlo[u];
+        const uint32_t id = whi[u] & kWordIdMask;
         const bool ok = (okm >> u) & 1u;
-        const bool disp = (wd[u] & kWordDisplaced) != 0;
+        const bool disp = (whi[u] & static_cast<uint32_t>(kWordDisplaced >> 32)) != 0;
         const bool big = pos > pm10;  // 10 POS > the job's largest POS
-        const bool ex = ok && !disp && code && pos >= W.p0 && ((pos - W.p0) >> kWinSpanBits) == 0;
-        xw[u] = ((pos - W.p0) << 6) | code;
+        const bool ex = ok && (!disp || big) && id && pos >= W.p0 && ((pos - W.p0) >> kWinSpanBits) == 0;
         em |= (ex ? 1u : 0u) << u;
         hm |= ((ok && !ex && (!disp || big)) ? 1u : 0u) << u;
         dm |= ((ok && disp && !big) ? 1u : 0u) << u;
+        if (ex) s_id[u * kThreads + threadIdx.x] = (1ull << 63) | (static_cast<uint64_t>(pos - W.p0) << 29) | id;
     }
-    unsigned long long hv[kWPer];
 #pragma unroll
-    for (uint32_t u = 0; u < kWPer; ++u) hv[u] = ((hm >> u) & 1u) ? ks.hash[kid[u]] : 0ull;
-    // per workgroup: hashed keys (sizes the two sets) and deferred keys (one
-    // reservation in the global list)
+    for (uint32_t u = 0; u < kWPer; ++u)
+        if ((hm >> u) & 1u) s_id[u * kThreads + threadIdx.x] = ks.hash[kid_of(u)] & ~(1ull << 63);
+    // deferred keys: one reservation per workgroup in the global list
     const uint32_t nd = static_cast<uint32_t>(__popc(dm));
     uint32_t dofs = 0;
     if (nd) dofs = atomicAdd(&s_def, nd);
-    {
-        const uint32_t nhw = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(
-            static_cast<int>(wave_sum_u32(static_cast<uint32_t>(__popc(hm))))));
-        if (lane == 0 && nhw) atomicAdd(&s_nh, nhw);
-    }
     __syncthreads();
     if (threadIdx.x == 0 && s_def) {
         const uint32_t at = atomicAdd(n_list, s_def);
         s_def0 = at;
         if (at + s_def > cap) atomicOr(overflow, 1u);
     }
-    // hashed set: H 64-bit slots (load <= 2/3); exact set: the rest
-    const uint32_t nh = s_nh;
-    const uint32_t H = nh ? min(nh + nh / 2 + 8u, kWSetWords / 2 - 8u) : 0u;
-    const uint32_t X = kWSetWords - 2u * H;
-    unsigned long long *hset = reinterpret_cast<unsigned long long *>(sets + X);
-    for (uint32_t i = threadIdx.x * 4; i < kWSetWords; i += kThreads * 4)
-        *reinterpret_cast<uint4 *>(sets + i) = uint4{~0u, ~0u, ~0u, ~0u};
-    __syncthreads();
-    if (nd) {
-        uint32_t at = s_def0 + dofs;
+    uint32_t pend = (dbg & 1u) ? 0u : (em | hm);  // timing ablation: no dedup rounds
+    uint32_t fresh = 0;
+    bool bad = false;
+    for (uint32_t round = 0; round < kWRounds; ++round) {
+        // write: every unresolved key's index to its identity's slot
+        uint32_t sl[kWPer];
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u)
-            if ((dm >> u) & 1u) {
-                if (at < cap) list[at] = uint2{kid[u], s_run[(pk >> (6 * u)) & 63u]};
-                ++at;
+            if ((pend >> u) & 1u) {
+                const uint64_t v = s_id[u * kThreads + threadIdx.x];
+                const uint32_t m = (static_cast<uint32_t>(v) ^ static_cast<uint32_t>(v >> 32) * 0x85EBCA6Bu ^
+                                    round * 0xC2B2AE35u) * 0x9E3779B1u;
+                sl[u] = static_cast<uint32_t>((static_cast<uint64_t>(m ^ (m >> 15)) * kWSlots) >> 32);
+                s_win[sl[u]] = static_cast<uint16_t>(u * kThreads + threadIdx.x);
             }
-    }
-    if (dbg & 1u) em = 0;  // timing ablation: no exact inserts
-    if (dbg & 2u) hm = 0;  // no hashed inserts
-    uint32_t fresh = 0;
-    // exact keys: 32-bit words; the probe loop runs while any lane of the
-    // wave still probes (linear probing, multiply-shift slot)
+        __syncthreads();
+        // read the winners back
 #pragma unroll
-    for (uint32_t u = 0; u < kWPer; ++u) {
-        bool todo = (em >> u) & 1u;
-        uint32_t h = static_cast<uint32_t>((static_cast<uint64_t>(xw[u] * 0x9E3779B1u) * X) >> 32);
-        while (__ballot(todo)) {
-            if (todo) {
-                const uint32_t was = atomicCAS(&sets[h], ~0u, xw[u]);
-                fresh += was == ~0u ? 1u : 0u;
-                todo = was != ~0u && was != xw[u];
-                h = h + 1 == X ? 0u : h + 1;
-            }
-        }
-    }
-    // hashed keys: hash bits 13..63 << 12 | window-local index
-    uint32_t pend = 0;    // hashed keys that met an entry with their hash bits
-    uint32_t ins[kWPer];  // ... and that entry's window-local key index
-#pragma unroll
-    for (uint32_t u = 0; u < kWPer; ++u) {
-        ins[u] = 0;
-        bool todo = (hm >> u) & 1u;
-        if (!__ballot(todo)) continue;
-        const unsigned long long e = ((hv[u] >> 13) << 12) | (u * kThreads + threadIdx.x);
-        uint32_t h = static_cast<uint32_t>((static_cast<uint64_t>(static_cast<uint32_t>(hv[u])) * H) >> 32);
-        while (__ballot(todo)) {
-            if (todo) {
-                const unsigned long long was = atomicCAS(&hset[h], ~0ull, e);
-                fresh += was == ~0ull ? 1u : 0u;
-                if (was != ~0ull && (was >> 12) == (e >> 12)) {
-                    pend |= 1u << u;
-                    ins[u] = static_cast<uint32_t>(was & 0xfff);
+        for (uint32_t u = 0; u < kWPer; ++u)
+            if ((pend >> u) & 1u) {
+                const uint32_t f = u * kThreads + threadIdx.x;
+                const uint32_t w = s_win[sl[u]];
+                const uint64_t v = s_id[f];
+                if (s_id[w] == v) {  // resolved: the winner counts, an equal identity is its duplicate
+                    pend &= ~(1u << u);
+                    if (w == f) {
+                        ++fresh;
+                    } else if (!(v >> 63)) {  // equal hashes: the strings are confirmed below
+                        const uint32_t at = atomicAdd(&s_nconf, 1u);
+                        if (at < kWConfirm) s_conf[at] = w | f << 16;
+                    }
                 }
-                todo = was != ~0ull && (was >> 12) != (e >> 12);
-                h = h + 1 == H ? 0u : h + 1;
             }
-        }
+        if (!__syncthreads_or(pend != 0u)) break;  // also orders this round's reads before the next writes
+        if (round + 1 == kWRounds && threadIdx.x == 0) atomicOr(overflow, 1u);  // unresolved: the sorted path
     }
-    // the strings of a repeated hash must match the inserter's (rare: key by
-    // key; the general decimal-concatenation comparison only for different
-    // POS or two blob tails)
-    bool bad = false;
-#pragma unroll
-    for (uint32_t u = 0; u < kWPer; ++u) {
-        if (!__ballot((pend >> u) & 1u)) continue;
-        if ((pend >> u) & 1u) {
-            uint32_t q = 0;  // the inserter's piece
-            while (q + 1 < np && s_pre[q + 1] <= ins[u]) ++q;
-            const KBody xb = ks.body[ins[u] + s_base[q]], b = ks.body[kid[u]];
+    // hashed duplicates: the strings of every pair (winner, key) must be equal
+    // (the general decimal-concatenation comparison only for different POS
+    // or two blob tails); more pairs than the list: the sorted path
+    {
+        const uint32_t nc = s_nconf;
+        if (nc > kWConfirm && threadIdx.x == 0) bad = true;
+        for (uint32_t i = threadIdx.x; i < min(nc, kWConfirm); i += kThreads) {
+            const uint32_t w = s_conf[i] & 0xffffu, f = s_conf[i] >> 16;
+            uint32_t q = 0, r = 0;
+            while (q + 1 < np && s_pre[q + 1] <= w) ++q;
+            while (r + 1 < np && s_pre[r + 1] <= f) ++r;
+            const KBody xb = ks.body[w + s_base[q]], b = ks.body[f + s_base[r]];
             if (!(xb.pos == b.pos && xb.tail == b.tail)) {
                 if (xb.pos == b.pos && !((xb.tail & b.tail) & kTailBlob)) bad = true;
                 else if (!body_equal(ks, xb, b)) bad = true;
             }
         }
+    }
+    if (nd) {
+        uint32_t at = s_def0 + dofs;
+#pragma unroll
+        for (uint32_t u = 0; u < kWPer; ++u)
+            if ((dm >> u) & 1u) {
+                const uint32_t pc = static_cast<uint32_t>(pk >> (6 * u)) & 63u;
+                if (at < cap) list[at] = uint2{u * kThreads + threadIdx.x + s_base[pc], s_run[pc]};
+                ++at;
+            }
     }
     if (bad) atomicOr(overflow, 1u);
     const uint32_t fw = wave_sum_u32(fresh);

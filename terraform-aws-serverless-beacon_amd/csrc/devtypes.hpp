@@ -570,11 +570,13 @@ inline constexpr uint32_t kWinTarget = 1536; // keys a window is planned for (ru
 inline constexpr uint32_t kWinPieces = 64;   // pieces (= runs) per window
 inline constexpr uint32_t kWinSpanBits = 26; // p1 - p0 < 2^26 - 1: exact words fit 32 bits
 
-// one 8-byte class word per key (window dedup reads only this for most
-// keys): POS in bits 0..31, the exact code c1 c2 (compressSeq codes of a
-// single-base REF and ALT, 0 = the key is not of that class) in bits 32..37,
-// kWordDisplaced when the tail starts with a digit
+// one 8-byte class word per key (the window dedup reads only this for
+// almost every key): POS in bits 0..31, the tail's store-wide id in bits
+// 32..60 (< 64: c1 << 3 | c2, the compressSeq codes of a single-base REF and
+// ALT; 0: no id, the key is hashed), kWordDisplaced when the tail starts
+// with a digit
 inline constexpr uint64_t kWordDisplaced = 1ull << 62;
+inline constexpr uint32_t kWordIdMask = (1u << 29) - 1;
 struct KStore {
     const uint64_t *hash;
     const KBody *body;

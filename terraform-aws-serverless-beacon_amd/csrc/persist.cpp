@@ -49,7 +49,7 @@
 namespace sb {
 
 constexpr uint64_t kMagic = 0x3150544f5453424full;  // "OBSTOTP1"
-constexpr uint32_t kFormat = 1;
+constexpr uint32_t kFormat = 2;  // 2: dedup class words carry tail ids
 
 // FNV-1a over the first and last 64 KiB (with the size and mtime, a change
 // detector -- not a content address)

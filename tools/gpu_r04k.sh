@@ -1,9 +1,8 @@
-# window_dedupe_kernel ablations (tools/dedup_ablate.py) + config-3 bench with
-# the pipelined delivered path
+# window dedup with tail ids (identified keys exact, no hash confirmation): tests + ablations
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/${TAG:-r04i}
+OUT=$R/gpurun_out/${TAG:-r04k}
 mkdir -p $OUT
 step() {  # name, limit, command...
   local name=$1 lim=$2; shift 2
@@ -11,8 +10,7 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; tail -2 $OUT/$name.log | cut -c1-300
   case $rc in 0) return 0;; *) exit $rc;; esac
 }
+step tests 500 python3 -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread -k "dedup or pipeline or persist"
 step ablate 500 python3 -u $R/tools/dedup_ablate.py
 grep mode $OUT/ablate.log
-step genome 600 python3 -u $R/bench.py --no-cpu-baseline
-grep -o '"delivered[^}]*}[^}]*}[^}]*}' $OUT/genome.log
 exit 0
