@@ -319,7 +319,43 @@ def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5)
                     'memory; routing, planning, upload, the pass and both D2H copies inside the timed region'}
 
 
-def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes=5, chunks=8):
+def cold_launch_probe(store, shape, reqs, world, rank, base, dev):
+    """The eval launch of a freshly prepared batch, timed alone (HIP events
+    around request_eval_kernel): its first launch, a second launch of the
+    same batch right after, and the first launch of another fresh batch
+    issued right behind ~2 ms of unrelated GPU work (a busy device: no clock
+    ramp)."""
+    import torch
+    from sbeacon.genome import prepare_shard_requests, shard_requests
+    sr = shard_requests(shape, reqs, world, rank)
+    out = {}
+    for label in ('fresh', 'after_busy'):
+        torch.cuda.synchronize()
+        time.sleep(0.05)  # an idle device, as after host planning
+        bt = prepare_shard_requests(store, sr)
+        bt.set_stream(torch.cuda.current_stream().cuda_stream)
+        cap = int(bt.stats()['hits'])
+        rows = torch.empty((max(sr.n_rows, 1), 5), dtype=torch.int64, device=dev)
+        hits = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
+        ro = torch.empty(sr.n_rows + 1, dtype=torch.int64, device=dev)
+        if label == 'after_busy':
+            a = torch.randn(4096, 4096, device=dev)
+            for _ in range(8):
+                a = a @ a
+                a = a / a.norm()
+        bt.time_eval(True)
+        ms = []
+        for _ in range(2):
+            bt.run(rows.data_ptr(), hits.data_ptr(), ro.data_ptr(), base)
+            bt.sync()
+            ms.append(round(bt.timing()['scan_ms'], 4))
+        bt.time_eval(False)
+        bt.free()
+        out[label] = {'first_ms': ms[0], 'second_ms': ms[1]}
+    return out
+
+
+def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes=5, chunks=8, workers=2):
     """The delivered path in chunks of consecutive request rows, pipelined:
     two host threads route and prepare chunks ahead (numpy, then
     sb_requests_prepare_columns: pack, upload and the planning kernels on the
@@ -349,7 +385,7 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
     ro_d = torch.empty(n + chunks, dtype=torch.int64, device=dev)
     hits_d, hits_h = [None] * chunks, [None] * chunks
     times, total_hits = [], 0
-    with ThreadPoolExecutor(2) as ex:
+    with ThreadPoolExecutor(workers) as ex:
         for p in range(passes + 1):  # pass 0 sizes the hit buffers (untimed)
             torch.cuda.synchronize()
             t0 = time.perf_counter()
@@ -391,7 +427,7 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
                 times.append(dt)
     dt = sum(times) / len(times)
     return {'requests_per_s': round(n / dt, 1), 'ms_per_pass': round(dt * 1e3, 2),
-            'best_ms': round(min(times) * 1e3, 2), 'passes': passes, 'chunks': chunks,
+            'best_ms': round(min(times) * 1e3, 2), 'passes': passes, 'chunks': chunks, 'workers': workers,
             'hits_returned': total_hits,
             'note': 'pipelined: the requests cut into chunks of consecutive rows; 2 host threads route + prepare '
                     'chunks ahead while each prepared chunk runs and copies back (rows, per-chunk row offsets, '

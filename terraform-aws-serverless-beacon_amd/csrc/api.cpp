@@ -378,6 +378,9 @@ struct sb_batch {
         }
     };
     std::unique_ptr<Req> req;
+    // slice batches: device buffers from the store's pool (a steady stream
+    // of batches then allocates nothing), given back when the batch is freed
+    std::shared_ptr<ReqPool> pool;
     // general records (general_slice_kernel): work list [count, launch
     // indices], per-wave scratch, slices with counts past 64 bits
     DevMem gen_work, gen_scratch, gen_big_n, gen_big, gen_limbs;
@@ -390,11 +393,40 @@ struct sb_batch {
     ~sb_batch() {
         for (auto e : ev)
             if (e) (void)hipEventDestroy(e);
-        if (req && req->pool) {  // the pass may still be in flight on the batch's stream
-            (void)hipStreamSynchronize(strm());
-            req->give_back();
-        }
+        if ((req && req->pool) || pool) (void)hipStreamSynchronize(strm());  // a pass may still be in flight
+        if (req && req->pool) req->give_back();
+        if (pool)
+            for (DevMem *m : {&q, &hoff, &qbytes, &subsets, &lut, &res, &hits, &samples_out, &chains, &runs, &corig,
+                              &srcoff, &cpart, &gen_work, &gen_scratch, &gen_big_n, &gen_big, &gen_limbs})
+                if (m->p) pool->put_dev(std::move(*m));
     }
+};
+
+// a batch buffer: from the batch's pool when it has one
+void palloc(sb_batch &B, DevMem &m, size_t n) {
+    if (!B.pool) {
+        m.alloc(n);
+        return;
+    }
+    if (m.p) B.pool->put_dev(std::move(m));
+    m = B.pool->get_dev(std::max<size_t>(n, 16));
+}
+
+// a result set's dense hit list: pinned host memory from the store's pool
+// (the D2H lands there directly; no zero-filled pageable copy)
+struct HitBuf {
+    std::shared_ptr<ReqPool> pool;
+    ReqPool::Pinned mem;
+    size_t n = 0;
+    HitBuf() = default;
+    HitBuf(const HitBuf &) = delete;
+    HitBuf &operator=(const HitBuf &) = delete;
+    ~HitBuf() {
+        if (mem.p) pool->put_pinned(mem);
+    }
+    uint64_t *data() { return static_cast<uint64_t *>(mem.p); }
+    const uint64_t &operator[](size_t i) const { return static_cast<const uint64_t *>(mem.p)[i]; }
+    size_t size() const { return n; }
 };
 
 struct sb_result_set {
@@ -404,7 +436,7 @@ struct sb_result_set {
     }
     std::vector<QRes> res;
     std::vector<uint64_t> dense_off;
-    std::vector<uint64_t> hit;                  // rec | alt << 32
+    HitBuf hit;                                 // rec | alt << 32
     std::vector<std::vector<uint32_t>> sidx;    // emitted-list positions
     std::vector<std::vector<uint32_t>> emitted;
     std::vector<uint32_t> vcf_of;
@@ -417,7 +449,9 @@ struct sb_result_set {
     // per VCF of the set, per header sample: its name as JSON list items
     // (sb::result_prepare_json; "\x01" = not UTF-8)
     std::vector<std::vector<std::string>> names_json;
-    std::vector<uint32_t> tmp_rec, tmp_alt;     // views for sb_result_get
+    // views for sb_result_get, split out of `hit` on its first call
+    mutable std::vector<uint32_t> tmp_rec, tmp_alt;
+    mutable std::once_flag tmp_once;
     // queries whose counts need more than 64 bits: 2 x big_limbs limbs each
     uint32_t big_limbs = 0;
     std::unordered_map<uint32_t, std::vector<uint32_t>> big;
@@ -1017,6 +1051,25 @@ void parallel_for(size_t n, F fn, unsigned threads = 16, size_t grain = 4096) {
     for (auto &x : th) x.join();
 }
 
+}  // namespace
+
+namespace sb {
+// n tasks on the persistent worker pool (own threads when it is taken):
+// the wire formatter's phases (csrc/wire.cpp)
+void run_tasks(size_t n, const std::function<void(size_t)> &fn) {
+    if (n <= 1) {
+        for (size_t i = 0; i < n; ++i) fn(i);
+        return;
+    }
+    if (WorkerPool::get().try_run(n, [&](size_t k) { fn(k); })) return;
+    std::vector<std::thread> th;
+    for (size_t k = 0; k < n; ++k) th.emplace_back([&, k] { fn(k); });
+    for (auto &x : th) x.join();
+}
+}  // namespace sb
+
+namespace {
+
 // Chains of consecutive variantType slices (devtypes.hpp ChainDev).  vt =
 // the MODE_VTYPE queries in input order; returns those left to vt_slice.
 // Slices chain when they share the VCF segment and every filter, each starts
@@ -1190,6 +1243,14 @@ std::vector<uint32_t> plan_chains(sb_batch &B, const std::vector<uint32_t> &segi
 void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     sb_store &s = *B.s;
     if (nq >= (1u << 31)) throw Error(SB_EINVAL, "batch too large");
+    static const bool trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;  // phase times (bench diagnostics)
+    auto t_last = std::chrono::steady_clock::now();
+    auto tick = [&](const char *what) {
+        if (!trace) return;
+        const auto t = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[prepare] %-8s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+        t_last = t;
+    };
     B.nq = static_cast<uint32_t>(nq);
     std::vector<uint32_t> segi(nq, UINT32_MAX);  // segment index of each query in its VCF
     std::vector<uint64_t> cap(nq, 0);           // hit-region capacity of each query
@@ -1210,15 +1271,18 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     std::vector<uint32_t> lut_all;
     std::unordered_map<std::string, uint32_t> lut_cache;
     uint64_t samples_words = 0;
-    for (size_t i = 0; i < nq; ++i) {
+    for (size_t i = 0; i < nq; ++i) {  // what raises for the whole batch, first
+        if (qs[i].vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "query " + std::to_string(i) + ": unknown vcf id");
+        if (!qs[i].region) throw Error(SB_EINVAL, "query " + std::to_string(i) + ": region is NULL");
+    }
+    // per query, in parallel: region, segment, bounds, predicates (no shared state)
+    parallel_for(nq, [&](size_t i) {
         const sb_query &x = qs[i];
         QDev &d = B.hq[i];
         d.subset_off = ~0ull;
         d.samples_out_off = ~0ull;
-        if (x.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "query " + std::to_string(i) + ": unknown vcf id");
         const VcfData &v = s.vcfs[x.vcf_id];
         B.vcf[i] = x.vcf_id;
-        if (!x.region) throw Error(SB_EINVAL, "query " + std::to_string(i) + ": region is NULL");
         const ParsedRegion rg = parse_region(x.region, x.region_len);
         B.chrom[i] = rg.chrom;
         if (!rg.ok) {
@@ -1245,15 +1309,94 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         d.end_max = x.end_max;
         const bool samples_variant = x.selected_samples_only != 0;
         B.samples_variant[i] = samples_variant;
-        const uint32_t n_samples = static_cast<uint32_t>(v.samples.size());
         d.words = v.words;
-        d.n_samples = n_samples;
+        d.n_samples = static_cast<uint32_t>(v.samples.size());
         d.rec_base = v.rec_base;
         d.x_base = v.x_base;
         d.an_default = v.an_default;
         d.plane0_base = v.plane0_base;
         d.planex_base = v.planex_base;
         if (v.nonneg) d.flags |= F_NONNEG;
+        // REF predicate (:59, :94 / svs:87-91)
+        if (!x.reference_bases) {
+            if (samples_variant) {
+                d.ref_mode = REF_ERROR;
+                d.ref_err = SB_QERR_ATTRIBUTE;
+            } else {
+                d.ref_mode = REF_NEVER;
+            }
+        } else {
+            const char *rb = x.reference_bases;
+            const size_t rn = x.reference_len;
+            d.ref_len = static_cast<uint32_t>(rn);
+            auto has_any = [&](const char *set) {
+                for (size_t k = 0; k < rn; ++k)
+                    if (std::strchr(set, rb[k]) && rb[k]) return true;
+                return false;
+            };
+            if (rn == 1 && rb[0] == 'N') {
+                d.ref_mode = REF_ANY;
+            } else if (samples_variant && has_any(kRegexMeta)) {
+                d.ref_mode = REF_ERROR;
+                d.ref_err = SB_QERR_UNSUPPORTED;
+            } else if (samples_variant && has_any("N.")) {
+                d.ref_mode = REF_WILD;
+            } else {
+                d.ref_mode = REF_EXACT;
+                bool h;
+                d.ref_key = allele_key(reinterpret_cast<const uint8_t *>(rb), rn, false, &h);
+            }
+        }
+        // ALT predicate (:100-183)
+        if (!x.alternate_bases) {
+            d.alt_mode = ALT_VTYPE;
+            if (x.strict_variant_type) d.flags |= F_STRICT_UNBOUND;
+            const std::string_view vt = x.variant_type ? std::string_view(x.variant_type, x.variant_type_len)
+                                                       : std::string_view("None");
+            const bool has = x.variant_type != nullptr;
+            d.vt_kind = !has                 ? VT_OTHER
+                        : vt == "DEL"        ? VT_DEL
+                        : vt == "INS"        ? VT_INS
+                        : vt == "DUP"        ? VT_DUP
+                        : vt == "DUP:TANDEM" ? VT_DUPT
+                        : vt == "CNV"        ? VT_CNV
+                                             : VT_OTHER;
+        } else {
+            const char *ab = x.alternate_bases;
+            const size_t an = x.alternate_len;
+            d.alt_len = static_cast<uint32_t>(an);
+            if (an == 1 && ab[0] == 'N') {
+                d.alt_mode = ALT_N;
+            } else {
+                d.alt_mode = ALT_EXACT;
+                bool h;
+                d.alt_key = allele_key(reinterpret_cast<const uint8_t *>(ab), an, false, &h);
+            }
+        }
+        d.vmin = x.variant_min_length;
+        d.vmax = x.variant_max_length < 0 ? INT64_MAX : x.variant_max_length;
+        if (x.include_details) d.flags |= F_DETAILS;
+        if (samples_variant) d.flags |= F_SAMPLES_VARIANT;
+        if (x.granularity == SB_GRAN_BOOLEAN && !samples_variant) d.flags |= F_BOOL_BREAK;
+        // output region: every ALT row of the records in the coarse bracket
+        // (offsets assigned below, once the chains are known)
+        if (!(d.flags & F_EMPTY) && d.first_bp <= d.last_bp) {
+            const uint32_t lo = bucket_floor(s, d, d.first_bp);
+            const uint32_t hi = std::max(lo, bucket_ceil(s, d, d.last_bp + 1));
+            cap[i] = static_cast<uint64_t>(hi - lo) + (s.h_x_lo[hi] - s.h_x_lo[lo]);
+        }
+    }, 16, 1024);
+    // in batch order: the shared tables (sample subsets, predicate bytes,
+    // variantType LUTs, sample output words)
+    const char *last_vt = nullptr;
+    size_t last_vt_len = 0;
+    uint32_t last_vt_kind = ~0u, last_lut = 0;
+    for (size_t i = 0; i < nq; ++i) {
+        const sb_query &x = qs[i];
+        QDev &d = B.hq[i];
+        const VcfData &v = s.vcfs[x.vcf_id];
+        const bool samples_variant = B.samples_variant[i] != 0;
+        const uint32_t n_samples = d.n_samples;
         if (samples_variant) {  // bcftools --samples (svs:36-42), header order
             const std::string names = x.sample_names ? std::string(x.sample_names, x.sample_names_len) : std::string("_");
             // requests of one batch often share a sampleNames list: one mask each
@@ -1288,71 +1431,30 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
             d.subset_off = hit->second.off;
             B.emitted[i] = hit->second.emitted;
         }
-        // REF predicate (:59, :94 / svs:87-91)
         d.qbytes_off = static_cast<uint32_t>(qbytes.size());
-        if (!x.reference_bases) {
-            if (samples_variant) {
-                d.ref_mode = REF_ERROR;
-                d.ref_err = SB_QERR_ATTRIBUTE;
-            } else {
-                d.ref_mode = REF_NEVER;
-            }
-        } else {
-            const std::string rb(x.reference_bases, x.reference_len);
-            d.ref_len = static_cast<uint32_t>(rb.size());
-            qbytes.insert(qbytes.end(), rb.begin(), rb.end());
-            if (rb == "N") {
-                d.ref_mode = REF_ANY;
-            } else if (samples_variant && rb.find_first_of(kRegexMeta) != std::string::npos) {
-                d.ref_mode = REF_ERROR;
-                d.ref_err = SB_QERR_UNSUPPORTED;
-            } else if (samples_variant && rb.find_first_of("N.") != std::string::npos) {
-                d.ref_mode = REF_WILD;
-            } else {
-                d.ref_mode = REF_EXACT;
-                bool h;
-                d.ref_key = allele_key(reinterpret_cast<const uint8_t *>(rb.data()), rb.size(), false, &h);
-            }
-        }
-        // ALT predicate (:100-183)
+        if (x.reference_bases) qbytes.insert(qbytes.end(), x.reference_bases, x.reference_bases + x.reference_len);
         if (!x.alternate_bases) {
-            d.alt_mode = ALT_VTYPE;
-            if (x.strict_variant_type) d.flags |= F_STRICT_UNBOUND;
-            const std::string vt = x.variant_type ? std::string(x.variant_type, x.variant_type_len) : std::string("None");
-            const bool has = x.variant_type != nullptr;
-            d.vt_kind = !has                 ? VT_OTHER
-                        : vt == "DEL"        ? VT_DEL
-                        : vt == "INS"        ? VT_INS
-                        : vt == "DUP"        ? VT_DUP
-                        : vt == "DUP:TANDEM" ? VT_DUPT
-                        : vt == "CNV"        ? VT_CNV
-                                             : VT_OTHER;
-            const std::string key = std::to_string(d.vt_kind) + "|" + vt;
-            auto lt = lut_cache.find(key);
-            if (lt == lut_cache.end()) {
-                const auto lut = sym_lut(s, d.vt_kind, "<" + vt);
-                const uint32_t off = static_cast<uint32_t>(lut_all.size());
-                lut_all.insert(lut_all.end(), lut.begin(), lut.end());
-                lt = lut_cache.emplace(key, off).first;
+            const char *vt = x.variant_type ? x.variant_type : "None";
+            const size_t vl = x.variant_type ? x.variant_type_len : 4;
+            if (!(d.vt_kind == last_vt_kind && vl == last_vt_len && last_vt &&
+                  (vt == last_vt || std::memcmp(vt, last_vt, vl) == 0))) {  // a new (kind, variantType) pair
+                const std::string key = std::to_string(d.vt_kind) + "|" + std::string(vt, vl);
+                auto lt = lut_cache.find(key);
+                if (lt == lut_cache.end()) {
+                    const auto lut = sym_lut(s, d.vt_kind, "<" + std::string(vt, vl));
+                    const uint32_t off = static_cast<uint32_t>(lut_all.size());
+                    lut_all.insert(lut_all.end(), lut.begin(), lut.end());
+                    lt = lut_cache.emplace(key, off).first;
+                }
+                last_vt = vt;
+                last_vt_len = vl;
+                last_vt_kind = d.vt_kind;
+                last_lut = lt->second;
             }
-            d.lut_off = lt->second;
+            d.lut_off = last_lut;
         } else {
-            const std::string ab(x.alternate_bases, x.alternate_len);
-            d.alt_len = static_cast<uint32_t>(ab.size());
-            qbytes.insert(qbytes.end(), ab.begin(), ab.end());
-            if (ab == "N") {
-                d.alt_mode = ALT_N;
-            } else {
-                d.alt_mode = ALT_EXACT;
-                bool h;
-                d.alt_key = allele_key(reinterpret_cast<const uint8_t *>(ab.data()), ab.size(), false, &h);
-            }
+            qbytes.insert(qbytes.end(), x.alternate_bases, x.alternate_bases + x.alternate_len);
         }
-        d.vmin = x.variant_min_length;
-        d.vmax = x.variant_max_length < 0 ? INT64_MAX : x.variant_max_length;
-        if (x.include_details) d.flags |= F_DETAILS;
-        if (samples_variant) d.flags |= F_SAMPLES_VARIANT;
-        if (x.granularity == SB_GRAN_BOOLEAN && !samples_variant) d.flags |= F_BOOL_BREAK;
         const bool collect = (x.granularity == SB_GRAN_RECORD || x.granularity == SB_GRAN_AGGREGATED) &&
                              (samples_variant || x.include_samples);
         if (collect) {
@@ -1363,15 +1465,9 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
                 samples_words += v.words;
             }
         }
-        // output region: every ALT row of the records in the coarse bracket
-        // (offsets assigned below, once the chains are known)
-        if (!(d.flags & F_EMPTY) && d.first_bp <= d.last_bp) {
-            const uint32_t lo = bucket_floor(s, d, d.first_bp);
-            const uint32_t hi = std::max(lo, bucket_ceil(s, d, d.last_bp + 1));
-            cap[i] = static_cast<uint64_t>(hi - lo) + (s.h_x_lo[hi] - s.h_x_lo[lo]);
-        }
     }
     B.samples_words = samples_words;
+    tick("queries");
     {
         // collect -> general kernel with the sample path; otherwise the
         // narrowest specialisation whose predicates cover the query
@@ -1404,19 +1500,42 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
             auto &vg = B.groups[MODE_VTYPE].idx;
             vg = plan_chains(B, segi, vg);
         }
+        tick("chains");
         std::vector<sb_batch::Group> keep;
         for (auto &g : B.groups)
             if (!g.idx.empty()) keep.push_back(std::move(g));
         B.groups = std::move(keep);
         // launch order = (segment, first base): neighbouring waves scan
         // neighbouring records (with the kernels' XCD-aware block order,
-        // one XCD's L2 serves a contiguous stretch of the store)
-        for (auto &g : B.groups)
-            std::stable_sort(g.idx.begin(), g.idx.end(), [&](uint32_t a, uint32_t b) {
-                const QDev &x = B.hq[a], &y = B.hq[b];
-                return x.seg_lo != y.seg_lo ? x.seg_lo < y.seg_lo : x.first_bp < y.first_bp;
-            });
+        // one XCD's L2 serves a contiguous stretch of the store).  Sorted as
+        // packed (segment, first base, position) words: the same order as a
+        // stable sort on (seg_lo, first_bp)
+        for (auto &g : B.groups) {
+            const size_t m = g.idx.size();
+            bool packable = true;
+            for (uint32_t i : g.idx) {
+                const QDev &x = B.hq[i];
+                packable = packable && x.first_bp >= 0 && x.first_bp < (int64_t(1) << 32);
+            }
+            if (!packable || m >= (size_t(1) << 31)) {
+                std::stable_sort(g.idx.begin(), g.idx.end(), [&](uint32_t a, uint32_t b) {
+                    const QDev &x = B.hq[a], &y = B.hq[b];
+                    return x.seg_lo != y.seg_lo ? x.seg_lo < y.seg_lo : x.first_bp < y.first_bp;
+                });
+                continue;
+            }
+            std::vector<std::pair<uint64_t, uint32_t>> key(m);  // (seg_lo, first_bp), then input position
+            for (size_t k = 0; k < m; ++k) {
+                const QDev &x = B.hq[g.idx[k]];
+                key[k] = {static_cast<uint64_t>(x.seg_lo) << 32 | static_cast<uint64_t>(x.first_bp), static_cast<uint32_t>(k)};
+            }
+            std::sort(key.begin(), key.end());
+            std::vector<uint32_t> idx(m);
+            for (size_t k = 0; k < m; ++k) idx[k] = g.idx[key[k].second];
+            g.idx = std::move(idx);
+        }
     }
+    tick("groups");
     {  // hit regions: unchained queries in batch order, then each chain's slices
         // back to back (a chain writes its hits densely from its first slot)
         uint64_t at = 0;
@@ -1441,6 +1560,7 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     if (s.device < 0) return;  // a host-only store: the plan stays on the host
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = s.stream;
+    if (!B.pool) B.pool = req_pool(s);
     // device query array in launch order (groups back to back, each sorted by
     // segment and first base): a wave reads its query at qs + w, with no index
     // load in front; QDev::orig names the QRes row
@@ -1472,11 +1592,11 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
         }
         B.hruns.push_back(static_cast<uint32_t>(B.hchains.size()));
     }
-    B.runs.alloc(B.hruns.size() * 4);
+    palloc(B, B.runs, B.hruns.size() * 4);
     HIP_OK(hipMemcpyAsync(B.runs.p, B.hruns.data(), B.hruns.size() * 4, hipMemcpyHostToDevice, st));
-    B.chains.alloc(B.hchains.size() * sizeof(ChainDev));
-    B.corig.alloc(B.chain_members.size() * 4);
-    B.cpart.alloc(B.hchains.size() * sizeof(ReqPartial));
+    palloc(B, B.chains, B.hchains.size() * sizeof(ChainDev));
+    palloc(B, B.corig, B.chain_members.size() * 4);
+    palloc(B, B.cpart, B.hchains.size() * sizeof(ReqPartial));
     if (!B.hchains.empty()) {
         HIP_OK(hipMemcpyAsync(B.chains.p, B.hchains.data(), B.hchains.size() * sizeof(ChainDev), hipMemcpyHostToDevice,
                               st));
@@ -1485,37 +1605,39 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     }
     std::vector<uint64_t> hoff(nq);
     for (uint32_t i = 0; i < nq; ++i) hoff[i] = B.hq[i].hit_off;
-    B.q.alloc(nq * sizeof(QDev));
-    B.hoff.alloc(nq * 8);
-    B.qbytes.alloc(qbytes.size());
-    B.subsets.alloc(subsets.size() * 8);
-    B.lut.alloc(lut_all.size() * 4);
+    palloc(B, B.q, nq * sizeof(QDev));
+    palloc(B, B.hoff, nq * 8);
+    palloc(B, B.qbytes, qbytes.size());
+    palloc(B, B.subsets, subsets.size() * 8);
+    palloc(B, B.lut, lut_all.size() * 4);
     if (nq) HIP_OK(hipMemcpyAsync(B.q.p, lq.data(), nq * sizeof(QDev), hipMemcpyHostToDevice, st));
     if (nq) HIP_OK(hipMemcpyAsync(B.hoff.p, hoff.data(), nq * 8, hipMemcpyHostToDevice, st));
     if (!B.hchains.empty()) {
-        B.srcoff.alloc(nq * 8);
+        palloc(B, B.srcoff, nq * 8);
         HIP_OK(hipMemcpyAsync(B.srcoff.p, hoff.data(), nq * 8, hipMemcpyHostToDevice, st));
     }
     if (!qbytes.empty()) HIP_OK(hipMemcpyAsync(B.qbytes.p, qbytes.data(), qbytes.size(), hipMemcpyHostToDevice, st));
     if (!subsets.empty()) HIP_OK(hipMemcpyAsync(B.subsets.p, subsets.data(), subsets.size() * 8, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(B.lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
 
-    B.res.alloc(size_t(nq) * sizeof(QRes));
-    B.hits.alloc(B.cap_total * 8);
-    B.samples_out.alloc(samples_words * 8);
+    palloc(B, B.res, size_t(nq) * sizeof(QRes));
+    palloc(B, B.hits, B.cap_total * 8);
+    palloc(B, B.samples_out, samples_words * 8);
     if (s.g.n && nq) {  // general records: work list + scratch (general_slice_kernel)
         uint32_t hw, tc;
         const uint64_t wb = general_wave_bytes(s.g, &hw, &tc);
         const uint64_t budget = uint64_t(256) << 20;
         B.gen_grid = static_cast<uint32_t>(std::max<uint64_t>(1, std::min<uint64_t>({nq, 1024, budget / wb})));
-        B.gen_work.alloc((size_t(nq) + 1) * 4);
-        B.gen_scratch.alloc(size_t(B.gen_grid) * wb);
+        palloc(B, B.gen_work, (size_t(nq) + 1) * 4);
+        palloc(B, B.gen_scratch, size_t(B.gen_grid) * wb);
         B.gen_big_cap = std::min<uint32_t>(nq, 4096);
-        B.gen_big_n.alloc(4);
-        B.gen_big.alloc(size_t(B.gen_big_cap) * sizeof(GenBig));
-        B.gen_limbs.alloc(size_t(B.gen_big_cap) * 2 * kGenAccMax * 4);
+        palloc(B, B.gen_big_n, 4);
+        palloc(B, B.gen_big, size_t(B.gen_big_cap) * sizeof(GenBig));
+        palloc(B, B.gen_limbs, size_t(B.gen_big_cap) * 2 * kGenAccMax * 4);
     }
+    tick("buffers");
     HIP_OK(hipStreamSynchronize(st));
+    tick("upload");
 }
 
 // timing: one event before the first run since the last sync and one at the
@@ -1654,11 +1776,12 @@ sb_result_set *fetch(sb_batch &B) {
     R->dense_off.assign(size_t(nq) + 1, 0);
     for (uint32_t i = 0; i < nq; ++i) R->dense_off[i + 1] = R->dense_off[i] + (R->res[i].error ? 0 : R->res[i].n_hits);
     const uint64_t total = R->dense_off[nq];
-    R->hit.resize(total);
+    R->hit.pool = req_pool(s);
+    R->hit.n = total;
     if (total) {
-        DevMem doff, dense;
-        doff.alloc((size_t(nq) + 1) * 8);
-        dense.alloc(total * 8);
+        ReqPool &P = *R->hit.pool;
+        DevMem doff = P.get_dev((size_t(nq) + 1) * 8), dense = P.get_dev(total * 8);
+        R->hit.mem = P.get_pinned(total * 8);
         HIP_OK(hipMemcpyAsync(doff.p, R->dense_off.data(), (size_t(nq) + 1) * 8, hipMemcpyHostToDevice, st));
         const uint64_t *hoff = src_offsets(B, st);
         // queries with an error report n_hits = 0 on the device (host errors are F_EMPTY)
@@ -1666,6 +1789,8 @@ sb_result_set *fetch(sb_batch &B) {
         HIP_OK(hipGetLastError());
         HIP_OK(hipMemcpyAsync(R->hit.data(), dense.p, total * 8, hipMemcpyDeviceToHost, st));
         HIP_OK(hipStreamSynchronize(st));
+        P.put_dev(std::move(doff));
+        P.put_dev(std::move(dense));
     }
     R->sidx.assign(nq, std::vector<uint32_t>());
     R->emitted = B.emitted;
@@ -1692,12 +1817,6 @@ sb_result_set *fetch(sb_batch &B) {
     R->ntext.assign(nq, std::string());
     R->vbuilt.assign(nq, 0);
     R->nbuilt.assign(nq, 0);
-    R->tmp_rec.resize(total);
-    R->tmp_alt.resize(total);
-    for (uint64_t h = 0; h < total; ++h) {
-        R->tmp_rec[h] = static_cast<uint32_t>(R->hit[h]);
-        R->tmp_alt[h] = static_cast<uint32_t>(R->hit[h] >> kHitAltShift);
-    }
     R->stats.n_queries = nq;
     R->stats.records_scanned = scanned;
     R->stats.chained_slices = B.chain_members.size();
@@ -4115,15 +4234,43 @@ int sb_query_batch(sb_store *s, const sb_query *q, size_t nq, uint32_t flags, sb
     return guard([&] {
         if (!s || (!q && nq) || !out) throw Error(SB_EINVAL, "NULL argument");
         std::lock_guard<std::mutex> lk(s->mu);
+        static const bool trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;  // phase times (bench diagnostics)
+        auto t0 = std::chrono::steady_clock::now();
+        auto tick = [&](const char *what) {
+            if (!trace) return;
+            const auto t = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "[query] %-8s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t0).count());
+            t0 = t;
+        };
         sb_batch B;
         B.s = s;
         prepare(B, q, nq);
+        tick("prepare");
         run(B);
+        tick("run");
         *out = fetch(B);
+        tick("fetch");
     });
 }
 
 int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out) {
+    if (!r || !out || i >= r->res.size()) return SB_EINVAL;
+    std::call_once(r->tmp_once, [r] {  // the record / ALT views of every hit
+        const size_t total = r->hit.size();
+        r->tmp_rec.resize(total);
+        r->tmp_alt.resize(total);
+        parallel_for(total, [r](size_t h) {
+            r->tmp_rec[h] = static_cast<uint32_t>(r->hit[h]);
+            r->tmp_alt[h] = static_cast<uint32_t>(r->hit[h] >> kHitAltShift);
+        }, 16, 1 << 16);
+    });
+    return sb::result_view(r, i, out);
+}
+}  // extern "C"
+
+namespace sb {
+// sb_result_get without the hit views (the wire formatter)
+int result_view(const sb_result_set *r, size_t i, sb_result_view *out) {
     if (!r || !out || i >= r->res.size()) return SB_EINVAL;
     const QRes &q = r->res[i];
     out->error = q.error;
@@ -4132,8 +4279,9 @@ int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out) {
     out->all_alleles_count = q.all_alleles_count;
     const uint64_t a = r->dense_off[i], b = r->dense_off[i + 1];
     out->n_variants = q.error ? 0 : b - a;
-    out->hit_record = r->tmp_rec.data() + a;
-    out->hit_alt = r->tmp_alt.data() + a;
+    const bool views = r->tmp_rec.size() == r->hit.size();  // sb_result_get split them
+    out->hit_record = views ? r->tmp_rec.data() + a : nullptr;
+    out->hit_alt = views ? r->tmp_alt.data() + a : nullptr;
     out->n_sample_indices = r->sidx[i].size();
     out->sample_indices = r->sidx[i].data();
     out->big_limbs = 0;
@@ -4149,7 +4297,9 @@ int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out) {
     }
     return SB_OK;
 }
+}  // namespace sb
 
+extern "C" {
 int sb_result_get_all(const sb_result_set *r, sb_result_view *out, size_t n) {
     if (!r || (!out && n) || n > r->res.size()) return SB_EINVAL;
     for (size_t i = 0; i < n; ++i) sb_result_get(r, i, out + i);
@@ -4190,8 +4340,103 @@ void append_variant(std::string &o, const sb_store &s, const std::string &chrom,
 }  // extern "C"
 
 namespace sb {
+// The wire formatter's per-store cache: for every ALT row (record rec's ALT
+// 0 = row rec, its extra ALT x = row n_records + x) the JSON-escaped tail of
+// its variant string, "\\t" POS "\\t" REF "\\t" ALT "\\t" VT
+// (search_variants.py:210), built once on first use (parallel): a response's
+// variant list is then its chrom and one copy per hit.  A row whose text is
+// not UTF-8 has no entry (bad): its events take the Python handler.
+struct VarText {
+    std::vector<uint64_t> off;  // rows + 1
+    std::vector<char> text;
+    std::vector<uint8_t> bad;
+};
+
+const VarText &var_text(sb_store &s) {
+    std::call_once(s.var_text_once, [&] {
+        auto V = std::make_shared<VarText>();
+        const size_t nr = s.n_records, rows = nr + s.n_extra;
+        std::vector<std::string> vt(s.vt.items.size());
+        std::vector<uint8_t> vt_bad(vt.size(), 0);
+        for (size_t k = 0; k < vt.size(); ++k)
+            if (!json_escape_append(vt[k], s.vt.items[k].data(), s.vt.items[k].size())) vt_bad[k] = 1;
+        std::vector<uint32_t> xrec(s.n_extra);  // extra ALT row -> its record
+        for (size_t r = 0; r < nr; ++r) {
+            const uint32_t nx = (r + 1 < nr ? s.h_x_lo[r + 1] : static_cast<uint32_t>(s.n_extra)) - s.h_x_lo[r];
+            for (uint32_t j = 0; j < nx; ++j) xrec[s.h_x_lo[r] + j] = static_cast<uint32_t>(r);
+        }
+        const char *blob = reinterpret_cast<const char *>(s.h_blob.data());
+        auto parts = [&](size_t row, const char *&alt, size_t &al, uint32_t &rec) {
+            if (row < nr) {
+                rec = static_cast<uint32_t>(row);
+                alt = blob + s.h_a0_off[rec];
+                al = s.h_a0_len[rec];
+            } else {
+                const size_t x = row - nr;
+                rec = xrec[x];
+                alt = blob + s.h_x_off[x];
+                al = s.h_x_len[x];
+            }
+        };
+        // pass 1: each row's escaped length (0 + bad mark where not UTF-8)
+        std::vector<uint32_t> len(rows, 0);
+        V->bad.assign(rows, 0);
+        parallel_for(rows, [&](size_t row) {
+            const char *alt;
+            size_t al;
+            uint32_t rec;
+            parts(row, alt, al, rec);
+            const size_t rl = s.h_end[rec] - s.h_pos[rec] + 1;
+            thread_local std::string tmp;
+            tmp.clear();
+            bool ok = json_escape_append(tmp, blob + s.h_ref_off[rec], rl) && json_escape_append(tmp, alt, al) &&
+                      !vt_bad[s.h_vt[rec]];
+            uint32_t digits = 1;
+            for (uint32_t v = s.h_pos[rec]; v >= 10; v /= 10) ++digits;
+            if (!ok) V->bad[row] = 1;
+            else len[row] = static_cast<uint32_t>(8 + digits + tmp.size() + vt[s.h_vt[rec]].size());
+        });
+        V->off.assign(rows + 1, 0);
+        for (size_t r = 0; r < rows; ++r) V->off[r + 1] = V->off[r] + len[r];
+        V->text.resize(V->off[rows]);
+        // pass 2: the text
+        parallel_for(rows, [&](size_t row) {
+            if (V->bad[row]) return;
+            const char *alt;
+            size_t al;
+            uint32_t rec;
+            parts(row, alt, al, rec);
+            char *p = V->text.data() + V->off[row];
+            *p++ = '\\';
+            *p++ = 't';
+            char num[16];
+            uint32_t v = s.h_pos[rec];
+            char *e = num + sizeof num, *q = e;
+            do {
+                *--q = static_cast<char>('0' + v % 10);
+                v /= 10;
+            } while (v);
+            std::memcpy(p, q, static_cast<size_t>(e - q));
+            p += e - q;
+            *p++ = '\\';
+            *p++ = 't';
+            p = json_escape_to(p, blob + s.h_ref_off[rec], s.h_end[rec] - s.h_pos[rec] + 1);
+            *p++ = '\\';
+            *p++ = 't';
+            p = json_escape_to(p, alt, al);
+            *p++ = '\\';
+            *p++ = 't';
+            const std::string &t = vt[s.h_vt[rec]];
+            std::memcpy(p, t.data(), t.size());
+        });
+        s.var_text = V;
+    });
+    return *static_cast<const VarText *>(s.var_text.get());
+}
+
 void result_prepare_json(sb_result_set *r) {
     if (!r->vt_json.empty()) return;
+    (void)var_text(*r->s);
     const auto &items = r->s->vt.items;
     r->vt_json.resize(items.size());
     for (size_t k = 0; k < items.size(); ++k)
@@ -4231,6 +4476,7 @@ bool result_variants_json(const sb_result_set *r, size_t i, std::string &o) {
     const sb_store &s = *r->s;
     const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
     if (b == a) return true;
+    const VarText &V = *static_cast<const VarText *>(s.var_text.get());  // result_prepare_json built it
     char cbuf[256];  // the chrom escaped (longer names: the string path)
     std::string chrom_long;
     const std::string &cs = r->chrom[i];
@@ -4245,25 +4491,25 @@ bool result_variants_json(const sb_result_set *r, size_t i, std::string &o) {
         chrom = chrom_long.data();
         clen = chrom_long.size();
     }
-    // an upper bound of the text (escapes at most 6x a string's bytes), one
-    // resize, raw writes, then the true length
-    size_t need = 0;
-    for (uint64_t h = a; h < b; ++h) {
-        const uint64_t hit = r->hit[h];
+    const uint64_t nr = s.n_records;
+    auto row_of = [&](uint64_t hit) -> uint64_t {
         const uint32_t rec = static_cast<uint32_t>(hit);
         const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
-        const size_t al = k == 0 ? s.h_a0_len[rec] : s.h_x_len[s.h_x_lo[rec] + k - 1];
-        need += 2 + 2 + clen + 2 + 10 + 2 + 6 * (size_t(s.h_end[rec]) - s.h_pos[rec] + 1) + 2 + 6 * al + 2 +
-                r->vt_json[s.h_vt[rec]].size();
+        return k == 0 ? rec : nr + s.h_x_lo[rec] + k - 1;
+    };
+    // the exact text length, one resize, then copies
+    size_t need = 0;
+    for (uint64_t h = a; h < b; ++h) {
+        const uint64_t row = row_of(r->hit[h]);
+        if (V.bad[row]) return false;  // not UTF-8: the Python handler
+        need += 4 + clen + (V.off[row + 1] - V.off[row]);
     }
+    need -= 2;  // no ", " before the first
     const size_t o0 = o.size();
     o.resize(o0 + need);
     char *p = &o[o0];
-    const char *blob = reinterpret_cast<const char *>(s.h_blob.data());
     for (uint64_t h = a; h < b; ++h) {
-        const uint64_t hit = r->hit[h];
-        const uint32_t rec = static_cast<uint32_t>(hit);
-        const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
+        const uint64_t row = row_of(r->hit[h]);
         if (h > a) {
             *p++ = ',';
             *p++ = ' ';
@@ -4271,41 +4517,11 @@ bool result_variants_json(const sb_result_set *r, size_t i, std::string &o) {
         *p++ = '"';
         std::memcpy(p, chrom, clen);
         p += clen;
-        *p++ = '\\';
-        *p++ = 't';
-        {
-            char num[16];
-            uint32_t v = s.h_pos[rec];
-            char *e = num + sizeof num, *q = e;
-            do {
-                *--q = static_cast<char>('0' + v % 10);
-                v /= 10;
-            } while (v);
-            std::memcpy(p, q, static_cast<size_t>(e - q));
-            p += e - q;
-        }
-        *p++ = '\\';
-        *p++ = 't';
-        p = json_escape_to(p, blob + s.h_ref_off[rec], s.h_end[rec] - s.h_pos[rec] + 1);
-        if (!p) return o.resize(o0), false;
-        *p++ = '\\';
-        *p++ = 't';
-        if (k == 0) {
-            p = json_escape_to(p, blob + s.h_a0_off[rec], s.h_a0_len[rec]);
-        } else {
-            const uint32_t x = s.h_x_lo[rec] + k - 1;
-            p = json_escape_to(p, blob + s.h_x_off[x], s.h_x_len[x]);
-        }
-        if (!p) return o.resize(o0), false;
-        *p++ = '\\';
-        *p++ = 't';
-        const std::string &vt = r->vt_json[s.h_vt[rec]];
-        if (vt.size() == 1 && vt[0] == '\x01') return o.resize(o0), false;  // a VT string that is not UTF-8
-        std::memcpy(p, vt.data(), vt.size());
-        p += vt.size();
+        const size_t n = V.off[row + 1] - V.off[row];
+        std::memcpy(p, V.text.data() + V.off[row], n);
+        p += n;
         *p++ = '"';
     }
-    o.resize(static_cast<size_t>(p - o.data()));
     return true;
 }
 

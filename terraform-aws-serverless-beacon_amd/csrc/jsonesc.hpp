@@ -5,6 +5,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <string>
 
 #include "../../include/sbeacon.h"
@@ -134,6 +135,8 @@ inline char *json_escape_to(char *p, const char *s, size_t n) {
 // result_prepare_json first (once per result set, single-threaded); then
 // result_variants_json may run on many threads for different i.
 void result_prepare_json(sb_result_set *r);
+int result_view(const sb_result_set *r, size_t i, sb_result_view *out);  // sb_result_get without hit views
+void run_tasks(size_t n, const std::function<void(size_t)> &fn);          // on the host worker pool
 bool result_variants_json(const sb_result_set *r, size_t i, std::string &o);
 // the sample_names list items of query i (false: a name that is not UTF-8)
 bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o);

@@ -164,6 +164,8 @@ struct sb_store {
     std::shared_ptr<void> req_pool;      // request batches' pinned / device buffers (api.cpp ReqPool)
     std::shared_ptr<void> region_cache;  // strict dedup: slices' region files (api.cpp RegionCache)
     std::once_flag req_pool_once;
+    std::shared_ptr<void> var_text;      // wire: escaped variant-string tails (api.cpp VarText)
+    std::once_flag var_text_once;
     std::vector<sb::VcfData> vcfs;  // metadata (columns are moved to the globals below)
     std::unordered_map<std::string, uint32_t> vcf_by_location;
     sb::Dict vt, sym;

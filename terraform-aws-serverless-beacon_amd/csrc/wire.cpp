@@ -43,13 +43,37 @@ namespace {
 struct FreeDel {
     void operator()(char *p) const { std::free(p); }
 };
-std::unique_ptr<char, FreeDel> big_alloc(size_t n) {
+// one released output buffer is kept for the next call (freeing and
+// re-faulting ~200 MB of response text cost ~10 ms per call)
+std::mutex g_spare_mu;
+std::unique_ptr<char, FreeDel> g_spare;
+size_t g_spare_sz = 0;
+
+std::unique_ptr<char, FreeDel> big_alloc(size_t n, size_t *cap) {
     constexpr size_t kHuge = size_t(2) << 20;
     const size_t sz = (std::max<size_t>(n, 1) + kHuge - 1) / kHuge * kHuge;
+    {
+        std::lock_guard<std::mutex> lk(g_spare_mu);
+        if (g_spare && g_spare_sz >= sz && g_spare_sz <= 2 * sz + (size_t(64) << 20)) {
+            *cap = g_spare_sz;
+            g_spare_sz = 0;
+            return std::move(g_spare);
+        }
+    }
     char *p = static_cast<char *>(std::aligned_alloc(kHuge, sz));
     if (!p) throw std::bad_alloc();
     (void)madvise(p, sz, MADV_HUGEPAGE);
+    *cap = sz;
     return std::unique_ptr<char, FreeDel>(p);
+}
+
+void big_release(std::unique_ptr<char, FreeDel> &b, size_t cap) {
+    if (!b) return;
+    std::lock_guard<std::mutex> lk(g_spare_mu);
+    if (cap > g_spare_sz) {  // keep the larger one
+        g_spare = std::move(b);
+        g_spare_sz = cap;
+    }
 }
 // the formatting threads' buffers, kept across calls (capacity already
 // faulted in); a concurrent call formats into buffers of its own
@@ -61,6 +85,7 @@ std::vector<std::string> g_tbuf;
 struct sb_json_out {
     std::unique_ptr<char, sb::FreeDel> buf;  // n bytes (uninitialised storage: filled in parallel)
     uint64_t n = 0;
+    size_t cap = 0;  // buf's allocation (kept for the next call when released)
     std::vector<uint64_t> off;   // n + 1
     std::vector<uint8_t> status;  // 0 answered, 1 = answer through the Python handler
 };
@@ -183,10 +208,17 @@ struct Parser {
                 }
                 continue;
             }
-            // raw bytes: must be valid UTF-8 (the event text is decoded as UTF-8)
+            // raw bytes: must be valid UTF-8 (the event text is decoded as UTF-8);
+            // a run of plain ASCII is appended at once
             if (c < 0x80) {
-                o.push_back(static_cast<char>(c));
-                ++p;
+                const char *q = p + 1;
+                while (q < e) {
+                    const unsigned char d = static_cast<unsigned char>(*q);
+                    if (d < 0x20 || d >= 0x80 || d == '"' || d == '\\') break;
+                    ++q;
+                }
+                o.append(p, static_cast<size_t>(q - p));
+                p = q;
                 continue;
             }
             const int n = (c & 0xe0) == 0xc0 ? 2 : (c & 0xf0) == 0xe0 ? 3 : (c & 0xf8) == 0xf0 ? 4 : 0;
@@ -266,6 +298,7 @@ struct Parser {
         const char c = *p;
         if (c == '{') {
             v.kind = JVal::OBJ;
+            v.o.reserve(16);  // a payload's keys: no regrowth
             ++p;
             ws();
             if (p < e && *p == '}') {
@@ -360,6 +393,7 @@ struct Event {
     std::string region, ref, alt, vt, names, location, dataset;
     bool has_ref = false, has_alt = false, has_vt = false, has_names = false, dataset_null = true;
 };
+std::vector<Event> g_ev;  // kept across calls, under g_tbuf_mu
 
 // PerformQueryPayload.__init__ keyword arguments (lambda_payloads.py:46-77)
 const char *const kPayloadKeys[] = {"passthrough",   "dataset_id",      "query_id",     "region",
@@ -395,6 +429,12 @@ bool req_int(const JVal *v, int64_t &out) {
 
 // event text -> Event (ok = false: answer through the Python handler)
 void load_event(const char *text, size_t len, sb_store *const *stores, size_t n_stores, bool strict_vt, Event &E) {
+    E.ok = false;  // an Event kept from an earlier call: its flags reset, its strings overwritten where used
+    E.store = 0;
+    E.q = sb_query{};
+    E.has_ref = E.has_alt = E.has_vt = E.has_names = false;
+    E.dataset_null = true;
+    E.names.clear();
     JVal root;
     bool bad = false;
     if (!parse_json(text, len, root, bad) || bad) return;
@@ -635,7 +675,7 @@ const bool g_wire_trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;  // read
 bool put_response(std::string &o, sb_result_set *rs, size_t i, const Event &E) {
     const size_t start = o.size();  // o may already hold earlier responses
     sb_result_view v;
-    if (sb_result_get(rs, i, &v) != SB_OK) return false;
+    if (result_view(rs, i, &v) != SB_OK) return false;
     if (v.error) {
         put_error(o, v.error);
         return true;
@@ -706,12 +746,9 @@ void par(size_t n, unsigned threads, F fn) {
         for (size_t i = 0; i < n; ++i) fn(i, 0u);
         return;
     }
-    std::vector<std::thread> th;
-    for (unsigned k = 0; k < t; ++k)
-        th.emplace_back([&, k] {
-            for (size_t i = n * k / t, e = n * (k + 1) / t; i < e; ++i) fn(i, k);
-        });
-    for (auto &x : th) x.join();
+    run_tasks(t, [&](size_t k) {  // the host worker pool: no thread spawns per phase
+        for (size_t i = n * k / t, e = n * (k + 1) / t; i < e; ++i) fn(i, static_cast<unsigned>(k));
+    });
 }
 
 }  // namespace
@@ -738,7 +775,13 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
                          std::chrono::duration<double, std::milli>(t - t_last).count());
             t_last = t;
         };
-        std::vector<Event> ev(n);
+        // the event and formatting buffers persist across calls (their strings'
+        // capacity kept); a concurrent call uses buffers of its own
+        std::unique_lock<std::mutex> tb_lk(g_tbuf_mu, std::try_to_lock);
+        std::vector<Event> own_ev;
+        std::vector<Event> &ev = tb_lk.owns_lock() ? g_ev : own_ev;
+        if (ev.size() < n) ev.resize(n);
+        tick("events");
         par(n, threads, [&](size_t i, unsigned) {
             load_event(text + offsets[i], offsets[i + 1] - offsets[i], stores, n_stores, strict_vt, ev[i]);
             if (ev[i].ok) bind_strings(ev[i]);
@@ -751,7 +794,6 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
         // buffers are then copied once, in parallel, into the output in event order
         std::vector<uint32_t> where(n, 0);   // formatting thread
         std::vector<uint64_t> pos(n, 0), len(n, 0);
-        std::unique_lock<std::mutex> tb_lk(g_tbuf_mu, std::try_to_lock);
         std::vector<std::string> own;
         std::vector<std::string> &tbuf = tb_lk.owns_lock() ? g_tbuf : own;
         tbuf.resize(threads);
@@ -774,11 +816,11 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
             {
                 const size_t m = idx.size();
                 const unsigned tt = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, m / 256)));
-                par(tt, tt, [&](size_t k, unsigned) {
+                run_tasks(tt, [&](size_t k) {
                     size_t need = 0;
                     for (size_t j = m * k / tt, e = m * (k + 1) / tt; j < e; ++j) {
                         sb_result_view v;
-                        if (sb_result_get(rs, j, &v) == SB_OK)
+                        if (result_view(rs, j, &v) == SB_OK)
                             need += 320 + ev[idx[j]].location.size() + ev[idx[j]].dataset.size() + 56 * v.n_variants +
                                     12 * v.n_sample_indices;
                     }
@@ -788,27 +830,29 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
             std::vector<double> t_ms(threads, 0.0);
             std::mutex tot_mu;
             double tot[6] = {0, 0, 0, 0, 0, 0};
-            std::vector<uint64_t> t_n(threads, 0);
-            par(idx.size(), threads, [&](size_t j, unsigned t) {
-                const auto t0 = trace ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
-                struct Acc {  // per-thread time in put_response (SBEACON_WIRE_TRACE)
-                    std::chrono::steady_clock::time_point t0;
-                    double *ms;
-                    bool on;
-                    ~Acc() {
-                        if (on) *ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            {
+                const size_t m = idx.size();
+                const unsigned tt = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, m / 256)));
+                // thread k formats events [m k / tt, m (k + 1) / tt) into its buffer (as sized above)
+                run_tasks(tt, [&](size_t k) {
+                    const auto t0 = trace ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
+                    std::string &o = tbuf[k];
+                    for (size_t j = m * k / tt, e = m * (k + 1) / tt; j < e; ++j) {
+                        const uint32_t i = idx[j];
+                        const size_t at = o.size();
+                        if (put_response(o, rs, j, ev[i])) {
+                            o.push_back('\n');
+                            where[i] = static_cast<uint32_t>(k);
+                            pos[i] = at;
+                            len[i] = o.size() - at;
+                            R->status[i] = 0;
+                        } else {
+                            o.resize(at);
+                        }
                     }
-                } acc{t0, &t_ms[t], trace};
-                ++t_n[t];
-                const uint32_t i = idx[j];
-                std::string &o = tbuf[t];
-                struct Flush {  // this thread's writer times into the call's totals
-                    bool on;
-                    std::mutex *mu;
-                    double *tot;
-                    ~Flush() {
-                        if (!on) return;
-                        std::lock_guard<std::mutex> lk(*mu);
+                    if (trace) {  // this thread's writer times into the call's totals (once per thread)
+                        t_ms[k] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+                        std::lock_guard<std::mutex> lk(tot_mu);
                         tot[0] += tl_var_ms;
                         tot[1] += tl_samp_ms;
                         tot[2] += static_cast<double>(tl_var_n);
@@ -818,18 +862,8 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
                         tl_var_ms = tl_samp_ms = 0;
                         tl_var_n = tl_samp_n = tl_var_b = tl_samp_b = 0;
                     }
-                } flush{trace, &tot_mu, tot};
-                const size_t at = o.size();
-                if (put_response(o, rs, j, ev[i])) {
-                    o.push_back('\n');
-                    where[i] = t;
-                    pos[i] = at;
-                    len[i] = o.size() - at;
-                    R->status[i] = 0;
-                } else {
-                    o.resize(at);
-                }
-            });
+                });
+            }
             if (trace) {
                 double mx = 0, sum = 0;
                 size_t bytes = 0;
@@ -851,12 +885,13 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
         R->off[0] = 0;
         for (size_t i = 0; i < n; ++i) R->off[i + 1] = R->off[i] + len[i];
         R->n = R->off[n];
-        R->buf = big_alloc(R->n);
+        R->buf = big_alloc(R->n, &R->cap);
         char *dst = R->buf.get();
         par(n, threads, [&](size_t i, unsigned) {
             if (len[i]) memcpy(dst + R->off[i], tbuf[where[i]].data() + pos[i], len[i]);
         });
         tick("concat");
+        tick("cleanup");
         *out = R.release();
         return SB_OK;
     } catch (const Error &e) {
@@ -881,6 +916,9 @@ int sb_json_out_get(const sb_json_out *o, const char **buf, size_t *len, const u
     return SB_OK;
 }
 
-void sb_json_out_free(sb_json_out *o) { delete o; }
+void sb_json_out_free(sb_json_out *o) {
+    if (o) sb::big_release(o->buf, o->cap);
+    delete o;
+}
 
 }  // extern "C"

@@ -1,0 +1,17 @@
+# full GPU test suite + config-2 wire split (pooled slice-batch buffers, pinned hits, text cache)
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${TAG:-r04r}
+mkdir -p $OUT
+step() {  # name, limit, command...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 $lim "$@" > $OUT/$name.log 2>&1; local rc=$?
+  echo "$name rc=$rc"; tail -2 $OUT/$name.log | cut -c1-300
+  case $rc in 0) return 0;; *) exit $rc;; esac
+}
+step tests 900 python3 -u -m pytest $R/tests -m gpu -x -v --timeout 120 --timeout-method thread
+step wire_plain 400 python3 -u $R/tools/wire_split.py
+SBEACON_WIRE_TRACE=1 step wire 400 python3 -u $R/tools/wire_split.py
+grep "\[wire\]\|\[query\]\|\[prepare\]" $OUT/wire.log | tail -24
+exit 0

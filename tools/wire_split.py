@@ -28,11 +28,16 @@ def main():
     buf, off = pack_events([json.dumps(p) for p in payloads])
     t_pack = time.perf_counter() - t0
     out = {}
+    r = None
     for rep in range(4):
         print(f'--- rep {rep}', file=sys.stderr, flush=True)
+        t1 = time.perf_counter()
+        r = None  # the previous result freed outside the timed call
+        t_free = time.perf_counter() - t1
         t0 = time.perf_counter()
         r = perform_query_events_packed(buf, off)
-        out = {'call_ms': round((time.perf_counter() - t0) * 1e3, 2), 'pack_ms': round(t_pack * 1e3, 2),
+        out = {'call_ms': round((time.perf_counter() - t0) * 1e3, 2), 'free_ms': round(t_free * 1e3, 2),
+               'pack_ms': round(t_pack * 1e3, 2),
                'events': len(payloads), 'requests': len(reqs), 'response_bytes': len(r.buf),
                'fallbacks': int(r.fallback.sum())}
     print(json.dumps(out), flush=True)
