@@ -764,6 +764,9 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
         for (size_t i = 0; i < n; ++i)
             if (offsets[i + 1] < offsets[i]) throw Error(SB_EINVAL, "offsets not non-decreasing");
         const unsigned threads = 16;
+        // phases cut into more pieces than the pool has threads: the pool
+        // drains them dynamically (events differ a lot in response size)
+        const unsigned chunks = 64;
         const bool strict_vt = (flags & 1u) != 0;
         // SBEACON_WIRE_TRACE=1: phase times to stderr (bench diagnostics)
         const bool trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;
@@ -782,7 +785,7 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
         std::vector<Event> &ev = tb_lk.owns_lock() ? g_ev : own_ev;
         if (ev.size() < n) ev.resize(n);
         tick("events");
-        par(n, threads, [&](size_t i, unsigned) {
+        par(n, chunks, [&](size_t i, unsigned) {
             load_event(text + offsets[i], offsets[i + 1] - offsets[i], stores, n_stores, strict_vt, ev[i]);
             if (ev[i].ok) bind_strings(ev[i]);
         });
@@ -796,7 +799,7 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
         std::vector<uint64_t> pos(n, 0), len(n, 0);
         std::vector<std::string> own;
         std::vector<std::string> &tbuf = tb_lk.owns_lock() ? g_tbuf : own;
-        tbuf.resize(threads);
+        tbuf.resize(chunks);
         for (auto &b : tbuf) b.clear();  // capacity kept
         for (size_t k = 0; k < n_stores; ++k) {
             std::vector<uint32_t> idx;
@@ -815,7 +818,7 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
             // events (par's contiguous split): no reallocation while writing
             {
                 const size_t m = idx.size();
-                const unsigned tt = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, m / 256)));
+                const unsigned tt = static_cast<unsigned>(std::min<size_t>(chunks, std::max<size_t>(1, m / 64)));
                 run_tasks(tt, [&](size_t k) {
                     size_t need = 0;
                     for (size_t j = m * k / tt, e = m * (k + 1) / tt; j < e; ++j) {
@@ -827,12 +830,12 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
                     tbuf[k].reserve(tbuf[k].size() + need);
                 });
             }
-            std::vector<double> t_ms(threads, 0.0);
+            std::vector<double> t_ms(chunks, 0.0);
             std::mutex tot_mu;
             double tot[6] = {0, 0, 0, 0, 0, 0};
             {
                 const size_t m = idx.size();
-                const unsigned tt = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, m / 256)));
+                const unsigned tt = static_cast<unsigned>(std::min<size_t>(chunks, std::max<size_t>(1, m / 64)));
                 // thread k formats events [m k / tt, m (k + 1) / tt) into its buffer (as sized above)
                 run_tasks(tt, [&](size_t k) {
                     const auto t0 = trace ? std::chrono::steady_clock::now() : std::chrono::steady_clock::time_point{};
@@ -867,7 +870,7 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
             if (trace) {
                 double mx = 0, sum = 0;
                 size_t bytes = 0;
-                for (unsigned t = 0; t < threads; ++t) {
+                for (unsigned t = 0; t < chunks; ++t) {
                     mx = std::max(mx, t_ms[t]);
                     sum += t_ms[t];
                     bytes += tbuf[t].size();
