@@ -159,6 +159,11 @@ def main_genome(args):
             raise RuntimeError(f'pipelined delivery returned {delivered["hits_returned"]} hits, serial '
                                f'{serial["hits_returned"]}')
         delivered['serial'] = serial
+        delivered['cold_launch'] = cold_launch_probe(store, shape, reqs, world, rank, base, dev)
+        delivered['cold_launch']['note'] = (
+            'request_eval_kernel of a freshly prepared batch, HIP events: first and second launch after a 50 ms idle '
+            'gap, and after ~8 fp32 GEMMs (a busy device); round 3 traced 0.76-0.81 ms launches in its serial '
+            'delivered passes')
     vals = [elapsed, kern_ms, float(len(sl)), float(st['cand_loaded']), float(nhits), achieved, float(uniq), comp,
             contract, step_dev_ms, pass_ms, achieved_pass, comp_pass]
     if dist:

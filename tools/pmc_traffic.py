@@ -36,8 +36,16 @@ def load(d, counter):
                 name = row['Kernel_Name']
                 if not PHASE.search(name):
                     continue
-                per.setdefault(name, []).append((int(row['Dispatch_Id']), float(row['Counter_Value'])))
-    return {k: [v for _, v in sorted(x)] for k, x in per.items()}
+                per.setdefault(name, []).append((int(row['Dispatch_Id']), float(row['Counter_Value']),
+                                                 int(row.get('Grid_Size') or 0)))
+    # a bench run launches a kernel at several sizes (the timed batch, the
+    # delivered path's chunks, probes): only the launches of the largest grid
+    # -- the timed full batch -- are priced
+    out = {}
+    for k, x in per.items():
+        g = max(v[2] for v in x)
+        out[k] = [v for _, v, gs in sorted(x) if gs == g]
+    return out
 
 
 def short(name):
