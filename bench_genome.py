@@ -270,35 +270,35 @@ def make_step(run, ex, part, hits, row_off):
 
 
 def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5):
-    """End to end on one GPU: requests (numpy, host) -> routing to the rank
-    (shard_requests, numpy) -> request batch planning + upload
-    (sb_requests_prepare, C++) -> one pass -> rows, row offsets and the hit
+    """End to end on one GPU: requests (numpy, host) -> the rank's row range
+    (shard_rows) -> request batch planning + upload
+    (sb_requests_prepare_beacon: conversion, the core cut and packing in C++,
+    then the planning kernels) -> one pass -> rows, row offsets and the hit
     lists copied back into pinned host memory.  Every part inside the timed
     region; a fresh batch each pass."""
-    import numpy as np
     import torch
-    from sbeacon.genome import prepare_shard_requests, shard_requests
+    from sbeacon.genome import prepare_beacon_shard, shard_rows
     t_route = t_prep = t_dev = 0.0
     best = None
     rows_h = hits_h = ro_h = None
     for k in range(passes + 1):  # pass 0 warms the allocator / pinned buffers (untimed)
         torch.cuda.synchronize()
         a = time.perf_counter()
-        sr = shard_requests(shape, reqs, world, rank)
+        rr = shard_rows(shape, reqs, world, rank)
         b0 = time.perf_counter()
-        batch = prepare_shard_requests(store, sr)
+        _, n_rows, batch = prepare_beacon_shard(store, shape, reqs, world, rank, rows=rr)
         batch.set_stream(torch.cuda.current_stream().cuda_stream)
         cap = int(batch.stats()['hits'])
         c0 = time.perf_counter()
-        if rows_h is None or rows_h.shape[0] < sr.n_rows or hits_h.shape[0] < cap:
-            rows_d = torch.empty((max(sr.n_rows, 1), 5), dtype=torch.int64, device=dev)
-            ro_d = torch.empty(sr.n_rows + 1, dtype=torch.int64, device=dev)
+        if rows_h is None or rows_h.shape[0] < n_rows or hits_h.shape[0] < cap:
+            rows_d = torch.empty((max(n_rows, 1), 5), dtype=torch.int64, device=dev)
+            ro_d = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
             hits_d = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
             rows_h = torch.empty(rows_d.shape, dtype=torch.int64, pin_memory=True)
             ro_h = torch.empty(ro_d.shape, dtype=torch.int64, pin_memory=True)
             hits_h = torch.empty(hits_d.shape, dtype=torch.int64, pin_memory=True)
         batch.run(rows_d.data_ptr(), hits_d.data_ptr(), ro_d.data_ptr(), base)
-        rows_h[:sr.n_rows].copy_(rows_d[:sr.n_rows], non_blocking=True)
+        rows_h[:n_rows].copy_(rows_d[:n_rows], non_blocking=True)
         ro_h.copy_(ro_d, non_blocking=True)
         torch.cuda.current_stream().synchronize()
         total = int(ro_h[-1])
@@ -316,7 +316,7 @@ def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5)
     n = len(reqs)
     return {'requests_per_s': round(n / dt, 1), 'ms_per_pass': round(dt * 1e3, 2),
             'best_ms': round(best * 1e3, 2), 'passes': passes,
-            'split_ms': {'route_numpy': round(t_route / passes * 1e3, 2),
+            'split_ms': {'route_rows': round(t_route / passes * 1e3, 2),
                          'prepare_upload': round(t_prep / passes * 1e3, 2),
                          'device_pass_and_d2h': round(t_dev / passes * 1e3, 2)},
             'hits_returned': int(ro_h[-1]),
@@ -362,27 +362,26 @@ def cold_launch_probe(store, shape, reqs, world, rank, base, dev):
 
 def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes=5, chunks=8, workers=2):
     """The delivered path in chunks of consecutive request rows, pipelined:
-    two host threads route and prepare chunks ahead (numpy, then
-    sb_requests_prepare_columns: pack, upload and the planning kernels on the
-    store's stream) while the main thread enqueues each prepared chunk's pass
-    and its row / row-offset D2H on the torch stream, and a chunk's hit list
-    D2H once its row offsets are back.  Requests in host memory -> rows, row
-    offsets (per chunk) and dense hit lists in pinned host memory, all inside
-    the timed region."""
+    two host threads route and prepare chunks ahead (the chunk's row range,
+    then sb_requests_prepare_beacon: the Beacon columns converted, cut to the
+    rank's core and packed in one pass, uploaded, and the planning kernels on
+    the thread's planning stream) while the main thread enqueues each
+    prepared chunk's pass and its row / row-offset D2H on the torch stream,
+    and a chunk's hit list D2H once its row offsets are back.  Requests in
+    host memory -> rows, row offsets (per chunk) and dense hit lists in
+    pinned host memory, all inside the timed region."""
     import numpy as np
     import torch
     from concurrent.futures import ThreadPoolExecutor
-    from sbeacon.genome import Requests, prepare_shard_requests, shard_requests
+    from sbeacon.genome import prepare_beacon_shard
     n = len(reqs)
     cuts = np.linspace(0, n, chunks + 1).astype(np.int64)
     stream = torch.cuda.current_stream()
 
     def prep(k):
         a, b = int(cuts[k]), int(cuts[k + 1])
-        sub = Requests(reqs.ci[a:b], reqs.start[a:b], reqs.width[a:b], reqs.vt[a:b], reqs.vmin[a:b], reqs.vmax[a:b])
-        sr = shard_requests(shape, sub, world, rank)
-        bt = prepare_shard_requests(store, sr)
-        return sr, bt, int(bt.stats()['hits'])
+        lo, m, bt = prepare_beacon_shard(store, shape, reqs.rows(a, b), world, rank)
+        return a + lo, m, bt, int(bt.stats()['hits'])
 
     rows_h = torch.empty((n, 5), dtype=torch.int64, pin_memory=True)
     ro_h = torch.empty(n + chunks, dtype=torch.int64, pin_memory=True)
@@ -398,9 +397,7 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
             live, pend = [], []
             total_hits = 0
             for k in range(chunks):
-                sr, bt, cap = futs[k].result()
-                a = int(cuts[k])
-                m = sr.n_rows
+                a, m, bt, cap = futs[k].result()
                 if hits_d[k] is None or hits_d[k].numel() < max(cap, 1):
                     hits_d[k] = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
                     hits_h[k] = torch.empty(max(cap, 1), dtype=torch.int64, pin_memory=True)
@@ -434,9 +431,11 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
     return {'requests_per_s': round(n / dt, 1), 'ms_per_pass': round(dt * 1e3, 2),
             'best_ms': round(min(times) * 1e3, 2), 'passes': passes, 'chunks': chunks, 'workers': workers,
             'hits_returned': total_hits,
-            'note': 'pipelined: the requests cut into chunks of consecutive rows; 2 host threads route + prepare '
-                    'chunks ahead while each prepared chunk runs and copies back (rows, per-chunk row offsets, '
-                    'dense hits into pinned host memory); everything inside the timed region'}
+            'note': f'pipelined: the requests cut into chunks of consecutive rows; {workers} host threads route + '
+                    'prepare chunks ahead (sb_requests_prepare_beacon: Beacon int64 columns -> SplitQueryPayloads '
+                    'cut to the core and packed in the library) while each prepared chunk runs and copies back '
+                    '(rows, per-chunk row offsets, dense hits into pinned host memory); everything inside the '
+                    'timed region'}
 
 
 def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20000, seed=7):

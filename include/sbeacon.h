@@ -466,6 +466,46 @@ typedef struct {
 } sb_request_columns;
 
 int sb_requests_prepare_columns(sb_store *s, const sb_request_columns *c, size_t n, sb_batch **out);
+
+/* The same batch straight from the route's query parameters: one row = one
+ * /g_variants query against ONE VCF, turned into its SplitQueryPayload as
+ * perform_variant_search_sync does (shared_resources/variantutils/
+ * search_variants.py:179-197: start / end of one or two elements ->
+ * start_min, start_max, end_min, end_max, each + 1), optionally restricted to
+ * one shard's core: only the splitQuery slices (lambda/splitQuery/
+ * lambda_function.py:74-110) whose (contig, first base) lies in [lo, hi) are
+ * answered -- sbeacon.sharding.ShardPlan.slice_runs in the library, fused
+ * into the packing pass (no per-request conversion by the caller).  Numeric
+ * columns are the caller's int64 arrays as they are. */
+typedef struct {
+    uint32_t vcf_id;
+    const int64_t *contig;         /* request contig code (n values) */
+    const uint32_t *contig_map;    /* code -> contig index in the VCF (sb_store_contig_name); NULL = identity; */
+    uint32_t n_contig_map;         /* a code past the map or mapped to UINT32_MAX: absent (no slices) */
+    const int64_t *start, *start2; /* requestParameters start[0], start[1] (start2 NULL: one-element start) */
+    const int64_t *end, *end2;     /* end[0], end[1] (end2 NULL: one-element end) */
+    const int64_t *variant_type_code; /* into variant_type_dict (NULL: every row takes dict[0]) */
+    const sb_str *variant_type_dict;  /* NULL = None for every row */
+    uint32_t n_variant_type;
+    const int64_t *variant_min_length; int64_t variant_min_length_all;
+    const int64_t *variant_max_length; int64_t variant_max_length_all;
+    sb_str reference_bases;        /* p NULL = None */
+    sb_str alternate_bases;        /* p NULL = None (a variantType query) */
+    uint8_t granularity;           /* SB_GRAN_* */
+    uint8_t include_details;       /* includeResultsetResponses in {HIT, ALL} */
+} sb_beacon_requests;
+
+/* A shard's core in one VCF: slices whose (contig index, first base) is >=
+ * (contig_lo, pos_lo) and < (contig_hi, pos_hi).  contig_hi == UINT32_MAX:
+ * no upper end; contig_lo == UINT32_MAX: an empty core. */
+typedef struct {
+    uint32_t contig_lo; int64_t pos_lo;
+    uint32_t contig_hi; int64_t pos_hi;
+} sb_shard_core;
+
+/* core NULL: every slice.  The batch is sb_requests_prepare_columns's. */
+int sb_requests_prepare_beacon(sb_store *s, const sb_beacon_requests *q, size_t n, const sb_shard_core *core,
+                               sb_batch **out);
 /* Enqueue one pass: answer every request, then write dev_rows[n]
  * (sb_request_partial), dev_row_off[n + 1] and the rows' hit lists densely
  * in request order: row w's hits ((record + rec_base) | alt << 32, the

@@ -953,6 +953,12 @@ class WorkerPool {
         static WorkerPool pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
         return pool;
     }
+    // a second, smaller pool for a concurrent caller (two pipelined
+    // preparers): spawning threads per call costs more than the work
+    static WorkerPool &second() {
+        static WorkerPool pool(std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2)) - 1);
+        return pool;
+    }
     template <class F>
     void run(size_t n, F fn) {
         std::unique_lock<std::mutex> one(run_mu_);
@@ -1039,10 +1045,10 @@ void parallel_for(size_t n, F fn, unsigned threads = 16, size_t grain = 4096) {
         for (size_t i = 0; i < n; ++i) fn(i);
         return;
     }
-    if (WorkerPool::get().try_run(t, [&](size_t k) {
-            for (size_t i = n * k / t, e = n * (k + 1) / t; i < e; ++i) fn(i);
-        }))
-        return;
+    auto part = [&](size_t k) {
+        for (size_t i = n * k / t, e = n * (k + 1) / t; i < e; ++i) fn(i);
+    };
+    if (WorkerPool::get().try_run(t, part) || WorkerPool::second().try_run(t, part)) return;
     std::vector<std::thread> th;
     for (unsigned k = 0; k < t; ++k)
         th.emplace_back([&, k] {
@@ -3470,8 +3476,41 @@ void upload_slice_part(sb_batch &B, sb_batch::Req &R, const std::vector<uint32_t
 // descriptors; request_stage_scan_kernel lays the runs' staging regions end
 // to end.  One readback (chains, slices, staging total) sizes the buffers.
 // Returns false when the columns do not qualify: prepare_requests plans on
-// the host.
-bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n) {
+// the host.  The per-row numbers come from `get` (PackRow: the columns as
+// they are, or the Beacon conversion + shard cut of sb_requests_prepare_beacon
+// fused into the same pass); `full()` gives columns the per-slice part can
+// read (only called when some row goes per slice).
+// The calling thread's planning stream on `device`: concurrent preparers
+// (pipelined callers) neither queue behind nor wait for each other's uploads
+// and planning kernels on the store stream.  Everything planned on it is
+// synchronised before prepare returns.
+hipStream_t planning_stream(int device) {
+    thread_local std::vector<hipStream_t> per_dev;
+    if (per_dev.size() <= static_cast<size_t>(device)) per_dev.resize(device + 1, nullptr);
+    hipStream_t &st = per_dev[device];
+    if (!st) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    return st;
+}
+struct PackRow {
+    uint32_t contig;
+    uint32_t vt;  // variant_type code
+    int64_t smin, smax, emin, emax, vmin, vmax;
+};
+struct ColRows {
+    const sb_request_columns &c;
+    PackRow operator()(size_t i) const {
+        return PackRow{c.contig ? c.contig[i] : c.contig_all,
+                       c.variant_type_dict && c.variant_type_code ? c.variant_type_code[i] : 0u,
+                       c.start_min[i],
+                       c.start_max[i],
+                       c.end_min ? c.end_min[i] : c.end_min_all,
+                       c.end_max ? c.end_max[i] : c.end_max_all,
+                       c.variant_min_length ? c.variant_min_length[i] : c.variant_min_length_all,
+                       c.variant_max_length ? c.variant_max_length[i] : c.variant_max_length_all};
+    }
+};
+template <class Get, class Full>
+bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n, const Get &get, const Full &full) {
     sb_store &s = *B.s;
     if (s.device < 0 || n == 0 || n >= (1u << 31) || c.vcf_id || c.vcf_id_all >= s.vcfs.size()) return false;
     const VcfData &v = s.vcfs[c.vcf_id_all];
@@ -3517,12 +3556,13 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n)
     std::vector<uint8_t> cls(n, 0);
     std::atomic<bool> any_slices{false};
     parallel_for(n, [&](size_t i) {
-        const uint32_t contig = c.contig ? c.contig[i] : c.contig_all;
-        const int64_t smin = c.start_min[i], smax = c.start_max[i];
+        const PackRow x = get(i);
+        const uint32_t contig = x.contig;
+        const int64_t smin = x.smin, smax = x.smax;
         ReqIn o{0, 0, 0, 0, 0, 0, 0, REQ_NONE};
         if (contig < v.segments.size() && smin <= smax) {  // else bcftools emits nothing / no slice
             const int64_t nsl = (smax - smin) / kSplitSize + 1;
-            const auto &kl = tab[c.variant_type_dict && c.variant_type_code ? c.variant_type_code[i] : 0u];
+            const auto &kl = tab[x.vt];
             bool chain = smin >= 1 && smax <= 0xfffffffell && nsl <= kReqChainSlices && kl.second < kReqLutMax;
             if (chain && !slow_pos[contig].empty()) {  // a VT_SLOW / general record in the window: per slice
                 const auto &sp = slow_pos[contig];
@@ -3534,15 +3574,14 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n)
                 cls[i] = 2;
                 any_slices.store(true, std::memory_order_relaxed);
             } else {
-                const int64_t emin = c.end_min ? c.end_min[i] : c.end_min_all, emax = c.end_max ? c.end_max[i] : c.end_max_all;
+                const int64_t emin = x.emin, emax = x.emax;
                 const bool end_void = emax < 0 || emin > 0xffffffffll || emin > emax;
                 o.first = static_cast<uint32_t>(smin);
                 o.last = static_cast<uint32_t>(smax);
                 o.e0 = emin < 0 ? 0u : static_cast<uint32_t>(emin);
                 o.espan = (emax > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(emax)) - o.e0;
-                const int64_t vmin = c.variant_min_length ? c.variant_min_length[i] : c.variant_min_length_all;
-                const int64_t vmax0 = c.variant_max_length ? c.variant_max_length[i] : c.variant_max_length_all;
-                const int64_t vmax = vmax0 < 0 ? INT64_MAX : vmax0;
+                const int64_t vmin = x.vmin;
+                const int64_t vmax = x.vmax < 0 ? INT64_MAX : x.vmax;
                 const int64_t vl = vmin < 0 ? 0 : vmin, vh = vmax > 255 ? 255 : vmax;
                 o.bits = req_bits(vh < vl ? 256u : static_cast<uint32_t>(vl), vh < vl ? 0u : static_cast<uint32_t>(vh - vl),
                                   0u, kl.first, end_void);
@@ -3555,10 +3594,10 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n)
     });
     tick("pack");
     std::vector<uint32_t> seg;
-    if (any_slices.load()) slice_part(B, *R, ColSrc{c}, n, cls, seg);
+    if (any_slices.load()) slice_part(B, *R, ColSrc{full()}, n, cls, seg);
     tick("slices");
     HIP_OK(hipSetDevice(s.device));
-    hipStream_t st = s.stream;
+    hipStream_t st = planning_stream(s.device);
     const uint32_t n_runs = static_cast<uint32_t>((n + kRunRows - 1) / kRunRows);
     const size_t chain_bytes = size_t(n_runs) * kReqRun * sizeof(ReqChain), run_bytes = size_t(n_runs) * sizeof(RowRun);
     DevMem din = P.get_dev(n * sizeof(ReqIn)), rc = P.get_dev(size_t(n_runs) * 8 + 32);
@@ -3928,7 +3967,153 @@ int sb_requests_prepare_columns(sb_store *s, const sb_request_columns *c, size_t
         check_columns(cc, n);
         auto B = std::make_unique<sb_batch>();
         B->s = s;
-        if (!prepare_requests_device(*B, cc, n)) prepare_requests(*B, ColSrc{cc}, n);
+        if (!prepare_requests_device(*B, cc, n, ColRows{cc}, [&]() -> const sb_request_columns & { return cc; }))
+            prepare_requests(*B, ColSrc{cc}, n);
+        store_hold(s);
+        *out = B.release();
+    });
+}
+
+namespace {
+// sb_requests_prepare_beacon: row i's SplitQueryPayload numbers
+// (search_variants.py:179-197) cut to the shard core (ShardPlan.slice_runs,
+// sbeacon/sharding.py): slice k of [start_min, start_max] starts at
+// start_min + 10000 k; the core keeps the slices k0 <= k < k1
+struct BeaconRows {
+    const sb_beacon_requests &q;
+    const sb_shard_core *core;
+    std::atomic<size_t> *bad;  // first row with a variant_type code out of range
+    // first slice index routed at or past key (kc, kp): ceil((kp - smin) / 10000) clipped to [0, nsl]
+    static int64_t first_k(uint32_t c, int64_t smin, int64_t nsl, uint32_t kc, int64_t kp) {
+        if (c > kc) return 0;
+        if (c < kc) return nsl;
+        if (kp <= smin) return 0;
+        const uint64_t d = static_cast<uint64_t>(kp) - static_cast<uint64_t>(smin);  // > 0, exact in 64 bits
+        const uint64_t need = d / kSplitSize + (d % kSplitSize != 0);
+        return need >= static_cast<uint64_t>(nsl) ? nsl : static_cast<int64_t>(need);
+    }
+    PackRow operator()(size_t i) const {
+        const int64_t code = q.contig[i];
+        uint32_t contig = UINT32_MAX;
+        if (!q.contig_map) contig = code >= 0 && code < UINT32_MAX ? static_cast<uint32_t>(code) : UINT32_MAX;
+        else if (code >= 0 && static_cast<uint64_t>(code) < q.n_contig_map) contig = q.contig_map[code];
+        const int64_t s0 = q.start[i], e0 = q.end[i];
+        int64_t smin = s0, smax, emin, emax;
+        if (q.end2) {
+            emin = e0;
+            emax = q.end2[i];
+        } else {
+            emin = s0;
+            emax = e0;
+        }
+        smax = q.start2 ? q.start2[i] : emax;
+        constexpr int64_t kLim = int64_t(1) << 62;  // past any contig: a row with no slices (no overflow below)
+        auto out = [&](int64_t x) { return x < -kLim || x > kLim; };
+        if (out(smin) || out(smax) || out(emin) || out(emax)) {
+            contig = UINT32_MAX;
+            smin = smax = emin = emax = 0;
+        }
+        ++smin, ++smax, ++emin, ++emax;
+        if (core && smin <= smax) {
+            const int64_t nsl = (smax - smin) / kSplitSize + 1;
+            const int64_t k0 = core->contig_lo == UINT32_MAX ? nsl : first_k(contig, smin, nsl, core->contig_lo, core->pos_lo);
+            const int64_t k1 = std::max(
+                k0, core->contig_hi == UINT32_MAX ? nsl : first_k(contig, smin, nsl, core->contig_hi, core->pos_hi));
+            const int64_t a = smin + kSplitSize * k0;
+            smax = k1 > k0 ? std::min(smax, smin + kSplitSize * k1 - 1) : a - 1;
+            smin = a;
+        }
+        uint32_t vt = 0;
+        if (q.variant_type_dict && q.variant_type_code) {
+            const int64_t v = q.variant_type_code[i];
+            if (v < 0 || v >= q.n_variant_type) {
+                size_t cur = bad->load(std::memory_order_relaxed);
+                while (i < cur && !bad->compare_exchange_weak(cur, i)) {
+                }
+            } else {
+                vt = static_cast<uint32_t>(v);
+            }
+        }
+        return PackRow{contig, vt, smin, smax, emin, emax,
+                       q.variant_min_length ? q.variant_min_length[i] : q.variant_min_length_all,
+                       q.variant_max_length ? q.variant_max_length[i] : q.variant_max_length_all};
+    }
+};
+
+// the same rows as sb_request_columns arrays (the host planner and the
+// per-slice part read columns)
+struct BeaconColumns {
+    std::vector<uint32_t> contig, vt;
+    std::vector<int64_t> smin, smax, emin, emax, vmin, vmax;
+    sb_request_columns c{};
+    BeaconColumns(const sb_request_columns &base, const BeaconRows &rows, size_t n)
+        : contig(n), vt(n), smin(n), smax(n), emin(n), emax(n), vmin(n), vmax(n), c(base) {
+        parallel_for(n, [&](size_t i) {
+            const PackRow x = rows(i);
+            contig[i] = x.contig;
+            vt[i] = x.vt;
+            smin[i] = x.smin;
+            smax[i] = x.smax;
+            emin[i] = x.emin;
+            emax[i] = x.emax;
+            vmin[i] = x.vmin;
+            vmax[i] = x.vmax;
+        });
+        c.contig = contig.data();
+        c.start_min = smin.data();
+        c.start_max = smax.data();
+        c.end_min = emin.data();
+        c.end_max = emax.data();
+        c.variant_min_length = vmin.data();
+        c.variant_max_length = vmax.data();
+        if (c.variant_type_dict) c.variant_type_code = vt.data();
+    }
+};
+}  // namespace
+
+int sb_requests_prepare_beacon(sb_store *s, const sb_beacon_requests *q, size_t n, const sb_shard_core *core,
+                               sb_batch **out) {
+    return guard([&] {
+        if (!s || !q || !out) throw Error(SB_EINVAL, "NULL argument");
+        if (n && (!q->contig || !q->start || !q->end)) throw Error(SB_EINVAL, "contig / start / end columns are required");
+        if (q->vcf_id >= s->vcfs.size()) throw Error(SB_EINVAL, "vcf_id out of range");
+        if (q->variant_type_dict && !q->n_variant_type) throw Error(SB_EINVAL, "variant_type: empty dictionary");
+        if (!q->variant_type_dict && q->variant_type_code) throw Error(SB_EINVAL, "variant_type: codes without a dictionary");
+        if (q->reference_bases.len && !q->reference_bases.p) throw Error(SB_EINVAL, "reference_bases: NULL with a length");
+        if (q->alternate_bases.len && !q->alternate_bases.p) throw Error(SB_EINVAL, "alternate_bases: NULL with a length");
+        // the batch-wide values as columns with scalars (the qualification
+        // of the device planner reads these)
+        sb_request_columns c{};
+        c.vcf_id_all = q->vcf_id;
+        c.reference_dict = q->reference_bases.p ? &q->reference_bases : nullptr;
+        c.n_reference = c.reference_dict ? 1 : 0;
+        c.alternate_dict = q->alternate_bases.p ? &q->alternate_bases : nullptr;
+        c.n_alternate = c.alternate_dict ? 1 : 0;
+        c.variant_type_dict = q->variant_type_dict;
+        c.n_variant_type = q->variant_type_dict ? q->n_variant_type : 0;
+        c.variant_min_length_all = q->variant_min_length_all;
+        c.variant_max_length_all = q->variant_max_length_all;
+        c.granularity_all = q->granularity;
+        c.include_details_all = q->include_details;
+        std::atomic<size_t> bad{SIZE_MAX};
+        const BeaconRows rows{*q, core, &bad};
+        auto B = std::make_unique<sb_batch>();
+        B->s = s;
+        std::unique_ptr<BeaconColumns> cols;
+        auto full = [&]() -> const sb_request_columns & {
+            if (!cols) cols = std::make_unique<BeaconColumns>(c, rows, n);
+            return cols->c;
+        };
+        auto check_codes = [&] {
+            if (bad.load() != SIZE_MAX)
+                throw Error(SB_EINVAL, "variant_type: code out of range at request " + std::to_string(bad.load()));
+        };
+        if (!prepare_requests_device(*B, c, n, rows, full)) {
+            const sb_request_columns &m = full();
+            check_codes();
+            prepare_requests(*B, ColSrc{m}, n);
+        }
+        check_codes();
         store_hold(s);
         *out = B.release();
     });

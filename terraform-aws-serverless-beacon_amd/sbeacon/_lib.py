@@ -88,6 +88,24 @@ class RequestColumns(C.Structure):
                 ('strict_variant_type', C.c_uint8)]
 
 
+class BeaconRequests(C.Structure):
+    """sb_beacon_requests (include/sbeacon.h): the route's query parameters
+    as int64 columns, one VCF."""
+    _fields_ = [('vcf_id', C.c_uint32), ('contig', C.c_void_p), ('contig_map', C.c_void_p),
+                ('n_contig_map', C.c_uint32), ('start', C.c_void_p), ('start2', C.c_void_p),
+                ('end', C.c_void_p), ('end2', C.c_void_p),
+                ('variant_type_code', C.c_void_p), ('variant_type_dict', C.c_void_p), ('n_variant_type', C.c_uint32),
+                ('variant_min_length', C.c_void_p), ('variant_min_length_all', C.c_int64),
+                ('variant_max_length', C.c_void_p), ('variant_max_length_all', C.c_int64),
+                ('reference_bases', Str), ('alternate_bases', Str),
+                ('granularity', C.c_uint8), ('include_details', C.c_uint8)]
+
+
+class ShardCore(C.Structure):
+    """sb_shard_core: [(contig_lo, pos_lo), (contig_hi, pos_hi)) in one VCF."""
+    _fields_ = [('contig_lo', C.c_uint32), ('pos_lo', C.c_int64), ('contig_hi', C.c_uint32), ('pos_hi', C.c_int64)]
+
+
 class ResultView(C.Structure):
     _fields_ = [('error', C.c_int32), ('exists', C.c_int32), ('call_count', C.c_int64),
                 ('all_alleles_count', C.c_int64), ('n_variants', C.c_uint64),
@@ -222,6 +240,7 @@ SIGNATURES = {
     'sb_requests_prepare': (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(P)]),
     'sb_requests_run': (C.c_int, [P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64]),
     'sb_requests_prepare_columns': (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(P)]),
+    'sb_requests_prepare_beacon': (C.c_int, [P, C.c_void_p, C.c_size_t, C.c_void_p, C.POINTER(P)]),
     'sb_requests_time_eval': (C.c_int, [P, C.c_int]),
     'sb_requests_inexact_rows': (C.c_int, [P, P]),
     'sb_store_trim': (C.c_int, [P]),

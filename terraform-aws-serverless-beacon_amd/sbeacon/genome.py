@@ -191,6 +191,20 @@ class Requests:
     def __len__(self):
         return len(self.ci)
 
+    @property
+    def end(self) -> np.ndarray:
+        """requestParameters.end[0] (computed once)."""
+        e = self.__dict__.get('_end')
+        if e is None:
+            e = self.__dict__['_end'] = self.start + self.width
+        return e
+
+    def rows(self, a: int, b: int) -> 'Requests':
+        """Requests [a, b) as views (the end column too)."""
+        sub = Requests(self.ci[a:b], self.start[a:b], self.width[a:b], self.vt[a:b], self.vmin[a:b], self.vmax[a:b])
+        sub.__dict__['_end'] = self.end[a:b]
+        return sub
+
 
 def config3_requests(shape: GenomeShape, n: int = 1_000_000, seed: int = 1003) -> Requests:
     rng = np.random.default_rng(seed)
@@ -464,6 +478,62 @@ def shard_requests(shape: GenomeShape, reqs: Requests, world: int, rank: int) ->
     w = slice(r0 + lo, r0 + hi)
     return ShardRequests(r0 + lo, hi - lo, ci[lo:hi], a, b, smin[lo:hi], smax[lo:hi], reqs.vt[w], reqs.vmin[w],
                          reqs.vmax[w])
+
+
+def shard_rows(shape: GenomeShape, reqs: Requests, world: int, rank: int) -> tuple[int, int]:
+    """Rows [lo, hi) of the requests with at least one slice on rank (the
+    ShardRequests row range): requests are ordered by (contig, start), so
+    only the rows of the two cut contigs go through the plan's splitQuery
+    cut; the library cuts every row itself (sb_requests_prepare_beacon)."""
+    cuts = shape.cuts(world)
+    (c0, _), (c1, _) = cuts[rank], cuts[rank + 1]
+    r0 = int(np.searchsorted(reqs.ci, c0, side='left'))
+    r1 = int(np.searchsorted(reqs.ci, c1, side='right'))
+    ci = reqs.ci[r0:r1]
+    n = len(ci)
+    e0 = int(np.searchsorted(ci, c0, side='right'))
+    s1 = int(np.searchsorted(ci, c1, side='left'))
+    plan = shape.plan(world)
+    firsts, lasts = [], []
+    for x0, x1 in ([(0, n)] if c0 == c1 else [(0, e0), (s1, n)]):
+        if x1 <= x0:
+            continue
+        smin = reqs.start[r0 + x0:r0 + x1] + 1
+        aa, bb = plan.slice_runs(rank, 0, ci[x0:x1], smin, smin + reqs.width[r0 + x0:r0 + x1])
+        has = bb >= aa
+        if has.any():
+            firsts.append(x0 + int(np.argmax(has)))
+            lasts.append(x0 + len(has) - int(np.argmax(has[::-1])))
+    if e0 < s1 and c0 != c1:
+        firsts.append(e0)
+        lasts.append(s1)
+    if not firsts:
+        return r0, r0
+    return r0 + min(firsts), r0 + max(lasts)
+
+
+def prepare_beacon_shard(store, shape: GenomeShape, reqs: Requests, world: int, rank: int, rows=None):
+    """The rank's request batch straight from the Beacon request columns:
+    (row_lo, n_rows, RequestBatch).  The library builds each request's
+    SplitQueryPayload and cuts it to the rank's core (the plan's
+    sb_shard_core) while packing -- the same batch as prepare_shard_requests
+    over shard_requests, with no per-request numpy work here."""
+    from .requests import RequestBatch, beacon_requests
+    lo, hi = rows if rows is not None else shard_rows(shape, reqs, world, rank)
+    n = hi - lo
+    cache = store.__dict__.setdefault('_genome_cmap', {})
+    cmap = cache.get(LOCATION)
+    if cmap is None:
+        at = {c: i for i, c in enumerate(store.contigs(LOCATION))}
+        cmap = cache[LOCATION] = np.array([at.get(c, 0xffffffff) for c in CONTIGS], dtype=np.uint32)
+    q, keep = beacon_requests(
+        n, vcf_id=store.vcf_id(LOCATION), contig=reqs.ci[lo:hi], contig_map=cmap, start=reqs.start[lo:hi],
+        end=reqs.end[lo:hi], reference='N', alternate=None, variant_type=VARIANT_TYPES,
+        variant_type_code=reqs.vt[lo:hi], variant_min_length=reqs.vmin[lo:hi], variant_max_length=reqs.vmax[lo:hi],
+        granularity='record', include_details=True)
+    batch = RequestBatch(store, q, n, core=shape.plan(world).core(rank, 0))
+    del keep
+    return lo, n, batch
 
 
 def prepare_shard_requests(store, sr: ShardRequests):

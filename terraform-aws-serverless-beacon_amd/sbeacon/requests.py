@@ -170,6 +170,67 @@ def request_columns(n: int, *, vcf_id, contig, start_min, start_max, end_min, en
     return c, keep
 
 
+def beacon_requests(n: int, *, vcf_id: int, contig, start, end, start2=None, end2=None, contig_map=None,
+                    reference='N', alternate=None, variant_type=(None,), variant_type_code=None,
+                    variant_min_length=0, variant_max_length=-1, granularity='record', include_details=True):
+    """sb_beacon_requests over the route's query parameters as int64 numpy
+    columns (views, no conversion when they already are contiguous int64):
+    contig codes (contig_map: code -> contig index in the VCF, None =
+    identity), requestParameters start[0] / end[0] (start2 / end2: the second
+    elements of two-element start / end), variantType as distinct values plus
+    a code per request, min / max length columns or scalars.  The library
+    builds each SplitQueryPayload as perform_variant_search_sync does
+    (search_variants.py:179-197).  Returns (BeaconRequests, keep-alive)."""
+    q = _lib.BeaconRequests()
+    keep = [q]
+
+    def col(x):
+        a = np.ascontiguousarray(x, dtype=np.int64)
+        if len(a) != n:
+            raise ValueError(f'{len(a)} values for {n} requests')
+        keep.append(a)
+        return a.ctypes.data
+
+    q.vcf_id = int(vcf_id)
+    q.contig, q.start, q.end = col(contig), col(start), col(end)
+    if start2 is not None:
+        q.start2 = col(start2)
+    if end2 is not None:
+        q.end2 = col(end2)
+    if contig_map is not None:
+        m = np.ascontiguousarray(contig_map, dtype=np.uint32)
+        keep.append(m)
+        q.contig_map, q.n_contig_map = m.ctypes.data, len(m)
+    for f, x in (('variant_min_length', variant_min_length), ('variant_max_length', variant_max_length)):
+        if np.ndim(x) == 0:
+            setattr(q, f + '_all', int(x))
+        else:
+            setattr(q, f, col(x))
+
+    def text(v):
+        s = _lib.Str()
+        if v is not None:
+            b = v.encode() if isinstance(v, str) else bytes(v)
+            buf = C.create_string_buffer(b, len(b) + 1)
+            keep.append(buf)
+            s.p, s.len = C.addressof(buf), len(b)
+        return s
+
+    q.reference_bases, q.alternate_bases = text(reference), text(alternate)
+    vals = list(variant_type)
+    if not all(v is None for v in vals):
+        d = (_lib.Str * len(vals))()
+        for k, v in enumerate(vals):
+            d[k] = text(v)
+        keep.append(d)
+        q.variant_type_dict, q.n_variant_type = C.addressof(d), len(vals)
+        if variant_type_code is not None:
+            q.variant_type_code = col(variant_type_code)
+    q.granularity = _lib.SB_GRAN[granularity] if isinstance(granularity, str) else int(granularity)
+    q.include_details = 1 if include_details else 0
+    return q, keep
+
+
 def requests_from_split_payloads(store, payloads: list[dict], *, strict_variant_type: bool = False,
                                  columns: bool = False):
     """SplitQueryPayload dicts -> (sb_request array, keep-alive, owners):
@@ -225,13 +286,17 @@ def requests_from_split_payloads(store, payloads: list[dict], *, strict_variant_
 class RequestBatch:
     """A prepared request batch (sb_requests_prepare) on the store's device."""
 
-    def __init__(self, store, arr, n: int):
-        """arr: an sb_request array (requests_array) or RequestColumns
-        (request_columns)."""
+    def __init__(self, store, arr, n: int, core=None):
+        """arr: an sb_request array (requests_array), RequestColumns
+        (request_columns) or BeaconRequests (beacon_requests; core: the
+        shard's ShardCore, None = every slice)."""
         self.store = store
         self.n = n
         h = C.c_void_p()
-        if isinstance(arr, _lib.RequestColumns):
+        if isinstance(arr, _lib.BeaconRequests):
+            check(lib().sb_requests_prepare_beacon(store.handle, C.byref(arr), n,
+                                                   C.byref(core) if core is not None else None, C.byref(h)))
+        elif isinstance(arr, _lib.RequestColumns):
             check(lib().sb_requests_prepare_columns(store.handle, C.byref(arr), n, C.byref(h)))
         else:
             check(lib().sb_requests_prepare(store.handle, C.cast(arr, C.c_void_p), n, C.byref(h)))

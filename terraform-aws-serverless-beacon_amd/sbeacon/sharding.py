@@ -259,6 +259,35 @@ class ShardPlan:
         b = np.minimum(smax, smin + SPLIT_SIZE * k1 - 1)
         return a, np.where(k1 > k0, b, a - 1)
 
+    def core(self, rank: int, v: int = 0):
+        """Rank r's core in VCF v as the library's sb_shard_core (slice_runs
+        inside sb_requests_prepare_beacon): slices whose (contig, first base)
+        lies in [key r, key r+1) restricted to VCF v."""
+        from ._lib import ShardCore
+        NONE, LO = 0xffffffff, -(1 << 62)
+        c = ShardCore()
+        if rank <= 0:
+            c.contig_lo, c.pos_lo = 0, LO
+        else:
+            kv, kc, kp = self.keys[rank]
+            if kv < v:
+                c.contig_lo, c.pos_lo = 0, LO
+            elif kv > v:
+                c.contig_lo, c.pos_lo = NONE, 0
+            else:
+                c.contig_lo, c.pos_lo = kc, kp
+        if rank + 1 >= self.world:
+            c.contig_hi, c.pos_hi = NONE, 0
+        else:
+            kv, kc, kp = self.keys[rank + 1]
+            if kv > v:
+                c.contig_hi, c.pos_hi = NONE, 0
+            elif kv < v:
+                c.contig_hi, c.pos_hi = 0, LO
+            else:
+                c.contig_hi, c.pos_hi = kc, kp
+        return c
+
     def split_requests(self, split_payloads: list[dict], rank: int):
         """The request-level fan-out on rank r: one sb_request per
         (SplitQueryPayload, vcf_location) pair -- every rank gets the same
