@@ -495,9 +495,11 @@ typedef struct {
     uint8_t include_details;       /* includeResultsetResponses in {HIT, ALL} */
 } sb_beacon_requests;
 
-/* A shard's core in one VCF: slices whose (contig index, first base) is >=
- * (contig_lo, pos_lo) and < (contig_hi, pos_hi).  contig_hi == UINT32_MAX:
- * no upper end; contig_lo == UINT32_MAX: an empty core. */
+/* A shard's core in one VCF: slices whose (contig code, first base) is >=
+ * (contig_lo, pos_lo) and < (contig_hi, pos_hi) -- contig codes as the
+ * request columns carry them (the VCF's contig order, before contig_map: a
+ * shard store may hold only some contigs).  contig_hi == UINT32_MAX: no
+ * upper end; contig_lo == UINT32_MAX: an empty core. */
 typedef struct {
     uint32_t contig_lo; int64_t pos_lo;
     uint32_t contig_hi; int64_t pos_hi;

@@ -3993,10 +3993,14 @@ struct BeaconRows {
         return need >= static_cast<uint64_t>(nsl) ? nsl : static_cast<int64_t>(need);
     }
     PackRow operator()(size_t i) const {
+        // the core is cut in the caller's contig codes (the VCF's contig
+        // order: a shard store may hold only some of the contigs), then the
+        // code is mapped to the store's contig index
         const int64_t code = q.contig[i];
+        const uint32_t cc = code >= 0 && code < UINT32_MAX ? static_cast<uint32_t>(code) : UINT32_MAX;
         uint32_t contig = UINT32_MAX;
-        if (!q.contig_map) contig = code >= 0 && code < UINT32_MAX ? static_cast<uint32_t>(code) : UINT32_MAX;
-        else if (code >= 0 && static_cast<uint64_t>(code) < q.n_contig_map) contig = q.contig_map[code];
+        if (!q.contig_map) contig = cc;
+        else if (cc < q.n_contig_map) contig = q.contig_map[cc];
         const int64_t s0 = q.start[i], e0 = q.end[i];
         int64_t smin = s0, smax, emin, emax;
         if (q.end2) {
@@ -4016,9 +4020,9 @@ struct BeaconRows {
         ++smin, ++smax, ++emin, ++emax;
         if (core && smin <= smax) {
             const int64_t nsl = (smax - smin) / kSplitSize + 1;
-            const int64_t k0 = core->contig_lo == UINT32_MAX ? nsl : first_k(contig, smin, nsl, core->contig_lo, core->pos_lo);
-            const int64_t k1 = std::max(
-                k0, core->contig_hi == UINT32_MAX ? nsl : first_k(contig, smin, nsl, core->contig_hi, core->pos_hi));
+            const int64_t k0 = core->contig_lo == UINT32_MAX ? nsl : first_k(cc, smin, nsl, core->contig_lo, core->pos_lo);
+            const int64_t k1 =
+                std::max(k0, core->contig_hi == UINT32_MAX ? nsl : first_k(cc, smin, nsl, core->contig_hi, core->pos_hi));
             const int64_t a = smin + kSplitSize * k0;
             smax = k1 > k0 ? std::min(smax, smin + kSplitSize * k1 - 1) : a - 1;
             smin = a;

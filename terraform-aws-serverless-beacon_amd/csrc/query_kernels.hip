@@ -2092,6 +2092,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     auto eval = [&](const ReqChunk &q, uint32_t c) {
         const ChainChunk &x = q.x;
         const uint32_t k = q.k;
+        // every column of this chunk is waited for here, at once: the wait
+        // counter pass then knows them ready on every path below.  Without
+        // it the first use of the record id (the staging store) sits after
+        // branches that may issue loads, where the pass can only wait for
+        // vmcnt(0) -- the NEXT chunk's prefetch included, which serialised
+        // the pipeline
+        asm volatile("" ::"v"(x.p), "v"(x.h.end), "v"(x.h.w), "v"(x.h.ac0), "v"(x.h.an), "v"(x.r));
         const uint32_t base = kWave * c;
         const uint32_t g = base + ul;
         const uint4 A = L.a[k], Bw = L.b[k];
@@ -2134,6 +2141,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             uint32_t x0 = 0;
             if (xl) {
                 x0 = st.x_lo[x.r];
+                // consumed here: no load left pending on this register past
+                // the branch (a later writer of the register would wait for
+                // vmcnt(0) on every path)
+                asm volatile("" ::"v"(x0));
                 const uint32_t nx = w >> VT_NX_SHIFT;
                 for (uint32_t j = 0; j < nx; ++j) {
                     const uint32_t xw = st.xvt[x0 + j];
@@ -2221,21 +2232,27 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             }
         }
     };
-    {
+    if (nch) {
+        // The prefetch is unconditional (past the run a load reads the valid
+        // index i_safe, one cache line): every path of the steady loop then
+        // issues the same loads, so the wait-counter pass can wait for chunk
+        // c's columns with the next chunks' loads still in flight.  A
+        // conditional prefetch leaves a path with no later load, where the
+        // only safe wait is vmcnt(0) -- the pipeline serialised.
         ReqChunk buf[kReqPipe];
 #pragma unroll
-        for (int a = 0; a < kReqPipe; ++a)
-            if (static_cast<uint32_t>(a) < nch) buf[a] = load(a);
-        for (uint32_t c0 = 0; c0 < nch; c0 += kReqPipe) {
+        for (int a = 0; a < kReqPipe; ++a) buf[a] = load(a);
+        uint32_t c0 = 0;
+        for (; c0 + kReqPipe <= nch; c0 += kReqPipe) {
 #pragma unroll
             for (int a = 0; a < kReqPipe; ++a) {
-                const uint32_t c = c0 + a;
-                if (c < nch) {
-                    eval(buf[a], c);
-                    if (c + kReqPipe < nch) buf[a] = load(c + kReqPipe);
-                }
+                eval(buf[a], c0 + a);
+                buf[a] = load(c0 + a + kReqPipe);
             }
         }
+#pragma unroll
+        for (int a = 0; a < kReqPipe; ++a)
+            if (c0 + a < nch) eval(buf[a], c0 + a);
     }
     wave_lds_sync();
     // ---- per chain (lane k < R): staging start (scan of the hit counts), partial

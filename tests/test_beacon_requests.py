@@ -41,9 +41,11 @@ def test_beacon_batch_plans_like_the_sharded_columns(world):
     from sbeacon.genome import prepare_beacon_shard, prepare_shard_requests
     shape = _shape()
     reqs = _straddling(shape, world)
-    store = shape.build_shard_store(1, 0, device=HOST_ONLY)
-    try:
-        for rank in range(world):
+    for rank in range(world):
+        # the rank's own shard store: it holds only the contigs of its
+        # records (store contig indexes differ from the plan's contig codes)
+        store = shape.build_shard_store(world, rank, device=HOST_ONLY)
+        try:
             sr = _same_rows(shape, reqs, world, rank)
             a = prepare_shard_requests(store, sr)
             lo, n, b = prepare_beacon_shard(store, shape, reqs, world, rank)
@@ -53,8 +55,8 @@ def test_beacon_batch_plans_like_the_sharded_columns(world):
             assert sa['chained_slices'] > 0
             a.free()
             b.free()
-    finally:
-        store.close()
+        finally:
+            store.close()
 
 
 def test_beacon_columns_two_element_ranges_and_errors():
