@@ -3551,8 +3551,12 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     // pack
     const uint32_t vid = c.vcf_id_all;
     const auto &slow_pos = s.seg_slow_pos[vid];
-    ReqPool::Pinned pin = P.get_pinned(n * sizeof(ReqIn));
+    // one pinned block: the packed requests, then the LUT words, then the
+    // planner's three counters (one upload of each, one readback, one sync)
+    const size_t lut_at = n * sizeof(ReqIn), cnt_at = (lut_at + lut_all.size() * 4 + 15) & ~size_t(15);
+    ReqPool::Pinned pin = P.get_pinned(cnt_at + 32);
     ReqIn *pk = static_cast<ReqIn *>(pin.p);
+    std::memcpy(static_cast<char *>(pin.p) + lut_at, lut_all.data(), lut_all.size() * 4);
     std::vector<uint8_t> cls(n, 0);
     std::atomic<bool> any_slices{false};
     parallel_for(n, [&](size_t i) {
@@ -3605,16 +3609,18 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     R->runs_at = chain_bytes;
     R->n_runs = n_runs;
     unsigned long long *cnt = reinterpret_cast<unsigned long long *>(rc.as<char>() + size_t(n_runs) * 8);
+    R->lut = P.get_dev(lut_all.size() * 4);
+    R->n_lut = static_cast<uint32_t>(lut_all.size());
     HIP_OK(hipMemcpyAsync(din.p, pk, n * sizeof(ReqIn), hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync(R->lut.p, static_cast<char *>(pin.p) + lut_at, lut_all.size() * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(cnt, 0, 32, st));
     launch_request_plan(s.d, din.as<ReqIn>(), static_cast<uint32_t>(n), R->dchains.as<ReqChain>(),
                         reinterpret_cast<RowRun *>(R->dchains.as<char>() + chain_bytes), rc.as<unsigned long long>(),
                         cnt, st);
     HIP_OK(hipGetLastError());
-    unsigned long long *hc = reinterpret_cast<unsigned long long *>(static_cast<char *>(pin.p));
-    HIP_OK(hipStreamSynchronize(st));  // the packed requests are consumed: the pinned buffer carries the counters back
+    unsigned long long *hc = reinterpret_cast<unsigned long long *>(static_cast<char *>(pin.p) + cnt_at);
     HIP_OK(hipMemcpyAsync(hc, cnt, 24, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
+    HIP_OK(hipStreamSynchronize(st));  // uploads, planning and the counters: one wait
     R->n_chains = hc[0];
     R->n_chain_slices = hc[1];
     const uint64_t stage_total = hc[2];
@@ -3627,11 +3633,7 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     R->tstatus = P.get_dev(size_t(request_tiles(n_runs)) * 8);
     R->stage = P.get_dev(stage_total * 8);
     R->row_src = P.get_dev(R->slices ? n * 8 : 0);
-    R->lut = P.get_dev(lut_all.size() * 4);
-    R->n_lut = static_cast<uint32_t>(lut_all.size());
-    HIP_OK(hipMemcpyAsync(R->lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
-    upload_slice_part(B, *R, seg, n, st);
-    HIP_OK(hipStreamSynchronize(st));
+    upload_slice_part(B, *R, seg, n, st);  // (synchronises when there is a per-slice part)
     tick("upload");
     B.req = std::move(R);
     return true;

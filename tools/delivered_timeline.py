@@ -14,7 +14,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, 'terraform-aws-serverless-beacon_amd'))
 
 
-def timeline(store, shape, reqs, base, dev, chunks, workers, passes=3):
+def timeline(store, shape, reqs, base, dev, chunks, workers, passes=5):
     import numpy as np
     import torch
     from concurrent.futures import ThreadPoolExecutor
@@ -101,7 +101,7 @@ def main():
         print(json.dumps({'serial_prepare_ms': round((time.perf_counter() - t) * 1e3, 2)}), flush=True)
         b.free()
     del os.environ['SBEACON_PREP_TRACE']
-    for chunks, workers in ((8, 2), (8, 1), (4, 2), (16, 2)):
+    for chunks, workers in ((8, 2), (6, 2), (8, 3), (12, 3), (4, 2)):
         tl = timeline(store, shape, reqs, base, dev, chunks, workers)
         print(json.dumps({'chunks': chunks, 'workers': workers, 'ms': [x['ms'] for x in tl]}), flush=True)
         print(json.dumps(tl[-1]['chunks']), flush=True)
