@@ -2250,7 +2250,7 @@ struct PinnedHost {  // grow-only pinned host staging (hipHostMalloc)
 };
 
 struct WinWs {
-    DevMem jobs, wins, e, runs, counts, overflow, list, n_list;
+    DevMem jobs, wins, e, runs, counts, overflow, list, n_list, wfresh;
     PinnedHost stage;  // jobs | runs for one H2D copy; counts + overflow back
 };
 
@@ -2276,6 +2276,7 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     W.e.reserve(std::max<size_t>(P.n_e, 1) * 4);
     W.runs.reserve(std::max<size_t>(runs.size(), 1) * sizeof(KRun));
     W.counts.reserve(std::max<size_t>(nj, 1) * 8);
+    W.wfresh.reserve(std::max<size_t>(nw, 1) * 4);
     W.overflow.reserve(4);
     // deferred displaced keys (10 POS <= the job's largest POS): a list of a
     // quarter of the keys; a fuller list is an overflow (the sorted path)
@@ -2301,7 +2302,7 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     HIP_OK(hipEventRecord(e0, st));
     launch_window_dedupe(s.dk, W.jobs.as<KJob>(), static_cast<uint32_t>(P.jobs.size()), W.wins.as<KWin>(), nw,
                          W.e.as<uint32_t>(), W.runs.as<KRun>(), W.counts.as<unsigned long long>(), W.list.as<uint2>(),
-                         W.n_list.as<uint32_t>(), cap, W.overflow.as<uint32_t>(), st);
+                         W.n_list.as<uint32_t>(), cap, W.overflow.as<uint32_t>(), W.wfresh.as<uint32_t>(), st);
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipGetLastError());
     std::vector<uint64_t> cnt(std::max<size_t>(nj, 1));

@@ -845,7 +845,7 @@ __global__ __launch_bounds__(kThreads) void dedup_plan_kernel(KStore ks, const K
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void window_dedupe_kernel(KStore ks, const KWin *wins, const uint32_t *E,
                                                                  unsigned long long *counts, uint2 *list,
                                                                  uint32_t *n_list, uint32_t cap, uint32_t *overflow,
-                                                                 uint32_t dbg) {
+                                                                 uint32_t *wfresh, uint32_t dbg) {
     __shared__ __attribute__((aligned(16))) unsigned long long s_id[kWinCap];  // identity of window key f
     __shared__ __attribute__((aligned(16))) uint16_t s_win[kWSlots];            // a round's winner per slot
     __shared__ uint32_t s_pre[kWinPieces + 1], s_base[kWinPieces], s_run[kWinPieces];
@@ -875,7 +875,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     __syncthreads();
     const uint32_t np = W.nruns, total = s_pre[np];
     if (total > kWinCap) {  // a pile-up past the window (the host recounts on the sorted path)
-        if (threadIdx.x == 0) atomicOr(overflow, 1u);
+        if (threadIdx.x == 0) {
+            atomicOr(overflow, 1u);
+            wfresh[blockIdx.x] = 0;
+        }
         return;
     }
     // every key's 8-byte class word (key u = u * kThreads + tid): POS, the
@@ -908,6 +911,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u) x += wlo[u] ^ whi[u];
         if (x == 0xdeadbeefu) atomicOr(overflow, x);
+        if (threadIdx.x == 0) wfresh[blockIdx.x] = 0;
         return;
     }
     auto kid_of = [&](uint32_t u) { return u * kThreads + threadIdx.x + s_base[static_cast<uint32_t>(pk >> (6 * u)) & 63u]; };
@@ -1010,7 +1014,25 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     const uint32_t fw = wave_sum_u32(fresh);
     if (lane == 0 && fw) atomicAdd(&s_fresh, fw);
     __syncthreads();
-    if (threadIdx.x == 0 && s_fresh) atomicAdd(&counts[W.job], static_cast<unsigned long long>(s_fresh));
+    // the window's count, folded per job by window_fold_kernel: one device
+    // atomic per window on the jobs' few counter lines (73 k windows for 50
+    // jobs) serialised in L2
+    if (threadIdx.x == 0) wfresh[blockIdx.x] = s_fresh;
+}
+
+// one wave per planned job: its windows' counts [w0, w0 + nw) summed into
+// counts[its runs' job] (the job each of its windows counted for)
+__global__ __launch_bounds__(kThreads) void window_fold_kernel(const KJob *__restrict__ jobs, uint32_t nj,
+                                                               const KRun *__restrict__ runs,
+                                                               const uint32_t *__restrict__ wfresh,
+                                                               unsigned long long *__restrict__ counts) {
+    const uint32_t j = (blockIdx.x * kThreads + threadIdx.x) >> 6, lane = threadIdx.x & 63u;
+    if (j >= nj) return;
+    const KJob J = jobs[j];
+    uint32_t sum = 0;
+    for (uint32_t i = lane; i < J.nw; i += 64) sum += wfresh[J.w0 + i];
+    const uint32_t tot = wave_sum_u32(sum);
+    if (lane == 0 && tot) atomicAdd(&counts[runs[J.run_lo].job], static_cast<unsigned long long>(tot));
 }
 
 uint32_t tiles_of(uint64_t n) { return static_cast<uint32_t>((n + kTile - 1) / kTile); }
@@ -1094,12 +1116,13 @@ int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1,
 
 void launch_window_dedupe(const KStore &ks, const KJob *jobs, uint32_t nj, KWin *wins, uint32_t nw, uint32_t *E,
                           const KRun *runs, unsigned long long *counts, uint2 *list, uint32_t *n_list, uint32_t cap,
-                          uint32_t *overflow, hipStream_t s) {
+                          uint32_t *overflow, uint32_t *wfresh, hipStream_t s) {
     if (!nw) return;
     const char *dbge = std::getenv("SBEACON_DEDUP_WIN_DBG");  // timing ablations (never set by the benches)
     const uint32_t dbg = dbge ? static_cast<uint32_t>(std::atoi(dbge)) : 0u;
     dedup_plan_kernel<<<(nw + kThreads - 1) / kThreads, kThreads, 0, s>>>(ks, jobs, nj, runs, nw, wins, E);
-    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, wins, E, counts, list, n_list, cap, overflow, dbg);
+    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, wins, E, counts, list, n_list, cap, overflow, wfresh, dbg);
+    window_fold_kernel<<<(nj * 64 + kThreads - 1) / kThreads, kThreads, 0, s>>>(jobs, nj, runs, wfresh, counts);
     deferred_dedupe_kernel<<<1024, kThreads, 0, s>>>(ks, runs, list, n_list, cap, counts);
 }
 

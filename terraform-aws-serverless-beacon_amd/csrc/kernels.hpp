@@ -169,11 +169,12 @@ int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1,
 // then one workgroup per window (runs at most kWinPieces, keys at most
 // kWinCap), then one lane per deferred displaced key (list: cap entries,
 // *n_list zeroed by the caller; runs = every job's KRun table); adds each
-// job's distinct keys to counts[job]; *overflow = the window path cannot
+// job's distinct keys to counts[job] (each window's count to wfresh[w], nw
+// entries, then one fold per job); *overflow = the window path cannot
 // answer this call exactly
 void launch_window_dedupe(const KStore &ks, const KJob *jobs, uint32_t nj, KWin *wins, uint32_t nw, uint32_t *E,
                           const KRun *runs, unsigned long long *counts, uint2 *list, uint32_t *n_list, uint32_t cap,
-                          uint32_t *overflow, hipStream_t s);
+                          uint32_t *overflow, uint32_t *wfresh, hipStream_t s);
 void launch_dedup_unique(const uint64_t *keys, const uint32_t *vals, uint64_t n, const KStore &ks, uint32_t job_shift,
                          bool verify, unsigned long long *counts, uint4 *part, uint32_t *coll, uint32_t *ncoll,
                          hipStream_t s);
