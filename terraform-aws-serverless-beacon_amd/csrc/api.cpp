@@ -1530,15 +1530,37 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
                 });
                 continue;
             }
-            std::vector<std::pair<uint64_t, uint32_t>> key(m);  // (seg_lo, first_bp), then input position
+            // (seg_lo, first_bp) words; a stable LSD radix sort over their
+            // used bits (11-bit digits) keeps equal words in input order --
+            // std::sort of the (word, position) pairs took ~2 ms for 32 k
+            // slices; already ordered input (slices of sorted requests) is
+            // detected and left alone
+            std::vector<uint64_t> key(m);
+            uint64_t any = 0;
+            bool sorted = true;
             for (size_t k = 0; k < m; ++k) {
                 const QDev &x = B.hq[g.idx[k]];
-                key[k] = {static_cast<uint64_t>(x.seg_lo) << 32 | static_cast<uint64_t>(x.first_bp), static_cast<uint32_t>(k)};
+                key[k] = static_cast<uint64_t>(x.seg_lo) << 32 | static_cast<uint64_t>(x.first_bp);
+                any |= key[k];
+                sorted = sorted && (k == 0 || key[k - 1] <= key[k]);
             }
-            std::sort(key.begin(), key.end());
-            std::vector<uint32_t> idx(m);
-            for (size_t k = 0; k < m; ++k) idx[k] = g.idx[key[k].second];
-            g.idx = std::move(idx);
+            if (sorted) continue;
+            std::vector<uint64_t> key2(m);
+            std::vector<uint32_t> idx2(m);
+            std::vector<uint32_t> &idx = g.idx;
+            const int bits = 64 - __builtin_clzll(any | 1);
+            for (int sh = 0; sh < bits; sh += 11) {
+                uint32_t cnt[2049] = {0};
+                for (size_t k = 0; k < m; ++k) ++cnt[((key[k] >> sh) & 2047u) + 1];
+                for (int d = 0; d < 2048; ++d) cnt[d + 1] += cnt[d];
+                for (size_t k = 0; k < m; ++k) {
+                    const uint32_t at = cnt[(key[k] >> sh) & 2047u]++;
+                    key2[at] = key[k];
+                    idx2[at] = idx[k];
+                }
+                key.swap(key2);
+                idx.swap(idx2);
+            }
         }
     }
     tick("groups");
