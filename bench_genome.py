@@ -64,7 +64,10 @@ def main_genome(args):
             last[0] = time.perf_counter()
             log(f'[rank {rank}] ingest: {done}/{n_shard} records (contig {contig}), {last[0] - t0:.0f} s')
 
-    store = shape.build_shard_store(world, rank, device=local, threads=args.threads, progress=progress)
+    # the store north_star describes: sites + the 2,504-sample carrier
+    # bit-matrix (~320 B per ALT row; the requests never read it)
+    store = shape.build_shard_store(world, rank, device=local, threads=args.threads, progress=progress,
+                                    genotypes=True)
     info = store.info()
     t_ingest = time.perf_counter() - t0
     log(f'[rank {rank}] shard: {info["n_records"]} records, {info["device_bytes"] / 2**20:.0f} MiB HBM, '
@@ -194,7 +197,8 @@ def main_genome(args):
         'scaling': args.scaling,
         'vs_baseline': None,
         'dtype': 'int64',
-        'data': 'synthetic (seeded whole-genome 1000G-shape VCF text per contig shard, generated + ingested in-process)',
+        'data': 'synthetic (seeded whole-genome 1000G-shape VCF text per contig shard + its 2504-sample carrier '
+                'bit-matrix, generated + ingested in-process)',
         'config': {'workload': 'config3-wgs-1000g-shape', 'records': shape.n_total, 'requests': n_req,
                    'requests_per_gpu': args.genome_requests if args.scaling == 'weak' else None,
                    'slice_queries': int(tot_slices),

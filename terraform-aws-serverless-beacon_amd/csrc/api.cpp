@@ -4686,76 +4686,102 @@ void result_prepare_json(sb_result_set *r) {
     }
 }
 
-bool result_variants_json(const sb_result_set *r, size_t i, std::string &o) {
+namespace {
+// query i's chrom, JSON-escaped (in buf when it fits); false: not UTF-8
+struct ChromText {
+    char buf[256];
+    std::string lng;
+    const char *p = nullptr;
+    size_t n = 0;
+    bool make(const std::string &cs) {
+        if (6 * cs.size() <= sizeof buf) {
+            char *e = json_escape_to(buf, cs.data(), cs.size());
+            if (!e) return false;
+            p = buf;
+            n = static_cast<size_t>(e - buf);
+        } else {
+            if (!json_escape_append(lng, cs.data(), cs.size())) return false;
+            p = lng.data();
+            n = lng.size();
+        }
+        return true;
+    }
+};
+uint64_t variant_row(const sb_store &s, uint64_t hit) {
+    const uint32_t rec = static_cast<uint32_t>(hit);
+    const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
+    return k == 0 ? rec : s.n_records + s.h_x_lo[rec] + k - 1;
+}
+}  // namespace
+
+bool result_variants_len(const sb_result_set *r, size_t i, size_t *need) {
     const sb_store &s = *r->s;
     const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
+    *need = 0;
     if (b == a) return true;
     const VarText &V = *static_cast<const VarText *>(s.var_text.get());  // result_prepare_json built it
-    char cbuf[256];  // the chrom escaped (longer names: the string path)
-    std::string chrom_long;
-    const std::string &cs = r->chrom[i];
-    const char *chrom = cbuf;
-    size_t clen;
-    if (6 * cs.size() <= sizeof cbuf) {
-        char *e = json_escape_to(cbuf, cs.data(), cs.size());
-        if (!e) return false;
-        clen = static_cast<size_t>(e - cbuf);
-    } else {
-        if (!json_escape_append(chrom_long, cs.data(), cs.size())) return false;
-        chrom = chrom_long.data();
-        clen = chrom_long.size();
-    }
-    const uint64_t nr = s.n_records;
-    auto row_of = [&](uint64_t hit) -> uint64_t {
-        const uint32_t rec = static_cast<uint32_t>(hit);
-        const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
-        return k == 0 ? rec : nr + s.h_x_lo[rec] + k - 1;
-    };
-    // the exact text length, one resize, then copies
-    size_t need = 0;
+    ChromText c;
+    if (!c.make(r->chrom[i])) return false;
+    size_t n = 0;
     for (uint64_t h = a; h < b; ++h) {
-        const uint64_t row = row_of(r->hit[h]);
+        const uint64_t row = variant_row(s, r->hit[h]);
         if (V.bad[row]) return false;  // not UTF-8: the Python handler
-        need += 4 + clen + (V.off[row + 1] - V.off[row]);
+        n += 4 + c.n + (V.off[row + 1] - V.off[row]);
     }
-    need -= 2;  // no ", " before the first
-    const size_t o0 = o.size();
-    o.resize(o0 + need);
-    char *p = &o[o0];
+    *need = n - 2;  // no ", " before the first
+    return true;
+}
+
+void result_variants_write(const sb_result_set *r, size_t i, char *p) {
+    const sb_store &s = *r->s;
+    const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
+    if (b == a) return;
+    const VarText &V = *static_cast<const VarText *>(s.var_text.get());
+    ChromText c;
+    c.make(r->chrom[i]);  // (result_variants_len accepted it)
     for (uint64_t h = a; h < b; ++h) {
-        const uint64_t row = row_of(r->hit[h]);
+        const uint64_t row = variant_row(s, r->hit[h]);
         if (h > a) {
             *p++ = ',';
             *p++ = ' ';
         }
         *p++ = '"';
-        std::memcpy(p, chrom, clen);
-        p += clen;
+        std::memcpy(p, c.p, c.n);
+        p += c.n;
         const size_t n = V.off[row + 1] - V.off[row];
         std::memcpy(p, V.text.data() + V.off[row], n);
         p += n;
         *p++ = '"';
     }
+}
+
+bool result_variants_json(const sb_result_set *r, size_t i, std::string &o) {
+    size_t need;
+    if (!result_variants_len(r, i, &need)) return false;
+    const size_t o0 = o.size();
+    o.resize(o0 + need);
+    result_variants_write(r, i, &o[o0]);
     return true;
 }
 
-bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o) {
+bool result_sample_names_len(const sb_result_set *r, size_t i, size_t *need) {
     const auto &ix = r->sidx[i];
     const auto &nj = r->names_json[r->vcf_of[i]];
-    auto name = [&](size_t j) -> const std::string & {
-        return nj[r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j]];
-    };
-    size_t need = ix.empty() ? 0 : 2 * (ix.size() - 1);
+    size_t n = ix.empty() ? 0 : 2 * (ix.size() - 1);
     for (size_t j = 0; j < ix.size(); ++j) {
-        const std::string &x = name(j);
+        const std::string &x = nj[r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j]];
         if (x.size() == 1 && x[0] == '\x01') return false;  // not UTF-8
-        need += x.size();
+        n += x.size();
     }
-    const size_t o0 = o.size();
-    o.resize(o0 + need);
-    char *p = &o[o0];
+    *need = n;
+    return true;
+}
+
+void result_sample_names_write(const sb_result_set *r, size_t i, char *p) {
+    const auto &ix = r->sidx[i];
+    const auto &nj = r->names_json[r->vcf_of[i]];
     for (size_t j = 0; j < ix.size(); ++j) {
-        const std::string &x = name(j);
+        const std::string &x = nj[r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j]];
         if (j) {
             *p++ = ',';
             *p++ = ' ';
@@ -4763,6 +4789,14 @@ bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o) 
         std::memcpy(p, x.data(), x.size());
         p += x.size();
     }
+}
+
+bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o) {
+    size_t need;
+    if (!result_sample_names_len(r, i, &need)) return false;
+    const size_t o0 = o.size();
+    o.resize(o0 + need);
+    result_sample_names_write(r, i, &o[o0]);
     return true;
 }
 }  // namespace sb

@@ -138,6 +138,12 @@ void result_prepare_json(sb_result_set *r);
 int result_view(const sb_result_set *r, size_t i, sb_result_view *out);  // sb_result_get without hit views
 void run_tasks(size_t n, const std::function<void(size_t)> &fn);          // on the host worker pool
 bool result_variants_json(const sb_result_set *r, size_t i, std::string &o);
+// the same text in two steps: its exact length (false: the Python handler),
+// then exactly that many bytes written at p (the wire writes in place)
+bool result_variants_len(const sb_result_set *r, size_t i, size_t *need);
+void result_variants_write(const sb_result_set *r, size_t i, char *p);
+bool result_sample_names_len(const sb_result_set *r, size_t i, size_t *need);
+void result_sample_names_write(const sb_result_set *r, size_t i, char *p);
 // the sample_names list items of query i (false: a name that is not UTF-8)
 bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o);
 

@@ -4,7 +4,11 @@ SURVEY.md §8d config 3, §8e).
 Store: a 1000 Genomes-shape whole genome — ~85 M records over contigs 1-22,
 X, Y, counts proportional to contig length (``chrom_matching.py:12-38``),
 one synthetic generator per contig (seed ``1000 * seed + contig index``),
-sites-only (the config-3 queries never read genotypes).
+generated as sites-only text; the bench store carries the generator's
+2,504-sample carrier bit-matrix beside it (``build_shard_store(genotypes=
+True)``: the planes the GT columns would give, attached through
+``sb_builder_attach_carriers``) -- the HBM-resident store north_star
+describes, although the config-3 queries never read genotypes.
 
 Sharding (one rank per GPU).  The genome's records, in (contig, POS) order,
 are cut into ``world`` ranges of equal record count; rank r's *core* is
@@ -168,11 +172,31 @@ class GenomeShape:
         lo, hi = self.plan(world).record_range(rank, 0)
         return self.text(lo, hi, chunk, threads, progress)
 
-    def build_shard_store(self, world: int, rank: int, *, device=0, threads=0, progress=None):
-        """Rank's store, built by ShardPlan.build_store from the generated text."""
+    def build_shard_store(self, world: int, rank: int, *, device=0, threads=0, progress=None, genotypes=False):
+        """Rank's store, built by ShardPlan.build_store from the generated
+        text (sites only); ``genotypes``: with the generator's n_samples
+        carrier bit-matrix attached (the rows the GT columns would give,
+        SyntheticVcf.carrier_planes: ~320 B per ALT row at 2,504 samples)."""
         return self.plan(world).build_store(
             rank, device=device, keep_genotypes=False, n_threads=threads,
-            text=lambda v, lo, hi: self.text(lo, hi, threads=threads, progress=progress))
+            text=lambda v, lo, hi: self.text(lo, hi, threads=threads, progress=progress),
+            carriers=(lambda v, lo, hi: self.carriers(lo, hi, threads)) if genotypes and self.n_samples else None)
+
+    def carriers(self, lo: int, hi: int, threads: int = 0):
+        """(sample names, carrier planes) of genome records [lo, hi),
+        record-then-ALT order."""
+        pieces = []
+        for ci in range(len(CONTIGS)):
+            a, b = max(lo, int(self.offsets[ci])), min(hi, int(self.offsets[ci + 1]))
+            if b > a:
+                pieces.append((ci, a - int(self.offsets[ci]), b - int(self.offsets[ci])))
+        rows = [self.gen(ci).alt_rows(a, b, threads) for ci, a, b in pieces]
+        out = np.empty((sum(rows), (self.n_samples + 63) // 64), dtype=np.uint64)
+        r = 0
+        for (ci, a, b), n in zip(pieces, rows):
+            self.gen(ci).carrier_planes(a, b, threads, out=out[r:r + n])
+            r += n
+        return self.gen(0).sample_names(), out
 
     def shard_records(self, world: int, rank: int) -> int:
         return sum(hi - lo for _, lo, hi in self.shard_pieces(world, rank))

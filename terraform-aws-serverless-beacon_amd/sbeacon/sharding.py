@@ -161,10 +161,13 @@ class ShardPlan:
 
     # ---------------------------------------------------------------- stores
     def build_store(self, rank: int, *, device: int = 0, keep_genotypes: bool = True, n_threads: int = 0,
-                    text=None):
+                    text=None, carriers=None):
         """Rank r's store: every VCF of the plan restricted to its record range.
         ``text(v, lo, hi)``, when given, yields VCF v's header + records
-        [lo, hi) as text chunks (a generated VCF) instead of reading its file."""
+        [lo, hi) as text chunks (a generated VCF) instead of reading its file;
+        ``carriers(v, lo, hi)``, when given, returns (sample names, planes) --
+        the carrier bit-matrix of a sites-only text, uint64 [ALT rows of
+        records lo..hi, ceil(n/64)] (sb_builder_attach_carriers) -- or None."""
         from ._lib import BuildOpts
         from .engine import Store
         L = lib()
@@ -182,6 +185,18 @@ class ShardPlan:
                 else:
                     for chunk in text(v, lo, hi):
                         check(L.sb_builder_add_text(b, vid.value, chunk, len(chunk)))
+                car = carriers(v, lo, hi) if carriers is not None else None
+                if car is not None:
+                    names = [n.encode() for n in car[0]]
+                    planes = np.ascontiguousarray(car[1], dtype=np.uint64)
+                    del car
+                    if planes.ndim != 2 or planes.shape[1] != (len(names) + 63) // 64:
+                        raise ValueError('carrier planes must be [alt rows, ceil(n_samples / 64)] uint64')
+                    arr = (C.c_char_p * len(names))(*names)
+                    lens = (C.c_uint32 * len(names))(*[len(x) for x in names])
+                    check(L.sb_builder_attach_carriers(b, vid.value, arr, lens, len(names), planes.ctypes.data,
+                                                       planes.shape[0]))
+                    del planes
             s = C.c_void_p()
             check(L.sb_builder_finish(b, int(device), C.byref(s)))
         finally:

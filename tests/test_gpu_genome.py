@@ -119,3 +119,46 @@ def test_compact_hits_match_fetch(genome, monkeypatch, chains):
     assert ro[-1] == sum(len(x) for x in per_row) > 0
     for w in range(sl.n_rows):
         assert [int(x) for x in h[ro[w]:ro[w + 1]]] == per_row[w], w
+
+
+def test_genotype_bitmatrix_shard_answers_like_gt_text():
+    """The config-3 store with its carrier bit-matrix attached
+    (build_shard_store(genotypes=True): sites-only text + the planes the GT
+    columns would give, sb_builder_attach_carriers), on the second shard of
+    two (carrier rows aligned to the shard's record range): sample-collecting
+    payloads answer exactly as the oracle over the same records' GT text."""
+    import random
+    from oracle.oracle import OracleVcf
+    from sbeacon.genome import CONTIGS, LOCATION, GenomeShape
+    shape = GenomeShape(n_total=120_000, seed=3, n_samples=96)
+    world, rank = 2, 1
+    pieces = shape.shard_pieces(world, rank)
+    store = shape.build_shard_store(world, rank, device=0, genotypes=True)
+    assert store.info()['device_bytes'] > 0
+    rng = random.Random(17)
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, 'shard_gt.vcf')
+        with open(path, 'wb') as f:
+            f.write(shape.gen(pieces[0][0]).header(sites_only=False))
+            for ci, a, b in pieces:
+                f.write(shape.gen(ci).records(a, b, sites_only=False))
+        orc = OracleVcf(path)
+        payloads = []
+        for _ in range(60):
+            ci, a, b = pieces[rng.randrange(len(pieces))]
+            pos = shape.gen(ci).positions()[a:b]
+            x = int(pos[rng.randrange(len(pos))])
+            payloads.append(dict(passthrough={'includeSamples': True}, dataset_id='d', query_id='g',
+                                 region=f'{CONTIGS[ci]}:{x}-{x + rng.randrange(1, 9999)}', reference_bases='N',
+                                 end_min=0, end_max=10**9, alternate_bases='N', variant_type=None,
+                                 include_details=True, requested_granularity='record', variant_min_length=0,
+                                 variant_max_length=-1, vcf_location=LOCATION))
+        rs = store.query(payloads)
+        hits = 0
+        for i, p in enumerate(payloads):
+            got = rs.response(i).dump()
+            exp = orc.perform_query(p)
+            assert normalise(got) == normalise(exp), p
+            hits += len(got['sample_indices'])
+        assert hits > 0
+    store.close()

@@ -86,12 +86,18 @@ def test_wire_random_and_fallback_events(stores):
                dict(base, passthrough=False),                   # the same
                {'Records': {'0': 1}}]                           # an envelope that does not unwrap
         evs.extend(odd)
-        buf, off = pack_events([json.dumps(e) for e in evs])
+        texts = [json.dumps(e) for e in evs]
+        # a duplicated keyword: json.loads keeps the last value (dict
+        # semantics), so the fast path must too
+        dup = json.dumps(dict(base, end_max='not an int'))[:-1] + ', "end_max": ' + str(base['end_max']) + '}'
+        texts.append(dup)
+        evs.append(json.loads(dup))
+        buf, off = pack_events(texts)
         out = perform_query_events_packed(buf, off)
         fb = out.fallback.tolist()
-        assert fb[-8:] == [1, 1, 1, 1, 0, 1, 1, 1]
-        assert not any(fb[:-8])
-        assert 'AttributeError' in out[len(evs) - 3] and 'AttributeError' in out[len(evs) - 2]
+        assert fb[-9:] == [1, 1, 1, 1, 0, 1, 1, 1, 0]
+        assert not any(fb[:-9])
+        assert 'AttributeError' in out[len(evs) - 4] and 'AttributeError' in out[len(evs) - 3]
         for i, ev in enumerate(evs):
             assert out[i] == _python(ev), (ev, out[i])
         assert out.texts() == [out[i] for i in range(len(evs))]
