@@ -148,7 +148,11 @@ def test_genotype_bitmatrix_shard_answers_like_gt_text():
             ci, a, b = pieces[rng.randrange(len(pieces))]
             pos = shape.gen(ci).positions()[a:b]
             x = int(pos[rng.randrange(len(pos))])
-            payloads.append(dict(passthrough={'includeSamples': True}, dataset_id='d', query_id='g',
+            pt = {'includeSamples': True}
+            if len(payloads) % 2:  # a sample subset (the selected-samples path)
+                pt = {'includeSamples': True, 'selectedSamplesOnly': True,
+                      'sampleNames': rng.sample(shape.gen(0).sample_names(), 20)}
+            payloads.append(dict(passthrough=pt, dataset_id='d', query_id='g',
                                  region=f'{CONTIGS[ci]}:{x}-{x + rng.randrange(1, 9999)}', reference_bases='N',
                                  end_min=0, end_max=10**9, alternate_bases='N', variant_type=None,
                                  include_details=True, requested_granularity='record', variant_min_length=0,
@@ -159,6 +163,6 @@ def test_genotype_bitmatrix_shard_answers_like_gt_text():
             got = rs.response(i).dump()
             exp = orc.perform_query(p)
             assert normalise(got) == normalise(exp), p
-            hits += len(got['sample_indices'])
+            hits += len(got['sample_names'])
         assert hits > 0
     store.close()
