@@ -213,16 +213,21 @@ def main():
             # batch in one library call (sbeacon/wire.py, csrc/wire.cpp)
             from sbeacon.wire import pack_events, perform_query_events_packed
             ebuf, eoff = pack_events([json.dumps(p) for p in payloads])
-            perform_query_events_packed(ebuf, eoff[:65])
-            t2 = time.perf_counter()
-            for _ in range(reps):
+            wout = perform_query_events_packed(ebuf, eoff)  # warm: the output / event buffers sized once
+            tw = []
+            for _ in range(5):  # steady state: the previous output released outside the timed call
+                wout = None
+                t2 = time.perf_counter()
                 wout = perform_query_events_packed(ebuf, eoff)
-            dtw = (time.perf_counter() - t2) / reps
+                tw.append(time.perf_counter() - t2)
+            dtw = sorted(tw)[len(tw) // 2]  # median call
             delivered['wire'] = {'requests_per_s': round(n_req / dtw, 1), 'slice_payloads_per_s': round(n_slice / dtw, 1),
                                  'ms_per_batch': round(dtw * 1e3, 2), 'event_bytes': len(ebuf),
                                  'response_bytes': len(wout.buf), 'python_fallbacks': int(wout.fallback.sum()),
+                                 'call_ms': [round(t * 1e3, 2) for t in tw],
                                  'note': 'event JSON texts in -> response JSON texts out (json.dumps(response.dump()) '
-                                         'byte for byte): C++ parse + one device batch + C++ formatting'}
+                                         'byte for byte): C++ parse + one device batch + C++ formatting; median of 5 '
+                                         'calls after a warm-up call'}
         finally:
             engine.registry.clear()
 
