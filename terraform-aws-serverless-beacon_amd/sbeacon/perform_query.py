@@ -14,8 +14,10 @@ inside the engine (one flag per query), so a batch may mix both variants.
 with the evident intent (branch on ``payload.variant_type``; SURVEY.md
 §8a.1-4); set ``SBEACON_STRICT_VARIANT_TYPE=1`` to reproduce the crash.
 
-The async path (``is_async``: DynamoDB/S3 result hand-off, ``:273-317``) is
-out of scope: results are always returned synchronously.
+The async path (``is_async``: the SNS-delivered event; ``:273-317``) also
+records the response for the route's fan-in: a response number, the body
+and ``markFinished`` on the query's record (``sbeacon.variant_queries``,
+in process instead of DynamoDB/S3).
 """
 from __future__ import annotations
 
@@ -33,9 +35,13 @@ def _as_dict(payload) -> dict:
 
 
 def perform_query(payload, is_async=False) -> PerformQueryResponse:
-    res = query_payloads([_as_dict(payload)], strict_variant_type=STRICT_VARIANT_TYPE)[0]
+    d = _as_dict(payload)
+    res = query_payloads([d], strict_variant_type=STRICT_VARIANT_TYPE)[0]
     if isinstance(res, Exception):
         raise res
+    if is_async:
+        from .variant_queries import record_response
+        record_response(d.get('query_id', 'test'), res)
     return res
 
 
