@@ -161,6 +161,13 @@ def main_genome(args):
         if delivered['hits_returned'] != serial['hits_returned']:
             raise RuntimeError(f'pipelined delivery returned {delivered["hits_returned"]} hits, serial '
                                f'{serial["hits_returned"]}')
+        # full-size property: the step's rows + hit lists (one batch, resident),
+        # the serial delivered pass and the pipelined chunks are bit-identical
+        step_digest = digest(part[:sr.n_rows].cpu().numpy(), [hits[:nhits].cpu().numpy()])
+        if not (step_digest == serial['digest'] == delivered['digest']):
+            raise RuntimeError(f'delivery digests differ: step {step_digest}, serial {serial["digest"]}, '
+                               f'pipelined {delivered["digest"]}')
+        delivered['digests_equal_step'] = True
         delivered['serial'] = serial
         delivered['cold_launch'] = cold_launch_probe(store, shape, reqs, world, rank, base, dev)
         delivered['cold_launch']['note'] = (
@@ -263,6 +270,19 @@ def shard_setup(shape, reqs, world, rank, deliver):
     return sr, owner_ranks(first, deliver, rank), shard_record_base(shape, world, rank)
 
 
+def digest(rows, hit_parts) -> str:
+    """blake2b over the request rows (int64 [n, 5]) and the hit lists in
+    request order (uint64 arrays, concatenated): the delivery paths' outputs
+    compared at full size without keeping copies."""
+    import hashlib
+    import numpy as np
+    h = hashlib.blake2b(digest_size=16)
+    h.update(np.ascontiguousarray(rows, dtype=np.int64).tobytes())
+    for x in hit_parts:
+        h.update(np.ascontiguousarray(x).view(np.uint64).tobytes())
+    return h.hexdigest()
+
+
 def make_step(run, ex, part, hits, row_off):
     """The bench step: ``run(part, hits, row_off)`` answers the rank's
     sub-requests into its rows / dense hit lists, then ResultExchange
@@ -324,6 +344,7 @@ def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5)
                          'prepare_upload': round(t_prep / passes * 1e3, 2),
                          'device_pass_and_d2h': round(t_dev / passes * 1e3, 2)},
             'hits_returned': int(ro_h[-1]),
+            'digest': digest(rows_h[:n_rows].numpy(), [hits_h[:int(ro_h[-1])].numpy()]),
             'note': 'requests as numpy columns in host memory -> rows + row offsets + dense hit lists in pinned host '
                     'memory; routing, planning, upload, the pass and both D2H copies inside the timed region'}
 
@@ -398,6 +419,7 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
     rows_d = torch.empty((n, 5), dtype=torch.int64, device=dev)
     ro_d = torch.empty(n + chunks, dtype=torch.int64, device=dev)
     hits_d, hits_h = [None] * chunks, [None] * chunks
+    hit_n = [0] * chunks
     times, total_hits = [], 0
     with ThreadPoolExecutor(workers) as ex:
         for p in range(passes + 1):  # pass 0 sizes the hit buffers (untimed)
@@ -423,12 +445,12 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
                 while len(pend) > 1:  # the previous chunk's hits, once its offsets are back
                     kk, e, last = pend.pop(0)
                     e.synchronize()
-                    nh = int(ro_h[last])
+                    nh = hit_n[kk] = int(ro_h[last])
                     total_hits += nh
                     hits_h[kk][:nh].copy_(hits_d[kk][:nh], non_blocking=True)
             for kk, e, last in pend:
                 e.synchronize()
-                nh = int(ro_h[last])
+                nh = hit_n[kk] = int(ro_h[last])
                 total_hits += nh
                 hits_h[kk][:nh].copy_(hits_d[kk][:nh], non_blocking=True)
             stream.synchronize()
@@ -442,6 +464,7 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
             'mean_ms': round(sum(times) / len(times) * 1e3, 2), 'best_ms': round(min(times) * 1e3, 2),
             'pass_ms': [round(t * 1e3, 2) for t in times], 'passes': passes, 'chunks': chunks, 'workers': workers,
             'hits_returned': total_hits,
+            'digest': digest(rows_h.numpy(), [hits_h[k][:hit_n[k]].numpy() for k in range(chunks)]),
             'note': f'pipelined: the requests cut into chunks of consecutive rows; {workers} host threads route + '
                     'prepare chunks ahead (sb_requests_prepare_beacon: Beacon int64 columns -> SplitQueryPayloads '
                     'cut to the core and packed in the library) while each prepared chunk runs and copies back '
