@@ -421,6 +421,9 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
     hits_d, hits_h = [None] * chunks, [None] * chunks
     hit_n = [0] * chunks
     times, total_hits = [], 0
+    import gc
+    gc.collect()
+    gc.disable()  # as timeit does: a collector pause inside a ~3.5 ms pass is noise, not the path
     with ThreadPoolExecutor(workers) as ex:
         for p in range(passes + 1):  # pass 0 sizes the hit buffers (untimed)
             torch.cuda.synchronize()
@@ -459,6 +462,7 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
                 bt.free()
             if p:
                 times.append(dt)
+    gc.enable()
     dt = sorted(times)[len(times) // 2]  # the median pass (host threads make single passes noisy)
     return {'requests_per_s': round(n / dt, 1), 'ms_per_pass': round(dt * 1e3, 2),
             'mean_ms': round(sum(times) / len(times) * 1e3, 2), 'best_ms': round(min(times) * 1e3, 2),
