@@ -1997,6 +1997,9 @@ struct ReqChunk {
     uint32_t k;  // the lane's chain
 };
 
+#ifdef SBEACON_ENDCAP_CHECK
+__device__ unsigned g_endcap_prints = 0;
+#endif
 template <bool LDS_LUT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_eval_kernel(
     DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
@@ -2089,6 +2092,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     uint32_t carry = 0;  // the last positive hit's slice key + 1 (keys grow with the position)
     uint32_t acc_nv = 0, acc_ex = 0;
     uint64_t acc_cc = 0, acc_an = 0;
+#ifdef SBEACON_ENDCAP_CHECK
+    // diagnostic build only (tools/endcap_check.sh): per-chain sums by end
+    // captures computed beside the shipping pull-and-subtract and compared
+    const uint32_t qpos = pin - 1u, qlane = qpos & 63u;
+    const uint32_t qchunk = pin ? qpos >> 6 : ~0u;
+    uint32_t e_nv = 0, e_ex = 0, run_nv = 0, run_ex = 0;
+#endif
     auto eval = [&](const ReqChunk &q, uint32_t c) {
         const ChainChunk &x = q.x;
         const uint32_t k = q.k;
@@ -2202,6 +2212,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint64_t nb = __ballot(isnew);
         // inclusive per-lane counts of the chunk: variants | new slices << 16
         const uint32_t nvex = (pre + cn) | (popc_below(nb) + (isnew ? 1u : 0u)) << 16;
+#ifdef SBEACON_ENDCAP_CHECK
+        {
+            const uint32_t pq = bperm(nvex, qlane);
+            if (qchunk == c) {
+                e_nv = run_nv + (pq & 0xffffu);
+                e_ex = run_ex + (pq >> 16);
+            }
+            run_nv += tot;
+            run_ex += static_cast<uint32_t>(__popcll(nb));
+        }
+#endif
         // ---- chain k's part of the chunk, pulled by lane k from its last lane
         const uint32_t lim = min(base + kWave, T);
         const bool inter = pex < lim && pin > base;
@@ -2255,6 +2276,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             if (c0 + a < nch) eval(buf[a], c0 + a);
     }
     wave_lds_sync();
+#ifdef SBEACON_ENDCAP_CHECK
+    {
+        const uint32_t sn = wave_shr1(e_nv), sx = wave_shr1(e_ex);
+        const uint32_t n2 = e_nv - sn, x2 = e_ex - sx;
+        const bool bad = n2 != acc_nv || x2 != acc_ex;
+        const uint64_t mb = __ballot(bad);
+        if (mb && ul == static_cast<uint32_t>(ffs64(mb)) && atomicAdd(&g_endcap_prints, 1u) < 24)
+            printf("endcap w=%u lane=%u R=%u Rn=%u T=%u nch=%u pin=%u pex=%u qchunk=%u acc_nv=%u n2=%u acc_ex=%u x2=%u "
+                   "e_nv=%u prev=%u run_nv=%u hpos=%u e_ex=%u prev_ex=%u run_ex=%u pacc_ex=%u\n",
+                   w, ul, R, Rn, T, nch, pin, pex, qchunk, acc_nv, n2, acc_ex, x2, e_nv, sn, run_nv, hpos, e_ex, sx,
+                   run_ex, wave_shr1(acc_ex));
+    }
+#endif
     // ---- per chain (lane k < R): staging start (scan of the hit counts), partial
     const uint32_t cs = incl_sum_u32(acc_nv) - acc_nv;
     ReqPartial part{0, 0, 0, 0, 0};
