@@ -46,7 +46,10 @@ def parse():
     ap.add_argument('--samples', type=int, default=2504)
     ap.add_argument('--range-requests', type=int, default=5000)
     ap.add_argument('--point-requests', type=int, default=5000)
-    ap.add_argument('--threads', type=int, default=16, help='host ingest / CPU-baseline threads')
+    ap.add_argument('--threads', type=int, default=None,
+                    help='host ingest / CPU-baseline threads (default: every CPU the process may use, host_cores())')
+    ap.add_argument('--batches', type=int, default=4,
+                    help='config 3: request batches the step rotates over (each answered every --batches steps)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='target CPU-baseline sample duration')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--parity-requests', type=int, default=2000,
@@ -63,7 +66,35 @@ def parse():
                     help="config 3: each request's rows + hits go to the rank of its first slice, or all to rank 0")
     ap.add_argument('--gnomad-records', type=int, default=750_000_000)
     ap.add_argument('--gnomad-requests', type=int, default=50_000, help='config-5 requests per GPU')
-    return ap.parse_args()
+    args = ap.parse_args()
+    if args.threads is None:
+        args.threads = host_cores()['cores']
+    return args
+
+
+def host_cores() -> dict:
+    """The CPUs this process may run on: its affinity mask, capped by the
+    cgroup's CPU quota when one is set (a 16-CPU quota on a 256-CPU affinity
+    mask gives 16 CPUs' worth of time: more threads only time-slice), with the
+    CPU model (lscpu's "Model name", from /proc/cpuinfo)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, period = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        if q != 'max':
+            quota = int(q) / int(period)
+    except (OSError, ValueError):
+        pass
+    model = None
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                model = line.split(':', 1)[1].strip()
+                break
+    except OSError:
+        pass
+    cores = aff if quota is None else max(1, min(aff, int(quota)))
+    return {'cores': cores, 'affinity': aff, 'cgroup_cpu_quota': quota, 'model': model}
 
 
 def unique_rows(gen, payloads) -> int:
@@ -301,7 +332,7 @@ def cpu_baseline_and_parity(args, gen, reqs, payloads, owner, rs):
     dt, passes = orc.time_batch(pl, patched=True, threads=threads, min_seconds=args.cpu_seconds)
     done = passes * len(order)
     sample = f'all {len(reqs)} requests ({len(pl)} slice payloads) x {passes} passes'
-    cpu = {'value': round(done / dt, 1), 'unit': 'requests/s', 'cores': threads, 'kind': 'port',
+    cpu = {'value': round(done / dt, 1), 'unit': 'requests/s', 'cores': threads, 'kind': 'port', 'host': host_cores(),
            'sample': sample + f' through oracle/sbeacon_oracle.c (CPU restatement of search_variants.py), '
                               f'OpenMP x{threads}, sites-only VCF text (config-2 queries read no GT)',
            'seconds': round(dt, 2), 'host_cpus': os.cpu_count()}

@@ -73,58 +73,102 @@ def main_genome(args):
     log(f'[rank {rank}] shard: {info["n_records"]} records, {info["device_bytes"] / 2**20:.0f} MiB HBM, '
         f'ingest {t_ingest:.1f} s')
     # weak scaling (default): genome-wide requests, args.genome_requests per GPU, routed
-    # to the shards by position; strong: args.genome_requests in total
+    # to the shards by position; strong: args.genome_requests in total.  The
+    # step rotates over args.batches independently drawn request sets (seeds
+    # 1003, 1004, ...), each prepared once: a step answers a batch the device
+    # did not answer in the previous step (its ~220 MB working set is out of
+    # the 256 MB MALL by the time it comes round again), starting from the
+    # packed requests resident in HBM -- the planning kernels run inside the
+    # step (sb_requests_set_replan)
     n_req = args.genome_requests * (world if args.scaling == 'weak' else 1)
-    reqs = config3_requests(shape, n=n_req, seed=1003)
+    stream = torch.cuda.current_stream().cuda_stream
     t0 = time.perf_counter()
-    sr, owners, base = shard_setup(shape, reqs, world, rank, args.deliver)  # ShardPlan routing
-    batch = prepare_shard_requests(store, sr)      # request batch: planning + upload (C++)
-    t_prepare = time.perf_counter() - t0
-    batch.set_stream(torch.cuda.current_stream().cuda_stream)  # one stream: kernels, torch ops, RCCL
-    pst = batch.stats()
-    part = torch.zeros((max(sr.n_rows, 1), 5), dtype=torch.int64, device=dev)
-    hits = torch.zeros(max(int(pst['hits']), 1), dtype=torch.int64, device=dev)
-    row_off = torch.zeros(sr.n_rows + 1, dtype=torch.int64, device=dev)
-    sl = shard_slices(shape, reqs, world, rank)  # slice view (statistics / roofline pricing only)
-    ex = ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, dev)
-    log(f'[rank {rank}] {n_req} requests, {len(sl)} slices on this rank (rows {sr.row_lo}+{sr.n_rows}, '
-        f'{pst["chains"]} chains), delivery {args.deliver}: owns {ex.n_own} rows, receives {len(ex.recvs)} '
-        f'range(s), prepare {t_prepare:.2f} s')
+    B = []
+    for k in range(args.batches):
+        reqs_k = config3_requests(shape, n=n_req, seed=1003 + k)
+        sr, owners, base = shard_setup(shape, reqs_k, world, rank, args.deliver)  # ShardPlan routing
+        batch = prepare_shard_requests(store, sr)      # request batch: packing + upload + planning (C++)
+        batch.set_stream(stream)  # torch's stream: kernels, torch ops and RCCL in one order
+        batch.set_replan(True)
+        pst = batch.stats()
+        B.append(dict(reqs=reqs_k, sr=sr, batch=batch, pst=pst,
+                      part=torch.zeros((max(sr.n_rows, 1), 5), dtype=torch.int64, device=dev),
+                      hits=torch.zeros(max(int(pst['hits']), 1), dtype=torch.int64, device=dev),
+                      row_off=torch.zeros(sr.n_rows + 1, dtype=torch.int64, device=dev),
+                      ex=ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, dev)))
+    t_prepare = (time.perf_counter() - t0) / args.batches
+    reqs, sr, batch, pst = B[0]['reqs'], B[0]['sr'], B[0]['batch'], B[0]['pst']
+    part, hits, row_off, ex = B[0]['part'], B[0]['hits'], B[0]['row_off'], B[0]['ex']
+    log(f'[rank {rank}] {args.batches} batches of {n_req} requests; batch 0: rows {sr.row_lo}+{sr.n_rows}, '
+        f'{pst["chains"]} chains, delivery {args.deliver}: owns {ex.n_own} rows, receives {len(ex.recvs)} '
+        f'range(s), prepare {t_prepare:.2f} s per batch')
 
     # answer + deliver: request rows + dense hit lists (one pass), exchange
-    step = make_step(lambda p, h, o: batch.run(p.data_ptr(), h.data_ptr(), o.data_ptr(), base), ex, part, hits,
-                     row_off)
+    steps = [make_step(lambda p, h, o, b=b: b['batch'].run(p.data_ptr(), h.data_ptr(), o.data_ptr(), base), b['ex'],
+                       b['part'], b['hits'], b['row_off']) for b in B]
 
-    for _ in range(args.warmup):
-        step()
-    batch.sync()
+    for i in range(max(args.warmup, args.batches)):
+        steps[i % len(steps)]()
+    torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t1 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    batch.sync()  # records the closing event on the stream
+    e0.record()
+    for i in range(args.steps):
+        steps[i % len(steps)]()
+    e1.record()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t1
     if dist:
         dist.barrier()
-    step_dev_ms = batch.timing()['total_ms']  # HIP events on the stream: first run -> sync, / steps
+    step_dev_ms = e0.elapsed_time(e1) / args.steps  # events on the stream around the K steps
     # the dominant kernel (request_eval_kernel) alone: events around its launch
-    # in each of K passes on its stream (sb_requests_time_eval); the whole pass beside it
-    batch.time_eval(True)
-    for _ in range(args.steps):
-        batch.run(part.data_ptr(), hits.data_ptr(), row_off.data_ptr(), base)
-    batch.sync()
-    tm = batch.timing()
-    kern_ms, pass_ms = tm['scan_ms'], tm['total_ms']
-    batch.time_eval(False)
+    # in each pass on its stream (sb_requests_time_eval), the same rotation
+    for b in B:
+        b['batch'].time_eval(True)
+    for i in range(args.steps):
+        b = B[i % len(B)]
+        b['batch'].run(b['part'].data_ptr(), b['hits'].data_ptr(), b['row_off'].data_ptr(), base)
+    n_pass = [len(range(k, args.steps, len(B))) for k in range(len(B))]
+    eval_ms = []
+    for b, n in zip(B, n_pass):
+        b['batch'].sync()
+        if n:
+            eval_ms.append((b['batch'].timing()['scan_ms'], n))
+        b['batch'].time_eval(False)
+    kern_ms = sum(t * n for t, n in eval_ms) / max(sum(n for _, n in eval_ms), 1)
+    # the pass without the exchange (re-plan + eval + tile scan + deliver), same rotation
+    torch.cuda.synchronize()
+    e0.record()
+    for i in range(args.steps):
+        b = B[i % len(B)]
+        b['batch'].run(b['part'].data_ptr(), b['hits'].data_ptr(), b['row_off'].data_ptr(), base)
+    e1.record()
+    torch.cuda.synchronize()
+    pass_ms = e0.elapsed_time(e1) / args.steps
     nhits = int(row_off[-1].item())
-    # candidate statistics of the rank's chains (the slice view of the same requests)
+    # candidate statistics of each batch's chains (the slice view of the same
+    # requests), averaged over the rotation as the timing is
     from sbeacon.genome import prepare_shard_batch
-    sbat = prepare_shard_batch(store, sl)
-    st = sbat.stats()
-    sbat.free()
+    agg = dict(chains=0.0, cand_unique=0.0, cand_window=0.0, cand_loaded=0.0, hits=0.0, slices=0.0, uniq=0.0,
+               rows=0.0)
+    for b, n in zip(B, n_pass):
+        sl = shard_slices(shape, b['reqs'], world, rank)  # slice view (statistics / roofline pricing only)
+        sbat = prepare_shard_batch(store, sl)
+        st = sbat.stats()
+        sbat.free()
+        w = n / max(args.steps, 1)
+        agg['chains'] += w * float(b['pst']['chains'])
+        agg['cand_unique'] += w * st['cand_unique']
+        agg['cand_window'] += w * st['cand_window']
+        agg['cand_loaded'] += w * st['cand_loaded']
+        agg['hits'] += w * float(b['row_off'][-1].item())
+        agg['slices'] += w * len(sl)
+        agg['uniq'] += w * union_rows(shape, sl)
+        agg['rows'] += w * b['sr'].n_rows
+    st = {'cand_unique': agg['cand_unique'], 'cand_window': agg['cand_window'], 'cand_loaded': agg['cand_loaded']}
     # Roofline of the request pass, priced on the bytes it must move at least
     # once.  request_eval_kernel: per request its 32 B chain
     # descriptor (ReqChain), 40 B row and 8 B row count; 24 B per candidate in
@@ -132,22 +176,23 @@ def main_genome(args):
     # however many overlapping requests read it); 8 B per hit staged.  Beside
     # it the SURVEY §8d contract: 32 B x unique records in the slice windows +
     # 8 B / hit.
-    chains = int(pst['chains'])
-    comp = (32.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * nhits
+    chains, hits_avg = agg['chains'], agg['hits']
+    comp = (32.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * hits_avg
     achieved = comp / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
-    # the whole pass (eval + tile scan + delivery): + 8 B row offset per request
-    # and the hits' dense copy (8 B read + 8 B written per hit)
-    comp_pass = comp + 8.0 * chains + 16.0 * nhits
+    # the whole pass: the planning kernels (32 B packed request read, 32 B
+    # descriptor written per request), eval, tile scan, delivery (+ 8 B row
+    # offset per request and the hits' dense copy: 8 B read + 8 B written per hit)
+    comp_pass = comp + 64.0 * agg['rows'] + 8.0 * chains + 16.0 * hits_avg
     achieved_pass = comp_pass / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
-    uniq = union_rows(shape, sl)
-    contract = 32.0 * uniq + 8.0 * nhits
+    uniq = agg['uniq']
+    contract = 32.0 * uniq + 8.0 * hits_avg
     traffic = None  # HBM bytes per launch from the PMC passes (tools/gpu_r03_pmc.sh)
     tf = os.path.join(REPO, 'profiles', 'traffic_genome.json')
     if world == 1 and os.path.exists(tf):
         try:
             tj = json.load(open(tf))
             if tj.get('records') == shape.n_total and tj.get('requests') == len(reqs) and \
-                    tj.get('kernel') == 'request_eval_kernel':
+                    tj.get('kernel') == 'request_eval_kernel' and tj.get('batches') == args.batches:
                 traffic = tj.get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
@@ -174,7 +219,7 @@ def main_genome(args):
             'request_eval_kernel of a freshly prepared batch, HIP events: first and second launch after a 50 ms idle '
             'gap, and after ~8 fp32 GEMMs (a busy device); round 3 traced 0.76-0.81 ms launches in its serial '
             'delivered passes')
-    vals = [elapsed, kern_ms, float(len(sl)), float(st['cand_loaded']), float(nhits), achieved, float(uniq), comp,
+    vals = [elapsed, kern_ms, agg['slices'], float(st['cand_loaded']), hits_avg, achieved, float(uniq), comp,
             contract, step_dev_ms, pass_ms, achieved_pass, comp_pass]
     if dist:
         t = torch.tensor(vals, dtype=torch.float64, device=dev)
@@ -191,6 +236,15 @@ def main_genome(args):
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline_and_parity(args, shape, reqs, ex.exchange(part, hits, row_off).cpu().numpy(),
                                               hits.cpu().numpy(), row_off.cpu().numpy())
+        # the other batches of the rotation: a smaller sample each, parity only
+        parity['other_batches'] = []
+        for k, b in enumerate(B[1:], start=1):
+            _, pk = cpu_baseline_and_parity(args, shape, b['reqs'],
+                                            b['ex'].exchange(b['part'], b['hits'], b['row_off']).cpu().numpy(),
+                                            b['hits'].cpu().numpy(), b['row_off'].cpu().numpy(), n_sample=4000,
+                                            seed=7 + k, timed=False)
+            pk['batch'] = k
+            parity['other_batches'].append(pk)
     r0 = allv[0]
     out = {
         'metric': 'region queries/sec (Beacon g_variants variantType requests, whole-genome store sharded by contig)',
@@ -212,10 +266,13 @@ def main_genome(args):
                    'parallelism': f'contig shards x{world} (+10 kb halo); request rows + hit lists delivered to '
                                   f'the {"first slice" if args.deliver == "first" else "rank 0"} rank over '
                                   f'{"RCCL" if world > 1 else "(no peer)"}'},
-        'step': 'request batch pass (request_eval_kernel: every request = one chain of its 10 kb slices, rows + '
-                'hits staged per run; request_tile_scan_kernel + request_deliver_kernel: offsets from run totals scanned over tiles of runs, '
-                'dense hit lists in request order) + exchange (send/recv of straddling rows and hits); inputs '
-                'resident in HBM',
+        'step': f'one request batch of a rotation over {args.batches} independently drawn 1 M-request batches '
+                f'(step i answers batch i mod {args.batches}; packed requests resident in HBM): planning '
+                '(request_plan_kernel: each request\'s candidate range by a batched lower / upper bound of its '
+                'splitQuery window in the (segment, kind) index + its staging capacity; request_stage_scan_kernel), '
+                'request_eval_kernel (every request = one chain of its 10 kb slices, rows + hits staged per run), '
+                'request_tile_scan_kernel + request_deliver_kernel (row offsets, dense hit lists in request order), '
+                'then the exchange (send/recv of straddling rows and hits)',
         'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
         'candidates_loaded_per_s': round(tot_cand * args.steps / elapsed, 1),
         'hits_per_step': int(tot_hits),
@@ -225,16 +282,16 @@ def main_genome(args):
         'roofline': {'bound': 'hbm', 'achieved': round(r0[5], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(r0[5] / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'kernel': 'request_eval_kernel (rank 0, the dominant kernel of the pass): HIP events around '
-                               'its launch in each of K passes on its stream, averaged (rocprof per-kernel averages: '
-                               'profiles/)',
+                               'its launch in each of K rotating passes on its stream, averaged (rocprof per-kernel '
+                               'averages: profiles/)',
                      'algorithmic_bytes_per_launch': r0[7],
                      'pricing': 'bytes the launch must move at least once: 80 B/request (32 B chain descriptor + '
                                 '40 B row + 8 B row count) + 24 B per candidate in the union of the chain windows + '
                                 '8 B/hit staged',
                      'pass': {'ms': round(r0[10], 4), 'achieved': round(r0[11], 1),
                               'frac': round(r0[11] / HBM_PEAK_GBS, 4), 'bytes': r0[12],
-                              'note': 'eval + tile scan + delivery (row offsets, dense hit copy: +8 B/request, '
-                                      '+16 B/hit)'},
+                              'note': 'planning (+64 B/request: packed request read, descriptor written) + eval + '
+                                      'tile scan + delivery (row offsets, dense hit copy: +8 B/request, +16 B/hit)'},
                      'candidates': {'unique': int(st['cand_unique']), 'in_windows': int(st['cand_window']),
                                     'loaded': int(st['cand_loaded'])},
                      'contract_bytes_per_launch': r0[8],
@@ -247,6 +304,7 @@ def main_genome(args):
         'parity_sample': parity,
         'ingest_s': round(t_ingest, 2),
         'prepare_s': round(t_prepare, 3),
+        'batches': args.batches,
     }
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -476,7 +534,8 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
                     'timed region'}
 
 
-def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20000, seed=7):
+def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20000, seed=7, timed=True):
+    from bench import host_cores
     """C oracle (OpenMP) over a random sample of the requests, on a VCF that
     holds exactly the records those requests can reach; also checks the
     device's request rows and hit lists for the sample."""
@@ -512,7 +571,8 @@ def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20
     orc = OracleVcf(path, load_gt=False)
     whole = shard_slices(shape, sub, 1, 0)
     pl = slice_payloads(whole)
-    dt, passes = orc.time_batch(pl, patched=True, threads=args.threads, min_seconds=args.cpu_seconds)
+    if timed:
+        dt, passes = orc.time_batch(pl, patched=True, threads=args.threads, min_seconds=args.cpu_seconds)
     res = orc.perform_query_batch(pl, patched=True, threads=args.threads)
     exp = request_rows_from_responses(whole.req, res, whole.n_rows)
     got = total[pick]
@@ -539,7 +599,9 @@ def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20
             c, p, alts = alts_cache[(ci, i)]
             dv.append((c, p, alts[k]))
         bad_hits += int(dv != exp_v[j])
-    cpu = {'value': round(passes * len(pick) / dt, 1), 'unit': 'requests/s', 'cores': args.threads, 'kind': 'port',
+    cpu = None if not timed else {
+           'value': round(passes * len(pick) / dt, 1), 'unit': 'requests/s', 'cores': args.threads, 'kind': 'port',
+           'host': host_cores(),
            'sample': f'{len(pick)} random requests ({len(pl)} slice payloads) x {passes} passes through oracle/sbeacon_oracle.c '
                      f'(CPU restatement of search_variants.py, patched variantType branch), OpenMP x{args.threads}, '
                      f'on a sites-only VCF holding the records those requests reach',

@@ -45,12 +45,16 @@ def main():
     ap.add_argument('--records', type=int, default=1103547)
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--warmup', type=int, default=2)
-    ap.add_argument('--threads', type=int, default=16)
+    ap.add_argument('--threads', type=int, default=None,
+                    help='host threads (ingest, CPU baselines); default: every CPU the process may use')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--only', choices=['summarise', 'dedup'], default=None)
     ap.add_argument('--strict-datasets', type=int, default=10,
                     help='datasets whose messages also run in the reference-exact dedup mode (0: skip)')
     args = ap.parse_args()
+    from bench import host_cores
+    if args.threads is None:
+        args.threads = host_cores()['cores']
     import torch
     torch.cuda.set_device(0)
     from sbeacon.engine import Store
@@ -132,8 +136,10 @@ def summarise_line(args, store, files, plan_slices):
     achieved = alg / (dev_ms * 1e-3) / 1e9
     cpu = parity = None
     if not args.no_cpu_baseline:
-        cpu, parity = summarise_cpu(files[0], [s for s in slices if s[0] == files[0][0]],
-                                    [r for s, r in zip(slices, res) if s[0] == files[0][0]])
+        k = max(1, min(args.threads, len(files)))  # one VCF per host thread
+        cpu, parity = summarise_cpu(files[:k], [[s for s in slices if s[0] == f[0]] for f in files[:k]],
+                                    [[r for s, r in zip(slices, res) if s[0] == f[0]] for f in files[:k]],
+                                    args.threads)
     print(json.dumps({
         'metric': 'summariseSlice records/s (all slices of every VCF in one call)',
         'value': round(n_records / (wall * 1e-0), 1) if wall > 0 else None,
@@ -150,20 +156,32 @@ def summarise_line(args, store, files, plan_slices):
                      'algorithmic_bytes_per_launch': alg},
         'cpu_baseline': cpu, 'parity_sample': parity}), flush=True)
 
-def summarise_cpu(file, slices, got):
+def summarise_cpu(files, slices, got, threads):
+    """oracle/summarise_oracle.c over every slice of the first VCFs (one per
+    host thread), the slices spread over a pool of `threads` host threads
+    (ctypes drops the GIL in the C call); each VCF inflated in memory first
+    (inflate time excluded)."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    from bench import host_cores
     from oracle.oracle import OracleBgzf
-    o = OracleBgzf(file[1])
-    t = time.perf_counter()
-    exp = [o.summarise_slice(a, b) for _, a, b in slices]
-    dt = time.perf_counter() - t
+    orcs = [OracleBgzf(f[1]) for f in files]
+    work = [(o, a, b) for o, sl in zip(orcs, slices) for _, a, b in sl]
+    with ThreadPoolExecutor(threads) as ex:
+        t = time.perf_counter()
+        exp = list(ex.map(lambda w: w[0].summarise_slice(w[1], w[2]), work))
+        dt = time.perf_counter() - t
     recs = sum(e['records'] for e in exp)
-    bad = sum(int(g != e) for g, e in zip(got, exp))
-    o.close()
-    cpu = {'value': round(recs / dt, 1), 'unit': 'records/s', 'cores': 1, 'kind': 'port',
-           'sample': f'every slice of one VCF ({len(slices)} slices, {recs} records) through '
-                     'oracle/summarise_oracle.c (inflated stream in memory; inflate time excluded)',
+    flat = [g for gs in got for g in gs]
+    bad = sum(int(g != e) for g, e in zip(flat, exp))
+    for o in orcs:
+        o.close()
+    cpu = {'value': round(recs / dt, 1), 'unit': 'records/s', 'cores': threads, 'kind': 'port', 'host': host_cores(),
+           'sample': f'every slice of {len(files)} VCFs ({len(work)} slices, {recs} records) through '
+                     f'oracle/summarise_oracle.c on {threads} host threads (inflated streams in memory; inflate '
+                     'time excluded)',
            'seconds': round(dt, 3)}
-    return cpu, {'slices': len(slices), 'mismatches': bad}
+    return cpu, {'slices': len(work), 'mismatches': bad}
 
 
 def dedup_line(args, store, datasets, files):
@@ -203,16 +221,22 @@ def dedup_line(args, store, datasets, files):
     achieved = alg / (dev_ms * 1e-3) / 1e9
     cpu = parity = None
     if not args.no_cpu_baseline:
+        from concurrent.futures import ThreadPoolExecutor
+
+        from bench import host_cores
         from oracle.oracle import dedup_count
-        ds, parts = datasets[0]
-        text = b''.join(parts[0][1].chunks(sites_only=True))
-        t = time.perf_counter()
-        e = dedup_count([text, text], '22', 0, 2**32 - 1)
-        dt = time.perf_counter() - t
-        cpu = {'value': round(2 * args.records / dt, 1), 'unit': 'keys/s', 'cores': 1, 'kind': 'port',
-               'sample': f'dataset {ds}: its 2 VCFs ({2 * args.records} records) through orc_dedup_count '
-                         '(string keys, qsort + unique; text parse included)', 'seconds': round(dt, 3)}
-        parity = {'jobs': 1, 'mismatches': int(res[0] != e), 'unique': e}
+        k = max(1, min(args.threads, len(datasets)))  # one dataset job per host thread
+        texts = [b''.join(parts[0][1].chunks(sites_only=True, threads=args.threads)) for _, parts in datasets[:k]]
+        with ThreadPoolExecutor(args.threads) as ex:
+            t = time.perf_counter()
+            exp = list(ex.map(lambda x: dedup_count([x, x], '22', 0, 2**32 - 1), texts))
+            dt = time.perf_counter() - t
+        cpu = {'value': round(k * 2 * args.records / dt, 1), 'unit': 'keys/s', 'cores': args.threads, 'kind': 'port',
+               'host': host_cores(),
+               'sample': f'the first {k} datasets\' jobs (2 VCFs each, {2 * args.records} records per job) through '
+                         f'orc_dedup_count (string keys, qsort + unique; text parse included), one job per host '
+                         f'thread on {args.threads} threads', 'seconds': round(dt, 3)}
+        parity = {'jobs': k, 'mismatches': int(sum(r != e for r, e in zip(res[:k], exp))), 'unique_first': exp[0]}
     strict = strict_sample(args, store, datasets) if args.strict_datasets else None
     print(json.dumps({
         'metric': 'duplicateVariantSearch region keys/s (per-dataset unique counts, one batched call)',
@@ -235,7 +259,7 @@ def dedup_line(args, store, datasets, files):
 
 
 def strict_sample(args, store, datasets):
-    """The reference-exact duplicateVariantSearch (SBEACON_STRICT_DEDUP=1:
+    """The reference-exact duplicateVariantSearch (the default mode:
     every region file a message names read as ReadVcfData::getVcfData reads
     it, sb_dedup_count_files) beside the intended-range device path, over the
     same initDuplicateVariantSearch messages of the first datasets: the
@@ -255,15 +279,15 @@ def strict_sample(args, store, datasets):
         log(f'strict: dataset {ds} planned ({len(msgs)} messages, {len(refs)} region files)')
     out = {'datasets': min(args.strict_datasets, len(datasets)), 'messages': len(msgs),
            'region_files': len(refs)}
-    for mode, fr in (('strict', refs), ('intended', None)):
+    for mode, strict in (('strict', True), ('intended', False)):
         t = time.perf_counter()
-        dedup_batch(msgs, registry=reg, file_refs=fr)
+        dedup_batch(msgs, registry=reg, file_refs=refs, strict=strict)
         first = time.perf_counter() - t  # strict: writes (gzip level 9) and caches the slices' region files
         log(f'strict: {mode} first call {first * 1e3:.2f} ms')
         reps = 3
         t = time.perf_counter()
         for _ in range(reps):
-            res = dedup_batch(msgs, registry=reg, file_refs=fr)
+            res = dedup_batch(msgs, registry=reg, file_refs=refs, strict=strict)
         dt = (time.perf_counter() - t) / reps
         log(f'strict: {mode} {dt * 1e3:.2f} ms per call')
         out[mode] = {'ms_per_call': round(dt * 1e3, 2), 'first_call_ms': round(first * 1e3, 2),

@@ -521,6 +521,16 @@ int sb_requests_run(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_o
  * sync (total_ms stays the whole pass).  Off by default: the markers add
  * stream gaps. */
 int sb_requests_time_eval(sb_batch *b, int on);
+/* With on != 0 every pass of a device-planned batch (sb_requests_prepare_columns
+ * / _beacon when the columns qualify) first re-runs the planning kernels
+ * (request_plan_kernel: each chain's candidate range by a batched lower /
+ * upper bound in its (segment, kind) index and its staging capacity;
+ * request_stage_scan_kernel) from the packed requests the batch keeps in HBM
+ * -- the whole device path of a request batch in one pass, with the sizes
+ * the prepare already read back.  SB_EINVAL for a host-planned batch.
+ * Replaces splitQuery's per-request fan-out (lambda/splitQuery/
+ * lambda_function.py:74-110) as a device step. */
+int sb_requests_set_replan(sb_batch *b, int on);
 /* After a pass (waits for it): flags[w] = 1 when row w's call_count or
  * all_alleles_count is not exact in int64 -- a slice's count past 64 bits
  * (Python ints, records answered by the general path) or a sum that

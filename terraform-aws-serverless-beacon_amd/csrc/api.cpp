@@ -364,6 +364,12 @@ struct sb_batch {
         }
         // dchains: ReqChain slots (kReqRun per run), then the RowRuns at runs_at
         DevMem dchains, status, tstatus, stage, row_src, lut, sseg, sherr;
+        // device-planned batches: the packed requests (ReqIn) and the
+        // planner's per-run capacities + counters stay resident, so a pass can
+        // re-run the planning kernels first (sb_requests_set_replan)
+        DevMem din, rcap;
+        uint32_t n_in = 0;
+        bool replan = false;
         // rows whose counts are not exact in int64 (sb_requests_inexact_rows):
         // per-slice wide marks + one flag per row (batches with general records)
         DevMem wide, row_flag;
@@ -373,7 +379,8 @@ struct sb_batch {
         std::shared_ptr<ReqPool> pool;  // where the device buffers go back when the batch is freed
         bool slices = false;           // some rows answered per slice (the batch's query part)
         void give_back() {
-            for (DevMem *m : {&dchains, &status, &tstatus, &stage, &row_src, &lut, &sseg, &sherr, &wide, &row_flag})
+            for (DevMem *m : {&dchains, &status, &tstatus, &stage, &row_src, &lut, &sseg, &sherr, &wide, &row_flag, &din,
+                              &rcap})
                 if (m->p) pool->put_dev(std::move(*m));
         }
     };
@@ -3649,8 +3656,9 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     const uint64_t stage_total = hc[2];
     tick("plan");
     P.put_pinned(pin);
-    P.put_dev(std::move(din));
-    P.put_dev(std::move(rc));
+    R->din = std::move(din);  // kept: sb_requests_set_replan re-plans from them
+    R->rcap = std::move(rc);
+    R->n_in = static_cast<uint32_t>(n);
     R->cap = B.cap_total + stage_total;
     R->status = P.get_dev(size_t(n_runs) * 8);
     R->tstatus = P.get_dev(size_t(request_tiles(n_runs)) * 8);
@@ -3946,6 +3954,12 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
         launch_request_reduce(B.res.as<QRes>(), R.sseg.as<uint32_t>(), R.sherr.as<uint8_t>(), R.wide.as<uint8_t>(),
                               R.n_rows, static_cast<ReqPartial *>(rows), R.row_flag.as<uint8_t>(), st);
     }
+    if (R.replan) {  // the planning kernels again, from the resident packed requests (same descriptors, same sizes)
+        launch_request_plan(s.d, R.din.as<ReqIn>(), R.n_in, R.dchains.as<ReqChain>(),
+                            reinterpret_cast<RowRun *>(R.dchains.as<char>() + R.runs_at), R.rcap.as<unsigned long long>(),
+                            reinterpret_cast<unsigned long long *>(R.rcap.as<char>() + size_t(R.n_runs) * 8), st);
+        HIP_OK(hipGetLastError());
+    }
     DStore d = s.d;
     d.sym_lut = R.lut.as<uint32_t>();
     std::array<hipEvent_t, 2> ev{nullptr, nullptr};
@@ -4172,6 +4186,18 @@ int sb_requests_inexact_rows(sb_batch *b, uint8_t *flags) {
         HIP_OK(hipSetDevice(b->s->device));
         HIP_OK(hipStreamSynchronize(b->strm()));
         HIP_OK(hipMemcpy(flags, R.row_flag.p, R.n_rows, hipMemcpyDeviceToHost));
+    });
+}
+
+int sb_requests_set_replan(sb_batch *b, int on) {
+    return guard([&] {
+        if (!b || !b->req) throw Error(SB_EINVAL, "not a request batch");
+        if (on && !b->req->din.p)
+            throw Error(SB_EINVAL, "sb_requests_set_replan: the batch was planned on the host (no packed requests on "
+                                   "the device)");
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_set_replan between a run and its sync");
+        b->req->replan = on != 0;
     });
 }
 

@@ -242,6 +242,7 @@ SIGNATURES = {
     'sb_requests_prepare_columns': (C.c_int, [P, C.c_void_p, C.c_size_t, C.POINTER(P)]),
     'sb_requests_prepare_beacon': (C.c_int, [P, C.c_void_p, C.c_size_t, C.c_void_p, C.POINTER(P)]),
     'sb_requests_time_eval': (C.c_int, [P, C.c_int]),
+    'sb_requests_set_replan': (C.c_int, [P, C.c_int]),
     'sb_requests_inexact_rows': (C.c_int, [P, P]),
     'sb_store_trim': (C.c_int, [P]),
     'sb_store_save': (C.c_int, [P, C.c_char_p]),
@@ -283,3 +284,19 @@ def check(rc):
         msg = lib().sb_last_error()
         raise SbError(rc, msg.decode() if msg else '')
     return rc
+
+
+HIP_STREAM_LEGACY = 1  # hipStreamLegacy: the null stream, which torch's default stream is
+
+
+def stream_arg(stream_ptr):
+    """The ``void *stream`` of sb_batch_set_stream for a caller stream
+    handle: None -> NULL (the store's own stream); 0 -> hipStreamLegacy.
+
+    torch reports its default stream as ``cuda_stream == 0``.  Passed as
+    NULL, the batch would run on the store's non-blocking stream, unordered
+    with the caller's default-stream copies of its outputs (a D2H copy then
+    reads rows while request_eval_kernel is still writing them)."""
+    if stream_ptr is None:
+        return None
+    return C.c_void_p(int(stream_ptr) if int(stream_ptr) else HIP_STREAM_LEGACY)

@@ -3,13 +3,23 @@
 Mirrors lambda/duplicateVariantSearch/source/main.cpp:31-43 (the SNS message
 {"bucket", "rangeStart", "rangeEnd", "contig", "targetFilepaths", "dataset"})
 and duplicateVariantSearch.cpp:31-84 (unique region keys of the range, then
-the two DynamoDB updates).  The region files named in ``targetFilepaths``
-are not read: each names the VCF it summarises
-(``vcf-summaries/contig/{CHROM}/{bucket%key}/regions/...``,
-write_data_to_s3.h:39-101, summariseSlice main.cpp), and that VCF's region
-keys are already resident in the store, so the unique count is one device
-call (``sb_dedup_count``).  Many messages go to the device together through
-:func:`dedup_batch`.
+the two DynamoDB updates).  Each key in ``targetFilepaths`` names the VCF it
+summarises (``vcf-summaries/contig/{CHROM}/{bucket%key}/regions/...``,
+write_data_to_s3.h:39-101) and one region file of it; that VCF's region keys
+are already resident in the store, so the unique count is one device call.
+Many messages go to the device together through :func:`dedup_batch`.
+
+Default (the reference's answer): every target file is read as
+``ReadVcfData::getVcfData`` reads it (readVcfData.cpp:15-35 over the gzip
+reader of gzip.cpp:61-144: entries from the first POS >= rangeStart up to the
+first one past rangeEnd inside the reader's final refill, a throw when a
+skipped entry straddles its 1 KiB buffer), on the device
+(``sb_dedup_count_files``).  The key resolves to its file through the region
+files summariseSlice writes for the VCF's summariseVcf slices
+(:func:`region_file_refs`).  ``SBEACON_STRICT_DEDUP=0`` (or ``strict=False``)
+selects an extension instead: the distinct keys of the intended inclusive
+range ``[rangeStart, rangeEnd]`` (``sb_dedup_count``), with no dependence on
+how the region files were cut.
 
 The two DynamoDB tables the reference updates are modelled by
 :class:`DuplicateTally` (VARIANT_DUPLICATES_TABLE: per (contig, dataset) an
@@ -198,13 +208,42 @@ class DuplicateTally:
         self.dataset_counts[dataset] = self.dataset_counts.get(dataset, 0) + final_tally
 
 
-def dedup_batch(messages, *, tally: DuplicateTally | None = None, registry=None, file_refs=None):
+def strict_default() -> bool:
+    """The reference's file-reading semantics unless SBEACON_STRICT_DEDUP=0."""
+    return os.environ.get('SBEACON_STRICT_DEDUP', '1') != '0'
+
+
+def region_file_refs(store, location) -> dict:
+    """region-file key -> (location, virtual_start, virtual_end, file index)
+    for every region file summariseSlice writes for ``location``
+    (write_data_to_s3.h:39-101) over the slices summariseVcf plans for it
+    (summarise_vcf.plan_slices); built once per store and VCF.  Keys that
+    sbeacon.summarise.region_file_keys produced for other slices of the store
+    are in the same map (a later file with the same key replaces the earlier,
+    as an S3 PUT does)."""
+    refs = store.__dict__.setdefault('_region_refs', {})
+    planned = store.__dict__.setdefault('_region_refs_planned', set())
+    if location not in planned:
+        from .summarise import region_file_keys
+        from .summarise_vcf import plan_slices
+        region_file_keys(store, location, plan_slices(store, location))
+        planned.add(location)
+    return refs
+
+
+def dedup_batch(messages, *, tally: DuplicateTally | None = None, registry=None, file_refs=None, strict=None):
     """Answer many duplicateVariantSearch messages with one device call per
     store.  Returns the unique count per message (or the exception).
-    file_refs (region-file key -> (location, virtual_start, virtual_end, file
-    index), summarise.region_file_keys) selects the reference-exact mode: each
-    target file is read as ReadVcfData::getVcfData reads it
-    (sb_dedup_count_files) instead of counting the intended inclusive range."""
+
+    strict (default :func:`strict_default`): the reference's count -- each
+    target file read as ReadVcfData::getVcfData reads it
+    (sb_dedup_count_files); its key resolves through ``file_refs`` (key ->
+    (location, virtual_start, virtual_end, file index),
+    summarise.region_file_keys) or else the store's :func:`region_file_refs`;
+    a key naming no region file the store's summaries write is that
+    message's KeyError (the reference's S3 download would fail).  strict
+    False: the intended inclusive range (sb_dedup_count)."""
+    strict = strict_default() if strict is None else strict
     reg = registry or engine.registry
     known = reg.locations()
     jobs = [message_job(m, known) for m in messages]
@@ -221,13 +260,30 @@ def dedup_batch(messages, *, tally: DuplicateTally | None = None, registry=None,
             for i in idx:
                 out[i] = 0
             continue
-        if file_refs is not None:
-            res = st.dedup_counts_files([([file_refs[p] for p in messages[i]['targetFilepaths']], jobs[i][2],
-                                          jobs[i][3]) for i in idx])
-        else:
+        if not strict:
             res = st.dedup_counts([jobs[i] for i in idx])
-        for i, r in zip(idx, res):
-            out[i] = r
+            for i, r in zip(idx, res):
+                out[i] = r
+            continue
+        calls, call_idx = [], []
+        for i in idx:
+            refs = []
+            try:
+                for p in messages[i]['targetFilepaths']:
+                    fr = file_refs.get(p) if file_refs is not None else None
+                    if fr is None:
+                        fr = region_file_refs(st, _location_of(p, jobs[i][0])).get(p)
+                    if fr is None:
+                        raise KeyError(f'no region file {p!r} in the summaries of the store')
+                    refs.append(fr)
+            except KeyError as e:
+                out[i] = e
+                continue
+            calls.append((refs, jobs[i][2], jobs[i][3]))
+            call_idx.append(i)
+        if calls:
+            for i, r in zip(call_idx, st.dedup_counts_files(calls)):
+                out[i] = r
     if tally is not None:
         for m, (locs, contig, rs, re_), r in zip(messages, jobs, out):
             if isinstance(r, Exception):
@@ -238,12 +294,23 @@ def dedup_batch(messages, *, tally: DuplicateTally | None = None, registry=None,
     return out
 
 
-def lambda_handler(event, context=None, *, tally: DuplicateTally | None = None):
+def _location_of(path, locations):
+    k = region_path_bucket_key(path)
+    for l in locations:
+        if bucket_key(l) == k:
+            return l
+    raise KeyError(path)
+
+
+def lambda_handler(event, context=None, *, tally: DuplicateTally | None = None, strict=None):
     """SNS event -> the reference's bundleResponse("Success", 200)
-    (duplicateVariantSearch/source/main.cpp:11-47)."""
+    (duplicateVariantSearch/source/main.cpp:11-47); the count the reference
+    adds to its tables rides along as ``uniqueVariants``.  A reader throw
+    (gzip.cpp:97 "proccesData input invalid") is raised, as the Lambda
+    fails."""
     rec = event['Records'][0]['Sns']['Message'] if 'Records' in event else event
     msg = json.loads(rec) if isinstance(rec, str) else rec
-    r = dedup_batch([msg], tally=tally)[0]
+    r = dedup_batch([msg], tally=tally, strict=strict)[0]
     if isinstance(r, Exception):
         raise r
     return {'headers': {'Access-Control-Allow-Origin': '*'}, 'statusCode': 200, 'body': 'Success',

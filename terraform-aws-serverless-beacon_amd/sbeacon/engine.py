@@ -503,7 +503,7 @@ class Batch:
     def set_stream(self, stream_ptr):
         """Run this batch's work on a caller stream (e.g.
         ``torch.cuda.current_stream().cuda_stream``); None = the store's."""
-        check(lib().sb_batch_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+        check(lib().sb_batch_set_stream(self._h, _lib.stream_arg(stream_ptr)))
 
     def deliver(self, rows_ptr, hits_ptr, row_off_ptr, rec_base=0):
         """reduce_requests(rows_ptr) + compact_hits(hits_ptr, row_off_ptr,

@@ -35,9 +35,14 @@ class StoreSet:
             if os.path.exists(os.path.join(d, 'manifest.json')):
                 try:
                     st = Store.open(d, device=device)
-                    if sorted(st.locations) != sorted(loc for loc, _ in sources):
+                    want = {loc: os.path.abspath(os.fspath(p)) for loc, p in sources}
+                    have = {loc: os.path.abspath(os.fspath(p)) for loc, p in st.paths.items()}
+                    if sorted(st.locations) != sorted(want) or have != want:
+                        # the group's membership changed, or a location now
+                        # names another file (the saved fingerprints are of
+                        # the old files, which may well be unchanged)
                         st.close()
-                        st = None  # the group's membership changed
+                        st = None
                     else:
                         self.opened.append(name)
                 except StaleStore:

@@ -325,6 +325,12 @@ class RequestBatch:
         timing()['scan_ms'] then reports that kernel alone."""
         check(lib().sb_requests_time_eval(self._h, 1 if on else 0))
 
+    def set_replan(self, on: bool):
+        """Every pass first re-runs the device planning kernels from the
+        packed requests kept in HBM (sb_requests_set_replan; device-planned
+        batches only)."""
+        check(lib().sb_requests_set_replan(self._h, 1 if on else 0))
+
     def inexact_rows(self) -> np.ndarray:
         """After a pass: True for rows whose call_count / all_alleles_count
         are not exact in int64 (low 64 bits held; sb_requests_inexact_rows)."""
@@ -338,7 +344,7 @@ class RequestBatch:
         return {f: getattr(st, f) for f, _ in _lib.BatchStats._fields_}
 
     def set_stream(self, stream_ptr):
-        check(lib().sb_batch_set_stream(self._h, C.c_void_p(stream_ptr) if stream_ptr else None))
+        check(lib().sb_batch_set_stream(self._h, _lib.stream_arg(stream_ptr)))
 
     def free(self):
         if self._h:

@@ -14,7 +14,6 @@ call (``summarise_batch``) — the analogue of summariseVcf's SNS fan-out
 from __future__ import annotations
 
 import json
-import os
 
 from .engine import registry
 
@@ -53,12 +52,14 @@ def lambda_handler(event, context=None):
 def region_file_keys(store, location, slices, refs=None):
     """The S3 keys summariseSlice writes for these slices of one VCF
     (write_data_to_s3.h:93-101: vcf-summaries/contig/{CHROM}/{bucket%key}/
-    regions/{first}-{last}-{bytes}), in slice then file order.  ``refs``
-    (optional dict) receives key -> (location, virtual_start, virtual_end,
-    file index): the file a strict duplicateVariantSearch reads (a later
-    file with the same key replaces it, as an S3 PUT does)."""
+    regions/{first}-{last}-{bytes}), in slice then file order.  Each key's
+    file -- (location, virtual_start, virtual_end, file index), what a
+    duplicateVariantSearch of the key reads -- goes into the store's region
+    file map (sbeacon.dedup.region_file_refs; a later file with the same key
+    replaces it, as an S3 PUT does) and into ``refs`` when given."""
     from .dedup import bucket_key
     bk = bucket_key(location)
+    known = store.__dict__.setdefault('_region_refs', {})
     keys = []
     for sl, files in zip(slices, store.region_files([(location, a, b) for a, b in slices])):
         if isinstance(files, Exception):
@@ -66,16 +67,18 @@ def region_file_keys(store, location, slices, refs=None):
         for i, f in enumerate(files):
             k = f"vcf-summaries/contig/{f['contig']}/{bk}/regions/{f['first_pos']}-{f['last_pos']}-{f['bytes']}"
             keys.append(k)
+            known[k] = (location, sl[0], sl[1], i)
             if refs is not None:
-                refs[k] = (location, sl[0], sl[1], i)
+                refs[k] = known[k]
     return keys
 
 
 def strict_dedup_default() -> bool:
-    """SBEACON_STRICT_DEDUP=1: duplicateVariantSearch reads the region files
-    exactly as the reference does (sb_dedup_count_files) instead of counting
-    the intended inclusive range (sb_dedup_count)."""
-    return os.environ.get('SBEACON_STRICT_DEDUP', '0') == '1'
+    """duplicateVariantSearch reads the region files exactly as the
+    reference does (sb_dedup_count_files) unless SBEACON_STRICT_DEDUP=0,
+    which counts the intended inclusive range instead (sb_dedup_count)."""
+    from .dedup import strict_default
+    return strict_default()
 
 
 def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None, strict=None, vcf_groups=None):
@@ -88,8 +91,8 @@ def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None, st
     variantCount / callCount from the summaries (summariseDataset
     lambda_function.py:102-125) and uniqueVariants = the sum of the ranges'
     distinct counts (the DATASETS_TABLE variantCount duplicateVariantSearch
-    leaves, duplicateVariantSearch.cpp:76-84).  strict (default
-    SBEACON_STRICT_DEDUP): the reference's file-reading semantics.
+    leaves, duplicateVariantSearch.cpp:76-84).  strict (default: unless
+    SBEACON_STRICT_DEDUP=0): the reference's file-reading semantics.
     sampleCount is counted once per VCF group (summariseDataset
     lambda_function.py:118-124; vcf_groups defaults to one group of all the
     locations, submitDataset lambda_function.py:93)."""
@@ -112,7 +115,7 @@ def summarise_dataset(store, dataset, locations, *, tally=None, abs_max=None, st
         keys += region_file_keys(store, loc, slices, refs)
     messages = init_duplicate_variant_search(dataset, locations, keys, tally=tally, abs_max=abs_max)
     per_range = dedup_batch(messages, tally=tally, registry=_single_store_registry(store),
-                            file_refs=refs if strict else None) if messages else []
+                            file_refs=refs, strict=strict) if messages else []
     for r in per_range:
         if isinstance(r, Exception):
             raise r

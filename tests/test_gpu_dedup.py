@@ -190,9 +190,11 @@ def test_handler_with_region_paths(texts):
         assert paths[0] == 'vcf-summaries/contig/22/bkt%dir%dd0/regions/1-2999'
         msgs = [{'bucket': 'b', 'rangeStart': a, 'rangeEnd': b, 'contig': '22', 'targetFilepaths': paths,
                  'dataset': 'ds'} for a, b in [(0, 1499), (1500, 10**9)]]
-        r0 = dedup.lambda_handler({'Records': [{'Sns': {'Message': json.dumps(msgs[0])}}]}, tally=tally)
+        # these keys name no real region file: the intended-range extension
+        r0 = dedup.lambda_handler({'Records': [{'Sns': {'Message': json.dumps(msgs[0])}}]}, tally=tally,
+                                  strict=False)
         assert r0['statusCode'] == 200
-        r1 = dedup.dedup_batch([msgs[1]], tally=tally)
+        r1 = dedup.dedup_batch([msgs[1]], tally=tally, strict=False)
         names = ['dd0.vcf.gz', 'dd1.vcf.gz']
         assert r0['uniqueVariants'] == oracle(texts, names, '22', 0, 1499)
         assert r1[0] == oracle(texts, names, '22', 1500, 10**9)

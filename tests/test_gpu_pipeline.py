@@ -30,7 +30,8 @@ def test_summarise_dataset_pipeline(tmp_path):
     for ds, parts in datasets:
         locs = [loc for loc, _ in parts]
         # a small abs_max so the contig is cut into several ranges
-        counts, messages, per_range = summarise_dataset(store, ds, locs, abs_max=20_000)
+        # the intended-range extension (strict=False) against the intended-range oracle
+        counts, messages, per_range = summarise_dataset(store, ds, locs, abs_max=20_000, strict=False)
         assert len(messages) > 3
         exp_v = exp_c = 0
         for loc in locs:
@@ -115,3 +116,75 @@ def test_region_files_gzip_and_strict_dedup(tmp_path, monkeypatch):
             assert n_throw == 0
             counts, _, pr = summarise_dataset(store, 'dsS', locs, abs_max=abs_max, strict=True)
             assert counts['uniqueVariants'] == sum(pr) == sum(per_range)
+
+
+def test_sns_handler_answers_the_reference_count(tmp_path):
+    """The drop-in duplicateVariantSearch handler, default mode: the
+    messages initDuplicateVariantSearch fans out, each delivered as an SNS
+    event to dedup.lambda_handler with nothing but its keys -- each count
+    equals |union of the REFERENCE reader's key sets| over the target files
+    (oracle/_ref: ReadVcfData::getVcfData's loop over gzip.cpp), and a
+    reference throw is the handler's exception."""
+    import json
+    from oracle import ref
+    if ref.lib() is None:
+        pytest.skip('oracle/_ref missing')
+    from sbeacon import dedup, engine
+    from sbeacon.engine import Store
+    from sbeacon.summarise import region_file_keys
+    from sbeacon.summarise_vcf import plan_slices
+    from sbeacon.workload import SyntheticVcf, write_bgzf
+    pool = SyntheticVcf(seed=18, n_records=5000, n_samples=4, mean_gap=20000)
+    parts = [(f's3://bkt/dsH/p{k}.vcf.gz', pool.member(900 + k, share=0.6)) for k in (0, 1, 2)]
+    paths = []
+    for loc, gen in parts:
+        path = str(tmp_path / (loc.replace('/', '_') + '.gz'))
+        write_bgzf(path, gen.chunks(threads=4), threads=4)
+        paths.append((loc, path))
+    locs = [l for l, _ in paths]
+    store = Store.build(paths, device=0)
+    gz_files, refs, keys = {}, {}, []
+    for loc in locs:
+        slices = plan_slices(store, loc)
+        keys += region_file_keys(store, loc, slices, refs)
+        gz = store.region_files([(loc, a, b) for a, b in slices], with_data='gzip')
+        for (a, b), fg in zip(slices, gz):
+            for i, y in enumerate(fg):
+                gz_files[(loc, a, b, i)] = y['data']
+    # a fresh store: the handler resolves every key through its own map
+    store2 = Store.build(paths, device=0)
+    engine.registry.register(store2)
+    try:
+        n_ok = n_throw = 0
+        for abs_max in (8_000, 10**9):
+            tally = dedup.DuplicateTally()
+            messages = dedup.init_duplicate_variant_search('dsH', locs, keys, abs_max=abs_max, tally=tally)
+            assert messages
+            for m in messages:
+                exp = set()
+                for p in m['targetFilepaths']:
+                    kf = ref.region_keys(gz_files[refs[p]], m['rangeStart'], m['rangeEnd'])
+                    if isinstance(kf, Exception):
+                        exp = kf
+                        break
+                    exp |= set(kf)
+                ev = {'Records': [{'Sns': {'Message': json.dumps(m)}}]}
+                if isinstance(exp, Exception):
+                    n_throw += 1
+                    with pytest.raises(RuntimeError):
+                        dedup.lambda_handler(ev, tally=tally)
+                else:
+                    n_ok += 1
+                    r = dedup.lambda_handler(ev, tally=tally)
+                    assert r['statusCode'] == 200 and r['body'] == 'Success'
+                    assert r['uniqueVariants'] == len(exp), m
+            # the intended-range extension stays available on request
+            alt = dedup.dedup_batch(messages, strict=False)
+            assert all(isinstance(x, int) for x in alt)
+        assert n_ok > 5
+        # a key no summary of the store writes: the message fails (the S3 download would)
+        bad = dict(messages[0], targetFilepaths=[messages[0]['targetFilepaths'][0].rsplit('/', 1)[0] + '/1-2-3'])
+        with pytest.raises(KeyError):
+            dedup.lambda_handler({'Records': [{'Sns': {'Message': json.dumps(bad)}}]})
+    finally:
+        engine.registry.clear()

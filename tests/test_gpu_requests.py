@@ -349,4 +349,15 @@ def test_device_planned_requests_match_host_planned():
     # their candidates run past the chain-start bitmap's 4 k positions
     runs = np.add.reduceat(rows_d[:, 1], np.arange(0, len(rows_d), 64))
     assert runs[:3].min() > 4096, runs[:3]
+    # every pass re-planned on the device (the bench step): the same answers
+    # pass after pass
+    from sbeacon import _lib
+    dev_b.set_replan(True)
+    for _ in range(2):
+        rows_r, hits_r, ro_r = dev_b.answer()
+        np.testing.assert_array_equal(rows_r, rows_h)
+        np.testing.assert_array_equal(ro_r, ro_h)
+        np.testing.assert_array_equal(hits_r, hits_h)
+    with pytest.raises(_lib.SbError):
+        host_b.set_replan(True)  # planned on the host: nothing to re-plan from
     del keep, dev_b, host_b

@@ -85,3 +85,23 @@ def test_store_set_rebuilds_only_changed_groups(tmp_path):
         f.write(text.replace(b'AN=', b'AM=', 1))
     ss.load(groups, device=HOST_ONLY)
     assert ss.rebuilt == ['ds_b'] and ss.opened == ['ds_a']
+
+
+def test_store_set_rebuilds_a_repointed_location(tmp_path):
+    """A location re-pointed to another file (the old one unchanged, so its
+    saved fingerprint still matches) is a rebuild, not a re-open of the old
+    file's data."""
+    from sbeacon.persist import StoreSet
+    a = _copy(tmp_path, 'tiny22.vcf')
+    other = str(tmp_path / 'tiny22_v2.vcf')
+    text = open(a, 'rb').read()
+    with open(other, 'wb') as f:
+        f.write(text.replace(b'AN=', b'AM=', 1))
+    ss = StoreSet(str(tmp_path / 'stores'))
+    ss.load({'ds': [('tiny22.vcf', a)]}, device=HOST_ONLY)
+    assert ss.rebuilt == ['ds']
+    ss.load({'ds': [('tiny22.vcf', other)]}, device=HOST_ONLY)
+    assert ss.rebuilt == ['ds'] and ss.opened == []
+    assert ss.stores['ds'].paths['tiny22.vcf'] == other
+    ss.load({'ds': [('tiny22.vcf', other)]}, device=HOST_ONLY)
+    assert ss.rebuilt == [] and ss.opened == ['ds']
