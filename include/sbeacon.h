@@ -41,6 +41,7 @@ enum {
     SB_EPARSE = -5,     /* VCF text the store cannot represent exactly */
     SB_ENOMEM = -6,
     SB_ESTALE = -7,     /* a persisted store's source VCF changed since it was saved */
+    SB_EINTERNAL = -8,  /* a device pass failed its own consistency checks (a bug, never a wrong answer) */
 };
 
 /* per-query error: the Python exception the reference raises on this input

@@ -370,6 +370,9 @@ struct sb_batch {
         DevMem din, rcap;
         uint32_t n_in = 0;
         bool replan = false;
+        // request_eval_kernel's invariant word (sticky; checked at sync: SB_EINTERNAL)
+        DevMem err;
+        ReqPool::Pinned err_h;
         // rows whose counts are not exact in int64 (sb_requests_inexact_rows):
         // per-slice wide marks + one flag per row (batches with general records)
         DevMem wide, row_flag;
@@ -380,8 +383,12 @@ struct sb_batch {
         bool slices = false;           // some rows answered per slice (the batch's query part)
         void give_back() {
             for (DevMem *m : {&dchains, &status, &tstatus, &stage, &row_src, &lut, &sseg, &sherr, &wide, &row_flag, &din,
-                              &rcap})
+                              &rcap, &err})
                 if (m->p) pool->put_dev(std::move(*m));
+            if (err_h.p) {
+                pool->put_pinned(err_h);
+                err_h = ReqPool::Pinned{};
+            }
         }
     };
     std::unique_ptr<Req> req;
@@ -736,6 +743,12 @@ void upload_store(sb_builder &b, sb_store &s) {
         // kind) pair, aiming at ~2 candidates per bucket (chain_pack_kernel)
         std::vector<uint32_t> cpos(cw.size() + 1, 0u);
         for (size_t j = 0; j < ci.size(); ++j) cpos[j] = pos[ci[j]];
+        {  // request_eval_kernel's 16-byte candidate words; staged hits carry the candidate index
+            if (cw.size() > kStageCandMask) throw Error(SB_EINVAL, "variantType candidate index exceeds 2^29 entries");
+            std::vector<VcQ> cq(std::max<size_t>(cw.size(), 1), VcQ{0, 0, VT_SLOW, 0});
+            for (size_t j = 0; j < cw.size(); ++j) cq[j] = VcQ{cpos[j], cw[j].end, cw[j].w, cw[j].ac0};
+            s.d.vc_q = dev_upload(s, cq);
+        }
         // ALTs of the candidates, as a prefix (a chain's hit capacity: every
         // ALT of every candidate its coarse-index range can load)
         s.h_vc_altpre.assign(ci.size() + 1, 0);
@@ -758,6 +771,21 @@ void upload_store(sb_builder &b, sb_store &s) {
                     VcIndex &x = v.vc_index[g][k];
                     x.c_lo = cand_before(k, sg.lo);
                     x.c_hi = cand_before(k, sg.hi);
+                    {  // kVcNarrow / common AN of the pair's (non-VT_SLOW) candidates
+                        bool narrow = true, common = true;
+                        int32_t an0 = -1;
+                        for (uint32_t j = x.c_lo; j < x.c_hi && narrow; ++j) {
+                            const VtHot &h = cw[j];
+                            if (h.w & VT_SLOW) continue;
+                            int64_t sac = h.ac0 < 0 ? -int64_t(h.ac0) : h.ac0;
+                            for (uint32_t e = x_lo[ci[j]]; e < x_lo[ci[j] + 1]; ++e)
+                                sac += x_ac[e] < 0 ? -int64_t(x_ac[e]) : x_ac[e];
+                            narrow = h.an >= 0 && h.an < (1 << 25) && sac < (1 << 25);
+                            if (an0 < 0) an0 = h.an;
+                            common = common && h.an == an0;
+                        }
+                        x.xinfo = narrow ? kVcNarrow | (common && an0 >= 0 ? static_cast<uint32_t>(an0) + 1u : 0u) : 0u;
+                    }
                     x.off = vcb.size();
                     const uint32_t nc = x.c_hi - x.c_lo;
                     if (nc == 0) {
@@ -1740,6 +1768,8 @@ void run_kernels(sb_batch &B) {
 void sync(sb_batch &B) {
     HIP_OK(hipSetDevice(B.s->device));
     if (B.runs_pending) HIP_OK(hipEventRecord(B.ev[1], B.strm()));
+    const bool chk = B.req && B.req->err.p && B.req->err_h.p;
+    if (chk) HIP_OK(hipMemcpyAsync(B.req->err_h.p, B.req->err.p, 4, hipMemcpyDeviceToHost, B.strm()));
     HIP_OK(hipStreamSynchronize(B.strm()));
     if (B.runs_pending) {  // device time per run = the span / runs (back-to-back launches)
         float x;
@@ -1757,6 +1787,9 @@ void sync(sb_batch &B) {
         B.req->last_eval_ms = sum / static_cast<double>(B.req->eval_used);
         B.req->eval_used = 0;
     }
+    if (chk && *static_cast<volatile uint32_t *>(B.req->err_h.p))
+        throw Error(SB_EINTERNAL, "request_eval_kernel: the per-chain sums of a pass failed their invariants "
+                                  "(chain counts vs the wave's staged hits / exists-slices)");
 }
 
 // each query's hit-region offset: chained slices' hits are dense per chain,
@@ -3634,11 +3667,12 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     hipStream_t st = planning_stream(s.device);
     const uint32_t n_runs = static_cast<uint32_t>((n + kRunRows - 1) / kRunRows);
     const size_t chain_bytes = size_t(n_runs) * kReqRun * sizeof(ReqChain), run_bytes = size_t(n_runs) * sizeof(RowRun);
-    DevMem din = P.get_dev(n * sizeof(ReqIn)), rc = P.get_dev(size_t(n_runs) * 8 + 32);
+    // rc: per run {capacity, slices << 32 | chains} (request_plan_kernel), then the 3 counters
+    DevMem din = P.get_dev(n * sizeof(ReqIn)), rc = P.get_dev(size_t(n_runs) * 16 + 32);
     R->dchains = P.get_dev(chain_bytes + run_bytes);
     R->runs_at = chain_bytes;
     R->n_runs = n_runs;
-    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(rc.as<char>() + size_t(n_runs) * 8);
+    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(rc.as<char>() + size_t(n_runs) * 16);
     R->lut = P.get_dev(lut_all.size() * 4);
     R->n_lut = static_cast<uint32_t>(lut_all.size());
     HIP_OK(hipMemcpyAsync(din.p, pk, n * sizeof(ReqIn), hipMemcpyHostToDevice, st));
@@ -3662,7 +3696,7 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     R->cap = B.cap_total + stage_total;
     R->status = P.get_dev(size_t(n_runs) * 8);
     R->tstatus = P.get_dev(size_t(request_tiles(n_runs)) * 8);
-    R->stage = P.get_dev(stage_total * 8);
+    R->stage = P.get_dev(stage_total * 4);
     R->row_src = P.get_dev(R->slices ? n * 8 : 0);
     upload_slice_part(B, *R, seg, n, st);  // (synchronises when there is a per-slice part)
     tick("upload");
@@ -3918,7 +3952,7 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     R->dchains = P.get_dev(chain_bytes + run_bytes);
     R->status = P.get_dev(n_runs * 8);
     R->tstatus = P.get_dev(size_t(request_tiles(static_cast<uint32_t>(n_runs))) * 8);
-    R->stage = P.get_dev(stage_total * 8);
+    R->stage = P.get_dev(stage_total * 4);
     R->row_src = P.get_dev(R->slices || std::any_of(R->runs.begin(), R->runs.end(),
                                                     [](const RowRun &r) { return !(r.flags & kRunSimple); })
                                ? size_t(n) * 8 : 0);
@@ -3954,10 +3988,15 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
         launch_request_reduce(B.res.as<QRes>(), R.sseg.as<uint32_t>(), R.sherr.as<uint8_t>(), R.wide.as<uint8_t>(),
                               R.n_rows, static_cast<ReqPartial *>(rows), R.row_flag.as<uint8_t>(), st);
     }
+    if (!R.err.p) {
+        R.err = R.pool->get_dev(16);
+        R.err_h = R.pool->get_pinned(16);
+        HIP_OK(hipMemsetAsync(R.err.p, 0, 16, st));
+    }
     if (R.replan) {  // the planning kernels again, from the resident packed requests (same descriptors, same sizes)
         launch_request_plan(s.d, R.din.as<ReqIn>(), R.n_in, R.dchains.as<ReqChain>(),
                             reinterpret_cast<RowRun *>(R.dchains.as<char>() + R.runs_at), R.rcap.as<unsigned long long>(),
-                            reinterpret_cast<unsigned long long *>(R.rcap.as<char>() + size_t(R.n_runs) * 8), st);
+                            reinterpret_cast<unsigned long long *>(R.rcap.as<char>() + size_t(R.n_runs) * 16), st);
         HIP_OK(hipGetLastError());
     }
     DStore d = s.d;
@@ -3977,8 +4016,8 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
                         R.slices ? B.res.as<QRes>() : nullptr,
                         R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
                         static_cast<ReqPartial *>(rows), static_cast<uint64_t *>(row_off), R.row_src.as<uint64_t>(),
-                        R.stage.as<uint64_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
-                        st, ev[0], ev[1]);
+                        R.stage.as<uint32_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
+                        R.err.as<unsigned int>(), st, ev[0], ev[1]);
     HIP_OK(hipGetLastError());
 }
 

@@ -193,11 +193,31 @@ constexpr uint32_t kChainMax = 32;
 // coarse POS index of the variantType candidates of one (segment, kind):
 // vc_bucket[off + b] = first candidate with POS >= base + (b << shift), b <= n
 // (host planning, and DStore::vcx for request planning on the device)
+// The request path's copy of a candidate (request_eval_kernel reads one
+// 16-byte word per candidate): POS, END, the VtHot word and ALT0's AC.  The
+// record index (vc_idx) is read only for staged hits (request_deliver_kernel)
+// and extra-ALT lookups, AN (vc_word) only by runs without a common AN.
+struct alignas(16) VcQ {
+    uint32_t pos, end, w;
+    int32_t ac0;
+};
+// a staged request hit: candidate index | ALT label << kStageAltShift (labels <= VT_MAX_NX)
+constexpr uint32_t kStageAltShift = 29;
+constexpr uint32_t kStageCandMask = (1u << kStageAltShift) - 1u;
 struct VcIndex {
     uint64_t off = 0;
     uint32_t base = 0, shift = 31, n = 1;
     uint32_t c_lo = 0, c_hi = 0;  // the pair's candidates in the kind's list
+    // what request_eval_kernel may assume of the pair's candidates (VT_SLOW
+    // ones aside: a chain that reaches one is answered per slice):
+    // kVcNarrow = every record's AN and sum of |AC| over its ALTs in [0, 2^25)
+    // (a chunk's sums fit 32 bits); below it AN + 1 when they all share one
+    // AN (then a chain's AN sum is its hit records times that AN), else 0
+    uint32_t xinfo = 0;
 };
+static_assert(sizeof(VcIndex) == 32, "VcIndex is two 16-byte words");
+constexpr uint32_t kVcNarrow = 1u << 31;
+constexpr uint32_t kVcAnMask = (1u << 26) - 1u;
 // first candidate of the pair with POS >= x (up = 0), or the end of the
 // bucket holding x - 1 (up = 1: a bound >= the exact upper bound of x - 1)
 __host__ __device__ inline uint32_t vc_bound(const VcIndex &vi, const uint32_t *bucket, uint64_t x, uint32_t up) {
@@ -234,12 +254,15 @@ constexpr uint32_t kChainEndVoid = 1u << 8;  // no END can match
 // gathered there too).
 constexpr uint32_t kRunRows = 64;     // rows per run at most (one lane each)
 constexpr uint32_t kRunSimple = 1u;   // RowRun::flags: no row of the run is answered per slice
+constexpr uint32_t kRunNarrow = 2u;   // every chain's (segment, kind) pair is kVcNarrow
+constexpr uint32_t kRunAnCommon = 4u; // ... and they share one AN: flags >> kRunAnShift
+constexpr uint32_t kRunAnShift = 6u;
 struct alignas(16) RowRun {
     uint32_t row_lo, row_hi;  // rows [row_lo, row_hi)
     uint32_t c_lo, c_hi;      // the run's chains, rows increasing
     uint64_t stage;           // first staging slot of the run (its chains' hit capacity follows)
     uint32_t n_slots;         // slices of its chains
-    uint32_t flags;           // kRunSimple
+    uint32_t flags;           // kRunSimple | kRunNarrow | kRunAnCommon | common AN << kRunAnShift
 };
 static_assert(sizeof(RowRun) == 32, "RowRun is two 16-byte words");
 
@@ -366,6 +389,7 @@ struct DStore {
     const VcBlock *vc_blk;    // [kVtKinds][vc_nblk]
     uint64_t vc_nblk;
     const uint32_t *vc_pos;   // POS of each candidate (parallel to vc_word)
+    const VcQ *vc_q;          // request_eval_kernel's copy of each candidate (parallel to vc_word)
     const uint32_t *vc_bucket;  // coarse POS index per (kind, segment) over candidates (ChainDev)
     const VcIndex *vcx;         // [segment (store-wide) * kVtKinds + kind]: the pair's coarse index
     const uint64_t *vc_altpre;  // ALTs of candidates [0, j) (a chain's hit capacity)

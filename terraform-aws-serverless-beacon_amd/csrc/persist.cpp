@@ -49,7 +49,7 @@
 namespace sb {
 
 constexpr uint64_t kMagic = 0x3150544f5453424full;  // "OBSTOTP1"
-constexpr uint32_t kFormat = 2;  // 2: dedup class words carry tail ids
+constexpr uint32_t kFormat = 3;  // 2: dedup class words carry tail ids; 3: VcIndex::xinfo
 
 // FNV-1a over the first and last 64 KiB (with the size and mtime, a change
 // detector -- not a content address)

@@ -18,6 +18,7 @@
 // nothing here is a dense contraction, so no MFMA: the bound is memory
 // bandwidth on the RecHot stream.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include <cstdlib>
 #include <stdexcept>
@@ -1937,7 +1938,13 @@ __global__ __launch_bounds__(kBlock) void chain_src_kernel(const ChainDev *__res
 // then an LDS read, not a dependent global load behind the candidate's load
 constexpr uint32_t kReqLut = 512;
 constexpr uint32_t kDeliverTile = 16;  // runs per request_deliver_kernel wave
-constexpr int kReqPipe = 2;            // candidate chunks in flight per wave
+#ifndef SBEACON_REQ_PIPE
+#define SBEACON_REQ_PIPE 2
+#endif
+#ifndef SBEACON_REQ_WAVES
+#define SBEACON_REQ_WAVES 8
+#endif
+constexpr int kReqPipe = SBEACON_REQ_PIPE;  // candidate chunks in flight per wave
 
 // DPP lane moves (GFX9 controls; lanes without a source read 0)
 template <int CTRL, int ROW = 0xf, int BANK = 0xf>
@@ -1993,18 +2000,18 @@ struct ReqLds {
 };
 
 struct ReqChunk {
-    ChainChunk x;
+    VcQ q;       // the candidate's POS, END, VtHot word and ALT0 AC: one 16-byte load
+    int32_t an;  // its record's AN (loaded only by runs without a common AN)
+    uint32_t i;  // candidate index: staged as the hit (request_deliver_kernel maps it to the record)
     uint32_t k;  // the lane's chain
 };
 
-#ifdef SBEACON_ENDCAP_CHECK
-__device__ unsigned g_endcap_prints = 0;
-#endif
 template <bool LDS_LUT>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void request_eval_kernel(
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_REQ_WAVES, SBEACON_REQ_WAVES))) void request_eval_kernel(
     DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
     unsigned long long *__restrict__ status, const QRes *__restrict__ sres, ReqPartial *__restrict__ rows,
-    uint64_t *__restrict__ row_cnt, uint64_t *__restrict__ row_src, uint64_t *__restrict__ stage, uint32_t n_lut) {
+    uint64_t *__restrict__ row_cnt, uint64_t *__restrict__ row_src, uint32_t *__restrict__ stage, uint32_t n_lut,
+    unsigned int *__restrict__ err) {
     __shared__ ReqLds lds_all[kWavesPerBlock];
     __shared__ uint32_t slut[LDS_LUT ? kReqLut : 1];
     ReqLds &L = lds_all[threadIdx.x >> 6];
@@ -2028,7 +2035,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     if (!live) return;
     const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
     const uint64_t stage_at = uniform64(rr.stage);
-    const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
+    const uint32_t rflags = uniform(rr.flags);
+    const bool simple = (rflags & kRunSimple) != 0;
+    // request_plan_kernel's guarantees over every candidate the run's chains
+    // can load: chunk sums fit 32 bits (no wide path); one AN, so a chain's
+    // AN sum is its hit records times it (no AN scan)
+    const bool narrow = (rflags & kRunNarrow) != 0;
+    const bool anc = (rflags & kRunAnCommon) != 0;
+    const uint64_t an_c = rflags >> kRunAnShift;
     const bool slot = C.first != 0;
     const uint32_t R = static_cast<uint32_t>(__popcll(__ballot(slot)));
     const uint32_t cnt = slot ? C.c_hi - C.c_lo : 0u;
@@ -2062,7 +2076,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const uint32_t cumv = incl_sum_u32(static_cast<uint32_t>(__popcll(wl))) - static_cast<uint32_t>(__popcll(wl));
     const uint32_t nch = (T + kWave - 1) / kWave;
     const uint32_t i_safe = rdl(C.c_lo, 0);  // a valid candidate index (chain 0 is non-empty when T > 0)
-    uint64_t *const hdst = stage + stage_at;  // the run's staging region (capacity planned on the host)
+    // the run's staging region (capacity planned with the batch): a hit is
+    // staged as its candidate index | ALT label << 29 (4 bytes)
+    uint32_t *const hdst = stage + stage_at;
+    uint32_t hpos = 0;   // hits staged so far (wave-uniform)
+    uint32_t carry = 0;  // the last positive hit's slice key + 1 (keys grow with the position)
+    uint32_t run_ex = 0; // slices with exists = True so far (wave-uniform; the invariant check)
+    uint32_t acc_nv = 0, acc_ex = 0, acc_hr = 0;
+    uint64_t acc_cc = 0, acc_an = 0;
+    // one instantiation per AN mode (a wave-uniform run flag): under a
+    // common AN no AN column is loaded and no AN sum is scanned
+    auto pass = [&](auto anc_t) {
+    constexpr bool ANC = decltype(anc_t)::value;
     // ---- candidates
     auto load = [&](uint32_t c) -> ReqChunk {
         const uint32_t g = kWave * c + ul;
@@ -2084,23 +2109,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         ReqChunk q;
         q.k = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(W1 >> 32),
                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(W1), s0));
+#ifdef SBEACON_ABL_LOADS  // timing ablation only: every lane loads one cached candidate
+        const uint32_t i = i_safe + (g & 0u);
+#else
         const uint32_t i = g < T ? g + L.a[q.k].x : i_safe;
-        q.x = ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]};
+#endif
+        q.q = st.vc_q[i];
+        if constexpr (ANC) q.an = 0;
+        else q.an = st.vc_word[i].an;
+        q.i = i;
         return q;
     };
-    uint32_t hpos = 0;   // hits staged so far (wave-uniform)
-    uint32_t carry = 0;  // the last positive hit's slice key + 1 (keys grow with the position)
-    uint32_t acc_nv = 0, acc_ex = 0;
-    uint64_t acc_cc = 0, acc_an = 0;
-#ifdef SBEACON_ENDCAP_CHECK
-    // diagnostic build only (tools/endcap_check.sh): per-chain sums by end
-    // captures computed beside the shipping pull-and-subtract and compared
-    const uint32_t qpos = pin - 1u, qlane = qpos & 63u;
-    const uint32_t qchunk = pin ? qpos >> 6 : ~0u;
-    uint32_t e_nv = 0, e_ex = 0, run_nv = 0, run_ex = 0;
-#endif
     auto eval = [&](const ReqChunk &q, uint32_t c) {
-        const ChainChunk &x = q.x;
+        const VcQ &x = q.q;
         const uint32_t k = q.k;
         // every column of this chunk is waited for here, at once: the wait
         // counter pass then knows them ready on every path below.  Without
@@ -2108,16 +2129,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         // branches that may issue loads, where the pass can only wait for
         // vmcnt(0) -- the NEXT chunk's prefetch included, which serialised
         // the pipeline
-        asm volatile("" ::"v"(x.p), "v"(x.h.end), "v"(x.h.w), "v"(x.h.ac0), "v"(x.h.an), "v"(x.r));
+        asm volatile("" ::"v"(x.pos), "v"(x.end), "v"(x.w), "v"(x.ac0));
+        if constexpr (!ANC) asm volatile("" ::"v"(q.an));
         const uint32_t base = kWave * c;
         const uint32_t g = base + ul;
         const uint4 A = L.a[k], Bw = L.b[k];
         const uint32_t first = A.y;
-        const uint32_t w = x.h.w;
+        const uint32_t w = x.w;
         // window, END bounds: every operand evaluated (bitwise, not
         // short-circuit: no divergent LDS reads)
-        uint32_t cand = static_cast<uint32_t>(g < T) & static_cast<uint32_t>(x.p - first <= A.z) &
-                        static_cast<uint32_t>(x.h.end - A.w <= Bw.x);
+        uint32_t cand = static_cast<uint32_t>(g < T) & static_cast<uint32_t>(x.pos - first <= A.z) &
+                        static_cast<uint32_t>(x.end - A.w <= Bw.x);
         if (__ballot(cand & (w >> 28))) {  // VT_SLOW: never (prepare sends such requests per slice)
             if (cand & (w >> 28)) atomicOr(&L.slow[k >> 5], 1u << (k & 31u));
             cand &= ~(w >> 28) & 1u;
@@ -2134,23 +2156,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint32_t h0 = cand & static_cast<uint32_t>((w & 0xffu) - vlo <= vspan) & a0;
         // ALTs 2..n (:124 loop): only records whose word says an extra ALT
         // of an accepted class (or a symbolic one) might match (Bw.w = xneed)
+#ifdef SBEACON_ABL_XL  // timing ablation only (wrong answers): no extra-ALT lookups
+        const uint32_t xl = 0;
+#else
         const uint32_t xl = cand & static_cast<uint32_t>((w >> VT_NX_SHIFT) != 0) & static_cast<uint32_t>((w & Bw.w) != 0);
+#endif
         bool hit;
         uint32_t cn;      // variants emitted (ALTs with AC != 0)
-        uint64_t em;      // their label indexes
         int64_t cv;       // call count contribution
         uint32_t anv;     // AN contribution
-        if (!__ballot(xl)) {  // every hit lane has one ALT
+        uint32_t pre, tot;
+        if (!__ballot(xl)) {  // every hit lane has one ALT: ALT0 (label 0) is the only variant
             hit = h0 != 0;
-            cv = hit ? x.h.ac0 : 0;
-            cn = static_cast<uint32_t>(hit & (x.h.ac0 != 0));
-            em = cn;
-            anv = hit ? static_cast<uint32_t>(x.h.an) : 0u;
+            cv = hit ? x.ac0 : 0;
+            cn = static_cast<uint32_t>(hit & (x.ac0 != 0));
+            anv = hit ? static_cast<uint32_t>(q.an) : 0u;
+            const uint64_t one = __ballot(cn);
+            pre = popc_below(one);
+            tot = static_cast<uint32_t>(__popcll(one));
+#ifndef SBEACON_ABL_STAGE  // (timing ablation only: no staging stores)
+            if (cn) hdst[hpos + pre] = q.i;
+#endif
         } else {
             uint64_t hm = h0;
             uint32_t x0 = 0;
             if (xl) {
-                x0 = st.x_lo[x.r];
+                x0 = st.x_lo[st.vc_idx[q.i]];
                 // consumed here: no load left pending on this register past
                 // the branch (a later writer of the register would wait for
                 // vmcnt(0) on every path)
@@ -2168,60 +2199,61 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             }
             hit = hm != 0;
             cv = 0;
-            em = 0;
+            uint64_t em = 0;  // labels of the emitted variants
             for (uint64_t b = hm; b; b &= b - 1) {  // :205-214, AC of each matching ALT
                 const int j = ffs64(b);
-                const int64_t v = j ? st.xrow[x0 + j - 1].ac : x.h.ac0;
+                const int64_t v = j ? st.xrow[x0 + j - 1].ac : x.ac0;
                 cv += v;
                 if (v != 0) em |= 1ull << j;
             }
             cn = static_cast<uint32_t>(__popcll(em));
-            anv = hit ? static_cast<uint32_t>(x.h.an) : 0u;
-        }
-        // ---- staging: hits in candidate order, ALTs of a record in label order
-        uint32_t pre, tot;
-        const bool multi = __ballot(cn > 1) != 0;
-        if (!multi) {
-            const uint64_t one = __ballot(cn == 1);
-            pre = popc_below(one);
-            tot = static_cast<uint32_t>(__popcll(one));
-            if (cn == 1) hdst[hpos + pre] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(em)) << kHitAltShift);
-        } else {  // bit-sliced prefix (multi-ALT hit lanes)
-            pre = 0;
-            tot = 0;
-            for (uint32_t bb = 0; bb < 7; ++bb) {
-                const uint64_t m = __ballot((cn >> bb) & 1u);
-                pre += popc_below(m) << bb;
-                tot += static_cast<uint32_t>(__popcll(m)) << bb;
-                if (!__ballot(cn >> (bb + 1))) break;
+            anv = hit ? static_cast<uint32_t>(q.an) : 0u;
+            // ---- staging: hits in candidate order, ALTs of a record in label order
+            if (!__ballot(cn > 1)) {
+                const uint64_t one = __ballot(cn == 1);
+                pre = popc_below(one);
+                tot = static_cast<uint32_t>(__popcll(one));
+                if (cn == 1) hdst[hpos + pre] = q.i | static_cast<uint32_t>(ffs64(em)) << kStageAltShift;
+            } else {  // bit-sliced prefix (multi-ALT hit lanes)
+                pre = 0;
+                tot = 0;
+                for (uint32_t bb = 0; bb < 7; ++bb) {
+                    const uint64_t m = __ballot((cn >> bb) & 1u);
+                    pre += popc_below(m) << bb;
+                    tot += static_cast<uint32_t>(__popcll(m)) << bb;
+                    if (!__ballot(cn >> (bb + 1))) break;
+                }
+                uint32_t at = hpos + pre;
+                for (uint64_t b = em; b; b &= b - 1)
+                    hdst[at++] = q.i | static_cast<uint32_t>(ffs64(b)) << kStageAltShift;
             }
-            uint32_t at = hpos + pre;
-            for (uint64_t b = em; b; b &= b - 1)
-                hdst[at++] = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
         }
         hpos += tot;
         // ---- slices with exists = True: a positive hit whose slice differs
         // from the previous positive hit's (keys: chain << 20 | slice, growing
         // with the position), the carry from the chunks before
         const bool pos = hit && cv > 0;
-        const uint32_t key1 = pos ? (k << 20 | (x.p - first) / kReqWidth) + 1u : 0u;
+        const uint32_t key1 = pos ? (k << 20 | (x.pos - first) / kReqWidth) + 1u : 0u;
+#ifdef SBEACON_ABL_KEY  // timing ablation only: no slice-key scan
+        const uint32_t mx = key1;
+#else
         const uint32_t mx = incl_max_u32(key1);
+#endif
         const uint32_t prev = max(wave_shr1(mx), carry);
         const bool isnew = pos && key1 != prev;
         carry = max(carry, rdl(mx, kWave - 1));
         const uint64_t nb = __ballot(isnew);
-        // inclusive per-lane counts of the chunk: variants | new slices << 16
-        const uint32_t nvex = (pre + cn) | (popc_below(nb) + (isnew ? 1u : 0u)) << 16;
-#ifdef SBEACON_ENDCAP_CHECK
-        {
-            const uint32_t pq = bperm(nvex, qlane);
-            if (qchunk == c) {
-                e_nv = run_nv + (pq & 0xffffu);
-                e_ex = run_ex + (pq >> 16);
-            }
-            run_nv += tot;
-            run_ex += static_cast<uint32_t>(__popcll(nb));
-        }
+        run_ex += static_cast<uint32_t>(__popcll(nb));
+        // inclusive per-lane counts of the chunk, three fields pulled and
+        // subtracted at once (each field's prefix grows with the lane, so
+        // no field borrows): variants (<= 8 ALTs x 64 lanes) | new slices
+        // << 10 | hit records << 17 (only read under a common AN)
+        uint32_t nvex = (pre + cn) | (popc_below(nb) + (isnew ? 1u : 0u)) << 10;
+        if constexpr (ANC) nvex |= (popc_below(__ballot(hit)) + (hit ? 1u : 0u)) << 17;
+#ifdef SBEACON_ABL_SUMS  // timing ablation only: no per-chain sums
+        acc_nv += nvex & 1u;
+        acc_cc += static_cast<uint64_t>(cv);
+        return;
 #endif
         // ---- chain k's part of the chunk, pulled by lane k from its last lane
         const uint32_t lim = min(base + kWave, T);
@@ -2231,9 +2263,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         const uint32_t pn = bperm(nvex, e);
         const uint32_t qn = wave_shr1(pn);
         const uint32_t dn = inter ? pn - (opens ? 0u : qn) : 0u;
-        acc_nv += dn & 0xffffu;
-        acc_ex += dn >> 16;
-        const bool big = __ballot(hit && (cv < 0 || cv >= (1ll << 25) || x.h.an < 0 || x.h.an >= (1 << 25))) != 0;
+        acc_nv += dn & 0x3ffu;
+        acc_ex += (dn >> 10) & 0x7fu;
+        acc_hr += dn >> 17;
+        if constexpr (ANC) {  // (a common AN implies narrow) the chunk's sums fit 32 bits; AN sums from hit records
+            const uint32_t scc = incl_sum_u32(static_cast<uint32_t>(cv));
+            const uint32_t pc = bperm(scc, e);
+            const uint32_t qc = wave_shr1(pc);
+            if (inter) acc_cc += pc - (opens ? 0u : qc);
+            return;
+        }
+        const bool big = !narrow &&
+                         __ballot(hit && (cv < 0 || cv >= (1ll << 25) || q.an < 0 || q.an >= (1 << 25))) != 0;
         if (!big) {  // the chunk's sums fit 32 bits
             const uint32_t scc = incl_sum_u32(static_cast<uint32_t>(cv)), san = incl_sum_u32(anv);
             const uint32_t pc = bperm(scc, e), pa = bperm(san, e);
@@ -2275,28 +2316,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         for (int a = 0; a < kReqPipe; ++a)
             if (c0 + a < nch) eval(buf[a], c0 + a);
     }
+    };
+    if (anc) pass(std::true_type{});
+    else pass(std::false_type{});
     wave_lds_sync();
-#ifdef SBEACON_ENDCAP_CHECK
-    {
-        const uint32_t sn = wave_shr1(e_nv), sx = wave_shr1(e_ex);
-        const uint32_t n2 = e_nv - sn, x2 = e_ex - sx;
-        const bool bad = n2 != acc_nv || x2 != acc_ex;
-        const uint64_t mb = __ballot(bad);
-        if (mb && ul == static_cast<uint32_t>(ffs64(mb)) && atomicAdd(&g_endcap_prints, 1u) < 24)
-            printf("endcap w=%u lane=%u R=%u Rn=%u T=%u nch=%u pin=%u pex=%u qchunk=%u acc_nv=%u n2=%u acc_ex=%u x2=%u "
-                   "e_nv=%u prev=%u run_nv=%u hpos=%u e_ex=%u prev_ex=%u run_ex=%u pacc_ex=%u\n",
-                   w, ul, R, Rn, T, nch, pin, pex, qchunk, acc_nv, n2, acc_ex, x2, e_nv, sn, run_nv, hpos, e_ex, sx,
-                   run_ex, wave_shr1(acc_ex));
-    }
-#endif
     // ---- per chain (lane k < R): staging start (scan of the hit counts), partial
-    const uint32_t cs = incl_sum_u32(acc_nv) - acc_nv;
+    const uint32_t cs_incl = incl_sum_u32(acc_nv), cs = cs_incl - acc_nv;
+    // invariants of the per-chain sums (the pulls are cross-lane: a lane
+    // reading another's stale value would break them): the chains' variant
+    // counts add up to the hits staged, their new-slice counts to the
+    // wave's, and a chain has no more exists-slices than variants nor (under
+    // a common AN) than hit records.  A violation fails the batch at sync
+    // (SB_EINTERNAL), never a silent wrong row.
+    {
+        const uint32_t ex_tot = rdl(incl_sum_u32(acc_ex), kWave - 1);
+        const bool bad_lane = acc_ex > acc_nv || (anc && acc_ex > acc_hr);
+#if !defined(SBEACON_ABL_XL) && !defined(SBEACON_ABL_KEY) && !defined(SBEACON_ABL_SUMS) && !defined(SBEACON_ABL_LOADS)
+        if (rdl(cs_incl, kWave - 1) != hpos || ex_tot != run_ex || __ballot(bad_lane))
+            if (ul == 0) atomicOr(err, 1u);
+#endif
+    }
     ReqPartial part{0, 0, 0, 0, 0};
     if (ul < R) {
         const bool slow = (L.slow[ul >> 5] >> (ul & 31u)) & 1u;  // never for prepared chains
+        const uint64_t an_sum = anc ? static_cast<uint64_t>(acc_hr) * an_c : acc_an;
         part = slow ? ReqPartial{0, static_cast<int64_t>(acc_nv), 0, 0, static_cast<int64_t>(nsl)}
                     : ReqPartial{static_cast<int64_t>(acc_ex), static_cast<int64_t>(acc_nv),
-                                 static_cast<int64_t>(acc_cc), static_cast<int64_t>(acc_an), 0};
+                                 static_cast<int64_t>(acc_cc), static_cast<int64_t>(an_sum), 0};
         rows[rowk] = part;
     }
     // ---- rows (lane i < nrows = row row_lo + i): hit counts, staging starts
@@ -2336,13 +2382,14 @@ __global__ __launch_bounds__(kBlock) void request_plan_kernel(DStore st, const R
     if (row < n) q = in[row];
     const uint32_t cls = row < n ? (q.cls & 3u) : static_cast<uint32_t>(REQ_NONE);
     const bool chain = cls == REQ_CHAIN;
-    uint32_t c0 = 0, c1 = 0;
+    uint32_t c0 = 0, c1 = 0, vi_xinfo = 0;
     uint64_t cap = 0;
     if (chain) {
         const VcIndex vi = st.vcx[static_cast<uint64_t>(q.seg) * kVtKinds + ((q.bits >> 23) & 7u)];
         c0 = vc_bound(vi, st.vc_bucket, q.first, 0);
         c1 = (q.bits >> 26) & 1u ? c0 : max(c0, vc_bound(vi, st.vc_bucket, static_cast<uint64_t>(q.last) + 1, 1));
         cap = st.vc_altpre[c1] - st.vc_altpre[c0];
+        vi_xinfo = vi.xinfo;
     }
     const bool ne = chain && c1 > c0;
     const uint64_t mne = __ballot(ne), mem = __ballot(chain && !ne);
@@ -2357,56 +2404,89 @@ __global__ __launch_bounds__(kBlock) void request_plan_kernel(DStore st, const R
     const uint32_t nsl = chain ? q.cls >> 2 : 0u;
     const uint32_t slsum = rdl(incl_sum_u32(nsl), kWave - 1);
     const bool simple = __ballot(cls == REQ_SLICES) == 0;
+    // what request_eval_kernel may assume of every chain with candidates
+    // (VcIndex::xinfo): 32-bit chunk sums, one AN (AN sum = hit records x AN)
+    const uint32_t xi = ne ? vi_xinfo : kVcNarrow;
+    const bool narrow = __ballot(!(xi & kVcNarrow)) == 0;
+    const uint32_t a = xi & kVcAnMask;  // AN + 1, 0 = no common AN
+    const uint32_t a0 = mne ? rdl(a, static_cast<uint32_t>(ffs64(mne))) : 1u;
+    const bool anc = narrow && a0 != 0u && __ballot(ne && a != a0) == 0;
+    const uint32_t flags = (simple ? kRunSimple : 0u) | (narrow ? kRunNarrow : 0u) |
+                           (anc ? kRunAnCommon | (a0 - 1u) << kRunAnShift : 0u);
     if (ul == 0) {  // (the batch's chain / slice totals: request_stage_scan_kernel -- one counter
                     // atomically bumped by every wave serialised the launch, ~350 us for 15.6 k runs)
-        runs[w] = RowRun{w * kRunRows, min(w * kRunRows + kRunRows, n), 0u, nslots, 0ull, slsum,
-                         simple ? kRunSimple : 0u};
-        rcap[w] = capsum;
+        runs[w] = RowRun{w * kRunRows, min(w * kRunRows + kRunRows, n), 0u, nslots, 0ull, slsum, flags};
+        rcap[2 * w] = capsum;
+        rcap[2 * w + 1] = static_cast<unsigned long long>(slsum) << 32 | nslots;
     }
 }
 
-// request_stage_scan_kernel (one workgroup): each run's staging offset =
-// the exclusive prefix of the runs' capacities; counters = (chains, chain
-// slices, staging total)
-__global__ __launch_bounds__(1024) void request_stage_scan_kernel(RowRun *__restrict__ runs,
-                                                                  const unsigned long long *__restrict__ rcap,
-                                                                  uint32_t n_runs,
-                                                                  unsigned long long *__restrict__ counters) {
-    __shared__ unsigned long long wsum[16];
-    __shared__ unsigned long long carry_s, chains_s, slices_s;
-    const uint32_t tid = threadIdx.x, wave = tid >> 6;
-    if (tid == 0) carry_s = chains_s = slices_s = 0;
+// request_stage_scan_kernel: each run's staging offset = the exclusive
+// prefix of the runs' capacities; counters = (chains, chain slices, staging
+// total).  request_plan_kernel left per run {capacity, slices << 32 |
+// chains} (16 B).  One workgroup per tile of 1,024 runs: it sums the
+// capacities of every earlier tile (coalesced, a few loads per thread, all in
+// flight at once), then scans its own tile; the last workgroup, which reads
+// every run anyway, writes the counters.  (One workgroup walking the runs in
+// 16 dependent rounds took 32 us for 15.6 k runs; one workgroup with every
+// thread's 16 runs loaded up front, 19 us: one CU's load issue.)
+constexpr uint32_t kStageTile = 1024;
+__device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, unsigned long long *wsum) {
+    const uint32_t wave = threadIdx.x >> 6;
+    const uint64_t t = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(v)), kWave - 1));
     __syncthreads();
-    uint32_t nch = 0;  // this thread's runs: chains (c_hi) and their slices (n_slots)
-    uint64_t nsl = 0;
-    for (uint32_t base = 0; base < n_runs; base += 1024) {
-        const uint32_t i = base + tid;
-        const uint64_t v = i < n_runs ? rcap[i] : 0ull;
-        if (i < n_runs) {
-            nch += runs[i].c_hi;
-            nsl += runs[i].n_slots;
+    if (lane_id() == 0) wsum[wave] = t;
+    __syncthreads();
+    uint64_t r = 0;
+    for (uint32_t k = 0; k < blockDim.x / kWave; ++k) r += wsum[k];
+    return r;
+}
+__global__ __launch_bounds__(kStageTile) void request_stage_scan_kernel(RowRun *__restrict__ runs,
+                                                                        const unsigned long long *__restrict__ rcap,
+                                                                        uint32_t n_runs,
+                                                                        unsigned long long *__restrict__ counters) {
+    __shared__ unsigned long long wsum[kStageTile / kWave];
+    const uint32_t tid = threadIdx.x, wave = tid >> 6, t0 = blockIdx.x * kStageTile;
+    const bool last = blockIdx.x + 1 == gridDim.x;
+    const ulonglong2 *rc2 = reinterpret_cast<const ulonglong2 *>(rcap);
+    uint64_t pre = 0, nch = 0, nsl = 0;
+    constexpr uint32_t kU = 8;
+    for (uint32_t i0 = 0; i0 < t0; i0 += kStageTile * kU) {
+        ulonglong2 x[kU];
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint32_t i = i0 + u * kStageTile + tid;
+            x[u] = i < t0 ? rc2[i] : ulonglong2{0ull, 0ull};
         }
-        const uint64_t incl = incl_sum_u64(v);
-        if (lane_id() == kWave - 1) wsum[wave] = incl;
-        __syncthreads();
-        uint64_t before = carry_s;
-        for (uint32_t k = 0; k < wave; ++k) before += wsum[k];
-        if (i < n_runs) runs[i].stage = before + incl - v;
-        __syncthreads();
-        if (tid == 1023) carry_s = before + incl;
-        __syncthreads();
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            pre += x[u].x;
+            nch += x[u].y & 0xffffffffull;
+            nsl += x[u].y >> 32;
+        }
     }
-    const uint64_t wc = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(nch)), kWave - 1));
-    const uint64_t ws = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(nsl)), kWave - 1));
-    if (lane_id() == 0) {  // 16 LDS atomics, not one device counter per run
-        atomicAdd(&chains_s, wc);
-        atomicAdd(&slices_s, ws);
-    }
+    const uint32_t i = t0 + tid;
+    const ulonglong2 me = i < n_runs ? rc2[i] : ulonglong2{0ull, 0ull};
+    nch += me.y & 0xffffffffull;
+    nsl += me.y >> 32;
+    pre = block_sum_u64(pre, wsum);
+    // the tile's exclusive scan
+    const uint64_t incl = incl_sum_u64(me.x);
     __syncthreads();
-    if (tid == 0) {
-        counters[0] = chains_s;
-        counters[1] = slices_s;
-        counters[2] = carry_s;
+    if (lane_id() == kWave - 1) wsum[wave] = incl;
+    __syncthreads();
+    uint64_t before = pre;
+    for (uint32_t k = 0; k < wave; ++k) before += wsum[k];
+    if (i < n_runs) runs[i].stage = before + incl - me.x;
+    uint64_t tile = 0;
+    for (uint32_t k = 0; k < kStageTile / kWave; ++k) tile += wsum[k];
+    if (last) {
+        const uint64_t ch = block_sum_u64(nch, wsum), sl = block_sum_u64(nsl, wsum);
+        if (tid == 0) {
+            counters[0] = ch;
+            counters[1] = sl;
+            counters[2] = pre + tile;
+        }
     }
 }
 
@@ -2466,8 +2546,14 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const RowRun *__restrict__ runs, uint32_t n_runs, const unsigned long long *__restrict__ status,
     const unsigned long long *__restrict__ toff, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
     const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr, const uint64_t *__restrict__ shits,
-    uint64_t *__restrict__ row_off, const uint64_t *__restrict__ row_src, const uint64_t *__restrict__ stage,
-    uint64_t *__restrict__ out, uint32_t n_rows, uint64_t rec_base) {
+    uint64_t *__restrict__ row_off, const uint64_t *__restrict__ row_src, const uint32_t *__restrict__ stage,
+    const uint32_t *__restrict__ vc_idx, uint64_t *__restrict__ out, uint32_t n_rows, uint64_t rec_base) {
+    // a staged hit (candidate | ALT label << kStageAltShift) as the output's
+    // (record + rec_base) | label << kHitAltShift
+    auto hit_of = [&](uint32_t v) -> uint64_t {
+        return (static_cast<uint64_t>(vc_idx[v & kStageCandMask]) + rec_base) |
+               static_cast<uint64_t>(v >> kStageAltShift) << kHitAltShift;
+    };
     const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     if (w >= n_runs) return;
     const uint32_t ul = static_cast<uint32_t>(lane_id());
@@ -2489,16 +2575,19 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     if (simple) {  // chain rows (and empty rows) only: the staging region is the output, in order
         constexpr uint32_t kU = 4;
         for (uint64_t j0 = 0; j0 < H; j0 += kWave * kU) {
-            uint64_t v[kU];
+            uint32_t v[kU];
 #pragma unroll
             for (uint32_t u = 0; u < kU; ++u) {
                 const uint64_t j = j0 + kWave * u + ul;
-                v[u] = j < H ? stage[stage_at + j] : 0ull;
+                v[u] = j < H ? stage[stage_at + j] : 0u;
             }
+            uint64_t h[kU];
+#pragma unroll
+            for (uint32_t u = 0; u < kU; ++u) h[u] = hit_of(v[u]);
 #pragma unroll
             for (uint32_t u = 0; u < kU; ++u) {
                 const uint64_t j = j0 + kWave * u + ul;
-                if (j < H) out[O + j] = v[u] + rec_base;
+                if (j < H) out[O + j] = h[u];
             }
         }
         return;
@@ -2511,7 +2600,7 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
         const uint32_t q0 = uniform(sseg[r]), q1 = uniform(sseg[r + 1]);
         if (q1 == q0) {  // a chain row: its hits are contiguous in the staging region
             const uint64_t src = uniform64(row_src[r]);
-            for (uint64_t k = ul; k < nv; k += kWave) out[at + k] = stage[src + k] + rec_base;
+            for (uint64_t k = ul; k < nv; k += kWave) out[at + k] = hit_of(stage[src + k]);
         } else {
             uint64_t dst = at;
             for (uint32_t q = q0; q < q1; ++q) {
@@ -3705,9 +3794,9 @@ void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, ui
 void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun *runs, uint32_t n_runs,
                          unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
-                         ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint64_t *stage, uint64_t *out,
-                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, hipStream_t s,
-                         hipEvent_t ev0, hipEvent_t ev1) {
+                         ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
+                         uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
+                         hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (!n_runs) {
         (void)hipMemsetAsync(row_off, 0, 8, s);
         return;
@@ -3717,7 +3806,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
     if (ev0) (void)hipEventRecord(ev0, s);
     auto eval = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres, rows, row_off,
-                           row_src, stage, n_lut);
+                           row_src, stage, n_lut, err);
     };
     (void)run;
     if (n_lut <= kReqLut) eval(request_eval_kernel<true>);
@@ -3725,7 +3814,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
     if (ev1) (void)hipEventRecord(ev1, s);
     hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, status, n_runs, tstatus, n_tiles);
     hipLaunchKernelGGL(request_deliver_kernel, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg,
-                       shoff, sherr, shits, row_off, row_src, stage, out, n_rows, rec_base);
+                       shoff, sherr, shits, row_off, row_src, stage, st.vc_idx, out, n_rows, rec_base);
 }
 
 void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,
@@ -3734,7 +3823,8 @@ void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain
     if (!n_runs) return;
     hipLaunchKernelGGL(request_plan_kernel, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, in, n, n_runs, chains,
                        runs, rcap, counters);
-    hipLaunchKernelGGL(request_stage_scan_kernel, dim3(1), dim3(1024), 0, s, runs, rcap, n_runs, counters);
+    hipLaunchKernelGGL(request_stage_scan_kernel, dim3((n_runs + kStageTile - 1) / kStageTile), dim3(kStageTile), 0, s,
+                       runs, rcap, n_runs, counters);
 }
 
 // run totals (request_eval_kernel) -> tile offsets (request_tile_scan_kernel)

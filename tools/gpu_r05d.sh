@@ -1,0 +1,16 @@
+# round 5: request_eval_kernel timing ablations (wrong answers, timing only)
+mkdir -p gpurun_out/r05d
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r05d
+step() {  # name, limit, command...
+  local name=$1 lim=$2; shift 2
+  timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?
+  echo "$name rc=$rc"; tail -1 $O/$name.log | cut -c1-400
+  case $rc in 0) return 0;; *) exit $rc;; esac
+}
+step full 300 python3 -u $R/tools/req_tune.py --save /tmp/st --digest
+for v in p3w7 p3w6 p4w6 p4w5; do
+  step $v 200 env SBEACON_LIB=$R/tools/variants/$v/libsbeacon_hip.so python3 -u $R/tools/req_tune.py --open /tmp/st --digest
+done
+exit 0

@@ -1,0 +1,99 @@
+#!/usr/bin/env python3
+"""Config-3 request-pass A/B harness (kernel tuning, not the bench): the
+whole-genome store (sites only unless --genotypes; --save DIR writes it with
+sb_store_save, --open DIR re-opens it in ~0.5 s so library variants
+(SBEACON_LIB) can be compared on one box without re-ingesting), 4 rotating
+1 M-request batches re-planned every pass as bench.py's step does.  Prints
+one JSON line: per-kernel medians from HIP events (eval alone; the pass)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, 'terraform-aws-serverless-beacon_amd'))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--records', type=int, default=85_000_000)
+    ap.add_argument('--requests', type=int, default=1_000_000)
+    ap.add_argument('--batches', type=int, default=4)
+    ap.add_argument('--rounds', type=int, default=15)
+    ap.add_argument('--save', default=None)
+    ap.add_argument('--open', default=None)
+    ap.add_argument('--genotypes', action='store_true')
+    ap.add_argument('--digest', action='store_true', help='blake2b of every batch\'s rows + hits (A/B parity)')
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.device('cuda', 0)
+    from sbeacon.engine import Store
+    from sbeacon.genome import GenomeShape, config3_requests, prepare_shard_requests, shard_requests
+    shape = GenomeShape(n_total=args.records, seed=3)
+    t0 = time.perf_counter()
+    if args.open:
+        store = Store.open(args.open, device=0)
+    else:
+        store = shape.build_shard_store(1, 0, device=0, genotypes=args.genotypes)
+        if args.save:
+            store.save(args.save)
+    t_store = time.perf_counter() - t0
+    stream = torch.cuda.current_stream().cuda_stream
+    B = []
+    for k in range(args.batches):
+        sr = shard_requests(shape, config3_requests(shape, n=args.requests, seed=1003 + k), 1, 0)
+        b = prepare_shard_requests(store, sr)
+        b.set_stream(stream)
+        b.set_replan(True)
+        n = sr.n_rows
+        B.append((b, torch.zeros((max(n, 1), 5), dtype=torch.int64, device=dev),
+                  torch.zeros(int(b.stats()['hits']) + 1, dtype=torch.int64, device=dev),
+                  torch.zeros(n + 1, dtype=torch.int64, device=dev)))
+
+    def run(b, p, h, o):
+        b.run(p.data_ptr(), h.data_ptr(), o.data_ptr(), 0)
+
+    for _ in range(2):
+        for x in B:
+            run(*x)
+    torch.cuda.synchronize()
+    ev, pas = [], []
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(args.rounds):
+        for x in B:
+            x[0].time_eval(True)
+        for x in B:
+            run(*x)
+        for x in B:
+            x[0].sync()
+            ev.append(x[0].timing()['scan_ms'])
+            x[0].time_eval(False)
+        e0.record()
+        for x in B:
+            run(*x)
+        e1.record()
+        torch.cuda.synchronize()
+        pas.append(e0.elapsed_time(e1) / len(B))
+    ev.sort()
+    pas.sort()
+    out = {'lib': os.environ.get('SBEACON_LIB', 'in-tree'), 'records': args.records, 'store_s': round(t_store, 2),
+           'eval_ms_median': round(ev[len(ev) // 2], 4), 'eval_ms_min': round(ev[0], 4),
+           'pass_ms_median': round(pas[len(pas) // 2], 4), 'pass_ms_min': round(pas[0], 4)}
+    if args.digest:
+        import hashlib
+        h = hashlib.blake2b(digest_size=16)
+        for b, p, hh, o in B:
+            ro = o.cpu().numpy()
+            h.update(p[:len(ro) - 1].cpu().numpy().tobytes())
+            h.update(hh[:int(ro[-1])].cpu().numpy().tobytes())
+            h.update(ro.tobytes())
+        out['digest'] = h.hexdigest()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == '__main__':
+    main()
