@@ -171,17 +171,21 @@ def main_genome(args):
     st = {'cand_unique': agg['cand_unique'], 'cand_window': agg['cand_window'], 'cand_loaded': agg['cand_loaded']}
     # Roofline of the request pass, priced on the bytes it must move at least
     # once.  request_eval_kernel: per request its 32 B chain
-    # descriptor (ReqChain), 40 B row and 8 B row count; 24 B per candidate in
-    # the union of the chain windows (POS 4 + VtHot 16 + record 4, each once
-    # however many overlapping requests read it); 8 B per hit staged.  Beside
-    # it the SURVEY §8d contract: 32 B x unique records in the slice windows +
-    # 8 B / hit.
+    # descriptor (ReqChain), 40 B row and 8 B row count; 16 B per candidate in
+    # the union of the chain windows (the VcQ word: POS, END, VtHot word, AC;
+    # each once however many overlapping requests read it; runs under a
+    # common AN read nothing else); 4 B per hit staged.  Beside it the round-4
+    # basis (24 B per candidate, 8 B per hit: what the round-4 kernel read and
+    # wrote) and the SURVEY §8d contract: 32 B x unique records in the slice
+    # windows + 8 B / hit.
     chains, hits_avg = agg['chains'], agg['hits']
-    comp = (32.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * hits_avg
+    comp = (32.0 + 40.0 + 8.0) * chains + 16.0 * st['cand_unique'] + 4.0 * hits_avg
     achieved = comp / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
+    comp_r04 = (32.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * hits_avg
     # the whole pass: the planning kernels (32 B packed request read, 32 B
     # descriptor written per request), eval, tile scan, delivery (+ 8 B row
-    # offset per request and the hits' dense copy: 8 B read + 8 B written per hit)
+    # offset per request; per hit its staged word read (4 B), its record id
+    # read (4 B), the 8 B hit written)
     comp_pass = comp + 64.0 * agg['rows'] + 8.0 * chains + 16.0 * hits_avg
     achieved_pass = comp_pass / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
     uniq = agg['uniq']
@@ -220,7 +224,7 @@ def main_genome(args):
             'gap, and after ~8 fp32 GEMMs (a busy device); round 3 traced 0.76-0.81 ms launches in its serial '
             'delivered passes')
     vals = [elapsed, kern_ms, agg['slices'], float(st['cand_loaded']), hits_avg, achieved, float(uniq), comp,
-            contract, step_dev_ms, pass_ms, achieved_pass, comp_pass]
+            contract, step_dev_ms, pass_ms, achieved_pass, comp_pass, comp_r04]
     if dist:
         t = torch.tensor(vals, dtype=torch.float64, device=dev)
         allv = [torch.zeros_like(t) for _ in range(world)]
@@ -286,12 +290,17 @@ def main_genome(args):
                                'averages: profiles/)',
                      'algorithmic_bytes_per_launch': r0[7],
                      'pricing': 'bytes the launch must move at least once: 80 B/request (32 B chain descriptor + '
-                                '40 B row + 8 B row count) + 24 B per candidate in the union of the chain windows + '
-                                '8 B/hit staged',
+                                '40 B row + 8 B row count) + 16 B per candidate in the union of the chain windows '
+                                '(POS, END, VtHot word, AC) + 4 B/hit staged',
+                     'r04_basis': {'bytes': r0[13], 'frac': round(r0[13] / (r0[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
+                                   if r0[1] > 0 else None,
+                                   'note': 'the round-4 pricing (24 B per candidate, 8 B per hit staged: what the '
+                                           'round-4 kernel read and wrote) over this kernel time, for comparison'},
                      'pass': {'ms': round(r0[10], 4), 'achieved': round(r0[11], 1),
                               'frac': round(r0[11] / HBM_PEAK_GBS, 4), 'bytes': r0[12],
                               'note': 'planning (+64 B/request: packed request read, descriptor written) + eval + '
-                                      'tile scan + delivery (row offsets, dense hit copy: +8 B/request, +16 B/hit)'},
+                                      'tile scan + delivery (+8 B/request row offsets; +16 B/hit: staged word and '
+                                      'record id read, 8 B hit written)'},
                      'candidates': {'unique': int(st['cand_unique']), 'in_windows': int(st['cand_window']),
                                     'loaded': int(st['cand_loaded'])},
                      'contract_bytes_per_launch': r0[8],
@@ -355,11 +364,14 @@ def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5)
     """End to end on one GPU: requests (numpy, host) -> the rank's row range
     (shard_rows) -> request batch planning + upload
     (sb_requests_prepare_beacon: conversion, the core cut and packing in C++,
-    then the planning kernels) -> one pass -> rows, row offsets and the hit
-    lists copied back into pinned host memory.  Every part inside the timed
-    region; a fresh batch each pass."""
+    then the planning kernels) -> one pass in the compact output form
+    (sb_requests_set_compact: 16 B rows, u32 row offsets, u32 hits) -> rows,
+    row offsets and the hit lists copied back into pinned host memory.  Every
+    part inside the timed region; a fresh batch each pass."""
+    import numpy as np
     import torch
     from sbeacon.genome import prepare_beacon_shard, shard_rows
+    from sbeacon.requests import widen_compact
     t_route = t_prep = t_dev = 0.0
     best = None
     rows_h = hits_h = ro_h = None
@@ -370,23 +382,25 @@ def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5)
         b0 = time.perf_counter()
         _, n_rows, batch = prepare_beacon_shard(store, shape, reqs, world, rank, rows=rr)
         batch.set_stream(torch.cuda.current_stream().cuda_stream)
+        batch.set_compact(True)
         cap = int(batch.stats()['hits'])
         c0 = time.perf_counter()
         if rows_h is None or rows_h.shape[0] < n_rows or hits_h.shape[0] < cap:
-            rows_d = torch.empty((max(n_rows, 1), 5), dtype=torch.int64, device=dev)
-            ro_d = torch.empty(n_rows + 1, dtype=torch.int64, device=dev)
-            hits_d = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
-            rows_h = torch.empty(rows_d.shape, dtype=torch.int64, pin_memory=True)
-            ro_h = torch.empty(ro_d.shape, dtype=torch.int64, pin_memory=True)
-            hits_h = torch.empty(hits_d.shape, dtype=torch.int64, pin_memory=True)
+            rows_d = torch.empty((max(n_rows, 1), 4), dtype=torch.int32, device=dev)
+            ro_d = torch.empty(n_rows + 1, dtype=torch.int32, device=dev)
+            hits_d = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+            rows_h = torch.empty(rows_d.shape, dtype=torch.int32, pin_memory=True)
+            ro_h = torch.empty(ro_d.shape, dtype=torch.int32, pin_memory=True)
+            hits_h = torch.empty(hits_d.shape, dtype=torch.int32, pin_memory=True)
         batch.run(rows_d.data_ptr(), hits_d.data_ptr(), ro_d.data_ptr(), base)
         rows_h[:n_rows].copy_(rows_d[:n_rows], non_blocking=True)
         ro_h.copy_(ro_d, non_blocking=True)
         torch.cuda.current_stream().synchronize()
-        total = int(ro_h[-1])
+        total = int(ro_h[-1].numpy().view(np.uint32))
         hits_h[:total].copy_(hits_d[:total], non_blocking=True)
         torch.cuda.current_stream().synchronize()
         d0 = time.perf_counter()
+        batch.sync()  # (the pass's invariant word; outside the timed region)
         batch.free()
         if k == 0:
             continue
@@ -396,15 +410,19 @@ def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5)
         best = (d0 - a) if best is None else min(best, d0 - a)
     dt = (t_route + t_prep + t_dev) / passes
     n = len(reqs)
+    total = int(ro_h[-1].numpy().view(np.uint32))
+    rows_w, hits_w, _ = widen_compact(rows_h[:n_rows].numpy(), hits_h[:total].numpy(), ro_h.numpy())
     return {'requests_per_s': round(n / dt, 1), 'ms_per_pass': round(dt * 1e3, 2),
             'best_ms': round(best * 1e3, 2), 'passes': passes,
             'split_ms': {'route_rows': round(t_route / passes * 1e3, 2),
                          'prepare_upload': round(t_prep / passes * 1e3, 2),
                          'device_pass_and_d2h': round(t_dev / passes * 1e3, 2)},
-            'hits_returned': int(ro_h[-1]),
-            'digest': digest(rows_h[:n_rows].numpy(), [hits_h[:int(ro_h[-1])].numpy()]),
-            'note': 'requests as numpy columns in host memory -> rows + row offsets + dense hit lists in pinned host '
-                    'memory; routing, planning, upload, the pass and both D2H copies inside the timed region'}
+            'hits_returned': total,
+            'd2h_bytes': int(16 * n_rows + 4 * (n_rows + 1) + 4 * total),
+            'digest': digest(rows_w, [hits_w]),
+            'note': 'requests as numpy columns in host memory -> compact rows (16 B) + u32 row offsets + u32 hit '
+                    'lists in pinned host memory; routing, planning, upload, the pass and both D2H copies inside '
+                    'the timed region (digest over the widened outputs)'}
 
 
 def cold_launch_probe(store, shape, reqs, world, rank, base, dev):
@@ -449,14 +467,16 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
     then sb_requests_prepare_beacon: the Beacon columns converted, cut to the
     rank's core and packed in one pass, uploaded, and the planning kernels on
     the thread's planning stream) while the main thread enqueues each
-    prepared chunk's pass and its row / row-offset D2H on the torch stream,
-    and a chunk's hit list D2H once its row offsets are back.  Requests in
-    host memory -> rows, row offsets (per chunk) and dense hit lists in
-    pinned host memory, all inside the timed region."""
+    prepared chunk's pass (compact outputs) and its row / row-offset D2H on
+    the torch stream, and a chunk's hit list D2H once its row offsets are
+    back.  Requests in host memory -> compact rows (16 B), u32 row offsets
+    (per chunk) and u32 hit lists in pinned host memory, all inside the timed
+    region."""
     import numpy as np
     import torch
     from concurrent.futures import ThreadPoolExecutor
     from sbeacon.genome import prepare_beacon_shard
+    from sbeacon.requests import widen_compact
     n = len(reqs)
     # chunk sizes tapered at both ends (a quarter, then 0.6, of the others):
     # the pipeline fills and drains sooner (`profiles/r04_y/` sweep)
@@ -472,16 +492,16 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
         lo, m, bt = prepare_beacon_shard(store, shape, reqs.rows(a, b), world, rank)
         return a + lo, m, bt, int(bt.stats()['hits'])
 
-    rows_h = torch.empty((n, 5), dtype=torch.int64, pin_memory=True)
-    ro_h = torch.empty(n + chunks, dtype=torch.int64, pin_memory=True)
-    rows_d = torch.empty((n, 5), dtype=torch.int64, device=dev)
-    ro_d = torch.empty(n + chunks, dtype=torch.int64, device=dev)
+    rows_h = torch.empty((n, 4), dtype=torch.int32, pin_memory=True)
+    ro_h = torch.empty(n + chunks, dtype=torch.int32, pin_memory=True)
+    rows_d = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    ro_d = torch.empty(n + chunks, dtype=torch.int32, device=dev)
     hits_d, hits_h = [None] * chunks, [None] * chunks
     hit_n = [0] * chunks
     times, total_hits = [], 0
     import gc
     gc.collect()
-    gc.disable()  # as timeit does: a collector pause inside a ~3.5 ms pass is noise, not the path
+    gc.disable()  # as timeit does: a collector pause inside a ~2 ms pass is noise, not the path
     with ThreadPoolExecutor(workers) as ex:
         for p in range(passes + 1):  # pass 0 sizes the hit buffers (untimed)
             torch.cuda.synchronize()
@@ -492,9 +512,10 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
             for k in range(chunks):
                 a, m, bt, cap = futs[k].result()
                 if hits_d[k] is None or hits_d[k].numel() < max(cap, 1):
-                    hits_d[k] = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
-                    hits_h[k] = torch.empty(max(cap, 1), dtype=torch.int64, pin_memory=True)
+                    hits_d[k] = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+                    hits_h[k] = torch.empty(max(cap, 1), dtype=torch.int32, pin_memory=True)
                 bt.set_stream(stream.cuda_stream)
+                bt.set_compact(True)
                 ro = ro_d[a + k:a + k + m + 1]
                 bt.run(rows_d[a:a + m].data_ptr(), hits_d[k].data_ptr(), ro.data_ptr(), base)
                 rows_h[a:a + m].copy_(rows_d[a:a + m], non_blocking=True)
@@ -506,32 +527,37 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
                 while len(pend) > 1:  # the previous chunk's hits, once its offsets are back
                     kk, e, last = pend.pop(0)
                     e.synchronize()
-                    nh = hit_n[kk] = int(ro_h[last])
+                    nh = hit_n[kk] = int(ro_h[last].numpy().view(np.uint32))
                     total_hits += nh
                     hits_h[kk][:nh].copy_(hits_d[kk][:nh], non_blocking=True)
             for kk, e, last in pend:
                 e.synchronize()
-                nh = hit_n[kk] = int(ro_h[last])
+                nh = hit_n[kk] = int(ro_h[last].numpy().view(np.uint32))
                 total_hits += nh
                 hits_h[kk][:nh].copy_(hits_d[kk][:nh], non_blocking=True)
             stream.synchronize()
             dt = time.perf_counter() - t0
             for bt in live:
+                bt.sync()  # (the passes' invariant words; outside the timed region)
                 bt.free()
             if p:
                 times.append(dt)
     gc.enable()
     dt = sorted(times)[len(times) // 2]  # the median pass (host threads make single passes noisy)
+    rows_w, _, _ = widen_compact(rows_h.numpy(), np.zeros(0, np.uint32), np.zeros(1, np.uint32))
+    hit_parts = [widen_compact(np.zeros((0, 4), np.uint32), hits_h[k][:hit_n[k]].numpy(), np.zeros(1, np.uint32))[1]
+                 for k in range(chunks)]
     return {'requests_per_s': round(n / dt, 1), 'ms_per_pass': round(dt * 1e3, 2),
             'mean_ms': round(sum(times) / len(times) * 1e3, 2), 'best_ms': round(min(times) * 1e3, 2),
             'pass_ms': [round(t * 1e3, 2) for t in times], 'passes': passes, 'chunks': chunks, 'workers': workers,
             'hits_returned': total_hits,
-            'digest': digest(rows_h.numpy(), [hits_h[k][:hit_n[k]].numpy() for k in range(chunks)]),
+            'd2h_bytes': int(16 * n + 4 * (n + chunks) + 4 * total_hits),
+            'digest': digest(rows_w, hit_parts),
             'note': f'pipelined: the requests cut into chunks of consecutive rows; {workers} host threads route + '
                     'prepare chunks ahead (sb_requests_prepare_beacon: Beacon int64 columns -> SplitQueryPayloads '
                     'cut to the core and packed in the library) while each prepared chunk runs and copies back '
-                    '(rows, per-chunk row offsets, dense hits into pinned host memory); everything inside the '
-                    'timed region'}
+                    '(compact rows, per-chunk u32 row offsets, u32 hits into pinned host memory); everything inside '
+                    'the timed region (digest over the widened outputs)'}
 
 
 def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20000, seed=7, timed=True):

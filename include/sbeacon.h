@@ -532,6 +532,19 @@ int sb_requests_time_eval(sb_batch *b, int on);
  * Replaces splitQuery's per-request fan-out (lambda/splitQuery/
  * lambda_function.py:74-110) as a device step. */
 int sb_requests_set_replan(sb_batch *b, int on);
+/* One row of the compact output (sb_requests_set_compact): the
+ * sb_request_partial sums as u32 (no error count: compact batches have no
+ * per-slice part, whose slices are the only ones that can raise). */
+typedef struct {
+    uint32_t exists, n_variants, call_count, all_alleles_count;
+} sb_request_row32;
+/* With on != 0, sb_requests_run writes the narrow form a host copy-back
+ * wants: dev_rows[n] as sb_request_row32 (16 B instead of 40), dev_row_off[n + 1]
+ * as uint32, and each hit as uint32 (record + rec_base) | ALT label << 29.
+ * SB_EINVAL for a batch with a per-slice part, or (at run) when record
+ * numbers reach 2^29; a count or offset past 32 bits fails the pass at
+ * sb_batch_sync (SB_EINTERNAL). */
+int sb_requests_set_compact(sb_batch *b, int on);
 /* After a pass (waits for it): flags[w] = 1 when row w's call_count or
  * all_alleles_count is not exact in int64 -- a slice's count past 64 bits
  * (Python ints, records answered by the general path) or a sum that

@@ -205,7 +205,7 @@ struct ReqPool {
     std::mutex mu;
     std::vector<Pinned> pinned;
     std::vector<DevMem> dev;
-    static constexpr size_t kKeep = 64;                      // buffers kept per kind at most
+    static constexpr size_t kKeep = 256;                     // buffers kept per kind at most (a pipelined caller holds ~10 per chunk batch)
     static constexpr size_t kKeepDevBytes = size_t(4) << 30;  // and bytes: the largest go first
     static constexpr size_t kKeepPinnedBytes = size_t(2) << 30;
     ~ReqPool() { trim(); }
@@ -370,6 +370,7 @@ struct sb_batch {
         DevMem din, rcap;
         uint32_t n_in = 0;
         bool replan = false;
+        bool compact = false;  // sb_requests_set_compact
         // request_eval_kernel's invariant word (sticky; checked at sync: SB_EINTERNAL)
         DevMem err;
         ReqPool::Pinned err_h;
@@ -761,8 +762,8 @@ void upload_store(sb_builder &b, sb_store &s) {
         std::vector<uint32_t> vcb;
         // candidates per bucket: a chain loads about this many outside its
         // window at each end (SBEACON_VC_BUCKET overrides)
-        double per_bucket = 2.0;
-        if (const char *e = std::getenv("SBEACON_VC_BUCKET")) per_bucket = std::max(1.0, std::atof(e));
+        double per_bucket = 1.0;  // round 5: 2 -> 1 (request eval 69.5 -> 66.7 us: ~15 % of its loads were bucket overfetch)
+        if (const char *e = std::getenv("SBEACON_VC_BUCKET")) per_bucket = std::max(0.25, std::atof(e));
         for (auto &v : b.vcfs) {
             v.vc_index.assign(v.segments.size(), std::array<VcIndex, kVtKinds>{});
             for (size_t g = 0; g < v.segments.size(); ++g) {
@@ -3993,6 +3994,8 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
         R.err_h = R.pool->get_pinned(16);
         HIP_OK(hipMemsetAsync(R.err.p, 0, 16, st));
     }
+    if (R.compact && rec_base + s.n_records > kStageCandMask)
+        throw Error(SB_EINVAL, "compact request output: record numbers (rec_base + records) reach 2^29");
     if (R.replan) {  // the planning kernels again, from the resident packed requests (same descriptors, same sizes)
         launch_request_plan(s.d, R.din.as<ReqIn>(), R.n_in, R.dchains.as<ReqChain>(),
                             reinterpret_cast<RowRun *>(R.dchains.as<char>() + R.runs_at), R.rcap.as<unsigned long long>(),
@@ -4017,7 +4020,7 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
                         R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
                         static_cast<ReqPartial *>(rows), static_cast<uint64_t *>(row_off), R.row_src.as<uint64_t>(),
                         R.stage.as<uint32_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
-                        R.err.as<unsigned int>(), st, ev[0], ev[1]);
+                        R.err.as<unsigned int>(), R.compact, st, ev[0], ev[1]);
     HIP_OK(hipGetLastError());
 }
 
@@ -4225,6 +4228,17 @@ int sb_requests_inexact_rows(sb_batch *b, uint8_t *flags) {
         HIP_OK(hipSetDevice(b->s->device));
         HIP_OK(hipStreamSynchronize(b->strm()));
         HIP_OK(hipMemcpy(flags, R.row_flag.p, R.n_rows, hipMemcpyDeviceToHost));
+    });
+}
+
+int sb_requests_set_compact(sb_batch *b, int on) {
+    return guard([&] {
+        if (!b || !b->req) throw Error(SB_EINVAL, "not a request batch");
+        if (on && b->req->slices)
+            throw Error(SB_EINVAL, "sb_requests_set_compact: the batch answers some rows per slice (wide rows only)");
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_set_compact between a run and its sync");
+        b->req->compact = on != 0;
     });
 }
 

@@ -469,6 +469,13 @@ struct ReqPartial {
     int64_t errors;  // slices whose performQuery raised
 };
 
+// A request row in the compact output (sb_requests_set_compact; the layout
+// of sb_request_row32): the ReqPartial sums as u32, no error count
+struct RowC {
+    uint32_t exists, n_variants, call_count, all_alleles_count;
+};
+static_assert(sizeof(RowC) == 16, "RowC is one 16-byte word");
+
 // hit = record | (alt index << 32); alt index is the label index (the GT
 // fallback labels with alts[i] for a 1-based i, search_variants.py:223)
 inline constexpr uint64_t kHitAltShift = 32;

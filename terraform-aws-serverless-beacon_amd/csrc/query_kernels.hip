@@ -2006,12 +2006,16 @@ struct ReqChunk {
     uint32_t k;  // the lane's chain
 };
 
-template <bool LDS_LUT>
+// COMPACT (sb_requests_set_compact): rows as RowC (16 B), row counts /
+// offsets as u32; only batches without a per-slice part (sres == nullptr)
+template <bool LDS_LUT, bool COMPACT>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_REQ_WAVES, SBEACON_REQ_WAVES))) void request_eval_kernel(
     DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
-    unsigned long long *__restrict__ status, const QRes *__restrict__ sres, ReqPartial *__restrict__ rows,
-    uint64_t *__restrict__ row_cnt, uint64_t *__restrict__ row_src, uint32_t *__restrict__ stage, uint32_t n_lut,
+    unsigned long long *__restrict__ status, const QRes *__restrict__ sres, void *__restrict__ rows_out,
+    void *__restrict__ row_cnt_out, uint64_t *__restrict__ row_src, uint32_t *__restrict__ stage, uint32_t n_lut,
     unsigned int *__restrict__ err) {
+    ReqPartial *const rows = static_cast<ReqPartial *>(rows_out);
+    uint64_t *const row_cnt = static_cast<uint64_t *>(row_cnt_out);
     __shared__ ReqLds lds_all[kWavesPerBlock];
     __shared__ uint32_t slut[LDS_LUT ? kReqLut : 1];
     ReqLds &L = lds_all[threadIdx.x >> 6];
@@ -2336,25 +2340,38 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
             if (ul == 0) atomicOr(err, 1u);
 #endif
     }
-    ReqPartial part{0, 0, 0, 0, 0};
     if (ul < R) {
         const bool slow = (L.slow[ul >> 5] >> (ul & 31u)) & 1u;  // never for prepared chains
         const uint64_t an_sum = anc ? static_cast<uint64_t>(acc_hr) * an_c : acc_an;
-        part = slow ? ReqPartial{0, static_cast<int64_t>(acc_nv), 0, 0, static_cast<int64_t>(nsl)}
-                    : ReqPartial{static_cast<int64_t>(acc_ex), static_cast<int64_t>(acc_nv),
-                                 static_cast<int64_t>(acc_cc), static_cast<int64_t>(an_sum), 0};
-        rows[rowk] = part;
+        if constexpr (COMPACT) {
+            // (counts past 32 bits or a slow chain: the batch fails at sync, SB_EINTERNAL)
+            if (slow || acc_cc > 0xffffffffull || an_sum > 0xffffffffull) atomicOr(err, 2u);
+            static_cast<RowC *>(rows_out)[rowk] = RowC{acc_ex, acc_nv, static_cast<uint32_t>(acc_cc),
+                                                       static_cast<uint32_t>(an_sum)};
+        } else {
+            rows[rowk] = slow ? ReqPartial{0, static_cast<int64_t>(acc_nv), 0, 0, static_cast<int64_t>(nsl)}
+                              : ReqPartial{static_cast<int64_t>(acc_ex), static_cast<int64_t>(acc_nv),
+                                           static_cast<int64_t>(acc_cc), static_cast<int64_t>(an_sum), 0};
+        }
     }
     // ---- rows (lane i < nrows = row row_lo + i): hit counts, staging starts
     const uint32_t row = row_lo + ul;
     const uint32_t ch = ul < nrows ? L.rowchain[ul] : 0xffu;
     const uint32_t chn = bperm(acc_nv, ch & 63u), chs = bperm(cs, ch & 63u);
     uint64_t nvr = 0;
-    if (ul < nrows) nvr = ch != 0xffu ? chn : (sres ? static_cast<uint64_t>(rows[row].n_variants) : 0ull);
-    if (!sres && ul < nrows && ch == 0xffu) rows[row] = ReqPartial{0, 0, 0, 0, 0};
-    if (ul < nrows) {
-        row_cnt[row] = nvr;
-        if (!simple && ch != 0xffu) row_src[row] = stage_at + chs;
+    if constexpr (COMPACT) {  // no per-slice part: a row without a chain has no slice (or no candidate)
+        if (ul < nrows) {
+            nvr = ch != 0xffu ? chn : 0u;
+            if (ch == 0xffu) static_cast<RowC *>(rows_out)[row] = RowC{0, 0, 0, 0};
+            static_cast<uint32_t *>(row_cnt_out)[row] = static_cast<uint32_t>(nvr);
+        }
+    } else {
+        if (ul < nrows) nvr = ch != 0xffu ? chn : (sres ? static_cast<uint64_t>(rows[row].n_variants) : 0ull);
+        if (!sres && ul < nrows && ch == 0xffu) rows[row] = ReqPartial{0, 0, 0, 0, 0};
+        if (ul < nrows) {
+            row_cnt[row] = nvr;
+            if (!simple && ch != 0xffu) row_src[row] = stage_at + chs;
+        }
     }
     const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(nvr)), kWave - 1));
     if (ul == 0) status[w] = H;  // read by the tile scan and request_deliver_kernel (kernel boundaries)
@@ -2542,17 +2559,28 @@ __global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned 
 // contiguous range for a run of chain rows; row by row where some rows were
 // answered per slice).  No inter-wave dependency.  (One wave per tile of 16
 // runs, or a look-back, left the chip mostly idle: ~2 k waves, 0.1 ms.)
+// COMPACT: row counts / offsets u32, hits u32 = (record + rec_base) | label
+// << kStageAltShift (the host checks records + rec_base < 2^29; an offset
+// past 32 bits fails the batch at sync)
+template <bool COMPACT>
 __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const RowRun *__restrict__ runs, uint32_t n_runs, const unsigned long long *__restrict__ status,
     const unsigned long long *__restrict__ toff, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
     const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr, const uint64_t *__restrict__ shits,
-    uint64_t *__restrict__ row_off, const uint64_t *__restrict__ row_src, const uint32_t *__restrict__ stage,
-    const uint32_t *__restrict__ vc_idx, uint64_t *__restrict__ out, uint32_t n_rows, uint64_t rec_base) {
+    void *__restrict__ row_off_out, const uint64_t *__restrict__ row_src, const uint32_t *__restrict__ stage,
+    const uint32_t *__restrict__ vc_idx, void *__restrict__ out_v, uint32_t n_rows, uint64_t rec_base,
+    unsigned int *__restrict__ err) {
+    using Hit = std::conditional_t<COMPACT, uint32_t, uint64_t>;
+    Hit *const out = static_cast<Hit *>(out_v);
+    Hit *const row_off = static_cast<Hit *>(row_off_out);  // (counts in, offsets out: the hits' width)
     // a staged hit (candidate | ALT label << kStageAltShift) as the output's
     // (record + rec_base) | label << kHitAltShift
-    auto hit_of = [&](uint32_t v) -> uint64_t {
-        return (static_cast<uint64_t>(vc_idx[v & kStageCandMask]) + rec_base) |
-               static_cast<uint64_t>(v >> kStageAltShift) << kHitAltShift;
+    auto hit_of = [&](uint32_t v) -> Hit {
+        if constexpr (COMPACT)
+            return (vc_idx[v & kStageCandMask] + static_cast<uint32_t>(rec_base)) | (v & ~kStageCandMask);
+        else
+            return (static_cast<uint64_t>(vc_idx[v & kStageCandMask]) + rec_base) |
+                   static_cast<uint64_t>(v >> kStageAltShift) << kHitAltShift;
     };
     const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     if (w >= n_runs) return;
@@ -2563,17 +2591,20 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const uint64_t stage_at = uniform64(rr.stage);
     const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
     const uint32_t row = row_lo + ul;
-    const uint64_t c = row < row_hi ? row_off[row] : 0ull;  // the counts request_eval_kernel left
+    const uint64_t c = row < row_hi ? static_cast<uint64_t>(row_off[row]) : 0ull;  // the counts request_eval_kernel left
     const uint64_t before = t0 + ul < w ? status[t0 + ul] : 0ull;
     const uint64_t O = uniform64(toff[w / kDeliverTile]) +
                        static_cast<uint64_t>(rdl64(wave_incl_scan_i64(static_cast<int64_t>(before)), kWave - 1));
     const uint64_t linc = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(c)));
     const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(linc), kWave - 1));
     const uint64_t off = O + linc - c;
-    if (row < row_hi) row_off[row] = off;
-    if (row_hi == n_rows && ul == 0) row_off[n_rows] = O + H;
+    if constexpr (COMPACT) {
+        if (ul == 0 && O + H > 0xffffffffull) atomicOr(err, 2u);
+    }
+    if (row < row_hi) row_off[row] = static_cast<Hit>(off);
+    if (row_hi == n_rows && ul == 0) row_off[n_rows] = static_cast<Hit>(O + H);
     if (simple) {  // chain rows (and empty rows) only: the staging region is the output, in order
-        constexpr uint32_t kU = 4;
+        constexpr uint32_t kU = 8;  // 512 hits per round: most runs in one (~480 hits per run)
         for (uint64_t j0 = 0; j0 < H; j0 += kWave * kU) {
             uint32_t v[kU];
 #pragma unroll
@@ -2581,7 +2612,7 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
                 const uint64_t j = j0 + kWave * u + ul;
                 v[u] = j < H ? stage[stage_at + j] : 0u;
             }
-            uint64_t h[kU];
+            Hit h[kU];
 #pragma unroll
             for (uint32_t u = 0; u < kU; ++u) h[u] = hit_of(v[u]);
 #pragma unroll
@@ -2592,6 +2623,7 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
         }
         return;
     }
+    if constexpr (COMPACT) return;  // (compact batches have no per-slice part: every run is simple)
     for (uint32_t i = 0; i < row_hi - row_lo; ++i) {  // row by row (some rows answered per slice)
         const uint64_t nv = static_cast<uint64_t>(rdl64(static_cast<int64_t>(c), i));
         if (!nv) continue;
@@ -3796,25 +3828,36 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
-                         hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+                         bool compact, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     if (!n_runs) {
-        (void)hipMemsetAsync(row_off, 0, 8, s);
+        (void)hipMemsetAsync(row_off, 0, compact ? 4 : 8, s);
         return;
     }
     const dim3 grid(blocks_for(n_runs));
     const uint32_t n_tiles = request_tiles(n_runs);
     if (ev0) (void)hipEventRecord(ev0, s);
     auto eval = [&](auto kern) {
-        hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres, rows, row_off,
-                           row_src, stage, n_lut, err);
+        hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
+                           static_cast<void *>(rows), static_cast<void *>(row_off), row_src, stage, n_lut, err);
     };
     (void)run;
-    if (n_lut <= kReqLut) eval(request_eval_kernel<true>);
-    else eval(request_eval_kernel<false>);
+    if (compact) {
+        if (n_lut <= kReqLut) eval(request_eval_kernel<true, true>);
+        else eval(request_eval_kernel<false, true>);
+    } else {
+        if (n_lut <= kReqLut) eval(request_eval_kernel<true, false>);
+        else eval(request_eval_kernel<false, false>);
+    }
     if (ev1) (void)hipEventRecord(ev1, s);
     hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, status, n_runs, tstatus, n_tiles);
-    hipLaunchKernelGGL(request_deliver_kernel, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg,
-                       shoff, sherr, shits, row_off, row_src, stage, st.vc_idx, out, n_rows, rec_base);
+    if (compact)
+        hipLaunchKernelGGL(request_deliver_kernel<true>, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres,
+                           sseg, shoff, sherr, shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx,
+                           static_cast<void *>(out), n_rows, rec_base, err);
+    else
+        hipLaunchKernelGGL(request_deliver_kernel<false>, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres,
+                           sseg, shoff, sherr, shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx,
+                           static_cast<void *>(out), n_rows, rec_base, err);
 }
 
 void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,

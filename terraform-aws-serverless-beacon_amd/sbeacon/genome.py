@@ -519,15 +519,37 @@ def shard_rows(shape: GenomeShape, reqs: Requests, world: int, rank: int) -> tup
     s1 = int(np.searchsorted(ci, c1, side='left'))
     plan = shape.plan(world)
     firsts, lasts = [], []
+
+    def has(x0, x1):  # rows [x0, x1) of the cut contig's rows: a slice on rank?
+        smin = reqs.start[r0 + x0:r0 + x1] + 1
+        aa, bb = plan.slice_runs(rank, 0, ci[x0:x1], smin, smin + reqs.width[r0 + x0:r0 + x1])
+        return bb >= aa
+
     for x0, x1 in ([(0, n)] if c0 == c1 else [(0, e0), (s1, n)]):
         if x1 <= x0:
             continue
-        smin = reqs.start[r0 + x0:r0 + x1] + 1
-        aa, bb = plan.slice_runs(rank, 0, ci[x0:x1], smin, smin + reqs.width[r0 + x0:r0 + x1])
-        has = bb >= aa
-        if has.any():
-            firsts.append(x0 + int(np.argmax(has)))
-            lasts.append(x0 + len(has) - int(np.argmax(has[::-1])))
+        # only the first and the last row with a slice matter: grow a window
+        # from each end (a pipelined caller prepares ~125 k-row chunks, and
+        # the whole cut contig through slice_runs cost ~0.3 ms per chunk)
+        k, f = 64, None
+        while f is None:
+            hh = has(x0, min(x1, x0 + k))
+            if hh.any():
+                f = x0 + int(np.argmax(hh))
+            elif x0 + k >= x1:
+                break
+            k *= 4
+        if f is None:
+            continue
+        k, l = 64, None
+        while l is None:
+            a = max(f, x1 - k)
+            hh = has(a, x1)
+            if hh.any():
+                l = a + len(hh) - int(np.argmax(hh[::-1]))
+            k *= 4
+        firsts.append(f)
+        lasts.append(l)
     if e0 < s1 and c0 != c1:
         firsts.append(e0)
         lasts.append(s1)

@@ -331,6 +331,13 @@ class RequestBatch:
         batches only)."""
         check(lib().sb_requests_set_replan(self._h, 1 if on else 0))
 
+    def set_compact(self, on: bool):
+        """Narrow outputs (sb_requests_set_compact): rows [n, 4] uint32
+        (exists, n_variants, call_count, all_alleles_count), n + 1 uint32
+        row offsets, uint32 hits (record + rec_base) | ALT label << 29."""
+        check(lib().sb_requests_set_compact(self._h, 1 if on else 0))
+        self.compact = bool(on)
+
     def inexact_rows(self) -> np.ndarray:
         """After a pass: True for rows whose call_count / all_alleles_count
         are not exact in int64 (low 64 bits held; sb_requests_inexact_rows)."""
@@ -360,9 +367,19 @@ class RequestBatch:
     def answer(self, rec_base: int = 0, device=None):
         """One pass, rows + hit lists copied to the host (torch tensors on
         the store's device as staging): (rows [n, 5] int64, hits uint64,
-        row_off [n + 1] int64)."""
+        row_off [n + 1] int64) -- in the wide form whichever output form the
+        batch writes (compact outputs widened by widen_compact)."""
         import torch
         dev = device if device is not None else torch.device('cuda', self.store.info()['device'])
+        if getattr(self, 'compact', False):
+            rows = torch.zeros((max(self.n, 1), 4), dtype=torch.int32, device=dev)
+            hits = torch.zeros(max(int(self.stats()['hits']), 1), dtype=torch.int32, device=dev)
+            row_off = torch.zeros(self.n + 1, dtype=torch.int32, device=dev)
+            self.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            self.run(rows.data_ptr(), hits.data_ptr(), row_off.data_ptr(), rec_base)
+            self.sync()
+            ro = row_off.cpu().numpy().view(np.uint32)
+            return widen_compact(rows[:self.n].cpu().numpy().view(np.uint32), hits[:int(ro[-1])].cpu().numpy(), ro)
         rows = torch.zeros((max(self.n, 1), 5), dtype=torch.int64, device=dev)
         hits = torch.zeros(max(int(self.stats()['hits']), 1), dtype=torch.int64, device=dev)
         row_off = torch.zeros(self.n + 1, dtype=torch.int64, device=dev)
@@ -371,3 +388,15 @@ class RequestBatch:
         self.sync()
         ro = row_off.cpu().numpy()
         return rows[:self.n].cpu().numpy(), hits[:int(ro[-1])].cpu().numpy().view(np.uint64), ro
+
+
+def widen_compact(rows32, hits32, row_off32):
+    """Compact request outputs (sb_requests_set_compact) in the wide form:
+    (rows [n, 5] int64 with a zero error count, hits uint64 = record | ALT
+    label << 32, row_off int64)."""
+    rows32 = np.asarray(rows32).view(np.uint32).reshape(-1, 4)
+    rows = np.zeros((len(rows32), 5), dtype=np.int64)
+    rows[:, :4] = rows32
+    h = np.asarray(hits32).view(np.uint32).astype(np.uint64)
+    hits = (h & np.uint64((1 << 29) - 1)) | ((h >> np.uint64(29)) << np.uint64(32))
+    return rows, hits, np.asarray(row_off32).view(np.uint32).astype(np.int64)

@@ -360,4 +360,16 @@ def test_device_planned_requests_match_host_planned():
         np.testing.assert_array_equal(hits_r, hits_h)
     with pytest.raises(_lib.SbError):
         host_b.set_replan(True)  # planned on the host: nothing to re-plan from
+    # the compact output form (u32 rows, offsets and hits), widened on the host: the same answers
+    for b in (dev_b, host_b):
+        if b.stats()['n_queries']:  # some rows answered per slice: wide rows only
+            with pytest.raises(_lib.SbError):
+                b.set_compact(True)
+            continue
+        b.set_compact(True)
+        rows_c, hits_c, ro_c = b.answer()
+        np.testing.assert_array_equal(rows_c, rows_h)
+        np.testing.assert_array_equal(ro_c, ro_h)
+        np.testing.assert_array_equal(hits_c, hits_h)
+        b.set_compact(False)
     del keep, dev_b, host_b

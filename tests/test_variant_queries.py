@@ -7,7 +7,9 @@ poll, yield in response-number order), performQuery's async tail
 CPU: the fan-in bookkeeping with the device batch replaced by a stub (the
 coordinates, fan-out sizes, response numbering, the poll's completion and
 timeout, the 300 KB checkS3 mark, the handler's SNS path recording).  GPU:
-the same search on a real store yields what perform_variant_search_sync
+the same search on a real store yields, slice for slice, what the C oracle
+(oracle/sbeacon_oracle.c, pinned to the reference goldens) answers for the
+payloads the fan-out published, and what perform_variant_search_sync
 returns."""
 import json
 import os
@@ -103,23 +105,57 @@ def test_sns_handler_records_its_response(monkeypatch):
 
 
 @pytest.mark.gpu
-def test_async_search_matches_sync_on_device():
-    from sbeacon import engine
+@pytest.mark.parametrize('kw', [dict(referenceBases='N', alternateBases='N'),
+                                dict(referenceBases='N', alternateBases=None, variantType='DEL'),
+                                dict(referenceBases='N', alternateBases=None, variantType='INS', variantMaxLength=20),
+                                dict(requestedGranularity='boolean', includeResultsetResponses='NONE')])
+def test_async_search_matches_oracle_on_device(kw):
+    """The async fan-in (search_variants.py:27-155 + performQuery's SNS tail
+    :273-317) on the device: every slice response it yields equals the C
+    oracle's answer to the payload it published (variantType payloads: the
+    patched-oracle intent, as the goldens), and the multiset equals the
+    sync search's."""
+    sys.path.insert(0, REPO)
+    from oracle.oracle import OracleVcf
+    from sbeacon import engine, perform_query
     from sbeacon.engine import Store
     from sbeacon.variant_queries import perform_variant_search
     from sbeacon.variant_search import perform_variant_search_sync
     fx = os.path.join(FIXTURES, 'tiny22.vcf')
     store = Store.build([('tiny22.vcf', fx)], device=0)
     engine.registry.register(store)
+    published = []
+    real = perform_query.perform_query_batch
+
+    def spy(payloads, **k):
+        published.extend(payloads)
+        return real(payloads, **k)
+    orc = OracleVcf(fx)
     try:
         ds = [_DS('d1', ['tiny22.vcf'])]
         ds[0]._vcfChromosomeMap = [{'vcf': 'tiny22.vcf', 'chromosomes': ['22']}]
-        kw = dict(KW, start=[16050000], end=[16110000])
-        sync = perform_variant_search_sync(datasets=ds, **kw)
-        got = list(perform_variant_search(datasets=ds, query_id='q-dev', timeout=60, **kw))
-        key = lambda r: json.dumps(r.dump(), sort_keys=True)  # noqa: E731
-        assert len(sync) == len(got) > 1
-        assert sorted(map(key, sync)) == sorted(map(key, got))
-        assert any(r.exists for r in got)
+        args = dict(KW, start=[16050000], end=[16110000])
+        args.update(kw)
+        sync = perform_variant_search_sync(datasets=ds, **args)
+        perform_query.perform_query_batch = spy
+        got = list(perform_variant_search(datasets=ds, query_id=f'q-dev-{len(published)}-{id(kw)}', timeout=60,
+                                          **args))
+        key = lambda d: json.dumps(d, sort_keys=True)  # noqa: E731
+        assert len(published) == len(got) > 1
+        exp = []
+        for p in published:
+            e = orc.perform_query(p, patched=p.get('variant_type') is not None)
+            e['sample_indices'] = sorted(e['sample_indices'])
+            exp.append(key(e))
+        dumps = []
+        for r in got:
+            d = r.dump()
+            d['sample_indices'] = sorted(d['sample_indices'])
+            dumps.append(key(d))
+        assert sorted(dumps) == sorted(exp)
+        assert sorted(dumps) == sorted(key(dict(r.dump(), sample_indices=sorted(r.dump()['sample_indices'])))
+                                       for r in sync)
     finally:
+        perform_query.perform_query_batch = real
+        orc.close()
         engine.registry.clear()
