@@ -27,6 +27,7 @@
 
 #include <zlib.h>
 
+#include "config.hpp"
 #include "jsonesc.hpp"
 #include "kernels.hpp"
 #include "store.hpp"
@@ -689,8 +690,7 @@ void upload_store(sb_builder &b, sb_store &s) {
             }
             v.an_default = mode;
             // SBEACON_NO_RANGE8=1 keeps every VCF on RangeHot (tests cover both paths)
-            const char *no8e = std::getenv("SBEACON_NO_RANGE8");
-            const bool no8 = no8e && no8e[0] == '1';
+            const bool no8 = config().no_range8;
             v.range8 = !no8 && slow * 50 <= hit;
         }
         s.d.rng8 = dev_upload(s, rng8);
@@ -763,7 +763,7 @@ void upload_store(sb_builder &b, sb_store &s) {
         // candidates per bucket: a chain loads about this many outside its
         // window at each end (SBEACON_VC_BUCKET overrides)
         double per_bucket = 1.0;  // round 5: 2 -> 1 (request eval 69.5 -> 66.7 us: ~15 % of its loads were bucket overfetch)
-        if (const char *e = std::getenv("SBEACON_VC_BUCKET")) per_bucket = std::max(0.25, std::atof(e));
+        per_bucket = config().vc_bucket;
         for (auto &v : b.vcfs) {
             v.vc_index.assign(v.segments.size(), std::array<VcIndex, kVtKinds>{});
             for (size_t g = 0; g < v.segments.size(); ++g) {
@@ -1123,8 +1123,7 @@ namespace {
 std::vector<uint32_t> plan_chains(sb_batch &B, const std::vector<uint32_t> &segi, const std::vector<uint32_t> &vt) {
     sb_store &s = *B.s;
     std::vector<uint32_t> rest;
-    const char *off = std::getenv("SBEACON_NO_CHAINS");
-    if ((off && off[0] == '1') || B.no_chains) return vt;
+    if (config().no_chains || B.no_chains) return vt;
     struct Ch {
         std::vector<uint32_t> m;
         int64_t first = 0, last = 0, width = 0;
@@ -1285,7 +1284,7 @@ std::vector<uint32_t> plan_chains(sb_batch &B, const std::vector<uint32_t> &segi
 void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     sb_store &s = *B.s;
     if (nq >= (1u << 31)) throw Error(SB_EINVAL, "batch too large");
-    static const bool trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;  // phase times (bench diagnostics)
+    static const bool trace = config().wire_trace;  // phase times (bench diagnostics)
     auto t_last = std::chrono::steady_clock::now();
     auto tick = [&](const char *what) {
         if (!trace) return;
@@ -1642,8 +1641,8 @@ void prepare(sb_batch &B, const sb_query *qs, size_t nq) {
     B.hruns.clear();
     {
         uint32_t slots = 0, cnt = 0, run_max = pack_run_max();
-        if (const char *e = std::getenv("SBEACON_PACK_RUN"))  // A/B: shorter runs
-            run_max = std::max(1u, std::min(run_max, static_cast<uint32_t>(std::atoi(e))));
+        if (const int k = config().pack_run)  // A/B: shorter runs
+            run_max = std::max(1u, std::min(run_max, static_cast<uint32_t>(k)));
         for (uint32_t c = 0; c < B.hchains.size(); ++c) {
             const uint32_t n = B.hchains[c].n;
             if (cnt == 0 || cnt == run_max || slots + n > pack_slots_max()) {
@@ -2258,7 +2257,7 @@ struct WinPlan {
 
 bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan &P) {
     uint32_t target = kWinTarget;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
-    if (const char *e = std::getenv("SBEACON_DEDUP_WIN_TARGET")) target = std::max(1, std::min(static_cast<int>(kWinCap), std::atoi(e)));
+    if (const int k = config().dedup_win_target) target = std::max(1, std::min(static_cast<int>(kWinCap), k));
     if (s.n_keys >= 0x80000000ull) return P.why = "2^31 keys", false;
     std::vector<char> seen(nj, 0);
     for (size_t g0 = 0; g0 < runs.size();) {
@@ -2321,7 +2320,7 @@ struct WinWs {
 bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t nj, uint64_t *unique,
                       const int32_t *status, sb_dedup_stats *stats) {
     WinPlan P;
-    const bool dbg = std::getenv("SBEACON_DEDUP_DEBUG") != nullptr;
+    const bool dbg = config().dedup_debug;
     const auto t0 = std::chrono::steady_clock::now();
     auto since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
     if (!plan_windows(s, runs, nj, P)) {
@@ -2403,17 +2402,16 @@ void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj
     if (n >= 0xffffffffull) throw Error(SB_EINVAL, "dedup batch exceeds 2^32 keys; split it");
     {
         // SBEACON_DEDUP_EXACT=bucket / radix (tests, A/B) skip the window path
-        const char *exm = std::getenv("SBEACON_DEDUP_EXACT");
-        const bool hash_hook = std::getenv("SBEACON_DEDUP_HASH_BITS") != nullptr;
-        if (runs && !force_radix && !hash_hook && !(exm && (exm[0] == 'r' || exm[0] == 'b')) &&
+        const Config cf = config();
+        const bool hash_hook = cf.dedup_hash_bits != 0;
+        if (runs && !force_radix && !hash_hook && !cf.dedup_exact &&
             dedup_window_run(s, *runs, n, nj, unique, status, stats))
             return;
     }
     uint32_t job_bits = 0;
     while ((1ull << job_bits) < nj) ++job_bits;
     uint64_t mask = ~0ull;
-    if (const char *e = getenv("SBEACON_DEDUP_HASH_BITS")) {  // test hook: force collisions
-        const int b = atoi(e);
+    if (const int b = config().dedup_hash_bits) {  // test hook: force collisions
         if (b > 0 && b < 64) mask = (1ull << b) - 1;
     }
     // exact-word window: POS - rangeStart of every gathered key fits pos_bits
@@ -2475,8 +2473,7 @@ void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj
     // an LDS hash set per workgroup; SBEACON_DEDUP_EXACT=radix forces the
     // full sort) or as many 8-bit radix passes as its words have bits + an
     // adjacent-unique pass; the first pass compacts the gather tiles
-    const char *exm = std::getenv("SBEACON_DEDUP_EXACT");
-    const bool bucket = !force_radix && !(exm && exm[0] == 'r') && ne > 0;
+    const bool bucket = !force_radix && config().dedup_exact != 'r' && ne > 0;
     const uint32_t be = bucket ? 0u : dedup_unique_blocks(ne), bh = bucket ? 0u : dedup_unique_blocks(nh);
     pe.reserve(std::max<uint32_t>(be, 1) * sizeof(uint4));
     ph.reserve(std::max<uint32_t>(bh, 1) * sizeof(uint4));
@@ -2891,7 +2888,7 @@ void dedup_files(sb_store &s, const sb_dedup_file_job *jobs, size_t nj, uint64_t
     // each pair's entries as the reference reader returns them: from the
     // file's profile (two binary searches), or by the walk itself for an
     // unsorted file; SBEACON_STRICT_CHECK=1 (tests) runs both and compares
-    const bool check = std::getenv("SBEACON_STRICT_CHECK") != nullptr;
+    const bool check = config().strict_check;
     std::atomic<bool> mismatch{false};
     parallel_for(pairs.size(), [&](size_t p) {
         Pair &P = pairs[p];
@@ -3210,7 +3207,7 @@ int sb_builder_attach_carriers(sb_builder *b, uint32_t vcf_id, const char *const
 int sb_builder_finish(sb_builder *b, int device, sb_store **out) {
     return guard([&] {
         if (!b || !out) throw Error(SB_EINVAL, "NULL argument");
-        const bool trace = std::getenv("SBEACON_INGEST_TRACE") != nullptr;  // phase times to stderr
+        const bool trace = config().ingest_trace;  // phase times to stderr
         const auto t0 = std::chrono::steady_clock::now();
         for (uint32_t i = 0; i < b->vcfs.size(); ++i) builder_flush(*b, i);
         const auto t1 = std::chrono::steady_clock::now();
@@ -3590,7 +3587,7 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     const bool collect = (c.granularity_all == SB_GRAN_RECORD || c.granularity_all == SB_GRAN_AGGREGATED) &&
                          c.include_samples_all;
     if (collect && v.words) return false;
-    const bool trace = std::getenv("SBEACON_PREP_TRACE") != nullptr;
+    const bool trace = config().prep_trace;
     auto t_last = std::chrono::steady_clock::now();
     auto tick = [&](const char *what) {
         if (!trace) return;
@@ -3753,7 +3750,7 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     auto R = std::make_unique<sb_batch::Req>();
     R->n_rows = static_cast<uint32_t>(n);
     // SBEACON_PREP_TRACE=1: host phase times to stderr (bench diagnostics)
-    const bool trace = std::getenv("SBEACON_PREP_TRACE") != nullptr;
+    const bool trace = config().prep_trace;
     auto t_last = std::chrono::steady_clock::now();
     auto tick = [&](const char *what) {
         if (!trace) return;
@@ -4438,7 +4435,7 @@ int sb_batch_deliver(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_
                                b->res.as<QRes>(), b->herr.as<uint8_t>(), b->poff.as<uint32_t>(),
                                b->piece.as<uint32_t>(), b->n_rows, static_cast<ReqPartial *>(dev_rows),
                                b->rowsrc.as<ulonglong2>(),
-                               std::getenv("SBEACON_NO_ROWOUT") ? nullptr : b->rowout.as<uint64_t>(),  // A/B knob
+                               config().no_rowout ? nullptr : b->rowout.as<uint64_t>(),  // A/B knob
                                b->nvs.as<int64_t>(), b->tsum.as<uint64_t>(),
                                b->hits.as<uint64_t>(), rec_base, static_cast<uint64_t *>(dev_row_off),
                                static_cast<uint64_t *>(dev_hits), b->strm());
@@ -4527,7 +4524,7 @@ int sb_query_batch(sb_store *s, const sb_query *q, size_t nq, uint32_t flags, sb
     return guard([&] {
         if (!s || (!q && nq) || !out) throw Error(SB_EINVAL, "NULL argument");
         std::lock_guard<std::mutex> lk(s->mu);
-        static const bool trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;  // phase times (bench diagnostics)
+        static const bool trace = config().wire_trace;  // phase times (bench diagnostics)
         auto t0 = std::chrono::steady_clock::now();
         auto tick = [&](const char *what) {
             if (!trace) return;

@@ -27,6 +27,7 @@
 #include <algorithm>
 #include <cstdlib>
 
+#include "config.hpp"
 #include "kernels.hpp"
 
 namespace sb {
@@ -1101,10 +1102,9 @@ int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1,
     // SBEACON_DEDUP_BUCKET_CAP (tests): a smaller cap forces the overflow fallback
     const uint32_t slots = v0 ? 4096u : kBSlots;
     uint32_t cap = slots * 3 / 4;
-    if (const char *e = std::getenv("SBEACON_DEDUP_BUCKET_CAP")) cap = std::min<uint32_t>(cap, static_cast<uint32_t>(std::atoi(e)));
+    if (const int k = config().dedup_bucket_cap) cap = std::min<uint32_t>(cap, static_cast<uint32_t>(k));
     const uint32_t njl = nj < 256 ? nj : 256u;
-    const char *dbge = std::getenv("SBEACON_DEDUP_BUCKET_DBG");
-    const uint32_t dbg = dbge ? static_cast<uint32_t>(std::atoi(dbge)) : 0u;
+    const uint32_t dbg = static_cast<uint32_t>(config().dedup_bucket_dbg);
     if (v0)
         bucket_dedupe_kernel<true, 4096><<<nb, kThreads, 0, s>>>(keys, vals, n, ks, job_shift, njl, counts, overflow, cap,
                                                                  dbg);
@@ -1118,8 +1118,7 @@ void launch_window_dedupe(const KStore &ks, const KJob *jobs, uint32_t nj, KWin 
                           const KRun *runs, unsigned long long *counts, uint2 *list, uint32_t *n_list, uint32_t cap,
                           uint32_t *overflow, uint32_t *wfresh, hipStream_t s) {
     if (!nw) return;
-    const char *dbge = std::getenv("SBEACON_DEDUP_WIN_DBG");  // timing ablations (never set by the benches)
-    const uint32_t dbg = dbge ? static_cast<uint32_t>(std::atoi(dbge)) : 0u;
+    const uint32_t dbg = static_cast<uint32_t>(config().dedup_win_dbg);  // timing ablations (never set by the benches)
     dedup_plan_kernel<<<(nw + kThreads - 1) / kThreads, kThreads, 0, s>>>(ks, jobs, nj, runs, nw, wins, E);
     window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, wins, E, counts, list, n_list, cap, overflow, wfresh, dbg);
     window_fold_kernel<<<(nj * 64 + kThreads - 1) / kThreads, kThreads, 0, s>>>(jobs, nj, runs, wfresh, counts);

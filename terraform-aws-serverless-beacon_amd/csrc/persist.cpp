@@ -18,6 +18,7 @@
 //   <dir>/host.bin       host columns + VCF metadata + kernel views
 //   <dir>/device.bin     the device buffers, back to back (4 KiB aligned)
 #include <hip/hip_runtime.h>
+#include <dirent.h>
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -49,7 +50,7 @@
 namespace sb {
 
 constexpr uint64_t kMagic = 0x3150544f5453424full;  // "OBSTOTP1"
-constexpr uint32_t kFormat = 3;  // 2: dedup class words carry tail ids; 3: VcIndex::xinfo
+constexpr uint32_t kFormat = 4;  // 2: dedup class words carry tail ids; 3: VcIndex::xinfo; 4: view sizes + pointer table
 
 // FNV-1a over the first and last 64 KiB (with the size and mtime, a change
 // detector -- not a content address)
@@ -109,12 +110,20 @@ void run_jobs(std::vector<std::pair<size_t, std::function<void()>>> &jobs, unsig
 struct Writer {
     FILE *f = nullptr;
     uint64_t at = 0;
-    explicit Writer(const std::string &path) {
+    std::string path;
+    explicit Writer(const std::string &p) : path(p) {
         f = fopen(path.c_str(), "wb");
         if (!f) throw Error(SB_EIO, "cannot write " + path);
     }
     ~Writer() {
-        if (f) fclose(f);
+        if (f) fclose(f);  // (an error path: close() reports the normal one)
+    }
+    // flush + close, every failure an SB_EIO (ENOSPC in the final flush included)
+    void close() {
+        const bool ok = fflush(f) == 0 && fsync(fileno(f)) == 0;
+        const int rc = fclose(f);
+        f = nullptr;
+        if (!ok || rc != 0) throw Error(SB_EIO, "cannot finish writing " + path);
     }
     void raw(const void *p, size_t n) {
         if (n && fwrite(p, 1, n, f) != n) throw Error(SB_EIO, "short write");
@@ -336,6 +345,49 @@ uint64_t *words(T &v) {
     static_assert(sizeof(T) % 8 == 0, "views are 8-byte multiples");
     return reinterpret_cast<uint64_t *>(&v);
 }
+template <class T>
+const uint64_t *words(const T &v) {
+    return reinterpret_cast<const uint64_t *>(&v);
+}
+
+// The views' pointer words, classified once at save: (view, word, buffer,
+// offset) for every word that points into -- or one past the end of -- a
+// device buffer (strict containment wins over an end pointer).  Open remaps
+// exactly these words; no word is guessed at from its value on open.
+struct RemapEntry {
+    uint32_t view, word, buf, pad;
+    uint64_t off;
+};
+std::vector<RemapEntry> remap_table(const sb_store &s) {
+    std::vector<RemapEntry> out;
+    auto scan = [&](uint32_t view, const uint64_t *w, size_t n) {
+        for (size_t i = 0; i < n; ++i) {
+            if (!w[i]) continue;
+            int end_hit = -1;
+            bool done = false;
+            for (size_t b = 0; b < s.bufs.size() && !done; ++b) {
+                const uint64_t base = reinterpret_cast<uint64_t>(s.bufs[b].p), bytes = s.bufs[b].bytes;
+                if (w[i] >= base && w[i] < base + bytes) {
+                    out.push_back(RemapEntry{view, static_cast<uint32_t>(i), static_cast<uint32_t>(b), 0, w[i] - base});
+                    done = true;
+                } else if (w[i] == base + bytes && end_hit < 0) {
+                    end_hit = static_cast<int>(b);
+                }
+            }
+            if (!done && end_hit >= 0)
+                out.push_back(RemapEntry{view, static_cast<uint32_t>(i), static_cast<uint32_t>(end_hit), 0,
+                                         s.bufs[end_hit].bytes});
+        }
+    };
+    scan(0, words(s.d), sizeof(DStore) / 8);
+    scan(1, words(s.ds), sizeof(SStore) / 8);
+    scan(2, words(s.dk), sizeof(KStore) / 8);
+    scan(3, words(s.g), sizeof(GStore) / 8);
+    return out;
+}
+// the views' layout as saved: sizes (a changed struct without a kFormat bump
+// is refused instead of misread)
+constexpr uint64_t kViewSizes[4] = {sizeof(DStore), sizeof(SStore), sizeof(KStore), sizeof(GStore)};
 
 std::string manifest_text(const sb_store &s, uint64_t host_bytes, uint64_t device_bytes) {
     std::string o = "{\n  \"format\": " + std::to_string(kFormat) + ",\n  \"abi\": " + std::to_string(SB_ABI_VERSION) +
@@ -365,8 +417,46 @@ std::string manifest_text(const sb_store &s, uint64_t host_bytes, uint64_t devic
 
 }  // namespace
 
-void store_save(sb_store &s, const std::string &dir) {
-    mkdir(dir.c_str(), 0755);
+namespace {
+void save_files(sb_store &s, const std::string &dir);
+void remove_tree(const std::string &d) {  // a save directory: plain files only
+    if (DIR *x = opendir(d.c_str())) {
+        while (const dirent *e = readdir(x))
+            if (std::strcmp(e->d_name, ".") && std::strcmp(e->d_name, "..")) (void)unlink((d + "/" + e->d_name).c_str());
+        closedir(x);
+    }
+    (void)rmdir(d.c_str());
+}
+}  // namespace
+
+// The three files are written into `dir.tmp` and the directory renamed into
+// place: a crash mid-save leaves the previous save (or none), never a new
+// device.bin beside an old host.bin.
+void store_save(sb_store &s, const std::string &dir_in) {
+    std::string dir = dir_in;
+    while (dir.size() > 1 && dir.back() == '/') dir.pop_back();
+    const std::string tmp = dir + ".tmp", prev = dir + ".old";
+    remove_tree(tmp);
+    if (mkdir(tmp.c_str(), 0755) != 0) throw Error(SB_EIO, "cannot create " + tmp);
+    try {
+        save_files(s, tmp);
+    } catch (...) {
+        remove_tree(tmp);
+        throw;
+    }
+    struct stat st {};
+    const bool had = stat(dir.c_str(), &st) == 0;
+    remove_tree(prev);
+    if (had && rename(dir.c_str(), prev.c_str()) != 0) throw Error(SB_EIO, "cannot replace " + dir);
+    if (rename(tmp.c_str(), dir.c_str()) != 0) {
+        if (had) (void)rename(prev.c_str(), dir.c_str());
+        throw Error(SB_EIO, "cannot move " + tmp + " to " + dir);
+    }
+    if (had) remove_tree(prev);
+}
+
+namespace {
+void save_files(sb_store &s, const std::string &dir) {
     if (s.device >= 0) {
         HIP_OK(hipSetDevice(s.device));
         HIP_OK(hipStreamSynchronize(s.stream));
@@ -394,8 +484,10 @@ void store_save(sb_store &s, const std::string &dir) {
         }
         (void)hipHostFree(pin);
         dev_bytes = w.at;
+        w.close();
     } else {
         Writer w(dir + "/device.bin");  // empty: no device image
+        w.close();
     }
     uint64_t host_bytes = 0;
     {
@@ -416,7 +508,9 @@ void store_save(sb_store &s, const std::string &dir) {
         w.strs(s.sym.items);
         w.pod<uint64_t>(s.vcfs.size());
         for (const VcfData &v : s.vcfs) put_vcf(w, v);
-        // kernel views and the buffers their pointers index
+        // kernel views (their sizes first), the buffers their pointers index
+        // and the pointer words (remap_table)
+        for (uint64_t z : kViewSizes) w.pod(z);
         w.pod(s.d);
         w.pod(s.ds);
         w.pod(s.dk);
@@ -426,15 +520,17 @@ void store_save(sb_store &s, const std::string &dir) {
             w.pod<uint64_t>(reinterpret_cast<uint64_t>(b.p));
             w.pod<uint64_t>(b.bytes);
         }
+        w.vec(s.device >= 0 ? remap_table(s) : std::vector<RemapEntry>{});
         w.pod(kMagic);
         host_bytes = w.at;
+        w.close();
     }
     const std::string m = manifest_text(s, host_bytes, dev_bytes);
-    FILE *f = fopen((dir + "/manifest.json").c_str(), "wb");
-    if (!f) throw Error(SB_EIO, "cannot write " + dir + "/manifest.json");
-    fwrite(m.data(), 1, m.size(), f);
-    fclose(f);
+    Writer w(dir + "/manifest.json");
+    w.raw(m.data(), m.size());
+    w.close();
 }
+}  // namespace
 
 // dir of a manifest path (or the directory itself)
 std::string store_dir(const std::string &p) {
@@ -480,6 +576,8 @@ sb_store *store_open(const std::string &path, int device, std::string *stale) {
             }
         }
     if (stale && !stale->empty()) return nullptr;
+    for (uint64_t z : kViewSizes)
+        if (r.pod<uint64_t>() != z) throw Error(SB_EIO, "persisted store: kernel view layout differs (" + dir + ")");
     s->d = r.pod<DStore>();
     s->ds = r.pod<SStore>();
     s->dk = r.pod<KStore>();
@@ -489,6 +587,8 @@ sb_store *store_open(const std::string &path, int device, std::string *stale) {
         b.p = reinterpret_cast<void *>(r.pod<uint64_t>());
         b.bytes = r.pod<uint64_t>();
     }
+    std::vector<RemapEntry> rmap;
+    r.vec(rmap);
     if (r.pod<uint64_t>() != kMagic) throw Error(SB_EIO, "persisted store: corrupt host.bin");
     for (uint32_t i = 0; i < s->vcfs.size(); ++i) s->vcf_by_location.emplace(s->vcfs[i].location, i);
     if (device == SB_HOST_ONLY) {  // the host side only (planning, region files, index)
@@ -590,23 +690,13 @@ sb_store *store_open(const std::string &path, int device, std::string *stale) {
     for (const std::string &e : errs)
         if (!e.empty()) throw Error(SB_EIO, "persisted store: " + e);
     if (!host_err.empty()) throw Error(SB_EIO, host_err);
-    // remap: every view word inside an old buffer now points into its new copy
-    auto remap = [&](uint64_t *w, size_t n) {
-        for (size_t i = 0; i < n; ++i) {
-            if (!w[i]) continue;
-            for (size_t b = 0; b < old.size(); ++b) {
-                const uint64_t base = reinterpret_cast<uint64_t>(old[b].p);
-                if (w[i] >= base && w[i] < base + old[b].bytes) {
-                    w[i] = reinterpret_cast<uint64_t>(s->bufs[b].p) + (w[i] - base);
-                    break;
-                }
-            }
-        }
-    };
-    remap(words(s->d), sizeof(DStore) / 8);
-    remap(words(s->ds), sizeof(SStore) / 8);
-    remap(words(s->dk), sizeof(KStore) / 8);
-    remap(words(s->g), sizeof(GStore) / 8);
+    // remap exactly the pointer words the save classified (remap_table)
+    uint64_t *views[4] = {words(s->d), words(s->ds), words(s->dk), words(s->g)};
+    for (const RemapEntry &e : rmap) {
+        if (e.view >= 4 || e.word >= kViewSizes[e.view] / 8 || e.buf >= s->bufs.size() || e.off > old[e.buf].bytes)
+            throw Error(SB_EIO, "persisted store: corrupt pointer table (" + dir + ")");
+        views[e.view][e.word] = reinterpret_cast<uint64_t>(s->bufs[e.buf].p) + e.off;
+    }
     return s.release();
 }
 

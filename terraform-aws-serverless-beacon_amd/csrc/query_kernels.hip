@@ -24,6 +24,7 @@
 #include <stdexcept>
 
 #include "../../include/sbeacon.h"
+#include "config.hpp"
 #include "devtypes.hpp"
 #include "kernels.hpp"
 
@@ -3113,10 +3114,7 @@ inline uint32_t blocks_for(uint32_t nwaves) { return (nwaves + kWavesPerBlock - 
 // still has >= 4 waves per slot of a full chip (256 CUs x 4 SIMDs x 8)
 // (SBEACON_SLICES_PER_WAVE=k forces k, 1..kRun: tests drive run_slices with small batches)
 inline uint32_t run_for(uint32_t nq) {
-    if (const char *e = std::getenv("SBEACON_SLICES_PER_WAVE")) {
-        const long k = std::strtol(e, nullptr, 10);
-        if (k >= 1) return std::min<uint32_t>(kRun, static_cast<uint32_t>(k));
-    }
+    if (const int k = config().slices_per_wave; k >= 1) return std::min<uint32_t>(kRun, static_cast<uint32_t>(k));
     return std::max(1u, std::min(kRun, nq / 32768u));
 }
 inline uint32_t run_waves(uint32_t nq, uint32_t run) { return (nq + run - 1) / run; }
@@ -3773,13 +3771,11 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const u
 void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *runs, uint32_t n_runs,
                    const uint32_t *corig, QRes *res, uint64_t *hits, ReqPartial *cpart, hipStream_t s) {
     if (!n_chains) return;
-    const char *kern = std::getenv("SBEACON_CHAIN_KERNEL");  // "seq": the chain-sequential kernel
-    if (!(kern && kern[0] == 's')) {
+    if (!config().chain_seq) {  // SBEACON_CHAIN_KERNEL=seq: the chain-sequential kernel
         // timing ablations (skip evaluation / results) exist only in a bench
         // build (-DSBEACON_ABLATION): the product library always runs the full kernel
 #ifdef SBEACON_ABLATION
-        const char *dbg = std::getenv("SBEACON_PACK_DBG");
-        const uint32_t dbgv = dbg ? static_cast<uint32_t>(std::atoi(dbg)) : 0u;
+        const uint32_t dbgv = static_cast<uint32_t>(config().pack_dbg);
 #else
         const uint32_t dbgv = 0u;
 #endif
@@ -3794,8 +3790,7 @@ void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, 
     // runs of kChainRun chains per wave while the launch still fills the chip
     // (256 CUs x 4 SIMDs x 8 waves, 4 deep)
     uint32_t run = kChainRun;
-    if (const char *e = std::getenv("SBEACON_CHAIN_RUN")) {
-        const long k = std::strtol(e, nullptr, 10);
+    if (const int k = config().chain_run; k != 0) {
         if (k >= 1) run = std::min<uint32_t>(kChainRun, static_cast<uint32_t>(k));
     } else {
         while (run > 1 && (n_chains + run - 1) / run < 32768u) run >>= 1;
@@ -3946,8 +3941,7 @@ void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, cons
         return;
     }
     hipLaunchKernelGGL(field_tile_scan_kernel, dim3(nt), dim3(kBlock), 0, s, nv, stride, n_rows, tsum, row_off);
-    const char *g = std::getenv("SBEACON_ROW_GATHER");  // "team": 8 lanes per row
-    if (g && g[0] == 't') {
+    if (config().row_gather_team) {  // SBEACON_ROW_GATHER=team: 8 lanes per row
         const uint64_t threads = static_cast<uint64_t>(n_rows) * kGatherTeam;
         hipLaunchKernelGGL(row_gather_kernel, dim3(static_cast<uint32_t>((threads + kBlock - 1) / kBlock)), dim3(kBlock),
                            0, s, poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
@@ -4000,8 +3994,7 @@ void launch_scan(const DStore &st, const QDev *q, const uint32_t *qidx, uint32_t
     int nacc = max_words == 0 ? 0 : max_words <= 64 ? 1 : max_words <= 256 ? 4 : 16;
     // SBEACON_MAX_NACC (tests): shrink the register window so small cohorts
     // exercise the words-beyond-the-window path of >65,536-sample VCFs
-    const char *cap_env = std::getenv("SBEACON_MAX_NACC");
-    const int cap = cap_env ? std::atoi(cap_env) : 16;
+    const int cap = config().max_nacc;
     if (nacc > 0 && cap >= 1) nacc = std::min(nacc, cap >= 16 ? 16 : cap >= 4 ? 4 : 1);
     if (nacc == 0) {  // every sample-free specialisation goes through the fused kernel
         if (qidx) throw std::runtime_error("launch_scan: sample-free queries must be contiguous (qidx = null)");

@@ -33,6 +33,7 @@
 #include <unordered_map>
 #include <vector>
 
+#include "config.hpp"
 #include "common.hpp"
 #include "jsonesc.hpp"
 
@@ -685,7 +686,7 @@ void put_error(std::string &o, int32_t err) {
 // SBEACON_WIRE_TRACE: time in the variant / sample-name writers, per thread
 thread_local double tl_var_ms = 0, tl_samp_ms = 0;
 thread_local uint64_t tl_var_n = 0, tl_samp_n = 0, tl_var_b = 0, tl_samp_b = 0;
-const bool g_wire_trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;  // read once at load
+const bool g_wire_trace = config().wire_trace;  // read once at load
 
 // d != null: the variant list and the sample-name list are not written --
 // their positions in o and exact lengths go to *d (the caller writes them in
@@ -805,7 +806,7 @@ int sb_perform_query_events(sb_store *const *stores, size_t n_stores, const char
         const unsigned chunks = 64;
         const bool strict_vt = (flags & 1u) != 0;
         // SBEACON_WIRE_TRACE=1: phase times to stderr (bench diagnostics)
-        const bool trace = std::getenv("SBEACON_WIRE_TRACE") != nullptr;
+        const bool trace = config().wire_trace;
         auto t_last = std::chrono::steady_clock::now();
         auto tick = [&](const char *what) {
             if (!trace) return;

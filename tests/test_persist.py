@@ -105,3 +105,19 @@ def test_store_set_rebuilds_a_repointed_location(tmp_path):
     assert ss.stores['ds'].paths['tiny22.vcf'] == other
     ss.load({'ds': [('tiny22.vcf', other)]}, device=HOST_ONLY)
     assert ss.rebuilt == [] and ss.opened == ['ds']
+
+
+def test_save_replaces_the_directory_whole(tmp_path):
+    """sb_store_save writes into DIR.tmp and renames it into place (ADVICE
+    round 4): a second save over the first leaves one complete directory and
+    no temporary or previous copy; the re-opened store is the saved one."""
+    from sbeacon.engine import Store
+    src = _copy(tmp_path, 'tiny22.vcf')
+    st = Store.build([('tiny22.vcf', src)], device=HOST_ONLY)
+    d = str(tmp_path / 'store')
+    st.save(d)
+    st.save(d + '/')
+    assert sorted(os.listdir(d)) == ['device.bin', 'host.bin', 'manifest.json', 'sbeacon.json']
+    assert not os.path.exists(d + '.tmp') and not os.path.exists(d + '.old')
+    again = Store.open(d, device=HOST_ONLY)
+    assert again.contigs('tiny22.vcf') == st.contigs('tiny22.vcf')

@@ -10,7 +10,7 @@ step() {  # name, limit, command...
   case $rc in 0) return 0;; *) exit $rc;; esac
 }
 step full 300 python3 -u $R/tools/req_tune.py --save /tmp/st --digest
-for v in p3w7 p3w6 p4w6 p4w5; do
+for v in $VARIANTS; do
   step $v 200 env SBEACON_LIB=$R/tools/variants/$v/libsbeacon_hip.so python3 -u $R/tools/req_tune.py --open /tmp/st --digest
 done
 exit 0
