@@ -353,10 +353,15 @@ def digest(rows, hit_parts) -> str:
 def make_step(run, ex, part, hits, row_off):
     """The bench step: ``run(part, hits, row_off)`` answers the rank's
     sub-requests into its rows / dense hit lists, then ResultExchange
-    delivers them to their host-facing ranks.  Returns the owned rows."""
+    delivers them to their host-facing ranks and merges each owned request's
+    received hits into the owner's dense lists (ResultExchange.merge).
+    Returns the owned rows."""
     def step():
         run(part, hits, row_off)
-        return ex.exchange(part, hits, row_off)
+        rows = ex.exchange(part, hits, row_off)
+        if ex.world > 1:
+            ex.merge()
+        return rows
     return step
 
 

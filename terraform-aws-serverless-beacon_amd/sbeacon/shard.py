@@ -157,6 +157,7 @@ class ResultExchange:
         self.recv_hits = [None] * len(self.recvs)
         self.recv_hits_n = {}
         self._my_hits = None
+        self._merge = None  # merge plan (dest indices), fixed per batch (merge)
         self._allc = None  # hit ranges [src, dst, (start, n)], fixed per batch (exchange)
         self._ops, self._ops_key, self._nccl = [], None, False
 
@@ -221,6 +222,95 @@ class ResultExchange:
         for k, (_, g, n) in enumerate(self.recvs):
             self.rows[g - self.own_lo:g - self.own_lo + n] += self.recv_rows[k]
         return self.rows
+
+    def merge(self):
+        """The owned requests' hit lists, merged densely on the device: each
+        owned request's own slices' hits, then every sender's (rank order =
+        position order), in request order.  Returns (hits, offs): request
+        ``own_lo + i`` has ``hits[offs[i]:offs[i + 1]]``.  In 'first' mode
+        the received rows are the last rows of the window (requests whose
+        window crosses the next cut), so only the hits from the first such
+        row on move: the rest of the window's dense output stays where the
+        pass wrote it, and the merged lists are written into the pass's
+        ``hits`` / ``row_off`` in place when the hit buffer has the room
+        (else into new buffers).  The destination of every moved hit is
+        planned once per batch (a batch's hit counts are fixed); a step is
+        then one gather and one scatter, with no host round trip."""
+        import torch
+        hits, row_off = self._my_hits
+        key = (hits.data_ptr(), row_off.data_ptr())
+        if self._merge is None or self._merge['key'] != key:
+            self._merge = self._merge_plan(hits, row_off, key)
+        m = self._merge
+        if m['trivial']:
+            return hits, row_off[self.own_a:self.own_b + 1]
+        vals = [hits[m['own_lo']:m['own_hi']].clone()] if m['own_hi'] > m['own_lo'] else []
+        for k, nh in m['recv']:
+            if nh:
+                vals.append(self.recv_hits[k][:nh])
+        if m['prefix'] is not None:  # new buffers: the unmoved prefix, one block
+            a, n = m['prefix']
+            m['out'][:n] = hits[a:a + n]
+        if vals:
+            m['out'][m['dest']] = torch.cat(vals) if len(vals) > 1 else vals[0]
+        if m['off_tail'] is not None:  # in place: the moved rows' offsets (the pass rewrote them)
+            m['off'][m['t'] + 1:] = m['off_tail']
+        return m['out'], m['off']
+
+    def _merge_plan(self, hits, row_off, key):
+        import torch
+        dev = hits.device
+        ro = row_off.cpu().numpy().astype(np.int64)
+        n = self.n_own
+        recv = [(k, int(self.recv_hits_n.get(k, 0))) for k in range(len(self.recvs))]
+        if self.inplace and not any(nh for _, nh in recv):
+            return {'key': key, 'trivial': True}
+        o = self.row_lo + self.own_a - self.own_lo  # first own row, relative to own_lo
+        n_o = self.own_b - self.own_a               # own rows
+        own_cnt = np.zeros(n, dtype=np.int64)
+        if n_o:
+            own_cnt[o:o + n_o] = np.diff(ro[self.own_a:self.own_b + 1])
+        rcnt = []
+        for k, (_, g, nr) in enumerate(self.recvs):
+            c = np.zeros(n, dtype=np.int64)
+            c[g - self.own_lo:g - self.own_lo + nr] = self.recv_rows[k][:, 1].cpu().numpy()
+            rcnt.append(c)
+        rsum = sum(rcnt) if rcnt else np.zeros(n, dtype=np.int64)
+        off = np.zeros(n + 1, dtype=np.int64)
+        np.cumsum(own_cnt + rsum, out=off[1:])
+        # rows before t receive nothing: their hits keep their places (the
+        # own rows start at 0 then, so their positions are the merged ones)
+        got = np.flatnonzero(rsum)
+        t = int(got[0]) if len(got) else n
+        own_lo = int(ro[self.own_a + min(max(t - o, 0), n_o)]) if n_o else 0
+        own_hi = int(ro[self.own_b]) if n_o else own_lo
+        rows_t = np.arange(t, n)
+        dest = []
+        c = own_cnt[t:]
+        first = np.repeat(np.cumsum(c) - c, c)
+        dest.append(np.repeat(off[t:n], c) + (np.arange(int(c.sum())) - first))
+        filled = own_cnt.copy()
+        for ck_all in rcnt:
+            ck = ck_all[t:]
+            first = np.repeat(np.cumsum(ck) - ck, ck)
+            dest.append(np.repeat(off[t:n] + filled[t:n], ck) + (np.arange(int(ck.sum())) - first))
+            filled += ck_all
+        dest = np.concatenate(dest).astype(np.int64)
+        total = int(off[-1])
+        base = int(ro[self.own_a]) if n_o else 0
+        off_tail = None
+        if self.inplace and hits.numel() >= base + total:
+            out = hits
+            m_off = row_off[self.own_a:self.own_a + n + 1]
+            off_tail = torch.from_numpy(off[t + 1:] + base).to(dev)
+            dest += base
+            prefix = None
+        else:
+            out = torch.zeros(max(total, 1), dtype=hits.dtype, device=dev)
+            m_off = torch.from_numpy(off).to(dev)
+            prefix = (base, int(off[t])) if t > 0 and n_o else None
+        return {'key': key, 'trivial': False, 'dest': torch.from_numpy(dest).to(dev), 'out': out, 'off': m_off,
+                'off_tail': off_tail, 't': t, 'own_lo': own_lo, 'own_hi': own_hi, 'recv': recv, 'prefix': prefix}
 
     def hit_lists(self):
         """{global request row: [hit, ...]} of the owned requests (host; tests)."""

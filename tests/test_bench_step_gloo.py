@@ -59,14 +59,21 @@ def _worker(rank, world, port, tmp, mode, q):
             o.copy_(torch.from_numpy(row_off))
 
         part = torch.zeros((max(sr.n_rows, 1), 5), dtype=torch.int64)
-        hbuf = torch.zeros(len(hits) + 8, dtype=torch.int64)
+        # 'first': room for the received hits, so the merge writes in place;
+        # 'rank0': none, so it writes new buffers (both merge paths run)
+        hbuf = torch.zeros(len(hits) + (4096 if mode == 'first' else 8), dtype=torch.int64)
         obuf = torch.zeros(sr.n_rows + 1, dtype=torch.int64)
         ex = ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, 'cpu')
         step = make_step(run, ex, part, hbuf, obuf)
-        for _ in range(3):  # later steps re-issue the cached P2P op list
+        for _ in range(3):  # later steps re-issue the cached P2P op list and the cached merge plan
             got = step()
+        mh, mo = ex.merge()
+        if ex.recv_hits_n and any(ex.recv_hits_n.values()):
+            assert (mh.data_ptr() == hbuf.data_ptr()) == (mode == 'first'), (mode, rank)
+        mh, mo = mh.numpy().view(np.uint64), mo.numpy()
+        merged = {ex.own_lo + i: [int(h) for h in mh[mo[i]:mo[i + 1]]] for i in range(ex.n_own)}
         q.put((rank, ex.own_lo, ex.n_own, got.numpy()[:ex.n_own].copy(),
-               {k: [int(h) for h in v] for k, v in ex.hit_lists().items()}))
+               {k: [int(h) for h in v] for k, v in ex.hit_lists().items()}, merged))
     finally:
         dist.destroy_process_group()
 
@@ -94,7 +101,7 @@ def test_bench_step_world2_matches_unsharded_oracle(mode):
             p.join(timeout=60)
             assert p.exitcode == 0
     owned = np.zeros(len(reqs), dtype=np.int64)
-    for rank, lo, n, rows, hl in got:
+    for rank, lo, n, rows, hl, merged in got:
         if mode == 'rank0' and rank:
             assert n == 0
         owned[lo:lo + n] += 1
@@ -102,5 +109,6 @@ def test_bench_step_world2_matches_unsharded_oracle(mode):
         for r in range(lo, lo + n):
             e = [int(h) for h in exp_hits.view(np.uint64)[exp_off[r]:exp_off[r + 1]]]
             assert hl.get(r, []) == e, (rank, r)
+            assert merged[r] == e, (rank, r, 'merged')
     assert (owned == 1).all()
     assert exp_off[-1] > 20
