@@ -2587,10 +2587,24 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     if (w >= n_runs) return;
     const uint32_t ul = static_cast<uint32_t>(lane_id());
     const uint32_t t0 = (w / kDeliverTile) * kDeliverTile;
+    // the run record and the run's total (status[w] = its staged hits, which
+    // request_eval_kernel wrote) first: a simple run's first round of staged
+    // hits is loaded before its output offset is known, so those loads and
+    // the record-id gathers behind them overlap the offset scans
     const RowRun rr = runs[w];
+    const uint64_t Hs = uniform64(status[w]);
     const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
     const uint64_t stage_at = uniform64(rr.stage);
     const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
+    constexpr uint32_t kU = 8;  // 512 hits per round: most runs in one (~480 hits per run)
+    uint32_t v0[kU];
+    if (simple) {
+#pragma unroll
+        for (uint32_t u = 0; u < kU; ++u) {
+            const uint64_t j = kWave * u + ul;
+            v0[u] = j < Hs ? stage[stage_at + j] : 0u;
+        }
+    }
     const uint32_t row = row_lo + ul;
     const uint64_t c = row < row_hi ? static_cast<uint64_t>(row_off[row]) : 0ull;  // the counts request_eval_kernel left
     const uint64_t before = t0 + ul < w ? status[t0 + ul] : 0ull;
@@ -2605,13 +2619,12 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     if (row < row_hi) row_off[row] = static_cast<Hit>(off);
     if (row_hi == n_rows && ul == 0) row_off[n_rows] = static_cast<Hit>(O + H);
     if (simple) {  // chain rows (and empty rows) only: the staging region is the output, in order
-        constexpr uint32_t kU = 8;  // 512 hits per round: most runs in one (~480 hits per run)
         for (uint64_t j0 = 0; j0 < H; j0 += kWave * kU) {
             uint32_t v[kU];
 #pragma unroll
             for (uint32_t u = 0; u < kU; ++u) {
                 const uint64_t j = j0 + kWave * u + ul;
-                v[u] = j < H ? stage[stage_at + j] : 0u;
+                v[u] = j0 == 0 ? v0[u] : (j < H ? stage[stage_at + j] : 0u);
             }
             Hit h[kU];
 #pragma unroll
