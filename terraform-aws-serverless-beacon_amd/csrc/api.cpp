@@ -1,4 +1,6 @@
 // api.cpp — the C ABI (include/sbeacon.h): builder, HBM store, query batches.
+// Request batches live in requests.cpp, summarise / dedup in summarise.cpp,
+// result sets in results.cpp; what they share is internal.hpp.
 //
 // The query path mirrors one splitQuery fan-out (lambda/splitQuery/
 // lambda_function.py:74-110) handed to the device as ONE batch: every
@@ -7,30 +9,9 @@
 // a query step is a single kernel launch (query_kernels.hip).  Result strings
 // are formatted on the host from the store's allele blob in the reference's
 // exact format.
-#include <algorithm>
-#include <deque>
-#include <atomic>
-#include <array>
-#include <chrono>
-#include <condition_variable>
-#include <functional>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <map>
-#include <memory>
-#include <thread>
-#include <tuple>
-#include <string_view>
-#include <unordered_map>
-#include <unordered_set>
+#include "internal.hpp"
 
 #include <zlib.h>
-
-#include "config.hpp"
-#include "jsonesc.hpp"
-#include "kernels.hpp"
-#include "store.hpp"
 
 namespace sb {
 void builder_add_text(sb_builder &b, uint32_t vcf_id, const char *text, size_t len);
@@ -42,129 +23,6 @@ void builder_attach_carriers(sb_builder &b, uint32_t vcf_id, const char *const *
 
 namespace {
 thread_local std::string g_last_error;
-
-#define HIP_OK(expr)                                                                                  \
-    do {                                                                                              \
-        hipError_t e_ = (expr);                                                                       \
-        if (e_ != hipSuccess)                                                                         \
-            throw ::sb::Error(SB_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));            \
-    } while (0)
-
-template <class F>
-int guard(F &&f) {
-    try {
-        f();
-        return SB_OK;
-    } catch (const Error &e) {
-        set_last_error(e.what());
-        return e.code;
-    } catch (const std::bad_alloc &) {
-        set_last_error("out of host memory");
-        return SB_ENOMEM;
-    } catch (const std::exception &e) {
-        set_last_error(e.what());
-        return SB_EINVAL;
-    }
-}
-
-template <class T>
-T *dev_upload(sb_store &s, const std::vector<T> &v) {
-    if (s.device < 0) return nullptr;  // a host-only store (SB_HOST_ONLY): no device image
-    DeviceBuffer b;
-    b.bytes = std::max<size_t>(v.size() * sizeof(T), 16);
-    HIP_OK(hipMalloc(&b.p, b.bytes));
-    if (!v.empty()) {
-        HIP_OK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s.stream));
-        HIP_OK(hipStreamSynchronize(s.stream));  // callers free pageable temporaries right after
-    }
-    s.bufs.push_back(b);
-    s.device_bytes += b.bytes;
-    return static_cast<T *>(b.p);
-}
-
-struct DevMem {  // RAII device allocation for batches (move-only)
-    void *p = nullptr;
-    size_t bytes = 0;
-    DevMem() = default;
-    DevMem(const DevMem &) = delete;
-    DevMem &operator=(const DevMem &) = delete;
-    DevMem(DevMem &&o) noexcept : p(o.p), bytes(o.bytes) {
-        o.p = nullptr;
-        o.bytes = 0;
-    }
-    DevMem &operator=(DevMem &&o) noexcept {
-        if (this != &o) {
-            release();
-            p = o.p;
-            bytes = o.bytes;
-            o.p = nullptr;
-            o.bytes = 0;
-        }
-        return *this;
-    }
-    void alloc(size_t n) {
-        release();
-        bytes = std::max<size_t>(n, 16);
-        HIP_OK(hipMalloc(&p, bytes));
-    }
-    // keep the allocation when it is large enough (per-store scratch reused
-    // across calls: hipMalloc / hipFree of ~1 GB per call cost more than the
-    // kernels)
-    void reserve(size_t n) {
-        if (p && bytes >= n) return;
-        alloc(n + n / 4);
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        bytes = 0;
-    }
-    template <class T>
-    T *as() const { return static_cast<T *>(p); }
-    ~DevMem() { release(); }
-};
-
-struct ParsedRegion {
-    std::string chrom;
-    int64_t first = 0, last = 0;
-    bool ok = false;
-};
-
-// search_variants.py:56-58 — chrom up to the first ':', first_bp up to the
-// first '-', last_bp after it (Python int()).
-ParsedRegion parse_region(const char *p, size_t n) {
-    ParsedRegion r;
-    const std::string s(p, n);
-    const size_t c = s.find(':'), d = s.find('-');
-    if (c == std::string::npos || d == std::string::npos || d < c) return r;
-    r.chrom = s.substr(0, c);
-    if (!py_int(s.data() + c + 1, d - c - 1, &r.first)) return r;
-    if (!py_int(s.data() + d + 1, s.size() - d - 1, &r.last)) return r;
-    r.ok = true;
-    return r;
-}
-
-bool starts(const std::string &s, const char *pre) { return s.compare(0, strlen(pre), pre) == 0; }
-
-// Host-side evaluation of the symbolic-ALT predicates of :101-166 for one
-// variantType string over the store's symbolic dictionary.
-std::vector<uint32_t> sym_lut(const sb_store &s, uint32_t kind, const std::string &vprefix) {
-    std::vector<uint32_t> lut((s.sym.items.size() + 31) / 32 + 1, 0u);
-    for (size_t i = 0; i < s.sym.items.size(); ++i) {
-        const std::string &a = s.sym.items[i];
-        bool ok = starts(a, vprefix.c_str());
-        switch (kind) {
-            case VT_DEL: ok = ok || a == "<CN0>"; break;
-            case VT_DUP: ok = ok || (starts(a, "<CN") && a != "<CN0>" && a != "<CN1>"); break;
-            case VT_DUPT: ok = ok || a == "<CN2>"; break;
-            case VT_CNV: ok = ok || starts(a, "<CN") || starts(a, "<DEL") || starts(a, "<DUP"); break;
-            default: break;
-        }
-        if (ok) lut[i / 32] |= 1u << (i % 32);
-    }
-    return lut;
-}
-
 }  // namespace
 
 void set_last_error(const std::string &msg) { g_last_error = msg; }
@@ -192,287 +50,6 @@ sb_store::~sb_store() {
     if (stream) (void)hipStreamDestroy(stream);
 }
 
-// ------------------------------------------------------------------ batch
-// Request batches' buffers, pooled per store (sb_store::req_pool): planning
-// stages descriptors in pinned host memory and a pass needs seven device
-// buffers; allocating them per batch (hipHostMalloc pins pages, hipFree
-// synchronises the device) cost more than the pass itself.  Best fit among
-// the free buffers no more than twice the size asked for; bounded.
-struct ReqPool {
-    struct Pinned {
-        void *p = nullptr;
-        size_t bytes = 0;
-    };
-    std::mutex mu;
-    std::vector<Pinned> pinned;
-    std::vector<DevMem> dev;
-    static constexpr size_t kKeep = 256;                     // buffers kept per kind at most (a pipelined caller holds ~10 per chunk batch)
-    static constexpr size_t kKeepDevBytes = size_t(4) << 30;  // and bytes: the largest go first
-    static constexpr size_t kKeepPinnedBytes = size_t(2) << 30;
-    ~ReqPool() { trim(); }
-    template <class V>
-    static size_t total(const V &v) {
-        size_t t = 0;
-        for (const auto &x : v) t += x.bytes;
-        return t;
-    }
-    template <class V>
-    static size_t largest(const V &v) {
-        size_t b = 0;
-        for (size_t i = 1; i < v.size(); ++i)
-            if (v[i].bytes > v[b].bytes) b = i;
-        return b;
-    }
-    void trim() {  // free every cached buffer (sb_store_trim)
-        std::lock_guard<std::mutex> lk(mu);
-        for (Pinned &x : pinned) (void)hipHostFree(x.p);
-        pinned.clear();
-        dev.clear();
-    }
-    template <class V>
-    static ptrdiff_t fit(const V &v, size_t n) {
-        ptrdiff_t best = -1;
-        for (size_t i = 0; i < v.size(); ++i)
-            if (v[i].bytes >= n && v[i].bytes <= 2 * n + (1u << 20) && (best < 0 || v[i].bytes < v[best].bytes))
-                best = static_cast<ptrdiff_t>(i);
-        return best;
-    }
-    Pinned get_pinned(size_t n) {
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            const ptrdiff_t i = fit(pinned, n);
-            if (i >= 0) {
-                Pinned x = pinned[i];
-                pinned.erase(pinned.begin() + i);
-                return x;
-            }
-        }
-        Pinned x;
-        x.bytes = std::max<size_t>(n + n / 4, 4096);
-        HIP_OK(hipHostMalloc(&x.p, x.bytes, hipHostMallocDefault));
-        return x;
-    }
-    void put_pinned(Pinned x) {
-        std::lock_guard<std::mutex> lk(mu);
-        pinned.push_back(x);
-        if (pinned.size() > kKeep) {
-            (void)hipHostFree(pinned.front().p);
-            pinned.erase(pinned.begin());
-        }
-        while (pinned.size() > 1 && total(pinned) > kKeepPinnedBytes) {
-            const size_t i = largest(pinned);
-            (void)hipHostFree(pinned[i].p);
-            pinned.erase(pinned.begin() + static_cast<ptrdiff_t>(i));
-        }
-    }
-    DevMem get_dev(size_t n) {
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            const ptrdiff_t i = fit(dev, n);
-            if (i >= 0) {
-                DevMem x = std::move(dev[i]);
-                dev.erase(dev.begin() + i);
-                return x;
-            }
-        }
-        DevMem x;
-        x.alloc(n + n / 4);
-        return x;
-    }
-    void put_dev(DevMem &&x) {
-        std::lock_guard<std::mutex> lk(mu);
-        dev.push_back(std::move(x));
-        if (dev.size() > kKeep) dev.erase(dev.begin());
-        while (dev.size() > 1 && total(dev) > kKeepDevBytes) dev.erase(dev.begin() + static_cast<ptrdiff_t>(largest(dev)));
-    }
-};
-
-std::shared_ptr<ReqPool> req_pool(sb_store &s) {
-    std::call_once(s.req_pool_once, [&] {
-        s.req_pool = std::shared_ptr<void>(new ReqPool, [](void *w) { delete static_cast<ReqPool *>(w); });
-    });
-    return std::shared_ptr<ReqPool>(s.req_pool, static_cast<ReqPool *>(s.req_pool.get()));
-}
-
-struct sb_batch {
-    sb_store *s = nullptr;
-    uint32_t nq = 0;
-    std::vector<QDev> hq;
-    std::vector<int32_t> host_err;               // errors raised before any record is read
-    std::vector<std::string> chrom;              // region chrom per query (variant strings)
-    std::vector<std::vector<uint32_t>> emitted;  // header indices of the emitted samples
-    std::vector<uint8_t> samples_variant;
-    std::vector<uint32_t> vcf;
-    uint64_t cap_total = 0, samples_words = 0;
-    DevMem q, hoff, qbytes, subsets, lut, res, hits, samples_out;
-    // queries split by kernel variant: the sample path compiled in or out
-    // queries grouped by kernel specialisation: one launch per non-empty group
-    struct Group {
-        int mode;
-        uint32_t max_words;  // 0 = sample path compiled out
-        std::vector<uint32_t> idx;
-        uint32_t base;  // first entry of the group in the launch-ordered device array
-    };
-    std::vector<Group> groups;
-    // slice chains (ChainDev): their slices sit after the groups in the
-    // launch-ordered array; n_scanned of a chained slice is known on the host
-    std::vector<ChainDev> hchains;
-    DevMem chains;
-    std::vector<uint32_t> hruns;  // first chain of each chain_pack_kernel wave (+ end)
-    DevMem runs;
-    // chained slices also write their per-slice QRes rows (sb_batch_set_slice_results);
-    // off = request rows + hit lists only (row pieces), fetch refused
-    bool slice_rows = true;
-    bool slice_rows_stale = false;  // a run without them since the last run with them
-    std::vector<uint8_t> chained;
-    std::vector<uint32_t> nscan;
-    std::vector<uint32_t> chain_members;  // chained queries, chain by chain (device copy: corig)
-    uint32_t chain_base = 0;              // first chained slice in the launch-ordered array
-    DevMem corig;
-    DevMem srcoff;  // each query's hit-region offset (chained slices: rewritten by chain_src_kernel)
-    DevMem tsum, dense;  // dense hit lists (sb_batch_compact_hits)
-    DevMem cpart;        // per-chain request-row partials (chain_kernel)
-    std::vector<uint64_t> chain_cap;  // hit capacity of each chain (ALTs of its coarse candidate range)
-    // request rows as pieces (sb_batch_set_owners, when every chain lies in one row)
-    bool row_pieces = false;
-    DevMem poff, piece, rows_scratch, rowsrc, rowout;
-    DevMem nvs;  // sb_batch_deliver: each row's n_variants (8 B / row) for the offset scan
-    uint64_t cand_loaded = 0, cand_window = 0, cand_unique = 0;  // chain candidate statistics
-    hipStream_t stream = nullptr;  // sb_batch_set_stream (nullptr: the store's stream)
-    hipStream_t strm() const { return stream ? stream : s->stream; }
-    bool nonneg = true;
-    // per-request rows (sb_batch_set_owners): seg = n_rows + 1 query offsets
-    uint32_t n_rows = 0;
-    DevMem seg, herr;
-    bool no_chains = false;  // the slice part of a request batch: every slice answered on its own
-    // request batches (sb_requests_prepare): rows = requests
-    struct Req {
-        uint32_t n_rows = 0;
-        std::vector<RowRun> runs;
-        uint64_t cap = 0;              // output hit capacity
-        uint64_t n_chain_slices = 0;
-        uint32_t n_lut = 0;            // LUT words (request_eval_kernel stages them in LDS when they fit)
-        uint64_t n_chains = 0;         // chain-answered requests (dchains holds them padded per run)
-        uint32_t n_runs = 0;           // runs (runs: their host copy when planned on the host)
-        // sb_requests_time_eval: events around every pass's request_eval_kernel
-        bool time_eval = false;
-        std::vector<std::array<hipEvent_t, 2>> eval_ev;
-        size_t eval_used = 0;
-        double last_eval_ms = 0;
-        ~Req() {
-            for (auto &p : eval_ev)
-                for (auto e : p) (void)hipEventDestroy(e);
-        }
-        // dchains: ReqChain slots (kReqRun per run), then the RowRuns at runs_at
-        DevMem dchains, status, tstatus, stage, row_src, lut, sseg, sherr;
-        // device-planned batches: the packed requests (ReqIn) and the
-        // planner's per-run capacities + counters stay resident, so a pass can
-        // re-run the planning kernels first (sb_requests_set_replan)
-        DevMem din, rcap;
-        uint32_t n_in = 0;
-        bool replan = false;
-        bool compact = false;  // sb_requests_set_compact
-        // request_eval_kernel's invariant word (sticky; checked at sync: SB_EINTERNAL)
-        DevMem err;
-        ReqPool::Pinned err_h;
-        // rows whose counts are not exact in int64 (sb_requests_inexact_rows):
-        // per-slice wide marks + one flag per row (batches with general records)
-        DevMem wide, row_flag;
-        std::vector<char> hplan;  // host-only stores: the descriptors + runs (as dchains would hold them)
-        size_t runs_at = 0;
-        uint32_t run = kReqRun;        // chain slots per run (request_eval_kernel: one lane each)
-        std::shared_ptr<ReqPool> pool;  // where the device buffers go back when the batch is freed
-        bool slices = false;           // some rows answered per slice (the batch's query part)
-        void give_back() {
-            for (DevMem *m : {&dchains, &status, &tstatus, &stage, &row_src, &lut, &sseg, &sherr, &wide, &row_flag, &din,
-                              &rcap, &err})
-                if (m->p) pool->put_dev(std::move(*m));
-            if (err_h.p) {
-                pool->put_pinned(err_h);
-                err_h = ReqPool::Pinned{};
-            }
-        }
-    };
-    std::unique_ptr<Req> req;
-    // slice batches: device buffers from the store's pool (a steady stream
-    // of batches then allocates nothing), given back when the batch is freed
-    std::shared_ptr<ReqPool> pool;
-    // general records (general_slice_kernel): work list [count, launch
-    // indices], per-wave scratch, slices with counts past 64 bits
-    DevMem gen_work, gen_scratch, gen_big_n, gen_big, gen_limbs;
-    uint32_t gen_grid = 0, gen_big_cap = 0;
-    // events around the runs since the last sync (run() records [0], sync() [1])
-    std::array<hipEvent_t, 2> ev{};
-    size_t runs_pending = 0;
-    float last_total_ms = 0;
-    std::mutex mu;  // request batches: one pass at a time per batch
-    ~sb_batch() {
-        for (auto e : ev)
-            if (e) (void)hipEventDestroy(e);
-        if ((req && req->pool) || pool) (void)hipStreamSynchronize(strm());  // a pass may still be in flight
-        if (req && req->pool) req->give_back();
-        if (pool)
-            for (DevMem *m : {&q, &hoff, &qbytes, &subsets, &lut, &res, &hits, &samples_out, &chains, &runs, &corig,
-                              &srcoff, &cpart, &gen_work, &gen_scratch, &gen_big_n, &gen_big, &gen_limbs})
-                if (m->p) pool->put_dev(std::move(*m));
-    }
-};
-
-// a batch buffer: from the batch's pool when it has one
-void palloc(sb_batch &B, DevMem &m, size_t n) {
-    if (!B.pool) {
-        m.alloc(n);
-        return;
-    }
-    if (m.p) B.pool->put_dev(std::move(m));
-    m = B.pool->get_dev(std::max<size_t>(n, 16));
-}
-
-// a result set's dense hit list: pinned host memory from the store's pool
-// (the D2H lands there directly; no zero-filled pageable copy)
-struct HitBuf {
-    std::shared_ptr<ReqPool> pool;
-    ReqPool::Pinned mem;
-    size_t n = 0;
-    HitBuf() = default;
-    HitBuf(const HitBuf &) = delete;
-    HitBuf &operator=(const HitBuf &) = delete;
-    ~HitBuf() {
-        if (mem.p) pool->put_pinned(mem);
-    }
-    uint64_t *data() { return static_cast<uint64_t *>(mem.p); }
-    const uint64_t &operator[](size_t i) const { return static_cast<const uint64_t *>(mem.p)[i]; }
-    size_t size() const { return n; }
-};
-
-struct sb_result_set {
-    sb_store *s = nullptr;  // held (store_hold) while the set lives
-    ~sb_result_set() {
-        if (s) store_release(s);
-    }
-    std::vector<QRes> res;
-    std::vector<uint64_t> dense_off;
-    HitBuf hit;                                 // rec | alt << 32
-    std::vector<std::vector<uint32_t>> sidx;    // emitted-list positions
-    std::vector<std::vector<uint32_t>> emitted;
-    std::vector<uint32_t> vcf_of;
-    std::vector<uint8_t> samples_variant;
-    std::vector<std::string> chrom;
-    std::vector<std::string> vtext, ntext;
-    std::vector<uint8_t> vbuilt, nbuilt;
-    std::string distinct;                       // sb_result_distinct_variants
-    std::vector<std::string> vt_json;           // escaped VT strings (sb::result_prepare_json)
-    // per VCF of the set, per header sample: its name as JSON list items
-    // (sb::result_prepare_json; "\x01" = not UTF-8)
-    std::vector<std::vector<std::string>> names_json;
-    // views for sb_result_get, split out of `hit` on its first call
-    mutable std::vector<uint32_t> tmp_rec, tmp_alt;
-    mutable std::once_flag tmp_once;
-    // queries whose counts need more than 64 bits: 2 x big_limbs limbs each
-    uint32_t big_limbs = 0;
-    std::unordered_map<uint32_t, std::vector<uint32_t>> big;
-    sb_batch_stats stats{};
-};
 
 namespace {
 
@@ -979,120 +556,6 @@ uint32_t bucket_ceil(const sb_store &s, const QDev &d, int64_t x) {
     return s.h_bucket[d.bucket_off + b + 1];
 }
 
-// A persistent host worker pool (planning runs once per call: spawning
-// threads per call cost a few hundred microseconds).  run(n, fn) calls fn(i)
-// for i < n on the pool and the calling thread; one run at a time (try_run:
-// parallel_for falls back to its own threads when the pool is taken).
-class WorkerPool {
-  public:
-    static WorkerPool &get() {
-        static WorkerPool pool(std::max(1u, std::min(16u, std::thread::hardware_concurrency())) - 1);
-        return pool;
-    }
-    // a second, smaller pool for a concurrent caller (two pipelined
-    // preparers): spawning threads per call costs more than the work
-    static WorkerPool &second() {
-        static WorkerPool pool(std::max(1u, std::min(8u, std::thread::hardware_concurrency() / 2)) - 1);
-        return pool;
-    }
-    template <class F>
-    void run(size_t n, F fn) {
-        std::unique_lock<std::mutex> one(run_mu_);
-        run_locked(n, fn);
-    }
-    // the same, or false at once when another run holds the pool (a
-    // concurrent caller, or a call from inside a task)
-    template <class F>
-    bool try_run(size_t n, F fn) {
-        std::unique_lock<std::mutex> one(run_mu_, std::try_to_lock);
-        if (!one.owns_lock()) return false;
-        run_locked(n, fn);
-        return true;
-    }
-
-  private:
-    template <class F>
-    void run_locked(size_t n, F fn) {
-        std::function<void(size_t)> f = fn;
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            fn_ = &f;
-            n_ = n;
-            next_ = 0;
-            busy_ = workers_.size();
-            ++gen_;
-        }
-        cv_.notify_all();
-        drain();
-        std::unique_lock<std::mutex> lk(mu_);
-        done_.wait(lk, [&] { return busy_ == 0; });
-        fn_ = nullptr;
-    }
-
-  public:
-    ~WorkerPool() {
-        {
-            std::lock_guard<std::mutex> lk(mu_);
-            stop_ = true;
-            ++gen_;
-        }
-        cv_.notify_all();
-        for (auto &t : workers_) t.join();
-    }
-
-  private:
-    explicit WorkerPool(unsigned k) {
-        for (unsigned i = 0; i < k; ++i) workers_.emplace_back([this] { loop(); });
-    }
-    void drain() {
-        for (size_t i; (i = next_.fetch_add(1)) < n_;) (*fn_)(i);
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            {
-                std::unique_lock<std::mutex> lk(mu_);
-                cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
-                if (stop_) return;
-                seen = gen_;
-            }
-            drain();
-            std::lock_guard<std::mutex> lk(mu_);
-            if (--busy_ == 0) done_.notify_all();
-        }
-    }
-    std::vector<std::thread> workers_;
-    std::mutex mu_, run_mu_;
-    std::condition_variable cv_, done_;
-    std::function<void(size_t)> *fn_ = nullptr;
-    size_t n_ = 0;
-    std::atomic<size_t> next_{0};
-    size_t busy_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
-};
-
-// run fn(i) for i in [0, n) on up to `threads` host threads (the worker
-// pool's when it is free)
-template <class F>
-void parallel_for(size_t n, F fn, unsigned threads = 16, size_t grain = 4096) {
-    const unsigned t = static_cast<unsigned>(std::min<size_t>(threads, std::max<size_t>(1, n / grain)));
-    if (t <= 1) {
-        for (size_t i = 0; i < n; ++i) fn(i);
-        return;
-    }
-    auto part = [&](size_t k) {
-        for (size_t i = n * k / t, e = n * (k + 1) / t; i < e; ++i) fn(i);
-    };
-    if (WorkerPool::get().try_run(t, part) || WorkerPool::second().try_run(t, part)) return;
-    std::vector<std::thread> th;
-    for (unsigned k = 0; k < t; ++k)
-        th.emplace_back([&, k] {
-            for (size_t i = n * k / t, e = n * (k + 1) / t; i < e; ++i) fn(i);
-        });
-    for (auto &x : th) x.join();
-}
-
 }  // namespace
 
 namespace sb {
@@ -1110,7 +573,9 @@ void run_tasks(size_t n, const std::function<void(size_t)> &fn) {
 }
 }  // namespace sb
 
-namespace {
+// the query batch (sb_batch_*); prepare / mark_run / run_kernels / sync are
+// the request batches' too (requests.cpp)
+namespace sb {
 
 // Chains of consecutive variantType slices (devtypes.hpp ChainDev).  vt =
 // the MODE_VTYPE queries in input order; returns those left to vt_slice.
@@ -1897,1161 +1362,9 @@ sb_result_set *fetch(sb_batch &B) {
     return R.release();
 }
 
-// virtual offset -> offset in the VCF text stream (block table of the BGZF file)
-bool voff_to_stream(const VcfData &v, uint64_t voff, uint64_t *u) {
-    const uint64_t co = voff >> 16, uo = voff & 0xffffu;
-    auto it = std::lower_bound(v.blk_coff.begin(), v.blk_coff.end(), co);
-    if (it == v.blk_coff.end()) {
-        if (uo) return false;
-        *u = v.stream_len;  // one past the last block
-        return true;
-    }
-    if (*it != co) return false;
-    *u = v.blk_ustart[static_cast<size_t>(it - v.blk_coff.begin())] + uo;
-    return *u <= v.stream_len;
-}
-
-// summariseSlice scratch, kept per store (sb_store::summarise_ws)
-struct SumWs {
-    DevMem dsl, dbm, dres, dcs, dpart;
-};
-
-void summarise(sb_store &s, const sb_slice *sl, size_t n, sb_slice_stats *out, double *device_ms) {
-    std::vector<SDev> hs(n);
-    std::vector<uint32_t> chunk_slice;  // phase-A chunk -> slice
-    std::vector<int32_t> herr(n, 0);
-    uint64_t words = 0;
-    for (size_t i = 0; i < n; ++i) {
-        SDev &d = hs[i];
-        d.lo = d.hi = 0;
-        d.chunk_lo = static_cast<uint32_t>(chunk_slice.size());
-        d.n_chunks = 0;
-        d.bitmap_off = words;
-        if (sl[i].vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "slice " + std::to_string(i) + ": unknown vcf id");
-        const VcfData &v = s.vcfs[sl[i].vcf_id];
-        if (v.blk_coff.empty()) throw Error(SB_EINVAL, "summarise needs a VCF ingested from a BGZF file (virtual offsets)");
-        uint64_t u0, u1;
-        if (!voff_to_stream(v, sl[i].virtual_start, &u0) || !voff_to_stream(v, sl[i].virtual_end, &u1)) {
-            herr[i] = SB_QERR_UNSUPPORTED;  // offset not on a block of this file
-            continue;
-        }
-        if (u1 < u0) u1 = u0;
-        const uint32_t rb = v.rec_base;
-        uint32_t re = rb;
-        for (const auto &sg : v.segments) re = std::max(re, sg.hi);
-        auto first = s.h_start.begin() + rb, last = s.h_start.begin() + re;
-        const uint32_t lo = rb + static_cast<uint32_t>(std::lower_bound(first, last, u0) - first);
-        const uint32_t hi = rb + static_cast<uint32_t>(std::lower_bound(first, last, u1) - first);
-        if (hi > lo) {
-            // the slice must start on a record and must not cut one (index
-            // chunk boundaries are record boundaries); header bytes likewise
-            const uint64_t end_last = hi < re ? s.h_start[hi] : v.stream_len;
-            if (s.h_start[lo] != u0 || end_last > u1) herr[i] = SB_QERR_UNSUPPORTED;
-        } else if (u1 > u0) {
-            herr[i] = SB_QERR_UNSUPPORTED;  // a non-empty stretch with no record start
-        }
-        if (herr[i]) continue;
-        d.lo = lo;
-        d.hi = hi;
-        d.chunk_lo = static_cast<uint32_t>(chunk_slice.size());
-        d.n_chunks = (hi - lo + kSumChunk - 1) / kSumChunk;
-        chunk_slice.insert(chunk_slice.end(), d.n_chunks, static_cast<uint32_t>(i));
-        words += (hi - lo + 63) / 64;
-    }
-    HIP_OK(hipSetDevice(s.device));
-    hipStream_t st = s.stream;
-    if (!s.summarise_ws)
-        s.summarise_ws = std::shared_ptr<void>(new SumWs, [](void *w) { delete static_cast<SumWs *>(w); });
-    SumWs &W = *static_cast<SumWs *>(s.summarise_ws.get());
-    DevMem &dsl = W.dsl, &dbm = W.dbm, &dres = W.dres, &dcs = W.dcs, &dpart = W.dpart;
-    dsl.reserve(n * sizeof(SDev));
-    dbm.reserve(words * 8);  // every word is written by the chunk kernel
-    dres.reserve(n * sizeof(SRes));
-    dcs.reserve(chunk_slice.size() * 4);
-    dpart.reserve(chunk_slice.size() * sizeof(SPart));
-    if (n) HIP_OK(hipMemcpyAsync(dsl.p, hs.data(), n * sizeof(SDev), hipMemcpyHostToDevice, st));
-    if (!chunk_slice.empty())
-        HIP_OK(hipMemcpyAsync(dcs.p, chunk_slice.data(), chunk_slice.size() * 4, hipMemcpyHostToDevice, st));
-    hipEvent_t e0, e1;
-    HIP_OK(hipEventCreate(&e0));
-    HIP_OK(hipEventCreate(&e1));
-    HIP_OK(hipEventRecord(e0, st));
-    launch_summarise(s.ds, dsl.as<SDev>(), static_cast<uint32_t>(n), dcs.as<uint32_t>(),
-                     static_cast<uint32_t>(chunk_slice.size()), dbm.as<uint64_t>(), dpart.as<SPart>(), dres.as<SRes>(),
-                     st);
-    HIP_OK(hipEventRecord(e1, st));
-    HIP_OK(hipGetLastError());
-    std::vector<SRes> r(n);
-    if (n) HIP_OK(hipMemcpyAsync(r.data(), dres.p, n * sizeof(SRes), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    float ms = 0;
-    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    if (device_ms) *device_ms = ms;
-    for (size_t i = 0; i < n; ++i) {
-        out[i].error = herr[i] ? herr[i] : r[i].error;
-        out[i]._pad = 0;
-        out[i].num_variants = out[i].error ? 0 : r[i].num_variants;
-        out[i].num_calls = out[i].error ? 0 : r[i].num_calls;
-        out[i].records = out[i].error ? 0 : r[i].records;
-    }
-}
-
-// ---------------------------------------------------------- region files
-// summariseSlice's region files (lambda/summariseSlice/source/
-// write_data_to_s3.h): the reader visits the records of the slice exactly as
-// main.cpp:217-237 does (first record; then per record addCounts, seek
-// (skipSize), skipPast('\n') — the walk the device summarise kernels
-// reproduce), and recordHeader (:150-228) pushes one entry {pos, ref', alt'}
-// per ALT of every visited record; a file is closed when a record's POS is
-// more than MAX_SLICE_GAP past the buffer's last entry (:191-194) or when the
-// buffer holds more than VCF_S3_OUTPUT_SIZE_LIMIT entries (:224-227), and at
-// the end of the slice (~writeDataToS3).  File length = sum over entries of
-// pos u64 + len u16 + |ref'| + 1 + |alt'| (saveOutputToS3, :39-92).
-constexpr uint64_t kMaxSliceGap = 100000;        // main.tf:215 MAX_SLICE_GAP
-constexpr uint64_t kOutputSizeLimit = 50000000;  // main.tf:17,216 VCF_S3_OUTPUT_SIZE_LIMIT
-
-uint32_t key_tail_len(const sb_store &s, uint64_t k) {
-    const uint64_t t = s.h_dk_tail[k];
-    return (t & kTailBlob) ? static_cast<uint32_t>((t >> 40) & 0xffff) : static_cast<uint32_t>(t >> 56);
-}
-
-void append_key_entry(const sb_store &s, uint64_t k, std::vector<uint8_t> &out) {
-    const uint64_t pos = s.h_dk_pos[k];
-    const uint32_t tl = key_tail_len(s, k);
-    const uint16_t len = static_cast<uint16_t>(tl);
-    const size_t o = out.size();
-    out.resize(o + 10 + tl);
-    memcpy(out.data() + o, &pos, 8);
-    memcpy(out.data() + o + 8, &len, 2);
-    const uint64_t t = s.h_dk_tail[k];
-    if (t & kTailBlob)
-        memcpy(out.data() + o + 10, s.h_dk_blob.data() + (t & ((1ull << 40) - 1)), tl);
-    else
-        for (uint32_t j = 0; j < tl; ++j) out[o + 10 + j] = static_cast<uint8_t>(t >> (8 * j));
-}
-
-// One gzip member of buf (write_data_to_s3.h:51-52,64-65 -> gzip.cpp:19-59):
-// deflateInit2(level 9, 16 + MAX_WBITS, memLevel 9), a header named "c"; the
-// reference leaves the header's other fields uninitialised, here they are 0.
-void gzip_member(const uint8_t *buf, size_t n, std::vector<uint8_t> &out) {
-    z_stream zs{};
-    if (deflateInit2(&zs, Z_BEST_COMPRESSION, Z_DEFLATED, 16 + MAX_WBITS, 9, Z_DEFAULT_STRATEGY) != Z_OK)
-        throw Error(SB_EIO, "deflateInit2 failed");
-    gz_header h{};
-    static char name[] = "c";
-    h.name = reinterpret_cast<Bytef *>(name);
-    deflateSetHeader(&zs, &h);
-    zs.next_in = const_cast<Bytef *>(buf);
-    zs.avail_in = static_cast<uInt>(n);
-    uint8_t chunk[1 << 16];
-    int ret;
-    do {
-        zs.next_out = chunk;
-        zs.avail_out = sizeof chunk;
-        ret = deflate(&zs, Z_FINISH);
-        if (ret == Z_STREAM_ERROR) {
-            deflateEnd(&zs);
-            throw Error(SB_EIO, "deflate failed");
-        }
-        out.insert(out.end(), chunk, chunk + (sizeof chunk - zs.avail_out));
-    } while (zs.avail_out == 0);
-    deflateEnd(&zs);
-}
-
-// one slice: status (0 / SB_QERR_UNSUPPORTED), files appended to `files`,
-// file bytes appended to `data` when non-null (gz: as gzip members)
-int32_t slice_region_files(const sb_store &s, uint32_t si, const sb_slice &sl, std::vector<sb_region_file> &files,
-                           std::vector<uint8_t> *data, bool gz = false,
-                           std::vector<std::vector<uint32_t>> *file_keys = nullptr) {
-    if (sl.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "slice " + std::to_string(si) + ": unknown vcf id");
-    const VcfData &v = s.vcfs[sl.vcf_id];
-    if (v.blk_coff.empty()) throw Error(SB_EINVAL, "region files need a VCF ingested from a BGZF file (virtual offsets)");
-    uint64_t u0, u1;
-    if (!voff_to_stream(v, sl.virtual_start, &u0) || !voff_to_stream(v, sl.virtual_end, &u1)) return SB_QERR_UNSUPPORTED;
-    if (u1 < u0) u1 = u0;
-    const uint32_t rb = v.rec_base;
-    uint32_t re = rb;
-    for (const auto &sg : v.segments) re = std::max(re, sg.hi);
-    auto first = s.h_start.begin() + rb, last = s.h_start.begin() + re;
-    const uint32_t lo = rb + static_cast<uint32_t>(std::lower_bound(first, last, u0) - first);
-    const uint32_t hi = rb + static_cast<uint32_t>(std::lower_bound(first, last, u1) - first);
-    if (hi <= lo) return u1 > u0 ? SB_QERR_UNSUPPORTED : 0;
-    const uint64_t end_last = hi < re ? s.h_start[hi] : v.stream_len;
-    if (s.h_start[lo] != u0 || end_last > u1) return SB_QERR_UNSUPPORTED;
-    // contig of the slice (one contig per slice: index chunks never cross)
-    uint32_t contig = 0;
-    for (uint32_t g = 0; g < v.segments.size(); ++g)
-        if (lo >= v.segments[g].lo && lo < v.segments[g].hi) contig = g;
-    const size_t f0 = files.size();
-    const size_t d0 = data ? data->size() : 0;
-    sb_region_file cur{si, contig, 0, 0, 0, 0, 0};
-    bool open = false;
-    // the open file's bytes and, for gzip output, where saveOutputToS3 cuts
-    // members: before an entry when bufferLength + ref' + alt' + sizeof(pos)
-    // > VCF_S3_OUTPUT_SIZE_LIMIT (write_data_to_s3.h:49)
-    std::vector<uint8_t> fbuf;
-    std::vector<size_t> cuts;
-    size_t member_len = 0;
-    std::vector<uint32_t> fkeys;  // the open file's store keys, in entry order (file_keys)
-    const size_t k0 = file_keys ? file_keys->size() : 0;
-    auto close = [&]() {
-        if (open && cur.entries) {
-            if (file_keys) file_keys->push_back(fkeys);
-            if (data) {
-                const size_t at = data->size();
-                if (gz) {
-                    size_t a = 0;
-                    cuts.push_back(fbuf.size());
-                    for (size_t c : cuts) {
-                        if (c > a) gzip_member(fbuf.data() + a, c - a, *data);
-                        a = c;
-                    }
-                } else {
-                    data->insert(data->end(), fbuf.begin(), fbuf.end());
-                }
-                cur.data_bytes = data->size() - at;
-            }
-            files.push_back(cur);
-        }
-        cur = sb_region_file{si, contig, 0, 0, 0, 0, 0};
-        open = false;
-        fbuf.clear();
-        cuts.clear();
-        member_len = 0;
-        fkeys.clear();
-    };
-    const uint64_t skip = 2ull * s.h_dcount[lo];
-    uint32_t r = lo;
-    while (r < hi) {
-        if (s.h_sum_bad[r]) {  // the reference throws / reads past the line
-            files.resize(f0);
-            if (data) data->resize(d0);
-            if (file_keys) file_keys->resize(k0);
-            return SB_QERR_UNSUPPORTED;
-        }
-        const uint64_t pos = s.h_pos[r];
-        if (open && cur.entries) {
-            if (pos < cur.last_pos) throw Error(SB_EINVAL, "unsorted file");  // write_data_to_s3.h:184-188
-            if (pos > cur.last_pos + kMaxSliceGap) close();
-        }
-        for (uint32_t k = s.h_dk_lo[r]; k < s.h_dk_lo[r + 1]; ++k) {
-            if (!open || !cur.entries) {
-                cur.first_pos = s.h_dk_pos[k];
-                open = true;
-            }
-            cur.last_pos = s.h_dk_pos[k];
-            const uint32_t tl = key_tail_len(s, k);
-            cur.bytes += 10 + tl;
-            ++cur.entries;
-            if (data) {
-                if (gz && member_len + (tl - 1) + 8 > kOutputSizeLimit) {  // ref' + alt' = tail - '_'
-                    cuts.push_back(fbuf.size());
-                    member_len = 0;
-                }
-                append_key_entry(s, k, fbuf);
-                member_len += 10 + tl;
-            }
-            if (file_keys) fkeys.push_back(k);
-        }
-        if (cur.entries > kOutputSizeLimit) close();
-        // next visited record
-        if (r == lo) {
-            r = lo + 1;  // skipPastAndCountChars('\n') ends the first record's line
-        } else if (skip >= s.h_rem[r]) {  // seek(skipSize) lands past this line
-            const uint64_t P = s.h_start[r] + s.h_cur[r] + skip;
-            r = static_cast<uint32_t>(std::upper_bound(s.h_start.begin() + r + 1, s.h_start.begin() + hi, P) -
-                                      s.h_start.begin());
-        } else {
-            ++r;
-        }
-    }
-    close();
-    return 0;
-}
-
-// the key string of store key k: decimal(pos) ++ ref'_alt'
-std::string key_string(const sb_store &s, uint32_t k) {
-    std::string out = std::to_string(s.h_dk_pos[k]);
-    const uint64_t t = s.h_dk_tail[k];
-    if (t & kTailBlob) {
-        const uint64_t off = t & ((1ull << 40) - 1), len = (t >> 40) & 0xffff;
-        out.append(reinterpret_cast<const char *>(s.h_dk_blob.data() + off), len);
-    } else {
-        for (uint64_t j = 0, len = t >> 56; j < len; ++j) out.push_back(static_cast<char>((t >> (8 * j)) & 0xff));
-    }
-    return out;
-}
-
-// dedup scratch, kept per store (sb_store::dedup_ws) and grown on demand
-struct DedupWs {
-    DevMem dseg, dtiles, tcnt, ke0, ke1, kh0, vh0, kh1, vh1, hist, bsum, counts, coll, ncoll, pe, ph, overflow;
-};
-
-void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique, int32_t *status,
-               sb_dedup_stats *stats, bool force_radix = false, std::vector<KRun> *runs = nullptr);
-
-void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, int32_t *status,
-           sb_dedup_stats *stats) {
-    if (nj > (1u << 20)) throw Error(SB_EINVAL, "more than 2^20 dedup jobs in one call");
-    std::vector<KSeg> segs;
-    std::vector<KRun> runs;  // parallel to segs (window path)
-    uint64_t n = 0;
-    for (size_t j = 0; j < nj; ++j) {
-        const sb_dedup_job &J = jobs[j];
-        status[j] = 0;
-        unique[j] = 0;
-        if ((!J.vcf_ids && J.n_vcf) || (!J.contig && J.contig_len)) throw Error(SB_EINVAL, "dedup job: NULL array");
-        const std::string contig(J.contig ? J.contig : "", J.contig_len);
-        std::vector<uint32_t> seen;
-        const size_t seg0 = segs.size();
-        for (uint32_t t = 0; t < J.n_vcf; ++t) {
-            const uint32_t id = J.vcf_ids[t];
-            if (id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "dedup job " + std::to_string(j) + ": unknown vcf id");
-            if (std::find(seen.begin(), seen.end(), id) != seen.end()) continue;  // a file listed twice adds nothing
-            seen.push_back(id);
-            const VcfData &v = s.vcfs[id];
-            auto it = v.seg_index.find(contig);
-            if (it == v.seg_index.end() || J.range_start > J.range_end || J.range_start > 0xffffffffull) continue;
-            const Segment &sg = v.segments[it->second];
-            const uint32_t rs = static_cast<uint32_t>(J.range_start);
-            const uint32_t re = static_cast<uint32_t>(std::min<uint64_t>(J.range_end, 0xffffffffull));
-            // records the reference's summariseSlice throws on, inside the range
-            auto b0 = std::lower_bound(s.h_dk_bad.begin(), s.h_dk_bad.end(), sg.lo);
-            for (auto b = b0; b != s.h_dk_bad.end() && *b < sg.hi; ++b)
-                if (s.h_pos[*b] >= rs && s.h_pos[*b] <= re) status[j] = SB_QERR_UNSUPPORTED;
-            const auto kb = s.h_dk_pos.begin();
-            const uint32_t klo = s.h_dk_lo[sg.lo], khi = s.h_dk_lo[sg.hi];
-            const uint32_t a = static_cast<uint32_t>(std::lower_bound(kb + klo, kb + khi, rs) - kb);
-            const uint32_t e = static_cast<uint32_t>(std::upper_bound(kb + klo, kb + khi, re) - kb);
-            if (e > a) {
-                segs.push_back(KSeg{a, n, e - a, static_cast<uint32_t>(j), rs, 0});
-                const BucketIndex &bi = v.buckets[it->second];
-                runs.push_back(KRun{a, e, s.h_dk_pos[a], s.h_dk_pos[e - 1], sg.lo, sg.hi, bi.base, bi.shift, bi.off,
-                                    bi.n, static_cast<uint32_t>(j), 0, 0, {0, 0}});
-                n += e - a;
-            }
-        }
-        if (status[j]) {  // drop the job's keys
-            for (size_t g = seg0; g < segs.size(); ++g) n -= segs[g].n;
-            segs.resize(seg0);
-            runs.resize(seg0);
-        }
-    }
-    dedup_run(s, segs, n, nj, unique, status, stats, false, &runs);
-}
-
-// ---- window dedup planning (devtypes.hpp KWin / KJob)
-// Every key run of a job is POS-sorted: cutting the job's runs at common POS
-// boundaries into windows of about kWinTarget keys puts all keys of one
-// (string, POS) in one window.  The host only sizes each job (windows =
-// its keys / kWinTarget, its leader run, its POS span); dedup_plan_kernel
-// finds the cuts.  runs[g] = segs[g]'s KRun (key range, POS span, its
-// segment's coarse POS index for the cuts and the twin lookups).
-struct WinPlan {
-    std::vector<KJob> jobs;
-    uint64_t n_wins = 0, n_e = 0;
-    const char *why = "";  // why the plan was declined (SBEACON_DEDUP_DEBUG)
-};
-
-bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan &P) {
-    uint32_t target = kWinTarget;  // SBEACON_DEDUP_WIN_TARGET (tests): smaller windows
-    if (const int k = config().dedup_win_target) target = std::max(1, std::min(static_cast<int>(kWinCap), k));
-    if (s.n_keys >= 0x80000000ull) return P.why = "2^31 keys", false;
-    std::vector<char> seen(nj, 0);
-    for (size_t g0 = 0; g0 < runs.size();) {
-        size_t g1 = g0 + 1;
-        while (g1 < runs.size() && runs[g1].job == runs[g0].job) ++g1;
-        if (seen[runs[g0].job]) return P.why = "job runs not contiguous", false;
-        seen[runs[g0].job] = 1;
-        if (g1 - g0 > kWinPieces) return P.why = "runs", false;
-        KJob J{};
-        uint64_t keys = 0;
-        size_t lead = g0;
-        J.pmin = UINT32_MAX;
-        for (size_t g = g0; g < g1; ++g) {
-            runs[g].run_lo = static_cast<uint32_t>(g0);
-            runs[g].nruns = static_cast<uint32_t>(g1 - g0);
-            const uint32_t k = runs[g].key_hi - runs[g].key_lo;
-            keys += k;
-            if (k > runs[lead].key_hi - runs[lead].key_lo) lead = g;
-            J.pmin = std::min(J.pmin, runs[g].pos_lo);
-            J.pmax = std::max(J.pmax, runs[g].pos_hi);
-        }
-        J.lead_lo = runs[lead].key_lo;
-        J.lead_n = runs[lead].key_hi - runs[lead].key_lo;
-        J.nw = static_cast<uint32_t>(std::min<uint64_t>(std::max<uint64_t>(1, (keys + target - 1) / target), J.lead_n));
-        J.w0 = static_cast<uint32_t>(P.n_wins);
-        J.run_lo = static_cast<uint32_t>(g0);
-        J.nruns = static_cast<uint32_t>(g1 - g0);
-        J.eoff = static_cast<uint32_t>(P.n_e);
-        P.n_wins += J.nw;
-        P.n_e += uint64_t(J.nruns) * (J.nw + 1);
-        if (P.n_wins >= 0x7fffffffull || P.n_e >= 0xffffffffull) return P.why = "windows", false;
-        P.jobs.push_back(J);
-        g0 = g1;
-    }
-    return true;
-}
-
-struct PinnedHost {  // grow-only pinned host staging (hipHostMalloc)
-    void *p = nullptr;
-    size_t bytes = 0;
-    void reserve(size_t n) {
-        if (n <= bytes) return;
-        if (p) (void)hipHostFree(p);
-        p = nullptr;
-        bytes = 0;
-        HIP_OK(hipHostMalloc(&p, n, hipHostMallocDefault));
-        bytes = n;
-    }
-    ~PinnedHost() {
-        if (p) (void)hipHostFree(p);
-    }
-};
-
-struct WinWs {
-    DevMem jobs, wins, e, runs, counts, overflow, list, n_list, wfresh;
-    PinnedHost stage;  // jobs | runs for one H2D copy; counts + overflow back
-};
-
-// the window path: true when it answered every job (counts in unique[])
-bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t nj, uint64_t *unique,
-                      const int32_t *status, sb_dedup_stats *stats) {
-    WinPlan P;
-    const bool dbg = config().dedup_debug;
-    const auto t0 = std::chrono::steady_clock::now();
-    auto since = [&]() { return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(); };
-    if (!plan_windows(s, runs, nj, P)) {
-        if (dbg) std::fprintf(stderr, "[sbeacon] dedup windows: plan declined (%s)\n", P.why);
-        return false;
-    }
-    const double t_plan = since();
-    HIP_OK(hipSetDevice(s.device));
-    hipStream_t st = s.stream;
-    if (!s.win_ws) s.win_ws = std::shared_ptr<void>(new WinWs, [](void *w) { delete static_cast<WinWs *>(w); });
-    WinWs &W = *static_cast<WinWs *>(s.win_ws.get());
-    const uint32_t nw = static_cast<uint32_t>(P.n_wins);
-    W.jobs.reserve(std::max<size_t>(P.jobs.size(), 1) * sizeof(KJob));
-    W.wins.reserve(std::max<size_t>(nw, 1) * sizeof(KWin));
-    W.e.reserve(std::max<size_t>(P.n_e, 1) * 4);
-    W.runs.reserve(std::max<size_t>(runs.size(), 1) * sizeof(KRun));
-    W.counts.reserve(std::max<size_t>(nj, 1) * 8);
-    W.wfresh.reserve(std::max<size_t>(nw, 1) * 4);
-    W.overflow.reserve(4);
-    // deferred displaced keys (10 POS <= the job's largest POS): a list of a
-    // quarter of the keys; a fuller list is an overflow (the sorted path)
-    const uint32_t cap = static_cast<uint32_t>(std::min<uint64_t>(n / 4 + 65536, 0xffffffffull));
-    W.list.reserve(static_cast<size_t>(cap) * 8);
-    W.n_list.reserve(4);
-    HIP_OK(hipMemsetAsync(W.n_list.p, 0, 4, st));
-    // jobs and runs staged in pinned memory: DMA without a pageable bounce;
-    // the previous call's copies have completed (it synchronised)
-    const size_t bj = P.jobs.size() * sizeof(KJob), br = runs.size() * sizeof(KRun);
-    W.stage.reserve(bj + br + 64 + std::max<size_t>(nj, 1) * 8);
-    if (nw) {
-        std::memcpy(W.stage.p, P.jobs.data(), bj);
-        std::memcpy(static_cast<uint8_t *>(W.stage.p) + bj, runs.data(), br);
-        HIP_OK(hipMemcpyAsync(W.jobs.p, W.stage.p, bj, hipMemcpyHostToDevice, st));
-        HIP_OK(hipMemcpyAsync(W.runs.p, static_cast<uint8_t *>(W.stage.p) + bj, br, hipMemcpyHostToDevice, st));
-    }
-    HIP_OK(hipMemsetAsync(W.counts.p, 0, std::max<size_t>(nj, 1) * 8, st));
-    HIP_OK(hipMemsetAsync(W.overflow.p, 0, 4, st));
-    hipEvent_t e0, e1;
-    HIP_OK(hipEventCreate(&e0));
-    HIP_OK(hipEventCreate(&e1));
-    HIP_OK(hipEventRecord(e0, st));
-    launch_window_dedupe(s.dk, W.jobs.as<KJob>(), static_cast<uint32_t>(P.jobs.size()), W.wins.as<KWin>(), nw,
-                         W.e.as<uint32_t>(), W.runs.as<KRun>(), W.counts.as<unsigned long long>(), W.list.as<uint2>(),
-                         W.n_list.as<uint32_t>(), cap, W.overflow.as<uint32_t>(), W.wfresh.as<uint32_t>(), st);
-    HIP_OK(hipEventRecord(e1, st));
-    HIP_OK(hipGetLastError());
-    std::vector<uint64_t> cnt(std::max<size_t>(nj, 1));
-    uint32_t ovf = 0;
-    HIP_OK(hipMemcpyAsync(cnt.data(), W.counts.p, cnt.size() * 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(&ovf, W.overflow.p, 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    float ms = 0;
-    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    if (dbg)
-        std::fprintf(stderr, "[sbeacon] dedup windows: %u windows, plan %.3f ms, all %.3f ms (device %.3f ms)\n", nw,
-                     t_plan, since(), ms);
-    if (ovf) {
-        if (dbg) std::fprintf(stderr, "[sbeacon] dedup windows: device overflow over %u windows\n", nw);
-        return false;
-    }
-    for (size_t j = 0; j < nj; ++j) unique[j] = status[j] ? 0 : cnt[j];
-    if (stats) {
-        stats->keys = n;
-        stats->collisions = 0;
-        stats->device_ms = ms;
-        stats->path = SB_DEDUP_WINDOWS;
-        stats->windows = nw;
-    }
-    return true;
-}
-
-// the device part of duplicateVariantSearch over planned key runs: windows
-// (one read of every key), else gather, radix sort, adjacent-unique (+ host
-// recount of 64-bit word collisions)
-void dedup_run(sb_store &s, const std::vector<KSeg> &segs, uint64_t n, size_t nj, uint64_t *unique, int32_t *status,
-               sb_dedup_stats *stats, bool force_radix, std::vector<KRun> *runs) {
-    if (n >= 0xffffffffull) throw Error(SB_EINVAL, "dedup batch exceeds 2^32 keys; split it");
-    {
-        // SBEACON_DEDUP_EXACT=bucket / radix (tests, A/B) skip the window path
-        const Config cf = config();
-        const bool hash_hook = cf.dedup_hash_bits != 0;
-        if (runs && !force_radix && !hash_hook && !cf.dedup_exact &&
-            dedup_window_run(s, *runs, n, nj, unique, status, stats))
-            return;
-    }
-    uint32_t job_bits = 0;
-    while ((1ull << job_bits) < nj) ++job_bits;
-    uint64_t mask = ~0ull;
-    if (const int b = config().dedup_hash_bits) {  // test hook: force collisions
-        if (b > 0 && b < 64) mask = (1ull << b) - 1;
-    }
-    // exact-word window: POS - rangeStart of every gathered key fits pos_bits
-    uint64_t max_rel = 0;
-    for (const KSeg &g : segs) max_rel = std::max<uint64_t>(max_rel, s.h_dk_pos[g.key_lo + g.n - 1] - g.range_start);
-    uint32_t pos_bits = 1;
-    while (pos_bits < 40 && (max_rel >> pos_bits)) ++pos_bits;
-    if (job_bits + pos_bits + 6 > 64 || mask != ~0ull) pos_bits = 0;  // exact stream off (all keys hashed)
-    const uint32_t exact_job_shift = pos_bits + 6;
-    HIP_OK(hipSetDevice(s.device));
-    hipStream_t st = s.stream;
-    std::vector<uint2> tiles;  // gather tiles: (segment, first key offset)
-    const uint32_t gt = dedup_gather_tile();
-    for (uint32_t g = 0; g < segs.size(); ++g)
-        for (uint32_t o = 0; o < segs[g].n; o += gt) tiles.push_back(uint2{g, o});
-    const uint32_t ntiles = static_cast<uint32_t>(tiles.size());
-    const uint64_t slots = static_cast<uint64_t>(ntiles) * gt;  // sparse gather layout
-    const uint64_t maxt = std::max<uint64_t>(ntiles, (n + gt - 1) / gt);
-    if (!s.dedup_ws) s.dedup_ws = std::shared_ptr<void>(new DedupWs, [](void *w) { delete static_cast<DedupWs *>(w); });
-    DedupWs &W = *static_cast<DedupWs *>(s.dedup_ws.get());
-    DevMem &dseg = W.dseg, &dtiles = W.dtiles, &tcnt = W.tcnt, &ke0 = W.ke0, &ke1 = W.ke1, &kh0 = W.kh0, &vh0 = W.vh0,
-           &kh1 = W.kh1, &vh1 = W.vh1, &hist = W.hist, &bsum = W.bsum, &counts = W.counts, &coll = W.coll,
-           &ncoll = W.ncoll, &pe = W.pe, &ph = W.ph;
-    dseg.reserve(segs.size() * sizeof(KSeg));
-    dtiles.reserve(tiles.size() * sizeof(uint2));
-    tcnt.reserve(2 * static_cast<size_t>(ntiles) * 4);
-    ke0.reserve(slots * 8);
-    ke1.reserve(n * 8);
-    kh0.reserve(slots * 8);
-    vh0.reserve(slots * 4);
-    kh1.reserve(n * 8);
-    vh1.reserve(n * 4);
-    hist.reserve(maxt * 256 * 4);
-    bsum.reserve(radix_bsum_words(maxt * gt) * 4);
-    counts.reserve(std::max<size_t>(nj, 1) * 8);
-    coll.reserve(n * 4);
-    ncoll.reserve(4);
-    if (!segs.empty()) HIP_OK(hipMemcpyAsync(dseg.p, segs.data(), segs.size() * sizeof(KSeg), hipMemcpyHostToDevice, st));
-    if (!tiles.empty())
-        HIP_OK(hipMemcpyAsync(dtiles.p, tiles.data(), tiles.size() * sizeof(uint2), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemsetAsync(counts.p, 0, std::max<size_t>(nj, 1) * 8, st));
-    HIP_OK(hipMemsetAsync(ncoll.p, 0, 4, st));
-    hipEvent_t e0, e1;
-    HIP_OK(hipEventCreate(&e0));
-    HIP_OK(hipEventCreate(&e1));
-    HIP_OK(hipEventRecord(e0, st));
-    launch_dedup_gather(s.dk, dseg.as<KSeg>(), dtiles.as<uint2>(), ntiles, pos_bits, exact_job_shift, job_bits, mask,
-                        ke0.as<uint64_t>(), kh0.as<uint64_t>(), vh0.as<uint32_t>(), tcnt.as<uint32_t>(), st);
-    std::vector<uint32_t> htc(2 * static_cast<size_t>(ntiles));
-    if (!htc.empty()) HIP_OK(hipMemcpyAsync(htc.data(), tcnt.p, htc.size() * 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    uint64_t ne = 0, nh = 0;
-    for (uint32_t t = 0; t < ntiles; ++t) {
-        ne += htc[t];
-        nh += htc[ntiles + t];
-    }
-    if (ne + nh != n) throw Error(SB_EHIP, "dedup gather lost keys");
-    // exact stream: hash buckets (two radix passes on a mix of the word +
-    // an LDS hash set per workgroup; SBEACON_DEDUP_EXACT=radix forces the
-    // full sort) or as many 8-bit radix passes as its words have bits + an
-    // adjacent-unique pass; the first pass compacts the gather tiles
-    const bool bucket = !force_radix && config().dedup_exact != 'r' && ne > 0;
-    const uint32_t be = bucket ? 0u : dedup_unique_blocks(ne), bh = bucket ? 0u : dedup_unique_blocks(nh);
-    pe.reserve(std::max<uint32_t>(be, 1) * sizeof(uint4));
-    ph.reserve(std::max<uint32_t>(bh, 1) * sizeof(uint4));
-    W.overflow.reserve(4);
-    HIP_OK(hipMemsetAsync(W.overflow.p, 0, 4, st));
-    if (bucket) {
-        launch_bucket_dedupe(ke0.as<uint64_t>(), nullptr, ke1.as<uint64_t>(), nullptr, ne, s.dk, exact_job_shift,
-                             static_cast<uint32_t>(nj), counts.as<unsigned long long>(), W.overflow.as<uint32_t>(),
-                             hist.as<uint32_t>(), bsum.as<uint32_t>(), st, tcnt.as<uint32_t>(), ntiles);
-    } else {
-        const int re = launch_radix_sort(ke0.as<uint64_t>(), nullptr, ke1.as<uint64_t>(), nullptr, ne,
-                                         job_bits + pos_bits + 6, hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
-                                         tcnt.as<uint32_t>(), ntiles);
-        launch_dedup_unique(re ? ke1.as<uint64_t>() : ke0.as<uint64_t>(), nullptr, ne, s.dk, exact_job_shift, false,
-                            counts.as<unsigned long long>(), pe.as<uint4>(), coll.as<uint32_t>(), ncoll.as<uint32_t>(),
-                            st);
-    }
-    // hashed stream: (job | hash, key id); hash buckets with equal words
-    // confirmed on the strings (any collision: the sorted path below via the
-    // overflow rerun), or 8 radix passes + adjacent unique with the exact
-    // host recount of collided groups
-    const uint32_t hjob_shift = job_bits ? 64 - job_bits : 64;
-    int rh = 0;
-    if (bucket && nh) {
-        rh = launch_bucket_dedupe(kh0.as<uint64_t>(), vh0.as<uint32_t>(), kh1.as<uint64_t>(), vh1.as<uint32_t>(), nh, s.dk,
-                                  hjob_shift, static_cast<uint32_t>(nj), counts.as<unsigned long long>(),
-                                  W.overflow.as<uint32_t>(), hist.as<uint32_t>(), bsum.as<uint32_t>(), st,
-                                  tcnt.as<uint32_t>() + ntiles, ntiles);
-    } else {
-        rh = launch_radix_sort(kh0.as<uint64_t>(), vh0.as<uint32_t>(), kh1.as<uint64_t>(), vh1.as<uint32_t>(), nh, 64,
-                               hist.as<uint32_t>(), bsum.as<uint32_t>(), st, tcnt.as<uint32_t>() + ntiles, ntiles);
-        launch_dedup_unique((rh ? kh1 : kh0).as<uint64_t>(), (rh ? vh1 : vh0).as<uint32_t>(), nh, s.dk, hjob_shift,
-                            true, counts.as<unsigned long long>(), ph.as<uint4>(), coll.as<uint32_t>(),
-                            ncoll.as<uint32_t>(), st);
-    }
-    DevMem &kh = rh ? kh1 : kh0;
-    DevMem &vh = rh ? vh1 : vh0;
-    HIP_OK(hipEventRecord(e1, st));
-    HIP_OK(hipGetLastError());
-    std::vector<uint64_t> cnt(std::max<size_t>(nj, 1));
-    uint32_t nc = 0, ovf = 0;
-    HIP_OK(hipMemcpyAsync(cnt.data(), counts.p, cnt.size() * 8, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(&nc, ncoll.p, 4, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipMemcpyAsync(&ovf, W.overflow.p, 4, hipMemcpyDeviceToHost, st));
-    std::vector<uint4> hpe(be), hph(bh);
-    if (be) HIP_OK(hipMemcpyAsync(hpe.data(), pe.p, be * sizeof(uint4), hipMemcpyDeviceToHost, st));
-    if (bh) HIP_OK(hipMemcpyAsync(hph.data(), ph.p, bh * sizeof(uint4), hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));
-    for (const auto *P : {&hpe, &hph})
-        for (const uint4 &q : *P) {  // per-block partials: first and last job of each block
-            cnt[q.x] += q.y;
-            if (q.z != q.x) cnt[q.z] += q.w;
-        }
-    float ms = 0;
-    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-    (void)hipEventDestroy(e0);
-    (void)hipEventDestroy(e1);
-    if (ovf) {  // a workgroup's buckets outgrew its hash set: recount with the full sort
-        dedup_run(s, segs, n, nj, unique, status, stats, true);
-        return;
-    }
-    if (nc) {
-        // exact recount of every group holding a collision: the device counted
-        // 1 + (adjacent string changes) for it; replace that by |distinct|
-        const uint64_t n = nh;  // collisions live in the hashed stream
-        std::vector<uint64_t> hk(n);
-        std::vector<uint32_t> hv(n), ci(nc);
-        HIP_OK(hipMemcpy(hk.data(), kh.p, n * 8, hipMemcpyDeviceToHost));
-        HIP_OK(hipMemcpy(hv.data(), vh.p, n * 4, hipMemcpyDeviceToHost));
-        HIP_OK(hipMemcpy(ci.data(), coll.p, nc * 4, hipMemcpyDeviceToHost));
-        std::sort(ci.begin(), ci.end());
-        uint64_t done_to = 0;  // groups end before this index
-        for (uint32_t i : ci) {
-            if (i < done_to) continue;
-            uint64_t g0 = i, g1 = i + 1;
-            while (g0 > 0 && hk[g0 - 1] == hk[i]) --g0;
-            while (g1 < n && hk[g1] == hk[i]) ++g1;
-            std::vector<std::string> strs;
-            for (uint64_t x = g0; x < g1; ++x) strs.push_back(key_string(s, hv[x]));
-            uint64_t adjacent = 1;
-            for (size_t x = 1; x < strs.size(); ++x) adjacent += strs[x] != strs[x - 1];
-            std::sort(strs.begin(), strs.end());
-            const uint64_t exact = static_cast<uint64_t>(std::unique(strs.begin(), strs.end()) - strs.begin());
-            const uint32_t job = job_bits ? static_cast<uint32_t>(hk[i] >> (64 - job_bits)) : 0u;
-            cnt[job] = cnt[job] - adjacent + exact;
-            done_to = g1;
-        }
-    }
-    for (size_t j = 0; j < nj; ++j) unique[j] = status[j] ? 0 : cnt[j];
-    if (stats) {
-        stats->keys = n;
-        stats->collisions = nc;
-        stats->device_ms = ms;
-        stats->path = bucket ? SB_DEDUP_BUCKETS : SB_DEDUP_RADIX;
-        stats->windows = 0;
-    }
-}
-
-// ------------------------------------------------ reference-exact duplicateVariantSearch
-// What ReadVcfData::getVcfData (lambda/duplicateVariantSearch/source/
-// readVcfData.cpp:3-71) inserts from one region file depends on when its
-// gzip reader (lambda/shared/gzip/gzip.cpp:61-144) reports the end of the
-// stream: the loop keeps reading while hasMoreData(), whatever the POS, and
-// only inside the last decompressed window stops after the first entry past
-// rangeEnd.  So the strict mode reads the region files exactly that way, over
-// the gzip members this library writes (sb_slice_region_files with_data = 2):
-// a multi-member stream inflated with Z_BLOCK through a 1 KiB input window
-// into the reader's 1 KiB buffer, the buffer's unread tail moved to its front
-// at every refill.  The entries it would insert are then deduplicated on the
-// device like the intended-range mode's.
-struct RefThrow {};  // a runtime_error of the reference (the Lambda fails)
-
-class RegionReader {  // gzip.cpp:4-17 (constructor), 61-79, 81-144 (proccesData)
-  public:
-    RegionReader(const uint8_t *file, uint64_t size, char *buf, uint32_t buf_size)
-        : file_(file), size_(static_cast<uint32_t>(size)), buf_(buf), buf_size_(buf_size) {
-        if (size > 0xffffffffull) throw RefThrow{};  // gzip.cpp:16
-    }
-    ~RegionReader() {
-        if (live_) inflateEnd(&zs_);
-    }
-    int start() {
-        const int err = inflateInit2(&zs_, 16 + MAX_WBITS);
-        live_ = err == Z_OK;
-        if (err >= 0) more_ = true;
-        return err;
-    }
-    bool more() const { return more_; }
-    uint32_t fill(uint32_t beg, uint32_t end) {
-        if (beg > end) throw RefThrow{};  // "gzip Error: proccesData input invalid"
-        if (beg < end) memmove(buf_, buf_ + beg, end - beg);
-        zs_.avail_out = buf_size_ - (end - beg);
-        zs_.next_out = reinterpret_cast<Bytef *>(buf_ + (end - beg));
-        for (;;) {
-            if (zs_.avail_out == 0) return buf_size_;
-            if (zs_.avail_in == 0) {
-                zs_.avail_in = std::min<uint32_t>(sizeof window_, size_ - read_);
-                zs_.next_in = window_;
-                memcpy(window_, file_ + read_, zs_.avail_in);
-                read_ += zs_.avail_in;
-            }
-            int err = inflate(&zs_, Z_BLOCK);
-            if (err == Z_STREAM_END) {
-                if (zs_.avail_in == 0 && size_ == read_) break;  // end of the file
-                stop();  // another member: start the decompression again
-                if (start() < 0) break;
-            } else if (err < 0 || size_ - read_ + zs_.avail_in <= 8) {
-                break;  // an error, or only the gzip footer left
-            }
-        }
-        stop();
-        return buf_size_ - zs_.avail_out;
-    }
-
-  private:
-    void stop() {
-        more_ = false;
-        if (live_) inflateEnd(&zs_);
-        live_ = false;
-    }
-    const uint8_t *file_;
-    uint32_t size_, read_ = 0;
-    char *buf_;
-    uint32_t buf_size_;
-    z_stream zs_{};
-    bool more_ = false, live_ = false;
-    Bytef window_[1024];
-};
-
-// readVcfData.cpp:3-71 over one region file: the file positions (entry
-// indices) of the entries getVcfData returns.  false = the reference throws.
-bool strict_region_entries(const uint8_t *file, uint64_t size, uint64_t rs, uint64_t re, std::vector<uint32_t> &incl) {
-    constexpr size_t kMin = sizeof(uint64_t) + sizeof(uint16_t);  // readVcfData.hpp:8 MIN_DATA_SIZE
-    char buf[1024];                                               // readVcfData.hpp:7 BUFFER_SIZE
-    size_t pos = 0, len = 0;
-    uint64_t vpos = 0;
-    uint32_t entry = 0;
-    try {
-        RegionReader in(file, size, buf, sizeof buf);
-        in.start();
-        auto avail = [&](size_t need) -> bool {  // checkForAvailableData
-            if (len >= pos + need) return true;
-            if (!in.more()) return false;
-            len = in.fill(static_cast<uint32_t>(pos), static_cast<uint32_t>(len));
-            if (len > 0) {
-                pos = 0;
-                return true;
-            }
-            return false;
-        };
-        do {
-            if (!avail(kMin)) return false;  // "Invalid File Read - getVcfData()"
-            memcpy(&vpos, buf + pos, sizeof vpos);
-            pos += sizeof vpos;
-            uint16_t sl;
-            memcpy(&sl, buf + pos, sizeof sl);
-            if (rs <= vpos) {  // readString
-                pos += sizeof sl;
-                if (!avail(sl)) return false;  // "Invalid File Read - readString()"
-                pos += sl;
-                incl.push_back(entry);
-            } else {
-                pos += sl + sizeof sl;  // skipped with no availability check (:27-30)
-            }
-            ++entry;
-        } while ((len != pos && vpos <= re) || in.more());
-    } catch (const RefThrow &) {
-        return false;
-    }
-    return true;
-}
-
-// The same reader over a whole file, once (every entry read): what a call's
-// (rangeStart, rangeEnd) then selects follows in closed form.  Entries are
-// POS-sorted in a region file, so getVcfData skips a prefix [0, lo) (POS <
-// rangeStart) and reads on; the refills happen at the same entries on the
-// read and the skip path except where an entry's string crosses the end of
-// the buffer -- a skipped one leaves the read position past the data and the
-// next refill throws ("proccesData input invalid").  The loop stops after
-// the first entry at or past the final refill (`last`, more() false from
-// then on) whose POS exceeds rangeEnd; with no final refill before the last
-// entry it runs past the end and throws.
-struct FileProfile {
-    uint32_t n = 0;                   // entries
-    uint32_t last_fill = UINT32_MAX;  // entry during which the stream ended (more() false after it)
-    uint32_t fail_at = UINT32_MAX;    // entry at which the all-read walk failed (n: past the last)
-    bool sorted = true;               // POS non-decreasing (else: the walk per call)
-    bool consec = false;              // the entries' store keys are consecutive
-    std::vector<uint32_t> straddle;   // entries whose string crosses a refill
-    std::vector<uint64_t> vpos;
-};
-
-FileProfile profile_region_file(const uint8_t *file, uint64_t size) {
-    constexpr size_t kMin = sizeof(uint64_t) + sizeof(uint16_t);
-    char buf[1024];
-    size_t pos = 0, len = 0;
-    FileProfile P;
-    uint32_t entry = 0;
-    try {
-        RegionReader in(file, size, buf, sizeof buf);
-        in.start();
-        auto avail = [&](size_t need) -> bool {
-            if (len >= pos + need) return true;
-            if (!in.more()) return false;
-            len = in.fill(static_cast<uint32_t>(pos), static_cast<uint32_t>(len));
-            if (!in.more() && P.last_fill == UINT32_MAX) P.last_fill = entry;
-            if (len > 0) {
-                pos = 0;
-                return true;
-            }
-            return false;
-        };
-        do {
-            if (!avail(kMin)) {
-                P.fail_at = entry;
-                break;
-            }
-            uint64_t vpos;
-            uint16_t sl;
-            memcpy(&vpos, buf + pos, sizeof vpos);
-            pos += sizeof vpos;
-            memcpy(&sl, buf + pos, sizeof sl);
-            pos += sizeof sl;
-            if (len < pos + sl) P.straddle.push_back(entry);
-            if (!avail(sl)) {
-                P.fail_at = entry;
-                break;
-            }
-            pos += sl;
-            if (!P.vpos.empty() && vpos < P.vpos.back()) P.sorted = false;
-            P.vpos.push_back(vpos);
-            ++entry;
-        } while (len != pos || in.more());
-    } catch (const RefThrow &) {
-        P.fail_at = entry;
-    }
-    P.n = static_cast<uint32_t>(P.vpos.size());
-    return P;
-}
-
-// the entries [lo, last] getVcfData returns for (rs, re) (none when lo >
-// last); false = it throws
-bool profile_range(const FileProfile &P, uint64_t rs, uint64_t re, uint32_t &lo, uint32_t &last) {
-    const auto b = P.vpos.begin(), e = P.vpos.end();
-    lo = static_cast<uint32_t>(std::lower_bound(b, e, rs) - b);
-    const bool tail = !(P.last_fill < P.n);  // more() still true after the last entry
-    last = P.n ? P.n - 1 : 0;
-    if (!tail) {  // the first entry at or after the final refill with POS > re ends the loop
-        const uint32_t j = static_cast<uint32_t>(std::upper_bound(b + P.last_fill, e, re) - b);
-        if (j < P.n) last = j;
-    }
-    const uint32_t reach = tail ? P.n : last;  // the last entry the loop starts
-    if (P.fail_at != UINT32_MAX && P.fail_at <= reach) return false;
-    // a skipped entry whose string crosses the buffer end throws when the next entry starts
-    if (!P.straddle.empty() && P.straddle.front() < std::min(lo, reach)) return false;
-    return true;
-}
-
-// A slice's region files as summariseSlice writes them (gzip members, the
-// store key of every entry), kept per store: the reference writes them once
-// and every duplicateVariantSearch message reads them, so strict mode
-// compresses each slice's files once (level 9 dominates: ~10 MB/s) and then
-// only inflates.  Bounded by bytes (cleared when full).
-struct SliceFiles {
-    int32_t status = 0;
-    std::vector<sb_region_file> files;
-    std::vector<uint8_t> data;
-    std::vector<uint64_t> at;  // each file's first byte in data
-    std::vector<std::vector<uint32_t>> keys;
-    std::vector<FileProfile> prof;  // per file (profile_region_file)
-    size_t bytes() const {
-        size_t b = data.size() + files.size() * sizeof(sb_region_file);
-        for (const auto &k : keys) b += k.size() * 4;
-        for (const auto &f : prof) b += f.vpos.size() * 8 + f.straddle.size() * 4;
-        return b;
-    }
-};
-struct RegionCache {
-    std::map<std::tuple<uint32_t, uint64_t, uint64_t>, std::shared_ptr<const SliceFiles>> m;
-    size_t bytes = 0;
-    static constexpr size_t kCap = size_t(8) << 30;
-};
-
-void dedup_files(sb_store &s, const sb_dedup_file_job *jobs, size_t nj, uint64_t *unique, int32_t *status,
-                 sb_dedup_stats *stats) {
-    if (nj > (1u << 20)) throw Error(SB_EINVAL, "more than 2^20 dedup jobs in one call");
-    if (!s.region_cache)  // under the store lock (sb_dedup_count_files)
-        s.region_cache = std::shared_ptr<void>(new RegionCache, [](void *w) { delete static_cast<RegionCache *>(w); });
-    RegionCache &C = *static_cast<RegionCache *>(s.region_cache.get());
-    using Key = std::tuple<uint32_t, uint64_t, uint64_t>;
-    // every (job, file) pair, and the slices not cached yet
-    struct Pair {
-        uint32_t job;
-        const SliceFiles *sf = nullptr;
-        uint32_t file;
-        bool ok = true;
-        bool walked = false;          // entries listed in incl (an unsorted file)
-        uint32_t e_lo = 0, e_hi = 0;  // else the entries [e_lo, e_hi)
-        std::vector<uint32_t> incl;
-    };
-    std::vector<Pair> pairs;
-    std::vector<Key> missing;
-    std::vector<Key> pkey;
-    for (size_t j = 0; j < nj; ++j) {
-        const sb_dedup_file_job &J = jobs[j];
-        status[j] = 0;
-        unique[j] = 0;
-        if (!J.files && J.n_files) throw Error(SB_EINVAL, "dedup job: NULL file list");
-        for (uint32_t t = 0; t < J.n_files; ++t) {
-            const sb_region_ref &F = J.files[t];
-            if (F.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "dedup job " + std::to_string(j) + ": unknown vcf id");
-            const Key key = std::make_tuple(F.vcf_id, F.virtual_start, F.virtual_end);
-            if (!C.m.count(key)) missing.push_back(key);
-            pairs.push_back(Pair{static_cast<uint32_t>(j), nullptr, F.file, true, false, 0, 0, {}});
-            pkey.push_back(key);
-        }
-    }
-    std::sort(missing.begin(), missing.end());
-    missing.erase(std::unique(missing.begin(), missing.end()), missing.end());
-    // the missing slices' files, in parallel (gzip level 9 is the cost)
-    std::vector<std::shared_ptr<SliceFiles>> made(missing.size());
-    std::vector<std::unique_ptr<Error>> errs(missing.size());  // raised when a job reaches that file
-    parallel_for(missing.size(), [&](size_t i) {
-        try {
-            auto sf = std::make_shared<SliceFiles>();
-            const sb_slice sl{std::get<0>(missing[i]), 0, std::get<1>(missing[i]), std::get<2>(missing[i])};
-            sf->status = slice_region_files(s, 0, sl, sf->files, &sf->data, true, &sf->keys);
-            uint64_t a = 0;
-            for (const auto &f : sf->files) {
-                sf->at.push_back(a);
-                a += f.data_bytes;
-            }
-            for (size_t f = 0; f < sf->files.size(); ++f) {
-                sf->prof.push_back(profile_region_file(sf->data.data() + sf->at[f], sf->files[f].data_bytes));
-                const auto &fk = sf->keys[f];
-                bool c = fk.size() == sf->prof.back().n;
-                for (size_t k = 1; c && k < fk.size(); ++k) c = fk[k] == fk[k - 1] + 1;
-                sf->prof.back().consec = c;
-            }
-            made[i] = std::move(sf);
-        } catch (const Error &e) {
-            errs[i] = std::make_unique<Error>(e);
-        } catch (const std::exception &e) {
-            errs[i] = std::make_unique<Error>(SB_EINVAL, e.what());
-        }
-    }, 16, 1);
-    size_t add = 0;
-    for (const auto &m : made)
-        if (m) add += m->bytes();
-    if (C.bytes + add > RegionCache::kCap) {
-        C.m.clear();
-        C.bytes = 0;
-    }
-    // this call's slices stay referenced here even if the cache drops them
-    std::map<Key, std::shared_ptr<const SliceFiles>> use;
-    std::map<Key, const Error *> failed;
-    for (size_t i = 0; i < missing.size(); ++i) {
-        if (!made[i]) {
-            failed[missing[i]] = errs[i].get();
-            continue;
-        }
-        use[missing[i]] = made[i];
-        C.m[missing[i]] = made[i];
-        C.bytes += made[i]->bytes();
-    }
-    for (size_t p = 0; p < pairs.size(); ++p) {
-        if (failed.count(pkey[p])) continue;  // sf stays null
-        auto it = use.find(pkey[p]);
-        if (it == use.end()) it = use.emplace(pkey[p], C.m.at(pkey[p])).first;
-        pairs[p].sf = it->second.get();
-    }
-    // each pair's entries as the reference reader returns them: from the
-    // file's profile (two binary searches), or by the walk itself for an
-    // unsorted file; SBEACON_STRICT_CHECK=1 (tests) runs both and compares
-    const bool check = config().strict_check;
-    std::atomic<bool> mismatch{false};
-    parallel_for(pairs.size(), [&](size_t p) {
-        Pair &P = pairs[p];
-        if (!P.sf) return;
-        const SliceFiles &sf = *P.sf;
-        if (sf.status || P.file >= sf.files.size()) return;  // reported in job order below
-        const sb_dedup_file_job &J = jobs[P.job];
-        const FileProfile &F = sf.prof[P.file];
-        if (F.sorted) {
-            uint32_t lo = 0, last = 0;
-            P.ok = profile_range(F, J.range_start, J.range_end, lo, last);
-            P.e_lo = std::min(lo, F.n);
-            P.e_hi = std::max(P.e_lo, std::min(last + 1, F.n));
-        }
-        if (!F.sorted || check) {
-            std::vector<uint32_t> incl;
-            const bool ok = strict_region_entries(sf.data.data() + sf.at[P.file], sf.files[P.file].data_bytes,
-                                                  J.range_start, J.range_end, incl);
-            if (F.sorted) {
-                bool same = ok == P.ok;
-                if (same && ok) {
-                    same = incl.size() == P.e_hi - P.e_lo;
-                    for (size_t k = 0; same && k < incl.size(); ++k) same = incl[k] == P.e_lo + k;
-                }
-                if (!same) mismatch = true;
-            } else {
-                P.ok = ok;
-                P.walked = true;
-                P.incl = std::move(incl);
-            }
-        }
-    }, 16, 1);
-    if (mismatch) throw Error(SB_EINVAL, "strict dedup: region-file profile disagrees with the reader walk");
-    // key runs in job order (consecutive store keys; KRun pieces of the
-    // window path: a run is cut where the keys stop being consecutive or
-    // leave their contig segment); a job stops at its first failing file
-    std::vector<KSeg> segs;
-    std::vector<KRun> runs;
-    uint64_t n = 0;
-    auto add_run = [&](uint32_t vcf, uint32_t a, uint32_t e, uint32_t j, uint32_t rs) {
-        const VcfData &v = s.vcfs[vcf];
-        while (a < e) {
-            uint32_t k = 0;  // the segment holding key a
-            while (k < v.segments.size() && !(s.h_dk_lo[v.segments[k].lo] <= a && a < s.h_dk_lo[v.segments[k].hi])) ++k;
-            if (k == v.segments.size()) throw Error(SB_EINVAL, "strict dedup: a region-file key outside its VCF");
-            const Segment &sg = v.segments[k];
-            const uint32_t b = std::min(e, s.h_dk_lo[sg.hi]);
-            if (!runs.empty() && runs.back().job == j && runs.back().key_hi == a && runs.back().seg_lo == sg.lo) {
-                runs.back().key_hi = b;  // continues the previous run
-                runs.back().pos_hi = s.h_dk_pos[b - 1];
-                segs.back().n += b - a;
-            } else {
-                const BucketIndex &bi = v.buckets[k];
-                segs.push_back(KSeg{a, n, b - a, j, rs, 0});
-                runs.push_back(KRun{a, b, s.h_dk_pos[a], s.h_dk_pos[b - 1], sg.lo, sg.hi, bi.base, bi.shift, bi.off,
-                                    bi.n, j, 0, 0, {0, 0}});
-            }
-            n += b - a;
-            a = b;
-        }
-    };
-    for (size_t p = 0; p < pairs.size();) {
-        const uint32_t j = pairs[p].job;
-        const uint32_t rs = static_cast<uint32_t>(std::min<uint64_t>(jobs[j].range_start, 0xffffffffull));
-        const size_t seg0 = segs.size();
-        const uint64_t n0 = n;
-        for (; p < pairs.size() && pairs[p].job == j; ++p) {
-            if (status[j]) continue;
-            const Pair &P = pairs[p];
-            if (!P.sf) throw *failed.at(pkey[p]);  // the error writing that slice's files raised
-            const SliceFiles &sf = *P.sf;
-            if (sf.status) {  // that summariseSlice never wrote its files
-                status[j] = sf.status;
-                continue;
-            }
-            if (P.file >= sf.files.size())
-                throw Error(SB_EINVAL, "dedup job " + std::to_string(j) + ": no region file " + std::to_string(P.file) +
-                                           " in that slice");
-            if (!P.ok) {
-                status[j] = SB_QERR_RUNTIME;
-                continue;
-            }
-            const auto &fk = sf.keys[P.file];
-            const uint32_t vcf = std::get<0>(pkey[p]);
-            auto key_of = [&](uint32_t k) { return P.walked ? fk[P.incl[k]] : fk[P.e_lo + k]; };
-            const uint32_t cnt = P.walked ? static_cast<uint32_t>(P.incl.size()) : P.e_hi - P.e_lo;
-            for (uint32_t a = 0; a < cnt;) {  // runs of consecutive store keys
-                uint32_t b = a + 1;
-                if (!P.walked && sf.prof[P.file].consec) b = cnt;  // every key of the file is consecutive
-                else
-                    while (b < cnt && key_of(b) == key_of(b - 1) + 1) ++b;
-                add_run(vcf, key_of(a), key_of(b - 1) + 1, j, rs);
-                a = b;
-            }
-        }
-        if (status[j]) {
-            segs.resize(seg0);
-            runs.resize(seg0);
-            n = n0;
-        }
-    }
-    dedup_run(s, segs, n, nj, unique, status, stats, false, &runs);
-}
-
-}  // namespace
+}  // namespace sb
 
 extern "C" {
-
-int sb_summarise_slices(sb_store *s, const sb_slice *slices, size_t n, sb_slice_stats *out, double *device_ms) {
-    return guard([&] {
-        if (!s || (!slices && n) || (!out && n)) throw Error(SB_EINVAL, "NULL argument");
-        std::lock_guard<std::mutex> lk(s->mu);
-        summarise(*s, slices, n, out, device_ms);
-    });
-}
-
-struct sb_region_files {
-    std::vector<sb_region_file> files;
-    std::vector<uint8_t> data;
-};
-
-int sb_slice_region_files(sb_store *s, const sb_slice *slices, size_t n, int with_data, int32_t *status,
-                          sb_region_files **out) {
-    return guard([&] {
-        if (!s || (!slices && n) || (!status && n) || !out) throw Error(SB_EINVAL, "NULL argument");
-        auto R = std::make_unique<sb_region_files>();
-        if (with_data < 0 || with_data > 2) throw Error(SB_EINVAL, "with_data must be 0, 1 or 2");
-        for (size_t i = 0; i < n; ++i)
-            status[i] = slice_region_files(*s, static_cast<uint32_t>(i), slices[i], R->files,
-                                           with_data ? &R->data : nullptr, with_data == 2);
-        *out = R.release();
-    });
-}
-
-int sb_region_files_get(const sb_region_files *r, const sb_region_file **files, size_t *n, const uint8_t **data,
-                        size_t *data_len) {
-    if (!r || !files || !n) return SB_EINVAL;
-    *files = r->files.data();
-    *n = r->files.size();
-    if (data) *data = r->data.data();
-    if (data_len) *data_len = r->data.size();
-    return SB_OK;
-}
-
-void sb_region_files_free(sb_region_files *r) { delete r; }
-
-int sb_dedup_count(sb_store *s, const sb_dedup_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,
-                   sb_dedup_stats *stats) {
-    return guard([&] {
-        if (!s || (n_jobs && (!jobs || !unique || !status))) throw Error(SB_EINVAL, "NULL argument");
-        std::lock_guard<std::mutex> lk(s->mu);
-        dedup(*s, jobs, n_jobs, unique, status, stats);
-    });
-}
-
-int sb_dedup_count_files(sb_store *s, const sb_dedup_file_job *jobs, size_t n_jobs, uint64_t *unique, int32_t *status,
-                         sb_dedup_stats *stats) {
-    return guard([&] {
-        if (!s || (n_jobs && (!jobs || !unique || !status))) throw Error(SB_EINVAL, "NULL argument");
-        std::lock_guard<std::mutex> lk(s->mu);
-        dedup_files(*s, jobs, n_jobs, unique, status, stats);
-    });
-}
 
 int sb_store_n_contigs(const sb_store *s, uint32_t vcf_id, uint32_t *n) {
     if (!s || !n) return SB_EINVAL;
@@ -3304,960 +1617,6 @@ int sb_store_sample_name(const sb_store *s, uint32_t vcf_id, uint32_t i, const c
     *p = s->vcfs[vcf_id].samples[i].data();
     *len = s->vcfs[vcf_id].samples[i].size();
     return SB_OK;
-}
-
-namespace {
-
-constexpr int64_t kSplitSize = 10000;  // lambda/splitQuery/lambda_function.py:12
-
-// Request batch (sb_requests_prepare): rows = requests.  A request whose
-// slices need none of the order-dependent machinery (variantType query with
-// referenceBases 'N', include_details, no boolean break, a non-negative-AC
-// VCF, no samples, at most kReqChainSlices slices, no VT_SLOW / general
-// record in its window) becomes ONE chain answered by request_eval_kernel;
-// every other request is cut into its splitQuery slices (split_query_sync,
-// lambda/splitQuery/lambda_function.py:74-110) and answered per slice by the
-// query kernels (the batch's query part), its row reduced by request_reduce
-// and gathered by request_deliver_kernel.
-extern "C++" {  // overloads and templates inside the extern "C" block
-
-// Request sources: the sb_request array, or the same requests as columns
-// (sb_request_columns: numeric arrays or scalars, string columns as a
-// dictionary + a code per request).  src(i) is request i as an sb_request.
-struct AosSrc {
-    const sb_request *rq;
-    sb_request operator()(size_t i) const { return rq[i]; }
-};
-
-struct ColSrc {
-    const sb_request_columns &c;
-    static sb_str pick(const sb_str *dict, const uint32_t *code, size_t i) {
-        return dict ? dict[code ? code[i] : 0u] : sb_str{nullptr, 0};
-    }
-    sb_request operator()(size_t i) const {
-        sb_request r{};
-        r.vcf_id = c.vcf_id ? c.vcf_id[i] : c.vcf_id_all;
-        r.contig = c.contig ? c.contig[i] : c.contig_all;
-        r.start_min = c.start_min[i];
-        r.start_max = c.start_max[i];
-        r.end_min = c.end_min ? c.end_min[i] : c.end_min_all;
-        r.end_max = c.end_max ? c.end_max[i] : c.end_max_all;
-        const sb_str ref = pick(c.reference_dict, c.reference_code, i), alt = pick(c.alternate_dict, c.alternate_code, i),
-                     vt = pick(c.variant_type_dict, c.variant_type_code, i),
-                     sn = pick(c.sample_names_dict, c.sample_names_code, i);
-        r.reference_bases = ref.p;
-        r.reference_len = ref.len;
-        r.alternate_bases = alt.p;
-        r.alternate_len = alt.len;
-        r.variant_type = vt.p;
-        r.variant_type_len = vt.len;
-        r.variant_min_length = c.variant_min_length ? c.variant_min_length[i] : c.variant_min_length_all;
-        r.variant_max_length = c.variant_max_length ? c.variant_max_length[i] : c.variant_max_length_all;
-        r.granularity = c.granularity ? c.granularity[i] : c.granularity_all;
-        r.include_details = c.include_details ? c.include_details[i] : c.include_details_all;
-        r.include_samples = c.include_samples ? c.include_samples[i] : c.include_samples_all;
-        r.selected_samples_only = c.selected_samples_only ? c.selected_samples_only[i] : c.selected_samples_only_all;
-        r.strict_variant_type = c.strict_variant_type;
-        r.sample_names = sn.p;
-        r.sample_names_len = sn.len;
-        return r;
-    }
-};
-
-// variantType strings -> (kind, symbolic-ALT LUT offset), each distinct value once
-struct VtResolver {
-    sb_store &s;
-    std::unordered_map<std::string, std::pair<uint32_t, uint32_t>> map;
-    std::vector<uint32_t> lut_all;
-    std::pair<uint32_t, uint32_t> get(const char *p, size_t len) {
-        const std::string vt = p ? std::string(p, len) : std::string("None");
-        auto it = map.find(vt);
-        if (it == map.end()) {
-            const uint32_t kind = !p                    ? VT_OTHER
-                                  : vt == "DEL"        ? VT_DEL
-                                  : vt == "INS"        ? VT_INS
-                                  : vt == "DUP"        ? VT_DUP
-                                  : vt == "DUP:TANDEM" ? VT_DUPT
-                                  : vt == "CNV"        ? VT_CNV
-                                                       : VT_OTHER;
-            const auto lut = sym_lut(s, kind, "<" + vt);
-            const uint32_t off = static_cast<uint32_t>(lut_all.size());
-            lut_all.insert(lut_all.end(), lut.begin(), lut.end());
-            it = map.emplace(vt, std::make_pair(kind, off)).first;
-        }
-        return it->second;
-    }
-};
-
-// a handful of distinct values in practice: a pointer cache in front of the map
-void resolve_vtypes(VtResolver &V, const AosSrc &src, size_t n, std::vector<uint32_t> &vt_of,
-                    std::vector<uint32_t> &lut_of) {
-    struct VtEnt {
-        const char *p;
-        size_t len;
-        uint32_t kind, lut;
-    };
-    std::vector<VtEnt> seen;
-    for (size_t i = 0; i < n; ++i) {
-        const sb_request &x = src.rq[i];
-        if (x.alternate_bases) continue;
-        const VtEnt *hit = nullptr;
-        for (const VtEnt &e : seen)
-            if (e.p == x.variant_type && e.len == x.variant_type_len) {
-                hit = &e;
-                break;
-            }
-        if (!hit) {
-            const auto kl = V.get(x.variant_type, x.variant_type_len);
-            if (seen.size() < 16) seen.push_back(VtEnt{x.variant_type, x.variant_type_len, kl.first, kl.second});
-            vt_of[i] = kl.first;
-            lut_of[i] = kl.second;
-        } else {
-            vt_of[i] = hit->kind;
-            lut_of[i] = hit->lut;
-        }
-    }
-}
-
-// columns: per dictionary entry, then a table lookup per request
-void resolve_vtypes(VtResolver &V, const ColSrc &src, size_t n, std::vector<uint32_t> &vt_of,
-                    std::vector<uint32_t> &lut_of) {
-    const sb_request_columns &c = src.c;
-    std::vector<std::pair<uint32_t, uint32_t>> tab;
-    if (c.variant_type_dict)
-        for (uint32_t d = 0; d < c.n_variant_type; ++d) tab.push_back(V.get(c.variant_type_dict[d].p, c.variant_type_dict[d].len));
-    else
-        tab.push_back(V.get(nullptr, 0));
-    parallel_for(n, [&](size_t i) {
-        const auto &kl = tab[c.variant_type_dict && c.variant_type_code ? c.variant_type_code[i] : 0u];
-        vt_of[i] = kl.first;
-        lut_of[i] = kl.second;
-    });
-}
-
-void check_columns(const sb_request_columns &c, size_t n) {
-    if (n && (!c.start_min || !c.start_max)) throw Error(SB_EINVAL, "start_min / start_max columns are required");
-    auto codes = [&](const char *what, const sb_str *dict, const uint32_t *code, uint32_t nd) {
-        if (!dict) {
-            if (code) throw Error(SB_EINVAL, std::string(what) + ": codes without a dictionary");
-            return;
-        }
-        if (!nd) throw Error(SB_EINVAL, std::string(what) + ": empty dictionary");
-        for (uint32_t d = 0; d < nd; ++d)
-            if (!dict[d].p && dict[d].len) throw Error(SB_EINVAL, std::string(what) + ": NULL string with a length");
-        if (code)
-            for (size_t i = 0; i < n; ++i)
-                if (code[i] >= nd) throw Error(SB_EINVAL, std::string(what) + ": code out of range at request " + std::to_string(i));
-    };
-    codes("reference_bases", c.reference_dict, c.reference_code, c.n_reference);
-    codes("alternate_bases", c.alternate_dict, c.alternate_code, c.n_alternate);
-    codes("variant_type", c.variant_type_dict, c.variant_type_code, c.n_variant_type);
-    codes("sample_names", c.sample_names_dict, c.sample_names_code, c.n_sample_names);
-}
-
-// The per-slice part of a request batch: splitQuery's slices of the rows
-// with cls[i] == 2, in row order (split_query_sync,
-// lambda/splitQuery/lambda_function.py:74-110), planned as one slice batch
-// (prepare); seg[w] .. seg[w + 1] = row w's queries.
-template <class Src>
-void slice_part(sb_batch &B, sb_batch::Req &R, const Src &src, size_t n, const std::vector<uint8_t> &cls,
-                std::vector<uint32_t> &seg) {
-    sb_store &s = *B.s;
-    std::vector<sb_query> qs;
-    std::vector<uint32_t> owner;
-    std::deque<std::string> regions;  // stable storage for the region strings
-    for (size_t i = 0; i < n; ++i) {
-        if (cls[i] != 2) continue;
-        const sb_request x = src(i);
-        const std::string &chrom = s.vcfs[x.vcf_id].segments[x.contig].contig;
-        for (int64_t a = x.start_min; a <= x.start_max; a += kSplitSize) {
-            const int64_t b = std::min(a + kSplitSize - 1, x.start_max);
-            regions.push_back(chrom + ":" + std::to_string(a) + "-" + std::to_string(b));
-            sb_query q{};
-            q.vcf_id = x.vcf_id;
-            q.region = regions.back().data();
-            q.region_len = regions.back().size();
-            q.end_min = x.end_min;
-            q.end_max = x.end_max;
-            q.reference_bases = x.reference_bases;
-            q.reference_len = x.reference_len;
-            q.alternate_bases = x.alternate_bases;
-            q.alternate_len = x.alternate_len;
-            q.variant_type = x.variant_type;
-            q.variant_type_len = x.variant_type_len;
-            q.variant_min_length = x.variant_min_length;
-            q.variant_max_length = x.variant_max_length;
-            q.granularity = x.granularity;
-            q.include_details = x.include_details;
-            q.include_samples = x.include_samples;
-            q.selected_samples_only = x.selected_samples_only;
-            q.strict_variant_type = x.strict_variant_type;
-            q.sample_names = x.sample_names;
-            q.sample_names_len = x.sample_names_len;
-            qs.push_back(q);
-            owner.push_back(static_cast<uint32_t>(i));
-            if (a > INT64_MAX - kSplitSize) break;
-        }
-    }
-    B.no_chains = true;
-    if (!qs.empty()) {
-        prepare(B, qs.data(), qs.size());
-        R.slices = true;
-    }
-    seg.assign(n + 1, 0);
-    for (uint32_t o : owner) ++seg[o + 1];
-    for (size_t w = 0; w < n; ++w) seg[w + 1] += seg[w];
-}
-
-// the per-slice part's row table, host errors and (general records) the
-// inexact-row marks on the device
-void upload_slice_part(sb_batch &B, sb_batch::Req &R, const std::vector<uint32_t> &seg, size_t n, hipStream_t st) {
-    if (!R.slices) return;
-    ReqPool &P = *R.pool;
-    std::vector<uint8_t> he(std::max<size_t>(B.nq, 1), 0);
-    for (uint32_t q = 0; q < B.nq; ++q) he[q] = B.host_err[q] ? 1 : 0;
-    R.sseg = P.get_dev(seg.size() * 4);
-    R.sherr = P.get_dev(he.size());
-    if (B.gen_grid) {  // general records can make a row's counts wider than int64
-        R.wide = P.get_dev(std::max<size_t>(B.nq, 1));
-        R.row_flag = P.get_dev(std::max<size_t>(n, 1));
-    }
-    HIP_OK(hipMemcpyAsync(R.sseg.p, seg.data(), seg.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(R.sherr.p, he.data(), he.size(), hipMemcpyHostToDevice, st));
-    HIP_OK(hipStreamSynchronize(st));  // he / seg are freed by the caller
-}
-
-// sb_requests_prepare_columns, planned on the device: when the columns that
-// decide the chain test are batch-wide scalars (one VCF, referenceBases 'N',
-// alternateBases None, include_details, no boolean break, no samples) the
-// host only packs each request into a 32-byte ReqIn (one streaming pass on
-// 16 threads: window, END / length bounds, kind and LUT, class) and
-// request_plan_kernel forms the runs of 64 rows, resolves every chain's
-// candidate range from the coarse index and its hit capacity, and packs the
-// descriptors; request_stage_scan_kernel lays the runs' staging regions end
-// to end.  One readback (chains, slices, staging total) sizes the buffers.
-// Returns false when the columns do not qualify: prepare_requests plans on
-// the host.  The per-row numbers come from `get` (PackRow: the columns as
-// they are, or the Beacon conversion + shard cut of sb_requests_prepare_beacon
-// fused into the same pass); `full()` gives columns the per-slice part can
-// read (only called when some row goes per slice).
-// The calling thread's planning stream on `device`: concurrent preparers
-// (pipelined callers) neither queue behind nor wait for each other's uploads
-// and planning kernels on the store stream.  Everything planned on it is
-// synchronised before prepare returns.
-hipStream_t planning_stream(int device) {
-    thread_local std::vector<hipStream_t> per_dev;
-    if (per_dev.size() <= static_cast<size_t>(device)) per_dev.resize(device + 1, nullptr);
-    hipStream_t &st = per_dev[device];
-    if (!st) HIP_OK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    return st;
-}
-struct PackRow {
-    uint32_t contig;
-    uint32_t vt;  // variant_type code
-    int64_t smin, smax, emin, emax, vmin, vmax;
-};
-struct ColRows {
-    const sb_request_columns &c;
-    PackRow operator()(size_t i) const {
-        return PackRow{c.contig ? c.contig[i] : c.contig_all,
-                       c.variant_type_dict && c.variant_type_code ? c.variant_type_code[i] : 0u,
-                       c.start_min[i],
-                       c.start_max[i],
-                       c.end_min ? c.end_min[i] : c.end_min_all,
-                       c.end_max ? c.end_max[i] : c.end_max_all,
-                       c.variant_min_length ? c.variant_min_length[i] : c.variant_min_length_all,
-                       c.variant_max_length ? c.variant_max_length[i] : c.variant_max_length_all};
-    }
-};
-template <class Get, class Full>
-bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n, const Get &get, const Full &full) {
-    sb_store &s = *B.s;
-    if (s.device < 0 || n == 0 || n >= (1u << 31) || c.vcf_id || c.vcf_id_all >= s.vcfs.size()) return false;
-    const VcfData &v = s.vcfs[c.vcf_id_all];
-    auto single = [](const sb_str *d, const uint32_t *code, uint32_t nd) { return d && (!code || nd == 1); };
-    if (!v.nonneg || !single(c.reference_dict, c.reference_code, c.n_reference) ||
-        c.reference_dict[0].len != 1 || !c.reference_dict[0].p || c.reference_dict[0].p[0] != 'N')
-        return false;
-    if (c.alternate_dict && !(single(c.alternate_dict, c.alternate_code, c.n_alternate) && !c.alternate_dict[0].p))
-        return false;
-    if (c.granularity || c.granularity_all == SB_GRAN_BOOLEAN || c.include_details || !c.include_details_all ||
-        c.selected_samples_only || c.selected_samples_only_all || c.include_samples || c.strict_variant_type)
-        return false;
-    const bool collect = (c.granularity_all == SB_GRAN_RECORD || c.granularity_all == SB_GRAN_AGGREGATED) &&
-                         c.include_samples_all;
-    if (collect && v.words) return false;
-    const bool trace = config().prep_trace;
-    auto t_last = std::chrono::steady_clock::now();
-    auto tick = [&](const char *what) {
-        if (!trace) return;
-        const auto t = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[prep-dev] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
-        t_last = t;
-    };
-    auto R = std::make_unique<sb_batch::Req>();
-    R->n_rows = static_cast<uint32_t>(n);
-    R->run = kReqRun;
-    R->pool = req_pool(s);
-    ReqPool &P = *R->pool;
-    // variantType dictionary -> (kind, LUT offset)
-    VtResolver V{s, {}, {}};
-    std::vector<std::pair<uint32_t, uint32_t>> tab;
-    if (c.variant_type_dict)
-        for (uint32_t d = 0; d < c.n_variant_type; ++d) tab.push_back(V.get(c.variant_type_dict[d].p, c.variant_type_dict[d].len));
-    else
-        tab.push_back(V.get(nullptr, 0));
-    std::vector<uint32_t> &lut_all = V.lut_all;
-    lut_all.insert(lut_all.end(), 8, 0u);
-    // pack
-    const uint32_t vid = c.vcf_id_all;
-    const auto &slow_pos = s.seg_slow_pos[vid];
-    // one pinned block: the packed requests, then the LUT words, then the
-    // planner's three counters (one upload of each, one readback, one sync)
-    const size_t lut_at = n * sizeof(ReqIn), cnt_at = (lut_at + lut_all.size() * 4 + 15) & ~size_t(15);
-    ReqPool::Pinned pin = P.get_pinned(cnt_at + 32);
-    ReqIn *pk = static_cast<ReqIn *>(pin.p);
-    std::memcpy(static_cast<char *>(pin.p) + lut_at, lut_all.data(), lut_all.size() * 4);
-    std::vector<uint8_t> cls(n, 0);
-    std::atomic<bool> any_slices{false};
-    parallel_for(n, [&](size_t i) {
-        const PackRow x = get(i);
-        const uint32_t contig = x.contig;
-        const int64_t smin = x.smin, smax = x.smax;
-        ReqIn o{0, 0, 0, 0, 0, 0, 0, REQ_NONE};
-        if (contig < v.segments.size() && smin <= smax) {  // else bcftools emits nothing / no slice
-            const int64_t nsl = (smax - smin) / kSplitSize + 1;
-            const auto &kl = tab[x.vt];
-            bool chain = smin >= 1 && smax <= 0xfffffffell && nsl <= kReqChainSlices && kl.second < kReqLutMax;
-            if (chain && !slow_pos[contig].empty()) {  // a VT_SLOW / general record in the window: per slice
-                const auto &sp = slow_pos[contig];
-                auto a = std::lower_bound(sp.begin(), sp.end(), static_cast<uint32_t>(smin));
-                if (a != sp.end() && *a <= static_cast<uint64_t>(smax)) chain = false;
-            }
-            if (!chain) {
-                o.cls = REQ_SLICES;
-                cls[i] = 2;
-                any_slices.store(true, std::memory_order_relaxed);
-            } else {
-                const int64_t emin = x.emin, emax = x.emax;
-                const bool end_void = emax < 0 || emin > 0xffffffffll || emin > emax;
-                o.first = static_cast<uint32_t>(smin);
-                o.last = static_cast<uint32_t>(smax);
-                o.e0 = emin < 0 ? 0u : static_cast<uint32_t>(emin);
-                o.espan = (emax > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(emax)) - o.e0;
-                const int64_t vmin = x.vmin;
-                const int64_t vmax = x.vmax < 0 ? INT64_MAX : x.vmax;
-                const int64_t vl = vmin < 0 ? 0 : vmin, vh = vmax > 255 ? 255 : vmax;
-                o.bits = req_bits(vh < vl ? 256u : static_cast<uint32_t>(vl), vh < vl ? 0u : static_cast<uint32_t>(vh - vl),
-                                  0u, kl.first, end_void);
-                o.seg = v.seg_base + contig;
-                o.lut_off = kl.second;
-                o.cls = REQ_CHAIN | static_cast<uint32_t>(nsl) << 2;
-            }
-        }
-        pk[i] = o;
-    });
-    tick("pack");
-    std::vector<uint32_t> seg;
-    if (any_slices.load()) slice_part(B, *R, ColSrc{full()}, n, cls, seg);
-    tick("slices");
-    HIP_OK(hipSetDevice(s.device));
-    hipStream_t st = planning_stream(s.device);
-    const uint32_t n_runs = static_cast<uint32_t>((n + kRunRows - 1) / kRunRows);
-    const size_t chain_bytes = size_t(n_runs) * kReqRun * sizeof(ReqChain), run_bytes = size_t(n_runs) * sizeof(RowRun);
-    // rc: per run {capacity, slices << 32 | chains} (request_plan_kernel), then the 3 counters
-    DevMem din = P.get_dev(n * sizeof(ReqIn)), rc = P.get_dev(size_t(n_runs) * 16 + 32);
-    R->dchains = P.get_dev(chain_bytes + run_bytes);
-    R->runs_at = chain_bytes;
-    R->n_runs = n_runs;
-    unsigned long long *cnt = reinterpret_cast<unsigned long long *>(rc.as<char>() + size_t(n_runs) * 16);
-    R->lut = P.get_dev(lut_all.size() * 4);
-    R->n_lut = static_cast<uint32_t>(lut_all.size());
-    HIP_OK(hipMemcpyAsync(din.p, pk, n * sizeof(ReqIn), hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync(R->lut.p, static_cast<char *>(pin.p) + lut_at, lut_all.size() * 4, hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemsetAsync(cnt, 0, 32, st));
-    launch_request_plan(s.d, din.as<ReqIn>(), static_cast<uint32_t>(n), R->dchains.as<ReqChain>(),
-                        reinterpret_cast<RowRun *>(R->dchains.as<char>() + chain_bytes), rc.as<unsigned long long>(),
-                        cnt, st);
-    HIP_OK(hipGetLastError());
-    unsigned long long *hc = reinterpret_cast<unsigned long long *>(static_cast<char *>(pin.p) + cnt_at);
-    HIP_OK(hipMemcpyAsync(hc, cnt, 24, hipMemcpyDeviceToHost, st));
-    HIP_OK(hipStreamSynchronize(st));  // uploads, planning and the counters: one wait
-    R->n_chains = hc[0];
-    R->n_chain_slices = hc[1];
-    const uint64_t stage_total = hc[2];
-    tick("plan");
-    P.put_pinned(pin);
-    R->din = std::move(din);  // kept: sb_requests_set_replan re-plans from them
-    R->rcap = std::move(rc);
-    R->n_in = static_cast<uint32_t>(n);
-    R->cap = B.cap_total + stage_total;
-    R->status = P.get_dev(size_t(n_runs) * 8);
-    R->tstatus = P.get_dev(size_t(request_tiles(n_runs)) * 8);
-    R->stage = P.get_dev(stage_total * 4);
-    R->row_src = P.get_dev(R->slices ? n * 8 : 0);
-    upload_slice_part(B, *R, seg, n, st);  // (synchronises when there is a per-slice part)
-    tick("upload");
-    B.req = std::move(R);
-    return true;
-}
-
-#ifdef SBEACON_CHECKS
-// Plan invariants (the sanitizer build, tests/test_host_sanitizers.py): a
-// run's slots hold its chain rows once each (those with candidates first,
-// each row field inside the run, each range the one planned for the row and
-// inside the (segment, kind) pair's candidates); the staging regions are laid
-// end to end and each covers every ALT of its chains' ranges.
-void check_request_plan(const sb_store &s, const sb_batch::Req &R, const ReqChain *hc, const std::vector<uint8_t> &cls,
-                        const std::vector<uint32_t> &clo, const std::vector<uint32_t> &chi, size_t n) {
-    auto fail = [](const std::string &m) { throw Error(SB_EINVAL, "request plan check: " + m); };
-    uint64_t stage = 0, chains = 0;
-    const uint64_t n_cand = s.h_vc_altpre.empty() ? 0 : s.h_vc_altpre.size() - 1;
-    for (size_t r = 0; r < R.runs.size(); ++r) {
-        const RowRun &run = R.runs[r];
-        if (run.row_hi <= run.row_lo || run.row_hi - run.row_lo > kRunRows || run.row_hi > n) fail("run rows");
-        if (run.stage != stage) fail("staging regions not end to end");
-        std::vector<uint8_t> seen(kRunRows, 0);
-        uint64_t cap = 0;
-        bool empty_seen = false;
-        uint32_t j = 0;
-        for (; j < R.run; ++j) {
-            const ReqChain &c = hc[r * R.run + j];
-            if (c.first == 0) break;
-            const uint32_t row = (c.bits >> 17) & 63u;
-            if (run.row_lo + row >= run.row_hi || seen[row]++ || cls[run.row_lo + row] != 1) fail("slot row");
-            const size_t i = run.row_lo + row;
-            if (c.c_lo != clo[i] || c.c_hi != chi[i] || c.c_hi < c.c_lo || c.c_hi > n_cand) fail("slot range");
-            if (c.c_hi > c.c_lo && empty_seen) fail("a chain with candidates after an empty one");
-            empty_seen |= c.c_hi == c.c_lo;
-            cap += s.h_vc_altpre[c.c_hi] - s.h_vc_altpre[c.c_lo];
-            ++chains;
-        }
-        for (uint32_t k = j; k < R.run; ++k)
-            if (hc[r * R.run + k].first != 0) fail("a used slot after an empty one");
-        for (uint32_t i = run.row_lo; i < run.row_hi; ++i)
-            if (cls[i] == 1 && !seen[i - run.row_lo]) fail("a chain row without a slot");
-        stage += cap;
-    }
-    if (chains != R.n_chains) fail("chain count");
-}
-#endif
-
-template <class Src>
-void prepare_requests(sb_batch &B, const Src &src, size_t n) {
-    sb_store &s = *B.s;
-    if (n >= (1u << 31)) throw Error(SB_EINVAL, "too many requests");
-    auto R = std::make_unique<sb_batch::Req>();
-    R->n_rows = static_cast<uint32_t>(n);
-    // SBEACON_PREP_TRACE=1: host phase times to stderr (bench diagnostics)
-    const bool trace = config().prep_trace;
-    auto t_last = std::chrono::steady_clock::now();
-    auto tick = [&](const char *what) {
-        if (!trace) return;
-        const auto t = std::chrono::steady_clock::now();
-        std::fprintf(stderr, "[prep] %-10s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
-        t_last = t;
-    };
-    // variantType strings -> kind + LUT
-    VtResolver V{s, {}, {}};
-    std::vector<uint32_t> vt_of(n, 0u), lut_of(n, 0u);
-    resolve_vtypes(V, src, n, vt_of, lut_of);
-    std::vector<uint32_t> &lut_all = V.lut_all;
-    lut_all.insert(lut_all.end(), 8, 0u);
-    tick("vtypes");
-    // classify: 0 = no slices, 1 = one chain, 2 = per slice (and the slice
-    // count of a chain); the first bad request, if any, is reported
-    std::vector<uint8_t> cls(n, 0);
-    std::vector<uint32_t> nsl_of(n, 0), clo_of(n, 0), chi_of(n, 0);
-    std::atomic<size_t> bad{SIZE_MAX};
-    parallel_for(n, [&](size_t i) {
-        const sb_request x = src(i);
-        if (x.vcf_id >= s.vcfs.size() || (!x.reference_bases && x.reference_len)) {
-            size_t b = bad.load(std::memory_order_relaxed);
-            while (i < b && !bad.compare_exchange_weak(b, i, std::memory_order_relaxed)) {
-            }
-            return;
-        }
-        const VcfData &v = s.vcfs[x.vcf_id];
-        if (x.contig >= v.segments.size() || x.start_min > x.start_max) return;  // bcftools emits nothing / no slice
-        const int64_t nsl = (x.start_max - x.start_min) / kSplitSize + 1;
-        const bool collect = (x.granularity == SB_GRAN_RECORD || x.granularity == SB_GRAN_AGGREGATED) &&
-                             (x.selected_samples_only || x.include_samples);
-        bool chain = !x.alternate_bases && x.reference_bases && x.reference_len == 1 && x.reference_bases[0] == 'N' &&
-                     x.include_details && x.granularity != SB_GRAN_BOOLEAN && !x.selected_samples_only &&
-                     !x.strict_variant_type && !(collect && v.words) && v.nonneg && nsl <= kReqChainSlices &&
-                     x.start_min >= 1 && x.start_max <= 0xfffffffell && lut_of[i] < kReqLutMax;
-        if (chain) {  // a VT_SLOW / general record in the window: per slice
-            const auto &sp = s.seg_slow_pos[x.vcf_id][x.contig];
-            auto a = std::lower_bound(sp.begin(), sp.end(), static_cast<uint32_t>(x.start_min));
-            if (a != sp.end() && *a <= static_cast<uint64_t>(x.start_max)) chain = false;
-        }
-        cls[i] = chain ? 1 : 2;
-        if (chain) {
-            nsl_of[i] = static_cast<uint32_t>(nsl);
-            // the candidate range from the (kind, segment) coarse index (no
-            // END can match: none)
-            const VcIndex &vi = v.vc_index[x.contig][vt_of[i]];
-            auto cb = [&](uint64_t xx, uint32_t up) -> uint32_t {
-                if (xx <= vi.base) return vi.c_lo;
-                const uint64_t b = (xx - vi.base) >> vi.shift;
-                return b >= vi.n ? vi.c_hi : s.h_vc_bucket[vi.off + b + up];
-            };
-            const int64_t emin = x.end_min, emax = x.end_max;
-            const bool end_void = emax < 0 || emin > 0xffffffffll || emin > emax;
-            const uint32_t C0 = cb(static_cast<uint64_t>(x.start_min), 0);
-            clo_of[i] = C0;
-            chi_of[i] = end_void ? C0 : std::max(C0, cb(static_cast<uint64_t>(x.start_max) + 1, 1));
-        }
-    });
-    if (bad.load() != SIZE_MAX) {
-        const size_t i = bad.load();
-        const sb_request x = src(i);
-        if (x.vcf_id >= s.vcfs.size()) throw Error(SB_ENOSTORE, "request " + std::to_string(i) + ": unknown vcf id");
-        throw Error(SB_EINVAL, "request " + std::to_string(i) + ": bad REF");
-    }
-    tick("classify");
-    // the per-slice part: splitQuery's slices of the other requests, in row order
-    std::vector<uint32_t> seg;
-    slice_part(B, *R, src, n, cls, seg);
-    tick("slices");
-    // runs of consecutive rows (<= kRunRows rows, R->run chains, every chain
-    // starting below position kReqStartPos of the run's candidates), formed
-    // greedily in blocks of rows on several threads (a block boundary also
-    // ends a run)
-    R->run = req_run_max();
-    const uint32_t run_max = R->run;
-    constexpr uint64_t kReqStartPos = 64ull * kReqStartChunks;
-    {
-        const size_t nb = std::max<size_t>(1, std::min<size_t>(16, n / 65536));
-        std::vector<std::vector<RowRun>> part(nb);
-        std::vector<uint64_t> part_chains(nb, 0), part_slices(nb, 0);
-        parallel_for(nb, [&](size_t k) {
-            const uint32_t r0 = static_cast<uint32_t>(n * k / nb), r1 = static_cast<uint32_t>(n * (k + 1) / nb);
-            auto &out = part[k];
-            out.reserve((r1 - r0) / 16 + 1);
-            RowRun cur{r0, r0, 0, 0, 0, 0, kRunSimple};
-            uint32_t c = 0;
-            uint64_t sl = 0, tpos = 0;  // the run's candidates so far
-            for (uint32_t i = r0; i < r1; ++i) {
-                const bool ch = cls[i] == 1;
-                const uint32_t need = nsl_of[i];
-                if (i > cur.row_lo && (i - cur.row_lo == kRunRows ||
-                                       (ch && (cur.c_hi - cur.c_lo == run_max || tpos >= kReqStartPos)))) {
-                    cur.row_hi = i;
-                    out.push_back(cur);
-                    cur = RowRun{i, i, c, c, 0, 0, kRunSimple};
-                    tpos = 0;
-                }
-                if (cls[i] == 2) cur.flags &= ~kRunSimple;  // a row answered per slice: gathered row by row
-                if (ch) {
-                    cur.c_hi = ++c;
-                    cur.n_slots += need;
-                    sl += need;
-                    tpos += chi_of[i] - clo_of[i];
-                }
-            }
-            if (r1 > r0) {
-                cur.row_hi = r1;
-                out.push_back(cur);
-            }
-            part_chains[k] = c;
-            part_slices[k] = sl;
-        }, 16, 1);
-        size_t total = 0;
-        for (auto &p : part) total += p.size();
-        R->runs.reserve(total);
-        uint32_t cbase = 0;
-        for (size_t k = 0; k < nb; ++k) {  // chain ordinals made batch-wide
-            for (RowRun r : part[k]) {
-                r.c_lo += cbase;
-                r.c_hi += cbase;
-                R->runs.push_back(r);
-            }
-            cbase += static_cast<uint32_t>(part_chains[k]);
-            R->n_chain_slices += part_slices[k];
-        }
-        R->n_chains = cbase;
-    }
-    tick("runs");
-    // chain descriptors straight into pinned staging, kReqRun slots per run
-    // (request_eval_kernel loads a run's slots beside its RowRun), the runs
-    // after them: one H2D copy from pinned memory
-    const size_t n_runs = R->runs.size(), slots = run_max;
-    const size_t chain_bytes = n_runs * slots * sizeof(ReqChain), run_bytes = n_runs * sizeof(RowRun);
-    R->pool = req_pool(s);
-    const bool host_only = s.device < 0;
-    ReqPool::Pinned pin = host_only ? ReqPool::Pinned{} : R->pool->get_pinned(chain_bytes + run_bytes);
-    if (host_only) {  // no device: the plan is kept in host memory (R->hplan)
-        R->hplan.resize(chain_bytes + run_bytes);
-        pin.p = R->hplan.data();
-    }
-    ReqChain *hc = static_cast<ReqChain *>(pin.p);
-    RowRun *hr = reinterpret_cast<RowRun *>(static_cast<char *>(pin.p) + chain_bytes);
-    std::vector<uint64_t> rcap(n_runs, 0);  // each run's hit capacity (staging slots)
-    parallel_for(n_runs, [&](size_t r) {
-        const RowRun &run = R->runs[r];
-        ReqChain *out = hc + r * slots;
-        uint32_t j = 0;
-        uint64_t cap = 0;
-        // the chains with candidates first (row order: their hits are staged
-        // in slot order), then those without
-        for (int pass = 0; pass < 2; ++pass)
-        for (uint32_t i = run.row_lo; i < run.row_hi; ++i) {
-            if (cls[i] != 1 || (chi_of[i] > clo_of[i]) != (pass == 0)) continue;
-            const sb_request x = src(i);
-            ReqChain &cd = out[j++];
-            cd.first = static_cast<uint32_t>(x.start_min);
-            cd.last = static_cast<uint32_t>(x.start_max);
-            const int64_t emin = x.end_min, emax = x.end_max;
-            const bool end_void = emax < 0 || emin > 0xffffffffll || emin > emax;
-            cd.e0 = emin < 0 ? 0u : static_cast<uint32_t>(emin);
-            cd.espan = (emax > 0xffffffffll ? 0xffffffffu : static_cast<uint32_t>(emax)) - cd.e0;
-            const int64_t vmax = x.variant_max_length < 0 ? INT64_MAX : x.variant_max_length;
-            const int64_t vl = x.variant_min_length < 0 ? 0 : x.variant_min_length, vh = vmax > 255 ? 255 : vmax;
-            cd.bits = req_bits(vh < vl ? 256u : static_cast<uint32_t>(vl), vh < vl ? 0u : static_cast<uint32_t>(vh - vl),
-                               i - run.row_lo, vt_of[i], end_void);
-            cd.lut_off = lut_of[i];
-            // the candidate range (classify); hit capacity: every ALT of it
-            cd.c_lo = clo_of[i];
-            cd.c_hi = chi_of[i];
-            cap += s.h_vc_altpre[cd.c_hi] - s.h_vc_altpre[cd.c_lo];
-        }
-        std::memset(static_cast<void *>(out + j), 0, (slots - j) * sizeof(ReqChain));  // empty slots: first == 0
-        rcap[r] = cap;
-    });
-    uint64_t stage_total = 0;  // staging slots: every run's chain hit capacity, back to back
-    for (size_t r = 0; r < n_runs; ++r) {
-        R->runs[r].stage = stage_total;
-        stage_total += rcap[r];
-    }
-    std::memcpy(static_cast<void *>(hr), R->runs.data(), run_bytes);
-    R->cap = B.cap_total + stage_total;
-    R->n_runs = static_cast<uint32_t>(n_runs);
-    R->runs_at = chain_bytes;
-    tick("chains");
-#ifdef SBEACON_CHECKS
-    check_request_plan(s, *R, hc, cls, clo_of, chi_of, n);
-#endif
-    if (host_only) {
-        B.req = std::move(R);
-        return;
-    }
-    // device buffers (pooled per store: a batch returns them when freed)
-    HIP_OK(hipSetDevice(s.device));
-    hipStream_t st = s.stream;
-    ReqPool &P = *R->pool;
-    R->dchains = P.get_dev(chain_bytes + run_bytes);
-    R->status = P.get_dev(n_runs * 8);
-    R->tstatus = P.get_dev(size_t(request_tiles(static_cast<uint32_t>(n_runs))) * 8);
-    R->stage = P.get_dev(stage_total * 4);
-    R->row_src = P.get_dev(R->slices || std::any_of(R->runs.begin(), R->runs.end(),
-                                                    [](const RowRun &r) { return !(r.flags & kRunSimple); })
-                               ? size_t(n) * 8 : 0);
-    R->lut = P.get_dev(lut_all.size() * 4);
-    R->n_lut = static_cast<uint32_t>(lut_all.size());
-    if (chain_bytes + run_bytes)
-        HIP_OK(hipMemcpyAsync(R->dchains.p, pin.p, chain_bytes + run_bytes, hipMemcpyHostToDevice, st));
-    R->runs_at = chain_bytes;
-    HIP_OK(hipMemcpyAsync(R->lut.p, lut_all.data(), lut_all.size() * 4, hipMemcpyHostToDevice, st));
-    upload_slice_part(B, *R, seg, n, st);
-    HIP_OK(hipStreamSynchronize(st));
-    R->n_runs = static_cast<uint32_t>(n_runs);
-    P.put_pinned(pin);
-    tick("upload");
-    B.req = std::move(R);
-}
-
-}  // extern "C++"
-
-void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t rec_base) {
-    sb_store &s = *B.s;
-    sb_batch::Req &R = *B.req;
-    if (s.device < 0) throw Error(SB_EHIP, "the store has no device image (SB_HOST_ONLY)");
-    HIP_OK(hipSetDevice(s.device));
-    hipStream_t st = B.strm();
-    mark_run(B);
-    if (R.slices) {  // the per-slice part, then its rows (chain rows come out zero; the row kernel writes them)
-        run_kernels(B);
-        if (R.wide.p) {
-            HIP_OK(hipMemsetAsync(R.wide.p, 0, B.nq, st));
-            mark_wide(B.gen_big_n.as<uint32_t>(), B.gen_big.as<GenBig>(), B.gen_big_cap, R.wide.as<uint8_t>(), st);
-        }
-        launch_request_reduce(B.res.as<QRes>(), R.sseg.as<uint32_t>(), R.sherr.as<uint8_t>(), R.wide.as<uint8_t>(),
-                              R.n_rows, static_cast<ReqPartial *>(rows), R.row_flag.as<uint8_t>(), st);
-    }
-    if (!R.err.p) {
-        R.err = R.pool->get_dev(16);
-        R.err_h = R.pool->get_pinned(16);
-        HIP_OK(hipMemsetAsync(R.err.p, 0, 16, st));
-    }
-    if (R.compact && rec_base + s.n_records > kStageCandMask)
-        throw Error(SB_EINVAL, "compact request output: record numbers (rec_base + records) reach 2^29");
-    if (R.replan) {  // the planning kernels again, from the resident packed requests (same descriptors, same sizes)
-        launch_request_plan(s.d, R.din.as<ReqIn>(), R.n_in, R.dchains.as<ReqChain>(),
-                            reinterpret_cast<RowRun *>(R.dchains.as<char>() + R.runs_at), R.rcap.as<unsigned long long>(),
-                            reinterpret_cast<unsigned long long *>(R.rcap.as<char>() + size_t(R.n_runs) * 16), st);
-        HIP_OK(hipGetLastError());
-    }
-    DStore d = s.d;
-    d.sym_lut = R.lut.as<uint32_t>();
-    std::array<hipEvent_t, 2> ev{nullptr, nullptr};
-    if (R.time_eval) {
-        if (R.eval_used == R.eval_ev.size()) {
-            std::array<hipEvent_t, 2> p{};
-            for (auto &e : p) HIP_OK(hipEventCreate(&e));
-            R.eval_ev.push_back(p);
-        }
-        ev = R.eval_ev[R.eval_used++];
-    }
-    launch_request_rows(d, R.dchains.as<ReqChain>(), reinterpret_cast<const RowRun *>(R.dchains.as<char>() + R.runs_at),
-                        R.n_runs,
-                        R.status.as<unsigned long long>(), R.tstatus.as<unsigned long long>(),
-                        R.slices ? B.res.as<QRes>() : nullptr,
-                        R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
-                        static_cast<ReqPartial *>(rows), static_cast<uint64_t *>(row_off), R.row_src.as<uint64_t>(),
-                        R.stage.as<uint32_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
-                        R.err.as<unsigned int>(), R.compact, st, ev[0], ev[1]);
-    HIP_OK(hipGetLastError());
-}
-
-}  // namespace
-
-int sb_requests_prepare(sb_store *s, const sb_request *r, size_t n, sb_batch **out) {
-    return guard([&] {
-        if (!s || (!r && n) || !out) throw Error(SB_EINVAL, "NULL argument");
-        // request batches do not take the store lock: planning reads the
-        // store's host columns only, and each batch owns its device buffers
-        // (runs on separate streams overlap on the device)
-        auto B = std::make_unique<sb_batch>();
-        B->s = s;
-        prepare_requests(*B, AosSrc{r}, n);
-        store_hold(s);
-        *out = B.release();
-    });
-}
-
-int sb_requests_prepare_columns(sb_store *s, const sb_request_columns *c, size_t n, sb_batch **out) {
-    return guard([&] {
-        if (!s || (!c && n) || !out) throw Error(SB_EINVAL, "NULL argument");
-        static const sb_request_columns kNone{};
-        const sb_request_columns &cc = c ? *c : kNone;
-        check_columns(cc, n);
-        auto B = std::make_unique<sb_batch>();
-        B->s = s;
-        if (!prepare_requests_device(*B, cc, n, ColRows{cc}, [&]() -> const sb_request_columns & { return cc; }))
-            prepare_requests(*B, ColSrc{cc}, n);
-        store_hold(s);
-        *out = B.release();
-    });
-}
-
-namespace {
-// sb_requests_prepare_beacon: row i's SplitQueryPayload numbers
-// (search_variants.py:179-197) cut to the shard core (ShardPlan.slice_runs,
-// sbeacon/sharding.py): slice k of [start_min, start_max] starts at
-// start_min + 10000 k; the core keeps the slices k0 <= k < k1
-struct BeaconRows {
-    const sb_beacon_requests &q;
-    const sb_shard_core *core;
-    std::atomic<size_t> *bad;  // first row with a variant_type code out of range
-    // first slice index routed at or past key (kc, kp): ceil((kp - smin) / 10000) clipped to [0, nsl]
-    static int64_t first_k(uint32_t c, int64_t smin, int64_t nsl, uint32_t kc, int64_t kp) {
-        if (c > kc) return 0;
-        if (c < kc) return nsl;
-        if (kp <= smin) return 0;
-        const uint64_t d = static_cast<uint64_t>(kp) - static_cast<uint64_t>(smin);  // > 0, exact in 64 bits
-        const uint64_t need = d / kSplitSize + (d % kSplitSize != 0);
-        return need >= static_cast<uint64_t>(nsl) ? nsl : static_cast<int64_t>(need);
-    }
-    PackRow operator()(size_t i) const {
-        // the core is cut in the caller's contig codes (the VCF's contig
-        // order: a shard store may hold only some of the contigs), then the
-        // code is mapped to the store's contig index
-        const int64_t code = q.contig[i];
-        const uint32_t cc = code >= 0 && code < UINT32_MAX ? static_cast<uint32_t>(code) : UINT32_MAX;
-        uint32_t contig = UINT32_MAX;
-        if (!q.contig_map) contig = cc;
-        else if (cc < q.n_contig_map) contig = q.contig_map[cc];
-        const int64_t s0 = q.start[i], e0 = q.end[i];
-        int64_t smin = s0, smax, emin, emax;
-        if (q.end2) {
-            emin = e0;
-            emax = q.end2[i];
-        } else {
-            emin = s0;
-            emax = e0;
-        }
-        smax = q.start2 ? q.start2[i] : emax;
-        constexpr int64_t kLim = int64_t(1) << 62;  // past any contig: a row with no slices (no overflow below)
-        auto out = [&](int64_t x) { return x < -kLim || x > kLim; };
-        if (out(smin) || out(smax) || out(emin) || out(emax)) {
-            contig = UINT32_MAX;
-            smin = smax = emin = emax = 0;
-        }
-        ++smin, ++smax, ++emin, ++emax;
-        if (core && smin <= smax) {
-            const int64_t nsl = (smax - smin) / kSplitSize + 1;
-            const int64_t k0 = core->contig_lo == UINT32_MAX ? nsl : first_k(cc, smin, nsl, core->contig_lo, core->pos_lo);
-            const int64_t k1 =
-                std::max(k0, core->contig_hi == UINT32_MAX ? nsl : first_k(cc, smin, nsl, core->contig_hi, core->pos_hi));
-            const int64_t a = smin + kSplitSize * k0;
-            smax = k1 > k0 ? std::min(smax, smin + kSplitSize * k1 - 1) : a - 1;
-            smin = a;
-        }
-        uint32_t vt = 0;
-        if (q.variant_type_dict && q.variant_type_code) {
-            const int64_t v = q.variant_type_code[i];
-            if (v < 0 || v >= q.n_variant_type) {
-                size_t cur = bad->load(std::memory_order_relaxed);
-                while (i < cur && !bad->compare_exchange_weak(cur, i)) {
-                }
-            } else {
-                vt = static_cast<uint32_t>(v);
-            }
-        }
-        return PackRow{contig, vt, smin, smax, emin, emax,
-                       q.variant_min_length ? q.variant_min_length[i] : q.variant_min_length_all,
-                       q.variant_max_length ? q.variant_max_length[i] : q.variant_max_length_all};
-    }
-};
-
-// the same rows as sb_request_columns arrays (the host planner and the
-// per-slice part read columns)
-struct BeaconColumns {
-    std::vector<uint32_t> contig, vt;
-    std::vector<int64_t> smin, smax, emin, emax, vmin, vmax;
-    sb_request_columns c{};
-    BeaconColumns(const sb_request_columns &base, const BeaconRows &rows, size_t n)
-        : contig(n), vt(n), smin(n), smax(n), emin(n), emax(n), vmin(n), vmax(n), c(base) {
-        parallel_for(n, [&](size_t i) {
-            const PackRow x = rows(i);
-            contig[i] = x.contig;
-            vt[i] = x.vt;
-            smin[i] = x.smin;
-            smax[i] = x.smax;
-            emin[i] = x.emin;
-            emax[i] = x.emax;
-            vmin[i] = x.vmin;
-            vmax[i] = x.vmax;
-        });
-        c.contig = contig.data();
-        c.start_min = smin.data();
-        c.start_max = smax.data();
-        c.end_min = emin.data();
-        c.end_max = emax.data();
-        c.variant_min_length = vmin.data();
-        c.variant_max_length = vmax.data();
-        if (c.variant_type_dict) c.variant_type_code = vt.data();
-    }
-};
-}  // namespace
-
-int sb_requests_prepare_beacon(sb_store *s, const sb_beacon_requests *q, size_t n, const sb_shard_core *core,
-                               sb_batch **out) {
-    return guard([&] {
-        if (!s || !q || !out) throw Error(SB_EINVAL, "NULL argument");
-        if (n && (!q->contig || !q->start || !q->end)) throw Error(SB_EINVAL, "contig / start / end columns are required");
-        if (q->vcf_id >= s->vcfs.size()) throw Error(SB_EINVAL, "vcf_id out of range");
-        if (q->variant_type_dict && !q->n_variant_type) throw Error(SB_EINVAL, "variant_type: empty dictionary");
-        if (!q->variant_type_dict && q->variant_type_code) throw Error(SB_EINVAL, "variant_type: codes without a dictionary");
-        if (q->reference_bases.len && !q->reference_bases.p) throw Error(SB_EINVAL, "reference_bases: NULL with a length");
-        if (q->alternate_bases.len && !q->alternate_bases.p) throw Error(SB_EINVAL, "alternate_bases: NULL with a length");
-        // the batch-wide values as columns with scalars (the qualification
-        // of the device planner reads these)
-        sb_request_columns c{};
-        c.vcf_id_all = q->vcf_id;
-        c.reference_dict = q->reference_bases.p ? &q->reference_bases : nullptr;
-        c.n_reference = c.reference_dict ? 1 : 0;
-        c.alternate_dict = q->alternate_bases.p ? &q->alternate_bases : nullptr;
-        c.n_alternate = c.alternate_dict ? 1 : 0;
-        c.variant_type_dict = q->variant_type_dict;
-        c.n_variant_type = q->variant_type_dict ? q->n_variant_type : 0;
-        c.variant_min_length_all = q->variant_min_length_all;
-        c.variant_max_length_all = q->variant_max_length_all;
-        c.granularity_all = q->granularity;
-        c.include_details_all = q->include_details;
-        std::atomic<size_t> bad{SIZE_MAX};
-        const BeaconRows rows{*q, core, &bad};
-        auto B = std::make_unique<sb_batch>();
-        B->s = s;
-        std::unique_ptr<BeaconColumns> cols;
-        auto full = [&]() -> const sb_request_columns & {
-            if (!cols) cols = std::make_unique<BeaconColumns>(c, rows, n);
-            return cols->c;
-        };
-        auto check_codes = [&] {
-            if (bad.load() != SIZE_MAX)
-                throw Error(SB_EINVAL, "variant_type: code out of range at request " + std::to_string(bad.load()));
-        };
-        if (!prepare_requests_device(*B, c, n, rows, full)) {
-            const sb_request_columns &m = full();
-            check_codes();
-            prepare_requests(*B, ColSrc{m}, n);
-        }
-        check_codes();
-        store_hold(s);
-        *out = B.release();
-    });
-}
-
-int sb_requests_run(sb_batch *b, void *dev_rows, void *dev_hits, void *dev_row_off, uint64_t rec_base) {
-    return guard([&] {
-        if (!b) throw Error(SB_EINVAL, "NULL batch");
-        if (!b->req) throw Error(SB_EINVAL, "not a request batch (sb_requests_prepare)");
-        if ((!dev_rows && b->req->n_rows) || (!dev_hits && b->req->cap) || !dev_row_off)
-            throw Error(SB_EINVAL, "NULL argument");
-        std::lock_guard<std::mutex> lk(b->mu);  // this batch's buffers only (see sb_requests_prepare)
-        run_requests(*b, dev_rows, dev_hits, dev_row_off, rec_base);
-    });
-}
-
-int sb_requests_inexact_rows(sb_batch *b, uint8_t *flags) {
-    return guard([&] {
-        if (!b || (!flags && b->req && b->req->n_rows)) throw Error(SB_EINVAL, "NULL argument");
-        if (!b->req) throw Error(SB_EINVAL, "not a request batch (sb_requests_prepare)");
-        sb_batch::Req &R = *b->req;
-        std::lock_guard<std::mutex> lk(b->mu);
-        if (!R.row_flag.p) {
-            std::memset(flags, 0, R.n_rows);
-            return;
-        }
-        HIP_OK(hipSetDevice(b->s->device));
-        HIP_OK(hipStreamSynchronize(b->strm()));
-        HIP_OK(hipMemcpy(flags, R.row_flag.p, R.n_rows, hipMemcpyDeviceToHost));
-    });
-}
-
-int sb_requests_set_compact(sb_batch *b, int on) {
-    return guard([&] {
-        if (!b || !b->req) throw Error(SB_EINVAL, "not a request batch");
-        if (on && b->req->slices)
-            throw Error(SB_EINVAL, "sb_requests_set_compact: the batch answers some rows per slice (wide rows only)");
-        std::lock_guard<std::mutex> lk(b->mu);
-        if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_set_compact between a run and its sync");
-        b->req->compact = on != 0;
-    });
-}
-
-int sb_requests_set_replan(sb_batch *b, int on) {
-    return guard([&] {
-        if (!b || !b->req) throw Error(SB_EINVAL, "not a request batch");
-        if (on && !b->req->din.p)
-            throw Error(SB_EINVAL, "sb_requests_set_replan: the batch was planned on the host (no packed requests on "
-                                   "the device)");
-        std::lock_guard<std::mutex> lk(b->mu);
-        if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_set_replan between a run and its sync");
-        b->req->replan = on != 0;
-    });
-}
-
-int sb_requests_time_eval(sb_batch *b, int on) {
-    return guard([&] {
-        if (!b || !b->req) throw Error(SB_EINVAL, "not a request batch");
-        sync(*b);
-        b->req->time_eval = on != 0;
-        b->req->last_eval_ms = 0;
-    });
 }
 
 int sb_batch_prepare(sb_store *s, const sb_query *q, size_t nq, sb_batch **out) {
@@ -4542,418 +1901,5 @@ int sb_query_batch(sb_store *s, const sb_query *q, size_t nq, uint32_t flags, sb
         tick("fetch");
     });
 }
-
-int sb_result_get(const sb_result_set *r, size_t i, sb_result_view *out) {
-    if (!r || !out || i >= r->res.size()) return SB_EINVAL;
-    std::call_once(r->tmp_once, [r] {  // the record / ALT views of every hit
-        const size_t total = r->hit.size();
-        r->tmp_rec.resize(total);
-        r->tmp_alt.resize(total);
-        parallel_for(total, [r](size_t h) {
-            r->tmp_rec[h] = static_cast<uint32_t>(r->hit[h]);
-            r->tmp_alt[h] = static_cast<uint32_t>(r->hit[h] >> kHitAltShift);
-        }, 16, 1 << 16);
-    });
-    return sb::result_view(r, i, out);
-}
-}  // extern "C"
-
-namespace sb {
-// sb_result_get without the hit views (the wire formatter)
-int result_view(const sb_result_set *r, size_t i, sb_result_view *out) {
-    if (!r || !out || i >= r->res.size()) return SB_EINVAL;
-    const QRes &q = r->res[i];
-    out->error = q.error;
-    out->exists = q.exists;
-    out->call_count = q.call_count;
-    out->all_alleles_count = q.all_alleles_count;
-    const uint64_t a = r->dense_off[i], b = r->dense_off[i + 1];
-    out->n_variants = q.error ? 0 : b - a;
-    const bool views = r->tmp_rec.size() == r->hit.size();  // sb_result_get split them
-    out->hit_record = views ? r->tmp_rec.data() + a : nullptr;
-    out->hit_alt = views ? r->tmp_alt.data() + a : nullptr;
-    out->n_sample_indices = r->sidx[i].size();
-    out->sample_indices = r->sidx[i].data();
-    out->big_limbs = 0;
-    out->_pad = 0;
-    out->big_call_count = out->big_all_alleles_count = nullptr;
-    if (!r->big.empty()) {
-        auto it = r->big.find(static_cast<uint32_t>(i));
-        if (it != r->big.end() && !q.error) {
-            out->big_limbs = r->big_limbs;
-            out->big_call_count = it->second.data();
-            out->big_all_alleles_count = it->second.data() + r->big_limbs;
-        }
-    }
-    return SB_OK;
-}
-}  // namespace sb
-
-extern "C" {
-int sb_result_get_all(const sb_result_set *r, sb_result_view *out, size_t n) {
-    if (!r || (!out && n) || n > r->res.size()) return SB_EINVAL;
-    for (size_t i = 0; i < n; ++i) sb_result_get(r, i, out + i);
-    return SB_OK;
-}
-
-namespace {
-// f'{chrom}\t{position}\t{reference}\t{alts[i]}\t{variant_type}' (search_variants.py:210)
-void append_variant(std::string &o, const sb_store &s, const std::string &chrom, uint64_t hit) {
-    const uint32_t rec = static_cast<uint32_t>(hit);
-    const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
-    char num[16];
-    o += chrom;
-    o.push_back('\t');
-    {  // decimal POS (no snprintf: millions of variant strings per batch)
-        uint32_t v = s.h_pos[rec];
-        char *e = num + sizeof num, *q = e;
-        do {
-            *--q = static_cast<char>('0' + v % 10);
-            v /= 10;
-        } while (v);
-        o.append(q, static_cast<size_t>(e - q));
-    }
-    o.push_back('\t');
-    o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_ref_off[rec]), s.h_end[rec] - s.h_pos[rec] + 1);
-    o.push_back('\t');
-    if (k == 0) {
-        o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_a0_off[rec]), s.h_a0_len[rec]);
-    } else {
-        const uint32_t x = s.h_x_lo[rec] + k - 1;
-        o.append(reinterpret_cast<const char *>(s.h_blob.data() + s.h_x_off[x]), s.h_x_len[x]);
-    }
-    o.push_back('\t');
-    o += s.vt.items[s.h_vt[rec]];
-}
-}  // namespace
-
-}  // extern "C"
-
-namespace sb {
-// The wire formatter's per-store cache: for every ALT row (record rec's ALT
-// 0 = row rec, its extra ALT x = row n_records + x) the JSON-escaped tail of
-// its variant string, "\\t" POS "\\t" REF "\\t" ALT "\\t" VT
-// (search_variants.py:210), built once on first use (parallel): a response's
-// variant list is then its chrom and one copy per hit.  A row whose text is
-// not UTF-8 has no entry (bad): its events take the Python handler.
-struct VarText {
-    std::vector<uint64_t> off;  // rows + 1
-    std::vector<char> text;
-    std::vector<uint8_t> bad;
-};
-
-const VarText &var_text(sb_store &s) {
-    std::call_once(s.var_text_once, [&] {
-        auto V = std::make_shared<VarText>();
-        const size_t nr = s.n_records, rows = nr + s.n_extra;
-        std::vector<std::string> vt(s.vt.items.size());
-        std::vector<uint8_t> vt_bad(vt.size(), 0);
-        for (size_t k = 0; k < vt.size(); ++k)
-            if (!json_escape_append(vt[k], s.vt.items[k].data(), s.vt.items[k].size())) vt_bad[k] = 1;
-        std::vector<uint32_t> xrec(s.n_extra);  // extra ALT row -> its record
-        for (size_t r = 0; r < nr; ++r) {
-            const uint32_t nx = (r + 1 < nr ? s.h_x_lo[r + 1] : static_cast<uint32_t>(s.n_extra)) - s.h_x_lo[r];
-            for (uint32_t j = 0; j < nx; ++j) xrec[s.h_x_lo[r] + j] = static_cast<uint32_t>(r);
-        }
-        const char *blob = reinterpret_cast<const char *>(s.h_blob.data());
-        auto parts = [&](size_t row, const char *&alt, size_t &al, uint32_t &rec) {
-            if (row < nr) {
-                rec = static_cast<uint32_t>(row);
-                alt = blob + s.h_a0_off[rec];
-                al = s.h_a0_len[rec];
-            } else {
-                const size_t x = row - nr;
-                rec = xrec[x];
-                alt = blob + s.h_x_off[x];
-                al = s.h_x_len[x];
-            }
-        };
-        // pass 1: each row's escaped length (0 + bad mark where not UTF-8)
-        std::vector<uint32_t> len(rows, 0);
-        V->bad.assign(rows, 0);
-        parallel_for(rows, [&](size_t row) {
-            const char *alt;
-            size_t al;
-            uint32_t rec;
-            parts(row, alt, al, rec);
-            const size_t rl = s.h_end[rec] - s.h_pos[rec] + 1;
-            thread_local std::string tmp;
-            tmp.clear();
-            bool ok = json_escape_append(tmp, blob + s.h_ref_off[rec], rl) && json_escape_append(tmp, alt, al) &&
-                      !vt_bad[s.h_vt[rec]];
-            uint32_t digits = 1;
-            for (uint32_t v = s.h_pos[rec]; v >= 10; v /= 10) ++digits;
-            if (!ok) V->bad[row] = 1;
-            else len[row] = static_cast<uint32_t>(8 + digits + tmp.size() + vt[s.h_vt[rec]].size());
-        });
-        V->off.assign(rows + 1, 0);
-        for (size_t r = 0; r < rows; ++r) V->off[r + 1] = V->off[r] + len[r];
-        V->text.resize(V->off[rows]);
-        // pass 2: the text
-        parallel_for(rows, [&](size_t row) {
-            if (V->bad[row]) return;
-            const char *alt;
-            size_t al;
-            uint32_t rec;
-            parts(row, alt, al, rec);
-            char *p = V->text.data() + V->off[row];
-            *p++ = '\\';
-            *p++ = 't';
-            char num[16];
-            uint32_t v = s.h_pos[rec];
-            char *e = num + sizeof num, *q = e;
-            do {
-                *--q = static_cast<char>('0' + v % 10);
-                v /= 10;
-            } while (v);
-            std::memcpy(p, q, static_cast<size_t>(e - q));
-            p += e - q;
-            *p++ = '\\';
-            *p++ = 't';
-            p = json_escape_to(p, blob + s.h_ref_off[rec], s.h_end[rec] - s.h_pos[rec] + 1);
-            *p++ = '\\';
-            *p++ = 't';
-            p = json_escape_to(p, alt, al);
-            *p++ = '\\';
-            *p++ = 't';
-            const std::string &t = vt[s.h_vt[rec]];
-            std::memcpy(p, t.data(), t.size());
-        });
-        s.var_text = V;
-    });
-    return *static_cast<const VarText *>(s.var_text.get());
-}
-
-void result_prepare_json(sb_result_set *r) {
-    if (!r->vt_json.empty()) return;
-    (void)var_text(*r->s);
-    const auto &items = r->s->vt.items;
-    r->vt_json.resize(items.size());
-    for (size_t k = 0; k < items.size(); ++k)
-        if (!json_escape_append(r->vt_json[k], items[k].data(), items[k].size())) r->vt_json[k] = std::string("\x01");
-    // sample names: the reference joins the selected names with ',' and the
-    // response lists the pieces of splitting that text on ',' -- per name,
-    // the pieces of the name split on ','
-    r->names_json.assign(r->s->vcfs.size(), {});
-    std::vector<uint8_t> need(r->s->vcfs.size(), 0);
-    for (size_t i = 0; i < r->res.size(); ++i)
-        if (!r->sidx[i].empty()) need[r->vcf_of[i]] = 1;
-    for (size_t f = 0; f < need.size(); ++f) {
-        if (!need[f]) continue;
-        const auto &names = r->s->vcfs[f].samples;
-        auto &out = r->names_json[f];
-        out.resize(names.size());
-        for (size_t h = 0; h < names.size(); ++h) {
-            const std::string &nm = names[h];
-            std::string &o = out[h];
-            size_t a = 0;
-            for (size_t k = 0; k <= nm.size(); ++k)
-                if (k == nm.size() || nm[k] == ',') {
-                    if (a) o += ", ";
-                    o.push_back('"');
-                    if (!json_escape_append(o, nm.data() + a, k - a)) {
-                        o = std::string("\x01");
-                        break;
-                    }
-                    o.push_back('"');
-                    a = k + 1;
-                }
-        }
-    }
-}
-
-namespace {
-// query i's chrom, JSON-escaped (in buf when it fits); false: not UTF-8
-struct ChromText {
-    char buf[256];
-    std::string lng;
-    const char *p = nullptr;
-    size_t n = 0;
-    bool make(const std::string &cs) {
-        if (6 * cs.size() <= sizeof buf) {
-            char *e = json_escape_to(buf, cs.data(), cs.size());
-            if (!e) return false;
-            p = buf;
-            n = static_cast<size_t>(e - buf);
-        } else {
-            if (!json_escape_append(lng, cs.data(), cs.size())) return false;
-            p = lng.data();
-            n = lng.size();
-        }
-        return true;
-    }
-};
-uint64_t variant_row(const sb_store &s, uint64_t hit) {
-    const uint32_t rec = static_cast<uint32_t>(hit);
-    const uint32_t k = static_cast<uint32_t>(hit >> kHitAltShift);
-    return k == 0 ? rec : s.n_records + s.h_x_lo[rec] + k - 1;
-}
-}  // namespace
-
-bool result_variants_len(const sb_result_set *r, size_t i, size_t *need) {
-    const sb_store &s = *r->s;
-    const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
-    *need = 0;
-    if (b == a) return true;
-    const VarText &V = *static_cast<const VarText *>(s.var_text.get());  // result_prepare_json built it
-    ChromText c;
-    if (!c.make(r->chrom[i])) return false;
-    size_t n = 0;
-    for (uint64_t h = a; h < b; ++h) {
-        const uint64_t row = variant_row(s, r->hit[h]);
-        if (V.bad[row]) return false;  // not UTF-8: the Python handler
-        n += 4 + c.n + (V.off[row + 1] - V.off[row]);
-    }
-    *need = n - 2;  // no ", " before the first
-    return true;
-}
-
-void result_variants_write(const sb_result_set *r, size_t i, char *p) {
-    const sb_store &s = *r->s;
-    const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
-    if (b == a) return;
-    const VarText &V = *static_cast<const VarText *>(s.var_text.get());
-    ChromText c;
-    c.make(r->chrom[i]);  // (result_variants_len accepted it)
-    for (uint64_t h = a; h < b; ++h) {
-        const uint64_t row = variant_row(s, r->hit[h]);
-        if (h > a) {
-            *p++ = ',';
-            *p++ = ' ';
-        }
-        *p++ = '"';
-        std::memcpy(p, c.p, c.n);
-        p += c.n;
-        const size_t n = V.off[row + 1] - V.off[row];
-        std::memcpy(p, V.text.data() + V.off[row], n);
-        p += n;
-        *p++ = '"';
-    }
-}
-
-bool result_variants_json(const sb_result_set *r, size_t i, std::string &o) {
-    size_t need;
-    if (!result_variants_len(r, i, &need)) return false;
-    const size_t o0 = o.size();
-    o.resize(o0 + need);
-    result_variants_write(r, i, &o[o0]);
-    return true;
-}
-
-bool result_sample_names_len(const sb_result_set *r, size_t i, size_t *need) {
-    const auto &ix = r->sidx[i];
-    const auto &nj = r->names_json[r->vcf_of[i]];
-    size_t n = ix.empty() ? 0 : 2 * (ix.size() - 1);
-    for (size_t j = 0; j < ix.size(); ++j) {
-        const std::string &x = nj[r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j]];
-        if (x.size() == 1 && x[0] == '\x01') return false;  // not UTF-8
-        n += x.size();
-    }
-    *need = n;
-    return true;
-}
-
-void result_sample_names_write(const sb_result_set *r, size_t i, char *p) {
-    const auto &ix = r->sidx[i];
-    const auto &nj = r->names_json[r->vcf_of[i]];
-    for (size_t j = 0; j < ix.size(); ++j) {
-        const std::string &x = nj[r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j]];
-        if (j) {
-            *p++ = ',';
-            *p++ = ' ';
-        }
-        std::memcpy(p, x.data(), x.size());
-        p += x.size();
-    }
-}
-
-bool result_sample_names_json(const sb_result_set *r, size_t i, std::string &o) {
-    size_t need;
-    if (!result_sample_names_len(r, i, &need)) return false;
-    const size_t o0 = o.size();
-    o.resize(o0 + need);
-    result_sample_names_write(r, i, &o[o0]);
-    return true;
-}
-}  // namespace sb
-
-extern "C" {
-
-int sb_result_variants_text(sb_result_set *r, size_t i, const char **p, size_t *len) {
-    if (!r || !p || !len || i >= r->res.size()) return SB_EINVAL;
-    if (!r->vbuilt[i]) {
-        std::string &o = r->vtext[i];
-        const uint64_t a = r->dense_off[i], b = r->res[i].error ? a : r->dense_off[i + 1];
-        for (uint64_t h = a; h < b; ++h) {
-            if (h > a) o.push_back('\n');
-            append_variant(o, *r->s, r->chrom[i], r->hit[h]);
-        }
-        r->vbuilt[i] = 1;
-    }
-    *p = r->vtext[i].data();
-    *len = r->vtext[i].size();
-    return SB_OK;
-}
-
-int sb_result_distinct_variants(sb_result_set *r, const uint32_t *queries, size_t n, const char **p, size_t *len,
-                                uint64_t *count) {
-    return guard([&] {
-        if (!r || !p || !len || !count || (n && !queries)) throw Error(SB_EINVAL, "NULL argument");
-        // (chrom string, record, alt) first, then the formatted strings: two
-        // records (or two VCFs naming the contig alike) can print the same line
-        std::unordered_map<std::string, uint32_t> chrom_id;
-        std::unordered_set<uint64_t> seen_hit;
-        std::unordered_set<std::string> seen_text;
-        std::string &o = r->distinct;
-        o.clear();
-        uint64_t c = 0;
-        std::string line;
-        for (size_t j = 0; j < n; ++j) {
-            const uint32_t i = queries[j];
-            if (i >= r->res.size()) throw Error(SB_EINVAL, "query index out of range");
-            if (r->res[i].error) continue;
-            const uint32_t cid = chrom_id.emplace(r->chrom[i], static_cast<uint32_t>(chrom_id.size())).first->second;
-            for (uint64_t h = r->dense_off[i]; h < r->dense_off[i + 1]; ++h) {
-                // hit = rec | alt << kHitAltShift; rec < 2^32, alt < 64: fold the chrom id above both
-                const uint64_t key = r->hit[h] ^ (static_cast<uint64_t>(cid) << 40);
-                if (!seen_hit.insert(key).second) continue;
-                line.clear();
-                append_variant(line, *r->s, r->chrom[i], r->hit[h]);
-                if (!seen_text.insert(line).second) continue;
-                if (c++) o.push_back('\n');
-                o += line;
-            }
-        }
-        *p = o.data();
-        *len = o.size();
-        *count = c;
-    });
-}
-
-int sb_result_sample_names_text(sb_result_set *r, size_t i, const char **p, size_t *len) {
-    if (!r || !p || !len || i >= r->res.size()) return SB_EINVAL;
-    if (!r->nbuilt[i]) {
-        std::string &o = r->ntext[i];
-        const VcfData &v = r->s->vcfs[r->vcf_of[i]];
-        const auto &ix = r->sidx[i];
-        for (size_t j = 0; j < ix.size(); ++j) {
-            const uint32_t h = r->samples_variant[i] ? r->emitted[i][ix[j]] : ix[j];
-            if (j) o.push_back(',');
-            o += v.samples[h];
-        }
-        r->nbuilt[i] = 1;
-    }
-    *p = r->ntext[i].data();
-    *len = r->ntext[i].size();
-    return SB_OK;
-}
-
-int sb_result_stats(const sb_result_set *r, sb_batch_stats *out) {
-    if (!r || !out) return SB_EINVAL;
-    *out = r->stats;
-    return SB_OK;
-}
-
-void sb_result_free(sb_result_set *r) { delete r; }
 
 }  // extern "C"

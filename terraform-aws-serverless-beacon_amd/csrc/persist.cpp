@@ -41,12 +41,6 @@
 #include "jsonesc.hpp"
 #include "store.hpp"
 
-#define HIP_OK(x)                                                                                  \
-    do {                                                                                           \
-        hipError_t e_ = (x);                                                                       \
-        if (e_ != hipSuccess) throw sb::Error(SB_EHIP, std::string(#x ": ") + hipGetErrorString(e_)); \
-    } while (0)
-
 namespace sb {
 
 constexpr uint64_t kMagic = 0x3150544f5453424full;  // "OBSTOTP1"

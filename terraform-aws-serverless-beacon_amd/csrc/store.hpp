@@ -16,6 +16,15 @@
 #include <vector>
 
 #include "common.hpp"
+
+// a HIP runtime call that must succeed (sb::Error SB_EHIP otherwise)
+#define HIP_OK(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            throw ::sb::Error(SB_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));            \
+    } while (0)
+
 #include "devtypes.hpp"
 
 namespace sb {

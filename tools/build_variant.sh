@@ -17,7 +17,7 @@ else
 fi
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$W/include $*"
 objs=""
-for s in api.cpp ingest.cpp index.cpp wire.cpp persist.cpp query_kernels.hip dedup_kernels.hip; do
+for s in api.cpp requests.cpp summarise.cpp results.cpp ingest.cpp index.cpp wire.cpp persist.cpp query_kernels.hip dedup_kernels.hip; do
   x=""; case $s in *.cpp) x="-x hip";; esac
   /opt/rocm/bin/hipcc $x $FL -c $W/pkg/csrc/$s -o $W/$s.o &
   objs="$objs $W/$s.o"
