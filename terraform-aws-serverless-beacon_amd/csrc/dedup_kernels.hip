@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 
 #include "config.hpp"
@@ -669,7 +670,10 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
 // duplicate -- for hashed identities after the strings are confirmed); a
 // different identity (a collision) leaves it for the next round.  Equal
 // identities always meet in one slot, so a value is counted once.
-constexpr uint32_t kWSlots = 4096;   // 8 KB of 16-bit winners, load <= 1/2
+#ifndef SBEACON_WIN_SLOTS
+#define SBEACON_WIN_SLOTS 4096
+#endif
+constexpr uint32_t kWSlots = SBEACON_WIN_SLOTS;  // 8 KB of 16-bit winners, load <= 1/2
 constexpr uint32_t kWRounds = 24;    // unresolved after that: the sorted path
 constexpr uint32_t kWConfirm = 128;  // hashed duplicate pairs confirmed per window
 constexpr uint32_t kWPer = kWinCap / kThreads;
@@ -851,7 +855,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     __shared__ __attribute__((aligned(16))) uint16_t s_win[kWSlots];            // a round's winner per slot
     __shared__ uint32_t s_pre[kWinPieces + 1], s_base[kWinPieces], s_run[kWinPieces];
     __shared__ uint32_t s_conf[kWConfirm];  // hashed duplicate pairs (winner | key << 16) to confirm
-    __shared__ uint32_t s_fresh, s_def, s_def0, s_nconf;
+    __shared__ uint32_t s_fresh, s_def, s_def0, s_nconf, s_pend;
     const KWin W = wins[blockIdx.x];
     const uint32_t lane = threadIdx.x & 63u;
     if (threadIdx.x < 64) {  // wave 0: the pieces' inclusive prefix (DPP scan)
@@ -871,6 +875,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
             s_fresh = 0;
             s_def = 0;
             s_nconf = 0;
+            s_pend = 0;
         }
     }
     __syncthreads();
@@ -920,6 +925,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
     // (displaced keys that may have a copy at a larger POS of the job).  A
     // displaced key with no such copy meets its equal strings at its own POS
     uint32_t em = 0, hm = 0, dm = 0;
+    uint64_t idv[kWPer];  // the keys' identities, also kept in registers (the rounds read only the winners')
     const uint32_t pm10 = W.pmax / 10;
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u) {
@@ -932,11 +938,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         em |= (ex ? 1u : 0u) << u;
         hm |= ((ok && !ex && (!disp || big)) ? 1u : 0u) << u;
         dm |= ((ok && disp && !big) ? 1u : 0u) << u;
-        if (ex) s_id[u * kThreads + threadIdx.x] = (1ull << 63) | (static_cast<uint64_t>(pos - W.p0) << 29) | id;
+        idv[u] = (1ull << 63) | (static_cast<uint64_t>(pos - W.p0) << 29) | id;
     }
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u)
-        if ((hm >> u) & 1u) s_id[u * kThreads + threadIdx.x] = ks.hash[kid_of(u)] & ~(1ull << 63);
+        if ((hm >> u) & 1u) idv[u] = ks.hash[kid_of(u)] & ~(1ull << 63);
+#pragma unroll
+    for (uint32_t u = 0; u < kWPer; ++u)
+        if (((em | hm) >> u) & 1u) s_id[u * kThreads + threadIdx.x] = idv[u];
     // deferred keys: one reservation per workgroup in the global list
     const uint32_t nd = static_cast<uint32_t>(__popc(dm));
     uint32_t dofs = 0;
@@ -956,7 +965,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u)
             if ((pend >> u) & 1u) {
-                const uint64_t v = s_id[u * kThreads + threadIdx.x];
+                const uint64_t v = idv[u];
                 const uint32_t m = (static_cast<uint32_t>(v) ^ static_cast<uint32_t>(v >> 32) * 0x85EBCA6Bu ^
                                     round * 0xC2B2AE35u) * 0x9E3779B1u;
                 sl[u] = static_cast<uint32_t>((static_cast<uint64_t>(m ^ (m >> 15)) * kWSlots) >> 32);
@@ -969,8 +978,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
             if ((pend >> u) & 1u) {
                 const uint32_t f = u * kThreads + threadIdx.x;
                 const uint32_t w = s_win[sl[u]];
-                const uint64_t v = s_id[f];
-                if (s_id[w] == v) {  // resolved: the winner counts, an equal identity is its duplicate
+                const uint64_t v = idv[u];
+                // resolved: the winner counts, an equal identity is its
+                // duplicate (a key that won its own slot reads nothing)
+                if (w == f || s_id[w] == v) {
                     pend &= ~(1u << u);
                     if (w == f) {
                         ++fresh;
@@ -980,7 +991,11 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
                     }
                 }
             }
-        if (!__syncthreads_or(pend != 0u)) break;  // also orders this round's reads before the next writes
+        // any key left?  (round + 1 in one LDS word: no earlier round's
+        // value reads as this one's)
+        if (pend) s_pend = round + 1;
+        __syncthreads();  // also orders this round's reads before the next writes
+        if (s_pend != round + 1) break;
         if (round + 1 == kWRounds && threadIdx.x == 0) atomicOr(overflow, 1u);  // unresolved: the sorted path
     }
     // hashed duplicates: the strings of every pair (winner, key) must be equal
