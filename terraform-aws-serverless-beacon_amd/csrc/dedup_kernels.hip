@@ -670,15 +670,22 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
 // duplicate -- for hashed identities after the strings are confirmed); a
 // different identity (a collision) leaves it for the next round.  Equal
 // identities always meet in one slot, so a value is counted once.
+// LDS per workgroup (identities 16 KB + winners 5.5 KB + pieces) <= 22.7 KB:
+// 7 workgroups per CU (4,096 slots and 128 confirmations: 6, and 4 % slower,
+// profiles/r05_dedup/slots.log); the set's load is <= 0.73 (1,024 distinct
+// identities in a config-4 window: ~0.36)
 #ifndef SBEACON_WIN_SLOTS
-#define SBEACON_WIN_SLOTS 4096
+#define SBEACON_WIN_SLOTS 2816
 #endif
-constexpr uint32_t kWSlots = SBEACON_WIN_SLOTS;  // 8 KB of 16-bit winners, load <= 1/2
+constexpr uint32_t kWSlots = SBEACON_WIN_SLOTS;  // 16-bit winners
 constexpr uint32_t kWRounds = 24;    // unresolved after that: the sorted path
-constexpr uint32_t kWConfirm = 128;  // hashed duplicate pairs confirmed per window
+#ifndef SBEACON_WIN_CONFIRM
+#define SBEACON_WIN_CONFIRM 32
+#endif
+constexpr uint32_t kWConfirm = SBEACON_WIN_CONFIRM;  // hashed duplicate pairs confirmed per window
 constexpr uint32_t kWPer = kWinCap / kThreads;
 static_assert(kWPer * kThreads == kWinCap, "window keys per thread");
-static_assert(kWinCap <= kWSlots / 2 && kWinCap <= 65536, "window slot load / 16-bit winners");
+static_assert(kWinCap <= kWSlots && kWinCap <= 65536, "window slot load / 16-bit winners");
 static_assert(kWinPieces == 64, "one wave scans the pieces");
 
 // wave-wide sums (DPP row shifts, then the row broadcasts)
@@ -847,29 +854,30 @@ __global__ __launch_bounds__(kThreads) void dedup_plan_kernel(KStore ks, const K
     wins[w] = KWin{i, J.nruns, runs[J.run_lo].job, P, J.run_lo, J.pmax, J.eoff, J.nw};
 }
 
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))) void window_dedupe_kernel(KStore ks, const KWin *wins, const uint32_t *E,
+#ifndef SBEACON_WIN_WAVES
+#define SBEACON_WIN_WAVES 7
+#endif
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACON_WIN_WAVES, 8))) void window_dedupe_kernel(KStore ks, const KWin *wins, const uint32_t *E,
                                                                  unsigned long long *counts, uint2 *list,
                                                                  uint32_t *n_list, uint32_t cap, uint32_t *overflow,
                                                                  uint32_t *wfresh, uint32_t dbg) {
     __shared__ __attribute__((aligned(16))) unsigned long long s_id[kWinCap];  // identity of window key f
     __shared__ __attribute__((aligned(16))) uint16_t s_win[kWSlots];            // a round's winner per slot
-    __shared__ uint32_t s_pre[kWinPieces + 1], s_base[kWinPieces], s_run[kWinPieces];
+    __shared__ uint32_t s_pre[kWinPieces + 1], s_base[kWinPieces];  // piece p = run W.run_lo + p
     __shared__ uint32_t s_conf[kWConfirm];  // hashed duplicate pairs (winner | key << 16) to confirm
     __shared__ uint32_t s_fresh, s_def, s_def0, s_nconf, s_pend;
     const KWin W = wins[blockIdx.x];
     const uint32_t lane = threadIdx.x & 63u;
     if (threadIdx.x < 64) {  // wave 0: the pieces' inclusive prefix (DPP scan)
-        uint32_t len = 0, klo = 0, run = 0;
+        uint32_t len = 0, klo = 0;
         if (lane < W.nruns) {  // run `lane`'s piece of the window
             const uint32_t *e = E + W.eoff + static_cast<uint64_t>(lane) * (W.nw + 1) + W.i;
             klo = e[0];
             len = e[1] - e[0];
-            run = W.run_lo + lane;
         }
         const uint32_t inc = wave_incl_sum(len);
         s_pre[lane + 1] = inc;
         s_base[lane] = klo - (inc - len);  // key id = window-local index + base
-        s_run[lane] = run;
         if (lane == 0) {
             s_pre[0] = 0;
             s_fresh = 0;
@@ -1022,7 +1030,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(6, 8))
         for (uint32_t u = 0; u < kWPer; ++u)
             if ((dm >> u) & 1u) {
                 const uint32_t pc = static_cast<uint32_t>(pk >> (6 * u)) & 63u;
-                if (at < cap) list[at] = uint2{u * kThreads + threadIdx.x + s_base[pc], s_run[pc]};
+                if (at < cap) list[at] = uint2{u * kThreads + threadIdx.x + s_base[pc], W.run_lo + pc};
                 ++at;
             }
     }

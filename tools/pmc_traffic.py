@@ -38,13 +38,14 @@ def load(d, counter):
                     continue
                 per.setdefault(name, []).append((int(row['Dispatch_Id']), float(row['Counter_Value']),
                                                  int(row.get('Grid_Size') or 0)))
-    # a bench run launches a kernel at several sizes (the timed batch, the
-    # delivered path's chunks, probes): only the launches of the largest grid
-    # -- the timed full batch -- are priced
+    # a bench run launches a kernel at several sizes (the timed batches, the
+    # delivered path's chunks, probes): only the full-batch launches -- grids
+    # within 20 % of the largest (the rotating batches differ a little) -- are
+    # priced
     out = {}
     for k, x in per.items():
         g = max(v[2] for v in x)
-        out[k] = [v for _, v, gs in sorted(x) if gs == g]
+        out[k] = [v for _, v, gs in sorted(x) if gs >= 0.8 * g]
     return out
 
 
@@ -61,6 +62,7 @@ def main():
     ap.add_argument('--records', type=int, default=1103547)
     ap.add_argument('--requests', type=int, default=10000)
     ap.add_argument('--kernel', default=None, help='the dominant kernel the bench line prices (top-level entry)')
+    ap.add_argument('--batches', type=int, default=None, help='rotating batches of the measured run (config 3)')
     a = ap.parse_args()
     fetch = load(a.fetch_dir, 'FETCH_SIZE')
     write = load(a.write_dir, 'WRITE_SIZE')
@@ -81,6 +83,7 @@ def main():
     out = {
         'records': a.records,
         'requests': a.requests,
+        'batches': a.batches,
         'phase': 'query step = one launch of each kernel below (fused_kernel: range_n8 + exact groups)',
         'kernels': kernels,
         'scan_kernel_hbm_bytes_per_launch': step_bytes,
