@@ -829,10 +829,13 @@ __device__ uint32_t key_lower_bound(const KStore &ks, const KRun &R, uint32_t x)
 // window.  Window i of job J starts at POS P_i = the POS of the leader
 // run's key i * lead_n / nw (P_0 = the job's smallest POS); every run of the
 // job starts it at its lower bound of P_i, so windows are POS ranges and the
-// keys of one POS meet in one window.
+// keys of one POS meet in one window.  Thread w writes window w's record
+// (devtypes.hpp kWinRecHead): the header, each run's piece start, and the
+// same start as the end of window w - 1's piece (the job's last window ends
+// at the run's end).
 __global__ __launch_bounds__(kThreads) void dedup_plan_kernel(KStore ks, const KJob *__restrict__ jobs, uint32_t nj,
                                                               const KRun *__restrict__ runs, uint32_t nw_total,
-                                                              KWin *__restrict__ wins, uint32_t *__restrict__ E) {
+                                                              uint32_t *__restrict__ rec, uint32_t rec_words) {
     const uint32_t w = blockIdx.x * kThreads + threadIdx.x;
     if (w >= nw_total) return;
     uint32_t lo = 0, hi = nj;  // the last job with w0 <= w
@@ -845,19 +848,22 @@ __global__ __launch_bounds__(kThreads) void dedup_plan_kernel(KStore ks, const K
     const uint32_t i = w - J.w0;
     const uint32_t P = i == 0 ? J.pmin
                               : static_cast<uint32_t>(ks.word[J.lead_lo + static_cast<uint64_t>(i) * J.lead_n / J.nw]);
+    uint32_t *const me = rec + static_cast<uint64_t>(w) * rec_words;
     for (uint32_t r = 0; r < J.nruns; ++r) {
         const KRun R = runs[J.run_lo + r];
-        uint32_t *e = E + J.eoff + static_cast<uint64_t>(r) * (J.nw + 1);
-        e[i] = i == 0 ? R.key_lo : key_lower_bound(ks, R, P);
-        if (i + 1 == J.nw) e[J.nw] = R.key_hi;
+        const uint32_t at = i == 0 ? R.key_lo : key_lower_bound(ks, R, P);
+        me[kWinRecHead + 2 * r] = at;
+        if (i > 0) (me - rec_words)[kWinRecHead + 2 * r + 1] = at;  // window w - 1 of the job ends here
+        if (i + 1 == J.nw) me[kWinRecHead + 2 * r + 1] = R.key_hi;
     }
-    wins[w] = KWin{i, J.nruns, runs[J.run_lo].job, P, J.run_lo, J.pmax, J.eoff, J.nw};
+    *reinterpret_cast<uint4 *>(me) = uint4{i, J.nruns, runs[J.run_lo].job, P};
+    *reinterpret_cast<uint4 *>(me + 4) = uint4{J.run_lo, J.pmax, 0u, J.nw};
 }
 
 #ifndef SBEACON_WIN_WAVES
 #define SBEACON_WIN_WAVES 7
 #endif
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACON_WIN_WAVES, 8))) void window_dedupe_kernel(KStore ks, const KWin *wins, const uint32_t *E,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACON_WIN_WAVES, 8))) void window_dedupe_kernel(KStore ks, const uint32_t *__restrict__ rec, uint32_t rec_words,
                                                                  unsigned long long *counts, uint2 *list,
                                                                  uint32_t *n_list, uint32_t cap, uint32_t *overflow,
                                                                  uint32_t *wfresh, uint32_t dbg) {
@@ -866,15 +872,15 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
     __shared__ uint32_t s_pre[kWinPieces + 1], s_base[kWinPieces];  // piece p = run W.run_lo + p
     __shared__ uint32_t s_conf[kWConfirm];  // hashed duplicate pairs (winner | key << 16) to confirm
     __shared__ uint32_t s_fresh, s_def, s_def0, s_nconf, s_pend;
-    const KWin W = wins[blockIdx.x];
+    // the window's record: its header and (wave 0, lane = run) the pieces,
+    // loaded side by side (lanes past the call's largest run count load nothing)
+    const uint32_t *const me = rec + static_cast<uint64_t>(blockIdx.x) * rec_words;
+    const KWin W = *reinterpret_cast<const KWin *>(me);
     const uint32_t lane = threadIdx.x & 63u;
     if (threadIdx.x < 64) {  // wave 0: the pieces' inclusive prefix (DPP scan)
-        uint32_t len = 0, klo = 0;
-        if (lane < W.nruns) {  // run `lane`'s piece of the window
-            const uint32_t *e = E + W.eoff + static_cast<uint64_t>(lane) * (W.nw + 1) + W.i;
-            klo = e[0];
-            len = e[1] - e[0];
-        }
+        uint2 pr{0u, 0u};
+        if (kWinRecHead + 2 * lane < rec_words) pr = *reinterpret_cast<const uint2 *>(me + kWinRecHead + 2 * lane);
+        const uint32_t klo = pr.x, len = lane < W.nruns ? pr.y - pr.x : 0u;
         const uint32_t inc = wave_incl_sum(len);
         s_pre[lane + 1] = inc;
         s_base[lane] = klo - (inc - len);  // key id = window-local index + base
@@ -1137,13 +1143,13 @@ int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1,
     return r;
 }
 
-void launch_window_dedupe(const KStore &ks, const KJob *jobs, uint32_t nj, KWin *wins, uint32_t nw, uint32_t *E,
+void launch_window_dedupe(const KStore &ks, const KJob *jobs, uint32_t nj, uint32_t *rec, uint32_t rec_words, uint32_t nw,
                           const KRun *runs, unsigned long long *counts, uint2 *list, uint32_t *n_list, uint32_t cap,
                           uint32_t *overflow, uint32_t *wfresh, hipStream_t s) {
     if (!nw) return;
     const uint32_t dbg = static_cast<uint32_t>(config().dedup_win_dbg);  // timing ablations (never set by the benches)
-    dedup_plan_kernel<<<(nw + kThreads - 1) / kThreads, kThreads, 0, s>>>(ks, jobs, nj, runs, nw, wins, E);
-    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, wins, E, counts, list, n_list, cap, overflow, wfresh, dbg);
+    dedup_plan_kernel<<<(nw + kThreads - 1) / kThreads, kThreads, 0, s>>>(ks, jobs, nj, runs, nw, rec, rec_words);
+    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, rec, rec_words, counts, list, n_list, cap, overflow, wfresh, dbg);
     window_fold_kernel<<<(nj * 64 + kThreads - 1) / kThreads, kThreads, 0, s>>>(jobs, nj, runs, wfresh, counts);
     deferred_dedupe_kernel<<<1024, kThreads, 0, s>>>(ks, runs, list, n_list, cap, counts);
 }

@@ -570,13 +570,19 @@ inline constexpr uint32_t kKeyDisplaced = 1u;
 // per key: y counts when no key of the job's runs holds its string at a
 // larger POS (its twin, found through the record POS index) and no earlier
 // key of the job's runs (earlier run, or earlier in its run) equals it.
-struct KWin {  // window w of a call (dedup_plan_kernel writes it)
+// Window w's record (dedup_plan_kernel writes it; rec_words u32 per window):
+// the KWin header, then run r's piece of the window's keys as [lo, hi) at
+// words kWinRecHead + 2 r, + 1 -- one load round for the window kernel
+// (header and pieces side by side, no dependent read of a run-start table)
+inline constexpr uint32_t kWinRecHead = 8;
+struct KWin {  // header of window w's record
     uint32_t i, nruns, job, p0;  // window i of its job; the job's runs; POS where it starts
     uint32_t run_lo;  // the job's first KRun
     uint32_t pmax;    // largest POS of the job's runs
-    uint32_t eoff;    // run r's window starts: E[eoff + r * (nw + 1) + i], ends at ... + i + 1
+    uint32_t pad;
     uint32_t nw;      // the job's windows
 };
+static_assert(sizeof(KWin) == 4 * kWinRecHead, "KWin is the record header");
 // One job of a window-dedup call (host-built): its windows [w0, w0 + nw) cut
 // its POS axis at the leader run's key ranks i * lead_n / nw, every run of the
 // job split at the same POS (dedup_plan_kernel: a lower bound per run and cut)
@@ -584,8 +590,7 @@ struct KJob {
     uint32_t w0, nw, run_lo, nruns;
     uint32_t lead_lo, lead_n;  // the leader run's (the job's longest) keys
     uint32_t pmin, pmax;       // POS span of the job's runs
-    uint32_t eoff;             // first E entry of the job's runs (nruns x (nw + 1))
-    uint32_t pad[3];
+    uint32_t pad[4];
 };
 struct KRun {  // one POS-sorted key run of a job + its segment's POS index
     uint32_t key_lo, key_hi, pos_lo, pos_hi;  // keys, POS of the first / last

@@ -164,15 +164,16 @@ int launch_bucket_dedupe(uint64_t *k0, uint32_t *v0, uint64_t *k1, uint32_t *v1,
                          uint32_t job_shift, uint32_t nj, unsigned long long *counts, uint32_t *overflow,
                          uint32_t *hist, uint32_t *bsum, hipStream_t s, const uint32_t *tile_n, uint32_t sparse_tiles);
 // window dedup: dedup_plan_kernel cuts every job (devtypes.hpp KJob; nj of
-// them, windows [w0, w0 + nw) each, nw in all) into windows (KWin, nw of
-// them) and run starts (E: every job's nruns x (nw + 1) entries at its eoff);
-// then one workgroup per window (runs at most kWinPieces, keys at most
+// them, windows [w0, w0 + nw) each, nw in all) into window records (rec:
+// nw records of rec_words u32 each = the KWin header, then each run's piece
+// [lo, hi) of the window's keys; rec_words = kWinRecHead + 2 x the call's
+// largest run count, rounded to 4); then one workgroup per window (runs at most kWinPieces, keys at most
 // kWinCap), then one lane per deferred displaced key (list: cap entries,
 // *n_list zeroed by the caller; runs = every job's KRun table); adds each
 // job's distinct keys to counts[job] (each window's count to wfresh[w], nw
 // entries, then one fold per job); *overflow = the window path cannot
 // answer this call exactly
-void launch_window_dedupe(const KStore &ks, const KJob *jobs, uint32_t nj, KWin *wins, uint32_t nw, uint32_t *E,
+void launch_window_dedupe(const KStore &ks, const KJob *jobs, uint32_t nj, uint32_t *rec, uint32_t rec_words, uint32_t nw,
                           const KRun *runs, unsigned long long *counts, uint2 *list, uint32_t *n_list, uint32_t cap,
                           uint32_t *overflow, uint32_t *wfresh, hipStream_t s);
 void launch_dedup_unique(const uint64_t *keys, const uint32_t *vals, uint64_t n, const KStore &ks, uint32_t job_shift,

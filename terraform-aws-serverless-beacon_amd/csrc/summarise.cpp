@@ -360,7 +360,8 @@ void dedup(sb_store &s, const sb_dedup_job *jobs, size_t nj, uint64_t *unique, i
 // segment's coarse POS index for the cuts and the twin lookups).
 struct WinPlan {
     std::vector<KJob> jobs;
-    uint64_t n_wins = 0, n_e = 0;
+    uint64_t n_wins = 0;
+    uint32_t rec_words = kWinRecHead;  // window record: header + 2 words per run of the call's largest job
     const char *why = "";  // why the plan was declined (SBEACON_DEDUP_DEBUG)
 };
 
@@ -394,10 +395,9 @@ bool plan_windows(const sb_store &s, std::vector<KRun> &runs, size_t nj, WinPlan
         J.w0 = static_cast<uint32_t>(P.n_wins);
         J.run_lo = static_cast<uint32_t>(g0);
         J.nruns = static_cast<uint32_t>(g1 - g0);
-        J.eoff = static_cast<uint32_t>(P.n_e);
         P.n_wins += J.nw;
-        P.n_e += uint64_t(J.nruns) * (J.nw + 1);
-        if (P.n_wins >= 0x7fffffffull || P.n_e >= 0xffffffffull) return P.why = "windows", false;
+        P.rec_words = std::max(P.rec_words, (kWinRecHead + 2 * J.nruns + 3) / 4 * 4);
+        if (P.n_wins >= 0x7fffffffull) return P.why = "windows", false;
         P.jobs.push_back(J);
         g0 = g1;
     }
@@ -421,7 +421,7 @@ struct PinnedHost {  // grow-only pinned host staging (hipHostMalloc)
 };
 
 struct WinWs {
-    DevMem jobs, wins, e, runs, counts, overflow, list, n_list, wfresh;
+    DevMem jobs, rec, runs, counts, overflow, list, n_list, wfresh;
     PinnedHost stage;  // jobs | runs for one H2D copy; counts + overflow back
 };
 
@@ -443,8 +443,7 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     WinWs &W = *static_cast<WinWs *>(s.win_ws.get());
     const uint32_t nw = static_cast<uint32_t>(P.n_wins);
     W.jobs.reserve(std::max<size_t>(P.jobs.size(), 1) * sizeof(KJob));
-    W.wins.reserve(std::max<size_t>(nw, 1) * sizeof(KWin));
-    W.e.reserve(std::max<size_t>(P.n_e, 1) * 4);
+    W.rec.reserve(std::max<size_t>(nw, 1) * P.rec_words * 4);
     W.runs.reserve(std::max<size_t>(runs.size(), 1) * sizeof(KRun));
     W.counts.reserve(std::max<size_t>(nj, 1) * 8);
     W.wfresh.reserve(std::max<size_t>(nw, 1) * 4);
@@ -471,8 +470,8 @@ bool dedup_window_run(sb_store &s, std::vector<KRun> &runs, uint64_t n, size_t n
     HIP_OK(hipEventCreate(&e0));
     HIP_OK(hipEventCreate(&e1));
     HIP_OK(hipEventRecord(e0, st));
-    launch_window_dedupe(s.dk, W.jobs.as<KJob>(), static_cast<uint32_t>(P.jobs.size()), W.wins.as<KWin>(), nw,
-                         W.e.as<uint32_t>(), W.runs.as<KRun>(), W.counts.as<unsigned long long>(), W.list.as<uint2>(),
+    launch_window_dedupe(s.dk, W.jobs.as<KJob>(), static_cast<uint32_t>(P.jobs.size()), W.rec.as<uint32_t>(), P.rec_words,
+                         nw, W.runs.as<KRun>(), W.counts.as<unsigned long long>(), W.list.as<uint2>(),
                          W.n_list.as<uint32_t>(), cap, W.overflow.as<uint32_t>(), W.wfresh.as<uint32_t>(), st);
     HIP_OK(hipEventRecord(e1, st));
     HIP_OK(hipGetLastError());

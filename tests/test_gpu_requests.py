@@ -115,7 +115,9 @@ def test_requests_match_slices(fixture):
 
 def test_genome_requests_match_oracle_and_slices():
     """Config-3 shape (small): shard request batches at world 1 and 2 vs the
-    per-slice shard batches (rows + hit lists) and the C oracle (rows)."""
+    per-slice shard batches (rows + hit lists) and the C oracle (rows; at
+    world 1 also every hit list, rendered as (chrom, POS, ALT) against the
+    oracle's variant strings in order)."""
     from oracle.oracle import OracleVcf
     from sbeacon.genome import (GenomeShape, config3_requests, prepare_shard_batch, prepare_shard_requests,
                                 shard_record_base, shard_requests, shard_slices, slice_payloads)
@@ -130,8 +132,23 @@ def test_genome_requests_match_oracle_and_slices():
                 f.write(c)
         orc = OracleVcf(full, load_gt=False)
         whole = shard_slices(shape, reqs, 1, 0)
-        exp = request_rows_from_responses(whole.req, orc.perform_query_batch(slice_payloads(whole), patched=True),
-                                          whole.n_rows)
+        res = orc.perform_query_batch(slice_payloads(whole), patched=True)
+        exp = request_rows_from_responses(whole.req, res, whole.n_rows)
+        exp_v = [[] for _ in range(len(reqs))]
+        for o, r in zip(whole.req, res):
+            if isinstance(r, dict):
+                exp_v[o].extend(tuple(v.split('\t')[i] for i in (0, 1, 3)) for v in r['variants'])
+        orc.close()
+    alts = {}
+
+    def variant(g, k):  # global record g, ALT k -> (chrom, POS, ALT) from the generator
+        ci = int(np.searchsorted(shape.offsets, g, side='right') - 1)
+        i = g - int(shape.offsets[ci])
+        if (ci, i) not in alts:
+            line = shape.gen(ci).records(i, i + 1, sites_only=True).decode().split('\t')
+            alts[(ci, i)] = (line[0], line[1], line[4].split(','))
+        c, pos, a = alts[(ci, i)]
+        return c, pos, a[k]
     for world in (1, 2):
         total = np.zeros((len(reqs), 5), dtype=np.int64)
         for rank in range(world):
@@ -158,6 +175,14 @@ def test_genome_requests_match_oracle_and_slices():
             for w in range(sr.n_rows):
                 assert sorted(hits[ro[w]:ro[w + 1]].tolist()) == sorted(h2[ro2[w]:ro2[w + 1]].tolist()), w
             total[sr.row_lo:sr.row_lo + sr.n_rows] += rows
+            if world == 1:
+                hv = hits.view(np.uint64)
+                checked = 0
+                for w in range(sr.n_rows):
+                    got = [variant(x & 0xffffffff, x >> 32) for x in hv[ro[w]:ro[w + 1]].tolist()]
+                    assert got == exp_v[sr.row_lo + w], w
+                    checked += len(got)
+                assert checked > 1000
         np.testing.assert_array_equal(total, exp)
 
 
