@@ -182,7 +182,7 @@ def test_genome_requests_match_oracle_and_slices():
                     got = [variant(x & 0xffffffff, x >> 32) for x in hv[ro[w]:ro[w + 1]].tolist()]
                     assert got == exp_v[sr.row_lo + w], w
                     checked += len(got)
-                assert checked > 1000
+                assert checked == int(exp[:, 1].sum()) > 0  # every variant the oracle emits
         np.testing.assert_array_equal(total, exp)
 
 
