@@ -35,6 +35,7 @@ struct Config {
     bool dedup_debug = false;     // SBEACON_DEDUP_DEBUG: dedup call details (stderr)
     int dedup_bucket_dbg = 0;     // SBEACON_DEDUP_BUCKET_DBG: bucket-kernel timing ablations
     int dedup_win_dbg = 0;        // SBEACON_DEDUP_WIN_DBG: window-kernel timing ablations
+    bool req_inject = false;      // SBEACON_REQ_INJECT=1 (tests): one wrong per-chain sum, so the pass's invariants fire
     int pack_dbg = 0;             // SBEACON_PACK_DBG: chain-kernel ablations (SBEACON_ABLATION builds)
 };
 
@@ -68,6 +69,7 @@ inline Config config() {
     c.dedup_debug = flag("SBEACON_DEDUP_DEBUG");
     c.dedup_bucket_dbg = num("SBEACON_DEDUP_BUCKET_DBG", 0);
     c.dedup_win_dbg = num("SBEACON_DEDUP_WIN_DBG", 0);
+    c.req_inject = one("SBEACON_REQ_INJECT");
     c.pack_dbg = num("SBEACON_PACK_DBG", 0);
     return c;
 }

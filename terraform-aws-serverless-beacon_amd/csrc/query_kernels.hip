@@ -2014,7 +2014,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
     unsigned long long *__restrict__ status, const QRes *__restrict__ sres, void *__restrict__ rows_out,
     void *__restrict__ row_cnt_out, uint64_t *__restrict__ row_src, uint32_t *__restrict__ stage, uint32_t n_lut,
-    unsigned int *__restrict__ err) {
+    unsigned int *__restrict__ err, uint32_t inject) {
     ReqPartial *const rows = static_cast<ReqPartial *>(rows_out);
     uint64_t *const row_cnt = static_cast<uint64_t *>(row_cnt_out);
     __shared__ ReqLds lds_all[kWavesPerBlock];
@@ -2325,6 +2325,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     if (anc) pass(std::true_type{});
     else pass(std::false_type{});
     wave_lds_sync();
+    if (inject && w == 0 && ul == 0) ++acc_ex;  // (tests, SBEACON_REQ_INJECT: the checks below must fire)
     // ---- per chain (lane k < R): staging start (scan of the hit counts), partial
     const uint32_t cs_incl = incl_sum_u32(acc_nv), cs = cs_incl - acc_nv;
     // invariants of the per-chain sums (the pulls are cross-lane: a lane
@@ -3846,7 +3847,8 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
     if (ev0) (void)hipEventRecord(ev0, s);
     auto eval = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
-                           static_cast<void *>(rows), static_cast<void *>(row_off), row_src, stage, n_lut, err);
+                           static_cast<void *>(rows), static_cast<void *>(row_off), row_src, stage, n_lut, err,
+                           static_cast<uint32_t>(config().req_inject));
     };
     (void)run;
     if (compact) {

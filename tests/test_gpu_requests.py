@@ -219,6 +219,36 @@ def test_request_batch_is_repeatable():
     assert ro[-1] > 320  # more than one LDS buffer of hits in some run
 
 
+def test_pass_invariants_fail_the_batch(monkeypatch):
+    """The request pass checks its per-chain sums against the run's staged
+    hits (query_kernels.hip request_eval_kernel): with one sum perturbed on
+    the device (SBEACON_REQ_INJECT, a test hook) the batch fails at sync with
+    SB_EINTERNAL instead of returning its rows; without it the same batch
+    answers normally."""
+    from payload_gen import read_records
+    from sbeacon._lib import SB_EINTERNAL, SbError
+    from sbeacon.engine import Store
+    from sbeacon.requests import RequestBatch, requests_from_split_payloads
+    path = os.path.join(FIXTURES, 'tiny22.vcf')
+    store = Store.build([('tiny22.vcf', path)], device=0)
+    recs, _ = read_records(path)
+    lo, hi = recs[0][1], recs[-1][1]
+    sps = [dict(passthrough={}, dataset_id='d', query_id='q', reference_bases='N', start_min=lo + k,
+                start_max=min(hi, lo + k + 300000), end_min=0, end_max=10**9, alternate_bases=None,
+                variant_type=['DEL', 'INS', 'CNV', 'DUP'][k % 4], include_datasets='HIT',
+                vcf_locations={'tiny22.vcf': '22'}, vcf_groups=[], requested_granularity='record',
+                variant_min_length=0, variant_max_length=-1) for k in range(16)]
+    arr, _, owners = requests_from_split_payloads(store, sps)
+    monkeypatch.setenv('SBEACON_REQ_INJECT', '1')
+    with pytest.raises(SbError) as e:
+        RequestBatch(store, arr, len(owners)).answer()
+    assert e.value.code == SB_EINTERNAL
+    monkeypatch.delenv('SBEACON_REQ_INJECT')
+    rows, _, _ = RequestBatch(store, arr, len(owners)).answer()
+    exp_rows, _, _ = _expected(store, sps)
+    np.testing.assert_array_equal(rows, exp_rows)
+
+
 def test_shard_plan_stores_on_device():
     """sbeacon.sharding over real fixture VCFs on the device: three shard
     stores (sb_builder_set_record_range: core + halo), every golden payload
