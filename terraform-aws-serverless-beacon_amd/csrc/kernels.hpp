@@ -122,6 +122,7 @@ uint32_t req_run_max();
 // the caller) = chain rows, their slices, the staging total.
 void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,
                          unsigned long long *rcap, unsigned long long *counters, hipStream_t s);
+size_t request_plan_words(uint32_t n_runs);  // planning scratch: per-run and per-workgroup totals + counters
 uint32_t request_tiles(uint32_t n_runs);
 
 // Fetch-time gather of every query's hits into one dense array.

@@ -2392,10 +2392,15 @@ __global__ __launch_bounds__(kBlock) void request_plan_kernel(DStore st, const R
                                                               uint32_t n_runs, ReqChain *__restrict__ chains,
                                                               RowRun *__restrict__ runs,
                                                               unsigned long long *__restrict__ rcap,
-                                                              unsigned long long *__restrict__ counters) {
+                                                              unsigned long long *__restrict__ gcap) {
+    __shared__ ulonglong2 wtot[kWavesPerBlock];
     const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    if (w >= n_runs) return;
     const uint32_t ul = static_cast<uint32_t>(lane_id());
+    if (w >= n_runs) {  // (no run: its part of the workgroup total is zero)
+        if (ul == 0) wtot[threadIdx.x >> 6] = ulonglong2{0ull, 0ull};
+        __syncthreads();
+        return;
+    }
     const uint32_t row = w * kRunRows + ul;
     ReqIn q{};
     if (row < n) q = in[row];
@@ -2435,21 +2440,82 @@ __global__ __launch_bounds__(kBlock) void request_plan_kernel(DStore st, const R
     if (ul == 0) {  // (the batch's chain / slice totals: request_stage_scan_kernel -- one counter
                     // atomically bumped by every wave serialised the launch, ~350 us for 15.6 k runs)
         runs[w] = RowRun{w * kRunRows, min(w * kRunRows + kRunRows, n), 0u, nslots, 0ull, slsum, flags};
+        const unsigned long long cw = static_cast<unsigned long long>(slsum) << 32 | nslots;
         rcap[2 * w] = capsum;
-        rcap[2 * w + 1] = static_cast<unsigned long long>(slsum) << 32 | nslots;
+        rcap[2 * w + 1] = cw;
+        wtot[threadIdx.x >> 6] = ulonglong2{capsum, cw};
     }
+    // the workgroup's totals (request_stage_scan_kernel sums these for the
+    // runs before its tile: a quarter of the words per-run totals would be)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        ulonglong2 t{0ull, 0ull};
+#pragma unroll
+        for (uint32_t k = 0; k < kWavesPerBlock; ++k) {
+            t.x += wtot[k].x;
+            t.y += wtot[k].y;
+        }
+        reinterpret_cast<ulonglong2 *>(gcap)[blockIdx.x] = t;
+    }
+}
+
+// The two scans of the pass (staging offsets per run, output offsets per
+// tile of kDeliverTile runs) run in ONE workgroup of 1,024 threads over
+// rounds of kRunScanRound runs, every load coalesced: item u of thread t is run
+// base + 1,024 u + t, so a wave instruction reads 64 consecutive runs, and a
+// tile (16 consecutive runs) is one 16-lane DPP row -- its sums by row
+// shifts, its total in the row's last lane.  The round's 512 tile totals are
+// scanned in LDS.  (Round 4's forms loaded each thread's runs contiguously --
+// 16-byte loads 256 B apart across the lanes, four times the cache-line
+// accesses -- and took 7.4 us (tile scan, one workgroup) and 6.3 us (staging
+// scan, a workgroup per 1,024 runs re-reading every earlier run).)
+constexpr uint32_t kRunScanPer = 8;                          // runs per thread per round
+constexpr uint32_t kRunScanRound = 1024 * kRunScanPer;           // runs per round
+constexpr uint32_t kRunScanTiles = kRunScanRound / kDeliverTile; // tiles per round (512)
+static_assert(kDeliverTile == 16, "a tile is one DPP row");
+
+// inclusive sum inside each 16-lane row (row_shr 1, 2, 4, 8)
+__device__ __forceinline__ uint64_t row_incl_sum_u64(uint64_t v) {
+    v += static_cast<uint64_t>(dpp_i64<0x111, 0xf, 0xf>(static_cast<int64_t>(v)));
+    v += static_cast<uint64_t>(dpp_i64<0x112, 0xf, 0xf>(static_cast<int64_t>(v)));
+    v += static_cast<uint64_t>(dpp_i64<0x114, 0xf, 0xf>(static_cast<int64_t>(v)));
+    v += static_cast<uint64_t>(dpp_i64<0x118, 0xf, 0xf>(static_cast<int64_t>(v)));
+    return v;
+}
+
+// exclusive scan of the round's kRunScanTiles tile totals held in tl[] (thread
+// t < kRunScanTiles takes tile t), written back in place plus `carry`; returns
+// the round's total.  Every thread calls it (barriers).
+__device__ __forceinline__ uint64_t scan_round_tiles(unsigned long long *tl, unsigned long long *wsum, uint64_t carry) {
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
+    constexpr uint32_t kW = kRunScanTiles / kWave;  // waves holding tiles (8)
+    const uint64_t x = tid < kRunScanTiles ? tl[tid] : 0ull;
+    const uint64_t inc = incl_sum_u64(x);
+    if (lane_id() == kWave - 1 && wave < kW) wsum[wave] = inc;
+    __syncthreads();
+    uint64_t before = carry, total = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kW; ++k) {
+        const uint64_t w = wsum[k];
+        if (k < wave) before += w;
+        total += w;
+    }
+    if (tid < kRunScanTiles) tl[tid] = before + inc - x;
+    __syncthreads();
+    return total;
 }
 
 // request_stage_scan_kernel: each run's staging offset = the exclusive
 // prefix of the runs' capacities; counters = (chains, chain slices, staging
 // total).  request_plan_kernel left per run {capacity, slices << 32 |
-// chains} (16 B).  One workgroup per tile of 1,024 runs: it sums the
-// capacities of every earlier tile (coalesced, a few loads per thread, all in
-// flight at once), then scans its own tile; the last workgroup, which reads
-// every run anyway, writes the counters.  (One workgroup walking the runs in
-// 16 dependent rounds took 32 us for 15.6 k runs; one workgroup with every
-// thread's 16 runs loaded up front, 19 us: one CU's load issue.)
+// chains} (16 B) and the same per plan workgroup of kWavesPerBlock runs.
+// One workgroup per tile of kStageTile runs: it sums the workgroup totals of
+// every earlier tile (coalesced, all loads of a round in flight), then scans
+// its own tile; the last workgroup, which reads every total anyway, writes
+// the counters.  (Summing the earlier tiles' per-run words took 6.3 us: the
+// last workgroup read 250 KB; one workgroup scanning all runs, 10.5 us.)
 constexpr uint32_t kStageTile = 1024;
+static_assert(kStageTile % kWavesPerBlock == 0, "a stage tile is whole plan workgroups");
 __device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, unsigned long long *wsum) {
     const uint32_t wave = threadIdx.x >> 6;
     const uint64_t t = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(v)), kWave - 1));
@@ -2462,20 +2528,23 @@ __device__ __forceinline__ uint64_t block_sum_u64(uint64_t v, unsigned long long
 }
 __global__ __launch_bounds__(kStageTile) void request_stage_scan_kernel(RowRun *__restrict__ runs,
                                                                         const unsigned long long *__restrict__ rcap,
+                                                                        const unsigned long long *__restrict__ gcap,
                                                                         uint32_t n_runs,
                                                                         unsigned long long *__restrict__ counters) {
     __shared__ unsigned long long wsum[kStageTile / kWave];
     const uint32_t tid = threadIdx.x, wave = tid >> 6, t0 = blockIdx.x * kStageTile;
     const bool last = blockIdx.x + 1 == gridDim.x;
     const ulonglong2 *rc2 = reinterpret_cast<const ulonglong2 *>(rcap);
+    const ulonglong2 *gc2 = reinterpret_cast<const ulonglong2 *>(gcap);
+    const uint32_t g0 = t0 / kWavesPerBlock;  // plan workgroups before this tile
     uint64_t pre = 0, nch = 0, nsl = 0;
-    constexpr uint32_t kU = 8;
-    for (uint32_t i0 = 0; i0 < t0; i0 += kStageTile * kU) {
+    constexpr uint32_t kU = 4;
+    for (uint32_t i0 = 0; i0 < g0; i0 += kStageTile * kU) {
         ulonglong2 x[kU];
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
             const uint32_t i = i0 + u * kStageTile + tid;
-            x[u] = i < t0 ? rc2[i] : ulonglong2{0ull, 0ull};
+            x[u] = i < g0 ? gc2[i] : ulonglong2{0ull, 0ull};
         }
 #pragma unroll
         for (uint32_t u = 0; u < kU; ++u) {
@@ -2509,48 +2578,35 @@ __global__ __launch_bounds__(kStageTile) void request_stage_scan_kernel(RowRun *
     }
 }
 
-// request_tile_scan_kernel: one workgroup adds up each tile's run totals
-// (tiles of kDeliverTile runs) and scans them into exclusive tile offsets.
-// A thread takes two adjacent tiles per round (2,048 tiles: 32 k runs, 1 M
-// requests) and issues all 16 of their 16-byte loads before adding: one
-// memory round trip per round.  (Tile totals by device atomics in
-// request_eval_kernel needed a memset launch before every pass.)
+// request_tile_scan_kernel: the runs' totals (request_eval_kernel's status
+// words) summed per tile of kDeliverTile runs and scanned into exclusive tile
+// offsets.  (Tile totals by device atomics in request_eval_kernel needed a
+// memset launch before every pass.)
 __global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned long long *__restrict__ status,
                                                                  uint32_t n_runs, unsigned long long *__restrict__ tsum,
                                                                  uint32_t nt) {
-    __shared__ unsigned long long wsum[16];
-    __shared__ unsigned long long carry_s;
-    const uint32_t tid = threadIdx.x, wave = tid >> 6;
-    if (tid == 0) carry_s = 0;
-    __syncthreads();
-    for (uint32_t base = 0; base < nt; base += 2048) {
-        const uint32_t i0 = base + 2 * tid, i1 = i0 + 1;
-        uint64_t v0 = 0, v1 = 0;
-        if ((i1 + 1) * kDeliverTile <= n_runs) {  // both tiles whole: 16 words each, 128 B aligned
-            const ulonglong2 *q = reinterpret_cast<const ulonglong2 *>(status + i0 * kDeliverTile);
-            ulonglong2 x[kDeliverTile];
+    __shared__ unsigned long long tl[kRunScanTiles];
+    __shared__ unsigned long long wsum[1024 / kWave];
+    const uint32_t tid = threadIdx.x;
+    uint64_t carry = 0;
+    for (uint32_t base = 0; base < n_runs; base += kRunScanRound) {
+        uint64_t v[kRunScanPer];
 #pragma unroll
-            for (uint32_t k = 0; k < kDeliverTile; ++k) x[k] = q[k];
-#pragma unroll
-            for (uint32_t k = 0; k < kDeliverTile / 2; ++k) {
-                v0 += x[k].x + x[k].y;
-                v1 += x[k + kDeliverTile / 2].x + x[k + kDeliverTile / 2].y;
-            }
-        } else {
-            for (uint32_t r = i0 * kDeliverTile; r < min(i1 * kDeliverTile, n_runs); ++r) v0 += status[r];
-            for (uint32_t r = i1 * kDeliverTile; r < min((i1 + 1) * kDeliverTile, n_runs); ++r) v1 += status[r];
+        for (uint32_t u = 0; u < kRunScanPer; ++u) {
+            const uint32_t r = base + u * 1024 + tid;
+            v[u] = r < n_runs ? status[r] : 0ull;
         }
-        const uint64_t v = v0 + v1;
-        const uint64_t incl = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(v)));
-        if (lane_id() == kWave - 1) wsum[wave] = incl;
+#pragma unroll
+        for (uint32_t u = 0; u < kRunScanPer; ++u) {
+            const uint64_t t = row_incl_sum_u64(v[u]);
+            if ((lane_id() & 15u) == 15u) tl[u * (1024 / kDeliverTile) + tid / kDeliverTile] = t;
+        }
         __syncthreads();
-        uint64_t before = carry_s;
-        for (uint32_t k = 0; k < wave; ++k) before += wsum[k];
-        if (i0 < nt) tsum[i0] = before + incl - v;
-        if (i1 < nt) tsum[i1] = before + incl - v + v0;
-        __syncthreads();
-        if (tid == 1023) carry_s = before + incl;
-        __syncthreads();
+        const uint64_t total = scan_round_tiles(tl, wsum, carry);
+        const uint32_t t0 = base / kDeliverTile;
+        if (tid < kRunScanTiles && t0 + tid < nt) tsum[t0 + tid] = tl[tid];
+        carry += total;
+        __syncthreads();  // tl is rewritten by the next round
     }
 }
 
@@ -3874,11 +3930,17 @@ void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain
                          unsigned long long *rcap, unsigned long long *counters, hipStream_t s) {
     const uint32_t n_runs = (n + kRunRows - 1) / kRunRows;
     if (!n_runs) return;
+    // per plan workgroup totals after the counters (requests.cpp sizes the buffer: request_plan_words)
+    unsigned long long *gcap = counters + 4;
     hipLaunchKernelGGL(request_plan_kernel, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, in, n, n_runs, chains,
-                       runs, rcap, counters);
+                       runs, rcap, gcap);
     hipLaunchKernelGGL(request_stage_scan_kernel, dim3((n_runs + kStageTile - 1) / kStageTile), dim3(kStageTile), 0, s,
-                       runs, rcap, n_runs, counters);
+                       runs, rcap, gcap, n_runs, counters);
 }
+
+// planning scratch (u64 words): per run {capacity, slices | chains}, the
+// three batch counters (+ pad), per plan workgroup the same two totals
+size_t request_plan_words(uint32_t n_runs) { return size_t(n_runs) * 2 + 4 + size_t(blocks_for(n_runs)) * 2; }
 
 // run totals (request_eval_kernel) -> tile offsets (request_tile_scan_kernel)
 uint32_t request_tiles(uint32_t n_runs) { return (n_runs + kDeliverTile - 1) / kDeliverTile; }

@@ -364,7 +364,7 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     const uint32_t n_runs = static_cast<uint32_t>((n + kRunRows - 1) / kRunRows);
     const size_t chain_bytes = size_t(n_runs) * kReqRun * sizeof(ReqChain), run_bytes = size_t(n_runs) * sizeof(RowRun);
     // rc: per run {capacity, slices << 32 | chains} (request_plan_kernel), then the 3 counters
-    DevMem din = P.get_dev(n * sizeof(ReqIn)), rc = P.get_dev(size_t(n_runs) * 16 + 32);
+    DevMem din = P.get_dev(n * sizeof(ReqIn)), rc = P.get_dev(request_plan_words(n_runs) * 8);
     R->dchains = P.get_dev(chain_bytes + run_bytes);
     R->runs_at = chain_bytes;
     R->n_runs = n_runs;
