@@ -124,6 +124,7 @@ void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain
                          unsigned long long *rcap, unsigned long long *counters, hipStream_t s);
 size_t request_plan_words(uint32_t n_runs);  // planning scratch: per-run and per-workgroup totals + counters
 uint32_t request_tiles(uint32_t n_runs);
+size_t request_tstatus_words(uint32_t n_runs);  // tile offsets + eval workgroup totals
 
 // Fetch-time gather of every query's hits into one dense array.
 void launch_compact(const uint64_t *hit_off, const uint64_t *dense_off, const QRes *res, uint32_t nq,

@@ -2014,14 +2014,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
     unsigned long long *__restrict__ status, const QRes *__restrict__ sres, void *__restrict__ rows_out,
     void *__restrict__ row_cnt_out, uint64_t *__restrict__ row_src, uint32_t *__restrict__ stage, uint32_t n_lut,
-    unsigned int *__restrict__ err, uint32_t inject) {
+    unsigned int *__restrict__ err, uint32_t inject, unsigned long long *__restrict__ gtot) {
     ReqPartial *const rows = static_cast<ReqPartial *>(rows_out);
     uint64_t *const row_cnt = static_cast<uint64_t *>(row_cnt_out);
     __shared__ ReqLds lds_all[kWavesPerBlock];
     __shared__ uint32_t slut[LDS_LUT ? kReqLut : 1];
+    // the workgroup's run totals: the last wave to finish writes their sum
+    // (gtot[group], request_tile_scan_kernel), counted by an LDS atomic --
+    // no barrier, a finished wave leaves at once
+    __shared__ unsigned long long s_tot[kWavesPerBlock];
+    __shared__ uint32_t s_done;
     ReqLds &L = lds_all[threadIdx.x >> 6];
     const uint32_t ul = static_cast<uint32_t>(lane_id());
     const uint32_t w = launch_wave();
+    auto finish = [&](uint64_t H) {  // lane 0
+        s_tot[threadIdx.x >> 6] = H;
+        if (__hip_atomic_fetch_add(&s_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) == kWavesPerBlock - 1) {
+            uint64_t t = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < kWavesPerBlock; ++k) t += s_tot[k];
+            gtot[w / kWavesPerBlock] = t;
+        }
+    };
     // the run record and the run's chain descriptors (lane k = slot k; the
     // non-empty chains first, then the empty ones, then first == 0 slots)
     // and the workgroup's LUT words: independent loads, one round trip
@@ -2032,12 +2046,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         rr = runs[w];
         C = chains[static_cast<uint64_t>(w) * kReqRun + ul];
     }
-    if constexpr (LDS_LUT) {
+    if (threadIdx.x == 0) s_done = 0;
+    if constexpr (LDS_LUT)
         for (uint32_t i = threadIdx.x; i < n_lut; i += kBlock) slut[i] = st.sym_lut[i];
-        __syncthreads();
-    }
+    __syncthreads();
     const uint32_t *lut_base = LDS_LUT ? slut : st.sym_lut;
-    if (!live) return;
+    if (!live) {
+        if (ul == 0) finish(0);
+        return;
+    }
     const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
     const uint64_t stage_at = uniform64(rr.stage);
     const uint32_t rflags = uniform(rr.flags);
@@ -2376,7 +2393,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         }
     }
     const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(nvr)), kWave - 1));
-    if (ul == 0) status[w] = H;  // read by the tile scan and request_deliver_kernel (kernel boundaries)
+    if (ul == 0) {
+        status[w] = H;  // read by request_deliver_kernel (kernel boundary)
+        finish(H);
+    }
 }
 
 // ---- request planning on the device (sb_requests_prepare_columns)
@@ -2578,35 +2598,52 @@ __global__ __launch_bounds__(kStageTile) void request_stage_scan_kernel(RowRun *
     }
 }
 
-// request_tile_scan_kernel: the runs' totals (request_eval_kernel's status
-// words) summed per tile of kDeliverTile runs and scanned into exclusive tile
-// offsets.  (Tile totals by device atomics in request_eval_kernel needed a
-// memset launch before every pass.)
-__global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned long long *__restrict__ status,
-                                                                 uint32_t n_runs, unsigned long long *__restrict__ tsum,
+// request_tile_scan_kernel: the tiles' totals (a tile of kDeliverTile runs =
+// kDeliverTile / kWavesPerBlock eval workgroups, whose totals
+// request_eval_kernel left in gtot) scanned into exclusive tile offsets, one
+// workgroup, rounds of 1,024 tiles with every load coalesced: a tile is a
+// quad of lanes (DPP quad permutes sum it).  (Reading the runs' own totals:
+// 6.3 us, one CU's loads of 8 B per run; tile totals by device atomics in
+// request_eval_kernel needed a memset launch before every pass.)
+static_assert(kDeliverTile == 4 * kWavesPerBlock, "a tile is four eval workgroups (a quad of lanes)");
+constexpr uint32_t kTilePer = 4;  // group totals per thread per round: 1,024 tiles
+__global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned long long *__restrict__ gtot,
+                                                                 uint32_t n_groups,
+                                                                 unsigned long long *__restrict__ tsum,
                                                                  uint32_t nt) {
-    __shared__ unsigned long long tl[kRunScanTiles];
+    __shared__ unsigned long long tl[1024];
     __shared__ unsigned long long wsum[1024 / kWave];
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, wave = tid >> 6;
     uint64_t carry = 0;
-    for (uint32_t base = 0; base < n_runs; base += kRunScanRound) {
-        uint64_t v[kRunScanPer];
+    for (uint32_t base = 0; base < n_groups; base += 1024 * kTilePer) {
+        uint64_t v[kTilePer];
 #pragma unroll
-        for (uint32_t u = 0; u < kRunScanPer; ++u) {
-            const uint32_t r = base + u * 1024 + tid;
-            v[u] = r < n_runs ? status[r] : 0ull;
+        for (uint32_t u = 0; u < kTilePer; ++u) {
+            const uint32_t g = base + u * 1024 + tid;
+            v[u] = g < n_groups ? gtot[g] : 0ull;
         }
 #pragma unroll
-        for (uint32_t u = 0; u < kRunScanPer; ++u) {
-            const uint64_t t = row_incl_sum_u64(v[u]);
-            if ((lane_id() & 15u) == 15u) tl[u * (1024 / kDeliverTile) + tid / kDeliverTile] = t;
+        for (uint32_t u = 0; u < kTilePer; ++u) {  // quad sums: [1,0,3,2] then [2,3,0,1]
+            uint64_t q = v[u] + static_cast<uint64_t>(dpp_i64<0xB1, 0xf, 0xf>(static_cast<int64_t>(v[u])));
+            q += static_cast<uint64_t>(dpp_i64<0x4E, 0xf, 0xf>(static_cast<int64_t>(q)));
+            if ((lane_id() & 3u) == 0) tl[u * 256 + tid / 4] = q;
         }
         __syncthreads();
-        const uint64_t total = scan_round_tiles(tl, wsum, carry);
-        const uint32_t t0 = base / kDeliverTile;
-        if (tid < kRunScanTiles && t0 + tid < nt) tsum[t0 + tid] = tl[tid];
+        const uint64_t x = tl[tid];
+        const uint64_t inc = incl_sum_u64(x);
+        if (lane_id() == kWave - 1) wsum[wave] = inc;
+        __syncthreads();
+        uint64_t before = carry, total = 0;
+#pragma unroll
+        for (uint32_t k = 0; k < 1024 / kWave; ++k) {
+            const uint64_t ws = wsum[k];
+            if (k < wave) before += ws;
+            total += ws;
+        }
+        const uint32_t t = base / 4 + tid;
+        if (t < nt) tsum[t] = before + inc - x;
         carry += total;
-        __syncthreads();  // tl is rewritten by the next round
+        __syncthreads();  // tl / wsum are rewritten by the next round
     }
 }
 
@@ -3899,12 +3936,13 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
         return;
     }
     const dim3 grid(blocks_for(n_runs));
-    const uint32_t n_tiles = request_tiles(n_runs);
+    const uint32_t n_tiles = request_tiles(n_runs), n_groups = blocks_for(n_runs);
+    unsigned long long *const gtot = tstatus + n_tiles;  // eval workgroup totals (request_tstatus_words)
     if (ev0) (void)hipEventRecord(ev0, s);
     auto eval = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
                            static_cast<void *>(rows), static_cast<void *>(row_off), row_src, stage, n_lut, err,
-                           static_cast<uint32_t>(config().req_inject));
+                           static_cast<uint32_t>(config().req_inject), gtot);
     };
     (void)run;
     if (compact) {
@@ -3915,7 +3953,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
         else eval(request_eval_kernel<false, false>);
     }
     if (ev1) (void)hipEventRecord(ev1, s);
-    hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, status, n_runs, tstatus, n_tiles);
+    hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, gtot, n_groups, tstatus, n_tiles);
     if (compact)
         hipLaunchKernelGGL(request_deliver_kernel<true>, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres,
                            sseg, shoff, sherr, shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx,
@@ -3944,6 +3982,8 @@ size_t request_plan_words(uint32_t n_runs) { return size_t(n_runs) * 2 + 4 + siz
 
 // run totals (request_eval_kernel) -> tile offsets (request_tile_scan_kernel)
 uint32_t request_tiles(uint32_t n_runs) { return (n_runs + kDeliverTile - 1) / kDeliverTile; }
+// tile offsets, then the eval workgroups' totals
+size_t request_tstatus_words(uint32_t n_runs) { return size_t(request_tiles(n_runs)) + blocks_for(n_runs); }
 
 uint32_t pack_run_max() { return kPackRun; }
 uint32_t req_run_max() { return kReqRun; }

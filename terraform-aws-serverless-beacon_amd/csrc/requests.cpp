@@ -391,7 +391,7 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     R->n_in = static_cast<uint32_t>(n);
     R->cap = B.cap_total + stage_total;
     R->status = P.get_dev(size_t(n_runs) * 8);
-    R->tstatus = P.get_dev(size_t(request_tiles(n_runs)) * 8);
+    R->tstatus = P.get_dev(request_tstatus_words(n_runs) * 8);
     R->stage = P.get_dev(stage_total * 4);
     R->row_src = P.get_dev(R->slices ? n * 8 : 0);
     upload_slice_part(B, *R, seg, n, st);  // (synchronises when there is a per-slice part)
@@ -647,7 +647,7 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
     ReqPool &P = *R->pool;
     R->dchains = P.get_dev(chain_bytes + run_bytes);
     R->status = P.get_dev(n_runs * 8);
-    R->tstatus = P.get_dev(size_t(request_tiles(static_cast<uint32_t>(n_runs))) * 8);
+    R->tstatus = P.get_dev(request_tstatus_words(static_cast<uint32_t>(n_runs)) * 8);
     R->stage = P.get_dev(stage_total * 4);
     R->row_src = P.get_dev(R->slices || std::any_of(R->runs.begin(), R->runs.end(),
                                                     [](const RowRun &r) { return !(r.flags & kRunSimple); })
