@@ -1,8 +1,10 @@
-# round 5: request_eval_kernel timing ablations (wrong answers, timing only)
-mkdir -p gpurun_out/r05d
+# request pass on 4 rotating 1 M batches (tools/req_tune.py): eval / pass
+# timing and the outputs' digest of the in-tree library, then of every
+# library variant named in $VARIANTS (tools/build_variant.sh NAME ...)
+mkdir -p gpurun_out/${TAG:-gpu_pass_ab}
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r05d
+O=$R/gpurun_out/${TAG:-gpu_pass_ab}
 step() {  # name, limit, command...
   local name=$1 lim=$2; shift 2
   timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?

@@ -1,9 +1,9 @@
-# round 5: coalesced one-workgroup scans of the request pass -- request
-# tests, the rotating-batch digest / timing, and their kernel durations
-mkdir -p gpurun_out/r05q
+# request pass: the request GPU tests, the rotating-batch digest / timing,
+# and every kernel's duration from a kernel trace (tools/kernel_table.py)
+mkdir -p gpurun_out/${TAG:-gpu_pass_kernels}
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r05q
+O=$R/gpurun_out/${TAG:-gpu_pass_kernels}
 step() {  # name, limit, command...
   local name=$1 lim=$2; shift 2
   timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?

@@ -1,8 +1,8 @@
-# round 5: memory-side counters of the request pass (TCP / UTCL1 / TCC / TA / TD / GRBM), one pass each
-mkdir -p gpurun_out/r05e
+# memory-side counters of the request pass (TCP / UTCL1 / TCC / TA / TD / GRBM), one pass each
+mkdir -p gpurun_out/${TAG:-gpu_pass_pmc}
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-O=$R/gpurun_out/r05e
+O=$R/gpurun_out/${TAG:-gpu_pass_pmc}
 step() {  # name, limit, command...
   local name=$1 lim=$2; shift 2
   timeout -k 10 $lim "$@" > $O/$name.log 2>&1; local rc=$?
