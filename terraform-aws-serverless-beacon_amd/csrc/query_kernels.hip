@@ -2316,7 +2316,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
             }
         }
     };
+#ifdef SBEACON_ABL_NOCHUNK  // timing ablation only: setup and epilogue without the candidate loop
+    if (false) {
+#else
     if (nch) {
+#endif
         // The prefetch is unconditional (past the run a load reads the valid
         // index i_safe, one cache line): every path of the steady loop then
         // issues the same loads, so the wait-counter pass can wait for chunk
