@@ -52,6 +52,7 @@ def main_genome(args):
         import torch.distributed as dist
         dist.init_process_group('nccl', device_id=dev)
     from sbeacon.genome import GenomeShape, config3_requests, prepare_shard_requests, union_rows, shard_slices
+    from sbeacon.requests import COMPACT_HITS, widen_hits
     from sbeacon.shard import ResultExchange
 
     t0 = time.perf_counter()
@@ -90,10 +91,14 @@ def main_genome(args):
         batch = prepare_shard_requests(store, sr)      # request batch: packing + upload + planning (C++)
         batch.set_stream(stream)  # torch's stream: kernels, torch ops and RCCL in one order
         batch.set_replan(True)
+        # hits as u32 (record + base) | ALT << 29 (the genome's 85 M records fit
+        # 29 bits; the library refuses a batch whose records would not): half
+        # the delivery's writes and the exchange's hit volume; rows stay int64
+        batch.set_compact(COMPACT_HITS)
         pst = batch.stats()
         B.append(dict(reqs=reqs_k, sr=sr, batch=batch, pst=pst,
                       part=torch.zeros((max(sr.n_rows, 1), 5), dtype=torch.int64, device=dev),
-                      hits=torch.zeros(max(int(pst['hits']), 1), dtype=torch.int64, device=dev),
+                      hits=torch.zeros(max(int(pst['hits']), 1), dtype=torch.int32, device=dev),
                       row_off=torch.zeros(sr.n_rows + 1, dtype=torch.int64, device=dev),
                       ex=ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, dev)))
     t_prepare = (time.perf_counter() - t0) / args.batches
@@ -185,8 +190,8 @@ def main_genome(args):
     # the whole pass: the planning kernels (32 B packed request read, 32 B
     # descriptor written per request), eval, tile scan, delivery (+ 8 B row
     # offset per request; per hit its staged word read (4 B), its record id
-    # read (4 B), the 8 B hit written)
-    comp_pass = comp + 64.0 * agg['rows'] + 8.0 * chains + 16.0 * hits_avg
+    # read (4 B), the 4 B hit written: u32 hits, sb_requests_set_compact)
+    comp_pass = comp + 64.0 * agg['rows'] + 8.0 * chains + 12.0 * hits_avg
     achieved_pass = comp_pass / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
     uniq = agg['uniq']
     contract = 32.0 * uniq + 8.0 * hits_avg
@@ -212,7 +217,7 @@ def main_genome(args):
                                f'{serial["hits_returned"]}')
         # full-size property: the step's rows + hit lists (one batch, resident),
         # the serial delivered pass and the pipelined chunks are bit-identical
-        step_digest = digest(part[:sr.n_rows].cpu().numpy(), [hits[:nhits].cpu().numpy()])
+        step_digest = digest(part[:sr.n_rows].cpu().numpy(), [widen_hits(hits[:nhits].cpu().numpy())])
         if not (step_digest == serial['digest'] == delivered['digest']):
             raise RuntimeError(f'delivery digests differ: step {step_digest}, serial {serial["digest"]}, '
                                f'pipelined {delivered["digest"]}')
@@ -239,13 +244,13 @@ def main_genome(args):
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline_and_parity(args, shape, reqs, ex.exchange(part, hits, row_off).cpu().numpy(),
-                                              hits.cpu().numpy(), row_off.cpu().numpy())
+                                              widen_hits(hits.cpu().numpy()), row_off.cpu().numpy())
         # the other batches of the rotation: a smaller sample each, parity only
         parity['other_batches'] = []
         for k, b in enumerate(B[1:], start=1):
             _, pk = cpu_baseline_and_parity(args, shape, b['reqs'],
                                             b['ex'].exchange(b['part'], b['hits'], b['row_off']).cpu().numpy(),
-                                            b['hits'].cpu().numpy(), b['row_off'].cpu().numpy(), n_sample=4000,
+                                            widen_hits(b['hits'].cpu().numpy()), b['row_off'].cpu().numpy(), n_sample=4000,
                                             seed=7 + k, timed=False)
             pk['batch'] = k
             parity['other_batches'].append(pk)
@@ -275,7 +280,7 @@ def main_genome(args):
                 '(request_plan_kernel: each request\'s candidate range by a batched lower / upper bound of its '
                 'splitQuery window in the (segment, kind) index + its staging capacity; request_stage_scan_kernel), '
                 'request_eval_kernel (every request = one chain of its 10 kb slices, rows + hits staged per run), '
-                'request_tile_scan_kernel + request_deliver_kernel (row offsets, dense hit lists in request order), '
+                'request_tile_scan_kernel + request_deliver_kernel (row offsets, dense hit lists in request order, hits as u32 (record | ALT << 29)), '
                 'then the exchange (send/recv of straddling rows and hits)',
         'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
         'candidates_loaded_per_s': round(tot_cand * args.steps / elapsed, 1),
@@ -299,8 +304,8 @@ def main_genome(args):
                      'pass': {'ms': round(r0[10], 4), 'achieved': round(r0[11], 1),
                               'frac': round(r0[11] / HBM_PEAK_GBS, 4), 'bytes': r0[12],
                               'note': 'planning (+64 B/request: packed request read, descriptor written) + eval + '
-                                      'tile scan + delivery (+8 B/request row offsets; +16 B/hit: staged word and '
-                                      'record id read, 8 B hit written)'},
+                                      'tile scan + delivery (+8 B/request row offsets; +12 B/hit: staged word and '
+                                      'record id read, 4 B hit written)'},
                      'candidates': {'unique': int(st['cand_unique']), 'in_windows': int(st['cand_window']),
                                     'loaded': int(st['cand_loaded'])},
                      'contract_bytes_per_launch': r0[8],

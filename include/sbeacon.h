@@ -538,12 +538,15 @@ int sb_requests_set_replan(sb_batch *b, int on);
 typedef struct {
     uint32_t exists, n_variants, call_count, all_alleles_count;
 } sb_request_row32;
-/* With on != 0, sb_requests_run writes the narrow form a host copy-back
- * wants: dev_rows[n] as sb_request_row32 (16 B instead of 40), dev_row_off[n + 1]
- * as uint32, and each hit as uint32 (record + rec_base) | ALT label << 29.
- * SB_EINVAL for a batch with a per-slice part, or (at run) when record
- * numbers reach 2^29; a count or offset past 32 bits fails the pass at
- * sb_batch_sync (SB_EINTERNAL). */
+/* Output widths of sb_requests_run.  SB_COMPACT_ALL: the narrow form a host
+ * copy-back wants -- dev_rows[n] as sb_request_row32 (16 B instead of 40),
+ * dev_row_off[n + 1] as uint32, and each hit as uint32 (record + rec_base) |
+ * ALT label << 29; SB_EINVAL for a batch with a per-slice part.
+ * SB_COMPACT_HITS: wide rows and offsets, uint32 hits as above (any batch).
+ * Either: SB_EINVAL at run when record numbers reach 2^29; a count or offset
+ * past 32 bits fails the pass at sb_batch_sync (SB_EINTERNAL).  0: wide. */
+#define SB_COMPACT_ALL 1
+#define SB_COMPACT_HITS 2
 int sb_requests_set_compact(sb_batch *b, int on);
 /* After a pass (waits for it): flags[w] = 1 when row w's call_count or
  * all_alleles_count is not exact in int64 -- a slice's count past 64 bits

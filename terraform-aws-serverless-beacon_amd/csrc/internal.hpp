@@ -446,7 +446,7 @@ struct sb_batch {
         DevMem din, rcap;
         uint32_t n_in = 0;
         bool replan = false;
-        bool compact = false;  // sb_requests_set_compact
+        int compact = 0;  // sb_requests_set_compact: 0 wide, SB_COMPACT_ALL, SB_COMPACT_HITS
         // request_eval_kernel's invariant word (sticky; checked at sync: SB_EINTERNAL)
         DevMem err;
         ReqPool::Pinned err_h;

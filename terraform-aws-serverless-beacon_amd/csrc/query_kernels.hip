@@ -2661,7 +2661,7 @@ __global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned 
 // COMPACT: row counts / offsets u32, hits u32 = (record + rec_base) | label
 // << kStageAltShift (the host checks records + rec_base < 2^29; an offset
 // past 32 bits fails the batch at sync)
-template <bool COMPACT>
+template <bool ROWC, bool HITC>
 __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const RowRun *__restrict__ runs, uint32_t n_runs, const unsigned long long *__restrict__ status,
     const unsigned long long *__restrict__ toff, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
@@ -2669,13 +2669,14 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     void *__restrict__ row_off_out, const uint64_t *__restrict__ row_src, const uint32_t *__restrict__ stage,
     const uint32_t *__restrict__ vc_idx, void *__restrict__ out_v, uint32_t n_rows, uint64_t rec_base,
     unsigned int *__restrict__ err) {
-    using Hit = std::conditional_t<COMPACT, uint32_t, uint64_t>;
+    using Hit = std::conditional_t<HITC, uint32_t, uint64_t>;
+    using Off = std::conditional_t<ROWC, uint32_t, uint64_t>;
     Hit *const out = static_cast<Hit *>(out_v);
-    Hit *const row_off = static_cast<Hit *>(row_off_out);  // (counts in, offsets out: the hits' width)
+    Off *const row_off = static_cast<Off *>(row_off_out);  // (counts in, offsets out)
     // a staged hit (candidate | ALT label << kStageAltShift) as the output's
     // (record + rec_base) | label << kHitAltShift
     auto hit_of = [&](uint32_t v) -> Hit {
-        if constexpr (COMPACT)
+        if constexpr (HITC)
             return (vc_idx[v & kStageCandMask] + static_cast<uint32_t>(rec_base)) | (v & ~kStageCandMask);
         else
             return (static_cast<uint64_t>(vc_idx[v & kStageCandMask]) + rec_base) |
@@ -2711,11 +2712,11 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const uint64_t linc = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(c)));
     const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(linc), kWave - 1));
     const uint64_t off = O + linc - c;
-    if constexpr (COMPACT) {
+    if constexpr (ROWC) {
         if (ul == 0 && O + H > 0xffffffffull) atomicOr(err, 2u);
     }
-    if (row < row_hi) row_off[row] = static_cast<Hit>(off);
-    if (row_hi == n_rows && ul == 0) row_off[n_rows] = static_cast<Hit>(O + H);
+    if (row < row_hi) row_off[row] = static_cast<Off>(off);
+    if (row_hi == n_rows && ul == 0) row_off[n_rows] = static_cast<Off>(O + H);
     if (simple) {  // chain rows (and empty rows) only: the staging region is the output, in order
         for (uint64_t j0 = 0; j0 < H; j0 += kWave * kU) {
             uint32_t v[kU];
@@ -2735,7 +2736,7 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
         }
         return;
     }
-    if constexpr (COMPACT) return;  // (compact batches have no per-slice part: every run is simple)
+    if constexpr (ROWC) return;  // (compact-row batches have no per-slice part: every run is simple)
     for (uint32_t i = 0; i < row_hi - row_lo; ++i) {  // row by row (some rows answered per slice)
         const uint64_t nv = static_cast<uint64_t>(rdl64(static_cast<int64_t>(c), i));
         if (!nv) continue;
@@ -2751,7 +2752,14 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
                 const QRes rq = sres[q];
                 if (rq.error || sherr[q]) continue;
                 const uint64_t src = shoff[q];
-                for (uint32_t k = ul; k < rq.n_hits; k += kWave) out[dst + k] = shits[src + k] + rec_base;
+                for (uint32_t k = ul; k < rq.n_hits; k += kWave) {
+                    const uint64_t h = shits[src + k];  // record | ALT << kHitAltShift
+                    if constexpr (HITC)
+                        out[dst + k] = (static_cast<uint32_t>(h) + static_cast<uint32_t>(rec_base)) |
+                                       static_cast<uint32_t>(h >> kHitAltShift) << kStageAltShift;
+                    else
+                        out[dst + k] = h + rec_base;
+                }
                 dst += rq.n_hits;
             }
         }
@@ -3934,9 +3942,10 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
-                         bool compact, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+                         int compact, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+    const bool rowc = compact == SB_COMPACT_ALL, hitc = compact != 0;  // u32 rows / offsets; u32 hits
     if (!n_runs) {
-        (void)hipMemsetAsync(row_off, 0, compact ? 4 : 8, s);
+        (void)hipMemsetAsync(row_off, 0, rowc ? 4 : 8, s);
         return;
     }
     const dim3 grid(blocks_for(n_runs));
@@ -3949,7 +3958,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                            static_cast<uint32_t>(config().req_inject), gtot);
     };
     (void)run;
-    if (compact) {
+    if (rowc) {
         if (n_lut <= kReqLut) eval(request_eval_kernel<true, true>);
         else eval(request_eval_kernel<false, true>);
     } else {
@@ -3958,14 +3967,14 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
     }
     if (ev1) (void)hipEventRecord(ev1, s);
     hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, gtot, n_groups, tstatus, n_tiles);
-    if (compact)
-        hipLaunchKernelGGL(request_deliver_kernel<true>, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres,
-                           sseg, shoff, sherr, shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx,
-                           static_cast<void *>(out), n_rows, rec_base, err);
-    else
-        hipLaunchKernelGGL(request_deliver_kernel<false>, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres,
-                           sseg, shoff, sherr, shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx,
-                           static_cast<void *>(out), n_rows, rec_base, err);
+    auto deliver = [&](auto kern) {
+        hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg, shoff, sherr,
+                           shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx, static_cast<void *>(out),
+                           n_rows, rec_base, err);
+    };
+    if (rowc) deliver(request_deliver_kernel<true, true>);
+    else if (hitc) deliver(request_deliver_kernel<false, true>);
+    else deliver(request_deliver_kernel<false, false>);
 }
 
 void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,

@@ -929,11 +929,13 @@ int sb_requests_inexact_rows(sb_batch *b, uint8_t *flags) {
 int sb_requests_set_compact(sb_batch *b, int on) {
     return guard([&] {
         if (!b || !b->req) throw Error(SB_EINVAL, "not a request batch");
-        if (on && b->req->slices)
+        if (on != 0 && on != SB_COMPACT_ALL && on != SB_COMPACT_HITS)
+            throw Error(SB_EINVAL, "sb_requests_set_compact: mode 0, SB_COMPACT_ALL or SB_COMPACT_HITS");
+        if (on == SB_COMPACT_ALL && b->req->slices)
             throw Error(SB_EINVAL, "sb_requests_set_compact: the batch answers some rows per slice (wide rows only)");
         std::lock_guard<std::mutex> lk(b->mu);
         if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_set_compact between a run and its sync");
-        b->req->compact = on != 0;
+        b->req->compact = on;
     });
 }
 

@@ -27,6 +27,7 @@ from . import _lib
 from ._lib import Request, check, lib
 
 _FIELDS = [f for f, _ in Request._fields_ if f != '_pad']
+COMPACT_ALL, COMPACT_HITS = 1, 2  # sb_requests_set_compact modes (include/sbeacon.h)
 
 
 def request_dtype() -> np.dtype:
@@ -331,12 +332,15 @@ class RequestBatch:
         batches only)."""
         check(lib().sb_requests_set_replan(self._h, 1 if on else 0))
 
-    def set_compact(self, on: bool):
-        """Narrow outputs (sb_requests_set_compact): rows [n, 4] uint32
-        (exists, n_variants, call_count, all_alleles_count), n + 1 uint32
-        row offsets, uint32 hits (record + rec_base) | ALT label << 29."""
-        check(lib().sb_requests_set_compact(self._h, 1 if on else 0))
-        self.compact = bool(on)
+    def set_compact(self, on):
+        """Narrow outputs (sb_requests_set_compact).  True / COMPACT_ALL:
+        rows [n, 4] uint32 (exists, n_variants, call_count,
+        all_alleles_count), n + 1 uint32 row offsets, uint32 hits (record +
+        rec_base) | ALT label << 29.  COMPACT_HITS: wide rows and offsets,
+        uint32 hits.  False / 0: wide."""
+        mode = COMPACT_ALL if on is True else int(on)
+        check(lib().sb_requests_set_compact(self._h, mode))
+        self.compact = mode
 
     def inexact_rows(self) -> np.ndarray:
         """After a pass: True for rows whose call_count / all_alleles_count
@@ -371,7 +375,17 @@ class RequestBatch:
         batch writes (compact outputs widened by widen_compact)."""
         import torch
         dev = device if device is not None else torch.device('cuda', self.store.info()['device'])
-        if getattr(self, 'compact', False):
+        mode = getattr(self, 'compact', 0)
+        if mode == COMPACT_HITS:
+            rows = torch.zeros((max(self.n, 1), 5), dtype=torch.int64, device=dev)
+            hits = torch.zeros(max(int(self.stats()['hits']), 1), dtype=torch.int32, device=dev)
+            row_off = torch.zeros(self.n + 1, dtype=torch.int64, device=dev)
+            self.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+            self.run(rows.data_ptr(), hits.data_ptr(), row_off.data_ptr(), rec_base)
+            self.sync()
+            ro = row_off.cpu().numpy()
+            return rows[:self.n].cpu().numpy(), widen_hits(hits[:int(ro[-1])].cpu().numpy()), ro
+        if mode:
             rows = torch.zeros((max(self.n, 1), 4), dtype=torch.int32, device=dev)
             hits = torch.zeros(max(int(self.stats()['hits']), 1), dtype=torch.int32, device=dev)
             row_off = torch.zeros(self.n + 1, dtype=torch.int32, device=dev)
@@ -390,6 +404,13 @@ class RequestBatch:
         return rows[:self.n].cpu().numpy(), hits[:int(ro[-1])].cpu().numpy().view(np.uint64), ro
 
 
+def widen_hits(hits32):
+    """uint32 hits ((record + rec_base) | ALT label << 29) as the wide form's
+    uint64 record | ALT label << 32."""
+    h = np.asarray(hits32).view(np.uint32).astype(np.uint64)
+    return (h & np.uint64((1 << 29) - 1)) | ((h >> np.uint64(29)) << np.uint64(32))
+
+
 def widen_compact(rows32, hits32, row_off32):
     """Compact request outputs (sb_requests_set_compact) in the wide form:
     (rows [n, 5] int64 with a zero error count, hits uint64 = record | ALT
@@ -397,6 +418,4 @@ def widen_compact(rows32, hits32, row_off32):
     rows32 = np.asarray(rows32).view(np.uint32).reshape(-1, 4)
     rows = np.zeros((len(rows32), 5), dtype=np.int64)
     rows[:, :4] = rows32
-    h = np.asarray(hits32).view(np.uint32).astype(np.uint64)
-    hits = (h & np.uint64((1 << 29) - 1)) | ((h >> np.uint64(29)) << np.uint64(32))
-    return rows, hits, np.asarray(row_off32).view(np.uint32).astype(np.int64)
+    return rows, widen_hits(hits32), np.asarray(row_off32).view(np.uint32).astype(np.int64)

@@ -194,7 +194,7 @@ class ResultExchange:
                 for k, (s_, g, n) in enumerate(self.recvs):
                     nh = int(allc[s_, self.rank, 1])
                     if self.recv_hits[k] is None or self.recv_hits[k].numel() < nh:
-                        self.recv_hits[k] = torch.zeros(nh + nh // 4 + 64, dtype=torch.int64, device=self.device)
+                        self.recv_hits[k] = torch.zeros(nh + nh // 4 + 64, dtype=hits.dtype, device=self.device)
                     self.recv_hits_n[k] = nh
                     ops.append((dist.irecv, self.recv_rows[k], s_))
                     if nh:

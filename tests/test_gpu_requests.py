@@ -416,7 +416,15 @@ def test_device_planned_requests_match_host_planned():
     with pytest.raises(_lib.SbError):
         host_b.set_replan(True)  # planned on the host: nothing to re-plan from
     # the compact output form (u32 rows, offsets and hits), widened on the host: the same answers
+    from sbeacon.requests import COMPACT_HITS
     for b in (dev_b, host_b):
+        # u32 hits with wide rows: any batch (per-slice rows included)
+        b.set_compact(COMPACT_HITS)
+        rows_c, hits_c, ro_c = b.answer()
+        np.testing.assert_array_equal(rows_c, rows_h)
+        np.testing.assert_array_equal(ro_c, ro_h)
+        np.testing.assert_array_equal(hits_c, hits_h)
+        b.set_compact(False)
         if b.stats()['n_queries']:  # some rows answered per slice: wide rows only
             with pytest.raises(_lib.SbError):
                 b.set_compact(True)
