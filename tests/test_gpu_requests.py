@@ -186,6 +186,35 @@ def test_genome_requests_match_oracle_and_slices():
         np.testing.assert_array_equal(total, exp)
 
 
+def test_large_batch_scans_multiple_rounds():
+    """A batch past one round of the pass's scans (> 4,096 eval workgroups =
+    > 1,048,576 requests for the tile scan; > 16 staging tiles): its rows
+    and hit lists equal those of the same requests answered as two batches
+    (each within one round), in the compact-hit form the bench step uses."""
+    from sbeacon.genome import GenomeShape, Requests, config3_requests, prepare_shard_requests, shard_requests
+    from sbeacon.requests import COMPACT_HITS
+    shape = GenomeShape(n_total=240_000, seed=3, n_samples=0)
+    reqs = config3_requests(shape, n=1_150_000, seed=1009)
+    store = shape.build_shard_store(1, 0, device=0)
+
+    def answer(r):
+        b = prepare_shard_requests(store, shard_requests(shape, r, 1, 0))
+        b.set_compact(COMPACT_HITS)
+        out = b.answer()
+        b.free()
+        return out
+
+    rows, hits, ro = answer(reqs)
+    assert len(rows) == len(reqs) and (len(reqs) + 63) // 64 > 4 * 4096
+    k = 600_000
+    part = [answer(Requests(*(getattr(reqs, f)[sl] for f in ('ci', 'start', 'width', 'vt', 'vmin', 'vmax'))))
+            for sl in (slice(0, k), slice(k, None))]
+    np.testing.assert_array_equal(rows, np.concatenate([part[0][0], part[1][0]]))
+    np.testing.assert_array_equal(ro, np.concatenate([part[0][2][:-1], part[1][2] + part[0][2][-1]]))
+    np.testing.assert_array_equal(hits, np.concatenate([part[0][1], part[1][1]]))
+    assert ro[-1] > 0
+
+
 def test_request_batch_is_repeatable():
     """Back-to-back passes (ticket / status re-zeroed per pass) give the same
     rows and hits; the spill path (more hits per run than the LDS buffer)
