@@ -52,7 +52,7 @@ def main_genome(args):
         import torch.distributed as dist
         dist.init_process_group('nccl', device_id=dev)
     from sbeacon.genome import GenomeShape, config3_requests, prepare_shard_requests, union_rows, shard_slices
-    from sbeacon.requests import COMPACT_HITS, widen_hits
+    from sbeacon.requests import COMPACT_ALL, widen_compact, widen_hits, widen_rows
     from sbeacon.shard import ResultExchange
 
     t0 = time.perf_counter()
@@ -91,16 +91,20 @@ def main_genome(args):
         batch = prepare_shard_requests(store, sr)      # request batch: packing + upload + planning (C++)
         batch.set_stream(stream)  # torch's stream: kernels, torch ops and RCCL in one order
         batch.set_replan(True)
-        # hits as u32 (record + base) | ALT << 29 (the genome's 85 M records fit
-        # 29 bits; the library refuses a batch whose records would not): half
-        # the delivery's writes and the exchange's hit volume; rows stay int64
-        batch.set_compact(COMPACT_HITS)
+        # the narrow outputs (sb_requests_set_compact): rows as four u32 sums
+        # (16 B instead of 40), u32 row offsets, hits as u32 (record + base) |
+        # ALT << 29 -- the genome's 85 M records fit 29 bits and a request's
+        # sums 32; the library refuses a batch or fails a pass (SB_EINTERNAL)
+        # that would not fit, and the exchange flags a cross-rank row sum
+        # past 32 bits (row_overflow)
+        batch.set_compact(COMPACT_ALL)
         pst = batch.stats()
         B.append(dict(reqs=reqs_k, sr=sr, batch=batch, pst=pst,
-                      part=torch.zeros((max(sr.n_rows, 1), 5), dtype=torch.int64, device=dev),
+                      part=torch.zeros((max(sr.n_rows, 1), 4), dtype=torch.int32, device=dev),
                       hits=torch.zeros(max(int(pst['hits']), 1), dtype=torch.int32, device=dev),
-                      row_off=torch.zeros(sr.n_rows + 1, dtype=torch.int64, device=dev),
-                      ex=ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, dev)))
+                      row_off=torch.zeros(sr.n_rows + 1, dtype=torch.int32, device=dev),
+                      ex=ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, dev, row_fields=4,
+                                        row_dtype=torch.int32)))
     t_prepare = (time.perf_counter() - t0) / args.batches
     reqs, sr, batch, pst = B[0]['reqs'], B[0]['sr'], B[0]['batch'], B[0]['pst']
     part, hits, row_off, ex = B[0]['part'], B[0]['hits'], B[0]['row_off'], B[0]['ex']
@@ -129,6 +133,8 @@ def main_genome(args):
     if dist:
         dist.barrier()
     step_dev_ms = e0.elapsed_time(e1) / args.steps  # events on the stream around the K steps
+    if any(b['ex'].row_overflow() for b in B):  # (u32 rows: a cross-rank sum left 32 bits)
+        raise RuntimeError('a request row sum left 32 bits in the exchange: compact rows cannot hold it')
     # the dominant kernel (request_eval_kernel) alone: events around its launch
     # in each pass on its stream (sb_requests_time_eval), the same rotation
     for b in B:
@@ -176,7 +182,8 @@ def main_genome(args):
     st = {'cand_unique': agg['cand_unique'], 'cand_window': agg['cand_window'], 'cand_loaded': agg['cand_loaded']}
     # Roofline of the request pass, priced on the bytes it must move at least
     # once.  request_eval_kernel: per request its 32 B chain
-    # descriptor (ReqChain), 40 B row and 8 B row count; 16 B per candidate in
+    # descriptor (ReqChain), 16 B row and 4 B row count (the compact outputs
+    # the step writes); 16 B per candidate in
     # the union of the chain windows (the VcQ word: POS, END, VtHot word, AC;
     # each once however many overlapping requests read it; runs under a
     # common AN read nothing else); 4 B per hit staged.  Beside it the round-4
@@ -184,12 +191,12 @@ def main_genome(args):
     # wrote) and the SURVEY §8d contract: 32 B x unique records in the slice
     # windows + 8 B / hit.
     chains, hits_avg = agg['chains'], agg['hits']
-    comp = (32.0 + 40.0 + 8.0) * chains + 16.0 * st['cand_unique'] + 4.0 * hits_avg
+    comp = (32.0 + 16.0 + 4.0) * chains + 16.0 * st['cand_unique'] + 4.0 * hits_avg
     achieved = comp / (kern_ms * 1e-3) / 1e9 if kern_ms > 0 else 0.0
     comp_r04 = (32.0 + 40.0 + 8.0) * chains + 24.0 * st['cand_unique'] + 8.0 * hits_avg
     # the whole pass: the planning kernels (32 B packed request read, 32 B
-    # descriptor written per request), eval, tile scan, delivery (+ 8 B row
-    # offset per request; per hit its staged word read (4 B), its record id
+    # descriptor written per request), eval, tile scan, delivery (+ 4 B row
+    # count read and 4 B row offset written per request; per hit its staged word read (4 B), its record id
     # read (4 B), the 4 B hit written: u32 hits, sb_requests_set_compact)
     comp_pass = comp + 64.0 * agg['rows'] + 8.0 * chains + 12.0 * hits_avg
     achieved_pass = comp_pass / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
@@ -217,7 +224,7 @@ def main_genome(args):
                                f'{serial["hits_returned"]}')
         # full-size property: the step's rows + hit lists (one batch, resident),
         # the serial delivered pass and the pipelined chunks are bit-identical
-        step_digest = digest(part[:sr.n_rows].cpu().numpy(), [widen_hits(hits[:nhits].cpu().numpy())])
+        step_digest = digest(widen_rows(part[:sr.n_rows].cpu().numpy()), [widen_hits(hits[:nhits].cpu().numpy())])
         if not (step_digest == serial['digest'] == delivered['digest']):
             raise RuntimeError(f'delivery digests differ: step {step_digest}, serial {serial["digest"]}, '
                                f'pipelined {delivered["digest"]}')
@@ -243,14 +250,16 @@ def main_genome(args):
     tot_hits = sum(v[4] for v in allv)
     cpu = parity = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu, parity = cpu_baseline_and_parity(args, shape, reqs, ex.exchange(part, hits, row_off).cpu().numpy(),
-                                              widen_hits(hits.cpu().numpy()), row_off.cpu().numpy())
+        cpu, parity = cpu_baseline_and_parity(args, shape, reqs, widen_rows(ex.exchange(part, hits, row_off).cpu().numpy()),
+                                              widen_hits(hits.cpu().numpy()),
+                                              row_off.cpu().numpy().view(np.uint32).astype(np.int64))
         # the other batches of the rotation: a smaller sample each, parity only
         parity['other_batches'] = []
         for k, b in enumerate(B[1:], start=1):
             _, pk = cpu_baseline_and_parity(args, shape, b['reqs'],
-                                            b['ex'].exchange(b['part'], b['hits'], b['row_off']).cpu().numpy(),
-                                            widen_hits(b['hits'].cpu().numpy()), b['row_off'].cpu().numpy(), n_sample=4000,
+                                            widen_rows(b['ex'].exchange(b['part'], b['hits'], b['row_off']).cpu().numpy()),
+                                            widen_hits(b['hits'].cpu().numpy()),
+                                            b['row_off'].cpu().numpy().view(np.uint32).astype(np.int64), n_sample=4000,
                                             seed=7 + k, timed=False)
             pk['batch'] = k
             parity['other_batches'].append(pk)
@@ -280,7 +289,7 @@ def main_genome(args):
                 '(request_plan_kernel: each request\'s candidate range by a batched lower / upper bound of its '
                 'splitQuery window in the (segment, kind) index + its staging capacity; request_stage_scan_kernel), '
                 'request_eval_kernel (every request = one chain of its 10 kb slices, rows + hits staged per run), '
-                'request_tile_scan_kernel + request_deliver_kernel (row offsets, dense hit lists in request order, hits as u32 (record | ALT << 29)), '
+                'request_tile_scan_kernel + request_deliver_kernel (row offsets, dense hit lists in request order; compact outputs: rows as four u32 sums, u32 offsets and hits), '
                 'then the exchange (send/recv of straddling rows and hits)',
         'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
         'candidates_loaded_per_s': round(tot_cand * args.steps / elapsed, 1),
@@ -294,18 +303,19 @@ def main_genome(args):
                                'its launch in each of K rotating passes on its stream, averaged (rocprof per-kernel '
                                'averages: profiles/)',
                      'algorithmic_bytes_per_launch': r0[7],
-                     'pricing': 'bytes the launch must move at least once: 80 B/request (32 B chain descriptor + '
-                                '40 B row + 8 B row count) + 16 B per candidate in the union of the chain windows '
-                                '(POS, END, VtHot word, AC) + 4 B/hit staged',
+                     'pricing': 'bytes the launch must move at least once: 52 B/request (32 B chain descriptor + '
+                                '16 B row + 4 B row count: the compact outputs) + 16 B per candidate in the union of '
+                                'the chain windows (POS, END, VtHot word, AC) + 4 B/hit staged',
                      'r04_basis': {'bytes': r0[13], 'frac': round(r0[13] / (r0[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                    if r0[1] > 0 else None,
-                                   'note': 'the round-4 pricing (24 B per candidate, 8 B per hit staged: what the '
-                                           'round-4 kernel read and wrote) over this kernel time, for comparison'},
+                                   'note': 'the round-4 pricing (80 B per request, 24 B per candidate, 8 B per hit '
+                                           'staged: what the round-4 kernel read and wrote) over this kernel time, '
+                                           'for comparison'},
                      'pass': {'ms': round(r0[10], 4), 'achieved': round(r0[11], 1),
                               'frac': round(r0[11] / HBM_PEAK_GBS, 4), 'bytes': r0[12],
                               'note': 'planning (+64 B/request: packed request read, descriptor written) + eval + '
-                                      'tile scan + delivery (+8 B/request row offsets; +12 B/hit: staged word and '
-                                      'record id read, 4 B hit written)'},
+                                      'tile scan + delivery (+8 B/request: row count read, offset written; +12 B/hit: '
+                                      'staged word and record id read, 4 B hit written)'},
                      'candidates': {'unique': int(st['cand_unique']), 'in_windows': int(st['cand_window']),
                                     'loaded': int(st['cand_loaded'])},
                      'contract_bytes_per_launch': r0[8],

@@ -411,11 +411,17 @@ def widen_hits(hits32):
     return (h & np.uint64((1 << 29) - 1)) | ((h >> np.uint64(29)) << np.uint64(32))
 
 
+def widen_rows(rows32):
+    """Compact rows (sb_request_row32: u32 exists, n_variants, call_count,
+    all_alleles_count) as the wide [n, 5] int64 rows with a zero error count."""
+    rows32 = np.asarray(rows32).view(np.uint32).reshape(-1, 4)
+    rows = np.zeros((len(rows32), 5), dtype=np.int64)
+    rows[:, :4] = rows32
+    return rows
+
+
 def widen_compact(rows32, hits32, row_off32):
     """Compact request outputs (sb_requests_set_compact) in the wide form:
     (rows [n, 5] int64 with a zero error count, hits uint64 = record | ALT
     label << 32, row_off int64)."""
-    rows32 = np.asarray(rows32).view(np.uint32).reshape(-1, 4)
-    rows = np.zeros((len(rows32), 5), dtype=np.int64)
-    rows[:, :4] = rows32
-    return rows, widen_hits(hits32), np.asarray(row_off32).view(np.uint32).astype(np.int64)
+    return widen_rows(rows32), widen_hits(hits32), np.asarray(row_off32).view(np.uint32).astype(np.int64)

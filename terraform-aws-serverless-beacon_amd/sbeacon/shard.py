@@ -111,8 +111,14 @@ class ResultExchange:
     request's hits: its own slices' first, then each sender's in rank order
     (= position order: shards are cut in (contig, POS) order)."""
 
-    def __init__(self, dist, rank: int, world: int, row_lo: int, n_rows: int, owners, device):
+    def __init__(self, dist, rank: int, world: int, row_lo: int, n_rows: int, owners, device, row_fields: int = NF,
+                 row_dtype=None):
+        """``row_fields`` / ``row_dtype``: the rows' layout -- NF int64
+        fields (sb_request_partial), or 4 int32 fields holding u32 sums
+        (sb_request_row32, sb_requests_set_compact): received rows are then
+        added modulo 2^32 with a device-side carry check (row_overflow)."""
         import torch
+        row_dtype = torch.int64 if row_dtype is None else row_dtype
         self.dist, self.rank, self.world, self.device = dist, rank, world, device
         owners = np.asarray(owners, dtype=np.int64)
         assert len(owners) == n_rows and (np.diff(owners) >= 0).all()
@@ -152,8 +158,10 @@ class ResultExchange:
         # `part` in place and the owned rows are a view of it
         self.inplace = self.n_own == 0 or (row_lo + self.own_a <= self.own_lo and
                                            self.own_lo + self.n_own <= row_lo + self.own_b)
-        self.rows = None if self.inplace else torch.zeros((max(self.n_own, 1), NF), dtype=torch.int64, device=device)
-        self.recv_rows = [torch.zeros((n, NF), dtype=torch.int64, device=device) for _, _, n in self.recvs]
+        self.rows = None if self.inplace else torch.zeros((max(self.n_own, 1), row_fields), dtype=row_dtype,
+                                                          device=device)
+        self.recv_rows = [torch.zeros((n, row_fields), dtype=row_dtype, device=device) for _, _, n in self.recvs]
+        self._ovf = torch.zeros((), dtype=torch.bool, device=device) if row_dtype == torch.int32 else None
         self.recv_hits = [None] * len(self.recvs)
         self.recv_hits_n = {}
         self._my_hits = None
@@ -213,15 +221,31 @@ class ResultExchange:
         self._my_hits = (hits, row_off)
         if self.inplace:
             for k, (_, g, n) in enumerate(self.recvs):
-                part[g - self.row_lo:g - self.row_lo + n] += self.recv_rows[k]
+                self._add(part[g - self.row_lo:g - self.row_lo + n], self.recv_rows[k])
             return part[self.own_a:self.own_b] if self.n_own else part[:0]
         self.rows.zero_()
         if self.own_b > self.own_a:
             o = self.row_lo + self.own_a - self.own_lo
-            self.rows[o:o + self.own_b - self.own_a] += part[self.own_a:self.own_b]
+            self._add(self.rows[o:o + self.own_b - self.own_a], part[self.own_a:self.own_b])
         for k, (_, g, n) in enumerate(self.recvs):
-            self.rows[g - self.own_lo:g - self.own_lo + n] += self.recv_rows[k]
+            self._add(self.rows[g - self.own_lo:g - self.own_lo + n], self.recv_rows[k])
         return self.rows
+
+    def _add(self, dst, src):
+        """dst += src in place; u32 rows (int32 tensors) modulo 2^32, a sum
+        past 32 bits flagged on the device (row_overflow), no host sync."""
+        import torch
+        if self._ovf is None:
+            dst += src
+            return
+        t = (dst.to(torch.int64) & 0xffffffff) + (src.to(torch.int64) & 0xffffffff)
+        self._ovf |= (t >> 32).any()
+        dst.copy_(t.to(torch.int32))
+
+    def row_overflow(self) -> bool:
+        """True when a u32 row sum of some exchange left 32 bits (host sync):
+        those rows are not exact and the caller must not use them."""
+        return bool(self._ovf.item()) if self._ovf is not None else False
 
     def merge(self):
         """The owned requests' hit lists, merged densely on the device: each

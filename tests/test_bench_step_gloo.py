@@ -29,7 +29,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, tmp, mode, q):
+def _worker(rank, world, port, tmp, mode, compact, q):
     for p in (REPO, PKG, os.path.dirname(__file__)):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -53,33 +53,52 @@ def _worker(rank, world, port, tmp, mode, q):
             first = next(line for line in f if not line.startswith('#')).split('\t')[:2]
         assert _hit_map(os.path.join(tmp, 'full.vcf'))[(first[0], int(first[1]))][0] == base
 
+        from sbeacon.requests import widen_hits, widen_rows
+        dt = torch.int64
+        if compact:  # the bench step's narrow outputs: u32 rows, offsets and hits (record | ALT << 29)
+            rows = rows[:, :4].astype(np.uint32).view(np.int32)
+            h = hits.view(np.uint64)
+            hits = ((h & np.uint64(0xffffffff)) | ((h >> np.uint64(32)) << np.uint64(29))).astype(np.uint32).view(np.int32)
+            row_off = row_off.astype(np.int32)
+            dt = torch.int32
+
         def run(p, h, o):  # the oracle in place of the device pass
             p.copy_(torch.from_numpy(rows))
             h[:len(hits)].copy_(torch.from_numpy(hits))
             o.copy_(torch.from_numpy(row_off))
 
-        part = torch.zeros((max(sr.n_rows, 1), 5), dtype=torch.int64)
+        part = torch.zeros((max(sr.n_rows, 1), 4 if compact else 5), dtype=dt)
         # 'first': room for the received hits, so the merge writes in place;
         # 'rank0': none, so it writes new buffers (both merge paths run)
-        hbuf = torch.zeros(len(hits) + (4096 if mode == 'first' else 8), dtype=torch.int64)
-        obuf = torch.zeros(sr.n_rows + 1, dtype=torch.int64)
-        ex = ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, 'cpu')
+        hbuf = torch.zeros(len(hits) + (4096 if mode == 'first' else 8), dtype=dt)
+        obuf = torch.zeros(sr.n_rows + 1, dtype=dt)
+        ex = ResultExchange(dist, rank, world, sr.row_lo, sr.n_rows, owners, 'cpu', row_fields=4 if compact else 5,
+                            row_dtype=dt)
         step = make_step(run, ex, part, hbuf, obuf)
         for _ in range(3):  # later steps re-issue the cached P2P op list and the cached merge plan
             got = step()
         mh, mo = ex.merge()
         if ex.recv_hits_n and any(ex.recv_hits_n.values()):
             assert (mh.data_ptr() == hbuf.data_ptr()) == (mode == 'first'), (mode, rank)
-        mh, mo = mh.numpy().view(np.uint64), mo.numpy()
+        assert not ex.row_overflow()
+        if compact:
+            mh, mo = widen_hits(mh.numpy()), mo.numpy().astype(np.int64)
+            rows_got = widen_rows(got.numpy()[:ex.n_own])
+            hl = {k: [int(h) for h in widen_hits(np.array(v, dtype=np.uint64).astype(np.uint32))]
+                  for k, v in ex.hit_lists().items()}
+        else:
+            mh, mo = mh.numpy().view(np.uint64), mo.numpy()
+            rows_got = got.numpy()[:ex.n_own].copy()
+            hl = {k: [int(h) for h in v] for k, v in ex.hit_lists().items()}
         merged = {ex.own_lo + i: [int(h) for h in mh[mo[i]:mo[i + 1]]] for i in range(ex.n_own)}
-        q.put((rank, ex.own_lo, ex.n_own, got.numpy()[:ex.n_own].copy(),
-               {k: [int(h) for h in v] for k, v in ex.hit_lists().items()}, merged))
+        q.put((rank, ex.own_lo, ex.n_own, rows_got, hl, merged))
     finally:
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize('compact', [False, True])
 @pytest.mark.parametrize('mode', ['first', 'rank0'])
-def test_bench_step_world2_matches_unsharded_oracle(mode):
+def test_bench_step_world2_matches_unsharded_oracle(mode, compact):
     from oracle.oracle import OracleVcf
     from sbeacon.genome import shard_slices, slice_payloads
     world = 2
@@ -93,7 +112,7 @@ def test_bench_step_world2_matches_unsharded_oracle(mode):
         ctx = mp.get_context('spawn')
         q = ctx.Queue()
         port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, tmp, mode, q)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, port, tmp, mode, compact, q)) for r in range(world)]
         for p in procs:
             p.start()
         got = [q.get(timeout=300) for _ in range(world)]
