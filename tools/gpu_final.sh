@@ -21,7 +21,7 @@ step bench 600 python3 -u $R/bench.py --steps 20 --warmup 5
 step paths 600 python3 -u $R/bench_paths.py --datasets 50
 cd /tmp
 step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 -u $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline
-step save 300 python3 -u $R/tools/req_tune.py --save /tmp/st --rounds 3
+step save 300 python3 -u $R/tools/req_tune.py --save /tmp/st --rounds 3 --digest
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o p -- python3 -u $R/tools/req_tune.py --open /tmp/st --rounds 2
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o p -- python3 -u $R/tools/req_tune.py --open /tmp/st --rounds 2
 step traffic 60 python3 $R/tools/pmc_traffic.py $O/pmc_fetch $O/pmc_write --out $O/traffic_genome.json --records 85000000 --requests 1000000 --kernel request_eval_kernel --batches 4

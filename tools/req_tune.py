@@ -26,6 +26,8 @@ def main():
     ap.add_argument('--open', default=None)
     ap.add_argument('--genotypes', action='store_true')
     ap.add_argument('--digest', action='store_true', help='blake2b of every batch\'s rows + hits (A/B parity)')
+    ap.add_argument('--wide', action='store_true', help='wide outputs (int64 rows, offsets, hits) instead of the '
+                                                         'compact ones the bench step writes')
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -50,9 +52,15 @@ def main():
         b.set_stream(stream)
         b.set_replan(True)
         n = sr.n_rows
-        B.append((b, torch.zeros((max(n, 1), 5), dtype=torch.int64, device=dev),
-                  torch.zeros(int(b.stats()['hits']) + 1, dtype=torch.int64, device=dev),
-                  torch.zeros(n + 1, dtype=torch.int64, device=dev)))
+        if args.wide:
+            B.append((b, torch.zeros((max(n, 1), 5), dtype=torch.int64, device=dev),
+                      torch.zeros(int(b.stats()['hits']) + 1, dtype=torch.int64, device=dev),
+                      torch.zeros(n + 1, dtype=torch.int64, device=dev)))
+        else:  # the bench step's form (sb_requests_set_compact)
+            b.set_compact(True)
+            B.append((b, torch.zeros((max(n, 1), 4), dtype=torch.int32, device=dev),
+                      torch.zeros(int(b.stats()['hits']) + 1, dtype=torch.int32, device=dev),
+                      torch.zeros(n + 1, dtype=torch.int32, device=dev)))
 
     def run(b, p, h, o):
         b.run(p.data_ptr(), h.data_ptr(), o.data_ptr(), 0)
@@ -83,13 +91,20 @@ def main():
     out = {'lib': os.environ.get('SBEACON_LIB', 'in-tree'), 'records': args.records, 'store_s': round(t_store, 2),
            'eval_ms_median': round(ev[len(ev) // 2], 4), 'eval_ms_min': round(ev[0], 4),
            'pass_ms_median': round(pas[len(pas) // 2], 4), 'pass_ms_min': round(pas[0], 4)}
-    if args.digest:
+    if args.digest:  # over the wide form (compact outputs widened): one digest for both forms
         import hashlib
+        from sbeacon.requests import widen_compact
         h = hashlib.blake2b(digest_size=16)
         for b, p, hh, o in B:
-            ro = o.cpu().numpy()
-            h.update(p[:len(ro) - 1].cpu().numpy().tobytes())
-            h.update(hh[:int(ro[-1])].cpu().numpy().tobytes())
+            if args.wide:
+                ro = o.cpu().numpy()
+                rows, hits = p[:len(ro) - 1].cpu().numpy(), hh[:int(ro[-1])].cpu().numpy()
+            else:
+                ro32 = o.cpu().numpy().view(np.uint32)
+                rows, hits, ro = widen_compact(p[:len(ro32) - 1].cpu().numpy(), hh[:int(ro32[-1])].cpu().numpy(), ro32)
+                hits = hits.view(np.int64)
+            h.update(rows.tobytes())
+            h.update(hits.tobytes())
             h.update(ro.tobytes())
         out['digest'] = h.hexdigest()
     print(json.dumps(out), flush=True)
