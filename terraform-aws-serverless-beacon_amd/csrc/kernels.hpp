@@ -118,10 +118,14 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
 uint32_t req_run_max();
 // Request planning on the device: rows in runs of kRunRows (n_runs =
 // ceil(n / 64)); chains gets kReqRun ReqChain slots per run, runs the RowRuns
-// with staging offsets, rcap one word per run; counters (3 words, zeroed by
-// the caller) = chain rows, their slices, the staging total.
+// with staging offsets, rcap one word per run; counters (4 words, zeroed by
+// the caller) = chain rows, their slices, the staging total, the largest run
+// capacity.  stride != 0 (a re-planning pass of a batch laid out at a fixed
+// stride): run w stages at w x stride, no staging scan, *err bit 0 when a
+// run would not fit.
 void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,
-                         unsigned long long *rcap, unsigned long long *counters, hipStream_t s);
+                         unsigned long long *rcap, unsigned long long *counters, hipStream_t s, uint64_t stride = 0,
+                         unsigned int *err = nullptr);
 size_t request_plan_words(uint32_t n_runs);  // planning scratch: per-run and per-workgroup totals + counters
 uint32_t request_tiles(uint32_t n_runs);
 size_t request_tstatus_words(uint32_t n_runs);  // tile offsets + eval workgroup totals

@@ -2446,7 +2446,8 @@ __global__ __launch_bounds__(kBlock) void request_plan_kernel(DStore st, const R
                                                               uint32_t n_runs, ReqChain *__restrict__ chains,
                                                               RowRun *__restrict__ runs,
                                                               unsigned long long *__restrict__ rcap,
-                                                              unsigned long long *__restrict__ gcap) {
+                                                              unsigned long long *__restrict__ gcap, uint64_t stride,
+                                                              unsigned int *__restrict__ err) {
     __shared__ ulonglong2 wtot[kWavesPerBlock];
     const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     const uint32_t ul = static_cast<uint32_t>(lane_id());
@@ -2493,7 +2494,10 @@ __global__ __launch_bounds__(kBlock) void request_plan_kernel(DStore st, const R
                            (anc ? kRunAnCommon | (a0 - 1u) << kRunAnShift : 0u);
     if (ul == 0) {  // (the batch's chain / slice totals: request_stage_scan_kernel -- one counter
                     // atomically bumped by every wave serialised the launch, ~350 us for 15.6 k runs)
-        runs[w] = RowRun{w * kRunRows, min(w * kRunRows + kRunRows, n), 0u, nslots, 0ull, slsum, flags};
+        // staging: at a fixed stride per run when the batch has one (a
+        // re-planning pass: no scan), else request_stage_scan_kernel's offset
+        runs[w] = RowRun{w * kRunRows, min(w * kRunRows + kRunRows, n), 0u, nslots, stride * w, slsum, flags};
+        if (stride && capsum > stride) atomicOr(err, 1u);  // (never: the prepare sized the stride on these requests)
         const unsigned long long cw = static_cast<unsigned long long>(slsum) << 32 | nslots;
         rcap[2 * w] = capsum;
         rcap[2 * w + 1] = cw;
@@ -2611,6 +2615,11 @@ __global__ __launch_bounds__(kStageTile) void request_stage_scan_kernel(RowRun *
     const ulonglong2 me = i < n_runs ? rc2[i] : ulonglong2{0ull, 0ull};
     nch += me.y & 0xffffffffull;
     nsl += me.y >> 32;
+    {  // the largest run capacity (counters[3]: sizes a fixed-stride staging layout)
+        uint32_t mx = static_cast<uint32_t>(min(me.x, 0xffffffffull));
+        for (uint32_t d = 1; d < kWave; d <<= 1) mx = max(mx, static_cast<uint32_t>(__shfl_xor(static_cast<int>(mx), d)));
+        if (lane_id() == 0 && mx) atomicMax(reinterpret_cast<unsigned int *>(counters + 3), mx);
+    }
     pre = block_sum_u64(pre, wsum);
     // the tile's exclusive scan
     const uint64_t incl = incl_sum_u64(me.x);
@@ -4008,15 +4017,17 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
 }
 
 void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,
-                         unsigned long long *rcap, unsigned long long *counters, hipStream_t s) {
+                         unsigned long long *rcap, unsigned long long *counters, hipStream_t s, uint64_t stride,
+                         unsigned int *err) {
     const uint32_t n_runs = (n + kRunRows - 1) / kRunRows;
     if (!n_runs) return;
     // per plan workgroup totals after the counters (requests.cpp sizes the buffer: request_plan_words)
     unsigned long long *gcap = counters + 4;
     hipLaunchKernelGGL(request_plan_kernel, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, in, n, n_runs, chains,
-                       runs, rcap, gcap);
-    hipLaunchKernelGGL(request_stage_scan_kernel, dim3((n_runs + kStageTile - 1) / kStageTile), dim3(kStageTile), 0, s,
-                       runs, rcap, gcap, n_runs, counters);
+                       runs, rcap, gcap, stride, err);
+    if (!stride)  // (a fixed-stride batch re-planning: the offsets are w x stride, the totals known)
+        hipLaunchKernelGGL(request_stage_scan_kernel, dim3((n_runs + kStageTile - 1) / kStageTile), dim3(kStageTile),
+                           0, s, runs, rcap, gcap, n_runs, counters);
 }
 
 // planning scratch (u64 words): per run {capacity, slices | chains}, the

@@ -379,11 +379,23 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
                         cnt, st);
     HIP_OK(hipGetLastError());
     unsigned long long *hc = reinterpret_cast<unsigned long long *>(static_cast<char *>(pin.p) + cnt_at);
-    HIP_OK(hipMemcpyAsync(hc, cnt, 24, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(hc, cnt, 32, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));  // uploads, planning and the counters: one wait
     R->n_chains = hc[0];
     R->n_chain_slices = hc[1];
     const uint64_t stage_total = hc[2];
+    // staging at a fixed stride per run (the largest run capacity) when that
+    // costs at most twice the packed size or 64 MiB: a re-planning pass then
+    // needs no staging scan (w x stride) -- HBM traded for a launch
+    uint64_t stage_alloc = stage_total;
+    {
+        const uint64_t stride = std::max<uint64_t>((hc[3] + 15) & ~uint64_t(15), 16);
+        const uint64_t fixed = stride * n_runs;
+        if (fixed <= std::max<uint64_t>(2 * stage_total, (64ull << 20) / 4)) {
+            R->stage_stride = stride;
+            stage_alloc = fixed;  // (the packed offsets of this first plan fit inside it)
+        }
+    }
     tick("plan");
     P.put_pinned(pin);
     R->din = std::move(din);  // kept: sb_requests_set_replan re-plans from them
@@ -392,7 +404,7 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     R->cap = B.cap_total + stage_total;
     R->status = P.get_dev(size_t(n_runs) * 8);
     R->tstatus = P.get_dev(request_tstatus_words(n_runs) * 8);
-    R->stage = P.get_dev(stage_total * 4);
+    R->stage = P.get_dev(stage_alloc * 4);
     R->row_src = P.get_dev(R->slices ? n * 8 : 0);
     upload_slice_part(B, *R, seg, n, st);  // (synchronises when there is a per-slice part)
     tick("upload");
@@ -694,7 +706,8 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
     if (R.replan) {  // the planning kernels again, from the resident packed requests (same descriptors, same sizes)
         launch_request_plan(s.d, R.din.as<ReqIn>(), R.n_in, R.dchains.as<ReqChain>(),
                             reinterpret_cast<RowRun *>(R.dchains.as<char>() + R.runs_at), R.rcap.as<unsigned long long>(),
-                            reinterpret_cast<unsigned long long *>(R.rcap.as<char>() + size_t(R.n_runs) * 16), st);
+                            reinterpret_cast<unsigned long long *>(R.rcap.as<char>() + size_t(R.n_runs) * 16), st,
+                            R.stage_stride, R.err.as<unsigned int>());
         HIP_OK(hipGetLastError());
     }
     DStore d = s.d;
