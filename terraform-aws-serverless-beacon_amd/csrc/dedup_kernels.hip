@@ -674,8 +674,12 @@ __global__ __launch_bounds__(kThreads) void bucket_dedupe_kernel(const uint64_t 
 // 7 workgroups per CU (4,096 slots and 128 confirmations: 6, and 4 % slower,
 // profiles/r05_dedup/slots.log); the set's load is <= 0.73 (1,024 distinct
 // identities in a config-4 window: ~0.36)
+#ifndef SBEACON_WIN_THREADS
+#define SBEACON_WIN_THREADS 256  // threads of window_dedupe_kernel (64: one wave per window, no cross-wave barriers)
+#endif
+constexpr uint32_t kWT = SBEACON_WIN_THREADS;
 #ifndef SBEACON_WIN_SLOTS
-#define SBEACON_WIN_SLOTS 2816
+#define SBEACON_WIN_SLOTS (kWinCap / 8 * 11)
 #endif
 constexpr uint32_t kWSlots = SBEACON_WIN_SLOTS;  // 16-bit winners
 constexpr uint32_t kWRounds = 24;    // unresolved after that: the sorted path
@@ -683,8 +687,8 @@ constexpr uint32_t kWRounds = 24;    // unresolved after that: the sorted path
 #define SBEACON_WIN_CONFIRM 32
 #endif
 constexpr uint32_t kWConfirm = SBEACON_WIN_CONFIRM;  // hashed duplicate pairs confirmed per window
-constexpr uint32_t kWPer = kWinCap / kThreads;
-static_assert(kWPer * kThreads == kWinCap, "window keys per thread");
+constexpr uint32_t kWPer = kWinCap / kWT;
+static_assert(kWPer * kWT == kWinCap && kWT % 64 == 0, "window keys per thread");
 static_assert(kWinCap <= kWSlots && kWinCap <= 65536, "window slot load / 16-bit winners");
 static_assert(kWinPieces == 64, "one wave scans the pieces");
 
@@ -863,7 +867,18 @@ __global__ __launch_bounds__(kThreads) void dedup_plan_kernel(KStore ks, const K
 #ifndef SBEACON_WIN_WAVES
 #define SBEACON_WIN_WAVES 7
 #endif
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACON_WIN_WAVES, 8))) void window_dedupe_kernel(KStore ks, const uint32_t *__restrict__ rec, uint32_t rec_words,
+// a barrier over the window's workgroup (a single wave: its LDS operations
+// are ordered by the fence alone)
+__device__ __forceinline__ void win_sync() {
+    if constexpr (kWT == 64) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(kWT) __attribute__((amdgpu_waves_per_eu(SBEACON_WIN_WAVES, 8))) void window_dedupe_kernel(KStore ks, const uint32_t *__restrict__ rec, uint32_t rec_words,
                                                                  unsigned long long *counts, uint2 *list,
                                                                  uint32_t *n_list, uint32_t cap, uint32_t *overflow,
                                                                  uint32_t *wfresh, uint32_t dbg) {
@@ -892,7 +907,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
             s_pend = 0;
         }
     }
-    __syncthreads();
+    win_sync();
     const uint32_t np = W.nruns, total = s_pre[np];
     if (total > kWinCap) {  // a pile-up past the window (the host recounts on the sorted path)
         if (threadIdx.x == 0) {
@@ -901,10 +916,10 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
         }
         return;
     }
-    // every key's 8-byte class word (key u = u * kThreads + tid): POS, the
+    // every key's 8-byte class word (key u = u * kWT + tid): POS, the
     // tail's id, displaced flag -- the 8-byte hash and 16-byte body only for
     // the few keys without an id.  The lane's piece only moves forward with
-    // u (f grows by kThreads): a short catch-up walk per key, the pieces kept
+    // u (f grows by kWT): a short catch-up walk per key, the pieces kept
     // 6 bits each for later
     uint32_t wlo[kWPer], whi[kWPer];  // the class words' halves
     uint32_t okm = 0;
@@ -913,7 +928,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
         uint32_t pc = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u) {
-            const uint32_t f = u * kThreads + threadIdx.x;
+            const uint32_t f = u * kWT + threadIdx.x;
             wlo[u] = 0;
             whi[u] = 0;
             if (f < total) {
@@ -934,7 +949,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
         if (threadIdx.x == 0) wfresh[blockIdx.x] = 0;
         return;
     }
-    auto kid_of = [&](uint32_t u) { return u * kThreads + threadIdx.x + s_base[static_cast<uint32_t>(pk >> (6 * u)) & 63u]; };
+    auto kid_of = [&](uint32_t u) { return u * kWT + threadIdx.x + s_base[static_cast<uint32_t>(pk >> (6 * u)) & 63u]; };
     // classes: identified (the tail has an id), hashed (no id), deferred
     // (displaced keys that may have a copy at a larger POS of the job).  A
     // displaced key with no such copy meets its equal strings at its own POS
@@ -959,12 +974,12 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
         if ((hm >> u) & 1u) idv[u] = ks.hash[kid_of(u)] & ~(1ull << 63);
 #pragma unroll
     for (uint32_t u = 0; u < kWPer; ++u)
-        if (((em | hm) >> u) & 1u) s_id[u * kThreads + threadIdx.x] = idv[u];
+        if (((em | hm) >> u) & 1u) s_id[u * kWT + threadIdx.x] = idv[u];
     // deferred keys: one reservation per workgroup in the global list
     const uint32_t nd = static_cast<uint32_t>(__popc(dm));
     uint32_t dofs = 0;
     if (nd) dofs = atomicAdd(&s_def, nd);
-    __syncthreads();
+    win_sync();
     if (threadIdx.x == 0 && s_def) {
         const uint32_t at = atomicAdd(n_list, s_def);
         s_def0 = at;
@@ -983,14 +998,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
                 const uint32_t m = (static_cast<uint32_t>(v) ^ static_cast<uint32_t>(v >> 32) * 0x85EBCA6Bu ^
                                     round * 0xC2B2AE35u) * 0x9E3779B1u;
                 sl[u] = static_cast<uint32_t>((static_cast<uint64_t>(m ^ (m >> 15)) * kWSlots) >> 32);
-                s_win[sl[u]] = static_cast<uint16_t>(u * kThreads + threadIdx.x);
+                s_win[sl[u]] = static_cast<uint16_t>(u * kWT + threadIdx.x);
             }
-        __syncthreads();
+        win_sync();
         // read the winners back
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u)
             if ((pend >> u) & 1u) {
-                const uint32_t f = u * kThreads + threadIdx.x;
+                const uint32_t f = u * kWT + threadIdx.x;
                 const uint32_t w = s_win[sl[u]];
                 const uint64_t v = idv[u];
                 // resolved: the winner counts, an equal identity is its
@@ -1008,7 +1023,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
         // any key left?  (round + 1 in one LDS word: no earlier round's
         // value reads as this one's)
         if (pend) s_pend = round + 1;
-        __syncthreads();  // also orders this round's reads before the next writes
+        win_sync();  // also orders this round's reads before the next writes
         if (s_pend != round + 1) break;
         if (round + 1 == kWRounds && threadIdx.x == 0) atomicOr(overflow, 1u);  // unresolved: the sorted path
     }
@@ -1018,7 +1033,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
     {
         const uint32_t nc = s_nconf;
         if (nc > kWConfirm && threadIdx.x == 0) bad = true;
-        for (uint32_t i = threadIdx.x; i < min(nc, kWConfirm); i += kThreads) {
+        for (uint32_t i = threadIdx.x; i < min(nc, kWConfirm); i += kWT) {
             const uint32_t w = s_conf[i] & 0xffffu, f = s_conf[i] >> 16;
             uint32_t q = 0, r = 0;
             while (q + 1 < np && s_pre[q + 1] <= w) ++q;
@@ -1036,14 +1051,14 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(SBEACO
         for (uint32_t u = 0; u < kWPer; ++u)
             if ((dm >> u) & 1u) {
                 const uint32_t pc = static_cast<uint32_t>(pk >> (6 * u)) & 63u;
-                if (at < cap) list[at] = uint2{u * kThreads + threadIdx.x + s_base[pc], W.run_lo + pc};
+                if (at < cap) list[at] = uint2{u * kWT + threadIdx.x + s_base[pc], W.run_lo + pc};
                 ++at;
             }
     }
     if (bad) atomicOr(overflow, 1u);
     const uint32_t fw = wave_sum_u32(fresh);
     if (lane == 0 && fw) atomicAdd(&s_fresh, fw);
-    __syncthreads();
+    win_sync();
     // the window's count, folded per job by window_fold_kernel: one device
     // atomic per window on the jobs' few counter lines (73 k windows for 50
     // jobs) serialised in L2
@@ -1149,7 +1164,7 @@ void launch_window_dedupe(const KStore &ks, const KJob *jobs, uint32_t nj, uint3
     if (!nw) return;
     const uint32_t dbg = static_cast<uint32_t>(config().dedup_win_dbg);  // timing ablations (never set by the benches)
     dedup_plan_kernel<<<(nw + kThreads - 1) / kThreads, kThreads, 0, s>>>(ks, jobs, nj, runs, nw, rec, rec_words);
-    window_dedupe_kernel<<<nw, kThreads, 0, s>>>(ks, rec, rec_words, counts, list, n_list, cap, overflow, wfresh, dbg);
+    window_dedupe_kernel<<<nw, kWT, 0, s>>>(ks, rec, rec_words, counts, list, n_list, cap, overflow, wfresh, dbg);
     window_fold_kernel<<<(nj * 64 + kThreads - 1) / kThreads, kThreads, 0, s>>>(jobs, nj, runs, wfresh, counts);
     deferred_dedupe_kernel<<<1024, kThreads, 0, s>>>(ks, runs, list, n_list, cap, counts);
 }

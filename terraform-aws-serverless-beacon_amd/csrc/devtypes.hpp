@@ -601,8 +601,11 @@ struct KRun {  // one POS-sorted key run of a job + its segment's POS index
     uint32_t run_lo, nruns;  // the job's runs [run_lo, run_lo + nruns)
     uint32_t pad[2];
 };
-inline constexpr uint32_t kWinCap = 2048;    // keys per window (LDS sets sized for it)
-inline constexpr uint32_t kWinTarget = 1536; // keys a window is planned for (runs of a job differ in density)
+#ifndef SBEACON_WIN_CAP
+#define SBEACON_WIN_CAP 2048
+#endif
+inline constexpr uint32_t kWinCap = SBEACON_WIN_CAP;         // keys per window (LDS sets sized for it)
+inline constexpr uint32_t kWinTarget = kWinCap / 4 * 3;      // keys a window is planned for (runs of a job differ in density)
 inline constexpr uint32_t kWinPieces = 64;   // pieces (= runs) per window
 inline constexpr uint32_t kWinSpanBits = 26; // p1 - p0 < 2^26 - 1: exact words fit 32 bits
 
