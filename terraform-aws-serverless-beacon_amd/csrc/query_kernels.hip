@@ -1977,6 +1977,23 @@ __device__ __forceinline__ uint32_t incl_max_u32(uint32_t v) {
     v = max(v, dpp32<0x143, 0xc>(v));
     return v;
 }
+// the two scans of a chunk side by side: inclusive max of m, inclusive sum of v
+__device__ __forceinline__ void incl_max_sum_u32(uint32_t m, uint32_t v, uint32_t &mo, uint32_t &vo) {
+    m = max(m, dpp32<0x111>(m));
+    v += dpp32<0x111>(v);
+    m = max(m, dpp32<0x112>(m));
+    v += dpp32<0x112>(v);
+    m = max(m, dpp32<0x114>(m));
+    v += dpp32<0x114>(v);
+    m = max(m, dpp32<0x118>(m));
+    v += dpp32<0x118>(v);
+    m = max(m, dpp32<0x142, 0xa>(m));
+    v += dpp32<0x142, 0xa>(v);
+    m = max(m, dpp32<0x143, 0xc>(m));
+    v += dpp32<0x143, 0xc>(v);
+    mo = m;
+    vo = v;
+}
 __device__ __forceinline__ uint64_t incl_sum_u64(uint64_t v) {
     v += static_cast<uint64_t>(dpp_i64<0x111, 0xf, 0xf>(static_cast<int64_t>(v)));
     v += static_cast<uint64_t>(dpp_i64<0x112, 0xf, 0xf>(static_cast<int64_t>(v)));
@@ -2263,8 +2280,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         const uint32_t key1 = pos ? (k << 20 | (x.pos - first) / kReqWidth) + 1u : 0u;
 #ifdef SBEACON_ABL_KEY  // timing ablation only: no slice-key scan
         const uint32_t mx = key1;
+        const uint32_t scc_anc = ANC ? incl_sum_u32(static_cast<uint32_t>(cv)) : 0u;
 #else
-        const uint32_t mx = incl_max_u32(key1);
+        // (under a common AN the call-count scan runs beside the slice-key
+        // scan: two independent DPP chains interleave, no wait states)
+        uint32_t mx, scc_anc = 0;
+        if constexpr (ANC) {
+            incl_max_sum_u32(key1, static_cast<uint32_t>(cv), mx, scc_anc);
+        } else {
+            mx = incl_max_u32(key1);
+        }
 #endif
         const uint32_t prev = max(wave_shr1(mx), carry);
         const bool isnew = pos && key1 != prev;
@@ -2294,7 +2319,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         acc_ex += (dn >> 10) & 0x7fu;
         acc_hr += dn >> 17;
         if constexpr (ANC) {  // (a common AN implies narrow) the chunk's sums fit 32 bits; AN sums from hit records
-            const uint32_t scc = incl_sum_u32(static_cast<uint32_t>(cv));
+            const uint32_t scc = scc_anc;
             const uint32_t pc = bperm(scc, e);
             const uint32_t qc = wave_shr1(pc);
             if (inter) acc_cc += pc - (opens ? 0u : qc);
