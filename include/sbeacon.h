@@ -543,8 +543,10 @@ typedef struct {
  * dev_row_off[n + 1] as uint32, and each hit as uint32 (record + rec_base) |
  * ALT label << 29; SB_EINVAL for a batch with a per-slice part.
  * SB_COMPACT_HITS: wide rows and offsets, uint32 hits as above (any batch).
- * Either: SB_EINVAL at run when record numbers reach 2^29; a count or offset
- * past 32 bits fails the pass at sb_batch_sync (SB_EINTERNAL).  0: wide. */
+ * Either: SB_EINVAL at run when record numbers reach 2^29; at sb_batch_sync,
+ * SB_EINVAL when a count or offset passes 32 bits (SB_COMPACT_ALL) or a
+ * per-slice hit's ALT index passes 7 (the labels 3 bits hold); the batch is
+ * then answered wide.  0: wide. */
 #define SB_COMPACT_ALL 1
 #define SB_COMPACT_HITS 2
 int sb_requests_set_compact(sb_batch *b, int on);

@@ -1252,9 +1252,16 @@ void sync(sb_batch &B) {
         B.req->last_eval_ms = sum / static_cast<double>(B.req->eval_used);
         B.req->eval_used = 0;
     }
-    if (chk && *static_cast<volatile uint32_t *>(B.req->err_h.p))
+    const uint32_t e = chk ? *static_cast<volatile uint32_t *>(B.req->err_h.p) : 0u;
+    if (e & 1u)
         throw Error(SB_EINTERNAL, "request_eval_kernel: the per-chain sums of a pass failed their invariants "
                                   "(chain counts vs the wave's staged hits / exists-slices)");
+    if (e & 2u)
+        throw Error(SB_EINVAL, "compact request output (SB_COMPACT_ALL): a row's counts or the hit offsets "
+                               "pass 32 bits (or a chain needs wide sums); answer this batch with wide rows");
+    if (e & 4u)
+        throw Error(SB_EINVAL, "compact request hits: a per-slice hit has an ALT index past 7, which "
+                               "record | ALT << 29 cannot hold; answer this batch with wide hits");
 }
 
 // each query's hit-region offset: chained slices' hits are dense per chain,

@@ -36,6 +36,7 @@ struct Config {
     int dedup_bucket_dbg = 0;     // SBEACON_DEDUP_BUCKET_DBG: bucket-kernel timing ablations
     int dedup_win_dbg = 0;        // SBEACON_DEDUP_WIN_DBG: window-kernel timing ablations
     bool req_inject = false;      // SBEACON_REQ_INJECT=1 (tests): one wrong per-chain sum, so the pass's invariants fire
+    bool req_index_stage = false; // SBEACON_REQ_INDEX_STAGE=1 (tests): stage candidate indices, as stores past 2^29 records do
     int pack_dbg = 0;             // SBEACON_PACK_DBG: chain-kernel ablations (SBEACON_ABLATION builds)
 };
 
@@ -70,6 +71,7 @@ inline Config config() {
     c.dedup_bucket_dbg = num("SBEACON_DEDUP_BUCKET_DBG", 0);
     c.dedup_win_dbg = num("SBEACON_DEDUP_WIN_DBG", 0);
     c.req_inject = one("SBEACON_REQ_INJECT");
+    c.req_index_stage = one("SBEACON_REQ_INDEX_STAGE");
     c.pack_dbg = num("SBEACON_PACK_DBG", 0);
     return c;
 }

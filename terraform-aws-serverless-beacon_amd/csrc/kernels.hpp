@@ -113,7 +113,8 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
-                         int compact, hipStream_t s, hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr);
+                         int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0 = nullptr,
+                         hipEvent_t ev1 = nullptr);
 // chain slots per run (kReqRun)
 uint32_t req_run_max();
 // Request planning on the device: rows in runs of kRunRows (n_runs =

@@ -2022,7 +2022,7 @@ struct ReqLds {
 struct ReqChunk {
     VcQ q;       // the candidate's POS, END, VtHot word and ALT0 AC: one 16-byte load
     int32_t an;  // its record's AN (loaded only by runs without a common AN)
-    uint32_t i;  // candidate index: staged as the hit (request_deliver_kernel maps it to the record)
+    uint32_t i;  // staged as the hit: the candidate's record (REC), else its index (the deliver maps it)
     uint32_t k;  // the lane's chain
 };
 
@@ -2031,7 +2031,11 @@ static_assert(offsetof(ReqLds, b) == sizeof(uint4) * kReqRun && offsetof(ReqLds,
               "a, b, wch are one block that holds a run's rows");
 // COMPACT (sb_requests_set_compact): rows as RowC (16 B), row counts /
 // offsets as u32; only batches without a per-slice part (sres == nullptr)
-template <bool LDS_LUT, bool COMPACT>
+// REC: hits are staged as their record numbers (the store's records fit 29
+// bits): the record id is loaded with the candidate word, coalesced, and
+// request_deliver_kernel copies without a per-hit gather; else the
+// candidate index is staged and the deliver maps it (vc_idx)
+template <bool LDS_LUT, bool COMPACT, bool REC>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_REQ_WAVES, SBEACON_REQ_WAVES))) void request_eval_kernel(
     DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
     unsigned long long *__restrict__ status, const QRes *__restrict__ sres, void *__restrict__ rows_out,
@@ -2161,7 +2165,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         q.q = st.vc_q[i];
         if constexpr (ANC) q.an = 0;
         else q.an = st.vc_word[i].an;
-        q.i = i;
+        if constexpr (REC) q.i = st.vc_idx[i];
+        else q.i = i;
         return q;
     };
     auto eval = [&](const ReqChunk &q, uint32_t c) {
@@ -2175,6 +2180,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         // the pipeline
         asm volatile("" ::"v"(x.pos), "v"(x.end), "v"(x.w), "v"(x.ac0));
         if constexpr (!ANC) asm volatile("" ::"v"(q.an));
+        if constexpr (REC) asm volatile("" ::"v"(q.i));
         const uint32_t base = kWave * c;
         const uint32_t g = base + ul;
         const uint4 A = L.a[k], Bw = L.b[k];
@@ -2225,7 +2231,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
             uint64_t hm = h0;
             uint32_t x0 = 0;
             if (xl) {
-                x0 = st.x_lo[st.vc_idx[q.i]];
+                x0 = st.x_lo[REC ? q.i : st.vc_idx[q.i]];
                 // consumed here: no load left pending on this register past
                 // the branch (a later writer of the register would wait for
                 // vmcnt(0) on every path)
@@ -2405,7 +2411,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         const bool slow = (L.slow[ul >> 5] >> (ul & 31u)) & 1u;  // never for prepared chains
         const uint64_t an_sum = anc ? static_cast<uint64_t>(acc_hr) * an_c : acc_an;
         if constexpr (COMPACT) {
-            // (counts past 32 bits or a slow chain: the batch fails at sync, SB_EINTERNAL)
+            // (counts past 32 bits or a slow chain: the batch fails at sync, SB_EINVAL)
             if (slow || acc_cc > 0xffffffffull || an_sum > 0xffffffffull) atomicOr(err, 2u);
             static_cast<RowC *>(rows_out)[rowk] = RowC{acc_ex, acc_nv, static_cast<uint32_t>(acc_cc),
                                                        static_cast<uint32_t>(an_sum)};
@@ -2725,7 +2731,7 @@ __global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned 
 // COMPACT: row counts / offsets u32, hits u32 = (record + rec_base) | label
 // << kStageAltShift (the host checks records + rec_base < 2^29; an offset
 // past 32 bits fails the batch at sync)
-template <bool ROWC, bool HITC>
+template <bool ROWC, bool HITC, bool REC>
 __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const RowRun *__restrict__ runs, uint32_t n_runs, const unsigned long long *__restrict__ status,
     const unsigned long long *__restrict__ toff, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
@@ -2740,11 +2746,11 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     // a staged hit (candidate | ALT label << kStageAltShift) as the output's
     // (record + rec_base) | label << kHitAltShift
     auto hit_of = [&](uint32_t v) -> Hit {
+        const uint32_t r = REC ? (v & kStageCandMask) : vc_idx[v & kStageCandMask];  // the staged record
         if constexpr (HITC)
-            return (vc_idx[v & kStageCandMask] + static_cast<uint32_t>(rec_base)) | (v & ~kStageCandMask);
+            return (r + static_cast<uint32_t>(rec_base)) | (v & ~kStageCandMask);
         else
-            return (static_cast<uint64_t>(vc_idx[v & kStageCandMask]) + rec_base) |
-                   static_cast<uint64_t>(v >> kStageAltShift) << kHitAltShift;
+            return (static_cast<uint64_t>(r) + rec_base) | static_cast<uint64_t>(v >> kStageAltShift) << kHitAltShift;
     };
     const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
     if (w >= n_runs) return;
@@ -2816,14 +2822,17 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
                 const QRes rq = sres[q];
                 if (rq.error || sherr[q]) continue;
                 const uint64_t src = shoff[q];
+                bool wide_alt = false;  // HITC: an ALT label the u32 hit cannot hold (> VT_MAX_NX)
                 for (uint32_t k = ul; k < rq.n_hits; k += kWave) {
                     const uint64_t h = shits[src + k];  // record | ALT << kHitAltShift
-                    if constexpr (HITC)
+                    if constexpr (HITC) {
+                        wide_alt |= (h >> kHitAltShift) > VT_MAX_NX;
                         out[dst + k] = (static_cast<uint32_t>(h) + static_cast<uint32_t>(rec_base)) |
                                        static_cast<uint32_t>(h >> kHitAltShift) << kStageAltShift;
-                    else
+                    } else
                         out[dst + k] = h + rec_base;
                 }
+                if (HITC && __ballot(wide_alt) && ul == 0) atomicOr(err, 4u);
                 dst += rq.n_hits;
             }
         }
@@ -4006,7 +4015,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
-                         int compact, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+                         int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
     const bool rowc = compact == SB_COMPACT_ALL, hitc = compact != 0;  // u32 rows / offsets; u32 hits
     if (!n_runs) {
         (void)hipMemsetAsync(row_off, 0, rowc ? 4 : 8, s);
@@ -4022,13 +4031,18 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                            static_cast<uint32_t>(config().req_inject), gtot);
     };
     (void)run;
-    if (rowc) {
-        if (n_lut <= kReqLut) eval(request_eval_kernel<true, true>);
-        else eval(request_eval_kernel<false, true>);
-    } else {
-        if (n_lut <= kReqLut) eval(request_eval_kernel<true, false>);
-        else eval(request_eval_kernel<false, false>);
-    }
+    auto eval_rec = [&](auto rec) {
+        constexpr bool R = decltype(rec)::value;
+        if (rowc) {
+            if (n_lut <= kReqLut) eval(request_eval_kernel<true, true, R>);
+            else eval(request_eval_kernel<false, true, R>);
+        } else {
+            if (n_lut <= kReqLut) eval(request_eval_kernel<true, false, R>);
+            else eval(request_eval_kernel<false, false, R>);
+        }
+    };
+    if (rec_staged) eval_rec(std::true_type{});
+    else eval_rec(std::false_type{});
     if (ev1) (void)hipEventRecord(ev1, s);
     hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, gtot, n_groups, tstatus, n_tiles);
     auto deliver = [&](auto kern) {
@@ -4036,9 +4050,14 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
                            shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx, static_cast<void *>(out),
                            n_rows, rec_base, err);
     };
-    if (rowc) deliver(request_deliver_kernel<true, true>);
-    else if (hitc) deliver(request_deliver_kernel<false, true>);
-    else deliver(request_deliver_kernel<false, false>);
+    auto deliver_rec = [&](auto rec) {
+        constexpr bool R = decltype(rec)::value;
+        if (rowc) deliver(request_deliver_kernel<true, true, R>);
+        else if (hitc) deliver(request_deliver_kernel<false, true, R>);
+        else deliver(request_deliver_kernel<false, false, R>);
+    };
+    if (rec_staged) deliver_rec(std::true_type{});
+    else deliver_rec(std::false_type{});
 }
 
 void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,

@@ -728,7 +728,8 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
                         R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
                         static_cast<ReqPartial *>(rows), static_cast<uint64_t *>(row_off), R.row_src.as<uint64_t>(),
                         R.stage.as<uint32_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
-                        R.err.as<unsigned int>(), R.compact, st, ev[0], ev[1]);
+                        R.err.as<unsigned int>(), R.compact,
+                        s.n_records <= kStageCandMask && !config().req_index_stage, st, ev[0], ev[1]);
     HIP_OK(hipGetLastError());
 }
 

@@ -16,6 +16,7 @@ SB_OK = 0
 SB_GRAN = {'boolean': 0, 'count': 1, 'aggregated': 2, 'record': 3}
 
 
+SB_EINVAL = -1  # malformed argument / payload (and compact outputs a batch cannot fit)
 SB_ESTALE = -7  # sb_store_open: a source VCF changed since the save
 SB_EINTERNAL = -8  # a device pass failed its own consistency checks
 SB_HOST_ONLY = -1  # sb_builder_finish / sb_store_open: no device image

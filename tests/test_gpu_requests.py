@@ -113,6 +113,48 @@ def test_requests_match_slices(fixture):
     np.testing.assert_array_equal(hits_c, hits)
 
 
+@pytest.mark.parametrize('fixture', ['quirk22', 'general22'])
+def test_index_staged_hits_match(fixture, monkeypatch):
+    """request_eval_kernel stages each hit as its record number (the
+    store's records fit 29 bits) or, for larger stores, as its candidate
+    index that request_deliver_kernel maps through vc_idx: the index form,
+    forced with SBEACON_REQ_INDEX_STAGE (a test hook), gives the same rows
+    and hit lists, full-width and compact."""
+    from payload_gen import read_records
+    from sbeacon.engine import Store
+    from sbeacon._lib import SB_EINVAL, SbError
+    from sbeacon.requests import COMPACT_ALL, COMPACT_HITS, RequestBatch, requests_from_split_payloads
+    path = os.path.join(FIXTURES, fixture + '.vcf')
+    store = Store.build([(fixture + '.vcf', path)], device=0)
+    recs, names = read_records(path)
+    rng = random.Random(7 + len(fixture))
+    sps = [_split_payload(rng, recs, names, fixture + '.vcf') for _ in range(300)]
+    arr, keep, owners = requests_from_split_payloads(store, sps)  # keep: the buffers arr points into
+    exp_rows, exp_hits, _ = _expected(store, sps)
+    # u32 hits hold ALT labels 0..7: a per-slice hit past that fails the batch (SB_EINVAL), never a cut label
+    wide_alt = any(h >> 32 > 7 for hl in exp_hits for h in hl)
+    assert wide_alt == (fixture == 'general22')
+    for index_stage in ('0', '1'):
+        monkeypatch.setenv('SBEACON_REQ_INDEX_STAGE', index_stage)
+        for mode in (0, COMPACT_HITS, COMPACT_ALL):
+            b = RequestBatch(store, arr, len(owners))
+            try:
+                b.set_compact(mode)
+            except SbError:  # COMPACT_ALL: not for batches with per-slice rows
+                assert mode == COMPACT_ALL
+                continue
+            if mode and wide_alt:
+                with pytest.raises(SbError) as e:
+                    b.answer()
+                assert e.value.code == SB_EINVAL and 'ALT index past 7' in str(e.value)
+                continue
+            rows, hits, ro = b.answer()
+            np.testing.assert_array_equal(rows, exp_rows)
+            for w in range(len(sps)):
+                assert [int(x) for x in hits[ro[w]:ro[w + 1]]] == exp_hits[w], (index_stage, mode, w)
+    assert ro[-1] > 0
+
+
 def test_genome_requests_match_oracle_and_slices():
     """Config-3 shape (small): shard request batches at world 1 and 2 vs the
     per-slice shard batches (rows + hit lists) and the C oracle (rows; at
@@ -381,7 +423,7 @@ def test_request_batches_concurrent_streams():
             np.testing.assert_array_equal(x, y)
 
 
-def test_device_planned_requests_match_host_planned():
+def test_device_planned_requests_match_host_planned(monkeypatch):
     """sb_requests_prepare_columns with batch-wide scalar filters plans on the
     device (request_plan_kernel: runs of 64 rows, candidate ranges from the
     coarse index); the same requests as an sb_request array plan on the host.
@@ -444,9 +486,11 @@ def test_device_planned_requests_match_host_planned():
         np.testing.assert_array_equal(hits_r, hits_h)
     with pytest.raises(_lib.SbError):
         host_b.set_replan(True)  # planned on the host: nothing to re-plan from
-    # the compact output form (u32 rows, offsets and hits), widened on the host: the same answers
+    # the compact output form (u32 rows, offsets and hits), widened on the host: the same answers,
+    # with hits staged as records and (SBEACON_REQ_INDEX_STAGE) as candidate indices
     from sbeacon.requests import COMPACT_HITS
-    for b in (dev_b, host_b):
+    for b, index_stage in ((dev_b, '0'), (host_b, '0'), (dev_b, '1')):
+        monkeypatch.setenv('SBEACON_REQ_INDEX_STAGE', index_stage)
         # u32 hits with wide rows: any batch (per-slice rows included)
         b.set_compact(COMPACT_HITS)
         rows_c, hits_c, ro_c = b.answer()
