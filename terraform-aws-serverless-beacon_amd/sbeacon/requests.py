@@ -101,6 +101,7 @@ def requests_array(n: int, *, vcf_id, contig, start_min, start_max, end_min, end
     v['include_samples'] = np.asarray(include_samples, dtype=np.uint8)
     v['selected_samples_only'] = np.asarray(selected_samples_only, dtype=np.uint8)
     v['strict_variant_type'] = np.asarray(strict_variant_type, dtype=np.uint8)
+    arr._keep = keep  # the buffers its pointers name live as long as it does
     return arr, keep
 
 
@@ -168,6 +169,7 @@ def request_columns(n: int, *, vcf_id, contig, start_min, start_max, end_min, en
         setattr(c, 'n_' + short, len(vals))
         if codes is not None:
             setattr(c, f + '_code', arr(np.broadcast_to(np.asarray(codes), (n,)), np.uint32))
+    c._keep = keep  # the buffers its pointers name live as long as it does
     return c, keep
 
 
@@ -229,6 +231,7 @@ def beacon_requests(n: int, *, vcf_id: int, contig, start, end, start2=None, end
             q.variant_type_code = col(variant_type_code)
     q.granularity = _lib.SB_GRAN[granularity] if isinstance(granularity, str) else int(granularity)
     q.include_details = 1 if include_details else 0
+    q._keep = keep  # the buffers its pointers name live as long as it does
     return q, keep
 
 
