@@ -197,7 +197,9 @@ def main_genome(args):
     # the whole pass: the planning kernels (32 B packed request read, 32 B
     # descriptor written per request), eval, tile scan, delivery (+ 4 B row
     # count read and 4 B row offset written per request; per hit its staged word read (4 B), its record id
-    # read (4 B), the 4 B hit written: u32 hits, sb_requests_set_compact)
+    # read (4 B), the 4 B hit written: u32 hits, sb_requests_set_compact).  The record id is priced once
+    # per hit although the eval now loads it beside each candidate's VcQ word (coalesced, instead of the
+    # delivery's per-hit gather): the pricing counts what the answer needs, not what the kernel reads.
     comp_pass = comp + 64.0 * agg['rows'] + 8.0 * chains + 12.0 * hits_avg
     achieved_pass = comp_pass / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
     uniq = agg['uniq']
