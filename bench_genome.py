@@ -200,7 +200,12 @@ def main_genome(args):
     # read (4 B), the 4 B hit written: u32 hits, sb_requests_set_compact).  The record id is priced once
     # per hit although the eval now loads it beside each candidate's VcQ word (coalesced, instead of the
     # delivery's per-hit gather): the pricing counts what the answer needs, not what the kernel reads.
-    comp_pass = comp + 64.0 * agg['rows'] + 8.0 * chains + 12.0 * hits_avg
+    # -- when the eval kernel plans its runs itself (sb_requests_plan_fused: a
+    # fixed-stride re-planning pass) the descriptors never reach HBM and the
+    # eval's 32 B per request is the packed request (ReqIn) instead: no
+    # planning bytes of their own
+    fused = all(b['batch'].plan_fused() for b in B)
+    comp_pass = comp + (0.0 if fused else 64.0) * agg['rows'] + 8.0 * chains + 12.0 * hits_avg
     achieved_pass = comp_pass / (pass_ms * 1e-3) / 1e9 if pass_ms > 0 else 0.0
     uniq = agg['uniq']
     contract = 32.0 * uniq + 8.0 * hits_avg
@@ -287,10 +292,14 @@ def main_genome(args):
                                   f'the {"first slice" if args.deliver == "first" else "rank 0"} rank over '
                                   f'{"RCCL" if world > 1 else "(no peer)"}'},
         'step': f'one request batch of a rotation over {args.batches} independently drawn 1 M-request batches '
-                f'(step i answers batch i mod {args.batches}; packed requests resident in HBM): planning '
-                '(request_plan_kernel: each request\'s candidate range by a batched lower / upper bound of its '
-                'splitQuery window in the (segment, kind) index + its staging capacity; request_stage_scan_kernel), '
-                'request_eval_kernel (every request = one chain of its 10 kb slices, rows + hits staged per run), '
+                f'(step i answers batch i mod {args.batches}; packed requests resident in HBM): '
+                + ('request_eval_kernel planning each run in the wave (each request\'s candidate range by a batched '
+                   'lower / upper bound of its splitQuery window in the (segment, kind) index; fixed-stride staging; '
+                   'sb_requests_plan_fused) and evaluating it ' if fused else
+                   'planning (request_plan_kernel: each request\'s candidate range by a batched lower / upper bound '
+                   'of its splitQuery window in the (segment, kind) index + its staging capacity), '
+                   'request_eval_kernel ')
+                + '(every request = one chain of its 10 kb slices, rows + hits staged per run), '
                 'request_tile_scan_kernel + request_deliver_kernel (row offsets, dense hit lists in request order; compact outputs: rows as four u32 sums, u32 offsets and hits), '
                 'then the exchange (send/recv of straddling rows and hits)',
         'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
@@ -305,9 +314,11 @@ def main_genome(args):
                                'its launch in each of K rotating passes on its stream, averaged (rocprof per-kernel '
                                'averages: profiles/)',
                      'algorithmic_bytes_per_launch': r0[7],
-                     'pricing': 'bytes the launch must move at least once: 52 B/request (32 B chain descriptor + '
-                                '16 B row + 4 B row count: the compact outputs) + 16 B per candidate in the union of '
-                                'the chain windows (POS, END, VtHot word, AC) + 4 B/hit staged',
+                     'pricing': 'bytes the launch must move at least once: 52 B/request (32 B '
+                                + ('packed request, planned in the wave' if fused else 'chain descriptor')
+                                + ' + 16 B row + 4 B row count: the compact outputs) + 16 B per candidate in the '
+                                'union of the chain windows (POS, END, VtHot word, AC) + 4 B/hit staged',
+                     'planning_fused': fused,
                      'r04_basis': {'bytes': r0[13], 'frac': round(r0[13] / (r0[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                    if r0[1] > 0 else None,
                                    'note': 'the round-4 pricing (80 B per request, 24 B per candidate, 8 B per hit '
@@ -315,9 +326,10 @@ def main_genome(args):
                                            'for comparison'},
                      'pass': {'ms': round(r0[10], 4), 'achieved': round(r0[11], 1),
                               'frac': round(r0[11] / HBM_PEAK_GBS, 4), 'bytes': r0[12],
-                              'note': 'planning (+64 B/request: packed request read, descriptor written) + eval + '
-                                      'tile scan + delivery (+8 B/request: row count read, offset written; +12 B/hit: '
-                                      'staged word and record id read, 4 B hit written)'},
+                              'note': ('eval with its planning (no descriptors in HBM)' if fused else
+                                       'planning (+64 B/request: packed request read, descriptor written) + eval')
+                                      + ' + tile scan + delivery (+8 B/request: row count read, offset written; '
+                                      '+12 B/hit: staged word and record id read, 4 B hit written)'},
                      'candidates': {'unique': int(st['cand_unique']), 'in_windows': int(st['cand_window']),
                                     'loaded': int(st['cand_loaded'])},
                      'contract_bytes_per_launch': r0[8],

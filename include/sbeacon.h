@@ -532,6 +532,12 @@ int sb_requests_time_eval(sb_batch *b, int on);
  * Replaces splitQuery's per-request fan-out (lambda/splitQuery/
  * lambda_function.py:74-110) as a device step. */
 int sb_requests_set_replan(sb_batch *b, int on);
+/* *fused = 1 when the batch's last pass planned each run inside
+ * request_eval_kernel (a re-planning pass of a fixed-stride batch with
+ * record staging and no per-slice part: no request_plan_kernel launch, the
+ * chain descriptors never leave LDS), else 0.  Measurement: the eval
+ * kernel's events then include the planning. */
+int sb_requests_plan_fused(sb_batch *b, int *fused);
 /* One row of the compact output (sb_requests_set_compact): the
  * sb_request_partial sums as u32 (no error count: compact batches have no
  * per-slice part, whose slices are the only ones that can raise). */

@@ -446,6 +446,7 @@ struct sb_batch {
         DevMem din, rcap;
         uint32_t n_in = 0;
         bool replan = false;
+        bool plan_fused = false;  // the last pass planned inside request_eval_kernel (sb_requests_plan_fused)
         uint64_t stage_stride = 0;  // staging slots per run when fixed (re-planning skips the staging scan); 0: packed
         int compact = 0;  // sb_requests_set_compact: 0 wide, SB_COMPACT_ALL, SB_COMPACT_HITS
         // request_eval_kernel's invariant word (sticky; checked at sync: SB_EINTERNAL)

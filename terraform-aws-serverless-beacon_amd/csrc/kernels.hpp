@@ -108,13 +108,14 @@ void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, ui
 // row order, one wave per run, offsets by decoupled look-back (ticket and
 // status zeroed by the caller; status n_runs words).  sres..shits: the
 // batch's per-slice part (rows of it already reduced into `rows`), or null.
-void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun *runs, uint32_t n_runs,
+void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs, uint32_t n_runs,
                          unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
                          int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0 = nullptr,
-                         hipEvent_t ev1 = nullptr);
+                         hipEvent_t ev1 = nullptr, const ReqIn *plan_in = nullptr, uint32_t n_in = 0,
+                         uint64_t stride = 0);
 // chain slots per run (kReqRun)
 uint32_t req_run_max();
 // Request planning on the device: rows in runs of kRunRows (n_runs =

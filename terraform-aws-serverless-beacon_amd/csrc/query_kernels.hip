@@ -2029,18 +2029,65 @@ struct ReqChunk {
 static_assert(offsetof(ReqLds, b) == sizeof(uint4) * kReqRun && offsetof(ReqLds, wch) == 2 * sizeof(uint4) * kReqRun &&
                   offsetof(ReqLds, slow) >= kRunRows * sizeof(ReqPartial),
               "a, b, wch are one block that holds a run's rows");
+// One run's planning (request_plan_kernel's, below, without the capacity
+// sums): lane = row; the chain descriptors packed into slots (rows with
+// candidates first, in row order, then those without, then first == 0 slots)
+// and written to `slots` (LDS, 64 x 32 B); returns the run record
+__device__ __forceinline__ RowRun plan_run(const DStore &st, const ReqIn *__restrict__ in, uint32_t n, uint32_t w,
+                                           uint64_t stride, ReqChain *slots, uint32_t ul) {
+    const uint32_t row = w * kRunRows + ul;
+    ReqIn q{};
+    if (row < n) q = in[row];
+    const uint32_t cls = row < n ? (q.cls & 3u) : static_cast<uint32_t>(REQ_NONE);
+    const bool chain = cls == REQ_CHAIN;
+    uint32_t c0 = 0, c1 = 0, vi_xinfo = 0;
+    if (chain) {
+        const VcIndex vi = st.vcx[static_cast<uint64_t>(q.seg) * kVtKinds + ((q.bits >> 23) & 7u)];
+        c0 = vc_bound(vi, st.vc_bucket, q.first, 0);
+        c1 = (q.bits >> 26) & 1u ? c0 : max(c0, vc_bound(vi, st.vc_bucket, static_cast<uint64_t>(q.last) + 1, 1));
+        vi_xinfo = vi.xinfo;
+    }
+    const bool ne = chain && c1 > c0;
+    const uint64_t mne = __ballot(ne), mem = __ballot(chain && !ne);
+    const uint32_t nne = static_cast<uint32_t>(__popcll(mne)), nslots = nne + static_cast<uint32_t>(__popcll(mem));
+    if (chain) {
+        const uint32_t slot = ne ? popc_below(mne) : nne + popc_below(mem);
+        slots[slot] = ReqChain{q.first, q.last, c0, c1, q.e0, q.espan, q.bits | (ul << 17), q.lut_off};
+    }
+    if (ul >= nslots) slots[ul] = ReqChain{0, 0, 0, 0, 0, 0, 0, 0};
+    const uint32_t nsl = chain ? q.cls >> 2 : 0u;
+    const uint32_t slsum = rdl(incl_sum_u32(nsl), kWave - 1);
+    const bool simple = __ballot(cls == REQ_SLICES) == 0;
+    const uint32_t xi = ne ? vi_xinfo : kVcNarrow;
+    const bool narrow = __ballot(!(xi & kVcNarrow)) == 0;
+    const uint32_t a = xi & kVcAnMask;
+    const uint32_t a0 = mne ? rdl(a, static_cast<uint32_t>(ffs64(mne))) : 1u;
+    const bool anc = narrow && a0 != 0u && __ballot(ne && a != a0) == 0;
+    const uint32_t flags = (simple ? kRunSimple : 0u) | (narrow ? kRunNarrow : 0u) |
+                           (anc ? kRunAnCommon | (a0 - 1u) << kRunAnShift : 0u);
+    wave_lds_sync();
+    return RowRun{w * kRunRows, min(w * kRunRows + kRunRows, n), 0u, nslots, stride * w, slsum, flags};
+}
+
 // COMPACT (sb_requests_set_compact): rows as RowC (16 B), row counts /
 // offsets as u32; only batches without a per-slice part (sres == nullptr)
 // REC: hits are staged as their record numbers (the store's records fit 29
 // bits): the record id is loaded with the candidate word, coalesced, and
 // request_deliver_kernel copies without a per-hit gather; else the
 // candidate index is staged and the deliver maps it (vc_idx)
-template <bool LDS_LUT, bool COMPACT, bool REC>
+// PLAN: the run is planned in the wave itself (a re-planning pass of a
+// fixed-stride batch: plan_run below, request_plan_kernel's work) from the
+// resident packed requests, its chain descriptors passed through LDS instead
+// of HBM, its run record written for request_deliver_kernel -- one launch
+// and 64 B per request fewer, the planner's dependent index loads hidden
+// behind other waves' candidate work
+template <bool LDS_LUT, bool COMPACT, bool REC, bool PLAN>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_REQ_WAVES, SBEACON_REQ_WAVES))) void request_eval_kernel(
-    DStore st, const ReqChain *__restrict__ chains, const RowRun *__restrict__ runs, uint32_t n_runs,
+    DStore st, const ReqChain *__restrict__ chains, RowRun *__restrict__ runs, uint32_t n_runs,
     unsigned long long *__restrict__ status, const QRes *__restrict__ sres, void *__restrict__ rows_out,
     void *__restrict__ row_cnt_out, uint64_t *__restrict__ row_src, uint32_t *__restrict__ stage, uint32_t n_lut,
-    unsigned int *__restrict__ err, uint32_t inject, unsigned long long *__restrict__ gtot) {
+    unsigned int *__restrict__ err, uint32_t inject, unsigned long long *__restrict__ gtot,
+    const ReqIn *__restrict__ in, uint32_t n_in, uint64_t stride) {
     ReqPartial *const rows = static_cast<ReqPartial *>(rows_out);
     uint64_t *const row_cnt = static_cast<uint64_t *>(row_cnt_out);
     __shared__ ReqLds lds_all[kWavesPerBlock];
@@ -2069,8 +2116,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     RowRun rr{};
     ReqChain C{};
     if (live) {
-        rr = runs[w];
-        C = chains[static_cast<uint64_t>(w) * kReqRun + ul];
+        if constexpr (PLAN) {
+            rr = plan_run(st, in, n_in, w, stride, reinterpret_cast<ReqChain *>(L.a), ul);
+            if (ul == 0) runs[w] = rr;
+            C = reinterpret_cast<const ReqChain *>(L.a)[ul];
+            wave_lds_sync();  // (L.a / L.b are rewritten below)
+        } else {
+            rr = runs[w];
+            C = chains[static_cast<uint64_t>(w) * kReqRun + ul];
+        }
     }
     if (threadIdx.x == 0) s_done = 0;
     if constexpr (LDS_LUT)
@@ -2406,6 +2460,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         if (rdl(cs_incl, kWave - 1) != hpos || ex_tot != run_ex || __ballot(bad_lane))
             if (ul == 0) atomicOr(err, 1u);
 #endif
+        // (PLAN: the run's hits within its fixed-stride staging region; never
+        // past it, the stride was sized on these requests)
+        if (PLAN && hpos > stride && ul == 0) atomicOr(err, 1u);
     }
     if (ul < R) {
         const bool slow = (L.slow[ul >> 5] >> (ul & 31u)) & 1u;  // never for prepared chains
@@ -4010,12 +4067,13 @@ void launch_general(const DStore &st, const GStore &gs, const uint32_t *work, ui
                        samples_out, scratch, wb, hwords, tcap, big_n, big, big_limbs, big_cap);
 }
 
-void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun *runs, uint32_t n_runs,
+void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs, uint32_t n_runs,
                          unsigned long long *status, unsigned long long *tstatus, const QRes *sres,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
-                         int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1) {
+                         int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                         const ReqIn *plan_in, uint32_t n_in, uint64_t stride) {
     const bool rowc = compact == SB_COMPACT_ALL, hitc = compact != 0;  // u32 rows / offsets; u32 hits
     if (!n_runs) {
         (void)hipMemsetAsync(row_off, 0, rowc ? 4 : 8, s);
@@ -4028,21 +4086,24 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, const RowRun 
     auto eval = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
                            static_cast<void *>(rows), static_cast<void *>(row_off), row_src, stage, n_lut, err,
-                           static_cast<uint32_t>(config().req_inject), gtot);
+                           static_cast<uint32_t>(config().req_inject), gtot, plan_in, n_in, stride);
     };
     (void)run;
-    auto eval_rec = [&](auto rec) {
-        constexpr bool R = decltype(rec)::value;
+    auto eval_rec = [&](auto rec, auto plan) {
+        constexpr bool R = decltype(rec)::value, P = decltype(plan)::value;
         if (rowc) {
-            if (n_lut <= kReqLut) eval(request_eval_kernel<true, true, R>);
-            else eval(request_eval_kernel<false, true, R>);
+            if (n_lut <= kReqLut) eval(request_eval_kernel<true, true, R, P>);
+            else eval(request_eval_kernel<false, true, R, P>);
         } else {
-            if (n_lut <= kReqLut) eval(request_eval_kernel<true, false, R>);
-            else eval(request_eval_kernel<false, false, R>);
+            if (n_lut <= kReqLut) eval(request_eval_kernel<true, false, R, P>);
+            else eval(request_eval_kernel<false, false, R, P>);
         }
     };
-    if (rec_staged) eval_rec(std::true_type{});
-    else eval_rec(std::false_type{});
+    // (the planning fused only with record staging: the form every store
+    // below 2^29 records takes)
+    if (plan_in && rec_staged) eval_rec(std::true_type{}, std::true_type{});
+    else if (rec_staged) eval_rec(std::true_type{}, std::false_type{});
+    else eval_rec(std::false_type{}, std::false_type{});
     if (ev1) (void)hipEventRecord(ev1, s);
     hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, gtot, n_groups, tstatus, n_tiles);
     auto deliver = [&](auto kern) {

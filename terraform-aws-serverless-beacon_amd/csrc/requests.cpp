@@ -703,7 +703,12 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
     }
     if (R.compact && rec_base + s.n_records > kStageCandMask)
         throw Error(SB_EINVAL, "compact request output: record numbers (rec_base + records) reach 2^29");
-    if (R.replan) {  // the planning kernels again, from the resident packed requests (same descriptors, same sizes)
+    const bool rec_staged = s.n_records <= kStageCandMask && !config().req_index_stage;
+    // a fixed-stride batch re-planning with record staging and no per-slice
+    // part: each eval wave plans its own run (request_eval_kernel PLAN)
+    const bool fuse = R.replan && R.stage_stride && !R.slices && rec_staged && !config().req_plan_apart;
+    R.plan_fused = fuse;
+    if (R.replan && !fuse) {  // the planning kernels again, from the resident packed requests (same descriptors, same sizes)
         launch_request_plan(s.d, R.din.as<ReqIn>(), R.n_in, R.dchains.as<ReqChain>(),
                             reinterpret_cast<RowRun *>(R.dchains.as<char>() + R.runs_at), R.rcap.as<unsigned long long>(),
                             reinterpret_cast<unsigned long long *>(R.rcap.as<char>() + size_t(R.n_runs) * 16), st,
@@ -721,15 +726,15 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
         }
         ev = R.eval_ev[R.eval_used++];
     }
-    launch_request_rows(d, R.dchains.as<ReqChain>(), reinterpret_cast<const RowRun *>(R.dchains.as<char>() + R.runs_at),
+    launch_request_rows(d, R.dchains.as<ReqChain>(), reinterpret_cast<RowRun *>(R.dchains.as<char>() + R.runs_at),
                         R.n_runs,
                         R.status.as<unsigned long long>(), R.tstatus.as<unsigned long long>(),
                         R.slices ? B.res.as<QRes>() : nullptr,
                         R.sseg.as<uint32_t>(), B.hoff.as<uint64_t>(), R.sherr.as<uint8_t>(), B.hits.as<uint64_t>(),
                         static_cast<ReqPartial *>(rows), static_cast<uint64_t *>(row_off), R.row_src.as<uint64_t>(),
                         R.stage.as<uint32_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
-                        R.err.as<unsigned int>(), R.compact,
-                        s.n_records <= kStageCandMask && !config().req_index_stage, st, ev[0], ev[1]);
+                        R.err.as<unsigned int>(), R.compact, rec_staged, st, ev[0], ev[1],
+                        fuse ? R.din.as<ReqIn>() : nullptr, R.n_in, R.stage_stride);
     HIP_OK(hipGetLastError());
 }
 
@@ -962,6 +967,14 @@ int sb_requests_set_replan(sb_batch *b, int on) {
         std::lock_guard<std::mutex> lk(b->mu);
         if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_set_replan between a run and its sync");
         b->req->replan = on != 0;
+    });
+}
+
+int sb_requests_plan_fused(sb_batch *b, int *fused) {
+    return guard([&] {
+        if (!b || !b->req || !fused) throw Error(SB_EINVAL, "not a request batch");
+        std::lock_guard<std::mutex> lk(b->mu);
+        *fused = b->req->plan_fused ? 1 : 0;
     });
 }
 

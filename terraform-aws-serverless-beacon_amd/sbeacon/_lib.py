@@ -245,6 +245,7 @@ SIGNATURES = {
     'sb_requests_prepare_beacon': (C.c_int, [P, C.c_void_p, C.c_size_t, C.c_void_p, C.POINTER(P)]),
     'sb_requests_time_eval': (C.c_int, [P, C.c_int]),
     'sb_requests_set_replan': (C.c_int, [P, C.c_int]),
+    'sb_requests_plan_fused': (C.c_int, [P, C.POINTER(C.c_int)]),
     'sb_requests_set_compact': (C.c_int, [P, C.c_int]),
     'sb_requests_inexact_rows': (C.c_int, [P, P]),
     'sb_store_trim': (C.c_int, [P]),

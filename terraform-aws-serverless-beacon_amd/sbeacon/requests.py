@@ -335,6 +335,13 @@ class RequestBatch:
         batches only)."""
         check(lib().sb_requests_set_replan(self._h, 1 if on else 0))
 
+    def plan_fused(self) -> bool:
+        """True when the last pass planned its runs inside request_eval_kernel
+        (sb_requests_plan_fused: a re-planning pass of a fixed-stride batch)."""
+        f = C.c_int()
+        check(lib().sb_requests_plan_fused(self._h, C.byref(f)))
+        return bool(f.value)
+
     def set_compact(self, on):
         """Narrow outputs (sb_requests_set_compact).  True / COMPACT_ALL:
         rows [n, 4] uint32 (exists, n_variants, call_count,

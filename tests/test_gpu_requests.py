@@ -478,9 +478,13 @@ def test_device_planned_requests_match_host_planned(monkeypatch):
     # every pass re-planned on the device (the bench step): the same answers
     # pass after pass
     from sbeacon import _lib
+    # (fixed-stride staging: each eval wave plans its own run; with
+    # SBEACON_REQ_PLAN_APART request_plan_kernel runs first, as before)
     dev_b.set_replan(True)
-    for _ in range(2):
+    for apart in ('0', '1', '0'):
+        monkeypatch.setenv('SBEACON_REQ_PLAN_APART', apart)
         rows_r, hits_r, ro_r = dev_b.answer()
+        assert dev_b.plan_fused() == (apart == '0')  # (this batch stages at a fixed stride)
         np.testing.assert_array_equal(rows_r, rows_h)
         np.testing.assert_array_equal(ro_r, ro_h)
         np.testing.assert_array_equal(hits_r, hits_h)
