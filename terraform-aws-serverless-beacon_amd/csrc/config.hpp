@@ -38,6 +38,7 @@ struct Config {
     bool req_inject = false;      // SBEACON_REQ_INJECT=1 (tests): one wrong per-chain sum, so the pass's invariants fire
     bool req_index_stage = false; // SBEACON_REQ_INDEX_STAGE=1 (tests): stage candidate indices, as stores past 2^29 records do
     bool req_plan_apart = false;  // SBEACON_REQ_PLAN_APART=1: re-planning passes launch request_plan_kernel (no fused planning)
+    bool req_tile_scan = false;   // SBEACON_REQ_TILE_SCAN=1: request_tile_scan_kernel before the delivery (no in-delivery sums)
     int pack_dbg = 0;             // SBEACON_PACK_DBG: chain-kernel ablations (SBEACON_ABLATION builds)
 };
 
@@ -74,6 +75,7 @@ inline Config config() {
     c.req_inject = one("SBEACON_REQ_INJECT");
     c.req_index_stage = one("SBEACON_REQ_INDEX_STAGE");
     c.req_plan_apart = one("SBEACON_REQ_PLAN_APART");
+    c.req_tile_scan = one("SBEACON_REQ_TILE_SCAN");
     c.pack_dbg = num("SBEACON_PACK_DBG", 0);
     return c;
 }

@@ -2788,14 +2788,18 @@ __global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned 
 // COMPACT: row counts / offsets u32, hits u32 = (record + rec_base) | label
 // << kStageAltShift (the host checks records + rec_base < 2^29; an offset
 // past 32 bits fails the batch at sync)
-template <bool ROWC, bool HITC, bool REC>
+// GSUM: no tile scan before it -- the workgroup (= one eval workgroup's 4
+// runs) sums the eval workgroup totals before its own (gtot, <= 16 coalesced
+// loads per thread from L2 per 4,096 groups) and each wave adds its group's
+// earlier runs: one launch and its boundary fewer
+template <bool ROWC, bool HITC, bool REC, bool GSUM>
 __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const RowRun *__restrict__ runs, uint32_t n_runs, const unsigned long long *__restrict__ status,
     const unsigned long long *__restrict__ toff, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
     const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr, const uint64_t *__restrict__ shits,
     void *__restrict__ row_off_out, const uint64_t *__restrict__ row_src, const uint32_t *__restrict__ stage,
     const uint32_t *__restrict__ vc_idx, void *__restrict__ out_v, uint32_t n_rows, uint64_t rec_base,
-    unsigned int *__restrict__ err) {
+    unsigned int *__restrict__ err, const unsigned long long *__restrict__ gtot) {
     using Hit = std::conditional_t<HITC, uint32_t, uint64_t>;
     using Off = std::conditional_t<ROWC, uint32_t, uint64_t>;
     Hit *const out = static_cast<Hit *>(out_v);
@@ -2810,15 +2814,18 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
             return (static_cast<uint64_t>(r) + rec_base) | static_cast<uint64_t>(v >> kStageAltShift) << kHitAltShift;
     };
     const uint32_t w = uniform(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6));
-    if (w >= n_runs) return;
+    // (GSUM: a wave past the last run still joins the workgroup's sum below)
+    const bool live = w < n_runs;
+    if (!GSUM && !live) return;
     const uint32_t ul = static_cast<uint32_t>(lane_id());
-    const uint32_t t0 = (w / kDeliverTile) * kDeliverTile;
+    constexpr uint32_t kTileRuns = GSUM ? kWavesPerBlock : kDeliverTile;
+    const uint32_t t0 = (w / kTileRuns) * kTileRuns;
     // the run record and the run's total (status[w] = its staged hits, which
     // request_eval_kernel wrote) first: a simple run's first round of staged
     // hits is loaded before its output offset is known, so those loads and
     // the record-id gathers behind them overlap the offset scans
-    const RowRun rr = runs[w];
-    const uint64_t Hs = uniform64(status[w]);
+    const RowRun rr = live ? runs[w] : RowRun{};
+    const uint64_t Hs = live ? uniform64(status[w]) : 0ull;
     const uint32_t row_lo = uniform(rr.row_lo), row_hi = uniform(rr.row_hi);
     const uint64_t stage_at = uniform64(rr.stage);
     const bool simple = (uniform(rr.flags) & kRunSimple) != 0;
@@ -2833,8 +2840,31 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     }
     const uint32_t row = row_lo + ul;
     const uint64_t c = row < row_hi ? static_cast<uint64_t>(row_off[row]) : 0ull;  // the counts request_eval_kernel left
-    const uint64_t before = t0 + ul < w ? status[t0 + ul] : 0ull;
-    const uint64_t O = uniform64(toff[w / kDeliverTile]) +
+    const uint64_t before = live && t0 + ul < w ? status[t0 + ul] : 0ull;
+    // (GSUM: issued behind the run's own loads, so their latencies overlap)
+    uint64_t gsum = 0;  // GSUM: the totals of the eval workgroups before this one
+    if constexpr (GSUM) {
+        __shared__ unsigned long long s_part[kWavesPerBlock];
+        constexpr uint32_t kG = 16;
+        uint64_t part = 0;
+        for (uint32_t base = 0; base < blockIdx.x; base += kG * kBlock) {
+            uint64_t v[kG];
+#pragma unroll
+            for (uint32_t u = 0; u < kG; ++u) {
+                const uint32_t g = base + u * kBlock + threadIdx.x;
+                v[u] = g < blockIdx.x ? gtot[g] : 0ull;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kG; ++u) part += v[u];
+        }
+        part = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(part)), kWave - 1));
+        if (lane_id() == 0) s_part[threadIdx.x >> 6] = part;
+        __syncthreads();  // (every wave of the workgroup, live or not, reaches it)
+#pragma unroll
+        for (uint32_t k = 0; k < kWavesPerBlock; ++k) gsum += s_part[k];
+    }
+    if (!live) return;
+    const uint64_t O = (GSUM ? uniform64(gsum) : uniform64(toff[w / kDeliverTile])) +
                        static_cast<uint64_t>(rdl64(wave_incl_scan_i64(static_cast<int64_t>(before)), kWave - 1));
     const uint64_t linc = static_cast<uint64_t>(wave_incl_scan_i64(static_cast<int64_t>(c)));
     const uint64_t H = static_cast<uint64_t>(rdl64(static_cast<int64_t>(linc), kWave - 1));
@@ -4105,20 +4135,25 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
     else if (rec_staged) eval_rec(std::true_type{}, std::false_type{});
     else eval_rec(std::false_type{}, std::false_type{});
     if (ev1) (void)hipEventRecord(ev1, s);
-    hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, gtot, n_groups, tstatus, n_tiles);
+    // record staging: the delivery sums the eval workgroup totals itself (no
+    // tile scan launch; SBEACON_REQ_TILE_SCAN=1 keeps it)
+    const bool gsum = rec_staged && !config().req_tile_scan;
+    if (!gsum)
+        hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, gtot, n_groups, tstatus, n_tiles);
     auto deliver = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg, shoff, sherr,
                            shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx, static_cast<void *>(out),
-                           n_rows, rec_base, err);
+                           n_rows, rec_base, err, gtot);
     };
-    auto deliver_rec = [&](auto rec) {
-        constexpr bool R = decltype(rec)::value;
-        if (rowc) deliver(request_deliver_kernel<true, true, R>);
-        else if (hitc) deliver(request_deliver_kernel<false, true, R>);
-        else deliver(request_deliver_kernel<false, false, R>);
+    auto deliver_rec = [&](auto rec, auto gs) {
+        constexpr bool R = decltype(rec)::value, G = decltype(gs)::value;
+        if (rowc) deliver(request_deliver_kernel<true, true, R, G>);
+        else if (hitc) deliver(request_deliver_kernel<false, true, R, G>);
+        else deliver(request_deliver_kernel<false, false, R, G>);
     };
-    if (rec_staged) deliver_rec(std::true_type{});
-    else deliver_rec(std::false_type{});
+    if (gsum) deliver_rec(std::true_type{}, std::true_type{});
+    else if (rec_staged) deliver_rec(std::true_type{}, std::false_type{});
+    else deliver_rec(std::false_type{}, std::false_type{});
 }
 
 void launch_request_plan(const DStore &st, const ReqIn *in, uint32_t n, ReqChain *chains, RowRun *runs,

@@ -228,7 +228,7 @@ def test_genome_requests_match_oracle_and_slices():
         np.testing.assert_array_equal(total, exp)
 
 
-def test_large_batch_scans_multiple_rounds():
+def test_large_batch_scans_multiple_rounds(monkeypatch):
     """A batch past one round of the pass's scans (> 4,096 eval workgroups =
     > 1,048,576 requests for the tile scan; > 16 staging tiles): its rows
     and hit lists equal those of the same requests answered as two batches
@@ -248,6 +248,14 @@ def test_large_batch_scans_multiple_rounds():
 
     rows, hits, ro = answer(reqs)
     assert len(rows) == len(reqs) and (len(reqs) + 63) // 64 > 4 * 4096
+    # (past 4,096 eval workgroups the delivery's group sums take a second
+    # round of loads; the tile scan gives the same offsets)
+    monkeypatch.setenv('SBEACON_REQ_TILE_SCAN', '1')
+    rows_t, hits_t, ro_t = answer(reqs)
+    monkeypatch.delenv('SBEACON_REQ_TILE_SCAN')
+    np.testing.assert_array_equal(rows_t, rows)
+    np.testing.assert_array_equal(ro_t, ro)
+    np.testing.assert_array_equal(hits_t, hits)
     k = 600_000
     part = [answer(Requests(*(getattr(reqs, f)[sl] for f in ('ci', 'start', 'width', 'vt', 'vmin', 'vmax'))))
             for sl in (slice(0, k), slice(k, None))]
@@ -481,8 +489,11 @@ def test_device_planned_requests_match_host_planned(monkeypatch):
     # (fixed-stride staging: each eval wave plans its own run; with
     # SBEACON_REQ_PLAN_APART request_plan_kernel runs first, as before)
     dev_b.set_replan(True)
-    for apart in ('0', '1', '0'):
+    # (the delivery sums the eval workgroup totals itself; with
+    # SBEACON_REQ_TILE_SCAN request_tile_scan_kernel runs before it)
+    for apart, tile in (('0', '0'), ('1', '0'), ('0', '1'), ('0', '0')):
         monkeypatch.setenv('SBEACON_REQ_PLAN_APART', apart)
+        monkeypatch.setenv('SBEACON_REQ_TILE_SCAN', tile)
         rows_r, hits_r, ro_r = dev_b.answer()
         assert dev_b.plan_fused() == (apart == '0')  # (this batch stages at a fixed stride)
         np.testing.assert_array_equal(rows_r, rows_h)
