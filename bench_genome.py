@@ -300,7 +300,9 @@ def main_genome(args):
                    'of its splitQuery window in the (segment, kind) index + its staging capacity), '
                    'request_eval_kernel ')
                 + '(every request = one chain of its 10 kb slices, rows + hits staged per run), '
-                'request_tile_scan_kernel + request_deliver_kernel (row offsets, dense hit lists in request order; compact outputs: rows as four u32 sums, u32 offsets and hits), '
+                'request_deliver_kernel (each workgroup\'s output base summed from the eval workgroup totals -- '
+                'request_tile_scan_kernel\'s tile offsets with SBEACON_REQ_TILE_SCAN=1 --, row offsets, dense hit lists '
+                'in request order; compact outputs: rows as four u32 sums, u32 offsets and hits), '
                 'then the exchange (send/recv of straddling rows and hits)',
         'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
         'candidates_loaded_per_s': round(tot_cand * args.steps / elapsed, 1),
@@ -328,7 +330,7 @@ def main_genome(args):
                               'frac': round(r0[11] / HBM_PEAK_GBS, 4), 'bytes': r0[12],
                               'note': ('eval with its planning (no descriptors in HBM)' if fused else
                                        'planning (+64 B/request: packed request read, descriptor written) + eval')
-                                      + ' + tile scan + delivery (+8 B/request: row count read, offset written; '
+                                      + ' + delivery (+8 B/request: row count read, offset written; '
                                       '+12 B/hit: staged word and record id read, 4 B hit written)'},
                      'candidates': {'unique': int(st['cand_unique']), 'in_windows': int(st['cand_window']),
                                     'loaded': int(st['cand_loaded'])},
