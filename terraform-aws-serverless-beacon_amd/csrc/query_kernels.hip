@@ -4103,7 +4103,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
                          int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
-                         const ReqIn *plan_in, uint32_t n_in, uint64_t stride) {
+                         const ReqIn *plan_in, uint32_t n_in, uint64_t stride, bool inject, bool tile_scan) {
     const bool rowc = compact == SB_COMPACT_ALL, hitc = compact != 0;  // u32 rows / offsets; u32 hits
     if (!n_runs) {
         (void)hipMemsetAsync(row_off, 0, rowc ? 4 : 8, s);
@@ -4116,7 +4116,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
     auto eval = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
                            static_cast<void *>(rows), static_cast<void *>(row_off), row_src, stage, n_lut, err,
-                           static_cast<uint32_t>(config().req_inject), gtot, plan_in, n_in, stride);
+                           static_cast<uint32_t>(inject), gtot, plan_in, n_in, stride);
     };
     (void)run;
     auto eval_rec = [&](auto rec, auto plan) {
@@ -4137,7 +4137,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
     if (ev1) (void)hipEventRecord(ev1, s);
     // record staging: the delivery sums the eval workgroup totals itself (no
     // tile scan launch; SBEACON_REQ_TILE_SCAN=1 keeps it)
-    const bool gsum = rec_staged && !config().req_tile_scan;
+    const bool gsum = rec_staged && !tile_scan;
     if (!gsum)
         hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, gtot, n_groups, tstatus, n_tiles);
     auto deliver = [&](auto kern) {

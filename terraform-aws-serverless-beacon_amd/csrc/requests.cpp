@@ -703,10 +703,11 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
     }
     if (R.compact && rec_base + s.n_records > kStageCandMask)
         throw Error(SB_EINVAL, "compact request output: record numbers (rec_base + records) reach 2^29");
-    const bool rec_staged = s.n_records <= kStageCandMask && !config().req_index_stage;
+    const Config cfg = config();  // (once per pass: each call reads every SBEACON_* variable)
+    const bool rec_staged = s.n_records <= kStageCandMask && !cfg.req_index_stage;
     // a fixed-stride batch re-planning with record staging and no per-slice
     // part: each eval wave plans its own run (request_eval_kernel PLAN)
-    const bool fuse = R.replan && R.stage_stride && !R.slices && rec_staged && !config().req_plan_apart;
+    const bool fuse = R.replan && R.stage_stride && !R.slices && rec_staged && !cfg.req_plan_apart;
     R.plan_fused = fuse;
     if (R.replan && !fuse) {  // the planning kernels again, from the resident packed requests (same descriptors, same sizes)
         launch_request_plan(s.d, R.din.as<ReqIn>(), R.n_in, R.dchains.as<ReqChain>(),
@@ -734,7 +735,8 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
                         static_cast<ReqPartial *>(rows), static_cast<uint64_t *>(row_off), R.row_src.as<uint64_t>(),
                         R.stage.as<uint32_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
                         R.err.as<unsigned int>(), R.compact, rec_staged, st, ev[0], ev[1],
-                        fuse ? R.din.as<ReqIn>() : nullptr, R.n_in, R.stage_stride);
+                        fuse ? R.din.as<ReqIn>() : nullptr, R.n_in, R.stage_stride, cfg.req_inject,
+                        cfg.req_tile_scan);
     HIP_OK(hipGetLastError());
 }
 
