@@ -564,6 +564,55 @@ int sb_requests_set_compact(sb_batch *b, int on);
  * Replaces nothing in the reference (its counts are Python ints). */
 int sb_requests_inexact_rows(sb_batch *b, uint8_t *flags);
 
+/* ---- g_variants route bodies (the route aggregation in the library) ------
+ * GET / POST /g_variants (lambda/getGenomicVariants/route_g_variants.py:
+ * 49-208) for a batch of route events whose fan-out -- one request row per
+ * (dataset, VCF) pair, perform_variant_search_sync's SplitQueryPayloads
+ * (shared_resources/variantutils/search_variants.py:158-244) -- was answered
+ * by a request pass (sb_requests_run).  Event e owns the consecutive rows
+ * [row_lo, row_hi).  The route's aggregation (:153-171) over them:
+ * exists = OR of the rows' exists; with check_all (includeResultsetResponses
+ * in {HIT, ALL}) variants = the distinct strings
+ * f'{chrom}\t{POS}\t{REF}\t{ALT}\t{VT}' of the rows' hits and one
+ * get_variant_entry (shared_resources/apiutils/entries.py:1-24) per distinct
+ * f'{assembly}\t{chrom}\t{pos}\t{ref}\t{alt}' (first-seen order); then the
+ * body of get_boolean_response / get_counts_response / get_result_sets_response
+ * (shared_resources/apiutils/responses.py:160-254) as json.dumps writes it
+ * (the `body` of bundle_response, api_response.py:37-46).  status[e]: 0 =
+ * body written; 1 = answer this event through the Python route (a row whose
+ * slices raised -- the route re-raises --, a VCF with negative AC (the
+ * route's completion-order gate on exists then matters), text that is not
+ * UTF-8, an escaped compact row or hit); 2 = the route returns None
+ * (another requestedGranularity). */
+typedef struct {
+    uint32_t row_lo, row_hi;  /* the event's request rows */
+    uint8_t granularity;      /* SB_GRAN_*; 255 = any other requestedGranularity */
+    uint8_t check_all;        /* includeResultsetResponses in {HIT, ALL} */
+    uint8_t _pad[2];
+    uint32_t assembly;        /* index into assembly_dict (assemblyId; p NULL = None) */
+    uint32_t pagination;      /* index into pagination_dict: json.dumps of {'limit': .., 'skip': ..} */
+} sb_route_event;
+
+typedef struct {
+    const sb_route_event *events;
+    size_t n_events;
+    /* per request row: its VCF and the contig index in it (NULL = the scalar) */
+    const uint32_t *row_vcf;    uint32_t vcf_all;
+    const uint32_t *row_contig; uint32_t contig_all;
+    /* the pass's outputs in host memory: compact = 0 (sb_request_partial rows,
+     * uint64 hits and row offsets) or SB_COMPACT_ALL (sb_request_row32, uint32) */
+    int32_t compact;
+    uint32_t _pad;
+    const void *rows, *hits, *row_off;
+    uint64_t rec_base;
+    const sb_str *assembly_dict;   uint32_t n_assembly;
+    const sb_str *pagination_dict; uint32_t n_pagination;
+    sb_str beacon_id, api_version; /* BEACON_ID / BEACON_API_VERSION (the envelope's meta) */
+} sb_route_input;
+
+/* *out: JSON lines (sb_json_out_get; status as above), one per event. */
+int sb_route_bodies(sb_store *s, const sb_route_input *in, sb_json_out **out);
+
 /* ---- device-resident batch (benchmarks / fused pipelines) ----------------
  * Upload a batch once, then launch the query kernels repeatedly on the
  * store's stream with inputs already resident in HBM. */

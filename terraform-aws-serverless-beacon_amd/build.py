@@ -20,7 +20,7 @@ INCLUDE = os.path.join(os.path.dirname(HERE), 'include')
 ARCH = os.environ.get('SBEACON_ARCH', 'gfx950')
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 
-SOURCES = ['api.cpp', 'requests.cpp', 'summarise.cpp', 'results.cpp', 'ingest.cpp', 'index.cpp', 'wire.cpp', 'persist.cpp', 'query_kernels.hip', 'dedup_kernels.hip']
+SOURCES = ['api.cpp', 'requests.cpp', 'summarise.cpp', 'results.cpp', 'ingest.cpp', 'index.cpp', 'wire.cpp', 'routes.cpp', 'persist.cpp', 'query_kernels.hip', 'dedup_kernels.hip']
 FLAGS = ['-O3', '-std=c++17', '-fPIC', f'--offload-arch={ARCH}', '-Wall', '-Wextra', '-Wno-unused-parameter',
          f'-I{INCLUDE}']
 
@@ -74,7 +74,7 @@ def build(verbose: bool = False) -> str:
 
 ASAN_DIR = os.path.join(BUILD, 'asan')
 ASAN_LIB = os.path.join(ASAN_DIR, 'libsbeacon_hip_asan.so')
-HOST_SOURCES = ['api.cpp', 'requests.cpp', 'summarise.cpp', 'results.cpp', 'ingest.cpp', 'index.cpp', 'wire.cpp', 'persist.cpp']
+HOST_SOURCES = ['api.cpp', 'requests.cpp', 'summarise.cpp', 'results.cpp', 'ingest.cpp', 'index.cpp', 'wire.cpp', 'routes.cpp', 'persist.cpp']
 # host code only (-Xarch_host): device code is never instrumented; the kernel
 # objects of build() are linked as they are.  SBEACON_CHECKS turns on the
 # request-plan invariant checks (api.cpp check_request_plan).

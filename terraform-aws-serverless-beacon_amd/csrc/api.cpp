@@ -1253,6 +1253,11 @@ void sync(sb_batch &B) {
         B.req->eval_used = 0;
     }
     const uint32_t e = chk ? *static_cast<volatile uint32_t *>(B.req->err_h.p) : 0u;
+    if (e) {  // reported once: the next pass of this batch (e.g. answered wide after an error) starts clean
+        HIP_OK(hipMemsetAsync(B.req->err.p, 0, 4, B.strm()));
+        HIP_OK(hipStreamSynchronize(B.strm()));
+        *static_cast<volatile uint32_t *>(B.req->err_h.p) = 0u;
+    }
     if (e & 1u)
         throw Error(SB_EINTERNAL, "request_eval_kernel: the per-chain sums of a pass failed their invariants "
                                   "(chain counts vs the wave's staged hits / exists-slices)");

@@ -413,19 +413,47 @@ std::string manifest_text(const sb_store &s, uint64_t host_bytes, uint64_t devic
 
 namespace {
 void save_files(sb_store &s, const std::string &dir);
-void remove_tree(const std::string &d) {  // a save directory: plain files only
-    if (DIR *x = opendir(d.c_str())) {
-        while (const dirent *e = readdir(x))
-            if (std::strcmp(e->d_name, ".") && std::strcmp(e->d_name, "..")) (void)unlink((d + "/" + e->d_name).c_str());
-        closedir(x);
+// the names a save directory holds (save_files): only such a directory is
+// ever removed -- a user's own DIR.tmp / DIR.old is left alone (the save fails)
+bool save_name(const char *n) {
+    return !std::strcmp(n, "manifest.json") || !std::strcmp(n, "host.bin") || !std::strcmp(n, "device.bin");
+}
+// remove a save directory (plain files named as save_files names them);
+// absent: nothing; anything else in it: SB_EIO, nothing removed
+void remove_tree(const std::string &d) {
+    DIR *x = opendir(d.c_str());
+    if (!x) {
+        struct stat st {};
+        if (lstat(d.c_str(), &st) == 0) throw Error(SB_EIO, "cannot replace " + d + ": not a store directory");
+        return;
     }
+    std::vector<std::string> names;
+    bool foreign = false;
+    while (const dirent *e = readdir(x)) {
+        if (!std::strcmp(e->d_name, ".") || !std::strcmp(e->d_name, "..")) continue;
+        if (!save_name(e->d_name)) foreign = true;
+        names.emplace_back(e->d_name);
+    }
+    closedir(x);
+    if (foreign) throw Error(SB_EIO, "refusing to remove " + d + ": it holds files a store save does not write");
+    for (const auto &n : names) (void)unlink((d + "/" + n).c_str());
     (void)rmdir(d.c_str());
+}
+// the directory entry of `path` made durable (its parent fsynced)
+void sync_parent(const std::string &path) {
+    const size_t k = path.find_last_of('/');
+    const std::string parent = k == std::string::npos ? "." : k == 0 ? "/" : path.substr(0, k);
+    const int fd = open(parent.c_str(), O_RDONLY | O_DIRECTORY);
+    if (fd < 0) return;
+    (void)fsync(fd);
+    close(fd);
 }
 }  // namespace
 
 // The three files are written into `dir.tmp` and the directory renamed into
-// place: a crash mid-save leaves the previous save (or none), never a new
-// device.bin beside an old host.bin.
+// place: a crash mid-save leaves the previous save, as `dir` or (between the
+// two renames) as `dir.old`, which store_open takes when `dir` is missing --
+// never a new device.bin beside an old host.bin.
 void store_save(sb_store &s, const std::string &dir_in) {
     std::string dir = dir_in;
     while (dir.size() > 1 && dir.back() == '/') dir.pop_back();
@@ -446,6 +474,7 @@ void store_save(sb_store &s, const std::string &dir_in) {
         if (had) (void)rename(prev.c_str(), dir.c_str());
         throw Error(SB_EIO, "cannot move " + tmp + " to " + dir);
     }
+    sync_parent(dir);
     if (had) remove_tree(prev);
 }
 
@@ -537,6 +566,13 @@ std::string store_dir(const std::string &p) {
 
 sb_store *store_open(const std::string &path, int device, std::string *stale) {
     const std::string dir = store_dir(path);
+    {  // a save interrupted between its two renames left the previous save as dir.old
+        struct stat st {};
+        const std::string prev = dir + ".old";
+        if (stat(dir.c_str(), &st) != 0 && stat((prev + "/manifest.json").c_str(), &st) == 0 &&
+            rename(prev.c_str(), dir.c_str()) == 0)
+            sync_parent(dir);
+    }
     Mapped hm(dir + "/host.bin");
     std::vector<std::pair<size_t, std::function<void()>>> host_jobs;
     Reader r;

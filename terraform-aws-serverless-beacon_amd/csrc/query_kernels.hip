@@ -4136,8 +4136,13 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
     else eval_rec(std::false_type{}, std::false_type{});
     if (ev1) (void)hipEventRecord(ev1, s);
     // record staging: the delivery sums the eval workgroup totals itself (no
-    // tile scan launch; SBEACON_REQ_TILE_SCAN=1 keeps it)
-    const bool gsum = rec_staged && !tile_scan;
+    // tile scan launch; SBEACON_REQ_TILE_SCAN=1 keeps it).  Each delivery
+    // workgroup reads every earlier group's total, so the reads grow with the
+    // square of the groups: 7.6 M words per pass at 3,906 groups (1 M
+    // requests), 4x that at twice the groups -- past kGsumMaxGroups the
+    // one-launch tile scan (linear) is cheaper than its saved launch
+    constexpr uint32_t kGsumMaxGroups = 4096;
+    const bool gsum = rec_staged && !tile_scan && n_groups <= kGsumMaxGroups;
     if (!gsum)
         hipLaunchKernelGGL(request_tile_scan_kernel, dim3(1), dim3(1024), 0, s, gtot, n_groups, tstatus, n_tiles);
     auto deliver = [&](auto kern) {

@@ -684,6 +684,10 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
     sb_store &s = *B.s;
     sb_batch::Req &R = *B.req;
     if (s.device < 0) throw Error(SB_EHIP, "the store has no device image (SB_HOST_ONLY)");
+    // every argument check before the run is marked or anything is queued: a
+    // refused run leaves the batch as it was (no run pending)
+    if (R.compact && rec_base + s.n_records > kStageCandMask)
+        throw Error(SB_EINVAL, "compact request output: record numbers (rec_base + records) reach 2^29");
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = B.strm();
     mark_run(B);
@@ -701,8 +705,6 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
         R.err_h = R.pool->get_pinned(16);
         HIP_OK(hipMemsetAsync(R.err.p, 0, 16, st));
     }
-    if (R.compact && rec_base + s.n_records > kStageCandMask)
-        throw Error(SB_EINVAL, "compact request output: record numbers (rec_base + records) reach 2^29");
     const Config cfg = config();  // (once per pass: each call reads every SBEACON_* variable)
     const bool rec_staged = s.n_records <= kStageCandMask && !cfg.req_index_stage;
     // a fixed-stride batch re-planning with record staging and no per-slice

@@ -170,6 +170,24 @@ class DedupStats(C.Structure):
                 ('path', C.c_uint32), ('windows', C.c_uint32)]
 
 
+class RouteEvent(C.Structure):
+    """sb_route_event: one /g_variants event over its request rows."""
+    _fields_ = [('row_lo', C.c_uint32), ('row_hi', C.c_uint32), ('granularity', C.c_uint8), ('check_all', C.c_uint8),
+                ('_pad', C.c_uint8 * 2), ('assembly', C.c_uint32), ('pagination', C.c_uint32)]
+
+
+class RouteInput(C.Structure):
+    """sb_route_input (include/sbeacon.h)."""
+    _fields_ = [('events', C.c_void_p), ('n_events', C.c_size_t),
+                ('row_vcf', C.c_void_p), ('vcf_all', C.c_uint32),
+                ('row_contig', C.c_void_p), ('contig_all', C.c_uint32),
+                ('compact', C.c_int32), ('_pad', C.c_uint32),
+                ('rows', C.c_void_p), ('hits', C.c_void_p), ('row_off', C.c_void_p), ('rec_base', C.c_uint64),
+                ('assembly_dict', C.c_void_p), ('n_assembly', C.c_uint32),
+                ('pagination_dict', C.c_void_p), ('n_pagination', C.c_uint32),
+                ('beacon_id', Str), ('api_version', Str)]
+
+
 DEDUP_PATHS = ('windows', 'buckets', 'radix')
 
 
@@ -256,6 +274,7 @@ SIGNATURES = {
     'sb_json_out_get': (C.c_int, [P, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
                                   C.POINTER(C.c_void_p)]),
     'sb_json_out_free': (None, [P]),
+    'sb_route_bodies': (C.c_int, [P, C.POINTER(RouteInput), C.POINTER(P)]),
 }
 
 _lib = None

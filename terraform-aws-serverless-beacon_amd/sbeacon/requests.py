@@ -378,11 +378,13 @@ class RequestBatch:
         except Exception:
             pass
 
-    def answer(self, rec_base: int = 0, device=None):
+    def answer(self, rec_base: int = 0, device=None, raw: bool = False):
         """One pass, rows + hit lists copied to the host (torch tensors on
         the store's device as staging): (rows [n, 5] int64, hits uint64,
         row_off [n + 1] int64) -- in the wide form whichever output form the
-        batch writes (compact outputs widened by widen_compact)."""
+        batch writes (compact outputs widened by widen_compact).  raw: the
+        outputs as the batch writes them, (rows, hits, row_off, compact) --
+        compact = True: [n, 4] uint32 rows, uint32 hits and offsets."""
         import torch
         dev = device if device is not None else torch.device('cuda', self.store.info()['device'])
         mode = getattr(self, 'compact', 0)
@@ -394,6 +396,8 @@ class RequestBatch:
             self.run(rows.data_ptr(), hits.data_ptr(), row_off.data_ptr(), rec_base)
             self.sync()
             ro = row_off.cpu().numpy()
+            if raw:
+                return rows[:self.n].cpu().numpy(), widen_hits(hits[:int(ro[-1])].cpu().numpy()), ro, False
             return rows[:self.n].cpu().numpy(), widen_hits(hits[:int(ro[-1])].cpu().numpy()), ro
         if mode:
             rows = torch.zeros((max(self.n, 1), 4), dtype=torch.int32, device=dev)
@@ -403,6 +407,9 @@ class RequestBatch:
             self.run(rows.data_ptr(), hits.data_ptr(), row_off.data_ptr(), rec_base)
             self.sync()
             ro = row_off.cpu().numpy().view(np.uint32)
+            if raw:
+                return (rows[:self.n].cpu().numpy().view(np.uint32), hits[:int(ro[-1])].cpu().numpy().view(np.uint32),
+                        ro, True)
             return widen_compact(rows[:self.n].cpu().numpy().view(np.uint32), hits[:int(ro[-1])].cpu().numpy(), ro)
         rows = torch.zeros((max(self.n, 1), 5), dtype=torch.int64, device=dev)
         hits = torch.zeros(max(int(self.stats()['hits']), 1), dtype=torch.int64, device=dev)
@@ -411,6 +418,8 @@ class RequestBatch:
         self.run(rows.data_ptr(), hits.data_ptr(), row_off.data_ptr(), rec_base)
         self.sync()
         ro = row_off.cpu().numpy()
+        if raw:
+            return rows[:self.n].cpu().numpy(), hits[:int(ro[-1])].cpu().numpy().view(np.uint64), ro, False
         return rows[:self.n].cpu().numpy(), hits[:int(ro[-1])].cpu().numpy().view(np.uint64), ro
 
 
