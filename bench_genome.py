@@ -242,6 +242,10 @@ def main_genome(args):
             'request_eval_kernel of a freshly prepared batch, HIP events: first and second launch after a 50 ms idle '
             'gap, and after ~8 fp32 GEMMs (a busy device); round 3 traced 0.76-0.81 ms launches in its serial '
             'delivered passes')
+        route_out, route_bodies_last = route_bodies_passes(args, store, shape, reqs, world, rank, base, dev)
+        if route_out['hits_returned'] != serial['hits_returned']:
+            raise RuntimeError(f'route bodies pass returned {route_out["hits_returned"]} hits, serial '
+                               f'{serial["hits_returned"]}')
     vals = [elapsed, kern_ms, agg['slices'], float(st['cand_loaded']), hits_avg, achieved, float(uniq), comp,
             contract, step_dev_ms, pass_ms, achieved_pass, comp_pass, comp_r04]
     if dist:
@@ -256,10 +260,17 @@ def main_genome(args):
     tot_cand = sum(v[3] for v in allv)
     tot_hits = sum(v[4] for v in allv)
     cpu = parity = None
+    if world != 1:
+        route_out = route_bodies_last = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu, parity = cpu_baseline_and_parity(args, shape, reqs, widen_rows(ex.exchange(part, hits, row_off).cpu().numpy()),
                                               widen_hits(hits.cpu().numpy()),
-                                              row_off.cpu().numpy().view(np.uint32).astype(np.int64))
+                                              row_off.cpu().numpy().view(np.uint32).astype(np.int64),
+                                              bodies=route_bodies_last)
+        if route_out is not None:
+            route_out['parity'] = parity.pop('bodies')
+        if route_bodies_last is not None:
+            route_bodies_last.free()
         # the other batches of the rotation: a smaller sample each, parity only
         parity['other_batches'] = []
         for k, b in enumerate(B[1:], start=1):
@@ -340,6 +351,7 @@ def main_genome(args):
                                       'unique records + 8 B/hit); the candidate index never reads most of them, so '
                                       'this is records covered per second, not bytes moved'},
         'delivered': delivered,
+        'route_bodies': route_out,
         'cpu_baseline': cpu,
         'parity_sample': parity,
         'ingest_s': round(t_ingest, 2),
@@ -596,7 +608,82 @@ def delivered_pipelined(args, store, shape, reqs, world, rank, base, dev, passes
                     'the timed region (digest over the widened outputs)'}
 
 
-def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20000, seed=7, timed=True):
+def route_bodies_passes(args, store, shape, reqs, world, rank, base, dev, passes=3):
+    """The drop-in at the route: Beacon /g_variants requests (the route's
+    parameters as int64 columns in host memory, one event per request) ->
+    the route's response bodies (JSON text in host memory).  Inside the timed
+    region: the rank's row range, sb_requests_prepare_beacon (SplitQueryPayload
+    per request, packing, device planning), one pass with compact outputs,
+    the D2H copies, and sb_route_bodies (route_g_variants.py:153-198 per
+    event: exists OR, distinct variant strings, one get_variant_entry per
+    distinct internal id, the result-set envelope as json.dumps writes it).
+    Returns (summary, the last pass's Bodies) -- the parity sample compares
+    those bodies with the reference fold over the oracle's responses."""
+    import numpy as np
+    import torch
+    from sbeacon.genome import LOCATION, prepare_beacon_shard, shard_rows
+    from sbeacon.route_batch import GRAN_CODE, route_bodies
+    vid = store.vcf_id(LOCATION)
+    times, split = [], np.zeros(3)
+    last = None
+    rows_h = hits_h = ro_h = None
+    for k in range(passes + 1):  # pass 0 warms the pinned buffers and the body buffer (untimed)
+        if last is not None:
+            last.free()
+            last = None
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        lo, hi = shard_rows(shape, reqs, world, rank)
+        lo, n, batch = prepare_beacon_shard(store, shape, reqs, world, rank, rows=(lo, hi))
+        batch.set_stream(torch.cuda.current_stream().cuda_stream)
+        batch.set_compact(True)
+        cap = int(batch.stats()['hits'])
+        if rows_h is None or rows_h.shape[0] < n or hits_h.shape[0] < cap:
+            rows_d = torch.empty((max(n, 1), 4), dtype=torch.int32, device=dev)
+            ro_d = torch.empty(n + 1, dtype=torch.int32, device=dev)
+            hits_d = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+            rows_h = torch.empty(rows_d.shape, dtype=torch.int32, pin_memory=True)
+            ro_h = torch.empty(ro_d.shape, dtype=torch.int32, pin_memory=True)
+            hits_h = torch.empty(hits_d.shape, dtype=torch.int32, pin_memory=True)
+        t1 = time.perf_counter()
+        batch.run(rows_d.data_ptr(), hits_d.data_ptr(), ro_d.data_ptr(), base)
+        rows_h[:n].copy_(rows_d[:n], non_blocking=True)
+        ro_h[:n + 1].copy_(ro_d[:n + 1], non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        total = int(ro_h[n].numpy().view(np.uint32))
+        hits_h[:total].copy_(hits_d[:total], non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        t2 = time.perf_counter()
+        cmap = store.__dict__['_genome_cmap'][LOCATION]
+        ev = np.arange(n + 1, dtype=np.uint32)
+        last = route_bodies(store, rows=rows_h[:n].numpy(), hits=hits_h[:total].numpy(), row_off=ro_h[:n + 1].numpy(),
+                            compact=True, rec_base=base, row_lo=ev[:n], row_hi=ev[1:], granularity=GRAN_CODE['record'],
+                            check_all=1, assembly=('GRCh38',), row_vcf=vid, row_contig=cmap[reqs.ci[lo:lo + n]])
+        t3 = time.perf_counter()
+        batch.sync()  # (the pass's invariant word; outside the timed region)
+        batch.free()
+        if k:
+            times.append(t3 - t0)
+            split += (t1 - t0, t2 - t1, t3 - t2)
+    dt = sorted(times)[len(times) // 2]
+    st = np.bincount(last.status, minlength=3)
+    out = {'requests_per_s': round(len(reqs) / dt, 1), 'ms_per_pass': round(dt * 1e3, 2),
+           'best_ms': round(min(times) * 1e3, 2), 'passes': passes,
+           'split_ms': {'prepare_upload': round(split[0] / passes * 1e3, 2),
+                        'device_pass_and_d2h': round(split[1] / passes * 1e3, 2),
+                        'route_bodies': round(split[2] / passes * 1e3, 2)},
+           'hits_returned': total, 'body_bytes': int(last.n_bytes),
+           'body_gb_per_s': round(last.n_bytes / (split[2] / passes) / 1e9, 2),
+           'events': int(n), 'status': {'body': int(st[0]), 'route_fallback': int(st[1]), 'none': int(st[2])},
+           'note': 'one GET/POST /g_variants event per request (granularity record, includeResultsetResponses HIT): '
+                   'Beacon int64 request columns in host memory -> the route\'s response bodies (json.dumps text of '
+                   'get_result_sets_response with one get_variant_entry per distinct internal id) in host memory; '
+                   'planning, the device pass (compact outputs), both D2H copies and sb_route_bodies inside the timed '
+                   'region (median pass)'}
+    return out, last
+
+
+def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20000, seed=7, timed=True, bodies=None):
     from bench import host_cores
     """C oracle (OpenMP) over a random sample of the requests, on a VCF that
     holds exactly the records those requests can reach; also checks the
@@ -670,6 +757,35 @@ def cpu_baseline_and_parity(args, shape, reqs, total, hits, row_off, n_sample=20
            'seconds': round(dt, 2), 'host_cpus': os.cpu_count()}
     parity = {'requests': len(pick), 'slice_queries': len(pl), 'mismatched_requests': bad,
               'mismatched_hit_lists': bad_hits, 'variants_checked': int(exp[:, 1].sum())}
+    if bodies is not None:
+        # the route's own fold (route_g_variants.aggregate + the result-set
+        # envelope) over the oracle's per-slice responses of each sampled
+        # request, against the body sb_route_bodies wrote for it
+        import json as _json
+        from sbeacon import responses as R
+        from sbeacon.payloads import PerformQueryResponse
+        from sbeacon.route_g_variants import _finish, aggregate
+        per = [[] for _ in range(len(pick))]
+        for o, r in zip(whole.req, res):
+            per[o].append(PerformQueryResponse(**r) if isinstance(r, dict) else r)
+        bad_b, n_entries = 0, 0
+        for j, r in enumerate(pick.tolist()):
+            if any(not isinstance(x, PerformQueryResponse) for x in per[j]):
+                bad_b += 1
+                continue
+            ex, vs, rs = aggregate(per[j], granularity='record', check_all=True, assembly_id='GRCh38')
+            want = _json.loads(_finish('record', ex, vs, rs, 'q', R.get_pagination_object(0, 100))['body'])
+            got = _json.loads(bodies.text(r)) if int(bodies.status[r]) == 0 else None
+            for b in (want, got):
+                if b is not None:
+                    for s_ in b['response']['resultSets']:
+                        s_['results'].sort(key=lambda e: e['variantInternalId'])
+            bad_b += int(got != want)
+            n_entries += len(want['response']['resultSets'][0]['results'])
+        parity['bodies'] = {'requests': len(pick), 'mismatched_bodies': bad_b, 'entries_checked': n_entries,
+                            'note': 'each sampled request\'s body from sb_route_bodies vs the reference route fold '
+                                    '(route_g_variants.aggregate + get_result_sets_response) over the C oracle\'s '
+                                    'per-slice responses; results compared as sets'}
     orc.close()
     try:
         os.remove(path)

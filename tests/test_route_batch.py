@@ -297,7 +297,8 @@ def test_route_batch_genome_matches_route():
     events = []
     for i in range(len(reqs)):
         s = int(reqs.start[i])
-        rp = {'start': [s], 'end': [s + int(reqs.width[i])], 'assemblyId': 'GRCh38',
+        w = int(reqs.width[i]) * (rng.choice([1, 6, 30]))  # (up to 3 Mb: some rows past 64 slices go per slice)
+        rp = {'start': [s], 'end': [s + w], 'assemblyId': 'GRCh38',
               'referenceName': CONTIGS[int(reqs.ci[i])], 'referenceBases': 'N',
               'variantType': VARIANT_TYPES[int(reqs.vt[i])], 'variantMinLength': int(reqs.vmin[i]),
               'variantMaxLength': int(reqs.vmax[i])}
@@ -317,6 +318,6 @@ def test_route_batch_genome_matches_route():
             assert got[i]['statusCode'] == exp['statusCode'] and got[i]['headers'] == exp['headers']
             assert _norm_body(got[i]['body']) == _norm_body(exp['body']), ev
             n_res += len(json.loads(exp['body']).get('response', {}).get('resultSets', [{}])[0].get('results', []))
-        assert n_res > 100
+        assert n_res > 50
     finally:
         engine.registry.clear()
