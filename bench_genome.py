@@ -81,12 +81,12 @@ def main_genome(args):
     # the 256 MB MALL by the time it comes round again), starting from the
     # packed requests resident in HBM -- the planning kernels run inside the
     # step (sb_requests_set_replan)
-    n_req = args.genome_requests * (world if args.scaling == 'weak' else 1)
+    n_req = step_request_count(args, world)
     stream = torch.cuda.current_stream().cuda_stream
     t0 = time.perf_counter()
     B = []
     for k in range(args.batches):
-        reqs_k = config3_requests(shape, n=n_req, seed=1003 + k)
+        reqs_k = step_requests(shape, args, world, k)
         sr, owners, base = shard_setup(shape, reqs_k, world, rank, args.deliver)  # ShardPlan routing
         batch = prepare_shard_requests(store, sr)      # request batch: packing + upload + planning (C++)
         batch.set_stream(stream)  # torch's stream: kernels, torch ops and RCCL in one order
@@ -246,8 +246,14 @@ def main_genome(args):
         if route_out['hits_returned'] != serial['hits_returned']:
             raise RuntimeError(f'route bodies pass returned {route_out["hits_returned"]} hits, serial '
                                f'{serial["hits_returned"]}')
+    # per-rank load (the first multi-GPU run shows its imbalance): rows
+    # answered, rows owned (host-facing), straddling rows sent / received
+    # by the exchange, hits staged
+    sent = sum(b - a for _, a, b in ex.sends)
+    recv = sum(n for _, _, n in ex.recvs)
     vals = [elapsed, kern_ms, agg['slices'], float(st['cand_loaded']), hits_avg, achieved, float(uniq), comp,
-            contract, step_dev_ms, pass_ms, achieved_pass, comp_pass, comp_r04]
+            contract, step_dev_ms, pass_ms, achieved_pass, comp_pass, comp_r04, float(agg['rows']), float(ex.n_own),
+            float(sent), float(recv)]
     if dist:
         t = torch.tensor(vals, dtype=torch.float64, device=dev)
         allv = [torch.zeros_like(t) for _ in range(world)]
@@ -321,6 +327,10 @@ def main_genome(args):
         'device_ms_per_step': {'step_rank0': round(r0[9], 4), 'pass_rank0': round(r0[10], 4),
                                'eval_kernel_rank0': round(r0[1], 4),
                                'eval_kernel_max': round(max(v[1] for v in allv), 4)},
+        'per_rank': [{'rank': r, 'step_ms': round(v[0] / args.steps * 1e3, 4), 'eval_kernel_ms': round(v[1], 4),
+                      'pass_ms': round(v[10], 4), 'rows': int(v[14]), 'owned_rows': int(v[15]),
+                      'straddling_rows_sent': int(v[16]), 'straddling_rows_received': int(v[17]),
+                      'hits_per_step': int(v[4]), 'slice_queries': int(v[2])} for r, v in enumerate(allv)],
         'roofline': {'bound': 'hbm', 'achieved': round(r0[5], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(r0[5] / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'kernel': 'request_eval_kernel (rank 0, the dominant kernel of the pass): HIP events around '
@@ -362,6 +372,21 @@ def main_genome(args):
         print(json.dumps(out), flush=True)
     if dist:
         dist.destroy_process_group()
+
+
+def step_request_count(args, world) -> int:
+    """Requests per step in total: args.genome_requests per GPU (weak
+    scaling: the per-GPU work is fixed as the world grows) or in total
+    (strong: the world splits a fixed batch)."""
+    return args.genome_requests * (world if args.scaling == 'weak' else 1)
+
+
+def step_requests(shape, args, world, k):
+    """Batch k of the step's rotation: genome-wide config-3 requests (seed
+    1003 + k), step_request_count of them, ordered by (contig, start); every
+    rank draws the same set and routes its part (shard_setup)."""
+    from sbeacon.genome import config3_requests
+    return config3_requests(shape, n=step_request_count(args, world), seed=1003 + k)
 
 
 def shard_setup(shape, reqs, world, rank, deliver):

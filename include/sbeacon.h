@@ -400,6 +400,16 @@ void sb_json_out_free(sb_json_out *o);
 
 typedef struct sb_batch sb_batch;
 
+/* One request row: the route-level sums of its slices' performQuery
+ * responses (lambda/getGenomicVariants/route_g_variants.py:144-171). */
+typedef struct {
+    int64_t exists;            /* slices whose response has exists = True */
+    int64_t n_variants;        /* variant strings emitted (hits) */
+    int64_t call_count;
+    int64_t all_alleles_count;
+    int64_t errors;            /* slices whose performQuery raised */
+} sb_request_partial;
+
 /* ---- split-query requests (the splitQuery fan-out in the library) ---------
  * One sb_request = one SplitQueryPayload (shared_resources/payloads/
  * lambda_payloads.py:8-44) for ONE of its vcf_locations: the VCF and the
@@ -547,15 +557,31 @@ typedef struct {
 /* Output widths of sb_requests_run.  SB_COMPACT_ALL: the narrow form a host
  * copy-back wants -- dev_rows[n] as sb_request_row32 (16 B instead of 40),
  * dev_row_off[n + 1] as uint32, and each hit as uint32 (record + rec_base) |
- * ALT label << 29; SB_EINVAL for a batch with a per-slice part.
- * SB_COMPACT_HITS: wide rows and offsets, uint32 hits as above (any batch).
- * Either: SB_EINVAL at run when record numbers reach 2^29; at sb_batch_sync,
- * SB_EINVAL when a count or offset passes 32 bits (SB_COMPACT_ALL) or a
- * per-slice hit's ALT index passes 7 (the labels 3 bits hold); the batch is
- * then answered wide.  0: wide. */
+ * ALT label << 29.  SB_COMPACT_HITS: wide rows and offsets, uint32 hits as
+ * above.  Either form holds every answer: a row the compact form cannot hold
+ * (a sum past 32 bits, a slice that raised, a count past int64) is written as
+ * {UINT32_MAX, n_variants, UINT32_MAX, UINT32_MAX} (SB_ROW32_ESCAPED) with its
+ * wide sums kept by the batch (sb_requests_wide_rows); a hit whose ALT index
+ * is 7 or more carries the label 7 (SB_HIT32_LABEL_ESCAPE) with its ALT index
+ * kept by the batch (sb_requests_hit_labels); sb_requests_escapes says whether
+ * the passes since the last sync wrote any.  Errors: SB_EINVAL at run when
+ * record numbers reach 2^29; at sb_batch_sync, SB_EINVAL when the hit
+ * offsets pass 32 bits (SB_COMPACT_ALL) or a per-slice ALT index passes 65,535.
+ * 0: wide. */
 #define SB_COMPACT_ALL 1
 #define SB_COMPACT_HITS 2
 int sb_requests_set_compact(sb_batch *b, int on);
+#define SB_ROW32_ESCAPED 0xffffffffu
+#define SB_HIT32_LABEL_ESCAPE 7u
+/* After sb_batch_sync of compact passes: *rows = 1 when some row was written
+ * escaped, *hits = 1 when some hit carries the escape label. */
+int sb_requests_escapes(sb_batch *b, int *rows, int *hits);
+/* The wide sums (sb_request_partial) of the listed rows of the last
+ * SB_COMPACT_ALL pass whose compact row is SB_ROW32_ESCAPED. */
+int sb_requests_wide_rows(sb_batch *b, const uint32_t *rows, size_t n, sb_request_partial *out);
+/* The ALT index of the listed output hit positions of the last compact pass
+ * whose label is SB_HIT32_LABEL_ESCAPE. */
+int sb_requests_hit_labels(sb_batch *b, const uint64_t *pos, size_t n, uint32_t *out);
 /* After a pass (waits for it): flags[w] = 1 when row w's call_count or
  * all_alleles_count is not exact in int64 -- a slice's count past 64 bits
  * (Python ints, records answered by the general path) or a sum that
@@ -640,13 +666,6 @@ int sb_batch_fetch(sb_batch *b, sb_result_set **out); /* D2H + host views */
  * preceding sb_batch_run, n_rows sb_request_partial rows into dev_out — a
  * device pointer on the store's device (e.g. a torch tensor's data_ptr);
  * sb_batch_sync waits for it.  Rows without a query are zero. */
-typedef struct {
-    int64_t exists;            /* slices whose response has exists = True */
-    int64_t n_variants;        /* variant strings emitted (hits) */
-    int64_t call_count;
-    int64_t all_alleles_count;
-    int64_t errors;            /* slices whose performQuery raised */
-} sb_request_partial;
 int sb_batch_set_owners(sb_batch *b, const uint32_t *owner, size_t nq, uint32_t n_rows);
 int sb_batch_reduce_requests(sb_batch *b, void *dev_out);
 /* The hit lists that go with the rows (the `variants` of each request's

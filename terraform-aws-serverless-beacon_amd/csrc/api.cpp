@@ -1258,15 +1258,16 @@ void sync(sb_batch &B) {
         HIP_OK(hipStreamSynchronize(B.strm()));
         *static_cast<volatile uint32_t *>(B.req->err_h.p) = 0u;
     }
+    if (chk) B.req->escapes = (e & kErrRowEscapes ? 1u : 0u) | (e & kErrHitEscapes ? 2u : 0u);
     if (e & 1u)
         throw Error(SB_EINTERNAL, "request_eval_kernel: the per-chain sums of a pass failed their invariants "
-                                  "(chain counts vs the wave's staged hits / exists-slices)");
+                                  "(chain counts, call counts or AN sums vs the wave's own totals)");
     if (e & 2u)
-        throw Error(SB_EINVAL, "compact request output (SB_COMPACT_ALL): a row's counts or the hit offsets "
-                               "pass 32 bits (or a chain needs wide sums); answer this batch with wide rows");
+        throw Error(SB_EINVAL, "compact request output (SB_COMPACT_ALL): the hit offsets pass 32 bits (more "
+                               "than 2^32 hits in the batch); answer this batch with wide rows");
     if (e & 4u)
-        throw Error(SB_EINVAL, "compact request hits: a per-slice hit has an ALT index past 7, which "
-                               "record | ALT << 29 cannot hold; answer this batch with wide hits");
+        throw Error(SB_EINVAL, "compact request hits: a per-slice hit has an ALT index past 65,535, which the "
+                               "label escape cannot hold; answer this batch with wide hits");
 }
 
 // each query's hit-region offset: chained slices' hits are dense per chain,

@@ -35,7 +35,7 @@ struct Config {
     bool dedup_debug = false;     // SBEACON_DEDUP_DEBUG: dedup call details (stderr)
     int dedup_bucket_dbg = 0;     // SBEACON_DEDUP_BUCKET_DBG: bucket-kernel timing ablations
     int dedup_win_dbg = 0;        // SBEACON_DEDUP_WIN_DBG: window-kernel timing ablations
-    bool req_inject = false;      // SBEACON_REQ_INJECT=1 (tests): one wrong per-chain sum, so the pass's invariants fire
+    int req_inject = 0;           // SBEACON_REQ_INJECT=1/2/3 (tests): one wrong per-chain exists / call-count / AN sum, so the pass's invariants fire
     bool req_index_stage = false; // SBEACON_REQ_INDEX_STAGE=1 (tests): stage candidate indices, as stores past 2^29 records do
     bool req_plan_apart = false;  // SBEACON_REQ_PLAN_APART=1: re-planning passes launch request_plan_kernel (no fused planning)
     bool req_tile_scan = false;   // SBEACON_REQ_TILE_SCAN=1: request_tile_scan_kernel before the delivery (no in-delivery sums)
@@ -72,7 +72,7 @@ inline Config config() {
     c.dedup_debug = flag("SBEACON_DEDUP_DEBUG");
     c.dedup_bucket_dbg = num("SBEACON_DEDUP_BUCKET_DBG", 0);
     c.dedup_win_dbg = num("SBEACON_DEDUP_WIN_DBG", 0);
-    c.req_inject = one("SBEACON_REQ_INJECT");
+    c.req_inject = num("SBEACON_REQ_INJECT", 0);
     c.req_index_stage = one("SBEACON_REQ_INDEX_STAGE");
     c.req_plan_apart = one("SBEACON_REQ_PLAN_APART");
     c.req_tile_scan = one("SBEACON_REQ_TILE_SCAN");

@@ -476,6 +476,22 @@ struct RowC {
 };
 static_assert(sizeof(RowC) == 16, "RowC is one 16-byte word");
 
+// Escapes of the compact outputs: a row the compact form cannot hold (a sum
+// past 32 bits, a raising or inexact slice) is written as
+// {kRowEscaped, n_variants, kRowEscaped, kRowEscaped} and its wide sums go to
+// xrows[row]; a u32 hit whose ALT label does not fit 3 bits, or is 7, carries
+// the label kHitLabelEscape and its ALT index goes to xlab[its output
+// position].  request_eval_kernel / request_deliver_kernel set the batch's
+// error word bits kErrRowEscapes / kErrHitEscapes when they wrote any.
+struct ReqEsc {
+    ReqPartial *xrows;        // n_rows (COMPACT_ALL batches)
+    const uint8_t *row_flag;  // inexact rows of the per-slice part (or null)
+    uint16_t *xlab;           // one label per output hit position (compact hits)
+};
+inline constexpr uint32_t kRowEscaped = 0xffffffffu;
+inline constexpr uint32_t kHitLabelEscape = 7u;
+inline constexpr uint32_t kErrRowEscapes = 8u, kErrHitEscapes = 16u;
+
 // hit = record | (alt index << 32); alt index is the label index (the GT
 // fallback labels with alts[i] for a 1-based i, search_variants.py:223)
 inline constexpr uint64_t kHitAltShift = 32;

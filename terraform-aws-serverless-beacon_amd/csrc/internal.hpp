@@ -455,6 +455,12 @@ struct sb_batch {
         // rows whose counts are not exact in int64 (sb_requests_inexact_rows):
         // per-slice wide marks + one flag per row (batches with general records)
         DevMem wide, row_flag;
+        // compact outputs' escapes (devtypes.hpp ReqEsc): the wide rows of
+        // escaped rows (SB_COMPACT_ALL; also the per-slice part's reduced rows)
+        // and the ALT index of escaped hit labels; escapes = what the passes
+        // since the last sync wrote (bit 0 rows, bit 1 hits)
+        DevMem xrows, xlab;
+        uint32_t escapes = 0;
         std::vector<char> hplan;  // host-only stores: the descriptors + runs (as dchains would hold them)
         size_t runs_at = 0;
         uint32_t run = kReqRun;        // chain slots per run (request_eval_kernel: one lane each)
@@ -462,7 +468,7 @@ struct sb_batch {
         bool slices = false;           // some rows answered per slice (the batch's query part)
         void give_back() {
             for (DevMem *m : {&dchains, &status, &tstatus, &stage, &row_src, &lut, &sseg, &sherr, &wide, &row_flag, &din,
-                              &rcap, &err})
+                              &rcap, &err, &xrows, &xlab})
                 if (m->p) pool->put_dev(std::move(*m));
             if (err_h.p) {
                 pool->put_pinned(err_h);

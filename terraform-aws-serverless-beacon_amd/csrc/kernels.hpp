@@ -113,9 +113,9 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
                          const uint32_t *sseg, const uint64_t *shoff, const uint8_t *sherr, const uint64_t *shits,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
-                         int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0 = nullptr,
-                         hipEvent_t ev1 = nullptr, const ReqIn *plan_in = nullptr, uint32_t n_in = 0,
-                         uint64_t stride = 0, bool inject = false, bool tile_scan = false);
+                         int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
+                         const ReqIn *plan_in, uint32_t n_in, uint64_t stride, int inject, bool tile_scan,
+                         const ReqEsc &esc);
 // chain slots per run (kReqRun)
 uint32_t req_run_max();
 // Request planning on the device: rows in runs of kRunRows (n_runs =

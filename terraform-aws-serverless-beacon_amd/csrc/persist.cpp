@@ -416,7 +416,9 @@ void save_files(sb_store &s, const std::string &dir);
 // the names a save directory holds (save_files): only such a directory is
 // ever removed -- a user's own DIR.tmp / DIR.old is left alone (the save fails)
 bool save_name(const char *n) {
-    return !std::strcmp(n, "manifest.json") || !std::strcmp(n, "host.bin") || !std::strcmp(n, "device.bin");
+    // (sbeacon.json: the Python layer's side file, sbeacon/engine.py Store.save)
+    return !std::strcmp(n, "manifest.json") || !std::strcmp(n, "host.bin") || !std::strcmp(n, "device.bin") ||
+           !std::strcmp(n, "sbeacon.json");
 }
 // remove a save directory (plain files named as save_files names them);
 // absent: nothing; anything else in it: SB_EIO, nothing removed

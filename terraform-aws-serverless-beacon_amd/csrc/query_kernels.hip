@@ -2087,7 +2087,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     unsigned long long *__restrict__ status, const QRes *__restrict__ sres, void *__restrict__ rows_out,
     void *__restrict__ row_cnt_out, uint64_t *__restrict__ row_src, uint32_t *__restrict__ stage, uint32_t n_lut,
     unsigned int *__restrict__ err, uint32_t inject, unsigned long long *__restrict__ gtot,
-    const ReqIn *__restrict__ in, uint32_t n_in, uint64_t stride) {
+    const ReqIn *__restrict__ in, uint32_t n_in, uint64_t stride, ReqEsc esc) {
     ReqPartial *const rows = static_cast<ReqPartial *>(rows_out);
     uint64_t *const row_cnt = static_cast<uint64_t *>(row_cnt_out);
     __shared__ ReqLds lds_all[kWavesPerBlock];
@@ -2186,6 +2186,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     uint32_t run_ex = 0; // slices with exists = True so far (wave-uniform; the invariant check)
     uint32_t acc_nv = 0, acc_ex = 0, acc_hr = 0;
     uint64_t acc_cc = 0, acc_an = 0;
+    // the wave's own totals over every chunk (wave-uniform): call count, AN
+    // and (under a common AN) hit records -- the per-chain pulls must add up
+    // to them (the invariants below)
+    uint64_t run_cc = 0, run_an = 0;
+    uint32_t run_hr = 0;
     // one instantiation per AN mode (a wave-uniform run flag): under a
     // common AN no AN column is loaded and no AN sum is scanned
     auto pass = [&](auto anc_t) {
@@ -2211,11 +2216,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         ReqChunk q;
         q.k = __builtin_amdgcn_mbcnt_hi(static_cast<uint32_t>(W1 >> 32),
                                         __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(W1), s0));
-#ifdef SBEACON_ABL_LOADS  // timing ablation only: every lane loads one cached candidate
-        const uint32_t i = i_safe + (g & 0u);
-#else
         const uint32_t i = g < T ? g + L.a[q.k].x : i_safe;
-#endif
         q.q = st.vc_q[i];
         if constexpr (ANC) q.an = 0;
         else q.an = st.vc_word[i].an;
@@ -2260,11 +2261,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         const uint32_t h0 = cand & static_cast<uint32_t>((w & 0xffu) - vlo <= vspan) & a0;
         // ALTs 2..n (:124 loop): only records whose word says an extra ALT
         // of an accepted class (or a symbolic one) might match (Bw.w = xneed)
-#ifdef SBEACON_ABL_XL  // timing ablation only (wrong answers): no extra-ALT lookups
-        const uint32_t xl = 0;
-#else
         const uint32_t xl = cand & static_cast<uint32_t>((w >> VT_NX_SHIFT) != 0) & static_cast<uint32_t>((w & Bw.w) != 0);
-#endif
         bool hit;
         uint32_t cn;      // variants emitted (ALTs with AC != 0)
         int64_t cv;       // call count contribution
@@ -2278,9 +2275,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
             const uint64_t one = __ballot(cn);
             pre = popc_below(one);
             tot = static_cast<uint32_t>(__popcll(one));
-#ifndef SBEACON_ABL_STAGE  // (timing ablation only: no staging stores)
             if (cn) hdst[hpos + pre] = q.i;
-#endif
         } else {
             uint64_t hm = h0;
             uint32_t x0 = 0;
@@ -2338,10 +2333,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         // with the position), the carry from the chunks before
         const bool pos = hit && cv > 0;
         const uint32_t key1 = pos ? (k << 20 | (x.pos - first) / kReqWidth) + 1u : 0u;
-#ifdef SBEACON_ABL_KEY  // timing ablation only: no slice-key scan
-        const uint32_t mx = key1;
-        const uint32_t scc_anc = ANC ? incl_sum_u32(static_cast<uint32_t>(cv)) : 0u;
-#else
         // (under a common AN the call-count scan runs beside the slice-key
         // scan: two independent DPP chains interleave, no wait states)
         uint32_t mx, scc_anc = 0;
@@ -2350,7 +2341,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         } else {
             mx = incl_max_u32(key1);
         }
-#endif
         const uint32_t prev = max(wave_shr1(mx), carry);
         const bool isnew = pos && key1 != prev;
         carry = max(carry, rdl(mx, kWave - 1));
@@ -2361,12 +2351,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         // no field borrows): variants (<= 8 ALTs x 64 lanes) | new slices
         // << 10 | hit records << 17 (only read under a common AN)
         uint32_t nvex = (pre + cn) | (popc_below(nb) + (isnew ? 1u : 0u)) << 10;
-        if constexpr (ANC) nvex |= (popc_below(__ballot(hit)) + (hit ? 1u : 0u)) << 17;
-#ifdef SBEACON_ABL_SUMS  // timing ablation only: no per-chain sums
-        acc_nv += nvex & 1u;
-        acc_cc += static_cast<uint64_t>(cv);
-        return;
-#endif
+        if constexpr (ANC) {
+            const uint64_t hb = __ballot(hit);
+            nvex |= (popc_below(hb) + (hit ? 1u : 0u)) << 17;
+            run_hr += static_cast<uint32_t>(__popcll(hb));
+        }
         // ---- chain k's part of the chunk, pulled by lane k from its last lane
         const uint32_t lim = min(base + kWave, T);
         const bool inter = pex < lim && pin > base;
@@ -2383,6 +2372,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
             const uint32_t pc = bperm(scc, e);
             const uint32_t qc = wave_shr1(pc);
             if (inter) acc_cc += pc - (opens ? 0u : qc);
+            run_cc += rdl(scc, kWave - 1);  // (the invariants: the chunk's call-count total)
             return;
         }
         const bool big = !narrow &&
@@ -2395,6 +2385,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
                 acc_cc += pc - (opens ? 0u : qc);
                 acc_an += pa - (opens ? 0u : qa);
             }
+            run_cc += rdl(scc, kWave - 1);
+            run_an += rdl(san, kWave - 1);
         } else {
             const uint64_t scc = incl_sum_u64(static_cast<uint64_t>(cv)),
                            san = incl_sum_u64(static_cast<uint64_t>(static_cast<int64_t>(static_cast<int32_t>(anv))));
@@ -2404,13 +2396,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
                 acc_cc += pc - (opens ? 0ull : qc);
                 acc_an += pa - (opens ? 0ull : qa);
             }
+            run_cc += static_cast<uint64_t>(rdl64(static_cast<int64_t>(scc), kWave - 1));
+            run_an += static_cast<uint64_t>(rdl64(static_cast<int64_t>(san), kWave - 1));
         }
     };
-#ifdef SBEACON_ABL_NOCHUNK  // timing ablation only: setup and epilogue without the candidate loop
-    if (false) {
-#else
     if (nch) {
-#endif
         // The prefetch is unconditional (past the run a load reads the valid
         // index i_safe, one cache line): every path of the steady loop then
         // issues the same loads, so the wait-counter pass can wait for chunk
@@ -2436,7 +2426,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     if (anc) pass(std::true_type{});
     else pass(std::false_type{});
     wave_lds_sync();
-    if (inject && w == 0 && ul == 0) ++acc_ex;  // (tests, SBEACON_REQ_INJECT: the checks below must fire)
+    // (tests, SBEACON_REQ_INJECT=1/2/3: one chain's exists-slice count, call
+    // count or AN pull perturbed -- the checks below must fire)
+    if (inject && w == 0 && ul == 0) {
+        if (inject == 1) ++acc_ex;
+        else if (inject == 2) ++acc_cc;
+        else if (anc) ++acc_hr;
+        else ++acc_an;
+    }
     // the run's rows staged over the candidate-loop LDS (a, b, wch: dead now)
     ReqPartial *const srow = reinterpret_cast<ReqPartial *>(&L.a[0]);
     if constexpr (!COMPACT) {
@@ -2456,10 +2453,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     {
         const uint32_t ex_tot = rdl(incl_sum_u32(acc_ex), kWave - 1);
         const bool bad_lane = acc_ex > acc_nv || (anc && acc_ex > acc_hr);
-#if !defined(SBEACON_ABL_XL) && !defined(SBEACON_ABL_KEY) && !defined(SBEACON_ABL_SUMS) && !defined(SBEACON_ABL_LOADS)
-        if (rdl(cs_incl, kWave - 1) != hpos || ex_tot != run_ex || __ballot(bad_lane))
+        // the call-count and AN pulls (the same cross-lane primitives) against
+        // the wave's chunk totals: one 64-bit wave sum each per run
+        const uint64_t cc_tot = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(acc_cc)), kWave - 1));
+        const uint64_t an_tot = anc ? static_cast<uint64_t>(rdl(incl_sum_u32(acc_hr), kWave - 1))
+                                    : static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(acc_an)), kWave - 1));
+        if (rdl(cs_incl, kWave - 1) != hpos || ex_tot != run_ex || __ballot(bad_lane) || cc_tot != run_cc ||
+            an_tot != (anc ? static_cast<uint64_t>(run_hr) : run_an))
             if (ul == 0) atomicOr(err, 1u);
-#endif
         // (PLAN: the run's hits within its fixed-stride staging region; never
         // past it, the stride was sized on these requests)
         if (PLAN && hpos > stride && ul == 0) atomicOr(err, 1u);
@@ -2468,10 +2469,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         const bool slow = (L.slow[ul >> 5] >> (ul & 31u)) & 1u;  // never for prepared chains
         const uint64_t an_sum = anc ? static_cast<uint64_t>(acc_hr) * an_c : acc_an;
         if constexpr (COMPACT) {
-            // (counts past 32 bits or a slow chain: the batch fails at sync, SB_EINVAL)
-            if (slow || acc_cc > 0xffffffffull || an_sum > 0xffffffffull) atomicOr(err, 2u);
-            static_cast<RowC *>(rows_out)[rowk] = RowC{acc_ex, acc_nv, static_cast<uint32_t>(acc_cc),
-                                                       static_cast<uint32_t>(an_sum)};
+            // counts past 32 bits or a slow chain: the row escapes (its wide
+            // sums in xrows, the compact row marked)
+            if (slow || acc_cc > 0xffffffffull || an_sum > 0xffffffffull) {
+                esc.xrows[rowk] = slow ? ReqPartial{0, static_cast<int64_t>(acc_nv), 0, 0, static_cast<int64_t>(nsl)}
+                                       : ReqPartial{static_cast<int64_t>(acc_ex), static_cast<int64_t>(acc_nv),
+                                                    static_cast<int64_t>(acc_cc), static_cast<int64_t>(an_sum), 0};
+                static_cast<RowC *>(rows_out)[rowk] = RowC{kRowEscaped, acc_nv, kRowEscaped, kRowEscaped};
+                atomicOr(err, kErrRowEscapes);
+            } else {
+                static_cast<RowC *>(rows_out)[rowk] = RowC{acc_ex, acc_nv, static_cast<uint32_t>(acc_cc),
+                                                           static_cast<uint32_t>(an_sum)};
+            }
         } else {
             const ReqPartial rp = slow ? ReqPartial{0, static_cast<int64_t>(acc_nv), 0, 0, static_cast<int64_t>(nsl)}
                                        : ReqPartial{static_cast<int64_t>(acc_ex), static_cast<int64_t>(acc_nv),
@@ -2500,11 +2509,28 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     const uint32_t ch = ul < nrows ? L.rowchain[ul] : 0xffu;
     const uint32_t chn = bperm(acc_nv, ch & 63u), chs = bperm(cs, ch & 63u);
     uint64_t nvr = 0;
-    if constexpr (COMPACT) {  // no per-slice part: a row without a chain has no slice (or no candidate)
+    if constexpr (COMPACT) {
         if (ul < nrows) {
-            nvr = ch != 0xffu ? chn : 0u;
-            if (ch == 0xffu) static_cast<RowC *>(rows_out)[row] = RowC{0, 0, 0, 0};
+            if (ch != 0xffu) {
+                nvr = chn;
+            } else if (sres) {  // a row answered per slice: its wide sums (request_reduce_kernel wrote xrows)
+                const ReqPartial p = esc.xrows[row];
+                const bool fits = !(esc.row_flag && esc.row_flag[row]) && p.errors == 0 && p.exists >= 0 &&
+                                  p.exists < kRowEscaped && p.n_variants >= 0 && p.call_count >= 0 &&
+                                  p.call_count <= 0xffffffffll && p.all_alleles_count >= 0 &&
+                                  p.all_alleles_count <= 0xffffffffll;
+                nvr = static_cast<uint64_t>(p.n_variants);
+                static_cast<RowC *>(rows_out)[row] =
+                    fits ? RowC{static_cast<uint32_t>(p.exists), static_cast<uint32_t>(nvr),
+                                static_cast<uint32_t>(p.call_count), static_cast<uint32_t>(p.all_alleles_count)}
+                         : RowC{kRowEscaped, static_cast<uint32_t>(nvr), kRowEscaped, kRowEscaped};
+                if (!fits) atomicOr(err, kErrRowEscapes);
+                if (nvr > 0xffffffffull) atomicOr(err, 2u);  // (the u32 offsets cannot hold it)
+            } else {  // no slice (or no candidate)
+                static_cast<RowC *>(rows_out)[row] = RowC{0, 0, 0, 0};
+            }
             static_cast<uint32_t *>(row_cnt_out)[row] = static_cast<uint32_t>(nvr);
+            if (!simple && ch != 0xffu) row_src[row] = stage_at + chs;
         }
     } else {
         if (ul < nrows) nvr = ch != 0xffu ? chn : (sres ? static_cast<uint64_t>(rows[row].n_variants) : 0ull);
@@ -2799,7 +2825,7 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr, const uint64_t *__restrict__ shits,
     void *__restrict__ row_off_out, const uint64_t *__restrict__ row_src, const uint32_t *__restrict__ stage,
     const uint32_t *__restrict__ vc_idx, void *__restrict__ out_v, uint32_t n_rows, uint64_t rec_base,
-    unsigned int *__restrict__ err, const unsigned long long *__restrict__ gtot) {
+    unsigned int *__restrict__ err, const unsigned long long *__restrict__ gtot, ReqEsc esc) {
     using Hit = std::conditional_t<HITC, uint32_t, uint64_t>;
     using Off = std::conditional_t<ROWC, uint32_t, uint64_t>;
     Hit *const out = static_cast<Hit *>(out_v);
@@ -2885,15 +2911,22 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
             Hit h[kU];
 #pragma unroll
             for (uint32_t u = 0; u < kU; ++u) h[u] = hit_of(v[u]);
+            bool lab7 = false;  // HITC: the label 7 is the escape -- an 8-ALT record's last ALT goes to xlab too
 #pragma unroll
             for (uint32_t u = 0; u < kU; ++u) {
                 const uint64_t j = j0 + kWave * u + ul;
-                if (j < H) out[O + j] = h[u];
+                if (j < H) {
+                    out[O + j] = h[u];
+                    if (HITC && (v[u] >> kStageAltShift) == kHitLabelEscape) {
+                        esc.xlab[O + j] = static_cast<uint16_t>(kHitLabelEscape);
+                        lab7 = true;
+                    }
+                }
             }
+            if (HITC && __ballot(lab7) && ul == 0) atomicOr(err, kErrHitEscapes);
         }
         return;
     }
-    if constexpr (ROWC) return;  // (compact-row batches have no per-slice part: every run is simple)
     for (uint32_t i = 0; i < row_hi - row_lo; ++i) {  // row by row (some rows answered per slice)
         const uint64_t nv = static_cast<uint64_t>(rdl64(static_cast<int64_t>(c), i));
         if (!nv) continue;
@@ -2902,24 +2935,43 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
         const uint32_t q0 = uniform(sseg[r]), q1 = uniform(sseg[r + 1]);
         if (q1 == q0) {  // a chain row: its hits are contiguous in the staging region
             const uint64_t src = uniform64(row_src[r]);
-            for (uint64_t k = ul; k < nv; k += kWave) out[at + k] = hit_of(stage[src + k]);
+            bool lab7 = false;
+            for (uint64_t k = ul; k < nv; k += kWave) {
+                const uint32_t v = stage[src + k];
+                out[at + k] = hit_of(v);
+                if (HITC && (v >> kStageAltShift) == kHitLabelEscape) {
+                    esc.xlab[at + k] = static_cast<uint16_t>(kHitLabelEscape);
+                    lab7 = true;
+                }
+            }
+            if (HITC && __ballot(lab7) && ul == 0) atomicOr(err, kErrHitEscapes);
         } else {
             uint64_t dst = at;
             for (uint32_t q = q0; q < q1; ++q) {
                 const QRes rq = sres[q];
                 if (rq.error || sherr[q]) continue;
                 const uint64_t src = shoff[q];
-                bool wide_alt = false;  // HITC: an ALT label the u32 hit cannot hold (> VT_MAX_NX)
+                // HITC: an ALT label of 7 or more escapes (label 7, the index
+                // in xlab); past 65,535 the side table cannot hold it (the batch fails)
+                bool escd = false, wide_alt = false;
                 for (uint32_t k = ul; k < rq.n_hits; k += kWave) {
                     const uint64_t h = shits[src + k];  // record | ALT << kHitAltShift
                     if constexpr (HITC) {
-                        wide_alt |= (h >> kHitAltShift) > VT_MAX_NX;
+                        const uint64_t a = h >> kHitAltShift;
+                        const bool x = a >= kHitLabelEscape;
+                        escd |= x;
+                        wide_alt |= a > 0xffffu;
+                        if (x) esc.xlab[dst + k] = static_cast<uint16_t>(a);
                         out[dst + k] = (static_cast<uint32_t>(h) + static_cast<uint32_t>(rec_base)) |
-                                       static_cast<uint32_t>(h >> kHitAltShift) << kStageAltShift;
+                                       static_cast<uint32_t>(x ? kHitLabelEscape : a) << kStageAltShift;
                     } else
                         out[dst + k] = h + rec_base;
                 }
-                if (HITC && __ballot(wide_alt) && ul == 0) atomicOr(err, 4u);
+                if constexpr (HITC) {
+                    const bool any_x = __ballot(escd) != 0, any_w = __ballot(wide_alt) != 0;
+                    if (ul == 0 && any_x) atomicOr(err, kErrHitEscapes);
+                    if (ul == 0 && any_w) atomicOr(err, 4u);
+                }
                 dst += rq.n_hits;
             }
         }
@@ -4103,7 +4155,8 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
                          ReqPartial *rows, uint64_t *row_off, uint64_t *row_src, uint32_t *stage, uint64_t *out,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
                          int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
-                         const ReqIn *plan_in, uint32_t n_in, uint64_t stride, bool inject, bool tile_scan) {
+                         const ReqIn *plan_in, uint32_t n_in, uint64_t stride, int inject, bool tile_scan,
+                         const ReqEsc &esc) {
     const bool rowc = compact == SB_COMPACT_ALL, hitc = compact != 0;  // u32 rows / offsets; u32 hits
     if (!n_runs) {
         (void)hipMemsetAsync(row_off, 0, rowc ? 4 : 8, s);
@@ -4116,7 +4169,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
     auto eval = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, st, chains, runs, n_runs, status, sres,
                            static_cast<void *>(rows), static_cast<void *>(row_off), row_src, stage, n_lut, err,
-                           static_cast<uint32_t>(inject), gtot, plan_in, n_in, stride);
+                           static_cast<uint32_t>(inject), gtot, plan_in, n_in, stride, esc);
     };
     (void)run;
     auto eval_rec = [&](auto rec, auto plan) {
@@ -4148,7 +4201,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
     auto deliver = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg, shoff, sherr,
                            shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx, static_cast<void *>(out),
-                           n_rows, rec_base, err, gtot);
+                           n_rows, rec_base, err, gtot, esc);
     };
     auto deliver_rec = [&](auto rec, auto gs) {
         constexpr bool R = decltype(rec)::value, G = decltype(gs)::value;

@@ -690,6 +690,9 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
         throw Error(SB_EINVAL, "compact request output: record numbers (rec_base + records) reach 2^29");
     HIP_OK(hipSetDevice(s.device));
     hipStream_t st = B.strm();
+    // the compact forms' escape buffers (devtypes.hpp ReqEsc), once per batch
+    if (R.compact == SB_COMPACT_ALL && !R.xrows.p) R.xrows = R.pool->get_dev(std::max<size_t>(R.n_rows, 1) * sizeof(ReqPartial));
+    if (R.compact && !R.xlab.p) R.xlab = R.pool->get_dev(std::max<uint64_t>(R.cap, 1) * sizeof(uint16_t));
     mark_run(B);
     if (R.slices) {  // the per-slice part, then its rows (chain rows come out zero; the row kernel writes them)
         run_kernels(B);
@@ -697,8 +700,12 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
             HIP_OK(hipMemsetAsync(R.wide.p, 0, B.nq, st));
             mark_wide(B.gen_big_n.as<uint32_t>(), B.gen_big.as<GenBig>(), B.gen_big_cap, R.wide.as<uint8_t>(), st);
         }
+        // (compact rows: the wide sums go to xrows; request_eval_kernel
+        // narrows each row or marks it escaped)
         launch_request_reduce(B.res.as<QRes>(), R.sseg.as<uint32_t>(), R.sherr.as<uint8_t>(), R.wide.as<uint8_t>(),
-                              R.n_rows, static_cast<ReqPartial *>(rows), R.row_flag.as<uint8_t>(), st);
+                              R.n_rows,
+                              R.compact == SB_COMPACT_ALL ? R.xrows.as<ReqPartial>() : static_cast<ReqPartial *>(rows),
+                              R.row_flag.as<uint8_t>(), st);
     }
     if (!R.err.p) {
         R.err = R.pool->get_dev(16);
@@ -738,7 +745,7 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
                         R.stage.as<uint32_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
                         R.err.as<unsigned int>(), R.compact, rec_staged, st, ev[0], ev[1],
                         fuse ? R.din.as<ReqIn>() : nullptr, R.n_in, R.stage_stride, cfg.req_inject,
-                        cfg.req_tile_scan);
+                        cfg.req_tile_scan, ReqEsc{R.xrows.as<ReqPartial>(), R.row_flag.as<uint8_t>(), R.xlab.as<uint16_t>()});
     HIP_OK(hipGetLastError());
 }
 
@@ -954,11 +961,68 @@ int sb_requests_set_compact(sb_batch *b, int on) {
         if (!b || !b->req) throw Error(SB_EINVAL, "not a request batch");
         if (on != 0 && on != SB_COMPACT_ALL && on != SB_COMPACT_HITS)
             throw Error(SB_EINVAL, "sb_requests_set_compact: mode 0, SB_COMPACT_ALL or SB_COMPACT_HITS");
-        if (on == SB_COMPACT_ALL && b->req->slices)
-            throw Error(SB_EINVAL, "sb_requests_set_compact: the batch answers some rows per slice (wide rows only)");
         std::lock_guard<std::mutex> lk(b->mu);
         if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_set_compact between a run and its sync");
         b->req->compact = on;
+    });
+}
+
+int sb_requests_escapes(sb_batch *b, int *rows, int *hits) {
+    return guard([&] {
+        if (!b || !b->req || !rows || !hits) throw Error(SB_EINVAL, "not a request batch");
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_escapes between a run and its sync");
+        *rows = b->req->escapes & 1u ? 1 : 0;
+        *hits = b->req->escapes & 2u ? 1 : 0;
+    });
+}
+
+extern "C++" {
+// n entries of `width` bytes at the given indexes of a device buffer: one
+// copy each when few, else the whole buffer once
+template <class Idx>
+void gather_down(const DevMem &m, size_t width, size_t count, const Idx *idx, size_t n, void *out, hipStream_t st) {
+    if (!n) return;
+    for (size_t i = 0; i < n; ++i)
+        if (static_cast<uint64_t>(idx[i]) >= count) throw Error(SB_EINVAL, "index past the batch's output");
+    char *o = static_cast<char *>(out);
+    if (n <= 64) {
+        for (size_t i = 0; i < n; ++i)
+            HIP_OK(hipMemcpyAsync(o + i * width, m.as<char>() + static_cast<uint64_t>(idx[i]) * width, width,
+                                  hipMemcpyDeviceToHost, st));
+        HIP_OK(hipStreamSynchronize(st));
+        return;
+    }
+    std::vector<char> all(count * width);
+    HIP_OK(hipMemcpyAsync(all.data(), m.p, all.size(), hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    for (size_t i = 0; i < n; ++i) std::memcpy(o + i * width, all.data() + static_cast<uint64_t>(idx[i]) * width, width);
+}
+}  // extern "C++"
+
+int sb_requests_wide_rows(sb_batch *b, const uint32_t *rows, size_t n, sb_request_partial *out) {
+    return guard([&] {
+        if (!b || !b->req || ((!rows || !out) && n)) throw Error(SB_EINVAL, "NULL argument");
+        sb_batch::Req &R = *b->req;
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_wide_rows between a run and its sync");
+        if (!R.xrows.p) throw Error(SB_EINVAL, "sb_requests_wide_rows: no SB_COMPACT_ALL pass on this batch");
+        HIP_OK(hipSetDevice(b->s->device));
+        gather_down(R.xrows, sizeof(ReqPartial), R.n_rows, rows, n, out, b->strm());
+    });
+}
+
+int sb_requests_hit_labels(sb_batch *b, const uint64_t *pos, size_t n, uint32_t *out) {
+    return guard([&] {
+        if (!b || !b->req || ((!pos || !out) && n)) throw Error(SB_EINVAL, "NULL argument");
+        sb_batch::Req &R = *b->req;
+        std::lock_guard<std::mutex> lk(b->mu);
+        if (b->runs_pending) throw Error(SB_EINVAL, "sb_requests_hit_labels between a run and its sync");
+        if (!R.xlab.p) throw Error(SB_EINVAL, "sb_requests_hit_labels: no compact pass on this batch");
+        HIP_OK(hipSetDevice(b->s->device));
+        std::vector<uint16_t> lab(n);
+        gather_down(R.xlab, sizeof(uint16_t), std::max<uint64_t>(R.cap, 1), pos, n, lab.data(), b->strm());
+        for (size_t i = 0; i < n; ++i) out[i] = lab[i];
     });
 }
 

@@ -266,6 +266,9 @@ SIGNATURES = {
     'sb_requests_plan_fused': (C.c_int, [P, C.POINTER(C.c_int)]),
     'sb_requests_set_compact': (C.c_int, [P, C.c_int]),
     'sb_requests_inexact_rows': (C.c_int, [P, P]),
+    'sb_requests_escapes': (C.c_int, [P, C.POINTER(C.c_int), C.POINTER(C.c_int)]),
+    'sb_requests_wide_rows': (C.c_int, [P, C.c_void_p, C.c_size_t, C.c_void_p]),
+    'sb_requests_hit_labels': (C.c_int, [P, C.c_void_p, C.c_size_t, C.c_void_p]),
     'sb_store_trim': (C.c_int, [P]),
     'sb_store_save': (C.c_int, [P, C.c_char_p]),
     'sb_store_open': (C.c_int, [C.c_char_p, C.c_int, C.POINTER(C.c_void_p)]),

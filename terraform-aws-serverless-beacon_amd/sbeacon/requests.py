@@ -352,6 +352,36 @@ class RequestBatch:
         check(lib().sb_requests_set_compact(self._h, mode))
         self.compact = mode
 
+    def escape_flags(self) -> tuple[bool, bool]:
+        """(rows escaped, hit labels escaped) by the compact passes up to the
+        last sync (sb_requests_escapes)."""
+        r, h = C.c_int(), C.c_int()
+        check(lib().sb_requests_escapes(self._h, C.byref(r), C.byref(h)))
+        return bool(r.value), bool(h.value)
+
+    def escapes(self, rows32=None, hits32=None):
+        """After a compact pass and its sync: the answers the compact form
+        could not hold (sb_requests_escapes).  Returns (wide, labels):
+        wide = (row indices, [k, 5] int64 wide rows) of the rows written as
+        SB_ROW32_ESCAPED, labels = (hit positions, ALT indices) of the hits
+        with the escape label -- either None when the passes wrote none."""
+        r, h = C.c_int(), C.c_int()
+        check(lib().sb_requests_escapes(self._h, C.byref(r), C.byref(h)))
+        wide = labels = None
+        if r.value and rows32 is not None:
+            idx = np.ascontiguousarray(np.flatnonzero(np.asarray(rows32).view(np.uint32).reshape(-1, 4)[:, 0] ==
+                                                      ROW32_ESCAPED), dtype=np.uint32)
+            out = np.zeros((len(idx), 5), dtype=np.int64)
+            check(lib().sb_requests_wide_rows(self._h, idx.ctypes.data, len(idx), out.ctypes.data))
+            wide = (idx, out)
+        if h.value and hits32 is not None:
+            pos = np.ascontiguousarray(np.flatnonzero((np.asarray(hits32).view(np.uint32) >> 29) == HIT32_LABEL_ESCAPE),
+                                       dtype=np.uint64)
+            lab = np.zeros(len(pos), dtype=np.uint32)
+            check(lib().sb_requests_hit_labels(self._h, pos.ctypes.data, len(pos), lab.ctypes.data))
+            labels = (pos, lab)
+        return wide, labels
+
     def inexact_rows(self) -> np.ndarray:
         """After a pass: True for rows whose call_count / all_alleles_count
         are not exact in int64 (low 64 bits held; sb_requests_inexact_rows)."""
@@ -396,9 +426,9 @@ class RequestBatch:
             self.run(rows.data_ptr(), hits.data_ptr(), row_off.data_ptr(), rec_base)
             self.sync()
             ro = row_off.cpu().numpy()
-            if raw:
-                return rows[:self.n].cpu().numpy(), widen_hits(hits[:int(ro[-1])].cpu().numpy()), ro, False
-            return rows[:self.n].cpu().numpy(), widen_hits(hits[:int(ro[-1])].cpu().numpy()), ro
+            h32 = hits[:int(ro[-1])].cpu().numpy()
+            _, labels = self.escapes(None, h32)
+            return (rows[:self.n].cpu().numpy(), widen_hits(h32, labels), ro) + ((False,) if raw else ())
         if mode:
             rows = torch.zeros((max(self.n, 1), 4), dtype=torch.int32, device=dev)
             hits = torch.zeros(max(int(self.stats()['hits']), 1), dtype=torch.int32, device=dev)
@@ -407,10 +437,13 @@ class RequestBatch:
             self.run(rows.data_ptr(), hits.data_ptr(), row_off.data_ptr(), rec_base)
             self.sync()
             ro = row_off.cpu().numpy().view(np.uint32)
-            if raw:
-                return (rows[:self.n].cpu().numpy().view(np.uint32), hits[:int(ro[-1])].cpu().numpy().view(np.uint32),
-                        ro, True)
-            return widen_compact(rows[:self.n].cpu().numpy().view(np.uint32), hits[:int(ro[-1])].cpu().numpy(), ro)
+            r32 = rows[:self.n].cpu().numpy().view(np.uint32)
+            h32 = hits[:int(ro[-1])].cpu().numpy().view(np.uint32)
+            wide, labels = self.escapes(r32, h32)
+            if raw and wide is None and labels is None:
+                return r32, h32, ro, True
+            out = widen_compact(r32, h32, ro, wide=wide, labels=labels)
+            return out + (False,) if raw else out
         rows = torch.zeros((max(self.n, 1), 5), dtype=torch.int64, device=dev)
         hits = torch.zeros(max(int(self.stats()['hits']), 1), dtype=torch.int64, device=dev)
         row_off = torch.zeros(self.n + 1, dtype=torch.int64, device=dev)
@@ -423,24 +456,37 @@ class RequestBatch:
         return rows[:self.n].cpu().numpy(), hits[:int(ro[-1])].cpu().numpy().view(np.uint64), ro
 
 
-def widen_hits(hits32):
+ROW32_ESCAPED = 0xffffffff  # SB_ROW32_ESCAPED
+HIT32_LABEL_ESCAPE = 7       # SB_HIT32_LABEL_ESCAPE
+
+
+def widen_hits(hits32, labels=None):
     """uint32 hits ((record + rec_base) | ALT label << 29) as the wide form's
-    uint64 record | ALT label << 32."""
+    uint64 record | ALT label << 32; labels = (positions, ALT indices) of the
+    escaped labels (RequestBatch.escapes)."""
     h = np.asarray(hits32).view(np.uint32).astype(np.uint64)
-    return (h & np.uint64((1 << 29) - 1)) | ((h >> np.uint64(29)) << np.uint64(32))
+    out = (h & np.uint64((1 << 29) - 1)) | ((h >> np.uint64(29)) << np.uint64(32))
+    if labels is not None:
+        pos, lab = labels
+        out[pos] = (out[pos] & np.uint64(0xffffffff)) | (np.asarray(lab, dtype=np.uint64) << np.uint64(32))
+    return out
 
 
-def widen_rows(rows32):
+def widen_rows(rows32, wide=None):
     """Compact rows (sb_request_row32: u32 exists, n_variants, call_count,
-    all_alleles_count) as the wide [n, 5] int64 rows with a zero error count."""
+    all_alleles_count) as the wide [n, 5] int64 rows with a zero error count;
+    wide = (row indices, wide rows) of the escaped rows (RequestBatch.escapes)."""
     rows32 = np.asarray(rows32).view(np.uint32).reshape(-1, 4)
     rows = np.zeros((len(rows32), 5), dtype=np.int64)
     rows[:, :4] = rows32
+    if wide is not None:
+        idx, w = wide
+        rows[np.asarray(idx, dtype=np.int64)] = w
     return rows
 
 
-def widen_compact(rows32, hits32, row_off32):
+def widen_compact(rows32, hits32, row_off32, wide=None, labels=None):
     """Compact request outputs (sb_requests_set_compact) in the wide form:
     (rows [n, 5] int64 with a zero error count, hits uint64 = record | ALT
-    label << 32, row_off int64)."""
-    return widen_rows(rows32), widen_hits(hits32), np.asarray(row_off32).view(np.uint32).astype(np.int64)
+    label << 32, row_off int64), escapes resolved (RequestBatch.escapes)."""
+    return widen_rows(rows32, wide), widen_hits(hits32, labels), np.asarray(row_off32).view(np.uint32).astype(np.int64)

@@ -29,7 +29,22 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, tmp, mode, compact, q):
+def _step_requests(shape, world, scaling):
+    """The bench's step requests (bench_genome.step_requests: 300 per GPU
+    under weak scaling, 300 in total under strong) plus requests straddling
+    every shard cut (their rows travel to the first slice's rank)."""
+    import argparse
+    from bench_genome import step_requests
+    from sbeacon.genome import Requests
+    a = step_requests(shape, argparse.Namespace(genome_requests=300, scaling=scaling), world, 0)
+    b = _requests_straddling(shape, world)
+    r = Requests(*(np.concatenate([getattr(a, f), getattr(b, f)]) for f in ('ci', 'start', 'width', 'vt', 'vmin',
+                                                                          'vmax')))
+    o = np.lexsort((r.start, r.ci))
+    return Requests(r.ci[o], r.start[o], r.width[o], r.vt[o], r.vmin[o], r.vmax[o])
+
+
+def _worker(rank, world, port, tmp, mode, compact, scaling, q):
     for p in (REPO, PKG, os.path.dirname(__file__)):
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -41,7 +56,7 @@ def _worker(rank, world, port, tmp, mode, compact, q):
         from sbeacon.genome import shard_slices, slice_payloads
         from sbeacon.shard import ResultExchange
         shape = _shape()
-        reqs = _requests_straddling(shape, world)
+        reqs = _step_requests(shape, world, scaling)
         sr, owners, base = shard_setup(shape, reqs, world, rank, mode)
         path = _write(os.path.join(tmp, f'b{world}_{rank}.vcf'), shape.shard_chunks(world, rank))
         sl = shard_slices(shape, reqs, world, rank)
@@ -96,14 +111,15 @@ def _worker(rank, world, port, tmp, mode, compact, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('compact', [False, True])
+@pytest.mark.parametrize('compact,scaling', [(False, 'weak'), (True, 'weak'), (True, 'strong')])
 @pytest.mark.parametrize('mode', ['first', 'rank0'])
-def test_bench_step_world2_matches_unsharded_oracle(mode, compact):
+def test_bench_step_world2_matches_unsharded_oracle(mode, compact, scaling):
     from oracle.oracle import OracleVcf
     from sbeacon.genome import shard_slices, slice_payloads
     world = 2
     shape = _shape()
-    reqs = _requests_straddling(shape, world)
+    reqs = _step_requests(shape, world, scaling)
+    assert len(reqs) == 300 * (world if scaling == 'weak' else 1) + len(_requests_straddling(shape, world))
     with tempfile.TemporaryDirectory() as tmp:
         full = _write(os.path.join(tmp, 'full.vcf'), shape.shard_chunks(1, 0))
         whole = shard_slices(shape, reqs, 1, 0)
@@ -112,7 +128,8 @@ def test_bench_step_world2_matches_unsharded_oracle(mode, compact):
         ctx = mp.get_context('spawn')
         q = ctx.Queue()
         port = _free_port()
-        procs = [ctx.Process(target=_worker, args=(r, world, port, tmp, mode, compact, q)) for r in range(world)]
+        procs = [ctx.Process(target=_worker, args=(r, world, port, tmp, mode, compact, scaling, q))
+                 for r in range(world)]
         for p in procs:
             p.start()
         got = [q.get(timeout=300) for _ in range(world)]

@@ -119,10 +119,12 @@ def test_index_staged_hits_match(fixture, monkeypatch):
     store's records fit 29 bits) or, for larger stores, as its candidate
     index that request_deliver_kernel maps through vc_idx: the index form,
     forced with SBEACON_REQ_INDEX_STAGE (a test hook), gives the same rows
-    and hit lists, full-width and compact."""
+    and hit lists, full-width and compact.  Compact outputs hold every
+    answer: rows that do not fit u32 (raising slices, general records) and
+    ALT labels past 6 escape (sb_requests_escapes), and the widened outputs
+    equal the wide ones -- general22 has hits on ALT indexes past 7."""
     from payload_gen import read_records
     from sbeacon.engine import Store
-    from sbeacon._lib import SB_EINVAL, SbError
     from sbeacon.requests import COMPACT_ALL, COMPACT_HITS, RequestBatch, requests_from_split_payloads
     path = os.path.join(FIXTURES, fixture + '.vcf')
     store = Store.build([(fixture + '.vcf', path)], device=0)
@@ -131,24 +133,19 @@ def test_index_staged_hits_match(fixture, monkeypatch):
     sps = [_split_payload(rng, recs, names, fixture + '.vcf') for _ in range(300)]
     arr, keep, owners = requests_from_split_payloads(store, sps)  # keep: the buffers arr points into
     exp_rows, exp_hits, _ = _expected(store, sps)
-    # u32 hits hold ALT labels 0..7: a per-slice hit past that fails the batch (SB_EINVAL), never a cut label
+    # u32 hits hold ALT labels 0..6 directly; 7 and past escape to the batch's side table
     wide_alt = any(h >> 32 > 7 for hl in exp_hits for h in hl)
     assert wide_alt == (fixture == 'general22')
+    raising = bool((exp_rows[:, 4] > 0).any())  # rows whose slices raise: no compact row holds them
     for index_stage in ('0', '1'):
         monkeypatch.setenv('SBEACON_REQ_INDEX_STAGE', index_stage)
         for mode in (0, COMPACT_HITS, COMPACT_ALL):
             b = RequestBatch(store, arr, len(owners))
-            try:
-                b.set_compact(mode)
-            except SbError:  # COMPACT_ALL: not for batches with per-slice rows
-                assert mode == COMPACT_ALL
-                continue
-            if mode and wide_alt:
-                with pytest.raises(SbError) as e:
-                    b.answer()
-                assert e.value.code == SB_EINVAL and 'ALT index past 7' in str(e.value)
-                continue
+            b.set_compact(mode)
             rows, hits, ro = b.answer()
+            er, eh = b.escape_flags()
+            assert eh == (mode != 0 and wide_alt), (mode, eh)
+            assert (er if mode == COMPACT_ALL and raising else True) and (mode == COMPACT_ALL or not er), (mode, er)
             np.testing.assert_array_equal(rows, exp_rows)
             for w in range(len(sps)):
                 assert [int(x) for x in hits[ro[w]:ro[w + 1]]] == exp_hits[w], (index_stage, mode, w)
@@ -299,15 +296,17 @@ def test_request_batch_is_repeatable():
 
 
 def test_pass_invariants_fail_the_batch(monkeypatch):
-    """The request pass checks its per-chain sums against the run's staged
-    hits (query_kernels.hip request_eval_kernel): with one sum perturbed on
-    the device (SBEACON_REQ_INJECT, a test hook) the batch fails at sync with
-    SB_EINTERNAL instead of returning its rows; without it the same batch
-    answers normally."""
+    """The request pass checks its per-chain sums against the wave's own
+    totals (query_kernels.hip request_eval_kernel): with one chain's
+    exists-slice count (SBEACON_REQ_INJECT=1), call-count pull (=2) or AN
+    pull (=3) perturbed on the device (a test hook) the batch fails at sync
+    with SB_EINTERNAL instead of returning its rows; the SAME batch then
+    answers normally once the hook is off (the error word is cleared at the
+    sync that reports it)."""
     from payload_gen import read_records
     from sbeacon._lib import SB_EINTERNAL, SbError
     from sbeacon.engine import Store
-    from sbeacon.requests import RequestBatch, requests_from_split_payloads
+    from sbeacon.requests import COMPACT_ALL, RequestBatch, requests_from_split_payloads
     path = os.path.join(FIXTURES, 'tiny22.vcf')
     store = Store.build([('tiny22.vcf', path)], device=0)
     recs, _ = read_records(path)
@@ -318,14 +317,19 @@ def test_pass_invariants_fail_the_batch(monkeypatch):
                 vcf_locations={'tiny22.vcf': '22'}, vcf_groups=[], requested_granularity='record',
                 variant_min_length=0, variant_max_length=-1) for k in range(16)]
     arr, _, owners = requests_from_split_payloads(store, sps)
-    monkeypatch.setenv('SBEACON_REQ_INJECT', '1')
-    with pytest.raises(SbError) as e:
-        RequestBatch(store, arr, len(owners)).answer()
-    assert e.value.code == SB_EINTERNAL
-    monkeypatch.delenv('SBEACON_REQ_INJECT')
-    rows, _, _ = RequestBatch(store, arr, len(owners)).answer()
     exp_rows, _, _ = _expected(store, sps)
-    np.testing.assert_array_equal(rows, exp_rows)
+    for mode in ('1', '2', '3'):
+        for compact in (0, COMPACT_ALL):
+            b = RequestBatch(store, arr, len(owners))
+            b.set_compact(compact)
+            monkeypatch.setenv('SBEACON_REQ_INJECT', mode)
+            with pytest.raises(SbError) as e:
+                b.answer()
+            assert e.value.code == SB_EINTERNAL, (mode, compact)
+            monkeypatch.delenv('SBEACON_REQ_INJECT')
+            rows, _, _ = b.answer()
+            np.testing.assert_array_equal(rows, exp_rows)
+            b.free()
 
 
 def test_shard_plan_stores_on_device():
@@ -513,14 +517,151 @@ def test_device_planned_requests_match_host_planned(monkeypatch):
         np.testing.assert_array_equal(ro_c, ro_h)
         np.testing.assert_array_equal(hits_c, hits_h)
         b.set_compact(False)
-        if b.stats()['n_queries']:  # some rows answered per slice: wide rows only
-            with pytest.raises(_lib.SbError):
-                b.set_compact(True)
-            continue
-        b.set_compact(True)
+        b.set_compact(True)  # (rows answered per slice narrow too, or escape)
         rows_c, hits_c, ro_c = b.answer()
         np.testing.assert_array_equal(rows_c, rows_h)
         np.testing.assert_array_equal(ro_c, ro_h)
         np.testing.assert_array_equal(hits_c, hits_h)
         b.set_compact(False)
     del keep, dev_b, host_b
+
+
+def _genome_oracle(shape, reqs, path, patched=True):
+    """(request rows, per-request [(chrom, POS, ALT)] in hit order) of the
+    C oracle over every splitQuery slice of reqs on the VCF at path."""
+    from oracle.oracle import OracleVcf
+    from sbeacon.genome import shard_slices, slice_payloads
+    from sbeacon.shard import request_rows_from_responses
+    orc = OracleVcf(path, load_gt=False)
+    whole = shard_slices(shape, reqs, 1, 0)
+    res = orc.perform_query_batch(slice_payloads(whole), patched=patched)
+    exp = request_rows_from_responses(whole.req, res, whole.n_rows)
+    exp_v = [[] for _ in range(len(reqs))]
+    for o, r in zip(whole.req, res):
+        if isinstance(r, dict):
+            exp_v[o].extend(tuple(v.split('\t')[i] for i in (0, 1, 3)) for v in r['variants'])
+    orc.close()
+    return exp, exp_v
+
+
+def _vcf_records(path):
+    """(chrom, POS, ALTs) of every record in file order (= the store's record ids for one VCF)."""
+    out = []
+    with open(path) as f:
+        for line in f:
+            if line[0] == '#':
+                continue
+            c = line.split('\t', 5)
+            out.append((c[0], c[1], c[4].split(',')))
+    return out
+
+
+def test_timed_step_variant_matches_oracle():
+    """The exact form the bench step times (bench_genome.py main_genome): 4
+    request batches prepared once, each re-planned on the device inside
+    every pass (sb_requests_set_replan; the planning fused into
+    request_eval_kernel: plan_fused), compact outputs (SB_COMPACT_ALL), run
+    in rotation on one stream into their own buffers -- every batch's rows
+    and every hit list against the C oracle (patched variantType semantics),
+    not against another device path."""
+    import torch
+    from sbeacon.genome import GenomeShape, config3_requests, prepare_shard_requests, shard_requests
+    from sbeacon.requests import COMPACT_ALL, widen_compact
+    shape = GenomeShape(n_total=240_000, seed=3, n_samples=0)
+    store = shape.build_shard_store(1, 0, device=0)
+    dev = torch.device('cuda', 0)
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    B = []
+    for k in range(4):
+        reqs = config3_requests(shape, n=4000, seed=1003 + k)
+        sr = shard_requests(shape, reqs, 1, 0)
+        b = prepare_shard_requests(store, sr)
+        b.set_stream(stream)
+        b.set_replan(True)
+        b.set_compact(COMPACT_ALL)
+        cap = max(int(b.stats()['hits']), 1)
+        B.append(dict(reqs=reqs, sr=sr, b=b, rows=torch.zeros((sr.n_rows, 4), dtype=torch.int32, device=dev),
+                      hits=torch.zeros(cap, dtype=torch.int32, device=dev),
+                      ro=torch.zeros(sr.n_rows + 1, dtype=torch.int32, device=dev)))
+    for i in range(10):  # the rotation (the bench's warmup + steps)
+        x = B[i % 4]
+        x['b'].run(x['rows'].data_ptr(), x['hits'].data_ptr(), x['ro'].data_ptr(), 0)
+    for x in B:
+        x['b'].sync()
+        assert x['b'].plan_fused()  # the timed variant: planning inside the eval kernel
+        assert x['b'].escape_flags() == (False, False)
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, 'full.vcf')
+        with open(path, 'wb') as f:
+            for c in shape.shard_chunks(1, 0):
+                f.write(c)
+        recs = _vcf_records(path)
+        checked = 0
+        for x in B:
+            ro32 = x['ro'].cpu().numpy().view(np.uint32)
+            rows, hits, ro = widen_compact(x['rows'].cpu().numpy(), x['hits'][:int(ro32[-1])].cpu().numpy(), ro32)
+            exp, exp_v = _genome_oracle(shape, x['reqs'], path)
+            np.testing.assert_array_equal(rows, exp[x['sr'].row_lo:x['sr'].row_lo + x['sr'].n_rows])
+            for w in range(x['sr'].n_rows):
+                got = [(recs[h & 0xffffffff][0], recs[h & 0xffffffff][1], recs[h & 0xffffffff][2][h >> 32])
+                       for h in hits[ro[w]:ro[w + 1]].tolist()]
+                assert got == exp_v[x['sr'].row_lo + w], w
+                checked += len(got)
+        assert checked > 200
+
+
+def test_compact_escapes_in_genome_batch():
+    """A config-3-shape batch whose windows reach a record with 10 ALTs and
+    one with an AC past 2^32 (general record): those requests are answered
+    per slice inside the batch, and SB_COMPACT_ALL still answers the whole
+    batch -- the ALT labels past 6 and the rows past u32 escape to the
+    batch's side tables (sb_requests_escapes), and the widened rows and hit
+    lists equal the C oracle's."""
+    from sbeacon.engine import Store
+    from sbeacon.genome import (CONTIGS, LOCATION, GenomeShape, Requests, config3_requests, prepare_shard_requests,
+                                shard_requests)
+    from sbeacon.requests import COMPACT_ALL
+    shape = GenomeShape(n_total=240_000, seed=3, n_samples=0)
+    ci_y = len(CONTIGS) - 1
+    _, last = shape.span(ci_y)
+    p1, p2 = last + 100, last + 300
+    ref = 'ACGTACGTACG'
+    alts = [ref[:k] for k in range(1, 11)]  # ten deletions: ALT indexes 0..9
+    extra = (f'{CONTIGS[ci_y]}\t{p1}\t.\t{ref}\t{",".join(alts)}\t.\tPASS\tAC={",".join(str(k + 1) for k in range(10))};'
+             f'AN=5008;VT=INDEL\n'
+             f'{CONTIGS[ci_y]}\t{p2}\t.\tACGT\tA\t.\tPASS\tAC=5000000000;AN=5000000000;VT=INDEL\n')
+    with tempfile.TemporaryDirectory() as tmp:
+        path = os.path.join(tmp, 'esc.vcf')
+        with open(path, 'wb') as f:
+            for c in shape.shard_chunks(1, 0):
+                f.write(c)
+            f.write(extra.encode())
+        store = Store.build([(LOCATION, path)], device=0)
+        base = config3_requests(shape, n=3000, seed=21)
+        k = 200  # DEL requests whose windows hold the two records
+        rng = np.random.default_rng(8)
+        start = (p1 - 1 - rng.integers(0, 5000, k)).astype(base.start.dtype)
+        reqs_ci = np.concatenate([base.ci, np.full(k, ci_y, dtype=base.ci.dtype)])
+        reqs_start = np.concatenate([base.start, start])
+        width = np.concatenate([base.width, rng.integers(5400, 30000, k).astype(base.width.dtype)])
+        vt = np.concatenate([base.vt, np.zeros(k, dtype=base.vt.dtype)])  # DEL
+        vmin = np.concatenate([base.vmin, np.zeros(k, dtype=base.vmin.dtype)])
+        vmax = np.concatenate([base.vmax, np.full(k, -1, dtype=base.vmax.dtype)])
+        order = np.lexsort((reqs_start, reqs_ci))
+        reqs = Requests(reqs_ci[order], reqs_start[order], width[order], vt[order], vmin[order], vmax[order])
+        sr = shard_requests(shape, reqs, 1, 0)
+        b = prepare_shard_requests(store, sr)
+        assert b.stats()['n_queries'] > 0  # some requests went per slice
+        b.set_compact(COMPACT_ALL)
+        rows, hits, ro = b.answer()
+        assert b.escape_flags() == (True, True)
+        exp, exp_v = _genome_oracle(shape, reqs, path)
+        recs = _vcf_records(path)
+        np.testing.assert_array_equal(rows, exp[sr.row_lo:sr.row_lo + sr.n_rows])
+        big = 0
+        for w in range(sr.n_rows):
+            got = [(recs[h & 0xffffffff][0], recs[h & 0xffffffff][1], recs[h & 0xffffffff][2][h >> 32])
+                   for h in hits[ro[w]:ro[w + 1]].tolist()]
+            assert got == exp_v[sr.row_lo + w], w
+            big += sum(1 for h in hits[ro[w]:ro[w + 1]].tolist() if h >> 32 >= 7)
+        assert big > 0 and (rows[:, 2] > 2**32).any()
