@@ -64,12 +64,35 @@ def parse():
     ap.add_argument('--scaling', choices=['weak', 'strong'], default='weak')
     ap.add_argument('--deliver', choices=['first', 'rank0'], default='first',
                     help="config 3: each request's rows + hits go to the rank of its first slice, or all to rank 0")
+    ap.add_argument('--no-config4', action='store_true',
+                    help='config 3 only: skip the config-4 sub-object (summariseSlice + duplicateVariantSearch on the '
+                         '50-dataset cohort, bench_paths.py) the default N=1 run appends')
+    ap.add_argument('--config4-datasets', type=int, default=50)
     ap.add_argument('--gnomad-records', type=int, default=750_000_000)
     ap.add_argument('--gnomad-requests', type=int, default=50_000, help='config-5 requests per GPU')
     args = ap.parse_args()
     if args.threads is None:
         args.threads = host_cores()['cores']
     return args
+
+
+def config4_lines(args) -> dict:
+    """BASELINE configs[3] beside the headline (N=1): bench_paths.run over the
+    50-dataset cohort after the config-3 store is freed -- summariseSlice over
+    every slice of the 100 VCFs in one call, the per-dataset
+    duplicateVariantSearch jobs in one call, the reference-exact mode over
+    the first 10 datasets' messages, each with its C-oracle parity sample and
+    CPU baseline.  Times measured inside bench_paths as in its own lines."""
+    import bench_paths
+    a = bench_paths.parse(['--datasets', str(args.config4_datasets), '--threads', str(args.threads)] +
+                          (['--no-cpu-baseline'] if args.no_cpu_baseline else []))
+    t0 = time.perf_counter()
+    lines = bench_paths.run(a)
+    keep = ('metric', 'value', 'unit', 'ms_per_step', 'device_ms_per_step', 'config', 'roofline', 'cpu_baseline',
+            'parity_sample', 'strict_mode', 'union', 'path', 'windows', 'ingest_s')
+    out = {x['config']['workload']: {k: x[k] for k in keep if k in x} for x in lines}
+    out['seconds'] = round(time.perf_counter() - t0, 1)
+    return out
 
 
 def host_cores() -> dict:
@@ -136,7 +159,12 @@ def main():
         sys.exit(spawn_ranks(args))
     if args.workload == 'genome':
         from bench_genome import main_genome
-        return main_genome(args)
+        out = main_genome(args)
+        if out is not None:  # rank 0
+            if int(os.environ.get('WORLD_SIZE', 1)) == 1 and not args.no_config4:
+                out['config4'] = config4_lines(args)
+            print(json.dumps(out), flush=True)
+        return
     if args.workload == 'gnomad':
         from bench_gnomad import main_gnomad
         return main_gnomad(args)

@@ -150,6 +150,26 @@ def main_genome(args):
             eval_ms.append((b['batch'].timing()['scan_ms'], n))
         b['batch'].time_eval(False)
     kern_ms = sum(t * n for t, n in eval_ms) / max(sum(n for _, n in eval_ms), 1)
+    # the memory level: the same rotation with L2 and the 256 MiB Infinity
+    # Cache evicted before every pass (a 1 GiB device buffer written between
+    # passes, outside the eval kernel's events), against the store's
+    # candidate columns (the VcQ words + record ids the eval reads)
+    n_cand, cand_bytes = store.candidates()
+    flush = torch.empty(1 << 28, dtype=torch.int32, device=dev)
+    for b in B:
+        b['batch'].time_eval(True)
+    for i in range(args.steps):
+        flush.fill_(i)
+        b = B[i % len(B)]
+        b['batch'].run(b['part'].data_ptr(), b['hits'].data_ptr(), b['row_off'].data_ptr(), base)
+    cold = []
+    for b, n in zip(B, n_pass):
+        b['batch'].sync()
+        if n:
+            cold.append((b['batch'].timing()['scan_ms'], n))
+        b['batch'].time_eval(False)
+    cold_ms = sum(t * n for t, n in cold) / max(sum(n for _, n in cold), 1)
+    del flush
     # the pass without the exchange (re-plan + eval + tile scan + deliver), same rotation
     torch.cuda.synchronize()
     e0.record()
@@ -342,6 +362,15 @@ def main_genome(args):
                                 + ' + 16 B row + 4 B row count: the compact outputs) + 16 B per candidate in the '
                                 'union of the chain windows (POS, END, VtHot word, AC) + 4 B/hit staged',
                      'planning_fused': fused,
+                     'memory_level': {
+                         'candidate_columns_bytes': int(cand_bytes), 'candidates': int(n_cand),
+                         'infinity_cache_bytes': 256 << 20,
+                         'eval_ms_warm': round(kern_ms, 4), 'eval_ms_cold': round(cold_ms, 4),
+                         'frac_cold': round(comp / (cold_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if cold_ms > 0 else None,
+                         'note': 'warm: the rotation as timed above; cold: the same passes with a 1 GiB device buffer '
+                                 'written before each (L2 and the MALL evicted; HIP events around the eval kernel '
+                                 'only).  candidate_columns_bytes: the whole store\'s VcQ words + record ids; a '
+                                 'batch reads those of its windows\' unique candidates (candidates.unique x 20 B)'},
                      'r04_basis': {'bytes': r0[13], 'frac': round(r0[13] / (r0[1] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)
                                    if r0[1] > 0 else None,
                                    'note': 'the round-4 pricing (80 B per request, 24 B per candidate, 8 B per hit '
@@ -368,10 +397,15 @@ def main_genome(args):
         'prepare_s': round(t_prepare, 3),
         'batches': args.batches,
     }
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    # the store and the batches' buffers go before the caller's next workload
+    for b in B:
+        b['batch'].free()
+    del B, steps, part, hits, row_off, ex
+    store.close()
+    torch.cuda.empty_cache()
     if dist:
         dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 def step_request_count(args, world) -> int:

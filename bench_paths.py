@@ -39,7 +39,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def main():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--datasets', type=int, default=10)
     ap.add_argument('--records', type=int, default=1103547)
@@ -51,10 +51,20 @@ def main():
     ap.add_argument('--only', choices=['summarise', 'dedup'], default=None)
     ap.add_argument('--strict-datasets', type=int, default=10,
                     help='datasets whose messages also run in the reference-exact dedup mode (0: skip)')
-    args = ap.parse_args()
+    args = ap.parse_args(argv)
     from bench import host_cores
     if args.threads is None:
         args.threads = host_cores()['cores']
+    return args
+
+
+def main():
+    for line in run(parse()):
+        print(json.dumps(line), flush=True)
+
+
+def run(args) -> list:
+    """The config-4 lines (summarise, dedup) as dicts."""
     import torch
     torch.cuda.set_device(0)
     from sbeacon.engine import Store
@@ -82,10 +92,15 @@ def main():
         info = store.info()
         log(f'{len(files)} VCFs, {info["n_records"]} records, {info["device_bytes"] / 2**20:.0f} MiB HBM; '
             f'generate {t_gen:.1f} s, ingest {t_ingest:.1f} s')
+        out = []
         if args.only != 'dedup':
-            summarise_line(args, store, files, plan_slices)
+            out.append(summarise_line(args, store, files, plan_slices))
         if args.only != 'summarise':
-            dedup_line(args, store, datasets, files)
+            out.append(dedup_line(args, store, datasets, files))
+        for x in out:
+            x['ingest_s'] = round(t_ingest, 2)
+        store.close()
+        return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -140,7 +155,7 @@ def summarise_line(args, store, files, plan_slices):
         cpu, parity = summarise_cpu(files[:k], [[s for s in slices if s[0] == f[0]] for f in files[:k]],
                                     [[r for s, r in zip(slices, res) if s[0] == f[0]] for f in files[:k]],
                                     args.threads)
-    print(json.dumps({
+    return ({
         'metric': 'summariseSlice records/s (all slices of every VCF in one call)',
         'value': round(n_records / (wall * 1e-0), 1) if wall > 0 else None,
         'unit': 'records/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
@@ -154,7 +169,8 @@ def summarise_line(args, store, files, plan_slices):
                      'traffic': pmc_traffic(n_records, ['summarise_chunk_kernel', 'summarise_finish_kernel']),
                      'kernel': 'summarise_chunk_kernel + summarise_finish_kernel',
                      'algorithmic_bytes_per_launch': alg},
-        'cpu_baseline': cpu, 'parity_sample': parity}), flush=True)
+        'cpu_baseline': cpu, 'parity_sample': parity})
+
 
 def summarise_cpu(files, slices, got, threads):
     """oracle/summarise_oracle.c over every slice of the first VCFs (one per
@@ -238,7 +254,7 @@ def dedup_line(args, store, datasets, files):
                          f'thread on {args.threads} threads', 'seconds': round(dt, 3)}
         parity = {'jobs': k, 'mismatches': int(sum(r != e for r, e in zip(res[:k], exp))), 'unique_first': exp[0]}
     strict = strict_sample(args, store, datasets) if args.strict_datasets else None
-    print(json.dumps({
+    return ({
         'metric': 'duplicateVariantSearch region keys/s (per-dataset unique counts, one batched call)',
         'value': round(keys / wall, 1) if wall > 0 else None,
         'unit': 'keys/s', 'n_gpus': 1, 'steps': args.steps, 'warmup': args.warmup,
@@ -255,7 +271,7 @@ def dedup_line(args, store, datasets, files):
                      'kernel': kern, 'algorithmic_bytes_per_launch': alg,
                      'implementation_bytes_per_launch_upper_bound': impl,
                      'implementation_GBs': round(impl / (dev_ms * 1e-3) / 1e9, 1)},
-        'cpu_baseline': cpu, 'parity_sample': parity, 'strict_mode': strict}), flush=True)
+        'cpu_baseline': cpu, 'parity_sample': parity, 'strict_mode': strict})
 
 
 def strict_sample(args, store, datasets):

@@ -136,6 +136,11 @@ typedef struct {
     int32_t device;
 } sb_store_info;
 int sb_store_get_info(const sb_store *s, sb_store_info *out);
+/* variantType candidates of every (segment, kind) list of the store and the
+ * bytes of the two columns request_eval_kernel reads per candidate (the
+ * 16-byte VcQ word and the 4-byte record id): the working set of the
+ * config-3 request pass, to set against the 256 MiB Infinity Cache. */
+int sb_store_candidates(const sb_store *s, uint64_t *n, uint64_t *bytes);
 /* vcf id for a vcf_location string, or SB_ENOSTORE */
 int sb_store_find_vcf(const sb_store *s, const char *location, size_t len, uint32_t *vcf_id);
 int sb_store_n_samples(const sb_store *s, uint32_t vcf_id, uint32_t *n);

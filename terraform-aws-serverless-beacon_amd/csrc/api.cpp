@@ -1611,6 +1611,14 @@ int sb_store_get_info(const sb_store *s, sb_store_info *out) {
     });
 }
 
+int sb_store_candidates(const sb_store *s, uint64_t *n, uint64_t *bytes) {
+    return guard([&] {
+        if (!s || !n || !bytes) throw Error(SB_EINVAL, "NULL argument");
+        *n = s->h_vc_altpre.empty() ? 0 : s->h_vc_altpre.size() - 1;
+        *bytes = *n * (sizeof(VcQ) + sizeof(uint32_t));  // the VcQ word + the record id request_eval_kernel loads
+    });
+}
+
 int sb_store_find_vcf(const sb_store *s, const char *location, size_t len, uint32_t *vcf_id) {
     if (!s || !location || !vcf_id) return SB_EINVAL;
     auto it = s->vcf_by_location.find(std::string(location, len));

@@ -14,7 +14,6 @@ struct Config {
     // ---- tuning
     double vc_bucket = 1.0;       // SBEACON_VC_BUCKET: variantType candidates per coarse-index bucket (>= 0.25)
     int pack_run = 0;             // SBEACON_PACK_RUN: chains per chain_pack_kernel run (0: the kernel's maximum)
-    int chain_run = 0;            // SBEACON_CHAIN_RUN: chains per chain_kernel wave (0: by batch size)
     int slices_per_wave = 0;      // SBEACON_SLICES_PER_WAVE: slices per scan wave (0: by batch size)
     int dedup_win_target = 0;     // SBEACON_DEDUP_WIN_TARGET: keys per dedup window (0: kWinTarget)
     int dedup_bucket_cap = 0;     // SBEACON_DEDUP_BUCKET_CAP: keys per bucket hash set (0: 3/4 of its slots)
@@ -23,8 +22,6 @@ struct Config {
     bool no_range8 = false;       // SBEACON_NO_RANGE8=1: every VCF on the 16-byte RangeHot words
     bool no_chains = false;       // SBEACON_NO_CHAINS=1: variantType slices answered one by one
     bool no_rowout = false;       // SBEACON_NO_ROWOUT: per-run row sources instead of static row hit regions
-    bool chain_seq = false;       // SBEACON_CHAIN_KERNEL=seq: the chain-sequential kernel
-    bool row_gather_team = false; // SBEACON_ROW_GATHER=team: 8 lanes per row in the slice-batch gather
     char dedup_exact = 0;         // SBEACON_DEDUP_EXACT=radix|bucket ('r' / 'b'): the sorted dedup paths
     int dedup_hash_bits = 0;      // SBEACON_DEDUP_HASH_BITS (test hook): key hashes cut to this many bits
     bool strict_check = false;    // SBEACON_STRICT_CHECK: reference-exact dedup entries re-checked by the reader walk
@@ -39,7 +36,6 @@ struct Config {
     bool req_index_stage = false; // SBEACON_REQ_INDEX_STAGE=1 (tests): stage candidate indices, as stores past 2^29 records do
     bool req_plan_apart = false;  // SBEACON_REQ_PLAN_APART=1: re-planning passes launch request_plan_kernel (no fused planning)
     bool req_tile_scan = false;   // SBEACON_REQ_TILE_SCAN=1: request_tile_scan_kernel before the delivery (no in-delivery sums)
-    int pack_dbg = 0;             // SBEACON_PACK_DBG: chain-kernel ablations (SBEACON_ABLATION builds)
 };
 
 inline Config config() {
@@ -53,7 +49,6 @@ inline Config config() {
         c.vc_bucket = x < 0.25 ? 0.25 : x;
     }
     c.pack_run = num("SBEACON_PACK_RUN", 0);
-    c.chain_run = num("SBEACON_CHAIN_RUN", 0);
     c.slices_per_wave = num("SBEACON_SLICES_PER_WAVE", 0);
     c.dedup_win_target = num("SBEACON_DEDUP_WIN_TARGET", 0);
     c.dedup_bucket_cap = num("SBEACON_DEDUP_BUCKET_CAP", 0);
@@ -61,8 +56,6 @@ inline Config config() {
     c.no_range8 = one("SBEACON_NO_RANGE8");
     c.no_chains = one("SBEACON_NO_CHAINS");
     c.no_rowout = flag("SBEACON_NO_ROWOUT");
-    if (const char *e = str("SBEACON_CHAIN_KERNEL")) c.chain_seq = e[0] == 's';
-    if (const char *e = str("SBEACON_ROW_GATHER")) c.row_gather_team = e[0] == 't';
     if (const char *e = str("SBEACON_DEDUP_EXACT")) c.dedup_exact = (e[0] == 'r' || e[0] == 'b') ? e[0] : 0;
     c.dedup_hash_bits = num("SBEACON_DEDUP_HASH_BITS", 0);
     c.strict_check = flag("SBEACON_STRICT_CHECK");
@@ -76,7 +69,6 @@ inline Config config() {
     c.req_index_stage = one("SBEACON_REQ_INDEX_STAGE");
     c.req_plan_apart = one("SBEACON_REQ_PLAN_APART");
     c.req_tile_scan = one("SBEACON_REQ_TILE_SCAN");
-    c.pack_dbg = num("SBEACON_PACK_DBG", 0);
     return c;
 }
 

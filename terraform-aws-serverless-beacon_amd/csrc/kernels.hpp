@@ -115,7 +115,9 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
                          int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
                          const ReqIn *plan_in, uint32_t n_in, uint64_t stride, int inject, bool tile_scan,
-                         const ReqEsc &esc);
+                         const ReqEsc &esc, bool lab7);
+// lab7: the store holds a record with 8 ALTs (a chain hit can carry the label
+// 7, which the compact hit form escapes; store_has_label7)
 // chain slots per run (kReqRun)
 uint32_t req_run_max();
 // Request planning on the device: rows in runs of kRunRows (n_runs =

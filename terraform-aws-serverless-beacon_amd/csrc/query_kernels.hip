@@ -1337,207 +1337,19 @@ __global__ __launch_bounds__(kBlock) void fused_kernel(DStore st, FusedGroups G,
 }
 
 // ---------------------------------------------------------------- slice chains
-// One wave answers a run of up to kChainRun chains (ChainDev): each chain is
-// the consecutive 10 kb slices one request was cut into by splitQuery, all
-// with the same filters, none needing the order-dependent machinery
-// (host-checked at prepare: include_details, no boolean break, non-negative
-// AC, no VT_SLOW record in the window).  For such slices vt_slice's answer is:
-// exists = some hit with AC > 0, call_count / all_alleles_count = sums over
-// the hit records, hits in record-then-ALT order -- each a sum (or an ordered
-// concatenation) over the slice's candidates.  So a chain needs ONE candidate
-// range, [C0, C1) from two entries of the (kind, segment) coarse POS index,
-// every candidate lane tests POS against the chain window and takes slice
-// (POS - first) / width, per-slice sums go to LDS by atomics and the chain's
-// hits are written densely in record order.  Memory rounds per wave: the
-// run's descriptors (lane k = chain k), then every chain's two index entries
-// and LUT words at once (lanes 2k / 2k+1, lanes 8k..8k+7), then candidate
-// chunks, chain k+1's first chunk issued before chain k is evaluated.
-constexpr uint32_t kChainRun = 8;  // chains per wave (lanes 8k..8k+7 hold chain k's LUT words)
-
-struct ChainLds {
-    unsigned long long cc[kChainMax], an[kChainMax];
-    unsigned int nh[kChainMax], ex[kChainMax];
-    unsigned long long tcc, tan;  // chain totals (cpart)
-};
-
+// A chain is the consecutive 10 kb slices one request was cut into by
+// splitQuery, all with the same filters, none needing the order-dependent
+// machinery (host-checked at prepare: include_details, no boolean break,
+// non-negative AC, no VT_SLOW record in the window).  For such slices
+// vt_slice's answer is: exists = some hit with AC > 0, call_count /
+// all_alleles_count = sums over the hit records, hits in record-then-ALT
+// order -- so a chain needs ONE candidate range, [C0, C1) from two entries of
+// the (kind, segment) coarse POS index (chain_pack_kernel below).
 struct ChainChunk {
     uint32_t p;  // candidate POS
     VtHot h;
     uint32_t r;  // candidate record
 };
-
-__global__ __launch_bounds__(kBlock) void chain_kernel(DStore st, const ChainDev *__restrict__ chains,
-                                                       uint32_t n_chains, uint32_t run,
-                                                       const uint32_t *__restrict__ corig, QRes *__restrict__ res,
-                                                       uint64_t *__restrict__ hits, ReqPartial *__restrict__ cpart) {
-    __shared__ ChainLds lds_all[kWavesPerBlock];
-    const uint32_t c_first = launch_wave() * run;
-    if (c_first >= n_chains) return;
-    const uint32_t R = min(run, n_chains - c_first);
-    ChainLds &L = lds_all[threadIdx.x >> 6];
-    const int lane = lane_id();
-    const uint32_t ul = static_cast<uint32_t>(lane);
-    // round 1: lane k < R holds chain k's descriptor
-    const uint4 *cd = reinterpret_cast<const uint4 *>(chains + c_first);
-    uint4 d0{0, 0, 0, 0}, d1{0, 0, 0, 0}, d2{0, 0, 0, 0}, d3{0, 0, 0, 0}, d4{0, 0, 0, 0};
-    if (ul < R) {
-        d0 = cd[5 * ul];
-        d1 = cd[5 * ul + 1];
-        d2 = cd[5 * ul + 2];
-        d3 = cd[5 * ul + 3];
-        d4 = cd[5 * ul + 4];
-    }
-    // round 2: lanes 2k / 2k+1 = chain k's candidate bounds from the coarse
-    // index (a superset of [first, last]); lanes 8k + t = LUT word t of chain k
-    uint32_t bound = 0, lutv = 0;
-    {
-        const int src = static_cast<int>(ul >> 1);
-        const uint32_t first = __shfl(d0.z, src, kWave), last = __shfl(d0.w, src, kWave);
-        const uint32_t c_lo = __shfl(d1.y, src, kWave), c_hi = __shfl(d1.z, src, kWave);
-        const uint32_t cb_base = __shfl(d1.w, src, kWave);
-        const uint64_t cb_off = static_cast<uint64_t>(static_cast<uint32_t>(__shfl(d2.x, src, kWave))) |
-                                (static_cast<uint64_t>(static_cast<uint32_t>(__shfl(d2.y, src, kWave))) << 32);
-        const uint32_t cb_shift = __shfl(d2.z, src, kWave), cb_n = __shfl(d2.w, src, kWave);
-        const uint32_t lut_off = __shfl(d4.y, static_cast<int>(ul >> 3), kWave);
-        if (ul < 2 * R) {
-            const uint32_t up = ul & 1u;
-            const uint64_t x = up ? static_cast<uint64_t>(last) + 1 : first;
-            if (x <= cb_base) {
-                bound = c_lo;
-            } else {
-                const uint64_t b = (x - cb_base) >> cb_shift;
-                bound = b >= cb_n ? c_hi : st.vc_bucket[cb_off + b + up];
-            }
-        }
-        if (ul < 8 * R) lutv = st.sym_lut[lut_off + (ul & 7u)];
-    }
-    // clamped and unconditional (an empty range reads slot C0, inside the
-    // kind lists + sentinel): no load sits under a branch, so the waitcnt pass
-    // keeps the next chain's chunk in flight while this one is evaluated
-    auto load_chunk = [&](uint32_t C1, uint32_t base) -> ChainChunk {
-        const uint32_t i = min(base + ul, max(C1, base + 1) - 1);
-        return ChainChunk{st.vc_pos[i], st.vc_word[i], st.vc_idx[i]};
-    };
-    auto range_of = [&](uint32_t k, uint32_t *C0, uint32_t *C1) {
-        *C0 = rdl(bound, 2 * k);
-        *C1 = (rdl(d4.x, k) & kChainEndVoid) ? *C0 : max(*C0, rdl(bound, 2 * k + 1));
-    };
-    // one chunk of chain candidates at positions [base, base + 64) of [C0, C1)
-    struct ChainCtx {
-        uint32_t first, last, width, n;
-        uint64_t out;
-        uint64_t nout;
-        uint32_t slow;
-    };
-    auto eval_chunk = [&](ChainCtx &X, const VtPred &P, const ChainChunk &x, uint32_t base, uint32_t C1) {
-        const bool inwin = base + ul < C1 && x.p >= X.first && x.p <= X.last;
-        const bool cand = inwin && P.end_ok(x.h.end);
-        X.slow |= static_cast<uint32_t>(__ballot(cand && (x.h.w & VT_SLOW)) != 0ull);  // excluded at prepare
-        const LaneOut o = P.eval(st, x.h, x.r, cand && !(x.h.w & VT_SLOW));
-        const bool hit = o.hm != 0;
-        if (!__ballot(hit)) return;
-        const uint32_t sid = inwin ? min((x.p - X.first) / X.width, X.n - 1) : 0u;
-        const uint32_t cnt = hit ? static_cast<uint32_t>(__popcll(o.em)) : 0u;
-        // exclusive prefix / total of the emitted counts over the wave
-        uint32_t pre, total;
-        if (!__ballot(cnt > 1)) {
-            const uint64_t one = __ballot(cnt == 1);
-            pre = popc_below(one);
-            total = static_cast<uint32_t>(__popcll(one));
-        } else {  // bit-sliced (multi-ALT hit lanes)
-            pre = 0;
-            total = 0;
-            for (uint32_t b = 0; b < 7; ++b) {
-                const uint64_t m = __ballot((cnt >> b) & 1u);
-                pre += popc_below(m) << b;
-                total += static_cast<uint32_t>(__popcll(m)) << b;
-                if (!__ballot(cnt >> (b + 1))) break;
-            }
-        }
-        if (cnt) {
-            uint64_t *dst = hits + X.out + X.nout + pre;
-            for (uint64_t b = o.em; b; b &= b - 1)
-                *dst++ = static_cast<uint64_t>(x.r) | (static_cast<uint64_t>(ffs64(b)) << kHitAltShift);
-            atomicAdd(&L.nh[sid], cnt);
-        }
-        if (hit) {
-            atomicAdd(&L.cc[sid], static_cast<unsigned long long>(o.c));
-            atomicAdd(&L.an[sid], static_cast<unsigned long long>(o.anv));
-            atomicAdd(&L.tcc, static_cast<unsigned long long>(o.c));
-            atomicAdd(&L.tan, static_cast<unsigned long long>(o.anv));
-            if (o.c > 0) L.ex[sid] = 1u;
-        }
-        X.nout += total;
-    };
-    // chain k with its first chunk in `cur`; issues chain k+1's first chunk
-    // (into the returned value) before evaluating anything of chain k
-    auto process = [&](uint32_t k, const ChainChunk &cur) -> ChainChunk {
-        ChainChunk nxt{0, VtHot{0, 0, 0, 0}, 0};
-        if (k + 1 < R) {
-            uint32_t C0n, C1n;
-            range_of(k + 1, &C0n, &C1n);
-            nxt = load_chunk(C1n, C0n);
-        }
-        ChainCtx X{rdl(d0.z, k), rdl(d0.w, k), rdl(d1.x, k), rdl(d0.y, k),
-                   static_cast<uint64_t>(rdl(d4.z, k)) | (static_cast<uint64_t>(rdl(d4.w, k)) << 32), 0, 0};
-        const uint32_t s0 = rdl(d0.x, k);
-        const VtPred P(st, rdl(d3.x, k), rdl(d3.y, k), rdl(d3.z, k), rdl(d3.w, k), rdl(d4.x, k), rdl(d4.y, k),
-                       lutv, 8 * k);
-        uint32_t C0, C1;
-        range_of(k, &C0, &C1);
-        const uint32_t orig = corig[s0 + min(ul, X.n - 1)];
-        if (ul < X.n) {
-            L.cc[ul] = 0;
-            L.an[ul] = 0;
-            L.nh[ul] = 0;
-            L.ex[ul] = 0;
-        }
-        if (lane == 0) {
-            L.tcc = 0;
-            L.tan = 0;
-        }
-        if (C0 < C1) {
-            eval_chunk(X, P, cur, C0, C1);
-            for (uint32_t base = C0 + kWave; base < C1; base += kWave)  // chains longer than one chunk
-                eval_chunk(X, P, load_chunk(C1, base), base, C1);
-        }
-        const bool sl = ul < X.n;
-        const bool ex = sl && L.ex[ul];
-        const int64_t cc = sl ? static_cast<int64_t>(L.cc[ul]) : 0, an = sl ? static_cast<int64_t>(L.an[ul]) : 0;
-        if (sl) {
-            QRes o{0, 0, 0, 0, 0, 0};  // n_scanned: filled on the host (prepare knows each slice's record range)
-            if (X.slow) {
-                o.error = SB_QERR_UNSUPPORTED;  // never: prepare routes chains with a VT_SLOW record to vt_slice
-            } else {
-                o.exists = ex ? 1 : 0;
-                o.call_count = cc;
-                o.all_alleles_count = an;
-                o.n_hits = L.nh[ul];
-            }
-            res[orig] = o;
-        }
-        if (cpart) {  // the chain's request-row partial (sb_batch_reduce_requests of its slices)
-            const uint64_t exm = __ballot(ex);
-            if (lane == 0)
-                cpart[c_first + k] =
-                    X.slow ? ReqPartial{0, 0, 0, 0, static_cast<int64_t>(X.n)}
-                           : ReqPartial{__popcll(exm), static_cast<int64_t>(X.nout), static_cast<int64_t>(L.tcc),
-                                        static_cast<int64_t>(L.tan), 0};
-        }
-        return nxt;
-    };
-    ChainChunk x;
-    {
-        uint32_t C0, C1;
-        range_of(0, &C0, &C1);
-        x = load_chunk(C1, C0);
-    }
-    // unrolled: no loop-carried chunk registers, so the waitcnt pass keeps
-    // chain k+1's loads in flight (exact vmcnt) while chain k is evaluated
-#pragma unroll
-    for (uint32_t k = 0; k < kChainRun; ++k)
-        if (k < R) x = process(k, x);
-}
 
 // Packed chain kernel: a run of up to kPackRun chains shares the wave's lanes
 // (runs built on the host so a run's slices fit kPackSlots LDS slots).
@@ -1600,7 +1412,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SLICES ?
                                                             const uint32_t *__restrict__ runs, uint32_t n_runs,
                                                             const uint32_t *__restrict__ corig,
                                                             QRes *__restrict__ res, uint64_t *__restrict__ hits,
-                                                            ReqPartial *__restrict__ cpart, uint32_t dbg) {
+                                                            ReqPartial *__restrict__ cpart) {
     __shared__ PackLds<SLICES> lds_all[kWavesPerBlock];
     const uint32_t w = launch_wave();
     if (w >= n_runs) return;
@@ -1796,8 +1608,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SLICES ?
         }
     };
     // every chunk of the run issued before the first is evaluated
-    // (dbg: timing ablations of SBEACON_PACK_DBG; 0 in production)
-    if (!(dbg & 1u)) {
+    {
         // software pipeline: chunk c + kPackAhead's loads are issued right
         // after chunk c is evaluated (static buffer slots: unrolled by kPackAhead)
         PackChunk buf[kPackAhead];
@@ -1814,7 +1625,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SLICES ?
             }
         }
     }
-    if (dbg & 2u) return;
     wave_lds_sync();
     if constexpr (SLICES) {
         // results: lane ul + 64 t = slot; chain totals by slot atomics
@@ -2186,11 +1996,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
     uint32_t run_ex = 0; // slices with exists = True so far (wave-uniform; the invariant check)
     uint32_t acc_nv = 0, acc_ex = 0, acc_hr = 0;
     uint64_t acc_cc = 0, acc_an = 0;
-    // the wave's own totals over every chunk (wave-uniform): call count, AN
-    // and (under a common AN) hit records -- the per-chain pulls must add up
-    // to them (the invariants below)
-    uint64_t run_cc = 0, run_an = 0;
-    uint32_t run_hr = 0;
+    // each lane's own totals over its positions (call count, AN, or under a
+    // common AN its hit records), modulo 2^32: the per-chain pulls must add
+    // up to their wave sum (the invariants below); plain per-lane adds, no
+    // cross-lane step and no scalar state in the loop
+    uint32_t lane_cc = 0, lane_an = 0;
     // one instantiation per AN mode (a wave-uniform run flag): under a
     // common AN no AN column is loaded and no AN sum is scanned
     auto pass = [&](auto anc_t) {
@@ -2351,10 +2161,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         // no field borrows): variants (<= 8 ALTs x 64 lanes) | new slices
         // << 10 | hit records << 17 (only read under a common AN)
         uint32_t nvex = (pre + cn) | (popc_below(nb) + (isnew ? 1u : 0u)) << 10;
+        lane_cc += static_cast<uint32_t>(cv);
         if constexpr (ANC) {
-            const uint64_t hb = __ballot(hit);
-            nvex |= (popc_below(hb) + (hit ? 1u : 0u)) << 17;
-            run_hr += static_cast<uint32_t>(__popcll(hb));
+            nvex |= (popc_below(__ballot(hit)) + (hit ? 1u : 0u)) << 17;
+            lane_an += hit ? 1u : 0u;
+        } else {
+            lane_an += anv;
         }
         // ---- chain k's part of the chunk, pulled by lane k from its last lane
         const uint32_t lim = min(base + kWave, T);
@@ -2372,7 +2184,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
             const uint32_t pc = bperm(scc, e);
             const uint32_t qc = wave_shr1(pc);
             if (inter) acc_cc += pc - (opens ? 0u : qc);
-            run_cc += rdl(scc, kWave - 1);  // (the invariants: the chunk's call-count total)
             return;
         }
         const bool big = !narrow &&
@@ -2385,8 +2196,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
                 acc_cc += pc - (opens ? 0u : qc);
                 acc_an += pa - (opens ? 0u : qa);
             }
-            run_cc += rdl(scc, kWave - 1);
-            run_an += rdl(san, kWave - 1);
+
         } else {
             const uint64_t scc = incl_sum_u64(static_cast<uint64_t>(cv)),
                            san = incl_sum_u64(static_cast<uint64_t>(static_cast<int64_t>(static_cast<int32_t>(anv))));
@@ -2396,8 +2206,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
                 acc_cc += pc - (opens ? 0ull : qc);
                 acc_an += pa - (opens ? 0ull : qa);
             }
-            run_cc += static_cast<uint64_t>(rdl64(static_cast<int64_t>(scc), kWave - 1));
-            run_an += static_cast<uint64_t>(rdl64(static_cast<int64_t>(san), kWave - 1));
+
         }
     };
     if (nch) {
@@ -2454,12 +2263,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(SBEACON_
         const uint32_t ex_tot = rdl(incl_sum_u32(acc_ex), kWave - 1);
         const bool bad_lane = acc_ex > acc_nv || (anc && acc_ex > acc_hr);
         // the call-count and AN pulls (the same cross-lane primitives) against
-        // the wave's chunk totals: one 64-bit wave sum each per run
-        const uint64_t cc_tot = static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(acc_cc)), kWave - 1));
-        const uint64_t an_tot = anc ? static_cast<uint64_t>(rdl(incl_sum_u32(acc_hr), kWave - 1))
-                                    : static_cast<uint64_t>(rdl64(static_cast<int64_t>(incl_sum_u64(acc_an)), kWave - 1));
-        if (rdl(cs_incl, kWave - 1) != hpos || ex_tot != run_ex || __ballot(bad_lane) || cc_tot != run_cc ||
-            an_tot != (anc ? static_cast<uint64_t>(run_hr) : run_an))
+        // the lanes' own totals, modulo 2^32: two wave sums of pairs per run
+        const uint32_t d_cc = static_cast<uint32_t>(acc_cc) - lane_cc;
+        const uint32_t d_an = (anc ? acc_hr : static_cast<uint32_t>(acc_an)) - lane_an;
+        if (rdl(cs_incl, kWave - 1) != hpos || ex_tot != run_ex || __ballot(bad_lane) ||
+            rdl(incl_sum_u32(d_cc), kWave - 1) != 0u || rdl(incl_sum_u32(d_an), kWave - 1) != 0u)
             if (ul == 0) atomicOr(err, 1u);
         // (PLAN: the run's hits within its fixed-stride staging region; never
         // past it, the stride was sized on these requests)
@@ -2631,51 +2439,7 @@ __global__ __launch_bounds__(kBlock) void request_plan_kernel(DStore st, const R
     }
 }
 
-// The two scans of the pass (staging offsets per run, output offsets per
-// tile of kDeliverTile runs) run in ONE workgroup of 1,024 threads over
-// rounds of kRunScanRound runs, every load coalesced: item u of thread t is run
-// base + 1,024 u + t, so a wave instruction reads 64 consecutive runs, and a
-// tile (16 consecutive runs) is one 16-lane DPP row -- its sums by row
-// shifts, its total in the row's last lane.  The round's 512 tile totals are
-// scanned in LDS.  (Round 4's forms loaded each thread's runs contiguously --
-// 16-byte loads 256 B apart across the lanes, four times the cache-line
-// accesses -- and took 7.4 us (tile scan, one workgroup) and 6.3 us (staging
-// scan, a workgroup per 1,024 runs re-reading every earlier run).)
-constexpr uint32_t kRunScanPer = 8;                          // runs per thread per round
-constexpr uint32_t kRunScanRound = 1024 * kRunScanPer;           // runs per round
-constexpr uint32_t kRunScanTiles = kRunScanRound / kDeliverTile; // tiles per round (512)
-static_assert(kDeliverTile == 16, "a tile is one DPP row");
-
-// inclusive sum inside each 16-lane row (row_shr 1, 2, 4, 8)
-__device__ __forceinline__ uint64_t row_incl_sum_u64(uint64_t v) {
-    v += static_cast<uint64_t>(dpp_i64<0x111, 0xf, 0xf>(static_cast<int64_t>(v)));
-    v += static_cast<uint64_t>(dpp_i64<0x112, 0xf, 0xf>(static_cast<int64_t>(v)));
-    v += static_cast<uint64_t>(dpp_i64<0x114, 0xf, 0xf>(static_cast<int64_t>(v)));
-    v += static_cast<uint64_t>(dpp_i64<0x118, 0xf, 0xf>(static_cast<int64_t>(v)));
-    return v;
-}
-
-// exclusive scan of the round's kRunScanTiles tile totals held in tl[] (thread
-// t < kRunScanTiles takes tile t), written back in place plus `carry`; returns
-// the round's total.  Every thread calls it (barriers).
-__device__ __forceinline__ uint64_t scan_round_tiles(unsigned long long *tl, unsigned long long *wsum, uint64_t carry) {
-    const uint32_t tid = threadIdx.x, wave = tid >> 6;
-    constexpr uint32_t kW = kRunScanTiles / kWave;  // waves holding tiles (8)
-    const uint64_t x = tid < kRunScanTiles ? tl[tid] : 0ull;
-    const uint64_t inc = incl_sum_u64(x);
-    if (lane_id() == kWave - 1 && wave < kW) wsum[wave] = inc;
-    __syncthreads();
-    uint64_t before = carry, total = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < kW; ++k) {
-        const uint64_t w = wsum[k];
-        if (k < wave) before += w;
-        total += w;
-    }
-    if (tid < kRunScanTiles) tl[tid] = before + inc - x;
-    __syncthreads();
-    return total;
-}
+static_assert(kDeliverTile == 16, "a delivery tile is 16 runs");
 
 // request_stage_scan_kernel: each run's staging offset = the exclusive
 // prefix of the runs' capacities; counters = (chains, chain slices, staging
@@ -2818,14 +2582,17 @@ __global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned 
 // runs) sums the eval workgroup totals before its own (gtot, <= 16 coalesced
 // loads per thread from L2 per 4,096 groups) and each wave adds its group's
 // earlier runs: one launch and its boundary fewer
-template <bool ROWC, bool HITC, bool REC, bool GSUM>
+// SLICED: the batch has a per-slice part (runs that are not simple); without
+// one a compact-row batch's runs are all simple and the row-by-row path is
+// not compiled in (registers of the common instantiation)
+template <bool ROWC, bool HITC, bool REC, bool GSUM, bool SLICED>
 __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const RowRun *__restrict__ runs, uint32_t n_runs, const unsigned long long *__restrict__ status,
     const unsigned long long *__restrict__ toff, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
     const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr, const uint64_t *__restrict__ shits,
     void *__restrict__ row_off_out, const uint64_t *__restrict__ row_src, const uint32_t *__restrict__ stage,
     const uint32_t *__restrict__ vc_idx, void *__restrict__ out_v, uint32_t n_rows, uint64_t rec_base,
-    unsigned int *__restrict__ err, const unsigned long long *__restrict__ gtot, ReqEsc esc) {
+    unsigned int *__restrict__ err, const unsigned long long *__restrict__ gtot, ReqEsc esc, uint32_t lab7) {
     using Hit = std::conditional_t<HITC, uint32_t, uint64_t>;
     using Off = std::conditional_t<ROWC, uint32_t, uint64_t>;
     Hit *const out = static_cast<Hit *>(out_v);
@@ -2911,22 +2678,27 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
             Hit h[kU];
 #pragma unroll
             for (uint32_t u = 0; u < kU; ++u) h[u] = hit_of(v[u]);
-            bool lab7 = false;  // HITC: the label 7 is the escape -- an 8-ALT record's last ALT goes to xlab too
 #pragma unroll
             for (uint32_t u = 0; u < kU; ++u) {
                 const uint64_t j = j0 + kWave * u + ul;
-                if (j < H) {
-                    out[O + j] = h[u];
-                    if (HITC && (v[u] >> kStageAltShift) == kHitLabelEscape) {
+                if (j < H) out[O + j] = h[u];
+            }
+            if (HITC && lab7) {  // (uniform: a store with an 8-ALT record) the label 7 escapes -- its ALT goes to xlab too
+                bool lab7x = false;
+#pragma unroll
+                for (uint32_t u = 0; u < kU; ++u) {
+                    const uint64_t j = j0 + kWave * u + ul;
+                    if (j < H && (v[u] >> kStageAltShift) == kHitLabelEscape) {
                         esc.xlab[O + j] = static_cast<uint16_t>(kHitLabelEscape);
-                        lab7 = true;
+                        lab7x = true;
                     }
                 }
+                if (__ballot(lab7x) && ul == 0) atomicOr(err, kErrHitEscapes);
             }
-            if (HITC && __ballot(lab7) && ul == 0) atomicOr(err, kErrHitEscapes);
         }
         return;
     }
+    if constexpr (ROWC && !SLICED) return;  // (never reached: every run is simple)
     for (uint32_t i = 0; i < row_hi - row_lo; ++i) {  // row by row (some rows answered per slice)
         const uint64_t nv = static_cast<uint64_t>(rdl64(static_cast<int64_t>(c), i));
         if (!nv) continue;
@@ -2935,16 +2707,16 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
         const uint32_t q0 = uniform(sseg[r]), q1 = uniform(sseg[r + 1]);
         if (q1 == q0) {  // a chain row: its hits are contiguous in the staging region
             const uint64_t src = uniform64(row_src[r]);
-            bool lab7 = false;
+            bool lab7x = false;
             for (uint64_t k = ul; k < nv; k += kWave) {
                 const uint32_t v = stage[src + k];
                 out[at + k] = hit_of(v);
                 if (HITC && (v >> kStageAltShift) == kHitLabelEscape) {
                     esc.xlab[at + k] = static_cast<uint16_t>(kHitLabelEscape);
-                    lab7 = true;
+                    lab7x = true;
                 }
             }
-            if (HITC && __ballot(lab7) && ul == 0) atomicOr(err, kErrHitEscapes);
+            if (HITC && __ballot(lab7x) && ul == 0) atomicOr(err, kErrHitEscapes);
         } else {
             uint64_t dst = at;
             for (uint32_t q = q0; q < q1; ++q) {
@@ -3236,53 +3008,6 @@ __global__ __launch_bounds__(kBlock) void field_scan_fused_kernel(const int64_t 
     if (blockIdx.x == gridDim.x - 1 && threadIdx.x == kBlock - 1) out[n] = pre + incl;
 }
 
-// a team of kGatherTeam lanes per row: its pieces' hits, in piece order,
-// from row_off[w], the team's lanes striding over each piece (a row holds a
-// handful of hits: a lane per row would issue one scattered 8-byte access per
-// hit, a team moves up to 64 contiguous bytes per access)
-constexpr uint32_t kGatherTeam = 8;
-
-__global__ __launch_bounds__(kBlock) void row_gather_kernel(const uint32_t *__restrict__ poff,
-                                                            const uint32_t *__restrict__ piece, uint32_t n_rows,
-                                                            const ChainDev *__restrict__ chains,
-                                                            const ReqPartial *__restrict__ cpart,
-                                                            const QRes *__restrict__ res,
-                                                            const uint64_t *__restrict__ hoff,
-                                                            const uint64_t *__restrict__ hits, uint64_t rec_base,
-                                                            const uint64_t *__restrict__ row_off,
-                                                            const ulonglong2 *__restrict__ rowsrc,
-                                                            uint64_t *__restrict__ out) {
-    const uint32_t t = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t w = t / kGatherTeam, m = t % kGatherTeam;
-    if (w >= n_rows) return;
-    uint64_t d = row_off[w];
-    const ulonglong2 rs = rowsrc[w];
-    if (rs.x != ~0ull) {  // a single piece (or none): one contiguous copy
-        for (uint64_t j = m; j < rs.y; j += kGatherTeam) out[d + j] = hits[rs.x + j] + rec_base;
-        return;
-    }
-    for (uint32_t k = poff[w], e = poff[w + 1]; k < e; ++k) {
-        const uint32_t p = piece[k];
-        uint64_t a, n;
-        if (p & kPieceChain) {
-            const uint32_t c = p & ~kPieceChain;
-            a = chains[c].out;
-            n = static_cast<uint64_t>(cpart[c].n_variants);
-        } else {
-            a = hoff[p];
-            n = hit_count(res[p]);
-        }
-        for (uint64_t j = m; j < n; j += kGatherTeam) out[d + j] = hits[a + j] + rec_base;
-        d += n;
-    }
-}
-
-// The same copy, one wave per 64 consecutive rows: their outputs are one
-// contiguous range [row_off[r0], row_off[r0 + 64]) of the dense list, so
-// lane j of each pass writes output base + j (coalesced) and finds its row
-// by a binary search over the lanes' row starts.  Rows of one piece (or
-// none) read their hits from rowsrc.x; rows of several pieces (rowsrc.x =
-// ~0) are copied afterwards by their own lane, piece by piece.
 __global__ __launch_bounds__(kBlock) void row_gather_seg_kernel(const uint32_t *__restrict__ poff,
                                                                 const uint32_t *__restrict__ piece, uint32_t n_rows,
                                                                 const ChainDev *__restrict__ chains,
@@ -4102,32 +3827,12 @@ void launch_summarise(const SStore &ss, const SDev *slices, uint32_t ns, const u
 void launch_chains(const DStore &st, const ChainDev *chains, uint32_t n_chains, const uint32_t *runs, uint32_t n_runs,
                    const uint32_t *corig, QRes *res, uint64_t *hits, ReqPartial *cpart, hipStream_t s) {
     if (!n_chains) return;
-    if (!config().chain_seq) {  // SBEACON_CHAIN_KERNEL=seq: the chain-sequential kernel
-        // timing ablations (skip evaluation / results) exist only in a bench
-        // build (-DSBEACON_ABLATION): the product library always runs the full kernel
-#ifdef SBEACON_ABLATION
-        const uint32_t dbgv = static_cast<uint32_t>(config().pack_dbg);
-#else
-        const uint32_t dbgv = 0u;
-#endif
-        if (res || !cpart)
-            hipLaunchKernelGGL(chain_pack_kernel<true>, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs,
-                               n_runs, corig, res, hits, cpart, dbgv);
-        else
-            hipLaunchKernelGGL(chain_pack_kernel<false>, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs,
-                               n_runs, corig, res, hits, cpart, dbgv);
-        return;
-    }
-    // runs of kChainRun chains per wave while the launch still fills the chip
-    // (256 CUs x 4 SIMDs x 8 waves, 4 deep)
-    uint32_t run = kChainRun;
-    if (const int k = config().chain_run; k != 0) {
-        if (k >= 1) run = std::min<uint32_t>(kChainRun, static_cast<uint32_t>(k));
-    } else {
-        while (run > 1 && (n_chains + run - 1) / run < 32768u) run >>= 1;
-    }
-    hipLaunchKernelGGL(chain_kernel, dim3(blocks_for((n_chains + run - 1) / run)), dim3(kBlock), 0, s, st, chains,
-                       n_chains, run, corig, res, hits, cpart);
+    if (res || !cpart)
+        hipLaunchKernelGGL(chain_pack_kernel<true>, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs, n_runs,
+                           corig, res, hits, cpart);
+    else
+        hipLaunchKernelGGL(chain_pack_kernel<false>, dim3(blocks_for(n_runs)), dim3(kBlock), 0, s, st, chains, runs,
+                           n_runs, corig, res, hits, cpart);
 }
 
 uint64_t general_wave_bytes(const GStore &gs, uint32_t *hwords, uint32_t *tcap) {
@@ -4156,7 +3861,7 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
                          uint32_t n_rows, uint64_t rec_base, uint32_t n_lut, uint32_t run, unsigned int *err,
                          int compact, bool rec_staged, hipStream_t s, hipEvent_t ev0, hipEvent_t ev1,
                          const ReqIn *plan_in, uint32_t n_in, uint64_t stride, int inject, bool tile_scan,
-                         const ReqEsc &esc) {
+                         const ReqEsc &esc, bool lab7) {
     const bool rowc = compact == SB_COMPACT_ALL, hitc = compact != 0;  // u32 rows / offsets; u32 hits
     if (!n_runs) {
         (void)hipMemsetAsync(row_off, 0, rowc ? 4 : 8, s);
@@ -4201,13 +3906,14 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
     auto deliver = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg, shoff, sherr,
                            shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx, static_cast<void *>(out),
-                           n_rows, rec_base, err, gtot, esc);
+                           n_rows, rec_base, err, gtot, esc, lab7 ? 1u : 0u);
     };
     auto deliver_rec = [&](auto rec, auto gs) {
         constexpr bool R = decltype(rec)::value, G = decltype(gs)::value;
-        if (rowc) deliver(request_deliver_kernel<true, true, R, G>);
-        else if (hitc) deliver(request_deliver_kernel<false, true, R, G>);
-        else deliver(request_deliver_kernel<false, false, R, G>);
+        if (rowc && sres) deliver(request_deliver_kernel<true, true, R, G, true>);
+        else if (rowc) deliver(request_deliver_kernel<true, true, R, G, false>);
+        else if (hitc) deliver(request_deliver_kernel<false, true, R, G, true>);
+        else deliver(request_deliver_kernel<false, false, R, G, true>);
     };
     if (gsum) deliver_rec(std::true_type{}, std::true_type{});
     else if (rec_staged) deliver_rec(std::true_type{}, std::false_type{});
@@ -4310,15 +4016,9 @@ void launch_row_hit_lists(const ReqPartial *rows, const ulonglong2 *rowsrc, cons
         return;
     }
     hipLaunchKernelGGL(field_tile_scan_kernel, dim3(nt), dim3(kBlock), 0, s, nv, stride, n_rows, tsum, row_off);
-    if (config().row_gather_team) {  // SBEACON_ROW_GATHER=team: 8 lanes per row
-        const uint64_t threads = static_cast<uint64_t>(n_rows) * kGatherTeam;
-        hipLaunchKernelGGL(row_gather_kernel, dim3(static_cast<uint32_t>((threads + kBlock - 1) / kBlock)), dim3(kBlock),
-                           0, s, poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off, rowsrc, out);
-    } else {
-        hipLaunchKernelGGL(row_gather_seg_kernel, dim3(blocks_for((n_rows + kWave - 1) / kWave)), dim3(kBlock), 0, s,
-                           poff, piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off,
-                           reinterpret_cast<const uint64_t *>(rowsrc), 2u, out);
-    }
+    hipLaunchKernelGGL(row_gather_seg_kernel, dim3(blocks_for((n_rows + kWave - 1) / kWave)), dim3(kBlock), 0, s, poff,
+                       piece, n_rows, chains, cpart, res, hoff, hits, rec_base, row_off,
+                       reinterpret_cast<const uint64_t *>(rowsrc), 2u, out);
 }
 
 void mark_wide(const uint32_t *big_n, const GenBig *big, uint32_t cap, uint8_t *wide, hipStream_t s) {

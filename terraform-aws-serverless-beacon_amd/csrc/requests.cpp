@@ -680,6 +680,20 @@ void prepare_requests(sb_batch &B, const Src &src, size_t n) {
 
 }  // extern "C++"
 
+// a record with 8 ALTs (VtHot: 7 extra ALTs, the 3-bit field's most): the
+// only way a chain's staged hit carries the ALT label 7, which the compact
+// hit form escapes (request_deliver_kernel checks for it only then)
+bool store_has_label7(sb_store &s) {
+    std::call_once(s.label7_once, [&s] {
+        const size_t n = s.n_records;
+        for (size_t r = 0; r < n && !s.label7; ++r) {
+            const uint32_t nx = (r + 1 < n ? s.h_x_lo[r + 1] : static_cast<uint32_t>(s.n_extra)) - s.h_x_lo[r];
+            if (nx >= VT_MAX_NX) s.label7 = true;
+        }
+    });
+    return s.label7;
+}
+
 void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t rec_base) {
     sb_store &s = *B.s;
     sb_batch::Req &R = *B.req;
@@ -745,7 +759,8 @@ void run_requests(sb_batch &B, void *rows, void *hits, void *row_off, uint64_t r
                         R.stage.as<uint32_t>(), static_cast<uint64_t *>(hits), R.n_rows, rec_base, R.n_lut, R.run,
                         R.err.as<unsigned int>(), R.compact, rec_staged, st, ev[0], ev[1],
                         fuse ? R.din.as<ReqIn>() : nullptr, R.n_in, R.stage_stride, cfg.req_inject,
-                        cfg.req_tile_scan, ReqEsc{R.xrows.as<ReqPartial>(), R.row_flag.as<uint8_t>(), R.xlab.as<uint16_t>()});
+                        cfg.req_tile_scan, ReqEsc{R.xrows.as<ReqPartial>(), R.row_flag.as<uint8_t>(), R.xlab.as<uint16_t>()},
+                        R.compact && store_has_label7(s));
     HIP_OK(hipGetLastError());
 }
 

@@ -110,7 +110,16 @@ char *lit(char *o, const char (&x)[N]) {
 }
 
 // escaped length of UTF-8 text as json.dumps writes it; SIZE_MAX: not UTF-8
+// (printable ASCII without '"' / '\\' -- every allele in practice -- is its own length)
+bool plain(const char *p, size_t n) {
+    for (size_t i = 0; i < n; ++i) {
+        const unsigned char c = static_cast<unsigned char>(p[i]);
+        if (c < 0x20 || c >= 0x7f || c == '"' || c == '\\') return false;
+    }
+    return true;
+}
 size_t esc_len(const char *p, size_t n) {
+    if (plain(p, n)) return n;
     thread_local std::string tmp;
     tmp.clear();
     if (!json_escape_append(tmp, p, n)) return SIZE_MAX;
@@ -267,9 +276,9 @@ char *entry_write(const Ctx &C, char *o, uint32_t a, uint32_t cid, uint32_t rec,
         {num, static_cast<size_t>(ne - num)}, {"\t", 1}, {rp, rn}, {"\t", 1}, {ap, an}};
     o = b64_write(o, parts, 9);
     o = lit(o, kE1);
-    o = json_escape_to(o, rp, rn);
+    o = plain(rp, rn) ? put(o, rp, rn) : json_escape_to(o, rp, rn);
     o = lit(o, kE2);
-    o = json_escape_to(o, ap, an);
+    o = plain(ap, an) ? put(o, ap, an) : json_escape_to(o, ap, an);
     o = lit(o, kE3);
     o = dec_write(o, pos);
     o = lit(o, kE4);

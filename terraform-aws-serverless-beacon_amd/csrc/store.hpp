@@ -175,6 +175,8 @@ struct sb_store {
     std::once_flag req_pool_once;
     std::shared_ptr<void> var_text;      // wire: escaped variant-string tails (api.cpp VarText)
     std::once_flag var_text_once;
+    std::once_flag label7_once;  // request batches: some chain record has 8 ALTs (label 7; requests.cpp)
+    bool label7 = false;
     std::vector<sb::VcfData> vcfs;  // metadata (columns are moved to the globals below)
     std::unordered_map<std::string, uint32_t> vcf_by_location;
     sb::Dict vt, sym;

@@ -207,6 +207,7 @@ SIGNATURES = {
     'sb_store_close': (None, [P]),
     'sb_store_get_info': (C.c_int, [P, C.POINTER(StoreInfo)]),
     'sb_store_find_vcf': (C.c_int, [P, C.c_char_p, C.c_size_t, C.POINTER(C.c_uint32)]),
+    'sb_store_candidates': (C.c_int, [P, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     'sb_store_n_samples': (C.c_int, [P, C.c_uint32, C.POINTER(C.c_uint32)]),
     'sb_store_sample_name': (C.c_int, [P, C.c_uint32, C.c_uint32, C.POINTER(C.c_char_p),
                                        C.POINTER(C.c_size_t)]),
@@ -297,8 +298,11 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise OSError(f'{LIB_PATH} not found: build it with `python -c "import __graft_entry__ as g; g.build()"`')
         L = C.CDLL(LIB_PATH)
+        variant = 'SBEACON_LIB' in os.environ  # an A/B build of another revision: bind what it has
         for name, (res, args) in SIGNATURES.items():
-            fn = getattr(L, name)
+            fn = getattr(L, name, None) if variant else getattr(L, name)
+            if fn is None:
+                continue
             fn.restype = res
             fn.argtypes = args
         _lib = L

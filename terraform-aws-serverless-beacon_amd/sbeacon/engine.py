@@ -235,6 +235,13 @@ class Store:
             meta = json.load(f)
         return cls(s, meta['locations'], meta['paths'])
 
+    def candidates(self) -> tuple[int, int]:
+        """(variantType candidates, bytes of their VcQ words + record ids):
+        the request pass's working set (sb_store_candidates)."""
+        n, b = C.c_uint64(), C.c_uint64()
+        _lib.check(_lib.lib().sb_store_candidates(self.handle, C.byref(n), C.byref(b)))
+        return n.value, b.value
+
     def close(self):
         if self._h:
             lib().sb_store_close(self._h)

@@ -15,9 +15,13 @@ else
     git -C $R show $REV:$f > $W/pkg/csrc/$(basename $f); done
   git -C $R show $REV:include/sbeacon.h > $W/include/sbeacon.h
 fi
+# SED: an optional sed script applied to the variant's query_kernels.hip
+# (timing ablations: e.g. SED='s/^    if (nch) {$/    if (false) {/' skips
+# request_eval_kernel's candidate loop -- wrong answers, counters only)
+if [ -n "$SED" ]; then sed -i -e "$SED" $W/pkg/csrc/query_kernels.hip; fi
 FL="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -I$W/include $*"
 objs=""
-for s in api.cpp requests.cpp summarise.cpp results.cpp ingest.cpp index.cpp wire.cpp persist.cpp query_kernels.hip dedup_kernels.hip; do
+for s in $(ls $W/pkg/csrc | grep -E "\.(cpp|hip)$" | grep -v synth.cpp); do
   x=""; case $s in *.cpp) x="-x hip";; esac
   /opt/rocm/bin/hipcc $x $FL -c $W/pkg/csrc/$s -o $W/$s.o &
   objs="$objs $W/$s.o"
