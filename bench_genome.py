@@ -319,7 +319,7 @@ def main_genome(args):
         'higher_is_better': True,
         'scaling': args.scaling,
         'vs_baseline': None,
-        'dtype': 'int64',
+        'dtype': 'u32',  # compact outputs: rows as checked u32 sums, u32 offsets and hits
         'data': 'synthetic (seeded whole-genome 1000G-shape VCF text per contig shard + its 2504-sample carrier '
                 'bit-matrix, generated + ingested in-process)',
         'config': {'workload': 'config3-wgs-1000g-shape', 'records': shape.n_total, 'requests': n_req,

@@ -2585,14 +2585,16 @@ __global__ __launch_bounds__(1024) void request_tile_scan_kernel(const unsigned 
 // SLICED: the batch has a per-slice part (runs that are not simple); without
 // one a compact-row batch's runs are all simple and the row-by-row path is
 // not compiled in (registers of the common instantiation)
-template <bool ROWC, bool HITC, bool REC, bool GSUM, bool SLICED>
+// LAB7: the store holds an 8-ALT record, so a chain hit can carry the label
+// 7 that the compact hit form escapes (store_has_label7)
+template <bool ROWC, bool HITC, bool REC, bool GSUM, bool SLICED, bool LAB7>
 __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
     const RowRun *__restrict__ runs, uint32_t n_runs, const unsigned long long *__restrict__ status,
     const unsigned long long *__restrict__ toff, const QRes *__restrict__ sres, const uint32_t *__restrict__ sseg,
     const uint64_t *__restrict__ shoff, const uint8_t *__restrict__ sherr, const uint64_t *__restrict__ shits,
     void *__restrict__ row_off_out, const uint64_t *__restrict__ row_src, const uint32_t *__restrict__ stage,
     const uint32_t *__restrict__ vc_idx, void *__restrict__ out_v, uint32_t n_rows, uint64_t rec_base,
-    unsigned int *__restrict__ err, const unsigned long long *__restrict__ gtot, ReqEsc esc, uint32_t lab7) {
+    unsigned int *__restrict__ err, const unsigned long long *__restrict__ gtot, ReqEsc esc) {
     using Hit = std::conditional_t<HITC, uint32_t, uint64_t>;
     using Off = std::conditional_t<ROWC, uint32_t, uint64_t>;
     Hit *const out = static_cast<Hit *>(out_v);
@@ -2683,7 +2685,7 @@ __global__ __launch_bounds__(kBlock) void request_deliver_kernel(
                 const uint64_t j = j0 + kWave * u + ul;
                 if (j < H) out[O + j] = h[u];
             }
-            if (HITC && lab7) {  // (uniform: a store with an 8-ALT record) the label 7 escapes -- its ALT goes to xlab too
+            if constexpr (HITC && LAB7) {  // the label 7 escapes -- its ALT goes to xlab too
                 bool lab7x = false;
 #pragma unroll
                 for (uint32_t u = 0; u < kU; ++u) {
@@ -3906,14 +3908,19 @@ void launch_request_rows(const DStore &st, const ReqChain *chains, RowRun *runs,
     auto deliver = [&](auto kern) {
         hipLaunchKernelGGL(kern, grid, dim3(kBlock), 0, s, runs, n_runs, status, tstatus, sres, sseg, shoff, sherr,
                            shits, static_cast<void *>(row_off), row_src, stage, st.vc_idx, static_cast<void *>(out),
-                           n_rows, rec_base, err, gtot, esc, lab7 ? 1u : 0u);
+                           n_rows, rec_base, err, gtot, esc);
     };
     auto deliver_rec = [&](auto rec, auto gs) {
         constexpr bool R = decltype(rec)::value, G = decltype(gs)::value;
-        if (rowc && sres) deliver(request_deliver_kernel<true, true, R, G, true>);
-        else if (rowc) deliver(request_deliver_kernel<true, true, R, G, false>);
-        else if (hitc) deliver(request_deliver_kernel<false, true, R, G, true>);
-        else deliver(request_deliver_kernel<false, false, R, G, true>);
+        auto lab = [&](auto l) {
+            constexpr bool L7 = decltype(l)::value;
+            if (rowc && sres) deliver(request_deliver_kernel<true, true, R, G, true, L7>);
+            else if (rowc) deliver(request_deliver_kernel<true, true, R, G, false, L7>);
+            else if (hitc) deliver(request_deliver_kernel<false, true, R, G, true, L7>);
+            else deliver(request_deliver_kernel<false, false, R, G, true, false>);
+        };
+        if (lab7) lab(std::true_type{});
+        else lab(std::false_type{});
     };
     if (gsum) deliver_rec(std::true_type{}, std::true_type{});
     else if (rec_staged) deliver_rec(std::true_type{}, std::false_type{});
