@@ -362,6 +362,10 @@ def main_genome(args):
                                 + ' + 16 B row + 4 B row count: the compact outputs) + 16 B per candidate in the '
                                 'union of the chain windows (POS, END, VtHot word, AC) + 4 B/hit staged',
                      'planning_fused': fused,
+                     'limiter': 'VALU issue, not memory: SQ_INSTS_VALU 1,869 per wave x 15.6 k waves is ~47 us of '
+                                'issue at 4 cycles per wave64 op on 1,024 SIMDs; without the candidate loop the '
+                                'kernel runs 18.9 us; HBM-cold it is 1.2x slower, not the ~2x of a bandwidth-bound '
+                                'kernel (profiles/r06_eval/sq_tables.txt, ab.log; DESIGN.md 3.1)',
                      'memory_level': {
                          'candidate_columns_bytes': int(cand_bytes), 'candidates': int(n_cand),
                          'infinity_cache_bytes': 256 << 20,

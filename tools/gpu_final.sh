@@ -1,5 +1,6 @@
-# round-end validation and evidence (round 5): smoke, every GPU test, the
-# default bench line (config 3), config 4 (bench_paths, 50 datasets), a
+# round-end validation and evidence (round 6): smoke, every GPU test, the
+# default bench line (config 3, with its config-4 sub-object: bench_paths at
+# 50 datasets), a
 # rocprofv3 kernel summary of the default bench, and the two PMC passes
 # (FETCH_SIZE, WRITE_SIZE: separate runs, kernel trace only) of the rotating
 # config-3 request passes folded into traffic_genome.json; stops at the
@@ -18,7 +19,6 @@ step() {  # name, limit, command...
 ${SKIP_TESTS:+false} step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" || true
 ${SKIP_TESTS:+false} step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread || true
 step bench 600 python3 -u $R/bench.py --steps 20 --warmup 5
-step paths 600 python3 -u $R/bench_paths.py --datasets 50
 cd /tmp
 step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 -u $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline
 step save 300 python3 -u $R/tools/req_tune.py --save /tmp/st --rounds 3 --digest
