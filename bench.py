@@ -68,6 +68,10 @@ def parse():
                     help='config 3 only: skip the config-4 sub-object (summariseSlice + duplicateVariantSearch on the '
                          '50-dataset cohort, bench_paths.py) the default N=1 run appends')
     ap.add_argument('--config4-datasets', type=int, default=50)
+    ap.add_argument('--no-config5', action='store_true',
+                    help='config 3 only: skip the config-5 sub-object (gnomAD-shape shard, bench_gnomad.py)')
+    ap.add_argument('--no-config2', action='store_true',
+                    help='config 3 only: skip the config-2 sub-object (chr22-shape requests + the wire figure)')
     ap.add_argument('--gnomad-records', type=int, default=750_000_000)
     ap.add_argument('--gnomad-requests', type=int, default=50_000, help='config-5 requests per GPU')
     args = ap.parse_args()
@@ -161,13 +165,43 @@ def main():
         from bench_genome import main_genome
         out = main_genome(args)
         if out is not None:  # rank 0
-            if int(os.environ.get('WORLD_SIZE', 1)) == 1 and not args.no_config4:
-                out['config4'] = config4_lines(args)
+            if int(os.environ.get('WORLD_SIZE', 1)) == 1:
+                # the other BASELINE configs beside the headline, each after
+                # the previous store is released (N=1 only; each carries its
+                # own timing, roofline, CPU baseline and oracle parity sample)
+                if not args.no_config4:
+                    out['config4'] = config4_lines(args)
+                if not args.no_config5:
+                    from bench_gnomad import main_gnomad
+                    t0 = time.perf_counter()
+                    out['config5'] = sub_line(main_gnomad(args))
+                    out['config5']['seconds'] = round(time.perf_counter() - t0, 1)
+                if not args.no_config2:
+                    t0 = time.perf_counter()
+                    out['config2'] = sub_line(main_chr22(args))
+                    out['config2']['seconds'] = round(time.perf_counter() - t0, 1)
             print(json.dumps(out), flush=True)
         return
     if args.workload == 'gnomad':
         from bench_gnomad import main_gnomad
-        return main_gnomad(args)
+        out = main_gnomad(args)
+    else:
+        out = main_chr22(args)
+    if out is not None:  # rank 0
+        print(json.dumps(out), flush=True)
+
+
+def sub_line(out: dict) -> dict:
+    """A workload's line as a sub-object of the headline line."""
+    keep = ('metric', 'value', 'unit', 'ms_per_step', 'dtype', 'device_ms_per_step', 'config', 'roofline',
+            'delivered', 'cpu_baseline', 'parity_sample', 'ingest_s', 'device_gib')
+    return {k: out[k] for k in keep if k in out}
+
+
+def main_chr22(args):
+    """Config 2 (BASELINE configs[1]): 10 k range / point requests on the
+    chr22-shape store, replicas across ranks.  Returns rank 0's line (None
+    on the other ranks); the store is released before returning."""
     rank = int(os.environ.get('RANK', 0))
     world = int(os.environ.get('WORLD_SIZE', 1))
     local = int(os.environ.get('LOCAL_RANK', 0))
@@ -327,10 +361,12 @@ def main():
         'parity_sample': parity,
         'ingest_s': round(t_ingest, 2),
     }
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    del batch, rs
+    store.close()
+    torch.cuda.empty_cache()
     if dist:
         dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 def cpu_baseline_and_parity(args, gen, reqs, payloads, owner, rs):

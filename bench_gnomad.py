@@ -170,10 +170,12 @@ def main_gnomad(args):
         'ingest_s': round(t_ingest, 2),
         'device_gib': round(info['device_bytes'] / 2**30, 2),
     }
-    if rank == 0:
-        print(json.dumps(out), flush=True)
+    del batch, rs
+    store.close()
+    torch.cuda.empty_cache()
     if dist:
         dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 def _write_vcf(path, shape, sl, idx, sites_only, threads):
