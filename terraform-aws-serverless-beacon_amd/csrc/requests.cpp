@@ -243,6 +243,16 @@ void upload_slice_part(sb_batch &B, sb_batch::Req &R, const std::vector<uint32_t
 // (pipelined callers) neither queue behind nor wait for each other's uploads
 // and planning kernels on the store stream.  Everything planned on it is
 // synchronised before prepare returns.
+// a packed request written with non-temporal stores: the pinned block is
+// read by the DMA engine, never again by this CPU, so its lines need no
+// read-for-ownership (a third less host memory traffic in the pack)
+inline void stream_store(ReqIn *dst, const ReqIn &v) {
+    typedef long long v2i __attribute__((vector_size(16)));
+    const v2i *src = reinterpret_cast<const v2i *>(&v);
+    v2i *d = reinterpret_cast<v2i *>(dst);
+    __builtin_nontemporal_store(src[0], d);
+    __builtin_nontemporal_store(src[1], d + 1);
+}
 hipStream_t planning_stream(int device) {
     thread_local std::vector<hipStream_t> per_dev;
     if (per_dev.size() <= static_cast<size_t>(device)) per_dev.resize(device + 1, nullptr);
@@ -318,7 +328,17 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
     std::memcpy(static_cast<char *>(pin.p) + lut_at, lut_all.data(), lut_all.size() * 4);
     std::vector<uint8_t> cls(n, 0);
     std::atomic<bool> any_slices{false};
-    parallel_for(n, [&](size_t i) {
+    HIP_OK(hipSetDevice(s.device));
+    hipStream_t st = planning_stream(s.device);
+    DevMem din = P.get_dev(n * sizeof(ReqIn));
+    // an exception past the first queued upload leaves by way of a stream
+    // wait: no DMA still reading the pinned block or writing `din` when they
+    // go back to the pool (on the normal path the stream is idle by then)
+    struct Drain {
+        hipStream_t s;
+        ~Drain() { (void)hipStreamSynchronize(s); }
+    } drain{st};
+    auto pack_row = [&](size_t i) {
         const PackRow x = get(i);
         const uint32_t contig = x.contig;
         const int64_t smin = x.smin, smax = x.smax;
@@ -353,25 +373,40 @@ bool prepare_requests_device(sb_batch &B, const sb_request_columns &c, size_t n,
                 o.cls = REQ_CHAIN | static_cast<uint32_t>(nsl) << 2;
             }
         }
-        pk[i] = o;
-    });
+        stream_store(pk + i, o);
+    };
+    // packed in pieces, each piece's upload queued as soon as it is packed:
+    // the DMA of piece j (pinned source, the planning stream) runs while the
+    // host packs piece j + 1, so the upload hides behind the pack but for
+    // the last piece
+    const size_t pieces = n >= (size_t(1) << 18) ? 4 : 1;
+    for (size_t j = 0; j < pieces; ++j) {
+        const size_t a = n * j / pieces, b = n * (j + 1) / pieces;
+        const size_t m = b - a, parts = std::min<size_t>(16, std::max<size_t>(1, m / 4096));
+        parallel_for(
+            parts,
+            [&](size_t k) {
+                for (size_t i = a + m * k / parts, e = a + m * (k + 1) / parts; i < e; ++i) pack_row(i);
+                __builtin_ia32_sfence();  // this thread's streaming stores drained before the upload is queued
+            },
+            16, 1);
+        HIP_OK(hipMemcpyAsync(din.as<char>() + a * sizeof(ReqIn), pk + a, (b - a) * sizeof(ReqIn),
+                              hipMemcpyHostToDevice, st));
+    }
     tick("pack");
     std::vector<uint32_t> seg;
     if (any_slices.load()) slice_part(B, *R, ColSrc{full()}, n, cls, seg);
     tick("slices");
-    HIP_OK(hipSetDevice(s.device));
-    hipStream_t st = planning_stream(s.device);
     const uint32_t n_runs = static_cast<uint32_t>((n + kRunRows - 1) / kRunRows);
     const size_t chain_bytes = size_t(n_runs) * kReqRun * sizeof(ReqChain), run_bytes = size_t(n_runs) * sizeof(RowRun);
     // rc: per run {capacity, slices << 32 | chains} (request_plan_kernel), then the 3 counters
-    DevMem din = P.get_dev(n * sizeof(ReqIn)), rc = P.get_dev(request_plan_words(n_runs) * 8);
+    DevMem rc = P.get_dev(request_plan_words(n_runs) * 8);
     R->dchains = P.get_dev(chain_bytes + run_bytes);
     R->runs_at = chain_bytes;
     R->n_runs = n_runs;
     unsigned long long *cnt = reinterpret_cast<unsigned long long *>(rc.as<char>() + size_t(n_runs) * 16);
     R->lut = P.get_dev(lut_all.size() * 4);
     R->n_lut = static_cast<uint32_t>(lut_all.size());
-    HIP_OK(hipMemcpyAsync(din.p, pk, n * sizeof(ReqIn), hipMemcpyHostToDevice, st));
     HIP_OK(hipMemcpyAsync(R->lut.p, static_cast<char *>(pin.p) + lut_at, lut_all.size() * 4, hipMemcpyHostToDevice, st));
     HIP_OK(hipMemsetAsync(cnt, 0, 32, st));
     launch_request_plan(s.d, din.as<ReqIn>(), static_cast<uint32_t>(n), R->dchains.as<ReqChain>(),

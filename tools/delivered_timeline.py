@@ -1,4 +1,4 @@
-"""Config-3 delivered path diagnostics: the device planner's phase times
+"""Config-3 delivered path diagnostics (compact outputs, as the bench's delivered path): the device planner's phase times
 (SBEACON_PREP_TRACE, one serial prepare of 1 M requests) and a per-chunk
 timeline of the pipelined path (worker prepare start/end, main-thread
 enqueue, offsets back, hits back) for a few chunk / worker settings.  Builds
@@ -96,10 +96,10 @@ def timeline(store, shape, reqs, base, dev, chunks, workers, passes=5, taper=Fal
     n = len(reqs)
     cuts = chunk_cuts(n, chunks, taper)
     stream = torch.cuda.current_stream()
-    rows_h = torch.empty((n, 5), dtype=torch.int64, pin_memory=True)
-    ro_h = torch.empty(n + chunks, dtype=torch.int64, pin_memory=True)
-    rows_d = torch.empty((n, 5), dtype=torch.int64, device=dev)
-    ro_d = torch.empty(n + chunks, dtype=torch.int64, device=dev)
+    rows_h = torch.empty((n, 4), dtype=torch.int32, pin_memory=True)
+    ro_h = torch.empty(n + chunks, dtype=torch.int32, pin_memory=True)
+    rows_d = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    ro_d = torch.empty(n + chunks, dtype=torch.int32, device=dev)
     hits_d, hits_h = [None] * chunks, [None] * chunks
     out = []
     with ThreadPoolExecutor(workers) as ex:
@@ -122,9 +122,10 @@ def timeline(store, shape, reqs, base, dev, chunks, workers, passes=5, taper=Fal
                 a, m, bt, cap = futs[k].result()
                 ev[k]['got'] = time.perf_counter() - t0
                 if hits_d[k] is None or hits_d[k].numel() < max(cap, 1):
-                    hits_d[k] = torch.empty(max(cap, 1), dtype=torch.int64, device=dev)
-                    hits_h[k] = torch.empty(max(cap, 1), dtype=torch.int64, pin_memory=True)
+                    hits_d[k] = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+                    hits_h[k] = torch.empty(max(cap, 1), dtype=torch.int32, pin_memory=True)
                 bt.set_stream(stream.cuda_stream)
+                bt.set_compact(True)
                 ro = ro_d[a + k:a + k + m + 1]
                 bt.run(rows_d[a:a + m].data_ptr(), hits_d[k].data_ptr(), ro.data_ptr(), base)
                 rows_h[a:a + m].copy_(rows_d[a:a + m], non_blocking=True)
@@ -138,16 +139,17 @@ def timeline(store, shape, reqs, base, dev, chunks, workers, passes=5, taper=Fal
                     kk, e2, last = pend.pop(0)
                     e2.synchronize()
                     ev[kk]['off'] = time.perf_counter() - t0
-                    nh = int(ro_h[last])
+                    nh = int(ro_h[last].numpy().view(np.uint32))
                     hits_h[kk][:nh].copy_(hits_d[kk][:nh], non_blocking=True)
             for kk, e2, last in pend:
                 e2.synchronize()
                 ev[kk]['off'] = time.perf_counter() - t0
-                nh = int(ro_h[last])
+                nh = int(ro_h[last].numpy().view(np.uint32))
                 hits_h[kk][:nh].copy_(hits_d[kk][:nh], non_blocking=True)
             stream.synchronize()
             dt = time.perf_counter() - t0
             for bt in live:
+                bt.sync()
                 bt.free()
             if p:
                 out.append({'ms': round(dt * 1e3, 2),
@@ -175,12 +177,7 @@ def main():
         print(json.dumps({'serial_prepare_ms': round((time.perf_counter() - t) * 1e3, 2)}), flush=True)
         b.free()
     del os.environ['SBEACON_PREP_TRACE']
-    for chunks, workers in ((8, 2), (12, 2), (16, 2)):
-        tl = timeline_zc(store, shape, reqs, base, dev, chunks, workers)
-        ms = sorted(x['ms'] for x in tl)
-        print(json.dumps({'zero_copy_hits': True, 'chunks': chunks, 'workers': workers, 'median_ms': ms[len(ms) // 2],
-                          'ms': [x['ms'] for x in tl], 'hits': tl[-1]['hits']}), flush=True)
-    for chunks, workers, taper in ((8, 2, False), (8, 2, True)):
+    for chunks, workers, taper in ((8, 2, True), (8, 3, True), (16, 2, True), (4, 2, True)):
         tl = timeline(store, shape, reqs, base, dev, chunks, workers, passes=7, taper=taper)
         ms = sorted(x['ms'] for x in tl)
         print(json.dumps({'chunks': chunks, 'workers': workers, 'taper': taper, 'median_ms': ms[len(ms) // 2],
