@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Config-3 delivered-path A/B (host preparation, not the bench): re-opens a
+"""Config-3 delivered-path A/B (host preparation and, with --routes, the
+route-body fold; not the bench): re-opens a
 store saved by tools/req_tune.py --save (library variants via SBEACON_LIB on
 one box), then times sb_requests_prepare_beacon of 1 M requests alone
 (median of --rounds) and the bench's serial and streaming delivered forms
@@ -20,6 +21,7 @@ def main():
     ap.add_argument('--open', required=True)
     ap.add_argument('--records', type=int, default=85_000_000)
     ap.add_argument('--rounds', type=int, default=15)
+    ap.add_argument('--routes', action='store_true', help='also time requests -> route bodies (route_bodies_passes)')
     args = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -43,7 +45,12 @@ def main():
     serial = bench_genome.delivered_passes(None, store, shape, reqs, 1, 0, base, dev)
     stream = [bench_genome.delivered_streaming(None, store, shape, reqs, 1, 0, base, dev) for _ in range(3)]
     stream.sort(key=lambda x: x['ms_per_batch'])
-    print(json.dumps({'lib': os.environ.get('SBEACON_LIB', 'in-tree'),
+    routes = None
+    if args.routes:
+        r, _ = bench_genome.route_bodies_passes(None, store, shape, reqs, 1, 0, base, dev)
+        routes = {'ms_per_pass': r['ms_per_pass'], 'best_ms': r['best_ms'], 'split_ms': r['split_ms'],
+                  'body_bytes': r['body_bytes']}
+    print(json.dumps({'routes': routes, 'lib': os.environ.get('SBEACON_LIB', 'in-tree'),
                       'prepare_ms_median': round(t[len(t) // 2] * 1e3, 3), 'prepare_ms_min': round(t[0] * 1e3, 3),
                       'serial_ms': serial['ms_per_pass'], 'serial_split': serial['split_ms'],
                       'streaming_ms': [x['ms_per_batch'] for x in stream],
