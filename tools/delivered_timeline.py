@@ -177,7 +177,7 @@ def main():
         print(json.dumps({'serial_prepare_ms': round((time.perf_counter() - t) * 1e3, 2)}), flush=True)
         b.free()
     del os.environ['SBEACON_PREP_TRACE']
-    for chunks, workers, taper in ((8, 2, True), (8, 3, True), (16, 2, True), (4, 2, True)):
+    for chunks, workers, taper in ((8, 2, True), (4, 1, True), (8, 1, True), (4, 2, True), (6, 1, True)):
         tl = timeline(store, shape, reqs, base, dev, chunks, workers, passes=7, taper=taper)
         ms = sorted(x['ms'] for x in tl)
         print(json.dumps({'chunks': chunks, 'workers': workers, 'taper': taper, 'median_ms': ms[len(ms) // 2],
