@@ -169,17 +169,27 @@ def main():
                 # the other BASELINE configs beside the headline, each after
                 # the previous store is released (N=1 only; each carries its
                 # own timing, roofline, CPU baseline and oracle parity sample)
+                # a sub-line that raises (a parity mismatch included) is
+                # recorded as its error; the headline line is still printed
+                def sub(key, fn):
+                    t0 = time.perf_counter()
+                    try:
+                        out[key] = fn()
+                    except Exception as e:  # noqa: BLE001 -- reported in the line, not swallowed
+                        import traceback
+                        log(traceback.format_exc())
+                        out[key] = {'error': f'{type(e).__name__}: {e}'}
+                        import torch
+                        torch.cuda.empty_cache()
+                    out[key]['seconds'] = round(time.perf_counter() - t0, 1)
+
                 if not args.no_config4:
-                    out['config4'] = config4_lines(args)
+                    sub('config4', lambda: config4_lines(args))
                 if not args.no_config5:
                     from bench_gnomad import main_gnomad
-                    t0 = time.perf_counter()
-                    out['config5'] = sub_line(main_gnomad(args))
-                    out['config5']['seconds'] = round(time.perf_counter() - t0, 1)
+                    sub('config5', lambda: sub_line(main_gnomad(args)))
                 if not args.no_config2:
-                    t0 = time.perf_counter()
-                    out['config2'] = sub_line(main_chr22(args))
-                    out['config2']['seconds'] = round(time.perf_counter() - t0, 1)
+                    sub('config2', lambda: sub_line(main_chr22(args)))
             print(json.dumps(out), flush=True)
         return
     if args.workload == 'gnomad':
