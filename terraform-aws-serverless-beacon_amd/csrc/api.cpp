@@ -1186,6 +1186,11 @@ void run(sb_batch &B) {
     run_kernels(B);
 }
 
+#ifndef SBEACON_PAR_GROUPS
+#define SBEACON_PAR_GROUPS 1
+#endif
+constexpr bool kParGroups = SBEACON_PAR_GROUPS != 0;
+
 void run_kernels(sb_batch &B) {
     sb_store &s = *B.s;
     HIP_OK(hipSetDevice(s.device));
@@ -1210,8 +1215,27 @@ void run_kernels(sb_batch &B) {
         for (const auto &g : B.groups)
             if (g.max_words == 0 && g.mode == mode)
                 fg.push_back(FusedGroup{B.q.as<QDev>() + g.base, static_cast<uint32_t>(g.idx.size()), g.mode});
+    // with sample-path groups too, the fused launch runs on a second stream
+    // beside them (disjoint results and hit regions; both may append to the
+    // general-record work list, atomically): a short scan-bound launch and a
+    // long carrier-row-bound one share the device instead of queueing
+    const bool scans = std::any_of(B.groups.begin(), B.groups.end(), [](const sb_batch::Group &g) {
+        return g.max_words != 0 && !g.idx.empty();
+    });
+    const bool split = kParGroups && scans && !fg.empty();
+    hipStream_t fs = st;
+    if (split) {
+        if (!B.aux) {
+            HIP_OK(hipStreamCreateWithFlags(&B.aux, hipStreamNonBlocking));
+            for (auto &e : B.fork) HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        }
+        HIP_OK(hipEventRecord(B.fork[0], st));
+        HIP_OK(hipStreamWaitEvent(B.aux, B.fork[0], 0));
+        fs = B.aux;
+    }
     launch_fused(d, fg.data(), static_cast<int>(fg.size()), B.nonneg, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(),
-                 B.res.as<QRes>(), B.hits.as<uint64_t>(), st);
+                 B.res.as<QRes>(), B.hits.as<uint64_t>(), fs);
+    if (split) HIP_OK(hipEventRecord(B.fork[1], B.aux));
     // the sample path ORs words past its register window into samples_out
     // (> 65,536-sample VCFs): start every run from zero
     if (B.samples_out.bytes && std::any_of(B.groups.begin(), B.groups.end(), [](const sb_batch::Group &g) {
@@ -1223,6 +1247,7 @@ void run_kernels(sb_batch &B) {
             launch_scan(d, B.q.as<QDev>() + g.base, nullptr, static_cast<uint32_t>(g.idx.size()), B.nonneg,
                         g.max_words, g.mode, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(), B.res.as<QRes>(),
                         B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), st);
+    if (split) HIP_OK(hipStreamWaitEvent(st, B.fork[1], 0));  // join before the general records and the next run
     // slices whose scan reached a general record (work list filled above)
     launch_general(d, s.g, B.gen_work.as<uint32_t>(), B.gen_grid, B.qbytes.as<uint8_t>(), B.subsets.as<uint64_t>(),
                    B.res.as<QRes>(), B.hits.as<uint64_t>(), B.samples_out.as<uint64_t>(), B.gen_scratch.as<uint8_t>(),

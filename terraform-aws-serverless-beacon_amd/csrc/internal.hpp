@@ -486,6 +486,10 @@ struct sb_batch {
     uint32_t gen_grid = 0, gen_big_cap = 0;
     // events around the runs since the last sync (run() records [0], sync() [1])
     std::array<hipEvent_t, 2> ev{};
+    // a second stream for the sample-free groups of a batch that also has
+    // sample-path groups (run_kernels): fork / join events on the batch stream
+    hipStream_t aux = nullptr;
+    std::array<hipEvent_t, 2> fork{};
     size_t runs_pending = 0;
     float last_total_ms = 0;
     std::mutex mu;  // request batches: one pass at a time per batch
@@ -493,6 +497,12 @@ struct sb_batch {
         for (auto e : ev)
             if (e) (void)hipEventDestroy(e);
         if ((req && req->pool) || pool) (void)hipStreamSynchronize(strm());  // a pass may still be in flight
+        if (aux) {  // (its work is joined into strm() by every run; waited for again here)
+            (void)hipStreamSynchronize(aux);
+            (void)hipStreamDestroy(aux);
+        }
+        for (auto e : fork)
+            if (e) (void)hipEventDestroy(e);
         if (req && req->pool) req->give_back();
         if (pool)
             for (DevMem *m : {&q, &hoff, &qbytes, &subsets, &lut, &res, &hits, &samples_out, &chains, &runs, &corig,
