@@ -1222,7 +1222,10 @@ void run_kernels(sb_batch &B) {
     const bool scans = std::any_of(B.groups.begin(), B.groups.end(), [](const sb_batch::Group &g) {
         return g.max_words != 0 && !g.idx.empty();
     });
-    const bool split = kParGroups && scans && !fg.empty();
+    // (not on the legacy default stream: an event recorded on hipStreamLegacy
+    // and waited for on another stream crashed the HIP runtime in
+    // hipStreamWaitEvent -- the request batches' tests found it)
+    const bool split = kParGroups && scans && !fg.empty() && st != hipStreamLegacy;
     hipStream_t fs = st;
     if (split) {
         if (!B.aux) {
