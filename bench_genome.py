@@ -544,7 +544,7 @@ def delivered_passes(args, store, shape, reqs, world, rank, base, dev, passes=5)
                     'the timed region (digest over the widened outputs)'}
 
 
-def delivered_streaming(args, store, shape, reqs, world, rank, base, dev, batches=8):
+def delivered_streaming(args, store, shape, reqs, world, rank, base, dev, batches=8, blocking=True):
     """A serving loop's steady state: consecutive 1 M-request batches, batch
     i + 1 routed and prepared on a host thread (sb_requests_prepare_beacon on
     every core the library's pool holds) while batch i runs and copies its
@@ -577,6 +577,17 @@ def delivered_streaming(args, store, shape, reqs, world, rank, base, dev, batche
     ro_h = torch.empty(ro_d.shape, dtype=torch.int32, pin_memory=True)
     hits_h = torch.empty(hits_d.shape, dtype=torch.int32, pin_memory=True)
     totals = []
+
+    # the main thread waits for its copies with a blocking-sync event (it
+    # sleeps instead of spinning on a core the preparing thread's pack needs)
+    def wait():
+        if not blocking:
+            stream.synchronize()
+            return
+        e = torch.cuda.Event(blocking=True)
+        e.record(stream)
+        e.synchronize()
+
     import gc
     gc.collect()
     gc.disable()
@@ -595,10 +606,10 @@ def delivered_streaming(args, store, shape, reqs, world, rank, base, dev, batche
             bt.run(rows_d.data_ptr(), hits_d.data_ptr(), ro_d.data_ptr(), base)
             rows_h[:m].copy_(rows_d[:m], non_blocking=True)
             ro_h.copy_(ro_d, non_blocking=True)
-            stream.synchronize()
+            wait()
             total = int(ro_h[m].numpy().view(np.uint32))
             hits_h[:total].copy_(hits_d[:total], non_blocking=True)
-            stream.synchronize()
+            wait()
             bt.sync()  # the pass's invariant word (a serving loop checks it too)
             bt.free()  # its buffers back to the store's pool for batch i + 2
             totals.append(total)
@@ -611,9 +622,11 @@ def delivered_streaming(args, store, shape, reqs, world, rank, base, dev, batche
     return {'requests_per_s': round(n * batches / dt, 1), 'ms_per_batch': round(dt / batches * 1e3, 2),
             'batches': batches, 'hits_returned': total, 'hits_equal_every_batch': len(set(totals)) == 1,
             'digest': digest(rows_w, [hits_w]),
+            'blocking_waits': blocking,
             'note': 'steady state of back-to-back 1 M-request batches: batch i+1 routed + prepared on one host '
                     'thread while batch i runs and copies back (compact rows, u32 offsets and hits into pinned '
-                    'host memory); requests over the wall time of all batches, the first preparation included'}
+                    'host memory; the main thread waits on blocking-sync events); requests over the wall time of '
+                    'all batches, the first preparation included'}
 
 
 def cold_launch_probe(store, shape, reqs, world, rank, base, dev):

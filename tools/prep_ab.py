@@ -45,6 +45,8 @@ def main():
     serial = bench_genome.delivered_passes(None, store, shape, reqs, 1, 0, base, dev)
     stream = [bench_genome.delivered_streaming(None, store, shape, reqs, 1, 0, base, dev) for _ in range(3)]
     stream.sort(key=lambda x: x['ms_per_batch'])
+    spin = [bench_genome.delivered_streaming(None, store, shape, reqs, 1, 0, base, dev, blocking=False) for _ in range(3)]
+    spin.sort(key=lambda x: x['ms_per_batch'])
     routes = None
     if args.routes:
         r, _ = bench_genome.route_bodies_passes(None, store, shape, reqs, 1, 0, base, dev)
@@ -54,6 +56,7 @@ def main():
                       'prepare_ms_median': round(t[len(t) // 2] * 1e3, 3), 'prepare_ms_min': round(t[0] * 1e3, 3),
                       'serial_ms': serial['ms_per_pass'], 'serial_split': serial['split_ms'],
                       'streaming_ms': [x['ms_per_batch'] for x in stream],
+                      'streaming_spin_ms': [x['ms_per_batch'] for x in spin],
                       'digest': serial['digest'], 'streaming_digest': stream[0]['digest']}), flush=True)
 
 
