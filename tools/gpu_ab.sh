@@ -16,8 +16,10 @@ step() {  # name, limit, command...
   case $rc in 0) return 0;; *) exit $rc;; esac
 }
 step save 400 python3 -u $R/tools/req_tune.py --save /tmp/st --rounds 2
-for v in $VARIANTS; do
-  SBEACON_LIB=$R/tools/variants/$v/libsbeacon_hip.so step ab_$v 200 python3 -u $R/tools/req_tune.py --open /tmp/st --rounds ${ROUNDS:-15} --digest
+i=0
+for v in $VARIANTS; do  # (ab_<variant>_<i>.log: a variant listed twice keeps both runs)
+  i=$((i+1))
+  SBEACON_LIB=$R/tools/variants/$v/libsbeacon_hip.so step ab_${v}_$i 200 python3 -u $R/tools/req_tune.py --open /tmp/st --rounds ${ROUNDS:-15} --digest
 done
 for v in $SQ; do  # SQ = variants whose SQ instruction counters are collected (one rocprofv3 pass each)
   ( cd /tmp && SBEACON_LIB=$R/tools/variants/$v/libsbeacon_hip.so step sq_$v 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES --kernel-trace --output-format csv -d $O/sq_$v -o p -- python3 -u $R/tools/req_tune.py --open /tmp/st --rounds 2 ) || exit 1
