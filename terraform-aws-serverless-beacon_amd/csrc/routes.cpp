@@ -26,6 +26,8 @@
 // argument (the gate then depends on completion order): its events go
 // through the Python route (status 1).
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -199,6 +201,34 @@ struct Ctx {
         const uint32_t x = s.h_x_lo[rec] + k - 1;
         n = s.h_x_len[x];
         return reinterpret_cast<const char *>(s.h_blob.data() + s.h_x_off[x]);
+    }
+    // the record columns a hit's fold reads, and (once those have arrived)
+    // its allele text: each hit's record is a random line in every column,
+    // so an event's hits are prefetched two and one events ahead of its fold
+    void prefetch_cols(uint64_t h0, uint64_t h1) const {
+        for (uint64_t h = h0; h < h1; ++h) {
+            const uint64_t v = compact ? static_cast<const uint32_t *>(in.hits)[h] & kStageCandMask
+                                       : static_cast<const uint64_t *>(in.hits)[h] & 0xffffffffull;
+            if (v < in.rec_base || v - in.rec_base >= s.n_records) continue;
+            const uint32_t r = static_cast<uint32_t>(v - in.rec_base);
+            __builtin_prefetch(&s.h_pos[r]);
+            __builtin_prefetch(&s.h_end[r]);
+            __builtin_prefetch(&s.h_x_lo[r]);
+            __builtin_prefetch(&s.h_vt[r]);
+            __builtin_prefetch(&s.h_ref_off[r]);
+            __builtin_prefetch(&s.h_a0_off[r]);
+            __builtin_prefetch(&s.h_a0_len[r]);
+        }
+    }
+    void prefetch_text(uint64_t h0, uint64_t h1) const {
+        for (uint64_t h = h0; h < h1; ++h) {
+            const uint64_t v = compact ? static_cast<const uint32_t *>(in.hits)[h] & kStageCandMask
+                                       : static_cast<const uint64_t *>(in.hits)[h] & 0xffffffffull;
+            if (v < in.rec_base || v - in.rec_base >= s.n_records) continue;
+            const uint32_t r = static_cast<uint32_t>(v - in.rec_base);
+            __builtin_prefetch(s.h_blob.data() + s.h_ref_off[r]);
+            __builtin_prefetch(s.h_blob.data() + s.h_a0_off[r]);
+        }
     }
     bool same_ref_alt(const EvHit &a, const EvHit &b) const {
         if (a.rec == b.rec && a.alt == b.alt) return true;
@@ -390,11 +420,42 @@ extern "C" int sb_route_bodies(sb_store *s, const sb_route_input *in, sb_json_ou
                      "\", \"requestedSchemas\": [], \"pagination\": ";
         const uint64_t n_hits = n_rows ? C.off(n_rows) : 0;
         if (n_hits && !in->hits) throw Error(SB_EINVAL, "NULL hits");
+        // SBEACON_WIRE_TRACE=1: the fold's phase times (stderr)
+        const bool trace = config().wire_trace;
+        auto t_last = std::chrono::steady_clock::now();
+        auto tick = [&](const char *what) {
+            if (!trace) return;
+            const auto t = std::chrono::steady_clock::now();
+            std::fprintf(stderr, "[route] %-8s %8.2f ms\n", what, std::chrono::duration<double, std::milli>(t - t_last).count());
+            t_last = t;
+        };
+        tick("setup");
         std::vector<uint8_t> first_id(n_hits, 0);  // hit h opens its internal id's entry
         std::vector<EvOut> eo(ne);
         // pass 1: fold each event, size its body
         FirstError fe;
+        // an event's hit range (prefetching: the events ahead of the fold)
+        auto ev_hits = [&](size_t e, uint64_t &h0, uint64_t &h1) {
+            const sb_route_event &E = in->events[e];
+            h0 = h1 = 0;
+            if (!n_hits || E.row_hi <= E.row_lo) return;
+            h0 = C.off(E.row_lo);
+            h1 = std::min<uint64_t>(C.off(E.row_hi), n_hits);
+            h0 = std::min(h0, h1);
+        };
+        auto prefetch_ahead = [&](size_t e) {
+            uint64_t a, b;
+            if (e + 4 < ne) {
+                ev_hits(e + 4, a, b);
+                C.prefetch_cols(a, b);
+            }
+            if (e + 2 < ne) {
+                ev_hits(e + 2, a, b);
+                C.prefetch_text(a, b);
+            }
+        };
         parallel_for(ne, fe.wrap([&](size_t e) {
+            prefetch_ahead(e);
             const sb_route_event &E = in->events[e];
             EvOut &O = eo[e];
             const uint8_t g = E.granularity;
@@ -502,6 +563,7 @@ extern "C" int sb_route_bodies(sb_store *s, const sb_route_input *in, sb_json_ou
             O.len = n;
         }), 16, 256);
         fe.rethrow();
+        tick("fold");
         auto R = std::make_unique<sb_json_out>();
         R->status.resize(ne);
         R->off.assign(ne + 1, 0);
@@ -512,8 +574,10 @@ extern "C" int sb_route_bodies(sb_store *s, const sb_route_input *in, sb_json_ou
         R->n = R->off[ne];
         R->buf = big_alloc(R->n, &R->cap);
         char *const base = R->buf.get();
+        tick("alloc");
         // pass 2: write each body in place
         parallel_for(ne, fe.wrap([&](size_t e) {
+            prefetch_ahead(e);
             const EvOut &O = eo[e];
             if (O.status) return;
             const sb_route_event &E = in->events[e];
@@ -572,6 +636,7 @@ extern "C" int sb_route_bodies(sb_store *s, const sb_route_input *in, sb_json_ou
                 throw Error(SB_EINTERNAL, "sb_route_bodies: body length mismatch at event " + std::to_string(e));
         }), 16, 256);
         fe.rethrow();
+        tick("write");
         *out = R.release();
     });
 }
