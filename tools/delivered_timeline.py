@@ -27,67 +27,6 @@ def chunk_cuts(n, chunks, taper):
     return np.round(c).astype(np.int64)
 
 
-def host_dev_ptr(t):
-    """Device address of a pinned host tensor (hipHostGetDevicePointer)."""
-    import ctypes as C
-    hip = C.CDLL('libamdhip64.so')
-    d = C.c_void_p()
-    rc = hip.hipHostGetDevicePointer(C.byref(d), C.c_void_p(t.data_ptr()), 0)
-    if rc != 0:
-        raise RuntimeError(f'hipHostGetDevicePointer: {rc}')
-    return d.value
-
-
-def timeline_zc(store, shape, reqs, base, dev, chunks, workers, passes=7, taper=True):
-    """Zero-copy hit lists: request_deliver_kernel writes each chunk's hits
-    straight into pinned host memory (its device address), so no chunk waits
-    for its row offsets before a hit copy; rows and offsets still by DMA."""
-    import numpy as np
-    import torch
-    from concurrent.futures import ThreadPoolExecutor
-    from sbeacon.genome import prepare_beacon_shard
-    n = len(reqs)
-    cuts = chunk_cuts(n, chunks, taper)
-    stream = torch.cuda.current_stream()
-    rows_h = torch.empty((n, 5), dtype=torch.int64, pin_memory=True)
-    ro_h = torch.empty(n + chunks, dtype=torch.int64, pin_memory=True)
-    rows_d = torch.empty((n, 5), dtype=torch.int64, device=dev)
-    ro_d = torch.empty(n + chunks, dtype=torch.int64, device=dev)
-    hits_h, hits_p = [None] * chunks, [None] * chunks
-    out = []
-    with ThreadPoolExecutor(workers) as ex:
-        for p in range(passes + 1):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-
-            def prep(k):
-                a, b = int(cuts[k]), int(cuts[k + 1])
-                lo, m, bt = prepare_beacon_shard(store, shape, reqs.rows(a, b), 1, 0)
-                return a + lo, m, bt, int(bt.stats()['hits'])
-
-            futs = [ex.submit(prep, k) for k in range(chunks)]
-            live = []
-            for k in range(chunks):
-                a, m, bt, cap = futs[k].result()
-                if hits_h[k] is None or hits_h[k].numel() < max(cap, 1):
-                    hits_h[k] = torch.empty(max(cap, 1), dtype=torch.int64, pin_memory=True)
-                    hits_p[k] = host_dev_ptr(hits_h[k])
-                bt.set_stream(stream.cuda_stream)
-                ro = ro_d[a + k:a + k + m + 1]
-                bt.run(rows_d[a:a + m].data_ptr(), hits_p[k], ro.data_ptr(), base)
-                rows_h[a:a + m].copy_(rows_d[a:a + m], non_blocking=True)
-                ro_h[a + k:a + k + m + 1].copy_(ro, non_blocking=True)
-                live.append(bt)
-            stream.synchronize()
-            dt = time.perf_counter() - t0
-            total = sum(int(ro_h[int(cuts[k]) + k + (int(cuts[k + 1]) - int(cuts[k]))]) for k in range(chunks))
-            for bt in live:
-                bt.free()
-            if p:
-                out.append({'ms': round(dt * 1e3, 2), 'hits': total})
-    return out
-
-
 def timeline(store, shape, reqs, base, dev, chunks, workers, passes=5, taper=False):
     import numpy as np
     import torch
