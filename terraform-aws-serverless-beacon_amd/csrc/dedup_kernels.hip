@@ -924,7 +924,31 @@ __global__ __launch_bounds__(kWT) __attribute__((amdgpu_waves_per_eu(SBEACON_WIN
     uint32_t wlo[kWPer], whi[kWPer];  // the class words' halves
     uint32_t okm = 0;
     uint64_t pk = 0;  // piece of key u in bits 6u..6u+5
-    {
+    if (np <= 4) {
+        // (jobs of <= 4 runs: two VCFs per dataset is the common case) the
+        // pieces' bounds in registers, read once: each key's piece is three
+        // compares and its load issues at once, with no LDS round trip per
+        // key before it.  s_pre[j] = total for j >= np, so those compares
+        // are false for every key
+        const uint32_t p1 = s_pre[1], p2 = s_pre[2], p3 = s_pre[3];
+        const uint32_t b0 = s_base[0], b1 = s_base[1], b2 = s_base[2], b3 = s_base[3];
+#pragma unroll
+        for (uint32_t u = 0; u < kWPer; ++u) {
+            const uint32_t f = u * kWT + threadIdx.x;
+            wlo[u] = 0;
+            whi[u] = 0;
+            if (f < total) {
+                const uint32_t pc = static_cast<uint32_t>(f >= p1) + static_cast<uint32_t>(f >= p2) +
+                                    static_cast<uint32_t>(f >= p3);
+                const uint32_t base = pc == 0 ? b0 : pc == 1 ? b1 : pc == 2 ? b2 : b3;
+                const uint64_t wv = ks.word[f + base];
+                wlo[u] = static_cast<uint32_t>(wv);
+                whi[u] = static_cast<uint32_t>(wv >> 32);
+                okm |= 1u << u;
+                pk |= static_cast<uint64_t>(pc) << (6 * u);
+            }
+        }
+    } else {
         uint32_t pc = 0;
 #pragma unroll
         for (uint32_t u = 0; u < kWPer; ++u) {

@@ -11,8 +11,8 @@ step() {  # name, limit, command...
   case $rc in 0) return 0;; *) exit $rc;; esac
 }
 V=$R/tools/variants
-step base 400 python3 -u $R/tools/dedup_ablate.py --save /tmp/dst --modes 0,1,0
+step base 400 python3 -u $R/tools/dedup_ablate.py --save /tmp/dst --modes ${MODES:-0,1,0}
 for v in $VARIANTS; do
-  step $v 200 env SBEACON_LIB=$V/$v/libsbeacon_hip.so python3 -u $R/tools/dedup_ablate.py --open /tmp/dst --modes 0,1,0
+  step $v 200 env SBEACON_LIB=$V/$v/libsbeacon_hip.so python3 -u $R/tools/dedup_ablate.py --open /tmp/dst --modes ${MODES:-0,1,0}
 done
 exit 0
