@@ -25,6 +25,8 @@ def main():
     ap.add_argument('--save', default=None)
     ap.add_argument('--open', default=None)
     ap.add_argument('--genotypes', action='store_true')
+    ap.add_argument('--streams', type=int, default=1,
+                    help='also time the rotation with batch k on stream k %% N (N > 1: independent batches overlap)')
     ap.add_argument('--digest', action='store_true', help='blake2b of every batch\'s rows + hits (A/B parity)')
     ap.add_argument('--wide', action='store_true', help='wide outputs (int64 rows, offsets, hits) instead of the '
                                                          'compact ones the bench step writes')
@@ -88,9 +90,33 @@ def main():
         pas.append(e0.elapsed_time(e1) / len(B))
     ev.sort()
     pas.sort()
+    pas_ms = []
+    if args.streams > 1:  # batch k on stream k % N (no cross-stream waits: events on each stream)
+        ss = [torch.cuda.Stream() for _ in range(args.streams)]
+        for k, x in enumerate(B):
+            x[0].set_stream(ss[k % len(ss)].cuda_stream)
+        for _ in range(args.rounds):
+            torch.cuda.synchronize()
+            a = [torch.cuda.Event(enable_timing=True) for _ in ss]
+            z = [torch.cuda.Event(enable_timing=True) for _ in ss]
+            for e, s_ in zip(a, ss):
+                e.record(s_)
+            for _ in range(4):
+                for x in B:
+                    run(*x)
+            for e, s_ in zip(z, ss):
+                e.record(s_)
+            torch.cuda.synchronize()
+            pas_ms.append(max(a[0].elapsed_time(e) for e in z) / (4 * len(B)))
+        for x in B:
+            x[0].sync()
+        pas_ms.sort()
     out = {'lib': os.environ.get('SBEACON_LIB', 'in-tree'), 'records': args.records, 'store_s': round(t_store, 2),
            'eval_ms_median': round(ev[len(ev) // 2], 4), 'eval_ms_min': round(ev[0], 4),
            'pass_ms_median': round(pas[len(pas) // 2], 4), 'pass_ms_min': round(pas[0], 4)}
+    if pas_ms:
+        out.update({'streams': args.streams, 'pass_ms_streams_median': round(pas_ms[len(pas_ms) // 2], 4),
+                    'pass_ms_streams_min': round(pas_ms[0], 4)})
     if args.digest:  # over the wide form (compact outputs widened): one digest for both forms
         import hashlib
         from sbeacon.requests import widen_compact
