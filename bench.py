@@ -50,6 +50,9 @@ def parse():
                     help='host ingest / CPU-baseline threads (default: every CPU the process may use, host_cores())')
     ap.add_argument('--batches', type=int, default=4,
                     help='config 3: request batches the step rotates over (each answered every --batches steps)')
+    ap.add_argument('--streams', type=int, default=2,
+                    help='config 3: HIP streams the step\'s batches alternate over (batch k on stream k mod N: N '
+                         'independent batches in flight, as a serving loop keeps them; 1 = every step behind the last)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='target CPU-baseline sample duration')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--parity-requests', type=int, default=2000,

@@ -39,6 +39,36 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def step_streams(torch, dev, n):
+    """n streams for the bench step, each on a hardware queue of its own.
+    HIP hands a process's streams its few hardware queues (GPU_MAX_HW_QUEUES,
+    4) and two plain streams shared one (measured: the steps never
+    overlapped, 0.085 ms/step as on one stream); a stream created with a CU
+    mask gets a queue of its own, and a mask over every CU restricts nothing
+    (0.0675 ms/step; the first stream at high priority instead: 0.0724).
+    SBEACON_BENCH_STREAMS (measurement): 'cumask' (default), 'prio', 'plain'."""
+    import ctypes
+    mode = os.environ.get('SBEACON_BENCH_STREAMS', 'cumask')
+    if mode == 'cumask':
+        # torch's own HIP runtime (the one process-wide copy the library binds to as well)
+        p = os.path.join(os.path.dirname(torch.__file__), 'lib', 'libamdhip64.so')
+        hip = ctypes.CDLL(p if os.path.exists(p) else 'libamdhip64.so')
+        n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
+        words = (n_cu + 31) // 32
+        mask = (ctypes.c_uint32 * words)(*([0xffffffff] * words))
+        out = []
+        for _ in range(n):
+            h = ctypes.c_void_p()
+            if hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), mask) != 0:
+                raise RuntimeError('hipExtStreamCreateWithCUMask failed')
+            out.append(torch.cuda.ExternalStream(h.value, device=dev))
+        return out
+    if mode == 'prio':
+        lo, hi = torch.cuda.Stream.priority_range()
+        return [torch.cuda.Stream(device=dev, priority=hi if k == 0 else lo) for k in range(n)]
+    return [torch.cuda.Stream(device=dev) for _ in range(n)]
+
+
 def main_genome(args):
     import numpy as np
     import torch
@@ -47,6 +77,12 @@ def main_genome(args):
     local = int(os.environ.get('LOCAL_RANK', 0))
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
+    # the step's streams (--streams, below), created before the store and
+    # the library's own streams: HIP hands a process's streams its few
+    # hardware queues (GPU_MAX_HW_QUEUES) as they are created, and two step
+    # streams created later shared one queue (measured: no overlap at all)
+    n_streams = max(1, args.streams)
+    ss = step_streams(torch, dev, n_streams) if n_streams > 1 else None
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -112,9 +148,26 @@ def main_genome(args):
         f'{pst["chains"]} chains, delivery {args.deliver}: owns {ex.n_own} rows, receives {len(ex.recvs)} '
         f'range(s), prepare {t_prepare:.2f} s per batch')
 
-    # answer + deliver: request rows + dense hit lists (one pass), exchange
-    steps = [make_step(lambda p, h, o, b=b: b['batch'].run(p.data_ptr(), h.data_ptr(), o.data_ptr(), base), b['ex'],
-                       b['part'], b['hits'], b['row_off']) for b in B]
+    # answer + deliver: request rows + dense hit lists (one pass), exchange.
+    # Consecutive steps' batches alternate over args.streams HIP streams
+    # (batch k on stream k mod N, its exchange too): independent batches in
+    # flight, as a serving loop keeps them -- one batch's delivery and its
+    # eval's ramp and drain overlap the next batch's eval.  Every step's work
+    # is inside the bracket (torch.cuda.synchronize() waits for every stream)
+    if ss is None:
+        ss = [torch.cuda.current_stream()]
+    for k, b in enumerate(B):
+        b['stream'] = ss[k % n_streams]
+        b['batch'].set_stream(b['stream'].cuda_stream)
+
+    def on_stream(f, s):
+        def g():
+            with torch.cuda.stream(s):
+                return f()
+        return g
+
+    steps = [on_stream(make_step(lambda p, h, o, b=b: b['batch'].run(p.data_ptr(), h.data_ptr(), o.data_ptr(), base),
+                                 b['ex'], b['part'], b['hits'], b['row_off']), b['stream']) for b in B]
 
     for i in range(max(args.warmup, args.batches)):
         steps[i % len(steps)]()
@@ -122,17 +175,28 @@ def main_genome(args):
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ea = [torch.cuda.Event(enable_timing=True) for _ in ss]
+    ez = [torch.cuda.Event(enable_timing=True) for _ in ss]
     t1 = time.perf_counter()
-    e0.record()
+    for e, s_ in zip(ea, ss):
+        e.record(s_)
     for i in range(args.steps):
         steps[i % len(steps)]()
-    e1.record()
+    for e, s_ in zip(ez, ss):
+        e.record(s_)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t1
     if dist:
         dist.barrier()
-    step_dev_ms = e0.elapsed_time(e1) / args.steps  # events on the stream around the K steps
+    # events on every step stream around the K steps: first start to last end
+    step_dev_ms = max(ea[0].elapsed_time(e) for e in ez) / args.steps
+    # the measurements below time one batch at a time on torch's stream (the
+    # eval kernel alone, the serial pass): each batch's runs synced first (the
+    # invariant word of every timed pass is checked here: SB_EINTERNAL raises)
+    for b in B:
+        b['batch'].sync()
+        b['batch'].set_stream(stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if any(b['ex'].row_overflow() for b in B):  # (u32 rows: a cross-rank sum left 32 bits)
         raise RuntimeError('a request row sum left 32 bits in the exchange: compact rows cannot hold it')
     # the dominant kernel (request_eval_kernel) alone: events around its launch
@@ -348,7 +412,12 @@ def main_genome(args):
                 'request_deliver_kernel (each workgroup\'s output base summed from the eval workgroup totals -- '
                 'request_tile_scan_kernel\'s tile offsets with SBEACON_REQ_TILE_SCAN=1 --, row offsets, dense hit lists '
                 'in request order; compact outputs: rows as four u32 sums, u32 offsets and hits), '
-                'then the exchange (send/recv of straddling rows and hits)',
+                'then the exchange (send/recv of straddling rows and hits)'
+                + (f'; consecutive steps on {n_streams} HIP streams (batch k on stream k mod {n_streams}: '
+                   f'{n_streams} independent batches in flight, one batch\'s delivery and its eval\'s ramp and drain '
+                   'overlapping the next batch\'s eval; every step inside the synchronize bracket)'
+                   if n_streams > 1 else ''),
+        'streams': n_streams,
         'slice_queries_per_s': round(tot_slices * args.steps / elapsed, 1),
         'candidates_loaded_per_s': round(tot_cand * args.steps / elapsed, 1),
         'hits_per_step': int(tot_hits),
@@ -362,8 +431,10 @@ def main_genome(args):
         'roofline': {'bound': 'hbm', 'achieved': round(r0[5], 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                      'frac': round(r0[5] / HBM_PEAK_GBS, 4), 'traffic': traffic,
                      'kernel': 'request_eval_kernel (rank 0, the dominant kernel of the pass): HIP events around '
-                               'its launch in each of K rotating passes on its stream, averaged (rocprof per-kernel '
-                               'averages: profiles/)',
+                               'its launch in each of K rotating passes on one stream, one pass at a time (not beside '
+                               'another batch as the timed steps run), averaged; rocprof: the launches of that serial '
+                               'phase (the timed steps\' launches share the device with the other stream\'s), '
+                               'profiles/',
                      'algorithmic_bytes_per_launch': r0[7],
                      'pricing': 'bytes the launch must move at least once: 52 B/request (32 B '
                                 + ('packed request, planned in the wave' if fused else 'chain descriptor')
