@@ -56,17 +56,23 @@ def step_streams(torch, dev, n):
         n_cu = torch.cuda.get_device_properties(dev).multi_processor_count
         words = (n_cu + 31) // 32
         mask = (ctypes.c_uint32 * words)(*([0xffffffff] * words))
-        out = []
+        out, raw = [], []
         for _ in range(n):
             h = ctypes.c_void_p()
             if hip.hipExtStreamCreateWithCUMask(ctypes.byref(h), ctypes.c_uint32(words), mask) != 0:
                 raise RuntimeError('hipExtStreamCreateWithCUMask failed')
+            raw.append(h)
             out.append(torch.cuda.ExternalStream(h.value, device=dev))
-        return out
+
+        def destroy():  # (ours, not torch's: destroyed once the steps are done, not left to process exit)
+            torch.cuda.synchronize()
+            for h in raw:
+                hip.hipStreamDestroy(h)
+        return out, destroy
     if mode == 'prio':
         lo, hi = torch.cuda.Stream.priority_range()
-        return [torch.cuda.Stream(device=dev, priority=hi if k == 0 else lo) for k in range(n)]
-    return [torch.cuda.Stream(device=dev) for _ in range(n)]
+        return [torch.cuda.Stream(device=dev, priority=hi if k == 0 else lo) for k in range(n)], lambda: None
+    return [torch.cuda.Stream(device=dev) for _ in range(n)], lambda: None
 
 
 def main_genome(args):
@@ -82,7 +88,7 @@ def main_genome(args):
     # hardware queues (GPU_MAX_HW_QUEUES) as they are created, and two step
     # streams created later shared one queue (measured: no overlap at all)
     n_streams = max(1, args.streams)
-    ss = step_streams(torch, dev, n_streams) if n_streams > 1 else None
+    ss, ss_destroy = step_streams(torch, dev, n_streams) if n_streams > 1 else (None, lambda: None)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -196,6 +202,7 @@ def main_genome(args):
     for b in B:
         b['batch'].sync()
         b['batch'].set_stream(stream)
+    ss_destroy()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if any(b['ex'].row_overflow() for b in B):  # (u32 rows: a cross-rank sum left 32 bits)
         raise RuntimeError('a request row sum left 32 bits in the exchange: compact rows cannot hold it')

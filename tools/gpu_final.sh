@@ -16,11 +16,17 @@ step() {  # name, limit, command...
   echo "$name rc=$rc"; tail -2 $O/$name.log | cut -c1-600
   case $rc in 0) return 0;; *) exit $rc;; esac
 }
-${SKIP_TESTS:+false} step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()" || true
-${SKIP_TESTS:+false} step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread || true
-step bench 600 python3 -u $R/bench.py --steps 20 --warmup 5
+# PARTS: which of tests / bench / prof / pmc to run (default all; one
+# gpurun call holds at most 1,200 s, so the final evidence is two calls)
+has() { case " ${PARTS:-tests bench prof pmc} " in *" $1 "*) return 0;; esac; return 1; }
+if has tests; then
+step smoke 300 python3 -c "import __graft_entry__ as g; g.smoke()"
+step gpu_tests 900 python3 -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread
+fi
+has bench && step bench 600 python3 -u $R/bench.py --steps 20 --warmup 5
 cd /tmp
-step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 -u $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline
+has prof && step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 -u $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline
+has pmc || exit 0
 step save 300 python3 -u $R/tools/req_tune.py --save /tmp/st --rounds 3 --digest
 step pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/pmc_fetch -o p -- python3 -u $R/tools/req_tune.py --open /tmp/st --rounds 2
 step pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/pmc_write -o p -- python3 -u $R/tools/req_tune.py --open /tmp/st --rounds 2
