@@ -51,7 +51,7 @@ def parse():
     ap.add_argument('--batches', type=int, default=4,
                     help='config 3: request batches the step rotates over (each answered every --batches steps)')
     ap.add_argument('--streams', type=int, default=2,
-                    help='config 3: HIP streams the step\'s batches alternate over (batch k on stream k mod N: N '
+                    help='configs 3 and 2: HIP streams the step\'s batches alternate over (batch k on stream k mod N: N '
                          'independent batches in flight, as a serving loop keeps them; 1 = every step behind the last)')
     ap.add_argument('--cpu-seconds', type=float, default=15.0, help='target CPU-baseline sample duration')
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -206,7 +206,7 @@ def main():
 
 def sub_line(out: dict) -> dict:
     """A workload's line as a sub-object of the headline line."""
-    keep = ('metric', 'value', 'unit', 'ms_per_step', 'dtype', 'device_ms_per_step', 'config', 'roofline',
+    keep = ('metric', 'value', 'unit', 'ms_per_step', 'streams', 'dtype', 'device_ms_per_step', 'config', 'roofline',
             'delivered', 'cpu_baseline', 'parity_sample', 'ingest_s', 'device_gib')
     return {k: out[k] for k in keep if k in out}
 
@@ -242,21 +242,44 @@ def main_chr22(args):
     batch = store.prepare(payloads)
     log(f'[rank {rank}] {len(reqs)} requests -> {len(payloads)} slice queries')
 
-    for _ in range(args.warmup):
-        batch.run()
-    batch.sync()
+    # --streams N: N copies of the batch (the same payloads, each its own
+    # buffers) alternate over N CU-masked streams, one hardware queue each,
+    # as config 3's step does (bench_genome.step_streams): step i runs copy
+    # i mod N, so one pass's ramp and drain overlap the next pass
+    n_streams = max(1, args.streams)
+    batches, ss_destroy = [batch], (lambda: None)
+    if n_streams > 1:
+        from bench_genome import step_streams
+        ss, ss_destroy = step_streams(torch, torch.device('cuda', local), n_streams)
+        batches += [store.prepare(payloads) for _ in range(n_streams - 1)]
+        for b, s_ in zip(batches, ss):
+            b.set_stream(s_.cuda_stream)
+    for i in range(max(args.warmup, n_streams)):
+        batches[i % n_streams].run()
+    for b in batches:
+        b.sync()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    for _ in range(args.steps):
-        batch.run()
-    batch.sync()
+    for i in range(args.steps):
+        batches[i % n_streams].run()
+    for b in batches:
+        b.sync()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t1
     if dist:
         dist.barrier()
-    timing = batch.timing()  # HIP events spanning the K back-to-back timed launches, / K
+    if n_streams > 1:  # the kernels' own time (the roofline's): one copy, one pass at a time, on the store's stream
+        for b in batches[1:]:
+            b.free()
+        batches = [batch]
+        batch.set_stream(None)
+        ss_destroy()
+        for _ in range(args.steps):
+            batch.run()
+        batch.sync()
+    timing = batch.timing()  # HIP events spanning K back-to-back launches of one batch, / K (set at its last sync)
     rs = batch.fetch()
     st = rs.stats()
     n_req, n_slice = len(reqs), len(payloads)
@@ -353,6 +376,7 @@ def main_chr22(args):
         'higher_is_better': True,
         'scaling': 'weak',
         'vs_baseline': None,
+        'streams': n_streams,
         'dtype': 'int64',
         'data': 'synthetic (seeded 1000G chr22-shape VCF, generated + ingested in-process)',
         'config': {'workload': 'config2-chr22-shape', 'records': args.records, 'samples': args.samples,
