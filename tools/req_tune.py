@@ -94,6 +94,7 @@ def main():
     if args.streams > 1:  # batch k on stream k % N (no cross-stream waits: events on each stream)
         ss = [torch.cuda.Stream() for _ in range(args.streams)]
         for k, x in enumerate(B):
+            x[0].sync()  # (the runs above: a batch changes stream only between a run's sync and the next run)
             x[0].set_stream(ss[k % len(ss)].cuda_stream)
         for _ in range(args.rounds):
             torch.cuda.synchronize()
