@@ -556,27 +556,32 @@ def _vcf_records(path):
     return out
 
 
-def test_timed_step_variant_matches_oracle():
+@pytest.mark.parametrize('n_streams', [1, 2])
+def test_timed_step_variant_matches_oracle(n_streams):
     """The exact form the bench step times (bench_genome.py main_genome): 4
     request batches prepared once, each re-planned on the device inside
     every pass (sb_requests_set_replan; the planning fused into
     request_eval_kernel: plan_fused), compact outputs (SB_COMPACT_ALL), run
-    in rotation on one stream into their own buffers -- every batch's rows
-    and every hit list against the C oracle (patched variantType semantics),
-    not against another device path."""
+    in rotation into their own buffers -- on one stream, or (the bench's
+    default, --streams 2) batch k on CU-masked stream k mod 2 with two
+    batches in flight -- every batch's rows and every hit list against the
+    C oracle (patched variantType semantics), not against another device
+    path."""
     import torch
+    from bench_genome import step_streams
     from sbeacon.genome import GenomeShape, config3_requests, prepare_shard_requests, shard_requests
     from sbeacon.requests import COMPACT_ALL, widen_compact
     shape = GenomeShape(n_total=240_000, seed=3, n_samples=0)
     store = shape.build_shard_store(1, 0, device=0)
     dev = torch.device('cuda', 0)
-    stream = torch.cuda.current_stream(dev).cuda_stream
+    ss, ss_destroy = step_streams(torch, dev, n_streams) if n_streams > 1 else \
+        ([torch.cuda.current_stream(dev)], lambda: None)
     B = []
     for k in range(4):
         reqs = config3_requests(shape, n=4000, seed=1003 + k)
         sr = shard_requests(shape, reqs, 1, 0)
         b = prepare_shard_requests(store, sr)
-        b.set_stream(stream)
+        b.set_stream(ss[k % n_streams].cuda_stream)
         b.set_replan(True)
         b.set_compact(COMPACT_ALL)
         cap = max(int(b.stats()['hits']), 1)
@@ -590,6 +595,9 @@ def test_timed_step_variant_matches_oracle():
         x['b'].sync()
         assert x['b'].plan_fused()  # the timed variant: planning inside the eval kernel
         assert x['b'].escape_flags() == (False, False)
+        x['b'].set_stream(None)  # (off the step streams before they are destroyed)
+    torch.cuda.synchronize()
+    ss_destroy()
     with tempfile.TemporaryDirectory() as tmp:
         path = os.path.join(tmp, 'full.vcf')
         with open(path, 'wb') as f:
